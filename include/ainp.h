@@ -1,0 +1,246 @@
+/*
+ * ainp.h — C ABI of the MI355X-native spectrogram-inpainting training path.
+ *
+ * Drop-in boundary.  The reference
+ * (savage-hacker14/ml-audio-inpainting) is pure Python: its "operator API" is
+ * the Python surface of utils.py / models/CNNBLSTM/{model,dataset,train}.py.
+ * Every entry point below replaces one implicit librosa / numpy / ATen kernel
+ * that surface launches today; the reference call site is cited per function.
+ *
+ * Conventions (all functions):
+ *   - every pointer is a caller-owned DEVICE buffer unless stated otherwise;
+ *     the library never allocates, frees or synchronises;
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream);
+ *   - layouts are dense row-major (C order) in the shapes stated;
+ *   - return 0 on success or a negative AINP_E* code; nothing throws across
+ *     the ABI; launches are asynchronous on `stream`.
+ * Callers: the Python host layer (ml-audio-inpainting_amd/ainp/_lib.py) via
+ * ctypes; see INTEGRATION.md for the binding stub.
+ */
+#ifndef AINP_H
+#define AINP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AINP_OK 0
+#define AINP_EINVAL (-1)     /* bad shape / argument */
+#define AINP_ELAUNCH (-2)    /* kernel launch failed */
+#define AINP_EUNSUPPORTED (-3)
+
+/* ------------------------------------------------------------------------ */
+/* Library identity                                                          */
+/* ------------------------------------------------------------------------ */
+/* ABI version: bumped on any signature change. */
+int ainp_abi_version(void);
+/* Name of the gfx target the code objects were built for ("gfx950"). */
+const char* ainp_build_target(void);
+/* Last hip error string recorded by a failing launch in this thread. */
+const char* ainp_last_error(void);
+
+/* ------------------------------------------------------------------------ */
+/* (a5/a6/a7) STFT + spectrogram features + gap mask, one fused kernel.      */
+/* ------------------------------------------------------------------------ */
+/* Replaces, per example:
+ *   utils.extract_spectrogram -> librosa.stft(center=True, window='hann',
+ *       pad_mode='constant')                           (utils.py:192-234)
+ *   CNNBLSTM mode: models/CNNBLSTM/dataset.py:95-119  (target STFT of the clean
+ *       clip, log10(|STFT(gapped clip)|+1e-9), time_to_frames gap mask, 1=gap)
+ *   GAN mode:      models/GAN/dataset.py:104-152      (log1p|STFT| of clean and
+ *       impaired clip, angle of the clean STFT, frame mask 1=valid)
+ * Arithmetic: both STFTs are computed in float64 (the reference's gapped CNNBLSTM
+ * path is complex128) and rounded once to the output type.
+ *
+ * audio      [n_clips, n_samples] f32 clean clips
+ * clip_index [batch] int32 clip used by each example (NULL: example b uses clip b)
+ * gap_start  [batch] int64 first zeroed sample of each example's gap
+ * window     [n_fft] f64 analysis window, already centre-padded to n_fft
+ *            (librosa get_window(...,fftbins=True) + util.pad_center)
+ * n_fft      power of two, 16..2048;   F = n_fft/2+1
+ * n_frames   frames written per example (<= 1 + n_samples/hop); CNNBLSTM slices
+ *            to ceil(sr*max_len_s/hop) (dataset.py:89,110-111)
+ * mode 0 (AINP_FEAT_CNNBLSTM):
+ *   out0 [batch,F,n_frames] f32  log10(|X_gap|+1e-9)
+ *   out1 [batch,F,n_frames,2] f32 complex64 target X_clean (re,im interleaved)
+ *   out2 [batch,F,n_frames] f32  mask, 1 on frames [fs,fe) with
+ *        fs = int((s/sr)*sr)//hop, fe = int(((s+g)/sr)*sr)//hop in IEEE double
+ *        (librosa.time_to_frames of the float seconds)
+ *   out3 unused (may be NULL)
+ * mode 1 (AINP_FEAT_GAN):
+ *   out0 log1p(|X_clean|)   out1 log1p(|X_imp|)   out2 angle(X_clean)
+ *   out3 mask 1=valid, 0 on [s//hop, min(T, ceil((s+g)/hop)))
+ * Any out pointer may be NULL to skip that output.
+ */
+#define AINP_FEAT_CNNBLSTM 0
+#define AINP_FEAT_GAN 1
+int ainp_stft_features(const float* audio, int64_t n_clips, int64_t n_samples,
+                       const int32_t* clip_index, const int64_t* gap_start,
+                       int64_t batch, int64_t gap_len, int64_t sample_rate,
+                       const double* window, int n_fft, int hop,
+                       int64_t n_frames, int mode, float* out0, float* out1,
+                       float* out2, float* out3, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32, exact fp32)                    */
+/* ------------------------------------------------------------------------ */
+/* C = alpha * op(A) * op(B) + beta * C + bias1 + bias2   (bias along n)
+ * Replaces the ATen GEMMs behind nn.LSTM's input projections and nn.Linear
+ * (models/CNNBLSTM/model.py:46-50,77,80) and their backward.
+ * Element (m,k) of op(A) is A[m*sam + k*sak]; (k,n) of op(B) is
+ * B[k*sbk + n*sbn]; (m,n) of C is C[m*scm + n*scn].  One of (sam,sak), one
+ * of (sbk,sbn) and one of (scm,scn) must be 1 (the contiguous dimension).
+ * Batches: nptr pointer batches (host arrays of device pointers, nptr <= 8)
+ * times nstrided strided batches; batch b uses pointer entry b % nptr offset
+ * by (b / nptr) * stride{A,B,C}.  bias1/bias2: host arrays (may be NULL, or
+ * hold NULL entries) of per-pointer-batch bias vectors of length N.
+ * ksplit != 0: all nptr*nstrided (A,B) pairs are summed into C[0]
+ * (K-concatenation across separate buffers / strided slabs). */
+int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
+                  const float* const* A, int64_t sam, int64_t sak,
+                  int64_t strideA, const float* const* B, int64_t sbk,
+                  int64_t sbn, int64_t strideB, float beta, float* const* C,
+                  int64_t scm, int64_t scn, int64_t strideC,
+                  const float* const* bias1, const float* const* bias2,
+                  int nptr, int64_t nstrided, int ksplit, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* 3x3 / stride 1 / pad 1 convolution over [N, C, F, T] spectrogram tiles    */
+/* ------------------------------------------------------------------------ */
+/* Replaces nn.Conv2d(kernel_size=3, padding=1) of models/CNNBLSTM/model.py:
+ * 35-60 with the preceding nn.BatchNorm2d + nn.ReLU fused into its input load.
+ * Forward: y = conv(act(x)) + bias, act(x) = relu(x*in_scale+in_shift) per
+ * input channel when in_scale != NULL, identity otherwise; zero padding is
+ * applied to act(x) as nn.Conv2d pads its (post-ReLU) input.
+ * w: [Cout, Cin, 3, 3]; bias: [Cout] or NULL; Cout <= 64.
+ * stats (may be NULL): double[ainp_conv3x3_fwd_stat_parts(N,H,W) * 2*Cout];
+ * row p receives this workgroup's [sum y (Cout) | sum y^2 (Cout)] for the
+ * following BatchNorm (reduced by ainp_bn_finalize). */
+int ainp_conv3x3_fwd_stat_parts(int64_t N, int64_t H, int64_t W);
+int ainp_conv3x3_fwd(const float* x, const float* w, const float* bias,
+                     const float* in_scale, const float* in_shift, float* y,
+                     double* stats, int64_t N, int Cin, int Cout, int64_t H,
+                     int64_t W, void* stream);
+/* Data gradient dx = conv_transpose(dy, w): [N,Cout,H,W] -> [N,Cin,H,W].
+ * workspace unused (may be NULL); Cin <= 64. */
+int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
+                       float* workspace, int64_t N, int Cin, int Cout,
+                       int64_t H, int64_t W, void* stream);
+/* Weight gradient dw[co,ci,ky,kx] = sum_{n,h,w} dy[n,co,h,w] *
+ *   act(x)[n,ci,h+ky-1,w+kx-1]; dbias[co] = sum dy (dbias may be NULL).
+ * act as in the forward.  Overwrites dw / dbias; deterministic.
+ * workspace: ainp_conv3x3_wgrad_workspace(...) bytes. */
+size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout, int64_t H,
+                                    int64_t W);
+int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
+                       const float* in_shift, const float* dy, float* dw,
+                       float* dbias, void* workspace, int64_t N, int Cin,
+                       int Cout, int64_t H, int64_t W, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* BatchNorm2d (training statistics) + ReLU                                   */
+/* ------------------------------------------------------------------------ */
+/* Reduce the conv epilogue partials to per-channel sums:
+ * sums[0:C] = sum y, sums[C:2C] = sum y^2 (double).  Between this and
+ * ainp_bn_finalize a data-parallel caller all-reduces `sums` (SyncBN). */
+int ainp_bn_stats_reduce(const double* stats, int nparts, double* sums, int C,
+                         void* stream);
+/* Finalise batch statistics into the affine form used by the next kernel:
+ * scale = gamma*rstd, shift = beta-mean*scale; save_mean_rstd (float[2*C])
+ * keeps mean / rstd for the backward; running stats updated in place with
+ * momentum and the unbiased variance, as torch.nn.BatchNorm2d in train mode
+ * (running_* may both be NULL).  count = elements per channel summed into
+ * `sums` (N*H*W, times the world size after an all-reduce). */
+int ainp_bn_finalize(const double* sums, int64_t count, const float* gamma,
+                     const float* beta, float* running_mean,
+                     float* running_var, float momentum, float eps,
+                     float* scale, float* shift, float* save_mean_rstd, int C,
+                     void* stream);
+/* Eval-mode affine from running statistics. */
+int ainp_bn_eval_affine(const float* gamma, const float* beta,
+                        const float* running_mean, const float* running_var,
+                        float eps, float* scale, float* shift, int C,
+                        void* stream);
+/* out = relu(x*scale[c] + shift[c]) over x [N,C,H,W].  If out_ntcf != 0 the
+ * result is written as [N, W, C*H] (feature c*H+h at time w): the LSTM input
+ * layout produced by model.py:73-74's permute(0,3,1,2).reshape. */
+int ainp_bn_relu_apply(const float* x, const float* scale, const float* shift,
+                       float* out, int64_t N, int C, int64_t H, int64_t W,
+                       int out_ntcf, void* stream);
+/* BatchNorm+ReLU backward.  z = relu(y*scale+shift); gz = g*(z>0).
+ * Step 1 (reduce): sums[0:C] = sum(gz), sums[C:2C] = sum(gz*xhat) (double),
+ *   xhat = (y-mean)*rstd.  workspace: ainp_bn_relu_bwd_workspace(...) bytes.
+ *   A data-parallel caller all-reduces `sums` before step 2 (SyncBN).
+ * Step 2 (apply): gy = gamma*rstd*(gz - sums0/count - xhat*sums1/count),
+ *   written [N,C,H,W]; dgamma = sums1, dbeta = sums0 (float[C], may be NULL).
+ * g is [N,C,H,W], or [N,W,C*H] (LSTM input layout) if g_ntcf != 0. */
+size_t ainp_bn_relu_bwd_workspace(int64_t N, int C, int64_t H, int64_t W);
+int ainp_bn_relu_bwd_reduce(const float* g, const float* y, const float* scale,
+                            const float* shift, const float* save_mean_rstd,
+                            void* workspace, double* sums, int64_t N, int C,
+                            int64_t H, int64_t W, int g_ntcf, void* stream);
+int ainp_bn_relu_bwd_apply(const float* g, const float* y, const float* scale,
+                           const float* shift, const float* gamma,
+                           const float* save_mean_rstd, const double* sums,
+                           int64_t count, float* gy, float* dgamma,
+                           float* dbeta, int64_t N, int C, int64_t H,
+                           int64_t W, int g_ntcf, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* BLSTM recurrence (one layer, both directions), batch_first                */
+/* ------------------------------------------------------------------------ */
+/* Replaces the recurrent part of nn.LSTM(bidirectional=True, batch_first)
+ * (models/CNNBLSTM/model.py:46-47,77). Gate order i,f,g,o; c'=f*c+i*g;
+ * h'=o*tanh(c'); h0=c0=0.
+ * zx    [N, T, 8H]  input projections x W_ih^T + b_ih + b_hh; forward
+ *       direction in columns [0,4H), reverse direction in [4H,8H)
+ * w_hh  host array of 2 device pointers to the [4H, H] recurrent weights
+ * h_out [N, T, 2H]  output (forward in [0,H), reverse in [H,2H))
+ * gates [N, T, 8H]  saved post-activation gates (needed by the backward)
+ * cell  [N, T, 2H]  saved cell states (needed by the backward)
+ * H in {32, 64, 128}. */
+int ainp_lstm_rec_fwd(const float* zx, const float* const* w_hh, float* h_out,
+                      float* gates, float* cell, int64_t N, int64_t T, int H,
+                      void* stream);
+/* Backward through time: dh_out [N,T,2H] -> dgates [N,T,8H] (gradient of the
+ * pre-activation gates, i.e. of zx). */
+int ainp_lstm_rec_bwd(const float* dh_out, const float* gates,
+                      const float* cell, const float* const* w_hh,
+                      float* dgates, int64_t N, int64_t T, int H,
+                      void* stream);
+/* hprev[n,t,:H] = h_out[n,t-1,:H], hprev[n,t,H:] = h_out[n,t+1,H:] (0 at the
+ * sequence start): the right-hand operand of dW_hh = dgates^T * hprev. */
+int ainp_lstm_hprev(const float* h_out, float* hprev, int64_t N, int64_t T,
+                    int H, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Loss, reductions, optimizer                                               */
+/* ------------------------------------------------------------------------ */
+/* CNNBLSTM training loss (models/CNNBLSTM/train.py:70,104):
+ *   L = sum | 10^y * m - |target| * m |    (nn.L1Loss(reduction='sum'))
+ * y, mask [n] f32; target [n] complex64 (interleaved). loss: double[1]
+ * accumulated (caller zeroes). dy (may be NULL): dL/dy * grad_scale. */
+int ainp_l1_pow10_loss(const float* y, const float* mask, const float* target,
+                       int64_t n, double* loss, float* dy, float grad_scale,
+                       void* stream);
+/* Column sums: out[j] (+)= sum_i x[i*ld + j], i<rows, j<cols. */
+int ainp_colsum(const float* x, int64_t rows, int64_t cols, int64_t ld,
+                float* out, int accumulate, void* stream);
+/* Multi-tensor Adam with torch.optim.Adam arithmetic (amsgrad=False,
+ * maximize=False): m = lerp(m, g, 1-b1); v = b2*v + (1-b2)*g*g;
+ * p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps); bc_i = 1 - b_i^step.
+ * weight_decay adds wd*p to g first (torch's L2 form).  Host arrays of
+ * n_tensors device pointers and element counts; step is 1-based. */
+int ainp_adam(float* const* params, const float* const* grads,
+              float* const* exp_avg, float* const* exp_avg_sq,
+              const int64_t* numel, int n_tensors, double lr, double beta1,
+              double beta2, double eps, double weight_decay, int64_t step,
+              void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* AINP_H */

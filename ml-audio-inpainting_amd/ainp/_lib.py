@@ -1,0 +1,97 @@
+"""ctypes binding of libainp.so (the C ABI declared in include/ainp.h).
+
+The library is the product: every call here launches a hand-written gfx950
+kernel.  There is no fallback path -- if the shared object is missing or was
+not built for this machine, import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_double, c_float, c_int, c_int64, c_size_t, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("AINP_LIB", os.path.join(_HERE, "libainp.so"))
+
+
+class AinpError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libainp.so not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` or "
+            "`make -C ml-audio-inpainting_amd/csrc`")
+    return ctypes.CDLL(LIB_PATH)
+
+
+lib = _load()
+
+P = c_void_p
+PP = POINTER(c_void_p)
+_SIGS = {
+    "ainp_abi_version": (c_int, []),
+    "ainp_build_target": (c_char_p, []),
+    "ainp_last_error": (c_char_p, []),
+    "ainp_stft_features": (c_int, [P, c_int64, c_int64, P, P, c_int64, c_int64, c_int64,
+                                   P, c_int, c_int, c_int64, c_int, P, P, P, P, P]),
+    "ainp_gemm_f32": (c_int, [c_int64, c_int64, c_int64, c_float, PP, c_int64, c_int64,
+                              c_int64, PP, c_int64, c_int64, c_int64, c_float, PP,
+                              c_int64, c_int64, c_int64, PP, PP, c_int, c_int64, c_int, P]),
+    "ainp_conv3x3_fwd_stat_parts": (c_int, [c_int64, c_int64, c_int64]),
+    "ainp_conv3x3_fwd": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
+                                 c_int64, P]),
+    "ainp_conv3x3_dgrad": (c_int, [P, P, P, P, c_int64, c_int, c_int, c_int64, c_int64, P]),
+    "ainp_conv3x3_wgrad_workspace": (c_size_t, [c_int64, c_int, c_int, c_int64, c_int64]),
+    "ainp_conv3x3_wgrad": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
+                                   c_int64, P]),
+    "ainp_bn_stats_reduce": (c_int, [P, c_int, P, c_int, P]),
+    "ainp_bn_finalize": (c_int, [P, c_int64, P, P, P, P, c_float, c_float, P, P, P, c_int, P]),
+    "ainp_bn_eval_affine": (c_int, [P, P, P, P, c_float, P, P, c_int, P]),
+    "ainp_bn_relu_apply": (c_int, [P, P, P, P, c_int64, c_int, c_int64, c_int64, c_int, P]),
+    "ainp_bn_relu_bwd_workspace": (c_size_t, [c_int64, c_int, c_int64, c_int64]),
+    "ainp_bn_relu_bwd_reduce": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int64,
+                                        c_int64, c_int, P]),
+    "ainp_bn_relu_bwd_apply": (c_int, [P, P, P, P, P, P, P, c_int64, P, P, P, c_int64, c_int,
+                                       c_int64, c_int64, c_int, P]),
+    "ainp_lstm_rec_fwd": (c_int, [P, PP, P, P, P, c_int64, c_int64, c_int, P]),
+    "ainp_lstm_rec_bwd": (c_int, [P, P, P, PP, P, c_int64, c_int64, c_int, P]),
+    "ainp_lstm_hprev": (c_int, [P, P, c_int64, c_int64, c_int, P]),
+    "ainp_l1_pow10_loss": (c_int, [P, P, P, c_int64, P, P, c_float, P]),
+    "ainp_colsum": (c_int, [P, c_int64, c_int64, c_int64, P, c_int, P]),
+    "ainp_adam": (c_int, [PP, PP, PP, PP, POINTER(c_int64), c_int, c_double, c_double,
+                          c_double, c_double, c_double, c_int64, P]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+for _name, (_res, _args) in _SIGS.items():
+    _fn = getattr(lib, _name)  # AttributeError here = ABI mismatch: fail loudly
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib.ainp_last_error().decode(errors="replace")
+        raise AinpError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib, name)(*args), name)
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    arr = (c_void_p * max(1, len(ptrs)))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr
+
+
+def int64_array(vals) -> ctypes.Array:
+    arr = (c_int64 * max(1, len(vals)))()
+    for i, v in enumerate(vals):
+        arr[i] = int(v)
+    return arr

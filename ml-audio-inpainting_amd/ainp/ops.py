@@ -1,0 +1,346 @@
+"""Tensor-level wrappers over the libainp C ABI.
+
+Each function validates its torch tensors (device, dtype, layout), allocates
+outputs through PyTorch's caching allocator and launches the gfx950 kernel on
+the current HIP stream.  These are the only entry points the rest of the
+package uses to compute; nothing here falls back to ATen or the CPU.
+"""
+from __future__ import annotations
+
+import functools
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import call, int64_array, ptr_array
+
+FEAT_CNNBLSTM = 0
+FEAT_GAN = 1
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _req(t: torch.Tensor, name: str, dtype=torch.float32, contiguous=True):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.device.type != "cuda":
+        raise RuntimeError(f"{name} must live on the GPU (got {t.device}); the ainp "
+                           "kernels have no CPU path")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if contiguous and not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return t
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+# --------------------------------------------------------------------- STFT
+@functools.lru_cache(maxsize=None)
+def analysis_window(window: str, win_length: int, n_fft: int) -> np.ndarray:
+    """librosa.filters.get_window(window, win_length, fftbins=True) centred in
+    n_fft (librosa.util.pad_center), float64 -- the window librosa.stft uses."""
+    import scipy.signal
+    w = scipy.signal.get_window(window, win_length, fftbins=True).astype(np.float64)
+    out = np.zeros(n_fft, dtype=np.float64)
+    lpad = (n_fft - win_length) // 2
+    out[lpad:lpad + win_length] = w
+    return out
+
+
+_WIN_CACHE: dict = {}
+
+
+def _device_window(window, win_length, n_fft, device):
+    key = (window, win_length, n_fft, str(device))
+    w = _WIN_CACHE.get(key)
+    if w is None:
+        w = torch.from_numpy(analysis_window(window, win_length, n_fft)).to(device)
+        _WIN_CACHE[key] = w
+    return w
+
+
+def stft_features(audio: torch.Tensor, gap_start: torch.Tensor, gap_len: int,
+                  n_fft: int, hop: int, win_length: int | None = None,
+                  n_frames: int | None = None, mode: int = FEAT_CNNBLSTM,
+                  sample_rate: int = 16000, clip_index: torch.Tensor | None = None,
+                  window: str = "hann", outputs=(True, True, True, True)):
+    """Fused STFT + features + gap mask (include/ainp.h ainp_stft_features).
+
+    audio [n_clips, S] f32 cuda; gap_start [B] int64 cuda.
+    Returns (out0, out1, out2, out3); CNNBLSTM: (log10 |X_gap| + 1e-9,
+    complex64 target, mask 1=gap, None); GAN: (log1p|X|, log1p|X_imp|,
+    angle X, mask 1=valid).
+    """
+    _req(audio, "audio")
+    if audio.dim() == 1:
+        audio = audio.unsqueeze(0)
+    _req(gap_start, "gap_start", torch.int64)
+    if clip_index is not None:
+        _req(clip_index, "clip_index", torch.int32)
+        batch = clip_index.numel()
+    else:
+        batch = audio.shape[0]
+    if gap_start.numel() != batch:
+        raise ValueError("gap_start must have one entry per example")
+    n_clips, S = audio.shape
+    win_length = n_fft if win_length is None else win_length
+    n_avail = 1 + S // hop
+    n_frames = n_avail if n_frames is None else int(n_frames)
+    F = n_fft // 2 + 1
+    dev = audio.device
+    w = _device_window(window, win_length, n_fft, dev)
+    o = [None, None, None, None]
+    if outputs[0]:
+        o[0] = torch.empty(batch, F, n_frames, device=dev, dtype=torch.float32)
+    if outputs[1]:
+        o[1] = (torch.empty(batch, F, n_frames, device=dev, dtype=torch.complex64)
+                if mode == FEAT_CNNBLSTM else
+                torch.empty(batch, F, n_frames, device=dev, dtype=torch.float32))
+    if outputs[2]:
+        o[2] = torch.empty(batch, F, n_frames, device=dev, dtype=torch.float32)
+    if outputs[3] and mode == FEAT_GAN:
+        o[3] = torch.empty(batch, F, n_frames, device=dev, dtype=torch.float32)
+    call("ainp_stft_features", audio.data_ptr(), n_clips, S, _p(clip_index),
+         gap_start.data_ptr(), batch, int(gap_len), int(sample_rate), w.data_ptr(),
+         int(n_fft), int(hop), n_frames, int(mode), _p(o[0]), _p(o[1]), _p(o[2]),
+         _p(o[3]), _stream(audio))
+    return tuple(o)
+
+
+# --------------------------------------------------------------------- GEMM
+def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
+         strideA=0, strideB=0, strideC=0, bias1=None, bias2=None, nstrided=1,
+         ksplit=False, stream_of=None):
+    """Raw strided/batched GEMM (ainp_gemm_f32).  A, B, C, bias1, bias2 are
+    lists (pointer batches) of cuda float32 tensors (views allowed) or None."""
+    A = list(A); B = list(B); C = list(C)
+    nptr = len(A)
+    assert len(B) == nptr and len(C) == nptr and 1 <= nptr <= 8
+    ref = C[0]
+    b1 = ptr_array([_p(t) for t in bias1]) if bias1 is not None else None
+    b2 = ptr_array([_p(t) for t in bias2]) if bias2 is not None else None
+    call("ainp_gemm_f32", int(M), int(N), int(K), float(alpha),
+         ptr_array([t.data_ptr() for t in A]), int(sam), int(sak), int(strideA),
+         ptr_array([t.data_ptr() for t in B]), int(sbk), int(sbn), int(strideB),
+         float(beta), ptr_array([t.data_ptr() for t in C]), int(scm), int(scn),
+         int(strideC), b1, b2, nptr, int(nstrided), 1 if ksplit else 0,
+         _stream(ref if stream_of is None else stream_of))
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
+    """y = x @ w^T + b for x [M, K] row-major (nn.Linear semantics)."""
+    _req(x, "x"); _req(w, "w")
+    M, K = x.shape
+    N = w.shape[0]
+    y = torch.empty(M, N, device=x.device, dtype=torch.float32)
+    gemm(M, N, K, [x], K, 1, [w], 1, K, [y], N, 1,
+         bias1=[b] if b is not None else None)
+    return y
+
+
+def matmul(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """a [M,K] @ b [K,N] for 2-D float32 cuda tensors (any unit-stride layout)."""
+    _req(a, "a", contiguous=False); _req(b, "b", contiguous=False)
+    M, K = a.shape
+    K2, N = b.shape
+    assert K == K2
+    c = torch.empty(M, N, device=a.device, dtype=torch.float32)
+    sam, sak = a.stride()
+    sbk, sbn = b.stride()
+    if sam != 1 and sak != 1:
+        a = a.contiguous(); sam, sak = a.stride()
+    if sbk != 1 and sbn != 1:
+        b = b.contiguous(); sbk, sbn = b.stride()
+    gemm(M, N, K, [a], sam, sak, [b], sbk, sbn, [c], N, 1)
+    return c
+
+
+# --------------------------------------------------------------------- conv
+def conv_stat_parts(N, H, W) -> int:
+    return _lib.lib.ainp_conv3x3_fwd_stat_parts(N, H, W)
+
+
+def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False):
+    _req(x, "x"); _req(w, "w")
+    N, Cin, H, W = x.shape
+    Cout = w.shape[0]
+    assert tuple(w.shape) == (Cout, Cin, 3, 3)
+    y = torch.empty(N, Cout, H, W, device=x.device, dtype=torch.float32)
+    stats = None
+    if want_stats:
+        stats = torch.empty(conv_stat_parts(N, H, W), 2 * Cout, device=x.device,
+                            dtype=torch.float64)
+    call("ainp_conv3x3_fwd", x.data_ptr(), w.data_ptr(), _p(b), _p(in_scale),
+         _p(in_shift), y.data_ptr(), _p(stats), N, Cin, Cout, H, W, _stream(x))
+    return y, stats
+
+
+def conv3x3_dgrad(dy, w):
+    _req(dy, "dy"); _req(w, "w")
+    N, Cout, H, W = dy.shape
+    Cin = w.shape[1]
+    dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=torch.float32)
+    call("ainp_conv3x3_dgrad", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), None,
+         N, Cin, Cout, H, W, _stream(dy))
+    return dx
+
+
+def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True):
+    _req(x, "x"); _req(dy, "dy")
+    N, Cin, H, W = x.shape
+    Cout = dy.shape[1]
+    dw = torch.empty(Cout, Cin, 3, 3, device=x.device, dtype=torch.float32)
+    db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
+    ws_bytes = _lib.lib.ainp_conv3x3_wgrad_workspace(N, Cin, Cout, H, W)
+    ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
+    call("ainp_conv3x3_wgrad", x.data_ptr(), _p(in_scale), _p(in_shift), dy.data_ptr(),
+         dw.data_ptr(), _p(db), ws.data_ptr(), N, Cin, Cout, H, W, _stream(x))
+    return dw, db
+
+
+# --------------------------------------------------------------------- BN
+def bn_stats_reduce(stats, C):
+    """conv epilogue partials [parts, 2C] -> per-channel [sum y | sum y^2] (f64)."""
+    sums = torch.empty(2 * C, device=stats.device, dtype=torch.float64)
+    call("ainp_bn_stats_reduce", stats.data_ptr(), stats.shape[0], sums.data_ptr(), C,
+         _stream(stats))
+    return sums
+
+
+def bn_finalize(sums, count, gamma, beta, running_mean, running_var, momentum, eps):
+    C = sums.numel() // 2
+    dev = sums.device
+    scale = torch.empty(C, device=dev, dtype=torch.float32)
+    shift = torch.empty(C, device=dev, dtype=torch.float32)
+    save = torch.empty(2, C, device=dev, dtype=torch.float32)
+    call("ainp_bn_finalize", sums.data_ptr(), int(count), _p(gamma), _p(beta),
+         _p(running_mean), _p(running_var), float(momentum), float(eps), scale.data_ptr(),
+         shift.data_ptr(), save.data_ptr(), C, _stream(sums))
+    return scale, shift, save
+
+
+def bn_eval_affine(gamma, beta, running_mean, running_var, eps):
+    C = running_mean.numel()
+    dev = running_mean.device
+    scale = torch.empty(C, device=dev, dtype=torch.float32)
+    shift = torch.empty(C, device=dev, dtype=torch.float32)
+    call("ainp_bn_eval_affine", _p(gamma), _p(beta), running_mean.data_ptr(),
+         running_var.data_ptr(), float(eps), scale.data_ptr(), shift.data_ptr(), C,
+         _stream(running_mean))
+    return scale, shift
+
+
+def bn_relu_apply(x, scale, shift, ntcf=False):
+    _req(x, "x")
+    N, C, H, W = x.shape
+    if ntcf:
+        out = torch.empty(N, W, C * H, device=x.device, dtype=torch.float32)
+    else:
+        out = torch.empty_like(x)
+    call("ainp_bn_relu_apply", x.data_ptr(), scale.data_ptr(), shift.data_ptr(),
+         out.data_ptr(), N, C, H, W, 1 if ntcf else 0, _stream(x))
+    return out
+
+
+def bn_relu_bwd_reduce(g, y, scale, shift, save, ntcf=False):
+    _req(g, "g"); _req(y, "y")
+    N, C, H, W = y.shape
+    ws = torch.empty(_lib.lib.ainp_bn_relu_bwd_workspace(N, C, H, W), device=y.device,
+                     dtype=torch.uint8)
+    sums = torch.empty(2 * C, device=y.device, dtype=torch.float64)
+    call("ainp_bn_relu_bwd_reduce", g.data_ptr(), y.data_ptr(), scale.data_ptr(),
+         shift.data_ptr(), save.data_ptr(), ws.data_ptr(), sums.data_ptr(), N, C, H, W,
+         1 if ntcf else 0, _stream(y))
+    return sums
+
+
+def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False):
+    N, C, H, W = y.shape
+    gy = torch.empty_like(y)
+    dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
+    dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
+    call("ainp_bn_relu_bwd_apply", g.data_ptr(), y.data_ptr(), scale.data_ptr(),
+         shift.data_ptr(), _p(gamma), save.data_ptr(), sums.data_ptr(), int(count),
+         gy.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), N, C, H, W, 1 if ntcf else 0,
+         _stream(y))
+    return gy, dgamma, dbeta
+
+
+def bn_relu_bwd(g, y, scale, shift, gamma, save, ntcf=False):
+    N, C, H, W = y.shape
+    sums = bn_relu_bwd_reduce(g, y, scale, shift, save, ntcf)
+    return bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, N * H * W, ntcf)
+
+
+# --------------------------------------------------------------------- LSTM
+def lstm_rec_fwd(zx, whh_f, whh_r, H, save=True):
+    _req(zx, "zx"); _req(whh_f, "whh_f"); _req(whh_r, "whh_r")
+    N, T, G = zx.shape
+    assert G == 8 * H
+    dev = zx.device
+    h_out = torch.empty(N, T, 2 * H, device=dev, dtype=torch.float32)
+    gates = torch.empty(N, T, 8 * H, device=dev, dtype=torch.float32) if save else None
+    cell = torch.empty(N, T, 2 * H, device=dev, dtype=torch.float32) if save else None
+    call("ainp_lstm_rec_fwd", zx.data_ptr(), ptr_array([whh_f.data_ptr(), whh_r.data_ptr()]),
+         h_out.data_ptr(), _p(gates), _p(cell), N, T, H, _stream(zx))
+    return h_out, gates, cell
+
+
+def lstm_rec_bwd(dh_out, gates, cell, whh_f, whh_r, H):
+    _req(dh_out, "dh_out")
+    N, T, _ = dh_out.shape
+    dgates = torch.empty(N, T, 8 * H, device=dh_out.device, dtype=torch.float32)
+    call("ainp_lstm_rec_bwd", dh_out.data_ptr(), gates.data_ptr(), cell.data_ptr(),
+         ptr_array([whh_f.data_ptr(), whh_r.data_ptr()]), dgates.data_ptr(), N, T, H,
+         _stream(dh_out))
+    return dgates
+
+
+def lstm_hprev(h_out, H):
+    N, T, _ = h_out.shape
+    hp = torch.empty_like(h_out)
+    call("ainp_lstm_hprev", h_out.data_ptr(), hp.data_ptr(), N, T, H, _stream(h_out))
+    return hp
+
+
+# --------------------------------------------------------------------- loss
+def l1_pow10_loss(y, mask, target, want_grad=True, grad_scale=1.0):
+    """sum |10^y*m - |target|*m| -> (loss float64 [1], dy or None)."""
+    _req(y, "y"); _req(mask, "mask"); _req(target, "target", torch.complex64)
+    n = y.numel()
+    assert mask.numel() == n and target.numel() == n
+    loss = torch.zeros(1, device=y.device, dtype=torch.float64)
+    dy = torch.empty_like(y) if want_grad else None
+    call("ainp_l1_pow10_loss", y.data_ptr(), mask.data_ptr(), target.data_ptr(), n,
+         loss.data_ptr(), _p(dy), float(grad_scale), _stream(y))
+    return loss, dy
+
+
+def colsum(x2d, out=None, accumulate=False):
+    rows, cols = x2d.shape
+    ld = x2d.stride(0)
+    assert x2d.stride(1) == 1
+    if out is None:
+        out = torch.empty(cols, device=x2d.device, dtype=torch.float32)
+    call("ainp_colsum", x2d.data_ptr(), rows, cols, ld, out.data_ptr(),
+         1 if accumulate else 0, _stream(x2d))
+    return out
+
+
+def adam_step(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, eps,
+              weight_decay, step):
+    if not params:
+        return
+    call("ainp_adam", ptr_array([p.data_ptr() for p in params]),
+         ptr_array([g.data_ptr() for g in grads]),
+         ptr_array([m.data_ptr() for m in exp_avgs]),
+         ptr_array([v.data_ptr() for v in exp_avg_sqs]),
+         int64_array([p.numel() for p in params]), len(params), float(lr), float(beta1),
+         float(beta2), float(eps), float(weight_decay), int(step), _stream(params[0]))

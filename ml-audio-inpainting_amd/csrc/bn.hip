@@ -1,0 +1,395 @@
+// bn.hip — BatchNorm2d (train/eval) + ReLU for [N, C, H, W] activations.
+//
+// Replaces nn.BatchNorm2d + nn.ReLU of models/CNNBLSTM/model.py:36-59 and the
+// permute/reshape layout bridge of model.py:73-74 (the last encoder block's
+// output is written straight into the LSTM's [N, T, C*F] layout).
+// Statistics are reduced in float64 from per-workgroup partials in a fixed
+// order, so results are deterministic run to run.
+#include "common.h"
+
+namespace ainp {
+
+// --------------------------------------------------------------- finalize
+// One workgroup per channel: sum the conv epilogue partials
+// stats[part][0:C] = sum y, stats[part][C:2C] = sum y^2  ->  sums[c], sums[C+c].
+__global__ void bn_stats_reduce_kernel(const double* __restrict__ stats,
+                                       int nparts, double* __restrict__ sums,
+                                       int C) {
+  const int c = blockIdx.x;
+  double s = 0.0, q = 0.0;
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
+    s += stats[(int64_t)p * 2 * C + c];
+    q += stats[(int64_t)p * 2 * C + C + c];
+  }
+  __shared__ double rs[4], rq[4];
+  s = wave_sum_d(s);
+  q = wave_sum_d(q);
+  if ((threadIdx.x & 63) == 0) {
+    rs[threadIdx.x >> 6] = s;
+    rq[threadIdx.x >> 6] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    sums[c] = rs[0] + rs[1] + rs[2] + rs[3];
+    sums[C + c] = rq[0] + rq[1] + rq[2] + rq[3];
+  }
+}
+
+// Per channel: mean/var (biased) from the (possibly all-reduced) sums;
+// running stats with the unbiased variance (torch BatchNorm2d train mode).
+__global__ void bn_finalize_kernel(const double* __restrict__ sums,
+                                   const float* __restrict__ gamma,
+                                   const float* __restrict__ beta,
+                                   float* __restrict__ running_mean,
+                                   float* __restrict__ running_var,
+                                   float momentum, float eps, int64_t count,
+                                   float* __restrict__ scale,
+                                   float* __restrict__ shift,
+                                   float* __restrict__ save, int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double mean = sums[c] / (double)count;
+  double var = sums[C + c] / (double)count - mean * mean;
+  if (var < 0.0) var = 0.0;
+  const float rstd = (float)(1.0 / sqrt(var + (double)eps));
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * rstd;
+  shift[c] = b - (float)mean * g * rstd;
+  save[c] = (float)mean;
+  save[C + c] = rstd;
+  if (running_mean) {
+    const double unbiased = count > 1 ? var * (double)count / (double)(count - 1) : var;
+    running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * (float)mean;
+    running_var[c] = (1.f - momentum) * running_var[c] + momentum * (float)unbiased;
+  }
+}
+
+__global__ void bn_eval_affine_kernel(const float* gamma, const float* beta,
+                                      const float* rm, const float* rv,
+                                      float eps, float* scale, float* shift,
+                                      int C) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float rstd = 1.f / sqrtf(rv[c] + eps);
+  const float g = gamma ? gamma[c] : 1.f;
+  const float b = beta ? beta[c] : 0.f;
+  scale[c] = g * rstd;
+  shift[c] = b - rm[c] * g * rstd;
+}
+
+// --------------------------------------------------------------- tiles
+// A tile is 32 (h) x 64 (w) of one (n, c) plane.  NCHW side: lanes along w;
+// NTCF side ([n][w][c*H+h]): lanes along h, staged through LDS.
+constexpr int TH = 32, TW = 64;
+
+struct TileIdx {
+  int n, c, h0, w0;
+};
+__device__ __forceinline__ TileIdx tile_of(int64_t b, int C, int64_t H,
+                                           int64_t W) {
+  const int th = (int)((H + TH - 1) / TH), tw = (int)((W + TW - 1) / TW);
+  TileIdx t;
+  t.w0 = (int)(b % tw) * TW;
+  t.h0 = (int)((b / tw) % th) * TH;
+  t.c = (int)((b / ((int64_t)tw * th)) % C);
+  t.n = (int)(b / ((int64_t)tw * th * C));
+  return t;
+}
+
+// out = relu(x*scale+shift); NCHW -> NCHW or NCHW -> NTCF
+template <bool NTCF>
+__global__ __launch_bounds__(256) void bn_relu_apply_kernel(
+    const float* __restrict__ x, const float* __restrict__ scale,
+    const float* __restrict__ shift, float* __restrict__ out, int C, int64_t H,
+    int64_t W) {
+  __shared__ float tile[TW][TH + 1];
+  const TileIdx ti = tile_of(blockIdx.x, C, H, W);
+  const float sc = scale[ti.c], sh = shift[ti.c];
+  const int tid = threadIdx.x;
+  const float* xp = x + ((int64_t)ti.n * C + ti.c) * H * W;
+  if (!NTCF) {
+    float* op = out + ((int64_t)ti.n * C + ti.c) * H * W;
+    const int tx = tid & 63, ty = tid >> 6;
+    for (int i = 0; i < TH / 4; ++i) {
+      const int64_t h = ti.h0 + ty + 4 * i, w = ti.w0 + tx;
+      if (h < H && w < W) op[h * W + w] = fmaxf(fmaf(xp[h * W + w], sc, sh), 0.f);
+    }
+  } else {
+    const int tx = tid & 63, ty = tid >> 6;
+    for (int i = 0; i < TH / 4; ++i) {
+      const int hh = ty + 4 * i;
+      const int64_t h = ti.h0 + hh, w = ti.w0 + tx;
+      float v = 0.f;
+      if (h < H && w < W) v = fmaxf(fmaf(xp[h * W + w], sc, sh), 0.f);
+      tile[tx][hh] = v;
+    }
+    __syncthreads();
+    // write [n][w][c*H + h], lanes along h
+    const int hx = tid & 31, wy = tid >> 5;  // 32 x 8
+    const int64_t CH = (int64_t)C * H;
+    for (int i = 0; i < TW / 8; ++i) {
+      const int ww = wy + 8 * i;
+      const int64_t h = ti.h0 + hx, w = ti.w0 + ww;
+      if (h < H && w < W) out[((int64_t)ti.n * W + w) * CH + (int64_t)ti.c * H + h] = tile[ww][hx];
+    }
+  }
+}
+
+// Load a tile of g (NCHW or NTCF) into LDS tile[w][h] layout.
+template <bool NTCF>
+__device__ __forceinline__ void load_g_tile(const float* __restrict__ g,
+                                            const TileIdx& ti, int C,
+                                            int64_t H, int64_t W,
+                                            float (*tile)[TH + 1]) {
+  const int tid = threadIdx.x;
+  if (NTCF) {
+    const int hx = tid & 31, wy = tid >> 5;
+    const int64_t CH = (int64_t)C * H;
+    for (int i = 0; i < TW / 8; ++i) {
+      const int ww = wy + 8 * i;
+      const int64_t h = ti.h0 + hx, w = ti.w0 + ww;
+      float v = 0.f;
+      if (h < H && w < W) v = g[((int64_t)ti.n * W + w) * CH + (int64_t)ti.c * H + h];
+      tile[ww][hx] = v;
+    }
+  } else {
+    const int tx = tid & 63, ty = tid >> 6;
+    const float* gp = g + ((int64_t)ti.n * C + ti.c) * H * W;
+    for (int i = 0; i < TH / 4; ++i) {
+      const int hh = ty + 4 * i;
+      const int64_t h = ti.h0 + hh, w = ti.w0 + tx;
+      tile[tx][hh] = (h < H && w < W) ? gp[h * W + w] : 0.f;
+    }
+  }
+  __syncthreads();
+}
+
+// partial[tile][0] = sum gz, partial[tile][1] = sum gz*xhat
+template <bool NTCF>
+__global__ __launch_bounds__(256) void bn_relu_bwd_reduce_kernel(
+    const float* __restrict__ g, const float* __restrict__ y,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ save, double* __restrict__ partial, int C,
+    int64_t H, int64_t W) {
+  __shared__ float tile[TW][TH + 1];
+  __shared__ double red[2][4];
+  const TileIdx ti = tile_of(blockIdx.x, C, H, W);
+  load_g_tile<NTCF>(g, ti, C, H, W, tile);
+  const float sc = scale[ti.c], sh = shift[ti.c];
+  const float mean = save[ti.c], rstd = save[C + ti.c];
+  const float* yp = y + ((int64_t)ti.n * C + ti.c) * H * W;
+  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
+  float s1 = 0.f, s2 = 0.f;
+  for (int i = 0; i < TH / 4; ++i) {
+    const int hh = ty + 4 * i;
+    const int64_t h = ti.h0 + hh, w = ti.w0 + tx;
+    if (h < H && w < W) {
+      const float yv = yp[h * W + w];
+      const float gz = (fmaf(yv, sc, sh) > 0.f) ? tile[tx][hh] : 0.f;
+      s1 += gz;
+      s2 += gz * ((yv - mean) * rstd);
+    }
+  }
+  double d1 = wave_sum_d((double)s1), d2 = wave_sum_d((double)s2);
+  if ((tid & 63) == 0) {
+    red[0][tid >> 6] = d1;
+    red[1][tid >> 6] = d2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    partial[(int64_t)blockIdx.x * 2 + 0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    partial[(int64_t)blockIdx.x * 2 + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+// Sum tile partials per channel: sums[c] = sum gz, sums[C+c] = sum gz*xhat
+__global__ void bn_bwd_sum_kernel(const double* __restrict__ partial, int N,
+                                  int C, int tiles_per_plane,
+                                  double* __restrict__ sums) {
+  const int c = blockIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  const int per = N * tiles_per_plane;
+  for (int i = threadIdx.x; i < per; i += blockDim.x) {
+    const int n = i / tiles_per_plane, t = i % tiles_per_plane;
+    const int64_t b = ((int64_t)n * C + c) * tiles_per_plane + t;
+    s1 += partial[b * 2];
+    s2 += partial[b * 2 + 1];
+  }
+  __shared__ double r1[4], r2[4];
+  s1 = wave_sum_d(s1);
+  s2 = wave_sum_d(s2);
+  if ((threadIdx.x & 63) == 0) {
+    r1[threadIdx.x >> 6] = s1;
+    r2[threadIdx.x >> 6] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    s1 = r1[0] + r1[1] + r1[2] + r1[3];
+    s2 = r2[0] + r2[1] + r2[2] + r2[3];
+    sums[c] = s1;
+    sums[C + c] = s2;
+  }
+}
+
+// gy = gamma*rstd*(gz - sum(gz)/M - xhat*sum(gz*xhat)/M), NCHW out
+template <bool NTCF>
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(
+    const float* __restrict__ g, const float* __restrict__ y,
+    const float* __restrict__ scale, const float* __restrict__ shift,
+    const float* __restrict__ gamma, const float* __restrict__ save,
+    const double* __restrict__ sums, float* __restrict__ gy,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int C, int64_t H,
+    int64_t W, double inv_count) {
+  __shared__ float tile[TW][TH + 1];
+  const TileIdx ti = tile_of(blockIdx.x, C, H, W);
+  if (blockIdx.x < (unsigned)C && threadIdx.x == 0) {
+    if (dbeta) dbeta[blockIdx.x] = (float)sums[blockIdx.x];
+    if (dgamma) dgamma[blockIdx.x] = (float)sums[C + blockIdx.x];
+  }
+  load_g_tile<NTCF>(g, ti, C, H, W, tile);
+  const float sc = scale[ti.c], sh = shift[ti.c];
+  const float mean = save[ti.c], rstd = save[C + ti.c];
+  const float gm = gamma ? gamma[ti.c] : 1.f;
+  const float k = gm * rstd;
+  const float m1 = (float)(sums[ti.c] * inv_count);
+  const float m2 = (float)(sums[C + ti.c] * inv_count);
+  const int64_t off = ((int64_t)ti.n * C + ti.c) * H * W;
+  const float* yp = y + off;
+  float* gp = gy + off;
+  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
+  for (int i = 0; i < TH / 4; ++i) {
+    const int hh = ty + 4 * i;
+    const int64_t h = ti.h0 + hh, w = ti.w0 + tx;
+    if (h < H && w < W) {
+      const float yv = yp[h * W + w];
+      const float gz = (fmaf(yv, sc, sh) > 0.f) ? tile[tx][hh] : 0.f;
+      const float xh = (yv - mean) * rstd;
+      gp[h * W + w] = k * (gz - m1 - xh * m2);
+    }
+  }
+}
+
+static int64_t tiles_per_plane(int64_t H, int64_t W) {
+  return cdiv(H, TH) * cdiv(W, TW);
+}
+
+}  // namespace ainp
+
+using namespace ainp;
+
+extern "C" int ainp_bn_stats_reduce(const double* stats, int nparts,
+                                    double* sums, int C, void* stream) {
+  if (!stats || nparts < 1 || !sums || C < 1)
+    return record_msg("ainp_bn_stats_reduce: bad argument");
+  hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3(C), dim3(256), 0,
+                     as_stream(stream), stats, nparts, sums, C);
+  return check_launch("bn_stats_reduce");
+}
+
+extern "C" int ainp_bn_finalize(const double* sums, int64_t count,
+                                const float* gamma, const float* beta,
+                                float* running_mean, float* running_var,
+                                float momentum, float eps, float* scale,
+                                float* shift, float* save_mean_rstd, int C,
+                                void* stream) {
+  if (!sums || !scale || !shift || !save_mean_rstd || C < 1 || count < 1 ||
+      ((running_mean == nullptr) != (running_var == nullptr)))
+    return record_msg("ainp_bn_finalize: bad argument");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0,
+                     as_stream(stream), sums, gamma, beta, running_mean,
+                     running_var, momentum, eps, count, scale, shift,
+                     save_mean_rstd, C);
+  return check_launch("bn_finalize");
+}
+
+extern "C" int ainp_bn_eval_affine(const float* gamma, const float* beta,
+                                   const float* running_mean,
+                                   const float* running_var, float eps,
+                                   float* scale, float* shift, int C,
+                                   void* stream) {
+  if (!running_mean || !running_var || !scale || !shift || C < 1)
+    return record_msg("ainp_bn_eval_affine: bad argument");
+  hipLaunchKernelGGL(bn_eval_affine_kernel, dim3((C + 63) / 64), dim3(64), 0,
+                     as_stream(stream), gamma, beta, running_mean, running_var,
+                     eps, scale, shift, C);
+  return check_launch("bn_eval_affine");
+}
+
+extern "C" int ainp_bn_relu_apply(const float* x, const float* scale,
+                                  const float* shift, float* out, int64_t N,
+                                  int C, int64_t H, int64_t W, int out_ntcf,
+                                  void* stream) {
+  if (!x || !scale || !shift || !out || N < 0 || C < 1 || H < 1 || W < 1)
+    return record_msg("ainp_bn_relu_apply: bad argument");
+  if (N == 0) return AINP_OK;
+  const int64_t blocks = N * C * tiles_per_plane(H, W);
+  hipStream_t s = as_stream(stream);
+  if (out_ntcf)
+    hipLaunchKernelGGL(bn_relu_apply_kernel<true>, dim3((unsigned)blocks),
+                       dim3(256), 0, s, x, scale, shift, out, C, H, W);
+  else
+    hipLaunchKernelGGL(bn_relu_apply_kernel<false>, dim3((unsigned)blocks),
+                       dim3(256), 0, s, x, scale, shift, out, C, H, W);
+  return check_launch("bn_relu_apply");
+}
+
+extern "C" size_t ainp_bn_relu_bwd_workspace(int64_t N, int C, int64_t H,
+                                             int64_t W) {
+  return (size_t)(N * C * tiles_per_plane(H, W) * 2) * sizeof(double);
+}
+
+extern "C" int ainp_bn_relu_bwd_reduce(const float* g, const float* y,
+                                       const float* scale, const float* shift,
+                                       const float* save_mean_rstd,
+                                       void* workspace, double* sums,
+                                       int64_t N, int C, int64_t H, int64_t W,
+                                       int g_ntcf, void* stream) {
+  if (!g || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
+      N < 1 || C < 1 || H < 1 || W < 1)
+    return record_msg("ainp_bn_relu_bwd_reduce: bad argument");
+  const int64_t tpp = tiles_per_plane(H, W);
+  const int64_t blocks = N * C * tpp;
+  double* partial = reinterpret_cast<double*>(workspace);
+  hipStream_t s = as_stream(stream);
+  if (g_ntcf)
+    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<true>, dim3((unsigned)blocks),
+                       dim3(256), 0, s, g, y, scale, shift, save_mean_rstd,
+                       partial, C, H, W);
+  else
+    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<false>, dim3((unsigned)blocks),
+                       dim3(256), 0, s, g, y, scale, shift, save_mean_rstd,
+                       partial, C, H, W);
+  int rc = check_launch("bn_relu_bwd_reduce");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial,
+                     (int)N, C, (int)tpp, sums);
+  return check_launch("bn_bwd_sum");
+}
+
+extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
+                                      const float* scale, const float* shift,
+                                      const float* gamma,
+                                      const float* save_mean_rstd,
+                                      const double* sums, int64_t count,
+                                      float* gy, float* dgamma, float* dbeta,
+                                      int64_t N, int C, int64_t H, int64_t W,
+                                      int g_ntcf, void* stream) {
+  if (!g || !y || !scale || !shift || !save_mean_rstd || !sums || !gy ||
+      N < 1 || C < 1 || H < 1 || W < 1 || count < 1)
+    return record_msg("ainp_bn_relu_bwd_apply: bad argument");
+  const int64_t blocks = N * C * tiles_per_plane(H, W);
+  const double inv_count = 1.0 / (double)count;
+  hipStream_t s = as_stream(stream);
+  if (g_ntcf)
+    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<true>, dim3((unsigned)blocks),
+                       dim3(256), 0, s, g, y, scale, shift, gamma,
+                       save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W,
+                       inv_count);
+  else
+    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<false>, dim3((unsigned)blocks),
+                       dim3(256), 0, s, g, y, scale, shift, gamma,
+                       save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W,
+                       inv_count);
+  return check_launch("bn_relu_bwd_apply");
+}

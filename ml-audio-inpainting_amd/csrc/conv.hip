@@ -1,0 +1,448 @@
+// conv.hip — 3x3 / stride 1 / pad 1 convolution over [N, C, F, T] on the
+// gfx950 f32-input MFMA (v_mfma_f32_16x16x4_f32, exact fp32).
+//
+// Replaces nn.Conv2d(k=3, p=1) of models/CNNBLSTM/model.py:35-60 (forward,
+// data gradient, weight gradient).  Implicit GEMM, nothing im2col'd in HBM:
+//   forward  D[pixel][co]       = sum_{ci,tap} act(x)[ci][pixel+tap] * w[co][ci][tap]
+//   dgrad    same kernel on dy with w'[ci][co][tap] = w[co][ci][8-tap]
+//   wgrad    D[co][(tap,ci)]    = sum_pixel dy[co][pixel] * act(x)[ci][pixel+tap]
+// act(x) = relu(x*scale[c]+shift[c]) is the previous BatchNorm2d+ReLU applied
+// while staging the input tile into LDS (never materialised in HBM); zero
+// padding is applied after act, as nn.Conv2d pads its post-ReLU input.
+//
+// Forward tile: one workgroup = one example, 8 rows (f) x 48 columns (t);
+// each of the 4 waves owns 2 rows x 3 sixteen-pixel MFMA row tiles x CT
+// sixteen-channel column tiles (CT = ceil(Cout/16)).  K = Cin*9 is walked in
+// chunks of 8 input channels; LDS k order inside a chunk is (tap, ci) so the
+// A-operand address is lane-constant + compile-time immediate.
+#include "common.h"
+
+namespace ainp {
+
+// ---------------------------------------------------------------- forward
+constexpr int CV_FT = 8;          // rows per tile
+constexpr int CV_TT = 48;         // columns per tile (3 MFMA tiles)
+constexpr int CV_CK = 8;          // input channels per K chunk
+constexpr int CV_LDT = 52;        // LDS row length (>= TT+2)
+constexpr int CV_PLANE = 528;     // >= (FT+2)*LDT, == 16 mod 32 (conflict-free A)
+constexpr int CV_KCH = CV_CK * 9; // k per chunk = 72
+
+template <int CT>
+struct FwdLds {
+  static constexpr int LDW = (CT * 16) % 32 == 0 ? CT * 16 + 16 : CT * 16;
+  static constexpr int IN = CV_CK * CV_PLANE;
+  static constexpr int WT = CV_KCH * LDW;
+};
+
+__host__ __device__ constexpr int fwd_stat_parts_dims(int) { return 0; }
+
+template <int CT, bool DGRAD>
+__global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
+    const float* __restrict__ x, const float* __restrict__ w,
+    const float* __restrict__ bias, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, float* __restrict__ y,
+    double* __restrict__ stats, int Cin, int Cout, int H, int W) {
+  using L = FwdLds<CT>;
+  __shared__ __attribute__((aligned(16))) float s_in[L::IN];
+  __shared__ __attribute__((aligned(16))) float s_w[L::WT];
+  __shared__ double s_red[2 * 4 * CT * 16];
+
+  const int n = blockIdx.z;
+  const int f0 = blockIdx.y * CV_FT;
+  const int t0 = blockIdx.x * CV_TT;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, kq = lane >> 4;
+  const int64_t HW = (int64_t)H * W;
+  const float* xn = x + (int64_t)n * Cin * HW;
+
+  f32x4 acc[2][3][CT];
+#pragma unroll
+  for (int r = 0; r < 2; ++r)
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int c = 0; c < CT; ++c) acc[r][p][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunk = (Cin + CV_CK - 1) / CV_CK;
+  for (int ch = 0; ch < nchunk; ++ch) {
+    const int ci0 = ch * CV_CK;
+    // stage input halo tile [CK][FT+2][TT+2] with prologue + zero padding
+    for (int idx = tid; idx < CV_CK * (CV_FT + 2) * (CV_TT + 2); idx += 256) {
+      const int cc = idx % (CV_TT + 2);
+      const int rr = (idx / (CV_TT + 2)) % (CV_FT + 2);
+      const int ci = idx / ((CV_TT + 2) * (CV_FT + 2));
+      const int f = f0 + rr - 1, t = t0 + cc - 1, cg = ci0 + ci;
+      float v = 0.f;
+      if (cg < Cin && f >= 0 && f < H && t >= 0 && t < W) {
+        v = xn[(int64_t)cg * HW + (int64_t)f * W + t];
+        if (in_scale) v = fmaxf(fmaf(v, in_scale[cg], in_shift[cg]), 0.f);
+      }
+      s_in[ci * CV_PLANE + rr * CV_LDT + cc] = v;
+    }
+    // stage weights as [k = tap*8+ci][co]
+    for (int idx = tid; idx < CV_KCH * CT * 16; idx += 256) {
+      const int co = idx % (CT * 16);
+      const int k = idx / (CT * 16);
+      const int tap = k >> 3, ci = k & 7, cg = ci0 + ci;
+      float v = 0.f;
+      if (cg < Cin && co < Cout) {
+        if (DGRAD)  // conv input channel cg = forward output channel
+          v = w[((int64_t)cg * Cout + co) * 9 + (8 - tap)];
+        else
+          v = w[((int64_t)co * Cin + cg) * 9 + tap];
+      }
+      s_w[k * L::LDW + co] = v;
+    }
+    __syncthreads();
+
+    const float* a_base = s_in + kq * CV_PLANE + li;
+    const float* b_base = s_w + kq * L::LDW + li;
+#pragma unroll
+    for (int s = 0; s < 18; ++s) {
+      const int tap = s >> 1, cb = (s & 1) * 4;
+      const int df = tap / 3, dt = tap % 3;
+      float bf[CT];
+#pragma unroll
+      for (int c = 0; c < CT; ++c) bf[c] = b_base[(s * 4) * L::LDW + c * 16];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const float af =
+              a_base[cb * CV_PLANE + (wave * 2 + r + df) * CV_LDT + p * 16 + dt];
+#pragma unroll
+          for (int c = 0; c < CT; ++c) acc[r][p][c] = mfma16x16x4(af, bf[c], acc[r][p][c]);
+        }
+    }
+    __syncthreads();
+  }
+
+  // epilogue: D[pixel = 4*kq + j][co = li] in register j
+  float* yn = y + (int64_t)n * Cout * HW;
+  float psum[CT], psq[CT];
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    psum[c] = 0.f;
+    psq[c] = 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < CT; ++c) {
+    const int co = c * 16 + li;
+    const bool cok = co < Cout;
+    const float bv = (bias && cok) ? bias[co] : 0.f;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const int f = f0 + wave * 2 + r;
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int t = t0 + p * 16 + kq * 4 + j;
+          if (cok && f < H && t < W) {
+            const float v = acc[r][p][c][j] + bv;
+            yn[(int64_t)co * HW + (int64_t)f * W + t] = v;
+            psum[c] += v;
+            psq[c] += v * v;
+          }
+        }
+    }
+  }
+  if (stats) {
+    // reduce over the 4 lane groups sharing a channel, then over waves
+#pragma unroll
+    for (int c = 0; c < CT; ++c) {
+      double a = psum[c], b = psq[c];
+      a += __shfl_xor(a, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 16, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (kq == 0) {
+        s_red[(wave * CT + c) * 16 + li] = a;
+        s_red[4 * CT * 16 + (wave * CT + c) * 16 + li] = b;
+      }
+    }
+    __syncthreads();
+    const int64_t part = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+    for (int co = tid; co < Cout; co += 256) {
+      const int c = co >> 4, l = co & 15;
+      double a = 0.0, b = 0.0;
+      for (int wv = 0; wv < 4; ++wv) {
+        a += s_red[(wv * CT + c) * 16 + l];
+        b += s_red[4 * CT * 16 + (wv * CT + c) * 16 + l];
+      }
+      stats[part * 2 * Cout + co] = a;
+      stats[part * 2 * Cout + Cout + co] = b;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- wgrad
+// Persistent workgroups each reduce a strided set of 4x64 pixel tiles into
+// register accumulators D[co][j], j = tap*Cin + ci, then write one partial
+// slab; a second kernel sums the slabs in fixed order (deterministic).
+constexpr int WG_FT = 4, WG_TT = 64;
+constexpr int WG_LDT = 68;         // >= TT+2
+constexpr int WG_XPLANE = 418;     // >= (FT+2)*LDT = 408, == 2 mod 32
+constexpr int WG_GPLANE = 258;     // >= FT*TT = 256, == 2 mod 32 (dy tile)
+constexpr int WG_CIMAX = 32;       // input channels staged per pass
+
+template <int CT, int JT>
+__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_mfma(
+    const float* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const float* __restrict__ dy,
+    float* __restrict__ partial, int N, int Cin, int Cout, int H, int W,
+    int ci0, int cin_pass) {
+  // this pass covers input channels [ci0, ci0+cin_pass), j = tap*cin_pass+ci
+  __shared__ __attribute__((aligned(16))) float s_x[WG_CIMAX * WG_XPLANE];
+  __shared__ __attribute__((aligned(16))) float s_g[64 * WG_GPLANE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, kq = lane >> 4;
+  // wave -> (co tile, subset of j tiles)
+  constexpr int WPC = 4 / CT;                 // waves per co tile
+  constexpr int JPW = (JT + WPC - 1) / WPC;   // j tiles per wave
+  const int ct = wave / WPC;
+  const int jt0 = (wave % WPC) * JPW;
+  const int J = 9 * cin_pass;
+
+  // per-lane B offsets (ci, tap) for each of the wave's j tiles
+  int boff[JPW];
+#pragma unroll
+  for (int q = 0; q < JPW; ++q) {
+    const int j = (jt0 + q) * 16 + li;
+    int o = 0;
+    if (j < J) {
+      const int tap = j / cin_pass, ci = j % cin_pass;
+      o = ci * WG_XPLANE + (tap / 3) * WG_LDT + (tap % 3);
+    }
+    boff[q] = o;
+  }
+  f32x4 acc[JPW];
+#pragma unroll
+  for (int q = 0; q < JPW; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbias = 0.f;
+
+  const int tiles_t = (W + WG_TT - 1) / WG_TT;
+  const int tiles_f = (H + WG_FT - 1) / WG_FT;
+  const int64_t ntiles = (int64_t)N * tiles_f * tiles_t;
+  const int64_t HW = (int64_t)H * W;
+  const bool ct_ok = ct < CT && wave < CT * WPC;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int tt = tile % tiles_t;
+    const int tf = (tile / tiles_t) % tiles_f;
+    const int n = tile / ((int64_t)tiles_t * tiles_f);
+    const int f0 = tf * WG_FT, t0 = tt * WG_TT;
+    // stage act(x) halo tile
+    for (int idx = tid; idx < cin_pass * (WG_FT + 2) * (WG_TT + 2); idx += 256) {
+      const int cc = idx % (WG_TT + 2);
+      const int rr = (idx / (WG_TT + 2)) % (WG_FT + 2);
+      const int ci = idx / ((WG_TT + 2) * (WG_FT + 2));
+      const int f = f0 + rr - 1, t = t0 + cc - 1, cg = ci0 + ci;
+      float v = 0.f;
+      if (f >= 0 && f < H && t >= 0 && t < W) {
+        v = x[((int64_t)n * Cin + cg) * HW + (int64_t)f * W + t];
+        if (in_scale) v = fmaxf(fmaf(v, in_scale[cg], in_shift[cg]), 0.f);
+      }
+      s_x[ci * WG_XPLANE + rr * WG_LDT + cc] = v;
+    }
+    // stage dy tile [co][FT*TT] (zero outside the image)
+    for (int idx = tid; idx < CT * 16 * WG_FT * WG_TT; idx += 256) {
+      const int cc = idx % WG_TT;
+      const int rr = (idx / WG_TT) % WG_FT;
+      const int co = idx / (WG_TT * WG_FT);
+      const int f = f0 + rr, t = t0 + cc;
+      float v = 0.f;
+      if (co < Cout && f < H && t < W)
+        v = dy[((int64_t)n * Cout + co) * HW + (int64_t)f * W + t];
+      s_g[co * WG_GPLANE + rr * WG_TT + cc] = v;
+    }
+    __syncthreads();
+    if (ct_ok) {
+      const float* ga = s_g + (ct * 16 + li) * WG_GPLANE + kq;
+#pragma unroll 4
+      for (int s = 0; s < WG_FT * WG_TT / 4; ++s) {
+        // pixel for this lane: p = 4s + kq  -> (row, col)
+        const int p = 4 * s + kq;
+        const int rr = p / WG_TT, cc = p % WG_TT;
+        const float af = ga[4 * s];
+        dbias += af;
+        const float* xb = s_x + rr * WG_LDT + cc;
+#pragma unroll
+        for (int q = 0; q < JPW; ++q) acc[q] = mfma16x16x4(af, xb[boff[q]], acc[q]);
+      }
+    }
+    __syncthreads();
+  }
+  // write partial slab: [Cout_pad=CT*16][J] for this block (+ bias partial)
+  float* slab = partial + (int64_t)blockIdx.x * (CT * 16) * (J + 1);
+  if (ct_ok) {
+#pragma unroll
+    for (int q = 0; q < JPW; ++q) {
+      const int j = (jt0 + q) * 16 + li;
+      if (jt0 + q < JT && j < J) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int co = ct * 16 + kq * 4 + r;
+          slab[co * (J + 1) + j] = acc[q][r];
+        }
+      }
+    }
+    // bias partial: lanes li hold co = ct*16+li summed over their kq pixels
+    float d = dbias;
+    d += __shfl_xor(d, 16, 64);
+    d += __shfl_xor(d, 32, 64);
+    if (kq == 0 && (wave % WPC) == 0) slab[(ct * 16 + li) * (J + 1) + J] = d;
+  }
+}
+
+// Sum the per-block slabs: out dw[co][ci0+ci][tap], dbias[co].
+__global__ void wgrad_reduce(const float* __restrict__ partial, int nparts,
+                             int CTp, int J, int cin_pass, int ci0, int Cin,
+                             int Cout, float* __restrict__ dw,
+                             float* __restrict__ dbias, int write_bias) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int per = CTp * (J + 1);
+  if (idx >= per) return;
+  const int co = idx / (J + 1), j = idx % (J + 1);
+  if (co >= Cout) return;
+  double s = 0.0;
+  for (int b = 0; b < nparts; ++b) s += partial[(int64_t)b * per + idx];
+  if (j == J) {
+    if (write_bias && dbias) dbias[co] = (float)s;
+  } else {
+    const int tap = j / cin_pass, ci = j % cin_pass;
+    dw[((int64_t)co * Cin + ci0 + ci) * 9 + tap] = (float)s;
+  }
+}
+
+constexpr int WG_BLOCKS = 512;
+
+static int wgrad_ct(int Cout) { return (Cout + 15) / 16; }
+static int wgrad_pass(int Cin) { return Cin < WG_CIMAX ? Cin : WG_CIMAX; }
+
+template <int CT, int JT>
+static void launch_wgrad(const float* x, const float* sc, const float* sh,
+                         const float* dy, float* partial, int N, int Cin,
+                         int Cout, int H, int W, int ci0, int cp,
+                         hipStream_t s) {
+  hipLaunchKernelGGL((conv3x3_wgrad_mfma<CT, JT>), dim3(WG_BLOCKS), dim3(256),
+                     0, s, x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp);
+}
+
+}  // namespace ainp
+
+using namespace ainp;
+
+extern "C" int ainp_conv3x3_fwd_stat_parts(int64_t N, int64_t H, int64_t W) {
+  return (int)(N * cdiv(H, CV_FT) * cdiv(W, CV_TT));
+}
+
+template <bool DG>
+static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
+                             const float* sc, const float* sh, float* y,
+                             double* stats, int64_t N, int Cin, int Cout,
+                             int64_t H, int64_t W, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
+  const int ct = (Cout + 15) / 16;
+#define AINP_FWD(CTV)                                                           \
+  hipLaunchKernelGGL((conv3x3_fwd_mfma<CTV, DG>), grid, dim3(256), 0, s, x, w, \
+                     bias, sc, sh, y, stats, Cin, Cout, (int)H, (int)W)
+  switch (ct) {
+    case 1: AINP_FWD(1); break;
+    case 2: AINP_FWD(2); break;
+    case 3: AINP_FWD(3); break;
+    case 4: AINP_FWD(4); break;
+    default: return record_msg("conv3x3: Cout > 64 unsupported");
+  }
+#undef AINP_FWD
+  return check_launch("conv3x3_fwd_mfma");
+}
+
+extern "C" int ainp_conv3x3_fwd(const float* x, const float* w,
+                                const float* bias, const float* in_scale,
+                                const float* in_shift, float* y, double* stats,
+                                int64_t N, int Cin, int Cout, int64_t H,
+                                int64_t W, void* stream) {
+  if (!x || !w || !y || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
+      N > 65535 || H > (1 << 24) || W > (1 << 24))
+    return record_msg("ainp_conv3x3_fwd: bad argument");
+  if ((in_scale == nullptr) != (in_shift == nullptr))
+    return record_msg("ainp_conv3x3_fwd: in_scale/in_shift must both be set");
+  if (N == 0) return AINP_OK;
+  return conv_fwd_dispatch<false>(x, w, bias, in_scale, in_shift, y, stats, N,
+                                  Cin, Cout, H, W, as_stream(stream));
+}
+
+extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
+                                  float* workspace, int64_t N, int Cin,
+                                  int Cout, int64_t H, int64_t W,
+                                  void* stream) {
+  (void)workspace;
+  if (!dy || !w || !dx || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
+      N > 65535)
+    return record_msg("ainp_conv3x3_dgrad: bad argument");
+  if (N == 0) return AINP_OK;
+  // conv over dy (Cout channels) producing Cin channels, flipped weights
+  return conv_fwd_dispatch<true>(dy, w, nullptr, nullptr, nullptr, dx, nullptr,
+                                 N, Cout, Cin, H, W, as_stream(stream));
+}
+
+extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
+                                               int64_t H, int64_t W) {
+  (void)N; (void)H; (void)W;
+  const int cp = wgrad_pass(Cin);
+  int ct = wgrad_ct(Cout);
+  if (ct == 3) ct = 4;
+  return (size_t)WG_BLOCKS * ct * 16 * (9 * cp + 1) * sizeof(float);
+}
+
+extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
+                                  const float* in_shift, const float* dy,
+                                  float* dw, float* dbias, void* workspace,
+                                  int64_t N, int Cin, int Cout, int64_t H,
+                                  int64_t W, void* stream) {
+  if (!x || !dy || !dw || !workspace || N < 1 || Cin < 1 || Cout < 1 ||
+      H < 1 || W < 1)
+    return record_msg("ainp_conv3x3_wgrad: bad argument");
+  if ((in_scale == nullptr) != (in_shift == nullptr))
+    return record_msg("ainp_conv3x3_wgrad: in_scale/in_shift must both be set");
+  const int CT = wgrad_ct(Cout);
+  if (CT > 4) return record_msg("ainp_conv3x3_wgrad: Cout > 64 unsupported");
+  const int CTp = CT == 3 ? 4 : CT;  // kernel co-tiles (waves split evenly)
+  hipStream_t s = as_stream(stream);
+  float* partial = reinterpret_cast<float*>(workspace);
+  for (int ci0 = 0; ci0 < Cin; ci0 += WG_CIMAX) {
+    const int cp = (Cin - ci0) < WG_CIMAX ? (Cin - ci0) : WG_CIMAX;
+    const int JT = (9 * cp + 15) / 16;  // 1..18
+#define AINP_WG(CTV)                                                                \
+  do {                                                                              \
+    if (JT <= 1) launch_wgrad<CTV, 1>(x, in_scale, in_shift, dy, partial, (int)N,  \
+                                      Cin, Cout, (int)H, (int)W, ci0, cp, s);       \
+    else if (JT <= 4) launch_wgrad<CTV, 4>(x, in_scale, in_shift, dy, partial,     \
+                                           (int)N, Cin, Cout, (int)H, (int)W, ci0, \
+                                           cp, s);                                  \
+    else if (JT <= 9) launch_wgrad<CTV, 9>(x, in_scale, in_shift, dy, partial,     \
+                                           (int)N, Cin, Cout, (int)H, (int)W, ci0, \
+                                           cp, s);                                  \
+    else launch_wgrad<CTV, 18>(x, in_scale, in_shift, dy, partial, (int)N, Cin,    \
+                               Cout, (int)H, (int)W, ci0, cp, s);                   \
+  } while (0)
+    switch (CTp) {
+      case 1: AINP_WG(1); break;
+      case 2: AINP_WG(2); break;
+      default: AINP_WG(4); break;
+    }
+#undef AINP_WG
+    int rc = check_launch("conv3x3_wgrad_mfma");
+    if (rc) return rc;
+    const int J = 9 * cp;
+    const int per = CTp * 16 * (J + 1);
+    hipLaunchKernelGGL(wgrad_reduce, dim3((per + 255) / 256), dim3(256), 0, s,
+                       partial, WG_BLOCKS, CTp * 16, J, cp, ci0, Cin, Cout, dw,
+                       dbias, ci0 == 0 ? 1 : 0);
+    rc = check_launch("wgrad_reduce");
+    if (rc) return rc;
+  }
+  return AINP_OK;
+}

@@ -1,0 +1,315 @@
+// gemm.hip — strided / batched fp32 GEMM on gfx950 f32-input MFMA.
+//
+// Replaces the ATen GEMMs behind nn.LSTM input projections and nn.Linear of
+// models/CNNBLSTM/model.py:46-50,77,80 (forward and backward).  Arithmetic is
+// exact f32 (v_mfma_f32_32x32x2_f32 = k-ordered fmaf chain, MI355X_MICROARCH
+// "Matrix cores"), matching the reference's fp32 numerics up to summation order.
+//
+// Tiling: 128x128 output tile per 256-thread workgroup (4 waves as 2x2, each
+// wave 64x64 = 2x2 MFMA 32x32 tiles, 64 accumulator VGPRs), K-tile 32,
+// LDS double buffer with register-staged prefetch of the next K-tile.
+// Both operands are staged k-major in LDS (As[k][m], Bs[k][n]) so every MFMA
+// operand read is one conflict-free ds_read_b32 with lanes along m (or n).
+#include "common.h"
+
+namespace ainp {
+
+constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int GEMM_THREADS = 256;
+
+struct GemmPtrs {
+  const float* A[8];
+  const float* B[8];
+  float* C[8];
+  const float* bias1[8];
+  const float* bias2[8];
+  int64_t sA, sB, sC;  // strides between strided batches
+  int nptr;            // pointer batches; batch b -> (b % nptr, b / nptr)
+};
+
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ f32x16v mfma32(float a, float b, f32x16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// Load a ROWSxBK operand tile (ROWS along m or n, BK along k) into registers.
+// KC: source contiguous along k (element (r,k) at p[r*ld + k]);
+// otherwise contiguous along rows (element (r,k) at p[k*ld + r]).
+// VEC: 16-byte vector loads are legal (ld%4==0, extent%4==0, base aligned).
+template <bool KC, bool VEC>
+struct TileLoader {
+  static constexpr int NV = (128 * BK) / (4 * GEMM_THREADS);  // float4 per thread = 4
+  float4 v[NV];
+
+  __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld,
+                                       int64_t r0, int64_t k0, int64_t R,
+                                       int64_t K) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = tid + i * GEMM_THREADS;  // 0..1023
+      int rr, kk;
+      if (KC) {  // 8 float4 per row of 32 k
+        rr = idx >> 3;
+        kk = (idx & 7) * 4;
+      } else {  // 32 float4 per k-row of 128 rows
+        kk = idx >> 5;
+        rr = (idx & 31) * 4;
+      }
+      const int64_t gr = r0 + rr, gk = k0 + kk;
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (KC) {
+        if (gr < R) {
+          const float* q = p + gr * ld + gk;
+          if (VEC) {
+            if (gk < K) x = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (gk + 0 < K) x.x = q[0];
+            if (gk + 1 < K) x.y = q[1];
+            if (gk + 2 < K) x.z = q[2];
+            if (gk + 3 < K) x.w = q[3];
+          }
+        }
+      } else {
+        if (gk < K) {
+          const float* q = p + gk * ld + gr;
+          if (VEC) {
+            if (gr < R) x = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (gr + 0 < R) x.x = q[0];
+            if (gr + 1 < R) x.y = q[1];
+            if (gr + 2 < R) x.z = q[2];
+            if (gr + 3 < R) x.w = q[3];
+          }
+        }
+      }
+      v[i] = x;
+    }
+  }
+
+  // Store into the k-major LDS image s[k][r] (row length LD).
+  template <int LD>
+  __device__ __forceinline__ void store(float* s) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int idx = tid + i * GEMM_THREADS;
+      if (KC) {
+        const int rr = idx >> 3, kk = (idx & 7) * 4;
+        s[(kk + 0) * LD + rr] = v[i].x;
+        s[(kk + 1) * LD + rr] = v[i].y;
+        s[(kk + 2) * LD + rr] = v[i].z;
+        s[(kk + 3) * LD + rr] = v[i].w;
+      } else {
+        const int kk = idx >> 5, rr = (idx & 31) * 4;
+        *reinterpret_cast<float4*>(&s[kk * LD + rr]) = v[i];
+      }
+    }
+  }
+};
+
+// LDS row length: 129 for transposing (KC) stores -> conflict-free
+// ds_write_b32; 132 keeps 16-byte alignment for the vector stores.
+template <bool KC>
+struct LdsLd {
+  static constexpr int v = KC ? 129 : 132;
+};
+
+template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+__global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_f32_kernel(
+    int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda,
+    int64_t ldb, float beta, int64_t scm, int64_t scn, int nseg, int tiles_n) {
+  constexpr int LDA = LdsLd<AKC>::v, LDB = LdsLd<BKC>::v;
+  __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
+  auto As = [&](int b) { return smem + b * (BK * LDA); };
+  auto Bs = [&](int b) { return smem + 2 * BK * LDA + b * (BK * LDB); };
+
+  // block -> tile; consecutive block ids walk down m within a column strip of
+  // 8 n-tiles so the B (weight) panel stays hot in the XCD's L2.
+  const int64_t bid = blockIdx.x;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t group = 8;
+  const int64_t per_group = group * tiles_m;
+  const int64_t g = bid / per_group;
+  const int64_t first_n = g * group;
+  const int64_t gsize = (tiles_n - first_n) < group ? (tiles_n - first_n) : group;
+  const int64_t in_g = bid % per_group;
+  const int64_t tn = first_n + (in_g % gsize);
+  const int64_t tm = in_g / gsize;
+  const int64_t m0 = tm * BM, n0 = tn * BN;
+
+  const int batch = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+
+  f32x16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  TileLoader<AKC, AVEC> la;
+  TileLoader<BKC, BVEC> lb;
+  const int64_t nk = (K + BK - 1) / BK;
+  const int64_t total = nk * nseg;
+
+  auto seg_ptr = [&](int64_t it, const float*& a, const float*& b, int64_t& k0) {
+    const int bi = (nseg > 1) ? (int)(it / nk) : batch;
+    const int pb = bi % ptrs.nptr, sb = bi / ptrs.nptr;
+    a = ptrs.A[pb] + sb * ptrs.sA;
+    b = ptrs.B[pb] + sb * ptrs.sB;
+    k0 = (it % nk) * BK;
+  };
+
+  {
+    const float *a, *b;
+    int64_t k0;
+    seg_ptr(0, a, b, k0);
+    la.load(a, lda, m0, k0, M, K);
+    lb.load(b, ldb, n0, k0, N, K);
+    la.template store<LDA>(As(0));
+    lb.template store<LDB>(Bs(0));
+  }
+  __syncthreads();
+
+  for (int64_t it = 0; it < total; ++it) {
+    const int cur = it & 1;
+    const bool more = it + 1 < total;
+    if (more) {
+      const float *a, *b;
+      int64_t k0;
+      seg_ptr(it + 1, a, b, k0);
+      la.load(a, lda, m0, k0, M, K);
+      lb.load(b, ldb, n0, k0, N, K);
+    }
+    const float* as = As(cur);
+    const float* bs = Bs(cur);
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 2) {
+      float af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = as[(kk + lh) * LDA + wm + i * 32 + li];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = bs[(kk + lh) * LDB + wn + j * 32 + li];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bf[j], acc[i][j]);
+    }
+    if (more) {
+      la.template store<LDA>(As(cur ^ 1));
+      lb.template store<LDB>(Bs(cur ^ 1));
+    }
+    __syncthreads();
+  }
+
+  // epilogue: D[row=(r&3)+8*(r>>2)+4*lh][col=li] of each 32x32 tile
+  const int cb = nseg > 1 ? 0 : batch;
+  float* C = ptrs.C[cb % ptrs.nptr] + (cb / ptrs.nptr) * ptrs.sC;
+  const float* bias1 = ptrs.bias1[cb % ptrs.nptr];
+  const float* bias2 = ptrs.bias2[cb % ptrs.nptr];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t n = n0 + wn + j * 32 + li;
+      if (n >= N) continue;
+      const float bv = (bias1 ? bias1[n] : 0.f) + (bias2 ? bias2[n] : 0.f);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) {
+          float* q = C + m * scm + n * scn;
+          float v = alpha * acc[i][j][r] + bv;
+          if (beta != 0.f) v += beta * *q;
+          *q = v;
+        }
+      }
+    }
+}
+
+template <bool AKC, bool BKC>
+static void launch_gemm(bool avec, bool bvec, dim3 grid, hipStream_t s,
+                        int64_t M, int64_t N, int64_t K, float alpha,
+                        const GemmPtrs& p, int64_t lda, int64_t ldb,
+                        float beta, int64_t scm, int64_t scn, int nseg,
+                        int tiles_n) {
+#define AINP_GEMM_LAUNCH(AV, BV)                                             \
+  hipLaunchKernelGGL((gemm_f32_kernel<AKC, BKC, AV, BV>), grid,             \
+                     dim3(GEMM_THREADS), 0, s, M, N, K, alpha, p, lda, ldb, \
+                     beta, scm, scn, nseg, tiles_n)
+  if (avec && bvec) AINP_GEMM_LAUNCH(true, true);
+  else if (avec) AINP_GEMM_LAUNCH(true, false);
+  else if (bvec) AINP_GEMM_LAUNCH(false, true);
+  else AINP_GEMM_LAUNCH(false, false);
+#undef AINP_GEMM_LAUNCH
+}
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace ainp
+
+using namespace ainp;
+
+extern "C" int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
+                             const float* const* A, int64_t sam, int64_t sak,
+                             int64_t strideA, const float* const* B,
+                             int64_t sbk, int64_t sbn, int64_t strideB,
+                             float beta, float* const* C, int64_t scm,
+                             int64_t scn, int64_t strideC,
+                             const float* const* bias1,
+                             const float* const* bias2, int nptr,
+                             int64_t nstrided, int ksplit, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || nptr < 1 || nptr > 8 || nstrided < 1 ||
+      !A || !B || !C)
+    return record_msg("ainp_gemm_f32: bad argument");
+  if (sam != 1 && sak != 1) return record_msg("ainp_gemm_f32: A needs a unit stride");
+  if (sbk != 1 && sbn != 1) return record_msg("ainp_gemm_f32: B needs a unit stride");
+  if (scm != 1 && scn != 1) return record_msg("ainp_gemm_f32: C needs a unit stride");
+  const int64_t nb = nptr * nstrided;
+  if (!ksplit && nb > 65535) return record_msg("ainp_gemm_f32: too many batches");
+  if (M == 0 || N == 0) return AINP_OK;
+  GemmPtrs p;
+  for (int i = 0; i < 8; ++i) {
+    p.A[i] = i < nptr ? A[i] : nullptr;
+    p.B[i] = i < nptr ? B[i] : nullptr;
+    p.C[i] = i < nptr ? C[i] : nullptr;
+    p.bias1[i] = (bias1 && i < nptr) ? bias1[i] : nullptr;
+    p.bias2[i] = (bias2 && i < nptr) ? bias2[i] : nullptr;
+  }
+  p.sA = strideA;
+  p.sB = strideB;
+  p.sC = strideC;
+  p.nptr = nptr;
+  // contiguous dimension of each operand (prefer k when both strides are 1)
+  const bool akc = (sak == 1);
+  const bool bkc = (sbk == 1);
+  const int64_t lda = akc ? sam : sak;
+  const int64_t ldb = bkc ? sbn : sbk;
+  // vector loads need 16-byte aligned rows and a contiguous extent % 4 == 0
+  bool avec = (lda % 4 == 0) && ((akc ? K : M) % 4 == 0) && (strideA % 4 == 0);
+  bool bvec = (ldb % 4 == 0) && ((bkc ? K : N) % 4 == 0) && (strideB % 4 == 0);
+  for (int i = 0; i < nptr; ++i) {
+    avec = avec && aligned16(A[i]);
+    bvec = bvec && aligned16(B[i]);
+  }
+  if (ksplit && nb > (1 << 20)) return record_msg("ainp_gemm_f32: too many segments");
+  const int nseg = ksplit ? (int)nb : 1;
+  const int64_t tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  dim3 grid((unsigned)(tiles_m * tiles_n), ksplit ? 1 : (unsigned)nb);
+  hipStream_t s = as_stream(stream);
+  if (akc && bkc)
+    launch_gemm<true, true>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
+  else if (akc)
+    launch_gemm<true, false>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
+  else if (bkc)
+    launch_gemm<false, true>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
+  else
+    launch_gemm<false, false>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
+  return check_launch("ainp_gemm_f32");
+}

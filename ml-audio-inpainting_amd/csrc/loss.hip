@@ -1,0 +1,90 @@
+// loss.hip — fused CNNBLSTM reconstruction loss and small reductions.
+#include "common.h"
+
+namespace ainp {
+
+// L = sum |10^y*m - |target|*m|  (models/CNNBLSTM/train.py:70,104:
+// nn.L1Loss(reduction='sum') on (10 ** y) * mask vs abs(target) * mask)
+// dL/dy = sign(d) * m * 10^y * ln(10), sign(0) = 0 as in torch's L1 backward.
+__global__ __launch_bounds__(256) void l1_pow10_kernel(
+    const float* __restrict__ y, const float* __restrict__ mask,
+    const float2* __restrict__ target, int64_t n, double* __restrict__ loss,
+    float* __restrict__ dy, float grad_scale) {
+  const float LN10 = 2.302585092994046f;
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float m = mask[i];
+    const float p = powf(10.f, y[i]);
+    const float2 t = target[i];
+    const float a = p * m;
+    const float b = hypotf(t.x, t.y) * m;
+    const float d = a - b;
+    acc += (double)fabsf(d);
+    if (dy) {
+      const float sg = d > 0.f ? 1.f : (d < 0.f ? -1.f : 0.f);
+      dy[i] = grad_scale * (sg * m) * (p * LN10);
+    }
+  }
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss, red[0] + red[1] + red[2] + red[3]);
+}
+
+// out[j] (+)= sum_i x[i*ld + j]; one thread per column, rows split over
+// blockIdx.y slabs reduced with atomics when more than one slab.
+__global__ void colsum_kernel(const float* __restrict__ x, int64_t rows,
+                              int64_t cols, int64_t ld, float* __restrict__ out,
+                              int64_t rows_per) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  const int64_t r0 = blockIdx.y * rows_per;
+  int64_t r1 = r0 + rows_per;
+  if (r1 > rows) r1 = rows;
+  float s = 0.f;
+  for (int64_t r = r0; r < r1; ++r) s += x[r * ld + j];
+  atomicAdd(&out[j], s);
+}
+
+__global__ void zero_kernel(float* p, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = 0.f;
+}
+
+}  // namespace ainp
+
+using namespace ainp;
+
+extern "C" int ainp_l1_pow10_loss(const float* y, const float* mask,
+                                  const float* target, int64_t n, double* loss,
+                                  float* dy, float grad_scale, void* stream) {
+  if (!y || !mask || !target || !loss || n < 0)
+    return record_msg("ainp_l1_pow10_loss: bad argument");
+  if (n == 0) return AINP_OK;
+  int64_t grid = cdiv(n, 256 * 8);
+  if (grid > 2048) grid = 2048;
+  hipLaunchKernelGGL(l1_pow10_kernel, dim3((unsigned)grid), dim3(256), 0,
+                     as_stream(stream), y, mask,
+                     reinterpret_cast<const float2*>(target), n, loss, dy,
+                     grad_scale);
+  return check_launch("l1_pow10_loss");
+}
+
+extern "C" int ainp_colsum(const float* x, int64_t rows, int64_t cols,
+                           int64_t ld, float* out, int accumulate,
+                           void* stream) {
+  if (!x || !out || rows < 0 || cols < 0 || ld < cols)
+    return record_msg("ainp_colsum: bad argument");
+  hipStream_t s = as_stream(stream);
+  if (!accumulate && cols > 0)
+    hipLaunchKernelGGL(zero_kernel, dim3((unsigned)cdiv(cols, 256)), dim3(256),
+                       0, s, out, cols);
+  if (rows == 0 || cols == 0) return check_launch("colsum");
+  const int64_t rows_per = 128;
+  dim3 grid((unsigned)cdiv(cols, 256), (unsigned)cdiv(rows, rows_per));
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, x, rows, cols, ld,
+                     out, rows_per);
+  return check_launch("colsum");
+}

@@ -1,0 +1,194 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+Run in the build container (where /root/reference exists):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py
+
+What it produces (data only -- inputs and expected outputs):
+  gap_frames.json      SURVEY Q3 known answers + random (start -> frame) cases for
+                       the CNNBLSTM rule (librosa.time_to_frames of the float seconds,
+                       models/CNNBLSTM/dataset.py:116-117) and the GAN rule
+                       (models/GAN/dataset.py:139-152), evaluated with the exact
+                       Python/numpy expressions those lines execute.
+  cnnblstm_small.npz   reference StackedBLSTMCNN (models/CNNBLSTM/model.py imported
+                       from /root/reference) at a small config: initial weights,
+                       input, mask, target, forward output, L1(sum) loss
+                       (models/CNNBLSTM/train.py:70,104), every parameter gradient,
+                       and parameters / BN running stats after two Adam steps
+                       (train.py:72,96-108).
+  cnnblstm_full.npz    the same model at the real config (F=257, T=334, H=128) for a
+                       2-example batch: output, loss, per-parameter grad norms and a
+                       strided sample of every gradient; weights are NOT stored --
+                       they are re-created from torch.manual_seed(0) by the same
+                       nn.Module construction order, and a per-parameter checksum is
+                       stored to prove the re-creation matches.
+The reference sources are only imported here, never copied.
+"""
+from __future__ import annotations
+
+import importlib.util
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.path.insert(0, ROOT)
+
+from oracle import stft_ref  # noqa: E402
+
+
+def load_ref_model_module():
+    path = os.path.join(REF, "models", "CNNBLSTM", "model.py")
+    spec = importlib.util.spec_from_file_location("ref_cnnblstm_model", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def write_cfg(path, n_fft, hidden, layers, enc, dec):
+    import yaml
+    cfg = {
+        "data": {"spectrogram": {"n_fft": n_fft}},
+        "model": {"in_channels": 1, "num_lstm_layers": layers, "lstm_hidden_dim": hidden,
+                  "enc_filters": list(enc), "dec_filters": list(dec)},
+    }
+    with open(path, "w") as f:
+        yaml.safe_dump(cfg, f)
+
+
+def make_inputs(N, F, T, seed, n_fft, hop, win):
+    """Spectrogram-shaped inputs from the STFT oracle on synthetic clips."""
+    rng = np.random.default_rng(seed)
+    S = (T - 1) * hop
+    xs, ms, ts = [], [], []
+    for i in range(N):
+        clip = stft_ref.synthetic_clip(seed * 100 + i, S)
+        g = max(1, S // 25)
+        start = int(rng.integers(0, S - g))
+        lg, tg, mk = stft_ref.cnnblstm_item(clip, start, g, n_fft, hop, win, 16000, T)
+        xs.append(lg); ms.append(mk); ts.append(tg)
+    return (np.stack(xs).astype(np.float32), np.stack(ms).astype(np.float32),
+            np.stack(ts).astype(np.complex64))
+
+
+def ref_step(model, x, m, tgt, steps=2, lr=1e-4):
+    crit = torch.nn.L1Loss(reduction="sum")
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    rec = {}
+    for s in range(steps):
+        opt.zero_grad()
+        y = model(x.unsqueeze(1))
+        loss = crit((10 ** y) * m, torch.abs(tgt) * m)
+        loss.backward()
+        if s == 0:
+            rec["y"] = y.detach().numpy().copy()
+            rec["loss"] = np.array([loss.item()])
+            rec["grads"] = {k: p.grad.detach().numpy().copy()
+                            for k, p in model.named_parameters()}
+        else:
+            rec["loss2"] = np.array([loss.item()])
+        opt.step()
+    rec["final"] = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    return rec
+
+
+def gen_small(mod):
+    torch.manual_seed(1234)
+    n_fft, hop, win, hidden, layers = 64, 16, 48, 32, 3
+    F, T, N = n_fft // 2 + 1, 24, 2
+    with tempfile.TemporaryDirectory() as d:
+        cfg = os.path.join(d, "cfg.yaml")
+        write_cfg(cfg, n_fft, hidden, layers, [16, 32], [16, 32])
+        model = mod.StackedBLSTMCNN(cfg)
+    model.train()
+    init = {k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    x, m, tgt = make_inputs(N, F, T, 7, n_fft, hop, win)
+    rec = ref_step(model, torch.from_numpy(x), torch.from_numpy(m), torch.from_numpy(tgt))
+    out = {"x": x, "mask": m, "target": tgt, "y": rec["y"], "loss": rec["loss"],
+           "loss2": rec["loss2"],
+           "config": np.array([n_fft, hop, win, hidden, layers, N, T])}
+    for k, v in init.items():
+        out["init/" + k] = v
+    for k, v in rec["grads"].items():
+        out["grad/" + k] = v
+    for k, v in rec["final"].items():
+        out["final/" + k] = v
+    np.savez_compressed(os.path.join(HERE, "cnnblstm_small.npz"), **out)
+
+
+def gen_full(mod):
+    n_fft, hop, win, hidden, layers = 512, 192, 384, 128, 3
+    F, T, N = 257, 334, 2
+    with tempfile.TemporaryDirectory() as d:
+        cfg = os.path.join(d, "cfg.yaml")
+        write_cfg(cfg, n_fft, hidden, layers, [16, 32], [16, 32])
+        torch.manual_seed(0)
+        model = mod.StackedBLSTMCNN(cfg)
+    model.train()
+    checks = {k: np.array([float(v.double().sum()), float((v.double() ** 2).sum())])
+              for k, v in model.state_dict().items()}
+    x, m, tgt = make_inputs(N, F, T, 11, n_fft, hop, win)
+    rec = ref_step(model, torch.from_numpy(x), torch.from_numpy(m), torch.from_numpy(tgt),
+                   steps=1)
+    out = {"x": x, "mask": m, "target": tgt, "y": rec["y"], "loss": rec["loss"],
+           "config": np.array([n_fft, hop, win, hidden, layers, N, T])}
+    for k, v in checks.items():
+        out["check/" + k] = v
+    for k, g in rec["grads"].items():
+        flat = g.reshape(-1)
+        step = max(1, flat.size // 2048)
+        out["gnorm/" + k] = np.array([np.sqrt((flat.astype(np.float64) ** 2).sum())])
+        out["gsample/" + k] = flat[::step].copy()
+    np.savez_compressed(os.path.join(HERE, "cnnblstm_full.npz"), **out)
+
+
+def gen_gap_frames():
+    cases = []
+    sr = 16000
+    # start samples whose float round trip lands one frame early
+    for k in (64320, 64704, 65088, 65472):
+        fs, fe = stft_ref.cnnblstm_gap_frames(k, 3200, sr, 192)
+        cases.append({"rule": "cnnblstm", "start": k, "gap": 3200, "hop": 192, "sr": sr,
+                      "fs": fs, "fe": fe})
+    # end samples with the same values
+    for k in (64320, 64704, 65088, 65472):
+        fs, fe = stft_ref.cnnblstm_gap_frames(k - 3200, 3200, sr, 192)
+        cases.append({"rule": "cnnblstm", "start": k - 3200, "gap": 3200, "hop": 192,
+                      "sr": sr, "fs": fs, "fe": fe})
+    # exhaustive sweep of every start that the CNNBLSTM loader can draw
+    # (utils.py:179: randint(0, 80000-3200)) is summarised by the list of
+    # starts where the float rule differs from integer floor division
+    diffs = []
+    for k in range(0, 80000 - 3200):
+        if stft_ref.cnnblstm_gap_frames(k, 0, sr, 192)[0] != k // 192:
+            diffs.append(k)
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        hop = int(rng.choice([128, 160, 192, 256]))
+        g = int(rng.choice([1600, 3200, 800]))
+        S = int(rng.choice([64000, 80000, 128000]))
+        k = int(rng.integers(0, S - g))
+        fs, fe = stft_ref.cnnblstm_gap_frames(k, g, sr, hop)
+        cases.append({"rule": "cnnblstm", "start": k, "gap": g, "hop": hop, "sr": sr,
+                      "fs": fs, "fe": fe})
+        T = 1 + S // hop
+        k2 = int(rng.integers(0, S - g + 1))
+        gs, ge = stft_ref.gan_gap_frames(k2, g, hop, T)
+        cases.append({"rule": "gan", "start": k2, "gap": g, "hop": hop, "n_frames": T,
+                      "fs": gs, "fe": ge})
+    with open(os.path.join(HERE, "gap_frames.json"), "w") as f:
+        json.dump({"cases": cases, "cnnblstm_hop192_sr16000_float_rule_differs_at": diffs},
+                  f, indent=0)
+
+
+if __name__ == "__main__":
+    mod = load_ref_model_module()
+    gen_gap_frames()
+    gen_small(mod)
+    gen_full(mod)
+    print("golden fixtures written to", HERE)

@@ -1,0 +1,305 @@
+"""Kernel-level parity: each libainp entry point vs its CPU reference.
+
+STFT/features/masks are checked against the oracle (oracle/stft_ref.py; masks
+bit-exact, floats to the stated tolerance).  Floating-point NN kernels (GEMM,
+conv, BatchNorm, LSTM, loss, Adam) are checked against a float64 PyTorch-CPU
+evaluation of the same op (the reference's own backend), relative L2 <= 1e-5
+unless stated.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as Fnn
+
+from oracle import stft_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def rel(a, b):
+    a = np.asarray(a, dtype=np.float64)
+    b = np.asarray(b, dtype=np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from ainp import ops as _ops
+    return _ops
+
+
+# ------------------------------------------------------------------ STFT
+@pytest.mark.parametrize("S,n_fft,hop,win,n_frames", [
+    (8000, 512, 192, 384, None),
+    (80000, 512, 192, 384, 334),     # dataset: 5 s load, slice to 4 s of frames
+    (64000, 512, 192, 384, 334),
+    (4000, 64, 16, 48, None),
+    (80000, 512, 192, 384, 420),     # more frames than the STFT has -> zeros
+])
+def test_stft_cnnblstm_vs_oracle(ops, S, n_fft, hop, win, n_frames):
+    B = 3
+    clips = np.stack([stft_ref.synthetic_clip(10 + i, S) for i in range(B)])
+    g = 3200 if S > 8000 else S // 20
+    rng = np.random.default_rng(5)
+    starts = rng.integers(0, S - g, size=B)
+    starts[0] = 0                      # gap touching the start
+    starts[-1] = S - g - 1             # gap at the very end
+    T = n_frames if n_frames is not None else 1 + S // hop
+    a = torch.from_numpy(clips).to(DEV)
+    gs = torch.from_numpy(starts.astype(np.int64)).to(DEV)
+    lg, tg, mk, _ = ops.stft_features(a, gs, g, n_fft, hop, win, n_frames=T)
+    torch.cuda.synchronize()
+    for b in range(B):
+        rl, rt, rm = stft_ref.cnnblstm_item(clips[b], int(starts[b]), g, n_fft, hop, win,
+                                            16000, T)
+        np.testing.assert_array_equal(mk[b].cpu().numpy(), rm)
+        assert np.max(np.abs(lg[b].cpu().numpy() - rl)) < 2e-5
+        tt = tg[b].cpu().numpy()
+        assert np.max(np.abs(tt - rt)) <= 2e-6 * max(1.0, np.abs(rt).max())
+
+
+@pytest.mark.parametrize("S,n_fft,hop,win", [(80000, 512, 128, 512), (128000, 512, 128, 512),
+                                             (3000, 64, 16, 64)])
+def test_stft_gan_vs_oracle(ops, S, n_fft, hop, win):
+    B = 2
+    clips = np.stack([stft_ref.synthetic_clip(20 + i, S) for i in range(B)])
+    g = 3200 if S >= 80000 else 200
+    starts = np.array([0, S - g], dtype=np.int64)  # inclusive max (utils.py:134)
+    a = torch.from_numpy(clips).to(DEV)
+    gs = torch.from_numpy(starts).to(DEV)
+    o0, o1, o2, o3 = ops.stft_features(a, gs, g, n_fft, hop, win, mode=ops.FEAT_GAN)
+    torch.cuda.synchronize()
+    for b in range(B):
+        r0, r1, r2, r3 = stft_ref.gan_item(clips[b], int(starts[b]), g, n_fft, hop, win)
+        np.testing.assert_array_equal(o3[b].cpu().numpy(), r3)
+        assert np.max(np.abs(o0[b].cpu().numpy() - r0)) < 1e-5
+        assert np.max(np.abs(o1[b].cpu().numpy() - r1)) < 1e-5
+        ph = o2[b].cpu().numpy()
+        d = np.abs(np.angle(np.exp(1j * (ph - r2))))  # wrap-aware
+        mag = np.expm1(r0)
+        assert np.max(d[mag > 1e-3]) < 1e-4
+
+
+def test_gap_frames_known_answers(ops, golden_dir):
+    """bit-exact frame indices incl. the float64 round-trip quirk."""
+    cases = json.load(open(os.path.join(golden_dir, "gap_frames.json")))["cases"]
+    for rule in ("cnnblstm", "gan"):
+        sel = [c for c in cases if c["rule"] == rule]
+        # one batch per hop (kernel takes one hop per launch)
+        for hop in sorted({c["hop"] for c in sel}):
+            cs = [c for c in sel if c["hop"] == hop]
+            for c in cs:
+                if rule == "gan":
+                    T = c["n_frames"]
+                    S = T * hop - 1          # 1 + S//hop == n_frames
+                else:
+                    T = max(c["fe"], 1) + 2
+                    S = max(c["start"] + c["gap"] + 1, 1000)
+                a = torch.zeros(1, S, device=DEV)
+                gs = torch.tensor([c["start"]], device=DEV, dtype=torch.int64)
+                mode = ops.FEAT_CNNBLSTM if rule == "cnnblstm" else ops.FEAT_GAN
+                out = ops.stft_features(a, gs, c["gap"], 64, hop, 64, n_frames=T, mode=mode,
+                                        outputs=(False, False, rule == "cnnblstm",
+                                                 rule == "gan"))
+                m = (out[2] if rule == "cnnblstm" else out[3])[0, 0].cpu().numpy()
+                if rule == "cnnblstm":
+                    exp = np.zeros(T, np.float32)
+                    exp[c["fs"]:c["fe"]] = 1
+                else:
+                    exp = np.ones(T, np.float32)
+                    if c["fe"] > c["fs"]:
+                        exp[c["fs"]:c["fe"]] = 0
+                np.testing.assert_array_equal(m, exp, err_msg=str(c))
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(333, 130, 77), (256, 512, 1024), (1, 5, 3), (129, 4112, 256)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_layouts(ops, M, N, K, ta, tb):
+    g = torch.Generator().manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, N, generator=g, dtype=torch.float64)
+    ref = A @ B
+    Ad = (A.t().contiguous() if ta else A).float().to(DEV)
+    Bd = (B.t().contiguous() if tb else B).float().to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    sam, sak = (1, M) if ta else (K, 1)
+    sbk, sbn = (1, K) if tb else (N, 1)
+    ops.gemm(M, N, K, [Ad], sam, sak, [Bd], sbk, sbn, [C], N, 1)
+    assert rel(C.cpu(), ref) < 1e-5
+
+
+def test_gemm_batched_bias_ksplit(ops):
+    g = torch.Generator().manual_seed(3)
+    M, N, K, nb = 100, 96, 40, 3
+    A = torch.randn(nb, M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(nb, K, N, generator=g, dtype=torch.float64)
+    b1 = torch.randn(N, generator=g, dtype=torch.float64)
+    b2 = torch.randn(N, generator=g, dtype=torch.float64)
+    Ad, Bd = A.float().to(DEV), B.float().to(DEV)
+    # strided batches with bias, output column-major
+    C = torch.empty(nb, N, M, device=DEV)
+    ops.gemm(M, N, K, [Ad], K, 1, [Bd], N, 1, [C], 1, M, strideA=M * K, strideB=K * N,
+             strideC=M * N, nstrided=nb, bias1=[b1.float().to(DEV)], bias2=[b2.float().to(DEV)])
+    ref = A @ B + b1 + b2
+    assert rel(C.cpu().transpose(1, 2), ref) < 1e-5
+    # k-split over strided batches: sum_b A_b B_b
+    C2 = torch.empty(M, N, device=DEV)
+    ops.gemm(M, N, K, [Ad], K, 1, [Bd], N, 1, [C2], N, 1, strideA=M * K, strideB=K * N,
+             nstrided=nb, ksplit=True)
+    assert rel(C2.cpu(), (A @ B).sum(0)) < 1e-5
+    # pointer batches with alpha/beta
+    C3 = torch.ones(2, M, N, device=DEV)
+    ops.gemm(M, N, K, [Ad[0], Ad[1]], K, 1, [Bd[0], Bd[1]], N, 1, [C3[0], C3[1]], N, 1,
+             alpha=0.5, beta=2.0)
+    assert rel(C3.cpu(), 0.5 * (A[:2] @ B[:2]) + 2.0) < 1e-5
+
+
+# ------------------------------------------------------------------ conv
+def _act(x, sc, sh):
+    if sc is None:
+        return x
+    return torch.relu(x * sc.view(1, -1, 1, 1) + sh.view(1, -1, 1, 1))
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,pro", [
+    (2, 1, 16, 33, 24, False), (2, 16, 32, 33, 50, True), (1, 32, 64, 40, 100, True),
+    (2, 32, 16, 17, 49, True), (2, 16, 1, 20, 30, True), (1, 64, 32, 9, 7, False),
+    (1, 8, 48, 11, 13, True)])
+def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
+    g = torch.Generator().manual_seed(N * 100 + Cin * 10 + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
+    w = torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) * 0.2
+    b = torch.randn(Cout, generator=g, dtype=torch.float64)
+    sc = torch.rand(Cin, generator=g, dtype=torch.float64) + 0.5 if pro else None
+    sh = torch.randn(Cin, generator=g, dtype=torch.float64) * 0.3 if pro else None
+    xa = _act(x, sc, sh).requires_grad_(True)
+    wr = w.clone().requires_grad_(True)
+    br = b.clone().requires_grad_(True)
+    yr = Fnn.conv2d(xa, wr, br, padding=1)
+    dy = torch.randn(yr.shape, generator=g, dtype=torch.float64)
+    yr.backward(dy)
+    d = lambda t: None if t is None else t.float().to(DEV)  # noqa: E731
+    y, stats = ops.conv3x3_fwd(d(x), d(w), d(b), d(sc), d(sh), want_stats=True)
+    assert rel(y.cpu(), yr.detach()) < 1e-5
+    st = stats.sum(0).cpu()
+    assert rel(st[:Cout], yr.detach().sum((0, 2, 3))) < 1e-5
+    assert rel(st[Cout:], (yr.detach() ** 2).sum((0, 2, 3))) < 1e-5
+    dx = ops.conv3x3_dgrad(d(dy), d(w))
+    assert rel(dx.cpu(), xa.grad) < 1e-5
+    dw, db = ops.conv3x3_wgrad(d(x), d(dy), d(sc), d(sh))
+    assert rel(dw.cpu(), wr.grad) < 1e-5
+    assert rel(db.cpu(), br.grad) < 1e-5
+
+
+# ------------------------------------------------------------------ BN
+@pytest.mark.parametrize("ntcf", [False, True])
+def test_bn_relu_fwd_bwd(ops, ntcf):
+    g = torch.Generator().manual_seed(9)
+    N, C, H, W = 3, 8, 37, 70
+    y = torch.randn(N, C, H, W, generator=g, dtype=torch.float64) * 2 + 0.5
+    gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    beta = torch.randn(C, generator=g, dtype=torch.float64) * 0.1
+    rm = torch.randn(C, generator=g, dtype=torch.float64)
+    rv = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    yq = y.clone().requires_grad_(True)
+    gq = gamma.clone().requires_grad_(True)
+    bq = beta.clone().requires_grad_(True)
+    rm_r, rv_r = rm.clone(), rv.clone()
+    z = torch.relu(Fnn.batch_norm(yq, rm_r, rv_r, gq, bq, training=True, momentum=0.1,
+                                  eps=1e-5))
+    if ntcf:
+        zr = z.permute(0, 3, 1, 2).reshape(N, W, C * H)
+    else:
+        zr = z
+    gz = torch.randn(zr.shape, generator=g, dtype=torch.float64)
+    zr.backward(gz)
+    # our path: stats from the conv epilogue layout (one partial row)
+    yd = y.float().to(DEV)
+    stats = torch.cat([y.sum((0, 2, 3)), (y ** 2).sum((0, 2, 3))]).view(1, -1).to(DEV)
+    rmd, rvd = rm.float().to(DEV), rv.float().to(DEV)
+    sums = ops.bn_stats_reduce(stats, C)
+    sc, sh, save = ops.bn_finalize(sums, N * H * W, gamma.float().to(DEV),
+                                   beta.float().to(DEV), rmd, rvd, 0.1, 1e-5)
+    out = ops.bn_relu_apply(yd, sc, sh, ntcf=ntcf)
+    assert rel(out.cpu(), zr.detach()) < 1e-5
+    assert rel(rmd.cpu(), rm_r) < 1e-6 and rel(rvd.cpu(), rv_r) < 1e-6
+    gy, dgam, dbet = ops.bn_relu_bwd(gz.float().to(DEV), yd, sc, sh, gamma.float().to(DEV),
+                                     save, ntcf=ntcf)
+    assert rel(gy.cpu(), yq.grad) < 1e-4
+    assert rel(dgam.cpu(), gq.grad) < 1e-5
+    assert rel(dbet.cpu(), bq.grad) < 1e-5
+
+
+# ------------------------------------------------------------------ LSTM
+@pytest.mark.parametrize("H,N,T", [(32, 3, 37), (128, 2, 50), (64, 1, 5)])
+def test_lstm_recurrence(ops, H, N, T):
+    g = torch.Generator().manual_seed(H + T)
+    I = 24
+    lstm = torch.nn.LSTM(I, H, num_layers=1, batch_first=True, bidirectional=True).double()
+    with torch.no_grad():
+        for p in lstm.parameters():
+            p.copy_(torch.randn(p.shape, generator=g, dtype=torch.float64) * 0.3)
+    x = torch.randn(N, T, I, generator=g, dtype=torch.float64, requires_grad=True)
+    out, _ = lstm(x)
+    dh = torch.randn(out.shape, generator=g, dtype=torch.float64)
+    out.backward(dh)
+    # zx = x W_ih^T + b_ih + b_hh for both directions
+    zf = x.detach() @ lstm.weight_ih_l0.detach().t() + lstm.bias_ih_l0.detach() + lstm.bias_hh_l0.detach()
+    zr = (x.detach() @ lstm.weight_ih_l0_reverse.detach().t() + lstm.bias_ih_l0_reverse.detach()
+          + lstm.bias_hh_l0_reverse.detach())
+    zx = torch.cat([zf, zr], dim=2).float().to(DEV).contiguous()
+    wf = lstm.weight_hh_l0.detach().float().to(DEV).contiguous()
+    wr = lstm.weight_hh_l0_reverse.detach().float().to(DEV).contiguous()
+    h, gates, cell = ops.lstm_rec_fwd(zx, wf, wr, H)
+    assert rel(h.cpu(), out.detach()) < 1e-5
+    dg = ops.lstm_rec_bwd(dh.float().to(DEV), gates, cell, wf, wr, H)
+    # dgates -> dx through W_ih, compare with autograd
+    dgc = dg.cpu().double()
+    dx = dgc[..., :4 * H] @ lstm.weight_ih_l0.detach() + dgc[..., 4 * H:] @ lstm.weight_ih_l0_reverse.detach()
+    assert rel(dx, x.grad) < 1e-4
+    db = dgc[..., :4 * H].sum((0, 1))
+    assert rel(db, lstm.bias_ih_l0.grad) < 1e-4
+    hp = ops.lstm_hprev(h, H).cpu().double()
+    dwhh = dgc[..., :4 * H].reshape(-1, 4 * H).t() @ hp[..., :H].reshape(-1, H)
+    assert rel(dwhh, lstm.weight_hh_l0.grad) < 1e-4
+    dwhh_r = dgc[..., 4 * H:].reshape(-1, 4 * H).t() @ hp[..., H:].reshape(-1, H)
+    assert rel(dwhh_r, lstm.weight_hh_l0_reverse.grad) < 1e-4
+
+
+# ------------------------------------------------------------------ loss / adam
+def test_l1_pow10_loss(ops):
+    g = torch.Generator().manual_seed(1)
+    n = (5, 33, 40)
+    y = (torch.randn(n, generator=g) * 0.5).double().requires_grad_(True)
+    m = (torch.rand(n, generator=g) > 0.7).double()
+    t = torch.complex(torch.randn(n, generator=g), torch.randn(n, generator=g))
+    loss = torch.nn.L1Loss(reduction="sum")((10 ** y) * m, torch.abs(t).double() * m)
+    loss.backward()
+    l, dy = ops.l1_pow10_loss(y.detach().float().to(DEV), m.float().to(DEV), t.to(DEV))
+    assert abs(l.item() - loss.item()) / loss.item() < 1e-6
+    assert rel(dy.cpu(), y.grad) < 1e-6
+
+
+def test_adam_matches_torch(ops):
+    g = torch.Generator().manual_seed(2)
+    shapes = [(7, 5), (1000,), (3, 3, 3, 3), (4097,)]
+    ps = [torch.randn(s, generator=g) for s in shapes]
+    ref = [p.clone().requires_grad_(True) for p in ps]
+    opt = torch.optim.Adam(ref, lr=1e-3)
+    dp = [p.to(DEV) for p in ps]
+    m = [torch.zeros_like(p) for p in dp]
+    v = [torch.zeros_like(p) for p in dp]
+    for step in range(1, 4):
+        grads = [torch.randn(s, generator=g) for s in shapes]
+        for r, gg in zip(ref, grads):
+            r.grad = gg.clone()
+        opt.step()
+        ops.adam_step(dp, [gg.to(DEV) for gg in grads], m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, step)
+    for r, p in zip(ref, dp):
+        assert torch.allclose(p.cpu(), r.detach(), rtol=1e-6, atol=1e-7)
