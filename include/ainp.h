@@ -226,6 +226,10 @@ int ainp_lstm_hprev(const float* h_out, float* hprev, int64_t N, int64_t T,
 int ainp_l1_pow10_loss(const float* y, const float* mask, const float* target,
                        int64_t n, double* loss, float* dy, float grad_scale,
                        void* stream);
+/* out[i] = x[i] * scalar[0] (scalar is a device pointer: scales a gradient
+ * by the autograd grad_output without a host sync). */
+int ainp_scale_by_dev(const float* x, float* out, int64_t n,
+                      const float* scalar, void* stream);
 /* Column sums: out[j] (+)= sum_i x[i*ld + j], i<rows, j<cols. */
 int ainp_colsum(const float* x, int64_t rows, int64_t cols, int64_t ld,
                 float* out, int accumulate, void* stream);

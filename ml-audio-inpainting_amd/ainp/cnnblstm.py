@@ -1,0 +1,377 @@
+"""StackedBLSTMCNN on the MI355X kernels (models/CNNBLSTM/model.py:16-108).
+
+The module keeps the reference's constructor (a YAML config path), its
+submodule tree (encoder / lstm / projection / decoder as nn.Sequential /
+nn.LSTM / nn.Linear, so state_dict keys and torch's default initialisation --
+including the RNG draw order -- are identical to the reference), and its
+forward/reconstruct_spectrogram semantics.  Only the arithmetic moves: the
+forward is four autograd Functions whose forward AND backward launch the
+libainp kernels:
+
+  _ConvStackFn  conv3x3 (+BatchNorm2d+ReLU) blocks; each BN+ReLU is applied
+                inside the next conv's input load, the encoder's last block is
+                written straight into the LSTM's [N, T, C*F] layout
+                (model.py:34-44,70-74 / 53-61,87)
+  _BLSTMFn      nn.LSTM(bidirectional, batch_first): one MFMA GEMM per layer
+                for both directions' input projections + the register-resident
+                recurrence kernel (model.py:46-47,77)
+  _ProjFn       nn.Linear(2H, 16F) written directly as the decoder's
+                [N, 16, F, T] input (model.py:50,80-83)
+  _L1Pow10LossFn the training loss of models/CNNBLSTM/train.py:70,104
+
+BatchNorm statistics are optionally all-reduced across data-parallel ranks
+through `comm` (SyncBN), so a DP run matches the single-process reference.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import yaml
+
+from . import ops
+
+
+def load_config(config_path):
+    """models/CNNBLSTM/model.py:10-14."""
+    with open(config_path, "r") as f:
+        return yaml.safe_load(f)
+
+
+def _allreduce(comm, t):
+    if comm is not None:
+        comm.allreduce_sum_(t)
+    return t
+
+
+# ------------------------------------------------------------------ conv stack
+class _ConvStackFn(torch.autograd.Function):
+    """Sequence of Conv2d(3x3,p1) [+ BatchNorm2d + ReLU] blocks.
+
+    spec: list of (has_bn, bn_module_or_None) per block; params: per block
+    (w, b[, gamma, beta]).  out_ntcf: final BN+ReLU output written [N,W,C*H].
+    """
+
+    @staticmethod
+    def forward(ctx, x, spec, training, out_ntcf, comm, *params):
+        N, _, H, W = x.shape
+        saved_y = []
+        affine = []          # per BN block: (scale, shift, save or None)
+        act = (None, None)   # prologue for the next conv
+        h = x
+        pi = 0
+        count = N * H * W * (comm.world_size if comm is not None else 1)
+        for bi, (has_bn, bn) in enumerate(spec):
+            w, b = params[pi], params[pi + 1]
+            pi += 2
+            want_stats = has_bn and training
+            y, stats = ops.conv3x3_fwd(h, w, b, act[0], act[1], want_stats=want_stats)
+            saved_y.append(y)
+            if has_bn:
+                gamma, beta = params[pi], params[pi + 1]
+                pi += 2
+                if training:
+                    sums = _allreduce(comm, ops.bn_stats_reduce(stats, y.shape[1]))
+                    rm = bn.running_mean if bn.track_running_stats else None
+                    rv = bn.running_var if bn.track_running_stats else None
+                    mom = bn.momentum if bn.momentum is not None else 0.1
+                    sc, sh, sv = ops.bn_finalize(sums, count, gamma, beta, rm, rv, mom, bn.eps)
+                    if bn.track_running_stats:
+                        bn.num_batches_tracked.add_(1)
+                else:
+                    sc, sh = ops.bn_eval_affine(gamma, beta, bn.running_mean,
+                                                bn.running_var, bn.eps)
+                    sv = None
+                affine.append((sc, sh, sv))
+                act = (sc, sh)
+            else:
+                affine.append(None)
+                act = (None, None)
+            h = y
+        last = affine[-1]
+        if last is not None:
+            out = ops.bn_relu_apply(saved_y[-1], last[0], last[1], ntcf=out_ntcf)
+        else:
+            out = saved_y[-1]
+        ctx.spec = spec
+        ctx.out_ntcf = out_ntcf
+        ctx.comm = comm
+        ctx.count = count
+        ctx.affine = affine
+        ctx.save_for_backward(x, *saved_y, *params)
+        ctx.nblocks = len(spec)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        nb = ctx.nblocks
+        tensors = ctx.saved_tensors
+        x = tensors[0]
+        ys = tensors[1:1 + nb]
+        params = tensors[1 + nb:]
+        # parameter index of each block
+        idx, pi = [], 0
+        for has_bn, _ in ctx.spec:
+            idx.append(pi)
+            pi += 4 if has_bn else 2
+        grads = [None] * len(params)
+        g = g.contiguous()
+        gx = None
+        for bi in range(nb - 1, -1, -1):
+            has_bn, _ = ctx.spec[bi]
+            p0 = idx[bi]
+            w = params[p0]
+            y = ys[bi]
+            if has_bn:
+                sc, sh, sv = ctx.affine[bi]
+                ntcf = ctx.out_ntcf and bi == nb - 1
+                sums = _allreduce(ctx.comm, ops.bn_relu_bwd_reduce(g, y, sc, sh, sv, ntcf))
+                gy, dgam, dbet = ops.bn_relu_bwd_apply(g, y, sc, sh, params[p0 + 2], sv, sums,
+                                                       ctx.count, ntcf)
+                grads[p0 + 2], grads[p0 + 3] = dgam, dbet
+            else:
+                gy = g.view_as(y) if g.shape != y.shape else g
+            if bi > 0:
+                prev = ctx.affine[bi - 1]
+                xin = ys[bi - 1]
+                pro = (prev[0], prev[1]) if prev is not None else (None, None)
+            else:
+                xin = x
+                pro = (None, None)
+            dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1])
+            grads[p0], grads[p0 + 1] = dw, db
+            if bi > 0 or ctx.needs_input_grad[0]:
+                g = ops.conv3x3_dgrad(gy, w)
+                if bi == 0:
+                    gx = g
+        return (gx, None, None, None, None, *grads)
+
+
+# ------------------------------------------------------------------ BLSTM
+class _BLSTMFn(torch.autograd.Function):
+    """nn.LSTM(I, H, L, batch_first=True, bidirectional=True) forward/backward.
+    params: nn.LSTM's _flat_weights order, per layer
+    (w_ih, w_hh, b_ih, b_hh, w_ih_rev, w_hh_rev, b_ih_rev, b_hh_rev)."""
+
+    @staticmethod
+    def forward(ctx, x, H, L, *params):
+        N, T, I = x.shape
+        NT = N * T
+        inp = x.reshape(NT, I)
+        saved = []
+        h = None
+        for l in range(L):
+            wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
+            Il = inp.shape[1]
+            zx = torch.empty(N, T, 8 * H, device=x.device, dtype=torch.float32)
+            ops.gemm(NT, 4 * H, Il, [inp, inp], Il, 1, [wf, wr], 1, Il,
+                     [zx, zx[:, :, 4 * H:]], 8 * H, 1, bias1=[bif, bir], bias2=[bhf, bhr])
+            h, gates, cell = ops.lstm_rec_fwd(zx, hf, hr, H)
+            saved += [inp, h, gates, cell]
+            inp = h.view(NT, 2 * H)
+        ctx.H, ctx.L = H, L
+        ctx.save_for_backward(*saved, *params)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        H, L = ctx.H, ctx.L
+        st = ctx.saved_tensors
+        saved, params = st[:4 * L], st[4 * L:]
+        dh = dh.contiguous()
+        N, T, _ = dh.shape
+        NT = N * T
+        grads = [None] * len(params)
+        dx = None
+        for l in range(L - 1, -1, -1):
+            inp, h, gates, cell = saved[4 * l:4 * l + 4]
+            wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
+            Il = inp.shape[1]
+            dg = ops.lstm_rec_bwd(dh, gates, cell, hf, hr, H)          # [N,T,8H]
+            dg2 = dg.view(NT, 8 * H)
+            hp = ops.lstm_hprev(h, H).view(NT, 2 * H)
+            gwh = [torch.empty(4 * H, H, device=dh.device) for _ in range(2)]
+            ops.gemm(4 * H, H, NT, [dg2, dg2[:, 4 * H:]], 1, 8 * H, [hp, hp[:, H:]], 2 * H, 1,
+                     gwh, H, 1)
+            gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
+            ops.gemm(4 * H, Il, NT, [dg2, dg2[:, 4 * H:]], 1, 8 * H, [inp, inp], Il, 1,
+                     gwi, Il, 1)
+            db_ih = ops.colsum(dg2)
+            db_hh = ops.colsum(dg2)
+            base = 8 * l
+            grads[base + 0], grads[base + 1] = gwi[0], gwh[0]
+            grads[base + 2], grads[base + 3] = db_ih[:4 * H], db_hh[:4 * H]
+            grads[base + 4], grads[base + 5] = gwi[1], gwh[1]
+            grads[base + 6], grads[base + 7] = db_ih[4 * H:], db_hh[4 * H:]
+            if l > 0 or ctx.needs_input_grad[0]:
+                dxi = torch.empty(NT, Il, device=dh.device)
+                ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,
+                         [dxi, dxi], Il, 1, ksplit=True)
+                dh = dxi.view(N, T, Il)
+                dx = dh
+        return (dx, None, None, *grads)
+
+
+# ------------------------------------------------------------------ projection
+class _ProjFn(torch.autograd.Function):
+    """nn.Linear(2H, C*F) + view(N,T,C,F).permute(0,2,3,1) -> [N, C, F, T]."""
+
+    @staticmethod
+    def forward(ctx, h, w, b, C, F):
+        N, T, K = h.shape
+        out = torch.empty(N, C, F, T, device=h.device, dtype=torch.float32)
+        NO = C * F
+        # per example n: out_n[t][col] = h_n[t] . w[col] + b[col], stored col*T + t
+        ops.gemm(T, NO, K, [h], K, 1, [w], 1, K, [out], 1, T, strideA=T * K,
+                 strideC=NO * T, nstrided=N, bias1=[b])
+        ctx.save_for_backward(h, w)
+        ctx.shape = (N, C, F, T)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.saved_tensors
+        N, C, F, T = ctx.shape
+        NO = C * F
+        K = h.shape[2]
+        g = g.contiguous()
+        dh = torch.empty(N, T, K, device=h.device, dtype=torch.float32)
+        # dh_n[t][k] = sum_col g_n[col][t] w[col][k]
+        ops.gemm(T, K, NO, [g], 1, T, [w], K, 1, [dh], K, 1, strideA=NO * T, strideC=T * K,
+                 nstrided=N)
+        dw = torch.empty(NO, K, device=h.device, dtype=torch.float32)
+        # dw[col][k] = sum_{n,t} g_n[col][t] h_n[t][k]   (k-split over examples)
+        ops.gemm(NO, K, T, [g], T, 1, [h], K, 1, [dw], K, 1, strideA=NO * T, strideB=T * K,
+                 nstrided=N, ksplit=True)
+        # db[col] = sum_{n,t} g_n[col][t]: the same k-split GEMM against ones
+        db = torch.empty(NO, device=h.device, dtype=torch.float32)
+        ops.gemm(NO, 1, T, [g], T, 1, [_ones(T, h.device)], 1, 1, [db], 1, 1,
+                 strideA=NO * T, nstrided=N, ksplit=True)
+        return dh, dw, db, None, None
+
+
+_ONES: dict = {}
+
+
+def _ones(n, device):
+    key = (n, str(device))
+    t = _ONES.get(key)
+    if t is None:
+        t = torch.ones(n, 1, device=device, dtype=torch.float32)
+        _ONES[key] = t
+    return t
+
+
+# ------------------------------------------------------------------ loss
+class _L1Pow10LossFn(torch.autograd.Function):
+    """nn.L1Loss(reduction='sum')((10 ** y) * m, |target| * m)."""
+
+    @staticmethod
+    def forward(ctx, y, mask, target):
+        y = y.contiguous()
+        loss, dy = ops.l1_pow10_loss(y, mask.contiguous(), target.contiguous(),
+                                     want_grad=y.requires_grad)
+        ctx.save_for_backward(dy if dy is not None else y)
+        return loss.to(torch.float32).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (dy,) = ctx.saved_tensors
+        return ops.scale_by_scalar(dy, g), None, None
+
+
+def l1_pow10_loss(y, mask, target):
+    """Training loss of models/CNNBLSTM/train.py:104 on the fused kernel."""
+    return _L1Pow10LossFn.apply(y, mask, target)
+
+
+train_step_reference_loss = l1_pow10_loss
+
+
+# ------------------------------------------------------------------ module
+class StackedBLSTMCNN(nn.Module):
+    """Drop-in for models/CNNBLSTM/model.py:StackedBLSTMCNN."""
+
+    def __init__(self, config_path=None, config: dict | None = None):
+        super().__init__()
+        full_cfg = config if config is not None else load_config(config_path)
+        mdl_cfg = full_cfg["model"]
+        self.in_channels = mdl_cfg["in_channels"]
+        self.n_layers = mdl_cfg["num_lstm_layers"]
+        self.hidden_dim = mdl_cfg["lstm_hidden_dim"]
+        self.freq_bins = full_cfg["data"]["spectrogram"]["n_fft"] // 2 + 1
+        self.using_phase = self.in_channels == 2
+        self.enc_filters = mdl_cfg["enc_filters"]
+        self.dec_filters = mdl_cfg["dec_filters"]
+        # identical construction order to model.py:34-61 (same init RNG draws)
+        self.encoder = nn.Sequential(
+            nn.Conv2d(self.in_channels, self.enc_filters[0], kernel_size=3, padding=1),
+            nn.BatchNorm2d(self.enc_filters[0]),
+            nn.ReLU(),
+            nn.Conv2d(self.enc_filters[0], self.enc_filters[1], kernel_size=3, padding=1),
+            nn.BatchNorm2d(self.enc_filters[1]),
+            nn.ReLU(),
+            nn.Conv2d(self.enc_filters[1], self.hidden_dim // 2, kernel_size=3, padding=1),
+            nn.BatchNorm2d(self.hidden_dim // 2),
+            nn.ReLU(),
+        )
+        self.lstm = nn.LSTM(input_size=self.freq_bins * self.hidden_dim // 2,
+                            hidden_size=self.hidden_dim, num_layers=self.n_layers,
+                            batch_first=True, bidirectional=True)
+        self.projection = nn.Linear(self.hidden_dim * 2, self.freq_bins * self.dec_filters[0])
+        self.decoder = nn.Sequential(
+            nn.Conv2d(self.dec_filters[0], self.dec_filters[1], kernel_size=3, padding=1),
+            nn.BatchNorm2d(self.dec_filters[1]),
+            nn.ReLU(),
+            nn.Conv2d(self.dec_filters[1], self.dec_filters[0], kernel_size=3, padding=1),
+            nn.BatchNorm2d(self.dec_filters[0]),
+            nn.ReLU(),
+            nn.Conv2d(self.dec_filters[0], self.in_channels, kernel_size=3, padding=1),
+        )
+        self.comm = None  # set by ainp.dist for SyncBN across DP ranks
+
+    # -- helpers ----------------------------------------------------------
+    @staticmethod
+    def _stack(seq):
+        spec, params = [], []
+        mods = list(seq)
+        i = 0
+        while i < len(mods):
+            conv = mods[i]
+            bn = mods[i + 1] if i + 1 < len(mods) and isinstance(mods[i + 1], nn.BatchNorm2d) else None
+            params += [conv.weight, conv.bias]
+            if bn is not None:
+                params += [bn.weight, bn.bias]
+                spec.append((True, bn))
+                i += 3  # conv, bn, relu
+            else:
+                spec.append((False, None))
+                i += 1
+        return spec, params
+
+    def forward(self, x):
+        """x: (batch, in_channels, freq_bins, timeframes) -> (batch, F, T)."""
+        if x.device.type != "cuda":
+            raise RuntimeError("ainp StackedBLSTMCNN runs on the MI355X kernels only; "
+                               "move the model and inputs to a GPU")
+        batch_size, _, freq_bins, timeframes = x.shape
+        x = x.contiguous()
+        spec, params = self._stack(self.encoder)
+        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, *params)
+        z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, *self.lstm._flat_weights)
+        # model.py:82 hard-codes 16 decoder channels
+        p = _ProjFn.apply(z, self.projection.weight, self.projection.bias, 16, freq_bins)
+        spec, params = self._stack(self.decoder)
+        y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, *params)
+        return y.squeeze(1)
+
+    def reconstruct_spectrogram(self, log_spectrogram_gap, gap_mask):
+        """model.py:92-108: model output inside the gap, input elsewhere."""
+        if not self.using_phase:
+            rec = self(log_spectrogram_gap.unsqueeze(1))
+        else:
+            rec = self(log_spectrogram_gap)
+        gap_mask = gap_mask.float()
+        if self.using_phase:
+            rec = rec[:, 0, :, :] + rec[:, 1, :, :] * 1j
+            log_spectrogram_gap = log_spectrogram_gap[:, 0, :, :] + log_spectrogram_gap[:, 1, :, :] * 1j
+        return rec * gap_mask + log_spectrogram_gap * (1 - gap_mask)

