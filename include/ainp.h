@@ -97,8 +97,10 @@ int ainp_stft_features(const float* audio, int64_t n_clips, int64_t n_samples,
  * times nstrided strided batches; batch b uses pointer entry b % nptr offset
  * by (b / nptr) * stride{A,B,C}.  bias1/bias2: host arrays (may be NULL, or
  * hold NULL entries) of per-pointer-batch bias vectors of length N.
- * ksplit != 0: all nptr*nstrided (A,B) pairs are summed into C[0]
- * (K-concatenation across separate buffers / strided slabs). */
+ * ksplit == 1: all nptr*nstrided (A,B) pairs are summed into C[0]
+ * (K-concatenation across separate buffers / strided slabs).
+ * ksplit == 2: for each pointer batch p, its nstrided (A,B) pairs are summed
+ * into C[p] (split-K with one partial slab per pointer batch). */
 int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
                   const float* const* A, int64_t sam, int64_t sak,
                   int64_t strideA, const float* const* B, int64_t sbk,
@@ -230,6 +232,13 @@ int ainp_l1_pow10_loss(const float* y, const float* mask, const float* target,
  * by the autograd grad_output without a host sync). */
 int ainp_scale_by_dev(const float* x, float* out, int64_t n,
                       const float* scalar, void* stream);
+/* out[i] = sum_s x[s*n + i] over nslabs slabs (split-K combine, fixed order). */
+int ainp_sum_slabs(const float* x, int64_t nslabs, int64_t n, float* out,
+                   void* stream);
+/* out[r] = sum_b sum_c x[(b*rows + r)*cols + c] (bias gradient of a layer
+ * whose output is [nb, rows, cols]). */
+int ainp_rowsum_batched(const float* x, int64_t nb, int64_t rows, int64_t cols,
+                        float* out, void* stream);
 /* Column sums: out[j] (+)= sum_i x[i*ld + j], i<rows, j<cols. */
 int ainp_colsum(const float* x, int64_t rows, int64_t cols, int64_t ld,
                 float* out, int accumulate, void* stream);

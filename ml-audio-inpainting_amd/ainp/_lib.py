@@ -61,6 +61,8 @@ _SIGS = {
     "ainp_lstm_hprev": (c_int, [P, P, c_int64, c_int64, c_int, P]),
     "ainp_l1_pow10_loss": (c_int, [P, P, P, c_int64, P, P, c_float, P]),
     "ainp_scale_by_dev": (c_int, [P, P, c_int64, P, P]),
+    "ainp_sum_slabs": (c_int, [P, c_int64, c_int64, P, P]),
+    "ainp_rowsum_batched": (c_int, [P, c_int64, c_int64, c_int64, P, P]),
     "ainp_colsum": (c_int, [P, c_int64, c_int64, c_int64, P, c_int, P]),
     "ainp_adam": (c_int, [PP, PP, PP, PP, POINTER(c_int64), c_int, c_double, c_double,
                           c_double, c_double, c_double, c_int64, P]),

@@ -189,12 +189,10 @@ class _BLSTMFn(torch.autograd.Function):
             dg = ops.lstm_rec_bwd(dh, gates, cell, hf, hr, H)          # [N,T,8H]
             dg2 = dg.view(NT, 8 * H)
             hp = ops.lstm_hprev(h, H).view(NT, 2 * H)
-            gwh = [torch.empty(4 * H, H, device=dh.device) for _ in range(2)]
-            ops.gemm(4 * H, H, NT, [dg2, dg2[:, 4 * H:]], 1, 8 * H, [hp, hp[:, H:]], 2 * H, 1,
-                     gwh, H, 1)
-            gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
-            ops.gemm(4 * H, Il, NT, [dg2, dg2[:, 4 * H:]], 1, 8 * H, [inp, inp], Il, 1,
-                     gwi, Il, 1)
+            # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs for
+            # the recurrent / upper layers -> parallel split-K over row chunks
+            gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H))
+            gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il, offsets_b=(0, 0))
             db_ih = ops.colsum(dg2)
             db_hh = ops.colsum(dg2)
             base = 8 * l
@@ -238,27 +236,27 @@ class _ProjFn(torch.autograd.Function):
         # dh_n[t][k] = sum_col g_n[col][t] w[col][k]
         ops.gemm(T, K, NO, [g], 1, T, [w], K, 1, [dh], K, 1, strideA=NO * T, strideC=T * K,
                  nstrided=N)
-        dw = torch.empty(NO, K, device=h.device, dtype=torch.float32)
-        # dw[col][k] = sum_{n,t} g_n[col][t] h_n[t][k]   (k-split over examples)
-        ops.gemm(NO, K, T, [g], T, 1, [h], K, 1, [dw], K, 1, strideA=NO * T, strideB=T * K,
-                 nstrided=N, ksplit=True)
-        # db[col] = sum_{n,t} g_n[col][t]: the same k-split GEMM against ones
-        db = torch.empty(NO, device=h.device, dtype=torch.float32)
-        ops.gemm(NO, 1, T, [g], T, 1, [_ones(T, h.device)], 1, 1, [db], 1, 1,
-                 strideA=NO * T, nstrided=N, ksplit=True)
+        # dw[col][k] = sum_{n,t} g_n[col][t] h_n[t][k]: split the example sum
+        # over S pointer batches (S partial slabs, ksplit mode 2) so the small
+        # [C*F, 2H] output still fills the chip, then combine in fixed order.
+        S = _split_count(N)
+        per = N // S
+        slabs = torch.empty(S, NO, K, device=h.device, dtype=torch.float32)
+        ops.gemm(NO, K, T, [g[i * per] for i in range(S)], T, 1,
+                 [h[i * per] for i in range(S)], K, 1, [slabs[i] for i in range(S)], K, 1,
+                 strideA=NO * T, strideB=T * K, nstrided=per, ksplit=2)
+        dw = ops.sum_slabs(slabs, S).view(NO, K)
+        # db[col] = sum_{n,t} g_n[col][t]
+        db = ops.rowsum_batched(g.view(N, NO, T))
         return dh, dw, db, None, None
 
 
-_ONES: dict = {}
-
-
-def _ones(n, device):
-    key = (n, str(device))
-    t = _ONES.get(key)
-    if t is None:
-        t = torch.ones(n, 1, device=device, dtype=torch.float32)
-        _ONES[key] = t
-    return t
+def _split_count(n):
+    """Largest divisor of n that is <= 8 (pointer batches of the GEMM)."""
+    for s in (8, 4, 2, 1):
+        if n % s == 0:
+            return s
+    return 1
 
 
 # ------------------------------------------------------------------ loss

@@ -130,8 +130,35 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
          ptr_array([t.data_ptr() for t in A]), int(sam), int(sak), int(strideA),
          ptr_array([t.data_ptr() for t in B]), int(sbk), int(sbn), int(strideB),
          float(beta), ptr_array([t.data_ptr() for t in C]), int(scm), int(scn),
-         int(strideC), b1, b2, nptr, int(nstrided), 1 if ksplit else 0,
+         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit),
          _stream(ref if stream_of is None else stream_of))
+
+
+def _chunks_for(K, tiles, target_blocks=512, min_rows=64):
+    """Split count S (a divisor of K) so tiles*S ~ target workgroups."""
+    want = max(1, min(K // min_rows, target_blocks // max(1, tiles)))
+    for s in range(want, 0, -1):
+        if K % s == 0:
+            return s
+    return 1
+
+
+def gemm_tn_splitk(a, lda, b, ldb, K, M, N, offsets_b=(0, 0)):
+    """Two-direction weight-gradient GEMM C[d] = A_d^T B_d for the BLSTM:
+    A_d = a[:, d*M:(d+1)*M] ([K, M] row-major view, row stride lda),
+    B_d = b[:, off_d:off_d+N] ([K, N], row stride ldb); returns [C_0, C_1]
+    ([M, N] each).  K (= N*T rows) is split into S strided chunks computed
+    by independent workgroups into slabs, then summed in fixed order."""
+    tiles = -(-M // 128) * -(-N // 128) * 2
+    S = _chunks_for(K, tiles)
+    kc = K // S
+    slabs = torch.empty(2, S, M, N, device=a.device, dtype=torch.float32)
+    gemm(M, N, kc, [a, a[:, M:]], 1, lda, [b[:, offsets_b[0]:], b[:, offsets_b[1]:]], ldb, 1,
+         [slabs[0], slabs[1]], N, 1, strideA=kc * lda, strideB=kc * ldb, strideC=M * N,
+         nstrided=S)
+    if S == 1:
+        return [slabs[0, 0], slabs[1, 0]]
+    return [sum_slabs(slabs[0], S).view(M, N), sum_slabs(slabs[1], S).view(M, N)]
 
 
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
@@ -329,6 +356,21 @@ def scale_by_scalar(x, s):
     out = torch.empty_like(x)
     call("ainp_scale_by_dev", x.data_ptr(), out.data_ptr(), x.numel(), s.data_ptr(),
          _stream(x))
+    return out
+
+
+def sum_slabs(x, nslabs, out=None):
+    n = x.numel() // nslabs
+    if out is None:
+        out = torch.empty(n, device=x.device, dtype=torch.float32)
+    call("ainp_sum_slabs", x.data_ptr(), int(nslabs), int(n), out.data_ptr(), _stream(x))
+    return out
+
+
+def rowsum_batched(x3d):
+    nb, rows, cols = x3d.shape
+    out = torch.empty(rows, device=x3d.device, dtype=torch.float32)
+    call("ainp_rowsum_batched", x3d.data_ptr(), nb, rows, cols, out.data_ptr(), _stream(x3d))
     return out
 
 

@@ -34,8 +34,10 @@ struct FwdLds {
   static constexpr int WT = CV_KCH * LDW;
 };
 
-__host__ __device__ constexpr int fwd_stat_parts_dims(int) { return 0; }
-
+// Staging is register double-buffered: chunk c+1's global loads are issued
+// right after chunk c is committed to LDS, so they are in flight during
+// chunk c's MFMAs (a load->store loop per element would serialise one HBM
+// round trip per element).
 template <int CT, bool DGRAD>
 __global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
     const float* __restrict__ x, const float* __restrict__ w,
@@ -64,37 +66,63 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
 #pragma unroll
       for (int c = 0; c < CT; ++c) acc[r][p][c] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Staging map (no per-element index decode): lane = tile column (50 of 64
+  // lanes active), input row r = wave + 4*i with row order (rr, ci):
+  // rr = i>>1, ci = wave + 4*(i&1); weight row k = wave + 4*i with
+  // tap = i>>1, ci = wave + 4*(i&1), lane = output channel.
+  constexpr int NIR = CV_CK * (CV_FT + 2) / 4;   // 20 input rows per thread
+  constexpr int NWR = CV_KCH / 4;                // 18 weight rows per thread
+  float pin[NIR], pw[NWR];
+  const int tcol = t0 - 1 + lane;                // input column of this lane
+  const bool col_ok = lane < CV_TT + 2 && tcol >= 0 && tcol < W;
+  auto fetch = [&](int ci0) {
+    const int cg0 = ci0 + wave;
+    const float* xb = xn + (int64_t)cg0 * HW + (int64_t)(f0 - 1) * W + tcol;
+#pragma unroll
+    for (int i = 0; i < NIR; ++i) {
+      const int rr = i >> 1, cg = cg0 + 4 * (i & 1), f = f0 - 1 + rr;
+      float v = 0.f;
+      if (col_ok && cg < Cin && f >= 0 && f < H)
+        v = xb[(int64_t)(4 * (i & 1)) * HW + (int64_t)rr * W];
+      pin[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NWR; ++i) {
+      const int tap = i >> 1, cg = cg0 + 4 * (i & 1);
+      float v = 0.f;
+      if (lane < CT * 16 && lane < Cout && cg < Cin)
+        v = DGRAD ? w[((int64_t)cg * Cout + lane) * 9 + (8 - tap)]   // w'[co][cg] = w[cg][co] flipped
+                  : w[((int64_t)lane * Cin + cg) * 9 + tap];
+      pw[i] = v;
+    }
+  };
+  auto commit = [&](int ci0) {
+    const int cg0 = ci0 + wave;
+#pragma unroll
+    for (int i = 0; i < NIR; ++i) {
+      const int rr = i >> 1, ci = wave + 4 * (i & 1), cg = cg0 + 4 * (i & 1);
+      float v = pin[i];
+      if (in_scale) {
+        const int f = f0 - 1 + rr;
+        const bool ok = col_ok && cg < Cin && f >= 0 && f < H;
+        v = ok ? fmaxf(fmaf(v, in_scale[cg], in_shift[cg]), 0.f) : 0.f;
+      }
+      if (lane < CV_TT + 2) s_in[ci * CV_PLANE + rr * CV_LDT + lane] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NWR; ++i) {
+      const int k = (i >> 1) * 8 + wave + 4 * (i & 1);
+      if (lane < CT * 16) s_w[k * L::LDW + lane] = pw[i];
+    }
+  };
+
   const int nchunk = (Cin + CV_CK - 1) / CV_CK;
+  fetch(0);
   for (int ch = 0; ch < nchunk; ++ch) {
-    const int ci0 = ch * CV_CK;
-    // stage input halo tile [CK][FT+2][TT+2] with prologue + zero padding
-    for (int idx = tid; idx < CV_CK * (CV_FT + 2) * (CV_TT + 2); idx += 256) {
-      const int cc = idx % (CV_TT + 2);
-      const int rr = (idx / (CV_TT + 2)) % (CV_FT + 2);
-      const int ci = idx / ((CV_TT + 2) * (CV_FT + 2));
-      const int f = f0 + rr - 1, t = t0 + cc - 1, cg = ci0 + ci;
-      float v = 0.f;
-      if (cg < Cin && f >= 0 && f < H && t >= 0 && t < W) {
-        v = xn[(int64_t)cg * HW + (int64_t)f * W + t];
-        if (in_scale) v = fmaxf(fmaf(v, in_scale[cg], in_shift[cg]), 0.f);
-      }
-      s_in[ci * CV_PLANE + rr * CV_LDT + cc] = v;
-    }
-    // stage weights as [k = tap*8+ci][co]
-    for (int idx = tid; idx < CV_KCH * CT * 16; idx += 256) {
-      const int co = idx % (CT * 16);
-      const int k = idx / (CT * 16);
-      const int tap = k >> 3, ci = k & 7, cg = ci0 + ci;
-      float v = 0.f;
-      if (cg < Cin && co < Cout) {
-        if (DGRAD)  // conv input channel cg = forward output channel
-          v = w[((int64_t)cg * Cout + co) * 9 + (8 - tap)];
-        else
-          v = w[((int64_t)co * Cin + cg) * 9 + tap];
-      }
-      s_w[k * L::LDW + co] = v;
-    }
+    if (ch > 0) __syncthreads();  // previous chunk's LDS reads are done
+    commit(ch * CV_CK);
     __syncthreads();
+    if (ch + 1 < nchunk) fetch((ch + 1) * CV_CK);
 
     const float* a_base = s_in + kq * CV_PLANE + li;
     const float* b_base = s_w + kq * L::LDW + li;
@@ -115,7 +143,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
           for (int c = 0; c < CT; ++c) acc[r][p][c] = mfma16x16x4(af, bf[c], acc[r][p][c]);
         }
     }
-    __syncthreads();
   }
 
   // epilogue: D[pixel = 4*kq + j][co = li] in register j
@@ -178,24 +205,26 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
 }
 
 // ---------------------------------------------------------------- wgrad
-// Persistent workgroups each reduce a strided set of 4x64 pixel tiles into
+// Persistent workgroups each reduce a strided set of 2x64 pixel tiles into
 // register accumulators D[co][j], j = tap*Cin + ci, then write one partial
-// slab; a second kernel sums the slabs in fixed order (deterministic).
-constexpr int WG_FT = 4, WG_TT = 64;
+// slab; a two-stage kernel sums the slabs in fixed order (deterministic).
+// Tile t+1's act(x) halo and dy are prefetched into registers while tile t's
+// MFMAs run.
+constexpr int WG_FT = 2, WG_TT = 64;
 constexpr int WG_LDT = 68;         // >= TT+2
-constexpr int WG_XPLANE = 418;     // >= (FT+2)*LDT = 408, == 2 mod 32
-constexpr int WG_GPLANE = 258;     // >= FT*TT = 256, == 2 mod 32 (dy tile)
+constexpr int WG_XPLANE = 290;     // >= (FT+2)*LDT = 272, == 2 mod 32
+constexpr int WG_GPLANE = 130;     // >= FT*TT = 128, == 2 mod 32 (dy tile)
 constexpr int WG_CIMAX = 32;       // input channels staged per pass
 
 template <int CT, int JT>
-__global__ __launch_bounds__(256, 1) void conv3x3_wgrad_mfma(
+__global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
     float* __restrict__ partial, int N, int Cin, int Cout, int H, int W,
     int ci0, int cin_pass) {
   // this pass covers input channels [ci0, ci0+cin_pass), j = tap*cin_pass+ci
   __shared__ __attribute__((aligned(16))) float s_x[WG_CIMAX * WG_XPLANE];
-  __shared__ __attribute__((aligned(16))) float s_g[64 * WG_GPLANE];
+  __shared__ __attribute__((aligned(16))) float s_g[CT * 16 * WG_GPLANE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 15, kq = lane >> 4;
   // wave -> (co tile, subset of j tiles)
@@ -228,36 +257,78 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_mfma(
   const int64_t HW = (int64_t)H * W;
   const bool ct_ok = ct < CT && wave < CT * WPC;
 
-  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // Staging map: lane = tile column.  act(x) interior: wave = halo row rr
+  // (0..3), loop index = input channel; the 2 halo columns x 4 rows x
+  // cin_pass are one element per thread.  dy: rr = wave&1, co = (wave>>1)+2i.
+  constexpr int NGR = CT * 8;                    // dy rows per thread
+  float px[WG_CIMAX], pxh, pg[NGR];
+  const int hside = tid & 1, hrr = (tid >> 1) & 3, hci = tid >> 3;  // halo element
+  auto tile_coords = [&](int64_t tile, int& n, int& f0, int& t0) {
     const int tt = tile % tiles_t;
     const int tf = (tile / tiles_t) % tiles_f;
-    const int n = tile / ((int64_t)tiles_t * tiles_f);
-    const int f0 = tf * WG_FT, t0 = tt * WG_TT;
-    // stage act(x) halo tile
-    for (int idx = tid; idx < cin_pass * (WG_FT + 2) * (WG_TT + 2); idx += 256) {
-      const int cc = idx % (WG_TT + 2);
-      const int rr = (idx / (WG_TT + 2)) % (WG_FT + 2);
-      const int ci = idx / ((WG_TT + 2) * (WG_FT + 2));
-      const int f = f0 + rr - 1, t = t0 + cc - 1, cg = ci0 + ci;
-      float v = 0.f;
-      if (f >= 0 && f < H && t >= 0 && t < W) {
-        v = x[((int64_t)n * Cin + cg) * HW + (int64_t)f * W + t];
-        if (in_scale) v = fmaxf(fmaf(v, in_scale[cg], in_shift[cg]), 0.f);
+    n = (int)(tile / ((int64_t)tiles_t * tiles_f));
+    f0 = tf * WG_FT;
+    t0 = tt * WG_TT;
+  };
+  auto fetch = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+    const int f = f0 - 1 + wave, t = t0 + lane;
+    const bool ok = f >= 0 && f < H && t < W;
+    const float* xb = x + ((int64_t)n * Cin + ci0) * HW + (int64_t)f * W + t;
+#pragma unroll
+    for (int i = 0; i < WG_CIMAX; ++i)
+      px[i] = (ok && i < cin_pass) ? xb[(int64_t)i * HW] : 0.f;
+    {
+      const int fh = f0 - 1 + hrr, th = hside ? t0 + WG_TT : t0 - 1;
+      pxh = (hci < cin_pass && fh >= 0 && fh < H && th >= 0 && th < W)
+                ? x[((int64_t)n * Cin + ci0 + hci) * HW + (int64_t)fh * W + th]
+                : 0.f;
+    }
+    const int fg = f0 + (wave & 1);
+    const bool gok = fg < H && t < W;
+    const float* gb = dy + ((int64_t)n * Cout + (wave >> 1)) * HW + (int64_t)fg * W + t;
+#pragma unroll
+    for (int i = 0; i < NGR; ++i) {
+      const int co = (wave >> 1) + 2 * i;
+      pg[i] = (gok && co < Cout) ? gb[(int64_t)(2 * i) * HW] : 0.f;
+    }
+  };
+  auto commit = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+    const int f = f0 - 1 + wave, t = t0 + lane;
+    const bool ok = f >= 0 && f < H && t < W;
+#pragma unroll
+    for (int i = 0; i < WG_CIMAX; ++i) {
+      if (i < cin_pass) {
+        float v = px[i];
+        if (in_scale) v = ok ? fmaxf(fmaf(v, in_scale[ci0 + i], in_shift[ci0 + i]), 0.f) : 0.f;
+        s_x[i * WG_XPLANE + wave * WG_LDT + lane + 1] = v;
       }
-      s_x[ci * WG_XPLANE + rr * WG_LDT + cc] = v;
     }
-    // stage dy tile [co][FT*TT] (zero outside the image)
-    for (int idx = tid; idx < CT * 16 * WG_FT * WG_TT; idx += 256) {
-      const int cc = idx % WG_TT;
-      const int rr = (idx / WG_TT) % WG_FT;
-      const int co = idx / (WG_TT * WG_FT);
-      const int f = f0 + rr, t = t0 + cc;
-      float v = 0.f;
-      if (co < Cout && f < H && t < W)
-        v = dy[((int64_t)n * Cout + co) * HW + (int64_t)f * W + t];
-      s_g[co * WG_GPLANE + rr * WG_TT + cc] = v;
+    if (hci < cin_pass) {
+      float v = pxh;
+      if (in_scale) {
+        const int fh = f0 - 1 + hrr, th = hside ? t0 + WG_TT : t0 - 1;
+        const bool hok = fh >= 0 && fh < H && th >= 0 && th < W;
+        v = hok ? fmaxf(fmaf(v, in_scale[ci0 + hci], in_shift[ci0 + hci]), 0.f) : 0.f;
+      }
+      s_x[hci * WG_XPLANE + hrr * WG_LDT + (hside ? WG_TT + 1 : 0)] = v;
     }
+#pragma unroll
+    for (int i = 0; i < NGR; ++i) {
+      const int co = (wave >> 1) + 2 * i;
+      s_g[co * WG_GPLANE + (wave & 1) * WG_TT + lane] = pg[i];
+    }
+  };
+
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    commit(tile);
     __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
     if (ct_ok) {
       const float* ga = s_g + (ct * 16 + li) * WG_GPLANE + kq;
 #pragma unroll 4
@@ -274,7 +345,7 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_mfma(
     }
     __syncthreads();
   }
-  // write partial slab: [Cout_pad=CT*16][J] for this block (+ bias partial)
+  // write partial slab: [Cout_pad=CT*16][J+1] for this block (+ bias column)
   float* slab = partial + (int64_t)blockIdx.x * (CT * 16) * (J + 1);
   if (ct_ok) {
 #pragma unroll
@@ -296,7 +367,28 @@ __global__ __launch_bounds__(256, 1) void conv3x3_wgrad_mfma(
   }
 }
 
-// Sum the per-block slabs: out dw[co][ci0+ci][tap], dbias[co].
+// Stage 1: tmp[g][idx] = sum of slabs [g*per_group, (g+1)*per_group).
+__global__ void wgrad_reduce1(const float* __restrict__ partial, int nparts,
+                              int per, int per_group, float* __restrict__ tmp) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= per) return;
+  const int g = blockIdx.y;
+  const int b0 = g * per_group;
+  int b1 = b0 + per_group;
+  if (b1 > nparts) b1 = nparts;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int b = b0;
+  for (; b + 3 < b1; b += 4) {
+    a0 += partial[(int64_t)(b + 0) * per + idx];
+    a1 += partial[(int64_t)(b + 1) * per + idx];
+    a2 += partial[(int64_t)(b + 2) * per + idx];
+    a3 += partial[(int64_t)(b + 3) * per + idx];
+  }
+  for (; b < b1; ++b) a0 += partial[(int64_t)b * per + idx];
+  tmp[(int64_t)g * per + idx] = (a0 + a1) + (a2 + a3);
+}
+
+// Stage 2: sum the group partials; out dw[co][ci0+ci][tap], dbias[co].
 __global__ void wgrad_reduce(const float* __restrict__ partial, int nparts,
                              int CTp, int J, int cin_pass, int ci0, int Cin,
                              int Cout, float* __restrict__ dw,
@@ -306,17 +398,18 @@ __global__ void wgrad_reduce(const float* __restrict__ partial, int nparts,
   if (idx >= per) return;
   const int co = idx / (J + 1), j = idx % (J + 1);
   if (co >= Cout) return;
-  double s = 0.0;
+  float s = 0.f;
   for (int b = 0; b < nparts; ++b) s += partial[(int64_t)b * per + idx];
   if (j == J) {
-    if (write_bias && dbias) dbias[co] = (float)s;
+    if (write_bias && dbias) dbias[co] = s;
   } else {
     const int tap = j / cin_pass, ci = j % cin_pass;
-    dw[((int64_t)co * Cin + ci0 + ci) * 9 + tap] = (float)s;
+    dw[((int64_t)co * Cin + ci0 + ci) * 9 + tap] = s;
   }
 }
 
 constexpr int WG_BLOCKS = 512;
+constexpr int WG_GROUPS = 16;  // stage-1 groups of WG_BLOCKS/WG_GROUPS slabs
 
 static int wgrad_ct(int Cout) { return (Cout + 15) / 16; }
 static int wgrad_pass(int Cin) { return Cin < WG_CIMAX ? Cin : WG_CIMAX; }
@@ -394,7 +487,7 @@ extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
   const int cp = wgrad_pass(Cin);
   int ct = wgrad_ct(Cout);
   if (ct == 3) ct = 4;
-  return (size_t)WG_BLOCKS * ct * 16 * (9 * cp + 1) * sizeof(float);
+  return (size_t)(WG_BLOCKS + WG_GROUPS) * ct * 16 * (9 * cp + 1) * sizeof(float);
 }
 
 extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
@@ -438,8 +531,13 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
     if (rc) return rc;
     const int J = 9 * cp;
     const int per = CTp * 16 * (J + 1);
+    float* tmp = partial + (size_t)WG_BLOCKS * per;
+    hipLaunchKernelGGL(wgrad_reduce1, dim3((per + 255) / 256, WG_GROUPS), dim3(256), 0, s,
+                       partial, WG_BLOCKS, per, WG_BLOCKS / WG_GROUPS, tmp);
+    rc = check_launch("wgrad_reduce1");
+    if (rc) return rc;
     hipLaunchKernelGGL(wgrad_reduce, dim3((per + 255) / 256), dim3(256), 0, s,
-                       partial, WG_BLOCKS, CTp * 16, J, cp, ci0, Cin, Cout, dw,
+                       tmp, WG_GROUPS, CTp * 16, J, cp, ci0, Cin, Cout, dw,
                        dbias, ci0 == 0 ? 1 : 0);
     rc = check_launch("wgrad_reduce");
     if (rc) return rc;

@@ -25,6 +25,7 @@ struct GemmPtrs {
   const float* bias2[8];
   int64_t sA, sB, sC;  // strides between strided batches
   int nptr;            // pointer batches; batch b -> (b % nptr, b / nptr)
+  int ksplit_mode;     // 0 none, 1 sum all batches into C[0], 2 per pointer batch
 };
 
 typedef float f32x16v __attribute__((ext_vector_type(16)));
@@ -158,9 +159,21 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_f32_kernel(
   const int64_t nk = (K + BK - 1) / BK;
   const int64_t total = nk * nseg;
 
+  // ksplit mode 1 (nseg = all batches): batch index = segment; mode 2
+  // (nseg = nstrided, grid.y = pointer batch): segment walks the strided
+  // batches of this block's pointer batch.
+  const bool per_ptr = ptrs.ksplit_mode == 2;
   auto seg_ptr = [&](int64_t it, const float*& a, const float*& b, int64_t& k0) {
-    const int bi = (nseg > 1) ? (int)(it / nk) : batch;
-    const int pb = bi % ptrs.nptr, sb = bi / ptrs.nptr;
+    const int seg = (int)(it / nk);
+    int pb, sb;
+    if (per_ptr) {
+      pb = batch;
+      sb = seg;
+    } else {
+      const int bi = (nseg > 1) ? seg : batch;
+      pb = bi % ptrs.nptr;
+      sb = bi / ptrs.nptr;
+    }
     a = ptrs.A[pb] + sb * ptrs.sA;
     b = ptrs.B[pb] + sb * ptrs.sB;
     k0 = (it % nk) * BK;
@@ -209,10 +222,10 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_f32_kernel(
   }
 
   // epilogue: D[row=(r&3)+8*(r>>2)+4*lh][col=li] of each 32x32 tile
-  const int cb = nseg > 1 ? 0 : batch;
-  float* C = ptrs.C[cb % ptrs.nptr] + (cb / ptrs.nptr) * ptrs.sC;
-  const float* bias1 = ptrs.bias1[cb % ptrs.nptr];
-  const float* bias2 = ptrs.bias2[cb % ptrs.nptr];
+  const int cb = per_ptr ? batch : (nseg > 1 ? 0 : batch);
+  float* C = per_ptr ? ptrs.C[cb] : ptrs.C[cb % ptrs.nptr] + (cb / ptrs.nptr) * ptrs.sC;
+  const float* bias1 = ptrs.bias1[per_ptr ? cb : cb % ptrs.nptr];
+  const float* bias2 = ptrs.bias2[per_ptr ? cb : cb % ptrs.nptr];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -286,6 +299,7 @@ extern "C" int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
   p.sB = strideB;
   p.sC = strideC;
   p.nptr = nptr;
+  p.ksplit_mode = ksplit;
   // contiguous dimension of each operand (prefer k when both strides are 1)
   const bool akc = (sak == 1);
   const bool bkc = (sbk == 1);
@@ -298,10 +312,12 @@ extern "C" int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
     avec = avec && aligned16(A[i]);
     bvec = bvec && aligned16(B[i]);
   }
+  if (ksplit < 0 || ksplit > 2) return record_msg("ainp_gemm_f32: ksplit must be 0, 1 or 2");
   if (ksplit && nb > (1 << 20)) return record_msg("ainp_gemm_f32: too many segments");
-  const int nseg = ksplit ? (int)nb : 1;
+  const int nseg = ksplit == 1 ? (int)nb : (ksplit == 2 ? (int)nstrided : 1);
   const int64_t tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
-  dim3 grid((unsigned)(tiles_m * tiles_n), ksplit ? 1 : (unsigned)nb);
+  const unsigned gy = ksplit == 1 ? 1u : (ksplit == 2 ? (unsigned)nptr : (unsigned)nb);
+  dim3 grid((unsigned)(tiles_m * tiles_n), gy);
   hipStream_t s = as_stream(stream);
   if (akc && bkc)
     launch_gemm<true, true>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);

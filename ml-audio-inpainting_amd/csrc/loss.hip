@@ -62,9 +62,69 @@ __global__ void scale_by_dev_kernel(const float* __restrict__ x,
     out[i] = x[i] * v;
 }
 
+// out[i] = sum_s x[s*n + i]  (fixed order: deterministic split-K combine)
+__global__ void sum_slabs_kernel(const float* __restrict__ x, int64_t nslabs,
+                                 int64_t n, float* __restrict__ out) {
+  for (int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i4 * 4 < n;
+       i4 += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = i4 * 4;
+    if (i + 3 < n && (n & 3) == 0) {
+      float4 a = *reinterpret_cast<const float4*>(x + i);
+      for (int64_t s = 1; s < nslabs; ++s) {
+        const float4 b = *reinterpret_cast<const float4*>(x + s * n + i);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      *reinterpret_cast<float4*>(out + i) = a;
+    } else {
+      for (int64_t e = i; e < i + 4 && e < n; ++e) {
+        float a = 0.f;
+        for (int64_t s = 0; s < nslabs; ++s) a += x[s * n + e];
+        out[e] = a;
+      }
+    }
+  }
+}
+
+// out[r] = sum_b sum_c x[(b*rows + r)*cols + c]; one wave per row.
+__global__ __launch_bounds__(256) void rowsum_batched_kernel(
+    const float* __restrict__ x, int64_t nb, int64_t rows, int64_t cols,
+    float* __restrict__ out) {
+  const int64_t r = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < nb; ++b) {
+    const float* p = x + (b * rows + r) * cols;
+    for (int64_t c = lane; c < cols; c += 64) s += p[c];
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[r] = s;
+}
+
 }  // namespace ainp
 
 using namespace ainp;
+
+extern "C" int ainp_sum_slabs(const float* x, int64_t nslabs, int64_t n,
+                              float* out, void* stream) {
+  if (!x || !out || nslabs < 1 || n < 0) return record_msg("ainp_sum_slabs: bad argument");
+  if (n == 0) return AINP_OK;
+  int64_t grid = cdiv(cdiv(n, 4), 256);
+  if (grid > 4096) grid = 4096;
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)grid), dim3(256), 0,
+                     as_stream(stream), x, nslabs, n, out);
+  return check_launch("sum_slabs");
+}
+
+extern "C" int ainp_rowsum_batched(const float* x, int64_t nb, int64_t rows,
+                                   int64_t cols, float* out, void* stream) {
+  if (!x || !out || nb < 1 || rows < 0 || cols < 1)
+    return record_msg("ainp_rowsum_batched: bad argument");
+  if (rows == 0) return AINP_OK;
+  hipLaunchKernelGGL(rowsum_batched_kernel, dim3((unsigned)cdiv(rows, 4)), dim3(256),
+                     0, as_stream(stream), x, nb, rows, cols, out);
+  return check_launch("rowsum_batched");
+}
 
 extern "C" int ainp_scale_by_dev(const float* x, float* out, int64_t n,
                                  const float* scalar, void* stream) {

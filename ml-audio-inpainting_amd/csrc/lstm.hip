@@ -5,13 +5,12 @@
 // are one big MFMA GEMM (gemm.hip) done before the recurrence; what remains
 // per time step is h_{t-1} W_hh^T (4H x H) plus the gate nonlinearities.
 //
-// Mapping: one workgroup of 2H lanes per (sequence, direction) pair, W_hh held
-// in VGPRs for the whole sequence (2H floats per lane: at H=128 that is 256
-// VGPRs, one wave per SIMD), h_{t-1} broadcast from LDS.  Lane pair (2j,2j+1)
-// owns hidden unit j: lane 2j the (i,f) gate rows, lane 2j+1 the (g,o) rows;
-// the pair swaps pre-activations with one xor-shuffle and both finish the cell
-// update.  No inter-workgroup traffic at all: the 2*N sequence-directions run
-// as independent workgroups, one step = one LDS barrier.
+// Mapping: one workgroup of 4H lanes per (sequence, direction) pair, W_hh held
+// in VGPRs for the whole sequence (one gate row = H floats per lane: 128 VGPRs
+// at H=128, two waves per SIMD), h_{t-1} broadcast from LDS.  The lane quad
+// (4u..4u+3) owns hidden unit u's gates i,f,g,o and exchanges them with DPP.
+// No inter-workgroup traffic at all: the 2*N sequence-directions run as
+// independent workgroups, one step = one LDS barrier.
 // Per-step inputs (zx rows, and for the backward the saved gates/cells/dh) are
 // staged 16 steps at a time through LDS by register-prefetched chunk loads.
 //
@@ -24,28 +23,46 @@ constexpr int LCH = 16;  // steps per staged chunk
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
 
+// Per-step workgroup barrier that orders LDS only.  __syncthreads() would also
+// wait (vmcnt(0)) for the step's global stores of h/c/gates, putting a full
+// store round trip on the sequential critical path of every time step.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Quad broadcast: value of lane (4*(lane/4) + Q) to every lane of the quad.
+template <int Q>
+__device__ __forceinline__ float quad_bcast(float v) {
+  constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);  // DPP quad_perm
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
+}
+
+// Forward recurrence.  4H lanes per (sequence, direction): lane = 4u + g owns
+// gate row r = g*H + u of W_hh (H VGPRs; at H=128 no accumulator-file round
+// trips), so a hidden unit's four gates (i,f,g,o) sit in one lane quad and are
+// exchanged with DPP quad broadcasts.  h_{t-1} is read from LDS as broadcast
+// ds_read_b128.  One LDS barrier per step.
 template <int H>
-__global__ __launch_bounds__(2 * H, 1) void lstm_fwd_kernel(
+__global__ __launch_bounds__(4 * H, 1) void lstm_fwd_kernel(
     const float* __restrict__ zx, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, float* __restrict__ h_out,
     float* __restrict__ gates, float* __restrict__ cell, int T) {
-  constexpr int NT = 2 * H;         // threads
+  constexpr int NT = 4 * H;         // threads
   constexpr int G4 = 4 * H;         // gate rows
-  constexpr int PF = LCH * G4 / 4 / NT;  // float4 prefetched per thread (=8)
+  constexpr int PF = LCH * G4 / 4 / NT;  // float4 prefetched per thread (=LCH/4)
   __shared__ __attribute__((aligned(16))) float zs[2][LCH][G4];
   __shared__ __attribute__((aligned(16))) float hb[2][H];
 
   const int n = blockIdx.x >> 1, dir = blockIdx.x & 1;
-  const int tid = threadIdx.x, j = tid >> 1, half = tid & 1;
+  const int tid = threadIdx.x, u = tid >> 2, g = tid & 3;
+  const int row = g * H + u;
   const float* whh = dir ? whh_r : whh_f;
-  const int row0 = half ? 2 * H + j : j;
-  const int row1 = half ? 3 * H + j : H + j;
 
-  float w0[H], w1[H];
+  float w[H];
 #pragma unroll
-  for (int k = 0; k < H; ++k) {
-    w0[k] = whh[(int64_t)row0 * H + k];
-    w1[k] = whh[(int64_t)row1 * H + k];
+  for (int k = 0; k < H; k += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(whh + (int64_t)row * H + k);
+    w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
   }
   if (tid < H) hb[1][tid] = 0.f;
 
@@ -79,9 +96,9 @@ __global__ __launch_bounds__(2 * H, 1) void lstm_fwd_kernel(
   __syncthreads();
 
   float c = 0.f;
-  float* hrow = h_out + (int64_t)n * T * 2 * H + dir * H + j;
-  float* crow = cell ? cell + (int64_t)n * T * 2 * H + dir * H + j : nullptr;
-  float* grow = gates ? gates + (int64_t)n * T * 8 * H + dir * G4 : nullptr;
+  float* hrow = h_out + (int64_t)n * T * 2 * H + dir * H + u;
+  float* crow = cell ? cell + (int64_t)n * T * 2 * H + dir * H + u : nullptr;
+  float* grow = gates ? gates + (int64_t)n * T * 8 * H + dir * G4 + row : nullptr;
 
   for (int ch = 0; ch < nch; ++ch) {
     const int buf = ch & 1;
@@ -90,43 +107,29 @@ __global__ __launch_bounds__(2 * H, 1) void lstm_fwd_kernel(
       const int t = ch * LCH + s;
       if (t >= T) break;  // uniform across the block
       const float* hp = hb[(t + 1) & 1];
-      float a0 = zs[buf][s][row0], a1 = zs[buf][s][row1];
-      float b0 = 0.f, b1 = 0.f, c0 = 0.f, c1 = 0.f, d0 = 0.f, d1 = 0.f;
+      float a0 = zs[buf][s][row], a1 = 0.f, a2 = 0.f, a3 = 0.f;
 #pragma unroll
       for (int k = 0; k < H; k += 4) {
         const float4 h4 = *reinterpret_cast<const float4*>(hp + k);
-        a0 = fmaf(w0[k + 0], h4.x, a0);
-        a1 = fmaf(w1[k + 0], h4.x, a1);
-        b0 = fmaf(w0[k + 1], h4.y, b0);
-        b1 = fmaf(w1[k + 1], h4.y, b1);
-        c0 = fmaf(w0[k + 2], h4.z, c0);
-        c1 = fmaf(w1[k + 2], h4.z, c1);
-        d0 = fmaf(w0[k + 3], h4.w, d0);
-        d1 = fmaf(w1[k + 3], h4.w, d1);
+        a0 = fmaf(w[k + 0], h4.x, a0);
+        a1 = fmaf(w[k + 1], h4.y, a1);
+        a2 = fmaf(w[k + 2], h4.z, a2);
+        a3 = fmaf(w[k + 3], h4.w, a3);
       }
-      const float p0 = (a0 + b0) + (c0 + d0);
-      const float p1 = (a1 + b1) + (c1 + d1);
-      const float q0 = __shfl_xor(p0, 1, 64);
-      const float q1 = __shfl_xor(p1, 1, 64);
-      const float ip = half ? q0 : p0, fp = half ? q1 : p1;
-      const float gp = half ? p0 : q0, op = half ? p1 : q1;
-      const float ig = sigm(ip), fg = sigm(fp), gg = tanhf(gp), og = sigm(op);
+      const float pre = (a0 + a1) + (a2 + a3);
+      const float act = (g == 2) ? tanhf(pre) : sigm(pre);
+      const float ig = quad_bcast<0>(act), fg = quad_bcast<1>(act);
+      const float gg = quad_bcast<2>(act), og = quad_bcast<3>(act);
       c = fmaf(fg, c, ig * gg);
       const float h = og * tanhf(c);
       const int64_t tt = tix(t);
-      if (!half) {
-        hb[t & 1][j] = h;
+      if (g == 0) {
+        hb[t & 1][u] = h;
         hrow[tt * 2 * H] = h;
         if (crow) crow[tt * 2 * H] = c;
-        if (grow) {
-          grow[tt * 8 * H + j] = ig;
-          grow[tt * 8 * H + H + j] = fg;
-        }
-      } else if (grow) {
-        grow[tt * 8 * H + 2 * H + j] = gg;
-        grow[tt * 8 * H + 3 * H + j] = og;
       }
-      __syncthreads();
+      if (grow) grow[tt * 8 * H] = act;
+      lds_barrier();
     }
     if (ch + 1 < nch) store_chunk(buf ^ 1);
     __syncthreads();
@@ -134,31 +137,33 @@ __global__ __launch_bounds__(2 * H, 1) void lstm_fwd_kernel(
 }
 
 // Backward through time.  Bwd step u walks the forward steps in reverse:
-// forward step t = T-1-u, time index tt(t).  Lane pair (2k,2k+1) also owns
-// the recurrent matvec output dh_rec[k] = sum_g dG[g] W[g][k]: lane 2k sums
-// g in [0,2H) (i,f rows), lane 2k+1 g in [2H,4H) (g,o rows).
+// forward step t = T-1-u, time index tt(t).  Lane = 4k + q: the quad of
+// hidden unit k computes the four gate gradients of unit k (lane q -> gate
+// q) and the recurrent matvec dh_rec[k] = sum_g dG[g] W[g][k], lane q summing
+// the gate block g in [qH, qH+H) with W[qH+m][k] (m < H) held in VGPRs; the
+// four partials are combined with DPP quad broadcasts.
 template <int H>
-__global__ __launch_bounds__(2 * H, 1) void lstm_bwd_kernel(
+__global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
     const float* __restrict__ dh_out, const float* __restrict__ gates,
     const float* __restrict__ cell, const float* __restrict__ whh_f,
     const float* __restrict__ whh_r, float* __restrict__ dgates, int T) {
-  constexpr int NT = 2 * H;
+  constexpr int NT = 4 * H;
   constexpr int G4 = 4 * H;
-  constexpr int PG = LCH * G4 / 4 / NT;            // float4 of gates per thread (8)
-  constexpr int PC = ((LCH + 1) * H + NT - 1) / NT;  // cell floats per thread (9)
-  constexpr int PD = LCH * H / NT;                 // dh floats per thread (8)
+  constexpr int DGS = H + 4;                        // padded gate-block stride (banks)
+  constexpr int PG = LCH * G4 / 4 / NT;             // float4 of gates per thread
+  constexpr int PC = ((LCH + 1) * H + NT - 1) / NT; // cell floats per thread
+  constexpr int PD = (LCH * H + NT - 1) / NT;       // dh floats per thread
   __shared__ __attribute__((aligned(16))) float gsm[2][LCH][G4];
   __shared__ float csm[2][LCH + 1][H];
   __shared__ float dsm[2][LCH][H];
-  __shared__ __attribute__((aligned(16))) float dgb[2][G4];
+  __shared__ __attribute__((aligned(16))) float dgb[2][4 * DGS];
 
   const int n = blockIdx.x >> 1, dir = blockIdx.x & 1;
-  const int tid = threadIdx.x, j = tid >> 1, half = tid & 1;
+  const int tid = threadIdx.x, k = tid >> 2, q = tid & 3;
   const float* whh = dir ? whh_r : whh_f;
-  // lane holds W[2H*half + q][j], q in [0, 2H)
-  float wt[2 * H];
+  float wt[H];  // W[q*H + m][k]
 #pragma unroll
-  for (int q = 0; q < 2 * H; ++q) wt[q] = whh[(int64_t)(2 * H * half + q) * H + j];
+  for (int m = 0; m < H; ++m) wt[m] = whh[(int64_t)(q * H + m) * H + k];
 
   auto tix = [&](int t) { return dir ? (T - 1 - t) : t; };
   const float* gbase = gates + (int64_t)n * T * 8 * H + dir * G4;
@@ -190,7 +195,7 @@ __global__ __launch_bounds__(2 * H, 1) void lstm_bwd_kernel(
       const int idx = tid + i * NT;
       const int s = idx / H, r = idx % H;
       const int t = T - 1 - (ch * LCH + s);
-      pd[i] = (t >= 0) ? dbase[(int64_t)tix(t) * 2 * H + r] : 0.f;
+      pd[i] = (s < LCH && t >= 0) ? dbase[(int64_t)tix(t) * 2 * H + r] : 0.f;
     }
   };
   auto store_chunk = [&](int buf) {
@@ -209,7 +214,8 @@ __global__ __launch_bounds__(2 * H, 1) void lstm_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < PD; ++i) {
       const int idx = tid + i * NT;
-      dsm[buf][idx / H][idx % H] = pd[i];
+      const int s = idx / H, r = idx % H;
+      if (s < LCH) dsm[buf][s][r] = pd[i];
     }
   };
 
@@ -219,55 +225,45 @@ __global__ __launch_bounds__(2 * H, 1) void lstm_bwd_kernel(
   __syncthreads();
 
   float dh_rec = 0.f, dc_next = 0.f;
-  float* dgrow = dgates + (int64_t)n * T * 8 * H + dir * G4;
+  float* dgrow = dgates + (int64_t)n * T * 8 * H + dir * G4 + q * H + k;
   for (int ch = 0; ch < nch; ++ch) {
     const int buf = ch & 1;
     if (ch + 1 < nch) load_chunk(ch + 1);
     for (int s = 0; s < LCH; ++s) {
-      const int u = ch * LCH + s;
-      if (u >= T) break;
-      const int t = T - 1 - u;
-      const float ig = gsm[buf][s][j], fg = gsm[buf][s][H + j];
-      const float gg = gsm[buf][s][2 * H + j], og = gsm[buf][s][3 * H + j];
-      const float cc = csm[buf][s][j];
-      const float cp = (t > 0) ? csm[buf][s + 1][j] : 0.f;
-      const float dh = dsm[buf][s][j] + dh_rec;
+      const int uu = ch * LCH + s;
+      if (uu >= T) break;
+      const int t = T - 1 - uu;
+      const float ig = gsm[buf][s][k], fg = gsm[buf][s][H + k];
+      const float gg = gsm[buf][s][2 * H + k], og = gsm[buf][s][3 * H + k];
+      const float cc = csm[buf][s][k];
+      const float cp = (t > 0) ? csm[buf][s + 1][k] : 0.f;
+      const float dh = dsm[buf][s][k] + dh_rec;
       const float tc = tanhf(cc);
-      const float dog = dh * tc;
       const float dc = fmaf(dh * og, 1.f - tc * tc, dc_next);
-      const float dig = dc * gg, dgg = dc * ig, dfg = dc * cp;
       dc_next = dc * fg;
-      const float dai = dig * ig * (1.f - ig);
-      const float daf = dfg * fg * (1.f - fg);
-      const float dag = dgg * (1.f - gg * gg);
-      const float dao = dog * og * (1.f - og);
+      float da;
+      if (q == 0) da = (dc * gg) * ig * (1.f - ig);            // d pre_i
+      else if (q == 1) da = (dc * cp) * fg * (1.f - fg);       // d pre_f
+      else if (q == 2) da = (dc * ig) * (1.f - gg * gg);       // d pre_g
+      else da = (dh * tc) * og * (1.f - og);                   // d pre_o
       const int64_t tt = tix(t);
-      float* dgr = dgrow + tt * 8 * H;
-      float* db = dgb[u & 1];
-      if (!half) {
-        db[j] = dai;
-        db[H + j] = daf;
-        dgr[j] = dai;
-        dgr[H + j] = daf;
-      } else {
-        db[2 * H + j] = dag;
-        db[3 * H + j] = dao;
-        dgr[2 * H + j] = dag;
-        dgr[3 * H + j] = dao;
-      }
-      __syncthreads();
-      const float* dq = db + 2 * H * half;
+      float* db = dgb[uu & 1];
+      db[q * DGS + k] = da;
+      dgrow[tt * 8 * H] = da;
+      lds_barrier();
+      const float* dq = db + q * DGS;
       float a = 0.f, b = 0.f, c = 0.f, d = 0.f;
 #pragma unroll
-      for (int q = 0; q < 2 * H; q += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(dq + q);
-        a = fmaf(wt[q + 0], v.x, a);
-        b = fmaf(wt[q + 1], v.y, b);
-        c = fmaf(wt[q + 2], v.z, c);
-        d = fmaf(wt[q + 3], v.w, d);
+      for (int m = 0; m < H; m += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(dq + m);
+        a = fmaf(wt[m + 0], v.x, a);
+        b = fmaf(wt[m + 1], v.y, b);
+        c = fmaf(wt[m + 2], v.z, c);
+        d = fmaf(wt[m + 3], v.w, d);
       }
       const float part = (a + b) + (c + d);
-      dh_rec = part + __shfl_xor(part, 1, 64);
+      dh_rec = (quad_bcast<0>(part) + quad_bcast<1>(part)) +
+               (quad_bcast<2>(part) + quad_bcast<3>(part));
     }
     if (ch + 1 < nch) store_chunk(buf ^ 1);
     __syncthreads();
@@ -305,9 +301,9 @@ extern "C" int ainp_lstm_rec_fwd(const float* zx, const float* const* w_hh,
   hipStream_t s = as_stream(stream);
   dim3 grid((unsigned)(2 * N));
   switch (H) {
-    case 32: hipLaunchKernelGGL(lstm_fwd_kernel<32>, grid, dim3(64), 0, s, zx, w_hh[0], w_hh[1], h_out, gates, cell, (int)T); break;
-    case 64: hipLaunchKernelGGL(lstm_fwd_kernel<64>, grid, dim3(128), 0, s, zx, w_hh[0], w_hh[1], h_out, gates, cell, (int)T); break;
-    case 128: hipLaunchKernelGGL(lstm_fwd_kernel<128>, grid, dim3(256), 0, s, zx, w_hh[0], w_hh[1], h_out, gates, cell, (int)T); break;
+    case 32: hipLaunchKernelGGL(lstm_fwd_kernel<32>, grid, dim3(128), 0, s, zx, w_hh[0], w_hh[1], h_out, gates, cell, (int)T); break;
+    case 64: hipLaunchKernelGGL(lstm_fwd_kernel<64>, grid, dim3(256), 0, s, zx, w_hh[0], w_hh[1], h_out, gates, cell, (int)T); break;
+    case 128: hipLaunchKernelGGL(lstm_fwd_kernel<128>, grid, dim3(512), 0, s, zx, w_hh[0], w_hh[1], h_out, gates, cell, (int)T); break;
     default: return record_msg("ainp_lstm_rec_fwd: H must be 32, 64 or 128");
   }
   return check_launch("lstm_fwd_kernel");
@@ -324,9 +320,9 @@ extern "C" int ainp_lstm_rec_bwd(const float* dh_out, const float* gates,
   hipStream_t s = as_stream(stream);
   dim3 grid((unsigned)(2 * N));
   switch (H) {
-    case 32: hipLaunchKernelGGL(lstm_bwd_kernel<32>, grid, dim3(64), 0, s, dh_out, gates, cell, w_hh[0], w_hh[1], dgates, (int)T); break;
-    case 64: hipLaunchKernelGGL(lstm_bwd_kernel<64>, grid, dim3(128), 0, s, dh_out, gates, cell, w_hh[0], w_hh[1], dgates, (int)T); break;
-    case 128: hipLaunchKernelGGL(lstm_bwd_kernel<128>, grid, dim3(256), 0, s, dh_out, gates, cell, w_hh[0], w_hh[1], dgates, (int)T); break;
+    case 32: hipLaunchKernelGGL(lstm_bwd_kernel<32>, grid, dim3(128), 0, s, dh_out, gates, cell, w_hh[0], w_hh[1], dgates, (int)T); break;
+    case 64: hipLaunchKernelGGL(lstm_bwd_kernel<64>, grid, dim3(256), 0, s, dh_out, gates, cell, w_hh[0], w_hh[1], dgates, (int)T); break;
+    case 128: hipLaunchKernelGGL(lstm_bwd_kernel<128>, grid, dim3(512), 0, s, dh_out, gates, cell, w_hh[0], w_hh[1], dgates, (int)T); break;
     default: return record_msg("ainp_lstm_rec_bwd: H must be 32, 64 or 128");
   }
   return check_launch("lstm_bwd_kernel");
