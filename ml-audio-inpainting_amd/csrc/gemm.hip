@@ -6,10 +6,12 @@
 // "Matrix cores"), matching the reference's fp32 numerics up to summation order.
 //
 // Tiling: 128x128 output tile per 256-thread workgroup (4 waves as 2x2, each
-// wave 64x64 = 2x2 MFMA 32x32 tiles, 64 accumulator VGPRs), K-tile 32,
-// LDS double buffer with register-staged prefetch of the next K-tile.
-// Both operands are staged k-major in LDS (As[k][m], Bs[k][n]) so every MFMA
-// operand read is one conflict-free ds_read_b32 with lanes along m (or n).
+// wave 64x64 = 2x2 MFMA 32x32 tiles, 64 accumulator VGPRs), K-tile 32, one
+// LDS image per operand with the next K-tile prefetched in registers.
+// k-contiguous operands keep a [row][k] image (16-byte stores, one
+// ds_read_b128 = 4 MFMA k-steps per lane); row-contiguous operands a [k][row]
+// image.  The MFMA k order inside an 8-k group is lane-half h -> k = 4h+e,
+// identical for A and B, so the sum over k is unchanged.
 #include "common.h"
 
 namespace ainp {
@@ -34,8 +36,8 @@ __device__ __forceinline__ f32x16v mfma32(float a, float b, f32x16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
 }
 
-// Load a ROWSxBK operand tile (ROWS along m or n, BK along k) into registers.
-// KC: source contiguous along k (element (r,k) at p[r*ld + k]);
+// Load a 128xBK operand tile (128 rows along m or n, BK along k) into
+// registers.  KC: source contiguous along k (element (r,k) at p[r*ld + k]);
 // otherwise contiguous along rows (element (r,k) at p[k*ld + r]).
 // VEC: 16-byte vector loads are legal (ld%4==0, extent%4==0, base aligned).
 template <bool KC, bool VEC>
@@ -89,8 +91,8 @@ struct TileLoader {
     }
   }
 
-  // Store into the k-major LDS image s[k][r] (row length LD).
-  template <int LD>
+  // KC: image s[r][k] (row length 36: 16-byte rows, conflict-free b128 reads
+  // and writes).  MC: image s[k][r] (row length 132).  Both 16-byte stores.
   __device__ __forceinline__ void store(float* s) const {
     const int tid = threadIdx.x;
 #pragma unroll
@@ -98,37 +100,46 @@ struct TileLoader {
       const int idx = tid + i * GEMM_THREADS;
       if (KC) {
         const int rr = idx >> 3, kk = (idx & 7) * 4;
-        s[(kk + 0) * LD + rr] = v[i].x;
-        s[(kk + 1) * LD + rr] = v[i].y;
-        s[(kk + 2) * LD + rr] = v[i].z;
-        s[(kk + 3) * LD + rr] = v[i].w;
+        *reinterpret_cast<float4*>(&s[rr * 36 + kk]) = v[i];
       } else {
         const int kk = idx >> 5, rr = (idx & 31) * 4;
-        *reinterpret_cast<float4*>(&s[kk * LD + rr]) = v[i];
+        *reinterpret_cast<float4*>(&s[kk * 132 + rr]) = v[i];
       }
     }
   }
 };
 
-// LDS row length: 129 for transposing (KC) stores -> conflict-free
-// ds_write_b32; 132 keeps 16-byte alignment for the vector stores.
 template <bool KC>
-struct LdsLd {
-  static constexpr int v = KC ? 129 : 132;
+struct Img {
+  static constexpr int SIZE = KC ? 128 * 36 : BK * 132;  // floats
+  // fragment of k-group kg (8 k): lane (row r, half h) gets k = 8kg+4h+e
+  __device__ __forceinline__ static float4 frag(const float* s, int r, int kg, int h) {
+    if (KC) return *reinterpret_cast<const float4*>(&s[r * 36 + kg * 8 + 4 * h]);
+    const int k = kg * 8 + 4 * h;
+    return make_float4(s[(k + 0) * 132 + r], s[(k + 1) * 132 + r], s[(k + 2) * 132 + r],
+                       s[(k + 3) * 132 + r]);
+  }
 };
 
+// Single-buffered LDS + one K-tile of register prefetch: 36 KB of LDS and
+// <=168 VGPRs -> 3 workgroups per CU (768 resident tiles on the chip).
 template <bool AKC, bool BKC, bool AVEC, bool BVEC>
-__global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_f32_kernel(
+__global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_kernel(
     int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda,
     int64_t ldb, float beta, int64_t scm, int64_t scn, int nseg, int tiles_n) {
-  constexpr int LDA = LdsLd<AKC>::v, LDB = LdsLd<BKC>::v;
-  __shared__ __attribute__((aligned(16))) float smem[2 * BK * (LDA + LDB)];
-  auto As = [&](int b) { return smem + b * (BK * LDA); };
-  auto Bs = [&](int b) { return smem + 2 * BK * LDA + b * (BK * LDB); };
+  __shared__ __attribute__((aligned(16))) float smem[Img<AKC>::SIZE + Img<BKC>::SIZE];
+  float* As = smem;
+  float* Bs = smem + Img<AKC>::SIZE;
 
-  // block -> tile; consecutive block ids walk down m within a column strip of
-  // 8 n-tiles so the B (weight) panel stays hot in the XCD's L2.
-  const int64_t bid = blockIdx.x;
+  // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs,
+  // so remap bid -> linear tile L giving each XCD a contiguous range of L
+  // (bijective for any grid size).  Within L, groups of 8 n-tiles walk down
+  // m, so the 8 blocks sharing an A panel run together on one XCD's L2.
+  const int64_t nwg = gridDim.x;
+  const int64_t bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8;
+  const int64_t q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
   const int64_t tiles_m = (M + BM - 1) / BM;
   const int64_t group = 8;
   const int64_t per_group = group * tiles_m;
@@ -185,40 +196,37 @@ __global__ __launch_bounds__(GEMM_THREADS, 2) void gemm_f32_kernel(
     seg_ptr(0, a, b, k0);
     la.load(a, lda, m0, k0, M, K);
     lb.load(b, ldb, n0, k0, N, K);
-    la.template store<LDA>(As(0));
-    lb.template store<LDB>(Bs(0));
   }
-  __syncthreads();
 
   for (int64_t it = 0; it < total; ++it) {
-    const int cur = it & 1;
-    const bool more = it + 1 < total;
-    if (more) {
+    if (it > 0) __syncthreads();  // every wave is done reading the LDS images
+    la.store(As);
+    lb.store(Bs);
+    __syncthreads();
+    if (it + 1 < total) {  // next K-tile's loads fly during this tile's MFMAs
       const float *a, *b;
       int64_t k0;
       seg_ptr(it + 1, a, b, k0);
       la.load(a, lda, m0, k0, M, K);
       lb.load(b, ldb, n0, k0, N, K);
     }
-    const float* as = As(cur);
-    const float* bs = Bs(cur);
 #pragma unroll
-    for (int kk = 0; kk < BK; kk += 2) {
-      float af[2], bf[2];
+    for (int kg = 0; kg < BK / 8; ++kg) {
+      float4 af[2], bf[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = as[(kk + lh) * LDA + wm + i * 32 + li];
+      for (int i = 0; i < 2; ++i) af[i] = Img<AKC>::frag(As, wm + i * 32 + li, kg, lh);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = bs[(kk + lh) * LDB + wn + j * 32 + li];
+      for (int j = 0; j < 2; ++j) bf[j] = Img<BKC>::frag(Bs, wn + j * 32 + li, kg, lh);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32(af[i], bf[j], acc[i][j]);
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mfma32(af[i].x, bf[j].x, acc[i][j]);
+          acc[i][j] = mfma32(af[i].y, bf[j].y, acc[i][j]);
+          acc[i][j] = mfma32(af[i].z, bf[j].z, acc[i][j]);
+          acc[i][j] = mfma32(af[i].w, bf[j].w, acc[i][j]);
+        }
     }
-    if (more) {
-      la.template store<LDA>(As(cur ^ 1));
-      lb.template store<LDB>(Bs(cur ^ 1));
-    }
-    __syncthreads();
   }
 
   // epilogue: D[row=(r&3)+8*(r>>2)+4*lh][col=li] of each 32x32 tile
