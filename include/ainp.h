@@ -84,6 +84,16 @@ int ainp_stft_features(const float* audio, int64_t n_clips, int64_t n_samples,
                        int64_t n_frames, int mode, float* out0, float* out1,
                        float* out2, float* out3, void* stream);
 
+/* Plain STFT, utils.extract_spectrogram -> librosa.stft (utils.py:192-234):
+ * audio [n_signals, n_samples] of dtype 0 = float32 or 1 = float64 (device);
+ * out complex64 (dtype 0) / complex128 (dtype 1) [n_signals, n_fft/2+1,
+ * n_frames], computed in float64.  center != 0: frame t starts at
+ * t*hop - n_fft/2 with zero padding (n_frames = 1 + n_samples/hop); else at
+ * t*hop (n_frames = 1 + (n_samples-n_fft)/hop). */
+int ainp_stft(const void* audio, int dtype, int64_t n_signals,
+              int64_t n_samples, const double* window, int n_fft, int hop,
+              int center, int64_t n_frames, void* out, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32, exact fp32)                    */
 /* ------------------------------------------------------------------------ */

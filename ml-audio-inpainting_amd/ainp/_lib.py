@@ -37,6 +37,7 @@ _SIGS = {
     "ainp_last_error": (c_char_p, []),
     "ainp_stft_features": (c_int, [P, c_int64, c_int64, P, P, c_int64, c_int64, c_int64,
                                    P, c_int, c_int, c_int64, c_int, P, P, P, P, P]),
+    "ainp_stft": (c_int, [P, c_int, c_int64, c_int64, P, c_int, c_int, c_int, c_int64, P, P]),
     "ainp_gemm_f32": (c_int, [c_int64, c_int64, c_int64, c_float, PP, c_int64, c_int64,
                               c_int64, PP, c_int64, c_int64, c_int64, c_float, PP,
                               c_int64, c_int64, c_int64, PP, PP, c_int, c_int64, c_int, P]),

@@ -114,6 +114,33 @@ def stft_features(audio: torch.Tensor, gap_start: torch.Tensor, gap_len: int,
     return tuple(o)
 
 
+def stft(audio: torch.Tensor, n_fft: int = 2048, hop_length: int = 512,
+         win_length: int | None = None, window: str = "hann", center: bool = True):
+    """librosa>=0.10 stft on the GPU: audio [..., S] float32/float64 cuda ->
+    complex64/complex128 [..., n_fft/2+1, n_frames] (ainp_stft)."""
+    _req(audio, "audio", dtype=None)
+    if audio.dtype not in (torch.float32, torch.float64):
+        raise TypeError("stft input must be float32 or float64")
+    lead = audio.shape[:-1]
+    S = audio.shape[-1]
+    x = audio.reshape(-1, S).contiguous()
+    win_length = n_fft if win_length is None else win_length
+    if center:
+        n_frames = 1 + S // hop_length
+    else:
+        if S < n_fft:
+            raise ValueError(f"n_fft={n_fft} is too large for input signal of length={S}")
+        n_frames = 1 + (S - n_fft) // hop_length
+    F = n_fft // 2 + 1
+    cdt = torch.complex64 if audio.dtype == torch.float32 else torch.complex128
+    out = torch.empty(x.shape[0], F, n_frames, device=audio.device, dtype=cdt)
+    w = _device_window(window, win_length, n_fft, audio.device)
+    call("ainp_stft", x.data_ptr(), 0 if audio.dtype == torch.float32 else 1, x.shape[0], S,
+         w.data_ptr(), int(n_fft), int(hop_length), 1 if center else 0, n_frames,
+         out.data_ptr(), _stream(audio))
+    return out.reshape(*lead, F, n_frames)
+
+
 # --------------------------------------------------------------------- GEMM
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
          strideA=0, strideB=0, strideC=0, bias1=None, bias2=None, nstrided=1,

@@ -173,6 +173,88 @@ __global__ __launch_bounds__(256) void stft_features_kernel(
   }
 }
 
+// Plain STFT (utils.extract_spectrogram / librosa.stft): one wave per
+// (signal, frame); real input of type Tin, output complex<Tin> [F][T] per
+// signal (real-FFT via one half-length complex FFT).  center: frames start at t*hop -
+// n_fft/2 with zero padding (librosa>=0.10 'constant'), else at t*hop.
+template <typename Tin>
+__global__ __launch_bounds__(256) void stft_plain_kernel(
+    const Tin* __restrict__ audio, int64_t n_samples, int64_t n_sig,
+    const double* __restrict__ window, int n_fft, int log2m, int hop,
+    int center, int64_t n_frames, Tin* __restrict__ out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int M = n_fft >> 1;
+  const int F = M + 1;
+  cd* tw = reinterpret_cast<cd*>(smem);
+  double* win = reinterpret_cast<double*>(tw + (M + 1));
+  cd* wbase = reinterpret_cast<cd*>(win + n_fft);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  cd* bufA = wbase + (size_t)wave * 2 * M;
+  cd* bufB = bufA + M;
+  for (int q = threadIdx.x; q <= M; q += blockDim.x) {
+    double sn, cs;
+    sincospi(-2.0 * (double)q / (double)n_fft, &sn, &cs);
+    tw[q] = {cs, sn};
+  }
+  for (int n = threadIdx.x; n < n_fft; n += blockDim.x) win[n] = window[n];
+  __syncthreads();
+  const int64_t total = n_sig * n_frames;
+  const int nw = blockDim.x >> 6;
+  for (int64_t base = (int64_t)blockIdx.x * nw; base < total;
+       base += (int64_t)gridDim.x * nw) {
+    const int64_t item = base + wave;
+    const bool valid = item < total;
+    const int64_t b = valid ? item / n_frames : 0;
+    const int64_t t = valid ? item % n_frames : 0;
+    const Tin* x = audio + b * n_samples;
+    const int64_t s0 = t * hop - (center ? (n_fft >> 1) : 0);
+    for (int m = lane; m < M; m += 64) {
+      double v[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int n = 2 * m + e;
+        const int64_t sidx = s0 + n;
+        const double a = (valid && sidx >= 0 && sidx < n_samples) ? (double)x[sidx] : 0.0;
+        v[e] = a * win[n];
+      }
+      bufA[m] = {v[0], v[1]};
+    }
+    __syncthreads();
+    cd* src = bufA;
+    cd* dst = bufB;
+    for (int st = 0; st < log2m; ++st) {
+      const int Ns = 1 << st;
+      for (int j = lane; j < (M >> 1); j += 64) {
+        const int k = j & (Ns - 1);
+        const cd w = tw[(k << (log2m - st))];
+        const int o = (j << 1) - k;
+        const cd aa = src[j];
+        const cd bb = cmul(w, src[j + (M >> 1)]);
+        dst[o] = {aa.re + bb.re, aa.im + bb.im};
+        dst[o + Ns] = {aa.re - bb.re, aa.im - bb.im};
+      }
+      __syncthreads();
+      cd* tmp = src;
+      src = dst;
+      dst = tmp;
+    }
+    if (valid) {
+      Tin* o = out + (b * F * n_frames + t) * 2;
+      for (int k = lane; k < F; k += 64) {
+        const cd zk = src[k & (M - 1)];
+        const cd zm = src[(M - k) & (M - 1)];
+        const cd ze = {0.5 * (zk.re + zm.re), 0.5 * (zk.im - zm.im)};
+        const cd zo = {0.5 * (zk.im + zm.im), -0.5 * (zk.re - zm.re)};
+        const cd r = cmul(tw[k], zo);
+        o[(size_t)k * n_frames * 2] = (Tin)(ze.re + r.re);
+        o[(size_t)k * n_frames * 2 + 1] = (Tin)(ze.im + r.im);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace ainp
 
 using namespace ainp;
@@ -215,4 +297,34 @@ extern "C" int ainp_stft_features(const float* audio, int64_t n_clips,
                        gap_start, batch, gap_len, sample_rate, window, n_fft,
                        log2m, hop, n_frames, out0, out1, out2, out3);
   return check_launch("ainp_stft_features");
+}
+
+extern "C" int ainp_stft(const void* audio, int dtype, int64_t n_signals,
+                         int64_t n_samples, const double* window, int n_fft,
+                         int hop, int center, int64_t n_frames, void* out,
+                         void* stream) {
+  if (!audio || !window || !out || n_signals < 0 || n_samples < 0 || hop <= 0 ||
+      n_frames < 0 || (dtype != 0 && dtype != 1))
+    return record_msg("ainp_stft: bad argument");
+  if (n_fft < 16 || n_fft > 2048 || (n_fft & (n_fft - 1)))
+    return record_msg("ainp_stft: n_fft must be a power of two in [16,2048]");
+  if (n_signals == 0 || n_frames == 0) return AINP_OK;
+  const int M = n_fft / 2;
+  int log2m = 0;
+  while ((1 << log2m) < M) ++log2m;
+  int nw = 4;
+  while (nw > 1 && (size_t)nw * 32 * M + 16 * (M + 1) + 8 * n_fft > 160 * 1024) nw >>= 1;
+  const size_t lds = (size_t)nw * 32 * M + 16 * (M + 1) + 8 * n_fft;
+  int64_t grid = cdiv(n_signals * n_frames, nw);
+  if (grid > 4096) grid = 4096;
+  hipStream_t s = as_stream(stream);
+  if (dtype == 0)
+    hipLaunchKernelGGL(stft_plain_kernel<float>, dim3(grid), dim3(64 * nw), lds, s,
+                       (const float*)audio, n_samples, n_signals, window, n_fft,
+                       log2m, hop, center, n_frames, (float*)out);
+  else
+    hipLaunchKernelGGL(stft_plain_kernel<double>, dim3(grid), dim3(64 * nw), lds, s,
+                       (const double*)audio, n_samples, n_signals, window, n_fft,
+                       log2m, hop, center, n_frames, (double*)out);
+  return check_launch("ainp_stft");
 }

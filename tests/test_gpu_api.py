@@ -1,0 +1,108 @@
+"""GPU tests of the mirrored reference API: utils.extract_spectrogram,
+LibriSpeechDataset.__getitem__ and the models/CNNBLSTM/train.py loop."""
+import os
+import wave
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from oracle import stft_ref
+from ainp import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _write_wav(path, x, sr=16000):
+    pcm = np.clip(np.round(np.asarray(x) * 32767), -32768, 32767).astype("<i2")
+    with wave.open(str(path), "wb") as w:
+        w.setnchannels(1)
+        w.setsampwidth(2)
+        w.setframerate(sr)
+        w.writeframes(pcm.tobytes())
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("center", [True, False])
+def test_extract_spectrogram_vs_oracle(dtype, center):
+    import utils
+    y = synth.synthetic_clip(7, 9000).astype(dtype)
+    X = utils.extract_spectrogram(y, n_fft=512, hop_length=192, win_length=384, center=center)
+    assert X.dtype == (np.complex64 if dtype == np.float32 else np.complex128)
+    if center:
+        R = stft_ref.stft(y, 512, 192, 384)
+    else:
+        w = stft_ref.padded_window("hann", 384, 512)
+        nfr = 1 + (len(y) - 512) // 192
+        idx = np.arange(512)[:, None] + 192 * np.arange(nfr)[None, :]
+        R = np.fft.rfft(y.astype(np.float64)[idx] * w[:, None], axis=0)
+    assert X.shape == R.shape
+    tol = 2e-6 if dtype == np.float32 else 1e-12
+    assert np.abs(X - R).max() <= tol * np.abs(R).max()
+    # torch tensor stays on the GPU
+    Xt = utils.extract_spectrogram(torch.from_numpy(y).cuda(), n_fft=512, hop_length=192,
+                                   win_length=384, center=center)
+    assert Xt.is_cuda and np.abs(Xt.cpu().numpy() - X).max() == 0
+
+
+def _tree(tmp_path, n_files, seconds):
+    for split in ("train-clean-100", "test-clean"):
+        d = tmp_path / "root" / split / "1" / "2"
+        d.mkdir(parents=True)
+        for i in range(n_files):
+            _write_wav(d / f"1-2-{i:04d}.wav", synth.synthetic_clip(50 + i, int(16000 * seconds)))
+
+
+def _cfg(tmp_path, n_files=2, gaps=3, max_len_s=4.0, batch=1, epochs=1):
+    return {
+        "data": {"dataset": "LibriSpeech", "root_path": str(tmp_path / "root"),
+                 "sample_rate": 16000, "train_path": "train-clean-100", "test_path": "test-clean",
+                 "max_len_s": max_len_s, "gap_len_s": 0.2, "n_files": n_files,
+                 "gaps_per_audio": gaps,
+                 "spectrogram": {"n_fft": 512, "hop_length": 192, "win_length": 384,
+                                 "window": "hann", "normalize": True, "power": 1.0}},
+        "model": {"input_dim": 334, "in_channels": 1, "num_lstm_layers": 2,
+                  "lstm_hidden_dim": 64, "enc_filters": [16, 32], "dec_filters": [16, 32]},
+        "training": {"batch_size": batch, "optimizer_type": "adam",
+                     "starter_learning_rate": 1e-4, "lr_decay": 1.0, "max_n_epochs": epochs},
+        "paths": {"tensorboard_dir": str(tmp_path / "tb"), "checkpoint_dir": str(tmp_path / "ck"),
+                  "log_dir": str(tmp_path / "logs"), "sample_dir": str(tmp_path / "samples"),
+                  "resume_mdl_path": None},
+        "logging": {"checkpoint_interval": 1, "metric_interval": 1, "spectrogram_interval": 100,
+                    "audio_interval": 500, "run_name": "t"},
+    }
+
+
+def test_dataset_item_matches_oracle(tmp_path):
+    from models.CNNBLSTM.dataset import LibriSpeechDataset
+    import utils
+    _tree(tmp_path, 2, 6.0)
+    cfg = _cfg(tmp_path)
+    ds = LibriSpeechDataset(None, "train", device="cuda", config=cfg)
+    np.random.seed(11)
+    lg, gi, gm, tg = ds[0]
+    assert lg.shape == (3, 257, 334) and tg.dtype == torch.complex64 and gi.shape == (3, 2)
+    audio, _ = utils.load_audio(ds.file_paths[0])
+    np.random.seed(11)
+    starts = [np.random.randint(0, 80000 - 3200) for _ in range(3)]
+    for i, s in enumerate(starts):
+        rl, rt, rm = stft_ref.cnnblstm_item(audio, s, 3200, 512, 192, 384, 16000, 334)
+        np.testing.assert_array_equal(gm[i].cpu().numpy(), rm)
+        assert np.abs(lg[i].cpu().numpy() - rl).max() < 2e-5
+        assert np.abs(tg[i].cpu().numpy() - rt).max() <= 2e-6 * np.abs(rt).max()
+        assert gi[i, 0].item() == np.float32(s / 16000)
+
+
+def test_train_script_runs_one_epoch(tmp_path):
+    from models.CNNBLSTM import train as train_mod
+    _tree(tmp_path, 3, 5.0)
+    cfg = _cfg(tmp_path, n_files=3, gaps=2, batch=2, epochs=1)  # 3 files, batch 2: partial batch (Q2)
+    p = tmp_path / "cfg.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    train_mod.main(str(p))
+    ck = list((tmp_path / "ck").rglob("blstm_cnn_epoch_1.pt"))
+    assert len(ck) == 1
+    sd = torch.load(ck[0], weights_only=True)
+    assert "lstm.weight_ih_l0_reverse" in sd and "encoder.1.running_var" in sd
+    assert all(torch.isfinite(v).all() for v in sd.values() if v.is_floating_point())

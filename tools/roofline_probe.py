@@ -1,0 +1,20 @@
+"""Launch only the bench's roofline kernel (LSTM layer-0 input projection GEMM,
+M=N*T=10688, N=8H=1024, K=C*F=16448, fp32) a few times: the target of the
+rocprofv3 --pmc passes that give profiles/traffic_gemm_l0.json."""
+import os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ml-audio-inpainting_amd"))
+import torch
+from ainp import ops
+H, F, B, T = 128, 257, 32, 334
+M, I = B * T, (H // 2) * F
+dev = "cuda"
+A = torch.randn(M, I, device=dev)
+W = [torch.randn(4 * H, I, device=dev) * 0.01 for _ in range(2)]
+b = [torch.zeros(4 * H, device=dev) for _ in range(4)]
+zx = torch.empty(M, 8 * H, device=dev)
+for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 5):
+    ops.gemm(M, 4 * H, I, [A, A], I, 1, W, 1, I, [zx, zx[:, 4 * H:]], 8 * H, 1,
+             bias1=b[:2], bias2=b[2:])
+torch.cuda.synchronize()
+print("done")
