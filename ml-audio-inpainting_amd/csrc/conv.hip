@@ -367,16 +367,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
   }
 }
 
-// Stage 1: tmp[g][idx] = sum of slabs [g*per_group, (g+1)*per_group).
+// Stage 1: tmp[g][idx] = sum of slabs [g*per_group, (g+1)*per_group), fp64
+// (the first conv's weight gradient is a heavily cancelling sum: its input
+// sits near log10(1e-9) while the BatchNorm-backward output sums to ~0).
 __global__ void wgrad_reduce1(const float* __restrict__ partial, int nparts,
-                              int per, int per_group, float* __restrict__ tmp) {
+                              int per, int per_group, double* __restrict__ tmp) {
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= per) return;
   const int g = blockIdx.y;
   const int b0 = g * per_group;
   int b1 = b0 + per_group;
   if (b1 > nparts) b1 = nparts;
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
   int b = b0;
   for (; b + 3 < b1; b += 4) {
     a0 += partial[(int64_t)(b + 0) * per + idx];
@@ -389,7 +391,7 @@ __global__ void wgrad_reduce1(const float* __restrict__ partial, int nparts,
 }
 
 // Stage 2: sum the group partials; out dw[co][ci0+ci][tap], dbias[co].
-__global__ void wgrad_reduce(const float* __restrict__ partial, int nparts,
+__global__ void wgrad_reduce(const double* __restrict__ partial, int nparts,
                              int CTp, int J, int cin_pass, int ci0, int Cin,
                              int Cout, float* __restrict__ dw,
                              float* __restrict__ dbias, int write_bias) {
@@ -398,13 +400,13 @@ __global__ void wgrad_reduce(const float* __restrict__ partial, int nparts,
   if (idx >= per) return;
   const int co = idx / (J + 1), j = idx % (J + 1);
   if (co >= Cout) return;
-  float s = 0.f;
+  double s = 0.0;
   for (int b = 0; b < nparts; ++b) s += partial[(int64_t)b * per + idx];
   if (j == J) {
-    if (write_bias && dbias) dbias[co] = s;
+    if (write_bias && dbias) dbias[co] = (float)s;
   } else {
     const int tap = j / cin_pass, ci = j % cin_pass;
-    dw[((int64_t)co * Cin + ci0 + ci) * 9 + tap] = s;
+    dw[((int64_t)co * Cin + ci0 + ci) * 9 + tap] = (float)s;
   }
 }
 
@@ -487,7 +489,7 @@ extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
   const int cp = wgrad_pass(Cin);
   int ct = wgrad_ct(Cout);
   if (ct == 3) ct = 4;
-  return (size_t)(WG_BLOCKS + WG_GROUPS) * ct * 16 * (9 * cp + 1) * sizeof(float);
+  return (size_t)(WG_BLOCKS + 2 * WG_GROUPS) * ct * 16 * (9 * cp + 1) * sizeof(float);
 }
 
 extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
@@ -531,7 +533,7 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
     if (rc) return rc;
     const int J = 9 * cp;
     const int per = CTp * 16 * (J + 1);
-    float* tmp = partial + (size_t)WG_BLOCKS * per;
+    double* tmp = reinterpret_cast<double*>(partial + (size_t)WG_BLOCKS * per);
     hipLaunchKernelGGL(wgrad_reduce1, dim3((per + 255) / 256, WG_GROUPS), dim3(256), 0, s,
                        partial, WG_BLOCKS, per, WG_BLOCKS / WG_GROUPS, tmp);
     rc = check_launch("wgrad_reduce1");

@@ -1,0 +1,40 @@
+"""Record the ReLU branch the HIP kernels took after every BatchNorm2d.
+
+The kernels apply BatchNorm+ReLU as relu(fmaf(y, scale, shift)) inside the
+next conv's input load, and the backward keeps gz = g where
+fmaf(y, scale, shift) > 0.  ainp_bn_relu_apply evaluates exactly that
+expression, so applying it to the recorded pre-BatchNorm conv output with the
+recorded (scale, shift) reproduces the kernels' mask bit for bit.  The masks
+feed oracle.cnnblstm_ref.forward(relu_masks=...) (test infrastructure only).
+"""
+import contextlib
+
+import torch.nn as nn
+
+
+@contextlib.contextmanager
+def recording(model):
+    """with recording(model) as masks: <forward>  ->  masks {bn_name: bool cpu}"""
+    from ainp import ops
+    names = [n for n, m in model.named_modules() if isinstance(m, nn.BatchNorm2d)]
+    masks = {}
+    last = {}
+    f_conv, f_fin = ops.conv3x3_fwd, ops.bn_finalize
+
+    def conv(*a, **k):
+        out = f_conv(*a, **k)
+        last["y"] = out[0]
+        return out
+
+    def fin(*a, **k):
+        out = f_fin(*a, **k)
+        sc, sh = out[0], out[1]
+        name = names[len(masks)]
+        masks[name] = (ops.bn_relu_apply(last["y"], sc, sh) > 0).cpu()
+        return out
+
+    ops.conv3x3_fwd, ops.bn_finalize = conv, fin
+    try:
+        yield masks
+    finally:
+        ops.conv3x3_fwd, ops.bn_finalize = f_conv, f_fin
