@@ -36,18 +36,86 @@ class Comm:
 
 
 class GradAllReducer:
-    """Bucketed SUM all-reduce of parameter gradients.
+    """Bucketed SUM all-reduce of parameter gradients, overlapped with backward.
 
-    Gradients are packed into flat buckets of at most `bucket_bytes` (fewer,
-    larger collectives suit xGMI's point-to-point links), reduced, and
-    unpacked.  Parameters larger than a bucket are reduced in place.
+    With overlap=True (default) a post-accumulate-grad hook on every parameter
+    appends its gradient to the open bucket in the order gradients become
+    ready.  That order is the same on every rank (same graph), so the
+    collectives match.  A bucket that reaches `bucket_bytes` is launched at
+    once as an async all-reduce.  On RCCL it runs on the communicator's own
+    stream, which waits only for the work already enqueued.  So the reduction
+    of the decoder/projection/LSTM gradients overlaps the encoder's backward
+    kernels.  `allreduce()` (called after loss.backward()) flushes the last
+    partial bucket, waits for all of them and unpacks.  A gradient larger
+    than a bucket is reduced in place; smaller ones are packed into one flat
+    buffer (fewer, larger collectives suit xGMI's point-to-point links).
+    overlap=False keeps the plain post-backward bucketed reduce.
     """
 
-    def __init__(self, params, comm: Comm, bucket_bytes: int = 64 << 20):
+    def __init__(self, params, comm: Comm, bucket_bytes: int = 32 << 20, overlap: bool = True):
         self.params = [p for p in params if p.requires_grad]
         self.comm = comm
         self.bucket_bytes = bucket_bytes
+        self.overlap = overlap and comm.world_size > 1
+        self._open, self._open_bytes = [], 0
+        self._inflight = []          # (work, params, flat or None)
+        self._seen = set()           # params queued since the last allreduce()
+        self._hooks = []
+        if self.overlap:
+            for p in self.params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._ready))
 
+    # -- overlapped path ------------------------------------------------------
+    def _ready(self, p):
+        if id(p) in self._seen:
+            raise RuntimeError("GradAllReducer: a gradient became ready twice before "
+                               "allreduce() (one backward per allreduce())")
+        self._seen.add(id(p))
+        nb = p.grad.numel() * p.grad.element_size()
+        if nb >= self.bucket_bytes:
+            self._launch([p])
+            return
+        self._open.append(p)
+        self._open_bytes += nb
+        if self._open_bytes >= self.bucket_bytes:
+            self._flush()
+
+    def _flush(self):
+        if self._open:
+            self._launch(self._open)
+        self._open, self._open_bytes = [], 0
+
+    @torch.no_grad()
+    def _launch(self, bucket):
+        if len(bucket) == 1:
+            flat = None
+            t = bucket[0].grad
+        else:
+            flat = torch.cat([p.grad.reshape(-1) for p in bucket])
+            t = flat
+        work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.comm.group, async_op=True)
+        self._inflight.append((work, bucket, flat))
+
+    @torch.no_grad()
+    def _finish(self):
+        self._flush()
+        for work, bucket, flat in self._inflight:
+            work.wait()
+            if flat is not None:
+                off = 0
+                for p in bucket:
+                    n = p.grad.numel()
+                    p.grad.copy_(flat[off:off + n].view_as(p.grad))
+                    off += n
+        self._inflight = []
+
+    def remove_hooks(self):
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        self.overlap = False
+
+    # -- post-backward path ---------------------------------------------------
     def _buckets(self):
         cur, size = [], 0
         for p in self.params:
@@ -67,19 +135,22 @@ class GradAllReducer:
 
     @torch.no_grad()
     def allreduce(self):
+        """Call after loss.backward(): completes the SUM all-reduce of every
+        parameter gradient (waits for the overlapped buckets)."""
         if self.comm.world_size == 1:
             return
+        if self.overlap:
+            # gradients that did not arrive through a hook (set by hand, or a
+            # parameter outside this backward's graph) are reduced here
+            for p in self.params:
+                if p.grad is not None and id(p) not in self._seen:
+                    self._ready(p)
+            self._finish()
+            self._seen.clear()
+            return
         for bucket in self._buckets():
-            if len(bucket) == 1:
-                self.comm.allreduce_sum_(bucket[0].grad)
-                continue
-            flat = torch.cat([p.grad.reshape(-1) for p in bucket])
-            self.comm.allreduce_sum_(flat)
-            off = 0
-            for p in bucket:
-                n = p.grad.numel()
-                p.grad.copy_(flat[off:off + n].view_as(p.grad))
-                off += n
+            self._launch(bucket)
+        self._finish()
 
 
 def init_from_env(backend: str | None = None):

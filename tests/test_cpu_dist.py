@@ -135,13 +135,25 @@ def _worker(rank, world, port, out_q):
     g, p, keys, H, L = _load_small()
     x, m, t = (torch.from_numpy(g[k]) for k in ("x", "mask", "target"))
     sl = slice(rank, rank + 1)
-    loss, grads = _grads(p, keys, x[sl], m[sl], t[sl], H, L, comm)
     params = [p[k] for k in keys]
-    GradAllReducer(params, comm).allreduce()
+    for q in params:
+        q.requires_grad_(True)
+    # overlapped: hooks queue each gradient as backward produces it, small
+    # buckets so several async all-reduces are in flight during backward
+    reducer = GradAllReducer(params, comm, bucket_bytes=1 << 14)
+    loss, grads = _grads(p, keys, x[sl], m[sl], t[sl], H, L, comm)
+    res["inflight_during_backward"] = len(reducer._inflight)
+    reducer.allreduce()
     lsum = loss.reshape(1).double()
     comm.allreduce_sum_(lsum)
     res["loss"] = float(lsum.item())
-    res["grads"] = {k: p[k].grad.numpy() for k in keys}
+    res["grads"] = {k: p[k].grad.clone().numpy() for k in keys}
+    # post-backward path gives the same sums
+    reducer.remove_hooks()
+    _grads(p, keys, x[sl], m[sl], t[sl], H, L, comm)
+    GradAllReducer(params, comm, overlap=False).allreduce()
+    res["same_without_overlap"] = all(np.array_equal(p[k].grad.numpy(), res["grads"][k])
+                                      for k in keys)
     out_q.put((rank, res))
     dist.destroy_process_group()
 
@@ -158,6 +170,8 @@ def test_dp_two_ranks_match_single_process():
         pr.join(timeout=60)
         assert pr.exitcode == 0
     assert results[0]["buckets_ok"] and results[1]["buckets_ok"]
+    assert results[0]["inflight_during_backward"] >= 2
+    assert results[0]["same_without_overlap"] and results[1]["same_without_overlap"]
     # single process, full batch, no comm
     g, p, keys, H, L = _load_small()
     x, m, t = (torch.from_numpy(g[k]) for k in ("x", "mask", "target"))
