@@ -263,6 +263,106 @@ int ainp_adam(float* const* params, const float* const* grads,
               double beta2, double eps, double weight_decay, int64_t step,
               void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* (a15-a20) GAN path: PConvUNet, spectral-norm Discriminator, VGG loss      */
+/* ------------------------------------------------------------------------ */
+/* Generic convolution, implicit GEMM on f32 MFMA (exact fp32).  Replaces:
+ *   PartialConv2d.conv + mask_ratio + bias (models/GAN/networks.py:77-96),
+ *   the Discriminator's spectral-norm Conv2d + LeakyReLU (networks.py:359-370,
+ *   402-405), the frozen VGG19 Conv2d+ReLU (models/GAN/loss.py:21,45-46),
+ *   and the torch.cat / nn.Upsample feeding each decoder block
+ *   (networks.py:282-298, 306-318): the input is read from two NCHW sources,
+ *   channels [0,C0) from x0 (H0 x W0; nearest-resampled to Hin x Win when
+ *   smaller, i.e. the x2 Upsample) and [C0,C0+C1) from x1 (H1 x W1 == Hin x Win),
+ *   each multiplied by its mask plane m0 / m1 ([N,H0,W0] / [N,H1,W1], NULL = 1).
+ * w [Cout][C0+C1][KH][KW]; y [N][Cout][Ho][Wo];
+ * y = act(conv * (*scale) * ratio[n][oy][ox] + bias[co]); scale / ratio / bias
+ * may be NULL.  act: 0 none, 1 ReLU, 2 LeakyReLU(slope), 3 tanh.
+ * stats (NULL or double[ainp_conv_gen_stat_parts(N,Ho,Wo)][2][Cout]): fixed-order
+ * per-tile (sum, sumsq) of the value before act, for ainp_bn_stats_reduce.
+ * Cout == 1 uses a direct kernel; crop_h / crop_w (> 0) then write only the
+ * top-left crop (networks.py:334), else pass 0. */
+int ainp_conv_gen_stat_parts(int64_t N, int64_t Ho, int64_t Wo);
+int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H0, int W0,
+                      const float* x1, const float* m1, int C1, int H1, int W1,
+                      const float* w, const float* bias, const float* ratio,
+                      const float* scale, float* y, double* stats, int64_t N,
+                      int Cout, int Hin, int Win, int KH, int KW, int stride,
+                      int pad, int act, float slope, int crop_h, int crop_w,
+                      void* stream);
+/* PartialConv2d mask update (networks.py:83-104, multi_channel=False):
+ * count = C0*window_sum(m0) + C1*window_sum(m1) over the conv's window (masks
+ * are planes of integer counts -- 0/1, or a channel sum -- repeated over their
+ * channels), ratio = winsize / (count + 1e-8) with winsize = C_in*KH*KW (pass
+ * <= 0 for (C0+C1)*KH*KW), newmask = clamp(count, 0, 1); both [N][Ho][Wo]
+ * (NULL skips). */
+int ainp_pconv_mask(const float* m0, int C0, int H0, int W0, const float* m1, int C1,
+                    int H1, int W1, int64_t N, int Hin, int Win, int KH, int KW,
+                    int stride, int pad, float winsize, float* ratio, float* newmask,
+                    void* stream);
+/* PConvUNet input padding (networks.py:255-261): x reflect, mask constant 1,
+ * bottom/right to Hp x Wp (pad < size, as F.pad(mode='reflect') requires). */
+int ainp_gan_pad_input(const float* x, const float* m, int64_t N, int H, int W,
+                       int Hp, int Wp, float* xp, float* mp, void* stream);
+/* y = act(y*scale[c] + shift[c]) in place: BatchNorm2d + LeakyReLU of the
+ * Encoder/DecoderBlocks (networks.py:149-151, 165-167). */
+int ainp_affine_act(float* y, const float* scale, const float* shift, int64_t N, int C,
+                    int64_t HW, int act, float slope, void* stream);
+/* nn.MaxPool2d(2, 2) of VGG19.features (loss.py:21). */
+int ainp_maxpool2(const float* x, float* y, int64_t NC, int H, int W, void* stream);
+/* VGGLoss._prepare_input_for_vgg + weights.transforms() (loss.py:65-86,104-106):
+ * generated: (x+1)/2; target: clamp(x,0)/(max+1e-6) with the batch max found on
+ * the device (max_ws: 1 uint scratch); clamp to [0,1]; antialiased bilinear
+ * resize evaluated only at the SxS centre-crop outputs with the separable
+ * tables (ry0, rn, rw[S][rtaps]) / (cx0, cn, cw[S][ctaps]) built by the host
+ * (torch's _upsample_bilinear2d_aa weights); ImageNet normalisation;
+ * out [N,3,S,S]. */
+int ainp_vgg_prep(const float* x, int64_t N, int H, int W, int generated,
+                  unsigned int* max_ws, const int* ry0, const int* rn, const float* rw,
+                  int rtaps, const int* cx0, const int* cn, const float* cw, int ctaps,
+                  int S, float* out, void* stream);
+/* Fixed-order reductions (workspace: ainp_reduce_workspace() bytes).
+ * absdiff_mean: *out = mean |a-b|  (nn.L1Loss(), loss.py:117,128).
+ * bce_logits: *out_mean = mean BCEWithLogits(x, target) (train.py:41-42,355-359),
+ *   grad (NULL to skip) = grad_scale * (sigmoid(x) - target).
+ * gan_recon_losses: out3 = {Lv, Lh, Lw} of calculate_losses (train.py:49-63). */
+size_t ainp_reduce_workspace(void);
+int ainp_absdiff_mean(const float* a, const float* b, int64_t n, void* workspace,
+                      double* out, void* stream);
+int ainp_bce_logits(const float* x, int64_t n, float target, float* grad, float grad_scale,
+                    void* workspace, double* out_mean, void* stream);
+int ainp_gan_recon_losses(const float* g, const float* o, const float* m, int64_t n,
+                          void* workspace, double* out3, void* stream);
+/* torch.nn.utils.spectral_norm for nl (<= 8) layers at once (networks.py:
+ * 360-361,403-404), W viewed [h][wd]: update != 0 (train-mode forward) runs one
+ * power iteration v = normalize(W^T u), u = normalize(W v) in place; always
+ * inv_sigma[l] = 1 / (u . W v).  workspace: ainp_sn_workspace(nl, maxdim)
+ * bytes, maxdim >= every h and wd. */
+size_t ainp_sn_workspace(int nl, int maxdim);
+int ainp_sn_power(const float* const* w, float* const* u, float* const* v, const int* h,
+                  const int* wd, int nl, float eps, void* workspace, int maxdim,
+                  float* inv_sigma, int update, void* stream);
+/* Gradient through W = W_orig / sigma with u, v held constant:
+ * out = G*inv_sigma - (sum G*W_orig) * inv_sigma^2 * u v^T.
+ * workspace: ainp_reduce_workspace() bytes. */
+int ainp_sn_weight_grad(const float* G, const float* w_orig, const float* u, const float* v,
+                        const float* inv_sigma, int h, int wd, void* workspace, float* out,
+                        void* stream);
+/* Discriminator backward glue: im2col col[N][C*KH*KW][Ho*Wo] (k = ci*KH*KW + tap),
+ * its adjoint col2im as a gather (deterministic), LeakyReLU backward from the
+ * activation output. */
+int ainp_im2col(const float* x, int64_t N, int C, int H, int W, int KH, int KW, int stride,
+                int pad, float* col, void* stream);
+int ainp_col2im(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW, int stride,
+                int pad, float* dx, void* stream);
+int ainp_leaky_bwd(const float* g, const float* y, int64_t n, float slope, float* out,
+                   void* stream);
+/* PartialConv2d called with a per-channel mask (networks.py:74-85 when
+ * mask.shape[1] == C_in): out = a*b elementwise, and the channel sum of the
+ * mask [N,C,HW] -> [N,HW] whose window sum is the mask_conv count. */
+int ainp_mul(const float* a, const float* b, int64_t n, float* out, void* stream);
+int ainp_channel_sum(const float* m, int64_t N, int C, int64_t HW, float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,615 @@
+"""GAN inpainting path on the MI355X kernels.
+
+Modules keep the reference's constructors, submodule trees, state_dict keys
+and default-init RNG draw order (models/GAN/networks.py, models/GAN/loss.py),
+so checkpoints move between the two unchanged; only the arithmetic moves onto
+libainp (ainp.ops):
+
+  PartialConv2d / EncoderBlock / DecoderBlock  networks.py:10-168
+  PConvUNet       networks.py:173-345  forward-only (the reference trains G
+                  under torch.no_grad).  Every PartialConv2d is ONE
+                  implicit-GEMM launch whose gather reads the upsampled decoder
+                  input and the skip directly (no torch.cat / nn.Upsample
+                  tensors) times their 0/1 mask planes, plus one mask-count
+                  launch; BatchNorm2d statistics come from the conv epilogue.
+  Discriminator   networks.py:352-409  spectral norm (one power iteration per
+                  train-mode forward, torch.nn.utils.spectral_norm semantics),
+                  forward = conv_gen with 1/sigma, bias and LeakyReLU fused;
+                  backward = im2col + MFMA GEMMs + the spectral-norm weight-grad
+                  correction.
+  VGGLoss         loss.py:6-131  VGG19.features[0..30] (frozen, forward only).
+  calculate_losses train.py:33-88.
+"""
+from __future__ import annotations
+
+import re
+from pathlib import Path
+from typing import Dict, List, Optional, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+from torch.nn.utils import spectral_norm
+
+from . import ops
+
+SLOPE = 0.2
+
+
+def _need_cuda(t, what):
+    if t.device.type != "cuda":
+        raise RuntimeError(f"ainp {what} runs on the MI355X kernels only; move it to a GPU")
+
+
+def _bn_affine(bn: nn.BatchNorm2d, stats, count, C):
+    """BatchNorm2d train (batch stats + running update) or eval -> (scale, shift)."""
+    if bn.training or not bn.track_running_stats:
+        sums = ops.bn_stats_reduce(stats, C)
+        rm = bn.running_mean if bn.track_running_stats else None
+        rv = bn.running_var if bn.track_running_stats else None
+        mom = bn.momentum if bn.momentum is not None else 0.1
+        sc, sh, _ = ops.bn_finalize(sums, count, bn.weight, bn.bias, rm, rv, mom, bn.eps)
+        if bn.track_running_stats:
+            bn.num_batches_tracked.add_(1)
+        return sc, sh
+    return ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+
+
+# ------------------------------------------------------------ partial conv
+class PartialConv2d(nn.Module):
+    """networks.py:10-106 (multi_channel=False)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride=1, padding=0, dilation=1,
+                 groups=1, bias=True, multi_channel=False):
+        super().__init__()
+        if dilation != 1 or groups != 1 or multi_channel:
+            raise NotImplementedError("the reference only uses dilation=1, groups=1, "
+                                      "multi_channel=False")
+        self.in_channels, self.out_channels = in_channels, out_channels
+        self.kernel_size, self.stride, self.padding = kernel_size, stride, padding
+        self.dilation, self.groups, self.multi_channel = dilation, groups, multi_channel
+        self.conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride, padding, dilation,
+                              groups, bias=False)
+        self.mask_kernel = torch.ones(1, in_channels, kernel_size, kernel_size)
+        self.mask_conv = nn.Conv2d(in_channels, 1, kernel_size, stride, padding, dilation,
+                                   groups=groups, bias=False)
+        self.mask_conv.weight.data.fill_(1.0)
+        for p in self.mask_conv.parameters():
+            p.requires_grad = False
+        self.bias = nn.Parameter(torch.zeros(out_channels)) if bias else None
+        self.window_size = float(in_channels * kernel_size * kernel_size)
+
+    # plane-level entry used by the U-Net: srcs = [(x, mask_plane [N,H,W]), ...]
+    def run(self, srcs, Hin, Win, act=ops.ACT_NONE, want_stats=False, crop=None):
+        k, s, p = self.kernel_size, self.stride, self.padding
+        (x0, m0) = srcs[0]
+        src1 = srcs[1] if len(srcs) > 1 else None
+        N = x0.shape[0]
+        ratio, newm = ops.pconv_mask((m0, x0.shape[1]),
+                                     (src1[1], src1[0].shape[1]) if src1 is not None else None,
+                                     N, Hin, Win, k, s, p)
+        y, stats = ops.conv_gen(srcs[0], self.conv.weight, src1=src1, Hin=Hin, Win=Win, stride=s,
+                                pad=p, bias=self.bias, ratio=ratio, act=act, slope=SLOPE,
+                                want_stats=want_stats, crop=crop)
+        return y, newm, stats
+
+    def run_full_mask(self, x, mask, want_stats=False):
+        """PartialConv2d with a per-channel mask [N, Cin, H, W]."""
+        N, C, H, W = x.shape
+        xm = ops.mul(x, mask)
+        msum = ops.channel_sum(mask)
+        k, s, p = self.kernel_size, self.stride, self.padding
+        # the window sum of the channel-summed plane is the full count; the
+        # ratio's numerator stays Cin*k*k
+        ratio, newm = ops.pconv_mask((msum, 1), None, N, H, W, k, s, p, winsize=self.window_size)
+        y, stats = ops.conv_gen((xm, None), self.conv.weight, stride=s, pad=p, bias=self.bias,
+                                ratio=ratio, want_stats=want_stats)
+        return y, newm, stats
+
+    def forward(self, x: torch.Tensor, mask: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """networks.py:63-106: (output, updated mask repeated to out_channels)."""
+        _need_cuda(x, "PartialConv2d")
+        x = x.contiguous().float()
+        mask = mask.contiguous().float()
+        N, C, H, W = x.shape
+        if mask.shape[1] == 1:
+            y, newm, _ = self.run([(x, mask.reshape(N, H, W))], H, W)
+        elif mask.shape[1] == C:
+            y, newm, _ = self.run_full_mask(x, mask)
+        else:
+            raise ValueError("mask must have 1 or in_channels channels")
+        Ho, Wo = y.shape[2:]
+        return y, newm.reshape(N, 1, Ho, Wo).expand(N, self.out_channels, Ho, Wo).contiguous()
+
+
+class EncoderBlock(nn.Module):
+    """networks.py:139-152: PartialConv -> BatchNorm2d -> LeakyReLU(0.2)."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, stride, padding,
+                 norm_layer=nn.BatchNorm2d, activation=None):
+        super().__init__()
+        self.pconv = PartialConv2d(in_channels, out_channels, kernel_size, stride, padding,
+                                   bias=False)
+        self.norm = norm_layer(out_channels) if norm_layer else nn.Identity()
+        self.activation = activation if activation is not None else nn.LeakyReLU(SLOPE, True)
+
+    def _finish(self, y, stats):
+        N, C, Ho, Wo = y.shape
+        if isinstance(self.norm, nn.BatchNorm2d):
+            sc, sh = _bn_affine(self.norm, stats, N * Ho * Wo, C)
+        else:
+            sc = torch.ones(C, device=y.device)
+            sh = torch.zeros(C, device=y.device)
+        ops.affine_act_(y, sc, sh, ops.ACT_LEAKY, SLOPE)
+        return y
+
+    def _want_stats(self):
+        return isinstance(self.norm, nn.BatchNorm2d) and (
+            self.norm.training or not self.norm.track_running_stats)
+
+    def run(self, srcs, Hin, Win):
+        y, newm, stats = self.pconv.run(srcs, Hin, Win, want_stats=self._want_stats())
+        return self._finish(y, stats), newm
+
+    def forward(self, x, mask):
+        _need_cuda(x, "EncoderBlock")
+        x = x.contiguous().float()
+        mask = mask.contiguous().float()
+        N, C, H, W = x.shape
+        if mask.shape[1] == 1:
+            y, newm = self.run([(x, mask.reshape(N, H, W))], H, W)
+        else:
+            y, newm, stats = self.pconv.run_full_mask(x, mask, want_stats=self._want_stats())
+            y = self._finish(y, stats)
+        Ho, Wo = y.shape[2:]
+        return y, newm.reshape(N, 1, Ho, Wo).expand(N, y.shape[1], Ho, Wo).contiguous()
+
+
+class DecoderBlock(EncoderBlock):
+    """networks.py:154-168."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1,
+                 norm_layer=nn.BatchNorm2d, activation=None):
+        super().__init__(in_channels, out_channels, kernel_size, stride, padding, norm_layer,
+                         activation)
+
+
+def get_pad_size(input_size: int, factor: int) -> int:
+    """networks.py:111-115."""
+    return 0 if input_size % factor == 0 else factor - (input_size % factor)
+
+
+def calculate_total_downsampling(layers) -> int:
+    """networks.py:117-134 (for EncoderBlock lists)."""
+    f = 1
+    for layer in layers:
+        conv = getattr(layer, "pconv", None) or getattr(layer, "conv", None)
+        if conv is not None:
+            s = conv.stride[0] if isinstance(conv.stride, tuple) else conv.stride
+            if s > 1:
+                f *= s
+    return f
+
+
+class PConvUNet(nn.Module):
+    """networks.py:173-345."""
+
+    def __init__(self, input_channels=1, mask_channels=1, output_channels=1,
+                 enc_layer_cfg=((64, 7, 2, 3), (128, 5, 2, 2), (256, 5, 2, 2), (512, 3, 2, 1),
+                                (512, 3, 2, 1), (512, 3, 2, 1), (512, 3, 2, 1)),
+                 dec_layer_cfg=((512, 3, 1, 1), (512, 3, 1, 1), (512, 3, 1, 1), (256, 3, 1, 1),
+                                (128, 3, 1, 1), (64, 3, 1, 1)),
+                 final_dec_cfg=None, norm_layer=nn.BatchNorm2d, activation=None,
+                 final_activation=None, upsample_mode="nearest"):
+        super().__init__()
+        if final_dec_cfg is None:
+            final_dec_cfg = {"interim_ch": 64, "out_ch": 1, "kernel": 3, "padding": 1}
+        if input_channels != 1 or mask_channels != 1:
+            raise NotImplementedError("the reference's skip logic assumes 1 input / mask channel")
+        if upsample_mode != "nearest":
+            raise NotImplementedError("upsample_mode must be 'nearest' (the reference default)")
+        self.input_channels, self.mask_channels = input_channels, mask_channels
+        self.upsample = nn.Upsample(scale_factor=2, mode=upsample_mode)
+        self.final_activation = final_activation if final_activation is not None else nn.Tanh()
+        act = activation if activation is not None else nn.LeakyReLU(SLOPE, inplace=True)
+        self.encoder_blocks = nn.ModuleList()
+        in_c = input_channels + mask_channels
+        self.enc_output_channels = []
+        for out_c, k, s, p in enc_layer_cfg:
+            self.encoder_blocks.append(EncoderBlock(in_c, out_c, k, s, p, norm_layer, act))
+            self.enc_output_channels.append(out_c)
+            in_c = out_c
+        self._total_downsampling = calculate_total_downsampling(self.encoder_blocks)
+        self.decoder_blocks = nn.ModuleList()
+        skip_rev = self.enc_output_channels[::-1]
+        up_c = skip_rev[0]
+        for i, (out_c, k, s, p) in enumerate(dec_layer_cfg):
+            self.decoder_blocks.append(DecoderBlock(up_c + skip_rev[i + 1], out_c, k, s, p,
+                                                    norm_layer, act))
+            up_c = out_c
+        fk, fp = final_dec_cfg["kernel"], final_dec_cfg["padding"]
+        self.final_decoder_layer = nn.Sequential(
+            PartialConv2d(up_c + input_channels, final_dec_cfg["interim_ch"], fk, 1, fp, bias=True),
+            act,
+            PartialConv2d(final_dec_cfg["interim_ch"], final_dec_cfg["out_ch"], fk, 1, fp, bias=True),
+        )
+        if final_dec_cfg["out_ch"] != 1:
+            raise NotImplementedError("out_ch must be 1 (the reference's configuration)")
+
+    @torch.no_grad()
+    def forward(self, x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        if x.shape[1] != self.input_channels:
+            raise ValueError(f"Input x channels ({x.shape[1]}) != expected ({self.input_channels})")
+        if mask.shape[1] != self.mask_channels:
+            raise ValueError(f"Input mask channels ({mask.shape[1]}) != expected ({self.mask_channels})")
+        if x.shape[2:] != mask.shape[2:]:
+            raise ValueError("x and mask spatial dims must match")
+        _need_cuda(x, "PConvUNet")
+        x = x.contiguous().float()
+        mask = mask.contiguous().float()
+        N, _, H, W = x.shape
+        f = self._total_downsampling
+        Hp, Wp = H + get_pad_size(H, f), W + get_pad_size(W, f)
+        xp, mp = ops.gan_pad_input(x, mask, Hp, Wp)          # [N, Hp, Wp] each
+        xp4, mp4 = xp.view(N, 1, Hp, Wp), mp.view(N, 1, Hp, Wp)
+        # encoder: the first input is cat(x_pad, mask_pad) * mask_pad
+        srcs = [(xp4, mp), (mp4, mp)]
+        Hc, Wc = Hp, Wp
+        feats, masks = [], []
+        for blk in self.encoder_blocks:
+            y, m = blk.run(srcs, Hc, Wc)
+            feats.append(y)
+            masks.append(m)
+            Hc, Wc = y.shape[2:]
+            srcs = [(y, m)]
+        d, dm = feats[-1], masks[-1]
+        for i, blk in enumerate(self.decoder_blocks):
+            j = len(feats) - 2 - i
+            Hs, Ws = feats[j].shape[2:]
+            if (2 * d.shape[2], 2 * d.shape[3]) != (Hs, Ws):
+                raise RuntimeError("decoder/skip size mismatch (cannot happen after padding to "
+                                   "the total downsampling factor)")
+            d, dm = blk.run([(d, dm), (feats[j], masks[j])], Hs, Ws)
+        if (2 * d.shape[2], 2 * d.shape[3]) != (Hp, Wp):
+            raise RuntimeError(f"Size mismatch before final layer. Dec: {d.shape[2:]}, "
+                               f"Skip: {(Hp, Wp)}")
+        pc1, pc2 = self.final_decoder_layer[0], self.final_decoder_layer[2]
+        y1, m1, _ = pc1.run([(d, dm), (xp4, mp)], Hp, Wp, act=ops.ACT_LEAKY)
+        # final PartialConv2d (Cout=1) + Tanh + crop to the input size in one launch
+        out, _, _ = pc2.run([(y1, m1)], Hp, Wp, act=ops.ACT_TANH, crop=(H, W))
+        return out.view(N, 1, H, W)
+
+
+# ------------------------------------------------------------ discriminator
+class DiscriminatorBlock(nn.Module):
+    """networks.py:352-373."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=4, stride=2, padding=1,
+                 use_spectral_norm=True, activation=None, use_norm=False):
+        super().__init__()
+        if use_norm or not use_spectral_norm:
+            raise NotImplementedError("the reference Discriminator uses spectral norm, no BN")
+        conv = nn.Conv2d(in_channels, out_channels, kernel_size, stride, padding, bias=True)
+        conv = spectral_norm(conv)
+        self.block = nn.Sequential(conv, nn.Identity(),
+                                   activation if activation is not None
+                                   else nn.LeakyReLU(SLOPE, inplace=True))
+
+    def forward(self, x):
+        raise RuntimeError("use Discriminator.forward (the blocks run fused)")
+
+
+class _DiscriminatorFn(torch.autograd.Function):
+    """The 5 spectral-norm convs (+LeakyReLU on the first 4) forward/backward.
+    params per layer: (weight_orig, bias); sn = (inv_sigma [L], u clones, v clones)."""
+
+    @staticmethod
+    def forward(ctx, x, cfg, inv, us, vs, *params):
+        h = x.contiguous()
+        ins, outs = [], []
+        for l, (k, s, p, act) in enumerate(cfg):
+            w, b = params[2 * l], params[2 * l + 1]
+            y, _ = ops.conv_gen((h, None), w, stride=s, pad=p, bias=b, scale=inv[l:l + 1],
+                                act=ops.ACT_LEAKY if act else ops.ACT_NONE, slope=SLOPE)
+            ins.append(h)
+            outs.append(y)
+            h = y
+        ctx.cfg = cfg
+        ctx.nl = len(cfg)
+        ctx.save_for_backward(inv, *ins, *outs, *us, *vs, *params)
+        return h
+
+    @staticmethod
+    def backward(ctx, g):
+        L = ctx.nl
+        st = ctx.saved_tensors
+        inv = st[0]
+        ins, outs = st[1:1 + L], st[1 + L:1 + 2 * L]
+        us, vs = st[1 + 2 * L:1 + 3 * L], st[1 + 3 * L:1 + 4 * L]
+        params = st[1 + 4 * L:]
+        grads = [None] * len(params)
+        g = g.contiguous()
+        gx = None
+        for l in range(L - 1, -1, -1):
+            k, s, p, act = ctx.cfg[l]
+            w = params[2 * l]
+            if act:
+                g = ops.leaky_bwd(g, outs[l], SLOPE)
+            N, Cout, Ho, Wo = g.shape
+            P = Ho * Wo
+            h = ins[l]
+            Cin, H, W = h.shape[1:]
+            K = Cin * k * k
+            grads[2 * l + 1] = ops.rowsum_batched(g.view(N, Cout, P))
+            col = ops.im2col(h, k, s, p)                       # [N, K, P]
+            S = _split_count(N)
+            per = N // S
+            slabs = torch.empty(S, Cout, K, device=g.device)
+            ops.gemm(Cout, K, P, [g[i * per] for i in range(S)], P, 1,
+                     [col[i * per] for i in range(S)], 1, P, [slabs[i] for i in range(S)], K, 1,
+                     strideA=Cout * P, strideB=K * P, nstrided=per, ksplit=2)
+            Gw = ops.sum_slabs(slabs, S).view(Cout, K) if S > 1 else slabs[0]
+            grads[2 * l] = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1]).view_as(w)
+            if l > 0 or ctx.needs_input_grad[0]:
+                wn = ops.scale_by_scalar(w, inv[l:l + 1])
+                dcol = torch.empty(N, K, P, device=g.device)
+                ops.gemm(K, P, Cout, [wn], 1, K, [g], P, 1, [dcol], P, 1, strideB=Cout * P,
+                         strideC=K * P, nstrided=N)
+                g = ops.col2im(dcol, N, Cin, H, W, k, s, p)
+                if l == 0:
+                    gx = g
+        return (gx, None, None, None, None, *grads)
+
+
+def _split_count(n):
+    for s in (8, 4, 2, 1):
+        if n % s == 0:
+            return s
+    return 1
+
+
+class Discriminator(nn.Module):
+    """networks.py:375-409."""
+
+    def __init__(self, input_channels=1,
+                 layer_cfg=((64, 2, False), (128, 2, False), (256, 2, False), (512, 1, False)),
+                 final_out_channels=1, kernel_size=4, padding=1, use_spectral_norm=True,
+                 activation=None):
+        super().__init__()
+        if not use_spectral_norm:
+            raise NotImplementedError("the reference Discriminator uses spectral norm")
+        act = activation if activation is not None else nn.LeakyReLU(SLOPE, inplace=True)
+        layers = []
+        in_c = input_channels
+        self._cfg = []
+        for out_c, stride, use_norm in layer_cfg:
+            layers.append(DiscriminatorBlock(in_c, out_c, kernel_size, stride, padding, True, act,
+                                             use_norm))
+            self._cfg.append((kernel_size, stride, padding, True))
+            in_c = out_c
+        final = spectral_norm(nn.Conv2d(in_c, final_out_channels, kernel_size, stride=1,
+                                        padding=padding, bias=True))
+        layers.append(final)
+        self._cfg.append((kernel_size, 1, padding, False))
+        self.model = nn.Sequential(*layers)
+        if final_out_channels != 1:
+            raise NotImplementedError("final_out_channels must be 1 (the reference's)")
+
+    def _convs(self):
+        return [m.block[0] for m in self.model[:-1]] + [self.model[-1]]
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        _need_cuda(x, "Discriminator")
+        convs = self._convs()
+        ws = [c.weight_orig for c in convs]
+        # torch spectral_norm: a power iteration per forward in train mode,
+        # u / v updated in place; the forward uses clones (constants for autograd)
+        training = convs[0].training
+        inv = ops.sn_power(ws, [c.weight_u for c in convs], [c.weight_v for c in convs],
+                           update=training)
+        us = [c.weight_u.clone() for c in convs]
+        vs = [c.weight_v.clone() for c in convs]
+        params = []
+        for c in convs:
+            params += [c.weight_orig, c.bias]
+        return _DiscriminatorFn.apply(x.contiguous().float(), self._cfg, inv, us, vs, *params)
+
+
+# ------------------------------------------------------------ losses
+class _BCEConstFn(torch.autograd.Function):
+    """nn.BCEWithLogitsLoss()(logits, full_like(logits, target)) (mean)."""
+
+    @staticmethod
+    def forward(ctx, logits, target):
+        loss, grad = ops.bce_logits(logits.contiguous(), target, want_grad=logits.requires_grad)
+        ctx.save_for_backward(grad if grad is not None else logits)
+        return loss.to(torch.float32)
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return ops.scale_by_scalar(grad, g), None
+
+
+def bce_with_logits_const(logits, target: float):
+    return _BCEConstFn.apply(logits, float(target))
+
+
+VGG19_CFG = [64, 64, "M", 128, 128, "M", 256, 256, 256, 256, "M", 512, 512, 512, 512, "M",
+             512, 512, 512, 512, "M"]
+
+
+def vgg19_features() -> nn.Sequential:
+    """Same module tree / state_dict keys as torchvision vgg19().features."""
+    layers, in_c = [], 3
+    for v in VGG19_CFG:
+        if v == "M":
+            layers.append(nn.MaxPool2d(2, 2))
+        else:
+            conv = nn.Conv2d(in_c, v, 3, padding=1)
+            nn.init.kaiming_normal_(conv.weight, mode="fan_out", nonlinearity="relu")
+            nn.init.constant_(conv.bias, 0)
+            layers += [conv, nn.ReLU(inplace=True)]
+            in_c = v
+    return nn.Sequential(*layers)
+
+
+class VGGLoss(nn.Module):
+    """loss.py:6-131.  The pretrained VGG19_Weights.DEFAULT cannot be fetched
+    offline: pass `weights` (a torchvision vgg19 features state_dict, or a path
+    to one saved with torch.save, loaded with weights_only=True) to use them;
+    otherwise the features keep torchvision's own random init."""
+
+    def __init__(self, device, layer_indices_style=(0, 5, 10, 19, 28),
+                 layer_indices_perceptual=(2, 7, 12, 21, 30), weights=None):
+        super().__init__()
+        vgg = vgg19_features()
+        if weights is not None:
+            sd = torch.load(weights, map_location="cpu", weights_only=True) \
+                if isinstance(weights, (str, Path)) else weights
+            vgg.load_state_dict(sd)
+        vgg = vgg.to(device).eval()
+        for p in vgg.parameters():
+            p.requires_grad = False
+        self.vgg_layers = vgg
+        self.layer_indices_style = set(layer_indices_style)
+        self.layer_indices_perceptual = set(layer_indices_perceptual)
+        idx = list(layer_indices_style) + list(layer_indices_perceptual)
+        self.max_layer_idx = max(idx) if idx else -1
+        self._tables = {}
+
+    def _prep_tables(self, H, W, device, S=224, short=256):
+        key = (H, W, str(device))
+        t = self._tables.get(key)
+        if t is None:
+            nh, nw = (short, int(short * W / H)) if H <= W else (int(short * H / W), short)
+            top, left = int(round((nh - S) / 2.0)), int(round((nw - S) / 2.0))
+            ry0, rn, rw = ops.aa_bilinear_weights(H, nh, top, S)
+            cx0, cn, cw = ops.aa_bilinear_weights(W, nw, left, S)
+            t = tuple(torch.from_numpy(a).to(device) for a in (ry0, rn, rw, cx0, cn, cw))
+            self._tables[key] = t
+        return t
+
+    def _prepare(self, x, generated):
+        if x.dim() == 3:
+            x = x.unsqueeze(1)
+        if x.shape[1] != 1:
+            raise ValueError(f"Input tensor must have 1 channel here, got {x.shape[1]}")
+        x = x.contiguous().float()
+        return ops.vgg_prep(x, generated, self._prep_tables(x.shape[2], x.shape[3], x.device))
+
+    def _extract_features(self, x) -> Dict[int, torch.Tensor]:
+        """loss.py:41-51 incl. the inplace-ReLU effect: a collected conv output
+        is the post-ReLU value unless the loop stops right after it."""
+        feats = {}
+        want = self.layer_indices_style | self.layer_indices_perceptual
+        layers = list(self.vgg_layers)
+        i = 0
+        while i < len(layers):
+            lay = layers[i]
+            if isinstance(lay, nn.Conv2d):
+                relu_next = (i < self.max_layer_idx and i + 1 < len(layers)
+                             and isinstance(layers[i + 1], nn.ReLU))
+                x, _ = ops.conv_gen((x, None), lay.weight, stride=1, pad=1, bias=lay.bias,
+                                    act=ops.ACT_RELU if relu_next else ops.ACT_NONE)
+                if i in want:
+                    feats[i] = x
+                if relu_next:
+                    i += 1          # the ReLU ran inside the conv epilogue
+                    if i in want:
+                        feats[i] = x
+            elif isinstance(lay, nn.MaxPool2d):
+                x = ops.maxpool2(x)
+                if i in want:
+                    feats[i] = x
+            if i >= self.max_layer_idx:
+                break
+            i += 1
+        return feats
+
+    def _gram(self, x):
+        b, c, h, w = x.shape
+        g = torch.empty(b, c, c, device=x.device)
+        hw = h * w
+        ops.gemm(c, c, hw, [x], hw, 1, [x], 1, hw, [g], c, 1, alpha=1.0 / (c * hw),
+                 strideA=c * hw, strideB=c * hw, strideC=c * c, nstrided=b)
+        return g
+
+    @torch.no_grad()
+    def forward(self, generated, target):
+        _need_cuda(generated, "VGGLoss")
+        fg = self._extract_features(self._prepare(generated, True))
+        ft = self._extract_features(self._prepare(target, False))
+        perc = torch.zeros((), device=generated.device, dtype=torch.float64)
+        style = torch.zeros((), device=generated.device, dtype=torch.float64)
+        n_p = n_s = 0
+        for i in self.layer_indices_perceptual:
+            if i in fg and i in ft:
+                perc = perc + ops.absdiff_mean(fg[i], ft[i])
+                n_p += 1
+        for i in self.layer_indices_style:
+            if i in fg and i in ft:
+                style = style + ops.absdiff_mean(self._gram(fg[i]), self._gram(ft[i]))
+                n_s += 1
+        if n_p:
+            perc = perc / n_p
+        if n_s:
+            style = style / n_s
+        return perc.to(torch.float32), style.to(torch.float32)
+
+
+def calculate_losses(cfg, generated_mag, original_mag, mask, d_fake_pred,
+                     vgg_loss_calculator: Optional[VGGLoss] = None):
+    """train.py:33-88 -> dict of 0-dim float32 tensors (g_adv differentiable
+    w.r.t. d_fake_pred)."""
+    lc = cfg["training"]
+    adv = bce_with_logits_const(d_fake_pred, 1.0)
+    mask = mask.view_as(generated_mag) if mask.dim() < generated_mag.dim() else mask
+    if generated_mag.shape[1] != 1:
+        generated_mag = generated_mag[:, :1]
+    if original_mag.shape[1] != 1:
+        original_mag = original_mag[:, :1]
+    rec = ops.gan_recon_losses(generated_mag.contiguous().float(),
+                               original_mag.contiguous().float(), mask.contiguous().float())
+    rec = rec.to(torch.float32)
+    l1v, l1h, lw = rec[0], rec[1], rec[2]
+    dev = generated_mag.device
+    perc = torch.zeros((), device=dev)
+    style = torch.zeros((), device=dev)
+    if vgg_loss_calculator is not None and (lc["lambda_vgg_perceptual"] > 0
+                                            or lc["lambda_vgg_style"] > 0):
+        perc, style = vgg_loss_calculator(generated_mag, original_mag)
+    total = (lc["lambda_adv"] * adv + lc["lambda_l1_valid"] * l1v + lc["lambda_l1_hole"] * l1h
+             + lc["lambda_mag_weighted"] * lw + lc["lambda_vgg_perceptual"] * perc
+             + lc["lambda_vgg_style"] * style)
+    return {"g_total": total, "g_adv": adv, "g_l1_valid": l1v, "g_l1_hole": l1h,
+            "g_mag_weighted": lw, "g_vgg_perceptual": perc, "g_vgg_style": style}
+
+
+def find_latest_checkpoint(checkpoint_dir: Path):
+    """train.py:90-129 (file-name logic only)."""
+    checkpoint_dir = Path(checkpoint_dir)
+    latest_epoch, latest_opt = -1, None
+    opt_files = list(checkpoint_dir.glob("*.pth"))
+    if not opt_files:
+        return None, None, None, -1
+    for f in opt_files:
+        m = re.search(r"optimizers_epoch_(\d+).pth", f.name)
+        if m and int(m.group(1)) > latest_epoch:
+            latest_epoch, latest_opt = int(m.group(1)), f
+    if latest_epoch == -1:
+        return None, None, None, -1
+    gen = checkpoint_dir / f"generator_epoch_{latest_epoch:04d}.pth"
+    disc = checkpoint_dir / f"discriminator_epoch_{latest_epoch:04d}.pth"
+    if gen.exists() and disc.exists() and latest_opt.exists():
+        return gen, disc, latest_opt, latest_epoch
+    cands = [f for f in opt_files if re.search(r"optimizers_epoch_(\d+).pth", f.name)]
+    cands.sort(key=lambda f: int(re.search(r"optimizers_epoch_(\d+).pth", f.name).group(1)),
+               reverse=True)
+    for f in cands:
+        e = int(re.search(r"optimizers_epoch_(\d+).pth", f.name).group(1))
+        g_ = checkpoint_dir / f"generator_epoch_{e:04d}.pth"
+        d_ = checkpoint_dir / f"discriminator_epoch_{e:04d}.pth"
+        if g_.exists() and d_.exists():
+            return g_, d_, f, e
+    return None, None, None, -1

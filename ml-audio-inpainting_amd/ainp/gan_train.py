@@ -1,0 +1,75 @@
+"""One GAN training iteration on the MI355X kernels (models/GAN/train.py:341-378).
+
+  D step   generated = G(impaired, mask) under no_grad (train-mode BatchNorm:
+           running statistics update), BCE(D(original), 1) and BCE(D(generated), 0)
+           averaged, backward through D, Adam(d_lr, (b1, b2)).
+  G step   D(generated) a third time (one more spectral-norm power iteration),
+           calculate_losses (adversarial, L1 valid / hole, magnitude-weighted,
+           VGG perceptual / style), g_optimizer.step().
+
+SURVEY Q1: `generated` carries no graph, so g_loss.backward() only fills D's
+.grad, which the next d_optimizer.zero_grad() discards, and g_optimizer.step()
+is a no-op (G never gets a gradient).  Parameters, buffers and every loss
+value are therefore the same with or without that backward; it is skipped
+unless faithful_g_backward=True (then D's .grad after the step also matches).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import gan as G
+from .optim import Adam
+
+
+class GanTrainer:
+    def __init__(self, cfg, generator, discriminator, vgg=None, faithful_g_backward=False,
+                 comm=None):
+        tc = cfg["training"]
+        self.cfg = cfg
+        self.G, self.D, self.vgg = generator, discriminator, vgg
+        betas = (tc.get("b1", 0.5), tc.get("b2", 0.999))
+        self.g_opt = Adam(generator.parameters(), lr=tc.get("g_lr", 2e-4), betas=betas)
+        self.d_opt = Adam(discriminator.parameters(), lr=tc.get("d_lr", 2e-4), betas=betas)
+        self.faithful = faithful_g_backward
+        self.comm = comm
+        self.reducer = None
+        if comm is not None and comm.world_size > 1:
+            from .dist import GradAllReducer
+            self.reducer = GradAllReducer(discriminator.parameters(), comm)
+
+    def step(self, original_mag, impaired_mag, mask):
+        self.G.train()
+        self.D.train()
+        # ---- discriminator step (train.py:348-363)
+        self.d_opt.zero_grad()
+        with torch.no_grad():
+            generated = self.G(impaired_mag, mask)
+        d_real = self.D(original_mag)
+        l_real = G.bce_with_logits_const(d_real, 1.0)
+        d_fake = self.D(generated)
+        l_fake = G.bce_with_logits_const(d_fake, 0.0)
+        d_loss = (l_real + l_fake) / 2
+        d_loss.backward()
+        if self.reducer is not None:
+            # the reference loss is a per-rank mean: DP averages D's gradients
+            self.reducer.allreduce()
+            for p in self.D.parameters():
+                if p.grad is not None:
+                    p.grad.div_(self.comm.world_size)
+        self.d_opt.step()
+        # ---- generator step (train.py:366-378)
+        self.g_opt.zero_grad()
+        if self.faithful:
+            d_fake_g = self.D(generated)
+            losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g, self.vgg)
+            losses["g_total"].backward()
+        else:
+            with torch.no_grad():
+                d_fake_g = self.D(generated)
+                losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g,
+                                            self.vgg)
+        self.g_opt.step()   # no-op: G has no gradients (Q1)
+        out = {k: v.detach() for k, v in losses.items()}
+        out.update(d_loss=d_loss.detach(), d_real=l_real.detach(), d_fake=l_fake.detach(),
+                   generated=generated)
+        return out

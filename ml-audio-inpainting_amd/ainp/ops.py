@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import functools
 import math
+from ctypes import c_int as ctypes_int
 
 import numpy as np
 import torch
@@ -422,3 +423,254 @@ def adam_step(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, eps,
          ptr_array([v.data_ptr() for v in exp_avg_sqs]),
          int64_array([p.numel() for p in params]), len(params), float(lr), float(beta1),
          float(beta2), float(eps), float(weight_decay), int(step), _stream(params[0]))
+
+
+# ===================================================================== GAN
+ACT_NONE, ACT_RELU, ACT_LEAKY, ACT_TANH = 0, 1, 2, 3
+
+
+def conv_out_size(n, k, stride, pad):
+    return (n + 2 * pad - k) // stride + 1
+
+
+def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=None, ratio=None,
+             scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None):
+    """ainp_conv_gen_fwd.  src0/src1 = (x [N,C,Hs,Ws], mask plane [N,Hs,Ws] or None);
+    the conv's input is cat(src0 nearest-resampled to (Hin, Win), src1) * masks.
+    Returns (y [N,Cout,Ho,Wo] (or [N,crop_h,crop_w] for Cout=1 with crop), stats)."""
+    x0, m0 = src0
+    _req(x0, "x0"); _req(w, "w")
+    N, C0, H0, W0 = x0.shape
+    x1 = m1 = None
+    C1 = H1 = W1 = 0
+    if src1 is not None:
+        x1, m1 = src1
+        _req(x1, "x1")
+        _, C1, H1, W1 = x1.shape
+    if Hin is None:
+        Hin, Win = (H1, W1) if src1 is not None else (H0, W0)
+    Cout, Cin, KH, KW = w.shape
+    if Cin != C0 + C1:
+        raise ValueError(f"conv_gen: weight expects {Cin} input channels, sources give {C0 + C1}")
+    for m, (h, ww) in ((m0, (H0, W0)), (m1, (H1, W1))):
+        if m is not None:
+            _req(m, "mask")
+            if m.numel() != N * h * ww:
+                raise ValueError("conv_gen: mask plane must be [N, Hs, Ws] of its source")
+    Ho, Wo = conv_out_size(Hin, KH, stride, pad), conv_out_size(Win, KW, stride, pad)
+    ch, cw = (0, 0) if crop is None else crop
+    if out is None:
+        if Cout == 1 and crop is not None:
+            out = torch.empty(N, ch, cw, device=x0.device, dtype=torch.float32)
+        else:
+            out = torch.empty(N, Cout, Ho, Wo, device=x0.device, dtype=torch.float32)
+    stats = None
+    if want_stats:
+        parts = _lib.lib.ainp_conv_gen_stat_parts(N, Ho, Wo)
+        stats = torch.empty(parts, 2, Cout, device=x0.device, dtype=torch.float64)
+    for t, nm in ((bias, "bias"), (ratio, "ratio"), (scale, "scale")):
+        if t is not None:
+            _req(t, nm)
+    call("ainp_conv_gen_fwd", x0.data_ptr(), _p(m0), C0, H0, W0, _p(x1), _p(m1), C1, H1, W1,
+         w.data_ptr(), _p(bias), _p(ratio), _p(scale), out.data_ptr(), _p(stats), N, Cout,
+         Hin, Win, KH, KW, stride, pad, act, float(slope), ch, cw, _stream(x0))
+    return out, stats
+
+
+def pconv_mask(src0, src1, N, Hin, Win, k, stride, pad, want_ratio=True, want_mask=True,
+               winsize=0.0):
+    """ainp_pconv_mask: src = (mask plane [N,Hs,Ws], channels).  Returns
+    (ratio [N,Ho,Wo], newmask [N,Ho,Wo])."""
+    m0, C0 = src0
+    _req(m0, "m0")
+    H0, W0 = m0.shape[-2:]
+    m1, C1 = src1 if src1 is not None else (None, 0)
+    H1, W1 = (m1.shape[-2:] if m1 is not None else (0, 0))
+    Ho, Wo = conv_out_size(Hin, k, stride, pad), conv_out_size(Win, k, stride, pad)
+    ratio = torch.empty(N, Ho, Wo, device=m0.device) if want_ratio else None
+    newm = torch.empty(N, Ho, Wo, device=m0.device) if want_mask else None
+    call("ainp_pconv_mask", m0.data_ptr(), C0, H0, W0, _p(m1), C1, H1, W1, N, Hin, Win, k, k,
+         stride, pad, float(winsize), _p(ratio), _p(newm), _stream(m0))
+    return ratio, newm
+
+
+def gan_pad_input(x, m, Hp, Wp):
+    _req(x, "x"); _req(m, "mask")
+    N, _, H, W = x.shape
+    xp = torch.empty(N, Hp, Wp, device=x.device)
+    mp = torch.empty(N, Hp, Wp, device=x.device)
+    call("ainp_gan_pad_input", x.data_ptr(), m.data_ptr(), N, H, W, Hp, Wp, xp.data_ptr(),
+         mp.data_ptr(), _stream(x))
+    return xp, mp
+
+
+def affine_act_(y, scale, shift, act, slope=0.2):
+    _req(y, "y")
+    N, C = y.shape[:2]
+    call("ainp_affine_act", y.data_ptr(), scale.data_ptr(), shift.data_ptr(), N, C,
+         y[0, 0].numel(), act, float(slope), _stream(y))
+    return y
+
+
+def maxpool2(x):
+    _req(x, "x")
+    N, C, H, W = x.shape
+    y = torch.empty(N, C, H // 2, W // 2, device=x.device)
+    call("ainp_maxpool2", x.data_ptr(), y.data_ptr(), N * C, H, W, _stream(x))
+    return y
+
+
+_RED_WS: dict = {}
+
+
+def _reduce_ws(device):
+    key = str(device)
+    ws = _RED_WS.get(key)
+    if ws is None:
+        ws = torch.empty(int(_lib.lib.ainp_reduce_workspace()) // 8, device=device,
+                         dtype=torch.float64)
+        _RED_WS[key] = ws
+    return ws
+
+
+def absdiff_mean(a, b):
+    """mean |a - b| as a float64 device scalar (nn.L1Loss())."""
+    _req(a, "a"); _req(b, "b")
+    assert a.numel() == b.numel()
+    out = torch.empty((), device=a.device, dtype=torch.float64)
+    call("ainp_absdiff_mean", a.data_ptr(), b.data_ptr(), a.numel(), _reduce_ws(a.device).data_ptr(),
+         out.data_ptr(), _stream(a))
+    return out
+
+
+def bce_logits(x, target, want_grad=False, grad_scale=None):
+    """mean BCEWithLogits(x, const target) (float64 scalar), optional
+    gradient grad_scale * (sigmoid(x) - target) (default scale 1/numel)."""
+    _req(x, "logits")
+    n = x.numel()
+    out = torch.empty((), device=x.device, dtype=torch.float64)
+    grad = torch.empty_like(x) if want_grad else None
+    gs = 1.0 / n if grad_scale is None else grad_scale
+    call("ainp_bce_logits", x.data_ptr(), n, float(target), _p(grad), float(gs),
+         _reduce_ws(x.device).data_ptr(), out.data_ptr(), _stream(x))
+    return out, grad
+
+
+def gan_recon_losses(g, o, m):
+    """(Lv, Lh, Lw) of calculate_losses as a float64 [3] device tensor."""
+    for t, nm in ((g, "generated"), (o, "original"), (m, "mask")):
+        _req(t, nm)
+    out = torch.empty(3, device=g.device, dtype=torch.float64)
+    call("ainp_gan_recon_losses", g.data_ptr(), o.data_ptr(), m.data_ptr(), g.numel(),
+         _reduce_ws(g.device).data_ptr(), out.data_ptr(), _stream(g))
+    return out
+
+
+def sn_power(weights, us, vs, update=True, eps=1e-12):
+    """Spectral norm for several layers: power iteration (in place on us/vs)
+    when update, then inv_sigma [nl] (device float32)."""
+    nl = len(weights)
+    hs = [w.shape[0] for w in weights]
+    wds = [w[0].numel() for w in weights]
+    maxdim = max(hs + wds)
+    dev = weights[0].device
+    ws = torch.empty(int(_lib.lib.ainp_sn_workspace(nl, maxdim)) // 4, device=dev)
+    inv = torch.empty(nl, device=dev)
+    hh = (ctypes_int * nl)(*hs)
+    wd = (ctypes_int * nl)(*wds)
+    call("ainp_sn_power", ptr_array([w.data_ptr() for w in weights]),
+         ptr_array([u.data_ptr() for u in us]), ptr_array([v.data_ptr() for v in vs]),
+         hh, wd, nl, float(eps), ws.data_ptr(), maxdim, inv.data_ptr(), int(bool(update)),
+         _stream(weights[0]))
+    return inv
+
+
+def sn_weight_grad(G, w_orig, u, v, inv_sigma):
+    _req(G, "G"); _req(w_orig, "w_orig")
+    out = torch.empty_like(w_orig)
+    call("ainp_sn_weight_grad", G.data_ptr(), w_orig.data_ptr(), u.data_ptr(), v.data_ptr(),
+         inv_sigma.data_ptr(), w_orig.shape[0], w_orig[0].numel(),
+         _reduce_ws(G.device).data_ptr(), out.data_ptr(), _stream(G))
+    return out
+
+
+def im2col(x, k, stride, pad):
+    _req(x, "x")
+    N, C, H, W = x.shape
+    Ho, Wo = conv_out_size(H, k, stride, pad), conv_out_size(W, k, stride, pad)
+    col = torch.empty(N, C * k * k, Ho * Wo, device=x.device)
+    call("ainp_im2col", x.data_ptr(), N, C, H, W, k, k, stride, pad, col.data_ptr(), _stream(x))
+    return col
+
+
+def col2im(dcol, N, C, H, W, k, stride, pad):
+    _req(dcol, "dcol")
+    dx = torch.empty(N, C, H, W, device=dcol.device)
+    call("ainp_col2im", dcol.data_ptr(), N, C, H, W, k, k, stride, pad, dx.data_ptr(),
+         _stream(dcol))
+    return dx
+
+
+def leaky_bwd(g, y, slope=0.2):
+    _req(g, "g"); _req(y, "y")
+    out = torch.empty_like(g)
+    call("ainp_leaky_bwd", g.data_ptr(), y.data_ptr(), g.numel(), float(slope), out.data_ptr(),
+         _stream(g))
+    return out
+
+
+def aa_bilinear_weights(in_size, out_size, start, count):
+    """Separable weights of torch's antialiased bilinear resize
+    (aten/src/ATen/native/cpu/UpSampleKernel.cpp, _compute_indices_min_size_weights_aa,
+    align_corners=False) for output indices [start, start+count): returns
+    (first input index [count] int32, taps [count] int32, weights [count][max_taps] f32)."""
+    scale = np.float32(in_size) / np.float32(out_size)
+    support = np.float32(scale) if scale >= 1.0 else np.float32(1.0)
+    invscale = np.float32(1.0) / scale if scale >= 1.0 else np.float32(1.0)
+    x0s, ns, ws = [], [], []
+    for i in range(start, start + count):
+        center = np.float32(scale * np.float32(i + 0.5))
+        xmin = max(int(center - support + np.float32(0.5)), 0)
+        xsize = min(int(center + support + np.float32(0.5)), in_size) - xmin
+        w = []
+        for j in range(xsize):
+            x = np.float32((j + xmin - center + np.float32(0.5)) * invscale)
+            w.append(np.float32(1.0) - abs(x) if abs(x) < 1.0 else np.float32(0.0))
+        w = np.array(w, dtype=np.float32)
+        tot = w.sum(dtype=np.float32)
+        if tot != 0:
+            w = w / tot
+        x0s.append(xmin); ns.append(xsize); ws.append(w)
+    taps = max(ns)
+    W = np.zeros((count, taps), np.float32)
+    for i, w in enumerate(ws):
+        W[i, :len(w)] = w
+    return np.array(x0s, np.int32), np.array(ns, np.int32), W
+
+
+def vgg_prep(x, generated, tables, S=224):
+    """ainp_vgg_prep: x [N,1,H,W] -> [N,3,S,S] normalised VGG input."""
+    _req(x, "x")
+    N, _, H, W = x.shape
+    ry0, rn, rw, cx0, cn, cw = tables
+    out = torch.empty(N, 3, S, S, device=x.device)
+    mx = torch.empty(1, device=x.device, dtype=torch.int32)
+    call("ainp_vgg_prep", x.data_ptr(), N, H, W, int(bool(generated)), mx.data_ptr(),
+         ry0.data_ptr(), rn.data_ptr(), rw.data_ptr(), rw.shape[1], cx0.data_ptr(),
+         cn.data_ptr(), cw.data_ptr(), cw.shape[1], S, out.data_ptr(), _stream(x))
+    return out
+
+
+def mul(a, b):
+    _req(a, "a"); _req(b, "b")
+    out = torch.empty_like(a)
+    call("ainp_mul", a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), _stream(a))
+    return out
+
+
+def channel_sum(m):
+    _req(m, "mask")
+    N, C, H, W = m.shape
+    out = torch.empty(N, H, W, device=m.device)
+    call("ainp_channel_sum", m.data_ptr(), N, C, H * W, out.data_ptr(), _stream(m))
+    return out

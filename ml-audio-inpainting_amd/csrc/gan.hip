@@ -1,0 +1,981 @@
+// gan.hip — kernels of the GAN training path:
+// PConvUNet (models/GAN/networks.py:10-345), the spectral-norm Discriminator
+// (networks.py:352-409), VGGLoss (models/GAN/loss.py) and calculate_losses /
+// the D step (models/GAN/train.py:33-88, 341-378).
+//
+// conv_gen_fwd is the workhorse: an implicit-GEMM convolution on
+// v_mfma_f32_16x16x4_f32 (exact fp32) for any kernel size / stride / zero
+// padding, whose im2col gather reads up to two NCHW sources (the decoder's
+// nearest-x2-upsampled input and the encoder skip: the torch.cat of
+// networks.py:297-298,317-318 is never materialised), multiplies each element
+// by its source's partial-conv mask plane, and whose epilogue applies the
+// spectral-norm 1/sigma, the partial-conv window ratio, the bias, BatchNorm
+// statistics partials and ReLU / LeakyReLU.
+//
+// GEMM view: C[co][p] = sum_k W'[co][k] * X[k][p], p = (n, oy, ox) flattened,
+// k = tap * Cin + ci (tap-major).  When Cin and the concat split are
+// multiples of 32 every 32-deep K tile has ONE tap, so the gather's bounds,
+// mask and address arithmetic are per tile, not per element ("fast" path).
+#include "common.h"
+
+namespace ainp {
+
+struct ConvSrcDev {
+  const float* x;   // [N, C, Hs, Ws]
+  const float* m;   // mask plane [N, Hs, Ws] (same for every channel) or null
+  int C, Hs, Ws;
+  int up;           // 0: Hs==Hin; 1: exact nearest x2 (i>>1); 2: nearest i*Hs/Hin
+};
+
+struct ConvGenParams {
+  ConvSrcDev s0, s1;        // channels [0, s0.C) then [s0.C, s0.C + s1.C)
+  const float* w;           // [Cout][Cin][KH][KW]
+  const float* bias;        // [Cout] or null
+  const float* ratio;       // [N][Ho][Wo] partial-conv window ratio or null
+  const float* scale;       // device scalar multiplier (1/sigma) or null
+  float* y;                 // [N][Cout][Ho][Wo]
+  double* stats;            // [px_tiles][2][Cout] (sum, sumsq of the stored y) or null
+  int N, Cin, Cout, Hin, Win, Ho, Wo, KH, KW, stride, pad;
+  float slope;              // LeakyReLU negative slope (act == 2)
+};
+
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_LEAKY = 2, ACT_TANH = 3 };
+
+__device__ __forceinline__ int src_coord(int i, int S, int L, int up) {
+  return up == 0 ? i : (up == 1 ? (i >> 1) : (int)(((int64_t)i * S) / L));
+}
+
+__device__ __forceinline__ float apply_act(float v, int act, float slope) {
+  if (act == ACT_RELU) return fmaxf(v, 0.f);
+  if (act == ACT_LEAKY) return v > 0.f ? v : v * slope;
+  if (act == ACT_TANH) return tanhf(v);
+  return v;
+}
+
+constexpr int CG_BM = 64, CG_BN = 64, CG_BK = 32;
+constexpr int CG_LDA = 34;   // sA[co][k]: == 2 mod 32, conflict-free fragment reads
+constexpr int CG_LDB = 80;   // sB[k][px]: == 16 mod 32
+
+template <bool FAST>
+__global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, int act) {
+  __shared__ __attribute__((aligned(16))) float sA[CG_BM * CG_LDA];
+  __shared__ __attribute__((aligned(16))) float sB[CG_BK * CG_LDB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int KK = p.KH * p.KW;
+  const int K = p.Cin * KK;
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px0 = (int64_t)blockIdx.x * CG_BN;
+  const int co0 = blockIdx.y * CG_BM;
+  const int nkt = (K + CG_BK - 1) / CG_BK;
+
+  // B staging: lane = pixel, rows k = wave + 4i
+  const int64_t pix = px0 + lane;
+  const bool pv = pix < NP;
+  int n = 0, by = 0, bx = 0;
+  if (pv) {
+    n = (int)(pix / HWo);
+    const int r = (int)(pix - (int64_t)n * HWo);
+    const int oy = r / p.Wo, ox = r - oy * p.Wo;
+    by = oy * p.stride - p.pad;
+    bx = ox * p.stride - p.pad;
+  }
+  // A staging: lane&31 = k within the tile, rows (tid>>5) + 8i
+  const int akk = tid & 31, arow = tid >> 5;
+
+  float ra[8], rb[8];
+  auto gather1 = [&](int k) -> float {   // one element of X[k][pix] (generic path)
+    if (!pv || k >= K) return 0.f;
+    const int tap = k / p.Cin, ci = k - tap * p.Cin;
+    const int ky = tap / p.KW, kx = tap - ky * p.KW;
+    const int iy = by + ky, ix = bx + kx;
+    if (iy < 0 || iy >= p.Hin || ix < 0 || ix >= p.Win) return 0.f;
+    const bool first = ci < p.s0.C;
+    const ConvSrcDev& s = first ? p.s0 : p.s1;
+    const int cs = first ? ci : ci - p.s0.C;
+    const int sy = src_coord(iy, s.Hs, p.Hin, s.up), sx = src_coord(ix, s.Ws, p.Win, s.up);
+    const int64_t plane = (int64_t)s.Hs * s.Ws;
+    const int64_t off = (int64_t)sy * s.Ws + sx;
+    float v = s.x[((int64_t)n * s.C + cs) * plane + off];
+    if (s.m) v *= s.m[(int64_t)n * plane + off];
+    return v;
+  };
+  auto fetch = [&](int kt) {
+    const int k0 = kt * CG_BK;
+    {
+      const int k = k0 + akk;
+      int aoff = 0;
+      const bool kok = k < K;
+      if (kok) {
+        const int tap = k / p.Cin, ci = k - tap * p.Cin;
+        aoff = ci * KK + tap;
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int co = co0 + arow + 8 * i;
+        ra[i] = (kok && co < p.Cout) ? p.w[(int64_t)co * K + aoff] : 0.f;
+      }
+    }
+    if (FAST) {
+      // the whole tile shares one tap and one source; ci = ci0 + wave + 4i
+      const int tap = k0 / p.Cin, ci0 = k0 - tap * p.Cin;
+      const int ky = tap / p.KW, kx = tap - ky * p.KW;
+      const int iy = by + ky, ix = bx + kx;
+      const bool inb = pv && k0 < K && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const bool first = ci0 < p.s0.C;
+      const ConvSrcDev& s = first ? p.s0 : p.s1;
+      const int cs = (first ? ci0 : ci0 - p.s0.C) + wave;
+      const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
+      const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
+      const int64_t plane = (int64_t)s.Hs * s.Ws;
+      const int64_t off = (int64_t)sy * s.Ws + sx;
+      const float mv = (inb && s.m) ? s.m[(int64_t)n * plane + off] : 1.f;
+      const float* base = s.x + ((int64_t)n * s.C + cs) * plane + off;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) rb[i] = inb ? base[(int64_t)(4 * i) * plane] * mv : 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        rb[i] = gather1(__builtin_amdgcn_readfirstlane(k0 + wave + 4 * i));
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sA[(arow + 8 * i) * CG_LDA + akk] = ra[i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sB[(wave + 4 * i) * CG_LDB + lane] = rb[i];
+  };
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int li = lane & 15, kq = lane >> 4;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  fetch(0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    commit();
+    __syncthreads();
+    if (kt + 1 < nkt) fetch(kt + 1);
+    const float* pa = sA + (wm * 32 + li) * CG_LDA + kq;
+    const float* pb = sB + kq * CG_LDB + wn * 32 + li;
+#pragma unroll
+    for (int s = 0; s < CG_BK / 4; ++s) {
+      const float a0 = pa[4 * s], a1 = pa[16 * CG_LDA + 4 * s];
+      const float b0 = pb[4 * s * CG_LDB], b1 = pb[4 * s * CG_LDB + 16];
+      acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
+      acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
+      acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
+      acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+    }
+    __syncthreads();
+  }
+
+  // ---------------- epilogue
+  const float sc = p.scale ? *p.scale : 1.f;
+  double ssum[2][4], ssq[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.0;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t pg = px0 + wn * 32 + 16 * j + li;
+    const bool ok = pg < NP;
+    int pn = 0, prem = 0;
+    if (ok) {
+      pn = (int)(pg / HWo);
+      prem = (int)(pg - (int64_t)pn * HWo);
+    }
+    const float rt = (ok && p.ratio) ? p.ratio[pg] : 1.f;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * 32 + 16 * i + kq * 4 + r;
+        if (!ok || co >= p.Cout) continue;
+        float v = acc[i][j][r] * sc;
+        v *= rt;
+        if (p.bias) v += p.bias[co];
+        if (p.stats) {
+          ssum[i][r] += (double)v;
+          ssq[i][r] += (double)v * (double)v;
+        }
+        p.y[((int64_t)pn * p.Cout + co) * HWo + prem] = apply_act(v, act, p.slope);
+      }
+    }
+  }
+  if (p.stats) {
+    // reduce over the 16 pixel lanes, then over the two wn waves (LDS)
+    double* red = reinterpret_cast<double*>(sA);   // [2 wn][64 co][2]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        double a = ssum[i][r], b = ssq[i][r];
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if (li == 0) {
+          const int cl = wm * 32 + 16 * i + kq * 4 + r;
+          red[(wn * 64 + cl) * 2 + 0] = a;
+          red[(wn * 64 + cl) * 2 + 1] = b;
+        }
+      }
+    __syncthreads();
+    if (tid < 64) {
+      const int co = co0 + tid;
+      if (co < p.Cout) {
+        const double a = red[(0 * 64 + tid) * 2] + red[(1 * 64 + tid) * 2];
+        const double b = red[(0 * 64 + tid) * 2 + 1] + red[(1 * 64 + tid) * 2 + 1];
+        p.stats[((int64_t)blockIdx.x * 2 + 0) * p.Cout + co] = a;
+        p.stats[((int64_t)blockIdx.x * 2 + 1) * p.Cout + co] = b;
+      }
+    }
+  }
+}
+
+// Direct convolution for Cout == 1 (the generator's last PartialConv2d and
+// the discriminator's logit conv): one thread per output pixel, weights in
+// LDS, optional crop of the output to [Hc, Wc] (networks.py:334).
+__global__ __launch_bounds__(256) void conv_cout1_kernel(ConvGenParams p, int act, int Hc, int Wc) {
+  extern __shared__ float sw[];
+  const int KK = p.KH * p.KW;
+  const int K = p.Cin * KK;
+  for (int i = threadIdx.x; i < K; i += blockDim.x) sw[i] = p.w[i];
+  __syncthreads();
+  const int64_t np = (int64_t)p.N * Hc * Wc;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= np) return;
+  const int n = (int)(t / ((int64_t)Hc * Wc));
+  const int r = (int)(t - (int64_t)n * Hc * Wc);
+  const int oy = r / Wc, ox = r - oy * Wc;
+  const int by = oy * p.stride - p.pad, bx = ox * p.stride - p.pad;
+  float acc = 0.f;
+  for (int src = 0; src < 2; ++src) {
+    const ConvSrcDev& s = src == 0 ? p.s0 : p.s1;
+    if (s.C == 0) continue;
+    const int cbase = src == 0 ? 0 : p.s0.C;
+    const int64_t plane = (int64_t)s.Hs * s.Ws;
+    for (int ky = 0; ky < p.KH; ++ky) {
+      const int iy = by + ky;
+      if (iy < 0 || iy >= p.Hin) continue;
+      const int sy = src_coord(iy, s.Hs, p.Hin, s.up);
+      for (int kx = 0; kx < p.KW; ++kx) {
+        const int ix = bx + kx;
+        if (ix < 0 || ix >= p.Win) continue;
+        const int sx = src_coord(ix, s.Ws, p.Win, s.up);
+        const int64_t off = (int64_t)sy * s.Ws + sx;
+        const float mv = s.m ? s.m[(int64_t)n * plane + off] : 1.f;
+        const float* xb = s.x + (int64_t)n * s.C * plane + off;
+        const float* wb = sw + cbase * KK + ky * p.KW + kx;
+        float a = 0.f;
+        for (int c = 0; c < s.C; ++c) a = fmaf(wb[c * KK], xb[(int64_t)c * plane] * mv, a);
+        acc += a;
+      }
+    }
+  }
+  float v = acc * (p.scale ? *p.scale : 1.f);
+  if (p.ratio) v *= p.ratio[((int64_t)n * p.Ho + oy) * p.Wo + ox];
+  if (p.bias) v += p.bias[0];
+  p.y[t] = apply_act(v, act, p.slope);
+}
+
+// Partial-conv mask update (networks.py:83-104): count = sum over the window
+// of the channel-repeated masks = C0 * win(m0) + C1 * win(m1) (exact integers
+// in fp32), ratio = (Cin*k*k) / (count + 1e-8), new mask = clamp(count, 0, 1).
+__global__ void pconv_mask_kernel(ConvSrcDev s0, ConvSrcDev s1, int N, int Hin, int Win,
+                                  int KH, int KW, int stride, int pad, int Ho, int Wo,
+                                  float winsize, float* ratio, float* newmask) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t np = (int64_t)N * Ho * Wo;
+  if (t >= np) return;
+  const int n = (int)(t / ((int64_t)Ho * Wo));
+  const int r = (int)(t - (int64_t)n * Ho * Wo);
+  const int oy = r / Wo, ox = r - oy * Wo;
+  int c0 = 0, c1 = 0;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int iy = oy * stride - pad + ky;
+    if (iy < 0 || iy >= Hin) continue;
+    for (int kx = 0; kx < KW; ++kx) {
+      const int ix = ox * stride - pad + kx;
+      if (ix < 0 || ix >= Win) continue;
+      if (s0.C) {
+        const int sy = src_coord(iy, s0.Hs, Hin, s0.up), sx = src_coord(ix, s0.Ws, Win, s0.up);
+        c0 += (int)s0.m[((int64_t)n * s0.Hs + sy) * s0.Ws + sx];
+      }
+      if (s1.C) {
+        const int sy = src_coord(iy, s1.Hs, Hin, s1.up), sx = src_coord(ix, s1.Ws, Win, s1.up);
+        c1 += (int)s1.m[((int64_t)n * s1.Hs + sy) * s1.Ws + sx];
+      }
+    }
+  }
+  const float cnt = (float)(s0.C * c0 + s1.C * c1);
+  if (ratio) ratio[t] = winsize / (cnt + 1e-8f);
+  if (newmask) newmask[t] = fminf(fmaxf(cnt, 0.f), 1.f);
+}
+
+// PConvUNet input padding (networks.py:255-261): features reflect-padded,
+// mask constant-1 padded, bottom / right only.
+__global__ void gan_pad_input_kernel(const float* x, const float* m, int N, int H, int W,
+                                     int Hp, int Wp, float* xp, float* mp) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * Hp * Wp) return;
+  const int n = (int)(t / ((int64_t)Hp * Wp));
+  const int r = (int)(t - (int64_t)n * Hp * Wp);
+  const int y = r / Wp, xx = r - y * Wp;
+  const int ry = y < H ? y : 2 * (H - 1) - y;
+  const int rx = xx < W ? xx : 2 * (W - 1) - xx;
+  xp[t] = x[((int64_t)n * H + ry) * W + rx];
+  mp[t] = (y < H && xx < W) ? m[((int64_t)n * H + y) * W + xx] : 1.f;
+}
+
+// y = act(y * scale[c] + shift[c]) in place (BatchNorm2d train/eval + activation).
+__global__ void affine_act_kernel(float* y, const float* scale, const float* shift, int C,
+                                  int64_t HW, int64_t total, int act, float slope) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int c = (int)((t / HW) % C);
+  y[t] = apply_act(fmaf(y[t], scale[c], shift[c]), act, slope);
+}
+
+__global__ void maxpool2_kernel(const float* x, float* y, int64_t NC, int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= NC * Ho * Wo) return;
+  const int64_t nc = t / ((int64_t)Ho * Wo);
+  const int r = (int)(t - nc * Ho * Wo);
+  const int oy = r / Wo, ox = r - oy * Wo;
+  const float* b = x + nc * H * W + (int64_t)(2 * oy) * W + 2 * ox;
+  y[t] = fmaxf(fmaxf(b[0], b[1]), fmaxf(b[W], b[W + 1]));
+}
+
+// ---------------------------------------------------------------- VGG input
+// max(clamp(x, 0)) over the whole batch (loss.py:77-78).  Values are >= 0,
+// so the float ordering equals the uint ordering of their bit patterns.
+__global__ void clamp_max_kernel(const float* x, int64_t n, unsigned int* out) {
+  float m = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, x[i]);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+// loss.py:74-86 scaling + ImageClassification: antialiased bilinear resize
+// (separable weights precomputed by the host for the cropped rows/cols),
+// centre crop, ImageNet normalisation; out [N, 3, 224, 224].
+__global__ void vgg_prep_kernel(const float* x, int N, int H, int W, int generated,
+                                const unsigned int* maxbits, const int* ry0, const int* rn,
+                                const float* rw, int rtaps, const int* cx0, const int* cn,
+                                const float* cw, int ctaps, int S, float* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * S * S) return;
+  const int n = (int)(t / ((int64_t)S * S));
+  const int r = (int)(t - (int64_t)n * S * S);
+  const int oy = r / S, ox = r - oy * S;
+  float div = 1.f;
+  bool use_div = false;
+  if (!generated) {
+    const double mx = (double)__uint_as_float(*maxbits) + 1e-6;
+    use_div = mx > 1e-5;
+    div = (float)mx;
+  }
+  const float* xb = x + (int64_t)n * H * W;
+  float acc = 0.f;
+  for (int a = 0; a < rn[oy]; ++a) {
+    const int yy = ry0[oy] + a;
+    float row = 0.f;
+    for (int b = 0; b < cn[ox]; ++b) {
+      float v = xb[(int64_t)yy * W + cx0[ox] + b];
+      if (generated) {
+        v = (v + 1.0f) / 2.0f;
+      } else {
+        v = fmaxf(v, 0.f);
+        if (use_div) v = v / div;
+      }
+      v = fminf(fmaxf(v, 0.f), 1.f);
+      row = fmaf(cw[ox * ctaps + b], v, row);
+    }
+    acc = fmaf(rw[oy * rtaps + a], row, acc);
+  }
+  const float mean[3] = {0.485f, 0.456f, 0.406f};
+  const float stdv[3] = {0.229f, 0.224f, 0.225f};
+  for (int c = 0; c < 3; ++c)
+    out[(((int64_t)n * 3 + c) * S + oy) * S + ox] = (acc - mean[c]) / stdv[c];
+}
+
+// ------------------------------------------------------------ reductions
+// out[0] += sum |a-b| (fixed-order block partials -> one atomic per block is
+// not deterministic; use two stages: partial[block] then a single block).
+__global__ void absdiff_partial_kernel(const float* a, const float* b, int64_t n,
+                                       double* partial) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += (double)fabsf(a[i] - b[i]);
+  __shared__ double red[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void sum_partials_kernel(const double* partial, int np, double scale, double* out) {
+  double s = 0.0;
+  for (int i = threadIdx.x; i < np; i += blockDim.x) s += partial[i];
+  __shared__ double red[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (red[0] + red[1] + red[2] + red[3]) * scale;
+}
+
+// BCEWithLogits (torch's stable form) against a constant target y, mean over
+// n, optional gradient g = gscale * (sigmoid(x) - y).
+__global__ void bce_logits_partial_kernel(const float* x, int64_t n, float y, double* partial,
+                                          float* grad, float gscale) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float v = x[i];
+    const float mx = fmaxf(-v, 0.f);
+    const float l = (1.f - y) * v + mx + logf(expf(-mx) + expf(-v - mx));
+    s += (double)l;
+    if (grad) grad[i] = gscale * (1.f / (1.f + expf(-v)) - y);
+  }
+  __shared__ double red[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+// calculate_losses' reconstruction terms (train.py:49-63) in one pass:
+// partial[block][0..4] = sum|g*m - o*m|, sum m, sum|g*h - o*h|, sum h,
+// sum |g - o| * |o|   (h = 1 - m)
+__global__ void gan_recon_partial_kernel(const float* g, const float* o, const float* m,
+                                         int64_t n, double* partial) {
+  double s[5] = {0, 0, 0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const float gv = g[i], ov = o[i], mv = m[i], hv = 1.f - mv;
+    s[0] += (double)fabsf(gv * mv - ov * mv);
+    s[1] += (double)mv;
+    s[2] += (double)fabsf(gv * hv - ov * hv);
+    s[3] += (double)hv;
+    s[4] += (double)(fabsf(gv - ov) * fabsf(ov));
+  }
+  __shared__ double red[5][4];
+  for (int q = 0; q < 5; ++q) {
+    const double v = wave_sum_d(s[q]);
+    if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < 5)
+    partial[(int64_t)blockIdx.x * 5 + threadIdx.x] =
+        red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+}
+
+__global__ void gan_recon_final_kernel(const double* partial, int np, int64_t n, double* out3) {
+  __shared__ double tot[5];
+  if (threadIdx.x < 5) {
+    double s = 0.0;
+    for (int b = 0; b < np; ++b) s += partial[(int64_t)b * 5 + threadIdx.x];
+    tot[threadIdx.x] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // torch: fp32 sums / (fp32 sum + 1e-8); the fp64 sums are rounded once
+    const float nv = (float)tot[1] + 1e-8f, nh = (float)tot[3] + 1e-8f;
+    out3[0] = (double)((float)tot[0] / nv);
+    out3[1] = (double)((float)tot[2] / nh);
+    out3[2] = (double)((float)(tot[4] / (double)n));
+  }
+}
+
+// -------------------------------------------------------------- spectral norm
+// torch.nn.utils.spectral_norm, n_power_iterations = 1 (per train forward):
+//   v = normalize(W^T u), t = W v, u = normalize(t), sigma = u . t
+struct SnLayers {
+  const float* w[8];
+  float* u[8];
+  float* v[8];
+  int h[8], wd[8];
+  int nl;
+};
+
+// tv[l][j] = sum_i W[i][j] u[i]    (grid: x = column blocks, y = layer)
+__global__ void sn_tmv_kernel(SnLayers L, float* tv, int ldt) {
+  const int l = blockIdx.y;
+  if (l >= L.nl) return;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= L.wd[l]) return;
+  const float* W = L.w[l];
+  const float* u = L.u[l];
+  float s = 0.f;
+  for (int i = 0; i < L.h[l]; ++i) s = fmaf(W[(int64_t)i * L.wd[l] + j], u[i], s);
+  tv[(int64_t)l * ldt + j] = s;
+}
+
+__device__ float block_sum_f(float v, float* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float s = 0.f;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) s += red[i];
+  __syncthreads();
+  return s;
+}
+
+// v[l] = tv[l] / max(||tv[l]||, eps)     (one block per layer)
+__global__ void sn_normalize_v_kernel(SnLayers L, const float* tv, int ldt, float eps) {
+  __shared__ float red[16];
+  const int l = blockIdx.x;
+  const int n = L.wd[l];
+  const float* t = tv + (int64_t)l * ldt;
+  float s = 0.f;
+  for (int j = threadIdx.x; j < n; j += blockDim.x) s += t[j] * t[j];
+  const float nrm = sqrtf(block_sum_f(s, red));
+  const float d = fmaxf(nrm, eps);
+  for (int j = threadIdx.x; j < n; j += blockDim.x) L.v[l][j] = t[j] / d;
+}
+
+// tu[l][i] = sum_j W[i][j] v[j]     (one block per (row, layer))
+__global__ void sn_mv_kernel(SnLayers L, float* tu, int ldt) {
+  __shared__ float red[16];
+  const int l = blockIdx.y, i = blockIdx.x;
+  if (l >= L.nl || i >= L.h[l]) return;
+  const float* W = L.w[l] + (int64_t)i * L.wd[l];
+  const float* v = L.v[l];
+  float s = 0.f;
+  for (int j = threadIdx.x; j < L.wd[l]; j += blockDim.x) s = fmaf(W[j], v[j], s);
+  s = block_sum_f(s, red);
+  if (threadIdx.x == 0) tu[(int64_t)l * ldt + i] = s;
+}
+
+// u = tu / max(||tu||, eps); sigma = u . tu; inv_sigma[l] = 1 / sigma
+__global__ void sn_finish_kernel(SnLayers L, const float* tu, int ldt, float eps,
+                                 float* inv_sigma) {
+  __shared__ float red[16];
+  const int l = blockIdx.x;
+  const int n = L.h[l];
+  const float* t = tu + (int64_t)l * ldt;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) s += t[i] * t[i];
+  const float nrm = sqrtf(block_sum_f(s, red));
+  const float d = fmaxf(nrm, eps);
+  float dotp = 0.f;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float uu = t[i] / d;
+    L.u[l][i] = uu;
+    dotp = fmaf(uu, t[i], dotp);
+  }
+  const float sigma = block_sum_f(dotp, red);
+  if (threadIdx.x == 0) inv_sigma[l] = 1.f / sigma;
+}
+
+// eval mode (no power iteration): sigma = u . (W v) with the stored u, v
+__global__ void sn_sigma_kernel(SnLayers L, const float* tu, int ldt, float* inv_sigma) {
+  __shared__ float red[16];
+  const int l = blockIdx.x;
+  const float* t = tu + (int64_t)l * ldt;
+  float dotp = 0.f;
+  for (int i = threadIdx.x; i < L.h[l]; i += blockDim.x) dotp = fmaf(L.u[l][i], t[i], dotp);
+  const float sigma = block_sum_f(dotp, red);
+  if (threadIdx.x == 0) inv_sigma[l] = 1.f / sigma;
+}
+
+// dW_orig = G * inv_sigma - (sum G*W_orig) * inv_sigma^2 * u v^T
+// stage 1: partial[block] = sum G*W  (fixed order), stage 2: apply.
+__global__ void sn_gdot_partial_kernel(const float* G, const float* W, int64_t n, double* partial) {
+  double s = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x)
+    s += (double)G[i] * (double)W[i];
+  __shared__ double red[4];
+  s = wave_sum_d(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ void sn_wgrad_apply_kernel(const float* G, const double* partial, int np,
+                                      const float* u, const float* v, const float* inv_sigma,
+                                      int h, int wd, float* out) {
+  __shared__ float gw;
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    for (int b = 0; b < np; ++b) s += partial[b];
+    gw = (float)s;
+  }
+  __syncthreads();
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)h * wd) return;
+  const int i = (int)(t / wd), j = (int)(t - (int64_t)i * wd);
+  const float is = *inv_sigma;
+  out[t] = G[t] * is - gw * is * is * u[i] * v[j];
+}
+
+// ------------------------------------------------------------ D backward glue
+// col[n][ci*KK + tap][oy*Wo + ox] = x[n][ci][oy*s-p+ky][ox*s-p+kx] (0 outside)
+__global__ void im2col_kernel(const float* x, int N, int C, int H, int W, int KH, int KW,
+                              int stride, int pad, int Ho, int Wo, float* col) {
+  const int KK = KH * KW;
+  const int64_t P = (int64_t)Ho * Wo;
+  const int64_t total = (int64_t)N * C * KK * P;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int64_t pp = t % P;
+  const int64_t rest = t / P;
+  const int k = (int)(rest % ((int64_t)C * KK));
+  const int n = (int)(rest / ((int64_t)C * KK));
+  const int ci = k / KK, tap = k - ci * KK;
+  const int ky = tap / KW, kx = tap - ky * KW;
+  const int oy = (int)(pp / Wo), ox = (int)(pp - (int64_t)oy * Wo);
+  const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+  col[t] = (iy >= 0 && iy < H && ix >= 0 && ix < W)
+               ? x[(((int64_t)n * C + ci) * H + iy) * W + ix] : 0.f;
+}
+
+// dx[n][ci][iy][ix] = sum over taps with (iy+p-ky)/s, (ix+p-kx)/s integral and
+// in range of dcol[n][ci*KK+tap][oy*Wo+ox]   (gather: deterministic, no atomics)
+__global__ void col2im_kernel(const float* dcol, int N, int C, int H, int W, int KH, int KW,
+                              int stride, int pad, int Ho, int Wo, float* dx) {
+  const int KK = KH * KW;
+  const int64_t P = (int64_t)Ho * Wo;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)N * C * H * W) return;
+  const int ix = (int)(t % W);
+  const int iy = (int)((t / W) % H);
+  const int64_t nc = t / ((int64_t)H * W);
+  const int ci = (int)(nc % C);
+  const int n = (int)(nc / C);
+  float s = 0.f;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int ty = iy + pad - ky;
+    if (ty < 0 || ty % stride) continue;
+    const int oy = ty / stride;
+    if (oy >= Ho) continue;
+    for (int kx = 0; kx < KW; ++kx) {
+      const int tx = ix + pad - kx;
+      if (tx < 0 || tx % stride) continue;
+      const int ox = tx / stride;
+      if (ox >= Wo) continue;
+      s += dcol[(((int64_t)n * C + ci) * KK + ky * KW + kx) * P + (int64_t)oy * Wo + ox];
+    }
+  }
+  dx[t] = s;
+}
+
+// g_pre = g * (y > 0 ? 1 : slope)    (LeakyReLU backward from its output)
+__global__ void leaky_bwd_kernel(const float* g, const float* y, int64_t n, float slope,
+                                 float* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= n) return;
+  out[t] = y[t] > 0.f ? g[t] : g[t] * slope;
+}
+
+// standalone PartialConv2d with a per-channel mask: x*m and sum_c m
+__global__ void mul_kernel(const float* a, const float* b, int64_t n, float* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < n) out[t] = a[t] * b[t];
+}
+__global__ void channel_sum_kernel(const float* m, int64_t N, int C, int64_t HW, float* out) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= N * HW) return;
+  const int64_t n = t / HW, p = t - n * HW;
+  float s = 0.f;
+  for (int c = 0; c < C; ++c) s += m[(n * C + c) * HW + p];
+  out[t] = s;
+}
+
+}  // namespace ainp
+
+// ============================================================== C ABI
+using namespace ainp;
+
+static ConvSrcDev make_src(const float* x, const float* m, int C, int Hs, int Ws, int Hin,
+                           int Win) {
+  ConvSrcDev s;
+  s.x = x;
+  s.m = m;
+  s.C = C;
+  s.Hs = Hs;
+  s.Ws = Ws;
+  if (Hs == Hin && Ws == Win) s.up = 0;
+  else if (2 * Hs == Hin && 2 * Ws == Win) s.up = 1;
+  else s.up = 2;
+  return s;
+}
+
+extern "C" int ainp_conv_gen_stat_parts(int64_t N, int64_t Ho, int64_t Wo) {
+  return (int)cdiv(N * Ho * Wo, CG_BN);
+}
+
+extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H0, int W0,
+                                 const float* x1, const float* m1, int C1, int H1, int W1,
+                                 const float* w, const float* bias, const float* ratio,
+                                 const float* scale, float* y, double* stats, int64_t N,
+                                 int Cout, int Hin, int Win, int KH, int KW, int stride,
+                                 int pad, int act, float slope, int crop_h, int crop_w,
+                                 void* stream) {
+  if (!x0 || C0 < 1 || C1 < 0 || (C1 > 0 && !x1) || !w || !y || N < 1 || Cout < 1 ||
+      Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 || act < 0 || act > 3)
+    return record_msg("ainp_conv_gen_fwd: bad argument");
+  const int Ho = (Hin + 2 * pad - KH) / stride + 1;
+  const int Wo = (Win + 2 * pad - KW) / stride + 1;
+  if (Ho < 1 || Wo < 1) return record_msg("ainp_conv_gen_fwd: empty output");
+  ConvGenParams p;
+  p.s0 = make_src(x0, m0, C0, H0, W0, Hin, Win);
+  p.s1 = make_src(x1, m1, C1, C1 ? H1 : Hin, C1 ? W1 : Win, Hin, Win);
+  if ((p.s0.up == 1 && (H0 * 2 != Hin)) || H0 < 1 || W0 < 1)
+    return record_msg("ainp_conv_gen_fwd: bad source size");
+  p.w = w;
+  p.bias = bias;
+  p.ratio = ratio;
+  p.scale = scale;
+  p.y = y;
+  p.stats = stats;
+  p.N = (int)N;
+  p.Cin = C0 + C1;
+  p.Cout = Cout;
+  p.Hin = Hin;
+  p.Win = Win;
+  p.Ho = Ho;
+  p.Wo = Wo;
+  p.KH = KH;
+  p.KW = KW;
+  p.stride = stride;
+  p.pad = pad;
+  p.slope = slope;
+  hipStream_t s = as_stream(stream);
+  if (Cout == 1) {
+    const int Hc = crop_h > 0 ? crop_h : Ho, Wc = crop_w > 0 ? crop_w : Wo;
+    if (stats || Hc > Ho || Wc > Wo) return record_msg("ainp_conv_gen_fwd: Cout=1 options");
+    const size_t lds = (size_t)p.Cin * KH * KW * sizeof(float);
+    if (lds > 64 * 1024) return record_msg("ainp_conv_gen_fwd: Cout=1 weight > 64 KB");
+    const int64_t np = N * (int64_t)Hc * Wc;
+    hipLaunchKernelGGL(conv_cout1_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), lds, s, p,
+                       act, Hc, Wc);
+    return check_launch("conv_cout1");
+  }
+  if (crop_h > 0 || crop_w > 0) return record_msg("ainp_conv_gen_fwd: crop needs Cout=1");
+  const int64_t tiles = cdiv(N * (int64_t)Ho * Wo, CG_BN);
+  dim3 grid((unsigned)tiles, (unsigned)cdiv(Cout, CG_BM));
+  const bool fast = (p.Cin % CG_BK == 0) && (C0 % CG_BK == 0);
+  if (fast)
+    hipLaunchKernelGGL(conv_gen_fwd_kernel<true>, grid, dim3(256), 0, s, p, act);
+  else
+    hipLaunchKernelGGL(conv_gen_fwd_kernel<false>, grid, dim3(256), 0, s, p, act);
+  return check_launch("conv_gen_fwd");
+}
+
+extern "C" int ainp_pconv_mask(const float* m0, int C0, int H0, int W0, const float* m1, int C1,
+                               int H1, int W1, int64_t N, int Hin, int Win, int KH, int KW,
+                               int stride, int pad, float winsize, float* ratio, float* newmask,
+                               void* stream) {
+  if (!m0 || C0 < 1 || (C1 > 0 && !m1) || N < 1 || KH < 1 || KW < 1 || stride < 1)
+    return record_msg("ainp_pconv_mask: bad argument");
+  const int Ho = (Hin + 2 * pad - KH) / stride + 1;
+  const int Wo = (Win + 2 * pad - KW) / stride + 1;
+  ConvSrcDev s0 = make_src(nullptr, m0, C0, H0, W0, Hin, Win);
+  ConvSrcDev s1 = make_src(nullptr, m1, C1, C1 ? H1 : Hin, C1 ? W1 : Win, Hin, Win);
+  if (winsize <= 0.f) winsize = (float)((C0 + C1) * KH * KW);
+  const int64_t np = N * (int64_t)Ho * Wo;
+  hipLaunchKernelGGL(pconv_mask_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0,
+                     as_stream(stream), s0, s1, (int)N, Hin, Win, KH, KW, stride, pad, Ho, Wo,
+                     winsize, ratio, newmask);
+  return check_launch("pconv_mask");
+}
+
+extern "C" int ainp_gan_pad_input(const float* x, const float* m, int64_t N, int H, int W,
+                                  int Hp, int Wp, float* xp, float* mp, void* stream) {
+  if (!x || !m || !xp || !mp || N < 1 || Hp < H || Wp < W || Hp - H >= H || Wp - W >= W)
+    return record_msg("ainp_gan_pad_input: bad argument (reflect pad must be < size)");
+  const int64_t n = N * (int64_t)Hp * Wp;
+  hipLaunchKernelGGL(gan_pad_input_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), x, m, (int)N, H, W, Hp, Wp, xp, mp);
+  return check_launch("gan_pad_input");
+}
+
+extern "C" int ainp_affine_act(float* y, const float* scale, const float* shift, int64_t N,
+                               int C, int64_t HW, int act, float slope, void* stream) {
+  if (!y || !scale || !shift || N < 1 || C < 1 || HW < 1 || act < 0 || act > 3)
+    return record_msg("ainp_affine_act: bad argument");
+  const int64_t total = N * C * HW;
+  hipLaunchKernelGGL(affine_act_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     as_stream(stream), y, scale, shift, C, HW, total, act, slope);
+  return check_launch("affine_act");
+}
+
+extern "C" int ainp_maxpool2(const float* x, float* y, int64_t NC, int H, int W, void* stream) {
+  if (!x || !y || NC < 1 || H < 2 || W < 2) return record_msg("ainp_maxpool2: bad argument");
+  const int64_t n = NC * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(maxpool2_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), x, y, NC, H, W);
+  return check_launch("maxpool2");
+}
+
+extern "C" int ainp_vgg_prep(const float* x, int64_t N, int H, int W, int generated,
+                             unsigned int* max_ws, const int* ry0, const int* rn,
+                             const float* rw, int rtaps, const int* cx0, const int* cn,
+                             const float* cw, int ctaps, int S, float* out, void* stream) {
+  if (!x || N < 1 || !ry0 || !rn || !rw || !cx0 || !cn || !cw || !out || S < 1 ||
+      (!generated && !max_ws))
+    return record_msg("ainp_vgg_prep: bad argument");
+  hipStream_t s = as_stream(stream);
+  if (!generated) {
+    hipError_t me = hipMemsetAsync(max_ws, 0, sizeof(unsigned int), s);
+    if (me != hipSuccess) return record_error(me, "vgg_prep memset");
+    hipLaunchKernelGGL(clamp_max_kernel, dim3(256), dim3(256), 0, s, x, N * (int64_t)H * W,
+                       max_ws);
+  }
+  const int64_t n = N * (int64_t)S * S;
+  hipLaunchKernelGGL(vgg_prep_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, x, (int)N,
+                     H, W, generated, max_ws, ry0, rn, rw, rtaps, cx0, cn, cw, ctaps, S, out);
+  return check_launch("vgg_prep");
+}
+
+static const int kRedBlocks = 512;
+
+extern "C" size_t ainp_reduce_workspace(void) { return (size_t)kRedBlocks * 5 * sizeof(double); }
+
+extern "C" int ainp_absdiff_mean(const float* a, const float* b, int64_t n, void* workspace,
+                                 double* out, void* stream) {
+  if (!a || !b || n < 1 || !workspace || !out) return record_msg("ainp_absdiff_mean: bad argument");
+  hipStream_t s = as_stream(stream);
+  double* part = reinterpret_cast<double*>(workspace);
+  hipLaunchKernelGGL(absdiff_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, a, b, n, part);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, part, kRedBlocks,
+                     1.0 / (double)n, out);
+  return check_launch("absdiff_mean");
+}
+
+extern "C" int ainp_bce_logits(const float* x, int64_t n, float target, float* grad,
+                               float grad_scale, void* workspace, double* out_mean,
+                               void* stream) {
+  if (!x || n < 1 || !workspace || !out_mean) return record_msg("ainp_bce_logits: bad argument");
+  hipStream_t s = as_stream(stream);
+  double* part = reinterpret_cast<double*>(workspace);
+  hipLaunchKernelGGL(bce_logits_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, x, n, target,
+                     part, grad, grad_scale);
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(256), 0, s, part, kRedBlocks,
+                     1.0 / (double)n, out_mean);
+  return check_launch("bce_logits");
+}
+
+extern "C" int ainp_gan_recon_losses(const float* g, const float* o, const float* m, int64_t n,
+                                     void* workspace, double* out3, void* stream) {
+  if (!g || !o || !m || n < 1 || !workspace || !out3)
+    return record_msg("ainp_gan_recon_losses: bad argument");
+  hipStream_t s = as_stream(stream);
+  double* part = reinterpret_cast<double*>(workspace);
+  hipLaunchKernelGGL(gan_recon_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, g, o, m, n, part);
+  hipLaunchKernelGGL(gan_recon_final_kernel, dim3(1), dim3(64), 0, s, part, kRedBlocks, n, out3);
+  return check_launch("gan_recon_losses");
+}
+
+extern "C" size_t ainp_sn_workspace(int nl, int maxdim) {
+  return (size_t)2 * nl * maxdim * sizeof(float);
+}
+
+extern "C" int ainp_sn_power(const float* const* w, float* const* u, float* const* v,
+                             const int* h, const int* wd, int nl, float eps, void* workspace,
+                             int maxdim, float* inv_sigma, int update, void* stream) {
+  if (nl < 1 || nl > 8 || !w || !u || !v || !h || !wd || !workspace || !inv_sigma)
+    return record_msg("ainp_sn_power: bad argument");
+  SnLayers L;
+  int maxh = 0, maxw = 0;
+  for (int l = 0; l < nl; ++l) {
+    if (!w[l] || !u[l] || !v[l] || h[l] < 1 || wd[l] < 1 || h[l] > maxdim || wd[l] > maxdim)
+      return record_msg("ainp_sn_power: bad layer");
+    L.w[l] = w[l];
+    L.u[l] = u[l];
+    L.v[l] = v[l];
+    L.h[l] = h[l];
+    L.wd[l] = wd[l];
+    maxh = h[l] > maxh ? h[l] : maxh;
+    maxw = wd[l] > maxw ? wd[l] : maxw;
+  }
+  L.nl = nl;
+  float* tv = reinterpret_cast<float*>(workspace);
+  float* tu = tv + (size_t)nl * maxdim;
+  hipStream_t s = as_stream(stream);
+  if (update) {
+    hipLaunchKernelGGL(sn_tmv_kernel, dim3((unsigned)cdiv(maxw, 256), nl), dim3(256), 0, s, L,
+                       tv, maxdim);
+    hipLaunchKernelGGL(sn_normalize_v_kernel, dim3(nl), dim3(1024), 0, s, L, tv, maxdim, eps);
+  }
+  hipLaunchKernelGGL(sn_mv_kernel, dim3(maxh, nl), dim3(256), 0, s, L, tu, maxdim);
+  if (update)
+    hipLaunchKernelGGL(sn_finish_kernel, dim3(nl), dim3(1024), 0, s, L, tu, maxdim, eps,
+                       inv_sigma);
+  else
+    hipLaunchKernelGGL(sn_sigma_kernel, dim3(nl), dim3(1024), 0, s, L, tu, maxdim, inv_sigma);
+  return check_launch("sn_power");
+}
+
+extern "C" int ainp_sn_weight_grad(const float* G, const float* w_orig, const float* u,
+                                   const float* v, const float* inv_sigma, int h, int wd,
+                                   void* workspace, float* out, void* stream) {
+  if (!G || !w_orig || !u || !v || !inv_sigma || h < 1 || wd < 1 || !workspace || !out)
+    return record_msg("ainp_sn_weight_grad: bad argument");
+  hipStream_t s = as_stream(stream);
+  double* part = reinterpret_cast<double*>(workspace);
+  const int64_t n = (int64_t)h * wd;
+  hipLaunchKernelGGL(sn_gdot_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, G, w_orig, n, part);
+  hipLaunchKernelGGL(sn_wgrad_apply_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, G, part,
+                     kRedBlocks, u, v, inv_sigma, h, wd, out);
+  return check_launch("sn_weight_grad");
+}
+
+extern "C" int ainp_im2col(const float* x, int64_t N, int C, int H, int W, int KH, int KW,
+                           int stride, int pad, float* col, void* stream) {
+  if (!x || !col || N < 1 || C < 1 || KH < 1 || KW < 1 || stride < 1)
+    return record_msg("ainp_im2col: bad argument");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  const int64_t total = N * C * KH * KW * (int64_t)Ho * Wo;
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     as_stream(stream), x, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo, col);
+  return check_launch("im2col");
+}
+
+extern "C" int ainp_col2im(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW,
+                           int stride, int pad, float* dx, void* stream) {
+  if (!dcol || !dx || N < 1 || C < 1 || KH < 1 || KW < 1 || stride < 1)
+    return record_msg("ainp_col2im: bad argument");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  const int64_t total = N * C * (int64_t)H * W;
+  hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     as_stream(stream), dcol, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo, dx);
+  return check_launch("col2im");
+}
+
+extern "C" int ainp_leaky_bwd(const float* g, const float* y, int64_t n, float slope, float* out,
+                              void* stream) {
+  if (!g || !y || !out || n < 1) return record_msg("ainp_leaky_bwd: bad argument");
+  hipLaunchKernelGGL(leaky_bwd_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0,
+                     as_stream(stream), g, y, n, slope, out);
+  return check_launch("leaky_bwd");
+}
+
+extern "C" int ainp_mul(const float* a, const float* b, int64_t n, float* out, void* stream) {
+  if (!a || !b || !out || n < 1) return record_msg("ainp_mul: bad argument");
+  hipLaunchKernelGGL(mul_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, as_stream(stream),
+                     a, b, n, out);
+  return check_launch("mul");
+}
+
+extern "C" int ainp_channel_sum(const float* m, int64_t N, int C, int64_t HW, float* out,
+                                void* stream) {
+  if (!m || !out || N < 1 || C < 1 || HW < 1) return record_msg("ainp_channel_sum: bad argument");
+  hipLaunchKernelGGL(channel_sum_kernel, dim3((unsigned)cdiv(N * HW, 256)), dim3(256), 0,
+                     as_stream(stream), m, N, C, HW, out);
+  return check_launch("channel_sum");
+}

@@ -118,3 +118,22 @@ def test_vgg_feature_relu_semantics():
     for i in (0, 2, 5, 7, 10, 12, 19, 21, 28):
         assert float(f[i].min()) >= 0.0, i
     assert float(f[30].min()) < 0.0
+
+
+def test_product_modules_match_reference_init(golden_dir):
+    """ainp.gan modules: same state_dict keys and init RNG draws as networks.py."""
+    from ainp import gan as G
+    g = np.load(os.path.join(golden_dir, "gan_full.npz"), allow_pickle=False)
+    torch.manual_seed(0)
+    sd = G.PConvUNet().state_dict()
+    assert sorted(sd) == sorted(k[6:] for k in g.files if k.startswith("check/"))
+    for k, v in sd.items():
+        assert abs(float(v.double().sum()) - g["check/" + k][0]) <= 1e-6 * max(1, abs(g["check/" + k][0])), k
+    torch.manual_seed(1)
+    sd = G.Discriminator().state_dict()
+    assert sorted(sd) == sorted(k[7:] for k in g.files if k.startswith("dcheck/"))
+    for k, v in sd.items():
+        assert abs(float(v.double().sum()) - g["dcheck/" + k][0]) <= 1e-6 * max(1, abs(g["dcheck/" + k][0])), k
+    # VGG19 features: torchvision's key layout
+    v = G.VGGLoss("cpu")
+    assert "vgg_layers.28.weight" in v.state_dict() and "vgg_layers.34.bias" in v.state_dict()

@@ -1,0 +1,302 @@
+"""GPU parity of the GAN path against the oracle
+(oracle/gan_ref.py, pinned in test_cpu_oracle_gan.py) and the fixtures made by
+the reference's networks.py.  Tolerance: 1e-4 relative L2 (fp32, north_star);
+masks bit-exact."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import gan_ref as R
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4
+
+
+def rel(a, b):
+    a = np.asarray(a.detach().cpu() if torch.is_tensor(a) else a, np.float64)
+    b = np.asarray(b.detach().cpu() if torch.is_tensor(b) else b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+@pytest.fixture(scope="module")
+def small(golden_dir):
+    return np.load(os.path.join(golden_dir, "gan_small.npz"), allow_pickle=False)
+
+
+def _sd(g, prefix):
+    return {k[len(prefix):]: torch.from_numpy(np.array(g[k])).clone()
+            for k in g.files if k.startswith(prefix)}
+
+
+# ------------------------------------------------------------- conv_gen
+CONV_CASES = [
+    # N, C0, C1, Hin, Win, up0, Cout, k, s, p, masks, bias, ratio, scale, act
+    (2, 64, 0, 17, 23, False, 96, 3, 1, 1, True, False, True, False, 0),      # fast, 1 source
+    (2, 32, 32, 16, 20, True, 48, 3, 1, 1, True, False, True, False, 0),      # fast, up + skip
+    (2, 2, 0, 33, 40, False, 64, 7, 2, 3, True, False, True, False, 0),       # generic k7 s2
+    (2, 64, 1, 24, 30, True, 64, 3, 1, 1, True, True, True, False, 2),        # generic concat
+    (2, 1, 0, 30, 50, False, 16, 4, 2, 1, False, True, False, True, 2),       # D layer 1
+    (1, 128, 0, 13, 21, False, 70, 5, 2, 2, True, False, True, False, 0),     # k5 s2, Cout%64
+    (2, 64, 0, 12, 14, False, 32, 3, 1, 1, False, True, False, False, 1),     # VGG-like
+]
+
+
+def _conv_ref(x0, m0, x1, m1, Hin, Win, w, k, s, p, bias, ratio, scale, act):
+    a = x0
+    if a.shape[2] != Hin:
+        a = F.interpolate(a, size=(Hin, Win), mode="nearest")
+        mm = F.interpolate(m0.unsqueeze(1), size=(Hin, Win), mode="nearest") if m0 is not None else None
+    else:
+        mm = m0.unsqueeze(1) if m0 is not None else None
+    if mm is not None:
+        a = a * mm
+    if x1 is not None:
+        b = x1 * (m1.unsqueeze(1) if m1 is not None else 1.0)
+        a = torch.cat([a, b], 1)
+    y = F.conv2d(a.double(), w.double(), None, s, p)
+    if scale is not None:
+        y = y * scale.double()
+    if ratio is not None:
+        y = y * ratio.double().unsqueeze(1)
+    if bias is not None:
+        y = y + bias.double().view(1, -1, 1, 1)
+    pre = y
+    if act == 1:
+        y = F.relu(y)
+    elif act == 2:
+        y = F.leaky_relu(y, 0.2)
+    elif act == 3:
+        y = torch.tanh(y)
+    return y, pre
+
+
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_gen_matches_torch(case):
+    from ainp import ops
+    N, C0, C1, Hin, Win, up0, Cout, k, s, p, masks, hb, hr, hs, act = case
+    g = torch.Generator().manual_seed(hash(case) % 1000)
+    H0, W0 = (Hin // 2, Win // 2) if up0 else (Hin, Win)
+    x0 = torch.randn(N, C0, H0, W0, generator=g)
+    m0 = (torch.rand(N, H0, W0, generator=g) > 0.3).float() if masks else None
+    x1 = torch.randn(N, C1, Hin, Win, generator=g) if C1 else None
+    m1 = (torch.rand(N, Hin, Win, generator=g) > 0.3).float() if (masks and C1) else None
+    w = torch.randn(Cout, C0 + C1, k, k, generator=g) * 0.1
+    Ho, Wo = (Hin + 2 * p - k) // s + 1, (Win + 2 * p - k) // s + 1
+    bias = torch.randn(Cout, generator=g) if hb else None
+    ratio = torch.rand(N, Ho, Wo, generator=g) * 3 if hr else None
+    scale = torch.tensor([0.7]) if hs else None
+    d = lambda t: None if t is None else t.cuda()
+    y, stats = ops.conv_gen((d(x0), d(m0)), d(w), src1=(d(x1), d(m1)) if C1 else None, Hin=Hin,
+                            Win=Win, stride=s, pad=p, bias=d(bias), ratio=d(ratio),
+                            scale=d(scale), act=act, want_stats=True)
+    yr, pre = _conv_ref(x0, m0, x1, m1, Hin, Win, w, k, s, p, bias, ratio, scale, act)
+    assert y.shape == yr.shape
+    assert rel(y, yr) < 1e-5
+    st = stats.double().sum(0).cpu()
+    assert rel(st[0], pre.sum((0, 2, 3))) < 1e-5
+    assert rel(st[1], (pre * pre).sum((0, 2, 3))) < 1e-5
+
+
+@pytest.mark.parametrize("k,s,p,crop,act", [(3, 1, 1, (25, 30), 3), (4, 1, 1, None, 0),
+                                             (4, 2, 1, None, 2)])
+def test_conv_gen_cout1(k, s, p, crop, act):
+    from ainp import ops
+    g = torch.Generator().manual_seed(5)
+    N, C, H, W = 2, 64, 32, 40
+    x = torch.randn(N, C, H, W, generator=g)
+    m = (torch.rand(N, H, W, generator=g) > 0.2).float()
+    w = torch.randn(1, C, k, k, generator=g) * 0.1
+    b = torch.randn(1, generator=g)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    ratio = torch.rand(N, Ho, Wo, generator=g) + 0.5
+    sc = torch.tensor([1.3])
+    y, _ = ops.conv_gen((x.cuda(), m.cuda()), w.cuda(), stride=s, pad=p, bias=b.cuda(),
+                        ratio=ratio.cuda(), scale=sc.cuda(), act=act, crop=crop)
+    yr, _ = _conv_ref(x, m, None, None, H, W, w, k, s, p, b, ratio, sc, act)
+    yr = yr[:, 0]
+    if crop is not None:
+        yr = yr[:, :crop[0], :crop[1]]
+    else:
+        y = y[:, 0]
+    assert rel(y, yr) < 1e-5
+
+
+# ------------------------------------------------------------- partial conv
+def test_partial_conv_fixture_cases(small):
+    from ainp import gan as G
+    for ci in range(4):
+        cin, cout, k, s, p, hb = [int(v) for v in small[f"pc{ci}/cfg"]]
+        pc = G.PartialConv2d(cin, cout, k, s, p, bias=bool(hb))
+        with torch.no_grad():
+            pc.conv.weight.copy_(torch.from_numpy(small[f"pc{ci}/w"]))
+            if hb:
+                pc.bias.copy_(torch.from_numpy(small[f"pc{ci}/b"]))
+        pc = pc.cuda()
+        y, um = pc(torch.from_numpy(small[f"pc{ci}/x"]).cuda(), torch.from_numpy(small[f"pc{ci}/m"]).cuda())
+        assert rel(y, small[f"pc{ci}/y"]) < TOL, ci
+        np.testing.assert_array_equal(um.cpu().numpy(), small[f"pc{ci}/um"])
+
+
+# ------------------------------------------------------------- generator
+def test_generator_small_matches_reference(small):
+    from ainp import gan as G
+    from golden.gen_golden_gan import SMALL_DEC, SMALL_ENC, SMALL_FINAL
+    m = G.PConvUNet(enc_layer_cfg=SMALL_ENC, dec_layer_cfg=SMALL_DEC, final_dec_cfg=SMALL_FINAL)
+    m.load_state_dict(_sd(small, "g_init/"))
+    m = m.cuda().train()
+    y = m(torch.from_numpy(small["g_x"]).cuda(), torch.from_numpy(small["g_mask"]).cuda())
+    assert y.shape == small["g_y"].shape
+    assert rel(y, small["g_y"]) < TOL
+    after = _sd(small, "g_after/")
+    sd = m.state_dict()
+    for k, v in after.items():
+        if "running" in k:
+            assert rel(sd[k], v) < TOL, k
+        elif k.endswith("num_batches_tracked"):
+            assert int(sd[k]) == int(v)
+    # eval mode uses the running statistics: compare with the oracle
+    m.eval()
+    pe = {k: v.detach().cpu().clone() for k, v in m.state_dict().items()}
+    ye = m(torch.from_numpy(small["g_x"]).cuda(), torch.from_numpy(small["g_mask"]).cuda())
+    with torch.no_grad():
+        yr = R.generator(pe, torch.from_numpy(small["g_x"]), torch.from_numpy(small["g_mask"]),
+                         False, SMALL_ENC, SMALL_DEC)
+    assert rel(ye, yr) < TOL
+
+
+def test_generator_full_matches_reference(golden_dir):
+    from ainp import gan as G
+    g = np.load(os.path.join(golden_dir, "gan_full.npz"), allow_pickle=False)
+    torch.manual_seed(0)
+    m = G.PConvUNet().cuda().train()
+    y = m(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["mask"]).cuda())
+    yf = y.cpu().numpy().reshape(-1)
+    assert rel(yf[::97], g["y_sample"]) < TOL
+    assert abs(np.linalg.norm(yf.astype(np.float64)) - g["y_norm"][0]) < TOL * g["y_norm"][0]
+
+
+# ------------------------------------------------------------- discriminator
+def test_discriminator_step_matches_reference(small):
+    from ainp import gan as G
+    from ainp.optim import Adam
+    from golden.gen_golden_gan import SMALL_D
+    D = G.Discriminator(layer_cfg=SMALL_D)
+    D.load_state_dict(_sd(small, "d_init/"))
+    D = D.cuda().train()
+    opt = Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    opt.zero_grad()
+    dr = D(torch.from_numpy(small["d_real_in"]).cuda())
+    after1 = _sd(small, "d_after_fwd1/")
+    sd = D.state_dict()
+    for k in after1:
+        if k.endswith("weight_u") or k.endswith("weight_v"):
+            assert rel(sd[k], after1[k]) < 1e-5, k
+    lr_ = G.bce_with_logits_const(dr, 1.0)
+    df = D(torch.from_numpy(small["d_fake_in"]).cuda())
+    lf = G.bce_with_logits_const(df, 0.0)
+    dl = (lr_ + lf) / 2
+    dl.backward()
+    assert rel(dr, small["d_real_logits"]) < 1e-5
+    assert rel(df, small["d_fake_logits"]) < 1e-5
+    assert abs(dl.item() - small["d_loss"][0]) < 1e-5 * abs(small["d_loss"][0])
+    for k, p in D.named_parameters():
+        assert rel(p.grad, small["d_grad/" + k]) < TOL, k
+    opt.step()
+    after = _sd(small, "d_after_step/")
+    sd = D.state_dict()
+    for k, v in after.items():
+        assert rel(sd[k], v) < 1e-5, k
+
+
+def test_discriminator_full_logits(golden_dir):
+    from ainp import gan as G
+    g = np.load(os.path.join(golden_dir, "gan_full.npz"), allow_pickle=False)
+    torch.manual_seed(1)
+    D = G.Discriminator().cuda().train()
+    with torch.no_grad():
+        logits = D(torch.from_numpy(g["x"]).cuda())
+    assert rel(logits, g["d_logits"]) < TOL
+
+
+# ------------------------------------------------------------- VGG + losses
+def _vgg_pair(seed=0):
+    from ainp import gan as G
+    pv = R.vgg19_init(seed)
+    v = G.VGGLoss("cuda")
+    v.vgg_layers.load_state_dict({k: t for k, t in pv.items()}, strict=False)
+    return v, pv
+
+
+def test_vgg_prepare_matches_oracle():
+    from ainp import gan as G
+    g = torch.Generator().manual_seed(3)
+    gen = torch.tanh(torch.randn(2, 1, 257, 626, generator=g))
+    tgt = torch.rand(2, 1, 257, 626, generator=g) * 4 - 0.5
+    v = G.VGGLoss("cuda")
+    for x, is_gen in ((gen, True), (tgt, False)):
+        ours = v._prepare(x.cuda(), is_gen)
+        ref = R.vgg_prepare(x, is_gen)
+        assert (ours.cpu() - ref).abs().max().item() < 2e-5
+
+
+def test_vgg_losses_match_oracle():
+    g = torch.Generator().manual_seed(4)
+    gen = torch.tanh(torch.randn(2, 1, 257, 626, generator=g))
+    tgt = torch.rand(2, 1, 257, 626, generator=g) * 3
+    v, pv = _vgg_pair(0)
+    perc, style = v(gen.cuda(), tgt.cuda())
+    with torch.no_grad():
+        rp, rs = R.vgg_losses(pv, gen, tgt)
+    assert abs(perc.item() - rp.item()) <= TOL * abs(rp.item())
+    assert abs(style.item() - rs.item()) <= TOL * abs(rs.item())
+
+
+def test_calculate_losses_match_oracle():
+    from ainp import gan as G
+    g = torch.Generator().manual_seed(6)
+    gen = torch.tanh(torch.randn(2, 1, 257, 626, generator=g))
+    orig = torch.rand(2, 1, 257, 626, generator=g) * 3
+    mask = torch.ones(2, 1, 257, 626)
+    mask[:, :, :, 300:326] = 0
+    d_fake = torch.randn(2, 1, 30, 76, generator=g)
+    cfg = {"training": dict(R.LAMBDAS)}
+    v, pv = _vgg_pair(1)
+    ours = G.calculate_losses(cfg, gen.cuda(), orig.cuda(), mask.cuda(), d_fake.cuda(), v)
+    with torch.no_grad():
+        ref = R.generator_losses(gen, orig, mask, d_fake, pv)
+    for k in ref:
+        assert abs(ours[k].item() - ref[k].item()) <= TOL * max(abs(ref[k].item()), 1e-6), k
+
+
+# ------------------------------------------------------------- full GAN step
+def test_gan_step_matches_oracle(small):
+    from ainp.gan_train import GanTrainer
+    from golden.gen_golden_gan import SMALL_D, SMALL_DEC, SMALL_ENC, SMALL_FINAL
+    from ainp import gan as G
+    Gm = G.PConvUNet(enc_layer_cfg=SMALL_ENC, dec_layer_cfg=SMALL_DEC, final_dec_cfg=SMALL_FINAL)
+    Gm.load_state_dict(_sd(small, "g_init/"))
+    Dm = G.Discriminator(layer_cfg=SMALL_D)
+    Dm.load_state_dict(_sd(small, "d_init/"))
+    cfg = {"training": dict(R.LAMBDAS, g_lr=2e-4, d_lr=2e-4, b1=0.5, b2=0.999)}
+    tr = GanTrainer(cfg, Gm.cuda(), Dm.cuda(), vgg=None)
+    orig = torch.from_numpy(small["d_real_in"])
+    imp = torch.from_numpy(small["g_x"])
+    mask = torch.from_numpy(small["g_mask"])
+    out = tr.step(orig.cuda(), imp.cuda(), mask.cuda())
+    pg = _sd(small, "g_init/")
+    pd = _sd(small, "d_init/")
+    ref = R.GanStep(pg, pd, None, lr=2e-4, betas=(0.5, 0.999))
+    lam = dict(R.LAMBDAS)
+    ref.lam = lam
+    r = ref.step(orig, imp, mask)
+    assert rel(out["generated"], r["generated"]) < TOL
+    for k in ("d_loss", "g_total", "g_adv", "g_l1_valid", "g_l1_hole", "g_mag_weighted"):
+        assert abs(float(out[k]) - float(r[k])) <= TOL * max(abs(float(r[k])), 1e-6), k
+    sd = Dm.state_dict()
+    for k in R.d_trainable_keys(pd):
+        assert rel(sd[k], pd[k].detach()) < 1e-5, k
+    for k in [k for k in pd if k.endswith("weight_u") or k.endswith("weight_v")]:
+        assert rel(sd[k], pd[k]) < 1e-5, k
