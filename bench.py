@@ -94,7 +94,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--roofline-reps", type=int, default=10)
+    ap.add_argument("--workload", choices=("cnnblstm", "gan"), default="cnnblstm",
+                    help="cnnblstm = BASELINE configs[1] (the headline metric); gan = configs[3]")
     args = ap.parse_args()
+    if args.workload == "gan":
+        return run_gan(args)
 
     from ainp import ops
     from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
@@ -220,6 +224,148 @@ def main():
                                     / FP32_MFMA_PEAK_TFLOPS, 4),
             "roofline": roof,
             "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+# ====================================================================== GAN (C4)
+GAN_CFG = {
+    "training": {"g_lr": 2e-4, "d_lr": 2e-4, "b1": 0.5, "b2": 0.999, "lambda_adv": 0.01,
+                 "lambda_l1_valid": 1.0, "lambda_l1_hole": 2.0, "lambda_vgg_perceptual": 4.0,
+                 "lambda_vgg_style": 500.0, "lambda_mag_weighted": 0.2},
+}
+GAN_FLOP_PER_SAMPLE = 270.4e9   # SURVEY §8 d4 at T=626: G fwd + 3 D fwd + D-step bwd + 2 VGG fwd
+
+
+def gan_cpu_baseline(T, S, g, steps=1):
+    """Oracle (reference restatement) GAN step on the host cores, batch 1."""
+    from oracle import gan_ref, stft_ref
+    from ainp.synth import synthetic_clip
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    pg = gan_ref.init_generator(0)
+    pd = gan_ref.init_discriminator(1)
+    pv = gan_ref.vgg19_init(0)
+    st = gan_ref.GanStep(pg, pd, pv)
+    clip = synthetic_clip(4242, S)
+    o, i, _, m = stft_ref.gan_item(clip, 30000, g, 512, 128, 512)
+    t = lambda a: torch.from_numpy(a)[None, None]
+    st.step(t(o), t(i), t(m))            # warmup
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        st.step(t(o), t(i), t(m))
+    dt = (time.perf_counter() - t0) / steps
+    return {"value": round(T / dt, 2), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"oracle/gan_ref.py GanStep fp32 torch-CPU (G fwd, D step, G-step losses "
+                      f"incl. VGG19 and its backward into D as the reference), batch 1 x T={T}, "
+                      f"{steps} timed step after 1 warmup; features precomputed"}
+
+
+def run_gan(args):
+    from ainp import ops
+    from ainp import gan as G
+    from ainp.dist import Comm, init_from_env
+    from ainp.gan_train import GanTrainer
+    import torch.distributed as dist
+
+    rank, world, local = init_from_env()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    comm = Comm() if world > 1 else None
+    B = args.batch if args.batch != 32 else 8        # C4: batch 8 per GPU
+    S, hop, n_fft, g = 80000, 128, 512, 3200          # 5 s @ 16 kHz, gap 0.2 s
+    T = 1 + S // hop                                   # 626
+    torch.manual_seed(0)
+    gen = G.PConvUNet().to(dev)
+    disc = G.Discriminator().to(dev)
+    vgg = G.VGGLoss(dev)
+    tr = GanTrainer(GAN_CFG, gen, disc, vgg, comm=comm)
+    audio = torch.from_numpy(synthetic_clips(B, S, 200000 + 100000 * rank)).to(dev)
+    nsteps = args.warmup + args.steps
+    rng = np.random.default_rng(777 + rank)
+    starts = torch.from_numpy(rng.integers(0, S - g + 1, size=(nsteps, B)).astype(np.int64)).to(dev)
+    hole = torch.zeros(nsteps, device=dev)
+
+    def step(i):
+        o, im, _, m = ops.stft_features(audio, starts[i], g, n_fft, hop, n_fft, n_frames=T,
+                                        mode=ops.FEAT_GAN, outputs=(True, True, False, True))
+        out = tr.step(o.unsqueeze(1), im.unsqueeze(1), m.unsqueeze(1))
+        hole[i] = out["g_l1_hole"]
+
+    for i in range(args.warmup):
+        step(i)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, nsteps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    value = B * T * args.steps * world / elapsed
+    ms_step = 1000.0 * elapsed / args.steps
+
+    roof = None
+    if rank == 0:
+        # dominant kernel: the final PartialConv2d (65 -> 64, 3x3) at the padded
+        # 384 x 640 resolution, B examples: conv_gen generic path
+        Hp, Wp = 384, 640
+        x0 = torch.randn(B, 64, Hp // 2, Wp // 2, device=dev)
+        m0 = torch.ones(B, Hp // 2, Wp // 2, device=dev)
+        x1 = torch.randn(B, 1, Hp, Wp, device=dev)
+        m1 = torch.ones(B, Hp, Wp, device=dev)
+        w = torch.randn(64, 65, 3, 3, device=dev) * 0.05
+        ratio = torch.ones(B, Hp, Wp, device=dev)
+        bias = torch.zeros(64, device=dev)
+        out = torch.empty(B, 64, Hp, Wp, device=dev)
+        kw = dict(src1=(x1, m1), Hin=Hp, Win=Wp, stride=1, pad=1, bias=bias, ratio=ratio,
+                  act=ops.ACT_LEAKY, out=out)
+        for _ in range(2):
+            ops.conv_gen((x0, m0), w, **kw)
+        s = torch.cuda.current_stream(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(args.roofline_reps):
+            ops.conv_gen((x0, m0), w, **kw)
+        e1.record(s)
+        torch.cuda.synchronize()
+        avg_s = e0.elapsed_time(e1) / 1000.0 / args.roofline_reps
+        flops = 2.0 * 64 * 65 * 9 * B * Hp * Wp
+        ach = flops / avg_s / 1e12
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "kernel": f"conv_gen_fwd_kernel<false> (final PartialConv2d 65->64 3x3 at "
+                          f"{Hp}x{Wp}, B={B})", "avg_launch_ms": round(avg_s * 1e3, 4),
+                "flop_per_launch": flops}
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = gan_cpu_baseline(T, S, g)
+    if rank == 0:
+        step_flops = GAN_FLOP_PER_SAMPLE * B * world
+        out = {
+            "metric": "GAN spectrogram-frames/sec/node (train step), BASELINE configs[3]",
+            "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+            "data": "synthetic (5 s/16 kHz harmonic clips, seeded; random init; VGG19 random "
+                    "init: pretrained weights not downloadable offline)",
+            "config": {"workload": "C4: GAN step (GAN STFT features + PConvUNet fwd + D step "
+                                   "+ G-step losses incl. VGG19), fp32, 8 examples/GPU, F=257, "
+                                   "T=626, gap 0.2 s", "global_batch": B * world, "seq_len": T,
+                       "freq_bins": 257, "parallelism": f"dp{world}"},
+            "recon_l1_hole": float(hole[-1].item()),
+            "step_tflops": round(step_flops / (ms_step / 1e3) / 1e12, 2),
+            "mfma_util_step": round(step_flops / world / (ms_step / 1e3) / 1e12
+                                    / FP32_MFMA_PEAK_TFLOPS, 4),
+            "roofline": roof, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
