@@ -280,16 +280,18 @@ int ainp_adam(float* const* params, const float* const* grads,
  * may be NULL.  act: 0 none, 1 ReLU, 2 LeakyReLU(slope), 3 tanh.
  * stats (NULL or double[ainp_conv_gen_stat_parts(N,Ho,Wo)][2][Cout]): fixed-order
  * per-tile (sum, sumsq) of the value before act, for ainp_bn_stats_reduce.
- * Cout == 1 uses a direct kernel; crop_h / crop_w (> 0) then write only the
+ * Cout == 1 uses a direct channel-chunked kernel (workspace: ainp_conv_gen_workspace
+ * bytes; NULL allowed when Cout > 1); crop_h / crop_w (> 0) then write only the
  * top-left crop (networks.py:334), else pass 0. */
 int ainp_conv_gen_stat_parts(int64_t N, int64_t Ho, int64_t Wo);
+size_t ainp_conv_gen_workspace(int64_t N, int Cin, int Cout, int64_t Ho, int64_t Wo);
 int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H0, int W0,
                       const float* x1, const float* m1, int C1, int H1, int W1,
                       const float* w, const float* bias, const float* ratio,
                       const float* scale, float* y, double* stats, int64_t N,
                       int Cout, int Hin, int Win, int KH, int KW, int stride,
                       int pad, int act, float slope, int crop_h, int crop_w,
-                      void* stream);
+                      void* workspace, void* stream);
 /* PartialConv2d mask update (networks.py:83-104, multi_channel=False):
  * count = C0*window_sum(m0) + C1*window_sum(m1) over the conv's window (masks
  * are planes of integer counts -- 0/1, or a channel sum -- repeated over their
@@ -343,16 +345,18 @@ int ainp_sn_power(const float* const* w, float* const* u, float* const* v, const
                   const int* wd, int nl, float eps, void* workspace, int maxdim,
                   float* inv_sigma, int update, void* stream);
 /* Gradient through W = W_orig / sigma with u, v held constant:
- * out = G*inv_sigma - (sum G*W_orig) * inv_sigma^2 * u v^T.
+ * out = G*inv_sigma - (sum G*W_orig) * inv_sigma^2 * u v^T, G [h][ldg] (its
+ * first wd columns are dL/dW); out_bias (may be NULL) = G[:, wd] (the bias
+ * gradient computed as the ones-row column of the weight-grad GEMM).
  * workspace: ainp_reduce_workspace() bytes. */
-int ainp_sn_weight_grad(const float* G, const float* w_orig, const float* u, const float* v,
-                        const float* inv_sigma, int h, int wd, void* workspace, float* out,
-                        void* stream);
-/* Discriminator backward glue: im2col col[N][C*KH*KW][Ho*Wo] (k = ci*KH*KW + tap),
- * its adjoint col2im as a gather (deterministic), LeakyReLU backward from the
- * activation output. */
+int ainp_sn_weight_grad(const float* G, int ldg, const float* w_orig, const float* u,
+                        const float* v, const float* inv_sigma, int h, int wd, void* workspace,
+                        float* out, float* out_bias, void* stream);
+/* Discriminator backward glue: im2col col[N][C*KH*KW + ones_row][Ho*Wo]
+ * (k = ci*KH*KW + tap; ones_row = 1 appends a row of 1.0), its adjoint col2im
+ * as a gather (deterministic), LeakyReLU backward from the activation output. */
 int ainp_im2col(const float* x, int64_t N, int C, int H, int W, int KH, int KW, int stride,
-                int pad, float* col, void* stream);
+                int pad, int ones_row, float* col, void* stream);
 int ainp_col2im(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW, int stride,
                 int pad, float* dx, void* stream);
 int ainp_leaky_bwd(const float* g, const float* y, int64_t n, float slope, float* out,

@@ -68,9 +68,10 @@ _SIGS = {
     "ainp_adam": (c_int, [PP, PP, PP, PP, POINTER(c_int64), c_int, c_double, c_double,
                           c_double, c_double, c_double, c_int64, P]),
     "ainp_conv_gen_stat_parts": (c_int, [c_int64, c_int64, c_int64]),
+    "ainp_conv_gen_workspace": (c_size_t, [c_int64, c_int, c_int, c_int64, c_int64]),
     "ainp_conv_gen_fwd": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int,
                                   P, P, P, P, P, P, c_int64, c_int, c_int, c_int, c_int,
-                                  c_int, c_int, c_int, c_int, c_float, c_int, c_int, P]),
+                                  c_int, c_int, c_int, c_int, c_float, c_int, c_int, P, P]),
     "ainp_pconv_mask": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int64,
                                 c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "ainp_gan_pad_input": (c_int, [P, P, c_int64, c_int, c_int, c_int, c_int, P, P, P]),
@@ -84,8 +85,9 @@ _SIGS = {
     "ainp_gan_recon_losses": (c_int, [P, P, P, c_int64, P, P, P]),
     "ainp_sn_workspace": (c_size_t, [c_int, c_int]),
     "ainp_sn_power": (c_int, [PP, PP, PP, P, P, c_int, c_float, P, c_int, P, c_int, P]),
-    "ainp_sn_weight_grad": (c_int, [P, P, P, P, P, c_int, c_int, P, P, P]),
-    "ainp_im2col": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "ainp_sn_weight_grad": (c_int, [P, c_int, P, P, P, P, c_int, c_int, P, P, P, P]),
+    "ainp_im2col": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                            P, P]),
     "ainp_col2im": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "ainp_leaky_bwd": (c_int, [P, P, c_int64, c_float, P, P]),
     "ainp_mul": (c_int, [P, P, c_int64, P, P]),

@@ -340,16 +340,13 @@ class _DiscriminatorFn(torch.autograd.Function):
             h = ins[l]
             Cin, H, W = h.shape[1:]
             K = Cin * k * k
-            grads[2 * l + 1] = ops.rowsum_batched(g.view(N, Cout, P))
-            col = ops.im2col(h, k, s, p)                       # [N, K, P]
-            S = _split_count(N)
-            per = N // S
-            slabs = torch.empty(S, Cout, K, device=g.device)
-            ops.gemm(Cout, K, P, [g[i * per] for i in range(S)], P, 1,
-                     [col[i * per] for i in range(S)], 1, P, [slabs[i] for i in range(S)], K, 1,
-                     strideA=Cout * P, strideB=K * P, nstrided=per, ksplit=2)
-            Gw = ops.sum_slabs(slabs, S).view(Cout, K) if S > 1 else slabs[0]
-            grads[2 * l] = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1]).view_as(w)
+            # [dW | db] = sum_n g_n [Cout, P] . [col_n ; 1]^T, P split into chunks
+            col = ops.im2col(h, k, s, p, ones_row=True)        # [N, K+1, P]
+            Gw = torch.empty(Cout, K + 1, device=g.device)
+            ops.gemm_batched_splitk(Cout, K + 1, P, [g[n] for n in range(N)], P, 1,
+                                    [col[n] for n in range(N)], 1, P, Gw)
+            dw, db = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1], with_bias=True)
+            grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
             if l > 0 or ctx.needs_input_grad[0]:
                 wn = ops.scale_by_scalar(w, inv[l:l + 1])
                 dcol = torch.empty(N, K, P, device=g.device)
@@ -528,11 +525,13 @@ class VGGLoss(nn.Module):
         return feats
 
     def _gram(self, x):
+        """Gram matrices F F^T / (c h w) (loss.py:53-62), split-K over h*w."""
         b, c, h, w = x.shape
-        g = torch.empty(b, c, c, device=x.device)
         hw = h * w
-        ops.gemm(c, c, hw, [x], hw, 1, [x], 1, hw, [g], c, 1, alpha=1.0 / (c * hw),
-                 strideA=c * hw, strideB=c * hw, strideC=c * c, nstrided=b)
+        g = torch.empty(b, c, c, device=x.device)
+        ops.gemm_batched_splitk(c, c, hw, [x[i] for i in range(b)], hw, 1,
+                                [x[i] for i in range(b)], 1, hw, g, alpha=1.0 / (c * hw),
+                                per_batch_out=True)
         return g
 
     @torch.no_grad()

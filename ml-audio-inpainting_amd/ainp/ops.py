@@ -471,9 +471,13 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
     for t, nm in ((bias, "bias"), (ratio, "ratio"), (scale, "scale")):
         if t is not None:
             _req(t, nm)
+    ws = None
+    if Cout == 1:
+        nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, Cout, ch or Ho, cw or Wo))
+        ws = torch.empty(max(1, nb // 4), device=x0.device)
     call("ainp_conv_gen_fwd", x0.data_ptr(), _p(m0), C0, H0, W0, _p(x1), _p(m1), C1, H1, W1,
          w.data_ptr(), _p(bias), _p(ratio), _p(scale), out.data_ptr(), _p(stats), N, Cout,
-         Hin, Win, KH, KW, stride, pad, act, float(slope), ch, cw, _stream(x0))
+         Hin, Win, KH, KW, stride, pad, act, float(slope), ch, cw, _p(ws), _stream(x0))
     return out, stats
 
 
@@ -585,22 +589,59 @@ def sn_power(weights, us, vs, update=True, eps=1e-12):
     return inv
 
 
-def sn_weight_grad(G, w_orig, u, v, inv_sigma):
+def sn_weight_grad(G, w_orig, u, v, inv_sigma, with_bias=False):
+    """G [h, ldg] (ldg >= wd, +1 with the bias column) -> (dW_orig, dbias or None)."""
     _req(G, "G"); _req(w_orig, "w_orig")
     out = torch.empty_like(w_orig)
-    call("ainp_sn_weight_grad", G.data_ptr(), w_orig.data_ptr(), u.data_ptr(), v.data_ptr(),
-         inv_sigma.data_ptr(), w_orig.shape[0], w_orig[0].numel(),
-         _reduce_ws(G.device).data_ptr(), out.data_ptr(), _stream(G))
-    return out
+    h = w_orig.shape[0]
+    ob = torch.empty(h, device=G.device) if with_bias else None
+    call("ainp_sn_weight_grad", G.data_ptr(), G.shape[1], w_orig.data_ptr(), u.data_ptr(),
+         v.data_ptr(), inv_sigma.data_ptr(), h, w_orig[0].numel(),
+         _reduce_ws(G.device).data_ptr(), out.data_ptr(), _p(ob), _stream(G))
+    return out, ob
 
 
-def im2col(x, k, stride, pad):
+def im2col(x, k, stride, pad, ones_row=False):
     _req(x, "x")
     N, C, H, W = x.shape
     Ho, Wo = conv_out_size(H, k, stride, pad), conv_out_size(W, k, stride, pad)
-    col = torch.empty(N, C * k * k, Ho * Wo, device=x.device)
-    call("ainp_im2col", x.data_ptr(), N, C, H, W, k, k, stride, pad, col.data_ptr(), _stream(x))
+    col = torch.empty(N, C * k * k + int(ones_row), Ho * Wo, device=x.device)
+    call("ainp_im2col", x.data_ptr(), N, C, H, W, k, k, stride, pad, int(ones_row),
+         col.data_ptr(), _stream(x))
     return col
+
+
+def largest_divisor_at_most(n, cap):
+    for s in range(max(1, min(n, cap)), 0, -1):
+        if n % s == 0:
+            return s
+    return 1
+
+
+def gemm_batched_splitk(M, N, Kd, As, sam, sak, Bs, sbk, sbn, out, *, alpha=1.0,
+                        per_batch_out=False, target_blocks=768, min_k=256):
+    """C = alpha * sum_b A_b B_b (or C_b = alpha * A_b B_b when per_batch_out),
+    with the long reduction Kd split into S strided chunks per batch so the
+    small-M/N products still fill the chip.  A_b / B_b: tensors whose element
+    (m, k) / (k, n) sits at m*sam + k*sak / k*sbk + n*sbn (k-chunks advance by
+    chunk*sak / chunk*sbk).  Partial products go to slabs summed in fixed order."""
+    nb = len(As)
+    tiles = -(-M // 128) * -(-N // 128)
+    want = max(1, min(Kd // min_k, target_blocks // max(1, tiles * nb)))
+    S = largest_divisor_at_most(Kd, want)
+    kc = Kd // S
+    slabs = torch.empty(nb, S, M, N, device=out.device, dtype=torch.float32)
+    for g0 in range(0, nb, 8):
+        g1 = min(nb, g0 + 8)
+        gemm(M, N, kc, As[g0:g1], sam, sak, Bs[g0:g1], sbk, sbn,
+             [slabs[i] for i in range(g0, g1)], N, 1, alpha=alpha, strideA=kc * sak,
+             strideB=kc * sbk, strideC=M * N, nstrided=S)
+    if per_batch_out:
+        for b in range(nb):
+            sum_slabs(slabs[b], S, out=out[b].reshape(-1))
+    else:
+        sum_slabs(slabs, nb * S, out=out.reshape(-1))
+    return out
 
 
 def col2im(dcol, N, C, H, W, k, stride, pad):

@@ -240,13 +240,21 @@ __global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, i
 }
 
 // Direct convolution for Cout == 1 (the generator's last PartialConv2d and
-// the discriminator's logit conv): one thread per output pixel, weights in
-// LDS, optional crop of the output to [Hc, Wc] (networks.py:334).
-__global__ __launch_bounds__(256) void conv_cout1_kernel(ConvGenParams p, int act, int Hc, int Wc) {
-  extern __shared__ float sw[];
+// the discriminator's logit conv).  Stage 1: grid (pixel blocks, channel
+// chunks of C1_CC) -- each thread sums its pixel over one chunk of the
+// concatenated input channels x taps (weights of the chunk in LDS); stage 2
+// adds the chunk partials in fixed order, applies 1/sigma, the partial-conv
+// ratio, bias and activation, and writes the (optionally cropped, networks.py:334)
+// output.
+constexpr int C1_CC = 32;
+
+__global__ __launch_bounds__(256) void conv_cout1_partial_kernel(ConvGenParams p, int Hc, int Wc,
+                                                                 float* partial) {
+  __shared__ float sw[C1_CC * 64];
   const int KK = p.KH * p.KW;
-  const int K = p.Cin * KK;
-  for (int i = threadIdx.x; i < K; i += blockDim.x) sw[i] = p.w[i];
+  const int c0 = blockIdx.y * C1_CC;
+  const int cn = min(C1_CC, p.Cin - c0);
+  for (int i = threadIdx.x; i < cn * KK; i += blockDim.x) sw[i] = p.w[(int64_t)c0 * KK + i];
   __syncthreads();
   const int64_t np = (int64_t)p.N * Hc * Wc;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -258,8 +266,9 @@ __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvGenParams p, int ac
   float acc = 0.f;
   for (int src = 0; src < 2; ++src) {
     const ConvSrcDev& s = src == 0 ? p.s0 : p.s1;
-    if (s.C == 0) continue;
-    const int cbase = src == 0 ? 0 : p.s0.C;
+    const int sc0 = src == 0 ? 0 : p.s0.C;          // first concat channel of this source
+    const int lo = max(c0, sc0), hi = min(c0 + cn, sc0 + s.C);
+    if (lo >= hi) continue;
     const int64_t plane = (int64_t)s.Hs * s.Ws;
     for (int ky = 0; ky < p.KH; ++ky) {
       const int iy = by + ky;
@@ -271,14 +280,27 @@ __global__ __launch_bounds__(256) void conv_cout1_kernel(ConvGenParams p, int ac
         const int sx = src_coord(ix, s.Ws, p.Win, s.up);
         const int64_t off = (int64_t)sy * s.Ws + sx;
         const float mv = s.m ? s.m[(int64_t)n * plane + off] : 1.f;
-        const float* xb = s.x + (int64_t)n * s.C * plane + off;
-        const float* wb = sw + cbase * KK + ky * p.KW + kx;
+        const float* xb = s.x + ((int64_t)n * s.C + (lo - sc0)) * plane + off;
+        const float* wb = sw + (lo - c0) * KK + ky * p.KW + kx;
         float a = 0.f;
-        for (int c = 0; c < s.C; ++c) a = fmaf(wb[c * KK], xb[(int64_t)c * plane] * mv, a);
-        acc += a;
+        for (int c = 0; c < hi - lo; ++c) a = fmaf(wb[c * KK], xb[(int64_t)c * plane], a);
+        acc = fmaf(a, mv, acc);
       }
     }
   }
+  partial[(int64_t)blockIdx.y * np + t] = acc;
+}
+
+__global__ void conv_cout1_finish_kernel(ConvGenParams p, int act, int Hc, int Wc, int nchunk,
+                                         const float* partial) {
+  const int64_t np = (int64_t)p.N * Hc * Wc;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= np) return;
+  float acc = 0.f;
+  for (int c = 0; c < nchunk; ++c) acc += partial[(int64_t)c * np + t];
+  const int n = (int)(t / ((int64_t)Hc * Wc));
+  const int r = (int)(t - (int64_t)n * Hc * Wc);
+  const int oy = r / Wc, ox = r - oy * Wc;
   float v = acc * (p.scale ? *p.scale : 1.f);
   if (p.ratio) v *= p.ratio[((int64_t)n * p.Ho + oy) * p.Wo + ox];
   if (p.bias) v += p.bias[0];
@@ -593,11 +615,14 @@ __global__ void sn_sigma_kernel(SnLayers L, const float* tu, int ldt, float* inv
 
 // dW_orig = G * inv_sigma - (sum G*W_orig) * inv_sigma^2 * u v^T
 // stage 1: partial[block] = sum G*W  (fixed order), stage 2: apply.
-__global__ void sn_gdot_partial_kernel(const float* G, const float* W, int64_t n, double* partial) {
+__global__ void sn_gdot_partial_kernel(const float* G, int ldg, const float* W, int wd, int64_t n,
+                                       double* partial) {
   double s = 0.0;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
-       i += (int64_t)gridDim.x * blockDim.x)
-    s += (double)G[i] * (double)W[i];
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / wd, c = i - r * wd;
+    s += (double)G[r * ldg + c] * (double)W[i];
+  }
   __shared__ double red[4];
   s = wave_sum_d(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
@@ -605,9 +630,9 @@ __global__ void sn_gdot_partial_kernel(const float* G, const float* W, int64_t n
   if (threadIdx.x == 0) partial[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
 }
 
-__global__ void sn_wgrad_apply_kernel(const float* G, const double* partial, int np,
+__global__ void sn_wgrad_apply_kernel(const float* G, int ldg, const double* partial, int np,
                                       const float* u, const float* v, const float* inv_sigma,
-                                      int h, int wd, float* out) {
+                                      int h, int wd, float* out, float* out_bias) {
   __shared__ float gw;
   if (threadIdx.x == 0) {
     double s = 0.0;
@@ -619,22 +644,29 @@ __global__ void sn_wgrad_apply_kernel(const float* G, const double* partial, int
   if (t >= (int64_t)h * wd) return;
   const int i = (int)(t / wd), j = (int)(t - (int64_t)i * wd);
   const float is = *inv_sigma;
-  out[t] = G[t] * is - gw * is * is * u[i] * v[j];
+  out[t] = G[(int64_t)i * ldg + j] * is - gw * is * is * u[i] * v[j];
+  if (out_bias && j == 0) out_bias[i] = G[(int64_t)i * ldg + wd];
 }
 
 // ------------------------------------------------------------ D backward glue
 // col[n][ci*KK + tap][oy*Wo + ox] = x[n][ci][oy*s-p+ky][ox*s-p+kx] (0 outside)
+// ones_row: an extra row k = C*KK of 1.0 (the bias column of the weight-grad GEMM)
 __global__ void im2col_kernel(const float* x, int N, int C, int H, int W, int KH, int KW,
-                              int stride, int pad, int Ho, int Wo, float* col) {
+                              int stride, int pad, int Ho, int Wo, int ones_row, float* col) {
   const int KK = KH * KW;
   const int64_t P = (int64_t)Ho * Wo;
-  const int64_t total = (int64_t)N * C * KK * P;
+  const int Kr = C * KK + ones_row;
+  const int64_t total = (int64_t)N * Kr * P;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
   const int64_t pp = t % P;
   const int64_t rest = t / P;
-  const int k = (int)(rest % ((int64_t)C * KK));
-  const int n = (int)(rest / ((int64_t)C * KK));
+  const int k = (int)(rest % Kr);
+  const int n = (int)(rest / Kr);
+  if (k == C * KK) {
+    col[t] = 1.f;
+    return;
+  }
   const int ci = k / KK, tap = k - ci * KK;
   const int ky = tap / KW, kx = tap - ky * KW;
   const int oy = (int)(pp / Wo), ox = (int)(pp - (int64_t)oy * Wo);
@@ -718,13 +750,18 @@ extern "C" int ainp_conv_gen_stat_parts(int64_t N, int64_t Ho, int64_t Wo) {
   return (int)cdiv(N * Ho * Wo, CG_BN);
 }
 
+extern "C" size_t ainp_conv_gen_workspace(int64_t N, int Cin, int Cout, int64_t Ho, int64_t Wo) {
+  if (Cout != 1) return 0;
+  return (size_t)cdiv(Cin, C1_CC) * N * Ho * Wo * sizeof(float);
+}
+
 extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H0, int W0,
                                  const float* x1, const float* m1, int C1, int H1, int W1,
                                  const float* w, const float* bias, const float* ratio,
                                  const float* scale, float* y, double* stats, int64_t N,
                                  int Cout, int Hin, int Win, int KH, int KW, int stride,
                                  int pad, int act, float slope, int crop_h, int crop_w,
-                                 void* stream) {
+                                 void* workspace, void* stream) {
   if (!x0 || C0 < 1 || C1 < 0 || (C1 > 0 && !x1) || !w || !y || N < 1 || Cout < 1 ||
       Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 || act < 0 || act > 3)
     return record_msg("ainp_conv_gen_fwd: bad argument");
@@ -757,12 +794,15 @@ extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H
   hipStream_t s = as_stream(stream);
   if (Cout == 1) {
     const int Hc = crop_h > 0 ? crop_h : Ho, Wc = crop_w > 0 ? crop_w : Wo;
-    if (stats || Hc > Ho || Wc > Wo) return record_msg("ainp_conv_gen_fwd: Cout=1 options");
-    const size_t lds = (size_t)p.Cin * KH * KW * sizeof(float);
-    if (lds > 64 * 1024) return record_msg("ainp_conv_gen_fwd: Cout=1 weight > 64 KB");
+    if (stats || Hc > Ho || Wc > Wo || !workspace || KH * KW > 64)
+      return record_msg("ainp_conv_gen_fwd: Cout=1 options (workspace, kernel <= 8x8)");
     const int64_t np = N * (int64_t)Hc * Wc;
-    hipLaunchKernelGGL(conv_cout1_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), lds, s, p,
-                       act, Hc, Wc);
+    const int nchunk = (int)cdiv(p.Cin, C1_CC);
+    float* part = reinterpret_cast<float*>(workspace);
+    hipLaunchKernelGGL(conv_cout1_partial_kernel, dim3((unsigned)cdiv(np, 256), nchunk), dim3(256),
+                       0, s, p, Hc, Wc, part);
+    hipLaunchKernelGGL(conv_cout1_finish_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, s, p,
+                       act, Hc, Wc, nchunk, part);
     return check_launch("conv_cout1");
   }
   if (crop_h > 0 || crop_w > 0) return record_msg("ainp_conv_gen_fwd: crop needs Cout=1");
@@ -921,28 +961,32 @@ extern "C" int ainp_sn_power(const float* const* w, float* const* u, float* cons
   return check_launch("sn_power");
 }
 
-extern "C" int ainp_sn_weight_grad(const float* G, const float* w_orig, const float* u,
+extern "C" int ainp_sn_weight_grad(const float* G, int ldg, const float* w_orig, const float* u,
                                    const float* v, const float* inv_sigma, int h, int wd,
-                                   void* workspace, float* out, void* stream) {
-  if (!G || !w_orig || !u || !v || !inv_sigma || h < 1 || wd < 1 || !workspace || !out)
+                                   void* workspace, float* out, float* out_bias, void* stream) {
+  if (!G || !w_orig || !u || !v || !inv_sigma || h < 1 || wd < 1 || !workspace || !out ||
+      ldg < wd || (out_bias && ldg < wd + 1))
     return record_msg("ainp_sn_weight_grad: bad argument");
   hipStream_t s = as_stream(stream);
   double* part = reinterpret_cast<double*>(workspace);
   const int64_t n = (int64_t)h * wd;
-  hipLaunchKernelGGL(sn_gdot_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, G, w_orig, n, part);
-  hipLaunchKernelGGL(sn_wgrad_apply_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, G, part,
-                     kRedBlocks, u, v, inv_sigma, h, wd, out);
+  hipLaunchKernelGGL(sn_gdot_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, G, ldg, w_orig, wd,
+                     n, part);
+  hipLaunchKernelGGL(sn_wgrad_apply_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, G, ldg,
+                     part, kRedBlocks, u, v, inv_sigma, h, wd, out, out_bias);
   return check_launch("sn_weight_grad");
 }
 
 extern "C" int ainp_im2col(const float* x, int64_t N, int C, int H, int W, int KH, int KW,
-                           int stride, int pad, float* col, void* stream) {
-  if (!x || !col || N < 1 || C < 1 || KH < 1 || KW < 1 || stride < 1)
+                           int stride, int pad, int ones_row, float* col, void* stream) {
+  if (!x || !col || N < 1 || C < 1 || KH < 1 || KW < 1 || stride < 1 || ones_row < 0 ||
+      ones_row > 1)
     return record_msg("ainp_im2col: bad argument");
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
-  const int64_t total = N * C * KH * KW * (int64_t)Ho * Wo;
+  const int64_t total = N * (C * KH * KW + ones_row) * (int64_t)Ho * Wo;
   hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                     as_stream(stream), x, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo, col);
+                     as_stream(stream), x, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo,
+                     ones_row, col);
   return check_launch("im2col");
 }
 

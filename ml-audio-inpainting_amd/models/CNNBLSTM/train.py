@@ -31,8 +31,9 @@ for p in (HERE, _PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-from dataset import LibriSpeechDataset  # noqa: E402
-from model import StackedBLSTMCNN  # noqa: E402
+# package-qualified: the GAN scripts also have a `dataset` module
+from models.CNNBLSTM.dataset import LibriSpeechDataset  # noqa: E402
+from models.CNNBLSTM.model import StackedBLSTMCNN  # noqa: E402
 
 from ainp.cnnblstm import l1_pow10_loss  # noqa: E402
 from ainp.dist import Comm, GradAllReducer, init_from_env  # noqa: E402

@@ -35,9 +35,10 @@ for p in (HERE, _PKG):
     if p not in sys.path:
         sys.path.insert(0, p)
 
-from dataset import SpeechInpaintingDataset  # noqa: E402
-from loss import VGGLoss  # noqa: E402
-from networks import Discriminator, PConvUNet  # noqa: E402
+# package-qualified: the CNNBLSTM scripts also have a `dataset` module
+from models.GAN.dataset import SpeechInpaintingDataset  # noqa: E402
+from models.GAN.loss import VGGLoss  # noqa: E402
+from models.GAN.networks import Discriminator, PConvUNet  # noqa: E402
 
 from ainp.dist import Comm, init_from_env  # noqa: E402
 from ainp.gan import calculate_losses, find_latest_checkpoint  # noqa: E402
