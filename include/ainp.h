@@ -94,6 +94,26 @@ int ainp_stft(const void* audio, int dtype, int64_t n_signals,
               int64_t n_samples, const double* window, int n_fft, int hop,
               int center, int64_t n_frames, void* out, void* stream);
 
+/* Inverse STFT, librosa>=0.10 istft (utils.spectrogram_to_audio, utils.py:317-326):
+ * spectra [n_signals][n_bins = n_fft/2+1][n_frames] given as mode
+ *   0: complex64 (in0)            1: complex128 (in0, output float64)
+ *   2: magnitude f32 (in0) * complex64 unit angles (in1)  -- the Griffin-Lim inner istft
+ *   3: magnitude f32 (in0) * exp(i * phase f32 (in1))    -- spectrogram_to_audio with phase
+ * frames: float64 irfft (imaginary DC / Nyquist ignored, as numpy) x window;
+ * overlap-add gather, divided by the window sum-square where > tiny; center != 0
+ * trims n_fft/2 per side: out [n_signals][hop*(n_frames-1)] (center) or
+ * [n_signals][n_fft + hop*(n_frames-1)].  workspace: ainp_istft_workspace bytes.
+ * window: [n_fft] f64, centre-padded (as for ainp_stft). */
+size_t ainp_istft_workspace(int64_t n_signals, int64_t n_frames, int n_fft);
+int ainp_istft(const void* in0, const void* in1, int mode, int64_t n_signals, int n_bins,
+               int64_t n_frames, const double* window, int n_fft, int hop, int center,
+               void* workspace, void* out, void* stream);
+/* One Griffin-Lim phase update (librosa griffinlim, utils.py:330): a = rebuilt -
+ * m/(1+m) * tprev (no tprev term when first != 0), angles = a / (|a| + tiny),
+ * tprev = rebuilt; n complex64 elements (interleaved). */
+int ainp_gl_update(const float* rebuilt, float* tprev, float* angles, int64_t n,
+                   float momentum, int first, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32, exact fp32)                    */
 /* ------------------------------------------------------------------------ */
@@ -275,19 +295,28 @@ int ainp_adam(float* const* params, const float* const* grads,
  *   channels [0,C0) from x0 (H0 x W0; nearest-resampled to Hin x Win when
  *   smaller, i.e. the x2 Upsample) and [C0,C0+C1) from x1 (H1 x W1 == Hin x Win),
  *   each multiplied by its mask plane m0 / m1 ([N,H0,W0] / [N,H1,W1], NULL = 1).
- * w [Cout][C0+C1][KH][KW]; y [N][Cout][Ho][Wo];
+ * w [Cout][C0+C1][KH][KW] (used by the Cout == 1 path); wt = the same weights
+ * k-major from ainp_conv_weight_kmajor (required when Cout > 1; cacheable while
+ * w is unchanged); y [N][Cout][Ho][Wo];
  * y = act(conv * (*scale) * ratio[n][oy][ox] + bias[co]); scale / ratio / bias
  * may be NULL.  act: 0 none, 1 ReLU, 2 LeakyReLU(slope), 3 tanh.
- * stats (NULL or double[ainp_conv_gen_stat_parts(N,Ho,Wo)][2][Cout]): fixed-order
+ * stats (NULL or double[ainp_conv_gen_stat_parts(...)][2][Cout]): fixed-order
  * per-tile (sum, sumsq) of the value before act, for ainp_bn_stats_reduce.
- * Cout == 1 uses a direct channel-chunked kernel (workspace: ainp_conv_gen_workspace
- * bytes; NULL allowed when Cout > 1); crop_h / crop_w (> 0) then write only the
- * top-left crop (networks.py:334), else pass 0. */
-int ainp_conv_gen_stat_parts(int64_t N, int64_t Ho, int64_t Wo);
-size_t ainp_conv_gen_workspace(int64_t N, int Cin, int Cout, int64_t Ho, int64_t Wo);
+ * workspace: ainp_conv_gen_workspace(...) bytes (0 = may be NULL): the Cout == 1
+ * direct channel-chunked kernel and split-K launches (small tile grids with a
+ * long K) keep their partial sums there.  crop_h / crop_w (> 0, Cout == 1
+ * only) write only the top-left crop (networks.py:334), else pass 0. */
+int ainp_conv_gen_stat_parts(int64_t N, int Cin, int KH, int KW, int Cout, int64_t Ho,
+                             int64_t Wo);
+size_t ainp_conv_gen_workspace(int64_t N, int Cin, int KH, int KW, int Cout, int64_t Ho,
+                               int64_t Wo);
+/* wt[k][co] for the implicit GEMM: k runs over source 0 (k = tap*C0 + ci), then
+ * source 1 (k = KH*KW*C0 + tap*C1 + ci); wt[k][co] = w[co][ci (+C0)][tap]. */
+int ainp_conv_weight_kmajor(const float* w, int Cout, int C0, int C1, int KH, int KW,
+                            float* wt, void* stream);
 int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H0, int W0,
                       const float* x1, const float* m1, int C1, int H1, int W1,
-                      const float* w, const float* bias, const float* ratio,
+                      const float* w, const float* wt, const float* bias, const float* ratio,
                       const float* scale, float* y, double* stats, int64_t N,
                       int Cout, int Hin, int Win, int KH, int KW, int stride,
                       int pad, int act, float slope, int crop_h, int crop_w,

@@ -67,10 +67,11 @@ _SIGS = {
     "ainp_colsum": (c_int, [P, c_int64, c_int64, c_int64, P, c_int, P]),
     "ainp_adam": (c_int, [PP, PP, PP, PP, POINTER(c_int64), c_int, c_double, c_double,
                           c_double, c_double, c_double, c_int64, P]),
-    "ainp_conv_gen_stat_parts": (c_int, [c_int64, c_int64, c_int64]),
-    "ainp_conv_gen_workspace": (c_size_t, [c_int64, c_int, c_int, c_int64, c_int64]),
+    "ainp_conv_gen_stat_parts": (c_int, [c_int64, c_int, c_int, c_int, c_int, c_int64, c_int64]),
+    "ainp_conv_weight_kmajor": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "ainp_conv_gen_workspace": (c_size_t, [c_int64, c_int, c_int, c_int, c_int, c_int64, c_int64]),
     "ainp_conv_gen_fwd": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int,
-                                  P, P, P, P, P, P, c_int64, c_int, c_int, c_int, c_int,
+                                  P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_int, c_int, c_float, c_int, c_int, P, P]),
     "ainp_pconv_mask": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int64,
                                 c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P, P]),
@@ -91,6 +92,10 @@ _SIGS = {
     "ainp_col2im": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, P, P]),
     "ainp_leaky_bwd": (c_int, [P, P, c_int64, c_float, P, P]),
     "ainp_mul": (c_int, [P, P, c_int64, P, P]),
+    "ainp_istft_workspace": (c_size_t, [c_int64, c_int64, c_int]),
+    "ainp_istft": (c_int, [P, P, c_int, c_int64, c_int, c_int64, P, c_int, c_int, c_int, P, P,
+                           P]),
+    "ainp_gl_update": (c_int, [P, P, P, c_int64, c_float, c_int, P]),
     "ainp_channel_sum": (c_int, [P, c_int64, c_int, c_int64, P, P]),
 }
 

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import functools
 import math
+import weakref
 from ctypes import c_int as ctypes_int
 
 import numpy as np
@@ -433,6 +434,26 @@ def conv_out_size(n, k, stride, pad):
     return (n + 2 * pad - k) // stride + 1
 
 
+_WT_CACHE: dict = {}
+
+
+def conv_weight_kmajor(w, C0, C1):
+    """k-major copy of a conv weight for ainp_conv_gen_fwd, cached per weight
+    tensor (id + weakref identity check) and invalidated by any in-place
+    update (tensor._version) or reallocation (data_ptr)."""
+    key = (w._version, C0, C1, w.data_ptr())
+    ent = _WT_CACHE.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == key:
+        return ent[2]
+    Cout, Cin, KH, KW = w.shape
+    wt = torch.empty(Cin * KH * KW, Cout, device=w.device, dtype=torch.float32)
+    call("ainp_conv_weight_kmajor", w.data_ptr(), Cout, C0, C1, KH, KW, wt.data_ptr(),
+         _stream(w))
+    wid = id(w)
+    _WT_CACHE[wid] = (weakref.ref(w, lambda _r, wid=wid: _WT_CACHE.pop(wid, None)), key, wt)
+    return wt
+
+
 def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=None, ratio=None,
              scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None):
     """ainp_conv_gen_fwd.  src0/src1 = (x [N,C,Hs,Ws], mask plane [N,Hs,Ws] or None);
@@ -466,17 +487,21 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
             out = torch.empty(N, Cout, Ho, Wo, device=x0.device, dtype=torch.float32)
     stats = None
     if want_stats:
-        parts = _lib.lib.ainp_conv_gen_stat_parts(N, Ho, Wo)
+        parts = _lib.lib.ainp_conv_gen_stat_parts(N, Cin, KH, KW, Cout, Ho, Wo)
         stats = torch.empty(parts, 2, Cout, device=x0.device, dtype=torch.float64)
     for t, nm in ((bias, "bias"), (ratio, "ratio"), (scale, "scale")):
         if t is not None:
             _req(t, nm)
-    ws = None
+    ws = wt = None
     if Cout == 1:
-        nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, Cout, ch or Ho, cw or Wo))
+        nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, ch or Ho, cw or Wo))
+    else:
+        nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, Ho, Wo))
+        wt = conv_weight_kmajor(w, C0, C1)
+    if nb:
         ws = torch.empty(max(1, nb // 4), device=x0.device)
     call("ainp_conv_gen_fwd", x0.data_ptr(), _p(m0), C0, H0, W0, _p(x1), _p(m1), C1, H1, W1,
-         w.data_ptr(), _p(bias), _p(ratio), _p(scale), out.data_ptr(), _p(stats), N, Cout,
+         w.data_ptr(), _p(wt), _p(bias), _p(ratio), _p(scale), out.data_ptr(), _p(stats), N, Cout,
          Hin, Win, KH, KW, stride, pad, act, float(slope), ch, cw, _p(ws), _stream(x0))
     return out, stats
 
@@ -715,3 +740,80 @@ def channel_sum(m):
     out = torch.empty(N, H, W, device=m.device)
     call("ainp_channel_sum", m.data_ptr(), N, C, H * W, out.data_ptr(), _stream(m))
     return out
+
+
+# ============================================================ ISTFT / Griffin-Lim
+IST_C64, IST_C128, IST_MAG_ANGLES, IST_MAG_PHASE = 0, 1, 2, 3
+
+
+def istft(spec=None, *, mag=None, angles=None, phase=None, n_fft=None, hop_length=512,
+          win_length=None, window="hann", center=True):
+    """librosa>=0.10 istft on the GPU (ainp_istft).  Either a complex spectrum
+    spec [..., F, T] (complex64 -> float32, complex128 -> float64), or
+    mag [..., F, T] float32 with unit complex64 `angles` or float32 `phase`.
+    Returns [..., hop*(T-1)] (center) or [..., n_fft + hop*(T-1)]."""
+    if spec is not None:
+        _req(spec, "spec", dtype=None)
+        if spec.dtype not in (torch.complex64, torch.complex128):
+            raise TypeError("spec must be complex64 or complex128")
+        lead, (F, T) = spec.shape[:-2], spec.shape[-2:]
+        mode = IST_C64 if spec.dtype == torch.complex64 else IST_C128
+        in0, in1 = spec.contiguous(), None
+        odt = torch.float32 if mode == IST_C64 else torch.float64
+    else:
+        _req(mag, "mag")
+        lead, (F, T) = mag.shape[:-2], mag.shape[-2:]
+        if angles is not None:
+            _req(angles, "angles", dtype=torch.complex64)
+            mode, in1 = IST_MAG_ANGLES, angles
+        else:
+            _req(phase, "phase")
+            mode, in1 = IST_MAG_PHASE, phase
+        in0 = mag
+        odt = torch.float32
+    n_fft = 2 * (F - 1) if n_fft is None else n_fft
+    win_length = n_fft if win_length is None else win_length
+    nsig = int(np.prod(lead)) if len(lead) else 1
+    dev = in0.device
+    w = _device_window(window, win_length, n_fft, dev)
+    full = n_fft + hop_length * (T - 1)
+    out_len = full - 2 * (n_fft // 2) if center else full
+    out = torch.empty(*lead, out_len, device=dev, dtype=odt)
+    ws = torch.empty(int(_lib.lib.ainp_istft_workspace(nsig, T, n_fft)) // 8, device=dev,
+                     dtype=torch.float64)
+    call("ainp_istft", in0.data_ptr(), _p(in1), mode, nsig, F, T, w.data_ptr(), n_fft,
+         hop_length, int(bool(center)), ws.data_ptr(), out.data_ptr(), _stream(in0))
+    return out
+
+
+def griffinlim(S, n_iter=32, hop_length=None, win_length=None, n_fft=None, window="hann",
+               center=True, momentum=0.99, random_state=None, init_angles=None):
+    """librosa>=0.10 griffinlim (init='random') on the GPU: S [F, T] or [B, F, T]
+    float32 magnitudes.  The initial phases come from
+    np.random.default_rng(random_state).random(S.shape) exactly as librosa draws
+    them (or pass init_angles, complex64).  Each iteration = ainp_istft (S *
+    angles) + ainp_stft + ainp_gl_update."""
+    _req(S, "S")
+    F, T = S.shape[-2:]
+    n_fft = 2 * (F - 1) if n_fft is None else n_fft
+    win_length = n_fft if win_length is None else win_length
+    hop_length = win_length // 4 if hop_length is None else hop_length
+    if momentum > 1:
+        raise ValueError("momentum > 1 is not a stable algorithm (librosa)")
+    if momentum < 0:
+        raise ValueError("momentum must be non-negative")
+    if init_angles is None:
+        rng = np.random.default_rng(seed=random_state)
+        ph = 2 * np.pi * rng.random(size=tuple(S.shape))
+        init_angles = torch.from_numpy((np.cos(ph) + 1j * np.sin(ph)).astype(np.complex64))
+    angles = init_angles.to(S.device, torch.complex64).contiguous().clone()
+    tprev = torch.zeros_like(angles)
+    for it in range(n_iter):
+        inv = istft(mag=S, angles=angles, n_fft=n_fft, hop_length=hop_length,
+                    win_length=win_length, window=window, center=center)
+        rebuilt = stft(inv, n_fft, hop_length, win_length, window, center)
+        call("ainp_gl_update", torch.view_as_real(rebuilt).data_ptr(),
+             torch.view_as_real(tprev).data_ptr(), torch.view_as_real(angles).data_ptr(),
+             angles.numel(), float(momentum), int(it == 0), _stream(S))
+    return istft(mag=S, angles=angles, n_fft=n_fft, hop_length=hop_length,
+                 win_length=win_length, window=window, center=center)

@@ -58,4 +58,8 @@ class Adam(torch.optim.Optimizer):
             for s, (ps, gs, ms, vs) in by_step.items():
                 ops.adam_step(ps, gs, ms, vs, group["lr"], beta1, beta2, group["eps"],
                               group["weight_decay"], s)
+                # the kernel wrote the parameters in place through raw pointers:
+                # record it like any in-place op (autograd checks, weight caches)
+                for p in ps:
+                    torch.autograd.graph.increment_version(p)
         return loss

@@ -35,6 +35,8 @@ struct ConvGenParams {
   const float* scale;       // device scalar multiplier (1/sigma) or null
   float* y;                 // [N][Cout][Ho][Wo]
   double* stats;            // [px_tiles][2][Cout] (sum, sumsq of the stored y) or null
+  float* partial;           // split-K: raw sums [gridDim.z][Cout][N*Ho*Wo], epilogue deferred
+  int ktiles_per_split;     // K tiles per blockIdx.z
   int N, Cin, Cout, Hin, Win, Ho, Wo, KH, KW, stride, pad;
   float slope;              // LeakyReLU negative slope (act == 2)
 };
@@ -52,25 +54,70 @@ __device__ __forceinline__ float apply_act(float v, int act, float slope) {
   return v;
 }
 
-constexpr int CG_BM = 64, CG_BN = 64, CG_BK = 32;
-constexpr int CG_LDA = 34;   // sA[co][k]: == 2 mod 32, conflict-free fragment reads
-constexpr int CG_LDB = 80;   // sB[k][px]: == 16 mod 32
+constexpr int CG_BK = 32;
 
-template <bool FAST>
-__global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, int act) {
-  __shared__ __attribute__((aligned(16))) float sA[CG_BM * CG_LDA];
-  __shared__ __attribute__((aligned(16))) float sB[CG_BK * CG_LDB];
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// v_mfma_f32_32x32x2_f32: lane l holds A[row l&31][k l>>5], B[k l>>5][col l&31];
+// D[row (r&3) + 8(r>>2) + 4(l>>5)][col l&31] in register r.
+__device__ __forceinline__ f32x16 mfma32x32x2(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// K order: source region 0 (k = tap*C0 + ci) then region 1 (k = KK*C0 + tap*C1 + ci).
+// wt[k][co] = w[co][cbase(s) + ci][tap]   (k-major, co contiguous)
+__global__ void conv_weight_kmajor_kernel(const float* w, int Cout, int C0, int C1, int KK,
+                                          float* wt) {
+  const int Cin = C0 + C1;
+  const int64_t total = (int64_t)Cin * KK * Cout;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int co = (int)(t % Cout);
+  const int k = (int)(t / Cout);
+  const int K0 = KK * C0;
+  int tap, c;
+  if (k < K0) {
+    tap = k / C0;
+    c = k - tap * C0;
+  } else {
+    tap = (k - K0) / C1;
+    c = C0 + (k - K0 - tap * C1);
+  }
+  wt[t] = w[((int64_t)co * Cin + c) * KK + tap];
+}
+
+// Implicit-GEMM convolution: block tile BM (co) x BN (pixels) x 32 (k), four
+// waves each owning a 64x64 sub-tile (2x2 v_mfma_f32_32x32x2_f32).  BM=128,
+// BN=128 (waves 2x2) for Cout > 64; BM=64, BN=256 (waves 1x4) otherwise, so
+// narrow layers do not waste half the MFMA work.  The next K tile is gathered
+// into registers while the current one is multiplied (one LDS image each).
+template <int BM>
+__global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, const float* wt,
+                                                              int act) {
+  constexpr int BN = 16384 / BM;
+  constexpr int WN = BN / 64;                 // waves along pixels (2 or 4)
+  constexpr int LDA = BM + 4, LDB = BN + 4;
+  constexpr int AR = CG_BK * BM / 256;        // A elements per thread per tile (16 / 8)
+  constexpr int BR = CG_BK * BN / 256;        // B elements per thread per tile (16 / 32)
+  constexpr int AKS = 256 / BM;               // k-row step of the A staging map
+  constexpr int BKS = 256 / BN;               // k-row step of the B staging map (2 / 1)
+  __shared__ __attribute__((aligned(16))) float sA[CG_BK * LDA];
+  __shared__ __attribute__((aligned(16))) float sB[CG_BK * LDB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int KK = p.KH * p.KW;
-  const int K = p.Cin * KK;
+  const int K0 = KK * p.s0.C;
+  const int K = KK * p.Cin;
   const int HWo = p.Ho * p.Wo;
   const int64_t NP = (int64_t)p.N * HWo;
-  const int64_t px0 = (int64_t)blockIdx.x * CG_BN;
-  const int co0 = blockIdx.y * CG_BM;
-  const int nkt = (K + CG_BK - 1) / CG_BK;
+  const int64_t px0 = (int64_t)blockIdx.x * BN;
+  const int co0 = blockIdx.y * BM;
+  const int kt_begin = blockIdx.z * p.ktiles_per_split;
+  int kt_end = kt_begin + p.ktiles_per_split;
+  const int nkt_all = (K + CG_BK - 1) / CG_BK;
+  if (kt_end > nkt_all) kt_end = nkt_all;
 
-  // B staging: lane = pixel, rows k = wave + 4i
-  const int64_t pix = px0 + lane;
+  // B staging: pixel = tid % BN, k rows = tid / BN + BKS*i (wave-uniform)
+  const int bpx = tid % BN, bk0 = tid / BN;
+  const int64_t pix = px0 + bpx;
   const bool pv = pix < NP;
   int n = 0, by = 0, bx = 0;
   if (pv) {
@@ -80,19 +127,20 @@ __global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, i
     by = oy * p.stride - p.pad;
     bx = ox * p.stride - p.pad;
   }
-  // A staging: lane&31 = k within the tile, rows (tid>>5) + 8i
-  const int akk = tid & 31, arow = tid >> 5;
+  // A staging: co = tid % BM, k rows = tid / BM + AKS*i
+  const int aco = tid % BM, ak0 = tid / BM;
+  const bool acok = co0 + aco < p.Cout;
 
-  float ra[8], rb[8];
-  auto gather1 = [&](int k) -> float {   // one element of X[k][pix] (generic path)
+  float ra[AR], rb[BR];
+  auto gather1 = [&](int k) -> float {        // generic: one element of X[k][pix]
     if (!pv || k >= K) return 0.f;
-    const int tap = k / p.Cin, ci = k - tap * p.Cin;
+    const bool first = k < K0;
+    const ConvSrcDev& s = first ? p.s0 : p.s1;
+    const int kr = first ? k : k - K0;
+    const int tap = kr / s.C, cs = kr - tap * s.C;
     const int ky = tap / p.KW, kx = tap - ky * p.KW;
     const int iy = by + ky, ix = bx + kx;
     if (iy < 0 || iy >= p.Hin || ix < 0 || ix >= p.Win) return 0.f;
-    const bool first = ci < p.s0.C;
-    const ConvSrcDev& s = first ? p.s0 : p.s1;
-    const int cs = first ? ci : ci - p.s0.C;
     const int sy = src_coord(iy, s.Hs, p.Hin, s.up), sx = src_coord(ix, s.Ws, p.Win, s.up);
     const int64_t plane = (int64_t)s.Hs * s.Ws;
     const int64_t off = (int64_t)sy * s.Ws + sx;
@@ -102,139 +150,186 @@ __global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, i
   };
   auto fetch = [&](int kt) {
     const int k0 = kt * CG_BK;
-    {
-      const int k = k0 + akk;
-      int aoff = 0;
-      const bool kok = k < K;
-      if (kok) {
-        const int tap = k / p.Cin, ci = k - tap * p.Cin;
-        aoff = ci * KK + tap;
-      }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int co = co0 + arow + 8 * i;
-        ra[i] = (kok && co < p.Cout) ? p.w[(int64_t)co * K + aoff] : 0.f;
-      }
+    for (int i = 0; i < AR; ++i) {
+      const int k = k0 + ak0 + AKS * i;
+      ra[i] = (acok && k < K) ? wt[(int64_t)k * p.Cout + co0 + aco] : 0.f;
     }
-    if (FAST) {
-      // the whole tile shares one tap and one source; ci = ci0 + wave + 4i
-      const int tap = k0 / p.Cin, ci0 = k0 - tap * p.Cin;
+    // a tile lies in one region; in a region with C % 32 == 0 it has one tap
+    const bool first = k0 < K0;
+    const ConvSrcDev& s = first ? p.s0 : p.s1;
+    if (s.C % CG_BK == 0) {
+      const int kr = first ? k0 : k0 - K0;
+      const int tap = kr / s.C, ci0 = kr - tap * s.C;
       const int ky = tap / p.KW, kx = tap - ky * p.KW;
       const int iy = by + ky, ix = bx + kx;
-      const bool inb = pv && k0 < K && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-      const bool first = ci0 < p.s0.C;
-      const ConvSrcDev& s = first ? p.s0 : p.s1;
-      const int cs = (first ? ci0 : ci0 - p.s0.C) + wave;
+      const bool inb = pv && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
       const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
       const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
       const int64_t plane = (int64_t)s.Hs * s.Ws;
       const int64_t off = (int64_t)sy * s.Ws + sx;
       const float mv = (inb && s.m) ? s.m[(int64_t)n * plane + off] : 1.f;
-      const float* base = s.x + ((int64_t)n * s.C + cs) * plane + off;
+      const float* base = s.x + ((int64_t)n * s.C + ci0 + bk0) * plane + off;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) rb[i] = inb ? base[(int64_t)(4 * i) * plane] * mv : 0.f;
+      for (int i = 0; i < BR; ++i) rb[i] = inb ? base[(int64_t)(BKS * i) * plane] * mv : 0.f;
     } else {
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        rb[i] = gather1(__builtin_amdgcn_readfirstlane(k0 + wave + 4 * i));
+      for (int i = 0; i < BR; ++i)
+        rb[i] = gather1(__builtin_amdgcn_readfirstlane(k0 + bk0 + BKS * i));
     }
   };
   auto commit = [&]() {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sA[(arow + 8 * i) * CG_LDA + akk] = ra[i];
+    for (int i = 0; i < AR; ++i) sA[(ak0 + AKS * i) * LDA + aco] = ra[i];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sB[(wave + 4 * i) * CG_LDB + lane] = rb[i];
+    for (int i = 0; i < BR; ++i) sB[(bk0 + BKS * i) * LDB + bpx] = rb[i];
   };
 
-  const int wm = wave >> 1, wn = wave & 1;
-  const int li = lane & 15, kq = lane >> 4;
-  f32x4 acc[2][2];
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, lh = lane >> 5;
+  f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  fetch(0);
-  for (int kt = 0; kt < nkt; ++kt) {
+  if (kt_begin < kt_end) fetch(kt_begin);
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
     commit();
     __syncthreads();
-    if (kt + 1 < nkt) fetch(kt + 1);
-    const float* pa = sA + (wm * 32 + li) * CG_LDA + kq;
-    const float* pb = sB + kq * CG_LDB + wn * 32 + li;
+    if (kt + 1 < kt_end) fetch(kt + 1);
+    const float* pa = sA + lh * LDA + wm * 64 + l31;
+    const float* pb = sB + lh * LDB + wn * 64 + l31;
 #pragma unroll
-    for (int s = 0; s < CG_BK / 4; ++s) {
-      const float a0 = pa[4 * s], a1 = pa[16 * CG_LDA + 4 * s];
-      const float b0 = pb[4 * s * CG_LDB], b1 = pb[4 * s * CG_LDB + 16];
-      acc[0][0] = mfma16x16x4(a0, b0, acc[0][0]);
-      acc[0][1] = mfma16x16x4(a0, b1, acc[0][1]);
-      acc[1][0] = mfma16x16x4(a1, b0, acc[1][0]);
-      acc[1][1] = mfma16x16x4(a1, b1, acc[1][1]);
+    for (int s = 0; s < CG_BK / 2; ++s) {
+      const float a0 = pa[2 * s * LDA], a1 = pa[2 * s * LDA + 32];
+      const float b0 = pb[2 * s * LDB], b1 = pb[2 * s * LDB + 32];
+      acc[0][0] = mfma32x32x2(a0, b0, acc[0][0]);
+      acc[0][1] = mfma32x32x2(a0, b1, acc[0][1]);
+      acc[1][0] = mfma32x32x2(a1, b0, acc[1][0]);
+      acc[1][1] = mfma32x32x2(a1, b1, acc[1][1]);
     }
     __syncthreads();
   }
 
+  if (p.partial) {   // split-K: raw partial sums, the epilogue kernel finishes
+    float* pb = p.partial + (int64_t)blockIdx.z * p.Cout * NP;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t pg = px0 + wn * 64 + 32 * j + l31;
+      if (pg >= NP) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = co0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (co < p.Cout) pb[(int64_t)co * NP + pg] = acc[i][j][r];
+        }
+    }
+    return;
+  }
   // ---------------- epilogue
   const float sc = p.scale ? *p.scale : 1.f;
-  double ssum[2][4], ssq[2][4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ssum[i][r] = ssq[i][r] = 0.0;
+  bool ok[2];
+  float rt[2];
+  float* yb[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int64_t pg = px0 + wn * 32 + 16 * j + li;
-    const bool ok = pg < NP;
+    const int64_t pg = px0 + wn * 64 + 32 * j + l31;
+    ok[j] = pg < NP;
     int pn = 0, prem = 0;
-    if (ok) {
+    if (ok[j]) {
       pn = (int)(pg / HWo);
       prem = (int)(pg - (int64_t)pn * HWo);
     }
-    const float rt = (ok && p.ratio) ? p.ratio[pg] : 1.f;
+    rt[j] = (ok[j] && p.ratio) ? p.ratio[pg] : 1.f;
+    yb[j] = p.y + (int64_t)pn * p.Cout * HWo + prem;
+  }
+  double* red = reinterpret_cast<double*>(sA);     // [WN][BM][2] doubles (fits in sA)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < 2; ++i) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int co = co0 + wm * 32 + 16 * i + kq * 4 + r;
-        if (!ok || co >= p.Cout) continue;
+    for (int r = 0; r < 16; ++r) {
+      const int cl = wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int co = co0 + cl;
+      const bool cok = co < p.Cout;
+      const float bv = (cok && p.bias) ? p.bias[co] : 0.f;
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (!ok[j] || !cok) continue;
         float v = acc[i][j][r] * sc;
-        v *= rt;
-        if (p.bias) v += p.bias[co];
-        if (p.stats) {
-          ssum[i][r] += (double)v;
-          ssq[i][r] += (double)v * (double)v;
+        v *= rt[j];
+        v += bv;
+        a += (double)v;
+        b += (double)v * (double)v;
+        yb[j][(int64_t)co * HWo] = apply_act(v, act, p.slope);
+      }
+      if (p.stats) {
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
         }
-        p.y[((int64_t)pn * p.Cout + co) * HWo + prem] = apply_act(v, act, p.slope);
+        if (l31 == 0) {
+          red[(wn * BM + cl) * 2 + 0] = a;
+          red[(wn * BM + cl) * 2 + 1] = b;
+        }
       }
     }
   }
   if (p.stats) {
-    // reduce over the 16 pixel lanes, then over the two wn waves (LDS)
-    double* red = reinterpret_cast<double*>(sA);   // [2 wn][64 co][2]
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        double a = ssum[i][r], b = ssq[i][r];
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-        }
-        if (li == 0) {
-          const int cl = wm * 32 + 16 * i + kq * 4 + r;
-          red[(wn * 64 + cl) * 2 + 0] = a;
-          red[(wn * 64 + cl) * 2 + 1] = b;
-        }
-      }
     __syncthreads();
-    if (tid < 64) {
+    if (tid < BM) {
       const int co = co0 + tid;
       if (co < p.Cout) {
-        const double a = red[(0 * 64 + tid) * 2] + red[(1 * 64 + tid) * 2];
-        const double b = red[(0 * 64 + tid) * 2 + 1] + red[(1 * 64 + tid) * 2 + 1];
+        double a = 0.0, b = 0.0;
+        for (int q = 0; q < WN; ++q) {
+          a += red[(q * BM + tid) * 2];
+          b += red[(q * BM + tid) * 2 + 1];
+        }
         p.stats[((int64_t)blockIdx.x * 2 + 0) * p.Cout + co] = a;
         p.stats[((int64_t)blockIdx.x * 2 + 1) * p.Cout + co] = b;
       }
+    }
+  }
+}
+
+// Split-K epilogue: y[n][co][p] = act(sum_z partial[z][co][px] * scale * ratio + bias),
+// one block = 256 pixels of one channel; stats per (pixel block, channel).
+__global__ __launch_bounds__(256) void conv_gen_splitk_epilogue(ConvGenParams p, int nsplit,
+                                                                int act) {
+  const int co = blockIdx.y;
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double a = 0.0, b = 0.0;
+  if (px < NP) {
+    float v = 0.f;
+    for (int z = 0; z < nsplit; ++z) v += p.partial[((int64_t)z * p.Cout + co) * NP + px];
+    v *= p.scale ? *p.scale : 1.f;
+    if (p.ratio) v *= p.ratio[px];
+    if (p.bias) v += p.bias[co];
+    a = v;
+    b = (double)v * (double)v;
+    const int n = (int)(px / HWo);
+    const int r = (int)(px - (int64_t)n * HWo);
+    p.y[((int64_t)n * p.Cout + co) * HWo + r] = apply_act(v, act, p.slope);
+  }
+  if (p.stats) {
+    __shared__ double red[2][4];
+    a = wave_sum_d(a);
+    b = wave_sum_d(b);
+    if ((threadIdx.x & 63) == 0) {
+      red[0][threadIdx.x >> 6] = a;
+      red[1][threadIdx.x >> 6] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      p.stats[((int64_t)blockIdx.x * 2 + 0) * p.Cout + co] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      p.stats[((int64_t)blockIdx.x * 2 + 1) * p.Cout + co] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
     }
   }
 }
@@ -746,19 +841,53 @@ static ConvSrcDev make_src(const float* x, const float* m, int C, int Hs, int Ws
   return s;
 }
 
-extern "C" int ainp_conv_gen_stat_parts(int64_t N, int64_t Ho, int64_t Wo) {
-  return (int)cdiv(N * Ho * Wo, CG_BN);
+static int conv_gen_bm(int Cout) { return Cout > 64 ? 128 : 64; }
+
+// K splits for a launch: small tile grids with long K (the U-Net bottleneck,
+// VGG's last blocks) are split so ~768 workgroups run; >= 8 K tiles per split.
+static int conv_gen_nsplit(int64_t NP, int Cout, int K) {
+  if (Cout == 1) return 1;
+  const int BM = conv_gen_bm(Cout);
+  const int64_t blocks = cdiv(NP, 16384 / BM) * cdiv(Cout, BM);
+  const int nkt = (int)cdiv(K, CG_BK);
+  if (blocks >= 384 || nkt < 16) return 1;
+  int64_t s = cdiv(768, blocks);
+  if (s > nkt / 8) s = nkt / 8;
+  if (s < 1) s = 1;
+  const int per = (int)cdiv(nkt, s);
+  return (int)cdiv(nkt, per);   // no empty split
 }
 
-extern "C" size_t ainp_conv_gen_workspace(int64_t N, int Cin, int Cout, int64_t Ho, int64_t Wo) {
-  if (Cout != 1) return 0;
-  return (size_t)cdiv(Cin, C1_CC) * N * Ho * Wo * sizeof(float);
+extern "C" int ainp_conv_gen_stat_parts(int64_t N, int Cin, int KH, int KW, int Cout, int64_t Ho,
+                                        int64_t Wo) {
+  const int64_t NP = N * Ho * Wo;
+  if (conv_gen_nsplit(NP, Cout, Cin * KH * KW) > 1) return (int)cdiv(NP, 256);
+  return (int)cdiv(NP, 16384 / conv_gen_bm(Cout));
+}
+
+extern "C" int ainp_conv_weight_kmajor(const float* w, int Cout, int C0, int C1, int KH, int KW,
+                                       float* wt, void* stream) {
+  if (!w || !wt || Cout < 1 || C0 < 1 || C1 < 0 || KH < 1 || KW < 1)
+    return record_msg("ainp_conv_weight_kmajor: bad argument");
+  const int64_t total = (int64_t)(C0 + C1) * KH * KW * Cout;
+  hipLaunchKernelGGL(conv_weight_kmajor_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     as_stream(stream), w, Cout, C0, C1, KH * KW, wt);
+  return check_launch("conv_weight_kmajor");
+}
+
+extern "C" size_t ainp_conv_gen_workspace(int64_t N, int Cin, int KH, int KW, int Cout,
+                                          int64_t Ho, int64_t Wo) {
+  if (Cout == 1) return (size_t)cdiv(Cin, C1_CC) * N * Ho * Wo * sizeof(float);
+  const int64_t NP = N * Ho * Wo;
+  const int ns = conv_gen_nsplit(NP, Cout, Cin * KH * KW);
+  return ns > 1 ? (size_t)ns * Cout * NP * sizeof(float) : 0;
 }
 
 extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H0, int W0,
                                  const float* x1, const float* m1, int C1, int H1, int W1,
-                                 const float* w, const float* bias, const float* ratio,
-                                 const float* scale, float* y, double* stats, int64_t N,
+                                 const float* w, const float* wt, const float* bias,
+                                 const float* ratio, const float* scale, float* y, double* stats,
+                                 int64_t N,
                                  int Cout, int Hin, int Win, int KH, int KW, int stride,
                                  int pad, int act, float slope, int crop_h, int crop_w,
                                  void* workspace, void* stream) {
@@ -779,6 +908,8 @@ extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H
   p.scale = scale;
   p.y = y;
   p.stats = stats;
+  p.partial = nullptr;
+  p.ktiles_per_split = 1 << 30;
   p.N = (int)N;
   p.Cin = C0 + C1;
   p.Cout = Cout;
@@ -806,14 +937,27 @@ extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H
     return check_launch("conv_cout1");
   }
   if (crop_h > 0 || crop_w > 0) return record_msg("ainp_conv_gen_fwd: crop needs Cout=1");
-  const int64_t tiles = cdiv(N * (int64_t)Ho * Wo, CG_BN);
-  dim3 grid((unsigned)tiles, (unsigned)cdiv(Cout, CG_BM));
-  const bool fast = (p.Cin % CG_BK == 0) && (C0 % CG_BK == 0);
-  if (fast)
-    hipLaunchKernelGGL(conv_gen_fwd_kernel<true>, grid, dim3(256), 0, s, p, act);
+  if (!wt) return record_msg("ainp_conv_gen_fwd: k-major weights (ainp_conv_weight_kmajor) required");
+  const int BM = conv_gen_bm(Cout);
+  const int64_t NP = N * (int64_t)Ho * Wo;
+  const int K = p.Cin * KH * KW;
+  const int nsplit = conv_gen_nsplit(NP, Cout, K);
+  if (nsplit > 1) {
+    if (!workspace) return record_msg("ainp_conv_gen_fwd: split-K needs ainp_conv_gen_workspace");
+    p.partial = reinterpret_cast<float*>(workspace);
+    p.ktiles_per_split = (int)cdiv(cdiv(K, CG_BK), nsplit);
+  }
+  const int64_t tiles = cdiv(NP, 16384 / BM);
+  dim3 grid((unsigned)tiles, (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
+  if (BM == 128)
+    hipLaunchKernelGGL(conv_gen_fwd_kernel<128>, grid, dim3(256), 0, s, p, wt, act);
   else
-    hipLaunchKernelGGL(conv_gen_fwd_kernel<false>, grid, dim3(256), 0, s, p, act);
-  return check_launch("conv_gen_fwd");
+    hipLaunchKernelGGL(conv_gen_fwd_kernel<64>, grid, dim3(256), 0, s, p, wt, act);
+  int rc = check_launch("conv_gen_fwd");
+  if (rc || nsplit == 1) return rc;
+  hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), Cout), dim3(256), 0,
+                     s, p, nsplit, act);
+  return check_launch("conv_gen_splitk_epilogue");
 }
 
 extern "C" int ainp_pconv_mask(const float* m0, int C0, int H0, int W0, const float* m1, int C1,

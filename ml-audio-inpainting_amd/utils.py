@@ -11,8 +11,8 @@ Same names, signatures, return types and error behaviour as
   add_random_gap        utils.py:146-188 (host numpy, float64 result)
   extract_spectrogram   utils.py:192-234 (GPU, returns the complex STFT; power is
                                           validated then ignored)
-Functions the training hot path never calls (mel, Griffin-Lim/ISTFT,
-plotting) are listed in DESIGN.md: ISTFT/Griffin-Lim is SURVEY §8 f1 (next).
+  spectrogram_to_audio  utils.py:279-333  (GPU ISTFT / Griffin-Lim)
+Mel spectrograms and plotting are outside the hot path.
 """
 from __future__ import annotations
 
@@ -200,10 +200,45 @@ def extract_spectrogram(audio_data, n_fft: int = 2048, hop_length: int = 512,
     return ops.stft(t, n_fft, hop_length, win_length, window, center).cpu().numpy()
 
 
-def spectrogram_to_audio(*args, **kwargs):
-    """utils.py:279-333 (ISTFT / Griffin-Lim): SURVEY §8 f1, not on the
-    training path; scheduled for the next round."""
-    raise NotImplementedError("spectrogram_to_audio (ISTFT/Griffin-Lim) is SURVEY §8 f1 (next)")
+def db_to_amplitude(S_db, ref: float = 1.0):
+    """librosa.db_to_amplitude: ref * 10**(0.05 * S_db) (host numpy, as the reference)."""
+    return ref * np.power(10.0, 0.05 * np.asarray(S_db))
+
+
+def spectrogram_to_audio(spectrogram, phase=None, phase_info: bool = False, n_fft=512,
+                         n_iter=64, window="hann", hop_length=512, win_length=None,
+                         center=True, random_state=None):
+    """utils.py:279-333 on the GPU kernels (ainp_istft / ainp_stft / ainp_gl_update):
+    a dB-scaled input (max < 0 and mean < 0) is converted back to amplitude;
+    phase_info: the input is a complex spectrogram -> istft; phase given ->
+    istft(S * exp(i phase)); otherwise Griffin-Lim (n_iter, momentum 0.99,
+    random initial phases; random_state seeds them as in librosa).
+    numpy in -> numpy out (as the reference); torch cuda tensors stay on the GPU."""
+    import torch
+    from ainp import ops
+    as_numpy = not isinstance(spectrogram, torch.Tensor)
+    S = spectrogram
+    if as_numpy:
+        S = np.asarray(S)
+        if not np.iscomplexobj(S) and np.max(S) < 0 and np.mean(S) < 0:
+            S = db_to_amplitude(S)
+        S = torch.from_numpy(np.ascontiguousarray(S)).cuda()
+    elif not S.is_complex() and bool((S.max() < 0) & (S.mean() < 0)):
+        S = torch.from_numpy(db_to_amplitude(S.cpu().numpy())).to(S.device)
+    kw = dict(n_fft=n_fft, hop_length=hop_length, win_length=win_length, window=window,
+              center=center)
+    if phase_info:
+        if not S.is_complex():
+            S = S.to(torch.complex64)
+        y = ops.istft(S.contiguous(), **kw)
+    elif phase is not None:
+        ph = torch.as_tensor(np.asarray(phase) if as_numpy else phase).to(S.device, torch.float32)
+        y = ops.istft(mag=S.to(torch.float32).contiguous(), phase=ph.contiguous(), **kw)
+    else:
+        y = ops.griffinlim(S.to(torch.float32).contiguous(), n_iter=n_iter,
+                           hop_length=hop_length, win_length=win_length, n_fft=n_fft,
+                           window=window, center=center, random_state=random_state)
+    return y.cpu().numpy() if as_numpy else y
 
 
 def extract_mel_spectrogram(*args, **kwargs):

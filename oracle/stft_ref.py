@@ -114,3 +114,78 @@ def gan_item(audio_f32: np.ndarray, gap_start: int, gap_len_samples: int,
         mask[:, fs:fe] = 0
     return (orig.astype(np.float32), impm.astype(np.float32),
             phase.astype(np.float32), mask)
+
+
+# ------------------------------------------------------------- ISTFT / Griffin-Lim
+def window_sumsquare(window: str, n_frames: int, hop: int, win_length: int, n_fft: int):
+    """librosa.filters.window_sumsquare (norm=None): sum of the squared,
+    centre-padded window shifted by hop, length n_fft + hop*(n_frames-1)."""
+    w2 = padded_window(window, win_length, n_fft) ** 2
+    n = n_fft + hop * (n_frames - 1)
+    x = np.zeros(n, dtype=np.float64)
+    for i in range(n_frames):
+        s = i * hop
+        x[s:min(n, s + n_fft)] += w2[:max(0, min(n_fft, n - s))]
+    return x
+
+
+def istft(X: np.ndarray, hop_length: int, win_length=None, n_fft=None,
+          window: str = "hann", center: bool = True, length=None) -> np.ndarray:
+    """librosa>=0.10 istft restated in float64 (utils.py:317-326 call sites):
+    irfft per frame (imaginary DC/Nyquist ignored), synthesis window,
+    overlap-add, division by the window sum-square where it exceeds tiny,
+    n_fft/2 trimmed per side when center.  X [F, T] or [B, F, T]."""
+    X = np.asarray(X)
+    if X.ndim == 3:
+        return np.stack([istft(x, hop_length, win_length, n_fft, window, center, length)
+                         for x in X])
+    F, T = X.shape
+    n_fft = 2 * (F - 1) if n_fft is None else n_fft
+    win_length = n_fft if win_length is None else win_length
+    w = padded_window(window, win_length, n_fft)
+    frames = np.fft.irfft(X.astype(np.complex128), n=n_fft, axis=0) * w[:, None]
+    n = n_fft + hop_length * (T - 1)
+    y = np.zeros(n, dtype=np.float64)
+    for t in range(T):
+        y[t * hop_length:t * hop_length + n_fft] += frames[:, t]
+    wss = window_sumsquare(window, T, hop_length, win_length, n_fft)
+    tiny = np.finfo(np.float32 if X.dtype == np.complex64 else np.float64).tiny
+    nz = wss > tiny
+    y[nz] /= wss[nz]
+    if center:
+        y = y[n_fft // 2:n - n_fft // 2]
+    if length is not None:
+        y = y[:length] if len(y) >= length else np.pad(y, (0, length - len(y)))
+    return y
+
+
+def griffinlim(S: np.ndarray, n_iter: int = 32, hop_length=None, win_length=None, n_fft=None,
+               window: str = "hann", center: bool = True, momentum: float = 0.99,
+               random_state=None, init_angles=None) -> np.ndarray:
+    """librosa>=0.10 griffinlim (init='random', pad_mode='constant') restated:
+    angles = exp(2 pi i U) from np.random.default_rng(random_state); per
+    iteration inverse = istft(S*angles), rebuilt = stft(inverse),
+    angles = rebuilt - m/(1+m) * previous rebuilt (from the 2nd iteration),
+    angles /= |angles| + tiny; returns istft(S*angles).  float64 throughout."""
+    S = np.asarray(S, dtype=np.float64)
+    F, T = S.shape
+    n_fft = 2 * (F - 1) if n_fft is None else n_fft
+    win_length = n_fft if win_length is None else win_length
+    hop_length = win_length // 4 if hop_length is None else hop_length
+    if init_angles is None:
+        rng = np.random.default_rng(seed=random_state)
+        ph = 2 * np.pi * rng.random(size=S.shape)
+        angles = np.cos(ph) + 1j * np.sin(ph)
+    else:
+        angles = np.asarray(init_angles, dtype=np.complex128)
+    eps = np.finfo(np.float64).tiny
+    rebuilt = None
+    for _ in range(n_iter):
+        tprev = rebuilt
+        inv = istft(S * angles, hop_length, win_length, n_fft, window, center)
+        rebuilt = stft(inv, n_fft, hop_length, win_length, window)
+        angles = rebuilt.copy()
+        if tprev is not None:
+            angles -= (momentum / (1 + momentum)) * tprev
+        angles /= np.abs(angles) + eps
+    return istft(S * angles, hop_length, win_length, n_fft, window, center)

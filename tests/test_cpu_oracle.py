@@ -153,3 +153,28 @@ def test_state_dict_keys_match_reference_layout(golden_dir):
     keys = set(StackedBLSTMCNN(config=cfg).state_dict())
     ref_keys = {k[5:] for k in g.files if k.startswith("init/")}
     assert keys == ref_keys
+
+
+def test_oracle_istft_inverts_stft():
+    """tests/utils_test.py:780-849 property: ISTFT(STFT(x)) == x (to 1e-10), for
+    the configurations the reference uses (CNNBLSTM 512/192/384, GAN 512/128/512,
+    extract_spectrogram defaults 2048/512)."""
+    rng = np.random.default_rng(5)
+    for n_fft, hop, win, L in [(512, 192, 384, 9000), (512, 128, 512, 8000), (2048, 512, 2048, 22050)]:
+        x = rng.standard_normal(L)
+        y = stft_ref.istft(stft_ref.stft(x, n_fft, hop, win), hop, win, n_fft)
+        assert len(y) == hop * (1 + L // hop - 1)
+        assert np.abs(y - x[:len(y)]).max() < 1e-10
+
+
+def test_oracle_griffinlim_converges_toward_magnitude():
+    """Griffin-Lim restatement: consistent spectrogram error decreases with
+    iterations (librosa's own test idea, tests/utils_test.py:851-905)."""
+    from ainp.synth import synthetic_clip
+    x = synthetic_clip(3, 8000).astype(np.float64)
+    S = np.abs(stft_ref.stft(x, 512, 128, 512))
+    errs = []
+    for it in (1, 8):
+        y = stft_ref.griffinlim(S, it, 128, 512, 512, random_state=0)
+        errs.append(np.linalg.norm(np.abs(stft_ref.stft(y, 512, 128, 512)) - S) / np.linalg.norm(S))
+    assert errs[1] < errs[0]

@@ -41,6 +41,8 @@ CONV_CASES = [
     (2, 1, 0, 30, 50, False, 16, 4, 2, 1, False, True, False, True, 2),       # D layer 1
     (1, 128, 0, 13, 21, False, 70, 5, 2, 2, True, False, True, False, 0),     # k5 s2, Cout%64
     (2, 64, 0, 12, 14, False, 32, 3, 1, 1, False, True, False, False, 1),     # VGG-like
+    (2, 512, 512, 6, 10, True, 512, 3, 1, 1, True, False, True, False, 0),    # U-Net bottleneck: split-K
+    (3, 256, 0, 7, 9, False, 64, 3, 2, 1, True, True, True, False, 2),        # BM=64, split-K
 ]
 
 

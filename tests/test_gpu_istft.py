@@ -1,0 +1,94 @@
+"""GPU parity of ISTFT / Griffin-Lim (utils.spectrogram_to_audio)
+against the float64 oracle (oracle/stft_ref.py istft / griffinlim, pinned by
+the ISTFT(STFT(x)) = x property in test_cpu_oracle.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import stft_ref
+from ainp import synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _spec(n_fft, hop, win, L, seed=0, dtype=np.float32):
+    x = synth.synthetic_clip(seed, L).astype(dtype)
+    return x, stft_ref.stft(x, n_fft, hop, win)
+
+
+@pytest.mark.parametrize("n_fft,hop,win", [(512, 192, 384), (512, 128, 512), (2048, 512, 2048)])
+def test_istft_modes_match_oracle(n_fft, hop, win):
+    from ainp import ops
+    _, X = _spec(n_fft, hop, win, 12000, seed=n_fft + hop)
+    rng = np.random.default_rng(1)
+    X = X * (1 + 0.1 * rng.standard_normal(X.shape))      # not a consistent spectrogram
+    ref = stft_ref.istft(X, hop, win, n_fft)
+    # complex128 -> float64
+    y = ops.istft(torch.from_numpy(X).cuda(), n_fft=n_fft, hop_length=hop, win_length=win)
+    assert y.dtype == torch.float64
+    assert np.abs(y.cpu().numpy() - ref).max() <= 1e-12 * np.abs(ref).max()
+    # complex64 -> float32
+    X64 = X.astype(np.complex64)
+    ref64 = stft_ref.istft(X64.astype(np.complex128), hop, win, n_fft)
+    y = ops.istft(torch.from_numpy(X64).cuda(), n_fft=n_fft, hop_length=hop, win_length=win)
+    assert y.dtype == torch.float32
+    assert np.abs(y.cpu().numpy() - ref64).max() <= 1e-6 * np.abs(ref64).max()
+    # magnitude * exp(i phase)
+    mag = np.abs(X).astype(np.float32)
+    ph = np.angle(X).astype(np.float32)
+    refp = stft_ref.istft(mag.astype(np.float64) * np.exp(1j * ph.astype(np.float64)), hop, win, n_fft)
+    y = ops.istft(mag=torch.from_numpy(mag).cuda(), phase=torch.from_numpy(ph).cuda(),
+                  n_fft=n_fft, hop_length=hop, win_length=win)
+    assert np.abs(y.cpu().numpy() - refp).max() <= 1e-6 * np.abs(refp).max()
+    # batched magnitude * unit angles
+    ang = np.exp(1j * ph).astype(np.complex64)
+    mb = np.stack([mag, 0.5 * mag])
+    ab = np.stack([ang, ang])
+    y = ops.istft(mag=torch.from_numpy(mb).cuda(), angles=torch.from_numpy(ab).cuda(),
+                  n_fft=n_fft, hop_length=hop, win_length=win)
+    for b in range(2):
+        rb = stft_ref.istft((mb[b] * ab[b]).astype(np.complex128), hop, win, n_fft)
+        assert np.abs(y[b].cpu().numpy() - rb).max() <= 1e-6 * np.abs(rb).max()
+
+
+def test_gpu_stft_istft_round_trip():
+    from ainp import ops
+    x = torch.from_numpy(synth.synthetic_clip(9, 80000)).cuda()
+    X = ops.stft(x, 512, 128, 512)
+    y = ops.istft(X, n_fft=512, hop_length=128, win_length=512)
+    assert y.shape[-1] == 128 * (X.shape[-1] - 1)
+    err = (y - x[:y.shape[-1]]).abs().max().item()
+    assert err < 1e-6 * x.abs().max().item() + 1e-7
+
+
+def test_griffinlim_matches_oracle():
+    from ainp import ops
+    x = synth.synthetic_clip(11, 8000).astype(np.float64)
+    S = np.abs(stft_ref.stft(x, 512, 128, 512)).astype(np.float32)
+    for n_iter in (0, 1, 4):
+        y = ops.griffinlim(torch.from_numpy(S).cuda(), n_iter=n_iter, hop_length=128,
+                           win_length=512, n_fft=512, random_state=3)
+        ref = stft_ref.griffinlim(S.astype(np.float64), n_iter, 128, 512, 512, random_state=3)
+        rel = np.linalg.norm(y.cpu().numpy() - ref) / np.linalg.norm(ref)
+        assert rel < 1e-4, (n_iter, rel)
+
+
+def test_spectrogram_to_audio_paths():
+    import utils
+    x = synth.synthetic_clip(13, 8000)
+    X = stft_ref.stft(x.astype(np.float64), 512, 128, 512).astype(np.complex64)
+    mag, ph = np.abs(X), np.angle(X).astype(np.float32)
+    y = utils.spectrogram_to_audio(mag, ph, n_fft=512, hop_length=128, win_length=512)
+    assert isinstance(y, np.ndarray) and y.dtype == np.float32
+    assert np.abs(y - x[:len(y)]).max() < 1e-5
+    y2 = utils.spectrogram_to_audio(X, phase_info=True, n_fft=512, hop_length=128)
+    assert np.abs(y2 - x[:len(y2)]).max() < 1e-5
+    # dB input (max < 0, mean < 0) is converted back to amplitude first
+    Sdb = 20 * np.log10(np.maximum(mag, 1e-6) / (mag.max() * 1.01))
+    y3 = utils.spectrogram_to_audio(Sdb.astype(np.float32), ph, n_fft=512, hop_length=128)
+    ref3 = stft_ref.istft(10 ** (0.05 * Sdb.astype(np.float64)) * np.exp(1j * ph), 128, 512, 512)
+    assert np.abs(y3 - ref3).max() < 1e-5 * np.abs(ref3).max()
+    # Griffin-Lim path, seeded as librosa(random_state=...)
+    y4 = utils.spectrogram_to_audio(mag, n_fft=512, hop_length=128, n_iter=2, random_state=0)
+    ref4 = stft_ref.griffinlim(mag.astype(np.float64), 2, 128, 512, 512, random_state=0)
+    assert np.linalg.norm(y4 - ref4) / np.linalg.norm(ref4) < 1e-4
