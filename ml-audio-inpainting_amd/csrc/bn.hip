@@ -270,6 +270,109 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(
   }
 }
 
+
+// ---------------------------------------------------------- flat NCHW path
+// g and y both NCHW: a block owns BN_CHUNK contiguous elements of one (n, c)
+// plane -- float2 loads/stores straight from HBM, no LDS staging.  The
+// partial layout [n][c][chunk] is what bn_bwd_sum_kernel reduces.
+constexpr int BN_CHUNK = 4096;
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_relu_bwd_reduce_flat(
+    const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ save, double* __restrict__ partial,
+    int C, int64_t HW, int chunks) {
+  __shared__ double red[2][4];
+  const int64_t plane = blockIdx.x / chunks;
+  const int ch = blockIdx.x % chunks;
+  const int c = (int)(plane % C);
+  const int64_t o0 = (int64_t)ch * BN_CHUNK;
+  const int len = (int)((HW - o0) < BN_CHUNK ? (HW - o0) : BN_CHUNK);
+  const float* gp = g + plane * HW + o0;
+  const float* yp = y + plane * HW + o0;
+  const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
+  float s1 = 0.f, s2 = 0.f;
+  if (VEC) {
+    const float2* g2 = reinterpret_cast<const float2*>(gp);
+    const float2* y2 = reinterpret_cast<const float2*>(yp);
+#pragma unroll
+    for (int i = 0; i < BN_CHUNK / 512; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (2 * e < len) {
+        const float2 gv = g2[e], yv = y2[e];
+        const float gz0 = fmaf(yv.x, sc, sh) > 0.f ? gv.x : 0.f;
+        const float gz1 = fmaf(yv.y, sc, sh) > 0.f ? gv.y : 0.f;
+        s1 += gz0 + gz1;
+        s2 += gz0 * ((yv.x - mean) * rstd) + gz1 * ((yv.y - mean) * rstd);
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < len; e += 256) {
+      const float yv = yp[e];
+      const float gz = fmaf(yv, sc, sh) > 0.f ? gp[e] : 0.f;
+      s1 += gz;
+      s2 += gz * ((yv - mean) * rstd);
+    }
+  }
+  const double d1 = wave_sum_d((double)s1), d2 = wave_sum_d((double)s2);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = d1;
+    red[1][threadIdx.x >> 6] = d2;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    partial[(int64_t)blockIdx.x * 2 + 0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    partial[(int64_t)blockIdx.x * 2 + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+  }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
+    const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ gamma,
+    const float* __restrict__ save, const double* __restrict__ sums, float* __restrict__ gy,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int C, int64_t HW, int chunks,
+    double inv_count) {
+  if (blockIdx.x < (unsigned)C && threadIdx.x == 0) {
+    if (dbeta) dbeta[blockIdx.x] = (float)sums[blockIdx.x];
+    if (dgamma) dgamma[blockIdx.x] = (float)sums[C + blockIdx.x];
+  }
+  const int64_t plane = blockIdx.x / chunks;
+  const int ch = blockIdx.x % chunks;
+  const int c = (int)(plane % C);
+  const int64_t o0 = (int64_t)ch * BN_CHUNK;
+  const int len = (int)((HW - o0) < BN_CHUNK ? (HW - o0) : BN_CHUNK);
+  const int64_t off = plane * HW + o0;
+  const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
+  const float k = (gamma ? gamma[c] : 1.f) * rstd;
+  const float m1 = (float)(sums[c] * inv_count);
+  const float m2 = (float)(sums[C + c] * inv_count);
+  if (VEC) {
+    const float2* g2 = reinterpret_cast<const float2*>(g + off);
+    const float2* y2 = reinterpret_cast<const float2*>(y + off);
+    float2* o2 = reinterpret_cast<float2*>(gy + off);
+#pragma unroll
+    for (int i = 0; i < BN_CHUNK / 512; ++i) {
+      const int e = threadIdx.x + 256 * i;
+      if (2 * e < len) {
+        const float2 gv = g2[e], yv = y2[e];
+        const float gz0 = fmaf(yv.x, sc, sh) > 0.f ? gv.x : 0.f;
+        const float gz1 = fmaf(yv.y, sc, sh) > 0.f ? gv.y : 0.f;
+        float2 r;
+        r.x = k * (gz0 - m1 - ((yv.x - mean) * rstd) * m2);
+        r.y = k * (gz1 - m1 - ((yv.y - mean) * rstd) * m2);
+        o2[e] = r;
+      }
+    }
+  } else {
+    for (int e = threadIdx.x; e < len; e += 256) {
+      const float yv = y[off + e];
+      const float gz = fmaf(yv, sc, sh) > 0.f ? g[off + e] : 0.f;
+      gy[off + e] = k * (gz - m1 - ((yv - mean) * rstd) * m2);
+    }
+  }
+}
+
 static int64_t tiles_per_plane(int64_t H, int64_t W) {
   return cdiv(H, TH) * cdiv(W, TW);
 }
@@ -348,10 +451,26 @@ extern "C" int ainp_bn_relu_bwd_reduce(const float* g, const float* y,
   if (!g || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
       N < 1 || C < 1 || H < 1 || W < 1)
     return record_msg("ainp_bn_relu_bwd_reduce: bad argument");
-  const int64_t tpp = tiles_per_plane(H, W);
-  const int64_t blocks = N * C * tpp;
   double* partial = reinterpret_cast<double*>(workspace);
   hipStream_t s = as_stream(stream);
+  if (!g_ntcf) {
+    const int64_t HW = H * W;
+    const int chunks = (int)cdiv(HW, BN_CHUNK);   // <= tiles_per_plane: fits the workspace
+    const bool vec = (HW % 2 == 0) && ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(y)) % 8 == 0);
+    const dim3 grid((unsigned)(N * C * chunks));
+    if (vec)
+      hipLaunchKernelGGL(bn_relu_bwd_reduce_flat<true>, grid, dim3(256), 0, s, g, y, scale, shift,
+                         save_mean_rstd, partial, C, HW, chunks);
+    else
+      hipLaunchKernelGGL(bn_relu_bwd_reduce_flat<false>, grid, dim3(256), 0, s, g, y, scale, shift,
+                         save_mean_rstd, partial, C, HW, chunks);
+    int rc = check_launch("bn_relu_bwd_reduce_flat");
+    if (rc) return rc;
+    hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial, (int)N, C, chunks, sums);
+    return check_launch("bn_bwd_sum");
+  }
+  const int64_t tpp = tiles_per_plane(H, W);
+  const int64_t blocks = N * C * tpp;
   if (g_ntcf)
     hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<true>, dim3((unsigned)blocks),
                        dim3(256), 0, s, g, y, scale, shift, save_mean_rstd,
@@ -381,6 +500,23 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
   const int64_t blocks = N * C * tiles_per_plane(H, W);
   const double inv_count = 1.0 / (double)count;
   hipStream_t s = as_stream(stream);
+  if (!g_ntcf) {
+    const int64_t HW = H * W;
+    const int chunks = (int)cdiv(HW, BN_CHUNK);
+    const bool vec = (HW % 2 == 0) && ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(y) |
+                                        reinterpret_cast<uintptr_t>(gy)) % 8 == 0);
+    int64_t nb = N * C * chunks;
+    if (nb < C) nb = C;   // the dgamma / dbeta writers
+    if (vec)
+      hipLaunchKernelGGL(bn_relu_bwd_apply_flat<true>, dim3((unsigned)nb), dim3(256), 0, s, g, y,
+                         scale, shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, HW,
+                         chunks, inv_count);
+    else
+      hipLaunchKernelGGL(bn_relu_bwd_apply_flat<false>, dim3((unsigned)nb), dim3(256), 0, s, g, y,
+                         scale, shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, HW,
+                         chunks, inv_count);
+    return check_launch("bn_relu_bwd_apply_flat");
+  }
   if (g_ntcf)
     hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<true>, dim3((unsigned)blocks),
                        dim3(256), 0, s, g, y, scale, shift, gamma,

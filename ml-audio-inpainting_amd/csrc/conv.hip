@@ -416,6 +416,270 @@ constexpr int WG_GROUPS = 16;  // stage-1 groups of WG_BLOCKS/WG_GROUPS slabs
 static int wgrad_ct(int Cout) { return (Cout + 15) / 16; }
 static int wgrad_pass(int Cin) { return Cin < WG_CIMAX ? Cin : WG_CIMAX; }
 
+
+// ------------------------------------------------------------ small channels
+// Convolutions whose one side has 1-2 channels (the encoder's first conv
+// 1->16, the decoder's last 16->1 and its dgrad: models/CNNBLSTM/model.py:35,59)
+// are HBM-bound: the 16-row MFMA tiles above would waste 15/16 of their work.
+// fwd/dgrad: an 8x48 tile per block (the same tiling and stats-part
+// numbering as conv3x3_fwd_mfma), 128 threads = 8 rows x 16 x 3 pixels, input
+// tile + weights in LDS.  The tile is staged with every global load issued
+// before the first LDS store (no per-element load->store latency chain).
+template <int CIN, bool PRO, int NT>
+__device__ __forceinline__ void stage_small_tile(const float* __restrict__ x,
+                                                 const float* __restrict__ in_scale,
+                                                 const float* __restrict__ in_shift,
+                                                 float* sx, int n, int f0, int t0, int H, int W) {
+  constexpr int LR = CV_TT + 2, ROWS = CV_FT + 2, E = CIN * ROWS * LR;
+  constexpr int PER = (E + NT - 1) / NT;
+  constexpr int BATCH = PER < 16 ? PER : 16;      // loads in flight per thread
+  const int64_t HW = (int64_t)H * W;
+#pragma unroll
+  for (int b0 = 0; b0 < PER; b0 += BATCH) {
+    float v[BATCH];
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int e = threadIdx.x + NT * (b0 + i);
+      const int c = e / (ROWS * LR), rr = (e / LR) % ROWS, cc = e % LR;
+      const int f = f0 - 1 + rr, t = t0 - 1 + cc;
+      const bool ok = b0 + i < PER && e < E && f >= 0 && f < H && t >= 0 && t < W;
+      v[i] = ok ? x[((int64_t)n * CIN + c) * HW + (int64_t)f * W + t] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < BATCH; ++i) {
+      const int e = threadIdx.x + NT * (b0 + i);
+      if (b0 + i >= PER || e >= E) break;
+      float a = v[i];
+      if (PRO) {
+        const int c = e / (ROWS * LR), rr = (e / LR) % ROWS, cc = e % LR;
+        const int f = f0 - 1 + rr, t = t0 - 1 + cc;
+        // BatchNorm+ReLU of the previous layer; zero padding stays zero
+        if (f >= 0 && f < H && t >= 0 && t < W) a = fmaxf(fmaf(a, in_scale[c], in_shift[c]), 0.f);
+      }
+      sx[e] = a;
+    }
+  }
+}
+
+// PX pixels per thread: 3 (128 threads) when COUT is wide (per-thread outputs
+// amortise the stats reduction), 1 (384 threads) when it is 1-2 (more waves
+// in flight for the 16-channel staging).
+template <int CIN, int COUT, bool DGRAD, bool PRO, int PX>
+__global__ __launch_bounds__(384 / PX) void conv3x3_small_fwd(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+    float* __restrict__ y, double* __restrict__ stats, int H, int W) {
+  constexpr int TR = CV_FT, TC = CV_TT, LR = TC + 2, NT = 384 / PX, TPR = TC / PX, NWV = NT / 64;
+  __shared__ float sx[CIN * (TR + 2) * LR];
+  __shared__ float sw[COUT][CIN][9];
+  __shared__ double sred[2][NWV][COUT];
+  const int n = blockIdx.z, f0 = blockIdx.y * TR, t0 = blockIdx.x * TC;
+  const int tid = threadIdx.x;
+  const int64_t HW = (int64_t)H * W;
+  stage_small_tile<CIN, PRO, NT>(x, in_scale, in_shift, sx, n, f0, t0, H, W);
+  for (int i = tid; i < COUT * CIN * 9; i += blockDim.x) {
+    const int co = i / (CIN * 9), ci = (i / 9) % CIN, tap = i % 9;
+    sw[co][ci][tap] = DGRAD ? w[(ci * COUT + co) * 9 + 8 - tap] : w[(co * CIN + ci) * 9 + tap];
+  }
+  __syncthreads();
+  const int r = tid / TPR, c0 = tid % TPR;       // pixels (r, c0 + TPR*q), q < PX
+  const int f = f0 + r;
+  float acc[PX][COUT];
+#pragma unroll
+  for (int q = 0; q < PX; ++q)
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) acc[q][co] = bias ? bias[co] : 0.f;
+  constexpr int CUNR = CIN <= 2 ? CIN : 2;   // bound the hoisted weights per iteration
+#pragma unroll CUNR
+  for (int ci = 0; ci < CIN; ++ci)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const float* xr = sx + (ci * (TR + 2) + r + tap / 3) * LR + c0 + tap % 3;
+      float v[PX];
+#pragma unroll
+      for (int q = 0; q < PX; ++q) v[q] = xr[TPR * q];
+#pragma unroll
+      for (int co = 0; co < COUT; ++co) {
+        const float wv = sw[co][ci][tap];
+#pragma unroll
+        for (int q = 0; q < PX; ++q) acc[q][co] = fmaf(wv, v[q], acc[q][co]);
+      }
+    }
+  bool ok[PX];
+#pragma unroll
+  for (int q = 0; q < PX; ++q) {
+    const int t = t0 + c0 + TPR * q;
+    ok[q] = f < H && t < W;
+    if (ok[q]) {
+#pragma unroll
+      for (int co = 0; co < COUT; ++co)
+        y[((int64_t)n * COUT + co) * HW + (int64_t)f * W + t] = acc[q][co];
+    }
+  }
+  if (stats) {
+    const int wave = tid >> 6;
+#pragma unroll
+    for (int co = 0; co < COUT; ++co) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int q = 0; q < PX; ++q)
+        if (ok[q]) {
+          a += acc[q][co];
+          b += acc[q][co] * acc[q][co];
+        }
+      a = wave_sum(a);
+      b = wave_sum(b);
+      if ((tid & 63) == 0) {
+        sred[0][wave][co] = a;
+        sred[1][wave][co] = b;
+      }
+    }
+    __syncthreads();
+    if (tid < COUT) {
+      const int64_t part = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+      double a = 0.0, b = 0.0;
+      for (int q = 0; q < NWV; ++q) {
+        a += sred[0][q][tid];
+        b += sred[1][q][tid];
+      }
+      stats[part * 2 * COUT + tid] = a;
+      stats[part * 2 * COUT + COUT + tid] = b;
+    }
+  }
+}
+
+// wgrad: one thread per (co, ci, tap) output (+ COUT bias outputs) summing
+// dy * act(x) over the block's 8x48 pixels from LDS; one slab per block,
+// reduced by wgrad_reduce1 + small_wgrad_final in fixed order (fp64).
+template <int CIN, int COUT, bool PRO>
+__global__ __launch_bounds__(256) void conv3x3_small_wgrad(
+    const float* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const float* __restrict__ dy,
+    float* __restrict__ partial, int H, int W) {
+  constexpr int TR = CV_FT, TC = CV_TT, LR = TC + 2, GP = TR * TC + 1;
+  constexpr int NOUT = COUT * CIN * 9 + COUT;
+  constexpr int GE = COUT * TR * TC, GPER = (GE + 255) / 256;
+  __shared__ float sx[CIN * (TR + 2) * LR];
+  __shared__ float sg[COUT * GP];
+  const int n = blockIdx.z, f0 = blockIdx.y * TR, t0 = blockIdx.x * TC;
+  const int tid = threadIdx.x;
+  const int64_t HW = (int64_t)H * W;
+  {
+    float v[GPER];
+#pragma unroll
+    for (int i = 0; i < GPER; ++i) {
+      const int e = tid + 256 * i;
+      const int co = e / (TR * TC), p = e % (TR * TC);
+      const int f = f0 + p / TC, t = t0 + p % TC;
+      v[i] = (e < GE && f < H && t < W) ? dy[((int64_t)n * COUT + co) * HW + (int64_t)f * W + t] : 0.f;
+    }
+    stage_small_tile<CIN, PRO, 256>(x, in_scale, in_shift, sx, n, f0, t0, H, W);
+#pragma unroll
+    for (int i = 0; i < GPER; ++i) {
+      const int e = tid + 256 * i;
+      if (e < GE) sg[(e / (TR * TC)) * GP + e % (TR * TC)] = v[i];
+    }
+  }
+  __syncthreads();
+  const int64_t blk = ((int64_t)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x;
+  for (int o = tid; o < NOUT; o += blockDim.x) {
+    float s = 0.f;
+    if (o < COUT * CIN * 9) {
+      const int co = o / (CIN * 9), ci = (o / 9) % CIN, tap = o % 9;
+      const int ky = tap / 3, kx = tap % 3;
+      const float* g = sg + co * GP;
+      for (int r = 0; r < TR; ++r) {
+        const float* xr = sx + (ci * (TR + 2) + r + ky) * LR + kx;
+#pragma unroll 8
+        for (int c = 0; c < TC; ++c) s = fmaf(g[r * TC + c], xr[c], s);
+      }
+    } else {
+      const float* g = sg + (o - COUT * CIN * 9) * GP;
+      for (int p = 0; p < TR * TC; ++p) s += g[p];
+    }
+    partial[blk * NOUT + o] = s;
+  }
+}
+
+// dw[o] (o < COUT*CIN*9, [co][ci][tap] order) and dbias from the group sums
+__global__ void small_wgrad_final(const double* __restrict__ tmp, int ngroups, int nw, int nout,
+                                  float* __restrict__ dw, float* __restrict__ dbias) {
+  const int o = blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= nout) return;
+  double s = 0.0;
+  for (int g = 0; g < ngroups; ++g) s += tmp[(int64_t)g * nout + o];
+  if (o < nw) dw[o] = (float)s;
+  else if (dbias) dbias[o - nw] = (float)s;
+}
+
+// (Cin, Cout) pairs with a dedicated small-channel kernel
+static bool small_pair(int a, int b) {
+  return ((a == 1 || a == 2) && b == 16) || ((b == 1 || b == 2) && a == 16);
+}
+
+template <int CIN, int COUT>
+static void launch_small_fwd(bool dgrad, const float* x, const float* w, const float* bias,
+                             const float* sc, const float* sh, float* y, double* stats,
+                             int64_t N, int64_t H, int64_t W, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
+  constexpr int PX = COUT >= 16 ? 3 : 1;
+  const dim3 block(384 / PX);
+  if (dgrad)
+    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, true, false, PX>), grid, block, 0, s, x, w,
+                       bias, sc, sh, y, stats, (int)H, (int)W);
+  else if (sc)
+    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, true, PX>), grid, block, 0, s, x, w,
+                       bias, sc, sh, y, stats, (int)H, (int)W);
+  else
+    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, false, PX>), grid, block, 0, s, x, w,
+                       bias, sc, sh, y, stats, (int)H, (int)W);
+}
+
+static int small_fwd_dispatch(bool dgrad, const float* x, const float* w, const float* bias,
+                              const float* sc, const float* sh, float* y, double* stats,
+                              int64_t N, int Cin, int Cout, int64_t H, int64_t W, hipStream_t s) {
+#define AINP_SF(A, B) \
+  if (Cin == A && Cout == B) { launch_small_fwd<A, B>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s); return check_launch("conv3x3_small_fwd"); }
+  AINP_SF(1, 16) AINP_SF(2, 16) AINP_SF(16, 1) AINP_SF(16, 2)
+#undef AINP_SF
+  return record_msg("conv3x3: no small-channel kernel for this pair");
+}
+
+static size_t small_wgrad_ws(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+  const int64_t nblk = N * cdiv(H, CV_FT) * cdiv(W, CV_TT);
+  const int nout = Cout * Cin * 9 + Cout;
+  return (size_t)nblk * nout * sizeof(float) + (size_t)WG_GROUPS * nout * sizeof(double) + 16;
+}
+
+static int small_wgrad(const float* x, const float* sc, const float* sh, const float* dy,
+                       float* dw, float* dbias, void* workspace, int64_t N, int Cin, int Cout,
+                       int64_t H, int64_t W, hipStream_t s) {
+  dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
+  const int64_t nblk = (int64_t)grid.x * grid.y * grid.z;
+  const int nout = Cout * Cin * 9 + Cout;
+  float* partial = reinterpret_cast<float*>(workspace);
+#define AINP_SW(A, B) \
+  else if (Cin == A && Cout == B && sc) hipLaunchKernelGGL((conv3x3_small_wgrad<A, B, true>), grid, dim3(256), 0, s, x, sc, sh, dy, partial, (int)H, (int)W); \
+  else if (Cin == A && Cout == B) hipLaunchKernelGGL((conv3x3_small_wgrad<A, B, false>), grid, dim3(256), 0, s, x, sc, sh, dy, partial, (int)H, (int)W);
+  if (false) {}
+  AINP_SW(1, 16) AINP_SW(2, 16) AINP_SW(16, 1) AINP_SW(16, 2)
+  else return record_msg("conv3x3_wgrad: no small-channel kernel for this pair");
+#undef AINP_SW
+  int rc = check_launch("conv3x3_small_wgrad");
+  if (rc) return rc;
+  uintptr_t tp = reinterpret_cast<uintptr_t>(partial + nblk * nout);
+  tp = (tp + 15) & ~(uintptr_t)15;
+  double* tmp = reinterpret_cast<double*>(tp);
+  const int per_group = (int)cdiv(nblk, WG_GROUPS);
+  hipLaunchKernelGGL(wgrad_reduce1, dim3((nout + 255) / 256, WG_GROUPS), dim3(256), 0, s, partial,
+                     (int)nblk, nout, per_group, tmp);
+  rc = check_launch("wgrad_reduce1");
+  if (rc) return rc;
+  hipLaunchKernelGGL(small_wgrad_final, dim3((nout + 255) / 256), dim3(256), 0, s, tmp, WG_GROUPS,
+                     Cout * Cin * 9, nout, dw, dbias);
+  return check_launch("small_wgrad_final");
+}
+
 template <int CT, int JT>
 static void launch_wgrad(const float* x, const float* sc, const float* sh,
                          const float* dy, float* partial, int N, int Cin,
@@ -438,6 +702,8 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y,
                              double* stats, int64_t N, int Cin, int Cout,
                              int64_t H, int64_t W, hipStream_t s) {
+  if (small_pair(Cin, Cout))
+    return small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
   dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
   const int ct = (Cout + 15) / 16;
 #define AINP_FWD(CTV)                                                           \
@@ -485,7 +751,7 @@ extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
 
 extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
                                                int64_t H, int64_t W) {
-  (void)N; (void)H; (void)W;
+  if (small_pair(Cin, Cout)) return small_wgrad_ws(N, Cin, Cout, H, W);
   const int cp = wgrad_pass(Cin);
   int ct = wgrad_ct(Cout);
   if (ct == 3) ct = 4;
@@ -502,6 +768,9 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
     return record_msg("ainp_conv3x3_wgrad: bad argument");
   if ((in_scale == nullptr) != (in_shift == nullptr))
     return record_msg("ainp_conv3x3_wgrad: in_scale/in_shift must both be set");
+  if (small_pair(Cin, Cout))
+    return small_wgrad(x, in_scale, in_shift, dy, dw, dbias, workspace, N, Cin, Cout, H, W,
+                       as_stream(stream));
   const int CT = wgrad_ct(Cout);
   if (CT > 4) return record_msg("ainp_conv3x3_wgrad: Cout > 64 unsupported");
   const int CTp = CT == 3 ? 4 : CT;  // kernel co-tiles (waves split evenly)

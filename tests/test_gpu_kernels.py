@@ -171,7 +171,10 @@ def _act(x, sc, sh):
 @pytest.mark.parametrize("N,Cin,Cout,H,W,pro", [
     (2, 1, 16, 33, 24, False), (2, 16, 32, 33, 50, True), (1, 32, 64, 40, 100, True),
     (2, 32, 16, 17, 49, True), (2, 16, 1, 20, 30, True), (1, 64, 32, 9, 7, False),
-    (1, 8, 48, 11, 13, True)])
+    (1, 8, 48, 11, 13, True),
+    # small-channel kernels (1-2 channels on one side, 16 on the other), multi-tile
+    (2, 1, 16, 41, 100, False), (3, 16, 1, 19, 97, True), (1, 2, 16, 12, 50, True),
+    (1, 16, 2, 25, 60, False)])
 def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
     g = torch.Generator().manual_seed(N * 100 + Cin * 10 + Cout)
     x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
@@ -199,10 +202,11 @@ def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
 
 
 # ------------------------------------------------------------------ BN
-@pytest.mark.parametrize("ntcf", [False, True])
-def test_bn_relu_fwd_bwd(ops, ntcf):
+@pytest.mark.parametrize("ntcf,H,W", [(False, 37, 70), (True, 37, 70), (False, 37, 71),
+                                       (False, 65, 130)])
+def test_bn_relu_fwd_bwd(ops, ntcf, H, W):
     g = torch.Generator().manual_seed(9)
-    N, C, H, W = 3, 8, 37, 70
+    N, C = 3, 8
     y = torch.randn(N, C, H, W, generator=g, dtype=torch.float64) * 2 + 0.5
     gamma = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
     beta = torch.randn(C, generator=g, dtype=torch.float64) * 0.1
