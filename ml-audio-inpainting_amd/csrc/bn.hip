@@ -136,73 +136,6 @@ __global__ __launch_bounds__(256) void bn_relu_apply_kernel(
   }
 }
 
-// Load a tile of g (NCHW or NTCF) into LDS tile[w][h] layout.
-template <bool NTCF>
-__device__ __forceinline__ void load_g_tile(const float* __restrict__ g,
-                                            const TileIdx& ti, int C,
-                                            int64_t H, int64_t W,
-                                            float (*tile)[TH + 1]) {
-  const int tid = threadIdx.x;
-  if (NTCF) {
-    const int hx = tid & 31, wy = tid >> 5;
-    const int64_t CH = (int64_t)C * H;
-    for (int i = 0; i < TW / 8; ++i) {
-      const int ww = wy + 8 * i;
-      const int64_t h = ti.h0 + hx, w = ti.w0 + ww;
-      float v = 0.f;
-      if (h < H && w < W) v = g[((int64_t)ti.n * W + w) * CH + (int64_t)ti.c * H + h];
-      tile[ww][hx] = v;
-    }
-  } else {
-    const int tx = tid & 63, ty = tid >> 6;
-    const float* gp = g + ((int64_t)ti.n * C + ti.c) * H * W;
-    for (int i = 0; i < TH / 4; ++i) {
-      const int hh = ty + 4 * i;
-      const int64_t h = ti.h0 + hh, w = ti.w0 + tx;
-      tile[tx][hh] = (h < H && w < W) ? gp[h * W + w] : 0.f;
-    }
-  }
-  __syncthreads();
-}
-
-// partial[tile][0] = sum gz, partial[tile][1] = sum gz*xhat
-template <bool NTCF>
-__global__ __launch_bounds__(256) void bn_relu_bwd_reduce_kernel(
-    const float* __restrict__ g, const float* __restrict__ y,
-    const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ save, double* __restrict__ partial, int C,
-    int64_t H, int64_t W) {
-  __shared__ float tile[TW][TH + 1];
-  __shared__ double red[2][4];
-  const TileIdx ti = tile_of(blockIdx.x, C, H, W);
-  load_g_tile<NTCF>(g, ti, C, H, W, tile);
-  const float sc = scale[ti.c], sh = shift[ti.c];
-  const float mean = save[ti.c], rstd = save[C + ti.c];
-  const float* yp = y + ((int64_t)ti.n * C + ti.c) * H * W;
-  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
-  float s1 = 0.f, s2 = 0.f;
-  for (int i = 0; i < TH / 4; ++i) {
-    const int hh = ty + 4 * i;
-    const int64_t h = ti.h0 + hh, w = ti.w0 + tx;
-    if (h < H && w < W) {
-      const float yv = yp[h * W + w];
-      const float gz = (fmaf(yv, sc, sh) > 0.f) ? tile[tx][hh] : 0.f;
-      s1 += gz;
-      s2 += gz * ((yv - mean) * rstd);
-    }
-  }
-  double d1 = wave_sum_d((double)s1), d2 = wave_sum_d((double)s2);
-  if ((tid & 63) == 0) {
-    red[0][tid >> 6] = d1;
-    red[1][tid >> 6] = d2;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    partial[(int64_t)blockIdx.x * 2 + 0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    partial[(int64_t)blockIdx.x * 2 + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-  }
-}
-
 // Sum tile partials per channel: sums[c] = sum gz, sums[C+c] = sum gz*xhat
 __global__ void bn_bwd_sum_kernel(const double* __restrict__ partial, int N,
                                   int C, int tiles_per_plane,
@@ -231,45 +164,6 @@ __global__ void bn_bwd_sum_kernel(const double* __restrict__ partial, int N,
     sums[C + c] = s2;
   }
 }
-
-// gy = gamma*rstd*(gz - sum(gz)/M - xhat*sum(gz*xhat)/M), NCHW out
-template <bool NTCF>
-__global__ __launch_bounds__(256) void bn_relu_bwd_apply_kernel(
-    const float* __restrict__ g, const float* __restrict__ y,
-    const float* __restrict__ scale, const float* __restrict__ shift,
-    const float* __restrict__ gamma, const float* __restrict__ save,
-    const double* __restrict__ sums, float* __restrict__ gy,
-    float* __restrict__ dgamma, float* __restrict__ dbeta, int C, int64_t H,
-    int64_t W, double inv_count) {
-  __shared__ float tile[TW][TH + 1];
-  const TileIdx ti = tile_of(blockIdx.x, C, H, W);
-  if (blockIdx.x < (unsigned)C && threadIdx.x == 0) {
-    if (dbeta) dbeta[blockIdx.x] = (float)sums[blockIdx.x];
-    if (dgamma) dgamma[blockIdx.x] = (float)sums[C + blockIdx.x];
-  }
-  load_g_tile<NTCF>(g, ti, C, H, W, tile);
-  const float sc = scale[ti.c], sh = shift[ti.c];
-  const float mean = save[ti.c], rstd = save[C + ti.c];
-  const float gm = gamma ? gamma[ti.c] : 1.f;
-  const float k = gm * rstd;
-  const float m1 = (float)(sums[ti.c] * inv_count);
-  const float m2 = (float)(sums[C + ti.c] * inv_count);
-  const int64_t off = ((int64_t)ti.n * C + ti.c) * H * W;
-  const float* yp = y + off;
-  float* gp = gy + off;
-  const int tid = threadIdx.x, tx = tid & 63, ty = tid >> 6;
-  for (int i = 0; i < TH / 4; ++i) {
-    const int hh = ty + 4 * i;
-    const int64_t h = ti.h0 + hh, w = ti.w0 + tx;
-    if (h < H && w < W) {
-      const float yv = yp[h * W + w];
-      const float gz = (fmaf(yv, sc, sh) > 0.f) ? tile[tx][hh] : 0.f;
-      const float xh = (yv - mean) * rstd;
-      gp[h * W + w] = k * (gz - m1 - xh * m2);
-    }
-  }
-}
-
 
 // ---------------------------------------------------------- flat NCHW path
 // g and y both NCHW: a block owns BN_CHUNK contiguous elements of one (n, c)
@@ -373,6 +267,120 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
   }
 }
 
+
+// ----------------------------------------------------------- NTCF path
+// The encoder's last BatchNorm+ReLU reads / writes the LSTM layout
+// [n][w][c*H + h] (model.py:73-74) while y is NCHW: 64(h) x 64(w) tiles of one
+// (n, c), transposed through LDS; every global load of a tile is issued
+// before the barrier (both operands in flight together).
+constexpr int NT_T = 64;
+
+__device__ __forceinline__ void ntcf_tile(int64_t b, int C, int64_t H, int64_t W, int& n, int& c,
+                                          int& h0, int& w0) {
+  const int th = (int)((H + NT_T - 1) / NT_T), tw = (int)((W + NT_T - 1) / NT_T);
+  w0 = (int)(b % tw) * NT_T;
+  h0 = (int)((b / tw) % th) * NT_T;
+  c = (int)((b / ((int64_t)tw * th)) % C);
+  n = (int)(b / ((int64_t)tw * th * C));
+}
+
+__global__ __launch_bounds__(256) void bn_relu_apply_ntcf(const float* __restrict__ x,
+                                                          const float* __restrict__ scale,
+                                                          const float* __restrict__ shift,
+                                                          float* __restrict__ out, int C, int64_t H,
+                                                          int64_t W) {
+  __shared__ float tile[NT_T][NT_T + 1];   // [w][h]
+  int n, c, h0, w0;
+  ntcf_tile(blockIdx.x, C, H, W, n, c, h0, w0);
+  const float sc = scale[c], sh = shift[c];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const float* xp = x + ((int64_t)n * C + c) * H * W;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t h = h0 + q + 4 * i, w = w0 + lane;
+    v[i] = (h < H && w < W) ? fmaxf(fmaf(xp[h * W + w], sc, sh), 0.f) : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tile[lane][q + 4 * i] = v[i];
+  __syncthreads();
+  const int64_t CH = (int64_t)C * H;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int64_t h = h0 + lane, w = w0 + q + 4 * i;
+    if (h < H && w < W) out[((int64_t)n * W + w) * CH + (int64_t)c * H + h] = tile[q + 4 * i][lane];
+  }
+}
+
+template <bool APPLY>
+__global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
+    const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ gamma,
+    const float* __restrict__ save, const double* __restrict__ sums, double* __restrict__ partial,
+    float* __restrict__ gy, float* __restrict__ dgamma, float* __restrict__ dbeta, int C,
+    int64_t H, int64_t W, double inv_count) {
+  __shared__ float tile[NT_T][NT_T + 1];   // g as [w][h]
+  __shared__ double red[2][4];
+  if (APPLY && blockIdx.x < (unsigned)C && threadIdx.x == 0) {
+    if (dbeta) dbeta[blockIdx.x] = (float)sums[blockIdx.x];
+    if (dgamma) dgamma[blockIdx.x] = (float)sums[C + blockIdx.x];
+  }
+  int n, c, h0, w0;
+  ntcf_tile(blockIdx.x, C, H, W, n, c, h0, w0);
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int64_t CH = (int64_t)C * H;
+  const int64_t off = ((int64_t)n * C + c) * H * W;
+  float gv[16], yv[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {            // g: lanes along h (NTCF rows)
+    const int64_t h = h0 + lane, w = w0 + q + 4 * i;
+    gv[i] = (h < H && w < W) ? g[((int64_t)n * W + w) * CH + (int64_t)c * H + h] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {            // y: lanes along w (NCHW rows)
+    const int64_t h = h0 + q + 4 * i, w = w0 + lane;
+    yv[i] = (h < H && w < W) ? y[off + h * W + w] : 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < 16; ++i) tile[q + 4 * i][lane] = gv[i];
+  __syncthreads();
+  const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
+  if (APPLY) {
+    const float k = (gamma ? gamma[c] : 1.f) * rstd;
+    const float m1 = (float)(sums[c] * inv_count);
+    const float m2 = (float)(sums[C + c] * inv_count);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t h = h0 + q + 4 * i, w = w0 + lane;
+      if (h < H && w < W) {
+        const float gz = fmaf(yv[i], sc, sh) > 0.f ? tile[lane][q + 4 * i] : 0.f;
+        gy[off + h * W + w] = k * (gz - m1 - ((yv[i] - mean) * rstd) * m2);
+      }
+    }
+  } else {
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int64_t h = h0 + q + 4 * i, w = w0 + lane;
+      if (h < H && w < W) {
+        const float gz = fmaf(yv[i], sc, sh) > 0.f ? tile[lane][q + 4 * i] : 0.f;
+        s1 += gz;
+        s2 += gz * ((yv[i] - mean) * rstd);
+      }
+    }
+    const double d1 = wave_sum_d((double)s1), d2 = wave_sum_d((double)s2);
+    if (lane == 0) {
+      red[0][q] = d1;
+      red[1][q] = d2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      partial[(int64_t)blockIdx.x * 2 + 0] = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      partial[(int64_t)blockIdx.x * 2 + 1] = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    }
+  }
+}
+
 static int64_t tiles_per_plane(int64_t H, int64_t W) {
   return cdiv(H, TH) * cdiv(W, TW);
 }
@@ -429,7 +437,7 @@ extern "C" int ainp_bn_relu_apply(const float* x, const float* scale,
   const int64_t blocks = N * C * tiles_per_plane(H, W);
   hipStream_t s = as_stream(stream);
   if (out_ntcf)
-    hipLaunchKernelGGL(bn_relu_apply_kernel<true>, dim3((unsigned)blocks),
+    hipLaunchKernelGGL(bn_relu_apply_ntcf, dim3((unsigned)(N * C * cdiv(H, NT_T) * cdiv(W, NT_T))),
                        dim3(256), 0, s, x, scale, shift, out, C, H, W);
   else
     hipLaunchKernelGGL(bn_relu_apply_kernel<false>, dim3((unsigned)blocks),
@@ -469,17 +477,11 @@ extern "C" int ainp_bn_relu_bwd_reduce(const float* g, const float* y,
     hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial, (int)N, C, chunks, sums);
     return check_launch("bn_bwd_sum");
   }
-  const int64_t tpp = tiles_per_plane(H, W);
-  const int64_t blocks = N * C * tpp;
-  if (g_ntcf)
-    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<true>, dim3((unsigned)blocks),
-                       dim3(256), 0, s, g, y, scale, shift, save_mean_rstd,
-                       partial, C, H, W);
-  else
-    hipLaunchKernelGGL(bn_relu_bwd_reduce_kernel<false>, dim3((unsigned)blocks),
-                       dim3(256), 0, s, g, y, scale, shift, save_mean_rstd,
-                       partial, C, H, W);
-  int rc = check_launch("bn_relu_bwd_reduce");
+  const int64_t tpp = cdiv(H, NT_T) * cdiv(W, NT_T);   // <= tiles_per_plane: fits
+  hipLaunchKernelGGL(bn_relu_bwd_ntcf<false>, dim3((unsigned)(N * C * tpp)), dim3(256), 0, s, g,
+                     y, scale, shift, nullptr, save_mean_rstd, nullptr, partial, nullptr, nullptr,
+                     nullptr, C, H, W, 0.0);
+  int rc = check_launch("bn_relu_bwd_reduce_ntcf");
   if (rc) return rc;
   hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial,
                      (int)N, C, (int)tpp, sums);
@@ -517,15 +519,11 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
                          chunks, inv_count);
     return check_launch("bn_relu_bwd_apply_flat");
   }
-  if (g_ntcf)
-    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<true>, dim3((unsigned)blocks),
-                       dim3(256), 0, s, g, y, scale, shift, gamma,
-                       save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W,
-                       inv_count);
-  else
-    hipLaunchKernelGGL(bn_relu_bwd_apply_kernel<false>, dim3((unsigned)blocks),
-                       dim3(256), 0, s, g, y, scale, shift, gamma,
-                       save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W,
-                       inv_count);
-  return check_launch("bn_relu_bwd_apply");
+  (void)blocks;
+  int64_t nb = N * C * cdiv(H, NT_T) * cdiv(W, NT_T);
+  if (nb < C) nb = C;
+  hipLaunchKernelGGL(bn_relu_bwd_ntcf<true>, dim3((unsigned)nb), dim3(256), 0, s, g, y, scale,
+                     shift, gamma, save_mean_rstd, sums, nullptr, gy, dgamma, dbeta, C, H, W,
+                     inv_count);
+  return check_launch("bn_relu_bwd_apply_ntcf");
 }
