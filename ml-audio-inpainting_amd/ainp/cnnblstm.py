@@ -182,6 +182,11 @@ class _BLSTMFn(torch.autograd.Function):
         NT = N * T
         grads = [None] * len(params)
         dx = None
+        # The weight/bias gradients of layer l depend only on its gate
+        # gradients, so they run on a side stream while the main stream goes
+        # on with dX and layer l-1's recurrence (64 workgroups: most CUs idle).
+        main = torch.cuda.current_stream(dh.device)
+        side = _side_stream(dh.device)
         for l in range(L - 1, -1, -1):
             inp, h, gates, cell = saved[4 * l:4 * l + 4]
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
@@ -189,12 +194,18 @@ class _BLSTMFn(torch.autograd.Function):
             dg = ops.lstm_rec_bwd(dh, gates, cell, hf, hr, H)          # [N,T,8H]
             dg2 = dg.view(NT, 8 * H)
             hp = ops.lstm_hprev(h, H).view(NT, 2 * H)
-            # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs for
-            # the recurrent / upper layers -> parallel split-K over row chunks
-            gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H))
-            gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il, offsets_b=(0, 0))
-            db_ih = ops.colsum(dg2)
-            db_hh = ops.colsum(dg2)
+            ready = torch.cuda.Event()
+            ready.record(main)
+            side.wait_event(ready)
+            with torch.cuda.stream(side):
+                # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
+                # for the recurrent / upper layers -> parallel split-K over row chunks
+                gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H))
+                gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il, offsets_b=(0, 0))
+                db_ih = ops.colsum(dg2)
+                db_hh = ops.colsum(dg2)
+            for t in (dg, hp, inp):
+                t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l
             grads[base + 0], grads[base + 1] = gwi[0], gwh[0]
             grads[base + 2], grads[base + 3] = db_ih[:4 * H], db_hh[:4 * H]
@@ -206,7 +217,23 @@ class _BLSTMFn(torch.autograd.Function):
                          [dxi, dxi], Il, 1, ksplit=True)
                 dh = dxi.view(N, T, Il)
                 dx = dh
+        done = torch.cuda.Event()
+        done.record(side)
+        main.wait_event(done)
+        for gr in grads:
+            gr.record_stream(main)        # side-stream memory handed to autograd
         return (dx, None, None, *grads)
+
+
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(device):
+    s = _SIDE_STREAMS.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _SIDE_STREAMS[device] = s
+    return s
 
 
 # ------------------------------------------------------------------ projection
