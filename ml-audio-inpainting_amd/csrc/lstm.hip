@@ -31,6 +31,13 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 // Quad broadcast: value of lane (4*(lane/4) + Q) to every lane of the quad.
+// Packed fp32 pair: v_pk_fma_f32 issues two FMAs per instruction on gfx950,
+// halving the issue cost of the per-step W_hh matvec.  Lanes .x/.y of the two
+// accumulators are the same k mod 4 chains as four scalar accumulators, so the
+// result is bit-identical to the scalar form.
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2 pk_fma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
 template <int Q>
 __device__ __forceinline__ float quad_bcast(float v) {
   constexpr int ctrl = Q | (Q << 2) | (Q << 4) | (Q << 6);  // DPP quad_perm
@@ -58,11 +65,11 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_fwd_kernel(
   const int row = g * H + u;
   const float* whh = dir ? whh_r : whh_f;
 
-  float w[H];
+  f2 w[H / 2];
 #pragma unroll
   for (int k = 0; k < H; k += 4) {
     const float4 v = *reinterpret_cast<const float4*>(whh + (int64_t)row * H + k);
-    w[k] = v.x; w[k + 1] = v.y; w[k + 2] = v.z; w[k + 3] = v.w;
+    w[k / 2] = f2{v.x, v.y}; w[k / 2 + 1] = f2{v.z, v.w};
   }
   if (tid < H) hb[1][tid] = 0.f;
 
@@ -107,16 +114,14 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_fwd_kernel(
       const int t = ch * LCH + s;
       if (t >= T) break;  // uniform across the block
       const float* hp = hb[(t + 1) & 1];
-      float a0 = zs[buf][s][row], a1 = 0.f, a2 = 0.f, a3 = 0.f;
+      f2 a01 = f2{zs[buf][s][row], 0.f}, a23 = f2{0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < H; k += 4) {
         const float4 h4 = *reinterpret_cast<const float4*>(hp + k);
-        a0 = fmaf(w[k + 0], h4.x, a0);
-        a1 = fmaf(w[k + 1], h4.y, a1);
-        a2 = fmaf(w[k + 2], h4.z, a2);
-        a3 = fmaf(w[k + 3], h4.w, a3);
+        a01 = pk_fma(w[k / 2], f2{h4.x, h4.y}, a01);
+        a23 = pk_fma(w[k / 2 + 1], f2{h4.z, h4.w}, a23);
       }
-      const float pre = (a0 + a1) + (a2 + a3);
+      const float pre = (a01.x + a01.y) + (a23.x + a23.y);
       const float act = (g == 2) ? tanhf(pre) : sigm(pre);
       const float ig = quad_bcast<0>(act), fg = quad_bcast<1>(act);
       const float gg = quad_bcast<2>(act), og = quad_bcast<3>(act);
@@ -161,9 +166,10 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
   const int n = blockIdx.x >> 1, dir = blockIdx.x & 1;
   const int tid = threadIdx.x, k = tid >> 2, q = tid & 3;
   const float* whh = dir ? whh_r : whh_f;
-  float wt[H];  // W[q*H + m][k]
+  f2 wt[H / 2];  // W[q*H + m][k], m pairs
 #pragma unroll
-  for (int m = 0; m < H; ++m) wt[m] = whh[(int64_t)(q * H + m) * H + k];
+  for (int m = 0; m < H; m += 2)
+    wt[m / 2] = f2{whh[(int64_t)(q * H + m) * H + k], whh[(int64_t)(q * H + m + 1) * H + k]};
 
   auto tix = [&](int t) { return dir ? (T - 1 - t) : t; };
   const float* gbase = gates + (int64_t)n * T * 8 * H + dir * G4;
@@ -252,16 +258,14 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
       dgrow[tt * 8 * H] = da;
       lds_barrier();
       const float* dq = db + q * DGS;
-      float a = 0.f, b = 0.f, c = 0.f, d = 0.f;
+      f2 ab = f2{0.f, 0.f}, cd = f2{0.f, 0.f};
 #pragma unroll
       for (int m = 0; m < H; m += 4) {
         const float4 v = *reinterpret_cast<const float4*>(dq + m);
-        a = fmaf(wt[m + 0], v.x, a);
-        b = fmaf(wt[m + 1], v.y, b);
-        c = fmaf(wt[m + 2], v.z, c);
-        d = fmaf(wt[m + 3], v.w, d);
+        ab = pk_fma(wt[m / 2], f2{v.x, v.y}, ab);
+        cd = pk_fma(wt[m / 2 + 1], f2{v.z, v.w}, cd);
       }
-      const float part = (a + b) + (c + d);
+      const float part = (ab.x + ab.y) + (cd.x + cd.y);
       dh_rec = (quad_bcast<0>(part) + quad_bcast<1>(part)) +
                (quad_bcast<2>(part) + quad_bcast<3>(part));
     }
