@@ -367,6 +367,175 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
   }
 }
 
+// Specialised weight gradient for the model's channel pairs: CP input channels
+// per pass (16 or 32) and CO = Cout (16, 32 or 64) are compile-time, so
+//  * staging has no per-element predicates: every load is a buffer load at a
+//    clamped (always in-range) address, channel planes addressed by a scalar
+//    soffset, and out-of-image values are selected to zero at commit;
+//  * every LDS fragment address is a per-lane base + compile-time immediate,
+//    and each 4-pixel step issues all of its B-fragment reads before its MFMAs
+//    (the generic kernel above ran out of registers and serialised one LDS
+//    round trip per MFMA).
+// Same tiles, partial-slab format and deterministic reduction as
+// conv3x3_wgrad_mfma.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+template <int CP, int CO>
+struct WgradT {
+  static constexpr int CT = CO / 16;                      // co tiles
+  static constexpr int JT = 9 * CP / 16;                  // j tiles
+  static constexpr int WPC0 = 4 / CT, WPC1 = (JT + 8) / 9;
+  static constexpr int WPC = WPC0 > WPC1 ? WPC0 : WPC1;   // waves per co tile
+  static constexpr int NW = CT * WPC;                     // waves (4 or 8)
+  static constexpr int JPW = (JT + WPC - 1) / WPC;        // j tiles per wave (<= 9)
+};
+
+template <int CP, int CO>
+__global__ __launch_bounds__((WgradT<CP, CO>::NW * 64), (WgradT<CP, CO>::NW / 2)) void conv3x3_wgrad_t(
+    const float* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const float* __restrict__ dy,
+    float* __restrict__ partial, int N, int Cin, int H, int W, int ci0) {
+  using T = WgradT<CP, CO>;
+  constexpr int J = 9 * CP, JT = T::JT, WPC = T::WPC, JPW = T::JPW, NW = T::NW;
+  constexpr int XH = NW / 4;                  // channel groups of the x interior rows
+  constexpr int NXR = CP / XH;                // x rows per thread
+  constexpr int NGR = CO * 2 / NW;            // dy rows per thread
+  static_assert(CP % 16 == 0 && CP <= WG_CIMAX && CO % 16 == 0 && CO <= 64, "shape");
+  static_assert(8 * CP <= NW * 64, "halo: one element per thread");
+  __shared__ __attribute__((aligned(16))) float s_x[CP * WG_XPLANE];
+  __shared__ __attribute__((aligned(16))) float s_g[CO * WG_GPLANE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 15, kq = lane >> 4;
+  const int ct = wave / WPC;
+  const int jt0 = (wave % WPC) * JPW;
+
+  // B offset of j tile q for this lane (ci = li within the tile), row 0 col 0
+  int boff[JPW];
+#pragma unroll
+  for (int q = 0; q < JPW; ++q) {
+    const int jt = jt0 + q;
+    const int tap = CP == 32 ? (jt >> 1) : jt;
+    const int cih = CP == 32 ? (jt & 1) * 16 : 0;
+    boff[q] = (cih + li) * WG_XPLANE + (tap / 3) * WG_LDT + (tap % 3) + kq;
+  }
+  f32x4 acc[JPW];
+#pragma unroll
+  for (int q = 0; q < JPW; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float dbias = 0.f;
+
+  const int tiles_t = (W + WG_TT - 1) / WG_TT;
+  const int tiles_f = (H + WG_FT - 1) / WG_FT;
+  const int64_t ntiles = (int64_t)N * tiles_f * tiles_t;
+  const int64_t HW = (int64_t)H * W;
+
+  // staging map: x interior row xr = wave&3 (halo rows f0-1..f0+2), channels
+  // xc0 + XH*i; dy row gr = wave&1, channels gc0 + (NW/2)*i; one x halo-column
+  // element per thread
+  const int xr = wave & 3, xc0 = wave >> 2;
+  const int gr = wave & 1, gc0 = wave >> 1;
+  float px[NXR], pxh, pg[NGR];
+  const int hside = tid & 1, hrr = (tid >> 1) & 3, hci = tid >> 3;
+  auto tile_coords = [&](int64_t tile, int& n, int& f0, int& t0) {
+    const int tt = tile % tiles_t;
+    const int tf = (tile / tiles_t) % tiles_f;
+    n = (int)(tile / ((int64_t)tiles_t * tiles_f));
+    f0 = tf * WG_FT;
+    t0 = tt * WG_TT;
+  };
+  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
+  auto fetch = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+    int plane = (int)(HW * 4);
+    asm volatile("" : "+s"(plane));  // keep the per-plane offsets out of the tile loop
+    const int tc = clampi(t0 + lane, 0, W - 1);
+    const __amdgpu_buffer_rsrc_t rx = buf_rsrc(x + ((int64_t)n * Cin + ci0) * HW);
+    const int vo = (clampi(f0 - 1 + xr, 0, H - 1) * W + tc) * 4;
+#pragma unroll
+    for (int i = 0; i < NXR; ++i) px[i] = buf_ld(rx, vo, (xc0 + XH * i) * plane);
+    {
+      const int fh = clampi(f0 - 1 + hrr, 0, H - 1);
+      const int th = clampi(hside ? t0 + WG_TT : t0 - 1, 0, W - 1);
+      pxh = buf_ld(rx, (fh * W + th) * 4, (hci < CP ? hci : CP - 1) * plane);
+    }
+    const __amdgpu_buffer_rsrc_t rg = buf_rsrc(dy + (int64_t)n * CO * HW);
+    const int vg = (clampi(f0 + gr, 0, H - 1) * W + tc) * 4;
+#pragma unroll
+    for (int i = 0; i < NGR; ++i) pg[i] = buf_ld(rg, vg, (gc0 + (NW / 2) * i) * plane);
+  };
+  auto commit = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+    const int f = f0 - 1 + xr, t = t0 + lane;
+    const bool ok = f >= 0 && f < H && t < W;
+    if (in_scale) {
+#pragma unroll
+      for (int i = 0; i < NXR; ++i) {
+        const int ci = xc0 + XH * i;
+        s_x[ci * WG_XPLANE + xr * WG_LDT + lane + 1] =
+            ok ? fmaxf(fmaf(px[i], in_scale[ci0 + ci], in_shift[ci0 + ci]), 0.f) : 0.f;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NXR; ++i)
+        s_x[(xc0 + XH * i) * WG_XPLANE + xr * WG_LDT + lane + 1] = ok ? px[i] : 0.f;
+    }
+    if (hci < CP) {
+      const int fh = f0 - 1 + hrr, th = hside ? t0 + WG_TT : t0 - 1;
+      const bool hok = fh >= 0 && fh < H && th >= 0 && th < W;
+      float v = pxh;
+      if (in_scale) v = fmaxf(fmaf(v, in_scale[ci0 + hci], in_shift[ci0 + hci]), 0.f);
+      s_x[hci * WG_XPLANE + hrr * WG_LDT + (hside ? WG_TT + 1 : 0)] = hok ? v : 0.f;
+    }
+    const bool gok = f0 + gr < H && t < W;
+#pragma unroll
+    for (int i = 0; i < NGR; ++i)
+      s_g[(gc0 + (NW / 2) * i) * WG_GPLANE + gr * WG_TT + lane] = gok ? pg[i] : 0.f;
+  };
+
+  const float* ga = s_g + (ct * 16 + li) * WG_GPLANE + kq;
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    commit(tile);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
+#pragma unroll
+    for (int s = 0; s < WG_FT * WG_TT / 4; ++s) {
+      // pixel p = 4s + kq -> row s/16, column 4(s%16) + kq (kq folded into the bases)
+      const int roff = (s >> 4) * WG_LDT + (s & 15) * 4;
+      const float af = ga[4 * s];
+      dbias += af;
+      float bv[JPW];
+#pragma unroll
+      for (int q = 0; q < JPW; ++q) bv[q] = s_x[boff[q] + roff];
+#pragma unroll
+      for (int q = 0; q < JPW; ++q)
+        if (JPW * WPC == JT || jt0 + q < JT) acc[q] = mfma16x16x4(af, bv[q], acc[q]);
+    }
+    __syncthreads();
+  }
+  float* slab = partial + (int64_t)blockIdx.x * CO * (J + 1);
+#pragma unroll
+  for (int q = 0; q < JPW; ++q) {
+    const int j = (jt0 + q) * 16 + li;
+    if (jt0 + q < JT) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) slab[(ct * 16 + kq * 4 + r) * (J + 1) + j] = acc[q][r];
+    }
+  }
+  float d = dbias;
+  d += __shfl_xor(d, 16, 64);
+  d += __shfl_xor(d, 32, 64);
+  if (kq == 0 && (wave % WPC) == 0) slab[(ct * 16 + li) * (J + 1) + J] = d;
+}
+
 // Stage 1: tmp[g][idx] = sum of slabs [g*per_group, (g+1)*per_group), fp64
 // (the first conv's weight gradient is a heavily cancelling sum: its input
 // sits near log10(1e-9) while the BatchNorm-backward output sums to ~0).
@@ -792,11 +961,28 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
     else launch_wgrad<CTV, 18>(x, in_scale, in_shift, dy, partial, (int)N, Cin,    \
                                Cout, (int)H, (int)W, ci0, cp, s);                   \
   } while (0)
-    switch (CTp) {
-      case 1: AINP_WG(1); break;
-      case 2: AINP_WG(2); break;
-      default: AINP_WG(4); break;
+    // specialised kernel: 32-bit buffer offsets must cover a sample's planes
+    const bool fits = (int64_t)H * W * 4 * (Cout > WG_CIMAX ? Cout : WG_CIMAX) < ((int64_t)1 << 31);
+    const int key = fits ? cp * 100 + Cout : 0;
+#define AINP_WGT(CPV, COV)                                                           \
+  hipLaunchKernelGGL((conv3x3_wgrad_t<CPV, COV>), dim3(WG_BLOCKS),                    \
+                     dim3(WgradT<CPV, COV>::NW * 64), 0, s, x,                          \
+                     in_scale, in_shift, dy, partial, (int)N, Cin, (int)H, (int)W, ci0)
+    switch (key) {
+      case 1616: AINP_WGT(16, 16); break;
+      case 1632: AINP_WGT(16, 32); break;
+      case 1664: AINP_WGT(16, 64); break;
+      case 3216: AINP_WGT(32, 16); break;
+      case 3232: AINP_WGT(32, 32); break;
+      case 3264: AINP_WGT(32, 64); break;
+      default:
+        switch (CTp) {
+          case 1: AINP_WG(1); break;
+          case 2: AINP_WG(2); break;
+          default: AINP_WG(4); break;
+        }
     }
+#undef AINP_WGT
 #undef AINP_WG
     int rc = check_launch("conv3x3_wgrad_mfma");
     if (rc) return rc;
