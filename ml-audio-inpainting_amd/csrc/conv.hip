@@ -38,7 +38,22 @@ struct FwdLds {
 // right after chunk c is committed to LDS, so they are in flight during
 // chunk c's MFMAs (a load->store loop per element would serialise one HBM
 // round trip per element).
-template <int CT, bool DGRAD>
+// EX (exact shapes: Cin % 8 == 0, Cout == 16*CT, a sample's planes within
+// 2^31 bytes): staging without per-element predicates -- clamped-address
+// buffer loads, out-of-image values selected to zero at commit -- so the
+// compiler emits no branch/vmcnt(0) per element.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+__device__ __forceinline__ int clampi(int v, int lo, int hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+template <int CT, bool DGRAD, bool EX = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
     const float* __restrict__ x, const float* __restrict__ w,
     const float* __restrict__ bias, const float* __restrict__ in_scale,
@@ -77,6 +92,25 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
   const bool col_ok = lane < CV_TT + 2 && tcol >= 0 && tcol < W;
   auto fetch = [&](int ci0) {
     const int cg0 = ci0 + wave;
+    if constexpr (EX) {
+      int plane = (int)(HW * 4);
+      asm volatile("" : "+s"(plane));  // per-plane offsets stay per chunk, not hoisted
+      const __amdgpu_buffer_rsrc_t rx = buf_rsrc(xn);
+      const int tcl = clampi(tcol, 0, W - 1);
+#pragma unroll
+      for (int i = 0; i < NIR; ++i) {
+        const int rr = i >> 1, f = clampi(f0 - 1 + rr, 0, H - 1);
+        pin[i] = buf_ld(rx, (f * W + tcl) * 4, (cg0 + 4 * (i & 1)) * plane);
+      }
+      const int lc = lane < CT * 16 ? lane : CT * 16 - 1;
+#pragma unroll
+      for (int i = 0; i < NWR; ++i) {
+        const int tap = i >> 1, cg = cg0 + 4 * (i & 1);
+        pw[i] = DGRAD ? w[((int64_t)cg * Cout + lc) * 9 + (8 - tap)]
+                      : w[((int64_t)lc * Cin + cg) * 9 + tap];
+      }
+      return;
+    }
     const float* xb = xn + (int64_t)cg0 * HW + (int64_t)(f0 - 1) * W + tcol;
 #pragma unroll
     for (int i = 0; i < NIR; ++i) {
@@ -98,6 +132,23 @@ __global__ __launch_bounds__(256, 2) void conv3x3_fwd_mfma(
   };
   auto commit = [&](int ci0) {
     const int cg0 = ci0 + wave;
+    if constexpr (EX) {
+#pragma unroll
+      for (int i = 0; i < NIR; ++i) {
+        const int rr = i >> 1, ci = wave + 4 * (i & 1), cg = cg0 + 4 * (i & 1);
+        const int f = f0 - 1 + rr;
+        const bool ok = col_ok && f >= 0 && f < H;
+        float v = pin[i];
+        if (in_scale) v = fmaxf(fmaf(v, in_scale[cg], in_shift[cg]), 0.f);
+        if (lane < CV_TT + 2) s_in[ci * CV_PLANE + rr * CV_LDT + lane] = ok ? v : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < NWR; ++i) {
+        const int k = (i >> 1) * 8 + wave + 4 * (i & 1);
+        if (lane < CT * 16) s_w[k * L::LDW + lane] = pw[i];
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < NIR; ++i) {
       const int rr = i >> 1, ci = wave + 4 * (i & 1), cg = cg0 + 4 * (i & 1);
@@ -378,13 +429,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_wgrad_mfma(
 //    round trip per MFMA).
 // Same tiles, partial-slab format and deterministic reduction as
 // conv3x3_wgrad_mfma.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
-                                           0x00020000);
-}
-__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
 
 template <int CP, int CO>
 struct WgradT {
@@ -448,7 +492,6 @@ __global__ __launch_bounds__((WgradT<CP, CO>::NW * 64), (WgradT<CP, CO>::NW / 2)
     f0 = tf * WG_FT;
     t0 = tt * WG_TT;
   };
-  auto clampi = [](int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); };
   auto fetch = [&](int64_t tile) {
     int n, f0, t0;
     tile_coords(tile, n, f0, t0);
@@ -875,9 +918,17 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
     return small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
   dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
   const int ct = (Cout + 15) / 16;
-#define AINP_FWD(CTV)                                                           \
-  hipLaunchKernelGGL((conv3x3_fwd_mfma<CTV, DG>), grid, dim3(256), 0, s, x, w, \
-                     bias, sc, sh, y, stats, Cin, Cout, (int)H, (int)W)
+  const bool ex = Cin % CV_CK == 0 && Cout % 16 == 0 &&
+                  (int64_t)Cin * H * W * 4 < ((int64_t)1 << 31);
+#define AINP_FWD(CTV)                                                                  \
+  do {                                                                                 \
+    if (ex)                                                                            \
+      hipLaunchKernelGGL((conv3x3_fwd_mfma<CTV, DG, true>), grid, dim3(256), 0, s, x, w, \
+                         bias, sc, sh, y, stats, Cin, Cout, (int)H, (int)W);           \
+    else                                                                               \
+      hipLaunchKernelGGL((conv3x3_fwd_mfma<CTV, DG, false>), grid, dim3(256), 0, s, x, \
+                         w, bias, sc, sh, y, stats, Cin, Cout, (int)H, (int)W);        \
+  } while (0)
   switch (ct) {
     case 1: AINP_FWD(1); break;
     case 2: AINP_FWD(2); break;
