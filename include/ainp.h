@@ -139,6 +139,25 @@ int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
                   const float* const* bias1, const float* const* bias2,
                   int nptr, int64_t nstrided, int ksplit, void* stream);
 
+/* Same GEMM with a caller-provided workspace.  When the 128x128 tile grid
+ * would leave the resident workgroup slots unevenly filled (ksplit == 0 and
+ * K long), the work is split stream-K style into equal (tile, k) ranges;
+ * pieces of tiles that straddle two ranges go through the workspace and are
+ * summed in fixed order (deterministic).  ainp_gemm_f32_workspace returns the
+ * bytes needed (0 = the plain grid is used and workspace may be NULL); a
+ * smaller or NULL workspace silently selects the plain grid.  A workspace must
+ * not be shared by calls in flight on different streams. */
+size_t ainp_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int nptr,
+                               int64_t nstrided, int ksplit);
+int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
+                     const float* const* A, int64_t sam, int64_t sak,
+                     int64_t strideA, const float* const* B, int64_t sbk,
+                     int64_t sbn, int64_t strideB, float beta, float* const* C,
+                     int64_t scm, int64_t scn, int64_t strideC,
+                     const float* const* bias1, const float* const* bias2,
+                     int nptr, int64_t nstrided, int ksplit, void* workspace,
+                     size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* 3x3 / stride 1 / pad 1 convolution over [N, C, F, T] spectrogram tiles    */
 /* ------------------------------------------------------------------------ */

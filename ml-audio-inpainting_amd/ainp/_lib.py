@@ -41,6 +41,11 @@ _SIGS = {
     "ainp_gemm_f32": (c_int, [c_int64, c_int64, c_int64, c_float, PP, c_int64, c_int64,
                               c_int64, PP, c_int64, c_int64, c_int64, c_float, PP,
                               c_int64, c_int64, c_int64, PP, PP, c_int, c_int64, c_int, P]),
+    "ainp_gemm_f32_workspace": (c_size_t, [c_int64, c_int64, c_int64, c_int, c_int64, c_int]),
+    "ainp_gemm_f32_ws": (c_int, [c_int64, c_int64, c_int64, c_float, PP, c_int64, c_int64,
+                                 c_int64, PP, c_int64, c_int64, c_int64, c_float, PP,
+                                 c_int64, c_int64, c_int64, PP, PP, c_int, c_int64, c_int,
+                                 P, c_size_t, P]),
     "ainp_conv3x3_fwd_stat_parts": (c_int, [c_int64, c_int64, c_int64]),
     "ainp_conv3x3_fwd": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
                                  c_int64, P]),

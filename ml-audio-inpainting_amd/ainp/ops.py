@@ -155,12 +155,32 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
     ref = C[0]
     b1 = ptr_array([_p(t) for t in bias1]) if bias1 is not None else None
     b2 = ptr_array([_p(t) for t in bias2]) if bias2 is not None else None
-    call("ainp_gemm_f32", int(M), int(N), int(K), float(alpha),
+    st = _stream(ref if stream_of is None else stream_of)
+    ws, ws_bytes = _gemm_workspace(ref.device, st, int(M), int(N), int(K), nptr,
+                                   int(nstrided), int(ksplit))
+    call("ainp_gemm_f32_ws", int(M), int(N), int(K), float(alpha),
          ptr_array([t.data_ptr() for t in A]), int(sam), int(sak), int(strideA),
          ptr_array([t.data_ptr() for t in B]), int(sbk), int(sbn), int(strideB),
          float(beta), ptr_array([t.data_ptr() for t in C]), int(scm), int(scn),
-         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit),
-         _stream(ref if stream_of is None else stream_of))
+         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit), ws, ws_bytes, st)
+
+
+_GEMM_WS: dict = {}
+
+
+def _gemm_workspace(device, stream: int, M, N, K, nptr, nstrided, ksplit):
+    """Stream-K workspace (ainp_gemm_f32_workspace bytes), one buffer per
+    (device, stream) so concurrent streams never share it; (None, 0) when the
+    plain tile grid is used."""
+    need = int(_lib.lib.ainp_gemm_f32_workspace(M, N, K, nptr, nstrided, ksplit))
+    if need == 0:
+        return None, 0
+    key = (device.index, stream)
+    buf = _GEMM_WS.get(key)
+    if buf is None or buf.numel() * 4 < need:
+        buf = torch.empty((need + 3) // 4, device=device, dtype=torch.float32)
+        _GEMM_WS[key] = buf
+    return buf.data_ptr(), need
 
 
 def _chunks_for(K, tiles, target_blocks=512, min_rows=64):

@@ -254,6 +254,201 @@ __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_kernel(
     }
 }
 
+// ------------------------------------------------------------- stream-K
+// When the tile count does not fill the resident workgroup slots evenly (the
+// BLSTM layer-0 projections: 672 / 1032 tiles of 128x128 on 768 slots), a
+// persistent grid of exactly the resident slots splits the (batch, tile,
+// k-iteration) space into equal contiguous ranges.  Tiles whose whole K range
+// falls in one workgroup are written directly; a split tile's pieces go to a
+// workspace slot (first or last piece of the workgroup's range) and are summed
+// in workgroup (= k) order by gemm_streamk_fixup, so results are deterministic.
+// Logical workgroup ids are XCD-major (each XCD owns a contiguous range), and
+// tiles are ordered so that consecutive tiles share the larger operand panel.
+constexpr int SK_SLOTS = 768;   // 256 CUs x 3 resident workgroups
+
+struct SkGeom {
+  int64_t units, nk, tiles_m, tiles_n;
+  int nbatch, order, P;  // order 0: (tm, batch, tn); 1: (tn, batch, tm)
+};
+
+__device__ __forceinline__ void sk_decode(const SkGeom& g, int64_t t, int& b, int64_t& tm,
+                                          int64_t& tn) {
+  if (g.order == 0) {
+    tn = t % g.tiles_n;
+    b = (int)((t / g.tiles_n) % g.nbatch);
+    tm = t / (g.tiles_n * g.nbatch);
+  } else {
+    tm = t % g.tiles_m;
+    b = (int)((t / g.tiles_m) % g.nbatch);
+    tn = t / (g.tiles_m * g.nbatch);
+  }
+}
+__device__ __forceinline__ int64_t sk_u0(const SkGeom& g, int64_t L) { return g.units * L / g.P; }
+
+// full-tile epilogue (shared by the stream-K kernel and its fixup); get(idx)
+// returns accumulator idx = (i*2+j)*16 + r
+template <typename Get>
+__device__ __forceinline__ void sk_store(const GemmPtrs& ptrs, int b, int64_t m0, int64_t n0,
+                                         int64_t M, int64_t N, float alpha, float beta,
+                                         int64_t scm, int64_t scn, Get get) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+  float* C = ptrs.C[b % ptrs.nptr] + (int64_t)(b / ptrs.nptr) * ptrs.sC;
+  const float* bias1 = ptrs.bias1[b % ptrs.nptr];
+  const float* bias2 = ptrs.bias2[b % ptrs.nptr];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t n = n0 + wn + j * 32 + li;
+      if (n >= N) continue;
+      const float bv = (bias1 ? bias1[n] : 0.f) + (bias2 ? bias2[n] : 0.f);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) {
+          float* q = C + m * scm + n * scn;
+          float x = alpha * get((i * 2 + j) * 16 + r) + bv;
+          if (beta != 0.f) x += beta * *q;
+          *q = x;
+        }
+      }
+    }
+}
+
+template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+__global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_streamk(
+    int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda, int64_t ldb,
+    float beta, int64_t scm, int64_t scn, SkGeom g, float* __restrict__ ws) {
+  __shared__ __attribute__((aligned(16))) float smem[Img<AKC>::SIZE + Img<BKC>::SIZE];
+  float* As = smem;
+  float* Bs = smem + Img<AKC>::SIZE;
+  const int w = blockIdx.x;
+  const int64_t L = (int64_t)(w % 8) * (g.P / 8) + w / 8;
+  const int64_t u0 = sk_u0(g, L), u1 = sk_u0(g, L + 1);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+  TileLoader<AKC, AVEC> la;
+  TileLoader<BKC, BVEC> lb;
+
+  for (int64_t u = u0; u < u1;) {
+    const int64_t t = u / g.nk, kb = u % g.nk;
+    const int64_t ke = (g.nk - kb) < (u1 - u) ? g.nk : kb + (u1 - u);
+    int b;
+    int64_t tm, tn;
+    sk_decode(g, t, b, tm, tn);
+    const int64_t m0 = tm * BM, n0 = tn * BN;
+    const float* A = ptrs.A[b % ptrs.nptr] + (int64_t)(b / ptrs.nptr) * ptrs.sA;
+    const float* B = ptrs.B[b % ptrs.nptr] + (int64_t)(b / ptrs.nptr) * ptrs.sB;
+
+    f32x16v acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    __syncthreads();  // the previous segment's LDS reads are done
+    la.load(A, lda, m0, kb * BK, M, K);
+    lb.load(B, ldb, n0, kb * BK, N, K);
+    for (int64_t it = kb; it < ke; ++it) {
+      if (it > kb) __syncthreads();
+      la.store(As);
+      lb.store(Bs);
+      __syncthreads();
+      if (it + 1 < ke) {
+        la.load(A, lda, m0, (it + 1) * BK, M, K);
+        lb.load(B, ldb, n0, (it + 1) * BK, N, K);
+      }
+#pragma unroll
+      for (int kg = 0; kg < BK / 8; ++kg) {
+        float4 af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i] = Img<AKC>::frag(As, wm + i * 32 + li, kg, lh);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) bf[j] = Img<BKC>::frag(Bs, wn + j * 32 + li, kg, lh);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            acc[i][j] = mfma32(af[i].x, bf[j].x, acc[i][j]);
+            acc[i][j] = mfma32(af[i].y, bf[j].y, acc[i][j]);
+            acc[i][j] = mfma32(af[i].z, bf[j].z, acc[i][j]);
+            acc[i][j] = mfma32(af[i].w, bf[j].w, acc[i][j]);
+          }
+      }
+    }
+    if (kb == 0 && ke == g.nk) {
+      sk_store(ptrs, b, m0, n0, M, N, alpha, beta, scm, scn,
+               [&](int idx) { return acc[idx >> 5][(idx >> 4) & 1][idx & 15]; });
+    } else {
+      const int slot = (u == u0) ? 0 : 1;
+      float* q = ws + ((L * 2 + slot) * 64) * GEMM_THREADS + threadIdx.x;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) q[((i * 2 + j) * 16 + r) * GEMM_THREADS] = acc[i][j][r];
+    }
+    u += ke - kb;
+  }
+}
+
+// Sum the pieces of every split tile in workgroup order and apply the epilogue.
+__global__ __launch_bounds__(GEMM_THREADS) void gemm_streamk_fixup(
+    int64_t M, int64_t N, float alpha, GemmPtrs ptrs, float beta, int64_t scm, int64_t scn,
+    SkGeom g, const float* __restrict__ ws) {
+  const int64_t t = blockIdx.x;
+  const int64_t x0 = t * g.nk, x1 = x0 + g.nk - 1;  // first/last unit of the tile
+  auto owner = [&](int64_t x) {
+    int64_t L = x * g.P / g.units;
+    while (L > 0 && sk_u0(g, L) > x) --L;
+    while (sk_u0(g, L + 1) <= x) ++L;
+    return L;
+  };
+  const int64_t Lf = owner(x0), Ll = owner(x1);
+  if (Lf == Ll) return;  // written whole by its workgroup
+  float v[64];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) v[r] = 0.f;
+  for (int64_t L = Lf; L <= Ll; ++L) {
+    const int slot = sk_u0(g, L) >= x0 ? 0 : 1;
+    const float* q = ws + ((L * 2 + slot) * 64) * GEMM_THREADS + threadIdx.x;
+#pragma unroll
+    for (int r = 0; r < 64; ++r) v[r] += q[r * GEMM_THREADS];
+  }
+  int b;
+  int64_t tm, tn;
+  sk_decode(g, t, b, tm, tn);
+  sk_store(ptrs, b, tm * BM, tn * BN, M, N, alpha, beta, scm, scn,
+           [&](int idx) { return v[idx]; });
+}
+
+// Stream-K geometry for a non-split-K call, or P == 0 when the plain grid is
+// already balanced (>= 90 % of its last wave of resident slots filled) or K is
+// too short to amortise the fixup.
+static SkGeom streamk_geom(int64_t M, int64_t N, int64_t K, int64_t nb, int ksplit) {
+  SkGeom g{};
+  g.P = 0;
+  if (ksplit != 0 || nb > 65535) return g;
+  g.tiles_m = cdiv(M, BM);
+  g.tiles_n = cdiv(N, BN);
+  g.nk = cdiv(K, BK);
+  const int64_t tiles = g.tiles_m * g.tiles_n * nb;
+  if (g.nk < 64 || tiles < SK_SLOTS / 4) return g;
+  const int64_t waves = cdiv(tiles, SK_SLOTS);
+  if (tiles * 10 >= waves * SK_SLOTS * 9) return g;
+  g.units = tiles * g.nk;
+  g.nbatch = (int)nb;
+  g.order = g.tiles_n <= g.tiles_m ? 0 : 1;
+  g.P = SK_SLOTS;
+  return g;
+}
+
 template <bool AKC, bool BKC>
 static void launch_gemm(bool avec, bool bvec, dim3 grid, hipStream_t s,
                         int64_t M, int64_t N, int64_t K, float alpha,
@@ -277,6 +472,12 @@ static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 using namespace ainp;
 
+extern "C" size_t ainp_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int nptr,
+                                          int64_t nstrided, int ksplit) {
+  const SkGeom g = streamk_geom(M, N, K, (int64_t)nptr * nstrided, ksplit);
+  return g.P ? (size_t)g.P * 2 * 64 * GEMM_THREADS * sizeof(float) : 0;
+}
+
 extern "C" int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
                              const float* const* A, int64_t sam, int64_t sak,
                              int64_t strideA, const float* const* B,
@@ -286,6 +487,21 @@ extern "C" int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
                              const float* const* bias1,
                              const float* const* bias2, int nptr,
                              int64_t nstrided, int ksplit, void* stream) {
+  return ainp_gemm_f32_ws(M, N, K, alpha, A, sam, sak, strideA, B, sbk, sbn, strideB, beta, C,
+                          scm, scn, strideC, bias1, bias2, nptr, nstrided, ksplit, nullptr, 0,
+                          stream);
+}
+
+extern "C" int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
+                                const float* const* A, int64_t sam, int64_t sak,
+                                int64_t strideA, const float* const* B,
+                                int64_t sbk, int64_t sbn, int64_t strideB,
+                                float beta, float* const* C, int64_t scm,
+                                int64_t scn, int64_t strideC,
+                                const float* const* bias1,
+                                const float* const* bias2, int nptr,
+                                int64_t nstrided, int ksplit, void* workspace,
+                                size_t ws_bytes, void* stream) {
   if (M < 0 || N < 0 || K < 0 || nptr < 1 || nptr > 8 || nstrided < 1 ||
       !A || !B || !C)
     return record_msg("ainp_gemm_f32: bad argument");
@@ -324,6 +540,32 @@ extern "C" int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
   if (ksplit && nb > (1 << 20)) return record_msg("ainp_gemm_f32: too many segments");
   const int nseg = ksplit == 1 ? (int)nb : (ksplit == 2 ? (int)nstrided : 1);
   const int64_t tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
+  const SkGeom g = streamk_geom(M, N, K, nb, ksplit);
+  if (g.P && workspace && ws_bytes >= (size_t)g.P * 2 * 64 * GEMM_THREADS * sizeof(float)) {
+    hipStream_t s = as_stream(stream);
+    float* ws = reinterpret_cast<float*>(workspace);
+#define AINP_SK(AK, BK_, AV, BV)                                                            \
+  hipLaunchKernelGGL((gemm_f32_streamk<AK, BK_, AV, BV>), dim3(g.P), dim3(GEMM_THREADS), 0, s, \
+                     M, N, K, alpha, p, lda, ldb, beta, scm, scn, g, ws)
+#define AINP_SK2(AK, BK_)                               \
+  do {                                                  \
+    if (avec && bvec) AINP_SK(AK, BK_, true, true);     \
+    else if (avec) AINP_SK(AK, BK_, true, false);       \
+    else if (bvec) AINP_SK(AK, BK_, false, true);       \
+    else AINP_SK(AK, BK_, false, false);                \
+  } while (0)
+    if (akc && bkc) AINP_SK2(true, true);
+    else if (akc) AINP_SK2(true, false);
+    else if (bkc) AINP_SK2(false, true);
+    else AINP_SK2(false, false);
+#undef AINP_SK2
+#undef AINP_SK
+    int rc = check_launch("gemm_f32_streamk");
+    if (rc) return rc;
+    hipLaunchKernelGGL(gemm_streamk_fixup, dim3((unsigned)(g.units / g.nk)), dim3(GEMM_THREADS),
+                       0, s, M, N, alpha, p, beta, scm, scn, g, ws);
+    return check_launch("gemm_streamk_fixup");
+  }
   const unsigned gy = ksplit == 1 ? 1u : (ksplit == 2 ? (unsigned)nptr : (unsigned)nb);
   dim3 grid((unsigned)(tiles_m * tiles_n), gy);
   hipStream_t s = as_stream(stream);

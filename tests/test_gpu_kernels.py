@@ -161,6 +161,35 @@ def test_gemm_batched_bias_ksplit(ops):
     assert rel(C3.cpu(), 0.5 * (A[:2] @ B[:2]) + 2.0) < 1e-5
 
 
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_streamk(ops, ta, tb):
+    """Shapes whose 128x128 grid fills the resident slots unevenly take the
+    stream-K path (split tiles summed from the workspace in fixed order):
+    ragged edges, two pointer batches sharing A, bias + alpha/beta, and
+    bit-identical results on repeat (deterministic)."""
+    from ainp import _lib
+    g = torch.Generator().manual_seed(11)
+    M, N, K = 2000, 700, 2100            # 16 x 6 tiles x 2 batches = 192, nk = 66
+    assert _lib.lib.ainp_gemm_f32_workspace(M, N, K, 2, 1, 0) > 0
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(2, K, N, generator=g, dtype=torch.float64) * 0.5
+    bias = torch.randn(2, N, generator=g, dtype=torch.float64)
+    C0 = torch.randn(2, M, N, generator=g, dtype=torch.float64)
+    Ad = (A.t().contiguous() if ta else A).float().to(DEV)
+    Bd = [(B[i].t().contiguous() if tb else B[i]).float().to(DEV) for i in range(2)]
+    sam, sak = (1, M) if ta else (K, 1)
+    sbk, sbn = (1, K) if tb else (N, 1)
+    outs = []
+    for _ in range(2):
+        C = C0.float().to(DEV)
+        ops.gemm(M, N, K, [Ad, Ad], sam, sak, Bd, sbk, sbn, [C[0], C[1]], N, 1,
+                 alpha=0.75, beta=-0.5, bias1=[bias[0].float().to(DEV), bias[1].float().to(DEV)])
+        outs.append(C.cpu())
+    ref = 0.75 * (A @ B) - 0.5 * C0 + bias.view(2, 1, N)
+    assert rel(outs[0], ref) < 1e-5
+    assert torch.equal(outs[0], outs[1])
+
+
 # ------------------------------------------------------------------ conv
 def _act(x, sc, sh):
     if sc is None:
