@@ -35,6 +35,7 @@ import torch  # noqa: E402
 
 METRIC = "spectrogram-frames/sec/node (train step) + recon L1, CNNBLSTM @1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense bf16 MFMA (~2.5 PF)
 HBM_PEAK_GBS = 8000.0
 
 CFG = {
@@ -202,6 +203,14 @@ def main():
                 "traffic": traffic, "kernel": "gemm_f32_kernel (LSTM l0 input projection, "
                 f"M={M} N={8 * H} K={I}, both directions)", "avg_launch_ms": round(avg_s * 1e3, 4),
                 "flop_per_launch": flops}
+        if not ops.GEMM_EXACT:
+            # fp32-accurate three-piece bf16 split: 6 bf16 MFMA products per fp32
+            # product; its own instruction-stream ceiling is the dense bf16 peak / 6
+            roof.update({
+                "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross "
+                             "products on v_mfma_f32_32x32x16_bf16, f32 accumulate",
+                "executed_tflops": round(6 * achieved, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
+                "executed_frac": round(6 * achieved / BF16_MFMA_PEAK_TFLOPS, 4)})
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -146,7 +146,9 @@ int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
  * summed in fixed order (deterministic).  ainp_gemm_f32_workspace returns the
  * bytes needed (0 = the plain grid is used and workspace may be NULL); a
  * smaller or NULL workspace silently selects the plain grid.  A workspace must
- * not be shared by calls in flight on different streams. */
+ * not be shared by calls in flight on different streams.  Stream-K is used by
+ * the exact f32 main loop only (AINP_GEMM_EXACT_F32 below); the default split
+ * bf16 loop always runs the plain grid and ignores the workspace. */
 size_t ainp_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int nptr,
                                int64_t nstrided, int ksplit);
 int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
@@ -156,6 +158,22 @@ int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
                      int64_t scm, int64_t scn, int64_t strideC,
                      const float* const* bias1, const float* const* bias2,
                      int nptr, int64_t nstrided, int ksplit, void* workspace,
+                     size_t ws_bytes, void* stream);
+
+/* Same GEMM with a precision flag.  flags == 0 (what ainp_gemm_f32 and
+ * ainp_gemm_f32_ws use): each fp32 operand is split exactly into three bf16
+ * pieces and the six cross products of order >= 2^-16 are accumulated in f32
+ * on the bf16 MFMA (dropped terms <= ~2^-23 |a||b| per product, the level of
+ * f32 rounding); flags == AINP_GEMM_EXACT_F32: exact f32 MFMA (k-ordered fmaf
+ * chain). */
+#define AINP_GEMM_EXACT_F32 1
+int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
+                     const float* const* A, int64_t sam, int64_t sak,
+                     int64_t strideA, const float* const* B, int64_t sbk,
+                     int64_t sbn, int64_t strideB, float beta, float* const* C,
+                     int64_t scm, int64_t scn, int64_t strideC,
+                     const float* const* bias1, const float* const* bias2,
+                     int nptr, int64_t nstrided, int ksplit, int flags, void* workspace,
                      size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------ */

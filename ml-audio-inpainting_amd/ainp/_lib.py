@@ -46,6 +46,10 @@ _SIGS = {
                                  c_int64, PP, c_int64, c_int64, c_int64, c_float, PP,
                                  c_int64, c_int64, c_int64, PP, PP, c_int, c_int64, c_int,
                                  P, c_size_t, P]),
+    "ainp_gemm_f32_ex": (c_int, [c_int64, c_int64, c_int64, c_float, PP, c_int64, c_int64,
+                                 c_int64, PP, c_int64, c_int64, c_int64, c_float, PP,
+                                 c_int64, c_int64, c_int64, PP, PP, c_int, c_int64, c_int,
+                                 c_int, P, c_size_t, P]),
     "ainp_conv3x3_fwd_stat_parts": (c_int, [c_int64, c_int64, c_int64]),
     "ainp_conv3x3_fwd": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
                                  c_int64, P]),

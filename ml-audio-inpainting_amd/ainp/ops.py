@@ -8,6 +8,7 @@ package uses to compute; nothing here falls back to ATen or the CPU.
 from __future__ import annotations
 
 import functools
+import os
 import math
 import weakref
 from ctypes import c_int as ctypes_int
@@ -144,11 +145,19 @@ def stft(audio: torch.Tensor, n_fft: int = 2048, hop_length: int = 512,
 
 
 # --------------------------------------------------------------------- GEMM
+# ainp_gemm_f32_ex precision: False (default) = fp32-accurate three-piece bf16
+# split on the bf16 MFMA (include/ainp.h); True = exact f32 MFMA.  The
+# AINP_GEMM_EXACT=1 environment variable selects the exact path process-wide.
+GEMM_EXACT = os.environ.get("AINP_GEMM_EXACT", "0") == "1"
+GEMM_EXACT_F32 = 1
+
+
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
          strideA=0, strideB=0, strideC=0, bias1=None, bias2=None, nstrided=1,
-         ksplit=False, stream_of=None):
-    """Raw strided/batched GEMM (ainp_gemm_f32).  A, B, C, bias1, bias2 are
-    lists (pointer batches) of cuda float32 tensors (views allowed) or None."""
+         ksplit=False, stream_of=None, exact=None):
+    """Raw strided/batched GEMM (ainp_gemm_f32_ex).  A, B, C, bias1, bias2 are
+    lists (pointer batches) of cuda float32 tensors (views allowed) or None.
+    exact: None -> GEMM_EXACT; True -> exact f32 MFMA; False -> bf16x6 split."""
     A = list(A); B = list(B); C = list(C)
     nptr = len(A)
     assert len(B) == nptr and len(C) == nptr and 1 <= nptr <= 8
@@ -156,13 +165,15 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
     b1 = ptr_array([_p(t) for t in bias1]) if bias1 is not None else None
     b2 = ptr_array([_p(t) for t in bias2]) if bias2 is not None else None
     st = _stream(ref if stream_of is None else stream_of)
-    ws, ws_bytes = _gemm_workspace(ref.device, st, int(M), int(N), int(K), nptr,
-                                   int(nstrided), int(ksplit))
-    call("ainp_gemm_f32_ws", int(M), int(N), int(K), float(alpha),
+    exact = GEMM_EXACT if exact is None else bool(exact)
+    ws, ws_bytes = (_gemm_workspace(ref.device, st, int(M), int(N), int(K), nptr,
+                                    int(nstrided), int(ksplit)) if exact else (None, 0))
+    call("ainp_gemm_f32_ex", int(M), int(N), int(K), float(alpha),
          ptr_array([t.data_ptr() for t in A]), int(sam), int(sak), int(strideA),
          ptr_array([t.data_ptr() for t in B]), int(sbk), int(sbn), int(strideB),
          float(beta), ptr_array([t.data_ptr() for t in C]), int(scm), int(scn),
-         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit), ws, ws_bytes, st)
+         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit),
+         GEMM_EXACT_F32 if exact else 0, ws, ws_bytes, st)
 
 
 _GEMM_WS: dict = {}

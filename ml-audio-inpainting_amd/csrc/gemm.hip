@@ -1,17 +1,30 @@
-// gemm.hip — strided / batched fp32 GEMM on gfx950 f32-input MFMA.
+// gemm.hip — strided / batched fp32 GEMM on gfx950 MFMA.
 //
 // Replaces the ATen GEMMs behind nn.LSTM input projections and nn.Linear of
-// models/CNNBLSTM/model.py:46-50,77,80 (forward and backward).  Arithmetic is
-// exact f32 (v_mfma_f32_32x32x2_f32 = k-ordered fmaf chain, MI355X_MICROARCH
-// "Matrix cores"), matching the reference's fp32 numerics up to summation order.
+// models/CNNBLSTM/model.py:46-50,77,80 (forward and backward).  Two main loops
+// share the tiling, batching, stream-K and epilogue code:
+//
+//  * x6 (default): each fp32 operand element is split EXACTLY into three bf16
+//    pieces x = x0 + x1 + x2 (round-to-nearest at each step, |x1| <= 2^-8|x|,
+//    |x2| <= 2^-16|x|) while it is staged into LDS, and a*b is accumulated as
+//    the six cross terms of order >= 2^-16 (a2b0 + a1b1 + a0b2 + a1b0 + a0b1 +
+//    a0b0, smallest first) on v_mfma_f32_32x32x16_bf16 with f32 accumulation.
+//    The dropped terms are <= ~2^-23|ab|, the level of f32 rounding, so results
+//    are fp32-accurate (tests/test_gpu_kernels.py checks both paths against
+//    fp64); the bf16 MFMA rate (16x f32) leaves 2.7x of f32 headroom.
+//  * exact (AINP_GEMM_EXACT_F32): v_mfma_f32_32x32x2_f32, an exact k-ordered
+//    fmaf chain (MI355X_MICROARCH "Matrix cores").
 //
 // Tiling: 128x128 output tile per 256-thread workgroup (4 waves as 2x2, each
-// wave 64x64 = 2x2 MFMA 32x32 tiles, 64 accumulator VGPRs), K-tile 32, one
-// LDS image per operand with the next K-tile prefetched in registers.
-// k-contiguous operands keep a [row][k] image (16-byte stores, one
-// ds_read_b128 = 4 MFMA k-steps per lane); row-contiguous operands a [k][row]
-// image.  The MFMA k order inside an 8-k group is lane-half h -> k = 4h+e,
-// identical for A and B, so the sum over k is unchanged.
+// wave 64x64 = 2x2 MFMA 32x32 tiles, 64 accumulator VGPRs), one LDS image per
+// operand with the next K-tile prefetched in registers.
+//  exact: K-tile 32; k-contiguous operands keep a [row][k] f32 image (16-byte
+//    stores, one ds_read_b128 = 4 MFMA k-steps per lane), row-contiguous
+//    operands a [k][row] image.  The k order inside an 8-k group is lane-half
+//    h -> k = 4h+e, identical for A and B, so the sum over k is unchanged.
+//  x6: K-tile 16; three bf16 planes [row][16 k] per operand with 48-byte rows
+//    (conflict-free ds_read_b128 fragments: lane (r, h) reads k = 8h..8h+7 of
+//    row r, the 32x32x16 operand map, identical for A and B).
 #include "common.h"
 
 namespace ainp {
@@ -31,9 +44,13 @@ struct GemmPtrs {
 };
 
 typedef float f32x16v __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ f32x16v mfma32(float a, float b, f32x16v c) {
   return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x16v mfma32bf(bf16x8v a, bf16x8v b, f32x16v c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
 }
 
 // Load a 128xBK operand tile (128 rows along m or n, BK along k) into
@@ -121,15 +138,205 @@ struct Img {
   }
 };
 
-// Single-buffered LDS + one K-tile of register prefetch: 36 KB of LDS and
-// <=168 VGPRs -> 3 workgroups per CU (768 resident tiles on the chip).
+// ======================================================= x6 (split bf16) path
+namespace x6 {
+constexpr int KT = 16;            // K-tile
+constexpr int RS = 48;            // bytes per image row: 16 bf16 + 16 B pad
+constexpr int PLANE = 128 * RS;   // one bf16 plane of a 128-row operand tile
+constexpr int IMG = 3 * PLANE;    // three planes
+
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+__device__ __forceinline__ float bf_lo(uint32_t p) { return __uint_as_float(p << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 0xffff0000u); }
+
+// exact three-way split of (a, b) into packed bf16 pairs p0 + p1 + p2
+__device__ __forceinline__ void split2(float a, float b, uint32_t& p0, uint32_t& p1,
+                                       uint32_t& p2) {
+  p0 = cvt_pk_bf16(a, b);
+  const float ra = a - bf_lo(p0), rb = b - bf_hi(p0);
+  p1 = cvt_pk_bf16(ra, rb);
+  const float sa = ra - bf_lo(p1), sb = rb - bf_hi(p1);
+  p2 = cvt_pk_bf16(sa, sb);
+}
+
+// 128 x 16 fp32 operand tile -> registers -> split -> three LDS planes.
+//  KC: thread = one row x 4 consecutive k (two float4 per thread);
+//  MC: thread = 4 consecutive rows x 2 consecutive k (one float4 per k), so the
+//      4-row vector is transposed in registers into per-row k pairs.
+template <bool KC, bool VEC>
+struct Loader {
+  float4 v[2];
+
+  __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld, int64_t r0,
+                                       int64_t k0, int64_t R, int64_t K) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (KC) {
+        const int idx = tid + i * GEMM_THREADS;
+        const int64_t gr = r0 + (idx >> 2), gk = k0 + (idx & 3) * 4;
+        if (gr < R) {
+          const float* q = p + gr * ld + gk;
+          if (VEC) {
+            if (gk < K) x = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (gk + 0 < K) x.x = q[0];
+            if (gk + 1 < K) x.y = q[1];
+            if (gk + 2 < K) x.z = q[2];
+            if (gk + 3 < K) x.w = q[3];
+          }
+        }
+      } else {
+        const int64_t gk = k0 + 2 * (tid & 7) + i, gr = r0 + 4 * (tid >> 3);
+        if (gk < K) {
+          const float* q = p + gk * ld + gr;
+          if (VEC) {
+            if (gr < R) x = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (gr + 0 < R) x.x = q[0];
+            if (gr + 1 < R) x.y = q[1];
+            if (gr + 2 < R) x.z = q[2];
+            if (gr + 3 < R) x.w = q[3];
+          }
+        }
+      }
+      v[i] = x;
+    }
+  }
+
+  __device__ __forceinline__ void store(unsigned char* img) const {
+    const int tid = threadIdx.x;
+    if (KC) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int idx = tid + i * GEMM_THREADS;
+        uint32_t a0, a1, a2, b0, b1, b2;
+        split2(v[i].x, v[i].y, a0, a1, a2);
+        split2(v[i].z, v[i].w, b0, b1, b2);
+        unsigned char* q = img + (idx >> 2) * RS + (idx & 3) * 8;
+        *reinterpret_cast<uint2*>(q) = make_uint2(a0, b0);
+        *reinterpret_cast<uint2*>(q + PLANE) = make_uint2(a1, b1);
+        *reinterpret_cast<uint2*>(q + 2 * PLANE) = make_uint2(a2, b2);
+      }
+    } else {
+      const float* f0 = reinterpret_cast<const float*>(&v[0]);
+      const float* f1 = reinterpret_cast<const float*>(&v[1]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t a0, a1, a2;
+        split2(f0[j], f1[j], a0, a1, a2);
+        unsigned char* q = img + (4 * (tid >> 3) + j) * RS + (tid & 7) * 4;
+        *reinterpret_cast<uint32_t*>(q) = a0;
+        *reinterpret_cast<uint32_t*>(q + PLANE) = a1;
+        *reinterpret_cast<uint32_t*>(q + 2 * PLANE) = a2;
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x8v frag(const unsigned char* img, int plane, int row, int h) {
+  const uint4 u = *reinterpret_cast<const uint4*>(img + plane * PLANE + row * RS + 16 * h);
+  return __builtin_bit_cast(bf16x8v, u);
+}
+}  // namespace x6
+
+// ===================================================== main-loop policies
+// Exact f32 path: K-tile 32, f32 images, 32x32x2 f32 MFMA.
 template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+struct PolF32 {
+  static constexpr int KT = BK;
+  static constexpr int A_BYTES = Img<AKC>::SIZE * 4, B_BYTES = Img<BKC>::SIZE * 4;
+  static constexpr int SMEM = A_BYTES + B_BYTES;
+  using LA = TileLoader<AKC, AVEC>;
+  using LB = TileLoader<BKC, BVEC>;
+  __device__ static __forceinline__ void store(const LA& la, const LB& lb, unsigned char* sm) {
+    la.store(reinterpret_cast<float*>(sm));
+    lb.store(reinterpret_cast<float*>(sm + A_BYTES));
+  }
+  __device__ static __forceinline__ void compute(const unsigned char* sm, f32x16v (&acc)[2][2],
+                                                 int wm, int wn, int li, int lh) {
+    const float* As = reinterpret_cast<const float*>(sm);
+    const float* Bs = reinterpret_cast<const float*>(sm + A_BYTES);
+#pragma unroll
+    for (int kg = 0; kg < BK / 8; ++kg) {
+      float4 af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = Img<AKC>::frag(As, wm + i * 32 + li, kg, lh);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Img<BKC>::frag(Bs, wn + j * 32 + li, kg, lh);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = mfma32(af[i].x, bf[j].x, acc[i][j]);
+          acc[i][j] = mfma32(af[i].y, bf[j].y, acc[i][j]);
+          acc[i][j] = mfma32(af[i].z, bf[j].z, acc[i][j]);
+          acc[i][j] = mfma32(af[i].w, bf[j].w, acc[i][j]);
+        }
+    }
+  }
+};
+
+// x6 path: K-tile 16, three bf16 planes per operand, six 32x32x16 bf16 MFMAs.
+template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+struct PolX6 {
+  static constexpr int KT = x6::KT;
+  static constexpr int SMEM = 2 * x6::IMG;
+  using LA = x6::Loader<AKC, AVEC>;
+  using LB = x6::Loader<BKC, BVEC>;
+  __device__ static __forceinline__ void store(const LA& la, const LB& lb, unsigned char* sm) {
+    la.store(sm);
+    lb.store(sm + x6::IMG);
+  }
+  __device__ static __forceinline__ void compute(const unsigned char* sm, f32x16v (&acc)[2][2],
+                                                 int wm, int wn, int li, int lh) {
+    bf16x8v a[3][2], b[3][2];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[p][i] = x6::frag(sm, p, wm + i * 32 + li, lh);
+        b[p][i] = x6::frag(sm + x6::IMG, p, wn + i * 32 + li, lh);
+      }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16v c = acc[i][j];
+        c = mfma32bf(a[2][i], b[0][j], c);
+        c = mfma32bf(a[1][i], b[1][j], c);
+        c = mfma32bf(a[0][i], b[2][j], c);
+        c = mfma32bf(a[1][i], b[0][j], c);
+        c = mfma32bf(a[0][i], b[1][j], c);
+        c = mfma32bf(a[0][i], b[0][j], c);
+        acc[i][j] = c;
+      }
+  }
+};
+
+template <bool X6, bool AKC, bool BKC, bool AVEC, bool BVEC>
+struct PolSel {
+  using type = PolF32<AKC, BKC, AVEC, BVEC>;
+};
+template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+struct PolSel<true, AKC, BKC, AVEC, BVEC> {
+  using type = PolX6<AKC, BKC, AVEC, BVEC>;
+};
+
+// ================================================================ tile grid
+// Single-buffered LDS + one K-tile of register prefetch: <= 37 KB of LDS and
+// <= 168 VGPRs -> 3 workgroups per CU (768 resident tiles on the chip).
+template <bool X6, bool AKC, bool BKC, bool AVEC, bool BVEC>
 __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_kernel(
     int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda,
     int64_t ldb, float beta, int64_t scm, int64_t scn, int nseg, int tiles_n) {
-  __shared__ __attribute__((aligned(16))) float smem[Img<AKC>::SIZE + Img<BKC>::SIZE];
-  float* As = smem;
-  float* Bs = smem + Img<AKC>::SIZE;
+  using Pol = typename PolSel<X6, AKC, BKC, AVEC, BVEC>::type;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[Pol::SMEM];
 
   // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs,
   // so remap bid -> linear tile L giving each XCD a contiguous range of L
@@ -165,17 +372,17 @@ __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_kernel(
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  TileLoader<AKC, AVEC> la;
-  TileLoader<BKC, BVEC> lb;
-  const int64_t nk = (K + BK - 1) / BK;
+  typename Pol::LA la;
+  typename Pol::LB lb;
+  const int64_t nk = (K + Pol::KT - 1) / Pol::KT;
   const int64_t total = nk * nseg;
 
   // ksplit mode 1 (nseg = all batches): batch index = segment; mode 2
   // (nseg = nstrided, grid.y = pointer batch): segment walks the strided
-  // batches of this block's pointer batch.
+  // batches of this block's pointer batch.  The (segment, k) position is kept
+  // as counters so the main loop has no integer division.
   const bool per_ptr = ptrs.ksplit_mode == 2;
-  auto seg_ptr = [&](int64_t it, const float*& a, const float*& b, int64_t& k0) {
-    const int seg = (int)(it / nk);
+  auto seg_base = [&](int seg, const float*& a, const float*& b) {
     int pb, sb;
     if (per_ptr) {
       pb = batch;
@@ -187,46 +394,29 @@ __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_kernel(
     }
     a = ptrs.A[pb] + sb * ptrs.sA;
     b = ptrs.B[pb] + sb * ptrs.sB;
-    k0 = (it % nk) * BK;
   };
 
-  {
-    const float *a, *b;
-    int64_t k0;
-    seg_ptr(0, a, b, k0);
-    la.load(a, lda, m0, k0, M, K);
-    lb.load(b, ldb, n0, k0, N, K);
-  }
+  const float *pa, *pb;
+  seg_base(0, pa, pb);
+  int seg = 0;
+  int64_t k0 = 0;  // k offset of the tile in registers (prefetched next)
+  la.load(pa, lda, m0, 0, M, K);
+  lb.load(pb, ldb, n0, 0, N, K);
 
   for (int64_t it = 0; it < total; ++it) {
     if (it > 0) __syncthreads();  // every wave is done reading the LDS images
-    la.store(As);
-    lb.store(Bs);
+    Pol::store(la, lb, smem);
     __syncthreads();
     if (it + 1 < total) {  // next K-tile's loads fly during this tile's MFMAs
-      const float *a, *b;
-      int64_t k0;
-      seg_ptr(it + 1, a, b, k0);
-      la.load(a, lda, m0, k0, M, K);
-      lb.load(b, ldb, n0, k0, N, K);
+      k0 += Pol::KT;
+      if (k0 >= K) {
+        k0 = 0;
+        seg_base(++seg, pa, pb);
+      }
+      la.load(pa, lda, m0, k0, M, K);
+      lb.load(pb, ldb, n0, k0, N, K);
     }
-#pragma unroll
-    for (int kg = 0; kg < BK / 8; ++kg) {
-      float4 af[2], bf[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = Img<AKC>::frag(As, wm + i * 32 + li, kg, lh);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) bf[j] = Img<BKC>::frag(Bs, wn + j * 32 + li, kg, lh);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = mfma32(af[i].x, bf[j].x, acc[i][j]);
-          acc[i][j] = mfma32(af[i].y, bf[j].y, acc[i][j]);
-          acc[i][j] = mfma32(af[i].z, bf[j].z, acc[i][j]);
-          acc[i][j] = mfma32(af[i].w, bf[j].w, acc[i][j]);
-        }
-    }
+    Pol::compute(smem, acc, wm, wn, li, lh);
   }
 
   // epilogue: D[row=(r&3)+8*(r>>2)+4*lh][col=li] of each 32x32 tile
@@ -317,21 +507,20 @@ __device__ __forceinline__ void sk_store(const GemmPtrs& ptrs, int b, int64_t m0
     }
 }
 
-template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+template <bool X6, bool AKC, bool BKC, bool AVEC, bool BVEC>
 __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_streamk(
     int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda, int64_t ldb,
     float beta, int64_t scm, int64_t scn, SkGeom g, float* __restrict__ ws) {
-  __shared__ __attribute__((aligned(16))) float smem[Img<AKC>::SIZE + Img<BKC>::SIZE];
-  float* As = smem;
-  float* Bs = smem + Img<AKC>::SIZE;
+  using Pol = typename PolSel<X6, AKC, BKC, AVEC, BVEC>::type;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[Pol::SMEM];
   const int w = blockIdx.x;
   const int64_t L = (int64_t)(w % 8) * (g.P / 8) + w / 8;
   const int64_t u0 = sk_u0(g, L), u1 = sk_u0(g, L + 1);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
   const int li = lane & 31, lh = lane >> 5;
-  TileLoader<AKC, AVEC> la;
-  TileLoader<BKC, BVEC> lb;
+  typename Pol::LA la;
+  typename Pol::LB lb;
 
   for (int64_t u = u0; u < u1;) {
     const int64_t t = u / g.nk, kb = u % g.nk;
@@ -352,34 +541,17 @@ __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_streamk(
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
     __syncthreads();  // the previous segment's LDS reads are done
-    la.load(A, lda, m0, kb * BK, M, K);
-    lb.load(B, ldb, n0, kb * BK, N, K);
+    la.load(A, lda, m0, kb * Pol::KT, M, K);
+    lb.load(B, ldb, n0, kb * Pol::KT, N, K);
     for (int64_t it = kb; it < ke; ++it) {
       if (it > kb) __syncthreads();
-      la.store(As);
-      lb.store(Bs);
+      Pol::store(la, lb, smem);
       __syncthreads();
       if (it + 1 < ke) {
-        la.load(A, lda, m0, (it + 1) * BK, M, K);
-        lb.load(B, ldb, n0, (it + 1) * BK, N, K);
+        la.load(A, lda, m0, (it + 1) * Pol::KT, M, K);
+        lb.load(B, ldb, n0, (it + 1) * Pol::KT, N, K);
       }
-#pragma unroll
-      for (int kg = 0; kg < BK / 8; ++kg) {
-        float4 af[2], bf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) af[i] = Img<AKC>::frag(As, wm + i * 32 + li, kg, lh);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) bf[j] = Img<BKC>::frag(Bs, wn + j * 32 + li, kg, lh);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            acc[i][j] = mfma32(af[i].x, bf[j].x, acc[i][j]);
-            acc[i][j] = mfma32(af[i].y, bf[j].y, acc[i][j]);
-            acc[i][j] = mfma32(af[i].z, bf[j].z, acc[i][j]);
-            acc[i][j] = mfma32(af[i].w, bf[j].w, acc[i][j]);
-          }
-      }
+      Pol::compute(smem, acc, wm, wn, li, lh);
     }
     if (kb == 0 && ke == g.nk) {
       sk_store(ptrs, b, m0, n0, M, N, alpha, beta, scm, scn,
@@ -430,16 +602,16 @@ __global__ __launch_bounds__(GEMM_THREADS) void gemm_streamk_fixup(
 
 // Stream-K geometry for a non-split-K call, or P == 0 when the plain grid is
 // already balanced (>= 90 % of its last wave of resident slots filled) or K is
-// too short to amortise the fixup.
-static SkGeom streamk_geom(int64_t M, int64_t N, int64_t K, int64_t nb, int ksplit) {
+// too short (< 2048) to amortise the fixup.  kt: the main loop's K-tile.
+static SkGeom streamk_geom(int64_t M, int64_t N, int64_t K, int64_t nb, int ksplit, int kt) {
   SkGeom g{};
   g.P = 0;
   if (ksplit != 0 || nb > 65535) return g;
   g.tiles_m = cdiv(M, BM);
   g.tiles_n = cdiv(N, BN);
-  g.nk = cdiv(K, BK);
+  g.nk = cdiv(K, kt);
   const int64_t tiles = g.tiles_m * g.tiles_n * nb;
-  if (g.nk < 64 || tiles < SK_SLOTS / 4) return g;
+  if (K < 64 * BK || tiles < SK_SLOTS / 4) return g;
   const int64_t waves = cdiv(tiles, SK_SLOTS);
   if (tiles * 10 >= waves * SK_SLOTS * 9) return g;
   g.units = tiles * g.nk;
@@ -449,14 +621,14 @@ static SkGeom streamk_geom(int64_t M, int64_t N, int64_t K, int64_t nb, int kspl
   return g;
 }
 
-template <bool AKC, bool BKC>
+template <bool X6, bool AKC, bool BKC>
 static void launch_gemm(bool avec, bool bvec, dim3 grid, hipStream_t s,
                         int64_t M, int64_t N, int64_t K, float alpha,
                         const GemmPtrs& p, int64_t lda, int64_t ldb,
                         float beta, int64_t scm, int64_t scn, int nseg,
                         int tiles_n) {
 #define AINP_GEMM_LAUNCH(AV, BV)                                             \
-  hipLaunchKernelGGL((gemm_f32_kernel<AKC, BKC, AV, BV>), grid,             \
+  hipLaunchKernelGGL((gemm_f32_kernel<X6, AKC, BKC, AV, BV>), grid,         \
                      dim3(GEMM_THREADS), 0, s, M, N, K, alpha, p, lda, ldb, \
                      beta, scm, scn, nseg, tiles_n)
   if (avec && bvec) AINP_GEMM_LAUNCH(true, true);
@@ -466,15 +638,53 @@ static void launch_gemm(bool avec, bool bvec, dim3 grid, hipStream_t s,
 #undef AINP_GEMM_LAUNCH
 }
 
+template <bool X6, bool AKC, bool BKC>
+static void launch_streamk(bool avec, bool bvec, hipStream_t s, int64_t M, int64_t N, int64_t K,
+                           float alpha, const GemmPtrs& p, int64_t lda, int64_t ldb, float beta,
+                           int64_t scm, int64_t scn, const SkGeom& g, float* ws) {
+#define AINP_SK(AV, BV)                                                                       \
+  hipLaunchKernelGGL((gemm_f32_streamk<X6, AKC, BKC, AV, BV>), dim3(g.P), dim3(GEMM_THREADS), \
+                     0, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, g, ws)
+  if (avec && bvec) AINP_SK(true, true);
+  else if (avec) AINP_SK(true, false);
+  else if (bvec) AINP_SK(false, true);
+  else AINP_SK(false, false);
+#undef AINP_SK
+}
+
+// layout dispatch for both main loops: streamk selects the persistent kernel
+template <bool X6>
+static void dispatch_gemm(bool streamk, bool akc, bool bkc, bool avec, bool bvec, dim3 grid,
+                          hipStream_t s, int64_t M, int64_t N, int64_t K, float alpha,
+                          const GemmPtrs& p, int64_t lda, int64_t ldb, float beta, int64_t scm,
+                          int64_t scn, int nseg, int tiles_n, const SkGeom& g, float* ws) {
+#define AINP_DISPATCH(AK, BK_)                                                                 \
+  do {                                                                                         \
+    if (streamk)                                                                               \
+      launch_streamk<X6, AK, BK_>(avec, bvec, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, \
+                                  g, ws);                                                      \
+    else                                                                                       \
+      launch_gemm<X6, AK, BK_>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm,   \
+                               scn, nseg, tiles_n);                                           \
+  } while (0)
+  if (akc && bkc) AINP_DISPATCH(true, true);
+  else if (akc) AINP_DISPATCH(true, false);
+  else if (bkc) AINP_DISPATCH(false, true);
+  else AINP_DISPATCH(false, false);
+#undef AINP_DISPATCH
+}
+
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace ainp
 
 using namespace ainp;
 
+
 extern "C" size_t ainp_gemm_f32_workspace(int64_t M, int64_t N, int64_t K, int nptr,
                                           int64_t nstrided, int ksplit) {
-  const SkGeom g = streamk_geom(M, N, K, (int64_t)nptr * nstrided, ksplit);
+  // the same decision for both main loops (it depends on K, not on the K-tile)
+  const SkGeom g = streamk_geom(M, N, K, (int64_t)nptr * nstrided, ksplit, BK);
   return g.P ? (size_t)g.P * 2 * 64 * GEMM_THREADS * sizeof(float) : 0;
 }
 
@@ -487,8 +697,8 @@ extern "C" int ainp_gemm_f32(int64_t M, int64_t N, int64_t K, float alpha,
                              const float* const* bias1,
                              const float* const* bias2, int nptr,
                              int64_t nstrided, int ksplit, void* stream) {
-  return ainp_gemm_f32_ws(M, N, K, alpha, A, sam, sak, strideA, B, sbk, sbn, strideB, beta, C,
-                          scm, scn, strideC, bias1, bias2, nptr, nstrided, ksplit, nullptr, 0,
+  return ainp_gemm_f32_ex(M, N, K, alpha, A, sam, sak, strideA, B, sbk, sbn, strideB, beta, C,
+                          scm, scn, strideC, bias1, bias2, nptr, nstrided, ksplit, 0, nullptr, 0,
                           stream);
 }
 
@@ -502,9 +712,25 @@ extern "C" int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
                                 const float* const* bias2, int nptr,
                                 int64_t nstrided, int ksplit, void* workspace,
                                 size_t ws_bytes, void* stream) {
+  return ainp_gemm_f32_ex(M, N, K, alpha, A, sam, sak, strideA, B, sbk, sbn, strideB, beta, C,
+                          scm, scn, strideC, bias1, bias2, nptr, nstrided, ksplit, 0, workspace,
+                          ws_bytes, stream);
+}
+
+extern "C" int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
+                                const float* const* A, int64_t sam, int64_t sak,
+                                int64_t strideA, const float* const* B,
+                                int64_t sbk, int64_t sbn, int64_t strideB,
+                                float beta, float* const* C, int64_t scm,
+                                int64_t scn, int64_t strideC,
+                                const float* const* bias1,
+                                const float* const* bias2, int nptr,
+                                int64_t nstrided, int ksplit, int flags, void* workspace,
+                                size_t ws_bytes, void* stream) {
   if (M < 0 || N < 0 || K < 0 || nptr < 1 || nptr > 8 || nstrided < 1 ||
       !A || !B || !C)
     return record_msg("ainp_gemm_f32: bad argument");
+  if (flags & ~AINP_GEMM_EXACT_F32) return record_msg("ainp_gemm_f32: unknown flags");
   if (sam != 1 && sak != 1) return record_msg("ainp_gemm_f32: A needs a unit stride");
   if (sbk != 1 && sbn != 1) return record_msg("ainp_gemm_f32: B needs a unit stride");
   if (scm != 1 && scn != 1) return record_msg("ainp_gemm_f32: C needs a unit stride");
@@ -524,6 +750,7 @@ extern "C" int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
   p.sC = strideC;
   p.nptr = nptr;
   p.ksplit_mode = ksplit;
+  const bool use_x6 = !(flags & AINP_GEMM_EXACT_F32);
   // contiguous dimension of each operand (prefer k when both strides are 1)
   const bool akc = (sak == 1);
   const bool bkc = (sbk == 1);
@@ -540,42 +767,25 @@ extern "C" int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
   if (ksplit && nb > (1 << 20)) return record_msg("ainp_gemm_f32: too many segments");
   const int nseg = ksplit == 1 ? (int)nb : (ksplit == 2 ? (int)nstrided : 1);
   const int64_t tiles_m = cdiv(M, BM), tiles_n = cdiv(N, BN);
-  const SkGeom g = streamk_geom(M, N, K, nb, ksplit);
-  if (g.P && workspace && ws_bytes >= (size_t)g.P * 2 * 64 * GEMM_THREADS * sizeof(float)) {
-    hipStream_t s = as_stream(stream);
-    float* ws = reinterpret_cast<float*>(workspace);
-#define AINP_SK(AK, BK_, AV, BV)                                                            \
-  hipLaunchKernelGGL((gemm_f32_streamk<AK, BK_, AV, BV>), dim3(g.P), dim3(GEMM_THREADS), 0, s, \
-                     M, N, K, alpha, p, lda, ldb, beta, scm, scn, g, ws)
-#define AINP_SK2(AK, BK_)                               \
-  do {                                                  \
-    if (avec && bvec) AINP_SK(AK, BK_, true, true);     \
-    else if (avec) AINP_SK(AK, BK_, true, false);       \
-    else if (bvec) AINP_SK(AK, BK_, false, true);       \
-    else AINP_SK(AK, BK_, false, false);                \
-  } while (0)
-    if (akc && bkc) AINP_SK2(true, true);
-    else if (akc) AINP_SK2(true, false);
-    else if (bkc) AINP_SK2(false, true);
-    else AINP_SK2(false, false);
-#undef AINP_SK2
-#undef AINP_SK
-    int rc = check_launch("gemm_f32_streamk");
-    if (rc) return rc;
-    hipLaunchKernelGGL(gemm_streamk_fixup, dim3((unsigned)(g.units / g.nk)), dim3(GEMM_THREADS),
-                       0, s, M, N, alpha, p, beta, scm, scn, g, ws);
-    return check_launch("gemm_streamk_fixup");
-  }
-  const unsigned gy = ksplit == 1 ? 1u : (ksplit == 2 ? (unsigned)nptr : (unsigned)nb);
-  dim3 grid((unsigned)(tiles_m * tiles_n), gy);
   hipStream_t s = as_stream(stream);
-  if (akc && bkc)
-    launch_gemm<true, true>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
-  else if (akc)
-    launch_gemm<true, false>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
-  else if (bkc)
-    launch_gemm<false, true>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
+  // stream-K pays off for the exact f32 loop only: the x6 loop's plain grid
+  // (3 resident tiles per CU) measured 13 % faster on the layer-0 shapes
+  // (tools/gemm3_lab.hip), so it always takes the plain grid.
+  const SkGeom g = streamk_geom(M, N, K, nb, ksplit, BK);
+  const bool sk = !use_x6 && g.P && workspace &&
+                  ws_bytes >= (size_t)g.P * 2 * 64 * GEMM_THREADS * sizeof(float);
+  const unsigned gy = ksplit == 1 ? 1u : (ksplit == 2 ? (unsigned)nptr : (unsigned)nb);
+  const dim3 grid((unsigned)(tiles_m * tiles_n), gy);
+  float* ws = reinterpret_cast<float*>(workspace);
+  if (use_x6)
+    dispatch_gemm<true>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm,
+                        scn, nseg, (int)tiles_n, g, ws);
   else
-    launch_gemm<false, false>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, nseg, (int)tiles_n);
-  return check_launch("ainp_gemm_f32");
+    dispatch_gemm<false>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta,
+                         scm, scn, nseg, (int)tiles_n, g, ws);
+  int rc = check_launch(sk ? "gemm_f32_streamk" : "ainp_gemm_f32");
+  if (rc || !sk) return rc;
+  hipLaunchKernelGGL(gemm_streamk_fixup, dim3((unsigned)(g.units / g.nk)), dim3(GEMM_THREADS), 0,
+                     s, M, N, alpha, p, beta, scm, scn, g, ws);
+  return check_launch("gemm_streamk_fixup");
 }

@@ -121,7 +121,8 @@ def test_gap_frames_known_answers(ops, golden_dir):
 # ------------------------------------------------------------------ GEMM
 @pytest.mark.parametrize("M,N,K", [(333, 130, 77), (256, 512, 1024), (1, 5, 3), (129, 4112, 256)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
-def test_gemm_layouts(ops, M, N, K, ta, tb):
+@pytest.mark.parametrize("exact", [False, True])
+def test_gemm_layouts(ops, M, N, K, ta, tb, exact):
     g = torch.Generator().manual_seed(M * 7 + N)
     A = torch.randn(M, K, generator=g, dtype=torch.float64)
     B = torch.randn(K, N, generator=g, dtype=torch.float64)
@@ -131,8 +132,29 @@ def test_gemm_layouts(ops, M, N, K, ta, tb):
     C = torch.empty(M, N, device=DEV)
     sam, sak = (1, M) if ta else (K, 1)
     sbk, sbn = (1, K) if tb else (N, 1)
-    ops.gemm(M, N, K, [Ad], sam, sak, [Bd], sbk, sbn, [C], N, 1)
+    ops.gemm(M, N, K, [Ad], sam, sak, [Bd], sbk, sbn, [C], N, 1, exact=exact)
     assert rel(C.cpu(), ref) < 1e-5
+
+
+def test_gemm_x6_is_fp32_accurate(ops):
+    """The default (three-piece bf16 split) path against fp64 on the CNNBLSTM
+    layer-0 reduction length: its error is that of an fp32 GEMM, within 2x of
+    the exact f32 MFMA path on the same fp32 inputs."""
+    g = torch.Generator().manual_seed(5)
+    M, N, K = 256, 384, 16448
+    A = torch.randn(M, K, generator=g, dtype=torch.float64).float()
+    B = (torch.randn(K, N, generator=g, dtype=torch.float64) * 0.01).float()
+    ref = A.double() @ B.double()
+    Ad, Bd = A.to(DEV), B.to(DEV)
+    errs = {}
+    for exact in (False, True):
+        C = torch.empty(M, N, device=DEV)
+        ops.gemm(M, N, K, [Ad], K, 1, [Bd], N, 1, [C], N, 1, exact=exact)
+        errs[exact] = rel(C.cpu(), ref)
+    # fp32 accumulation over K=16448 random terms: ~u*sqrt(K) ~ 1e-6 relative
+    assert errs[True] < 1e-5 and errs[False] < 1e-5, errs
+    # a bf16x3 split (dropping the 2^-16 terms) would sit ~4x above exact f32
+    assert errs[False] < 2 * errs[True] + 1e-7, errs
 
 
 def test_gemm_batched_bias_ksplit(ops):
@@ -183,7 +205,8 @@ def test_gemm_streamk(ops, ta, tb):
     for _ in range(2):
         C = C0.float().to(DEV)
         ops.gemm(M, N, K, [Ad, Ad], sam, sak, Bd, sbk, sbn, [C[0], C[1]], N, 1,
-                 alpha=0.75, beta=-0.5, bias1=[bias[0].float().to(DEV), bias[1].float().to(DEV)])
+                 alpha=0.75, beta=-0.5, bias1=[bias[0].float().to(DEV), bias[1].float().to(DEV)],
+                 exact=True)   # stream-K serves the exact f32 loop
         outs.append(C.cpu())
     ref = 0.75 * (A @ B) - 0.5 * C0 + bias.view(2, 1, N)
     assert rel(outs[0], ref) < 1e-5
