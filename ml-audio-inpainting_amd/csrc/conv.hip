@@ -15,6 +15,8 @@
 // sixteen-channel column tiles (CT = ceil(Cout/16)).  K = Cin*9 is walked in
 // chunks of 8 input channels; LDS k order inside a chunk is (tap, ci) so the
 // A-operand address is lane-constant + compile-time immediate.
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace ainp {
@@ -905,8 +907,32 @@ static void launch_wgrad(const float* x, const float* sc, const float* sh,
 
 using namespace ainp;
 
+namespace ainp {
+int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W);
+int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
+                   const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
+                   int Cout, int64_t H, int64_t W, hipStream_t s);
+
+// conv_x6.hip (fp32-accurate split-bf16 MFMA) serves every pair it has an
+// instantiation for unless AINP_CONV_EXACT=1 selects the exact f32 kernels.
+static bool conv_exact_env() {
+  static const bool v = [] {
+    const char* e = getenv("AINP_CONV_EXACT");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
+static int64_t exact_stat_parts(int64_t N, int64_t H, int64_t W) {
+  return N * cdiv(H, CV_FT) * cdiv(W, CV_TT);
+}
+}  // namespace ainp
+
+// Upper bound over both kernel families' tilings; the launch zero-fills the
+// partials its tiling does not produce, so the fixed-order sum is unchanged.
 extern "C" int ainp_conv3x3_fwd_stat_parts(int64_t N, int64_t H, int64_t W) {
-  return (int)(N * cdiv(H, CV_FT) * cdiv(W, CV_TT));
+  const int64_t a = exact_stat_parts(N, H, W), b = conv_x6_stat_parts(N, H, W);
+  return (int)(a > b ? a : b);
 }
 
 template <bool DG>
@@ -914,8 +940,27 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y,
                              double* stats, int64_t N, int Cin, int Cout,
                              int64_t H, int64_t W, hipStream_t s) {
-  if (small_pair(Cin, Cout))
-    return small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
+  // partials [used, bound) of the BatchNorm statistics are zero
+  auto zero_tail = [&](int64_t used) -> int {
+    if (!stats) return AINP_OK;
+    const int64_t bound = ainp_conv3x3_fwd_stat_parts(N, H, W);
+    if (used >= bound) return AINP_OK;
+    hipError_t e = hipMemsetAsync(stats + used * 2 * Cout, 0,
+                                  (size_t)(bound - used) * 2 * Cout * sizeof(double), s);
+    return e == hipSuccess ? AINP_OK : record_error(e, "conv3x3 stats tail");
+  };
+  if (small_pair(Cin, Cout)) {
+    const int rc = small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
+    return rc ? rc : zero_tail(exact_stat_parts(N, H, W));
+  }
+  if (!conv_exact_env()) {
+    const int rc = conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
+    if (rc != 1) return rc ? rc : zero_tail(conv_x6_stat_parts(N, H, W));
+  }
+  {
+    const int rc = zero_tail(exact_stat_parts(N, H, W));
+    if (rc) return rc;
+  }
   dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
   const int ct = (Cout + 15) / 16;
   const bool ex = Cin % CV_CK == 0 && Cout % 16 == 0 &&
