@@ -21,7 +21,16 @@ namespace ainp {
 
 constexpr int LCH = 16;  // steps per staged chunk
 
-__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// Gate nonlinearities on the hardware transcendental units (v_exp_f32,
+// v_rcp_f32, ~1 ulp each) instead of libm's expf / IEEE division / tanhf: they
+// sit on the serial per-step critical path.  tanh(x) = 2*sigmoid(2x) - 1 is
+// within ~1.5e-7 absolute of tanhf (the tolerance of fp32 O(1) values); the
+// i,f,g,o quad evaluates ONE sigmoid per lane (g's argument doubled) instead of
+// a divergent tanhf/sigmoid pair.
+__device__ __forceinline__ float sigm(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.44269504088896341f * x));
+}
+__device__ __forceinline__ float tanh_hw(float x) { return 2.f * sigm(2.f * x) - 1.f; }
 
 // Per-step workgroup barrier that orders LDS only.  __syncthreads() would also
 // wait (vmcnt(0)) for the step's global stores of h/c/gates, putting a full
@@ -44,11 +53,32 @@ __device__ __forceinline__ float quad_bcast(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
 }
 
-// Forward recurrence.  4H lanes per (sequence, direction): lane = 4u + g owns
-// gate row r = g*H + u of W_hh (H VGPRs; at H=128 no accumulator-file round
-// trips), so a hidden unit's four gates (i,f,g,o) sit in one lane quad and are
-// exchanged with DPP quad broadcasts.  h_{t-1} is read from LDS as broadcast
-// ds_read_b128.  One LDS barrier per step.
+// Forward recurrence.  4H lanes per (sequence, direction): the lane quad
+// 4u..4u+3 owns hidden unit u, and lane q of the quad holds the k-quarter
+// [q*H/4, (q+1)*H/4) of all four of its gate rows (i,f,g,o) of W_hh (H VGPRs;
+// at H=128 no accumulator-file round trips).  Per step each lane reads only its
+// quarter of h_{t-1} (8 broadcast ds_read_b128 at H=128 instead of 32 for a
+// whole row: the LDS issue was the step's critical resource), forms four
+// partial dot products, and a two-stage DPP reduce-scatter inside the quad
+// leaves lane q with the full pre-activation of gate q.  One LDS barrier per
+// step.
+template <int Q0, int Q1, int Q2, int Q3>
+__device__ __forceinline__ float quad_perm(float v) {
+  constexpr int ctrl = Q0 | (Q1 << 2) | (Q2 << 4) | (Q3 << 6);
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), ctrl, 0xF, 0xF, false));
+}
+
+// p[g] = lane's partial of gate g; returns the quad total of gate q (fixed
+// addition order: pairs (0,1),(2,3) first, then (0,2),(1,3)).
+__device__ __forceinline__ float quad_reduce_scatter4(const float (&p)[4], int q) {
+  const bool b0 = q & 1, b1 = q >> 1;
+  const float s0 = b0 ? p[0] : p[1], s1 = b0 ? p[2] : p[3];
+  const float k0 = (b0 ? p[1] : p[0]) + quad_perm<1, 0, 3, 2>(s0);   // gate b0
+  const float k1 = (b0 ? p[3] : p[2]) + quad_perm<1, 0, 3, 2>(s1);   // gate b0 + 2
+  const float s2 = b1 ? k0 : k1;
+  return (b1 ? k1 : k0) + quad_perm<2, 3, 0, 1>(s2);                 // gate q
+}
+
 template <int H>
 __global__ __launch_bounds__(4 * H, 1) void lstm_fwd_kernel(
     const float* __restrict__ zx, const float* __restrict__ whh_f,
@@ -56,22 +86,27 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_fwd_kernel(
     float* __restrict__ gates, float* __restrict__ cell, int T) {
   constexpr int NT = 4 * H;         // threads
   constexpr int G4 = 4 * H;         // gate rows
+  constexpr int KQ = H / 4;         // k per lane
+  constexpr int HP = H + 16;        // padded h: k -> k + 4*(k/KQ) (conflict-free quarters)
   constexpr int PF = LCH * G4 / 4 / NT;  // float4 prefetched per thread (=LCH/4)
   __shared__ __attribute__((aligned(16))) float zs[2][LCH][G4];
-  __shared__ __attribute__((aligned(16))) float hb[2][H];
+  __shared__ __attribute__((aligned(16))) float hb[2][HP];
 
   const int n = blockIdx.x >> 1, dir = blockIdx.x & 1;
-  const int tid = threadIdx.x, u = tid >> 2, g = tid & 3;
-  const int row = g * H + u;
+  const int tid = threadIdx.x, u = tid >> 2, q = tid & 3;
+  const int row = q * H + u;        // the gate row this lane finishes (gate q of unit u)
   const float* whh = dir ? whh_r : whh_f;
 
-  f2 w[H / 2];
+  f2 w[4][KQ / 2];
 #pragma unroll
-  for (int k = 0; k < H; k += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(whh + (int64_t)row * H + k);
-    w[k / 2] = f2{v.x, v.y}; w[k / 2 + 1] = f2{v.z, v.w};
-  }
-  if (tid < H) hb[1][tid] = 0.f;
+  for (int g = 0; g < 4; ++g)
+#pragma unroll
+    for (int k = 0; k < KQ; k += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(whh + (int64_t)(g * H + u) * H + q * KQ + k);
+      w[g][k / 2] = f2{v.x, v.y};
+      w[g][k / 2 + 1] = f2{v.z, v.w};
+    }
+  if (tid < HP) hb[1][tid] = 0.f;
 
   const int64_t zrow = 8 * H;  // zx row length (both directions)
   const float* zbase = zx + (int64_t)n * T * zrow + dir * G4;
@@ -113,23 +148,32 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_fwd_kernel(
     for (int s = 0; s < LCH; ++s) {
       const int t = ch * LCH + s;
       if (t >= T) break;  // uniform across the block
-      const float* hp = hb[(t + 1) & 1];
-      f2 a01 = f2{zs[buf][s][row], 0.f}, a23 = f2{0.f, 0.f};
+      const float* hp = hb[(t + 1) & 1] + q * (KQ + 4);
+      f2 a[4], b[4];
 #pragma unroll
-      for (int k = 0; k < H; k += 4) {
+      for (int g = 0; g < 4; ++g) a[g] = b[g] = f2{0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KQ; k += 4) {
         const float4 h4 = *reinterpret_cast<const float4*>(hp + k);
-        a01 = pk_fma(w[k / 2], f2{h4.x, h4.y}, a01);
-        a23 = pk_fma(w[k / 2 + 1], f2{h4.z, h4.w}, a23);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          a[g] = pk_fma(w[g][k / 2], f2{h4.x, h4.y}, a[g]);
+          b[g] = pk_fma(w[g][k / 2 + 1], f2{h4.z, h4.w}, b[g]);
+        }
       }
-      const float pre = (a01.x + a01.y) + (a23.x + a23.y);
-      const float act = (g == 2) ? tanhf(pre) : sigm(pre);
+      float part[4];
+#pragma unroll
+      for (int g = 0; g < 4; ++g) part[g] = (a[g].x + a[g].y) + (b[g].x + b[g].y);
+      const float pre = quad_reduce_scatter4(part, q) + zs[buf][s][row];
+      const float sg = sigm(q == 2 ? 2.f * pre : pre);
+      const float act = (q == 2) ? 2.f * sg - 1.f : sg;
       const float ig = quad_bcast<0>(act), fg = quad_bcast<1>(act);
       const float gg = quad_bcast<2>(act), og = quad_bcast<3>(act);
       c = fmaf(fg, c, ig * gg);
-      const float h = og * tanhf(c);
+      const float h = og * tanh_hw(c);
       const int64_t tt = tix(t);
-      if (g == 0) {
-        hb[t & 1][u] = h;
+      if (q == 0) {
+        hb[t & 1][u + 4 * (u / KQ)] = h;
         hrow[tt * 2 * H] = h;
         if (crow) crow[tt * 2 * H] = c;
       }
@@ -142,11 +186,19 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_fwd_kernel(
 }
 
 // Backward through time.  Bwd step u walks the forward steps in reverse:
-// forward step t = T-1-u, time index tt(t).  Lane = 4k + q: the quad of
-// hidden unit k computes the four gate gradients of unit k (lane q -> gate
-// q) and the recurrent matvec dh_rec[k] = sum_g dG[g] W[g][k], lane q summing
-// the gate block g in [qH, qH+H) with W[qH+m][k] (m < H) held in VGPRs; the
-// four partials are combined with DPP quad broadcasts.
+// forward step t = T-1-u, time index tt(t).  Lane = 4k + q computes gate q's
+// gradient of hidden unit k (elementwise part).  The recurrent matvec
+// dh_rec[k] = sum_r dG[r] W[r][k] (r over the 4H gate rows) uses a different
+// split of the same lanes: lane l = 16*kg + rg holds W[rg*H/4 + j][4kg + kk]
+// (j < H/4, kk < 4: H VGPRs), reads only its H/4 gradients (8 broadcast
+// ds_read_b128 at H=128 instead of 32), and the 16 lanes of the DPP row all-
+// reduce their four partials (rotations 8,4,2,1: every lane ends with the
+// bitwise-identical sums) -- lane 4k+q is in the row of k = 4kg + rg/4.
+template <int R>
+__device__ __forceinline__ float row_ror(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x120 + R, 0xF, 0xF, false));
+}
+
 template <int H>
 __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
     const float* __restrict__ dh_out, const float* __restrict__ gates,
@@ -154,22 +206,30 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
     const float* __restrict__ whh_r, float* __restrict__ dgates, int T) {
   constexpr int NT = 4 * H;
   constexpr int G4 = 4 * H;
-  constexpr int DGS = H + 4;                        // padded gate-block stride (banks)
   constexpr int PG = LCH * G4 / 4 / NT;             // float4 of gates per thread
   constexpr int PC = ((LCH + 1) * H + NT - 1) / NT; // cell floats per thread
   constexpr int PD = (LCH * H + NT - 1) / NT;       // dh floats per thread
   __shared__ __attribute__((aligned(16))) float gsm[2][LCH][G4];
   __shared__ float csm[2][LCH + 1][H];
   __shared__ float dsm[2][LCH][H];
-  __shared__ __attribute__((aligned(16))) float dgb[2][4 * DGS];
+  constexpr int RPG = H / 4;                        // gate rows per lane (matvec)
+  constexpr int DGP = 4 * H + 64;                   // padded dG: r -> r + 4*(r/RPG)
+  __shared__ __attribute__((aligned(16))) float dgb[2][DGP];
 
   const int n = blockIdx.x >> 1, dir = blockIdx.x & 1;
   const int tid = threadIdx.x, k = tid >> 2, q = tid & 3;
+  const int kg = tid >> 4, rg = tid & 15;           // matvec split
   const float* whh = dir ? whh_r : whh_f;
-  f2 wt[H / 2];  // W[q*H + m][k], m pairs
+  f2 wt[4][RPG / 2];  // W[rg*RPG + j][4kg + kk], j pairs
 #pragma unroll
-  for (int m = 0; m < H; m += 2)
-    wt[m / 2] = f2{whh[(int64_t)(q * H + m) * H + k], whh[(int64_t)(q * H + m + 1) * H + k]};
+  for (int j = 0; j < RPG; j += 2) {
+    const float4 v0 = *reinterpret_cast<const float4*>(whh + (int64_t)(rg * RPG + j) * H + 4 * kg);
+    const float4 v1 = *reinterpret_cast<const float4*>(whh + (int64_t)(rg * RPG + j + 1) * H + 4 * kg);
+    wt[0][j / 2] = f2{v0.x, v1.x};
+    wt[1][j / 2] = f2{v0.y, v1.y};
+    wt[2][j / 2] = f2{v0.z, v1.z};
+    wt[3][j / 2] = f2{v0.w, v1.w};
+  }
 
   auto tix = [&](int t) { return dir ? (T - 1 - t) : t; };
   const float* gbase = gates + (int64_t)n * T * 8 * H + dir * G4;
@@ -244,7 +304,7 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
       const float cc = csm[buf][s][k];
       const float cp = (t > 0) ? csm[buf][s + 1][k] : 0.f;
       const float dh = dsm[buf][s][k] + dh_rec;
-      const float tc = tanhf(cc);
+      const float tc = tanh_hw(cc);
       const float dc = fmaf(dh * og, 1.f - tc * tc, dc_next);
       dc_next = dc * fg;
       float da;
@@ -254,20 +314,37 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
       else da = (dh * tc) * og * (1.f - og);                   // d pre_o
       const int64_t tt = tix(t);
       float* db = dgb[uu & 1];
-      db[q * DGS + k] = da;
+      {
+        const int r = q * H + k;
+        db[r + 4 * (r / RPG)] = da;
+      }
       dgrow[tt * 8 * H] = da;
       lds_barrier();
-      const float* dq = db + q * DGS;
-      f2 ab = f2{0.f, 0.f}, cd = f2{0.f, 0.f};
+      const float* dq = db + rg * (RPG + 4);
+      f2 a[4], b[4];
 #pragma unroll
-      for (int m = 0; m < H; m += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(dq + m);
-        ab = pk_fma(wt[m / 2], f2{v.x, v.y}, ab);
-        cd = pk_fma(wt[m / 2 + 1], f2{v.z, v.w}, cd);
+      for (int kk = 0; kk < 4; ++kk) a[kk] = b[kk] = f2{0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < RPG; j += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(dq + j);
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          a[kk] = pk_fma(wt[kk][j / 2], f2{v.x, v.y}, a[kk]);
+          b[kk] = pk_fma(wt[kk][j / 2 + 1], f2{v.z, v.w}, b[kk]);
+        }
       }
-      const float part = (ab.x + ab.y) + (cd.x + cd.y);
-      dh_rec = (quad_bcast<0>(part) + quad_bcast<1>(part)) +
-               (quad_bcast<2>(part) + quad_bcast<3>(part));
+      float part[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        float v = (a[kk].x + a[kk].y) + (b[kk].x + b[kk].y);
+        v += row_ror<8>(v);
+        v += row_ror<4>(v);
+        v += row_ror<2>(v);
+        v += row_ror<1>(v);
+        part[kk] = v;
+      }
+      const int sel = rg >> 2;                      // k = 4kg + sel
+      dh_rec = sel == 0 ? part[0] : (sel == 1 ? part[1] : (sel == 2 ? part[2] : part[3]));
     }
     if (ch + 1 < nch) store_chunk(buf ^ 1);
     __syncthreads();
