@@ -45,6 +45,11 @@ __device__ __forceinline__ float bf_hi(uint32_t p) { return __uint_as_float(p & 
 __device__ __forceinline__ void split2(float a, float b, uint32_t& p0, uint32_t& p1,
                                        uint32_t& p2) {
   p0 = cvt_pk_bf16(a, b);
+#ifdef LAB_NOSPLIT  // ceiling probe: same MFMA/LDS work, no split arithmetic (wrong results)
+  p1 = p0;
+  p2 = p0;
+  return;
+#endif
   const float ra = a - bf_lo(p0), rb = b - bf_hi(p0);
   p1 = cvt_pk_bf16(ra, rb);
   const float sa = ra - bf_lo(p1), sb = rb - bf_hi(p1);
