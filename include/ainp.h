@@ -115,7 +115,7 @@ int ainp_gl_update(const float* rebuilt, float* tprev, float* angles, int64_t n,
                    float momentum, int first, void* stream);
 
 /* ------------------------------------------------------------------------ */
-/* fp32 GEMM on MFMA (v_mfma_f32_32x32x2_f32, exact fp32)                    */
+/* fp32 GEMM on MFMA (fp32-accurate bf16 split by default, exact f32 on flag) */
 /* ------------------------------------------------------------------------ */
 /* C = alpha * op(A) * op(B) + beta * C + bias1 + bias2   (bias along n)
  * Replaces the ATen GEMMs behind nn.LSTM's input projections and nn.Linear
@@ -384,7 +384,8 @@ int ainp_maxpool2(const float* x, float* y, int64_t NC, int H, int W, void* stre
  * resize evaluated only at the SxS centre-crop outputs with the separable
  * tables (ry0, rn, rw[S][rtaps]) / (cx0, cn, cw[S][ctaps]) built by the host
  * (torch's _upsample_bilinear2d_aa weights); ImageNet normalisation;
- * out [N,3,S,S]. */
+ * out [N,3,S,S].  generated: 1 generated, 0 target (max found here), 2 target
+ * whose max max_ws already holds (ainp_vgg_target_max + a MAX all-reduce). */
 int ainp_vgg_prep(const float* x, int64_t N, int H, int W, int generated,
                   unsigned int* max_ws, const int* ry0, const int* rn, const float* rw,
                   int rtaps, const int* cx0, const int* cn, const float* cw, int ctaps,
@@ -401,6 +402,14 @@ int ainp_bce_logits(const float* x, int64_t n, float target, float* grad, float 
                     void* workspace, double* out_mean, void* stream);
 int ainp_gan_recon_losses(const float* g, const float* o, const float* m, int64_t n,
                           void* workspace, double* out3, void* stream);
+/* Data-parallel forms: the raw fp64 sums behind
+ * ainp_gan_recon_losses, out5 = [sum|(g-o)m|, sum m, sum|(g-o)(1-m)|, sum(1-m),
+ * sum|g-o||o|], to be SUM-all-reduced before the ratios; and the VGG target's
+ * batch max (clamp(x,0) bits, loss.py:78) alone, to be MAX-all-reduced and then
+ * passed to ainp_vgg_prep with generated == 2. */
+int ainp_gan_recon_sums(const float* g, const float* o, const float* m, int64_t n,
+                        void* workspace, double* out5, void* stream);
+int ainp_vgg_target_max(const float* x, int64_t n, unsigned int* max_ws, void* stream);
 /* torch.nn.utils.spectral_norm for nl (<= 8) layers at once (networks.py:
  * 360-361,403-404), W viewed [h][wd]: update != 0 (train-mode forward) runs one
  * power iteration v = normalize(W^T u), u = normalize(W v) in place; always

@@ -28,11 +28,32 @@ class Comm:
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        # gloo with GPU tensors (the multi-rank tests on a one-GPU box): stage
+        # through host memory; RCCL ("nccl") reduces device tensors directly
+        self.host_staging = dist.get_backend(group) == "gloo"
+
+    def _allreduce(self, t: torch.Tensor, op) -> torch.Tensor:
+        if self.world_size > 1:
+            if self.host_staging and t.is_cuda:
+                h = t.cpu()
+                dist.all_reduce(h, op=op, group=self.group)
+                t.copy_(h)
+            else:
+                dist.all_reduce(t, op=op, group=self.group)
+        return t
 
     def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
-        if self.world_size > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
-        return t
+        return self._allreduce(t, dist.ReduceOp.SUM)
+
+    def allreduce_max_(self, t: torch.Tensor) -> torch.Tensor:
+        return self._allreduce(t, dist.ReduceOp.MAX)
+
+
+class _Done:
+    """Completed-work stand-in for a synchronous (host-staged) reduction."""
+
+    def wait(self):
+        return True
 
 
 class GradAllReducer:
@@ -93,7 +114,11 @@ class GradAllReducer:
         else:
             flat = torch.cat([p.grad.reshape(-1) for p in bucket])
             t = flat
-        work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.comm.group, async_op=True)
+        if self.comm.host_staging and t.is_cuda:
+            self.comm.allreduce_sum_(t)
+            work = _Done()
+        else:
+            work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.comm.group, async_op=True)
         self._inflight.append((work, bucket, flat))
 
     @torch.no_grad()

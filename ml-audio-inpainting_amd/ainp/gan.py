@@ -42,9 +42,16 @@ def _need_cuda(t, what):
 
 
 def _bn_affine(bn: nn.BatchNorm2d, stats, count, C):
-    """BatchNorm2d train (batch stats + running update) or eval -> (scale, shift)."""
+    """BatchNorm2d train (batch stats + running update) or eval -> (scale, shift).
+    A data-parallel trainer sets `bn.ainp_comm`: the (sum, sum of squares)
+    are then all-reduced (SyncBN), so every rank normalises with the statistics
+    of the global batch, as the single-process reference does."""
     if bn.training or not bn.track_running_stats:
         sums = ops.bn_stats_reduce(stats, C)
+        comm = getattr(bn, "ainp_comm", None)
+        if comm is not None and comm.world_size > 1:
+            comm.allreduce_sum_(sums)
+            count = count * comm.world_size
         rm = bn.running_mean if bn.track_running_stats else None
         rv = bn.running_var if bn.track_running_stats else None
         mom = bn.momentum if bn.momentum is not None else 0.1
@@ -493,7 +500,13 @@ class VGGLoss(nn.Module):
         if x.shape[1] != 1:
             raise ValueError(f"Input tensor must have 1 channel here, got {x.shape[1]}")
         x = x.contiguous().float()
-        return ops.vgg_prep(x, generated, self._prep_tables(x.shape[2], x.shape[3], x.device))
+        tables = self._prep_tables(x.shape[2], x.shape[3], x.device)
+        comm = getattr(self, "comm", None)
+        if not generated and comm is not None and comm.world_size > 1:
+            # loss.py:78 scales by the max over the WHOLE batch: MAX-all-reduce it
+            mx = comm.allreduce_max_(ops.vgg_target_max(x))
+            return ops.vgg_prep(x, generated, tables, target_max=mx)
+        return ops.vgg_prep(x, generated, tables)
 
     def _extract_features(self, x) -> Dict[int, torch.Tensor]:
         """loss.py:41-51 incl. the inplace-ReLU effect: a collected conv output
@@ -558,9 +571,12 @@ class VGGLoss(nn.Module):
 
 
 def calculate_losses(cfg, generated_mag, original_mag, mask, d_fake_pred,
-                     vgg_loss_calculator: Optional[VGGLoss] = None):
+                     vgg_loss_calculator: Optional[VGGLoss] = None, comm=None):
     """train.py:33-88 -> dict of 0-dim float32 tensors (g_adv differentiable
-    w.r.t. d_fake_pred)."""
+    w.r.t. d_fake_pred).  comm (data parallel): the hole / valid L1 normalisers
+    and numerators are summed over ranks, so Lv / Lh are the global-batch
+    values; the mean-type terms are per-rank means (their rank average is the
+    global mean, taken by the trainer for logging)."""
     lc = cfg["training"]
     adv = bce_with_logits_const(d_fake_pred, 1.0)
     mask = mask.view_as(generated_mag) if mask.dim() < generated_mag.dim() else mask
@@ -568,8 +584,14 @@ def calculate_losses(cfg, generated_mag, original_mag, mask, d_fake_pred,
         generated_mag = generated_mag[:, :1]
     if original_mag.shape[1] != 1:
         original_mag = original_mag[:, :1]
-    rec = ops.gan_recon_losses(generated_mag.contiguous().float(),
-                               original_mag.contiguous().float(), mask.contiguous().float())
+    if comm is not None and comm.world_size > 1:
+        sums = comm.allreduce_sum_(ops.gan_recon_sums(generated_mag.contiguous().float(),
+                                                      original_mag.contiguous().float(),
+                                                      mask.contiguous().float()))
+        rec = ops.gan_recon_from_sums(sums, generated_mag.numel() * comm.world_size)
+    else:
+        rec = ops.gan_recon_losses(generated_mag.contiguous().float(),
+                                   original_mag.contiguous().float(), mask.contiguous().float())
     rec = rec.to(torch.float32)
     l1v, l1h, lw = rec[0], rec[1], rec[2]
     dev = generated_mag.device

@@ -36,6 +36,13 @@ class GanTrainer:
         if comm is not None and comm.world_size > 1:
             from .dist import GradAllReducer
             self.reducer = GradAllReducer(discriminator.parameters(), comm)
+            # SyncBN for G's BatchNorms and the global VGG target max: the
+            # N-rank step then equals the 1-process step on the whole batch
+            for m in generator.modules():
+                if isinstance(m, torch.nn.BatchNorm2d):
+                    m.ainp_comm = comm
+            if vgg is not None:
+                vgg.comm = comm
 
     def step(self, original_mag, impaired_mag, mask):
         self.G.train()
@@ -61,15 +68,23 @@ class GanTrainer:
         self.g_opt.zero_grad()
         if self.faithful:
             d_fake_g = self.D(generated)
-            losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g, self.vgg)
+            losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g, self.vgg,
+                                        comm=self.comm)
             losses["g_total"].backward()
         else:
             with torch.no_grad():
                 d_fake_g = self.D(generated)
                 losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g,
-                                            self.vgg)
+                                            self.vgg, comm=self.comm)
         self.g_opt.step()   # no-op: G has no gradients (Q1)
         out = {k: v.detach() for k, v in losses.items()}
-        out.update(d_loss=d_loss.detach(), d_real=l_real.detach(), d_fake=l_fake.detach(),
-                   generated=generated)
+        out.update(d_loss=d_loss.detach(), d_real=l_real.detach(), d_fake=l_fake.detach())
+        if self.comm is not None and self.comm.world_size > 1:
+            # per-rank batch means -> global-batch means (equal per-rank batches)
+            keys = sorted(out)
+            vec = torch.stack([out[k].to(torch.float64).reshape(()) for k in keys])
+            self.comm.allreduce_sum_(vec)
+            vec /= self.comm.world_size
+            out = {k: vec[i].to(torch.float32) for i, k in enumerate(keys)}
+        out["generated"] = generated
         return out

@@ -626,6 +626,27 @@ def gan_recon_losses(g, o, m):
     return out
 
 
+def gan_recon_sums(g, o, m):
+    """Raw fp64 sums [sum|(g-o)m|, sum m, sum|(g-o)(1-m)|, sum(1-m), sum|g-o||o|]
+    behind gan_recon_losses (ainp_gan_recon_sums), for a SUM all-reduce."""
+    for t, nm in ((g, "generated"), (o, "original"), (m, "mask")):
+        _req(t, nm)
+    out = torch.empty(5, device=g.device, dtype=torch.float64)
+    call("ainp_gan_recon_sums", g.data_ptr(), o.data_ptr(), m.data_ptr(), g.numel(),
+         _reduce_ws(g.device).data_ptr(), out.data_ptr(), _stream(g))
+    return out
+
+
+def gan_recon_from_sums(sums, n):
+    """(Lv, Lh, Lw) from the (all-reduced) sums with the kernel's rounding:
+    fp32 sums / (fp32 sum + 1e-8), Lw = fp32(sum / n)."""
+    f = sums.to(torch.float32)
+    lv = f[0] / (f[1] + 1e-8)
+    lh = f[2] / (f[3] + 1e-8)
+    lw = (sums[4] / float(n)).to(torch.float32)
+    return torch.stack([lv, lh, lw]).to(torch.float64)
+
+
 def sn_power(weights, us, vs, update=True, eps=1e-12):
     """Spectral norm for several layers: power iteration (in place on us/vs)
     when update, then inv_sigma [nl] (device float32)."""
@@ -745,14 +766,28 @@ def aa_bilinear_weights(in_size, out_size, start, count):
     return np.array(x0s, np.int32), np.array(ns, np.int32), W
 
 
-def vgg_prep(x, generated, tables, S=224):
-    """ainp_vgg_prep: x [N,1,H,W] -> [N,3,S,S] normalised VGG input."""
+def vgg_target_max(x):
+    """Batch max of clamp(x, 0) as its float bits in an int32 [1] device tensor
+    (ainp_vgg_target_max); non-negative floats order like their bits, so a MAX
+    all-reduce of this tensor is the global batch max (loss.py:78)."""
+    _req(x, "x")
+    mx = torch.empty(1, device=x.device, dtype=torch.int32)
+    call("ainp_vgg_target_max", x.data_ptr(), x.numel(), mx.data_ptr(), _stream(x))
+    return mx
+
+
+def vgg_prep(x, generated, tables, S=224, target_max=None):
+    """ainp_vgg_prep: x [N,1,H,W] -> [N,3,S,S] normalised VGG input.
+    target_max: precomputed (e.g. all-reduced) vgg_target_max for a target."""
     _req(x, "x")
     N, _, H, W = x.shape
     ry0, rn, rw, cx0, cn, cw = tables
     out = torch.empty(N, 3, S, S, device=x.device)
-    mx = torch.empty(1, device=x.device, dtype=torch.int32)
-    call("ainp_vgg_prep", x.data_ptr(), N, H, W, int(bool(generated)), mx.data_ptr(),
+    if target_max is not None and not generated:
+        mx, mode = target_max, 2
+    else:
+        mx, mode = torch.empty(1, device=x.device, dtype=torch.int32), int(bool(generated))
+    call("ainp_vgg_prep", x.data_ptr(), N, H, W, mode, mx.data_ptr(),
          ry0.data_ptr(), rn.data_ptr(), rw.data_ptr(), rw.shape[1], cx0.data_ptr(),
          cn.data_ptr(), cw.data_ptr(), cw.shape[1], S, out.data_ptr(), _stream(x))
     return out

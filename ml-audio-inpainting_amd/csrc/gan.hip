@@ -1011,10 +1011,11 @@ extern "C" int ainp_vgg_prep(const float* x, int64_t N, int H, int W, int genera
                              const float* rw, int rtaps, const int* cx0, const int* cn,
                              const float* cw, int ctaps, int S, float* out, void* stream) {
   if (!x || N < 1 || !ry0 || !rn || !rw || !cx0 || !cn || !cw || !out || S < 1 ||
-      (!generated && !max_ws))
+      generated < 0 || generated > 2 || (generated != 1 && !max_ws))
     return record_msg("ainp_vgg_prep: bad argument");
   hipStream_t s = as_stream(stream);
-  if (!generated) {
+  if (generated == 2) generated = 0;  // target whose batch max max_ws already holds
+  else if (!generated) {
     hipError_t me = hipMemsetAsync(max_ws, 0, sizeof(unsigned int), s);
     if (me != hipSuccess) return record_error(me, "vgg_prep memset");
     hipLaunchKernelGGL(clamp_max_kernel, dim3(256), dim3(256), 0, s, x, N * (int64_t)H * W,
@@ -1024,6 +1025,16 @@ extern "C" int ainp_vgg_prep(const float* x, int64_t N, int H, int W, int genera
   hipLaunchKernelGGL(vgg_prep_kernel, dim3((unsigned)cdiv(n, 256)), dim3(256), 0, s, x, (int)N,
                      H, W, generated, max_ws, ry0, rn, rw, rtaps, cx0, cn, cw, ctaps, S, out);
   return check_launch("vgg_prep");
+}
+
+extern "C" int ainp_vgg_target_max(const float* x, int64_t n, unsigned int* max_ws,
+                                   void* stream) {
+  if (!x || n < 1 || !max_ws) return record_msg("ainp_vgg_target_max: bad argument");
+  hipStream_t s = as_stream(stream);
+  hipError_t me = hipMemsetAsync(max_ws, 0, sizeof(unsigned int), s);
+  if (me != hipSuccess) return record_error(me, "vgg_target_max memset");
+  hipLaunchKernelGGL(clamp_max_kernel, dim3(256), dim3(256), 0, s, x, n, max_ws);
+  return check_launch("vgg_target_max");
 }
 
 static const int kRedBlocks = 512;
@@ -1063,6 +1074,25 @@ extern "C" int ainp_gan_recon_losses(const float* g, const float* o, const float
   hipLaunchKernelGGL(gan_recon_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, g, o, m, n, part);
   hipLaunchKernelGGL(gan_recon_final_kernel, dim3(1), dim3(64), 0, s, part, kRedBlocks, n, out3);
   return check_launch("gan_recon_losses");
+}
+
+__global__ void gan_recon_sums_kernel(const double* partial, int np, double* out5) {
+  if (threadIdx.x < 5) {
+    double s = 0.0;
+    for (int b = 0; b < np; ++b) s += partial[(int64_t)b * 5 + threadIdx.x];
+    out5[threadIdx.x] = s;
+  }
+}
+
+extern "C" int ainp_gan_recon_sums(const float* g, const float* o, const float* m, int64_t n,
+                                   void* workspace, double* out5, void* stream) {
+  if (!g || !o || !m || n < 1 || !workspace || !out5)
+    return record_msg("ainp_gan_recon_sums: bad argument");
+  hipStream_t s = as_stream(stream);
+  double* part = reinterpret_cast<double*>(workspace);
+  hipLaunchKernelGGL(gan_recon_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, g, o, m, n, part);
+  hipLaunchKernelGGL(gan_recon_sums_kernel, dim3(1), dim3(64), 0, s, part, kRedBlocks, out5);
+  return check_launch("gan_recon_sums");
 }
 
 extern "C" size_t ainp_sn_workspace(int nl, int maxdim) {
