@@ -442,6 +442,19 @@ int ainp_leaky_bwd(const float* g, const float* y, int64_t n, float slope, float
 int ainp_mul(const float* a, const float* b, int64_t n, float* out, void* stream);
 int ainp_channel_sum(const float* m, int64_t N, int C, int64_t HW, float* out, void* stream);
 
+/* ------------------------------------------------------------------------ */
+/* (f2) FLAC ingest -- HOST code, host pointers                              */
+/* ------------------------------------------------------------------------ */
+/* Replaces soundfile/libsndfile behind utils.load_audio -> librosa.load
+ * (utils.py:36).  data: the whole file in host memory.  ainp_flac_info parses
+ * STREAMINFO (md5: 16 bytes, may be NULL); ainp_flac_decode writes the
+ * interleaved signed samples [frames][channels] as int32 (as encoded: scale by
+ * 2^-(bps-1) for libsndfile's float), verifying every frame's CRC-8/CRC-16. */
+int ainp_flac_info(const uint8_t* data, size_t n, int* sample_rate, int* channels,
+                   int* bits_per_sample, int64_t* total_samples, uint8_t* md5);
+int ainp_flac_decode(const uint8_t* data, size_t n, int32_t* out, int64_t max_frames,
+                     int64_t* n_frames);
+
 #ifdef __cplusplus
 }
 #endif

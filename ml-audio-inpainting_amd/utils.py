@@ -4,7 +4,8 @@ Same names, signatures, return types and error behaviour as
 /root/reference/utils.py; the STFT runs on the MI355X kernel
 (ainp_stft / ainp_stft_features) instead of librosa.
 
-  load_audio            utils.py:14-52   (WAV via the stdlib; FLAC/other formats
+  load_audio            utils.py:14-52   (WAV via the stdlib, FLAC on the native
+                                          decoder ainp_flac_decode; other formats
                                           through soundfile when it is installed)
   save_audio            utils.py:54-89   (peak-normalised, WAV; FLAC via soundfile)
   create_gap_mask       utils.py:93-144  (host numpy, the reference's own RNG call)
@@ -49,6 +50,15 @@ def _read_wav(path: str) -> Tuple[np.ndarray, int]:
     return x.reshape(-1, nch), sr
 
 
+def _is_flac(path: str) -> bool:
+    try:
+        with open(path, "rb") as f:
+            head = f.read(4)
+    except OSError:
+        return False
+    return head == b"fLaC" or (head[:3] == b"ID3" and str(path).lower().endswith(".flac"))
+
+
 def _read_any(path: str) -> Tuple[np.ndarray, int]:
     """(frames, channels) float32 in [-1, 1) and the native rate."""
     if str(path).lower().endswith(".wav"):
@@ -56,12 +66,15 @@ def _read_any(path: str) -> Tuple[np.ndarray, int]:
             return _read_wav(str(path))
         except (wave.Error, EOFError):
             pass
+    if _is_flac(str(path)):
+        from ainp.audio_io import read_flac   # native decoder
+        return read_flac(str(path))
     try:
         import soundfile as sf  # optional dependency (not in this image)
     except ImportError as e:
         raise RuntimeError(
-            f"cannot decode {path}: only PCM WAV is readable without soundfile "
-            "(FLAC ingest on the GPU box is SURVEY §8 f2)") from e
+            f"cannot decode {path}: only PCM WAV and FLAC are readable without "
+            "soundfile") from e
     data, sr = sf.read(str(path), dtype="float32", always_2d=True)
     return data, sr
 

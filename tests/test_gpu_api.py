@@ -108,6 +108,61 @@ def test_train_script_runs_one_epoch(tmp_path):
     assert all(torch.isfinite(v).all() for v in sd.values() if v.is_floating_point())
 
 
+# ------------------------------------------------- C1: the bundled FLAC clips
+FLAC_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "flac")
+
+
+def _flac_tree(tmp_path):
+    import shutil
+    for split in ("train-clean-100", "test-clean"):
+        d = tmp_path / "root" / split / "19" / "198"
+        d.mkdir(parents=True)
+        for f in sorted(os.listdir(FLAC_DIR)):
+            shutil.copy(os.path.join(FLAC_DIR, f), d / f)
+
+
+def test_c1_flac_dataset_items_match_oracle(tmp_path):
+    """Real LibriSpeech speech through the native FLAC decoder and the fused
+    feature kernel vs the float64 oracle (BASELINE configs[0] shapes: 5 s,
+    T = 417, 25 gaps per file)."""
+    from models.CNNBLSTM.dataset import LibriSpeechDataset
+    import utils
+    _flac_tree(tmp_path)
+    cfg = _cfg(tmp_path, n_files=9, gaps=25, max_len_s=5.0)
+    ds = LibriSpeechDataset(None, "train", device="cuda", config=cfg)
+    assert len(ds) == 9
+    for idx in (0, 8):
+        np.random.seed(100 + idx)
+        lg, gi, gm, tg = ds[idx]
+        assert lg.shape == (25, 257, 417)
+        audio, _ = utils.load_audio(ds.file_paths[idx])
+        np.random.seed(100 + idx)
+        starts = [np.random.randint(0, 80000 - 3200) for _ in range(25)]
+        for i in (0, 7, 24):
+            rl, rt, rm = stft_ref.cnnblstm_item(audio, starts[i], 3200, 512, 192, 384, 16000, 417)
+            np.testing.assert_array_equal(gm[i].cpu().numpy(), rm)
+            assert np.abs(lg[i].cpu().numpy() - rl).max() < 2e-5
+            assert np.abs(tg[i].cpu().numpy() - rt).max() <= 2e-6 * np.abs(rt).max()
+
+
+def test_c1_train_script_on_bundled_flacs(tmp_path):
+    """BASELINE configs[0]: train.py on the 9 bundled clips, batch 2 files x 25
+    gaps, the reference model (3-layer BLSTM, H=128), one epoch incl. the
+    partial last batch the reference crashes on."""
+    from models.CNNBLSTM import train as train_mod
+    _flac_tree(tmp_path)
+    cfg = _cfg(tmp_path, n_files=9, gaps=25, max_len_s=5.0, batch=2, epochs=1)
+    cfg["model"].update({"input_dim": 417, "num_lstm_layers": 3, "lstm_hidden_dim": 128})
+    p = tmp_path / "cfg.yaml"
+    p.write_text(yaml.safe_dump(cfg))
+    train_mod.main(str(p))
+    ck = list((tmp_path / "ck").rglob("blstm_cnn_epoch_1.pt"))
+    assert len(ck) == 1
+    sd = torch.load(ck[0], weights_only=True)
+    assert sd["lstm.weight_ih_l0"].shape == (512, 64 * 257)
+    assert all(torch.isfinite(v).all() for v in sd.values() if v.is_floating_point())
+
+
 # ------------------------------------------------------------------ GAN API
 def _gan_cfg(tmp_path, limit=8, batch=2, epochs=1):
     return {
