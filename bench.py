@@ -351,9 +351,13 @@ def run_gan(args):
         ach = flops / avg_s / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": f"conv_gen_fwd_kernel<64> (final PartialConv2d 65->64 3x3 at "
+                "kernel": f"conv_gen_x6_kernel<64> (final PartialConv2d 65->64 3x3 at "
                           f"{Hp}x{Wp}, B={B})", "avg_launch_ms": round(avg_s * 1e3, 4),
-                "flop_per_launch": flops}
+                "flop_per_launch": flops,
+                "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross products "
+                             "on v_mfma_f32_32x32x16_bf16, f32 accumulate",
+                "executed_tflops": round(6 * ach, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
+                "executed_frac": round(6 * ach / BF16_MFMA_PEAK_TFLOPS, 4)}
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = gan_cpu_baseline(T, S, g)

@@ -16,6 +16,8 @@
 // k = tap * Cin + ci (tap-major).  When Cin and the concat split are
 // multiples of 32 every 32-deep K tile has ONE tap, so the gather's bounds,
 // mask and address arithmetic are per tile, not per element ("fast" path).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace ainp {
@@ -83,6 +85,103 @@ __global__ void conv_weight_kmajor_kernel(const float* w, int Cout, int C0, int 
     c = C0 + (k - K0 - tap * C1);
   }
   wt[t] = w[((int64_t)co * Cin + c) * KK + tap];
+}
+
+// Shared epilogue of the implicit-GEMM convolutions (both main loops):
+// split-K partial slab, or 1/sigma, partial-conv ratio, bias, BatchNorm
+// statistics (fixed order) and activation.  red: >= WN*BM*2 doubles of LDS.
+template <int BM>
+__device__ __forceinline__ void conv_gen_epilogue(const ConvGenParams& p, f32x16 (&acc)[2][2],
+                                                  int act, double* red) {
+  constexpr int BN = 16384 / BM;
+  constexpr int WN = BN / 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, lh = lane >> 5;
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px0 = (int64_t)blockIdx.x * BN;
+  const int co0 = blockIdx.y * BM;
+  if (p.partial) {   // split-K: raw partial sums, the epilogue kernel finishes
+    float* pb = p.partial + (int64_t)blockIdx.z * p.Cout * NP;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t pg = px0 + wn * 64 + 32 * j + l31;
+      if (pg >= NP) continue;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = co0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (co < p.Cout) pb[(int64_t)co * NP + pg] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  // ---------------- epilogue
+  const float sc = p.scale ? *p.scale : 1.f;
+  bool ok[2];
+  float rt[2];
+  float* yb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t pg = px0 + wn * 64 + 32 * j + l31;
+    ok[j] = pg < NP;
+    int pn = 0, prem = 0;
+    if (ok[j]) {
+      pn = (int)(pg / HWo);
+      prem = (int)(pg - (int64_t)pn * HWo);
+    }
+    rt[j] = (ok[j] && p.ratio) ? p.ratio[pg] : 1.f;
+    yb[j] = p.y + (int64_t)pn * p.Cout * HWo + prem;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int cl = wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int co = co0 + cl;
+      const bool cok = co < p.Cout;
+      const float bv = (cok && p.bias) ? p.bias[co] : 0.f;
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        if (!ok[j] || !cok) continue;
+        float v = acc[i][j][r] * sc;
+        v *= rt[j];
+        v += bv;
+        a += (double)v;
+        b += (double)v * (double)v;
+        yb[j][(int64_t)co * HWo] = apply_act(v, act, p.slope);
+      }
+      if (p.stats) {
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if (l31 == 0) {
+          red[(wn * BM + cl) * 2 + 0] = a;
+          red[(wn * BM + cl) * 2 + 1] = b;
+        }
+      }
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    if (tid < BM) {
+      const int co = co0 + tid;
+      if (co < p.Cout) {
+        double a = 0.0, b = 0.0;
+        for (int q = 0; q < WN; ++q) {
+          a += red[(q * BM + tid) * 2];
+          b += red[(q * BM + tid) * 2 + 1];
+        }
+        p.stats[((int64_t)blockIdx.x * 2 + 0) * p.Cout + co] = a;
+        p.stats[((int64_t)blockIdx.x * 2 + 1) * p.Cout + co] = b;
+      }
+    }
+  }
 }
 
 // Implicit-GEMM convolution: block tile BM (co) x BN (pixels) x 32 (k), four
@@ -214,87 +313,197 @@ __global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, c
     __syncthreads();
   }
 
-  if (p.partial) {   // split-K: raw partial sums, the epilogue kernel finishes
-    float* pb = p.partial + (int64_t)blockIdx.z * p.Cout * NP;
+  conv_gen_epilogue<BM>(p, acc, act, reinterpret_cast<double*>(sA));
+}
+
+// ---------------------------------------------------------------- x6 variant
+// The same implicit GEMM with gemm.hip's fp32-accurate split-bf16 main loop:
+// every staged element x = x0 + x1 + x2 (three bf16 pieces, round-to-nearest,
+// exact), six cross products of order >= 2^-16 per product on
+// v_mfma_f32_32x32x16_bf16 (dropped terms <= ~2^-23 |a||b|).  Staging maps
+// give each thread ONE row (output channel for A, pixel for B) and a run of
+// consecutive k, so the split pieces go to LDS as 16-byte vectors of three
+// bf16 planes [row][32 k] with 80-byte rows (conflict-free ds_read_b128
+// fragments: lane (row r, half h) reads k = 16s + 8h..+7).  The gather, the
+// one-tap-per-tile fast path and the epilogue are conv_gen_fwd_kernel's.
+namespace cgx {
+constexpr int RS = 80;                 // bytes per image row (32 bf16 + 16 pad)
+__device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
+  uint32_t r;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+// split 8 consecutive-k values into one 16-byte vector per piece, exactly
+__device__ __forceinline__ void split8(const float* v, uint4& p0, uint4& p1, uint4& p2) {
+  uint32_t q0[4], q1[4], q2[4];
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int64_t pg = px0 + wn * 64 + 32 * j + l31;
-      if (pg >= NP) continue;
+  for (int e = 0; e < 4; ++e) {
+    const float a = v[2 * e], b = v[2 * e + 1];
+    q0[e] = cvt_pk(a, b);
+    const float ra = a - __uint_as_float(q0[e] << 16), rb = b - __uint_as_float(q0[e] & 0xffff0000u);
+    q1[e] = cvt_pk(ra, rb);
+    const float sa = ra - __uint_as_float(q1[e] << 16), sb = rb - __uint_as_float(q1[e] & 0xffff0000u);
+    q2[e] = cvt_pk(sa, sb);
+  }
+  p0 = make_uint4(q0[0], q0[1], q0[2], q0[3]);
+  p1 = make_uint4(q1[0], q1[1], q1[2], q1[3]);
+  p2 = make_uint4(q2[0], q2[1], q2[2], q2[3]);
+}
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ bf16x8 frag(const unsigned char* q) {
+  return __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(q));
+}
+}  // namespace cgx
+
+template <int BM>
+__global__ __launch_bounds__(256, 2) void conv_gen_x6_kernel(ConvGenParams p, const float* wt,
+                                                             int act) {
+  constexpr int BN = 16384 / BM;
+  constexpr int WN = BN / 64;                 // waves along pixels (2 or 4)
+  constexpr int AR = CG_BK * BM / 256;        // consecutive k per thread, A (16 / 8)
+  constexpr int BR = CG_BK * BN / 256;        // consecutive k per thread, B (16 / 32)
+  constexpr int APL = BM * cgx::RS, BPL = BN * cgx::RS;   // plane bytes
+  __shared__ __attribute__((aligned(16))) unsigned char sA[3 * APL];
+  __shared__ __attribute__((aligned(16))) unsigned char sB[3 * BPL];
+  static_assert(3 * APL >= WN * BM * 2 * (int)sizeof(double), "epilogue scratch");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int KK = p.KH * p.KW;
+  const int K0 = KK * p.s0.C;
+  const int K = KK * p.Cin;
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px0 = (int64_t)blockIdx.x * BN;
+  const int co0 = blockIdx.y * BM;
+  const int kt_begin = blockIdx.z * p.ktiles_per_split;
+  int kt_end = kt_begin + p.ktiles_per_split;
+  const int nkt_all = (K + CG_BK - 1) / CG_BK;
+  if (kt_end > nkt_all) kt_end = nkt_all;
+
+  // B staging: pixel bpx = tid % BN, k run [bkq*BR, bkq*BR + BR) (wave-uniform)
+  const int bpx = tid % BN, bkq = tid / BN;
+  const int64_t pix = px0 + bpx;
+  const bool pv = pix < NP;
+  int n = 0, by = 0, bx = 0;
+  if (pv) {
+    n = (int)(pix / HWo);
+    const int r = (int)(pix - (int64_t)n * HWo);
+    const int oy = r / p.Wo, ox = r - oy * p.Wo;
+    by = oy * p.stride - p.pad;
+    bx = ox * p.stride - p.pad;
+  }
+  // A staging: output channel aco = tid % BM, k run [akq*AR, akq*AR + AR)
+  const int aco = tid % BM, akq = tid / BM;
+  const bool acok = co0 + aco < p.Cout;
+
+  float ra[AR], rb[BR];
+  auto gather1 = [&](int k) -> float {        // generic: one element of X[k][pix]
+    if (!pv || k >= K) return 0.f;
+    const bool first = k < K0;
+    const ConvSrcDev& s = first ? p.s0 : p.s1;
+    const int kr = first ? k : k - K0;
+    const int tap = kr / s.C, cs = kr - tap * s.C;
+    const int ky = tap / p.KW, kx = tap - ky * p.KW;
+    const int iy = by + ky, ix = bx + kx;
+    if (iy < 0 || iy >= p.Hin || ix < 0 || ix >= p.Win) return 0.f;
+    const int sy = src_coord(iy, s.Hs, p.Hin, s.up), sx = src_coord(ix, s.Ws, p.Win, s.up);
+    const int64_t plane = (int64_t)s.Hs * s.Ws;
+    const int64_t off = (int64_t)sy * s.Ws + sx;
+    float v = s.x[((int64_t)n * s.C + cs) * plane + off];
+    if (s.m) v *= s.m[(int64_t)n * plane + off];
+    return v;
+  };
+  auto fetch = [&](int kt) {
+    const int k0 = kt * CG_BK;
+#pragma unroll
+    for (int i = 0; i < AR; ++i) {
+      const int k = k0 + akq * AR + i;
+      ra[i] = (acok && k < K) ? wt[(int64_t)k * p.Cout + co0 + aco] : 0.f;
+    }
+    const bool first = k0 < K0;
+    const ConvSrcDev& s = first ? p.s0 : p.s1;
+    if (s.C % CG_BK == 0) {                   // the whole tile is one tap of one source
+      const int kr = first ? k0 : k0 - K0;
+      const int tap = kr / s.C, ci0 = kr - tap * s.C;
+      const int ky = tap / p.KW, kx = tap - ky * p.KW;
+      const int iy = by + ky, ix = bx + kx;
+      const bool inb = pv && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
+      const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
+      const int64_t plane = (int64_t)s.Hs * s.Ws;
+      const int64_t off = (int64_t)sy * s.Ws + sx;
+      const float mv = (inb && s.m) ? s.m[(int64_t)n * plane + off] : 1.f;
+      const float* base = s.x + ((int64_t)n * s.C + ci0 + bkq * BR) * plane + off;
+#pragma unroll
+      for (int i = 0; i < BR; ++i) rb[i] = inb ? base[(int64_t)i * plane] * mv : 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < BR; ++i)
+        rb[i] = gather1(__builtin_amdgcn_readfirstlane(k0 + bkq * BR + i));
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < AR; i += 8) {
+      uint4 q0, q1, q2;
+      cgx::split8(ra + i, q0, q1, q2);
+      unsigned char* q = sA + aco * cgx::RS + (akq * AR + i) * 2;
+      *reinterpret_cast<uint4*>(q) = q0;
+      *reinterpret_cast<uint4*>(q + APL) = q1;
+      *reinterpret_cast<uint4*>(q + 2 * APL) = q2;
+    }
+#pragma unroll
+    for (int i = 0; i < BR; i += 8) {
+      uint4 q0, q1, q2;
+      cgx::split8(rb + i, q0, q1, q2);
+      unsigned char* q = sB + bpx * cgx::RS + (bkq * BR + i) * 2;
+      *reinterpret_cast<uint4*>(q) = q0;
+      *reinterpret_cast<uint4*>(q + BPL) = q1;
+      *reinterpret_cast<uint4*>(q + 2 * BPL) = q2;
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, lh = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (kt_begin < kt_end) fetch(kt_begin);
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    commit();
+    __syncthreads();
+    if (kt + 1 < kt_end) fetch(kt + 1);
+#pragma unroll
+    for (int st = 0; st < CG_BK / 16; ++st) {
+      cgx::bf16x8 a[3][2], b[3][2];
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          a[q][i] = cgx::frag(sA + q * APL + (wm * 64 + i * 32 + l31) * cgx::RS + 32 * st + 16 * lh);
+          b[q][i] = cgx::frag(sB + q * BPL + (wn * 64 + i * 32 + l31) * cgx::RS + 32 * st + 16 * lh);
+        }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int co = co0 + wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (co < p.Cout) pb[(int64_t)co * NP + pg] = acc[i][j][r];
+        for (int j = 0; j < 2; ++j) {
+          f32x16 c = acc[i][j];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
+          acc[i][j] = c;
         }
     }
-    return;
-  }
-  // ---------------- epilogue
-  const float sc = p.scale ? *p.scale : 1.f;
-  bool ok[2];
-  float rt[2];
-  float* yb[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t pg = px0 + wn * 64 + 32 * j + l31;
-    ok[j] = pg < NP;
-    int pn = 0, prem = 0;
-    if (ok[j]) {
-      pn = (int)(pg / HWo);
-      prem = (int)(pg - (int64_t)pn * HWo);
-    }
-    rt[j] = (ok[j] && p.ratio) ? p.ratio[pg] : 1.f;
-    yb[j] = p.y + (int64_t)pn * p.Cout * HWo + prem;
-  }
-  double* red = reinterpret_cast<double*>(sA);     // [WN][BM][2] doubles (fits in sA)
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int cl = wm * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      const int co = co0 + cl;
-      const bool cok = co < p.Cout;
-      const float bv = (cok && p.bias) ? p.bias[co] : 0.f;
-      double a = 0.0, b = 0.0;
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        if (!ok[j] || !cok) continue;
-        float v = acc[i][j][r] * sc;
-        v *= rt[j];
-        v += bv;
-        a += (double)v;
-        b += (double)v * (double)v;
-        yb[j][(int64_t)co * HWo] = apply_act(v, act, p.slope);
-      }
-      if (p.stats) {
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-          a += __shfl_xor(a, o, 64);
-          b += __shfl_xor(b, o, 64);
-        }
-        if (l31 == 0) {
-          red[(wn * BM + cl) * 2 + 0] = a;
-          red[(wn * BM + cl) * 2 + 1] = b;
-        }
-      }
-    }
-  }
-  if (p.stats) {
     __syncthreads();
-    if (tid < BM) {
-      const int co = co0 + tid;
-      if (co < p.Cout) {
-        double a = 0.0, b = 0.0;
-        for (int q = 0; q < WN; ++q) {
-          a += red[(q * BM + tid) * 2];
-          b += red[(q * BM + tid) * 2 + 1];
-        }
-        p.stats[((int64_t)blockIdx.x * 2 + 0) * p.Cout + co] = a;
-        p.stats[((int64_t)blockIdx.x * 2 + 1) * p.Cout + co] = b;
-      }
-    }
   }
+  conv_gen_epilogue<BM>(p, acc, act, reinterpret_cast<double*>(sA));
 }
 
 // Split-K epilogue: y[n][co][p] = act(sum_z partial[z][co][px] * scale * ratio + bias),
@@ -949,7 +1158,16 @@ extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H
   }
   const int64_t tiles = cdiv(NP, 16384 / BM);
   dim3 grid((unsigned)tiles, (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
-  if (BM == 128)
+  // fp32-accurate split-bf16 main loop unless AINP_CONV_EXACT=1 (exact f32 MFMA)
+  static const bool exact = [] {
+    const char* e = getenv("AINP_CONV_EXACT");
+    return e && e[0] == '1';
+  }();
+  if (!exact && BM == 128)
+    hipLaunchKernelGGL(conv_gen_x6_kernel<128>, grid, dim3(256), 0, s, p, wt, act);
+  else if (!exact)
+    hipLaunchKernelGGL(conv_gen_x6_kernel<64>, grid, dim3(256), 0, s, p, wt, act);
+  else if (BM == 128)
     hipLaunchKernelGGL(conv_gen_fwd_kernel<128>, grid, dim3(256), 0, s, p, wt, act);
   else
     hipLaunchKernelGGL(conv_gen_fwd_kernel<64>, grid, dim3(256), 0, s, p, wt, act);
