@@ -295,23 +295,33 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
   for (int ch = 0; ch < nch; ++ch) {
     const int buf = ch & 1;
     if (ch + 1 < nch) load_chunk(ch + 1);
+    // Everything of a step that does not depend on dh_rec (the previous
+    // step's matvec) is loaded and folded into two coefficients one step
+    // ahead, while that matvec runs; the serial chain per step is then
+    // dh -> dc -> da -> LDS -> barrier -> matvec -> DPP reduce.
+    float ca = 0.f, cq = 0.f, cf = 0.f, dd = 0.f;  // og*(1-tc^2), gate-q factor, fg, dh_out
+    auto prep = [&](int s, int t) {
+      const float ig = gsm[buf][s][k], fg = gsm[buf][s][H + k];
+      const float gg = gsm[buf][s][2 * H + k], og = gsm[buf][s][3 * H + k];
+      const float tc = tanh_hw(csm[buf][s][k]);
+      const float cp = (t > 0) ? csm[buf][s + 1][k] : 0.f;
+      ca = og * (1.f - tc * tc);
+      cf = fg;
+      dd = dsm[buf][s][k];
+      if (q == 0) cq = gg * (ig * (1.f - ig));            // d pre_i = dc * cq
+      else if (q == 1) cq = cp * (fg * (1.f - fg));       // d pre_f = dc * cq
+      else if (q == 2) cq = ig * (1.f - gg * gg);         // d pre_g = dc * cq
+      else cq = tc * (og * (1.f - og));                   // d pre_o = dh * cq
+    };
+    if (ch * LCH < T) prep(0, T - 1 - ch * LCH);
     for (int s = 0; s < LCH; ++s) {
       const int uu = ch * LCH + s;
       if (uu >= T) break;
       const int t = T - 1 - uu;
-      const float ig = gsm[buf][s][k], fg = gsm[buf][s][H + k];
-      const float gg = gsm[buf][s][2 * H + k], og = gsm[buf][s][3 * H + k];
-      const float cc = csm[buf][s][k];
-      const float cp = (t > 0) ? csm[buf][s + 1][k] : 0.f;
-      const float dh = dsm[buf][s][k] + dh_rec;
-      const float tc = tanh_hw(cc);
-      const float dc = fmaf(dh * og, 1.f - tc * tc, dc_next);
-      dc_next = dc * fg;
-      float da;
-      if (q == 0) da = (dc * gg) * ig * (1.f - ig);            // d pre_i
-      else if (q == 1) da = (dc * cp) * fg * (1.f - fg);       // d pre_f
-      else if (q == 2) da = (dc * ig) * (1.f - gg * gg);       // d pre_g
-      else da = (dh * tc) * og * (1.f - og);                   // d pre_o
+      const float dh = dd + dh_rec;
+      const float dc = fmaf(dh, ca, dc_next);
+      dc_next = dc * cf;
+      const float da = (q == 3 ? dh : dc) * cq;
       const int64_t tt = tix(t);
       float* db = dgb[uu & 1];
       {
@@ -320,6 +330,7 @@ __global__ __launch_bounds__(4 * H, 1) void lstm_bwd_kernel(
       }
       dgrow[tt * 8 * H] = da;
       lds_barrier();
+      if (s + 1 < LCH && uu + 1 < T) prep(s + 1, t - 1);
       const float* dq = db + rg * (RPG + 4);
       f2 a[4], b[4];
 #pragma unroll

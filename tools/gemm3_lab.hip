@@ -301,6 +301,102 @@ __global__ __launch_bounds__(THREADS, WGS) void gemm3_kernel(int64_t M, int64_t 
     }
 }
 
+// ---- 8-wave variant (KC/KC only): 512 threads per 128x128 tile, wave = 64x32
+template <int WGS>
+__global__ __launch_bounds__(512, WGS) void gemm3w8_kernel(int64_t M, int64_t N, int64_t K,
+                                                            Ptrs P, int64_t lda, int64_t ldb,
+                                                            int64_t ldc, int tiles_n) {
+  constexpr int BK = 16;
+  using I = Img3<BK>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * I::BYTES];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + I::BYTES;
+  const int64_t nwg = gridDim.x;
+  const int64_t bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8;
+  const int64_t q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + 127) / 128;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t g = bid / per_group;
+  const int64_t first_n = g * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t tn = first_n + (in_g % gsize), tm = in_g / gsize;
+  const int64_t m0 = tm * 128, n0 = tn * 128;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 2) * 64, wn = (wave & 3) * 32;
+  const int li = lane & 31, lh = lane >> 5;
+  const int b = blockIdx.y;
+  const float* A = P.A[b];
+  const float* B = P.B[b];
+  f32x16 acc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  const int rr = tid >> 2, kk = (tid & 3) * 4;
+  float4 va, vb;
+  auto load = [&](int64_t k0) {
+    va = (m0 + rr < M) ? *reinterpret_cast<const float4*>(A + (m0 + rr) * lda + k0 + kk)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+    vb = (n0 + rr < N) ? *reinterpret_cast<const float4*>(B + (n0 + rr) * ldb + k0 + kk)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto store = [&]() {
+    uint32_t a0, a1, a2, b0, b1, b2;
+    unsigned char* q = As + rr * I::RS + kk * 2;
+    split2(va.x, va.y, a0, a1, a2);
+    split2(va.z, va.w, b0, b1, b2);
+    *reinterpret_cast<uint2*>(q) = make_uint2(a0, b0);
+    *reinterpret_cast<uint2*>(q + I::PLANE) = make_uint2(a1, b1);
+    *reinterpret_cast<uint2*>(q + 2 * I::PLANE) = make_uint2(a2, b2);
+    q = Bs + rr * I::RS + kk * 2;
+    split2(vb.x, vb.y, a0, a1, a2);
+    split2(vb.z, vb.w, b0, b1, b2);
+    *reinterpret_cast<uint2*>(q) = make_uint2(a0, b0);
+    *reinterpret_cast<uint2*>(q + I::PLANE) = make_uint2(a1, b1);
+    *reinterpret_cast<uint2*>(q + 2 * I::PLANE) = make_uint2(a2, b2);
+  };
+  const int64_t nk = K / BK;
+  load(0);
+  for (int64_t it = 0; it < nk; ++it) {
+    if (it > 0) __syncthreads();
+    store();
+    __syncthreads();
+    if (it + 1 < nk) load((it + 1) * BK);
+    bf16x8 a[3][2], bq[3];
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) a[p][i] = frag<BK>(As, p, wm + i * 32 + li, 0, lh);
+      bq[p] = frag<BK>(Bs, p, wn + li, 0, lh);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      f32x16 c = acc[i];
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], bq[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bq[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bq[2], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], bq[0], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bq[1], c, 0, 0, 0);
+      c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], bq[0], c, 0, 0, 0);
+      acc[i] = c;
+    }
+  }
+  float* C = P.C[b];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int64_t n = n0 + wn + li;
+    if (n >= N) continue;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (m < M) C[m * ldc + n] = acc[i][r];
+    }
+  }
+}
+
 // ------------------------------------------------------------------ harness
 struct Shape {
   const char* name;
@@ -459,6 +555,19 @@ int main() {
     check(dR0, "product x6 (stream-K if chosen)", mp);
     float mq = timeit([&] { prod(0, false); });
     check(dR0, "product x6 plain grid", mq);
+    if (s.akc && s.bkc) {
+      const int tn = (int)((s.N + 127) / 128), tmm = (int)((s.M + 127) / 128);
+      float w2 = timeit([&] {
+        hipLaunchKernelGGL((gemm3w8_kernel<2>), dim3(tmm * tn, 2), dim3(512), 0, st, s.M, s.N,
+                           s.K, P, s.lda, s.ldb, s.N, tn);
+      });
+      check(dC0, "8-wave 64x32/wave, 2 WG/CU", w2);
+      float w3 = timeit([&] {
+        hipLaunchKernelGGL((gemm3w8_kernel<3>), dim3(tmm * tn, 2), dim3(512), 0, st, s.M, s.N,
+                           s.K, P, s.lda, s.ldb, s.N, tn);
+      });
+      check(dC0, "8-wave 64x32/wave, 3 WG/CU", w3);
+    }
     float m1 = timeit([&] { run3<16, 2, true>(s, P, st); });
     CK(hipGetLastError());
     check(dC0, "bf16x6 BK16 2WG double-buffered", m1);
