@@ -909,6 +909,9 @@ using namespace ainp;
 
 namespace ainp {
 int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W);
+int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
+                         float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
+                         int ci0, int cp, int grid, hipStream_t s);
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s);
@@ -1064,7 +1067,13 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
   hipLaunchKernelGGL((conv3x3_wgrad_t<CPV, COV>), dim3(WG_BLOCKS),                    \
                      dim3(WgradT<CPV, COV>::NW * 64), 0, s, x,                          \
                      in_scale, in_shift, dy, partial, (int)N, Cin, (int)H, (int)W, ci0)
-    switch (key) {
+    // split-bf16 kernel where it is instantiated (conv_x6.hip), unless
+    // AINP_CONV_EXACT=1; same slab format
+    int rc = (fits && !conv_exact_env())
+                 ? conv_wgrad_x6_launch(x, in_scale, in_shift, dy, partial, N, Cin, Cout, H, W,
+                                        ci0, cp, WG_BLOCKS, s)
+                 : 1;
+    if (rc == 1) switch (key) {
       case 1616: AINP_WGT(16, 16); break;
       case 1632: AINP_WGT(16, 32); break;
       case 1664: AINP_WGT(16, 64); break;
@@ -1080,7 +1089,7 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
     }
 #undef AINP_WGT
 #undef AINP_WG
-    int rc = check_launch("conv3x3_wgrad_mfma");
+    if (rc == 1) rc = check_launch("conv3x3_wgrad_mfma");
     if (rc) return rc;
     const int J = 9 * cp;
     const int per = CTp * 16 * (J + 1);

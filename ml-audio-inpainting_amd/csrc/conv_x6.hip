@@ -42,6 +42,7 @@ constexpr int XI = (XU + NT - 1) / NT;   // units per thread (3)
 }  // namespace cx6
 
 typedef __bf16 bf16x8c __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4c __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t cx6_cvt_pk(float lo, float hi) {
   uint32_t r;
@@ -185,19 +186,18 @@ __global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
 #pragma unroll
         for (int j = 0; j < 2; ++j) b[p][j] = cx6_ld(xb + p * XPLANE + j * XROW);
       }
+      // term-major over the NI x 2 accumulators: no back-to-back dependent MFMAs
 #pragma unroll
-      for (int i = 0; i < NI; ++i)
+      for (int t = 0; t < 6; ++t) {
+        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
+        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x16 c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
-          acc[i][j] = c;
-        }
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa][i], b[pb][j], acc[i][j], 0,
+                                                                0, 0);
+      }
     }
   }
 
@@ -281,6 +281,258 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
   AINP_X6(32, 64) AINP_X6(64, 32)
 #undef AINP_X6
   return 1;
+}
+
+// ------------------------------------------------------------------ wgrad
+// Weight gradient D[co][(tap, ci)] = sum_pixel dy[co][pixel] * act(x)[ci][pixel + tap]
+// of a 32-input-channel pass, on the same split-bf16 arithmetic:
+//  * persistent workgroups walk strided sets of 2 x 48-pixel tiles (the
+//    reduction dimension) and write one fp32 partial slab each, in the slab
+//    format of conv.hip's wgrad kernels, summed there by wgrad_reduce1/
+//    wgrad_reduce in fixed order (deterministic);
+//  * A = dy [co][96 tile pixels], three bf16 planes with 208-byte rows (the
+//    32x32x16 A fragment is one conflict-free ds_read_b128);
+//  * B = act(x) on the 4 x 50 halo, channel-last [pixel][32 ci] per plane
+//    (pixel rows 52 apart, 16-byte channel groups XOR-swizzled by pixel bits
+//    1-2): the B fragment of a tap (8 pixels x one ci per lane) is two
+//    ds_read_b64_tr_b16 transposing reads, each 4 consecutive shifted pixels x
+//    16 channels, conflict-free and 8-byte aligned for every tap shift;
+//  * wave = (co tile, tap row): the three taps of a row reuse its A fragments;
+//  * the next tile's x and dy are prefetched into registers during the MFMAs;
+//  * dbias[co] = sum of dy, per staging unit in fp32, reduced in fixed order.
+namespace wx6 {
+constexpr int FT = 2, TT = 48;              // tile rows x columns (96 pixels, 6 k-steps)
+constexpr int HR = FT + 2, HC = TT + 2;     // halo 4 x 50
+constexpr int HS = 52;                      // halo row stride in pixels (== 4 mod 8)
+constexpr int XPL = ((HR - 1) * HS + HC) * 64;  // one plane: [pixel][32 ci] bf16
+constexpr int GRS = FT * TT * 2 + 16;       // dy row bytes (208)
+constexpr int XU = HR * HC * 4;             // x staging units (pixel, 8-ci group)
+constexpr int GPR = TT / 8;                 // dy units per tile row (8 columns each)
+}  // namespace wx6
+
+typedef short v4s16 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int wx6_clamp(int v, int lo, int hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+// buffer loads: 32-bit per-lane offsets + a scalar channel-plane offset, so no
+// per-load 64-bit addresses are kept live across the tile loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wx6_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ float wx6_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
+__device__ __forceinline__ v4s16 wx6_tr(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (__attribute__((address_space(3))) v4s16*)(p));
+}
+
+template <int CO>
+__global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
+    const float* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const float* __restrict__ dy,
+    float* __restrict__ partial, int N, int Cin, int H, int W, int ci0) {
+  using namespace wx6;
+  constexpr int CP = 32, J = 9 * CP, NI = CO / 32;
+  constexpr int NT = NI * 3 * 64;
+  constexpr int XI = (XU + NT - 1) / NT;
+  constexpr int GU = CO * FT * GPR, GI = (GU + NT - 1) / NT;
+  constexpr int GPL = CO * GRS;
+  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPL];
+  __shared__ __attribute__((aligned(16))) unsigned char sg[3 * GPL];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ct = wave % NI, dyt = wave / NI;  // co tile, tap row
+  // transposing-read bases: lane 4q+p of 16-lane group g supplies pixel
+  // (8*(g>>1) + q) at channels 16*(g&1) + 4p .. +3; the k-step and the second
+  // read add pixel offsets of 0 or 4 (mod 8), which flip swizzle bit 1
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  const int chunk = 2 * (g & 1) + (pp >> 1);
+  int bx[3][2];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int bp = dyt * HS + dx + 8 * (g >> 1) + q;
+#pragma unroll
+    for (int par = 0; par < 2; ++par)
+      bx[dx][par] = bp * 64 + 16 * (chunk ^ ((bp >> 1) & 3) ^ (2 * par)) + 8 * (pp & 1);
+  }
+  const int ga = (ct * 32 + li) * GRS + 16 * lh;
+
+  f32x16 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  float bsum[GI];
+#pragma unroll
+  for (int i = 0; i < GI; ++i) bsum[i] = 0.f;
+
+  const int tiles_t = (W + TT - 1) / TT, tiles_f = (H + FT - 1) / FT;
+  const int64_t ntiles = (int64_t)N * tiles_f * tiles_t;
+  const int64_t HW = (int64_t)H * W;
+  auto tile_coords = [&](int64_t tile, int& n, int& f0, int& t0) {
+    t0 = (int)(tile % tiles_t) * TT;
+    f0 = (int)((tile / tiles_t) % tiles_f) * FT;
+    n = (int)(tile / ((int64_t)tiles_t * tiles_f));
+  };
+
+  // act(x) = relu(x * scale + shift) coefficients of this pass's channels
+  __shared__ __attribute__((aligned(16))) float s_ss[2 * CP];
+  if (tid < 2 * CP)
+    s_ss[tid] = in_scale ? (tid < CP ? in_scale[ci0 + tid] : in_shift[ci0 + tid - CP]) : 0.f;
+  __syncthreads();
+
+  float px[XI][8], pg[GI][8];
+  auto fetch = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+    int plane = (int)(HW * 4);
+    asm volatile("" : "+s"(plane));  // keep c * plane out of the tile loop
+    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * Cin + ci0) * HW);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      const int pix = u % (HR * HC), grp = u < XU ? u / (HR * HC) : 3;
+      const int gr = wx6_clamp(f0 - 1 + pix / HC, 0, H - 1);
+      const int gc = wx6_clamp(t0 - 1 + pix % HC, 0, W - 1);
+      const int vo = 8 * grp * plane + (gr * W + gc) * 4;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+    }
+    const __amdgpu_buffer_rsrc_t rg = wx6_rsrc(dy + (int64_t)n * CO * HW);
+#pragma unroll
+    for (int i = 0; i < GI; ++i) {
+      const int u = tid + NT * i;
+      const int g8 = u % GPR, row = (u / GPR) % FT, co = u < GU ? u / (GPR * FT) : CO - 1;
+      const int vo = co * plane + wx6_clamp(f0 + row, 0, H - 1) * W * 4;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pg[i][e] = wx6_ld(rg, vo + wx6_clamp(t0 + 8 * g8 + e, 0, W - 1) * 4, 0);
+    }
+  };
+  auto commit = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      if (u < XU) {
+        const int pix = u % (HR * HC), grp = u / (HR * HC);
+        const int hr = pix / HC, hc = pix % HC;
+        const int gr = f0 - 1 + hr, gc = t0 - 1 + hc;
+        const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float t = px[i][c];
+          if (in_scale) t = fmaxf(fmaf(t, s_ss[8 * grp + c], s_ss[CP + 8 * grp + c]), 0.f);
+          v[c] = inb ? t : 0.f;
+        }
+        uint4 p0, p1, p2;
+        cx6_split8(v, p0, p1, p2);
+        const int sp = hr * HS + hc;
+        unsigned char* d = sx + sp * 64 + 16 * (grp ^ ((sp >> 1) & 3));
+        *reinterpret_cast<uint4*>(d) = p0;
+        *reinterpret_cast<uint4*>(d + XPL) = p1;
+        *reinterpret_cast<uint4*>(d + 2 * XPL) = p2;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < GI; ++i) {
+      const int u = tid + NT * i;
+      if (u < GU) {
+        const int g8 = u % GPR, row = (u / GPR) % FT, co = u / (GPR * FT);
+        const bool rok = f0 + row < H;
+        float v[8], sum = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[e] = (rok && t0 + 8 * g8 + e < W) ? pg[i][e] : 0.f;
+          sum += v[e];
+        }
+        bsum[i] += sum;
+        uint4 p0, p1, p2;
+        cx6_split8(v, p0, p1, p2);
+        unsigned char* d = sg + co * GRS + (row * TT + 8 * g8) * 2;
+        *reinterpret_cast<uint4*>(d) = p0;
+        *reinterpret_cast<uint4*>(d + GPL) = p1;
+        *reinterpret_cast<uint4*>(d + 2 * GPL) = p2;
+      }
+    }
+  };
+
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    commit(tile);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
+#pragma unroll
+    for (int ks = 0; ks < FT * TT / 16; ++ks) {
+      bf16x8c a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p] = cx6_ld(sg + p * GPL + ga + ks * 32);
+      const int kc = (ks / 3) * HS + (ks % 3) * 16;  // k-step's first pixel (row, column)
+      bf16x8c b[3][3];
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int blo = (ks / 3) & 1 ? bx[dx][1] : bx[dx][0];
+        const int bhi = (ks / 3) & 1 ? bx[dx][0] : bx[dx][1];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) {
+          const v4s16 lo = wx6_tr(sx + p * XPL + blo + kc * 64);
+          const v4s16 hi = wx6_tr(sx + p * XPL + bhi + (kc + 4) * 64);
+          b[dx][p] = __builtin_shufflevector(__builtin_bit_cast(bf16x4c, lo),
+                                             __builtin_bit_cast(bf16x4c, hi), 0, 1, 2, 3, 4, 5,
+                                             6, 7);
+        }
+      }
+      // the three taps' accumulators interleaved: no back-to-back dependent MFMAs
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
+        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+          acc[dx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[dx][pb], acc[dx], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // slab [CO][J + 1]: D[co = 32ct + (r&3) + 8(r>>2) + 4lh][ci = li] of tap 3dyt+dx
+  float* slab = partial + (int64_t)blockIdx.x * CO * (J + 1);
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      slab[co * (J + 1) + (3 * dyt + dx) * CP + li] = acc[dx][r];
+    }
+  float* red = reinterpret_cast<float*>(sx);  // free after the loop's last barrier
+#pragma unroll
+  for (int i = 0; i < GI; ++i)
+    if (tid + NT * i < GU) red[tid + NT * i] = bsum[i];
+  __syncthreads();
+  if (tid < CO) {
+    float sum = 0.f;
+#pragma unroll
+    for (int k = 0; k < FT * GPR; ++k) sum += red[tid * FT * GPR + k];
+    slab[tid * (J + 1) + J] = sum;
+  }
+}
+
+// Launch the split-bf16 weight gradient of one 32-channel pass if Cout has an
+// instantiation; returns 1 if not handled.  grid = persistent workgroups.
+int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
+                         float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
+                         int ci0, int cp, int grid, hipStream_t s) {
+  if (cp != 32 || Cout != 64) return 1;
+  hipLaunchKernelGGL((conv3x3_wgrad_x6<64>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy, partial,
+                     (int)N, Cin, (int)H, (int)W, ci0);
+  return check_launch("conv3x3_wgrad_x6");
 }
 
 }  // namespace ainp

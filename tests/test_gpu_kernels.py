@@ -226,7 +226,10 @@ def _act(x, sc, sh):
     (1, 8, 48, 11, 13, True),
     # small-channel kernels (1-2 channels on one side, 16 on the other), multi-tile
     (2, 1, 16, 41, 100, False), (3, 16, 1, 19, 97, True), (1, 2, 16, 12, 50, True),
-    (1, 16, 2, 25, 60, False)])
+    (1, 16, 2, 25, 60, False),
+    # split-bf16 weight gradient (32-channel passes x 64 outputs): the model's
+    # plane, two passes without a prologue, tiles smaller than one 2 x 48 tile
+    (2, 32, 64, 257, 334, True), (1, 64, 64, 19, 47, False), (3, 32, 64, 5, 3, True)])
 def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
     g = torch.Generator().manual_seed(N * 100 + Cin * 10 + Cout)
     x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
