@@ -286,28 +286,27 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
 // ------------------------------------------------------------------ wgrad
 // Weight gradient D[co][(tap, ci)] = sum_pixel dy[co][pixel] * act(x)[ci][pixel + tap]
 // of a 32-input-channel pass, on the same split-bf16 arithmetic:
-//  * persistent workgroups walk strided sets of 2 x 48-pixel tiles (the
-//    reduction dimension) and write one fp32 partial slab each, in the slab
-//    format of conv.hip's wgrad kernels, summed there by wgrad_reduce1/
-//    wgrad_reduce in fixed order (deterministic);
-//  * A = dy [co][96 tile pixels], three bf16 planes with 208-byte rows (the
-//    32x32x16 A fragment is one conflict-free ds_read_b128);
-//  * B = act(x) on the 4 x 50 halo, channel-last [pixel][32 ci] per plane
-//    (pixel rows 52 apart, 16-byte channel groups XOR-swizzled by pixel bits
-//    1-2): the B fragment of a tap (8 pixels x one ci per lane) is two
-//    ds_read_b64_tr_b16 transposing reads, each 4 consecutive shifted pixels x
-//    16 channels, conflict-free and 8-byte aligned for every tap shift;
-//  * wave = (co tile, tap row): the three taps of a row reuse its A fragments;
+//  * persistent workgroups walk strided sets of 4 x 24-pixel tiles (the
+//    reduction dimension, 6 k-steps of 16 pixels = two 8-pixel row segments)
+//    and write one fp32 partial slab each, in the slab format of conv.hip's
+//    wgrad kernels, summed there by wgrad_reduce1/wgrad_reduce in fixed order;
+//  * both operands are staged channel-last, three bf16 planes each, so every
+//    global load is coalesced along pixels and every fragment is two
+//    ds_read_b64_tr_b16 transposing reads (4 consecutive pixels x 16
+//    channels), conflict-free and 8-byte aligned for every tap shift:
+//      act(x): 6 x 26 halo, [pixel][32 ci], halo rows 32 pixels apart, the
+//              16-byte channel groups XOR-swizzled by pixel bits 1-2;
+//      dy:     [96 pixels][64 co], 16-byte groups swizzled by pixel bits 0-2;
+//  * wave = (co tile, tap row): the three taps of a row share the A fragments
+//    and interleave their accumulators;
 //  * the next tile's x and dy are prefetched into registers during the MFMAs;
 //  * dbias[co] = sum of dy, per staging unit in fp32, reduced in fixed order.
 namespace wx6 {
-constexpr int FT = 2, TT = 48;              // tile rows x columns (96 pixels, 6 k-steps)
-constexpr int HR = FT + 2, HC = TT + 2;     // halo 4 x 50
-constexpr int HS = 52;                      // halo row stride in pixels (== 4 mod 8)
-constexpr int XPL = ((HR - 1) * HS + HC) * 64;  // one plane: [pixel][32 ci] bf16
-constexpr int GRS = FT * TT * 2 + 16;       // dy row bytes (208)
-constexpr int XU = HR * HC * 4;             // x staging units (pixel, 8-ci group)
-constexpr int GPR = TT / 8;                 // dy units per tile row (8 columns each)
+constexpr int FT = 4, TT = 24, NPX = FT * TT;  // tile: 96 pixels, 6 k-steps
+constexpr int HR = FT + 2, HC = TT + 2;        // halo 6 x 26
+constexpr int HS = 32;                         // halo row stride (pixels, == 0 mod 8)
+constexpr int XPL = ((HR - 1) * HS + HC) * 64; // one plane: [pixel][32 ci] bf16
+constexpr int XU = HR * HC * 4;                // x staging units (pixel, 8-ci group)
 }  // namespace wx6
 
 typedef short v4s16 __attribute__((ext_vector_type(4)));
@@ -329,6 +328,15 @@ __device__ __forceinline__ v4s16 wx6_tr(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
       (__attribute__((address_space(3))) v4s16*)(p));
 }
+__device__ __forceinline__ bf16x8c wx6_cat(v4s16 lo, v4s16 hi) {
+  return __builtin_shufflevector(__builtin_bit_cast(bf16x4c, lo), __builtin_bit_cast(bf16x4c, hi),
+                                 0, 1, 2, 3, 4, 5, 6, 7);
+}
+// dy image: 16-byte group swizzle of a pixel (bijective on pixel bits 0-2;
+// pixels 2 apart use opposite 64-byte halves of their rows)
+__device__ __forceinline__ int wx6_gswz(int px) {
+  return (((px >> 1) & 1) << 2) | (((px >> 2) & 1) << 1) | (px & 1);
+}
 
 template <int CO>
 __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
@@ -339,37 +347,49 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
   constexpr int CP = 32, J = 9 * CP, NI = CO / 32;
   constexpr int NT = NI * 3 * 64;
   constexpr int XI = (XU + NT - 1) / NT;
-  constexpr int GU = CO * FT * GPR, GI = (GU + NT - 1) / NT;
-  constexpr int GPL = CO * GRS;
+  constexpr int NG = CO / 8;                   // dy 16-byte groups per pixel
+  constexpr int GU = NPX * NG, GI = (GU + NT - 1) / NT;
+  constexpr int GPX = CO * 2;                  // dy image bytes per pixel
+  constexpr int GPL = NPX * GPX;
+  static_assert(CO == 64 && NT % NPX == 0, "dy staging map: units of one thread share a pixel");
   __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPL];
   __shared__ __attribute__((aligned(16))) unsigned char sg[3 * GPL];
+  __shared__ __attribute__((aligned(16))) float s_ss[2 * CP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int ct = wave % NI, dyt = wave / NI;  // co tile, tap row
-  // transposing-read bases: lane 4q+p of 16-lane group g supplies pixel
-  // (8*(g>>1) + q) at channels 16*(g&1) + 4p .. +3; the k-step and the second
-  // read add pixel offsets of 0 or 4 (mod 8), which flip swizzle bit 1
+  // transposing reads: lane 4q+p of 16-lane group g supplies pixel q (+4 for
+  // the second read) of its 8-pixel segment at channels 16*(g&1) + 4p .. +3
   const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
-  const int chunk = 2 * (g & 1) + (pp >> 1);
-  int bx[3][2];
+  int bx[3][2];  // x: halo pixel dyt*HS + dx + q + 4s (segment origin added per k-step)
 #pragma unroll
-  for (int dx = 0; dx < 3; ++dx) {
-    const int bp = dyt * HS + dx + 8 * (g >> 1) + q;
+  for (int dx = 0; dx < 3; ++dx)
 #pragma unroll
-    for (int par = 0; par < 2; ++par)
-      bx[dx][par] = bp * 64 + 16 * (chunk ^ ((bp >> 1) & 3) ^ (2 * par)) + 8 * (pp & 1);
+    for (int sh = 0; sh < 2; ++sh) {
+      const int hp = dyt * HS + dx + q + 4 * sh;
+      bx[dx][sh] = hp * 64 + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((hp >> 1) & 3)) + 8 * (pp & 1);
+    }
+  int ba[2];     // dy: pixel 8*lh + q + 4s of the k-step, channels of co tile ct
+#pragma unroll
+  for (int sh = 0; sh < 2; ++sh) {
+    const int px = 8 * lh + q + 4 * sh;
+    ba[sh] = px * GPX + 16 * ((4 * ct + 2 * (g & 1) + (pp >> 1)) ^ wx6_gswz(px)) + 8 * (pp & 1);
   }
-  const int ga = (ct * 32 + li) * GRS + 16 * lh;
+
+  if (tid < 2 * CP)
+    s_ss[tid] = in_scale ? (tid < CP ? in_scale[ci0 + tid] : in_shift[ci0 + tid - CP]) : 0.f;
 
   f32x16 acc[3];
 #pragma unroll
   for (int t = 0; t < 3; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
-  float bsum[GI];
+  float bsum[GI][8];
 #pragma unroll
-  for (int i = 0; i < GI; ++i) bsum[i] = 0.f;
+  for (int i = 0; i < GI; ++i)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bsum[i][c] = 0.f;
 
   const int tiles_t = (W + TT - 1) / TT, tiles_f = (H + FT - 1) / FT;
   const int64_t ntiles = (int64_t)N * tiles_f * tiles_t;
@@ -379,12 +399,8 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     f0 = (int)((tile / tiles_t) % tiles_f) * FT;
     n = (int)(tile / ((int64_t)tiles_t * tiles_f));
   };
-
-  // act(x) = relu(x * scale + shift) coefficients of this pass's channels
-  __shared__ __attribute__((aligned(16))) float s_ss[2 * CP];
-  if (tid < 2 * CP)
-    s_ss[tid] = in_scale ? (tid < CP ? in_scale[ci0 + tid] : in_shift[ci0 + tid - CP]) : 0.f;
-  __syncthreads();
+  // the staging pixel of dy units (the same for all of a thread's units)
+  const int gpx = tid % NPX;
 
   float px[XI][8], pg[GI][8];
   auto fetch = [&](int64_t tile) {
@@ -396,21 +412,21 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
-      const int pix = u % (HR * HC), grp = u < XU ? u / (HR * HC) : 3;
-      const int gr = wx6_clamp(f0 - 1 + pix / HC, 0, H - 1);
-      const int gc = wx6_clamp(t0 - 1 + pix % HC, 0, W - 1);
+      const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : 3;
+      const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
+      const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
       const int vo = 8 * grp * plane + (gr * W + gc) * 4;
 #pragma unroll
       for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
     }
     const __amdgpu_buffer_rsrc_t rg = wx6_rsrc(dy + (int64_t)n * CO * HW);
+    const int gr = wx6_clamp(f0 + gpx / TT, 0, H - 1), gc = wx6_clamp(t0 + gpx % TT, 0, W - 1);
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int u = tid + NT * i;
-      const int g8 = u % GPR, row = (u / GPR) % FT, co = u < GU ? u / (GPR * FT) : CO - 1;
-      const int vo = co * plane + wx6_clamp(f0 + row, 0, H - 1) * W * 4;
+      const int grp = (tid + NT * i) / NPX;
+      const int vo = 8 * grp * plane + (gr * W + gc) * 4;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) pg[i][e] = wx6_ld(rg, vo + wx6_clamp(t0 + 8 * g8 + e, 0, W - 1) * 4, 0);
+      for (int c = 0; c < 8; ++c) pg[i][c] = wx6_ld(rg, vo, c * plane);
     }
   };
   auto commit = [&](int64_t tile) {
@@ -420,8 +436,8 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       if (u < XU) {
-        const int pix = u % (HR * HC), grp = u / (HR * HC);
-        const int hr = pix / HC, hc = pix % HC;
+        const int hp = u % (HR * HC), grp = u / (HR * HC);
+        const int hr = hp / HC, hc = hp % HC;
         const int gr = f0 - 1 + hr, gc = t0 - 1 + hc;
         const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
         float v[8];
@@ -440,29 +456,26 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
         *reinterpret_cast<uint4*>(d + 2 * XPL) = p2;
       }
     }
+    const bool pok = f0 + gpx / TT < H && t0 + gpx % TT < W;
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int u = tid + NT * i;
-      if (u < GU) {
-        const int g8 = u % GPR, row = (u / GPR) % FT, co = u / (GPR * FT);
-        const bool rok = f0 + row < H;
-        float v[8], sum = 0.f;
+      const int grp = (tid + NT * i) / NPX;
+      float v[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          v[e] = (rok && t0 + 8 * g8 + e < W) ? pg[i][e] : 0.f;
-          sum += v[e];
-        }
-        bsum[i] += sum;
-        uint4 p0, p1, p2;
-        cx6_split8(v, p0, p1, p2);
-        unsigned char* d = sg + co * GRS + (row * TT + 8 * g8) * 2;
-        *reinterpret_cast<uint4*>(d) = p0;
-        *reinterpret_cast<uint4*>(d + GPL) = p1;
-        *reinterpret_cast<uint4*>(d + 2 * GPL) = p2;
+      for (int c = 0; c < 8; ++c) {
+        v[c] = pok ? pg[i][c] : 0.f;
+        bsum[i][c] += v[c];
       }
+      uint4 p0, p1, p2;
+      cx6_split8(v, p0, p1, p2);
+      unsigned char* d = sg + gpx * GPX + 16 * (grp ^ wx6_gswz(gpx));
+      *reinterpret_cast<uint4*>(d) = p0;
+      *reinterpret_cast<uint4*>(d + GPL) = p1;
+      *reinterpret_cast<uint4*>(d + 2 * GPL) = p2;
     }
   };
 
+  __syncthreads();  // s_ss
   int64_t tile = blockIdx.x;
   if (tile < ntiles) fetch(tile);
   for (; tile < ntiles; tile += gridDim.x) {
@@ -470,33 +483,31 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     __syncthreads();
     if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
 #pragma unroll
-    for (int ks = 0; ks < FT * TT / 16; ++ks) {
+    for (int ks = 0; ks < NPX / 16; ++ks) {
+      // this lane's 8-pixel segment: G = 2ks + lh -> tile row G/3, column 8(G%3)
+      const int G0 = 2 * ks, G1 = 2 * ks + 1;
+      const int seg = lh ? (G1 / 3) * HS + (G1 % 3) * 8 : (G0 / 3) * HS + (G0 % 3) * 8;
       bf16x8c a[3];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) a[p] = cx6_ld(sg + p * GPL + ga + ks * 32);
-      const int kc = (ks / 3) * HS + (ks % 3) * 16;  // k-step's first pixel (row, column)
-      bf16x8c b[3][3];
+      for (int p = 0; p < 3; ++p)
+        a[p] = wx6_cat(wx6_tr(sg + p * GPL + ba[0] + ks * 16 * GPX),
+                       wx6_tr(sg + p * GPL + ba[1] + ks * 16 * GPX));
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
-        const int blo = (ks / 3) & 1 ? bx[dx][1] : bx[dx][0];
-        const int bhi = (ks / 3) & 1 ? bx[dx][0] : bx[dx][1];
+        const int o0 = bx[dx][0] + seg * 64, o1 = bx[dx][1] + seg * 64;
+        bf16x8c b[3];
 #pragma unroll
-        for (int p = 0; p < 3; ++p) {
-          const v4s16 lo = wx6_tr(sx + p * XPL + blo + kc * 64);
-          const v4s16 hi = wx6_tr(sx + p * XPL + bhi + (kc + 4) * 64);
-          b[dx][p] = __builtin_shufflevector(__builtin_bit_cast(bf16x4c, lo),
-                                             __builtin_bit_cast(bf16x4c, hi), 0, 1, 2, 3, 4, 5,
-                                             6, 7);
-        }
-      }
-      // the three taps' accumulators interleaved: no back-to-back dependent MFMAs
-#pragma unroll
-      for (int t = 0; t < 6; ++t) {
-        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
-        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
-          acc[dx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa], b[dx][pb], acc[dx], 0, 0, 0);
+        for (int p = 0; p < 3; ++p)
+          b[p] = wx6_cat(wx6_tr(sx + p * XPL + o0), wx6_tr(sx + p * XPL + o1));
+        // six cross terms, smallest first
+        f32x16 c = acc[dx];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+        acc[dx] = c;
       }
     }
     __syncthreads();
@@ -511,15 +522,18 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
       const int co = ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
       slab[co * (J + 1) + (3 * dyt + dx) * CP + li] = acc[dx][r];
     }
-  float* red = reinterpret_cast<float*>(sx);  // free after the loop's last barrier
+  // bias: [co][staging pixel] partials (free LDS after the loop's last barrier)
+  float* red = reinterpret_cast<float*>(sx);
 #pragma unroll
-  for (int i = 0; i < GI; ++i)
-    if (tid + NT * i < GU) red[tid + NT * i] = bsum[i];
+  for (int i = 0; i < GI; ++i) {
+    const int grp = (tid + NT * i) / NPX;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) red[(8 * grp + c) * NPX + gpx] = bsum[i][c];
+  }
   __syncthreads();
   if (tid < CO) {
     float sum = 0.f;
-#pragma unroll
-    for (int k = 0; k < FT * GPR; ++k) sum += red[tid * FT * GPR + k];
+    for (int k = 0; k < NPX; ++k) sum += red[tid * NPX + k];
     slab[tid * (J + 1) + J] = sum;
   }
 }
