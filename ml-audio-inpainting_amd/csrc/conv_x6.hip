@@ -538,11 +538,223 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
   }
 }
 
+// Small-channel variant for (Cin pass, Cout) = (32, 16) and (16, 32): one of
+// the two GEMM dimensions is 16, so the 32x32 tiles above would be half
+// empty.  Same tiles, staging, slabs and bias as conv3x3_wgrad_x6, on
+// v_mfma_f32_16x16x32_bf16 (16 x 16 outputs, 32 pixels per k-step):
+//  * 6 waves = (16-channel block of the 32-wide side, tap row) x 3 taps;
+//  * A (dy) and B (act(x)) fragments are two transposing reads each: lane
+//    group g (= lane >> 4) takes the k-step's 8-pixel segment 4ks + g;
+//  * both images keep 64 bytes per pixel; the 16-byte group swizzle
+//    f(px) = px bit 1 | (px bit 2 ^ px bit 3) << 1 keeps the writes
+//    (8 consecutive pixels) and the reads (two groups 8 pixels apart, the
+//    halo row stride being == 8 mod 16) conflict-free.
+namespace wx6s {
+constexpr int FT = 4, TT = 24, NPX = FT * TT;  // 96 pixels, 3 k-steps of 32
+constexpr int HR = FT + 2, HC = TT + 2;
+constexpr int HS = 40;                         // halo row stride (pixels, == 8 mod 16)
+constexpr int XPL = ((HR - 1) * HS + HC) * 64;
+constexpr int GPL = NPX * 64;
+}  // namespace wx6s
+
+__device__ __forceinline__ int wx6s_swz(int px) {
+  return ((px >> 1) & 1) | ((((px >> 2) ^ (px >> 3)) & 1) << 1);
+}
+
+template <int CP, int CO>
+__global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
+    const float* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const float* __restrict__ dy,
+    float* __restrict__ partial, int N, int Cin, int H, int W, int ci0) {
+  using namespace wx6s;
+  static_assert((CP == 32 && CO == 16) || (CP == 16 && CO == 32), "shape");
+  constexpr int J = 9 * CP, NT = 384;
+  constexpr int XG = CP / 8, XU = HR * HC * XG, XI = (XU + NT - 1) / NT;
+  constexpr int GG = CO / 8, GU = NPX * GG;     // dy units (pixel, 8-co group)
+  static_assert(GU <= NT, "one dy unit per thread");
+  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPL];
+  __shared__ __attribute__((aligned(16))) unsigned char sg[3 * GPL];
+  __shared__ __attribute__((aligned(16))) float s_ss[2 * CP];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int blk = wave & 1, dyt = wave >> 1;
+  const int cob = CO == 32 ? blk : 0, cib = CP == 32 ? blk : 0;
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  // transposing-read address of a pixel for this lane (lane 4q+pp of its
+  // group supplies pixel q (+4) at channels 4pp..4pp+3 of its 16-block)
+  auto xaddr = [&](int hp) {
+    return hp * 64 + 16 * ((2 * cib + (pp >> 1)) ^ wx6s_swz(hp)) + 8 * (pp & 1);
+  };
+  auto gaddr = [&](int px) {
+    return px * 64 + 16 * ((2 * cob + (pp >> 1)) ^ wx6s_swz(px)) + 8 * (pp & 1);
+  };
+
+  if (tid < 2 * CP)
+    s_ss[tid] = in_scale ? (tid < CP ? in_scale[ci0 + tid] : in_shift[ci0 + tid - CP]) : 0.f;
+
+  f32x4 acc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bsum[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) bsum[c] = 0.f;
+
+  const int tiles_t = (W + TT - 1) / TT, tiles_f = (H + FT - 1) / FT;
+  const int64_t ntiles = (int64_t)N * tiles_f * tiles_t;
+  const int64_t HW = (int64_t)H * W;
+  auto tile_coords = [&](int64_t tile, int& n, int& f0, int& t0) {
+    t0 = (int)(tile % tiles_t) * TT;
+    f0 = (int)((tile / tiles_t) % tiles_f) * FT;
+    n = (int)(tile / ((int64_t)tiles_t * tiles_f));
+  };
+  const int gpx = tid % NPX, ggrp = tid / NPX;   // this thread's dy unit (if tid < GU)
+
+  float px[XI][8], pg[8];
+  auto fetch = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+    int plane = (int)(HW * 4);
+    asm volatile("" : "+s"(plane));
+    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * Cin + ci0) * HW);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : XG - 1;
+      const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
+      const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
+      const int vo = 8 * grp * plane + (gr * W + gc) * 4;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+    }
+    const __amdgpu_buffer_rsrc_t rg = wx6_rsrc(dy + (int64_t)n * CO * HW);
+    const int gr = wx6_clamp(f0 + gpx / TT, 0, H - 1), gc = wx6_clamp(t0 + gpx % TT, 0, W - 1);
+    const int vo = 8 * (ggrp < GG ? ggrp : GG - 1) * plane + (gr * W + gc) * 4;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) pg[c] = wx6_ld(rg, vo, c * plane);
+  };
+  auto commit = [&](int64_t tile) {
+    int n, f0, t0;
+    tile_coords(tile, n, f0, t0);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      if (u < XU) {
+        const int hp = u % (HR * HC), grp = u / (HR * HC);
+        const int hr = hp / HC, hc = hp % HC;
+        const int gr = f0 - 1 + hr, gc = t0 - 1 + hc;
+        const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float t = px[i][c];
+          if (in_scale) t = fmaxf(fmaf(t, s_ss[8 * grp + c], s_ss[CP + 8 * grp + c]), 0.f);
+          v[c] = inb ? t : 0.f;
+        }
+        uint4 p0, p1, p2;
+        cx6_split8(v, p0, p1, p2);
+        const int sp = hr * HS + hc;
+        unsigned char* d = sx + sp * 64 + 16 * (grp ^ wx6s_swz(sp));
+        *reinterpret_cast<uint4*>(d) = p0;
+        *reinterpret_cast<uint4*>(d + XPL) = p1;
+        *reinterpret_cast<uint4*>(d + 2 * XPL) = p2;
+      }
+    }
+    if (tid < GU) {
+      const bool pok = f0 + gpx / TT < H && t0 + gpx % TT < W;
+      float v[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        v[c] = pok ? pg[c] : 0.f;
+        bsum[c] += v[c];
+      }
+      uint4 p0, p1, p2;
+      cx6_split8(v, p0, p1, p2);
+      unsigned char* d = sg + gpx * 64 + 16 * (ggrp ^ wx6s_swz(gpx));
+      *reinterpret_cast<uint4*>(d) = p0;
+      *reinterpret_cast<uint4*>(d + GPL) = p1;
+      *reinterpret_cast<uint4*>(d + 2 * GPL) = p2;
+    }
+  };
+
+  __syncthreads();  // s_ss
+  int64_t tile = blockIdx.x;
+  if (tile < ntiles) fetch(tile);
+  for (; tile < ntiles; tile += gridDim.x) {
+    commit(tile);
+    __syncthreads();
+    if (tile + gridDim.x < ntiles) fetch(tile + gridDim.x);
+#pragma unroll
+    for (int ks = 0; ks < NPX / 32; ++ks) {
+      // this lane group's 8-pixel segment G = 4ks + g: tile row G/3, column 8(G%3)
+      const int G = 4 * ks + g;
+      const int srow = G / 3, scol = (G % 3) * 8;
+      bf16x8c a[3];
+      {
+        const int o0 = gaddr(8 * G + q), o1 = gaddr(8 * G + q + 4);
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          a[p] = wx6_cat(wx6_tr(sg + p * GPL + o0), wx6_tr(sg + p * GPL + o1));
+      }
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        const int hp = (srow + dyt) * HS + scol + dx + q;
+        const int o0 = xaddr(hp), o1 = xaddr(hp + 4);
+        bf16x8c b[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          b[p] = wx6_cat(wx6_tr(sx + p * XPL + o0), wx6_tr(sx + p * XPL + o1));
+        // D[co][ci]: A = dy (rows co), B = act(x) (columns ci); six cross
+        // terms, smallest first
+        f32x4 c = acc[dx];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+        acc[dx] = c;
+      }
+    }
+    __syncthreads();
+  }
+
+  // slab [CO][J + 1]: D[co = 16cob + 4g + r][ci = 16cib + (lane & 15)] of tap 3dyt+dx
+  float* slab = partial + (int64_t)blockIdx.x * CO * (J + 1);
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int co = 16 * cob + 4 * g + r;
+      slab[co * (J + 1) + (3 * dyt + dx) * CP + 16 * cib + (lane & 15)] = acc[dx][r];
+    }
+  float* red = reinterpret_cast<float*>(sx);
+  if (tid < GU) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) red[(8 * ggrp + c) * NPX + gpx] = bsum[c];
+  }
+  __syncthreads();
+  if (tid < CO) {
+    float sum = 0.f;
+    for (int k = 0; k < NPX; ++k) sum += red[tid * NPX + k];
+    slab[tid * (J + 1) + J] = sum;
+  }
+}
+
 // Launch the split-bf16 weight gradient of one 32-channel pass if Cout has an
 // instantiation; returns 1 if not handled.  grid = persistent workgroups.
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
                          int ci0, int cp, int grid, hipStream_t s) {
+  if (cp == 32 && Cout == 16) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
+                       partial, (int)N, Cin, (int)H, (int)W, ci0);
+    return check_launch("conv3x3_wgrad_x6s");
+  }
+  if (cp == 16 && Cout == 32) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
+                       partial, (int)N, Cin, (int)H, (int)W, ci0);
+    return check_launch("conv3x3_wgrad_x6s");
+  }
   if (cp != 32 || Cout != 64) return 1;
   hipLaunchKernelGGL((conv3x3_wgrad_x6<64>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy, partial,
                      (int)N, Cin, (int)H, (int)W, ci0);

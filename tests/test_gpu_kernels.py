@@ -229,7 +229,9 @@ def _act(x, sc, sh):
     (1, 16, 2, 25, 60, False),
     # split-bf16 weight gradient (32-channel passes x 64 outputs): the model's
     # plane, two passes without a prologue, tiles smaller than one 2 x 48 tile
-    (2, 32, 64, 257, 334, True), (1, 64, 64, 19, 47, False), (3, 32, 64, 5, 3, True)])
+    (2, 32, 64, 257, 334, True), (1, 64, 64, 19, 47, False), (3, 32, 64, 5, 3, True),
+    # its 16x16x32 variant: (32 -> 16) and (16 -> 32) on the model's plane
+    (2, 32, 16, 257, 334, True), (2, 16, 32, 257, 334, False)])
 def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
     g = torch.Generator().manual_seed(N * 100 + Cin * 10 + Cout)
     x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64)
