@@ -914,7 +914,7 @@ int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const
                          int ci0, int cp, int grid, hipStream_t s);
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                   int Cout, int64_t H, int64_t W, hipStream_t s);
+                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts);
 
 // conv_x6.hip (fp32-accurate split-bf16 MFMA) serves every pair it has an
 // instantiation for unless AINP_CONV_EXACT=1 selects the exact f32 kernels.
@@ -957,8 +957,9 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
     return rc ? rc : zero_tail(exact_stat_parts(N, H, W));
   }
   if (!conv_exact_env()) {
-    const int rc = conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
-    if (rc != 1) return rc ? rc : zero_tail(conv_x6_stat_parts(N, H, W));
+    int64_t parts = 0;
+    const int rc = conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s, &parts);
+    if (rc != 1) return rc ? rc : zero_tail(parts);
   }
   {
     const int rc = zero_tail(exact_stat_parts(N, H, W));

@@ -26,6 +26,7 @@
 //    each output channel for the following BatchNorm (fp64, fixed order).
 // dgrad is the same kernel over dy with w'[ci][co][tap] = w[co][ci][8 - tap].
 #include "common.h"
+#include <stdlib.h>
 
 namespace ainp {
 
@@ -251,16 +252,33 @@ __global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
   }
 }
 
-// Number of BatchNorm partials the x6 kernel writes for an [N, H, W] output.
+// Upper bound on the BatchNorm partials an x6 launch writes for [N, H, W]
+// outputs: one per workgroup of the persistent kernel (<= 512), one per tile
+// of the tiled kernel.
 int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W) {
-  return N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
+  const int64_t tiled = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
+  return tiled > 512 ? tiled : 512;
 }
 
+int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
+                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
+                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts);
+
 // Launch if (Cin, Cout) has an x6 instantiation; returns 1 if not handled.
+// *parts = the number of BatchNorm partials written.  The persistent kernel
+// serves every pair it has (32-bit buffer offsets permitting); the tiled one
+// is kept for AINP_CONV_X6_TILED=1.
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                   int Cout, int64_t H, int64_t W, hipStream_t s) {
+                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts) {
   if (Cout > 64 || Cout < 16) return 1;
+  static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
+  if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
+    const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
+                                   parts);
+    if (rc != 1) return rc;
+  }
+  *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
 #define AINP_X6(CIV, COV)                                                                     \
@@ -738,6 +756,277 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     for (int k = 0; k < NPX; ++k) sum += red[tid * NPX + k];
     slab[tid * (J + 1) + J] = sum;
   }
+}
+
+// ------------------------------------------------------- persistent fwd/dgrad
+// Forward / data gradient as a persistent kernel: one workgroup per CU walks
+// a strided set of 8 x 32-pixel output tiles, so that
+//  * every K chunk's split weights stay resident in LDS for the whole launch
+//    (staged and split once, not per tile);
+//  * the next (tile, chunk) halo is prefetched into registers (buffer loads,
+//    32-bit offsets) while the current chunk's MFMAs run, across tile
+//    boundaries too;
+//  * the BatchNorm partials are accumulated per workgroup in fixed tile
+//    order (fp32 over a tile row's 32 pixels by a lane reduce-scatter, fp64
+//    across tiles) and written once: the partial count is the fixed grid.
+// Wave w owns output row w of the tile (32 pixels x COP channels); fragments,
+// layouts and the six-product arithmetic are those of conv3x3_x6_kernel.
+namespace cxp {
+constexpr int TC = 32, HC = TC + 2;      // tile columns, halo columns
+constexpr int CK = 16;                   // input channels per K chunk
+constexpr int XROW = HC * 32;            // halo row bytes per plane (16 bf16 per pixel)
+constexpr int WROW = 9 * 32 + 16;        // weight row bytes per chunk and plane
+}  // namespace cxp
+
+template <int CI, int COP, bool DGRAD, int NT, int TR>
+__global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W) {
+  using namespace cxp;
+  static_assert(CI % CK == 0 && (COP == 32 || COP == 64), "shape");
+  constexpr int NI = COP / 32, NCH = CI / CK;
+  // tile TR x 32 pixels; wave w = output row w % TR and 32-channel tiles
+  // [(w / TR) * NIW, +NIW): 8 waves of 8 rows x COP channels, or 16 waves
+  // (twice the waves to hide the staging) as 8 rows x 2 channel halves
+  // (COP = 64) or 16 rows (COP = 32)
+  constexpr int HR = TR + 2, XPLANE = HR * XROW, XU = 2 * HR * HC;
+  constexpr int NW = NT / 64, NIW = NI * TR / NW;
+  constexpr int XI = (XU + NT - 1) / NT;
+  static_assert(NIW >= 1 && NIW * NW == NI * TR, "waves");
+  constexpr int WPLANE = COP * WROW, WCH = 3 * WPLANE;
+  constexpr int WU = NCH * COP * 18;       // weight units (chunk, co, tap, half)
+  __shared__ __attribute__((aligned(16))) unsigned char sw[NCH * WCH];
+  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPLANE];
+  __shared__ float s_ss[2 * CI];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int wrow = wave % TR, wco = (wave / TR) * NIW;  // output row, first 32-channel tile
+  const int64_t HW = (int64_t)H * W;
+
+  for (int u = tid; u < WU; u += NT) {
+    const int half = u & 1, tap = (u >> 1) % 9, co = (u / 18) % COP, ch = u / (18 * COP);
+    float pw[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int ci = ch * CK + 8 * half + c;
+      pw[c] = co < Cout ? (DGRAD ? w[((int64_t)ci * Cout + co) * 9 + (8 - tap)]
+                                 : w[((int64_t)co * CI + ci) * 9 + tap])
+                        : 0.f;
+    }
+    uint4 p0, p1, p2;
+    cx6_split8(pw, p0, p1, p2);
+    unsigned char* d = sw + ch * WCH + co * WROW + tap * 32 + 16 * half;
+    *reinterpret_cast<uint4*>(d) = p0;
+    *reinterpret_cast<uint4*>(d + WPLANE) = p1;
+    *reinterpret_cast<uint4*>(d + 2 * WPLANE) = p2;
+  }
+  if (tid < 2 * CI)
+    s_ss[tid] = in_scale ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
+
+  const int tiles_c = (W + TC - 1) / TC, tiles_r = (H + TR - 1) / TR;
+  const int64_t ntiles = (int64_t)N * tiles_r * tiles_c;
+  auto tile_coords = [&](int64_t tile, int& n, int& r0, int& c0) {
+    c0 = (int)(tile % tiles_c) * TC;
+    r0 = (int)((tile / tiles_c) % tiles_r) * TR;
+    n = (int)(tile / ((int64_t)tiles_c * tiles_r));
+  };
+
+  float px[XI][8];
+  auto fetch = [&](int64_t tile, int ch) {
+    int n, r0, c0;
+    tile_coords(tile, n, r0, c0);
+    int plane = (int)(HW * 4);
+    asm volatile("" : "+s"(plane));  // keep c * plane out of the loop
+    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * CI + ch * CK) * HW);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
+      const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+      const int vo = 8 * half * plane + (gr * W + gc) * 4;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+    }
+  };
+  auto commit = [&](int64_t tile, int ch) {
+    int n, r0, c0;
+    tile_coords(tile, n, r0, c0);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      if (u < XU) {
+        const int col = u % HC, row = (u / HC) % HR, half = u / (HR * HC);
+        const int gr = r0 - 1 + row, gc = c0 - 1 + col;
+        const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float t = px[i][c];
+          if (in_scale) {
+            const int ci = ch * CK + 8 * half + c;
+            t = fmaxf(fmaf(t, s_ss[ci], s_ss[CI + ci]), 0.f);
+          }
+          v[c] = inb ? t : 0.f;
+        }
+        uint4 p0, p1, p2;
+        cx6_split8(v, p0, p1, p2);
+        unsigned char* d = sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1));
+        *reinterpret_cast<uint4*>(d) = p0;
+        *reinterpret_cast<uint4*>(d + XPLANE) = p1;
+        *reinterpret_cast<uint4*>(d + 2 * XPLANE) = p2;
+      }
+    }
+  };
+
+  f32x16 acc[NIW];
+#pragma unroll
+  for (int i = 0; i < NIW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+  double bs[NIW], bq[NIW];   // BatchNorm sums of channel row li>>1 (see epilogue)
+#pragma unroll
+  for (int i = 0; i < NIW; ++i) bs[i] = bq[i] = 0.0;
+
+  // 16 values per lane -> lane li holds the sum over the 32 lanes of its half
+  // of value li >> 1 (fixed butterfly order)
+  auto reduce16 = [&](const float (&v)[16]) {
+    float t8[8], t4[4], t2[2];
+    const bool b4 = li & 16, b3 = li & 8, b2 = li & 4, b1 = li & 2;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      t8[k] = (b4 ? v[k + 8] : v[k]) + __shfl_xor(b4 ? v[k] : v[k + 8], 16, 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      t4[k] = (b3 ? t8[k + 4] : t8[k]) + __shfl_xor(b3 ? t8[k] : t8[k + 4], 8, 64);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      t2[k] = (b2 ? t4[k + 2] : t4[k]) + __shfl_xor(b2 ? t4[k] : t4[k + 2], 4, 64);
+    const float t1 = (b1 ? t2[1] : t2[0]) + __shfl_xor(b1 ? t2[0] : t2[1], 2, 64);
+    return t1 + __shfl_xor(t1, 1, 64);
+  };
+
+  auto epilogue = [&](int64_t tile) {
+    int n, r0, c0;
+    tile_coords(tile, n, r0, c0);
+    const int row = r0 + wrow, col = c0 + li;
+    const bool pok = row < H && col < W;
+    float* yn = y + (int64_t)n * Cout * HW + (int64_t)row * W + col;
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) {
+      float s[16], q[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = 32 * (wco + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const bool ok = pok && co < Cout;
+        const float v = acc[i][r] + ((bias && co < Cout) ? bias[co] : 0.f);
+        if (ok) yn[(int64_t)co * HW] = v;
+        s[r] = ok ? v : 0.f;
+        q[r] = s[r] * s[r];
+      }
+      if (stats) {
+        bs[i] += (double)reduce16(s);
+        bq[i] += (double)reduce16(q);
+      }
+    }
+  };
+
+  __syncthreads();  // weights, s_ss
+  int64_t tile = blockIdx.x;
+  int ch = 0;
+  if (tile < ntiles) fetch(tile, 0);
+  while (tile < ntiles) {
+    commit(tile, ch);
+    __syncthreads();
+    int nch = ch + 1;
+    int64_t ntile = tile;
+    if (nch == NCH) {
+      nch = 0;
+      ntile += gridDim.x;
+    }
+    if (ntile < ntiles) fetch(ntile, nch);
+    const unsigned char* wb0 = sw + ch * WCH + li * WROW + 16 * lh;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int dy = tap / 3, dx = tap % 3;
+      const int hcol = li + dx;
+      const unsigned char* xb =
+          sx + (wrow + dy) * XROW + hcol * 32 + 16 * (lh ^ ((hcol >> 3) & 1));
+      bf16x8c a[3][NIW], b[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < NIW; ++i)
+          a[p][i] = cx6_ld(wb0 + p * WPLANE + (wco + i) * 32 * WROW + tap * 32);
+        b[p] = cx6_ld(xb + p * XPLANE);
+      }
+      // six cross terms smallest first, term-major over the NI accumulators
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
+        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < NIW; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa][i], b[pb], acc[i], 0, 0, 0);
+      }
+    }
+    if (nch == 0) {  // the tile's last chunk: store, BatchNorm sums, restart
+      epilogue(tile);
+#pragma unroll
+      for (int i = 0; i < NIW; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    }
+    __syncthreads();
+    tile = ntile;
+    ch = nch;
+  }
+
+  if (!stats) return;
+  // per-row sums -> [row][sum, sum of squares][COP] (the halo image is free)
+  double* red = reinterpret_cast<double*>(sx);
+  if ((li & 1) == 0) {
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) {
+      const int r = li >> 1;
+      const int co = 32 * (wco + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      red[(wrow * 2 + 0) * COP + co] = bs[i];
+      red[(wrow * 2 + 1) * COP + co] = bq[i];
+    }
+  }
+  __syncthreads();
+  for (int co = tid; co < Cout; co += NT) {
+    double s = 0.0, q = 0.0;
+    for (int wv = 0; wv < TR; ++wv) {
+      s += red[(wv * 2 + 0) * COP + co];
+      q += red[(wv * 2 + 1) * COP + co];
+    }
+    stats[(int64_t)blockIdx.x * 2 * Cout + co] = s;
+    stats[(int64_t)blockIdx.x * 2 * Cout + Cout + co] = q;
+  }
+}
+
+// Persistent launcher (conv_x6_launch routes here); returns 1 if (CI, COP)
+// has no instantiation.
+int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
+                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
+                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts) {
+  const int cop = Cout <= 32 ? 32 : 64;
+  // two workgroups per CU where the LDS allows it (one 16-channel chunk)
+#define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                    \
+  if (dgrad == DG && Cin == CIV && cop == COV) {                                               \
+    hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV>), dim3(G), dim3(NTV), 0, s, \
+                       x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);            \
+    *parts = G;                                                                                \
+    return check_launch("conv3x3_x6p");                                                        \
+  }
+  AINP_X6P(32, 64, false, 256, 1024, 8)
+  AINP_X6P(16, 32, false, 512, 512, 8) AINP_X6P(16, 32, true, 512, 512, 8)
+
+
+#undef AINP_X6P
+  return 1;
 }
 
 // Launch the split-bf16 weight gradient of one 32-channel pass if Cout has an
