@@ -306,9 +306,16 @@ int ainp_sum_slabs(const float* x, int64_t nslabs, int64_t n, float* out,
  * whose output is [nb, rows, cols]). */
 int ainp_rowsum_batched(const float* x, int64_t nb, int64_t rows, int64_t cols,
                         float* out, void* stream);
-/* Column sums: out[j] (+)= sum_i x[i*ld + j], i<rows, j<cols. */
+/* Column sums: out[j] (+)= sum_i x[i*ld + j], i<rows, j<cols.  Row slabs are
+ * combined with float atomics, so the summation order can vary run to run;
+ * ainp_colsum_slabs + ainp_sum_slabs is the fixed-order form. */
 int ainp_colsum(const float* x, int64_t rows, int64_t cols, int64_t ld,
                 float* out, int accumulate, void* stream);
+/* partial[s*cols + j] = sum of x[i*ld + j] over rows i of slab s (nslabs
+ * slabs of ceil(rows/nslabs) rows, fixed order).  Bias gradients of
+ * nn.LSTM (models/CNNBLSTM/model.py:46-47) then = ainp_sum_slabs(partial). */
+int ainp_colsum_slabs(const float* x, int64_t rows, int64_t cols, int64_t ld,
+                      int64_t nslabs, float* partial, void* stream);
 /* Multi-tensor Adam with torch.optim.Adam arithmetic (amsgrad=False,
  * maximize=False): m = lerp(m, g, 1-b1); v = b2*v + (1-b2)*g*g;
  * p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps); bc_i = 1 - b_i^step.

@@ -74,6 +74,7 @@ _SIGS = {
     "ainp_sum_slabs": (c_int, [P, c_int64, c_int64, P, P]),
     "ainp_rowsum_batched": (c_int, [P, c_int64, c_int64, c_int64, P, P]),
     "ainp_colsum": (c_int, [P, c_int64, c_int64, c_int64, P, c_int, P]),
+    "ainp_colsum_slabs": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P]),
     "ainp_adam": (c_int, [PP, PP, PP, PP, POINTER(c_int64), c_int, c_double, c_double,
                           c_double, c_double, c_double, c_int64, P]),
     "ainp_conv_gen_stat_parts": (c_int, [c_int64, c_int, c_int, c_int, c_int, c_int64, c_int64]),

@@ -202,8 +202,8 @@ class _BLSTMFn(torch.autograd.Function):
                 # for the recurrent / upper layers -> parallel split-K over row chunks
                 gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H))
                 gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il, offsets_b=(0, 0))
-                db_ih = ops.colsum(dg2)
-                db_hh = ops.colsum(dg2)
+                db_ih = ops.colsum(dg2)           # b_ih and b_hh get the same gradient
+                db_hh = db_ih.clone()
             for t in (dg, hp, inp):
                 t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l

@@ -435,14 +435,20 @@ def rowsum_batched(x3d):
 
 
 def colsum(x2d, out=None, accumulate=False):
+    """Column sums of a row-major [rows, cols] view.  Default: fixed-order row
+    slabs (~1024 workgroups) combined by sum_slabs (deterministic);
+    accumulate=True adds into `out` with float atomics."""
     rows, cols = x2d.shape
     ld = x2d.stride(0)
     assert x2d.stride(1) == 1
-    if out is None:
-        out = torch.empty(cols, device=x2d.device, dtype=torch.float32)
-    call("ainp_colsum", x2d.data_ptr(), rows, cols, ld, out.data_ptr(),
-         1 if accumulate else 0, _stream(x2d))
-    return out
+    if accumulate:
+        call("ainp_colsum", x2d.data_ptr(), rows, cols, ld, out.data_ptr(), 1, _stream(x2d))
+        return out
+    nslabs = max(1, min(512, rows // 16, 1024 // -(-cols // 256)))
+    part = torch.empty(nslabs, cols, device=x2d.device, dtype=torch.float32)
+    call("ainp_colsum_slabs", x2d.data_ptr(), rows, cols, ld, nslabs, part.data_ptr(),
+         _stream(x2d))
+    return sum_slabs(part, nslabs, out)
 
 
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, eps,

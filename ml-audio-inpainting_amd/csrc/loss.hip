@@ -48,6 +48,28 @@ __global__ void colsum_kernel(const float* __restrict__ x, int64_t rows,
   atomicAdd(&out[j], s);
 }
 
+// partial[s*cols + j] = sum of x[r*ld + j] over the rows of slab s, in a fixed
+// order (four interleaved partial sums); the slabs are combined by
+// sum_slabs_kernel, so the column sums are deterministic.
+__global__ void colsum_slabs_kernel(const float* __restrict__ x, int64_t rows, int64_t cols,
+                                    int64_t ld, int64_t rows_per, float* __restrict__ partial) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * rows_per;
+  const int64_t r1 = r0 + rows_per < rows ? r0 + rows_per : rows;
+  const float* p = x + j;
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+  int64_t r = r0;
+  for (; r + 3 < r1; r += 4) {
+    a0 += p[r * ld];
+    a1 += p[(r + 1) * ld];
+    a2 += p[(r + 2) * ld];
+    a3 += p[(r + 3) * ld];
+  }
+  for (; r < r1; ++r) a0 += p[r * ld];
+  partial[(int64_t)blockIdx.y * cols + j] = (a0 + a1) + (a2 + a3);
+}
+
 __global__ void zero_kernel(float* p, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) p[i] = 0.f;
@@ -167,4 +189,15 @@ extern "C" int ainp_colsum(const float* x, int64_t rows, int64_t cols,
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, x, rows, cols, ld,
                      out, rows_per);
   return check_launch("colsum");
+}
+
+extern "C" int ainp_colsum_slabs(const float* x, int64_t rows, int64_t cols, int64_t ld,
+                                 int64_t nslabs, float* partial, void* stream) {
+  if (!x || !partial || rows < 0 || cols < 1 || ld < cols || nslabs < 1 || nslabs > 65535)
+    return record_msg("ainp_colsum_slabs: bad argument");
+  const int64_t rows_per = cdiv(rows, nslabs);
+  dim3 grid((unsigned)cdiv(cols, 256), (unsigned)nslabs);
+  hipLaunchKernelGGL(colsum_slabs_kernel, grid, dim3(256), 0, as_stream(stream), x, rows, cols,
+                     ld, rows_per, partial);
+  return check_launch("colsum_slabs");
 }

@@ -348,6 +348,20 @@ def test_l1_pow10_loss(ops):
     assert rel(dy.cpu(), y.grad) < 1e-6
 
 
+@pytest.mark.parametrize("rows,cols,ld", [(10688, 1024, 1024), (10688, 512, 1024), (37, 130, 131),
+                                           (5, 3, 3)])
+def test_colsum_fixed_order(ops, rows, cols, ld):
+    """LSTM bias gradients (sum of the gate gradients over N*T rows): row
+    slabs in fixed order + sum_slabs, bit-identical across runs."""
+    g = torch.Generator().manual_seed(rows + cols)
+    x = torch.randn(rows, ld, generator=g, dtype=torch.float64)
+    xd = x.float().to(DEV)[:, :cols]
+    a = ops.colsum(xd).cpu()
+    b = ops.colsum(xd).cpu()
+    assert torch.equal(a, b)
+    assert rel(a, x[:, :cols].sum(0)) < 1e-6
+
+
 def test_adam_matches_torch(ops):
     g = torch.Generator().manual_seed(2)
     shapes = [(7, 5), (1000,), (3, 3, 3, 3), (4097,)]
