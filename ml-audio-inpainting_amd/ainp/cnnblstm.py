@@ -259,10 +259,17 @@ class _ProjFn(torch.autograd.Function):
         NO = C * F
         K = h.shape[2]
         g = g.contiguous()
-        dh = torch.empty(N, T, K, device=h.device, dtype=torch.float32)
-        # dh_n[t][k] = sum_col g_n[col][t] w[col][k]
-        ops.gemm(T, K, NO, [g], 1, T, [w], K, 1, [dh], K, 1, strideA=NO * T, strideC=T * K,
-                 nstrided=N)
+        # dh_n[t][k] = sum_col g_n[col][t] w[col][k]: only 6 output tiles per
+        # example, so the col sum (K = C*F) is split over S pointer batches into
+        # slabs (4x the workgroups) and combined in fixed order
+        S = 4 if NO % 4 == 0 else 1
+        kc = NO // S
+        hs = torch.empty(S, N, T, K, device=h.device, dtype=torch.float32)
+        gflat = g.view(-1)
+        ops.gemm(T, K, kc, [gflat[s * kc * T:] for s in range(S)], 1, T,
+                 [w[s * kc:] for s in range(S)], K, 1, [hs[s] for s in range(S)], K, 1,
+                 strideA=NO * T, strideC=T * K, nstrided=N)
+        dh = hs[0] if S == 1 else ops.sum_slabs(hs, S).view(N, T, K)
         # dw[col][k] = sum_{n,t} g_n[col][t] h_n[t][k]: split the example sum
         # over S pointer batches (S partial slabs, ksplit mode 2) so the small
         # [C*F, 2H] output still fills the chip, then combine in fixed order.

@@ -436,7 +436,7 @@ def rowsum_batched(x3d):
 
 def colsum(x2d, out=None, accumulate=False):
     """Column sums of a row-major [rows, cols] view.  Default: fixed-order row
-    slabs (~1024 workgroups) combined by sum_slabs (deterministic);
+    slabs combined by sum_slabs (deterministic);
     accumulate=True adds into `out` with float atomics."""
     rows, cols = x2d.shape
     ld = x2d.stride(0)
@@ -444,7 +444,8 @@ def colsum(x2d, out=None, accumulate=False):
     if accumulate:
         call("ainp_colsum", x2d.data_ptr(), rows, cols, ld, out.data_ptr(), 1, _stream(x2d))
         return out
-    nslabs = max(1, min(512, rows // 16, 1024 // -(-cols // 256)))
+    # ~256 workgroups of column sums; the slab combine then reads nslabs*cols
+    nslabs = max(1, min(64, rows // 16, 256 // -(-cols // 256)))
     part = torch.empty(nslabs, cols, device=x2d.device, dtype=torch.float32)
     call("ainp_colsum_slabs", x2d.data_ptr(), rows, cols, ld, nslabs, part.data_ptr(),
          _stream(x2d))
