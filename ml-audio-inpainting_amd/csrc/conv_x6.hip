@@ -1007,6 +1007,231 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
   }
 }
 
+// 16-output-channel variant (decoder 32->16 and the 16->32 convs' data
+// gradients): the persistent kernel above on v_mfma_f32_16x16x32_bf16, so no
+// half of a 32-wide tile is wasted.  A k-step is two taps x 16 channels of one
+// chunk (lane group g = lane >> 4 takes tap 2s + (g >> 1), channels
+// 8 (g & 1) .. +7); the tenth tap slot of a weight row is zero.  Wave = one
+// output row as two 16-pixel tiles sharing the A fragments.  Weight rows are
+// 336 bytes (10 tap slots + pad: conflict-free 16-lane b128 reads).
+namespace cxq {
+constexpr int TR = 8, HR = TR + 2;
+constexpr int WROW = 10 * 32 + 16;
+constexpr int XPLANE = HR * cxp::XROW;
+constexpr int XU = 2 * HR * cxp::HC;
+}  // namespace cxq
+
+template <int CI, bool DGRAD>
+__global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W) {
+  using cxp::CK;
+  using cxp::HC;
+  using cxp::TC;
+  using cxp::XROW;
+  using namespace cxq;
+  constexpr int NT = 512, CO = 16, NCH = CI / CK;
+  constexpr int WPLANE = CO * WROW, WCH = 3 * WPLANE;
+  constexpr int WU = NCH * CO * 20;          // weight units (chunk, co, tap slot, half)
+  constexpr int XI = (XU + NT - 1) / NT;
+  __shared__ __attribute__((aligned(16))) unsigned char sw[NCH * WCH];
+  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPLANE];
+  __shared__ float s_ss[2 * CI];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int l16 = lane & 15, g = lane >> 4;
+  const int64_t HW = (int64_t)H * W;
+
+  for (int u = tid; u < WU; u += NT) {
+    const int half = u & 1, tap = (u >> 1) % 10, co = (u / 20) % CO, ch = u / (20 * CO);
+    float pw[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int ci = ch * CK + 8 * half + c;
+      pw[c] = (co < Cout && tap < 9) ? (DGRAD ? w[((int64_t)ci * Cout + co) * 9 + (8 - tap)]
+                                              : w[((int64_t)co * CI + ci) * 9 + tap])
+                                     : 0.f;
+    }
+    uint4 p0, p1, p2;
+    cx6_split8(pw, p0, p1, p2);
+    unsigned char* d = sw + ch * WCH + co * WROW + tap * 32 + 16 * half;
+    *reinterpret_cast<uint4*>(d) = p0;
+    *reinterpret_cast<uint4*>(d + WPLANE) = p1;
+    *reinterpret_cast<uint4*>(d + 2 * WPLANE) = p2;
+  }
+  if (tid < 2 * CI)
+    s_ss[tid] = in_scale ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
+
+  const int tiles_c = (W + TC - 1) / TC, tiles_r = (H + TR - 1) / TR;
+  const int64_t ntiles = (int64_t)N * tiles_r * tiles_c;
+  auto tile_coords = [&](int64_t tile, int& n, int& r0, int& c0) {
+    c0 = (int)(tile % tiles_c) * TC;
+    r0 = (int)((tile / tiles_c) % tiles_r) * TR;
+    n = (int)(tile / ((int64_t)tiles_c * tiles_r));
+  };
+
+  float px[XI][8];
+  auto fetch = [&](int64_t tile, int ch) {
+    int n, r0, c0;
+    tile_coords(tile, n, r0, c0);
+    int plane = (int)(HW * 4);
+    asm volatile("" : "+s"(plane));
+    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * CI + ch * CK) * HW);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
+      const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+      const int vo = 8 * half * plane + (gr * W + gc) * 4;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+    }
+  };
+  auto commit = [&](int64_t tile, int ch) {
+    int n, r0, c0;
+    tile_coords(tile, n, r0, c0);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = tid + NT * i;
+      if (u < XU) {
+        const int col = u % HC, row = (u / HC) % HR, half = u / (HR * HC);
+        const int gr = r0 - 1 + row, gc = c0 - 1 + col;
+        const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float t = px[i][c];
+          if (in_scale) {
+            const int ci = ch * CK + 8 * half + c;
+            t = fmaxf(fmaf(t, s_ss[ci], s_ss[CI + ci]), 0.f);
+          }
+          v[c] = inb ? t : 0.f;
+        }
+        uint4 p0, p1, p2;
+        cx6_split8(v, p0, p1, p2);
+        unsigned char* d = sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1));
+        *reinterpret_cast<uint4*>(d) = p0;
+        *reinterpret_cast<uint4*>(d + XPLANE) = p1;
+        *reinterpret_cast<uint4*>(d + 2 * XPLANE) = p2;
+      }
+    }
+  };
+
+  f32x4 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  double bs = 0.0, bq = 0.0;   // BatchNorm sums of channel 4g + ((lane >> 2) & 3)
+
+  // 4 values per lane -> lane holds the sum over its 16-lane group of value
+  // (lane >> 2) & 3 (fixed butterfly order)
+  auto reduce4 = [&](const float (&v)[4]) {
+    const bool b3 = lane & 8, b2 = lane & 4;
+    float t2[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      t2[k] = (b3 ? v[k + 2] : v[k]) + __shfl_xor(b3 ? v[k] : v[k + 2], 8, 64);
+    float t1 = (b2 ? t2[1] : t2[0]) + __shfl_xor(b2 ? t2[0] : t2[1], 4, 64);
+    t1 += __shfl_xor(t1, 2, 64);
+    return t1 + __shfl_xor(t1, 1, 64);
+  };
+
+  auto epilogue = [&](int64_t tile) {
+    int n, r0, c0;
+    tile_coords(tile, n, r0, c0);
+    const int row = r0 + wave;
+    float* yn = y + (int64_t)n * Cout * HW + (int64_t)row * W;
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int col = c0 + 16 * j + l16;
+      const bool pok = row < H && col < W;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = 4 * g + r;
+        const bool ok = pok && co < Cout;
+        const float v = acc[j][r] + ((bias && co < Cout) ? bias[co] : 0.f);
+        if (ok) yn[(int64_t)co * HW + col] = v;
+        const float sv = ok ? v : 0.f;
+        s[r] += sv;
+        q[r] += sv * sv;
+      }
+    }
+    if (stats) {
+      bs += (double)reduce4(s);
+      bq += (double)reduce4(q);
+    }
+  };
+
+  __syncthreads();  // weights, s_ss
+  int64_t tile = blockIdx.x;
+  int ch = 0;
+  if (tile < ntiles) fetch(tile, 0);
+  while (tile < ntiles) {
+    commit(tile, ch);
+    __syncthreads();
+    int nch = ch + 1;
+    int64_t ntile = tile;
+    if (nch == NCH) {
+      nch = 0;
+      ntile += gridDim.x;
+    }
+    if (ntile < ntiles) fetch(ntile, nch);
+    const unsigned char* wb0 = sw + ch * WCH + l16 * WROW + 16 * (g & 1);
+#pragma unroll
+    for (int ks = 0; ks < 5; ++ks) {
+      const int tap = 2 * ks + (g >> 1);            // 9 = the zero slot
+      const int tp = tap < 9 ? tap : 8;             // its (unused) pixel shift
+      const int dy = tp / 3, dx = tp % 3;
+      bf16x8c a[3], b[3][2];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        a[p] = cx6_ld(wb0 + p * WPLANE + tap * 32);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int hcol = 16 * j + l16 + dx;
+          b[p][j] = cx6_ld(sx + p * XPLANE + (wave + dy) * XROW + hcol * 32 +
+                           16 * ((g & 1) ^ ((hcol >> 3) & 1)));
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
+        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[pa], b[pb][j], acc[j], 0, 0, 0);
+      }
+    }
+    if (nch == 0) {
+      epilogue(tile);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    __syncthreads();
+    tile = ntile;
+    ch = nch;
+  }
+
+  if (!stats) return;
+  double* red = reinterpret_cast<double*>(sx);   // [row][sum, sum of squares][16]
+  if ((lane & 3) == 0) {
+    const int co = 4 * g + ((lane >> 2) & 3);
+    red[(wave * 2 + 0) * CO + co] = bs;
+    red[(wave * 2 + 1) * CO + co] = bq;
+  }
+  __syncthreads();
+  for (int co = tid; co < Cout; co += NT) {
+    double sm = 0.0, sq = 0.0;
+    for (int wv = 0; wv < TR; ++wv) {
+      sm += red[(wv * 2 + 0) * CO + co];
+      sq += red[(wv * 2 + 1) * CO + co];
+    }
+    stats[(int64_t)blockIdx.x * 2 * Cout + co] = sm;
+    stats[(int64_t)blockIdx.x * 2 * Cout + Cout + co] = sq;
+  }
+}
+
 // Persistent launcher (conv_x6_launch routes here); returns 1 if (CI, COP)
 // has no instantiation.
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
@@ -1023,6 +1248,16 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
   }
   AINP_X6P(32, 64, false, 256, 1024, 8)
   AINP_X6P(16, 32, false, 512, 512, 8) AINP_X6P(16, 32, true, 512, 512, 8)
+  if (Cin == 32 && Cout == 16) {   // two workgroups per CU (65 KB of LDS)
+    if (dgrad)
+      hipLaunchKernelGGL((conv3x3_x6q_kernel<32, true>), dim3(512), dim3(512), 0, s, x, w, bias,
+                         sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);
+    else
+      hipLaunchKernelGGL((conv3x3_x6q_kernel<32, false>), dim3(512), dim3(512), 0, s, x, w, bias,
+                         sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);
+    *parts = 512;
+    return check_launch("conv3x3_x6q");
+  }
 
 
 #undef AINP_X6P
