@@ -5,6 +5,8 @@
 // output is written straight into the LSTM's [N, T, C*F] layout).
 // Statistics are reduced in float64 from per-workgroup partials in a fixed
 // order, so results are deterministic run to run.
+#include <initializer_list>
+
 #include "common.h"
 
 namespace ainp {
@@ -381,6 +383,115 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
   }
 }
 
+// NTCF v2 for C*H % 64 == 0 and even W (the model: C*H = 64*257): the NCHW
+// tensor is [n][k = c*H + h][w] and the NTCF one [n][w][k], so the layout
+// bridge is a batched 2-D transpose tiled 64 (k) x 64 (w) -- no 1-row h
+// tiles, 8-byte vectors on both sides (a wave moves two 256-byte rows per
+// instruction); the channel of row k is k / H.
+__device__ __forceinline__ void ntcf2_tile(int64_t b, int64_t K, int64_t W, int& n, int& k0,
+                                           int& w0) {
+  const int tw = (int)((W + NT_T - 1) / NT_T), tk = (int)(K / NT_T);
+  w0 = (int)(b % tw) * NT_T;
+  k0 = (int)((b / tw) % tk) * NT_T;
+  n = (int)(b / ((int64_t)tw * tk));
+}
+
+__global__ __launch_bounds__(256) void bn_relu_apply_ntcf2(const float* __restrict__ x,
+                                                           const float* __restrict__ scale,
+                                                           const float* __restrict__ shift,
+                                                           float* __restrict__ out, int C, int64_t H,
+                                                           int64_t W) {
+  __shared__ float tile[NT_T][NT_T + 1];   // [w][k]
+  const int64_t K = (int64_t)C * H;
+  int n, k0, w0;
+  ntcf2_tile(blockIdx.x, K, W, n, k0, w0);
+  const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
+  const float* xn = x + (int64_t)n * K * W;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {                 // rows k, lanes along w (float2)
+    const int kk = r + 8 * i;
+    const int64_t k = k0 + kk;
+    const int c = (int)(k / H);
+    const int w = w0 + 2 * l;
+    float2 v = make_float2(0.f, 0.f);
+    if (w < W) v = *reinterpret_cast<const float2*>(xn + k * W + w);
+    const float sc = scale[c], sh = shift[c];
+    tile[2 * l][kk] = fmaxf(fmaf(v.x, sc, sh), 0.f);
+    tile[2 * l + 1][kk] = fmaxf(fmaf(v.y, sc, sh), 0.f);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {                 // rows w, lanes along k (float2)
+    const int ww = r + 8 * i;
+    const int64_t w = w0 + ww;
+    if (w < W)
+      *reinterpret_cast<float2*>(out + ((int64_t)n * W + w) * K + k0 + 2 * l) =
+          make_float2(tile[ww][2 * l], tile[ww][2 * l + 1]);
+  }
+}
+
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
+    const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ gamma,
+    const float* __restrict__ save, const double* __restrict__ sums, float* __restrict__ gy,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int C, int64_t H, int64_t W,
+    double inv_count, int64_t ntiles) {
+  __shared__ float tile[NT_T][NT_T + 1];   // g as [w][k]
+  if (blockIdx.x < (unsigned)C && threadIdx.x == 0) {
+    if (dbeta) dbeta[blockIdx.x] = (float)sums[blockIdx.x];
+    if (dgamma) dgamma[blockIdx.x] = (float)sums[C + blockIdx.x];
+  }
+  if (blockIdx.x >= ntiles) return;         // a dgamma / dbeta writer only
+  const int64_t K = (int64_t)C * H;
+  int n, k0, w0;
+  ntcf2_tile(blockIdx.x, K, W, n, k0, w0);
+  const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
+  float2 yv[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {                 // g: rows w, lanes along k
+    const int ww = r + 8 * i;
+    const int64_t w = w0 + ww;
+    float2 v = make_float2(0.f, 0.f);
+    if (w < W) v = *reinterpret_cast<const float2*>(g + ((int64_t)n * W + w) * K + k0 + 2 * l);
+    tile[ww][2 * l] = v.x;
+    tile[ww][2 * l + 1] = v.y;
+  }
+  const float* yn = y + (int64_t)n * K * W;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {                 // y: rows k, lanes along w
+    const int64_t k = k0 + r + 8 * i;
+    const int w = w0 + 2 * l;
+    yv[i] = w < W ? *reinterpret_cast<const float2*>(yn + k * W + w) : make_float2(0.f, 0.f);
+  }
+  __syncthreads();
+  float* gn = gy + (int64_t)n * K * W;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int kk = r + 8 * i;
+    const int64_t k = k0 + kk;
+    const int w = w0 + 2 * l;
+    if (w >= W) continue;
+    const int c = (int)(k / H);
+    const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
+    const float kc = (gamma ? gamma[c] : 1.f) * rstd;
+    const float m1 = (float)(sums[c] * inv_count);
+    const float m2 = (float)(sums[C + c] * inv_count);
+    const float gz0 = fmaf(yv[i].x, sc, sh) > 0.f ? tile[2 * l][kk] : 0.f;
+    const float gz1 = fmaf(yv[i].y, sc, sh) > 0.f ? tile[2 * l + 1][kk] : 0.f;
+    float2 o;
+    o.x = kc * (gz0 - m1 - ((yv[i].x - mean) * rstd) * m2);
+    o.y = kc * (gz1 - m1 - ((yv[i].y - mean) * rstd) * m2);
+    *reinterpret_cast<float2*>(gn + k * W + w) = o;
+  }
+}
+
+static bool ntcf2_ok(int C, int64_t H, int64_t W, std::initializer_list<const void*> ptrs) {
+  if (((int64_t)C * H) % NT_T != 0 || W % 2 != 0) return false;
+  for (const void* p : ptrs)
+    if (reinterpret_cast<uintptr_t>(p) % 8 != 0) return false;
+  return true;
+}
+
 static int64_t tiles_per_plane(int64_t H, int64_t W) {
   return cdiv(H, TH) * cdiv(W, TW);
 }
@@ -436,7 +547,11 @@ extern "C" int ainp_bn_relu_apply(const float* x, const float* scale,
   if (N == 0) return AINP_OK;
   const int64_t blocks = N * C * tiles_per_plane(H, W);
   hipStream_t s = as_stream(stream);
-  if (out_ntcf)
+  if (out_ntcf && ntcf2_ok(C, H, W, {x, out}))
+    hipLaunchKernelGGL(bn_relu_apply_ntcf2,
+                       dim3((unsigned)(N * (C * H / NT_T) * cdiv(W, NT_T))), dim3(256), 0, s, x,
+                       scale, shift, out, C, H, W);
+  else if (out_ntcf)
     hipLaunchKernelGGL(bn_relu_apply_ntcf, dim3((unsigned)(N * C * cdiv(H, NT_T) * cdiv(W, NT_T))),
                        dim3(256), 0, s, x, scale, shift, out, C, H, W);
   else
@@ -520,6 +635,14 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
     return check_launch("bn_relu_bwd_apply_flat");
   }
   (void)blocks;
+  if (ntcf2_ok(C, H, W, {g, y, gy})) {
+    const int64_t nt2 = N * (C * H / NT_T) * cdiv(W, NT_T);
+    const int64_t nb2 = nt2 < C ? C : nt2;   // >= C blocks: the dgamma / dbeta writers
+    hipLaunchKernelGGL(bn_relu_bwd_apply_ntcf2, dim3((unsigned)nb2), dim3(256), 0, s, g, y, scale,
+                       shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W, inv_count,
+                       nt2);
+    return check_launch("bn_relu_bwd_apply_ntcf2");
+  }
   int64_t nb = N * C * cdiv(H, NT_T) * cdiv(W, NT_T);
   if (nb < C) nb = C;
   hipLaunchKernelGGL(bn_relu_bwd_ntcf<true>, dim3((unsigned)nb), dim3(256), 0, s, g, y, scale,

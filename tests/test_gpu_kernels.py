@@ -260,7 +260,9 @@ def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
 
 # ------------------------------------------------------------------ BN
 @pytest.mark.parametrize("ntcf,H,W", [(False, 37, 70), (True, 37, 70), (False, 37, 71),
-                                       (False, 65, 130)])
+                                       (False, 65, 130),
+                                       # C*H % 64 == 0, even W: the flattened-k NTCF kernels
+                                       (True, 48, 70), (True, 16, 134), (True, 8, 6)])
 def test_bn_relu_fwd_bwd(ops, ntcf, H, W):
     g = torch.Generator().manual_seed(9)
     N, C = 3, 8
