@@ -212,9 +212,21 @@ class _BLSTMFn(torch.autograd.Function):
             grads[base + 4], grads[base + 5] = gwi[1], gwh[1]
             grads[base + 6], grads[base + 7] = db_ih[4 * H:], db_hh[4 * H:]
             if l > 0 or ctx.needs_input_grad[0]:
-                dxi = torch.empty(NT, Il, device=dh.device)
-                ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,
-                         [dxi, dxi], Il, 1, ksplit=True)
+                # dX = dg_f W_ih + dg_r W_ih_rev.  Layer 0 (Il = 16448: 10836
+                # tiles) sums both directions inside each tile; the upper layers
+                # (Il = 256: 168 tiles) write 4 K-slabs (two per direction,
+                # 672 tiles) summed in fixed order.
+                if Il >= 1024:
+                    dxi = torch.empty(NT, Il, device=dh.device)
+                    ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,
+                             [dxi, dxi], Il, 1, ksplit=True)
+                else:
+                    hk = 2 * H                      # half of a direction's 4H gate columns
+                    sl = torch.empty(4, NT, Il, device=dh.device)
+                    ops.gemm(NT, Il, hk, [dg2[:, q * hk:] for q in range(4)], 8 * H, 1,
+                             [(wf if q < 2 else wr)[(q % 2) * hk:] for q in range(4)], Il, 1,
+                             [sl[q] for q in range(4)], Il, 1)
+                    dxi = ops.sum_slabs(sl, 4).view(NT, Il)
                 dh = dxi.view(N, T, Il)
                 dx = dh
         done = torch.cuda.Event()
