@@ -77,6 +77,24 @@ def check_against_golden(g, out, tol=1e-4):
             continue
         errs["final/" + k] = rel(v, ref)
     bad = {k: e for k, e in errs.items() if not e <= tol}
+    # BN-fed conv biases: Adam moves them by ~lr * sign(rounding noise) per
+    # step (the noise's sign is implementation-specific), so allow 2*lr*steps
+    # absolutely; a following BatchNorm's running_mean holds the step-1 update
+    # of that bias (a conv bias shifts its BN input mean 1:1): momentum*2*lr
+    lr, steps, momentum = 1e-4, 2, 0.1
+    for k in BN_FED_BIASES:
+        d = float(np.abs(out["final"][k] - g["final/" + k]).max())
+        errs["final/" + k] = d
+        if d <= 2 * lr * steps + 1e-7:
+            bad.pop("final/" + k, None)
+        else:
+            bad["final/" + k] = d
+    for k in list(bad):
+        if k.endswith("running_mean"):
+            ref = np.asarray(g[k], np.float64)
+            d = float(np.abs(out["final"][k[len("final/"):]] - ref).max())
+            if d <= momentum * 2 * lr + tol * float(np.abs(ref).max()):
+                bad.pop(k)
     return errs, bad
 
 
