@@ -185,10 +185,13 @@ int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
  * input channel when in_scale != NULL, identity otherwise; zero padding is
  * applied to act(x) as nn.Conv2d pads its (post-ReLU) input.
  * w: [Cout, Cin, 3, 3]; bias: [Cout] or NULL; Cout <= 64.
- * stats (may be NULL): double[ainp_conv3x3_fwd_stat_parts(N,H,W) * 2*Cout];
- * row p receives this workgroup's [sum y (Cout) | sum y^2 (Cout)] for the
- * following BatchNorm (reduced by ainp_bn_finalize). */
+ * stats (may be NULL): double[ainp_conv3x3_fwd_stat_rows(N,Cin,Cout,H,W) *
+ * 2*Cout] (ainp_conv3x3_fwd_stat_parts(N,H,W) is an upper bound over all
+ * channel counts); row p receives a workgroup's [sum y (Cout) | sum y^2
+ * (Cout)] for the following BatchNorm (reduced by ainp_bn_stats_reduce);
+ * rows a kernel does not produce are zeroed. */
 int ainp_conv3x3_fwd_stat_parts(int64_t N, int64_t H, int64_t W);
+int64_t ainp_conv3x3_fwd_stat_rows(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
 int ainp_conv3x3_fwd(const float* x, const float* w, const float* bias,
                      const float* in_scale, const float* in_shift, float* y,
                      double* stats, int64_t N, int Cin, int Cout, int64_t H,

@@ -262,8 +262,8 @@ def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False):
     y = torch.empty(N, Cout, H, W, device=x.device, dtype=torch.float32)
     stats = None
     if want_stats:
-        stats = torch.empty(conv_stat_parts(N, H, W), 2 * Cout, device=x.device,
-                            dtype=torch.float64)
+        stats = torch.empty(_lib.lib.ainp_conv3x3_fwd_stat_rows(N, Cin, Cout, H, W), 2 * Cout,
+                            device=x.device, dtype=torch.float64)
     call("ainp_conv3x3_fwd", x.data_ptr(), w.data_ptr(), _p(b), _p(in_scale),
          _p(in_shift), y.data_ptr(), _p(stats), N, Cin, Cout, H, W, _stream(x))
     return y, stats

@@ -909,6 +909,7 @@ using namespace ainp;
 
 namespace ainp {
 int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W);
+int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
                          int ci0, int cp, int grid, hipStream_t s);
@@ -938,15 +939,26 @@ extern "C" int ainp_conv3x3_fwd_stat_parts(int64_t N, int64_t H, int64_t W) {
   return (int)(a > b ? a : b);
 }
 
+// The BatchNorm partial rows ainp_conv3x3_fwd writes for this shape (the
+// kernel the dispatch below selects; fewer than the bound above when a
+// persistent kernel serves it).
+extern "C" int64_t ainp_conv3x3_fwd_stat_rows(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+  if (!small_pair(Cin, Cout) && !conv_exact_env()) {
+    const int64_t r = conv_x6_stat_rows(false, Cin, Cout, N, H, W);
+    if (r) return r;
+  }
+  return exact_stat_parts(N, H, W);
+}
+
 template <bool DG>
 static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y,
                              double* stats, int64_t N, int Cin, int Cout,
                              int64_t H, int64_t W, hipStream_t s) {
-  // partials [used, bound) of the BatchNorm statistics are zero
+  // partials [used, rows) of the BatchNorm statistics are zero
   auto zero_tail = [&](int64_t used) -> int {
     if (!stats) return AINP_OK;
-    const int64_t bound = ainp_conv3x3_fwd_stat_parts(N, H, W);
+    const int64_t bound = ainp_conv3x3_fwd_stat_rows(N, Cin, Cout, H, W);
     if (used >= bound) return AINP_OK;
     hipError_t e = hipMemsetAsync(stats + used * 2 * Cout, 0,
                                   (size_t)(bound - used) * 2 * Cout * sizeof(double), s);

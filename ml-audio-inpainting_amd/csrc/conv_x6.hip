@@ -268,10 +268,26 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
 // *parts = the number of BatchNorm partials written.  The persistent kernel
 // serves every pair it has (32-bit buffer offsets permitting); the tiled one
 // is kept for AINP_CONV_X6_TILED=1.
+// BatchNorm partial rows the x6 launch below writes for this shape (0: no x6
+// kernel serves it); mirrors conv_x6_launch / conv_x6p_launch.
+int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W) {
+  if (Cout > 64 || Cout < 16) return 0;
+  const int cop = Cout <= 32 ? 32 : 64;
+  static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
+  if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
+    if (!dgrad && Cin == 32 && cop == 64) return 256;
+    if (Cin == 16 && cop == 32) return 512;
+    if (Cin == 32 && Cout == 16) return 512;
+  }
+  if ((Cin == 32 && cop == 64) || (Cin == 64 && cop == 32))
+    return N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
+  return 0;
+}
+
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts) {
-  if (Cout > 64 || Cout < 16) return 1;
+  if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W) == 0) return 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
