@@ -301,6 +301,105 @@ __global__ __launch_bounds__(THREADS, WGS) void gemm3_kernel(int64_t M, int64_t 
     }
 }
 
+// ---- 16x16x32 variant: K-tile 32 ([row][32 k] planes, 80-byte rows), wave
+// tile 64x64 as 4x4 MFMA tiles of 16x16 (lane (r = l&15, g = l>>4) holds
+// k = 8g..8g+7 of row r: one ds_read_b128 per fragment)
+typedef float f32x4l __attribute__((ext_vector_type(4)));
+template <bool AKC, bool BKC, int WGS>
+__global__ __launch_bounds__(THREADS, WGS) void gemm16_kernel(int64_t M, int64_t N, int64_t K,
+                                                               Ptrs P, int64_t lda, int64_t ldb,
+                                                               int64_t ldc, int tiles_n) {
+  constexpr int BK = 32;
+  using I = Img3<BK>;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * I::BYTES];
+  unsigned char* As = smem;
+  unsigned char* Bs = smem + I::BYTES;
+  const int64_t nwg = gridDim.x;
+  const int64_t bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8;
+  const int64_t q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + 127) / 128;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t g8 = bid / per_group;
+  const int64_t first_n = g8 * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t tn = first_n + (in_g % gsize), tm = in_g / gsize;
+  const int64_t m0 = tm * 128, n0 = tn * 128;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int l16 = lane & 15, lg = lane >> 4;
+  f32x4l acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4l{0.f, 0.f, 0.f, 0.f};
+  const int b = P.ksum ? 0 : blockIdx.y;
+  const int nseg = P.ksum ? 2 : 1;
+  const int64_t nk = (K + BK - 1) / BK, total = nk * nseg;
+  Stage<AKC, BK> la;
+  Stage<BKC, BK> lb;
+  auto src = [&](int64_t it, const float*& a, const float*& bb, int64_t& k0) {
+    const int seg = P.ksum ? (int)(it / nk) : b;
+    a = P.A[seg];
+    bb = P.B[seg];
+    k0 = (it % nk) * BK;
+  };
+  {
+    const float *a, *bb;
+    int64_t k0;
+    src(0, a, bb, k0);
+    la.load(a, lda, m0, k0, M, K);
+    lb.load(bb, ldb, n0, k0, N, K);
+  }
+  for (int64_t it = 0; it < total; ++it) {
+    if (it > 0) __syncthreads();
+    la.store(As);
+    lb.store(Bs);
+    __syncthreads();
+    if (it + 1 < total) {
+      const float *a, *bb;
+      int64_t k0;
+      src(it + 1, a, bb, k0);
+      la.load(a, lda, m0, k0, M, K);
+      lb.load(bb, ldb, n0, k0, N, K);
+    }
+    bf16x8 bq[3][4];
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bq[p][j] = frag<BK>(Bs, p, wn + 16 * j + l16, lg >> 1, lg & 1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8 a[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[p] = frag<BK>(As, p, wm + 16 * i + l16, lg >> 1, lg & 1);
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
+        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[pa], bq[pb][j], acc[i][j], 0, 0, 0);
+      }
+    }
+  }
+  float* C = P.C[b];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t n = n0 + wn + 16 * j + l16;
+      if (n >= N) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wm + 16 * i + 4 * lg + r;
+        if (m < M) C[m * ldc + n] = acc[i][j][r];
+      }
+    }
+}
+
 // ---- 8-wave variant (KC/KC only): 512 threads per 128x128 tile, wave = 64x32
 template <int WGS>
 __global__ __launch_bounds__(512, WGS) void gemm3w8_kernel(int64_t M, int64_t N, int64_t K,
@@ -567,6 +666,20 @@ int main() {
                            s.K, P, s.lda, s.ldb, s.N, tn);
       });
       check(dC0, "8-wave 64x32/wave, 3 WG/CU", w3);
+    }
+    {
+      const int tn = (int)((s.N + 127) / 128), tmm = (int)((s.M + 127) / 128);
+      const dim3 grid(tmm * tn, P.ksum ? 1 : 2);
+#define AINP_G16(AK, BK_)                                                                      \
+  if (s.akc == AK && s.bkc == BK_) {                                                           \
+    float t16 = timeit([&] {                                                                   \
+      hipLaunchKernelGGL((gemm16_kernel<AK, BK_, 2>), grid, dim3(THREADS), 0, st, s.M, s.N,    \
+                         s.K, P, s.lda, s.ldb, s.N, tn);                                       \
+    });                                                                                        \
+    check(dC0, "16x16x32 x6 BK32 2WG", t16);                                                   \
+  }
+      AINP_G16(true, true) AINP_G16(true, false) AINP_G16(false, true) AINP_G16(false, false)
+#undef AINP_G16
     }
     float m1 = timeit([&] { run3<16, 2, true>(s, P, st); });
     CK(hipGetLastError());
