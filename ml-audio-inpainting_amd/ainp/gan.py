@@ -340,24 +340,28 @@ class _DiscriminatorFn(torch.autograd.Function):
         for l in range(L - 1, -1, -1):
             k, s, p, act = ctx.cfg[l]
             w = params[2 * l]
-            if act:
-                g = ops.leaky_bwd(g, outs[l], SLOPE)
             N, Cout, Ho, Wo = g.shape
             P = Ho * Wo
+            # pixel rows padded to a multiple of 4 (zeros) for 16-byte GEMM loads
+            P4 = P if (P % 4 == 0 or not act) else P + (-P) % 4
+            if act:
+                g = ops.leaky_bwd(g, outs[l], SLOPE, ldo=P4).view(N, Cout, P4)
+            else:
+                g = g.view(N, Cout, P)
             h = ins[l]
             Cin, H, W = h.shape[1:]
             K = Cin * k * k
             # [dW | db] = sum_n g_n [Cout, P] . [col_n ; 1]^T, P split into chunks
-            col = ops.im2col(h, k, s, p, ones_row=True)        # [N, K+1, P]
+            col = ops.im2col(h, k, s, p, ones_row=True, ldp=P4)    # [N, K+1, P4]
             Gw = torch.empty(Cout, K + 1, device=g.device)
-            ops.gemm_batched_splitk(Cout, K + 1, P, [g[n] for n in range(N)], P, 1,
-                                    [col[n] for n in range(N)], 1, P, Gw)
+            ops.gemm_batched_splitk(Cout, K + 1, P4, [g[n] for n in range(N)], P4, 1,
+                                    [col[n] for n in range(N)], 1, P4, Gw)
             dw, db = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1], with_bias=True)
             grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
             if l > 0 or ctx.needs_input_grad[0]:
                 wn = ops.scale_by_scalar(w, inv[l:l + 1])
                 dcol = torch.empty(N, K, P, device=g.device)
-                ops.gemm(K, P, Cout, [wn], 1, K, [g], P, 1, [dcol], P, 1, strideB=Cout * P,
+                ops.gemm(K, P, Cout, [wn], 1, K, [g], P4, 1, [dcol], P, 1, strideB=Cout * P4,
                          strideC=K * P, nstrided=N)
                 g = ops.col2im(dcol, N, Cin, H, W, k, s, p)
                 if l == 0:

@@ -685,12 +685,14 @@ def sn_weight_grad(G, w_orig, u, v, inv_sigma, with_bias=False):
     return out, ob
 
 
-def im2col(x, k, stride, pad, ones_row=False):
+def im2col(x, k, stride, pad, ones_row=False, ldp=None):
+    """[N, C*k*k (+1), ldp] (ldp >= Ho*Wo; columns past Ho*Wo are zero)."""
     _req(x, "x")
     N, C, H, W = x.shape
     Ho, Wo = conv_out_size(H, k, stride, pad), conv_out_size(W, k, stride, pad)
-    col = torch.empty(N, C * k * k + int(ones_row), Ho * Wo, device=x.device)
-    call("ainp_im2col", x.data_ptr(), N, C, H, W, k, k, stride, pad, int(ones_row),
+    ldp = Ho * Wo if ldp is None else int(ldp)
+    col = torch.empty(N, C * k * k + int(ones_row), ldp, device=x.device)
+    call("ainp_im2col_ld", x.data_ptr(), N, C, H, W, k, k, stride, pad, int(ones_row), ldp,
          col.data_ptr(), _stream(x))
     return col
 
@@ -712,7 +714,9 @@ def gemm_batched_splitk(M, N, Kd, As, sam, sak, Bs, sbk, sbn, out, *, alpha=1.0,
     nb = len(As)
     tiles = -(-M // 128) * -(-N // 128)
     want = max(1, min(Kd // min_k, target_blocks // max(1, tiles * nb)))
-    S = largest_divisor_at_most(Kd, want)
+    # chunks of a multiple of 4 when Kd allows (16-byte aligned chunk starts)
+    q = 4 if Kd % 4 == 0 else 1
+    S = largest_divisor_at_most(Kd // q, want)
     kc = Kd // S
     slabs = torch.empty(nb, S, M, N, device=out.device, dtype=torch.float32)
     for g0 in range(0, nb, 8):
@@ -736,11 +740,20 @@ def col2im(dcol, N, C, H, W, k, stride, pad):
     return dx
 
 
-def leaky_bwd(g, y, slope=0.2):
+def leaky_bwd(g, y, slope=0.2, ldo=None):
+    """LeakyReLU backward; with ldo, g/y [N, C, H, W] -> [N, C, ldo] rows of
+    H*W zero-padded to ldo."""
     _req(g, "g"); _req(y, "y")
-    out = torch.empty_like(g)
-    call("ainp_leaky_bwd", g.data_ptr(), y.data_ptr(), g.numel(), float(slope), out.data_ptr(),
-         _stream(g))
+    if ldo is None:
+        out = torch.empty_like(g)
+        call("ainp_leaky_bwd", g.data_ptr(), y.data_ptr(), g.numel(), float(slope),
+             out.data_ptr(), _stream(g))
+        return out
+    N, C = g.shape[:2]
+    P = g.numel() // (N * C)
+    out = torch.empty(N, C, int(ldo), device=g.device, dtype=torch.float32)
+    call("ainp_leaky_bwd_ld", g.data_ptr(), y.data_ptr(), N * C, P, float(slope), int(ldo),
+         out.data_ptr(), _stream(g))
     return out
 
 

@@ -955,28 +955,33 @@ __global__ void sn_wgrad_apply_kernel(const float* G, int ldg, const double* par
 // ------------------------------------------------------------ D backward glue
 // col[n][ci*KK + tap][oy*Wo + ox] = x[n][ci][oy*s-p+ky][ox*s-p+kx] (0 outside)
 // ones_row: an extra row k = C*KK of 1.0 (the bias column of the weight-grad GEMM)
+// col[n][k][p], p < ldp (row stride; p >= Ho*Wo is zero padding so a GEMM can
+// use 16-byte loads), k = ci*KH*KW + tap, plus a row of ones when ones_row;
+// grid = (pixel blocks, Kr, N): no 64-bit division per element.
 __global__ void im2col_kernel(const float* x, int N, int C, int H, int W, int KH, int KW,
-                              int stride, int pad, int Ho, int Wo, int ones_row, float* col) {
+                              int stride, int pad, int Ho, int Wo, int ones_row, int ldp,
+                              float* col) {
   const int KK = KH * KW;
-  const int64_t P = (int64_t)Ho * Wo;
+  const int P = Ho * Wo;
   const int Kr = C * KK + ones_row;
-  const int64_t total = (int64_t)N * Kr * P;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= total) return;
-  const int64_t pp = t % P;
-  const int64_t rest = t / P;
-  const int k = (int)(rest % Kr);
-  const int n = (int)(rest / Kr);
+  const int pp = blockIdx.x * blockDim.x + threadIdx.x;
+  if (pp >= ldp) return;
+  const int k = blockIdx.y, n = blockIdx.z;
+  float* dst = col + ((int64_t)n * Kr + k) * ldp + pp;
+  if (pp >= P) {
+    *dst = 0.f;
+    return;
+  }
   if (k == C * KK) {
-    col[t] = 1.f;
+    *dst = 1.f;
     return;
   }
   const int ci = k / KK, tap = k - ci * KK;
   const int ky = tap / KW, kx = tap - ky * KW;
-  const int oy = (int)(pp / Wo), ox = (int)(pp - (int64_t)oy * Wo);
+  const int oy = pp / Wo, ox = pp - oy * Wo;
   const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
-  col[t] = (iy >= 0 && iy < H && ix >= 0 && ix < W)
-               ? x[(((int64_t)n * C + ci) * H + iy) * W + ix] : 0.f;
+  *dst = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? x[(((int64_t)n * C + ci) * H + iy) * W + ix]
+                                                  : 0.f;
 }
 
 // dx[n][ci][iy][ix] = sum over taps with (iy+p-ky)/s, (ix+p-kx)/s integral and
@@ -1015,6 +1020,20 @@ __global__ void leaky_bwd_kernel(const float* g, const float* y, int64_t n, floa
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   out[t] = y[t] > 0.f ? g[t] : g[t] * slope;
+}
+
+// rows of P elements -> rows of ldo (zero padded), grid = (column blocks, rows)
+__global__ void leaky_bwd_ld_kernel(const float* g, const float* y, int P, float slope, int ldo,
+                                    float* out) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= ldo) return;
+  const int64_t r = blockIdx.y;
+  float v = 0.f;
+  if (p < P) {
+    const float gv = g[r * P + p];
+    v = y[r * P + p] > 0.f ? gv : gv * slope;
+  }
+  out[r * ldo + p] = v;
 }
 
 // standalone PartialConv2d with a per-channel mask: x*m and sum_c m
@@ -1369,17 +1388,27 @@ extern "C" int ainp_sn_weight_grad(const float* G, int ldg, const float* w_orig,
   return check_launch("sn_weight_grad");
 }
 
-extern "C" int ainp_im2col(const float* x, int64_t N, int C, int H, int W, int KH, int KW,
-                           int stride, int pad, int ones_row, float* col, void* stream) {
-  if (!x || !col || N < 1 || C < 1 || KH < 1 || KW < 1 || stride < 1 || ones_row < 0 ||
-      ones_row > 1)
+extern "C" int ainp_im2col_ld(const float* x, int64_t N, int C, int H, int W, int KH, int KW,
+                              int stride, int pad, int ones_row, int64_t ldp, float* col,
+                              void* stream) {
+  if (!x || !col || N < 1 || N > 65535 || C < 1 || KH < 1 || KW < 1 || stride < 1 ||
+      ones_row < 0 || ones_row > 1)
     return record_msg("ainp_im2col: bad argument");
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
-  const int64_t total = N * (C * KH * KW + ones_row) * (int64_t)Ho * Wo;
-  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                     as_stream(stream), x, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo,
-                     ones_row, col);
+  const int64_t Kr = (int64_t)C * KH * KW + ones_row;
+  if (Ho < 1 || Wo < 1 || ldp < (int64_t)Ho * Wo || ldp > (1 << 30) || Kr > 65535)
+    return record_msg("ainp_im2col: bad shape");
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(ldp, 256), (unsigned)Kr, (unsigned)N),
+                     dim3(256), 0, as_stream(stream), x, (int)N, C, H, W, KH, KW, stride, pad,
+                     Ho, Wo, ones_row, (int)ldp, col);
   return check_launch("im2col");
+}
+
+extern "C" int ainp_im2col(const float* x, int64_t N, int C, int H, int W, int KH, int KW,
+                           int stride, int pad, int ones_row, float* col, void* stream) {
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  return ainp_im2col_ld(x, N, C, H, W, KH, KW, stride, pad, ones_row, (int64_t)Ho * Wo, col,
+                        stream);
 }
 
 extern "C" int ainp_col2im(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW,
@@ -1391,6 +1420,15 @@ extern "C" int ainp_col2im(const float* dcol, int64_t N, int C, int H, int W, in
   hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                      as_stream(stream), dcol, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo, dx);
   return check_launch("col2im");
+}
+
+extern "C" int ainp_leaky_bwd_ld(const float* g, const float* y, int64_t rows, int64_t P,
+                                 float slope, int64_t ldo, float* out, void* stream) {
+  if (!g || !y || !out || rows < 1 || rows > 65535 || P < 1 || ldo < P || ldo > (1 << 30))
+    return record_msg("ainp_leaky_bwd_ld: bad argument");
+  hipLaunchKernelGGL(leaky_bwd_ld_kernel, dim3((unsigned)cdiv(ldo, 256), (unsigned)rows),
+                     dim3(256), 0, as_stream(stream), g, y, (int)P, slope, (int)ldo, out);
+  return check_launch("leaky_bwd_ld");
 }
 
 extern "C" int ainp_leaky_bwd(const float* g, const float* y, int64_t n, float slope, float* out,
