@@ -453,6 +453,8 @@ int ainp_im2col_ld(const float* x, int64_t N, int C, int H, int W, int KH, int K
                    int pad, int ones_row, int64_t ldp, float* col, void* stream);
 int ainp_leaky_bwd_ld(const float* g, const float* y, int64_t rows, int64_t P, float slope,
                       int64_t ldo, float* out, void* stream);
+int ainp_col2im_ld(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW, int stride,
+                   int pad, int64_t ldp, float* dx, void* stream);
 /* PartialConv2d called with a per-channel mask (networks.py:74-85 when
  * mask.shape[1] == C_in): out = a*b elementwise, and the channel sum of the
  * mask [N,C,HW] -> [N,HW] whose window sum is the mask_conv count. */

@@ -109,6 +109,8 @@ _SIGS = {
     "ainp_im2col_ld": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                c_int, c_int64, P, P]),
     "ainp_leaky_bwd_ld": (c_int, [P, P, c_int64, c_int64, c_float, c_int64, P, P]),
+    "ainp_col2im_ld": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                               c_int64, P, P]),
     "ainp_mul": (c_int, [P, P, c_int64, P, P]),
     "ainp_istft_workspace": (c_size_t, [c_int64, c_int64, c_int]),
     "ainp_istft": (c_int, [P, P, c_int, c_int64, c_int, c_int64, P, c_int, c_int, c_int, P, P,

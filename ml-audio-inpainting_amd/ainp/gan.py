@@ -360,9 +360,9 @@ class _DiscriminatorFn(torch.autograd.Function):
             grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
             if l > 0 or ctx.needs_input_grad[0]:
                 wn = ops.scale_by_scalar(w, inv[l:l + 1])
-                dcol = torch.empty(N, K, P, device=g.device)
-                ops.gemm(K, P, Cout, [wn], 1, K, [g], P4, 1, [dcol], P, 1, strideB=Cout * P4,
-                         strideC=K * P, nstrided=N)
+                dcol = torch.empty(N, K, P4, device=g.device)    # padded columns unused
+                ops.gemm(K, P4, Cout, [wn], 1, K, [g], P4, 1, [dcol], P4, 1, strideB=Cout * P4,
+                         strideC=K * P4, nstrided=N)
                 g = ops.col2im(dcol, N, Cin, H, W, k, s, p)
                 if l == 0:
                     gx = g

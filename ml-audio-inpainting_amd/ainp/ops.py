@@ -733,10 +733,11 @@ def gemm_batched_splitk(M, N, Kd, As, sam, sak, Bs, sbk, sbn, out, *, alpha=1.0,
 
 
 def col2im(dcol, N, C, H, W, k, stride, pad):
+    """dcol [N, C*k*k, ldp] (ldp >= Ho*Wo) -> dx [N, C, H, W]."""
     _req(dcol, "dcol")
     dx = torch.empty(N, C, H, W, device=dcol.device)
-    call("ainp_col2im", dcol.data_ptr(), N, C, H, W, k, k, stride, pad, dx.data_ptr(),
-         _stream(dcol))
+    call("ainp_col2im_ld", dcol.data_ptr(), N, C, H, W, k, k, stride, pad, dcol.shape[-1],
+         dx.data_ptr(), _stream(dcol))
     return dx
 
 

@@ -987,9 +987,9 @@ __global__ void im2col_kernel(const float* x, int N, int C, int H, int W, int KH
 // dx[n][ci][iy][ix] = sum over taps with (iy+p-ky)/s, (ix+p-kx)/s integral and
 // in range of dcol[n][ci*KK+tap][oy*Wo+ox]   (gather: deterministic, no atomics)
 __global__ void col2im_kernel(const float* dcol, int N, int C, int H, int W, int KH, int KW,
-                              int stride, int pad, int Ho, int Wo, float* dx) {
+                              int stride, int pad, int Ho, int Wo, int64_t P, float* dx) {
+  // P: row stride of dcol (>= Ho*Wo)
   const int KK = KH * KW;
-  const int64_t P = (int64_t)Ho * Wo;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)N * C * H * W) return;
   const int ix = (int)(t % W);
@@ -1411,15 +1411,23 @@ extern "C" int ainp_im2col(const float* x, int64_t N, int C, int H, int W, int K
                         stream);
 }
 
-extern "C" int ainp_col2im(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW,
-                           int stride, int pad, float* dx, void* stream) {
+extern "C" int ainp_col2im_ld(const float* dcol, int64_t N, int C, int H, int W, int KH,
+                              int KW, int stride, int pad, int64_t ldp, float* dx, void* stream) {
   if (!dcol || !dx || N < 1 || C < 1 || KH < 1 || KW < 1 || stride < 1)
     return record_msg("ainp_col2im: bad argument");
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  if (ldp < (int64_t)Ho * Wo) return record_msg("ainp_col2im: ldp < Ho*Wo");
   const int64_t total = N * C * (int64_t)H * W;
   hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
-                     as_stream(stream), dcol, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo, dx);
+                     as_stream(stream), dcol, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo, ldp,
+                     dx);
   return check_launch("col2im");
+}
+
+extern "C" int ainp_col2im(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW,
+                           int stride, int pad, float* dx, void* stream) {
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  return ainp_col2im_ld(dcol, N, C, H, W, KH, KW, stride, pad, (int64_t)Ho * Wo, dx, stream);
 }
 
 extern "C" int ainp_leaky_bwd_ld(const float* g, const float* y, int64_t rows, int64_t P,
