@@ -351,7 +351,7 @@ def run_gan(args):
         ach = flops / avg_s / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "kernel": f"conv_gen_x6_kernel<64> (final PartialConv2d 65->64 3x3 at "
+                "kernel": f"conv_gen_x6_kernel<64,16> (final PartialConv2d 65->64 3x3 at "
                           f"{Hp}x{Wp}, B={B})", "avg_launch_ms": round(avg_s * 1e3, 4),
                 "flop_per_launch": flops,
                 "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross products "

@@ -355,14 +355,19 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* q) {
 }
 }  // namespace cgx
 
-template <int BM>
-__global__ __launch_bounds__(256, 2) void conv_gen_x6_kernel(ConvGenParams p, const float* wt,
-                                                             int act) {
+// XBK = 16: 16-deep K-tiles with 48-byte image rows (37-46 KB of LDS and
+// <= 168 VGPRs: three workgroups per CU); XBK = 32: 80-byte rows, two.
+// Split-K ranges (p.ktiles_per_split) stay in CG_BK units.
+template <int BM, int XBK>
+__global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(ConvGenParams p,
+                                                                             const float* wt,
+                                                                             int act) {
   constexpr int BN = 16384 / BM;
   constexpr int WN = BN / 64;                 // waves along pixels (2 or 4)
-  constexpr int AR = CG_BK * BM / 256;        // consecutive k per thread, A (16 / 8)
-  constexpr int BR = CG_BK * BN / 256;        // consecutive k per thread, B (16 / 32)
-  constexpr int APL = BM * cgx::RS, BPL = BN * cgx::RS;   // plane bytes
+  constexpr int AR = XBK * BM / 256;          // consecutive k per thread, A
+  constexpr int BR = XBK * BN / 256;          // consecutive k per thread, B
+  constexpr int RS = XBK == 16 ? 48 : cgx::RS;
+  constexpr int APL = BM * RS, BPL = BN * RS;   // plane bytes
   __shared__ __attribute__((aligned(16))) unsigned char sA[3 * APL];
   __shared__ __attribute__((aligned(16))) unsigned char sB[3 * BPL];
   static_assert(3 * APL >= WN * BM * 2 * (int)sizeof(double), "epilogue scratch");
@@ -374,10 +379,12 @@ __global__ __launch_bounds__(256, 2) void conv_gen_x6_kernel(ConvGenParams p, co
   const int64_t NP = (int64_t)p.N * HWo;
   const int64_t px0 = (int64_t)blockIdx.x * BN;
   const int co0 = blockIdx.y * BM;
-  const int kt_begin = blockIdx.z * p.ktiles_per_split;
-  int kt_end = kt_begin + p.ktiles_per_split;
-  const int nkt_all = (K + CG_BK - 1) / CG_BK;
-  if (kt_end > nkt_all) kt_end = nkt_all;
+  constexpr int TPB = CG_BK / XBK;            // x6 tiles per split-range tile
+  const int nkt_all = (K + XBK - 1) / XBK;
+  const int64_t kb = (int64_t)blockIdx.z * p.ktiles_per_split * TPB;
+  const int64_t ke = kb + (int64_t)p.ktiles_per_split * TPB;
+  const int kt_begin = (int)(kb < nkt_all ? kb : nkt_all);
+  const int kt_end = (int)(ke < nkt_all ? ke : nkt_all);
 
   // B staging: pixel bpx = tid % BN, k run [bkq*BR, bkq*BR + BR) (wave-uniform)
   const int bpx = tid % BN, bkq = tid / BN;
@@ -413,7 +420,7 @@ __global__ __launch_bounds__(256, 2) void conv_gen_x6_kernel(ConvGenParams p, co
     return v;
   };
   auto fetch = [&](int kt) {
-    const int k0 = kt * CG_BK;
+    const int k0 = kt * XBK;
 #pragma unroll
     for (int i = 0; i < AR; ++i) {
       const int k = k0 + akq * AR + i;
@@ -421,7 +428,7 @@ __global__ __launch_bounds__(256, 2) void conv_gen_x6_kernel(ConvGenParams p, co
     }
     const bool first = k0 < K0;
     const ConvSrcDev& s = first ? p.s0 : p.s1;
-    if (s.C % CG_BK == 0) {                   // the whole tile is one tap of one source
+    if (s.C % XBK == 0) {                     // the whole tile is one tap of one source
       const int kr = first ? k0 : k0 - K0;
       const int tap = kr / s.C, ci0 = kr - tap * s.C;
       const int ky = tap / p.KW, kx = tap - ky * p.KW;
@@ -442,20 +449,30 @@ __global__ __launch_bounds__(256, 2) void conv_gen_x6_kernel(ConvGenParams p, co
     }
   };
   auto commit = [&]() {
+    if (AR >= 8) {
 #pragma unroll
-    for (int i = 0; i < AR; i += 8) {
+      for (int i = 0; i < AR; i += 8) {
+        uint4 q0, q1, q2;
+        cgx::split8(ra + i, q0, q1, q2);
+        unsigned char* q = sA + aco * RS + (akq * AR + i) * 2;
+        *reinterpret_cast<uint4*>(q) = q0;
+        *reinterpret_cast<uint4*>(q + APL) = q1;
+        *reinterpret_cast<uint4*>(q + 2 * APL) = q2;
+      }
+    } else {                                  // AR == 4: one 8-byte piece per plane
+      float v8[8] = {ra[0 % AR], ra[1 % AR], ra[2 % AR], ra[3 % AR], 0.f, 0.f, 0.f, 0.f};
       uint4 q0, q1, q2;
-      cgx::split8(ra + i, q0, q1, q2);
-      unsigned char* q = sA + aco * cgx::RS + (akq * AR + i) * 2;
-      *reinterpret_cast<uint4*>(q) = q0;
-      *reinterpret_cast<uint4*>(q + APL) = q1;
-      *reinterpret_cast<uint4*>(q + 2 * APL) = q2;
+      cgx::split8(v8, q0, q1, q2);
+      unsigned char* q = sA + aco * RS + (akq * AR) * 2;
+      *reinterpret_cast<uint2*>(q) = make_uint2(q0.x, q0.y);
+      *reinterpret_cast<uint2*>(q + APL) = make_uint2(q1.x, q1.y);
+      *reinterpret_cast<uint2*>(q + 2 * APL) = make_uint2(q2.x, q2.y);
     }
 #pragma unroll
     for (int i = 0; i < BR; i += 8) {
       uint4 q0, q1, q2;
       cgx::split8(rb + i, q0, q1, q2);
-      unsigned char* q = sB + bpx * cgx::RS + (bkq * BR + i) * 2;
+      unsigned char* q = sB + bpx * RS + (bkq * BR + i) * 2;
       *reinterpret_cast<uint4*>(q) = q0;
       *reinterpret_cast<uint4*>(q + BPL) = q1;
       *reinterpret_cast<uint4*>(q + 2 * BPL) = q2;
@@ -478,14 +495,14 @@ __global__ __launch_bounds__(256, 2) void conv_gen_x6_kernel(ConvGenParams p, co
     __syncthreads();
     if (kt + 1 < kt_end) fetch(kt + 1);
 #pragma unroll
-    for (int st = 0; st < CG_BK / 16; ++st) {
+    for (int st = 0; st < XBK / 16; ++st) {
       cgx::bf16x8 a[3][2], b[3][2];
 #pragma unroll
       for (int q = 0; q < 3; ++q)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          a[q][i] = cgx::frag(sA + q * APL + (wm * 64 + i * 32 + l31) * cgx::RS + 32 * st + 16 * lh);
-          b[q][i] = cgx::frag(sB + q * BPL + (wn * 64 + i * 32 + l31) * cgx::RS + 32 * st + 16 * lh);
+          a[q][i] = cgx::frag(sA + q * APL + (wm * 64 + i * 32 + l31) * RS + 32 * st + 16 * lh);
+          b[q][i] = cgx::frag(sB + q * BPL + (wn * 64 + i * 32 + l31) * RS + 32 * st + 16 * lh);
         }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -1182,10 +1199,18 @@ extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H
     const char* e = getenv("AINP_CONV_EXACT");
     return e && e[0] == '1';
   }();
-  if (!exact && BM == 128)
-    hipLaunchKernelGGL(conv_gen_x6_kernel<128>, grid, dim3(256), 0, s, p, wt, act);
+  static const int xbk = [] {
+    const char* e = getenv("AINP_CONV_GEN_BK");
+    return (e && e[0] == '3') ? 32 : 16;
+  }();
+  if (!exact && BM == 128 && xbk == 16)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 16>), grid, dim3(256), 0, s, p, wt, act);
+  else if (!exact && xbk == 16)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 16>), grid, dim3(256), 0, s, p, wt, act);
+  else if (!exact && BM == 128)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 32>), grid, dim3(256), 0, s, p, wt, act);
   else if (!exact)
-    hipLaunchKernelGGL(conv_gen_x6_kernel<64>, grid, dim3(256), 0, s, p, wt, act);
+    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 32>), grid, dim3(256), 0, s, p, wt, act);
   else if (BM == 128)
     hipLaunchKernelGGL(conv_gen_fwd_kernel<128>, grid, dim3(256), 0, s, p, wt, act);
   else
