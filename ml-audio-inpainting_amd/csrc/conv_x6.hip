@@ -43,6 +43,19 @@ constexpr int XI = (XU + NT - 1) / NT;   // units per thread (3)
 }  // namespace cx6
 
 typedef __bf16 bf16x8c __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ int wx6_clamp(int v, int lo, int hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+// buffer loads: 32-bit per-lane offsets + a scalar channel-plane offset, so no
+// per-load 64-bit addresses are kept live across the tile loop
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wx6_rsrc(const float* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+__device__ __forceinline__ float wx6_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
 typedef __bf16 bf16x4c __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t cx6_cvt_pk(float lo, float hi) {
@@ -72,12 +85,21 @@ __device__ __forceinline__ bf16x8c cx6_ld(const unsigned char* p) {
   return __builtin_bit_cast(bf16x8c, *reinterpret_cast<const uint4*>(p));
 }
 
-template <int CI, int COP, bool DGRAD>
-__global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
+// RPW output rows per wave: 2 (16-row tiles, one workgroup per CU) or 1
+// (8-row tiles: half the halo LDS, two workgroups per CU).
+template <int CI, int COP, bool DGRAD, int RPW>
+__global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
     float* __restrict__ y, double* __restrict__ stats, int Cout, int H, int W) {
-  using namespace cx6;
+  using cx6::HC;
+  using cx6::TC;
+  using cx6::CK;
+  using cx6::XROW;
+  using cx6::WROW;
+  using cx6::NT;
+  constexpr int TR = 8 * RPW, HR = TR + 2, XPLANE = HR * XROW;
+  constexpr int XU = 2 * HR * HC, XI = (XU + NT - 1) / NT;
   static_assert(CI % CK == 0 && (COP == 32 || COP == 64), "shape");
   constexpr int NI = COP / 32;
   constexpr int WPLANE = COP * WROW;
@@ -94,16 +116,20 @@ __global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
   const float* xn = x + (int64_t)n * CI * HW;
 
   float px[XI][8];
+  // clamped-address buffer loads (selected to zero at commit); valid while a
+  // sample's CI planes span < 2^31 bytes (the launcher checks)
   auto fetch = [&](int ci0) {
+    int plane = (int)(HW * 4);
+    asm volatile("" : "+s"(plane));
+    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(xn + (int64_t)ci0 * HW);
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
-      const int col = u % HC, row = (u / HC) % HR, half = u / (HR * HC);
-      const int gr = r0 - 1 + row, gc = c0 - 1 + col;
-      const bool inb = u < XU && gr >= 0 && gr < H && gc >= 0 && gc < W;
-      const float* src = xn + (int64_t)(ci0 + 8 * half) * HW + (int64_t)gr * W + gc;
+      const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
+      const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+      const int vo = 8 * half * plane + (gr * W + gc) * 4;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = inb ? src[(int64_t)c * HW] : 0.f;
+      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
     }
   };
   auto commit = [&](int ci0) {
@@ -157,11 +183,11 @@ __global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
     }
   };
 
-  f32x16 acc[NI][2];
+  f32x16 acc[NI][RPW];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < RPW; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -176,16 +202,16 @@ __global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3, dx = tap % 3;
-      bf16x8c a[3][NI], b[3][2];
+      bf16x8c a[3][NI], b[3][RPW];
       const int hcol = li + dx;
-      const unsigned char* xb = sx + (2 * wave + dy) * XROW + hcol * 32 + 16 * (lh ^ ((hcol >> 3) & 1));
+      const unsigned char* xb = sx + (RPW * wave + dy) * XROW + hcol * 32 + 16 * (lh ^ ((hcol >> 3) & 1));
       const unsigned char* wb = sw + li * WROW + tap * 32 + 16 * lh;
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) a[p][i] = cx6_ld(wb + p * WPLANE + i * 32 * WROW);
 #pragma unroll
-        for (int j = 0; j < 2; ++j) b[p][j] = cx6_ld(xb + p * XPLANE + j * XROW);
+        for (int j = 0; j < RPW; ++j) b[p][j] = cx6_ld(xb + p * XPLANE + j * XROW);
       }
       // term-major over the NI x 2 accumulators: no back-to-back dependent MFMAs
 #pragma unroll
@@ -195,7 +221,7 @@ __global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < RPW; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa][i], b[pb][j], acc[i][j], 0,
                                                                 0, 0);
       }
@@ -216,8 +242,8 @@ __global__ __launch_bounds__(cx6::NT, 1) void conv3x3_x6_kernel(
       const float bv = (bias && cok) ? bias[co] : 0.f;
       float s = 0.f, q = 0.f;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = r0 + 2 * wave + j;
+      for (int j = 0; j < RPW; ++j) {
+        const int row = r0 + RPW * wave + j;
         if (cok && row < H && col < W) {
           const float v = acc[i][j][r] + bv;
           yn[(int64_t)co * HW + (int64_t)row * W + col] = v;
@@ -279,7 +305,8 @@ int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, i
     if (Cin == 16 && cop == 32) return 512;
     if (Cin == 32 && Cout == 16) return 512;
   }
-  if ((Cin == 32 && cop == 64) || (Cin == 64 && cop == 32))
+  if (((Cin == 32 && cop == 64) || (Cin == 64 && cop == 32)) &&
+      (int64_t)Cin * H * W * 4 < ((int64_t)1 << 31))    // 32-bit buffer offsets
     return N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   return 0;
 }
@@ -294,17 +321,22 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
                                    parts);
     if (rc != 1) return rc;
   }
+  if ((int64_t)Cin * H * W * 4 >= ((int64_t)1 << 31)) return 1;   // 32-bit buffer offsets
   *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
 #define AINP_X6(CIV, COV)                                                                     \
   if (Cin == CIV && cop == COV) {                                                             \
-    if (dgrad)                                                                                \
-      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true>), grid, dim3(cx6::NT), 0, s, x, w, \
-                         bias, sc, sh, y, stats, Cout, (int)H, (int)W);                       \
-    else                                                                                      \
-      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, false>), grid, dim3(cx6::NT), 0, s, x, \
+    if (dgrad && !stats) {   /* 8-row tiles, two workgroups per CU (no BN partials) */         \
+      const dim3 g8((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, 8), (unsigned)N);           \
+      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1>), g8, dim3(cx6::NT), 0, s, x,  \
                          w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                    \
+    } else if (dgrad)                                                                         \
+      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 2>), grid, dim3(cx6::NT), 0, s, x, \
+                         w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                    \
+    else                                                                                      \
+      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, false, 2>), grid, dim3(cx6::NT), 0, s, \
+                         x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                 \
     return check_launch("conv3x3_x6");                                                        \
   }
   // Only the pairs where this kernel beats the exact f32 kernels on the model's
@@ -345,18 +377,6 @@ constexpr int XU = HR * HC * 4;                // x staging units (pixel, 8-ci g
 
 typedef short v4s16 __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int wx6_clamp(int v, int lo, int hi) {
-  return v < lo ? lo : (v > hi ? hi : v);
-}
-// buffer loads: 32-bit per-lane offsets + a scalar channel-plane offset, so no
-// per-load 64-bit addresses are kept live across the tile loop
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wx6_rsrc(const float* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(p), (short)0, 0x7fffffff,
-                                           0x00020000);
-}
-__device__ __forceinline__ float wx6_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
-  return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
-}
 
 __device__ __forceinline__ v4s16 wx6_tr(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
