@@ -47,6 +47,16 @@ CFG = {
 }
 
 
+def _traffic(name):
+    """HBM bytes per launch of a roofline kernel from its committed rocprofv3
+    FETCH_SIZE/WRITE_SIZE passes (profiles/<name>, tools/pmc_*.sh), or None."""
+    tf = os.path.join(ROOT, "profiles", name)
+    try:
+        return json.load(open(tf)).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
 def synthetic_clips(n, S, seed0):
     from ainp.synth import synthetic_clip
     return np.stack([synthetic_clip(seed0 + i, S) for i in range(n)])
@@ -191,13 +201,7 @@ def main():
         avg_s = e0.elapsed_time(e1) / 1000.0 / args.roofline_reps
         flops = 2.0 * M * (8 * H) * I
         achieved = flops / avg_s / 1e12
-        traffic = None
-        tf = os.path.join(ROOT, "profiles", "traffic_gemm_l0.json")
-        if os.path.exists(tf):
-            try:
-                traffic = json.load(open(tf)).get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
+        traffic = _traffic("traffic_gemm_l0.json")
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
                 "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
                 "traffic": traffic, "kernel": "gemm_f32_kernel (LSTM l0 input projection, "
@@ -350,7 +354,8 @@ def run_gan(args):
         flops = 2.0 * 64 * 65 * 9 * B * Hp * Wp
         ach = flops / avg_s / 1e12
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": _traffic("traffic_conv_gen_final.json"),
                 "kernel": f"conv_gen_x6_kernel<64,16> (final PartialConv2d 65->64 3x3 at "
                           f"{Hp}x{Wp}, B={B})", "avg_launch_ms": round(avg_s * 1e3, 4),
                 "flop_per_launch": flops,
