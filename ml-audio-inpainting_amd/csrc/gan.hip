@@ -1001,6 +1001,94 @@ __global__ void im2col_kernel(const float* x, int N, int C, int H, int W, int KH
                                                   : 0.f;
 }
 
+// im2col with 4 consecutive pixels x IM2COL_IK consecutive rows k per thread
+// and 16-byte stores (ldp % 4 == 0): the row/column split of the first pixel
+// is the only division, and 4*IM2COL_IK loads are in flight (clamped
+// addresses, masked values).  Same values as im2col_kernel.
+constexpr int IM2COL_IK = 4;
+__global__ void im2col4_kernel(const float* x, int C, int H, int W, int KH, int KW, int stride,
+                               int pad, int Ho, int Wo, int ones_row, int ldp, float* col) {
+  const int KK = KH * KW;
+  const int P = Ho * Wo;
+  const int Kr = C * KK + ones_row;
+  const int pp0 = 4 * (blockIdx.x * blockDim.x + threadIdx.x);
+  if (pp0 >= ldp) return;
+  const int n = blockIdx.z;
+  const int oy0 = pp0 / Wo, ox0 = pp0 - oy0 * Wo;
+  float v[IM2COL_IK][4];
+#pragma unroll
+  for (int j = 0; j < IM2COL_IK; ++j) {
+    const int k = blockIdx.y * IM2COL_IK + j;
+    if (k >= C * KK) {                       // the ones row, or past the end
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[j][e] = (k == C * KK && pp0 + e < P) ? 1.f : 0.f;
+      continue;
+    }
+    const int ci = k / KK, tap = k - ci * KK;
+    const int ky = tap / KW, kx = tap - ky * KW;
+    const float* xp = x + ((int64_t)n * C + ci) * H * W;
+    int oy = oy0, ox = ox0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+      const bool ok = pp0 + e < P && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      const float t = xp[ok ? iy * W + ix : 0];
+      v[j][e] = ok ? t : 0.f;
+      if (++ox == Wo) {
+        ox = 0;
+        ++oy;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < IM2COL_IK; ++j) {
+    const int k = blockIdx.y * IM2COL_IK + j;
+    if (k < Kr)
+      *reinterpret_cast<float4*>(col + ((int64_t)n * Kr + k) * ldp + pp0) =
+          make_float4(v[j][0], v[j][1], v[j][2], v[j][3]);
+  }
+}
+
+// col2im for a KSxKS kernel at stride S (the Discriminator's 4x4, stride 2 or
+// 1): one (n, ci) plane per blockIdx.y.  At stride 2 only the taps of the
+// pixel's parity contribute, so (KS/S)^2 loads, all issued before the sum
+// (clamped addresses, masked values); the sum runs in ascending (ky, kx) order
+// like col2im_kernel.
+template <int KS, int S>
+__global__ void col2im_ks_kernel(const float* dcol, int C, int H, int W, int pad, int Ho,
+                                 int Wo, int64_t P, float* dx) {
+  constexpr int KT = KS / S;
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= H * W) return;
+  const int nc = blockIdx.y;
+  const int iy = r / W, ix = r - iy * W;
+  const int by = iy + pad, bx = ix + pad;
+  const float* dp = dcol + (int64_t)nc * KS * KS * P;
+  float v[KT][KT];
+#pragma unroll
+  for (int a = 0; a < KT; ++a) {
+    const int ky = (S == 2 ? (by & 1) : 0) + S * a;
+    const int ty = by - ky;
+    const int oy = S == 2 ? ty >> 1 : ty;
+    const bool vy = ty >= 0 && oy < Ho;
+#pragma unroll
+    for (int b = 0; b < KT; ++b) {
+      const int kx = (S == 2 ? (bx & 1) : 0) + S * b;
+      const int tx = bx - kx;
+      const int ox = S == 2 ? tx >> 1 : tx;
+      const bool ok = vy && tx >= 0 && ox < Wo;
+      const float t = dp[ok ? (int64_t)(ky * KS + kx) * P + oy * Wo + ox : 0];
+      v[a][b] = ok ? t : 0.f;
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < KT; ++a)
+#pragma unroll
+    for (int b = 0; b < KT; ++b) s += v[a][b];
+  dx[(int64_t)nc * H * W + r] = s;
+}
+
 // dx[n][ci][iy][ix] = sum over taps with (iy+p-ky)/s, (ix+p-kx)/s integral and
 // in range of dcol[n][ci*KK+tap][oy*Wo+ox]   (gather: deterministic, no atomics)
 __global__ void col2im_kernel(const float* dcol, int N, int C, int H, int W, int KH, int KW,
@@ -1423,9 +1511,15 @@ extern "C" int ainp_im2col_ld(const float* x, int64_t N, int C, int H, int W, in
   const int64_t Kr = (int64_t)C * KH * KW + ones_row;
   if (Ho < 1 || Wo < 1 || ldp < (int64_t)Ho * Wo || ldp > (1 << 30) || Kr > 65535)
     return record_msg("ainp_im2col: bad shape");
-  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(ldp, 256), (unsigned)Kr, (unsigned)N),
-                     dim3(256), 0, as_stream(stream), x, (int)N, C, H, W, KH, KW, stride, pad,
-                     Ho, Wo, ones_row, (int)ldp, col);
+  if (ldp % 4 == 0 && ((uintptr_t)col & 15) == 0)
+    hipLaunchKernelGGL(im2col4_kernel, dim3((unsigned)cdiv(ldp / 4, 256),
+                                            (unsigned)cdiv(Kr, IM2COL_IK), (unsigned)N),
+                       dim3(256), 0, as_stream(stream), x, C, H, W, KH, KW, stride, pad, Ho, Wo,
+                       ones_row, (int)ldp, col);
+  else
+    hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)cdiv(ldp, 256), (unsigned)Kr, (unsigned)N),
+                       dim3(256), 0, as_stream(stream), x, (int)N, C, H, W, KH, KW, stride, pad,
+                       Ho, Wo, ones_row, (int)ldp, col);
   return check_launch("im2col");
 }
 
@@ -1443,6 +1537,17 @@ extern "C" int ainp_col2im_ld(const float* dcol, int64_t N, int C, int H, int W,
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   if (ldp < (int64_t)Ho * Wo) return record_msg("ainp_col2im: ldp < Ho*Wo");
   const int64_t total = N * C * (int64_t)H * W;
+  if (KH == 4 && KW == 4 && (stride == 1 || stride == 2) && N * C <= 65535 &&
+      (int64_t)H * W < (1 << 30)) {
+    const dim3 grid((unsigned)cdiv((int64_t)H * W, 256), (unsigned)(N * C));
+    if (stride == 2)
+      hipLaunchKernelGGL((col2im_ks_kernel<4, 2>), grid, dim3(256), 0, as_stream(stream), dcol,
+                         C, H, W, pad, Ho, Wo, ldp, dx);
+    else
+      hipLaunchKernelGGL((col2im_ks_kernel<4, 1>), grid, dim3(256), 0, as_stream(stream), dcol,
+                         C, H, W, pad, Ho, Wo, ldp, dx);
+    return check_launch("col2im");
+  }
   hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                      as_stream(stream), dcol, (int)N, C, H, W, KH, KW, stride, pad, Ho, Wo, ldp,
                      dx);

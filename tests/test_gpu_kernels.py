@@ -381,3 +381,36 @@ def test_adam_matches_torch(ops):
         ops.adam_step(dp, [gg.to(DEV) for gg in grads], m, v, 1e-3, 0.9, 0.999, 1e-8, 0.0, step)
     for r, p in zip(ref, dp):
         assert torch.allclose(p.cpu(), r.detach(), rtol=1e-6, atol=1e-7)
+
+
+# ------------------------------------------------------------------ im2col / col2im
+# The Discriminator backward's unfold / fold (4x4 kernels at stride 2 and 1;
+# 3x3 exercises the generic col2im).  im2col is a copy: bit-exact against
+# torch's unfold.  col2im sums up to k*k terms: float64 fold, 1e-6.
+@pytest.mark.parametrize("N,C,H,W,k,s,pad,ones,pad4", [
+    (2, 3, 17, 30, 4, 2, 1, False, True),
+    (2, 5, 16, 33, 4, 1, 1, True, True),
+    (1, 4, 13, 21, 4, 2, 1, True, False),
+    (2, 3, 12, 19, 3, 1, 1, False, True),
+    (1, 2, 9, 14, 3, 2, 1, False, False),
+])
+def test_im2col_col2im(ops, N, C, H, W, k, s, pad, ones, pad4):
+    g = torch.Generator().manual_seed(N * 1000 + C * 10 + H + k)
+    x = torch.randn(N, C, H, W, generator=g)
+    Ho, Wo = (H + 2 * pad - k) // s + 1, (W + 2 * pad - k) // s + 1
+    P = Ho * Wo
+    ldp = (P + 3) // 4 * 4 if pad4 else None
+    col = ops.im2col(x.to(DEV), k, s, pad, ones_row=ones, ldp=ldp).cpu()
+    ref = Fnn.unfold(x, k, padding=pad, stride=s)           # [N, C*k*k, P]
+    L = ldp or P
+    assert col.shape == (N, C * k * k + int(ones), L)
+    assert torch.equal(col[:, :C * k * k, :P], ref)
+    if ones:
+        assert torch.equal(col[:, -1, :P], torch.ones(N, P))
+    if L > P:
+        assert torch.count_nonzero(col[:, :, P:]) == 0
+    dcol = torch.randn(N, C * k * k, L, generator=g)
+    dx = ops.col2im(dcol.to(DEV), N, C, H, W, k, s, pad).cpu()
+    want = Fnn.fold(dcol[:, :, :P].double(), (H, W), k, padding=pad, stride=s)
+    assert dx.shape == (N, C, H, W)
+    assert rel(dx, want) < 1e-6
