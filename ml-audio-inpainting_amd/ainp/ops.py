@@ -718,15 +718,16 @@ def gemm_batched_splitk(M, N, Kd, As, sam, sak, Bs, sbk, sbn, out, *, alpha=1.0,
     q = 4 if Kd % 4 == 0 else 1
     S = largest_divisor_at_most(Kd // q, want)
     kc = Kd // S
-    slabs = torch.empty(nb, S, M, N, device=out.device, dtype=torch.float32)
+    # slab layout [S, nb, M, N]: the per-batch results are one sum over S
+    # slabs of nb*M*N, the batch total one sum over S*nb slabs of M*N
+    slabs = torch.empty(S, nb, M, N, device=out.device, dtype=torch.float32)
     for g0 in range(0, nb, 8):
         g1 = min(nb, g0 + 8)
         gemm(M, N, kc, As[g0:g1], sam, sak, Bs[g0:g1], sbk, sbn,
-             [slabs[i] for i in range(g0, g1)], N, 1, alpha=alpha, strideA=kc * sak,
-             strideB=kc * sbk, strideC=M * N, nstrided=S)
+             [slabs[0, i] for i in range(g0, g1)], N, 1, alpha=alpha, strideA=kc * sak,
+             strideB=kc * sbk, strideC=nb * M * N, nstrided=S)
     if per_batch_out:
-        for b in range(nb):
-            sum_slabs(slabs[b], S, out=out[b].reshape(-1))
+        sum_slabs(slabs, S, out=out.reshape(-1))
     else:
         sum_slabs(slabs, nb * S, out=out.reshape(-1))
     return out
