@@ -604,7 +604,15 @@ __global__ __launch_bounds__(256) void conv_cout1_partial_kernel(ConvGenParams p
         const float* xb = s.x + ((int64_t)n * s.C + (lo - sc0)) * plane + off;
         const float* wb = sw + (lo - c0) * KK + ky * p.KW + kx;
         float a = 0.f;
-        for (int c = 0; c < hi - lo; ++c) a = fmaf(wb[c * KK], xb[(int64_t)c * plane], a);
+        if (hi - lo == C1_CC) {   // a full chunk: 32 loads in flight, 4 partial chains
+          float a4[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int c = 0; c < C1_CC; ++c)
+            a4[c & 3] = fmaf(wb[c * KK], xb[(int64_t)c * plane], a4[c & 3]);
+          a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        } else {
+          for (int c = 0; c < hi - lo; ++c) a = fmaf(wb[c * KK], xb[(int64_t)c * plane], a);
+        }
         acc = fmaf(a, mv, acc);
       }
     }
@@ -852,17 +860,34 @@ struct SnLayers {
   int nl;
 };
 
-// tv[l][j] = sum_i W[i][j] u[i]    (grid: x = column blocks, y = layer)
-__global__ void sn_tmv_kernel(SnLayers L, float* tv, int ldt) {
+// tv[l][j] = sum_i W[i][j] u[i]    (grid: x = blocks of 64 columns, y = layer)
+// Each wave of the 256-thread block takes the rows i = q mod 4 of 64
+// coalesced columns with four independent FMA chains; the four waves' sums
+// are added in fixed order through LDS.
+constexpr int SN_TMV_COLS = 64;
+__global__ __launch_bounds__(256) void sn_tmv_kernel(SnLayers L, float* tv, int ldt) {
+  __shared__ float red[4][SN_TMV_COLS];
   const int l = blockIdx.y;
-  if (l >= L.nl) return;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= L.wd[l]) return;
-  const float* W = L.w[l];
-  const float* u = L.u[l];
-  float s = 0.f;
-  for (int i = 0; i < L.h[l]; ++i) s = fmaf(W[(int64_t)i * L.wd[l] + j], u[i], s);
-  tv[(int64_t)l * ldt + j] = s;
+  if (l >= L.nl) return;                      // uniform over the block
+  const int jl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int j = blockIdx.x * SN_TMV_COLS + jl;
+  const int wd = L.wd[l], h = L.h[l];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < wd) {
+    const float* W = L.w[l] + j;
+    const float* u = L.u[l];
+    int i = q;
+    for (; i + 12 < h; i += 16) {
+      s0 = fmaf(W[(int64_t)i * wd], u[i], s0);
+      s1 = fmaf(W[(int64_t)(i + 4) * wd], u[i + 4], s1);
+      s2 = fmaf(W[(int64_t)(i + 8) * wd], u[i + 8], s2);
+      s3 = fmaf(W[(int64_t)(i + 12) * wd], u[i + 12], s3);
+    }
+    for (; i < h; i += 4) s0 = fmaf(W[(int64_t)i * wd], u[i], s0);
+  }
+  red[q][jl] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (q == 0 && j < wd) tv[(int64_t)l * ldt + j] = (red[0][jl] + red[1][jl]) + (red[2][jl] + red[3][jl]);
 }
 
 __device__ float block_sum_f(float v, float* red) {
@@ -955,10 +980,11 @@ __global__ void sn_wgrad_apply_kernel(const float* G, int ldg, const double* par
                                       const float* u, const float* v, const float* inv_sigma,
                                       int h, int wd, float* out, float* out_bias) {
   __shared__ float gw;
-  if (threadIdx.x == 0) {
+  if (threadIdx.x < 64) {   // wave 0: strided lane sums + butterfly, same order in every block
     double s = 0.0;
-    for (int b = 0; b < np; ++b) s += partial[b];
-    gw = (float)s;
+    for (int b = threadIdx.x; b < np; b += 64) s += partial[b];
+    s = wave_sum_d(s);
+    if (threadIdx.x == 0) gw = (float)s;
   }
   __syncthreads();
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1472,7 +1498,7 @@ extern "C" int ainp_sn_power(const float* const* w, float* const* u, float* cons
   float* tu = tv + (size_t)nl * maxdim;
   hipStream_t s = as_stream(stream);
   if (update) {
-    hipLaunchKernelGGL(sn_tmv_kernel, dim3((unsigned)cdiv(maxw, 256), nl), dim3(256), 0, s, L,
+    hipLaunchKernelGGL(sn_tmv_kernel, dim3((unsigned)cdiv(maxw, SN_TMV_COLS), nl), dim3(256), 0, s, L,
                        tv, maxdim);
     hipLaunchKernelGGL(sn_normalize_v_kernel, dim3(nl), dim3(1024), 0, s, L, tv, maxdim, eps);
   }
