@@ -92,7 +92,19 @@ __global__ void sum_slabs_kernel(const float* __restrict__ x, int64_t nslabs,
     const int64_t i = i4 * 4;
     if (i + 3 < n && (n & 3) == 0) {
       float4 a = *reinterpret_cast<const float4*>(x + i);
-      for (int64_t s = 1; s < nslabs; ++s) {
+      int64_t s = 1;
+      // 4 slab loads in flight per iteration; the adds keep slab order.
+      for (; s + 3 < nslabs; s += 4) {
+        float4 b[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          b[u] = *reinterpret_cast<const float4*>(x + (s + u) * n + i);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a.x += b[u].x; a.y += b[u].y; a.z += b[u].z; a.w += b[u].w;
+        }
+      }
+      for (; s < nslabs; ++s) {
         const float4 b = *reinterpret_cast<const float4*>(x + s * n + i);
         a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
       }
