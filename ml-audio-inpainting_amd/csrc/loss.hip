@@ -60,6 +60,14 @@ __global__ void colsum_slabs_kernel(const float* __restrict__ x, int64_t rows, i
   const float* p = x + j;
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
   int64_t r = r0;
+  // 8 rows in flight; the adds keep the 4-accumulator order of the loop below.
+  for (; r + 7 < r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(r + u) * ld];
+    a0 += v[0]; a1 += v[1]; a2 += v[2]; a3 += v[3];
+    a0 += v[4]; a1 += v[5]; a2 += v[6]; a3 += v[7];
+  }
   for (; r + 3 < r1; r += 4) {
     a0 += p[r * ld];
     a1 += p[(r + 1) * ld];
