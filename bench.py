@@ -62,8 +62,23 @@ def synthetic_clips(n, S, seed0):
     return np.stack([synthetic_clip(seed0 + i, S) for i in range(n)])
 
 
-def cpu_baseline(batch, T, steps=2, warmup=1):
-    """Oracle (reference restatement) train step on the host cores."""
+def host_cpu():
+    """(nproc, CPU model) of the host this runs on (lscpu's 'Model name')."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return os.cpu_count(), model
+
+
+def cpu_baseline(batch, T, steps=5, warmup=1):
+    """Oracle (reference restatement) train step on the host cores; the numpy
+    float64 data path (STFT / log10 / mask, the librosa restatement) is timed
+    separately on the same batch."""
     from oracle import cnnblstm_ref, stft_ref
     from ainp.synth import synthetic_clip
     # the GPU box exposes the whole machine in os.cpu_count() but gives this job
@@ -76,31 +91,72 @@ def cpu_baseline(batch, T, steps=2, warmup=1):
     S = 64000
     rng = np.random.default_rng(1)
     xs, ms, ts = [], [], []
+    clips = [synthetic_clip(1000 + i, S) for i in range(batch)]
+    d0 = time.perf_counter()
     for i in range(batch):
-        clip = synthetic_clip(1000 + i, S)
-        lg, tg, mk = stft_ref.cnnblstm_item(clip, int(rng.integers(0, S - 3200)), 3200,
+        lg, tg, mk = stft_ref.cnnblstm_item(clips[i], int(rng.integers(0, S - 3200)), 3200,
                                             512, 192, 384, 16000, T)
         xs.append(lg); ms.append(mk); ts.append(tg)
+    data_s = time.perf_counter() - d0
     x = torch.from_numpy(np.stack(xs)); m = torch.from_numpy(np.stack(ms))
     t = torch.from_numpy(np.stack(ts))
     for _ in range(warmup):
         tr.step(x, m, t)
-    t0 = time.perf_counter()
+    times = []
     for _ in range(steps):
+        t0 = time.perf_counter()
         tr.step(x, m, t)
-    dt = (time.perf_counter() - t0) / steps
+        times.append(time.perf_counter() - t0)
+    dt = float(np.median(times))
+    nproc, model = host_cpu()
     return {"value": round(batch * T / dt, 2), "unit": "frames/s", "cores": cores,
-            "kind": "port",
+            "kind": "port", "nproc": nproc, "cpu_model": model,
+            "data_path_frames_per_s": round(batch * T / data_s, 1),
             "sample": f"oracle/cnnblstm_ref.py fp32 torch-CPU train step (fwd+L1+bwd+Adam), "
-                      f"batch {batch} x T={T} of the C2 shapes, {steps} timed steps after "
-                      f"{warmup} warmup; features precomputed (data path not timed)"}
+                      f"batch {batch} x T={T} of the C2 shapes, median of {steps} timed steps "
+                      f"after {warmup} warmup on {cores} threads; the numpy data path "
+                      f"(oracle/stft_ref.py, single thread) is timed separately"}
+
+
+def eval_recon_l1(model, n_fft, hop, win, T, S, g, dev, n_clips=64, batch=32):
+    """Reference test loss (models/CNNBLSTM/train.py:128-150,192): model.eval(),
+    L1(sum) of 10**y vs |target| inside the gap per batch, averaged over the
+    batches of a fixed 64-clip synthetic eval set."""
+    from ainp import ops
+    from ainp.cnnblstm import l1_pow10_loss
+    audio = torch.from_numpy(synthetic_clips(n_clips, S, 900000)).to(dev)
+    rng = np.random.default_rng(424242)
+    starts = torch.from_numpy(rng.integers(0, S - g, size=n_clips).astype(np.int64)).to(dev)
+    model.eval()
+    tot = 0.0
+    with torch.no_grad():
+        for i in range(0, n_clips, batch):
+            x, tgt, mask, _ = ops.stft_features(audio[i:i + batch], starts[i:i + batch], g,
+                                                n_fft, hop, win, n_frames=T)
+            tot += float(l1_pow10_loss(model(x.unsqueeze(1)), mask, tgt).item())
+    model.train()
+    return tot / (n_clips // batch)
+
+
+def time_kernel(fn, reps, dev):
+    """Average wall time of fn() (one launch) from HIP events on the current stream."""
+    for _ in range(2):
+        fn()
+    s = torch.cuda.current_stream(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / 1000.0 / reps
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=32, help="examples per GPU (C2: 32)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-batch", type=int, default=4)
@@ -155,26 +211,30 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev[0].record()
     for i in range(args.warmup, nsteps):
         step(i)
+        ev[i - args.warmup + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    step_ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]
+    med_ms = float(np.median(step_ms))
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        e = torch.tensor([elapsed, med_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-        lsum = losses.double().sum().reshape(1)
-        dist.all_reduce(lsum)
+        elapsed, med_ms = float(e[0].item()), float(e[1].item())
     frames = B * T * args.steps * world
     value = frames / elapsed
     ms_step = 1000.0 * elapsed / args.steps
-    recon_l1 = float(losses[-1].item())
+    train_loss = float(losses[-1].item())
+    recon_l1 = eval_recon_l1(model, n_fft, hop, win, T, S, g, dev) if rank == 0 else None
 
     # ---- roofline: dominant kernel (LSTM layer-0 input projection GEMM) timed live
     roof = None
@@ -189,16 +249,7 @@ def main():
                   [zx, zx[:, 4 * H:]], 8 * H, 1)
         kw = dict(bias1=[lw.bias_ih_l0, lw.bias_ih_l0_reverse],
                   bias2=[lw.bias_hh_l0, lw.bias_hh_l0_reverse])
-        for _ in range(2):
-            ops.gemm(*args_g, **kw)
-        s = torch.cuda.current_stream(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(args.roofline_reps):
-            ops.gemm(*args_g, **kw)
-        e1.record(s)
-        torch.cuda.synchronize()
-        avg_s = e0.elapsed_time(e1) / 1000.0 / args.roofline_reps
+        avg_s = time_kernel(lambda: ops.gemm(*args_g, **kw), args.roofline_reps, dev)
         flops = 2.0 * M * (8 * H) * I
         achieved = flops / avg_s / 1e12
         traffic = _traffic("traffic_gemm_l0.json")
@@ -216,6 +267,20 @@ def main():
                 "executed_tflops": round(6 * achieved, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
                 "executed_frac": round(6 * achieved / BF16_MFMA_PEAK_TFLOPS, 4)})
 
+    # ---- STFT / feature / mask path (HBM-bound): 4880 B per frame
+    roof_stft = None
+    if rank == 0:
+        st_s = time_kernel(lambda: ops.stft_features(audio, starts[0], g, n_fft, hop, win,
+                                                     n_frames=T), args.roofline_reps, dev)
+        st_bytes = 4880 * B * T
+        gbs = st_bytes / st_s / 1e9
+        roof_stft = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                     "traffic": _traffic("traffic_stft.json"),
+                     "kernel": "stft512_kernel<CNNBLSTM> (fused STFT + log10|X_gap| + c64 "
+                               f"target + gap mask, {B} x {T} frames)",
+                     "avg_launch_ms": round(st_s * 1e3, 4), "bytes_per_launch": st_bytes}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_batch, T)
@@ -231,11 +296,17 @@ def main():
                                    "fp32, 32 examples/GPU, F=257, T=334, H=128, 3-layer BLSTM",
                        "global_batch": B * world, "seq_len": T, "freq_bins": n_fft // 2 + 1,
                        "parallelism": f"dp{world}" + ("+syncbn" if world > 1 else "")},
+            "ms_per_step_median": round(med_ms, 3),
+            "value_median": round(B * T * world / (med_ms / 1e3), 2),
             "recon_l1": recon_l1,
+            "recon_l1_def": "mean over the 2 batches of a fixed 64-clip eval set of "
+                            "L1sum(10**y*m, |X|*m), model.eval() (train.py:128-150,192)",
+            "train_loss_last": train_loss,
             "step_tflops": round(step_flops / (ms_step / 1e3) / 1e12, 2),
             "mfma_util_step": round(step_flops / world / (ms_step / 1e3) / 1e12
                                     / FP32_MFMA_PEAK_TFLOPS, 4),
             "roofline": roof,
+            "roofline_stft": roof_stft,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

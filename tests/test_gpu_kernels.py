@@ -86,6 +86,98 @@ def test_stft_gan_vs_oracle(ops, S, n_fft, hop, win):
         assert np.max(d[mag > 1e-3]) < 1e-4
 
 
+def _feat_generic(ops, *a, **k):
+    """The generic (one-wave-per-frame radix-2) kernel, for cross-checks of the
+    n_fft=512 tiled kernel."""
+    os.environ["AINP_STFT_GENERIC"] = "1"
+    try:
+        return ops.stft_features(*a, **k)
+    finally:
+        del os.environ["AINP_STFT_GENERIC"]
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("S,hop,win,n_frames,g", [
+    (64000, 192, 384, 334, 3200),      # C2
+    (80000, 128, 512, None, 3200),     # C4
+    (128000, 128, 512, None, 1600),    # C5
+    (9001, 193, 384, 60, 700),         # odd hop and length: scalar-load variant
+    (8000, 192, 384, 50, 0),           # no gap
+    (6000, 160, 400, 45, 5999),        # gap covering almost everything, frames past the end
+])
+def test_stft512_tiled_vs_generic_and_oracle(ops, mode, S, hop, win, n_frames, g):
+    """Tiled n_fft=512 kernel vs the generic kernel and the oracle: masks
+    bit-exact, log-magnitudes / complex target / phase to the oracle tolerance;
+    several examples per clip through clip_index; gaps at the edges."""
+    n_clips, B = 2, 5
+    clips = np.stack([synth.synthetic_clip(70 + i, S) for i in range(n_clips)])
+    ci = np.array([0, 1, 0, 1, 1], np.int32)
+    hi = S - g + (1 if mode == 1 else 0)
+    starts = np.array([0, max(hi - 1, 0), 1234 % max(hi, 1), 77 % max(hi, 1), hi // 2], np.int64)
+    a = torch.from_numpy(clips).to(DEV)
+    gs = torch.from_numpy(starts).to(DEV)
+    cidx = torch.from_numpy(ci).to(DEV)
+    T = n_frames if n_frames is not None else 1 + S // hop
+    kw = dict(n_frames=T, mode=mode, clip_index=cidx)
+    new = ops.stft_features(a, gs, g, 512, hop, win, **kw)
+    old = _feat_generic(ops, a, gs, g, 512, hop, win, **kw)
+    torch.cuda.synchronize()
+    mi = 2 if mode == 0 else 3
+    np.testing.assert_array_equal(new[mi].cpu().numpy(), old[mi].cpu().numpy())
+    for b in range(B):
+        clip = clips[ci[b]]
+        if mode == 0:
+            rl, rt, rm = stft_ref.cnnblstm_item(clip, int(starts[b]), g, 512, hop, win, 16000, T)
+            np.testing.assert_array_equal(new[2][b].cpu().numpy(), rm)
+            assert np.max(np.abs(new[0][b].cpu().numpy() - rl)) < 2e-5
+            tt = new[1][b].cpu().numpy()
+            assert np.max(np.abs(tt - rt)) <= 2e-6 * max(1.0, np.abs(rt).max())
+        else:
+            r0, r1, r2, r3 = stft_ref.gan_item(clip, int(starts[b]), g, 512, hop, win)
+            Tc = min(T, r0.shape[1])       # frames past 1 + S//hop are zero
+            o = [new[i][b].cpu().numpy() for i in range(4)]
+            np.testing.assert_array_equal(o[3][:, :Tc], r3[:, :Tc])
+            assert np.max(np.abs(o[0][:, :Tc] - r0[:, :Tc])) < 1e-5
+            assert np.max(np.abs(o[1][:, :Tc] - r1[:, :Tc])) < 1e-5
+            d = np.abs(np.angle(np.exp(1j * (o[2][:, :Tc] - r2[:, :Tc]))))
+            assert np.max(d[np.expm1(r0[:, :Tc]) > 1e-3]) < 1e-4
+            assert not np.any(o[0][:, Tc:]) and not np.any(o[1][:, Tc:])
+    # partial output requests (null planes) give the same values
+    part = ops.stft_features(a, gs, g, 512, hop, win, outputs=(True, False, False, True), **kw)
+    torch.cuda.synchronize()
+    assert torch.equal(part[0], new[0])
+    if mode == 1:
+        assert torch.equal(part[3], new[3])
+
+
+def test_gap_frames_known_answers_n512(ops, golden_dir):
+    """The Q3 known answers through the tiled n_fft=512 kernel (mask-only launch)."""
+    cases = json.load(open(os.path.join(golden_dir, "gap_frames.json")))["cases"]
+    for c in cases:
+        rule = c["rule"]
+        hop = c["hop"]
+        if rule == "gan":
+            T = c["n_frames"]
+            S = T * hop - 1
+        else:
+            T = max(c["fe"], 1) + 2
+            S = max(c["start"] + c["gap"] + 1, 1000)
+        a = torch.zeros(1, S, device=DEV)
+        gs = torch.tensor([c["start"]], device=DEV, dtype=torch.int64)
+        mode = ops.FEAT_CNNBLSTM if rule == "cnnblstm" else ops.FEAT_GAN
+        out = ops.stft_features(a, gs, c["gap"], 512, hop, 512, n_frames=T, mode=mode,
+                                outputs=(False, False, rule == "cnnblstm", rule == "gan"))
+        m = (out[2] if rule == "cnnblstm" else out[3])[0, 0].cpu().numpy()
+        if rule == "cnnblstm":
+            exp = np.zeros(T, np.float32)
+            exp[c["fs"]:c["fe"]] = 1
+        else:
+            exp = np.ones(T, np.float32)
+            if c["fe"] > c["fs"]:
+                exp[c["fs"]:c["fe"]] = 0
+        np.testing.assert_array_equal(m, exp, err_msg=str(c))
+
+
 def test_gap_frames_known_answers(ops, golden_dir):
     """bit-exact frame indices incl. the float64 round-trip quirk."""
     cases = json.load(open(os.path.join(golden_dir, "gap_frames.json")))["cases"]
