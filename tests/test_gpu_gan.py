@@ -302,3 +302,91 @@ def test_gan_step_matches_oracle(small):
         assert rel(sd[k], pd[k].detach()) < 1e-5, k
     for k in [k for k in pd if k.endswith("weight_u") or k.endswith("weight_v")]:
         assert rel(sd[k], pd[k]) < 1e-5, k
+
+
+# ------------------------------------------------------------- C5 shape: 8 s, T=1001
+def test_generator_and_discriminator_t1001_match_reference(golden_dir):
+    """Default PConvUNet / Discriminator at [1,1,257,1001] (gan_t1001.npz from
+    the reference's networks.py): W pads 1001 -> 1024 (networks.py:255-261),
+    output crop, BN running statistics after the train-mode forward, D logits
+    [1,1,30,123] and the spectral-norm u/v after that forward."""
+    from ainp import gan as G
+    g = np.load(os.path.join(golden_dir, "gan_t1001.npz"), allow_pickle=False)
+    torch.manual_seed(0)
+    m = G.PConvUNet().cuda().train()
+    y = m(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["mask"]).cuda())
+    assert tuple(y.shape) == tuple(int(v) for v in g["y_shape"])
+    yf = y.cpu().numpy().reshape(-1)
+    assert rel(yf[::97], g["y_sample"]) < TOL
+    assert abs(np.linalg.norm(yf.astype(np.float64)) - g["y_norm"][0]) < TOL * g["y_norm"][0]
+    sd = m.state_dict()
+    for k in g.files:
+        if k.startswith("g_after/"):
+            assert rel(sd[k[len("g_after/"):]], g[k]) < TOL, k
+    torch.manual_seed(1)
+    D = G.Discriminator().cuda().train()
+    with torch.no_grad():
+        logits = D(torch.from_numpy(g["x"]).cuda())
+    assert tuple(logits.shape) == tuple(g["d_logits"].shape) == (1, 1, 30, 123)
+    assert rel(logits, g["d_logits"]) < TOL
+    sd = D.state_dict()
+    for k in g.files:
+        if k.startswith("d_after/"):
+            assert rel(sd[k[len("d_after/"):]], g[k]) < 1e-5, k
+
+
+# ------------------------------------------------------------- full-size GAN step
+@pytest.mark.timeout(600)
+def test_full_size_gan_step_matches_reference(golden_dir):
+    """One full-size GAN step (train.py:341-378) at B=2, T=626 on the GAN data
+    path (gan_step_full.npz from the reference's networks.py): generated
+    spectrogram, D logits and losses, every D gradient (norms and samples),
+    D parameters and u/v after Adam and after the G-step forward, G's
+    BatchNorm running statistics; the G-step losses (incl. VGG19 with seeded
+    weights, oracle/gan_ref.vgg19_init(0): pretrained weights parity-unpinned)
+    vs the oracle values stored with the fixture."""
+    from ainp import gan as G
+    from ainp.gan_train import GanTrainer
+    from golden.gen_golden_r02 import GSTEP, checksum, gan_step_inputs
+    g = np.load(os.path.join(golden_dir, "gan_step_full.npz"), allow_pickle=False)
+    orig, imp, mask = gan_step_inputs()
+    for a, k in ((orig, "orig_check"), (imp, "imp_check"), (mask, "mask_check")):
+        assert np.allclose(checksum(a), g[k], rtol=1e-12, atol=0), k
+    torch.manual_seed(GSTEP["g_seed"])
+    Gm = G.PConvUNet()
+    torch.manual_seed(GSTEP["d_seed"])
+    Dm = G.Discriminator()
+    v, _ = _vgg_pair(GSTEP["vgg_seed"])
+    cfg = {"training": dict(R.LAMBDAS, g_lr=2e-4, d_lr=2e-4, b1=0.5, b2=0.999)}
+    tr = GanTrainer(cfg, Gm.cuda(), Dm.cuda(), vgg=v)
+    out = tr.step(torch.from_numpy(orig).cuda(), torch.from_numpy(imp).cuda(),
+                  torch.from_numpy(mask).cuda())
+    gf = out["generated"].cpu().numpy().reshape(-1)
+    assert rel(gf[::97], g["gen_sample"]) < TOL
+    assert abs(np.linalg.norm(gf.astype(np.float64)) - g["gen_norm"][0]) < TOL * g["gen_norm"][0]
+    dl, lr_, lf = g["d_losses"]
+    for k, r in (("d_loss", dl), ("d_real", lr_), ("d_fake", lf)):
+        assert abs(float(out[k]) - r) <= TOL * abs(r), k
+    for k, p in Dm.named_parameters():
+        gr = p.grad.detach().cpu().numpy()
+        gn = np.linalg.norm(gr.astype(np.float64))
+        assert abs(gn - g["d_gnorm/" + k][0]) <= TOL * g["d_gnorm/" + k][0], (k, gn)
+        s = gr.reshape(-1)[::max(1, gr.size // 4096)]
+        assert rel(s, g["d_gsample/" + k]) < TOL, k
+    sd = Gm.state_dict()
+    for k in g.files:
+        if k.startswith("g_after/"):
+            assert rel(sd[k[len("g_after/"):]], g[k]) < TOL, k
+    sd = Dm.state_dict()
+    for k in g.files:
+        if k.startswith("d_after_g/"):
+            # u/v after the third power iteration, on the Adam-updated weights
+            assert rel(sd[k[len("d_after_g/"):]], g[k]) < TOL, k
+        elif k.startswith("d_after/") and "weight_u" not in k and "weight_v" not in k:
+            t = sd[k[len("d_after/"):]].cpu().numpy()
+            s = t.reshape(-1)[::max(1, t.size // 4096)]
+            assert rel(s, g[k]) < 1e-5, k
+    for k in ("g_total", "g_adv", "g_l1_valid", "g_l1_hole", "g_mag_weighted",
+              "g_vgg_perceptual", "g_vgg_style"):
+        r = float(g["oracle_loss/" + k][0])
+        assert abs(float(out[k]) - r) <= TOL * max(abs(r), 1e-6), (k, float(out[k]), r)

@@ -120,3 +120,146 @@ def test_eval_mode_and_reconstruct(golden_dir):
         yr = ref.decoder(z).squeeze(1)
         yr = yr * m + x * (1 - m)
     assert rel(y, yr) < TOL
+
+
+# --------------------------------------------------------------- headline shapes
+def _c2():
+    from golden.gen_golden_r02 import c2_config, c2_inputs
+    return c2_config(), c2_inputs()
+
+
+@pytest.mark.timeout(600)
+def test_c2_batch32_forward_backward_adam_match_reference(golden_dir):
+    """The bench's exact C2 batch (N=32, T=334, H=128; cnnblstm_c2.npz from the
+    reference's model.py): forward output and loss vs the reference's fp32
+    result (rel 1e-4); every gradient vs the fp64 oracle on the kernels' ReLU
+    branch (rel 1e-4; BN-fed conv biases absolutely) and vs the
+    reference's gradient norms (5e-3, the ReLU-branch effect); parameters after
+    one Adam step vs the reference's (rel 1e-4 on the stored samples)."""
+    from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
+    from ainp.optim import Adam
+    from ainp.smoke import BN_FED_BIASES
+    from golden.gen_golden_r02 import checksum
+    from oracle import cnnblstm_ref as R
+    from relu_branch import recording
+    g = np.load(os.path.join(golden_dir, "cnnblstm_c2.npz"), allow_pickle=False)
+    cfg, (x, m, t, starts) = _c2()
+    np.testing.assert_array_equal(starts, g["starts"])
+    for a, k in ((x, "x_check"), (m, "mask_check"), (t, "target_check")):
+        assert np.allclose(checksum(a), g[k], rtol=1e-12, atol=0), k
+    H, L = cfg["model"]["lstm_hidden_dim"], cfg["model"]["num_lstm_layers"]
+    torch.manual_seed(0)
+    model = StackedBLSTMCNN(config=cfg)
+    for k, v in model.state_dict().items():
+        assert np.allclose(checksum(v.numpy()), g["check/" + k], rtol=1e-9, atol=1e-12), k
+    model = model.cuda().train()
+    opt = Adam(model.parameters(), lr=1e-4)
+    X, M, Tg = torch.from_numpy(x).cuda(), torch.from_numpy(m).cuda(), torch.from_numpy(t).cuda()
+    opt.zero_grad()
+    with recording(model) as masks:
+        y = model(X.unsqueeze(1))
+    loss = l1_pow10_loss(y, M, Tg)
+    loss.backward()
+    yf = y.detach().cpu().numpy().reshape(-1)
+    assert rel(yf[::97], g["y_sample"]) < TOL
+    assert abs(np.linalg.norm(yf.astype(np.float64)) - g["y_norm"][0]) < TOL * g["y_norm"][0]
+    assert abs(loss.item() - g["loss"][0]) / g["loss"][0] < TOL
+    grads = {k: p.grad.detach().cpu().double() for k, p in model.named_parameters()}
+    for k, gr in grads.items():
+        if k in BN_FED_BIASES:       # exact gradient 0: both norms are rounding noise
+            continue
+        gn = float(gr.norm())
+        assert abs(gn - g["gnorm/" + k][0]) <= 5e-3 * g["gnorm/" + k][0] + 1e-6, (k, gn)
+    # fp64 oracle on the kernels' ReLU branch
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    p = {k: (v.double() if v.is_floating_point() else v) for k, v in R.init_params(cfg, 0).items()}
+    keys = R.trainable_keys(p)
+    for k in keys:
+        p[k].requires_grad_(True)
+    y64 = R.forward(p, torch.from_numpy(x).double().unsqueeze(1), H, L, relu_masks=masks)
+    R.loss_fn(y64, torch.from_numpy(m).double(), torch.from_numpy(t).to(torch.complex128)).backward()
+    assert rel(yf, y64.detach().numpy().reshape(-1)) < TOL
+    for k in keys:
+        a, b = grads[k], p[k].grad
+        if k in BN_FED_BIASES:
+            wk = k.replace("bias", "weight")
+            assert a.abs().max() <= 1e-4 * float(p[wk].grad.norm()), k
+            continue
+        assert rel(a.numpy(), b.numpy()) < TOL, (k, rel(a.numpy(), b.numpy()))
+    del p, y64
+    opt.step()
+    for k, v in model.state_dict().items():
+        ref = g["after/" + k]
+        v = v.detach().cpu().numpy()
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == int(ref)
+            continue
+        s = v.reshape(-1)[::max(1, v.size // 4096)]
+        if k in BN_FED_BIASES:
+            # Adam moves a zero-gradient parameter by +-lr on its noise sign
+            assert np.abs(s - ref).max() <= 2e-4 + 1e-7, k
+        elif k.endswith("running_mean"):
+            # holds 0.1 x the batch mean, which the BN-fed bias shifts 1:1
+            assert np.abs(s - ref).max() <= 1e-5 + TOL * np.abs(ref).max(), k
+        else:
+            assert rel(s, ref) < TOL, (k, rel(s, ref))
+
+
+def run_curve(g, steps=None, device="cuda", dtype=None):
+    """The cnnblstm_curve.npz schedule: Adam(1e-4) over batches cycling 0..3."""
+    from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
+    from ainp.optim import Adam
+    from ainp.smoke import small_config
+    cfgv = g["config"]
+    cfg = small_config(cfgv[:7])
+    if dtype is not None:
+        cfg["accel"] = {"dtype": dtype}
+    steps = int(cfgv[7]) if steps is None else steps
+    model = StackedBLSTMCNN(config=cfg).to(device)
+    sd = {k[len("init/"):]: torch.from_numpy(np.array(g[k])) for k in g.files
+          if k.startswith("init/")}
+    model.load_state_dict(sd)
+    model.train()
+    opt = Adam(model.parameters(), lr=1e-4)
+    data = [tuple(torch.from_numpy(g[f"{n}{b}"]).to(device) for n in ("x", "mask", "target"))
+            for b in range(4)]
+    losses = []
+    for s in range(steps):
+        x, m, t = data[s % 4]
+        opt.zero_grad()
+        loss = l1_pow10_loss(model(x.unsqueeze(1)), m, t)
+        loss.backward()
+        opt.step()
+        losses.append(float(loss.item()))
+    return np.array(losses), model
+
+
+CURVE_TOL = 1e-4
+
+
+def test_loss_curve_30_steps_matches_reference(golden_dir):
+    """30 reference training steps (train.py:96-108, cnnblstm_curve.npz): the
+    fp32 HIP loss curve matches the reference's step by step within 1e-4
+    relative; final parameters within 1e-4 (BN-fed conv biases: Adam moves
+    their zero gradient's rounding noise by <= lr per step)."""
+    from ainp.smoke import BN_FED_BIASES
+    g = np.load(os.path.join(golden_dir, "cnnblstm_curve.npz"), allow_pickle=False)
+    losses, model = run_curve(g)
+    ref = g["losses"]
+    err = np.abs(losses - ref) / np.abs(ref)
+    print("curve rel err max", err.max())
+    assert err.max() < CURVE_TOL, err
+    steps = len(ref)
+    for k, v in model.state_dict().items():
+        v = v.detach().cpu().numpy()
+        r = g["final/" + k]
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == int(r)
+        elif k in BN_FED_BIASES:
+            assert np.abs(v - r).max() <= 2 * 1e-4 * steps, k
+        elif k.endswith("running_mean"):
+            # an EMA of batch means that the BN-fed bias shifts 1:1: bounded by
+            # the bias drift 2 * lr * steps
+            assert np.abs(v - r).max() <= 2 * 1e-4 * steps + 1e-4 * np.abs(r).max(), k
+        else:
+            assert rel(v, r) < 1e-3, (k, rel(v, r))
