@@ -163,6 +163,9 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--workload", choices=("cnnblstm", "gan"), default="cnnblstm",
                     help="cnnblstm = BASELINE configs[1] (the headline metric); gan = configs[3]")
+    ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
+                    help="fp32 = C2 (headline); bf16 = the C3 per-GPU shape (bf16 GEMM/conv "
+                         "operands, fp32 accumulate / cell state / BN statistics / weights)")
     args = ap.parse_args()
     if args.workload == "gan":
         return run_gan(args)
@@ -186,8 +189,10 @@ def main():
     T = -(-S // hop)                                   # ceil(sr*max_len/hop) = 334
     g = int(CFG["data"]["gap_len_s"] * sr)             # 3200
 
+    bf16 = args.dtype == "bf16"
+    cfg = dict(CFG, accel={"dtype": args.dtype})
     torch.manual_seed(0)
-    model = StackedBLSTMCNN(config=CFG).to(dev).train()
+    model = StackedBLSTMCNN(config=cfg).to(dev).train()
     model.comm = comm
     opt = Adam(model.parameters(), lr=CFG["training"]["starter_learning_rate"])
     reducer = GradAllReducer(model.parameters(), comm) if comm is not None else None
@@ -249,16 +254,21 @@ def main():
                   [zx, zx[:, 4 * H:]], 8 * H, 1)
         kw = dict(bias1=[lw.bias_ih_l0, lw.bias_ih_l0_reverse],
                   bias2=[lw.bias_hh_l0, lw.bias_hh_l0_reverse])
+        kw["bf16"] = bf16
         avg_s = time_kernel(lambda: ops.gemm(*args_g, **kw), args.roofline_reps, dev)
         flops = 2.0 * M * (8 * H) * I
         achieved = flops / avg_s / 1e12
-        traffic = _traffic("traffic_gemm_l0.json")
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": traffic, "kernel": "gemm_f32_kernel (LSTM l0 input projection, "
-                f"M={M} N={8 * H} K={I}, both directions)", "avg_launch_ms": round(avg_s * 1e3, 4),
-                "flop_per_launch": flops}
-        if not ops.GEMM_EXACT:
+        peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+        traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else "traffic_gemm_l0.json")
+        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
+                "traffic": traffic, "kernel": f"gemm_f32_kernel<{2 if bf16 else 1},...> (LSTM l0 "
+                f"input projection, M={M} N={8 * H} K={I}, both directions)",
+                "avg_launch_ms": round(avg_s * 1e3, 4), "flop_per_launch": flops}
+        if bf16:
+            roof["main_loop"] = ("fp32 operands rounded to bf16 at LDS staging, "
+                                 "v_mfma_f32_32x32x16_bf16, f32 accumulate")
+        elif not ops.GEMM_EXACT:
             # fp32-accurate three-piece bf16 split: 6 bf16 MFMA products per fp32
             # product; its own instruction-stream ceiling is the dense bf16 peak / 6
             roof.update({
@@ -291,9 +301,13 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "frames/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "fp32", "data": "synthetic (4 s/16 kHz harmonic clips, seeded; random init)",
-            "config": {"workload": "C2: CNNBLSTM train step (STFT features+fwd+bwd+Adam), "
-                                   "fp32, 32 examples/GPU, F=257, T=334, H=128, 3-layer BLSTM",
+            "dtype": args.dtype,
+            "data": "synthetic (4 s/16 kHz harmonic clips, seeded; random init)",
+            "config": {"workload": ("C3 per-GPU shape: CNNBLSTM train step (STFT features+fwd+"
+                                    "bwd+Adam), bf16 GEMM/conv operands with fp32 accumulate, "
+                                    "32 examples/GPU" if bf16 else
+                                    "C2: CNNBLSTM train step (STFT features+fwd+bwd+Adam), "
+                                    "fp32, 32 examples/GPU") + ", F=257, T=334, H=128, 3-layer BLSTM",
                        "global_batch": B * world, "seq_len": T, "freq_bins": n_fft // 2 + 1,
                        "parallelism": f"dp{world}" + ("+syncbn" if world > 1 else "")},
             "ms_per_step_median": round(med_ms, 3),
@@ -304,7 +318,7 @@ def main():
             "train_loss_last": train_loss,
             "step_tflops": round(step_flops / (ms_step / 1e3) / 1e12, 2),
             "mfma_util_step": round(step_flops / world / (ms_step / 1e3) / 1e12
-                                    / FP32_MFMA_PEAK_TFLOPS, 4),
+                                    / (BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS), 4),
             "roofline": roof,
             "roofline_stft": roof_stft,
             "cpu_baseline": cpu,

@@ -165,8 +165,12 @@ int ainp_gemm_f32_ws(int64_t M, int64_t N, int64_t K, float alpha,
  * pieces and the six cross products of order >= 2^-16 are accumulated in f32
  * on the bf16 MFMA (dropped terms <= ~2^-23 |a||b| per product, the level of
  * f32 rounding); flags == AINP_GEMM_EXACT_F32: exact f32 MFMA (k-ordered fmaf
- * chain). */
+ * chain); flags == AINP_GEMM_BF16: every operand element rounded to bf16
+ * (nearest-even), f32 accumulation -- the bf16 configurations (BASELINE
+ * configs C3-C5, torch autocast(bfloat16) arithmetic for nn.LSTM / nn.Linear,
+ * models/CNNBLSTM/model.py:46-50). */
 #define AINP_GEMM_EXACT_F32 1
+#define AINP_GEMM_BF16 2
 int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
                      const float* const* A, int64_t sam, int64_t sak,
                      int64_t strideA, const float* const* B, int64_t sbk,
@@ -211,6 +215,25 @@ int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
                        const float* in_shift, const float* dy, float* dw,
                        float* dbias, void* workspace, int64_t N, int Cin,
                        int Cout, int64_t H, int64_t W, void* stream);
+/* The three entry points above with a precision flag (the plain ones pass 0:
+ * fp32-accurate split-bf16 MFMA, or exact f32 for the 1- and 16-channel
+ * pairs).  AINP_CONV_BF16: the 16/32/64-channel pairs round every activation /
+ * weight / gradient operand to bf16 (nearest-even) and accumulate in f32 --
+ * the bf16 configurations C3-C5 (torch autocast(bfloat16) nn.Conv2d of
+ * models/CNNBLSTM/model.py:35-60); BatchNorm statistics, biases and outputs
+ * stay fp32.  The 1 <-> 16 channel convs stay fp32 (HBM-bound). */
+#define AINP_CONV_BF16 2
+int ainp_conv3x3_fwd_ex(const float* x, const float* w, const float* bias,
+                        const float* in_scale, const float* in_shift, float* y,
+                        double* stats, int64_t N, int Cin, int Cout, int64_t H,
+                        int64_t W, int flags, void* stream);
+int ainp_conv3x3_dgrad_ex(const float* dy, const float* w, float* dx,
+                          float* workspace, int64_t N, int Cin, int Cout,
+                          int64_t H, int64_t W, int flags, void* stream);
+int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
+                          const float* in_shift, const float* dy, float* dw,
+                          float* dbias, void* workspace, int64_t N, int Cin,
+                          int Cout, int64_t H, int64_t W, int flags, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* BatchNorm2d (training statistics) + ReLU                                   */

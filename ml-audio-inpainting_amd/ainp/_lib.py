@@ -58,6 +58,12 @@ _SIGS = {
     "ainp_conv3x3_wgrad_workspace": (c_size_t, [c_int64, c_int, c_int, c_int64, c_int64]),
     "ainp_conv3x3_wgrad": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
                                    c_int64, P]),
+    "ainp_conv3x3_fwd_ex": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
+                                    c_int64, c_int, P]),
+    "ainp_conv3x3_dgrad_ex": (c_int, [P, P, P, P, c_int64, c_int, c_int, c_int64, c_int64, c_int,
+                                      P]),
+    "ainp_conv3x3_wgrad_ex": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
+                                      c_int64, c_int, P]),
     "ainp_bn_stats_reduce": (c_int, [P, c_int, P, c_int, P]),
     "ainp_bn_finalize": (c_int, [P, c_int64, P, P, P, P, c_float, c_float, P, P, P, c_int, P]),
     "ainp_bn_eval_affine": (c_int, [P, P, P, P, c_float, P, P, c_int, P]),

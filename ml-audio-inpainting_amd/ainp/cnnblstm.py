@@ -52,7 +52,7 @@ class _ConvStackFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, spec, training, out_ntcf, comm, *params):
+    def forward(ctx, x, spec, training, out_ntcf, comm, bf16, *params):
         N, _, H, W = x.shape
         saved_y = []
         affine = []          # per BN block: (scale, shift, save or None)
@@ -64,7 +64,7 @@ class _ConvStackFn(torch.autograd.Function):
             w, b = params[pi], params[pi + 1]
             pi += 2
             want_stats = has_bn and training
-            y, stats = ops.conv3x3_fwd(h, w, b, act[0], act[1], want_stats=want_stats)
+            y, stats = ops.conv3x3_fwd(h, w, b, act[0], act[1], want_stats=want_stats, bf16=bf16)
             saved_y.append(y)
             if has_bn:
                 gamma, beta = params[pi], params[pi + 1]
@@ -93,6 +93,7 @@ class _ConvStackFn(torch.autograd.Function):
         else:
             out = saved_y[-1]
         ctx.spec = spec
+        ctx.bf16 = bf16
         ctx.out_ntcf = out_ntcf
         ctx.comm = comm
         ctx.count = count
@@ -137,13 +138,13 @@ class _ConvStackFn(torch.autograd.Function):
             else:
                 xin = x
                 pro = (None, None)
-            dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1])
+            dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
             grads[p0], grads[p0 + 1] = dw, db
             if bi > 0 or ctx.needs_input_grad[0]:
-                g = ops.conv3x3_dgrad(gy, w)
+                g = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16)
                 if bi == 0:
                     gx = g
-        return (gx, None, None, None, None, *grads)
+        return (gx, None, None, None, None, None, *grads)
 
 
 # ------------------------------------------------------------------ BLSTM
@@ -153,7 +154,7 @@ class _BLSTMFn(torch.autograd.Function):
     (w_ih, w_hh, b_ih, b_hh, w_ih_rev, w_hh_rev, b_ih_rev, b_hh_rev)."""
 
     @staticmethod
-    def forward(ctx, x, H, L, *params):
+    def forward(ctx, x, H, L, bf16, *params):
         N, T, I = x.shape
         NT = N * T
         inp = x.reshape(NT, I)
@@ -164,17 +165,18 @@ class _BLSTMFn(torch.autograd.Function):
             Il = inp.shape[1]
             zx = torch.empty(N, T, 8 * H, device=x.device, dtype=torch.float32)
             ops.gemm(NT, 4 * H, Il, [inp, inp], Il, 1, [wf, wr], 1, Il,
-                     [zx, zx[:, :, 4 * H:]], 8 * H, 1, bias1=[bif, bir], bias2=[bhf, bhr])
+                     [zx, zx[:, :, 4 * H:]], 8 * H, 1, bias1=[bif, bir], bias2=[bhf, bhr],
+                     bf16=bf16)
             h, gates, cell = ops.lstm_rec_fwd(zx, hf, hr, H)
             saved += [inp, h, gates, cell]
             inp = h.view(NT, 2 * H)
-        ctx.H, ctx.L = H, L
+        ctx.H, ctx.L, ctx.bf16 = H, L, bf16
         ctx.save_for_backward(*saved, *params)
         return h
 
     @staticmethod
     def backward(ctx, dh):
-        H, L = ctx.H, ctx.L
+        H, L, bf16 = ctx.H, ctx.L, ctx.bf16
         st = ctx.saved_tensors
         saved, params = st[:4 * L], st[4 * L:]
         dh = dh.contiguous()
@@ -200,8 +202,10 @@ class _BLSTMFn(torch.autograd.Function):
             with torch.cuda.stream(side):
                 # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
                 # for the recurrent / upper layers -> parallel split-K over row chunks
-                gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H))
-                gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il, offsets_b=(0, 0))
+                gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H),
+                                         bf16=bf16)
+                gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il, offsets_b=(0, 0),
+                                         bf16=bf16)
                 db_ih = ops.colsum(dg2)           # b_ih and b_hh get the same gradient
                 db_hh = db_ih.clone()
             for t in (dg, hp, inp):
@@ -219,13 +223,13 @@ class _BLSTMFn(torch.autograd.Function):
                 if Il >= 1024:
                     dxi = torch.empty(NT, Il, device=dh.device)
                     ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,
-                             [dxi, dxi], Il, 1, ksplit=True)
+                             [dxi, dxi], Il, 1, ksplit=True, bf16=bf16)
                 else:
                     hk = 2 * H                      # half of a direction's 4H gate columns
                     sl = torch.empty(4, NT, Il, device=dh.device)
                     ops.gemm(NT, Il, hk, [dg2[:, q * hk:] for q in range(4)], 8 * H, 1,
                              [(wf if q < 2 else wr)[(q % 2) * hk:] for q in range(4)], Il, 1,
-                             [sl[q] for q in range(4)], Il, 1)
+                             [sl[q] for q in range(4)], Il, 1, bf16=bf16)
                     dxi = ops.sum_slabs(sl, 4).view(NT, Il)
                 dh = dxi.view(N, T, Il)
                 dx = dh
@@ -234,7 +238,7 @@ class _BLSTMFn(torch.autograd.Function):
         main.wait_event(done)
         for gr in grads:
             gr.record_stream(main)        # side-stream memory handed to autograd
-        return (dx, None, None, *grads)
+        return (dx, None, None, None, *grads)
 
 
 _SIDE_STREAMS: dict = {}
@@ -253,15 +257,16 @@ class _ProjFn(torch.autograd.Function):
     """nn.Linear(2H, C*F) + view(N,T,C,F).permute(0,2,3,1) -> [N, C, F, T]."""
 
     @staticmethod
-    def forward(ctx, h, w, b, C, F):
+    def forward(ctx, h, w, b, C, F, bf16=False):
         N, T, K = h.shape
         out = torch.empty(N, C, F, T, device=h.device, dtype=torch.float32)
         NO = C * F
         # per example n: out_n[t][col] = h_n[t] . w[col] + b[col], stored col*T + t
         ops.gemm(T, NO, K, [h], K, 1, [w], 1, K, [out], 1, T, strideA=T * K,
-                 strideC=NO * T, nstrided=N, bias1=[b])
+                 strideC=NO * T, nstrided=N, bias1=[b], bf16=bf16)
         ctx.save_for_backward(h, w)
         ctx.shape = (N, C, F, T)
+        ctx.bf16 = bf16
         return out
 
     @staticmethod
@@ -280,7 +285,7 @@ class _ProjFn(torch.autograd.Function):
         gflat = g.view(-1)
         ops.gemm(T, K, kc, [gflat[s * kc * T:] for s in range(S)], 1, T,
                  [w[s * kc:] for s in range(S)], K, 1, [hs[s] for s in range(S)], K, 1,
-                 strideA=NO * T, strideC=T * K, nstrided=N)
+                 strideA=NO * T, strideC=T * K, nstrided=N, bf16=ctx.bf16)
         dh = hs[0] if S == 1 else ops.sum_slabs(hs, S).view(N, T, K)
         # dw[col][k] = sum_{n,t} g_n[col][t] h_n[t][k]: split the example sum
         # over S pointer batches (S partial slabs, ksplit mode 2) so the small
@@ -290,11 +295,11 @@ class _ProjFn(torch.autograd.Function):
         slabs = torch.empty(S, NO, K, device=h.device, dtype=torch.float32)
         ops.gemm(NO, K, T, [g[i * per] for i in range(S)], T, 1,
                  [h[i * per] for i in range(S)], K, 1, [slabs[i] for i in range(S)], K, 1,
-                 strideA=NO * T, strideB=T * K, nstrided=per, ksplit=2)
+                 strideA=NO * T, strideB=T * K, nstrided=per, ksplit=2, bf16=ctx.bf16)
         dw = ops.sum_slabs(slabs, S).view(NO, K)
         # db[col] = sum_{n,t} g_n[col][t]
         db = ops.rowsum_batched(g.view(N, NO, T))
-        return dh, dw, db, None, None
+        return dh, dw, db, None, None, None
 
 
 def _split_count(n):
@@ -346,6 +351,13 @@ class StackedBLSTMCNN(nn.Module):
         self.using_phase = self.in_channels == 2
         self.enc_filters = mdl_cfg["enc_filters"]
         self.dec_filters = mdl_cfg["dec_filters"]
+        # optional accel block (not in the reference YAML): compute precision of
+        # the GEMMs / 16-64 channel convs; "bf16" = bf16 operands, fp32 accumulate,
+        # fp32 LSTM cell state, BatchNorm statistics and master weights (C3)
+        dtype = (full_cfg.get("accel") or {}).get("dtype", "fp32")
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError(f"accel.dtype must be fp32 or bf16, got {dtype!r}")
+        self.bf16 = dtype == "bf16"
         # identical construction order to model.py:34-61 (same init RNG draws)
         self.encoder = nn.Sequential(
             nn.Conv2d(self.in_channels, self.enc_filters[0], kernel_size=3, padding=1),
@@ -400,12 +412,13 @@ class StackedBLSTMCNN(nn.Module):
         batch_size, _, freq_bins, timeframes = x.shape
         x = x.contiguous()
         spec, params = self._stack(self.encoder)
-        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, *params)
-        z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, *self.lstm._flat_weights)
+        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, *params)
+        z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, self.bf16, *self.lstm._flat_weights)
         # model.py:82 hard-codes 16 decoder channels
-        p = _ProjFn.apply(z, self.projection.weight, self.projection.bias, 16, freq_bins)
+        p = _ProjFn.apply(z, self.projection.weight, self.projection.bias, 16, freq_bins,
+                          self.bf16)
         spec, params = self._stack(self.decoder)
-        y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, *params)
+        y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, self.bf16, *params)
         return y.squeeze(1)
 
     def reconstruct_spectrogram(self, log_spectrogram_gap, gap_mask):

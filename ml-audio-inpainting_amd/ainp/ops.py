@@ -150,14 +150,17 @@ def stft(audio: torch.Tensor, n_fft: int = 2048, hop_length: int = 512,
 # AINP_GEMM_EXACT=1 environment variable selects the exact path process-wide.
 GEMM_EXACT = os.environ.get("AINP_GEMM_EXACT", "0") == "1"
 GEMM_EXACT_F32 = 1
+GEMM_BF16 = 2          # include/ainp.h AINP_GEMM_BF16
+CONV_BF16 = 2          # include/ainp.h AINP_CONV_BF16
 
 
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
          strideA=0, strideB=0, strideC=0, bias1=None, bias2=None, nstrided=1,
-         ksplit=False, stream_of=None, exact=None):
+         ksplit=False, stream_of=None, exact=None, bf16=False):
     """Raw strided/batched GEMM (ainp_gemm_f32_ex).  A, B, C, bias1, bias2 are
     lists (pointer batches) of cuda float32 tensors (views allowed) or None.
-    exact: None -> GEMM_EXACT; True -> exact f32 MFMA; False -> bf16x6 split."""
+    exact: None -> GEMM_EXACT; True -> exact f32 MFMA; False -> bf16x6 split.
+    bf16=True: bf16-rounded operands, f32 accumulation (the bf16 configs)."""
     A = list(A); B = list(B); C = list(C)
     nptr = len(A)
     assert len(B) == nptr and len(C) == nptr and 1 <= nptr <= 8
@@ -165,15 +168,15 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
     b1 = ptr_array([_p(t) for t in bias1]) if bias1 is not None else None
     b2 = ptr_array([_p(t) for t in bias2]) if bias2 is not None else None
     st = _stream(ref if stream_of is None else stream_of)
-    exact = GEMM_EXACT if exact is None else bool(exact)
+    exact = False if bf16 else (GEMM_EXACT if exact is None else bool(exact))
     ws, ws_bytes = (_gemm_workspace(ref.device, st, int(M), int(N), int(K), nptr,
                                     int(nstrided), int(ksplit)) if exact else (None, 0))
+    flags = GEMM_BF16 if bf16 else (GEMM_EXACT_F32 if exact else 0)
     call("ainp_gemm_f32_ex", int(M), int(N), int(K), float(alpha),
          ptr_array([t.data_ptr() for t in A]), int(sam), int(sak), int(strideA),
          ptr_array([t.data_ptr() for t in B]), int(sbk), int(sbn), int(strideB),
          float(beta), ptr_array([t.data_ptr() for t in C]), int(scm), int(scn),
-         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit),
-         GEMM_EXACT_F32 if exact else 0, ws, ws_bytes, st)
+         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit), flags, ws, ws_bytes, st)
 
 
 _GEMM_WS: dict = {}
@@ -203,7 +206,7 @@ def _chunks_for(K, tiles, target_blocks=512, min_rows=64):
     return 1
 
 
-def gemm_tn_splitk(a, lda, b, ldb, K, M, N, offsets_b=(0, 0)):
+def gemm_tn_splitk(a, lda, b, ldb, K, M, N, offsets_b=(0, 0), bf16=False):
     """Two-direction weight-gradient GEMM C[d] = A_d^T B_d for the BLSTM:
     A_d = a[:, d*M:(d+1)*M] ([K, M] row-major view, row stride lda),
     B_d = b[:, off_d:off_d+N] ([K, N], row stride ldb); returns [C_0, C_1]
@@ -215,7 +218,7 @@ def gemm_tn_splitk(a, lda, b, ldb, K, M, N, offsets_b=(0, 0)):
     slabs = torch.empty(2, S, M, N, device=a.device, dtype=torch.float32)
     gemm(M, N, kc, [a, a[:, M:]], 1, lda, [b[:, offsets_b[0]:], b[:, offsets_b[1]:]], ldb, 1,
          [slabs[0], slabs[1]], N, 1, strideA=kc * lda, strideB=kc * ldb, strideC=M * N,
-         nstrided=S)
+         nstrided=S, bf16=bf16)
     if S == 1:
         return [slabs[0, 0], slabs[1, 0]]
     return [sum_slabs(slabs[0], S).view(M, N), sum_slabs(slabs[1], S).view(M, N)]
@@ -254,7 +257,7 @@ def conv_stat_parts(N, H, W) -> int:
     return _lib.lib.ainp_conv3x3_fwd_stat_parts(N, H, W)
 
 
-def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False):
+def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf16=False):
     _req(x, "x"); _req(w, "w")
     N, Cin, H, W = x.shape
     Cout = w.shape[0]
@@ -264,22 +267,23 @@ def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False):
     if want_stats:
         stats = torch.empty(_lib.lib.ainp_conv3x3_fwd_stat_rows(N, Cin, Cout, H, W), 2 * Cout,
                             device=x.device, dtype=torch.float64)
-    call("ainp_conv3x3_fwd", x.data_ptr(), w.data_ptr(), _p(b), _p(in_scale),
-         _p(in_shift), y.data_ptr(), _p(stats), N, Cin, Cout, H, W, _stream(x))
+    call("ainp_conv3x3_fwd_ex", x.data_ptr(), w.data_ptr(), _p(b), _p(in_scale),
+         _p(in_shift), y.data_ptr(), _p(stats), N, Cin, Cout, H, W, CONV_BF16 if bf16 else 0,
+         _stream(x))
     return y, stats
 
 
-def conv3x3_dgrad(dy, w):
+def conv3x3_dgrad(dy, w, bf16=False):
     _req(dy, "dy"); _req(w, "w")
     N, Cout, H, W = dy.shape
     Cin = w.shape[1]
     dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=torch.float32)
-    call("ainp_conv3x3_dgrad", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), None,
-         N, Cin, Cout, H, W, _stream(dy))
+    call("ainp_conv3x3_dgrad_ex", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), None,
+         N, Cin, Cout, H, W, CONV_BF16 if bf16 else 0, _stream(dy))
     return dx
 
 
-def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True):
+def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False):
     _req(x, "x"); _req(dy, "dy")
     N, Cin, H, W = x.shape
     Cout = dy.shape[1]
@@ -287,8 +291,9 @@ def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True):
     db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
     ws_bytes = _lib.lib.ainp_conv3x3_wgrad_workspace(N, Cin, Cout, H, W)
     ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
-    call("ainp_conv3x3_wgrad", x.data_ptr(), _p(in_scale), _p(in_shift), dy.data_ptr(),
-         dw.data_ptr(), _p(db), ws.data_ptr(), N, Cin, Cout, H, W, _stream(x))
+    call("ainp_conv3x3_wgrad_ex", x.data_ptr(), _p(in_scale), _p(in_shift), dy.data_ptr(),
+         dw.data_ptr(), _p(db), ws.data_ptr(), N, Cin, Cout, H, W, CONV_BF16 if bf16 else 0,
+         _stream(x))
     return dw, db
 
 

@@ -912,10 +912,10 @@ int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W);
 int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s);
+                         int ci0, int cp, int grid, hipStream_t s, bool b16);
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts);
+                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16);
 
 // conv_x6.hip (fp32-accurate split-bf16 MFMA) serves every pair it has an
 // instantiation for unless AINP_CONV_EXACT=1 selects the exact f32 kernels.
@@ -954,7 +954,7 @@ template <bool DG>
 static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y,
                              double* stats, int64_t N, int Cin, int Cout,
-                             int64_t H, int64_t W, hipStream_t s) {
+                             int64_t H, int64_t W, hipStream_t s, bool b16) {
   // partials [used, rows) of the BatchNorm statistics are zero
   auto zero_tail = [&](int64_t used) -> int {
     if (!stats) return AINP_OK;
@@ -970,7 +970,8 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
   }
   if (!conv_exact_env()) {
     int64_t parts = 0;
-    const int rc = conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s, &parts);
+    const int rc =
+        conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s, &parts, b16);
     if (rc != 1) return rc ? rc : zero_tail(parts);
   }
   {
@@ -1001,33 +1002,53 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
   return check_launch("conv3x3_fwd_mfma");
 }
 
-extern "C" int ainp_conv3x3_fwd(const float* x, const float* w,
-                                const float* bias, const float* in_scale,
-                                const float* in_shift, float* y, double* stats,
-                                int64_t N, int Cin, int Cout, int64_t H,
-                                int64_t W, void* stream) {
+static bool conv_flags_ok(int flags) { return (flags & ~AINP_CONV_BF16) == 0; }
+
+extern "C" int ainp_conv3x3_fwd_ex(const float* x, const float* w,
+                                   const float* bias, const float* in_scale,
+                                   const float* in_shift, float* y, double* stats,
+                                   int64_t N, int Cin, int Cout, int64_t H,
+                                   int64_t W, int flags, void* stream) {
   if (!x || !w || !y || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
-      N > 65535 || H > (1 << 24) || W > (1 << 24))
+      N > 65535 || H > (1 << 24) || W > (1 << 24) || !conv_flags_ok(flags))
     return record_msg("ainp_conv3x3_fwd: bad argument");
   if ((in_scale == nullptr) != (in_shift == nullptr))
     return record_msg("ainp_conv3x3_fwd: in_scale/in_shift must both be set");
   if (N == 0) return AINP_OK;
   return conv_fwd_dispatch<false>(x, w, bias, in_scale, in_shift, y, stats, N,
-                                  Cin, Cout, H, W, as_stream(stream));
+                                  Cin, Cout, H, W, as_stream(stream),
+                                  (flags & AINP_CONV_BF16) != 0);
+}
+
+extern "C" int ainp_conv3x3_fwd(const float* x, const float* w,
+                                const float* bias, const float* in_scale,
+                                const float* in_shift, float* y, double* stats,
+                                int64_t N, int Cin, int Cout, int64_t H,
+                                int64_t W, void* stream) {
+  return ainp_conv3x3_fwd_ex(x, w, bias, in_scale, in_shift, y, stats, N, Cin, Cout, H, W, 0,
+                             stream);
+}
+
+extern "C" int ainp_conv3x3_dgrad_ex(const float* dy, const float* w, float* dx,
+                                     float* workspace, int64_t N, int Cin,
+                                     int Cout, int64_t H, int64_t W, int flags,
+                                     void* stream) {
+  (void)workspace;
+  if (!dy || !w || !dx || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
+      N > 65535 || !conv_flags_ok(flags))
+    return record_msg("ainp_conv3x3_dgrad: bad argument");
+  if (N == 0) return AINP_OK;
+  // conv over dy (Cout channels) producing Cin channels, flipped weights
+  return conv_fwd_dispatch<true>(dy, w, nullptr, nullptr, nullptr, dx, nullptr,
+                                 N, Cout, Cin, H, W, as_stream(stream),
+                                 (flags & AINP_CONV_BF16) != 0);
 }
 
 extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
                                   float* workspace, int64_t N, int Cin,
                                   int Cout, int64_t H, int64_t W,
                                   void* stream) {
-  (void)workspace;
-  if (!dy || !w || !dx || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
-      N > 65535)
-    return record_msg("ainp_conv3x3_dgrad: bad argument");
-  if (N == 0) return AINP_OK;
-  // conv over dy (Cout channels) producing Cin channels, flipped weights
-  return conv_fwd_dispatch<true>(dy, w, nullptr, nullptr, nullptr, dx, nullptr,
-                                 N, Cout, Cin, H, W, as_stream(stream));
+  return ainp_conv3x3_dgrad_ex(dy, w, dx, workspace, N, Cin, Cout, H, W, 0, stream);
 }
 
 extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
@@ -1044,9 +1065,19 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
                                   float* dw, float* dbias, void* workspace,
                                   int64_t N, int Cin, int Cout, int64_t H,
                                   int64_t W, void* stream) {
+  return ainp_conv3x3_wgrad_ex(x, in_scale, in_shift, dy, dw, dbias, workspace, N, Cin, Cout, H,
+                               W, 0, stream);
+}
+
+extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
+                                     const float* in_shift, const float* dy,
+                                     float* dw, float* dbias, void* workspace,
+                                     int64_t N, int Cin, int Cout, int64_t H,
+                                     int64_t W, int flags, void* stream) {
   if (!x || !dy || !dw || !workspace || N < 1 || Cin < 1 || Cout < 1 ||
-      H < 1 || W < 1)
+      H < 1 || W < 1 || !conv_flags_ok(flags))
     return record_msg("ainp_conv3x3_wgrad: bad argument");
+  const bool b16 = (flags & AINP_CONV_BF16) != 0;
   if ((in_scale == nullptr) != (in_shift == nullptr))
     return record_msg("ainp_conv3x3_wgrad: in_scale/in_shift must both be set");
   if (small_pair(Cin, Cout))
@@ -1084,7 +1115,7 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
     // AINP_CONV_EXACT=1; same slab format
     int rc = (fits && !conv_exact_env())
                  ? conv_wgrad_x6_launch(x, in_scale, in_shift, dy, partial, N, Cin, Cout, H, W,
-                                        ci0, cp, WG_BLOCKS, s)
+                                        ci0, cp, WG_BLOCKS, s, b16)
                  : 1;
     if (rc == 1) switch (key) {
       case 1616: AINP_WGT(16, 16); break;

@@ -81,13 +81,39 @@ __device__ __forceinline__ void cx6_split8(const float (&v)[8], uint4& p0, uint4
   p2 = make_uint4(q2[0], q2[1], q2[2], q2[3]);
 }
 
+// Stage 8 activation / weight values as NP bf16 planes `plane` bytes apart:
+// NP = 3 -- the exact split (fp32-accurate path); NP = 1 -- one bf16 rounding
+// (round-to-nearest-even: the bf16 configurations' operand precision).
+template <int NP>
+__device__ __forceinline__ void cx6_stage(const float (&v)[8], unsigned char* d, int plane) {
+  if (NP == 1) {
+    *reinterpret_cast<uint4*>(d) = make_uint4(cx6_cvt_pk(v[0], v[1]), cx6_cvt_pk(v[2], v[3]),
+                                              cx6_cvt_pk(v[4], v[5]), cx6_cvt_pk(v[6], v[7]));
+  } else {
+    uint4 p0, p1, p2;
+    cx6_split8(v, p0, p1, p2);
+    *reinterpret_cast<uint4*>(d) = p0;
+    *reinterpret_cast<uint4*>(d + plane) = p1;
+    *reinterpret_cast<uint4*>(d + 2 * plane) = p2;
+  }
+}
+// MFMA terms per product: the six cross terms of order >= 2^-16, smallest
+// first (plane of A, plane of B), or the single bf16 product
+__host__ __device__ constexpr int cx6_terms(int NP) { return NP == 3 ? 6 : 1; }
+__host__ __device__ constexpr int cx6_pa(int NP, int t) {
+  return NP == 1 ? 0 : (t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0);
+}
+__host__ __device__ constexpr int cx6_pb(int NP, int t) {
+  return NP == 1 ? 0 : (t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0);
+}
+
 __device__ __forceinline__ bf16x8c cx6_ld(const unsigned char* p) {
   return __builtin_bit_cast(bf16x8c, *reinterpret_cast<const uint4*>(p));
 }
 
 // RPW output rows per wave: 2 (16-row tiles, one workgroup per CU) or 1
 // (8-row tiles: half the halo LDS, two workgroups per CU).
-template <int CI, int COP, bool DGRAD, int RPW>
+template <int CI, int COP, bool DGRAD, int RPW, int NP>
 __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -105,8 +131,8 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
   constexpr int WPLANE = COP * WROW;
   constexpr int WU = COP * 18;                // weight staging units (co, tap, half)
   constexpr int WI = (WU + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPLANE];
-  __shared__ __attribute__((aligned(16))) unsigned char sw[3 * WPLANE];
+  __shared__ __attribute__((aligned(16))) unsigned char sx[NP * XPLANE];
+  __shared__ __attribute__((aligned(16))) unsigned char sw[NP * WPLANE];
   __shared__ double red[8 * 2 * COP];          // BatchNorm partials per wave
 
   const int n = blockIdx.z, r0 = blockIdx.y * TR, c0 = blockIdx.x * TC;
@@ -150,12 +176,7 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
           }
           v[c] = inb ? t : 0.f;
         }
-        uint4 p0, p1, p2;
-        cx6_split8(v, p0, p1, p2);
-        unsigned char* q = sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1));
-        *reinterpret_cast<uint4*>(q) = p0;
-        *reinterpret_cast<uint4*>(q + XPLANE) = p1;
-        *reinterpret_cast<uint4*>(q + 2 * XPLANE) = p2;
+        cx6_stage<NP>(v, sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1)), XPLANE);
       }
     }
     // weights: L2-resident gathers loaded here rather than prefetched (the
@@ -173,12 +194,7 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
                                      : w[((int64_t)co * CI + ci) * 9 + tap])
                             : 0.f;
         }
-        uint4 p0, p1, p2;
-        cx6_split8(pw, p0, p1, p2);
-        unsigned char* q = sw + co * WROW + tap * 32 + 16 * half;
-        *reinterpret_cast<uint4*>(q) = p0;
-        *reinterpret_cast<uint4*>(q + WPLANE) = p1;
-        *reinterpret_cast<uint4*>(q + 2 * WPLANE) = p2;
+        cx6_stage<NP>(pw, sw + co * WROW + tap * 32 + 16 * half, WPLANE);
       }
     }
   };
@@ -202,12 +218,12 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int dy = tap / 3, dx = tap % 3;
-      bf16x8c a[3][NI], b[3][RPW];
+      bf16x8c a[NP][NI], b[NP][RPW];
       const int hcol = li + dx;
       const unsigned char* xb = sx + (RPW * wave + dy) * XROW + hcol * 32 + 16 * (lh ^ ((hcol >> 3) & 1));
       const unsigned char* wb = sw + li * WROW + tap * 32 + 16 * lh;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NP; ++p) {
 #pragma unroll
         for (int i = 0; i < NI; ++i) a[p][i] = cx6_ld(wb + p * WPLANE + i * 32 * WROW);
 #pragma unroll
@@ -215,9 +231,8 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
       }
       // term-major over the NI x 2 accumulators: no back-to-back dependent MFMAs
 #pragma unroll
-      for (int t = 0; t < 6; ++t) {
-        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
-        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
+      for (int t = 0; t < cx6_terms(NP); ++t) {
+        const int pa = cx6_pa(NP, t), pb = cx6_pb(NP, t);
 #pragma unroll
         for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -288,7 +303,7 @@ int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W) {
 
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts);
+                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16);
 
 // Launch if (Cin, Cout) has an x6 instantiation; returns 1 if not handled.
 // *parts = the number of BatchNorm partials written.  The persistent kernel
@@ -313,31 +328,37 @@ int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, i
 
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts) {
+                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16) {
   if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W) == 0) return 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                   parts);
+                                   parts, b16);
     if (rc != 1) return rc;
   }
   if ((int64_t)Cin * H * W * 4 >= ((int64_t)1 << 31)) return 1;   // 32-bit buffer offsets
   *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
+#define AINP_X6N(CIV, COV, NPV)                                                                \
+  if (Cin == CIV && cop == COV) {                                                               \
+    if (dgrad && !stats) {   /* 8-row tiles, two workgroups per CU (no BN partials) */           \
+      const dim3 g8((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, 8), (unsigned)N);             \
+      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV>), g8, dim3(cx6::NT), 0, s,  \
+                         x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                   \
+    } else if (dgrad)                                                                           \
+      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 2, NPV>), grid, dim3(cx6::NT), 0, s, \
+                         x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                   \
+    else                                                                                        \
+      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, false, 2, NPV>), grid, dim3(cx6::NT), 0,  \
+                         s, x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                \
+    return check_launch("conv3x3_x6");                                                          \
+  }
 #define AINP_X6(CIV, COV)                                                                     \
-  if (Cin == CIV && cop == COV) {                                                             \
-    if (dgrad && !stats) {   /* 8-row tiles, two workgroups per CU (no BN partials) */         \
-      const dim3 g8((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, 8), (unsigned)N);           \
-      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1>), g8, dim3(cx6::NT), 0, s, x,  \
-                         w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                    \
-    } else if (dgrad)                                                                         \
-      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 2>), grid, dim3(cx6::NT), 0, s, x, \
-                         w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                    \
-    else                                                                                      \
-      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, false, 2>), grid, dim3(cx6::NT), 0, s, \
-                         x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                 \
-    return check_launch("conv3x3_x6");                                                        \
+  if (b16) {                                                                                  \
+    AINP_X6N(CIV, COV, 1)                                                                     \
+  } else {                                                                                    \
+    AINP_X6N(CIV, COV, 3)                                                                     \
   }
   // Only the pairs where this kernel beats the exact f32 kernels on the model's
   // shapes (r01_v9 op timings): the encoder's 32->64 conv (1.17 vs 1.21 ms) and
@@ -346,6 +367,7 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
   // leaves the staging latency exposed and the exact kernels are faster.
   AINP_X6(32, 64) AINP_X6(64, 32)
 #undef AINP_X6
+#undef AINP_X6N
   return 1;
 }
 
@@ -392,7 +414,7 @@ __device__ __forceinline__ int wx6_gswz(int px) {
   return (((px >> 1) & 1) << 2) | (((px >> 2) & 1) << 1) | (px & 1);
 }
 
-template <int CO>
+template <int CO, int NP>
 __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -406,8 +428,10 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
   constexpr int GPX = CO * 2;                  // dy image bytes per pixel
   constexpr int GPL = NPX * GPX;
   static_assert(CO == 64 && NT % NPX == 0, "dy staging map: units of one thread share a pixel");
-  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPL];
-  __shared__ __attribute__((aligned(16))) unsigned char sg[3 * GPL];
+  // sx doubles as the bias reduction buffer [CO][NPX] floats after the loop
+  constexpr int SXB = NP * XPL > CO * NPX * 4 ? NP * XPL : CO * NPX * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char sx[SXB];
+  __shared__ __attribute__((aligned(16))) unsigned char sg[NP * GPL];
   __shared__ __attribute__((aligned(16))) float s_ss[2 * CP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -501,13 +525,8 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
           if (in_scale) t = fmaxf(fmaf(t, s_ss[8 * grp + c], s_ss[CP + 8 * grp + c]), 0.f);
           v[c] = inb ? t : 0.f;
         }
-        uint4 p0, p1, p2;
-        cx6_split8(v, p0, p1, p2);
         const int sp = hr * HS + hc;
-        unsigned char* d = sx + sp * 64 + 16 * (grp ^ ((sp >> 1) & 3));
-        *reinterpret_cast<uint4*>(d) = p0;
-        *reinterpret_cast<uint4*>(d + XPL) = p1;
-        *reinterpret_cast<uint4*>(d + 2 * XPL) = p2;
+        cx6_stage<NP>(v, sx + sp * 64 + 16 * (grp ^ ((sp >> 1) & 3)), XPL);
       }
     }
     const bool pok = f0 + gpx / TT < H && t0 + gpx % TT < W;
@@ -520,12 +539,7 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
         v[c] = pok ? pg[i][c] : 0.f;
         bsum[i][c] += v[c];
       }
-      uint4 p0, p1, p2;
-      cx6_split8(v, p0, p1, p2);
-      unsigned char* d = sg + gpx * GPX + 16 * (grp ^ wx6_gswz(gpx));
-      *reinterpret_cast<uint4*>(d) = p0;
-      *reinterpret_cast<uint4*>(d + GPL) = p1;
-      *reinterpret_cast<uint4*>(d + 2 * GPL) = p2;
+      cx6_stage<NP>(v, sg + gpx * GPX + 16 * (grp ^ wx6_gswz(gpx)), GPL);
     }
   };
 
@@ -541,26 +555,24 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
       // this lane's 8-pixel segment: G = 2ks + lh -> tile row G/3, column 8(G%3)
       const int G0 = 2 * ks, G1 = 2 * ks + 1;
       const int seg = lh ? (G1 / 3) * HS + (G1 % 3) * 8 : (G0 / 3) * HS + (G0 % 3) * 8;
-      bf16x8c a[3];
+      bf16x8c a[NP];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
+      for (int p = 0; p < NP; ++p)
         a[p] = wx6_cat(wx6_tr(sg + p * GPL + ba[0] + ks * 16 * GPX),
                        wx6_tr(sg + p * GPL + ba[1] + ks * 16 * GPX));
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const int o0 = bx[dx][0] + seg * 64, o1 = bx[dx][1] + seg * 64;
-        bf16x8c b[3];
+        bf16x8c b[NP];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           b[p] = wx6_cat(wx6_tr(sx + p * XPL + o0), wx6_tr(sx + p * XPL + o1));
-        // six cross terms, smallest first
+        // six cross terms smallest first (NP = 3), or the bf16 product
         f32x16 c = acc[dx];
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], c, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < cx6_terms(NP); ++t)
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[cx6_pa(NP, t)], b[cx6_pb(NP, t)], c, 0,
+                                                      0, 0);
         acc[dx] = c;
       }
     }
@@ -615,7 +627,7 @@ __device__ __forceinline__ int wx6s_swz(int px) {
   return ((px >> 1) & 1) | ((((px >> 2) ^ (px >> 3)) & 1) << 1);
 }
 
-template <int CP, int CO>
+template <int CP, int CO, int NP>
 __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -626,8 +638,10 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
   constexpr int XG = CP / 8, XU = HR * HC * XG, XI = (XU + NT - 1) / NT;
   constexpr int GG = CO / 8, GU = NPX * GG;     // dy units (pixel, 8-co group)
   static_assert(GU <= NT, "one dy unit per thread");
-  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPL];
-  __shared__ __attribute__((aligned(16))) unsigned char sg[3 * GPL];
+  // sx doubles as the bias reduction buffer [CO][NPX] floats after the loop
+  constexpr int SXB = NP * XPL > CO * NPX * 4 ? NP * XPL : CO * NPX * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char sx[SXB];
+  __shared__ __attribute__((aligned(16))) unsigned char sg[NP * GPL];
   __shared__ __attribute__((aligned(16))) float s_ss[2 * CP];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -704,13 +718,8 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
           if (in_scale) t = fmaxf(fmaf(t, s_ss[8 * grp + c], s_ss[CP + 8 * grp + c]), 0.f);
           v[c] = inb ? t : 0.f;
         }
-        uint4 p0, p1, p2;
-        cx6_split8(v, p0, p1, p2);
         const int sp = hr * HS + hc;
-        unsigned char* d = sx + sp * 64 + 16 * (grp ^ wx6s_swz(sp));
-        *reinterpret_cast<uint4*>(d) = p0;
-        *reinterpret_cast<uint4*>(d + XPL) = p1;
-        *reinterpret_cast<uint4*>(d + 2 * XPL) = p2;
+        cx6_stage<NP>(v, sx + sp * 64 + 16 * (grp ^ wx6s_swz(sp)), XPL);
       }
     }
     if (tid < GU) {
@@ -721,12 +730,7 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
         v[c] = pok ? pg[c] : 0.f;
         bsum[c] += v[c];
       }
-      uint4 p0, p1, p2;
-      cx6_split8(v, p0, p1, p2);
-      unsigned char* d = sg + gpx * 64 + 16 * (ggrp ^ wx6s_swz(gpx));
-      *reinterpret_cast<uint4*>(d) = p0;
-      *reinterpret_cast<uint4*>(d + GPL) = p1;
-      *reinterpret_cast<uint4*>(d + 2 * GPL) = p2;
+      cx6_stage<NP>(v, sg + gpx * 64 + 16 * (ggrp ^ wx6s_swz(gpx)), GPL);
     }
   };
 
@@ -742,30 +746,28 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
       // this lane group's 8-pixel segment G = 4ks + g: tile row G/3, column 8(G%3)
       const int G = 4 * ks + g;
       const int srow = G / 3, scol = (G % 3) * 8;
-      bf16x8c a[3];
+      bf16x8c a[NP];
       {
         const int o0 = gaddr(8 * G + q), o1 = gaddr(8 * G + q + 4);
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           a[p] = wx6_cat(wx6_tr(sg + p * GPL + o0), wx6_tr(sg + p * GPL + o1));
       }
 #pragma unroll
       for (int dx = 0; dx < 3; ++dx) {
         const int hp = (srow + dyt) * HS + scol + dx + q;
         const int o0 = xaddr(hp), o1 = xaddr(hp + 4);
-        bf16x8c b[3];
+        bf16x8c b[NP];
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = 0; p < NP; ++p)
           b[p] = wx6_cat(wx6_tr(sx + p * XPL + o0), wx6_tr(sx + p * XPL + o1));
         // D[co][ci]: A = dy (rows co), B = act(x) (columns ci); six cross
-        // terms, smallest first
+        // terms smallest first (NP = 3), or the bf16 product
         f32x4 c = acc[dx];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], c, 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < cx6_terms(NP); ++t)
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[cx6_pa(NP, t)], b[cx6_pb(NP, t)], c, 0,
+                                                      0, 0);
         acc[dx] = c;
       }
     }
@@ -814,7 +816,7 @@ constexpr int XROW = HC * 32;            // halo row bytes per plane (16 bf16 pe
 constexpr int WROW = 9 * 32 + 16;        // weight row bytes per chunk and plane
 }  // namespace cxp
 
-template <int CI, int COP, bool DGRAD, int NT, int TR>
+template <int CI, int COP, bool DGRAD, int NT, int TR, int NP>
 __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -830,11 +832,12 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
   constexpr int NW = NT / 64, NIW = NI * TR / NW;
   constexpr int XI = (XU + NT - 1) / NT;
   static_assert(NIW >= 1 && NIW * NW == NI * TR, "waves");
-  constexpr int WPLANE = COP * WROW, WCH = 3 * WPLANE;
+  constexpr int WPLANE = COP * WROW, WCH = NP * WPLANE;
   constexpr int WU = NCH * COP * 18;       // weight units (chunk, co, tap, half)
   __shared__ __attribute__((aligned(16))) unsigned char sw[NCH * WCH];
-  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPLANE];
+  __shared__ __attribute__((aligned(16))) unsigned char sx[NP * XPLANE];
   __shared__ float s_ss[2 * CI];
+  static_assert(NP * XPLANE >= TR * 2 * COP * 8, "BatchNorm row sums reuse the halo image");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
@@ -851,12 +854,7 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
                                  : w[((int64_t)co * CI + ci) * 9 + tap])
                         : 0.f;
     }
-    uint4 p0, p1, p2;
-    cx6_split8(pw, p0, p1, p2);
-    unsigned char* d = sw + ch * WCH + co * WROW + tap * 32 + 16 * half;
-    *reinterpret_cast<uint4*>(d) = p0;
-    *reinterpret_cast<uint4*>(d + WPLANE) = p1;
-    *reinterpret_cast<uint4*>(d + 2 * WPLANE) = p2;
+    cx6_stage<NP>(pw, sw + ch * WCH + co * WROW + tap * 32 + 16 * half, WPLANE);
   }
   if (tid < 2 * CI)
     s_ss[tid] = in_scale ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
@@ -906,12 +904,7 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
           }
           v[c] = inb ? t : 0.f;
         }
-        uint4 p0, p1, p2;
-        cx6_split8(v, p0, p1, p2);
-        unsigned char* d = sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1));
-        *reinterpret_cast<uint4*>(d) = p0;
-        *reinterpret_cast<uint4*>(d + XPLANE) = p1;
-        *reinterpret_cast<uint4*>(d + 2 * XPLANE) = p2;
+        cx6_stage<NP>(v, sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1)), XPLANE);
       }
     }
   };
@@ -989,9 +982,9 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
       const int hcol = li + dx;
       const unsigned char* xb =
           sx + (wrow + dy) * XROW + hcol * 32 + 16 * (lh ^ ((hcol >> 3) & 1));
-      bf16x8c a[3][NIW], b[3];
+      bf16x8c a[NP][NIW], b[NP];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NP; ++p) {
 #pragma unroll
         for (int i = 0; i < NIW; ++i)
           a[p][i] = cx6_ld(wb0 + p * WPLANE + (wco + i) * 32 * WROW + tap * 32);
@@ -999,9 +992,8 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
       }
       // six cross terms smallest first, term-major over the NI accumulators
 #pragma unroll
-      for (int t = 0; t < 6; ++t) {
-        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
-        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
+      for (int t = 0; t < cx6_terms(NP); ++t) {
+        const int pa = cx6_pa(NP, t), pb = cx6_pb(NP, t);
 #pragma unroll
         for (int i = 0; i < NIW; ++i)
           acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[pa][i], b[pb], acc[i], 0, 0, 0);
@@ -1057,7 +1049,7 @@ constexpr int XPLANE = HR * cxp::XROW;
 constexpr int XU = 2 * HR * cxp::HC;
 }  // namespace cxq
 
-template <int CI, bool DGRAD>
+template <int CI, bool DGRAD, int NP>
 __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -1068,12 +1060,13 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
   using cxp::XROW;
   using namespace cxq;
   constexpr int NT = 512, CO = 16, NCH = CI / CK;
-  constexpr int WPLANE = CO * WROW, WCH = 3 * WPLANE;
+  constexpr int WPLANE = CO * WROW, WCH = NP * WPLANE;
   constexpr int WU = NCH * CO * 20;          // weight units (chunk, co, tap slot, half)
   constexpr int XI = (XU + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) unsigned char sw[NCH * WCH];
-  __shared__ __attribute__((aligned(16))) unsigned char sx[3 * XPLANE];
+  __shared__ __attribute__((aligned(16))) unsigned char sx[NP * XPLANE];
   __shared__ float s_ss[2 * CI];
+  static_assert(NP * XPLANE >= TR * 2 * CO * 8, "BatchNorm row sums reuse the halo image");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
@@ -1089,12 +1082,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
                                               : w[((int64_t)co * CI + ci) * 9 + tap])
                                      : 0.f;
     }
-    uint4 p0, p1, p2;
-    cx6_split8(pw, p0, p1, p2);
-    unsigned char* d = sw + ch * WCH + co * WROW + tap * 32 + 16 * half;
-    *reinterpret_cast<uint4*>(d) = p0;
-    *reinterpret_cast<uint4*>(d + WPLANE) = p1;
-    *reinterpret_cast<uint4*>(d + 2 * WPLANE) = p2;
+    cx6_stage<NP>(pw, sw + ch * WCH + co * WROW + tap * 32 + 16 * half, WPLANE);
   }
   if (tid < 2 * CI)
     s_ss[tid] = in_scale ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
@@ -1144,12 +1132,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
           }
           v[c] = inb ? t : 0.f;
         }
-        uint4 p0, p1, p2;
-        cx6_split8(v, p0, p1, p2);
-        unsigned char* d = sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1));
-        *reinterpret_cast<uint4*>(d) = p0;
-        *reinterpret_cast<uint4*>(d + XPLANE) = p1;
-        *reinterpret_cast<uint4*>(d + 2 * XPLANE) = p2;
+        cx6_stage<NP>(v, sx + row * XROW + col * 32 + 16 * (half ^ ((col >> 3) & 1)), XPLANE);
       }
     }
   };
@@ -1219,9 +1202,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
       const int tap = 2 * ks + (g >> 1);            // 9 = the zero slot
       const int tp = tap < 9 ? tap : 8;             // its (unused) pixel shift
       const int dy = tp / 3, dx = tp % 3;
-      bf16x8c a[3], b[3][2];
+      bf16x8c a[NP], b[NP][2];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NP; ++p) {
         a[p] = cx6_ld(wb0 + p * WPLANE + tap * 32);
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
@@ -1231,9 +1214,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
         }
       }
 #pragma unroll
-      for (int t = 0; t < 6; ++t) {
-        const int pa = t == 0 ? 2 : (t == 1 || t == 3) ? 1 : 0;
-        const int pb = t == 2 ? 2 : (t == 1 || t == 4) ? 1 : 0;
+      for (int t = 0; t < cx6_terms(NP); ++t) {
+        const int pa = cx6_pa(NP, t), pb = cx6_pb(NP, t);
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[pa], b[pb][j], acc[j], 0, 0, 0);
@@ -1272,25 +1254,34 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
 // has no instantiation.
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts) {
+                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16) {
   const int cop = Cout <= 32 ? 32 : 64;
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
-#define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                    \
-  if (dgrad == DG && Cin == CIV && cop == COV) {                                               \
-    hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV>), dim3(G), dim3(NTV), 0, s, \
-                       x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);            \
-    *parts = G;                                                                                \
-    return check_launch("conv3x3_x6p");                                                        \
+#define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                      \
+  if (dgrad == DG && Cin == CIV && cop == COV) {                                                 \
+    if (b16)                                                                                     \
+      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 1>), dim3(G), dim3(NTV), 0, \
+                         s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);         \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 3>), dim3(G), dim3(NTV), 0, \
+                         s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);         \
+    *parts = G;                                                                                  \
+    return check_launch("conv3x3_x6p");                                                          \
   }
   AINP_X6P(32, 64, false, 256, 1024, 8)
   AINP_X6P(16, 32, false, 512, 512, 8) AINP_X6P(16, 32, true, 512, 512, 8)
   if (Cin == 32 && Cout == 16) {   // two workgroups per CU (65 KB of LDS)
-    if (dgrad)
-      hipLaunchKernelGGL((conv3x3_x6q_kernel<32, true>), dim3(512), dim3(512), 0, s, x, w, bias,
-                         sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);
-    else
-      hipLaunchKernelGGL((conv3x3_x6q_kernel<32, false>), dim3(512), dim3(512), 0, s, x, w, bias,
-                         sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);
+#define AINP_X6Q(DG, NPV)                                                                        \
+  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV>), dim3(512), dim3(512), 0, s, x, w, bias,  \
+                     sc, sh, y, stats, (int)N, Cout, (int)H, (int)W)
+    if (dgrad) {
+      if (b16) AINP_X6Q(true, 1);
+      else AINP_X6Q(true, 3);
+    } else {
+      if (b16) AINP_X6Q(false, 1);
+      else AINP_X6Q(false, 3);
+    }
+#undef AINP_X6Q
     *parts = 512;
     return check_launch("conv3x3_x6q");
   }
@@ -1304,20 +1295,27 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
 // instantiation; returns 1 if not handled.  grid = persistent workgroups.
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s) {
-  if (cp == 32 && Cout == 16) {
-    hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
-                       partial, (int)N, Cin, (int)H, (int)W, ci0);
-    return check_launch("conv3x3_wgrad_x6s");
-  }
-  if (cp == 16 && Cout == 32) {
-    hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
-                       partial, (int)N, Cin, (int)H, (int)W, ci0);
-    return check_launch("conv3x3_wgrad_x6s");
-  }
+                         int ci0, int cp, int grid, hipStream_t s, bool b16) {
+#define AINP_WX6S(CPV, COV)                                                                 \
+  do {                                                                                      \
+    if (b16)                                                                                \
+      hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, 1>), dim3(grid), dim3(384), 0, s, x, sc, \
+                         sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);                \
+    else                                                                                    \
+      hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, 3>), dim3(grid), dim3(384), 0, s, x, sc, \
+                         sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);                \
+    return check_launch("conv3x3_wgrad_x6s");                                               \
+  } while (0)
+  if (cp == 32 && Cout == 16) AINP_WX6S(32, 16);
+  if (cp == 16 && Cout == 32) AINP_WX6S(16, 32);
+#undef AINP_WX6S
   if (cp != 32 || Cout != 64) return 1;
-  hipLaunchKernelGGL((conv3x3_wgrad_x6<64>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy, partial,
-                     (int)N, Cin, (int)H, (int)W, ci0);
+  if (b16)
+    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 1>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
+                       partial, (int)N, Cin, (int)H, (int)W, ci0);
+  else
+    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
+                       partial, (int)N, Cin, (int)H, (int)W, ci0);
   return check_launch("conv3x3_wgrad_x6");
 }
 

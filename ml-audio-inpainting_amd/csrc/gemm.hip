@@ -245,6 +245,95 @@ __device__ __forceinline__ bf16x8v frag(const unsigned char* img, int plane, int
 }
 }  // namespace x6
 
+// ======================================================= bf16 operand path
+// AINP_GEMM_BF16 (the bf16 configurations C3-C5): each fp32 operand element is
+// rounded once to bf16 (round-to-nearest-even, v_cvt_pk_bf16_f32) while it is
+// staged, and a*b accumulates in f32 on v_mfma_f32_32x32x16_bf16 -- torch's
+// bf16-operand / fp32-accumulate autocast arithmetic.  K-tile 32, one plane per
+// operand, 80-byte image rows (conflict-free ds_read_b128 fragments).
+namespace b16 {
+constexpr int KT = 32;
+constexpr int RS = 80;            // bytes per image row: 32 bf16 + 16 B pad
+constexpr int IMG = 128 * RS;
+
+// 128 x 32 fp32 operand tile -> registers -> bf16 -> one LDS plane.
+//  KC: thread = one row x 4 consecutive k (four float4 per thread);
+//  MC: thread = 4 consecutive rows x k pairs {2p, 2p+1, 2p+16, 2p+17}.
+template <bool KC, bool VEC>
+struct Loader {
+  float4 v[4];
+
+  __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld, int64_t r0,
+                                       int64_t k0, int64_t R, int64_t K) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (KC) {
+        const int idx = tid + i * GEMM_THREADS;
+        const int64_t gr = r0 + (idx >> 3), gk = k0 + (idx & 7) * 4;
+        if (gr < R) {
+          const float* q = p + gr * ld + gk;
+          if (VEC) {
+            if (gk < K) x = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (gk + 0 < K) x.x = q[0];
+            if (gk + 1 < K) x.y = q[1];
+            if (gk + 2 < K) x.z = q[2];
+            if (gk + 3 < K) x.w = q[3];
+          }
+        }
+      } else {
+        const int64_t gk = k0 + 2 * (tid & 7) + (i & 1) + 16 * (i >> 1);
+        const int64_t gr = r0 + 4 * (tid >> 3);
+        if (gk < K) {
+          const float* q = p + gk * ld + gr;
+          if (VEC) {
+            if (gr < R) x = *reinterpret_cast<const float4*>(q);
+          } else {
+            if (gr + 0 < R) x.x = q[0];
+            if (gr + 1 < R) x.y = q[1];
+            if (gr + 2 < R) x.z = q[2];
+            if (gr + 3 < R) x.w = q[3];
+          }
+        }
+      }
+      v[i] = x;
+    }
+  }
+
+  __device__ __forceinline__ void store(unsigned char* img) const {
+    const int tid = threadIdx.x;
+    if (KC) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int idx = tid + i * GEMM_THREADS;
+        unsigned char* q = img + (idx >> 3) * RS + (idx & 7) * 8;
+        *reinterpret_cast<uint2*>(q) =
+            make_uint2(x6::cvt_pk_bf16(v[i].x, v[i].y), x6::cvt_pk_bf16(v[i].z, v[i].w));
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float* f0 = reinterpret_cast<const float*>(&v[2 * h]);
+        const float* f1 = reinterpret_cast<const float*>(&v[2 * h + 1]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          unsigned char* q = img + (4 * (tid >> 3) + j) * RS + (tid & 7) * 4 + 32 * h;
+          *reinterpret_cast<uint32_t*>(q) = x6::cvt_pk_bf16(f0[j], f1[j]);
+        }
+      }
+    }
+  }
+};
+
+// fragment of k-step ks (16 k): lane (row, half h) gets k = 16 ks + 8h .. +7
+__device__ __forceinline__ bf16x8v frag(const unsigned char* img, int row, int ks, int h) {
+  const uint4 u = *reinterpret_cast<const uint4*>(img + row * RS + 32 * ks + 16 * h);
+  return __builtin_bit_cast(bf16x8v, u);
+}
+}  // namespace b16
+
 // ===================================================== main-loop policies
 // Exact f32 path: K-tile 32, f32 images, 32x32x2 f32 MFMA.
 template <bool AKC, bool BKC, bool AVEC, bool BVEC>
@@ -319,23 +408,58 @@ struct PolX6 {
   }
 };
 
-template <bool X6, bool AKC, bool BKC, bool AVEC, bool BVEC>
+// bf16 path: K-tile 32, one bf16 plane per operand, two 32x32x16 MFMAs per tile.
+template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+struct PolB16 {
+  static constexpr int KT = b16::KT;
+  static constexpr int SMEM = 2 * b16::IMG;
+  using LA = b16::Loader<AKC, AVEC>;
+  using LB = b16::Loader<BKC, BVEC>;
+  __device__ static __forceinline__ void store(const LA& la, const LB& lb, unsigned char* sm) {
+    la.store(sm);
+    lb.store(sm + b16::IMG);
+  }
+  __device__ static __forceinline__ void compute(const unsigned char* sm, f32x16v (&acc)[2][2],
+                                                 int wm, int wn, int li, int lh) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8v a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = b16::frag(sm, wm + i * 32 + li, ks, lh);
+        b[i] = b16::frag(sm + b16::IMG, wn + i * 32 + li, ks, lh);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = mfma32bf(a[i], b[j], acc[i][j]);
+    }
+  }
+};
+
+// main loop: PM_F32 exact f32, PM_X6 fp32-accurate split bf16, PM_B16 bf16 operands
+constexpr int PM_F32 = 0, PM_X6 = 1, PM_B16 = 2;
+template <int PM, bool AKC, bool BKC, bool AVEC, bool BVEC>
 struct PolSel {
   using type = PolF32<AKC, BKC, AVEC, BVEC>;
 };
 template <bool AKC, bool BKC, bool AVEC, bool BVEC>
-struct PolSel<true, AKC, BKC, AVEC, BVEC> {
+struct PolSel<PM_X6, AKC, BKC, AVEC, BVEC> {
   using type = PolX6<AKC, BKC, AVEC, BVEC>;
+};
+template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+struct PolSel<PM_B16, AKC, BKC, AVEC, BVEC> {
+  using type = PolB16<AKC, BKC, AVEC, BVEC>;
 };
 
 // ================================================================ tile grid
 // Single-buffered LDS + one K-tile of register prefetch: <= 37 KB of LDS and
 // <= 168 VGPRs -> 3 workgroups per CU (768 resident tiles on the chip).
-template <bool X6, bool AKC, bool BKC, bool AVEC, bool BVEC>
+template <int PM, bool AKC, bool BKC, bool AVEC, bool BVEC>
 __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_kernel(
     int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda,
     int64_t ldb, float beta, int64_t scm, int64_t scn, int nseg, int tiles_n) {
-  using Pol = typename PolSel<X6, AKC, BKC, AVEC, BVEC>::type;
+  using Pol = typename PolSel<PM, AKC, BKC, AVEC, BVEC>::type;
   __shared__ __attribute__((aligned(16))) unsigned char smem[Pol::SMEM];
 
   // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs,
@@ -507,11 +631,11 @@ __device__ __forceinline__ void sk_store(const GemmPtrs& ptrs, int b, int64_t m0
     }
 }
 
-template <bool X6, bool AKC, bool BKC, bool AVEC, bool BVEC>
+template <int PM, bool AKC, bool BKC, bool AVEC, bool BVEC>
 __global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_streamk(
     int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda, int64_t ldb,
     float beta, int64_t scm, int64_t scn, SkGeom g, float* __restrict__ ws) {
-  using Pol = typename PolSel<X6, AKC, BKC, AVEC, BVEC>::type;
+  using Pol = typename PolSel<PM, AKC, BKC, AVEC, BVEC>::type;
   __shared__ __attribute__((aligned(16))) unsigned char smem[Pol::SMEM];
   const int w = blockIdx.x;
   const int64_t L = (int64_t)(w % 8) * (g.P / 8) + w / 8;
@@ -621,14 +745,14 @@ static SkGeom streamk_geom(int64_t M, int64_t N, int64_t K, int64_t nb, int kspl
   return g;
 }
 
-template <bool X6, bool AKC, bool BKC>
+template <int PM, bool AKC, bool BKC>
 static void launch_gemm(bool avec, bool bvec, dim3 grid, hipStream_t s,
                         int64_t M, int64_t N, int64_t K, float alpha,
                         const GemmPtrs& p, int64_t lda, int64_t ldb,
                         float beta, int64_t scm, int64_t scn, int nseg,
                         int tiles_n) {
 #define AINP_GEMM_LAUNCH(AV, BV)                                             \
-  hipLaunchKernelGGL((gemm_f32_kernel<X6, AKC, BKC, AV, BV>), grid,         \
+  hipLaunchKernelGGL((gemm_f32_kernel<PM, AKC, BKC, AV, BV>), grid,         \
                      dim3(GEMM_THREADS), 0, s, M, N, K, alpha, p, lda, ldb, \
                      beta, scm, scn, nseg, tiles_n)
   if (avec && bvec) AINP_GEMM_LAUNCH(true, true);
@@ -638,12 +762,12 @@ static void launch_gemm(bool avec, bool bvec, dim3 grid, hipStream_t s,
 #undef AINP_GEMM_LAUNCH
 }
 
-template <bool X6, bool AKC, bool BKC>
+template <int PM, bool AKC, bool BKC>
 static void launch_streamk(bool avec, bool bvec, hipStream_t s, int64_t M, int64_t N, int64_t K,
                            float alpha, const GemmPtrs& p, int64_t lda, int64_t ldb, float beta,
                            int64_t scm, int64_t scn, const SkGeom& g, float* ws) {
 #define AINP_SK(AV, BV)                                                                       \
-  hipLaunchKernelGGL((gemm_f32_streamk<X6, AKC, BKC, AV, BV>), dim3(g.P), dim3(GEMM_THREADS), \
+  hipLaunchKernelGGL((gemm_f32_streamk<PM, AKC, BKC, AV, BV>), dim3(g.P), dim3(GEMM_THREADS), \
                      0, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, g, ws)
   if (avec && bvec) AINP_SK(true, true);
   else if (avec) AINP_SK(true, false);
@@ -653,7 +777,7 @@ static void launch_streamk(bool avec, bool bvec, hipStream_t s, int64_t M, int64
 }
 
 // layout dispatch for both main loops: streamk selects the persistent kernel
-template <bool X6>
+template <int PM>
 static void dispatch_gemm(bool streamk, bool akc, bool bkc, bool avec, bool bvec, dim3 grid,
                           hipStream_t s, int64_t M, int64_t N, int64_t K, float alpha,
                           const GemmPtrs& p, int64_t lda, int64_t ldb, float beta, int64_t scm,
@@ -661,10 +785,10 @@ static void dispatch_gemm(bool streamk, bool akc, bool bkc, bool avec, bool bvec
 #define AINP_DISPATCH(AK, BK_)                                                                 \
   do {                                                                                         \
     if (streamk)                                                                               \
-      launch_streamk<X6, AK, BK_>(avec, bvec, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, \
+      launch_streamk<PM, AK, BK_>(avec, bvec, s, M, N, K, alpha, p, lda, ldb, beta, scm, scn, \
                                   g, ws);                                                      \
     else                                                                                       \
-      launch_gemm<X6, AK, BK_>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm,   \
+      launch_gemm<PM, AK, BK_>(avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm,   \
                                scn, nseg, tiles_n);                                           \
   } while (0)
   if (akc && bkc) AINP_DISPATCH(true, true);
@@ -730,7 +854,10 @@ extern "C" int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
   if (M < 0 || N < 0 || K < 0 || nptr < 1 || nptr > 8 || nstrided < 1 ||
       !A || !B || !C)
     return record_msg("ainp_gemm_f32: bad argument");
-  if (flags & ~AINP_GEMM_EXACT_F32) return record_msg("ainp_gemm_f32: unknown flags");
+  if (flags & ~(AINP_GEMM_EXACT_F32 | AINP_GEMM_BF16))
+    return record_msg("ainp_gemm_f32: unknown flags");
+  if ((flags & AINP_GEMM_EXACT_F32) && (flags & AINP_GEMM_BF16))
+    return record_msg("ainp_gemm_f32: EXACT_F32 and BF16 are exclusive");
   if (sam != 1 && sak != 1) return record_msg("ainp_gemm_f32: A needs a unit stride");
   if (sbk != 1 && sbn != 1) return record_msg("ainp_gemm_f32: B needs a unit stride");
   if (scm != 1 && scn != 1) return record_msg("ainp_gemm_f32: C needs a unit stride");
@@ -750,7 +877,8 @@ extern "C" int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
   p.sC = strideC;
   p.nptr = nptr;
   p.ksplit_mode = ksplit;
-  const bool use_x6 = !(flags & AINP_GEMM_EXACT_F32);
+  const int pm = (flags & AINP_GEMM_BF16) ? PM_B16 : (flags & AINP_GEMM_EXACT_F32) ? PM_F32 : PM_X6;
+  const bool use_x6 = pm != PM_F32;   // the split-bf16 and bf16 loops: plain grid
   // contiguous dimension of each operand (prefer k when both strides are 1)
   const bool akc = (sak == 1);
   const bool bkc = (sbk == 1);
@@ -777,12 +905,15 @@ extern "C" int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
   const unsigned gy = ksplit == 1 ? 1u : (ksplit == 2 ? (unsigned)nptr : (unsigned)nb);
   const dim3 grid((unsigned)(tiles_m * tiles_n), gy);
   float* ws = reinterpret_cast<float*>(workspace);
-  if (use_x6)
-    dispatch_gemm<true>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta, scm,
-                        scn, nseg, (int)tiles_n, g, ws);
-  else
-    dispatch_gemm<false>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta,
+  if (pm == PM_B16)
+    dispatch_gemm<PM_B16>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta,
+                          scm, scn, nseg, (int)tiles_n, g, ws);
+  else if (pm == PM_X6)
+    dispatch_gemm<PM_X6>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta,
                          scm, scn, nseg, (int)tiles_n, g, ws);
+  else
+    dispatch_gemm<PM_F32>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta,
+                          scm, scn, nseg, (int)tiles_n, g, ws);
   int rc = check_launch(sk ? "gemm_f32_streamk" : "ainp_gemm_f32");
   if (rc || !sk) return rc;
   hipLaunchKernelGGL(gemm_streamk_fixup, dim3((unsigned)(g.units / g.nk)), dim3(GEMM_THREADS), 0,

@@ -249,6 +249,70 @@ def test_gemm_x6_is_fp32_accurate(ops):
     assert errs[False] < 2 * errs[True] + 1e-7, errs
 
 
+def _bf(t):
+    """fp64 copy of t rounded to fp32, then to bf16 (nearest-even)."""
+    return t.float().bfloat16().double()
+
+
+@pytest.mark.parametrize("M,N,K", [(333, 130, 77), (256, 512, 1024), (129, 4112, 256),
+                                   (1, 5, 3)])
+@pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
+def test_gemm_bf16_layouts(ops, M, N, K, ta, tb):
+    """AINP_GEMM_BF16: operands rounded to bf16 (as torch autocast does),
+    fp32 accumulation -> equal to the fp64 product of the bf16 operands up to
+    fp32 accumulation error."""
+    g = torch.Generator().manual_seed(M * 11 + N + K)
+    A = torch.randn(M, K, generator=g, dtype=torch.float64)
+    B = torch.randn(K, N, generator=g, dtype=torch.float64)
+    ref = _bf(A) @ _bf(B)
+    Ad = (A.t().contiguous() if ta else A).float().to(DEV)
+    Bd = (B.t().contiguous() if tb else B).float().to(DEV)
+    C = torch.empty(M, N, device=DEV)
+    sam, sak = (1, M) if ta else (K, 1)
+    sbk, sbn = (1, K) if tb else (N, 1)
+    ops.gemm(M, N, K, [Ad], sam, sak, [Bd], sbk, sbn, [C], N, 1, bf16=True)
+    assert rel(C.cpu(), ref) < 1e-5
+    # and it is a bf16 product: far from the fp32 one on random data
+    assert rel(C.cpu(), A @ B) > 1e-4
+
+
+@pytest.mark.parametrize("N,Cin,Cout,H,W,pro", [
+    (2, 32, 64, 257, 334, True), (2, 16, 32, 257, 334, True), (2, 32, 16, 257, 334, True),
+    (2, 64, 32, 40, 70, False), (1, 32, 64, 19, 47, False)])
+def test_conv3x3_bf16(ops, N, Cin, Cout, H, W, pro):
+    """AINP_CONV_BF16 on the 16/32/64-channel pairs: act(x) (BatchNorm+ReLU
+    prologue in fp32), weights and dy rounded to bf16, fp32 accumulation; fp32
+    bias, outputs and BatchNorm partials.  Checked against fp64 convolutions
+    of the bf16-rounded operands."""
+    g = torch.Generator().manual_seed(N * 1000 + Cin * 10 + Cout)
+    x = torch.randn(N, Cin, H, W, generator=g, dtype=torch.float64).float().double()
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g, dtype=torch.float64) * 0.2).float().double()
+    b = torch.randn(Cout, generator=g, dtype=torch.float64).float().double()
+    sc = (torch.rand(Cin, generator=g, dtype=torch.float64) + 0.5).float().double() if pro else None
+    sh = (torch.randn(Cin, generator=g, dtype=torch.float64) * 0.3).float().double() if pro else None
+    xa = _act(x, sc, sh).float().double()        # fp32 prologue (fmaf: one rounding)
+    yr = Fnn.conv2d(_bf(xa), _bf(w), b, padding=1)
+    dy = torch.randn(yr.shape, generator=g, dtype=torch.float64).float().double()
+    d = lambda t: None if t is None else t.float().to(DEV)  # noqa: E731
+    y, stats = ops.conv3x3_fwd(d(x), d(w), d(b), d(sc), d(sh), want_stats=True, bf16=True)
+    assert rel(y.cpu(), yr) < 2e-5
+    st = stats.sum(0).cpu()
+    assert rel(st[:Cout], yr.sum((0, 2, 3))) < 2e-5
+    dxr = torch.nn.grad.conv2d_input(xa.shape, _bf(w), _bf(dy), padding=1)
+    dx = ops.conv3x3_dgrad(d(dy), d(w), bf16=True)
+    assert rel(dx.cpu(), dxr) < 2e-5
+    dw, db = ops.conv3x3_wgrad(d(x), d(dy), d(sc), d(sh), bf16=True)
+    if (Cin, Cout) in ((32, 64), (16, 32), (32, 16)):   # the model's weight gradients
+        dwr = torch.nn.grad.conv2d_weight(_bf(xa), w.shape, _bf(dy), padding=1)
+        assert rel(dw.cpu(), dwr) < 2e-5
+    else:   # no bf16 weight-gradient kernel for this pair: the fp32-accurate one serves it
+        dwr = torch.nn.grad.conv2d_weight(xa, w.shape, dy, padding=1)
+        assert rel(dw.cpu(), dwr) < 1e-5
+    assert rel(db.cpu(), dy.sum((0, 2, 3))) < 1e-5
+    # genuinely bf16 (not the fp32-accurate path)
+    assert rel(y.cpu(), Fnn.conv2d(xa, w, b, padding=1)) > 1e-5
+
+
 def test_gemm_batched_bias_ksplit(ops):
     g = torch.Generator().manual_seed(3)
     M, N, K, nb = 100, 96, 40, 3
