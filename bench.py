@@ -163,6 +163,8 @@ def main():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--workload", choices=("cnnblstm", "gan"), default="cnnblstm",
                     help="cnnblstm = BASELINE configs[1] (the headline metric); gan = configs[3]")
+    ap.add_argument("--clip-s", type=float, default=None,
+                    help="gan: clip length (5 s = C4, T=626; 8 s = C5, T=1001, 0.1 s gap)")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
                     help="fp32 = C2 (headline); bf16 = the C3 per-GPU shape (bf16 GEMM/conv "
                          "operands, fp32 accumulate / cell state / BN statistics / weights)")
@@ -334,7 +336,8 @@ GAN_CFG = {
                  "lambda_l1_valid": 1.0, "lambda_l1_hole": 2.0, "lambda_vgg_perceptual": 4.0,
                  "lambda_vgg_style": 500.0, "lambda_mag_weighted": 0.2},
 }
-GAN_FLOP_PER_SAMPLE = 270.4e9   # SURVEY §8 d4 at T=626: G fwd + 3 D fwd + D-step bwd + 2 VGG fwd
+# G fwd + 3 D fwd + D-step bwd + 2 VGG fwd, per sample
+GAN_FLOP_PER_SAMPLE = {626: 270.4e9, 1001: 388.7e9}
 
 
 def gan_cpu_baseline(T, S, g, steps=1):
@@ -372,50 +375,79 @@ def run_gan(args):
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     comm = Comm() if world > 1 else None
-    B = args.batch if args.batch != 32 else 8        # C4: batch 8 per GPU
-    S, hop, n_fft, g = 80000, 128, 512, 3200          # 5 s @ 16 kHz, gap 0.2 s
-    T = 1 + S // hop                                   # 626
+    B = args.batch if args.batch != 32 else 8        # C4 / C5: batch 8 per GPU
+    clip_s = args.clip_s if args.clip_s is not None else 5.0
+    c5 = clip_s >= 8.0
+    S, hop, n_fft = int(16000 * clip_s), 128, 512      # C4: 5 s, C5: 8 s @ 16 kHz
+    g = 1600 if c5 else 3200                           # C5: 0.1 s gaps, C4: 0.2 s
+    T = 1 + S // hop                                   # 626 / 1001
+    bf16 = args.dtype == "bf16"
     torch.manual_seed(0)
     gen = G.PConvUNet().to(dev)
     disc = G.Discriminator().to(dev)
     vgg = G.VGGLoss(dev)
-    tr = GanTrainer(GAN_CFG, gen, disc, vgg, comm=comm)
+    tr = GanTrainer(dict(GAN_CFG, accel={"dtype": args.dtype}), gen, disc, vgg, comm=comm)
     audio = torch.from_numpy(synthetic_clips(B, S, 200000 + 100000 * rank)).to(dev)
     nsteps = args.warmup + args.steps
     rng = np.random.default_rng(777 + rank)
     starts = torch.from_numpy(rng.integers(0, S - g + 1, size=(nsteps, B)).astype(np.int64)).to(dev)
     hole = torch.zeros(nsteps, device=dev)
 
+    last = {}
+
     def step(i):
-        o, im, _, m = ops.stft_features(audio, starts[i], g, n_fft, hop, n_fft, n_frames=T,
-                                        mode=ops.FEAT_GAN, outputs=(True, True, False, True))
+        o, im, ph, m = ops.stft_features(audio, starts[i], g, n_fft, hop, n_fft, n_frames=T,
+                                         mode=ops.FEAT_GAN, outputs=(True, True, c5, True))
         out = tr.step(o.unsqueeze(1), im.unsqueeze(1), m.unsqueeze(1))
         hole[i] = out["g_l1_hole"]
+        last.update(orig=o, phase=ph, mask=m, gen=out["generated"])
 
     for i in range(args.warmup):
         step(i)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev[0].record()
     for i in range(args.warmup, nsteps):
         step(i)
+        ev[i - args.warmup + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    med_ms = float(np.median([ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]))
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        e = torch.tensor([elapsed, med_ms], device=dev, dtype=torch.float64)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed, med_ms = float(e[0].item()), float(e[1].item())
     value = B * T * args.steps * world / elapsed
     ms_step = 1000.0 * elapsed / args.steps
+
+    # C5: on-GPU audio reconstruction of the last batch, the sample path of
+    # models/GAN/train.py:465-505: combined log-magnitude (generated in the
+    # hole, original elsewhere; passed to utils.spectrogram_to_audio as the
+    # magnitude, as the reference does), ISTFT with the original phase, and
+    # Griffin-Lim (spectrogram_to_audio's n_iter=64, librosa>=0.10 semantics)
+    # without phase; timed separately: the reference runs it every
+    # sample_interval steps, not per step
+    recon = None
+    if c5 and rank == 0:
+        mag = (last["gen"][:, 0] * (1 - last["mask"]) + last["orig"] * last["mask"]).contiguous()
+        ist_s = time_kernel(lambda: ops.istft(mag=mag, phase=last["phase"], n_fft=n_fft,
+                                              hop_length=hop), 5, dev)
+        gl_s = time_kernel(lambda: ops.griffinlim(mag, n_iter=64, hop_length=hop, n_fft=n_fft,
+                                                  random_state=0), 2, dev)
+        recon = {"istft_orig_phase_ms": round(ist_s * 1e3, 3),
+                 "griffinlim64_ms": round(gl_s * 1e3, 3),
+                 "batch": B, "samples_per_clip": hop * (T - 1)}
 
     roof = None
     if rank == 0:
         # dominant kernel: the final PartialConv2d (65 -> 64, 3x3) at the padded
         # 384 x 640 resolution, B examples: conv_gen generic path
-        Hp, Wp = 384, 640
+        Hp, Wp = 384, (1024 if c5 else 640)
         x0 = torch.randn(B, 64, Hp // 2, Wp // 2, device=dev)
         m0 = torch.ones(B, Hp // 2, Wp // 2, device=dev)
         x1 = torch.randn(B, 1, Hp, Wp, device=dev)
@@ -425,50 +457,55 @@ def run_gan(args):
         bias = torch.zeros(64, device=dev)
         out = torch.empty(B, 64, Hp, Wp, device=dev)
         kw = dict(src1=(x1, m1), Hin=Hp, Win=Wp, stride=1, pad=1, bias=bias, ratio=ratio,
-                  act=ops.ACT_LEAKY, out=out)
-        for _ in range(2):
-            ops.conv_gen((x0, m0), w, **kw)
-        s = torch.cuda.current_stream(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(s)
-        for _ in range(args.roofline_reps):
-            ops.conv_gen((x0, m0), w, **kw)
-        e1.record(s)
-        torch.cuda.synchronize()
-        avg_s = e0.elapsed_time(e1) / 1000.0 / args.roofline_reps
+                  act=ops.ACT_LEAKY, out=out, bf16=bf16)
+        avg_s = time_kernel(lambda: ops.conv_gen((x0, m0), w, **kw), args.roofline_reps, dev)
         flops = 2.0 * 64 * 65 * 9 * B * Hp * Wp
         ach = flops / avg_s / 1e12
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+        peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
+        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                 "traffic": _traffic("traffic_conv_gen_final.json"),
                 "kernel": f"conv_gen_x6_kernel<64,16> (final PartialConv2d 65->64 3x3 at "
                           f"{Hp}x{Wp}, B={B})", "avg_launch_ms": round(avg_s * 1e3, 4),
-                "flop_per_launch": flops,
+                "flop_per_launch": flops}
+        if bf16:
+            roof["main_loop"] = ("operands rounded to bf16 at LDS staging, "
+                                 "v_mfma_f32_32x32x16_bf16, f32 accumulate")
+        else:
+            roof.update({
                 "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross products "
                              "on v_mfma_f32_32x32x16_bf16, f32 accumulate",
                 "executed_tflops": round(6 * ach, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
-                "executed_frac": round(6 * ach / BF16_MFMA_PEAK_TFLOPS, 4)}
+                "executed_frac": round(6 * ach / BF16_MFMA_PEAK_TFLOPS, 4)})
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = gan_cpu_baseline(T, S, g)
     if rank == 0:
-        step_flops = GAN_FLOP_PER_SAMPLE * B * world
+        step_flops = GAN_FLOP_PER_SAMPLE[T] * B * world if T in GAN_FLOP_PER_SAMPLE else None
+        cname = "C5" if c5 else "C4"
         out = {
-            "metric": "GAN spectrogram-frames/sec/node (train step), BASELINE configs[3]",
+            "metric": f"GAN spectrogram-frames/sec/node (train step), BASELINE configs"
+                      f"[{4 if c5 else 3}]",
             "value": round(value, 2), "unit": "frames/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
-            "data": "synthetic (5 s/16 kHz harmonic clips, seeded; random init; VGG19 random "
-                    "init: pretrained weights not downloadable offline)",
-            "config": {"workload": "C4: GAN step (GAN STFT features + PConvUNet fwd + D step "
-                                   "+ G-step losses incl. VGG19), fp32, 8 examples/GPU, F=257, "
-                                   "T=626, gap 0.2 s", "global_batch": B * world, "seq_len": T,
+            "warmup": args.warmup, "ms_per_step": round(ms_step, 3),
+            "ms_per_step_median": round(med_ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": f"synthetic ({clip_s:g} s/16 kHz harmonic clips, seeded; random init; VGG19 "
+                    "random init: pretrained weights not downloadable offline)",
+            "config": {"workload": f"{cname}: GAN step (GAN STFT features + PConvUNet fwd + D "
+                                   "step + G-step losses incl. VGG19), "
+                                   + ("bf16 conv/GEMM operands, fp32 accumulate"
+                                      if bf16 else "fp32")
+                                   + f", {B} examples/GPU, F=257, T={T}, gap {g / 16000:g} s",
+                       "global_batch": B * world, "seq_len": T,
                        "freq_bins": 257, "parallelism": f"dp{world}"},
             "recon_l1_hole": float(hole[-1].item()),
-            "step_tflops": round(step_flops / (ms_step / 1e3) / 1e12, 2),
-            "mfma_util_step": round(step_flops / world / (ms_step / 1e3) / 1e12
-                                    / FP32_MFMA_PEAK_TFLOPS, 4),
-            "roofline": roof, "cpu_baseline": cpu,
+            "step_tflops": (round(step_flops / (ms_step / 1e3) / 1e12, 2)
+                            if step_flops else None),
+            "mfma_util_step": (round(step_flops / world / (ms_step / 1e3) / 1e12
+                                     / (BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS),
+                                     4) if step_flops else None),
+            "roofline": roof, "reconstruction": recon, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

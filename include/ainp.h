@@ -391,6 +391,16 @@ int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H0, int W0,
                       int Cout, int Hin, int Win, int KH, int KW, int stride,
                       int pad, int act, float slope, int crop_h, int crop_w,
                       void* workspace, void* stream);
+/* Same with a precision flag: AINP_CONV_BF16 rounds the gathered activations
+ * and the weights to bf16 (fp32 accumulation, fp32 epilogue) -- the GAN bf16
+ * configurations C4 / C5 (models/GAN/networks.py:63-106,359-405, loss.py). */
+int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, int H0, int W0,
+                         const float* x1, const float* m1, int C1, int H1, int W1,
+                         const float* w, const float* wt, const float* bias,
+                         const float* ratio, const float* scale, float* y, double* stats,
+                         int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
+                         int pad, int act, float slope, int crop_h, int crop_w, int flags,
+                         void* workspace, void* stream);
 /* PartialConv2d mask update (networks.py:83-104, multi_channel=False):
  * count = C0*window_sum(m0) + C1*window_sum(m1) over the conv's window (masks
  * are planes of integer counts -- 0/1, or a channel sum -- repeated over their

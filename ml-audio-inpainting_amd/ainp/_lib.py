@@ -90,6 +90,10 @@ _SIGS = {
     "ainp_conv_gen_fwd": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int,
                                   P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int, c_int,
                                   c_int, c_int, c_int, c_int, c_float, c_int, c_int, P, P]),
+    "ainp_conv_gen_fwd_ex": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int,
+                                     P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int, c_int,
+                                     c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int, P,
+                                     P]),
     "ainp_pconv_mask": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int64,
                                 c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "ainp_gan_pad_input": (c_int, [P, P, c_int64, c_int, c_int, c_int, c_int, P, P, P]),

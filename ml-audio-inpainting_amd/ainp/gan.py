@@ -85,6 +85,7 @@ class PartialConv2d(nn.Module):
             p.requires_grad = False
         self.bias = nn.Parameter(torch.zeros(out_channels)) if bias else None
         self.window_size = float(in_channels * kernel_size * kernel_size)
+        self.ainp_bf16 = False   # set_compute_dtype(): bf16 conv operands (C4 / C5)
 
     # plane-level entry used by the U-Net: srcs = [(x, mask_plane [N,H,W]), ...]
     def run(self, srcs, Hin, Win, act=ops.ACT_NONE, want_stats=False, crop=None):
@@ -97,7 +98,7 @@ class PartialConv2d(nn.Module):
                                      N, Hin, Win, k, s, p)
         y, stats = ops.conv_gen(srcs[0], self.conv.weight, src1=src1, Hin=Hin, Win=Win, stride=s,
                                 pad=p, bias=self.bias, ratio=ratio, act=act, slope=SLOPE,
-                                want_stats=want_stats, crop=crop)
+                                want_stats=want_stats, crop=crop, bf16=self.ainp_bf16)
         return y, newm, stats
 
     def run_full_mask(self, x, mask, want_stats=False):
@@ -110,7 +111,7 @@ class PartialConv2d(nn.Module):
         # ratio's numerator stays Cin*k*k
         ratio, newm = ops.pconv_mask((msum, 1), None, N, H, W, k, s, p, winsize=self.window_size)
         y, stats = ops.conv_gen((xm, None), self.conv.weight, stride=s, pad=p, bias=self.bias,
-                                ratio=ratio, want_stats=want_stats)
+                                ratio=ratio, want_stats=want_stats, bf16=self.ainp_bf16)
         return y, newm, stats
 
     def forward(self, x: torch.Tensor, mask: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -311,17 +312,19 @@ class _DiscriminatorFn(torch.autograd.Function):
     params per layer: (weight_orig, bias); sn = (inv_sigma [L], u clones, v clones)."""
 
     @staticmethod
-    def forward(ctx, x, cfg, inv, us, vs, *params):
+    def forward(ctx, x, cfg, bf16, inv, us, vs, *params):
         h = x.contiguous()
         ins, outs = [], []
         for l, (k, s, p, act) in enumerate(cfg):
             w, b = params[2 * l], params[2 * l + 1]
             y, _ = ops.conv_gen((h, None), w, stride=s, pad=p, bias=b, scale=inv[l:l + 1],
-                                act=ops.ACT_LEAKY if act else ops.ACT_NONE, slope=SLOPE)
+                                act=ops.ACT_LEAKY if act else ops.ACT_NONE, slope=SLOPE,
+                                bf16=bf16)
             ins.append(h)
             outs.append(y)
             h = y
         ctx.cfg = cfg
+        ctx.bf16 = bf16
         ctx.nl = len(cfg)
         ctx.save_for_backward(inv, *ins, *outs, *us, *vs, *params)
         return h
@@ -355,18 +358,18 @@ class _DiscriminatorFn(torch.autograd.Function):
             col = ops.im2col(h, k, s, p, ones_row=True, ldp=P4)    # [N, K+1, P4]
             Gw = torch.empty(Cout, K + 1, device=g.device)
             ops.gemm_batched_splitk(Cout, K + 1, P4, [g[n] for n in range(N)], P4, 1,
-                                    [col[n] for n in range(N)], 1, P4, Gw)
+                                    [col[n] for n in range(N)], 1, P4, Gw, bf16=ctx.bf16)
             dw, db = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1], with_bias=True)
             grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
             if l > 0 or ctx.needs_input_grad[0]:
                 wn = ops.scale_by_scalar(w, inv[l:l + 1])
                 dcol = torch.empty(N, K, P4, device=g.device)    # padded columns unused
                 ops.gemm(K, P4, Cout, [wn], 1, K, [g], P4, 1, [dcol], P4, 1, strideB=Cout * P4,
-                         strideC=K * P4, nstrided=N)
+                         strideC=K * P4, nstrided=N, bf16=ctx.bf16)
                 g = ops.col2im(dcol, N, Cin, H, W, k, s, p)
                 if l == 0:
                     gx = g
-        return (gx, None, None, None, None, *grads)
+        return (gx, None, None, None, None, None, *grads)
 
 
 def _split_count(n):
@@ -402,6 +405,7 @@ class Discriminator(nn.Module):
         self.model = nn.Sequential(*layers)
         if final_out_channels != 1:
             raise NotImplementedError("final_out_channels must be 1 (the reference's)")
+        self.ainp_bf16 = False   # set_compute_dtype(): bf16 conv / GEMM operands (C4 / C5)
 
     def _convs(self):
         return [m.block[0] for m in self.model[:-1]] + [self.model[-1]]
@@ -420,7 +424,8 @@ class Discriminator(nn.Module):
         params = []
         for c in convs:
             params += [c.weight_orig, c.bias]
-        return _DiscriminatorFn.apply(x.contiguous().float(), self._cfg, inv, us, vs, *params)
+        return _DiscriminatorFn.apply(x.contiguous().float(), self._cfg, self.ainp_bf16, inv, us,
+                                      vs, *params)
 
 
 # ------------------------------------------------------------ losses
@@ -485,6 +490,7 @@ class VGGLoss(nn.Module):
         idx = list(layer_indices_style) + list(layer_indices_perceptual)
         self.max_layer_idx = max(idx) if idx else -1
         self._tables = {}
+        self.ainp_bf16 = False   # set_compute_dtype(): bf16 conv / Gram operands (C4 / C5)
 
     def _prep_tables(self, H, W, device, S=224, short=256):
         key = (H, W, str(device))
@@ -525,7 +531,8 @@ class VGGLoss(nn.Module):
                 relu_next = (i < self.max_layer_idx and i + 1 < len(layers)
                              and isinstance(layers[i + 1], nn.ReLU))
                 x, _ = ops.conv_gen((x, None), lay.weight, stride=1, pad=1, bias=lay.bias,
-                                    act=ops.ACT_RELU if relu_next else ops.ACT_NONE)
+                                    act=ops.ACT_RELU if relu_next else ops.ACT_NONE,
+                                    bf16=self.ainp_bf16)
                 if i in want:
                     feats[i] = x
                 if relu_next:
@@ -548,7 +555,7 @@ class VGGLoss(nn.Module):
         g = torch.empty(b, c, c, device=x.device)
         ops.gemm_batched_splitk(c, c, hw, [x[i] for i in range(b)], hw, 1,
                                 [x[i] for i in range(b)], 1, hw, g, alpha=1.0 / (c * hw),
-                                per_batch_out=True)
+                                per_batch_out=True, bf16=self.ainp_bf16)
         return g
 
     @torch.no_grad()
@@ -572,6 +579,21 @@ class VGGLoss(nn.Module):
         if n_s:
             style = style / n_s
         return perc.to(torch.float32), style.to(torch.float32)
+
+
+def set_compute_dtype(module: nn.Module, dtype: str = "fp32") -> nn.Module:
+    """Select the GAN compute precision (the optional `accel.dtype` config
+    key; not in the reference's YAML): "bf16" runs every PartialConv2d, the
+    Discriminator's spectral-norm convs (forward and the backward GEMMs) and
+    VGGLoss's convs / Gram GEMMs with bf16 operands and fp32 accumulation --
+    BASELINE configs C4 / C5; BatchNorm statistics, the 1-channel convs, the
+    losses and the weights stay fp32.  Returns the module."""
+    if dtype not in ("fp32", "bf16"):
+        raise ValueError(f"accel.dtype must be fp32 or bf16, got {dtype!r}")
+    for m in module.modules():
+        if hasattr(m, "ainp_bf16"):
+            m.ainp_bf16 = dtype == "bf16"
+    return module
 
 
 def calculate_losses(cfg, generated_mag, original_mag, mask, d_fake_pred,

@@ -32,6 +32,10 @@ class GanTrainer:
         self.d_opt = Adam(discriminator.parameters(), lr=tc.get("d_lr", 2e-4), betas=betas)
         self.faithful = faithful_g_backward
         self.comm = comm
+        dtype = (cfg.get("accel") or {}).get("dtype", "fp32")
+        for m in (generator, discriminator, vgg):
+            if m is not None:
+                G.set_compute_dtype(m, dtype)
         self.reducer = None
         if comm is not None and comm.world_size > 1:
             from .dist import GradAllReducer

@@ -498,7 +498,8 @@ def conv_weight_kmajor(w, C0, C1):
 
 
 def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=None, ratio=None,
-             scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None):
+             scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None,
+             bf16=False):
     """ainp_conv_gen_fwd.  src0/src1 = (x [N,C,Hs,Ws], mask plane [N,Hs,Ws] or None);
     the conv's input is cat(src0 nearest-resampled to (Hin, Win), src1) * masks.
     Returns (y [N,Cout,Ho,Wo] (or [N,crop_h,crop_w] for Cout=1 with crop), stats)."""
@@ -543,9 +544,10 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
         wt = conv_weight_kmajor(w, C0, C1)
     if nb:
         ws = torch.empty(max(1, nb // 4), device=x0.device)
-    call("ainp_conv_gen_fwd", x0.data_ptr(), _p(m0), C0, H0, W0, _p(x1), _p(m1), C1, H1, W1,
+    call("ainp_conv_gen_fwd_ex", x0.data_ptr(), _p(m0), C0, H0, W0, _p(x1), _p(m1), C1, H1, W1,
          w.data_ptr(), _p(wt), _p(bias), _p(ratio), _p(scale), out.data_ptr(), _p(stats), N, Cout,
-         Hin, Win, KH, KW, stride, pad, act, float(slope), ch, cw, _p(ws), _stream(x0))
+         Hin, Win, KH, KW, stride, pad, act, float(slope), ch, cw, CONV_BF16 if bf16 else 0,
+         _p(ws), _stream(x0))
     return out, stats
 
 
@@ -710,7 +712,7 @@ def largest_divisor_at_most(n, cap):
 
 
 def gemm_batched_splitk(M, N, Kd, As, sam, sak, Bs, sbk, sbn, out, *, alpha=1.0,
-                        per_batch_out=False, target_blocks=768, min_k=256):
+                        per_batch_out=False, target_blocks=768, min_k=256, bf16=False):
     """C = alpha * sum_b A_b B_b (or C_b = alpha * A_b B_b when per_batch_out),
     with the long reduction Kd split into S strided chunks per batch so the
     small-M/N products still fill the chip.  A_b / B_b: tensors whose element
@@ -730,7 +732,7 @@ def gemm_batched_splitk(M, N, Kd, As, sam, sak, Bs, sbk, sbn, out, *, alpha=1.0,
         g1 = min(nb, g0 + 8)
         gemm(M, N, kc, As[g0:g1], sam, sak, Bs[g0:g1], sbk, sbn,
              [slabs[0, i] for i in range(g0, g1)], N, 1, alpha=alpha, strideA=kc * sak,
-             strideB=kc * sbk, strideC=nb * M * N, nstrided=S)
+             strideB=kc * sbk, strideC=nb * M * N, nstrided=S, bf16=bf16)
     if per_batch_out:
         sum_slabs(slabs, S, out=out.reshape(-1))
     else:

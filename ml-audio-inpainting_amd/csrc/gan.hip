@@ -358,7 +358,9 @@ __device__ __forceinline__ bf16x8 frag(const unsigned char* q) {
 // XBK = 16: 16-deep K-tiles with 48-byte image rows (37-46 KB of LDS and
 // <= 168 VGPRs: three workgroups per CU); XBK = 32: 80-byte rows, two.
 // Split-K ranges (p.ktiles_per_split) stay in CG_BK units.
-template <int BM, int XBK>
+// NPL = 3: the fp32-accurate split; NPL = 1 (AINP_CONV_BF16): one bf16 plane
+// per operand (operands rounded to bf16, fp32 accumulation).
+template <int BM, int XBK, int NPL>
 __global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(ConvGenParams p,
                                                                              const float* wt,
                                                                              int act) {
@@ -368,9 +370,9 @@ __global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(Con
   constexpr int BR = XBK * BN / 256;          // consecutive k per thread, B
   constexpr int RS = XBK == 16 ? 48 : cgx::RS;
   constexpr int APL = BM * RS, BPL = BN * RS;   // plane bytes
-  __shared__ __attribute__((aligned(16))) unsigned char sA[3 * APL];
-  __shared__ __attribute__((aligned(16))) unsigned char sB[3 * BPL];
-  static_assert(3 * APL >= WN * BM * 2 * (int)sizeof(double), "epilogue scratch");
+  constexpr int ESCR = WN * BM * 2 * (int)sizeof(double);   // epilogue scratch (in sA)
+  __shared__ __attribute__((aligned(16))) unsigned char sA[NPL * APL > ESCR ? NPL * APL : ESCR];
+  __shared__ __attribute__((aligned(16))) unsigned char sB[NPL * BPL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int KK = p.KH * p.KW;
   const int K0 = KK * p.s0.C;
@@ -448,34 +450,50 @@ __global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(Con
         rb[i] = gather1(__builtin_amdgcn_readfirstlane(k0 + bkq * BR + i));
     }
   };
+  // 8 consecutive-k values -> NP planes (the exact split, or one bf16 rounding)
+  auto pieces = [&](const float* v, uint4& q0, uint4& q1, uint4& q2) {
+    if (NPL == 3) {
+      cgx::split8(v, q0, q1, q2);
+    } else {
+      q0 = make_uint4(cgx::cvt_pk(v[0], v[1]), cgx::cvt_pk(v[2], v[3]), cgx::cvt_pk(v[4], v[5]),
+                      cgx::cvt_pk(v[6], v[7]));
+      q1 = q2 = q0;
+    }
+  };
   auto commit = [&]() {
     if (AR >= 8) {
 #pragma unroll
       for (int i = 0; i < AR; i += 8) {
         uint4 q0, q1, q2;
-        cgx::split8(ra + i, q0, q1, q2);
+        pieces(ra + i, q0, q1, q2);
         unsigned char* q = sA + aco * RS + (akq * AR + i) * 2;
         *reinterpret_cast<uint4*>(q) = q0;
-        *reinterpret_cast<uint4*>(q + APL) = q1;
-        *reinterpret_cast<uint4*>(q + 2 * APL) = q2;
+        if (NPL == 3) {
+          *reinterpret_cast<uint4*>(q + APL) = q1;
+          *reinterpret_cast<uint4*>(q + 2 * APL) = q2;
+        }
       }
     } else {                                  // AR == 4: one 8-byte piece per plane
       float v8[8] = {ra[0 % AR], ra[1 % AR], ra[2 % AR], ra[3 % AR], 0.f, 0.f, 0.f, 0.f};
       uint4 q0, q1, q2;
-      cgx::split8(v8, q0, q1, q2);
+      pieces(v8, q0, q1, q2);
       unsigned char* q = sA + aco * RS + (akq * AR) * 2;
       *reinterpret_cast<uint2*>(q) = make_uint2(q0.x, q0.y);
-      *reinterpret_cast<uint2*>(q + APL) = make_uint2(q1.x, q1.y);
-      *reinterpret_cast<uint2*>(q + 2 * APL) = make_uint2(q2.x, q2.y);
+      if (NPL == 3) {
+        *reinterpret_cast<uint2*>(q + APL) = make_uint2(q1.x, q1.y);
+        *reinterpret_cast<uint2*>(q + 2 * APL) = make_uint2(q2.x, q2.y);
+      }
     }
 #pragma unroll
     for (int i = 0; i < BR; i += 8) {
       uint4 q0, q1, q2;
-      cgx::split8(rb + i, q0, q1, q2);
+      pieces(rb + i, q0, q1, q2);
       unsigned char* q = sB + bpx * RS + (bkq * BR + i) * 2;
       *reinterpret_cast<uint4*>(q) = q0;
-      *reinterpret_cast<uint4*>(q + BPL) = q1;
-      *reinterpret_cast<uint4*>(q + 2 * BPL) = q2;
+      if (NPL == 3) {
+        *reinterpret_cast<uint4*>(q + BPL) = q1;
+        *reinterpret_cast<uint4*>(q + 2 * BPL) = q2;
+      }
     }
   };
 
@@ -496,9 +514,9 @@ __global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(Con
     if (kt + 1 < kt_end) fetch(kt + 1);
 #pragma unroll
     for (int st = 0; st < XBK / 16; ++st) {
-      cgx::bf16x8 a[3][2], b[3][2];
+      cgx::bf16x8 a[NPL][2], b[NPL][2];
 #pragma unroll
-      for (int q = 0; q < 3; ++q)
+      for (int q = 0; q < NPL; ++q)
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
           a[q][i] = cgx::frag(sA + q * APL + (wm * 64 + i * 32 + l31) * RS + 32 * st + 16 * lh);
@@ -509,11 +527,13 @@ __global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(Con
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
           f32x16 c = acc[i][j];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], c, 0, 0, 0);
+          if (NPL == 3) {   // six cross terms, smallest first
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2 % NPL][i], b[0][j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1 % NPL][i], b[1 % NPL][j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2 % NPL][j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1 % NPL][i], b[0][j], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1 % NPL][j], c, 0, 0, 0);
+          }
           c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], c, 0, 0, 0);
           acc[i][j] = c;
         }
@@ -1250,9 +1270,23 @@ extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H
                                  int Cout, int Hin, int Win, int KH, int KW, int stride,
                                  int pad, int act, float slope, int crop_h, int crop_w,
                                  void* workspace, void* stream) {
+  return ainp_conv_gen_fwd_ex(x0, m0, C0, H0, W0, x1, m1, C1, H1, W1, w, wt, bias, ratio, scale, y,
+                              stats, N, Cout, Hin, Win, KH, KW, stride, pad, act, slope, crop_h,
+                              crop_w, 0, workspace, stream);
+}
+
+extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, int H0, int W0,
+                                    const float* x1, const float* m1, int C1, int H1, int W1,
+                                    const float* w, const float* wt, const float* bias,
+                                    const float* ratio, const float* scale, float* y,
+                                    double* stats, int64_t N, int Cout, int Hin, int Win, int KH,
+                                    int KW, int stride, int pad, int act, float slope, int crop_h,
+                                    int crop_w, int flags, void* workspace, void* stream) {
   if (!x0 || C0 < 1 || C1 < 0 || (C1 > 0 && !x1) || !w || !y || N < 1 || Cout < 1 ||
-      Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 || act < 0 || act > 3)
+      Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 || act < 0 || act > 3 ||
+      (flags & ~AINP_CONV_BF16))
     return record_msg("ainp_conv_gen_fwd: bad argument");
+  const bool b16 = (flags & AINP_CONV_BF16) != 0;
   const int Ho = (Hin + 2 * pad - KH) / stride + 1;
   const int Wo = (Win + 2 * pad - KW) / stride + 1;
   if (Ho < 1 || Wo < 1) return record_msg("ainp_conv_gen_fwd: empty output");
@@ -1317,14 +1351,18 @@ extern "C" int ainp_conv_gen_fwd(const float* x0, const float* m0, int C0, int H
     const char* e = getenv("AINP_CONV_GEN_BK");
     return (e && e[0] == '3') ? 32 : 16;
   }();
-  if (!exact && BM == 128 && xbk == 16)
-    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 16>), grid, dim3(256), 0, s, p, wt, act);
+  if (b16 && BM == 128)   // bf16 operands: one plane, 32-deep K-tiles
+    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 32, 1>), grid, dim3(256), 0, s, p, wt, act);
+  else if (b16)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 32, 1>), grid, dim3(256), 0, s, p, wt, act);
+  else if (!exact && BM == 128 && xbk == 16)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 16, 3>), grid, dim3(256), 0, s, p, wt, act);
   else if (!exact && xbk == 16)
-    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 16>), grid, dim3(256), 0, s, p, wt, act);
+    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 16, 3>), grid, dim3(256), 0, s, p, wt, act);
   else if (!exact && BM == 128)
-    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 32>), grid, dim3(256), 0, s, p, wt, act);
+    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 32, 3>), grid, dim3(256), 0, s, p, wt, act);
   else if (!exact)
-    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 32>), grid, dim3(256), 0, s, p, wt, act);
+    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 32, 3>), grid, dim3(256), 0, s, p, wt, act);
   else if (BM == 128)
     hipLaunchKernelGGL(conv_gen_fwd_kernel<128>, grid, dim3(256), 0, s, p, wt, act);
   else

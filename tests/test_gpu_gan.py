@@ -102,6 +102,36 @@ def test_conv_gen_matches_torch(case):
     assert rel(st[1], (pre * pre).sum((0, 2, 3))) < 1e-5
 
 
+@pytest.mark.parametrize("case", CONV_CASES)
+def test_conv_gen_bf16_matches_torch(case):
+    """AINP_CONV_BF16: gathered (masked, upsampled, concatenated) activations
+    and weights rounded to bf16, fp32 accumulation, fp32 epilogue -- vs an
+    fp64 convolution of the bf16-rounded operands."""
+    from ainp import ops
+    N, C0, C1, Hin, Win, up0, Cout, k, s, p, masks, hb, hr, hs, act = case
+    g = torch.Generator().manual_seed(hash(case) % 1000 + 7)
+    H0, W0 = (Hin // 2, Win // 2) if up0 else (Hin, Win)
+    x0 = torch.randn(N, C0, H0, W0, generator=g)
+    m0 = (torch.rand(N, H0, W0, generator=g) > 0.3).float() if masks else None
+    x1 = torch.randn(N, C1, Hin, Win, generator=g) if C1 else None
+    m1 = (torch.rand(N, Hin, Win, generator=g) > 0.3).float() if (masks and C1) else None
+    w = torch.randn(Cout, C0 + C1, k, k, generator=g) * 0.1
+    Ho, Wo = (Hin + 2 * p - k) // s + 1, (Win + 2 * p - k) // s + 1
+    bias = torch.randn(Cout, generator=g) if hb else None
+    ratio = torch.rand(N, Ho, Wo, generator=g) * 3 if hr else None
+    scale = torch.tensor([0.7]) if hs else None
+    d = lambda t: None if t is None else t.cuda()  # noqa: E731
+    y, _ = ops.conv_gen((d(x0), d(m0)), d(w), src1=(d(x1), d(m1)) if C1 else None, Hin=Hin,
+                        Win=Win, stride=s, pad=p, bias=d(bias), ratio=d(ratio), scale=d(scale),
+                        act=act, bf16=True)
+    bf = lambda t: None if t is None else t.bfloat16().float()  # noqa: E731
+    # mask products are exact (0/1), so rounding x before or after masking agrees
+    yr, _ = _conv_ref(bf(x0), m0, bf(x1), m1, Hin, Win, bf(w), k, s, p, bias, ratio, scale, act)
+    assert rel(y, yr) < 2e-5
+    y32, _ = _conv_ref(x0, m0, x1, m1, Hin, Win, w, k, s, p, bias, ratio, scale, act)
+    assert rel(y, y32) > 1e-5          # a bf16 result, not the fp32-accurate one
+
+
 @pytest.mark.parametrize("k,s,p,crop,act", [(3, 1, 1, (25, 30), 3), (4, 1, 1, None, 0),
                                              (4, 2, 1, None, 2)])
 def test_conv_gen_cout1(k, s, p, crop, act):
@@ -390,3 +420,35 @@ def test_full_size_gan_step_matches_reference(golden_dir):
               "g_vgg_perceptual", "g_vgg_style"):
         r = float(g["oracle_loss/" + k][0])
         assert abs(float(out[k]) - r) <= TOL * max(abs(r), 1e-6), (k, float(out[k]), r)
+
+
+@pytest.mark.timeout(600)
+def test_full_size_gan_step_bf16_tracks_reference(golden_dir):
+    """The full-size B=2 step of gan_step_full.npz in the bf16 configuration
+    (accel.dtype = bf16: bf16 conv / GEMM operands in G, D and VGG, fp32
+    accumulation, BatchNorm statistics and weights): generated spectrogram,
+    D losses and G-step losses within 2e-2 relative of the fp32 reference."""
+    from ainp import gan as G
+    from ainp.gan_train import GanTrainer
+    from golden.gen_golden_r02 import GSTEP, gan_step_inputs
+    g = np.load(os.path.join(golden_dir, "gan_step_full.npz"), allow_pickle=False)
+    orig, imp, mask = gan_step_inputs()
+    torch.manual_seed(GSTEP["g_seed"])
+    Gm = G.PConvUNet()
+    torch.manual_seed(GSTEP["d_seed"])
+    Dm = G.Discriminator()
+    v, _ = _vgg_pair(GSTEP["vgg_seed"])
+    cfg = {"training": dict(R.LAMBDAS, g_lr=2e-4, d_lr=2e-4, b1=0.5, b2=0.999),
+           "accel": {"dtype": "bf16"}}
+    tr = GanTrainer(cfg, Gm.cuda(), Dm.cuda(), vgg=v)
+    assert Dm.ainp_bf16 and v.ainp_bf16
+    out = tr.step(torch.from_numpy(orig).cuda(), torch.from_numpy(imp).cuda(),
+                  torch.from_numpy(mask).cuda())
+    gf = out["generated"].cpu().numpy().reshape(-1)
+    errs = {"generated": rel(gf[::97], g["gen_sample"]),
+            "d_loss": abs(float(out["d_loss"]) - g["d_losses"][0]) / abs(g["d_losses"][0])}
+    for k in ("g_total", "g_l1_valid", "g_l1_hole", "g_vgg_perceptual", "g_vgg_style"):
+        r = float(g["oracle_loss/" + k][0])
+        errs[k] = abs(float(out[k]) - r) / abs(r)
+    print("bf16 GAN step rel errs", errs)
+    assert max(errs.values()) < 2e-2, errs
