@@ -248,7 +248,11 @@ int ainp_bn_stats_reduce(const double* stats, int nparts, double* sums, int C,
  * keeps mean / rstd for the backward; running stats updated in place with
  * momentum and the unbiased variance, as torch.nn.BatchNorm2d in train mode
  * (running_* may both be NULL).  count = elements per channel summed into
- * `sums` (N*H*W, times the world size after an all-reduce). */
+ * `sums` (N*H*W, times the world size after an all-reduce); count == 0: the
+ * count is read from sums[2*C] (a data-parallel caller appends its local
+ * N*H*W to the sums and all-reduces it with them: uneven shards then
+ * normalise with the true global count).  ainp_bn_relu_bwd_apply takes count
+ * the same way (count == 0: its sums[2*C] holds the forward's global count). */
 int ainp_bn_finalize(const double* sums, int64_t count, const float* gamma,
                      const float* beta, float* running_mean,
                      float* running_var, float momentum, float eps,

@@ -59,7 +59,10 @@ class _ConvStackFn(torch.autograd.Function):
         act = (None, None)   # prologue for the next conv
         h = x
         pi = 0
-        count = N * H * W * (comm.world_size if comm is not None else 1)
+        # SyncBN: the local element count rides in the all-reduced sums (sums[2C]),
+        # so ranks with uneven shards still normalise with the global count
+        count = N * H * W
+        count_dev = None
         for bi, (has_bn, bn) in enumerate(spec):
             w, b = params[pi], params[pi + 1]
             pi += 2
@@ -70,11 +73,17 @@ class _ConvStackFn(torch.autograd.Function):
                 gamma, beta = params[pi], params[pi + 1]
                 pi += 2
                 if training:
-                    sums = _allreduce(comm, ops.bn_stats_reduce(stats, y.shape[1]))
+                    C = y.shape[1]
+                    if comm is not None:
+                        sums = _allreduce(comm, ops.bn_stats_reduce(stats, C, count=count))
+                        count_dev = sums[2 * C:]
+                    else:
+                        sums = ops.bn_stats_reduce(stats, C)
                     rm = bn.running_mean if bn.track_running_stats else None
                     rv = bn.running_var if bn.track_running_stats else None
                     mom = bn.momentum if bn.momentum is not None else 0.1
-                    sc, sh, sv = ops.bn_finalize(sums, count, gamma, beta, rm, rv, mom, bn.eps)
+                    sc, sh, sv = ops.bn_finalize(sums, 0 if comm is not None else count, gamma,
+                                                 beta, rm, rv, mom, bn.eps)
                     if bn.track_running_stats:
                         bn.num_batches_tracked.add_(1)
                 else:
@@ -97,6 +106,7 @@ class _ConvStackFn(torch.autograd.Function):
         ctx.out_ntcf = out_ntcf
         ctx.comm = comm
         ctx.count = count
+        ctx.count_dev = count_dev     # global count (device) under SyncBN
         ctx.affine = affine
         ctx.save_for_backward(x, *saved_y, *params)
         ctx.nblocks = len(spec)
@@ -126,8 +136,11 @@ class _ConvStackFn(torch.autograd.Function):
                 sc, sh, sv = ctx.affine[bi]
                 ntcf = ctx.out_ntcf and bi == nb - 1
                 sums = _allreduce(ctx.comm, ops.bn_relu_bwd_reduce(g, y, sc, sh, sv, ntcf))
+                cnt = ctx.count
+                if ctx.count_dev is not None:
+                    sums, cnt = torch.cat([sums, ctx.count_dev]), 0
                 gy, dgam, dbet = ops.bn_relu_bwd_apply(g, y, sc, sh, params[p0 + 2], sv, sums,
-                                                       ctx.count, ntcf)
+                                                       cnt, ntcf)
                 grads[p0 + 2], grads[p0 + 3] = dgam, dbet
             else:
                 gy = g.view_as(y) if g.shape != y.shape else g
@@ -154,7 +167,7 @@ class _BLSTMFn(torch.autograd.Function):
     (w_ih, w_hh, b_ih, b_hh, w_ih_rev, w_hh_rev, b_ih_rev, b_hh_rev)."""
 
     @staticmethod
-    def forward(ctx, x, H, L, bf16, *params):
+    def forward(ctx, x, H, L, bf16, sink, *params):
         N, T, I = x.shape
         NT = N * T
         inp = x.reshape(NT, I)
@@ -171,12 +184,17 @@ class _BLSTMFn(torch.autograd.Function):
             saved += [inp, h, gates, cell]
             inp = h.view(NT, 2 * H)
         ctx.H, ctx.L, ctx.bf16 = H, L, bf16
+        # data parallel: the layer-0 input weights' gradients (89 % of the
+        # gradient bytes, produced late) are handed to the reducer chunk by chunk
+        ctx.sink = sink
+        ctx.wih0 = (params[0], params[4])     # the Parameters themselves
         ctx.save_for_backward(*saved, *params)
         return h
 
     @staticmethod
     def backward(ctx, dh):
         H, L, bf16 = ctx.H, ctx.L, ctx.bf16
+        ctx.early_done = False
         st = ctx.saved_tensors
         saved, params = st[:4 * L], st[4 * L:]
         dh = dh.contiguous()
@@ -199,18 +217,26 @@ class _BLSTMFn(torch.autograd.Function):
             ready = torch.cuda.Event()
             ready.record(main)
             side.wait_event(ready)
+            early = (l == 0 and ctx.sink is not None and ctx.sink.early_ok
+                     and all(p.grad is None for p in ctx.wih0))
             with torch.cuda.stream(side):
                 # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
                 # for the recurrent / upper layers -> parallel split-K over row chunks
                 gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H),
                                          bf16=bf16)
-                gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il, offsets_b=(0, 0),
-                                         bf16=bf16)
+                if early:
+                    gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0)
+                else:
+                    gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il,
+                                             offsets_b=(0, 0), bf16=bf16)
                 db_ih = ops.colsum(dg2)           # b_ih and b_hh get the same gradient
                 db_hh = db_ih.clone()
             for t in (dg, hp, inp):
                 t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l
+            if early:   # p.grad set and reduced by _wih_grad_chunked: nothing for autograd
+                gwi = [None, None]
+                ctx.early_done = True
             grads[base + 0], grads[base + 1] = gwi[0], gwh[0]
             grads[base + 2], grads[base + 3] = db_ih[:4 * H], db_hh[:4 * H]
             grads[base + 4], grads[base + 5] = gwi[1], gwh[1]
@@ -237,8 +263,40 @@ class _BLSTMFn(torch.autograd.Function):
         done.record(side)
         main.wait_event(done)
         for gr in grads:
-            gr.record_stream(main)        # side-stream memory handed to autograd
-        return (dx, None, None, None, *grads)
+            if gr is not None:
+                gr.record_stream(main)    # side-stream memory handed to autograd
+        if ctx.early_done:
+            for p in ctx.wih0:            # side-stream .grad buffers read by the optimizer
+                p.grad.record_stream(main)
+        return (dx, None, None, None, None, *grads)
+
+
+def _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, sink, wih0, rows=None):
+    """dW_ih_l0 (both directions) on the current (side) stream in gate-row
+    chunks of `rows`: dW[r0:r1] = dg[:, r0:r1]^T x, each chunk split-K over
+    the N*T reduction into slabs and summed in fixed order straight into the
+    parameter's .grad buffer, then handed to the reducer, whose SUM all-reduce
+    waits only for that chunk (the 67 MB gradient is produced
+    last; its transfer now starts while the remaining chunks, the layer-0
+    data gradient and the encoder backward run)."""
+    G4 = 4 * H
+    rows = H if rows is None else rows       # one gate (i, f, g, o) per chunk
+    bufs = [torch.empty(G4, Il, device=dg2.device, dtype=torch.float32) for _ in range(2)]
+    tiles = -(-rows // 128) * -(-Il // 128) * 2
+    S = ops._chunks_for(NT, tiles)
+    kc = NT // S
+    slabs = torch.empty(2, S, rows, Il, device=dg2.device, dtype=torch.float32)
+    for r0 in range(0, G4, rows):
+        ops.gemm(rows, Il, kc, [dg2[:, r0:], dg2[:, G4 + r0:]], 1, 8 * H, [inp, inp], Il, 1,
+                 [slabs[0], slabs[1]], Il, 1, strideA=kc * 8 * H, strideB=kc * Il,
+                 strideC=rows * Il, nstrided=S, bf16=bf16)
+        for d in range(2):
+            chunk = bufs[d][r0:r0 + rows]
+            ops.sum_slabs(slabs[d], S, out=chunk.view(-1))
+            sink.reduce_chunk(wih0[d], chunk)
+    for d in range(2):
+        wih0[d].grad = bufs[d]
+    return bufs
 
 
 _SIDE_STREAMS: dict = {}
@@ -384,6 +442,9 @@ class StackedBLSTMCNN(nn.Module):
             nn.Conv2d(self.dec_filters[0], self.in_channels, kernel_size=3, padding=1),
         )
         self.comm = None  # set by ainp.dist for SyncBN across DP ranks
+        # set to an ainp.dist.GradAllReducer (data parallel): the layer-0 input
+        # weight gradients are computed in chunks and all-reduced as they complete
+        self.grad_reducer = None
 
     # -- helpers ----------------------------------------------------------
     @staticmethod
@@ -413,7 +474,9 @@ class StackedBLSTMCNN(nn.Module):
         x = x.contiguous()
         spec, params = self._stack(self.encoder)
         z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, *params)
-        z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, self.bf16, *self.lstm._flat_weights)
+        sink = self.grad_reducer if (self.training and torch.is_grad_enabled()) else None
+        z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, self.bf16, sink,
+                           *self.lstm._flat_weights)
         # model.py:82 hard-codes 16 decoder channels
         p = _ProjFn.apply(z, self.projection.weight, self.projection.bias, 16, freq_bins,
                           self.bf16)

@@ -22,24 +22,41 @@ import torch.distributed as dist
 
 
 class Comm:
-    """All-reduce helper bound to a process group."""
+    """All-reduce helper bound to two process groups over the same ranks:
 
-    def __init__(self, group=None):
+    group       the synchronous, latency-bound exchanges the model makes
+                mid-step (SyncBN sums, the VGG target max, loss normalisers);
+    grad_group  the gradient buckets (GradAllReducer).
+
+    On RCCL a process group is one communicator whose collectives run in FIFO
+    order on its own stream.  Sharing one would queue the encoder's SyncBN
+    backward exchange behind the 34 MB W_ih_l0 gradient buckets, and the
+    compute stream waits on SyncBN.  With separate communicators the gradient
+    all-reduce overlaps the rest of the backward."""
+
+    def __init__(self, group=None, grad_group="new"):
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         # gloo with GPU tensors (the multi-rank tests on a one-GPU box): stage
         # through host memory; RCCL ("nccl") reduces device tensors directly
         self.host_staging = dist.get_backend(group) == "gloo"
+        if grad_group == "new":
+            # collective call: every rank constructs its Comm at the same point
+            ranks = dist.get_process_group_ranks(group) if group is not None else \
+                list(range(self.world_size))
+            grad_group = dist.new_group(ranks=ranks) if self.world_size > 1 else group
+        self.grad_group = grad_group
 
-    def _allreduce(self, t: torch.Tensor, op) -> torch.Tensor:
+    def _allreduce(self, t: torch.Tensor, op, group="sync") -> torch.Tensor:
+        g = self.group if group == "sync" else group
         if self.world_size > 1:
             if self.host_staging and t.is_cuda:
                 h = t.cpu()
-                dist.all_reduce(h, op=op, group=self.group)
+                dist.all_reduce(h, op=op, group=g)
                 t.copy_(h)
             else:
-                dist.all_reduce(t, op=op, group=self.group)
+                dist.all_reduce(t, op=op, group=g)
         return t
 
     def allreduce_sum_(self, t: torch.Tensor) -> torch.Tensor:
@@ -47,6 +64,21 @@ class Comm:
 
     def allreduce_max_(self, t: torch.Tensor) -> torch.Tensor:
         return self._allreduce(t, dist.ReduceOp.MAX)
+
+    def broadcast_module_(self, module: torch.nn.Module, src: int = 0) -> torch.nn.Module:
+        """Every parameter and buffer from rank `src` (as DDP does at wrap
+        time): identical starting weights no matter how each rank's RNG was
+        consumed, and after a resume."""
+        if self.world_size > 1:
+            with torch.no_grad():
+                for t in list(module.parameters()) + list(module.buffers()):
+                    if self.host_staging and t.is_cuda:
+                        h = t.detach().cpu()
+                        dist.broadcast(h, src, group=self.group)
+                        t.copy_(h)
+                    else:
+                        dist.broadcast(t.data, src, group=self.group)
+        return module
 
 
 class _Done:
@@ -76,18 +108,50 @@ class GradAllReducer:
     def __init__(self, params, comm: Comm, bucket_bytes: int = 32 << 20, overlap: bool = True):
         self.params = [p for p in params if p.requires_grad]
         self.comm = comm
+        self.group = getattr(comm, "grad_group", comm.group)
         self.bucket_bytes = bucket_bytes
         self.overlap = overlap and comm.world_size > 1
         self._open, self._open_bytes = [], 0
         self._inflight = []          # (work, params, flat or None)
         self._seen = set()           # params queued since the last allreduce()
+        self._chunked = set()        # params reduced chunk by chunk since then
         self._hooks = []
+        self.paused = False          # hooks ignore gradients (e.g. a discarded backward)
         if self.overlap:
             for p in self.params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._ready))
 
+    # -- chunked early reduction ------------------------------------------------
+    @property
+    def early_ok(self):
+        """The model may hand gradient chunks over as they are computed."""
+        return self.overlap and not self.paused
+
+    @torch.no_grad()
+    def reduce_chunk(self, p, chunk: torch.Tensor):
+        """All-reduce (SUM) one finished chunk of p's gradient now, from the
+        caller's current stream: the collective waits for exactly the work
+        queued on that stream (e.g. a side-stream weight-gradient GEMM) rather
+        than for everything on the compute stream.  The caller owns p.grad
+        (it sets it to the full buffer); allreduce() waits for the chunk."""
+        self._seen.add(id(p))
+        self._chunked.add(id(p))
+        if self.comm.host_staging and chunk.is_cuda:
+            self.comm._allreduce(chunk, dist.ReduceOp.SUM, group=self.group)
+            work = _Done()
+        else:
+            work = dist.all_reduce(chunk, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        self._inflight.append((work, [], None))
+        self.early_chunks += 1
+
+    early_chunks = 0
+
     # -- overlapped path ------------------------------------------------------
     def _ready(self, p):
+        # the accumulate hook may still fire for a parameter whose .grad the
+        # model set itself and handed over chunk by chunk (reduce_chunk)
+        if self.paused or id(p) in self._chunked:
+            return
         if id(p) in self._seen:
             raise RuntimeError("GradAllReducer: a gradient became ready twice before "
                                "allreduce() (one backward per allreduce())")
@@ -115,10 +179,10 @@ class GradAllReducer:
             flat = torch.cat([p.grad.reshape(-1) for p in bucket])
             t = flat
         if self.comm.host_staging and t.is_cuda:
-            self.comm.allreduce_sum_(t)
+            self.comm._allreduce(t, dist.ReduceOp.SUM, group=self.group)
             work = _Done()
         else:
-            work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.comm.group, async_op=True)
+            work = dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._inflight.append((work, bucket, flat))
 
     @torch.no_grad()
@@ -172,6 +236,7 @@ class GradAllReducer:
                     self._ready(p)
             self._finish()
             self._seen.clear()
+            self._chunked.clear()
             return
         for bucket in self._buckets():
             self._launch(bucket)
@@ -187,9 +252,12 @@ def init_from_env(backend: str | None = None):
     rank = int(os.environ["RANK"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        torch.cuda.set_device(local)
+        # AINP_DIST_BACKEND=gloo: rehearse several ranks on one GPU (RCCL needs
+        # one GPU per rank); default RCCL ("nccl") when GPUs are present
+        backend = os.environ.get("AINP_DIST_BACKEND") or \
+            ("nccl" if torch.cuda.is_available() else "gloo")
+    if backend == "nccl" or torch.cuda.is_available():
+        torch.cuda.set_device(local if backend == "nccl" else local % max(1, torch.cuda.device_count()))
     if not dist.is_initialized():
         dist.init_process_group(backend=backend, rank=rank, world_size=ws)
     return rank, ws, local

@@ -47,11 +47,13 @@ def _bn_affine(bn: nn.BatchNorm2d, stats, count, C):
     are then all-reduced (SyncBN), so every rank normalises with the statistics
     of the global batch, as the single-process reference does."""
     if bn.training or not bn.track_running_stats:
-        sums = ops.bn_stats_reduce(stats, C)
         comm = getattr(bn, "ainp_comm", None)
         if comm is not None and comm.world_size > 1:
-            comm.allreduce_sum_(sums)
-            count = count * comm.world_size
+            # the local count rides in sums[2C]: uneven shards get the true global count
+            sums = comm.allreduce_sum_(ops.bn_stats_reduce(stats, C, count=count))
+            count = 0
+        else:
+            sums = ops.bn_stats_reduce(stats, C)
         rm = bn.running_mean if bn.track_running_stats else None
         rv = bn.running_var if bn.track_running_stats else None
         mom = bn.momentum if bn.momentum is not None else 0.1

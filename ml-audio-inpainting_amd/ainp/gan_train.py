@@ -39,6 +39,10 @@ class GanTrainer:
         self.reducer = None
         if comm is not None and comm.world_size > 1:
             from .dist import GradAllReducer
+            # identical starting weights on every rank (as DDP broadcasts at wrap time)
+            for m in (generator, discriminator, vgg):
+                if m is not None:
+                    comm.broadcast_module_(m)
             self.reducer = GradAllReducer(discriminator.parameters(), comm)
             # SyncBN for G's BatchNorms and the global VGG target max: the
             # N-rank step then equals the 1-process step on the whole batch
@@ -74,7 +78,15 @@ class GanTrainer:
             d_fake_g = self.D(generated)
             losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g, self.vgg,
                                         comm=self.comm)
-            losses["g_total"].backward()
+            # this backward only fills D grads that the next zero_grad discards
+            # (SURVEY Q1): they are not exchanged, so the reducer ignores them
+            if self.reducer is not None:
+                self.reducer.paused = True
+            try:
+                losses["g_total"].backward()
+            finally:
+                if self.reducer is not None:
+                    self.reducer.paused = False
         else:
             with torch.no_grad():
                 d_fake_g = self.D(generated)

@@ -298,15 +298,22 @@ def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=Fals
 
 
 # --------------------------------------------------------------------- BN
-def bn_stats_reduce(stats, C):
-    """conv epilogue partials [parts, 2C] -> per-channel [sum y | sum y^2] (f64)."""
-    sums = torch.empty(2 * C, device=stats.device, dtype=torch.float64)
+def bn_stats_reduce(stats, C, count=None):
+    """conv epilogue partials [parts, 2C] -> per-channel [sum y | sum y^2] (f64).
+    count (data parallel): appended as sums[2C], so that all-reducing the
+    vector also sums the element counts; then pass count=0 to bn_finalize /
+    bn_relu_bwd_apply (include/ainp.h)."""
+    sums = torch.empty(2 * C + (1 if count is not None else 0), device=stats.device,
+                       dtype=torch.float64)
     call("ainp_bn_stats_reduce", stats.data_ptr(), stats.shape[0], sums.data_ptr(), C,
          _stream(stats))
+    if count is not None:
+        sums[2 * C:].fill_(float(count))
     return sums
 
 
 def bn_finalize(sums, count, gamma, beta, running_mean, running_var, momentum, eps):
+    """count == 0: the count is sums[2C] (see bn_stats_reduce)."""
     C = sums.numel() // 2
     dev = sums.device
     scale = torch.empty(C, device=dev, dtype=torch.float32)

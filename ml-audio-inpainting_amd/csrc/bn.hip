@@ -50,6 +50,9 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums,
                                    float* __restrict__ save, int C) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
+  // count <= 0: the element count travels with the sums (sums[2C], all-reduced
+  // with them by a data-parallel caller, so uneven shards normalise correctly)
+  if (count <= 0) count = (int64_t)sums[2 * C];
   const double mean = sums[c] / (double)count;
   double var = sums[C + c] / (double)count - mean * mean;
   if (var < 0.0) var = 0.0;
@@ -241,8 +244,9 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
   const int64_t off = plane * HW + o0;
   const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
   const float k = (gamma ? gamma[c] : 1.f) * rstd;
-  const float m1 = (float)(sums[c] * inv_count);
-  const float m2 = (float)(sums[C + c] * inv_count);
+  const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C];   // see bn_finalize
+  const float m1 = (float)(sums[c] * ic);
+  const float m2 = (float)(sums[C + c] * ic);
   if (VEC) {
     const float2* g2 = reinterpret_cast<const float2*>(g + off);
     const float2* y2 = reinterpret_cast<const float2*>(y + off);
@@ -349,8 +353,9 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
   const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
   if (APPLY) {
     const float k = (gamma ? gamma[c] : 1.f) * rstd;
-    const float m1 = (float)(sums[c] * inv_count);
-    const float m2 = (float)(sums[C + c] * inv_count);
+    const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C];   // see bn_finalize
+    const float m1 = (float)(sums[c] * ic);
+    const float m2 = (float)(sums[C + c] * ic);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int64_t h = h0 + q + 4 * i, w = w0 + lane;
@@ -474,8 +479,9 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
     const int c = (int)(k / H);
     const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
     const float kc = (gamma ? gamma[c] : 1.f) * rstd;
-    const float m1 = (float)(sums[c] * inv_count);
-    const float m2 = (float)(sums[C + c] * inv_count);
+    const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C];   // see bn_finalize
+    const float m1 = (float)(sums[c] * ic);
+    const float m2 = (float)(sums[C + c] * ic);
     const float gz0 = fmaf(yv[i].x, sc, sh) > 0.f ? tile[2 * l][kk] : 0.f;
     const float gz1 = fmaf(yv[i].y, sc, sh) > 0.f ? tile[2 * l + 1][kk] : 0.f;
     float2 o;
@@ -515,7 +521,7 @@ extern "C" int ainp_bn_finalize(const double* sums, int64_t count,
                                 float momentum, float eps, float* scale,
                                 float* shift, float* save_mean_rstd, int C,
                                 void* stream) {
-  if (!sums || !scale || !shift || !save_mean_rstd || C < 1 || count < 1 ||
+  if (!sums || !scale || !shift || !save_mean_rstd || C < 1 || count < 0 ||
       ((running_mean == nullptr) != (running_var == nullptr)))
     return record_msg("ainp_bn_finalize: bad argument");
   hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(64), 0,
@@ -612,10 +618,10 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
                                       int64_t N, int C, int64_t H, int64_t W,
                                       int g_ntcf, void* stream) {
   if (!g || !y || !scale || !shift || !save_mean_rstd || !sums || !gy ||
-      N < 1 || C < 1 || H < 1 || W < 1 || count < 1)
+      N < 1 || C < 1 || H < 1 || W < 1 || count < 0)
     return record_msg("ainp_bn_relu_bwd_apply: bad argument");
   const int64_t blocks = N * C * tiles_per_plane(H, W);
-  const double inv_count = 1.0 / (double)count;
+  const double inv_count = count > 0 ? 1.0 / (double)count : 0.0;   // 0: sums[2C]
   hipStream_t s = as_stream(stream);
   if (!g_ntcf) {
     const int64_t HW = H * W;

@@ -40,32 +40,45 @@ def _cnnblstm_batch(n=4, F=33, T=24):
     return x, mask, tgt
 
 
-def run_cnnblstm(comm=None, rank=0, world=1):
+def run_cnnblstm(comm=None, rank=0, world=1, uneven=False, steps=1):
+    """uneven: rank 0 takes 3 of the 4 examples, rank 1 one (SyncBN must use
+    the global element count).  The ranks start from different seeds and get
+    rank 0's weights by broadcast; the layer-0 input weights' gradients go to
+    the reducer chunk by chunk (model.grad_reducer)."""
     from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
     from ainp.dist import GradAllReducer
     from ainp.optim import Adam
     dev = torch.device("cuda", 0)
-    torch.manual_seed(0)
+    torch.manual_seed(0 if comm is None else 100 * rank)
     model = StackedBLSTMCNN(config=CNNBLSTM_CFG).to(dev).train()
+    if comm is not None:
+        comm.broadcast_module_(model)
     model.comm = comm
     opt = Adam(model.parameters(), lr=1e-3)
     red = GradAllReducer(model.parameters(), comm) if comm is not None else None
+    model.grad_reducer = red
     x, mask, tgt = _cnnblstm_batch()
-    per = x.shape[0] // world
-    sl = slice(rank * per, (rank + 1) * per)
+    if uneven and world == 2:
+        sl = slice(0, 3) if rank == 0 else slice(3, 4)
+    else:
+        per = x.shape[0] // world
+        sl = slice(rank * per, (rank + 1) * per)
     x, mask, tgt = x[sl].to(dev), mask[sl].to(dev), tgt[sl].to(dev)
-    opt.zero_grad()
-    loss = l1_pow10_loss(model(x), mask, tgt)
-    loss.backward()
-    if red is not None:
-        red.allreduce()
-    opt.step()
+    early = 0
+    for _ in range(steps):
+        opt.zero_grad()
+        loss = l1_pow10_loss(model(x), mask, tgt)
+        loss.backward()
+        if red is not None:
+            early = red.early_chunks
+            red.allreduce()
+        opt.step()
     loss = loss.detach().double().reshape(1)
     if comm is not None:
         comm.allreduce_sum_(loss)            # the reference loss is a batch SUM
     torch.cuda.synchronize()
     state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    return {"loss": loss.cpu(), "state": state}
+    return {"loss": loss.cpu(), "state": state, "early_chunks": early}
 
 
 def _gan_batch(n=2, F=257, T=100):
@@ -78,7 +91,9 @@ def _gan_batch(n=2, F=257, T=100):
     return orig, imp, mask
 
 
-def run_gan(comm=None, rank=0, world=1):
+def run_gan(comm=None, rank=0, world=1, faithful=False, steps=1):
+    """faithful: GanTrainer(faithful_g_backward=True), whose G-step backward
+    fills D grads that must not reach the gradient reducer."""
     from ainp import gan as G
     from ainp.gan_train import GanTrainer
     dev = torch.device("cuda", 0)
@@ -86,11 +101,12 @@ def run_gan(comm=None, rank=0, world=1):
     gen = G.PConvUNet().to(dev)
     disc = G.Discriminator().to(dev)
     vgg = G.VGGLoss(dev)
-    tr = GanTrainer(GAN_CFG, gen, disc, vgg, comm=comm)
+    tr = GanTrainer(GAN_CFG, gen, disc, vgg, comm=comm, faithful_g_backward=faithful)
     orig, imp, mask = _gan_batch()
     per = orig.shape[0] // world
     sl = slice(rank * per, (rank + 1) * per)
-    out = tr.step(orig[sl].to(dev), imp[sl].to(dev), mask[sl].to(dev))
+    for _ in range(steps):
+        out = tr.step(orig[sl].to(dev), imp[sl].to(dev), mask[sl].to(dev))
     torch.cuda.synchronize()
     losses = {k: v.detach().double().cpu() for k, v in out.items() if k != "generated"}
     dstate = {k: v.detach().cpu().clone() for k, v in disc.state_dict().items()}
@@ -107,7 +123,15 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = Comm()
-    res = (run_cnnblstm if mode == "cnnblstm" else run_gan)(comm, rank, world)
+    assert comm.grad_group is not comm.group     # SyncBN and gradients: two communicators
+    if mode == "cnnblstm":
+        res = run_cnnblstm(comm, rank, world)
+    elif mode == "cnnblstm_uneven":
+        res = run_cnnblstm(comm, rank, world, uneven=True, steps=2)
+    elif mode == "gan_faithful":
+        res = run_gan(comm, rank, world, faithful=True, steps=2)
+    else:
+        res = run_gan(comm, rank, world)
     torch.save(res, f"{out}.{rank}")
     dist.barrier()
     dist.destroy_process_group()

@@ -186,3 +186,49 @@ def test_dp_two_ranks_match_single_process():
             continue
         rel = np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30)
         assert rel < 1e-5, (k, rel)
+
+
+def _groups_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "ml-audio-inpainting_amd"))
+    from ainp.dist import Comm, GradAllReducer
+    comm = Comm()
+    # SyncBN / scalars and gradient buckets on distinct process groups
+    # (distinct RCCL communicators and streams on the GPU)
+    distinct = comm.grad_group is not comm.group and comm.grad_group is not None
+    p = torch.nn.Parameter(torch.full((3,), float(rank + 1)))
+    red = GradAllReducer([p], comm)
+    assert red.group is comm.grad_group
+    p.grad = torch.full((3,), float(rank + 1))
+    red.allreduce()
+    # broadcast from rank 0 over the sync group
+    m = torch.nn.Linear(2, 2)
+    torch.nn.init.constant_(m.weight, float(rank))
+    comm.broadcast_module_(m)
+    # paused reducer ignores gradients
+    red.paused = True
+    red._ready(p)
+    ignored = id(p) not in red._seen
+    red.paused = False
+    q.put((rank, distinct, p.grad.tolist(), float(m.weight.sum()), ignored))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_comm_groups_broadcast_and_pause():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_groups_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, distinct, grad, wsum, ignored in res:
+        assert distinct and ignored
+        assert grad == [3.0, 3.0, 3.0]
+        assert wsum == 0.0          # rank 0's weights everywhere
