@@ -510,6 +510,15 @@ int ainp_flac_info(const uint8_t* data, size_t n, int* sample_rate, int* channel
                    int* bits_per_sample, int64_t* total_samples, uint8_t* md5);
 int ainp_flac_decode(const uint8_t* data, size_t n, int32_t* out, int64_t max_frames,
                      int64_t* n_frames);
+/* Writer behind utils.save_audio (utils.py:84-87: soundfile FLAC, PCM_16)
+ * for add_gaps.py / pre_process_dataset.py: interleaved signed samples
+ * [frames][channels] -> a complete .flac file image in out[0..*out_len)
+ * (STREAMINFO with the samples' MD5; 4096-sample blocks; CONSTANT / FIXED
+ * 0-4 + partitioned Rice / VERBATIM subframes).  bits 8, 16 or 24.
+ * ainp_flac_encode_bound: a sufficient `cap`. */
+size_t ainp_flac_encode_bound(int64_t frames, int channels, int bits_per_sample);
+int ainp_flac_encode(const int32_t* samples, int64_t frames, int channels, int bits_per_sample,
+                     int sample_rate, uint8_t* out, size_t cap, size_t* out_len);
 
 #ifdef __cplusplus
 }

@@ -109,6 +109,8 @@ _SIGS = {
     "ainp_vgg_target_max": (c_int, [P, c_int64, P, P]),
     "ainp_flac_info": (c_int, [P, c_size_t, P, P, P, P, P]),
     "ainp_flac_decode": (c_int, [P, c_size_t, P, c_int64, P]),
+    "ainp_flac_encode_bound": (c_size_t, [c_int64, c_int, c_int]),
+    "ainp_flac_encode": (c_int, [P, c_int64, c_int, c_int, c_int, P, c_size_t, P]),
     "ainp_sn_workspace": (c_size_t, [c_int, c_int]),
     "ainp_sn_power": (c_int, [PP, PP, PP, P, P, c_int, c_float, P, c_int, P, c_int, P]),
     "ainp_sn_weight_grad": (c_int, [P, c_int, P, P, P, P, c_int, c_int, P, P, P, P]),

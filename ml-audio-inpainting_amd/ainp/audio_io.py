@@ -46,4 +46,35 @@ def read_flac(path):
     return pcm.astype(np.float32) * scale, info["sample_rate"]
 
 
-__all__ = ["flac_info", "decode_flac", "read_flac", "lib"]
+def encode_flac(pcm: np.ndarray, sample_rate: int, bits_per_sample: int = 16) -> bytes:
+    """Integer samples [frames] or [frames, channels] -> FLAC file bytes
+    (ainp_flac_encode: lossless, STREAMINFO MD5 set)."""
+    pcm = np.asarray(pcm)
+    if pcm.ndim == 1:
+        pcm = pcm[:, None]
+    x = np.ascontiguousarray(pcm, dtype=np.int32)
+    frames, ch = x.shape
+    cap = int(lib.ainp_flac_encode_bound(frames, ch, bits_per_sample))
+    out = np.empty(max(cap, 1), dtype=np.uint8)
+    n = ctypes.c_size_t()
+    call("ainp_flac_encode", x.ctypes.data, frames, ch, int(bits_per_sample), int(sample_rate),
+         out.ctypes.data, cap, ctypes.byref(n))
+    return out[:n.value].tobytes()
+
+
+def write_flac(path, audio: np.ndarray, sample_rate: int) -> None:
+    """soundfile.write(path, float_audio, sr) with the FLAC default subtype
+    PCM_16: libsndfile's conversion lrint(x * 0x7FFF) (round half to even),
+    in float32 for float32 data (sf_write_float) and float64 otherwise
+    (sf_write_double), then the native encoder."""
+    a = np.asarray(audio)
+    if a.dtype == np.float32:
+        pcm = np.rint(a * np.float32(32767.0))
+    else:
+        pcm = np.rint(a.astype(np.float64) * 32767.0)
+    pcm = np.clip(pcm, -32768, 32767).astype(np.int32)
+    with open(path, "wb") as f:
+        f.write(encode_flac(pcm, sample_rate, 16))
+
+
+__all__ = ["flac_info", "decode_flac", "read_flac", "encode_flac", "write_flac", "lib"]

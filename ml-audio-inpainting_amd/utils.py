@@ -130,6 +130,10 @@ def save_audio(audio_data: np.ndarray, file_path: Union[str, Path],
                 w.setsampwidth(2)
                 w.setframerate(int(sample_rate))
                 w.writeframes(pcm.tobytes())
+        elif file_format.lower() == "flac":
+            # soundfile's FLAC / PCM_16 write on the native encoder (csrc/flac.cpp)
+            from ainp.audio_io import write_flac
+            write_flac(str(file_path), audio_data, int(sample_rate))
         else:
             import soundfile as sf
             sf.write(file_path, audio_data, sample_rate, format=file_format)

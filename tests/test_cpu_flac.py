@@ -116,3 +116,103 @@ def test_decoder_stream_features(case):
     assert info["bits_per_sample"] == bps and info["channels"] == nch
     np.testing.assert_array_equal(out, pcm)
     assert hashlib.md5(_pcm_bytes(out, bps)).digest() == info["md5"]
+
+
+# ----------------------------------------------------------------- encoder
+@pytest.mark.parametrize("frames,ch,bits", [(80000, 1, 16), (4096, 1, 16), (4097, 2, 16),
+                                             (1, 1, 16), (0, 1, 16), (12345, 2, 24),
+                                             (5000, 1, 8)])
+def test_encoder_roundtrip_bit_exact(frames, ch, bits):
+    """ainp_flac_encode -> ainp_flac_decode returns the samples bit for bit;
+    STREAMINFO carries the right MD5 (computed as FLAC defines it)."""
+    import hashlib
+    from ainp.audio_io import decode_flac, encode_flac
+    from ainp.synth import synthetic_clip
+    rng = np.random.default_rng(frames + ch + bits)
+    lim = 1 << (bits - 1)
+    if frames >= 4096:
+        clip = synthetic_clip(frames, frames) * (lim - 1)
+        pcm = np.stack([np.rint(clip * (0.5 + 0.5 * c)) for c in range(ch)], 1).astype(np.int32)
+        pcm[:50] = 7                              # a constant run
+        pcm[100:130] = rng.integers(-lim, lim, size=(30, ch))   # full-scale noise
+    else:
+        pcm = rng.integers(-lim, lim, size=(frames, ch)).astype(np.int32)
+    data = encode_flac(pcm, 16000, bits)
+    out, info = decode_flac(data)
+    assert info["total_samples"] == frames and info["channels"] == ch
+    assert info["bits_per_sample"] == bits and info["sample_rate"] == 16000
+    np.testing.assert_array_equal(out, pcm)
+    le = pcm.astype(f"<i{4}").view(np.uint8).reshape(-1, 4)[:, :(bits + 7) // 8].tobytes()
+    assert info["md5"] == hashlib.md5(le).digest()
+    if frames >= 80000:      # the predictor + Rice coder compresses (noisy) harmonic audio
+        assert len(data) < 0.7 * frames * ch * 2
+
+
+def test_encoder_on_librispeech_fixtures(golden_dir):
+    """Re-encoding the bundled LibriSpeech clips is lossless and within 1.3x
+    of the size the reference's encoder (libFLAC) produced."""
+    from ainp.audio_io import decode_flac, encode_flac
+    d = os.path.join(golden_dir, "flac")
+    for name in sorted(os.listdir(d))[:3]:
+        raw = open(os.path.join(d, name), "rb").read()
+        pcm, info = decode_flac(raw)
+        data = encode_flac(pcm, info["sample_rate"], info["bits_per_sample"])
+        out, info2 = decode_flac(data)
+        np.testing.assert_array_equal(out, pcm)
+        assert info2["md5"] == info["md5"]
+        assert len(data) < 1.3 * len(raw), (name, len(data), len(raw))
+
+
+def test_save_audio_flac_roundtrip(tmp_path):
+    """utils.save_audio(.flac) (peak-normalised, PCM_16) is read back by
+    utils.load_audio as libsndfile would: x / max|x| quantised by 32767."""
+    import utils
+    from ainp.synth import synthetic_clip
+    x = synthetic_clip(9, 16000) * 0.3
+    p = tmp_path / "sub" / "a.flac"
+    utils.save_audio(x, p, 16000)
+    y, sr = utils.load_audio(str(p), sample_rate=16000, max_len=1)
+    assert sr == 16000
+    n = x / np.abs(x).max()                      # float32, as save_audio normalises it
+    ref = np.rint(n * np.float32(32767.0)) / 32768.0
+    np.testing.assert_array_equal(y, ref.astype(np.float32))
+
+
+def test_pre_process_dataset_on_a_librispeech_tree(tmp_path, golden_dir):
+    """pre_process_dataset.py:20-43 end to end on a LibriSpeech-shaped tree
+    (speaker/chapter/*.flac, here two bundled clips): mirrored tree, FLAC
+    output, 5 s (load_audio's max_len), one 0.1 s zero gap, peak-normalised."""
+    import shutil
+    import pre_process_dataset
+    from ainp.audio_io import read_flac
+    src = tmp_path / "LibriSpeech" / "train"
+    names = sorted(os.listdir(os.path.join(golden_dir, "flac")))[:2]
+    for i, name in enumerate(names):
+        d = src / f"{100 + i}" / "200"
+        d.mkdir(parents=True)
+        shutil.copy(os.path.join(golden_dir, "flac", name), d / name)
+    dst = tmp_path / "processed"
+    np.random.seed(3)
+    assert pre_process_dataset.process(str(src), str(dst)) == 2
+    for i, name in enumerate(names):
+        y, sr = read_flac(dst / f"{100 + i}" / "200" / name)
+        y = y[:, 0]
+        assert sr == 16000 and len(y) == 80000
+        assert np.abs(y).max() == np.float32(32767 / 32768)
+        z = (y == 0).astype(np.int8)
+        run, best = 0, 0
+        for v in z:
+            run = run + 1 if v else 0
+            best = max(best, run)
+        assert best >= 1600
+
+
+def test_add_gaps_writes_flac(tmp_path, golden_dir):
+    import add_gaps
+    from ainp.audio_io import read_flac
+    name = sorted(os.listdir(os.path.join(golden_dir, "flac")))[0]
+    out = tmp_path / "gap.flac"
+    y_new = add_gaps.insert_gap_file(os.path.join(golden_dir, "flac", name), out, 1.0, 0.25)
+    y, sr = read_flac(out)
+    assert not np.any(y[16000:20000, 0])
+    np.testing.assert_array_equal(y[:, 0], np.rint(y_new * np.float32(32767)) / 32768)
