@@ -246,8 +246,24 @@ class PConvUNet(nn.Module):
         if final_dec_cfg["out_ch"] != 1:
             raise NotImplementedError("out_ch must be 1 (the reference's configuration)")
 
-    @torch.no_grad()
     def forward(self, x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
+        """Forward only: the reference never back-propagates into G (its
+        optimizer step has no gradients), so there is no G backward
+        on this path.  Called with autograd enabled it warns once and returns a
+        tensor detached from G's parameters."""
+        if torch.is_grad_enabled() and not PConvUNet._warned_no_grad and \
+                any(p.requires_grad for p in self.parameters()):
+            import warnings
+            warnings.warn("ainp PConvUNet.forward is forward-only (no generator backward, "
+                          "SURVEY Q1): its output carries no gradient to G's parameters",
+                          stacklevel=2)
+            PConvUNet._warned_no_grad = True
+        with torch.no_grad():
+            return self._forward(x, mask)
+
+    _warned_no_grad = False
+
+    def _forward(self, x, mask):
         if x.shape[1] != self.input_channels:
             raise ValueError(f"Input x channels ({x.shape[1]}) != expected ({self.input_channels})")
         if mask.shape[1] != self.mask_channels:

@@ -9,10 +9,14 @@ blstm_cnn_epoch_{n}.pt every checkpoint_interval epochs.
 
 Differences (documented): the batch reshape uses the actual batch size (the
 reference crashes on a partial last batch); resume loads with
-weights_only=True; spectrogram figures and Griffin-Lim audio logging are not
-produced (plotting is out of scope, ISTFT/GL is SURVEY §8 f1).
+weights_only=True; spectrogram figures are not produced (plotting is out of
+scope); the audio samples are (train.py:178-189, every audio_interval steps on
+the GPU ISTFT / Griffin-Lim, with the reference's default hop of 512 -- the
+call passes only n_fft).
 Data parallel: launched under torchrun (WORLD_SIZE > 1) each rank trains on a
-DistributedSampler shard with SUM-all-reduced gradients and SyncBN.
+DistributedSampler shard with SUM-all-reduced gradients and SyncBN; rank 0's
+initial weights are broadcast; the layer-0 input-weight gradient is
+all-reduced chunk by chunk as the BLSTM backward produces it (model.grad_reducer).
 """
 from __future__ import annotations
 
@@ -44,6 +48,9 @@ class _NullWriter:
     def add_scalar(self, *a, **k):
         pass
 
+    def add_audio(self, *a, **k):
+        pass
+
     def close(self):
         pass
 
@@ -63,6 +70,32 @@ def _flatten(batch):
             gm.reshape(n, gm.shape[2], gm.shape[3]), tg.reshape(n, tg.shape[2], tg.shape[3]))
 
 
+def save_audio_samples(writer, model, config, x, mask, target, sample_dir, global_step):
+    """train.py:178-189 on the first item of the last test batch: the clean
+    complex spectrogram and the gapped one (target * (1 - mask)) through the
+    ISTFT, the reconstruction 10**reconstruct_spectrogram through Griffin-Lim
+    (n_iter 64); spectrogram_to_audio gets only n_fft, so hop_length is its
+    default 512 (reference quirk kept)."""
+    import utils
+    n_fft, sr = config["data"]["spectrogram"]["n_fft"], config["data"]["sample_rate"]
+    with torch.no_grad():
+        rec = (10 ** model.reconstruct_spectrogram(x, mask))[0].float().contiguous()
+    orig = target[0].contiguous()
+    gap = (target[0] * (1 - mask[0])).contiguous()
+    audio = {
+        "orig": utils.spectrogram_to_audio(orig, phase_info=True, n_fft=n_fft),
+        "gap": utils.spectrogram_to_audio(gap, phase_info=True, n_fft=n_fft),
+        "reconstructed": utils.spectrogram_to_audio(rec, phase_info=False, n_fft=n_fft),
+    }
+    audio = {k: v.cpu().numpy() for k, v in audio.items()}
+    for k, v in audio.items():
+        utils.save_audio(v, Path(sample_dir) / f"{k}_audio_{global_step}.flac")
+    for tag, k in (("Audio/Original", "orig"), ("Audio/Impaired", "gap"),
+                   ("Audio/Generated", "reconstructed")):
+        writer.add_audio(tag, audio[k], global_step, sample_rate=sr)
+    return audio
+
+
 def main(config_path="cnn_blstm.yaml"):
     with open(config_path, "r") as f:
         config = yaml.safe_load(f)
@@ -77,6 +110,8 @@ def main(config_path="cnn_blstm.yaml"):
     model.to(device)
     comm = Comm() if world > 1 else None
     model.comm = comm
+    if comm is not None:
+        comm.broadcast_module_(model)
 
     BATCH_SIZE = config["training"]["batch_size"]
     train_dataset = LibriSpeechDataset(config_path, dataset_type="train", device=device)
@@ -93,9 +128,9 @@ def main(config_path="cnn_blstm.yaml"):
     run_name = datetime.today().strftime("%Y_%m_%d_%H%M")
     tb_dir = Path(paths_cfg["tensorboard_dir"]) / run_name
     chkpt_dir = Path(paths_cfg["checkpoint_dir"]) / run_name
+    sample_dir = Path(paths_cfg["sample_dir"]) / run_name
     if rank == 0:
-        for d in (tb_dir, chkpt_dir, Path(paths_cfg["sample_dir"]) / run_name,
-                  Path(paths_cfg["log_dir"])):
+        for d in (tb_dir, chkpt_dir, sample_dir, Path(paths_cfg["log_dir"])):
             d.mkdir(parents=True, exist_ok=True)
     writer = _writer(tb_dir) if rank == 0 else _NullWriter()
 
@@ -104,6 +139,7 @@ def main(config_path="cnn_blstm.yaml"):
     else:
         raise ValueError("only optimizer_type: adam is used by the reference")
     reducer = GradAllReducer(model.parameters(), comm) if comm is not None else None
+    model.grad_reducer = reducer
 
     num_epochs = config["training"]["max_n_epochs"]
     global_step = 0
@@ -132,11 +168,16 @@ def main(config_path="cnn_blstm.yaml"):
 
         model.eval()
         running_test_loss = 0.0
+        last = None
         with torch.no_grad():
             for batch in test_loader:
                 x, _, mask, target = _flatten(batch)
                 y = model(x.unsqueeze(1))
                 running_test_loss += l1_pow10_loss(y, mask, target).item()
+                last = (x, mask, target)
+        if rank == 0 and last is not None and \
+                global_step % config["logging"]["audio_interval"] == 0:
+            save_audio_samples(writer, model, config, *last, sample_dir, global_step)
         writer.add_scalar("Test_Loss", running_test_loss / max(1, len(test_loader)), epoch + 1)
 
         if rank == 0 and (epoch + 1) % config["logging"]["checkpoint_interval"] == 0:

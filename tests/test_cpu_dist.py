@@ -212,7 +212,12 @@ def _groups_worker(rank, world, port, q):
     red._ready(p)
     ignored = id(p) not in red._seen
     red.paused = False
-    q.put((rank, distinct, p.grad.tolist(), float(m.weight.sum()), ignored))
+    # GAN train.py's train_limit subset: drawn on rank 0, identical everywhere
+    import random
+    from models.GAN.train import train_subset
+    random.seed(100 + rank)
+    idx = train_subset(1000, 30, rank, world)
+    q.put((rank, distinct, p.grad.tolist(), float(m.weight.sum()), ignored, idx))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -228,7 +233,8 @@ def test_comm_groups_broadcast_and_pause():
     for p in ps:
         p.join(timeout=60)
         assert p.exitcode == 0
-    for rank, distinct, grad, wsum, ignored in res:
+    assert res[0][5] == res[1][5] and len(set(res[0][5])) == 30
+    for rank, distinct, grad, wsum, ignored, _ in res:
         assert distinct and ignored
         assert grad == [3.0, 3.0, 3.0]
         assert wsum == 0.0          # rank 0's weights everywhere
