@@ -152,6 +152,69 @@ def time_kernel(fn, reps, dev):
     return e0.elapsed_time(e1) / 1000.0 / reps
 
 
+def graph_replay(model, opt, audio, starts, g, n_fft, hop, win, T, args, dev, eager_med_ms):
+    """The same train step (features + fwd + bwd + Adam) captured once in a HIP
+    graph (torch.cuda.CUDAGraph over the torch.ops.ainp launches) and replayed:
+    per step only the gap starts are copied into the graph's static input.
+    Adam runs in its capturable form (device step counter, ainp_adam_ex) on a
+    copy of the eager optimizer's state, so the replayed steps continue the
+    same training.  Returns graph vs eager ms/step."""
+    from ainp import ops
+    from ainp.cnnblstm import l1_pow10_loss
+    from ainp.optim import Adam
+    gopt = Adam(model.parameters(), lr=CFG["training"]["starter_learning_rate"], capturable=True)
+    for p in model.parameters():
+        st = opt.state.get(p)
+        if st:
+            gopt.state[p] = {k: v.clone() for k, v in st.items()}
+    gstart = starts[0].clone()
+    gloss = torch.zeros((), device=dev)
+
+    def body():
+        x, tgt, mask, _ = ops.stft_features(audio, gstart, g, n_fft, hop, win, n_frames=T)
+        y = model(x.unsqueeze(1))
+        loss = l1_pow10_loss(y, mask, tgt)
+        loss.backward()
+        gopt.step()
+        gloss.copy_(loss.detach())
+
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(side):
+        for i in range(3):                  # warm up on a side stream (torch's recipe)
+            gstart.copy_(starts[i])
+            gopt.zero_grad(set_to_none=True)
+            body()
+    torch.cuda.current_stream(dev).wait_stream(side)
+    gopt.zero_grad(set_to_none=True)
+    cg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(cg):
+        body()
+    n = len(starts)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    for i in range(min(args.warmup, 5)):
+        gstart.copy_(starts[i % n])
+        cg.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev[0].record()
+    for k in range(args.steps):
+        gstart.copy_(starts[k % n])
+        cg.replay()
+        ev[k + 1].record()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    step_ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]
+    med = float(np.median(step_ms))
+    return {"ms_per_step": round(1000.0 * el / args.steps, 3), "ms_per_step_median": round(med, 3),
+            "eager_ms_per_step_median": round(eager_med_ms, 3),
+            "speedup_median": round(eager_med_ms / med, 4),
+            "frames_per_s": round(args.batch * T * args.steps / el, 2),
+            "loss_last": float(gloss.item()),
+            "what": "whole train step (features+fwd+bwd+capturable Adam) in one HIP graph, "
+                    "replayed per step after a D2D copy of the gap starts"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,6 +228,8 @@ def main():
                     help="cnnblstm = BASELINE configs[1] (the headline metric); gan = configs[3]")
     ap.add_argument("--clip-s", type=float, default=None,
                     help="gan: clip length (5 s = C4, T=626; 8 s = C5, T=1001, 0.1 s gap)")
+    ap.add_argument("--no-graph", action="store_true",
+                    help="skip the HIP-graph replay measurement of the same step (N=1)")
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32",
                     help="fp32 = C2 (headline); bf16 = the C3 per-GPU shape (bf16 GEMM/conv "
                          "operands, fp32 accumulate / cell state / BN statistics / weights)")
@@ -282,6 +347,9 @@ def main():
               "groups": "SyncBN and gradients on separate communicators; W_ih_l0 gradient "
                         "in 8 gate chunks all-reduced as each completes",
               "backend": dist.get_backend()}
+    graph = None
+    if world == 1 and not args.no_graph:
+        graph = graph_replay(model, opt, audio, starts, g, n_fft, hop, win, T, args, dev, med_ms)
     recon_l1 = eval_recon_l1(model, n_fft, hop, win, T, S, g, dev) if rank == 0 else None
 
     # ---- roofline: dominant kernel (LSTM layer-0 input projection GEMM) timed live
@@ -365,6 +433,7 @@ def main():
             "roofline": roof,
             "roofline_stft": roof_stft,
             "dp": dp,
+            "graph": graph,
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -356,6 +356,16 @@ int ainp_adam(float* const* params, const float* const* grads,
               const int64_t* numel, int n_tensors, double lr, double beta1,
               double beta2, double eps, double weight_decay, int64_t step,
               void* stream);
+/* Same with the step counter on the device (HIP-graph capturable, torch's
+ * Adam(capturable=True) contract): step_dev (float[1]) is incremented by the
+ * launch and the bias corrections are formed from it on the device, in the
+ * same double arithmetic as the host form; scalars_dev (float[2]) is scratch.
+ * step_dev == NULL: the host `step` is used, as ainp_adam. */
+int ainp_adam_ex(float* const* params, const float* const* grads,
+                 float* const* exp_avg, float* const* exp_avg_sq,
+                 const int64_t* numel, int n_tensors, double lr, double beta1,
+                 double beta2, double eps, double weight_decay, int64_t step,
+                 float* step_dev, float* scalars_dev, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* (a15-a20) GAN path: PConvUNet, spectral-norm Discriminator, VGG loss      */

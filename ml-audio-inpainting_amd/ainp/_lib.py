@@ -84,6 +84,8 @@ _SIGS = {
     "ainp_colsum_slabs": (c_int, [P, c_int64, c_int64, c_int64, c_int64, P, P]),
     "ainp_adam": (c_int, [PP, PP, PP, PP, POINTER(c_int64), c_int, c_double, c_double,
                           c_double, c_double, c_double, c_int64, P]),
+    "ainp_adam_ex": (c_int, [PP, PP, PP, PP, POINTER(c_int64), c_int, c_double, c_double,
+                             c_double, c_double, c_double, c_int64, P, P, P]),
     "ainp_conv_gen_stat_parts": (c_int, [c_int64, c_int, c_int, c_int, c_int, c_int64, c_int64]),
     "ainp_conv_weight_kmajor": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "ainp_conv_gen_workspace": (c_size_t, [c_int64, c_int, c_int, c_int, c_int, c_int64, c_int64]),

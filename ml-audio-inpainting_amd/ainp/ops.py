@@ -1,9 +1,14 @@
-"""Tensor-level wrappers over the libainp C ABI.
+"""Tensor-level wrappers over the libainp kernels.
 
 Each function validates its torch tensors (device, dtype, layout), allocates
 outputs through PyTorch's caching allocator and launches the gfx950 kernel on
-the current HIP stream.  These are the only entry points the rest of the
-package uses to compute; nothing here falls back to ATen or the CPU.
+the current HIP stream through the PyTorch custom operators torch.ops.ainp.*
+(csrc/torch_ops.cpp: the TORCH_LIBRARY registration of every GPU entry point
+of include/ainp.h, out= style; the operator re-checks shapes on the host
+before the launch).  These are the only entry points the rest of the package
+uses to compute; nothing here falls back to ATen or the CPU, and importing
+this module fails when libainp_torch.so is missing.  Host-only queries
+(workspace sizes) use the plain C ABI through ctypes (_lib).
 """
 from __future__ import annotations
 
@@ -11,13 +16,18 @@ import functools
 import os
 import math
 import weakref
-from ctypes import c_int as ctypes_int
 
 import numpy as np
 import torch
 
 from . import _lib
-from ._lib import call, int64_array, ptr_array
+
+TORCH_OPS_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libainp_torch.so")
+if not os.path.exists(TORCH_OPS_PATH):
+    raise ImportError(f"libainp_torch.so not found at {TORCH_OPS_PATH}; build it with "
+                      "`make -C ml-audio-inpainting_amd/csrc` (or __graft_entry__.build())")
+torch.ops.load_library(TORCH_OPS_PATH)
+_T = torch.ops.ainp
 
 FEAT_CNNBLSTM = 0
 FEAT_GAN = 1
@@ -38,10 +48,6 @@ def _req(t: torch.Tensor, name: str, dtype=torch.float32, contiguous=True):
     if contiguous and not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
     return t
-
-
-def _p(t):
-    return None if t is None else t.data_ptr()
 
 
 # --------------------------------------------------------------------- STFT
@@ -110,10 +116,8 @@ def stft_features(audio: torch.Tensor, gap_start: torch.Tensor, gap_len: int,
         o[2] = torch.empty(batch, F, n_frames, device=dev, dtype=torch.float32)
     if outputs[3] and mode == FEAT_GAN:
         o[3] = torch.empty(batch, F, n_frames, device=dev, dtype=torch.float32)
-    call("ainp_stft_features", audio.data_ptr(), n_clips, S, _p(clip_index),
-         gap_start.data_ptr(), batch, int(gap_len), int(sample_rate), w.data_ptr(),
-         int(n_fft), int(hop), n_frames, int(mode), _p(o[0]), _p(o[1]), _p(o[2]),
-         _p(o[3]), _stream(audio))
+    _T.stft_features(audio, clip_index, gap_start, int(gap_len), int(sample_rate), w,
+                     int(n_fft), int(hop), n_frames, int(mode), o[0], o[1], o[2], o[3])
     return tuple(o)
 
 
@@ -138,9 +142,7 @@ def stft(audio: torch.Tensor, n_fft: int = 2048, hop_length: int = 512,
     cdt = torch.complex64 if audio.dtype == torch.float32 else torch.complex128
     out = torch.empty(x.shape[0], F, n_frames, device=audio.device, dtype=cdt)
     w = _device_window(window, win_length, n_fft, audio.device)
-    call("ainp_stft", x.data_ptr(), 0 if audio.dtype == torch.float32 else 1, x.shape[0], S,
-         w.data_ptr(), int(n_fft), int(hop_length), 1 if center else 0, n_frames,
-         out.data_ptr(), _stream(audio))
+    _T.stft(x, w, int(n_fft), int(hop_length), bool(center), n_frames, out)
     return out.reshape(*lead, F, n_frames)
 
 
@@ -165,18 +167,16 @@ def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
     nptr = len(A)
     assert len(B) == nptr and len(C) == nptr and 1 <= nptr <= 8
     ref = C[0]
-    b1 = ptr_array([_p(t) for t in bias1]) if bias1 is not None else None
-    b2 = ptr_array([_p(t) for t in bias2]) if bias2 is not None else None
-    st = _stream(ref if stream_of is None else stream_of)
+    if stream_of is not None and stream_of.device != ref.device:
+        raise ValueError("gemm: stream_of must be on the operands' device")
     exact = False if bf16 else (GEMM_EXACT if exact is None else bool(exact))
-    ws, ws_bytes = (_gemm_workspace(ref.device, st, int(M), int(N), int(K), nptr,
-                                    int(nstrided), int(ksplit)) if exact else (None, 0))
+    ws = (_gemm_workspace(ref.device, _stream(ref), int(M), int(N), int(K), nptr,
+                          int(nstrided), int(ksplit)) if exact else None)
     flags = GEMM_BF16 if bf16 else (GEMM_EXACT_F32 if exact else 0)
-    call("ainp_gemm_f32_ex", int(M), int(N), int(K), float(alpha),
-         ptr_array([t.data_ptr() for t in A]), int(sam), int(sak), int(strideA),
-         ptr_array([t.data_ptr() for t in B]), int(sbk), int(sbn), int(strideB),
-         float(beta), ptr_array([t.data_ptr() for t in C]), int(scm), int(scn),
-         int(strideC), b1, b2, nptr, int(nstrided), int(ksplit), flags, ws, ws_bytes, st)
+    _T.gemm(int(M), int(N), int(K), float(alpha), A, int(sam), int(sak), int(strideA),
+            B, int(sbk), int(sbn), int(strideB), float(beta), C, int(scm), int(scn),
+            int(strideC), list(bias1) if bias1 is not None else [],
+            list(bias2) if bias2 is not None else [], int(nstrided), int(ksplit), flags, ws)
 
 
 _GEMM_WS: dict = {}
@@ -188,13 +188,13 @@ def _gemm_workspace(device, stream: int, M, N, K, nptr, nstrided, ksplit):
     plain tile grid is used."""
     need = int(_lib.lib.ainp_gemm_f32_workspace(M, N, K, nptr, nstrided, ksplit))
     if need == 0:
-        return None, 0
+        return None
     key = (device.index, stream)
     buf = _GEMM_WS.get(key)
     if buf is None or buf.numel() * 4 < need:
         buf = torch.empty((need + 3) // 4, device=device, dtype=torch.float32)
         _GEMM_WS[key] = buf
-    return buf.data_ptr(), need
+    return buf
 
 
 def _chunks_for(K, tiles, target_blocks=512, min_rows=64):
@@ -267,9 +267,7 @@ def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf
     if want_stats:
         stats = torch.empty(_lib.lib.ainp_conv3x3_fwd_stat_rows(N, Cin, Cout, H, W), 2 * Cout,
                             device=x.device, dtype=torch.float64)
-    call("ainp_conv3x3_fwd_ex", x.data_ptr(), w.data_ptr(), _p(b), _p(in_scale),
-         _p(in_shift), y.data_ptr(), _p(stats), N, Cin, Cout, H, W, CONV_BF16 if bf16 else 0,
-         _stream(x))
+    _T.conv3x3_fwd(x, w, b, in_scale, in_shift, y, stats, CONV_BF16 if bf16 else 0)
     return y, stats
 
 
@@ -278,8 +276,7 @@ def conv3x3_dgrad(dy, w, bf16=False):
     N, Cout, H, W = dy.shape
     Cin = w.shape[1]
     dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=torch.float32)
-    call("ainp_conv3x3_dgrad_ex", dy.data_ptr(), w.data_ptr(), dx.data_ptr(), None,
-         N, Cin, Cout, H, W, CONV_BF16 if bf16 else 0, _stream(dy))
+    _T.conv3x3_dgrad(dy, w, dx, CONV_BF16 if bf16 else 0)
     return dx
 
 
@@ -291,9 +288,7 @@ def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=Fals
     db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
     ws_bytes = _lib.lib.ainp_conv3x3_wgrad_workspace(N, Cin, Cout, H, W)
     ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
-    call("ainp_conv3x3_wgrad_ex", x.data_ptr(), _p(in_scale), _p(in_shift), dy.data_ptr(),
-         dw.data_ptr(), _p(db), ws.data_ptr(), N, Cin, Cout, H, W, CONV_BF16 if bf16 else 0,
-         _stream(x))
+    _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws, CONV_BF16 if bf16 else 0)
     return dw, db
 
 
@@ -305,8 +300,7 @@ def bn_stats_reduce(stats, C, count=None):
     bn_relu_bwd_apply (include/ainp.h)."""
     sums = torch.empty(2 * C + (1 if count is not None else 0), device=stats.device,
                        dtype=torch.float64)
-    call("ainp_bn_stats_reduce", stats.data_ptr(), stats.shape[0], sums.data_ptr(), C,
-         _stream(stats))
+    _T.bn_stats_reduce(stats, sums, int(C))
     if count is not None:
         sums[2 * C:].fill_(float(count))
     return sums
@@ -319,9 +313,8 @@ def bn_finalize(sums, count, gamma, beta, running_mean, running_var, momentum, e
     scale = torch.empty(C, device=dev, dtype=torch.float32)
     shift = torch.empty(C, device=dev, dtype=torch.float32)
     save = torch.empty(2, C, device=dev, dtype=torch.float32)
-    call("ainp_bn_finalize", sums.data_ptr(), int(count), _p(gamma), _p(beta),
-         _p(running_mean), _p(running_var), float(momentum), float(eps), scale.data_ptr(),
-         shift.data_ptr(), save.data_ptr(), C, _stream(sums))
+    _T.bn_finalize(sums, int(count), gamma, beta, running_mean, running_var, float(momentum),
+                   float(eps), scale, shift, save)
     return scale, shift, save
 
 
@@ -330,9 +323,7 @@ def bn_eval_affine(gamma, beta, running_mean, running_var, eps):
     dev = running_mean.device
     scale = torch.empty(C, device=dev, dtype=torch.float32)
     shift = torch.empty(C, device=dev, dtype=torch.float32)
-    call("ainp_bn_eval_affine", _p(gamma), _p(beta), running_mean.data_ptr(),
-         running_var.data_ptr(), float(eps), scale.data_ptr(), shift.data_ptr(), C,
-         _stream(running_mean))
+    _T.bn_eval_affine(gamma, beta, running_mean, running_var, float(eps), scale, shift)
     return scale, shift
 
 
@@ -343,8 +334,7 @@ def bn_relu_apply(x, scale, shift, ntcf=False):
         out = torch.empty(N, W, C * H, device=x.device, dtype=torch.float32)
     else:
         out = torch.empty_like(x)
-    call("ainp_bn_relu_apply", x.data_ptr(), scale.data_ptr(), shift.data_ptr(),
-         out.data_ptr(), N, C, H, W, 1 if ntcf else 0, _stream(x))
+    _T.bn_relu_apply(x, scale, shift, out, bool(ntcf))
     return out
 
 
@@ -354,9 +344,7 @@ def bn_relu_bwd_reduce(g, y, scale, shift, save, ntcf=False):
     ws = torch.empty(_lib.lib.ainp_bn_relu_bwd_workspace(N, C, H, W), device=y.device,
                      dtype=torch.uint8)
     sums = torch.empty(2 * C, device=y.device, dtype=torch.float64)
-    call("ainp_bn_relu_bwd_reduce", g.data_ptr(), y.data_ptr(), scale.data_ptr(),
-         shift.data_ptr(), save.data_ptr(), ws.data_ptr(), sums.data_ptr(), N, C, H, W,
-         1 if ntcf else 0, _stream(y))
+    _T.bn_relu_bwd_reduce(g, y, scale, shift, save, ws, sums, bool(ntcf))
     return sums
 
 
@@ -365,10 +353,8 @@ def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False):
     gy = torch.empty_like(y)
     dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
-    call("ainp_bn_relu_bwd_apply", g.data_ptr(), y.data_ptr(), scale.data_ptr(),
-         shift.data_ptr(), _p(gamma), save.data_ptr(), sums.data_ptr(), int(count),
-         gy.data_ptr(), dgamma.data_ptr(), dbeta.data_ptr(), N, C, H, W, 1 if ntcf else 0,
-         _stream(y))
+    _T.bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, int(count), gy, dgamma, dbeta,
+                         bool(ntcf))
     return gy, dgamma, dbeta
 
 
@@ -387,8 +373,7 @@ def lstm_rec_fwd(zx, whh_f, whh_r, H, save=True):
     h_out = torch.empty(N, T, 2 * H, device=dev, dtype=torch.float32)
     gates = torch.empty(N, T, 8 * H, device=dev, dtype=torch.float32) if save else None
     cell = torch.empty(N, T, 2 * H, device=dev, dtype=torch.float32) if save else None
-    call("ainp_lstm_rec_fwd", zx.data_ptr(), ptr_array([whh_f.data_ptr(), whh_r.data_ptr()]),
-         h_out.data_ptr(), _p(gates), _p(cell), N, T, H, _stream(zx))
+    _T.lstm_rec_fwd(zx, whh_f, whh_r, h_out, gates, cell, int(H))
     return h_out, gates, cell
 
 
@@ -396,16 +381,14 @@ def lstm_rec_bwd(dh_out, gates, cell, whh_f, whh_r, H):
     _req(dh_out, "dh_out")
     N, T, _ = dh_out.shape
     dgates = torch.empty(N, T, 8 * H, device=dh_out.device, dtype=torch.float32)
-    call("ainp_lstm_rec_bwd", dh_out.data_ptr(), gates.data_ptr(), cell.data_ptr(),
-         ptr_array([whh_f.data_ptr(), whh_r.data_ptr()]), dgates.data_ptr(), N, T, H,
-         _stream(dh_out))
+    _T.lstm_rec_bwd(dh_out, gates, cell, whh_f, whh_r, dgates, int(H))
     return dgates
 
 
 def lstm_hprev(h_out, H):
     N, T, _ = h_out.shape
     hp = torch.empty_like(h_out)
-    call("ainp_lstm_hprev", h_out.data_ptr(), hp.data_ptr(), N, T, H, _stream(h_out))
+    _T.lstm_hprev(h_out, hp, int(H))
     return hp
 
 
@@ -417,8 +400,7 @@ def l1_pow10_loss(y, mask, target, want_grad=True, grad_scale=1.0):
     assert mask.numel() == n and target.numel() == n
     loss = torch.zeros(1, device=y.device, dtype=torch.float64)
     dy = torch.empty_like(y) if want_grad else None
-    call("ainp_l1_pow10_loss", y.data_ptr(), mask.data_ptr(), target.data_ptr(), n,
-         loss.data_ptr(), _p(dy), float(grad_scale), _stream(y))
+    _T.l1_pow10_loss(y, mask, target, loss, dy, float(grad_scale))
     return loss, dy
 
 
@@ -426,8 +408,7 @@ def scale_by_scalar(x, s):
     """x * s for a 0-dim/1-element float32 cuda tensor s (no host sync)."""
     s = s.reshape(1).to(torch.float32).contiguous()
     out = torch.empty_like(x)
-    call("ainp_scale_by_dev", x.data_ptr(), out.data_ptr(), x.numel(), s.data_ptr(),
-         _stream(x))
+    _T.scale_by_dev(x, out, s)
     return out
 
 
@@ -435,14 +416,14 @@ def sum_slabs(x, nslabs, out=None):
     n = x.numel() // nslabs
     if out is None:
         out = torch.empty(n, device=x.device, dtype=torch.float32)
-    call("ainp_sum_slabs", x.data_ptr(), int(nslabs), int(n), out.data_ptr(), _stream(x))
+    _T.sum_slabs(x, int(nslabs), int(n), out)
     return out
 
 
 def rowsum_batched(x3d):
     nb, rows, cols = x3d.shape
     out = torch.empty(rows, device=x3d.device, dtype=torch.float32)
-    call("ainp_rowsum_batched", x3d.data_ptr(), nb, rows, cols, out.data_ptr(), _stream(x3d))
+    _T.rowsum_batched(x3d, out)
     return out
 
 
@@ -454,26 +435,25 @@ def colsum(x2d, out=None, accumulate=False):
     ld = x2d.stride(0)
     assert x2d.stride(1) == 1
     if accumulate:
-        call("ainp_colsum", x2d.data_ptr(), rows, cols, ld, out.data_ptr(), 1, _stream(x2d))
+        _T.colsum(x2d, rows, cols, ld, out, True)
         return out
     # ~256 workgroups of column sums; the slab combine then reads nslabs*cols
     nslabs = max(1, min(64, rows // 16, 256 // -(-cols // 256)))
     part = torch.empty(nslabs, cols, device=x2d.device, dtype=torch.float32)
-    call("ainp_colsum_slabs", x2d.data_ptr(), rows, cols, ld, nslabs, part.data_ptr(),
-         _stream(x2d))
+    _T.colsum_slabs(x2d, rows, cols, ld, nslabs, part)
     return sum_slabs(part, nslabs, out)
 
 
 def adam_step(params, grads, exp_avgs, exp_avg_sqs, lr, beta1, beta2, eps,
-              weight_decay, step):
+              weight_decay, step, step_dev=None, scalars_dev=None):
+    """Multi-tensor Adam (ainp_adam_ex).  step_dev (float32 [1] device tensor,
+    with scalars_dev float32 [2] scratch): the step counter lives on the device
+    and is advanced by the launch (HIP-graph capturable); else host `step`."""
     if not params:
         return
-    call("ainp_adam", ptr_array([p.data_ptr() for p in params]),
-         ptr_array([g.data_ptr() for g in grads]),
-         ptr_array([m.data_ptr() for m in exp_avgs]),
-         ptr_array([v.data_ptr() for v in exp_avg_sqs]),
-         int64_array([p.numel() for p in params]), len(params), float(lr), float(beta1),
-         float(beta2), float(eps), float(weight_decay), int(step), _stream(params[0]))
+    _T.adam(list(params), list(grads), list(exp_avgs), list(exp_avg_sqs), float(lr),
+            float(beta1), float(beta2), float(eps), float(weight_decay),
+            int(step) if step_dev is None else 0, step_dev, scalars_dev)
 
 
 # ===================================================================== GAN
@@ -497,8 +477,7 @@ def conv_weight_kmajor(w, C0, C1):
         return ent[2]
     Cout, Cin, KH, KW = w.shape
     wt = torch.empty(Cin * KH * KW, Cout, device=w.device, dtype=torch.float32)
-    call("ainp_conv_weight_kmajor", w.data_ptr(), Cout, C0, C1, KH, KW, wt.data_ptr(),
-         _stream(w))
+    _T.conv_weight_kmajor(w, int(C0), int(C1), wt)
     wid = id(w)
     _WT_CACHE[wid] = (weakref.ref(w, lambda _r, wid=wid: _WT_CACHE.pop(wid, None)), key, wt)
     return wt
@@ -550,11 +529,10 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
         nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, Ho, Wo))
         wt = conv_weight_kmajor(w, C0, C1)
     if nb:
-        ws = torch.empty(max(1, nb // 4), device=x0.device)
-    call("ainp_conv_gen_fwd_ex", x0.data_ptr(), _p(m0), C0, H0, W0, _p(x1), _p(m1), C1, H1, W1,
-         w.data_ptr(), _p(wt), _p(bias), _p(ratio), _p(scale), out.data_ptr(), _p(stats), N, Cout,
-         Hin, Win, KH, KW, stride, pad, act, float(slope), ch, cw, CONV_BF16 if bf16 else 0,
-         _p(ws), _stream(x0))
+        ws = torch.empty(-(-nb // 4), device=x0.device)
+    _T.conv_gen_fwd(x0, m0, x1, m1, w, wt, bias, ratio, scale, out, stats, int(Hin), int(Win),
+                    int(stride), int(pad), int(act), float(slope), int(ch), int(cw),
+                    CONV_BF16 if bf16 else 0, ws)
     return out, stats
 
 
@@ -570,8 +548,8 @@ def pconv_mask(src0, src1, N, Hin, Win, k, stride, pad, want_ratio=True, want_ma
     Ho, Wo = conv_out_size(Hin, k, stride, pad), conv_out_size(Win, k, stride, pad)
     ratio = torch.empty(N, Ho, Wo, device=m0.device) if want_ratio else None
     newm = torch.empty(N, Ho, Wo, device=m0.device) if want_mask else None
-    call("ainp_pconv_mask", m0.data_ptr(), C0, H0, W0, _p(m1), C1, H1, W1, N, Hin, Win, k, k,
-         stride, pad, float(winsize), _p(ratio), _p(newm), _stream(m0))
+    _T.pconv_mask(m0, int(C0), m1, int(C1), int(N), int(Hin), int(Win), int(k), int(stride),
+                  int(pad), float(winsize), ratio, newm)
     return ratio, newm
 
 
@@ -580,16 +558,14 @@ def gan_pad_input(x, m, Hp, Wp):
     N, _, H, W = x.shape
     xp = torch.empty(N, Hp, Wp, device=x.device)
     mp = torch.empty(N, Hp, Wp, device=x.device)
-    call("ainp_gan_pad_input", x.data_ptr(), m.data_ptr(), N, H, W, Hp, Wp, xp.data_ptr(),
-         mp.data_ptr(), _stream(x))
+    _T.gan_pad_input(x, m, xp, mp)
     return xp, mp
 
 
 def affine_act_(y, scale, shift, act, slope=0.2):
     _req(y, "y")
     N, C = y.shape[:2]
-    call("ainp_affine_act", y.data_ptr(), scale.data_ptr(), shift.data_ptr(), N, C,
-         y[0, 0].numel(), act, float(slope), _stream(y))
+    _T.affine_act(y, scale, shift, int(act), float(slope))
     return y
 
 
@@ -597,7 +573,7 @@ def maxpool2(x):
     _req(x, "x")
     N, C, H, W = x.shape
     y = torch.empty(N, C, H // 2, W // 2, device=x.device)
-    call("ainp_maxpool2", x.data_ptr(), y.data_ptr(), N * C, H, W, _stream(x))
+    _T.maxpool2(x, y)
     return y
 
 
@@ -608,7 +584,7 @@ def _reduce_ws(device):
     key = str(device)
     ws = _RED_WS.get(key)
     if ws is None:
-        ws = torch.empty(int(_lib.lib.ainp_reduce_workspace()) // 8, device=device,
+        ws = torch.empty(-(-int(_lib.lib.ainp_reduce_workspace()) // 8), device=device,
                          dtype=torch.float64)
         _RED_WS[key] = ws
     return ws
@@ -619,8 +595,7 @@ def absdiff_mean(a, b):
     _req(a, "a"); _req(b, "b")
     assert a.numel() == b.numel()
     out = torch.empty((), device=a.device, dtype=torch.float64)
-    call("ainp_absdiff_mean", a.data_ptr(), b.data_ptr(), a.numel(), _reduce_ws(a.device).data_ptr(),
-         out.data_ptr(), _stream(a))
+    _T.absdiff_mean(a, b, _reduce_ws(a.device), out)
     return out
 
 
@@ -632,8 +607,7 @@ def bce_logits(x, target, want_grad=False, grad_scale=None):
     out = torch.empty((), device=x.device, dtype=torch.float64)
     grad = torch.empty_like(x) if want_grad else None
     gs = 1.0 / n if grad_scale is None else grad_scale
-    call("ainp_bce_logits", x.data_ptr(), n, float(target), _p(grad), float(gs),
-         _reduce_ws(x.device).data_ptr(), out.data_ptr(), _stream(x))
+    _T.bce_logits(x, float(target), grad, float(gs), _reduce_ws(x.device), out)
     return out, grad
 
 
@@ -642,8 +616,7 @@ def gan_recon_losses(g, o, m):
     for t, nm in ((g, "generated"), (o, "original"), (m, "mask")):
         _req(t, nm)
     out = torch.empty(3, device=g.device, dtype=torch.float64)
-    call("ainp_gan_recon_losses", g.data_ptr(), o.data_ptr(), m.data_ptr(), g.numel(),
-         _reduce_ws(g.device).data_ptr(), out.data_ptr(), _stream(g))
+    _T.gan_recon_losses(g, o, m, _reduce_ws(g.device), out)
     return out
 
 
@@ -653,8 +626,7 @@ def gan_recon_sums(g, o, m):
     for t, nm in ((g, "generated"), (o, "original"), (m, "mask")):
         _req(t, nm)
     out = torch.empty(5, device=g.device, dtype=torch.float64)
-    call("ainp_gan_recon_sums", g.data_ptr(), o.data_ptr(), m.data_ptr(), g.numel(),
-         _reduce_ws(g.device).data_ptr(), out.data_ptr(), _stream(g))
+    _T.gan_recon_sums(g, o, m, _reduce_ws(g.device), out)
     return out
 
 
@@ -676,14 +648,9 @@ def sn_power(weights, us, vs, update=True, eps=1e-12):
     wds = [w[0].numel() for w in weights]
     maxdim = max(hs + wds)
     dev = weights[0].device
-    ws = torch.empty(int(_lib.lib.ainp_sn_workspace(nl, maxdim)) // 4, device=dev)
+    ws = torch.empty(-(-int(_lib.lib.ainp_sn_workspace(nl, maxdim)) // 4), device=dev)
     inv = torch.empty(nl, device=dev)
-    hh = (ctypes_int * nl)(*hs)
-    wd = (ctypes_int * nl)(*wds)
-    call("ainp_sn_power", ptr_array([w.data_ptr() for w in weights]),
-         ptr_array([u.data_ptr() for u in us]), ptr_array([v.data_ptr() for v in vs]),
-         hh, wd, nl, float(eps), ws.data_ptr(), maxdim, inv.data_ptr(), int(bool(update)),
-         _stream(weights[0]))
+    _T.sn_power(list(weights), list(us), list(vs), float(eps), ws, inv, bool(update))
     return inv
 
 
@@ -693,9 +660,7 @@ def sn_weight_grad(G, w_orig, u, v, inv_sigma, with_bias=False):
     out = torch.empty_like(w_orig)
     h = w_orig.shape[0]
     ob = torch.empty(h, device=G.device) if with_bias else None
-    call("ainp_sn_weight_grad", G.data_ptr(), G.shape[1], w_orig.data_ptr(), u.data_ptr(),
-         v.data_ptr(), inv_sigma.data_ptr(), h, w_orig[0].numel(),
-         _reduce_ws(G.device).data_ptr(), out.data_ptr(), _p(ob), _stream(G))
+    _T.sn_weight_grad(G, w_orig, u, v, inv_sigma, _reduce_ws(G.device), out, ob)
     return out, ob
 
 
@@ -706,8 +671,7 @@ def im2col(x, k, stride, pad, ones_row=False, ldp=None):
     Ho, Wo = conv_out_size(H, k, stride, pad), conv_out_size(W, k, stride, pad)
     ldp = Ho * Wo if ldp is None else int(ldp)
     col = torch.empty(N, C * k * k + int(ones_row), ldp, device=x.device)
-    call("ainp_im2col_ld", x.data_ptr(), N, C, H, W, k, k, stride, pad, int(ones_row), ldp,
-         col.data_ptr(), _stream(x))
+    _T.im2col_ld(x, int(k), int(stride), int(pad), bool(ones_row), ldp, col)
     return col
 
 
@@ -751,8 +715,7 @@ def col2im(dcol, N, C, H, W, k, stride, pad):
     """dcol [N, C*k*k, ldp] (ldp >= Ho*Wo) -> dx [N, C, H, W]."""
     _req(dcol, "dcol")
     dx = torch.empty(N, C, H, W, device=dcol.device)
-    call("ainp_col2im_ld", dcol.data_ptr(), N, C, H, W, k, k, stride, pad, dcol.shape[-1],
-         dx.data_ptr(), _stream(dcol))
+    _T.col2im_ld(dcol, int(k), int(stride), int(pad), dx)
     return dx
 
 
@@ -762,14 +725,12 @@ def leaky_bwd(g, y, slope=0.2, ldo=None):
     _req(g, "g"); _req(y, "y")
     if ldo is None:
         out = torch.empty_like(g)
-        call("ainp_leaky_bwd", g.data_ptr(), y.data_ptr(), g.numel(), float(slope),
-             out.data_ptr(), _stream(g))
+        _T.leaky_bwd(g, y, float(slope), out)
         return out
     N, C = g.shape[:2]
     P = g.numel() // (N * C)
     out = torch.empty(N, C, int(ldo), device=g.device, dtype=torch.float32)
-    call("ainp_leaky_bwd_ld", g.data_ptr(), y.data_ptr(), N * C, P, float(slope), int(ldo),
-         out.data_ptr(), _stream(g))
+    _T.leaky_bwd_ld(g, y, N * C, float(slope), int(ldo), out)
     return out
 
 
@@ -808,7 +769,7 @@ def vgg_target_max(x):
     all-reduce of this tensor is the global batch max (loss.py:78)."""
     _req(x, "x")
     mx = torch.empty(1, device=x.device, dtype=torch.int32)
-    call("ainp_vgg_target_max", x.data_ptr(), x.numel(), mx.data_ptr(), _stream(x))
+    _T.vgg_target_max(x, mx)
     return mx
 
 
@@ -823,16 +784,14 @@ def vgg_prep(x, generated, tables, S=224, target_max=None):
         mx, mode = target_max, 2
     else:
         mx, mode = torch.empty(1, device=x.device, dtype=torch.int32), int(bool(generated))
-    call("ainp_vgg_prep", x.data_ptr(), N, H, W, mode, mx.data_ptr(),
-         ry0.data_ptr(), rn.data_ptr(), rw.data_ptr(), rw.shape[1], cx0.data_ptr(),
-         cn.data_ptr(), cw.data_ptr(), cw.shape[1], S, out.data_ptr(), _stream(x))
+    _T.vgg_prep(x, mode, mx, ry0, rn, rw, cx0, cn, cw, int(S), out)
     return out
 
 
 def mul(a, b):
     _req(a, "a"); _req(b, "b")
     out = torch.empty_like(a)
-    call("ainp_mul", a.data_ptr(), b.data_ptr(), a.numel(), out.data_ptr(), _stream(a))
+    _T.mul(a, b, out)
     return out
 
 
@@ -840,7 +799,7 @@ def channel_sum(m):
     _req(m, "mask")
     N, C, H, W = m.shape
     out = torch.empty(N, H, W, device=m.device)
-    call("ainp_channel_sum", m.data_ptr(), N, C, H * W, out.data_ptr(), _stream(m))
+    _T.channel_sum(m, out)
     return out
 
 
@@ -881,10 +840,9 @@ def istft(spec=None, *, mag=None, angles=None, phase=None, n_fft=None, hop_lengt
     full = n_fft + hop_length * (T - 1)
     out_len = full - 2 * (n_fft // 2) if center else full
     out = torch.empty(*lead, out_len, device=dev, dtype=odt)
-    ws = torch.empty(int(_lib.lib.ainp_istft_workspace(nsig, T, n_fft)) // 8, device=dev,
+    ws = torch.empty(-(-int(_lib.lib.ainp_istft_workspace(nsig, T, n_fft)) // 8), device=dev,
                      dtype=torch.float64)
-    call("ainp_istft", in0.data_ptr(), _p(in1), mode, nsig, F, T, w.data_ptr(), n_fft,
-         hop_length, int(bool(center)), ws.data_ptr(), out.data_ptr(), _stream(in0))
+    _T.istft(in0, in1, mode, F, T, w, int(n_fft), int(hop_length), bool(center), ws, out)
     return out
 
 
@@ -914,8 +872,6 @@ def griffinlim(S, n_iter=32, hop_length=None, win_length=None, n_fft=None, windo
         inv = istft(mag=S, angles=angles, n_fft=n_fft, hop_length=hop_length,
                     win_length=win_length, window=window, center=center)
         rebuilt = stft(inv, n_fft, hop_length, win_length, window, center)
-        call("ainp_gl_update", torch.view_as_real(rebuilt).data_ptr(),
-             torch.view_as_real(tprev).data_ptr(), torch.view_as_real(angles).data_ptr(),
-             angles.numel(), float(momentum), int(it == 0), _stream(S))
+        _T.gl_update(rebuilt, tprev, angles, float(momentum), it == 0)
     return istft(mag=S, angles=angles, n_fft=n_fft, hop_length=hop_length,
                  win_length=win_length, window=window, center=center)

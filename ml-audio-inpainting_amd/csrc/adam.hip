@@ -24,10 +24,28 @@ struct AdamList {
 
 constexpr int ADAM_CHUNK = 256 * 8;
 
+// Device-step form (HIP-graph capturable): one thread advances the step
+// counter kept on the device and forms step_size / sqrt(bc2) exactly as the
+// host path does (double pow, one rounding to f32), so a captured step
+// replays with the right bias corrections.
+__global__ void adam_prologue(float* step_dev, float* scalars, double lr, double beta1,
+                              double beta2) {
+  const float step = step_dev[0] + 1.0f;
+  step_dev[0] = step;
+  const double bc1 = 1.0 - pow(beta1, (double)step);
+  const double bc2 = 1.0 - pow(beta2, (double)step);
+  scalars[0] = (float)(lr / bc1);
+  scalars[1] = (float)sqrt(bc2);
+}
+
 __global__ __launch_bounds__(256) void adam_kernel(AdamList L, float step_size,
                                                    float w1, float b2, float w2,
                                                    float bc2_sqrt, float eps,
-                                                   float wd) {
+                                                   float wd, const float* scalars) {
+  if (scalars) {
+    step_size = scalars[0];
+    bc2_sqrt = scalars[1];
+  }
   const int64_t b = blockIdx.x;
   int ti = 0;
   while (ti + 1 < L.count && L.block_start[ti + 1] <= b) ++ti;
@@ -63,16 +81,33 @@ extern "C" int ainp_adam(float* const* params, const float* const* grads,
                          const int64_t* numel, int n_tensors, double lr,
                          double beta1, double beta2, double eps,
                          double weight_decay, int64_t step, void* stream) {
-  if (!params || !grads || !exp_avg || !exp_avg_sq || !numel ||
-      n_tensors < 0 || step < 1)
+  return ainp_adam_ex(params, grads, exp_avg, exp_avg_sq, numel, n_tensors, lr, beta1, beta2,
+                      eps, weight_decay, step, nullptr, nullptr, stream);
+}
+
+extern "C" int ainp_adam_ex(float* const* params, const float* const* grads,
+                            float* const* exp_avg, float* const* exp_avg_sq,
+                            const int64_t* numel, int n_tensors, double lr,
+                            double beta1, double beta2, double eps,
+                            double weight_decay, int64_t step, float* step_dev,
+                            float* scalars_dev, void* stream) {
+  if (!params || !grads || !exp_avg || !exp_avg_sq || !numel || n_tensors < 0 ||
+      (!step_dev && step < 1) || (!step_dev != !scalars_dev))
     return record_msg("ainp_adam: bad argument");
   // scalars exactly as torch/optim/adam.py forms them (Python doubles),
   // rounded once to the f32 op math
-  const double bc1 = 1.0 - pow(beta1, (double)step);
-  const double bc2 = 1.0 - pow(beta2, (double)step);
+  const double st = step_dev ? 1.0 : (double)step;
+  const double bc1 = 1.0 - pow(beta1, st);
+  const double bc2 = 1.0 - pow(beta2, st);
   const float step_size = (float)(lr / bc1);
   const float bc2_sqrt = (float)sqrt(bc2);
   hipStream_t s = as_stream(stream);
+  if (step_dev) {
+    hipLaunchKernelGGL(adam_prologue, dim3(1), dim3(1), 0, s, step_dev, scalars_dev, lr, beta1,
+                       beta2);
+    const int rc = check_launch("adam_prologue");
+    if (rc) return rc;
+  }
   for (int base = 0; base < n_tensors; base += ADAM_MAX) {
     AdamList L;
     L.count = 0;
@@ -92,7 +127,7 @@ extern "C" int ainp_adam(float* const* params, const float* const* grads,
     hipLaunchKernelGGL(adam_kernel, dim3((unsigned)blocks), dim3(256), 0, s, L,
                        step_size, (float)(1.0 - beta1), (float)beta2,
                        (float)(1.0 - beta2), bc2_sqrt, (float)eps,
-                       (float)weight_decay);
+                       (float)weight_decay, (const float*)scalars_dev);
     const int rc = check_launch("adam");
     if (rc) return rc;
   }

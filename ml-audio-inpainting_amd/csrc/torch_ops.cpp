@@ -1,0 +1,942 @@
+// torch_ops.cpp — TORCH_LIBRARY registration of the libainp C ABI.
+//
+// Every GPU entry point of include/ainp.h is registered as a PyTorch custom
+// operator torch.ops.ainp.<name> (the C name without the ainp_ prefix), with
+// the same argument meaning: device pointers become Tensors, `stream` becomes
+// PyTorch's current HIP stream of the operand's device, dimensions are read
+// from the tensor shapes (checked here, on the host, before any launch) where
+// the C signature takes them separately.  Operators follow the out= style of
+// the C ABI: outputs are caller-allocated mutable arguments (Tensor(a!)), so
+// the Python layer (ainp/ops.py) keeps the allocation policy and the caching
+// allocator / HIP-graph memory pools own every buffer.  Kernels are
+// registered for the CUDA dispatch key (ROCm PyTorch's HIP device), so a CPU
+// tensor fails in the dispatcher -- there is no CPU path.
+//
+// Host-only queries (workspace sizes, stat-part counts) and the FLAC codec
+// stay on the plain C ABI (ctypes); they launch nothing.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <torch/library.h>
+
+#include <algorithm>
+#include <optional>
+#include <vector>
+
+#include "ainp.h"
+
+namespace {
+
+using at::Tensor;
+using OptT = std::optional<Tensor>;
+
+void chk(int rc, const char* what) {
+  TORCH_CHECK(rc == 0, "ainp_", what, " failed (", rc, "): ", ainp_last_error());
+}
+
+void* stream_of(const Tensor& t) {
+  return (void*)c10::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
+
+// device tensor of the given dtype (unit-stride rows if contig); returns its pointer
+template <typename T = float>
+T* dev(const Tensor& t, const char* name, at::ScalarType st = at::kFloat, bool contig = true) {
+  TORCH_CHECK(t.defined(), name, " is required");
+  TORCH_CHECK(t.is_cuda(), name, " must live on the GPU (ainp has no CPU path), got ",
+              t.device());
+  TORCH_CHECK(t.scalar_type() == st, name, " must be ", st, ", got ", t.scalar_type());
+  TORCH_CHECK(!contig || t.is_contiguous(), name, " must be contiguous");
+  return static_cast<T*>(t.data_ptr());
+}
+template <typename T = float>
+T* opt(const OptT& t, const char* name, at::ScalarType st = at::kFloat, bool contig = true) {
+  return (t.has_value() && t->defined()) ? dev<T>(*t, name, st, contig) : nullptr;
+}
+void numel_is(const Tensor& t, int64_t n, const char* name) {
+  TORCH_CHECK(t.numel() == n, name, " has ", t.numel(), " elements, expected ", n);
+}
+void same_device(const Tensor& a, const Tensor& b) {
+  TORCH_CHECK(a.device() == b.device(), "operands on different devices: ", a.device(), " vs ",
+              b.device());
+}
+#define GUARD(t) c10::hip::HIPGuardMasqueradingAsCUDA guard_((t).device())
+
+// ------------------------------------------------------------------- STFT
+void stft_features(const Tensor& audio, const OptT& clip_index, const Tensor& gap_start,
+                   int64_t gap_len, int64_t sample_rate, const Tensor& window, int64_t n_fft,
+                   int64_t hop, int64_t n_frames, int64_t mode, const OptT& out0,
+                   const OptT& out1, const OptT& out2, const OptT& out3) {
+  GUARD(audio);
+  TORCH_CHECK(audio.dim() == 2, "audio must be [n_clips, n_samples]");
+  const int64_t n_clips = audio.size(0), S = audio.size(1);
+  const int32_t* ci = opt<int32_t>(clip_index, "clip_index", at::kInt);
+  const int64_t batch = ci ? clip_index->numel() : n_clips;
+  numel_is(gap_start, batch, "gap_start");
+  numel_is(window, n_fft, "window");
+  const int64_t plane = batch * (n_fft / 2 + 1) * n_frames;
+  // out1 is complex64 in the CNNBLSTM mode (interleaved re/im floats)
+  auto optf = [&](const OptT& t, const char* nm, bool cplx) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    if (cplx) {
+      numel_is(*t, plane, nm);
+      return reinterpret_cast<float*>(dev<void>(*t, nm, at::kComplexFloat));
+    }
+    numel_is(*t, plane, nm);
+    return dev(*t, nm);
+  };
+  chk(ainp_stft_features(dev(audio, "audio"), n_clips, S, ci,
+                         dev<int64_t>(gap_start, "gap_start", at::kLong), batch, gap_len,
+                         sample_rate, dev<double>(window, "window", at::kDouble), (int)n_fft,
+                         (int)hop, n_frames, (int)mode, optf(out0, "out0", false),
+                         optf(out1, "out1", mode == AINP_FEAT_CNNBLSTM), optf(out2, "out2", false),
+                         optf(out3, "out3", false), stream_of(audio)),
+      "stft_features");
+}
+
+void stft(const Tensor& audio, const Tensor& window, int64_t n_fft, int64_t hop, bool center,
+          int64_t n_frames, const Tensor& out) {
+  GUARD(audio);
+  TORCH_CHECK(audio.dim() == 2, "audio must be [n_signals, n_samples]");
+  const bool f64 = audio.scalar_type() == at::kDouble;
+  const void* a = f64 ? (const void*)dev<double>(audio, "audio", at::kDouble)
+                      : (const void*)dev(audio, "audio");
+  void* o = dev<void>(out, "out", f64 ? at::kComplexDouble : at::kComplexFloat);
+  numel_is(out, audio.size(0) * (n_fft / 2 + 1) * n_frames, "out");
+  numel_is(window, n_fft, "window");
+  chk(ainp_stft(a, f64 ? 1 : 0, audio.size(0), audio.size(1),
+                dev<double>(window, "window", at::kDouble), (int)n_fft, (int)hop, center ? 1 : 0,
+                n_frames, o, stream_of(audio)),
+      "stft");
+}
+
+void istft(const Tensor& in0, const OptT& in1, int64_t mode, int64_t n_bins, int64_t n_frames,
+           const Tensor& window, int64_t n_fft, int64_t hop, bool center, const Tensor& workspace,
+           const Tensor& out) {
+  GUARD(in0);
+  const void* p0;
+  const void* p1 = nullptr;
+  if (mode == 0) p0 = dev<void>(in0, "spec", at::kComplexFloat);
+  else if (mode == 1) p0 = dev<void>(in0, "spec", at::kComplexDouble);
+  else {
+    p0 = dev(in0, "mag");
+    TORCH_CHECK(in1.has_value() && in1->defined(), "istft modes 2/3 need angles / phase");
+    p1 = mode == 2 ? (const void*)dev<void>(*in1, "angles", at::kComplexFloat)
+                   : (const void*)dev(*in1, "phase");
+    numel_is(*in1, in0.numel(), "angles/phase");
+  }
+  TORCH_CHECK(in0.numel() % (n_bins * n_frames) == 0, "spectrum is not [..., F, T]");
+  const int64_t nsig = in0.numel() / (n_bins * n_frames);
+  const int64_t full = n_fft + hop * (n_frames - 1);
+  numel_is(out, nsig * (center ? full - 2 * (n_fft / 2) : full), "out");
+  TORCH_CHECK((size_t)workspace.nbytes() >= ainp_istft_workspace(nsig, n_frames, (int)n_fft),
+              "istft workspace too small");
+  chk(ainp_istft(p0, p1, (int)mode, nsig, (int)n_bins, n_frames,
+                 dev<double>(window, "window", at::kDouble), (int)n_fft, (int)hop, center ? 1 : 0,
+                 workspace.data_ptr(), out.data_ptr(), stream_of(in0)),
+      "istft");
+}
+
+void gl_update(const Tensor& rebuilt, const Tensor& tprev, const Tensor& angles, double momentum,
+               bool first) {
+  GUARD(rebuilt);
+  const int64_t n = angles.numel();
+  numel_is(rebuilt, n, "rebuilt");
+  numel_is(tprev, n, "tprev");
+  chk(ainp_gl_update((const float*)dev<void>(rebuilt, "rebuilt", at::kComplexFloat),
+                     (float*)dev<void>(tprev, "tprev", at::kComplexFloat),
+                     (float*)dev<void>(angles, "angles", at::kComplexFloat), n, (float)momentum,
+                     first ? 1 : 0, stream_of(rebuilt)),
+      "gl_update");
+}
+
+// ------------------------------------------------------------------- GEMM
+void gemm(int64_t M, int64_t N, int64_t K, double alpha, at::TensorList A, int64_t sam,
+          int64_t sak, int64_t strideA, at::TensorList B, int64_t sbk, int64_t sbn,
+          int64_t strideB, double beta, at::TensorList C, int64_t scm, int64_t scn,
+          int64_t strideC, const c10::List<OptT>& bias1, const c10::List<OptT>& bias2,
+          int64_t nstrided, int64_t ksplit, int64_t flags, const OptT& workspace) {
+  const int64_t nptr = (int64_t)A.size();
+  TORCH_CHECK(nptr >= 1 && nptr <= 8 && (int64_t)B.size() == nptr && (int64_t)C.size() == nptr,
+              "gemm: 1..8 pointer batches with as many A, B and C");
+  TORCH_CHECK(bias1.size() == 0 || (int64_t)bias1.size() == nptr, "gemm: bias1 per pointer batch");
+  TORCH_CHECK(bias2.size() == 0 || (int64_t)bias2.size() == nptr, "gemm: bias2 per pointer batch");
+  GUARD(C[0]);
+  const float* pa[8];
+  const float* pb[8];
+  float* pc[8];
+  const float* b1[8];
+  const float* b2[8];
+  for (int64_t i = 0; i < nptr; ++i) {
+    // views are allowed: the pointer carries the view's offset, strides are explicit
+    pa[i] = dev(A[i], "A", at::kFloat, false);
+    pb[i] = dev(B[i], "B", at::kFloat, false);
+    pc[i] = dev(C[i], "C", at::kFloat, false);
+    same_device(A[i], C[0]);
+    same_device(B[i], C[0]);
+    same_device(C[i], C[0]);
+    b1[i] = bias1.size() ? opt(bias1.get(i), "bias1") : nullptr;
+    b2[i] = bias2.size() ? opt(bias2.get(i), "bias2") : nullptr;
+  }
+  void* ws = nullptr;
+  size_t wsb = 0;
+  if (workspace.has_value() && workspace->defined()) {
+    ws = dev<void>(*workspace, "workspace", workspace->scalar_type());
+    wsb = workspace->nbytes();
+  }
+  chk(ainp_gemm_f32_ex(M, N, K, (float)alpha, pa, sam, sak, strideA, pb, sbk, sbn, strideB,
+                       (float)beta, pc, scm, scn, strideC, bias1.size() ? b1 : nullptr,
+                       bias2.size() ? b2 : nullptr, (int)nptr, nstrided, (int)ksplit, (int)flags,
+                       ws, wsb, stream_of(C[0])),
+      "gemm_f32_ex");
+}
+
+// ------------------------------------------------------------------- conv3x3
+void conv3x3_fwd(const Tensor& x, const Tensor& w, const OptT& bias, const OptT& in_scale,
+                 const OptT& in_shift, const Tensor& y, const OptT& stats, int64_t flags) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(1) == x.size(1) && w.size(2) == 3 &&
+                  w.size(3) == 3,
+              "conv3x3_fwd: x [N,Cin,H,W], w [Cout,Cin,3,3]");
+  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = w.size(0);
+  numel_is(y, N * Cout * H * W, "y");
+  double* st = opt<double>(stats, "stats", at::kDouble);
+  if (st) numel_is(*stats, ainp_conv3x3_fwd_stat_rows(N, (int)Cin, (int)Cout, H, W) * 2 * Cout, "stats");
+  chk(ainp_conv3x3_fwd_ex(dev(x, "x"), dev(w, "w"), opt(bias, "bias"), opt(in_scale, "in_scale"),
+                          opt(in_shift, "in_shift"), dev(y, "y"), st, N, (int)Cin, (int)Cout, H, W,
+                          (int)flags, stream_of(x)),
+      "conv3x3_fwd_ex");
+}
+
+void conv3x3_dgrad(const Tensor& dy, const Tensor& w, const Tensor& dx, int64_t flags) {
+  GUARD(dy);
+  TORCH_CHECK(dy.dim() == 4 && w.dim() == 4 && w.size(0) == dy.size(1),
+              "conv3x3_dgrad: dy [N,Cout,H,W], w [Cout,Cin,3,3]");
+  const int64_t N = dy.size(0), Cout = dy.size(1), H = dy.size(2), W = dy.size(3), Cin = w.size(1);
+  numel_is(dx, N * Cin * H * W, "dx");
+  chk(ainp_conv3x3_dgrad_ex(dev(dy, "dy"), dev(w, "w"), dev(dx, "dx"), nullptr, N, (int)Cin,
+                            (int)Cout, H, W, (int)flags, stream_of(dy)),
+      "conv3x3_dgrad_ex");
+}
+
+void conv3x3_wgrad(const Tensor& x, const OptT& in_scale, const OptT& in_shift, const Tensor& dy,
+                   const Tensor& dw, const OptT& dbias, const Tensor& workspace, int64_t flags) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == x.size(0) && dy.size(2) == x.size(2) &&
+                  dy.size(3) == x.size(3),
+              "conv3x3_wgrad: x [N,Cin,H,W], dy [N,Cout,H,W]");
+  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = dy.size(1);
+  numel_is(dw, Cout * Cin * 9, "dw");
+  TORCH_CHECK((size_t)workspace.nbytes() >= ainp_conv3x3_wgrad_workspace(N, (int)Cin, (int)Cout, H, W),
+              "conv3x3_wgrad workspace too small");
+  chk(ainp_conv3x3_wgrad_ex(dev(x, "x"), opt(in_scale, "in_scale"), opt(in_shift, "in_shift"),
+                            dev(dy, "dy"), dev(dw, "dw"), opt(dbias, "dbias"),
+                            workspace.data_ptr(), N, (int)Cin, (int)Cout, H, W, (int)flags,
+                            stream_of(x)),
+      "conv3x3_wgrad_ex");
+}
+
+// ------------------------------------------------------------------- BatchNorm
+void bn_stats_reduce(const Tensor& stats, const Tensor& sums, int64_t C) {
+  GUARD(stats);
+  // [parts, 2C] (conv3x3 epilogue) or [parts, 2, C] (conv_gen): rows of 2C
+  TORCH_CHECK(C > 0 && stats.numel() % (2 * C) == 0 && stats.size(-1) * (stats.dim() == 3 ? 2 : 1) == 2 * C,
+              "stats must be [parts, 2C] or [parts, 2, C]");
+  TORCH_CHECK(sums.numel() >= 2 * C, "sums needs 2C entries");
+  chk(ainp_bn_stats_reduce(dev<double>(stats, "stats", at::kDouble), (int)(stats.numel() / (2 * C)),
+                           dev<double>(sums, "sums", at::kDouble), (int)C, stream_of(stats)),
+      "bn_stats_reduce");
+}
+
+void bn_finalize(const Tensor& sums, int64_t count, const OptT& gamma, const OptT& beta,
+                 const OptT& running_mean, const OptT& running_var, double momentum, double eps,
+                 const Tensor& scale, const Tensor& shift, const Tensor& save) {
+  GUARD(sums);
+  const int64_t C = scale.numel();
+  TORCH_CHECK(sums.numel() >= 2 * C + (count == 0 ? 1 : 0), "sums too short");
+  numel_is(shift, C, "shift");
+  numel_is(save, 2 * C, "save");
+  chk(ainp_bn_finalize(dev<double>(sums, "sums", at::kDouble), count, opt(gamma, "gamma"),
+                       opt(beta, "beta"), opt(running_mean, "running_mean"),
+                       opt(running_var, "running_var"), (float)momentum, (float)eps,
+                       dev(scale, "scale"), dev(shift, "shift"), dev(save, "save"), (int)C,
+                       stream_of(sums)),
+      "bn_finalize");
+}
+
+void bn_eval_affine(const OptT& gamma, const OptT& beta, const Tensor& running_mean,
+                    const Tensor& running_var, double eps, const Tensor& scale,
+                    const Tensor& shift) {
+  GUARD(running_mean);
+  const int64_t C = running_mean.numel();
+  numel_is(running_var, C, "running_var");
+  numel_is(scale, C, "scale");
+  numel_is(shift, C, "shift");
+  chk(ainp_bn_eval_affine(opt(gamma, "gamma"), opt(beta, "beta"), dev(running_mean, "running_mean"),
+                          dev(running_var, "running_var"), (float)eps, dev(scale, "scale"),
+                          dev(shift, "shift"), (int)C, stream_of(running_mean)),
+      "bn_eval_affine");
+}
+
+void bn_relu_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, const Tensor& out,
+                   bool ntcf) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  numel_is(scale, C, "scale");
+  numel_is(shift, C, "shift");
+  numel_is(out, x.numel(), "out");
+  chk(ainp_bn_relu_apply(dev(x, "x"), dev(scale, "scale"), dev(shift, "shift"), dev(out, "out"), N,
+                         (int)C, H, W, ntcf ? 1 : 0, stream_of(x)),
+      "bn_relu_apply");
+}
+
+void bn_relu_bwd_reduce(const Tensor& g, const Tensor& y, const Tensor& scale, const Tensor& shift,
+                        const Tensor& save, const Tensor& workspace, const Tensor& sums, bool ntcf) {
+  GUARD(y);
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
+  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  numel_is(g, y.numel(), "g");
+  TORCH_CHECK(sums.numel() >= 2 * C, "sums needs 2C entries");
+  TORCH_CHECK((size_t)workspace.nbytes() >= ainp_bn_relu_bwd_workspace(N, (int)C, H, W),
+              "bn_relu_bwd workspace too small");
+  chk(ainp_bn_relu_bwd_reduce(dev(g, "g"), dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"),
+                              dev(save, "save"), workspace.data_ptr(),
+                              dev<double>(sums, "sums", at::kDouble), N, (int)C, H, W, ntcf ? 1 : 0,
+                              stream_of(y)),
+      "bn_relu_bwd_reduce");
+}
+
+void bn_relu_bwd_apply(const Tensor& g, const Tensor& y, const Tensor& scale, const Tensor& shift,
+                       const OptT& gamma, const Tensor& save, const Tensor& sums, int64_t count,
+                       const Tensor& gy, const OptT& dgamma, const OptT& dbeta, bool ntcf) {
+  GUARD(y);
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
+  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  numel_is(g, y.numel(), "g");
+  numel_is(gy, y.numel(), "gy");
+  TORCH_CHECK(sums.numel() >= 2 * C + (count == 0 ? 1 : 0), "sums too short");
+  chk(ainp_bn_relu_bwd_apply(dev(g, "g"), dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"),
+                             opt(gamma, "gamma"), dev(save, "save"),
+                             dev<double>(sums, "sums", at::kDouble), count, dev(gy, "gy"),
+                             opt(dgamma, "dgamma"), opt(dbeta, "dbeta"), N, (int)C, H, W,
+                             ntcf ? 1 : 0, stream_of(y)),
+      "bn_relu_bwd_apply");
+}
+
+// ------------------------------------------------------------------- BLSTM
+void lstm_rec_fwd(const Tensor& zx, const Tensor& whh_f, const Tensor& whh_r, const Tensor& h_out,
+                  const OptT& gates, const OptT& cell, int64_t H) {
+  GUARD(zx);
+  TORCH_CHECK(zx.dim() == 3 && zx.size(2) == 8 * H, "zx must be [N,T,8H]");
+  const int64_t N = zx.size(0), T = zx.size(1);
+  numel_is(whh_f, 4 * H * H, "whh_f");
+  numel_is(whh_r, 4 * H * H, "whh_r");
+  numel_is(h_out, N * T * 2 * H, "h_out");
+  float* gp = opt(gates, "gates");
+  float* cp = opt(cell, "cell");
+  if (gp) numel_is(*gates, N * T * 8 * H, "gates");
+  if (cp) numel_is(*cell, N * T * 2 * H, "cell");
+  const float* w[2] = {dev(whh_f, "whh_f"), dev(whh_r, "whh_r")};
+  chk(ainp_lstm_rec_fwd(dev(zx, "zx"), w, dev(h_out, "h_out"), gp, cp, N, T, (int)H, stream_of(zx)),
+      "lstm_rec_fwd");
+}
+
+void lstm_rec_bwd(const Tensor& dh_out, const Tensor& gates, const Tensor& cell,
+                  const Tensor& whh_f, const Tensor& whh_r, const Tensor& dgates, int64_t H) {
+  GUARD(dh_out);
+  TORCH_CHECK(dh_out.dim() == 3 && dh_out.size(2) == 2 * H, "dh_out must be [N,T,2H]");
+  const int64_t N = dh_out.size(0), T = dh_out.size(1);
+  numel_is(gates, N * T * 8 * H, "gates");
+  numel_is(cell, N * T * 2 * H, "cell");
+  numel_is(dgates, N * T * 8 * H, "dgates");
+  numel_is(whh_f, 4 * H * H, "whh_f");
+  numel_is(whh_r, 4 * H * H, "whh_r");
+  const float* w[2] = {dev(whh_f, "whh_f"), dev(whh_r, "whh_r")};
+  chk(ainp_lstm_rec_bwd(dev(dh_out, "dh_out"), dev(gates, "gates"), dev(cell, "cell"), w,
+                        dev(dgates, "dgates"), N, T, (int)H, stream_of(dh_out)),
+      "lstm_rec_bwd");
+}
+
+void lstm_hprev(const Tensor& h_out, const Tensor& hprev, int64_t H) {
+  GUARD(h_out);
+  TORCH_CHECK(h_out.dim() == 3 && h_out.size(2) == 2 * H, "h_out must be [N,T,2H]");
+  numel_is(hprev, h_out.numel(), "hprev");
+  chk(ainp_lstm_hprev(dev(h_out, "h_out"), dev(hprev, "hprev"), h_out.size(0), h_out.size(1),
+                      (int)H, stream_of(h_out)),
+      "lstm_hprev");
+}
+
+// ------------------------------------------------------------------- loss / reductions / Adam
+void l1_pow10_loss(const Tensor& y, const Tensor& mask, const Tensor& target, const Tensor& loss,
+                   const OptT& dy, double grad_scale) {
+  GUARD(y);
+  const int64_t n = y.numel();
+  numel_is(mask, n, "mask");
+  numel_is(target, n, "target");
+  float* d = opt(dy, "dy");
+  if (d) numel_is(*dy, n, "dy");
+  chk(ainp_l1_pow10_loss(dev(y, "y"), dev(mask, "mask"),
+                         (const float*)dev<void>(target, "target", at::kComplexFloat), n,
+                         dev<double>(loss, "loss", at::kDouble), d, (float)grad_scale,
+                         stream_of(y)),
+      "l1_pow10_loss");
+}
+
+void scale_by_dev(const Tensor& x, const Tensor& out, const Tensor& scalar) {
+  GUARD(x);
+  numel_is(out, x.numel(), "out");
+  chk(ainp_scale_by_dev(dev(x, "x"), dev(out, "out"), x.numel(), dev(scalar, "scalar"),
+                        stream_of(x)),
+      "scale_by_dev");
+}
+
+void sum_slabs(const Tensor& x, int64_t nslabs, int64_t n, const Tensor& out) {
+  GUARD(x);
+  TORCH_CHECK(x.numel() >= nslabs * n && out.numel() >= n, "sum_slabs: extents");
+  chk(ainp_sum_slabs(dev(x, "x", at::kFloat, false), nslabs, n, dev(out, "out", at::kFloat, false),
+                     stream_of(x)),
+      "sum_slabs");
+}
+
+void rowsum_batched(const Tensor& x, const Tensor& out) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 3, "x must be [nb, rows, cols]");
+  numel_is(out, x.size(1), "out");
+  chk(ainp_rowsum_batched(dev(x, "x"), x.size(0), x.size(1), x.size(2), dev(out, "out"),
+                          stream_of(x)),
+      "rowsum_batched");
+}
+
+void colsum(const Tensor& x, int64_t rows, int64_t cols, int64_t ld, const Tensor& out,
+            bool accumulate) {
+  GUARD(x);
+  TORCH_CHECK(out.numel() >= cols, "colsum: out too short");
+  chk(ainp_colsum(dev(x, "x", at::kFloat, false), rows, cols, ld, dev(out, "out", at::kFloat, false),
+                  accumulate ? 1 : 0, stream_of(x)),
+      "colsum");
+}
+
+void colsum_slabs(const Tensor& x, int64_t rows, int64_t cols, int64_t ld, int64_t nslabs,
+                  const Tensor& partial) {
+  GUARD(x);
+  numel_is(partial, nslabs * cols, "partial");
+  chk(ainp_colsum_slabs(dev(x, "x", at::kFloat, false), rows, cols, ld, nslabs,
+                        dev(partial, "partial"), stream_of(x)),
+      "colsum_slabs");
+}
+
+void adam(at::TensorList params, at::TensorList grads, at::TensorList exp_avg,
+          at::TensorList exp_avg_sq, double lr, double beta1, double beta2, double eps,
+          double weight_decay, int64_t step, const OptT& step_dev, const OptT& scalars_dev) {
+  const size_t n = params.size();
+  if (n == 0) return;
+  TORCH_CHECK(grads.size() == n && exp_avg.size() == n && exp_avg_sq.size() == n,
+              "adam: params, grads, exp_avg, exp_avg_sq differ in length");
+  GUARD(params[0]);
+  std::vector<float*> p(n), m(n), v(n);
+  std::vector<const float*> g(n);
+  std::vector<int64_t> ne(n);
+  for (size_t i = 0; i < n; ++i) {
+    p[i] = dev(params[i], "param");
+    g[i] = dev(grads[i], "grad");
+    m[i] = dev(exp_avg[i], "exp_avg");
+    v[i] = dev(exp_avg_sq[i], "exp_avg_sq");
+    ne[i] = params[i].numel();
+    numel_is(grads[i], ne[i], "grad");
+    numel_is(exp_avg[i], ne[i], "exp_avg");
+    numel_is(exp_avg_sq[i], ne[i], "exp_avg_sq");
+    same_device(params[i], params[0]);
+  }
+  float* sd = opt(step_dev, "step_dev");
+  float* sc = opt(scalars_dev, "scalars_dev");
+  chk(ainp_adam_ex(p.data(), g.data(), m.data(), v.data(), ne.data(), (int)n, lr, beta1, beta2,
+                   eps, weight_decay, step, sd, sc, stream_of(params[0])),
+      "adam_ex");
+}
+
+// ------------------------------------------------------------------- GAN
+void conv_weight_kmajor(const Tensor& w, int64_t C0, int64_t C1, const Tensor& wt) {
+  GUARD(w);
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == C0 + C1, "w must be [Cout, C0+C1, KH, KW]");
+  numel_is(wt, w.numel(), "wt");
+  chk(ainp_conv_weight_kmajor(dev(w, "w"), (int)w.size(0), (int)C0, (int)C1, (int)w.size(2),
+                              (int)w.size(3), dev(wt, "wt"), stream_of(w)),
+      "conv_weight_kmajor");
+}
+
+void conv_gen_fwd(const Tensor& x0, const OptT& m0, const OptT& x1, const OptT& m1,
+                  const Tensor& w, const OptT& wt, const OptT& bias, const OptT& ratio,
+                  const OptT& scale, const Tensor& y, const OptT& stats, int64_t Hin, int64_t Win,
+                  int64_t stride, int64_t pad, int64_t act, double slope, int64_t crop_h,
+                  int64_t crop_w, int64_t flags, const OptT& workspace) {
+  GUARD(x0);
+  TORCH_CHECK(x0.dim() == 4 && w.dim() == 4, "conv_gen: x0 [N,C0,H0,W0], w [Cout,Cin,KH,KW]");
+  const int64_t N = x0.size(0), C0 = x0.size(1), H0 = x0.size(2), W0 = x0.size(3);
+  int64_t C1 = 0, H1 = 0, W1 = 0;
+  const float* px1 = opt(x1, "x1");
+  if (px1) {
+    TORCH_CHECK(x1->dim() == 4 && x1->size(0) == N, "x1 must be [N,C1,H1,W1]");
+    C1 = x1->size(1);
+    H1 = x1->size(2);
+    W1 = x1->size(3);
+  }
+  const int64_t Cout = w.size(0), KH = w.size(2), KW = w.size(3);
+  TORCH_CHECK(w.size(1) == C0 + C1, "conv_gen: weight expects ", w.size(1),
+              " input channels, sources give ", C0 + C1);
+  const float* pm0 = opt(m0, "m0");
+  const float* pm1 = opt(m1, "m1");
+  if (pm0) numel_is(*m0, N * H0 * W0, "m0");
+  if (pm1) numel_is(*m1, N * H1 * W1, "m1");
+  const int64_t Ho = (Hin + 2 * pad - KH) / stride + 1, Wo = (Win + 2 * pad - KW) / stride + 1;
+  if (Cout == 1 && crop_h > 0) numel_is(y, N * crop_h * crop_w, "y");
+  else numel_is(y, N * Cout * Ho * Wo, "y");
+  const float* pwt = opt(wt, "wt");
+  TORCH_CHECK(Cout == 1 || pwt, "conv_gen: Cout > 1 needs the k-major weights wt");
+  double* st = opt<double>(stats, "stats", at::kDouble);
+  if (st)
+    numel_is(*stats,
+             (int64_t)ainp_conv_gen_stat_parts(N, (int)(C0 + C1), (int)KH, (int)KW, (int)Cout, Ho, Wo) *
+                 2 * Cout,
+             "stats");
+  const size_t need = ainp_conv_gen_workspace(N, (int)(C0 + C1), (int)KH, (int)KW, (int)Cout,
+                                              (Cout == 1 && crop_h > 0) ? crop_h : Ho,
+                                              (Cout == 1 && crop_w > 0) ? crop_w : Wo);
+  void* ws = nullptr;
+  if (workspace.has_value() && workspace->defined()) {
+    ws = dev<void>(*workspace, "workspace", workspace->scalar_type());
+    TORCH_CHECK((size_t)workspace->nbytes() >= need, "conv_gen workspace too small");
+  } else {
+    TORCH_CHECK(need == 0, "conv_gen needs a workspace of ", need, " bytes");
+  }
+  chk(ainp_conv_gen_fwd_ex(dev(x0, "x0"), pm0, (int)C0, (int)H0, (int)W0, px1, pm1, (int)C1,
+                           (int)H1, (int)W1, dev(w, "w"), pwt, opt(bias, "bias"), opt(ratio, "ratio"),
+                           opt(scale, "scale"), dev(y, "y"), st, N, (int)Cout, (int)Hin, (int)Win,
+                           (int)KH, (int)KW, (int)stride, (int)pad, (int)act, (float)slope,
+                           (int)crop_h, (int)crop_w, (int)flags, ws, stream_of(x0)),
+      "conv_gen_fwd_ex");
+}
+
+void pconv_mask(const Tensor& m0, int64_t C0, const OptT& m1, int64_t C1, int64_t N, int64_t Hin,
+                int64_t Win, int64_t k, int64_t stride, int64_t pad, double winsize,
+                const OptT& ratio, const OptT& newmask) {
+  GUARD(m0);
+  TORCH_CHECK(m0.dim() >= 2, "m0 must be [..., H, W]");
+  const int64_t H0 = m0.size(-2), W0 = m0.size(-1);
+  numel_is(m0, N * H0 * W0, "m0");
+  const float* p1 = opt(m1, "m1");
+  int64_t H1 = 0, W1 = 0;
+  if (p1) {
+    H1 = m1->size(-2);
+    W1 = m1->size(-1);
+    numel_is(*m1, N * H1 * W1, "m1");
+  }
+  const int64_t Ho = (Hin + 2 * pad - k) / stride + 1, Wo = (Win + 2 * pad - k) / stride + 1;
+  float* pr = opt(ratio, "ratio");
+  float* pn = opt(newmask, "newmask");
+  if (pr) numel_is(*ratio, N * Ho * Wo, "ratio");
+  if (pn) numel_is(*newmask, N * Ho * Wo, "newmask");
+  chk(ainp_pconv_mask(dev(m0, "m0"), (int)C0, (int)H0, (int)W0, p1, (int)C1, (int)H1, (int)W1, N,
+                      (int)Hin, (int)Win, (int)k, (int)k, (int)stride, (int)pad, (float)winsize, pr,
+                      pn, stream_of(m0)),
+      "pconv_mask");
+}
+
+void gan_pad_input(const Tensor& x, const Tensor& m, const Tensor& xp, const Tensor& mp) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4 && xp.dim() == 3, "x [N,1,H,W], xp [N,Hp,Wp]");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3), Hp = xp.size(1), Wp = xp.size(2);
+  numel_is(m, N * H * W, "mask");
+  numel_is(mp, N * Hp * Wp, "mp");
+  chk(ainp_gan_pad_input(dev(x, "x"), dev(m, "mask"), N, (int)H, (int)W, (int)Hp, (int)Wp,
+                         dev(xp, "xp"), dev(mp, "mp"), stream_of(x)),
+      "gan_pad_input");
+}
+
+void affine_act(const Tensor& y, const Tensor& scale, const Tensor& shift, int64_t act,
+                double slope) {
+  GUARD(y);
+  TORCH_CHECK(y.dim() >= 2, "y must be [N, C, ...]");
+  const int64_t N = y.size(0), C = y.size(1);
+  numel_is(scale, C, "scale");
+  numel_is(shift, C, "shift");
+  chk(ainp_affine_act(dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"), N, (int)C,
+                      y.numel() / (N * C), (int)act, (float)slope, stream_of(y)),
+      "affine_act");
+}
+
+void maxpool2(const Tensor& x, const Tensor& y) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  numel_is(y, x.size(0) * x.size(1) * (x.size(2) / 2) * (x.size(3) / 2), "y");
+  chk(ainp_maxpool2(dev(x, "x"), dev(y, "y"), x.size(0) * x.size(1), (int)x.size(2),
+                    (int)x.size(3), stream_of(x)),
+      "maxpool2");
+}
+
+void check_reduce_ws(const Tensor& ws) {
+  TORCH_CHECK((size_t)ws.nbytes() >= ainp_reduce_workspace(), "reduction workspace too small");
+}
+
+void absdiff_mean(const Tensor& a, const Tensor& b, const Tensor& workspace, const Tensor& out) {
+  GUARD(a);
+  numel_is(b, a.numel(), "b");
+  check_reduce_ws(workspace);
+  chk(ainp_absdiff_mean(dev(a, "a"), dev(b, "b"), a.numel(), workspace.data_ptr(),
+                        dev<double>(out, "out", at::kDouble), stream_of(a)),
+      "absdiff_mean");
+}
+
+void bce_logits(const Tensor& x, double target, const OptT& grad, double grad_scale,
+                const Tensor& workspace, const Tensor& out) {
+  GUARD(x);
+  float* gp = opt(grad, "grad");
+  if (gp) numel_is(*grad, x.numel(), "grad");
+  check_reduce_ws(workspace);
+  chk(ainp_bce_logits(dev(x, "logits"), x.numel(), (float)target, gp, (float)grad_scale,
+                      workspace.data_ptr(), dev<double>(out, "out", at::kDouble), stream_of(x)),
+      "bce_logits");
+}
+
+void gan_recon_losses(const Tensor& g, const Tensor& o, const Tensor& m, const Tensor& workspace,
+                      const Tensor& out) {
+  GUARD(g);
+  numel_is(o, g.numel(), "original");
+  numel_is(m, g.numel(), "mask");
+  numel_is(out, 3, "out");
+  check_reduce_ws(workspace);
+  chk(ainp_gan_recon_losses(dev(g, "generated"), dev(o, "original"), dev(m, "mask"), g.numel(),
+                            workspace.data_ptr(), dev<double>(out, "out", at::kDouble),
+                            stream_of(g)),
+      "gan_recon_losses");
+}
+
+void gan_recon_sums(const Tensor& g, const Tensor& o, const Tensor& m, const Tensor& workspace,
+                    const Tensor& out) {
+  GUARD(g);
+  numel_is(o, g.numel(), "original");
+  numel_is(m, g.numel(), "mask");
+  numel_is(out, 5, "out");
+  check_reduce_ws(workspace);
+  chk(ainp_gan_recon_sums(dev(g, "generated"), dev(o, "original"), dev(m, "mask"), g.numel(),
+                          workspace.data_ptr(), dev<double>(out, "out", at::kDouble),
+                          stream_of(g)),
+      "gan_recon_sums");
+}
+
+void vgg_target_max(const Tensor& x, const Tensor& max_ws) {
+  GUARD(x);
+  chk(ainp_vgg_target_max(dev(x, "x"), x.numel(),
+                          (unsigned int*)dev<int32_t>(max_ws, "max_ws", at::kInt), stream_of(x)),
+      "vgg_target_max");
+}
+
+void vgg_prep(const Tensor& x, int64_t generated, const Tensor& max_ws, const Tensor& ry0,
+              const Tensor& rn, const Tensor& rw, const Tensor& cx0, const Tensor& cn,
+              const Tensor& cw, int64_t S, const Tensor& out) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,1,H,W]");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  numel_is(out, N * 3 * S * S, "out");
+  TORCH_CHECK(rw.dim() == 2 && cw.dim() == 2 && rw.size(0) == S && cw.size(0) == S,
+              "vgg_prep: weight tables [S, taps]");
+  numel_is(ry0, S, "ry0");
+  numel_is(rn, S, "rn");
+  numel_is(cx0, S, "cx0");
+  numel_is(cn, S, "cn");
+  chk(ainp_vgg_prep(dev(x, "x"), N, (int)H, (int)W, (int)generated,
+                    (unsigned int*)dev<int32_t>(max_ws, "max_ws", at::kInt),
+                    dev<int32_t>(ry0, "ry0", at::kInt), dev<int32_t>(rn, "rn", at::kInt),
+                    dev(rw, "rw"), (int)rw.size(1), dev<int32_t>(cx0, "cx0", at::kInt),
+                    dev<int32_t>(cn, "cn", at::kInt), dev(cw, "cw"), (int)cw.size(1), (int)S,
+                    dev(out, "out"), stream_of(x)),
+      "vgg_prep");
+}
+
+void sn_power(at::TensorList w, at::TensorList u, at::TensorList v, double eps,
+              const Tensor& workspace, const Tensor& inv_sigma, bool update) {
+  const size_t nl = w.size();
+  TORCH_CHECK(nl >= 1 && nl <= 8 && u.size() == nl && v.size() == nl, "sn_power: 1..8 layers");
+  GUARD(w[0]);
+  std::vector<const float*> pw(nl);
+  std::vector<float*> pu(nl), pv(nl);
+  std::vector<int> h(nl), wd(nl);
+  int maxdim = 0;
+  for (size_t i = 0; i < nl; ++i) {
+    pw[i] = dev(w[i], "weight");
+    pu[i] = dev(u[i], "u");
+    pv[i] = dev(v[i], "v");
+    h[i] = (int)w[i].size(0);
+    wd[i] = (int)(w[i].numel() / w[i].size(0));
+    numel_is(u[i], h[i], "u");
+    numel_is(v[i], wd[i], "v");
+    maxdim = std::max(maxdim, std::max(h[i], wd[i]));
+  }
+  numel_is(inv_sigma, (int64_t)nl, "inv_sigma");
+  TORCH_CHECK((size_t)workspace.nbytes() >= ainp_sn_workspace((int)nl, maxdim),
+              "sn workspace too small");
+  chk(ainp_sn_power(pw.data(), pu.data(), pv.data(), h.data(), wd.data(), (int)nl, (float)eps,
+                    workspace.data_ptr(), maxdim, dev(inv_sigma, "inv_sigma"), update ? 1 : 0,
+                    stream_of(w[0])),
+      "sn_power");
+}
+
+void sn_weight_grad(const Tensor& G, const Tensor& w_orig, const Tensor& u, const Tensor& v,
+                    const Tensor& inv_sigma, const Tensor& workspace, const Tensor& out,
+                    const OptT& out_bias) {
+  GUARD(G);
+  const int64_t h = w_orig.size(0), wd = w_orig.numel() / h;
+  TORCH_CHECK(G.dim() == 2 && G.size(0) == h && G.size(1) >= wd, "G must be [h, ldg >= wd]");
+  numel_is(out, w_orig.numel(), "out");
+  numel_is(u, h, "u");
+  numel_is(v, wd, "v");
+  float* ob = opt(out_bias, "out_bias");
+  if (ob) {
+    numel_is(*out_bias, h, "out_bias");
+    TORCH_CHECK(G.size(1) > wd, "the bias gradient needs the ones-row column of G");
+  }
+  check_reduce_ws(workspace);
+  chk(ainp_sn_weight_grad(dev(G, "G"), (int)G.size(1), dev(w_orig, "w_orig"), dev(u, "u"),
+                          dev(v, "v"), dev(inv_sigma, "inv_sigma", at::kFloat, false), (int)h,
+                          (int)wd, workspace.data_ptr(), dev(out, "out"), ob, stream_of(G)),
+      "sn_weight_grad");
+}
+
+void im2col_ld(const Tensor& x, int64_t k, int64_t stride, int64_t pad, bool ones_row, int64_t ldp,
+               const Tensor& col) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  TORCH_CHECK(ldp >= Ho * Wo, "ldp < Ho*Wo");
+  numel_is(col, N * (C * k * k + (ones_row ? 1 : 0)) * ldp, "col");
+  chk(ainp_im2col_ld(dev(x, "x"), N, (int)C, (int)H, (int)W, (int)k, (int)k, (int)stride, (int)pad,
+                     ones_row ? 1 : 0, ldp, dev(col, "col"), stream_of(x)),
+      "im2col_ld");
+}
+
+void col2im_ld(const Tensor& dcol, int64_t k, int64_t stride, int64_t pad, const Tensor& dx) {
+  GUARD(dcol);
+  TORCH_CHECK(dx.dim() == 4 && dcol.dim() == 3, "dcol [N, C*k*k, ldp], dx [N,C,H,W]");
+  const int64_t N = dx.size(0), C = dx.size(1), H = dx.size(2), W = dx.size(3);
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  const int64_t ldp = dcol.size(2);
+  TORCH_CHECK(dcol.size(0) == N && dcol.size(1) >= C * k * k && ldp >= Ho * Wo,
+              "col2im: dcol shape");
+  chk(ainp_col2im_ld(dev(dcol, "dcol"), N, (int)C, (int)H, (int)W, (int)k, (int)k, (int)stride,
+                     (int)pad, ldp, dev(dx, "dx"), stream_of(dcol)),
+      "col2im_ld");
+}
+
+void leaky_bwd(const Tensor& g, const Tensor& y, double slope, const Tensor& out) {
+  GUARD(g);
+  numel_is(y, g.numel(), "y");
+  numel_is(out, g.numel(), "out");
+  chk(ainp_leaky_bwd(dev(g, "g"), dev(y, "y"), g.numel(), (float)slope, dev(out, "out"),
+                     stream_of(g)),
+      "leaky_bwd");
+}
+
+void leaky_bwd_ld(const Tensor& g, const Tensor& y, int64_t rows, double slope, int64_t ldo,
+                  const Tensor& out) {
+  GUARD(g);
+  TORCH_CHECK(rows > 0 && g.numel() % rows == 0, "leaky_bwd_ld: rows");
+  const int64_t P = g.numel() / rows;
+  TORCH_CHECK(ldo >= P, "ldo < P");
+  numel_is(y, g.numel(), "y");
+  numel_is(out, rows * ldo, "out");
+  chk(ainp_leaky_bwd_ld(dev(g, "g"), dev(y, "y"), rows, P, (float)slope, ldo, dev(out, "out"),
+                        stream_of(g)),
+      "leaky_bwd_ld");
+}
+
+void mul(const Tensor& a, const Tensor& b, const Tensor& out) {
+  GUARD(a);
+  numel_is(b, a.numel(), "b");
+  numel_is(out, a.numel(), "out");
+  chk(ainp_mul(dev(a, "a"), dev(b, "b"), a.numel(), dev(out, "out"), stream_of(a)), "mul");
+}
+
+void channel_sum(const Tensor& m, const Tensor& out) {
+  GUARD(m);
+  TORCH_CHECK(m.dim() == 4, "mask must be [N,C,H,W]");
+  const int64_t N = m.size(0), C = m.size(1), HW = m.size(2) * m.size(3);
+  numel_is(out, N * HW, "out");
+  chk(ainp_channel_sum(dev(m, "mask"), N, (int)C, HW, dev(out, "out"), stream_of(m)),
+      "channel_sum");
+}
+
+}  // namespace
+
+TORCH_LIBRARY(ainp, m) {
+  m.def("stft_features(Tensor audio, Tensor? clip_index, Tensor gap_start, int gap_len, "
+        "int sample_rate, Tensor window, int n_fft, int hop, int n_frames, int mode, "
+        "Tensor(a!)? out0, Tensor(b!)? out1, Tensor(c!)? out2, Tensor(d!)? out3) -> ()");
+  m.def("stft(Tensor audio, Tensor window, int n_fft, int hop, bool center, int n_frames, "
+        "Tensor(a!) out) -> ()");
+  m.def("istft(Tensor in0, Tensor? in1, int mode, int n_bins, int n_frames, Tensor window, "
+        "int n_fft, int hop, bool center, Tensor(a!) workspace, Tensor(b!) out) -> ()");
+  m.def("gl_update(Tensor rebuilt, Tensor(a!) tprev, Tensor(b!) angles, float momentum, "
+        "bool first) -> ()");
+  m.def("gemm(int M, int N, int K, float alpha, Tensor[] A, int sam, int sak, int strideA, "
+        "Tensor[] B, int sbk, int sbn, int strideB, float beta, Tensor(a!)[] C, int scm, int scn, "
+        "int strideC, Tensor?[] bias1, Tensor?[] bias2, int nstrided, int ksplit, int flags, "
+        "Tensor(b!)? workspace) -> ()");
+  m.def("conv3x3_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? in_scale, Tensor? in_shift, "
+        "Tensor(a!) y, Tensor(b!)? stats, int flags) -> ()");
+  m.def("conv3x3_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int flags) -> ()");
+  m.def("conv3x3_wgrad(Tensor x, Tensor? in_scale, Tensor? in_shift, Tensor dy, Tensor(a!) dw, "
+        "Tensor(b!)? dbias, Tensor(c!) workspace, int flags) -> ()");
+  m.def("bn_stats_reduce(Tensor stats, Tensor(a!) sums, int C) -> ()");
+  m.def("bn_finalize(Tensor sums, int count, Tensor? gamma, Tensor? beta, "
+        "Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, float eps, "
+        "Tensor(c!) scale, Tensor(d!) shift, Tensor(e!) save) -> ()");
+  m.def("bn_eval_affine(Tensor? gamma, Tensor? beta, Tensor running_mean, Tensor running_var, "
+        "float eps, Tensor(a!) scale, Tensor(b!) shift) -> ()");
+  m.def("bn_relu_apply(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, bool ntcf) -> ()");
+  m.def("bn_relu_bwd_reduce(Tensor g, Tensor y, Tensor scale, Tensor shift, Tensor save, "
+        "Tensor(a!) workspace, Tensor(b!) sums, bool ntcf) -> ()");
+  m.def("bn_relu_bwd_apply(Tensor g, Tensor y, Tensor scale, Tensor shift, Tensor? gamma, "
+        "Tensor save, Tensor sums, int count, Tensor(a!) gy, Tensor(b!)? dgamma, "
+        "Tensor(c!)? dbeta, bool ntcf) -> ()");
+  m.def("lstm_rec_fwd(Tensor zx, Tensor whh_f, Tensor whh_r, Tensor(a!) h_out, "
+        "Tensor(b!)? gates, Tensor(c!)? cell, int H) -> ()");
+  m.def("lstm_rec_bwd(Tensor dh_out, Tensor gates, Tensor cell, Tensor whh_f, Tensor whh_r, "
+        "Tensor(a!) dgates, int H) -> ()");
+  m.def("lstm_hprev(Tensor h_out, Tensor(a!) hprev, int H) -> ()");
+  m.def("l1_pow10_loss(Tensor y, Tensor mask, Tensor target, Tensor(a!) loss, Tensor(b!)? dy, "
+        "float grad_scale) -> ()");
+  m.def("scale_by_dev(Tensor x, Tensor(a!) out, Tensor scalar) -> ()");
+  m.def("sum_slabs(Tensor x, int nslabs, int n, Tensor(a!) out) -> ()");
+  m.def("rowsum_batched(Tensor x, Tensor(a!) out) -> ()");
+  m.def("colsum(Tensor x, int rows, int cols, int ld, Tensor(a!) out, bool accumulate) -> ()");
+  m.def("colsum_slabs(Tensor x, int rows, int cols, int ld, int nslabs, Tensor(a!) partial) -> ()");
+  m.def("adam(Tensor(a!)[] params, Tensor[] grads, Tensor(b!)[] exp_avg, "
+        "Tensor(c!)[] exp_avg_sq, float lr, float beta1, float beta2, float eps, "
+        "float weight_decay, int step, Tensor(d!)? step_dev, Tensor(e!)? scalars_dev) -> ()");
+  m.def("conv_weight_kmajor(Tensor w, int C0, int C1, Tensor(a!) wt) -> ()");
+  m.def("conv_gen_fwd(Tensor x0, Tensor? m0, Tensor? x1, Tensor? m1, Tensor w, Tensor? wt, "
+        "Tensor? bias, Tensor? ratio, Tensor? scale, Tensor(a!) y, Tensor(b!)? stats, int Hin, "
+        "int Win, int stride, int pad, int act, float slope, int crop_h, int crop_w, int flags, "
+        "Tensor(c!)? workspace) -> ()");
+  m.def("pconv_mask(Tensor m0, int C0, Tensor? m1, int C1, int N, int Hin, int Win, int k, "
+        "int stride, int pad, float winsize, Tensor(a!)? ratio, Tensor(b!)? newmask) -> ()");
+  m.def("gan_pad_input(Tensor x, Tensor m, Tensor(a!) xp, Tensor(b!) mp) -> ()");
+  m.def("affine_act(Tensor(a!) y, Tensor scale, Tensor shift, int act, float slope) -> ()");
+  m.def("maxpool2(Tensor x, Tensor(a!) y) -> ()");
+  m.def("absdiff_mean(Tensor a, Tensor b, Tensor(a!) workspace, Tensor(b!) out) -> ()");
+  m.def("bce_logits(Tensor x, float target, Tensor(a!)? grad, float grad_scale, "
+        "Tensor(b!) workspace, Tensor(c!) out) -> ()");
+  m.def("gan_recon_losses(Tensor g, Tensor o, Tensor m, Tensor(a!) workspace, Tensor(b!) out) -> ()");
+  m.def("gan_recon_sums(Tensor g, Tensor o, Tensor m, Tensor(a!) workspace, Tensor(b!) out) -> ()");
+  m.def("vgg_target_max(Tensor x, Tensor(a!) max_ws) -> ()");
+  m.def("vgg_prep(Tensor x, int generated, Tensor(a!) max_ws, Tensor ry0, Tensor rn, Tensor rw, "
+        "Tensor cx0, Tensor cn, Tensor cw, int S, Tensor(b!) out) -> ()");
+  m.def("sn_power(Tensor[] w, Tensor(a!)[] u, Tensor(b!)[] v, float eps, Tensor(c!) workspace, "
+        "Tensor(d!) inv_sigma, bool update) -> ()");
+  m.def("sn_weight_grad(Tensor G, Tensor w_orig, Tensor u, Tensor v, Tensor inv_sigma, "
+        "Tensor(a!) workspace, Tensor(b!) out, Tensor(c!)? out_bias) -> ()");
+  m.def("im2col_ld(Tensor x, int k, int stride, int pad, bool ones_row, int ldp, "
+        "Tensor(a!) col) -> ()");
+  m.def("col2im_ld(Tensor dcol, int k, int stride, int pad, Tensor(a!) dx) -> ()");
+  m.def("leaky_bwd(Tensor g, Tensor y, float slope, Tensor(a!) out) -> ()");
+  m.def("leaky_bwd_ld(Tensor g, Tensor y, int rows, float slope, int ldo, Tensor(a!) out) -> ()");
+  m.def("mul(Tensor a, Tensor b, Tensor(a!) out) -> ()");
+  m.def("channel_sum(Tensor m, Tensor(a!) out) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
+  m.impl("stft_features", &stft_features);
+  m.impl("stft", &stft);
+  m.impl("istft", &istft);
+  m.impl("gl_update", &gl_update);
+  m.impl("gemm", &gemm);
+  m.impl("conv3x3_fwd", &conv3x3_fwd);
+  m.impl("conv3x3_dgrad", &conv3x3_dgrad);
+  m.impl("conv3x3_wgrad", &conv3x3_wgrad);
+  m.impl("bn_stats_reduce", &bn_stats_reduce);
+  m.impl("bn_finalize", &bn_finalize);
+  m.impl("bn_eval_affine", &bn_eval_affine);
+  m.impl("bn_relu_apply", &bn_relu_apply);
+  m.impl("bn_relu_bwd_reduce", &bn_relu_bwd_reduce);
+  m.impl("bn_relu_bwd_apply", &bn_relu_bwd_apply);
+  m.impl("lstm_rec_fwd", &lstm_rec_fwd);
+  m.impl("lstm_rec_bwd", &lstm_rec_bwd);
+  m.impl("lstm_hprev", &lstm_hprev);
+  m.impl("l1_pow10_loss", &l1_pow10_loss);
+  m.impl("scale_by_dev", &scale_by_dev);
+  m.impl("sum_slabs", &sum_slabs);
+  m.impl("rowsum_batched", &rowsum_batched);
+  m.impl("colsum", &colsum);
+  m.impl("colsum_slabs", &colsum_slabs);
+  m.impl("adam", &adam);
+  m.impl("conv_weight_kmajor", &conv_weight_kmajor);
+  m.impl("conv_gen_fwd", &conv_gen_fwd);
+  m.impl("pconv_mask", &pconv_mask);
+  m.impl("gan_pad_input", &gan_pad_input);
+  m.impl("affine_act", &affine_act);
+  m.impl("maxpool2", &maxpool2);
+  m.impl("absdiff_mean", &absdiff_mean);
+  m.impl("bce_logits", &bce_logits);
+  m.impl("gan_recon_losses", &gan_recon_losses);
+  m.impl("gan_recon_sums", &gan_recon_sums);
+  m.impl("vgg_target_max", &vgg_target_max);
+  m.impl("vgg_prep", &vgg_prep);
+  m.impl("sn_power", &sn_power);
+  m.impl("sn_weight_grad", &sn_weight_grad);
+  m.impl("im2col_ld", &im2col_ld);
+  m.impl("col2im_ld", &col2im_ld);
+  m.impl("leaky_bwd", &leaky_bwd);
+  m.impl("leaky_bwd_ld", &leaky_bwd_ld);
+  m.impl("mul", &mul);
+  m.impl("channel_sum", &channel_sum);
+}
+
+// The ops write through raw device pointers like the C ABI; autograd is the
+// Python autograd.Function layer above them (ainp/cnnblstm.py, ainp/gan.py),
+// so the Autograd key falls through to the device kernel.
+TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
+  m.impl("stft_features", torch::CppFunction::makeFallthrough());
+  m.impl("stft", torch::CppFunction::makeFallthrough());
+  m.impl("istft", torch::CppFunction::makeFallthrough());
+  m.impl("gl_update", torch::CppFunction::makeFallthrough());
+  m.impl("gemm", torch::CppFunction::makeFallthrough());
+  m.impl("conv3x3_fwd", torch::CppFunction::makeFallthrough());
+  m.impl("conv3x3_dgrad", torch::CppFunction::makeFallthrough());
+  m.impl("conv3x3_wgrad", torch::CppFunction::makeFallthrough());
+  m.impl("bn_stats_reduce", torch::CppFunction::makeFallthrough());
+  m.impl("bn_finalize", torch::CppFunction::makeFallthrough());
+  m.impl("bn_eval_affine", torch::CppFunction::makeFallthrough());
+  m.impl("bn_relu_apply", torch::CppFunction::makeFallthrough());
+  m.impl("bn_relu_bwd_reduce", torch::CppFunction::makeFallthrough());
+  m.impl("bn_relu_bwd_apply", torch::CppFunction::makeFallthrough());
+  m.impl("lstm_rec_fwd", torch::CppFunction::makeFallthrough());
+  m.impl("lstm_rec_bwd", torch::CppFunction::makeFallthrough());
+  m.impl("lstm_hprev", torch::CppFunction::makeFallthrough());
+  m.impl("l1_pow10_loss", torch::CppFunction::makeFallthrough());
+  m.impl("scale_by_dev", torch::CppFunction::makeFallthrough());
+  m.impl("sum_slabs", torch::CppFunction::makeFallthrough());
+  m.impl("rowsum_batched", torch::CppFunction::makeFallthrough());
+  m.impl("colsum", torch::CppFunction::makeFallthrough());
+  m.impl("colsum_slabs", torch::CppFunction::makeFallthrough());
+  m.impl("adam", torch::CppFunction::makeFallthrough());
+  m.impl("conv_weight_kmajor", torch::CppFunction::makeFallthrough());
+  m.impl("conv_gen_fwd", torch::CppFunction::makeFallthrough());
+  m.impl("pconv_mask", torch::CppFunction::makeFallthrough());
+  m.impl("gan_pad_input", torch::CppFunction::makeFallthrough());
+  m.impl("affine_act", torch::CppFunction::makeFallthrough());
+  m.impl("maxpool2", torch::CppFunction::makeFallthrough());
+  m.impl("absdiff_mean", torch::CppFunction::makeFallthrough());
+  m.impl("bce_logits", torch::CppFunction::makeFallthrough());
+  m.impl("gan_recon_losses", torch::CppFunction::makeFallthrough());
+  m.impl("gan_recon_sums", torch::CppFunction::makeFallthrough());
+  m.impl("vgg_target_max", torch::CppFunction::makeFallthrough());
+  m.impl("vgg_prep", torch::CppFunction::makeFallthrough());
+  m.impl("sn_power", torch::CppFunction::makeFallthrough());
+  m.impl("sn_weight_grad", torch::CppFunction::makeFallthrough());
+  m.impl("im2col_ld", torch::CppFunction::makeFallthrough());
+  m.impl("col2im_ld", torch::CppFunction::makeFallthrough());
+  m.impl("leaky_bwd", torch::CppFunction::makeFallthrough());
+  m.impl("leaky_bwd_ld", torch::CppFunction::makeFallthrough());
+  m.impl("mul", torch::CppFunction::makeFallthrough());
+  m.impl("channel_sum", torch::CppFunction::makeFallthrough());
+}

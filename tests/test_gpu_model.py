@@ -305,3 +305,94 @@ def test_bf16_c2_batch32_forward_tracks_reference(golden_dir):
     assert e_y < 2e-2 and e_l < 2e-2
     for k, p in model.named_parameters():
         assert torch.isfinite(p.grad).all(), k
+
+
+def test_hip_graph_replayed_curve_matches_reference(golden_dir):
+    """The cnnblstm_curve.npz schedule with the training step captured once in
+    a HIP graph (torch.cuda.CUDAGraph over the torch.ops.ainp launches) and
+    replayed: 3 eager warm-up steps on a side stream (torch's recipe), then
+    27 replays with the batch copied into static inputs.  Adam is the
+    capturable form (device step counter, ainp_adam_ex).  Loss curve and final
+    parameters meet the eager fp32 gate (CURVE_TOL) against the reference."""
+    from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
+    from ainp.optim import Adam
+    from ainp.smoke import BN_FED_BIASES, small_config
+    g = np.load(os.path.join(golden_dir, "cnnblstm_curve.npz"), allow_pickle=False)
+    cfgv = g["config"]
+    steps = int(cfgv[7])
+    model = StackedBLSTMCNN(config=small_config(cfgv[:7])).cuda()
+    model.load_state_dict({k[len("init/"):]: torch.from_numpy(np.array(g[k])) for k in g.files
+                           if k.startswith("init/")})
+    model.train()
+    opt = Adam(model.parameters(), lr=1e-4, capturable=True)
+    data = [tuple(torch.from_numpy(g[f"{n}{b}"]).cuda() for n in ("x", "mask", "target"))
+            for b in range(4)]
+    sx, sm, st = (t.clone() for t in data[0])
+    sloss = torch.zeros((), device="cuda")
+
+    def body():
+        loss = l1_pow10_loss(model(sx.unsqueeze(1)), sm, st)
+        loss.backward()
+        opt.step()
+        sloss.copy_(loss.detach())
+
+    def load(s):
+        for dst, src in zip((sx, sm, st), data[s % 4]):
+            dst.copy_(src)
+
+    losses = []
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        for s in range(3):
+            load(s)
+            opt.zero_grad(set_to_none=True)
+            body()
+            losses.append(float(sloss.item()))
+    torch.cuda.current_stream().wait_stream(side)
+    opt.zero_grad(set_to_none=True)
+    cg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(cg):
+        body()
+    for s in range(3, steps):
+        load(s)
+        cg.replay()
+        losses.append(float(sloss.item()))
+    ref = g["losses"]
+    err = np.abs(np.array(losses) - ref) / np.abs(ref)
+    print("graph curve rel err max", err.max())
+    assert err.max() < CURVE_TOL, err
+    assert float(opt.state[next(model.parameters())]["step"]) == steps
+    for k, v in model.state_dict().items():
+        v = v.detach().cpu().numpy()
+        r = g["final/" + k]
+        if k.endswith("num_batches_tracked"):
+            assert int(v) == int(r)
+        elif k in BN_FED_BIASES:
+            assert np.abs(v - r).max() <= 2 * 1e-4 * steps, k
+        elif k.endswith("running_mean"):
+            assert np.abs(v - r).max() <= 2 * 1e-4 * steps + 1e-4 * np.abs(r).max(), k
+        else:
+            assert rel(v, r) < 1e-3, (k, rel(v, r))
+
+
+def test_capturable_adam_matches_host_step_adam():
+    """ainp_adam_ex with the device step counter == the host-step form, bit
+    for bit, over 5 steps (same double bias corrections, one f32 rounding)."""
+    from ainp.optim import Adam
+    gen = torch.Generator().manual_seed(7)
+    p0 = [torch.randn(n, generator=gen) for n in (1000, 37, 4096)]
+    grads = [[torch.randn(n, generator=gen) for n in (1000, 37, 4096)] for _ in range(5)]
+    res = []
+    for cap in (False, True):
+        ps = [torch.nn.Parameter(p.clone().cuda()) for p in p0]
+        opt = Adam(ps, lr=3e-3, betas=(0.8, 0.99), eps=1e-6, capturable=cap)
+        for gs in grads:
+            for p, gg in zip(ps, gs):
+                p.grad = gg.cuda()
+            opt.step()
+        res.append([p.detach().cpu() for p in ps])
+        if cap:
+            assert opt.state[ps[0]]["step"].is_cuda and float(opt.state[ps[0]]["step"]) == 5
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
