@@ -180,6 +180,27 @@ int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
                      int nptr, int64_t nstrided, int ksplit, int flags, void* workspace,
                      size_t ws_bytes, void* stream);
 
+/* bf16-operand GEMM (the bf16 configuration's layer-0 LSTM GEMMs,
+ * models/CNNBLSTM/model.py:46-47,77: input projection, data and weight
+ * gradients): C[m][n] (+ split s * strideC) = sum_k A[m][k] B[n][k] + bias(n),
+ * A [M][lda] and B [N][ldb] bf16 (uint16 bit patterns), both k-contiguous,
+ * 16-byte aligned rows (lda, ldb % 8 == 0), K % 8 == 0; fp32 accumulation
+ * on the bf16 MFMA; C fp32 row-major with ldc.  bias(n) = a1[n] + a2[n] for
+ * n < bias_nsplit, else b1[n - bias_nsplit] + b2[n - bias_nsplit] (NULLs = 0:
+ * the two LSTM directions' b_ih + b_hh).  nsplit > 1: split-K, split s sums k
+ * in [s*kc, min(K, (s+1)*kc)) (kc % 64 == 0) into slab C + s*strideC with
+ * no bias (combine with ainp_sum_slabs). */
+int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t* A, int64_t lda,
+                     const uint16_t* B, int64_t ldb, float* C, int64_t ldc,
+                     const float* bias_a1, const float* bias_a2, const float* bias_b1,
+                     const float* bias_b2, int64_t bias_nsplit, int nsplit, int64_t kc,
+                     int64_t strideC, void* stream);
+/* fp32 x [R][ld_in] -> bf16 (nearest-even) out [R][ld_out] and/or its
+ * transpose outT [C][ld_t] (either may be NULL): the BPTT gradient and the
+ * layer-0 weights as bf16 GEMM operands. */
+int ainp_cast_bf16_t(const float* x, int64_t R, int64_t C, int64_t ld_in, uint16_t* out,
+                     int64_t ld_out, uint16_t* outT, int64_t ld_t, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* 3x3 / stride 1 / pad 1 convolution over [N, C, F, T] spectrogram tiles    */
 /* ------------------------------------------------------------------------ */
@@ -287,6 +308,15 @@ int ainp_bn_relu_bwd_apply(const float* g, const float* y, const float* scale,
                            int64_t count, float* gy, float* dgamma,
                            float* dbeta, int64_t N, int C, int64_t H,
                            int64_t W, int g_ntcf, void* stream);
+
+/* bf16 configuration (BASELINE C3): the encoder's last BN+ReLU writes the
+ * layer-0 LSTM input directly as bf16 (nearest-even) in both layouts the
+ * bf16-operand GEMMs read: out [N][W][C*H] (the NTCF input, model.py:73-74)
+ * and outT [C*H][ld_t] with element (k, n*W + w) (its transpose, the weight
+ * gradient's k-contiguous operand).  Needs C*H % 64 == 0, W and ld_t even. */
+int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale, const float* shift,
+                                 uint16_t* out, uint16_t* outT, int64_t ld_t, int64_t N, int C,
+                                 int64_t H, int64_t W, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* BLSTM recurrence (one layer, both directions), batch_first                */

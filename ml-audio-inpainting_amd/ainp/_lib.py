@@ -131,6 +131,11 @@ _SIGS = {
                            P]),
     "ainp_gl_update": (c_int, [P, P, P, c_int64, c_float, c_int, P]),
     "ainp_channel_sum": (c_int, [P, c_int64, c_int, c_int64, P, P]),
+    "ainp_bn_relu_apply_ntcf_bf16": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, c_int64,
+                                             c_int64, P]),
+    "ainp_gemm_bf16nt": (c_int, [c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P, c_int64,
+                                 P, P, P, P, c_int64, c_int, c_int64, c_int64, P]),
+    "ainp_cast_bf16_t": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -52,7 +52,7 @@ class _ConvStackFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, spec, training, out_ntcf, comm, bf16, *params):
+    def forward(ctx, x, spec, training, out_ntcf, comm, bf16, l0_box, *params):
         N, _, H, W = x.shape
         saved_y = []
         affine = []          # per BN block: (scale, shift, save or None)
@@ -97,7 +97,16 @@ class _ConvStackFn(torch.autograd.Function):
                 act = (None, None)
             h = y
         last = affine[-1]
-        if last is not None:
+        if last is not None and l0_box is not None and _l0_bf16_ok(saved_y[-1]):
+            # bf16 configuration: the LSTM's layer-0 operands are written as bf16
+            # X / X^T for the bf16-operand GEMMs (gemm16.hip); the fp32 NTCF
+            # tensor is never materialised -- autograd gets a stride-0
+            # placeholder of its shape, and its gradient (dX, fp32) as usual
+            yl = saved_y[-1]
+            l0_box["x16"] = ops.bn_relu_apply_ntcf_bf16(yl, last[0], last[1])
+            Nl, Cl, Hl, Wl = yl.shape
+            out = torch.zeros((), device=yl.device).expand(Nl, Wl, Cl * Hl)
+        elif last is not None:
             out = ops.bn_relu_apply(saved_y[-1], last[0], last[1], ntcf=out_ntcf)
         else:
             out = saved_y[-1]
@@ -157,7 +166,16 @@ class _ConvStackFn(torch.autograd.Function):
                 g = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16)
                 if bi == 0:
                     gx = g
-        return (gx, None, None, None, None, None, *grads)
+        return (gx, None, None, None, None, None, None, *grads)
+
+
+def _l0_bf16_ok(y):
+    """Shapes the bf16 layer-0 operand path supports (ainp_bn_relu_apply_ntcf_bf16,
+    ainp_gemm_bf16nt): C*F % 64 == 0, even T, N*T % 8 == 0 (k-contiguous rows
+    of 16 bytes for the weight-gradient GEMM).  Otherwise the fp32-staged bf16
+    GEMM loop runs."""
+    N, C, F, T = y.shape
+    return (C * F) % 64 == 0 and T % 2 == 0 and (N * T) % 8 == 0
 
 
 # ------------------------------------------------------------------ BLSTM
@@ -167,23 +185,38 @@ class _BLSTMFn(torch.autograd.Function):
     (w_ih, w_hh, b_ih, b_hh, w_ih_rev, w_hh_rev, b_ih_rev, b_hh_rev)."""
 
     @staticmethod
-    def forward(ctx, x, H, L, bf16, sink, *params):
+    def forward(ctx, x, H, L, bf16, sink, l0_box, *params):
         N, T, I = x.shape
         NT = N * T
-        inp = x.reshape(NT, I)
+        x16 = l0_box.get("x16") if l0_box is not None else None
+        inp = x.reshape(NT, I) if x16 is None else x.new_empty(0)
         saved = []
         h = None
+        ctx.l016 = None
         for l in range(L):
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
-            Il = inp.shape[1]
+            Il = inp.shape[1] if (l > 0 or x16 is None) else I
             zx = torch.empty(N, T, 8 * H, device=x.device, dtype=torch.float32)
-            ops.gemm(NT, 4 * H, Il, [inp, inp], Il, 1, [wf, wr], 1, Il,
-                     [zx, zx[:, :, 4 * H:]], 8 * H, 1, bias1=[bif, bir], bias2=[bhf, bhr],
-                     bf16=bf16)
+            if l == 0 and x16 is not None:
+                # bf16-operand layer-0 projection: X (bf16 [NT, I]) x W_cat^T, both
+                # directions in one GEMM (W_cat = [W_ih; W_ih_rev] as bf16)
+                X16, XT16 = x16
+                W16 = torch.empty(8 * H, I, device=x.device, dtype=torch.bfloat16)
+                WT16 = torch.empty(I, 8 * H, device=x.device, dtype=torch.bfloat16)
+                ops.cast_bf16_t(wf, out=W16[:4 * H], outT=WT16[:, :4 * H])
+                ops.cast_bf16_t(wr, out=W16[4 * H:], outT=WT16[:, 4 * H:])
+                ops.gemm_bf16nt(X16.view(NT, I), W16, out=zx.view(NT, 8 * H),
+                                bias=(bif, bhf, bir, bhr), bias_nsplit=4 * H)
+                ctx.l016 = (XT16, WT16)
+            else:
+                ops.gemm(NT, 4 * H, Il, [inp, inp], Il, 1, [wf, wr], 1, Il,
+                         [zx, zx[:, :, 4 * H:]], 8 * H, 1, bias1=[bif, bir], bias2=[bhf, bhr],
+                         bf16=bf16)
             h, gates, cell = ops.lstm_rec_fwd(zx, hf, hr, H)
             saved += [inp, h, gates, cell]
             inp = h.view(NT, 2 * H)
         ctx.H, ctx.L, ctx.bf16 = H, L, bf16
+        ctx.I = I
         # data parallel: the layer-0 input weights' gradients (89 % of the
         # gradient bytes, produced late) are handed to the reducer chunk by chunk
         ctx.sink = sink
@@ -210,9 +243,15 @@ class _BLSTMFn(torch.autograd.Function):
         for l in range(L - 1, -1, -1):
             inp, h, gates, cell = saved[4 * l:4 * l + 4]
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
-            Il = inp.shape[1]
+            l016 = ctx.l016 if l == 0 else None
+            Il = inp.shape[1] if l016 is None else ctx.I
             dg = ops.lstm_rec_bwd(dh, gates, cell, hf, hr, H)          # [N,T,8H]
             dg2 = dg.view(NT, 8 * H)
+            if l016 is not None:
+                # bf16 operands of the layer-0 data / weight gradients
+                dg16 = torch.empty(NT, 8 * H, device=dh.device, dtype=torch.bfloat16)
+                dgT16 = torch.empty(8 * H, NT, device=dh.device, dtype=torch.bfloat16)
+                ops.cast_bf16_t(dg2, out=dg16, outT=dgT16)
             hp = ops.lstm_hprev(h, H).view(NT, 2 * H)
             ready = torch.cuda.Event()
             ready.record(main)
@@ -225,13 +264,17 @@ class _BLSTMFn(torch.autograd.Function):
                 gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H),
                                          bf16=bf16)
                 if early:
-                    gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0)
+                    gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0,
+                                            l016=(dgT16, l016[0]) if l016 is not None else None)
+                elif l016 is not None:
+                    gcat = ops.gemm_bf16nt_splitk(dgT16, l016[0], NT)     # [8H, I]
+                    gwi = [gcat[:4 * H], gcat[4 * H:]]
                 else:
                     gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il,
                                              offsets_b=(0, 0), bf16=bf16)
                 db_ih = ops.colsum(dg2)           # b_ih and b_hh get the same gradient
                 db_hh = db_ih.clone()
-            for t in (dg, hp, inp):
+            for t in (dg, hp, inp) + ((dgT16, l016[0]) if l016 is not None else ()):
                 t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l
             if early:   # p.grad set and reduced by _wih_grad_chunked: nothing for autograd
@@ -246,7 +289,9 @@ class _BLSTMFn(torch.autograd.Function):
                 # tiles) sums both directions inside each tile; the upper layers
                 # (Il = 256: 168 tiles) write 4 K-slabs (two per direction,
                 # 672 tiles) summed in fixed order.
-                if Il >= 1024:
+                if l016 is not None:
+                    dxi = ops.gemm_bf16nt(dg16, l016[1])                 # dg [NT,8H] x W_cat
+                elif Il >= 1024:
                     dxi = torch.empty(NT, Il, device=dh.device)
                     ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,
                              [dxi, dxi], Il, 1, ksplit=True, bf16=bf16)
@@ -268,10 +313,10 @@ class _BLSTMFn(torch.autograd.Function):
         if ctx.early_done:
             for p in ctx.wih0:            # side-stream .grad buffers read by the optimizer
                 p.grad.record_stream(main)
-        return (dx, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, *grads)
 
 
-def _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, sink, wih0, rows=None):
+def _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, sink, wih0, rows=None, l016=None):
     """dW_ih_l0 (both directions) on the current (side) stream in gate-row
     chunks of `rows`: dW[r0:r1] = dg[:, r0:r1]^T x, each chunk split-K over
     the N*T reduction into slabs and summed in fixed order straight into the
@@ -282,6 +327,17 @@ def _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, sink, wih0, rows=None):
     G4 = 4 * H
     rows = H if rows is None else rows       # one gate (i, f, g, o) per chunk
     bufs = [torch.empty(G4, Il, device=dg2.device, dtype=torch.float32) for _ in range(2)]
+    if l016 is not None:   # bf16 operands: dg^T [8H, NT], X^T [I, NT]
+        dgT16, XT16 = l016
+        for r0 in range(0, G4, rows):
+            for d in range(2):
+                chunk = bufs[d][r0:r0 + rows]
+                ops.gemm_bf16nt_splitk(dgT16[d * G4 + r0:d * G4 + r0 + rows], XT16, NT,
+                                       out=chunk)
+                sink.reduce_chunk(wih0[d], chunk)
+        for d in range(2):
+            wih0[d].grad = bufs[d]
+        return bufs
     tiles = -(-rows // 128) * -(-Il // 128) * 2
     S = ops._chunks_for(NT, tiles)
     kc = NT // S
@@ -473,15 +529,16 @@ class StackedBLSTMCNN(nn.Module):
         batch_size, _, freq_bins, timeframes = x.shape
         x = x.contiguous()
         spec, params = self._stack(self.encoder)
-        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, *params)
+        box = {} if self.bf16 else None       # layer-0 bf16 operands (encoder -> BLSTM)
+        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, box, *params)
         sink = self.grad_reducer if (self.training and torch.is_grad_enabled()) else None
-        z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, self.bf16, sink,
+        z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, self.bf16, sink, box,
                            *self.lstm._flat_weights)
         # model.py:82 hard-codes 16 decoder channels
         p = _ProjFn.apply(z, self.projection.weight, self.projection.bias, 16, freq_bins,
                           self.bf16)
         spec, params = self._stack(self.decoder)
-        y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, self.bf16, *params)
+        y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, self.bf16, None, *params)
         return y.squeeze(1)
 
     def reconstruct_spectrogram(self, log_spectrogram_gap, gap_mask):

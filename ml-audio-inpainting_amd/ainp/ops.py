@@ -224,6 +224,89 @@ def gemm_tn_splitk(a, lda, b, ldb, K, M, N, offsets_b=(0, 0), bf16=False):
     return [sum_slabs(slabs[0], S).view(M, N), sum_slabs(slabs[1], S).view(M, N)]
 
 
+# ------------------------------------------------------- bf16-operand GEMM (C3)
+def bn_relu_apply_ntcf_bf16(y, scale, shift):
+    """ainp_bn_relu_apply_ntcf_bf16: relu(y*scale+shift) of the encoder's last
+    block as bf16 X [N, W, C*H] and X^T [C*H, N*W] (row stride rounded up to 8
+    elements, so every row starts 16-byte aligned)."""
+    _req(y, "y")
+    N, C, H, W = y.shape
+    K, NW = C * H, N * W
+    out = torch.empty(N, W, K, device=y.device, dtype=torch.bfloat16)
+    ldt = -(-NW // 8) * 8
+    outT = torch.empty(K, ldt, device=y.device, dtype=torch.bfloat16)[:, :NW]
+    _T.bn_relu_apply_ntcf_bf16(y, scale, shift, out, outT)
+    return out, outT
+
+
+def cast_bf16_t(x, out=None, outT=None):
+    """ainp_cast_bf16_t: fp32 [R, C] (unit-stride rows) -> bf16 out [R, C] and/or
+    outT [C, R] (views with unit-stride rows; allocated when True is passed)."""
+    R, Cc = x.shape
+    if out is True:
+        out = torch.empty(R, Cc, device=x.device, dtype=torch.bfloat16)
+    if outT is True:
+        outT = torch.empty(Cc, R, device=x.device, dtype=torch.bfloat16)
+    _T.cast_bf16_t(x, out, outT)
+    return out, outT
+
+
+def gemm_bf16nt(A, B, K=None, out=None, bias=(None, None, None, None), bias_nsplit=0):
+    """C [M, N] = A [M, >=K] . B [N, >=K]^T + bias on bf16 operands (ainp_gemm_bf16nt);
+    bias = (a1, a2, b1, b2): a1 + a2 for columns < bias_nsplit, b1 + b2 after."""
+    M, N = A.shape[0], B.shape[0]
+    K = A.shape[1] if K is None else int(K)
+    if out is None:
+        out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    _T.gemm_bf16nt(A, B, out, K, *bias, int(bias_nsplit), 1, K)
+    return out
+
+
+# bf16 MFMA rate per resident workgroup slot and the HBM rate, for the split-K
+# choice below (measured orders of magnitude, not limits)
+_B16_TILE_RATE = 700e12 / 768
+_SLAB_RATE = 4e12
+
+
+def _splitk_bf16(M, N, K, slots=768, max_split=16):
+    """Split count S for a bf16 GEMM over a small M x N: minimise the wave-quantised
+    MFMA time ceil(tiles*S/slots) * tile_time(K/S) plus the slab round trip."""
+    tiles = -(-M // 128) * -(-N // 128)
+    best, best_t = 1, None
+    for S in range(1, max_split + 1):
+        kc = -(-K // S // 64) * 64
+        if kc < 64:
+            break
+        Sr = -(-K // kc)
+        if Sr != S:
+            continue
+        t = -(-tiles * S // slots) * 2.0 * 128 * 128 * kc / _B16_TILE_RATE
+        if S > 1:
+            t += 2.0 * S * M * N * 4 / _SLAB_RATE
+        if best_t is None or t < best_t:
+            best, best_t = S, t
+    return best
+
+
+def gemm_bf16nt_splitk(A, B, K, out=None):
+    """A [M, >=K] . B [N, >=K]^T (bf16, no bias) with the long K split over
+    slabs summed in fixed order (ainp_sum_slabs) -- the weight gradients."""
+    M, N = A.shape[0], B.shape[0]
+    if out is None:
+        out = torch.empty(M, N, device=A.device, dtype=torch.float32)
+    if not out.is_contiguous():
+        raise ValueError("gemm_bf16nt_splitk: out must be contiguous")
+    S = _splitk_bf16(M, N, K)
+    if S == 1:
+        _T.gemm_bf16nt(A, B, out, int(K), None, None, None, None, 0, 1, int(K))
+        return out
+    kc = -(-K // S // 64) * 64
+    slabs = torch.empty(S, M, N, device=A.device, dtype=torch.float32)
+    _T.gemm_bf16nt(A, B, slabs, int(K), None, None, None, None, 0, S, kc)
+    sum_slabs(slabs, S, out=out.view(-1))
+    return out
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor | None = None) -> torch.Tensor:
     """y = x @ w^T + b for x [M, K] row-major (nn.Linear semantics)."""
     _req(x, "x"); _req(w, "w")

@@ -491,6 +491,52 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
   }
 }
 
+// The bf16 configuration's layer-0 LSTM operands straight from the encoder
+// (gemm16.hip): relu(x*scale+shift) rounded to bf16 (nearest-even), written
+// both as X [n][w][k] (the NTCF input of the projection GEMM) and X^T
+// [k][n*W + w] (ld_t per row: the k-contiguous operand of the weight-gradient
+// GEMM); same 64 (k) x 64 (w) tiles as bn_relu_apply_ntcf2.
+__global__ __launch_bounds__(256) void bn_relu_apply_ntcf_bf16(
+    const float* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
+    uint16_t* __restrict__ out, uint16_t* __restrict__ outT, int64_t ld_t, int C, int64_t H,
+    int64_t W) {
+  __shared__ uint32_t tile[NT_T][NT_T / 2 + 1];   // [w][k pair] packed bf16x2
+  const int64_t K = (int64_t)C * H;
+  int n, k0, w0;
+  ntcf2_tile(blockIdx.x, K, W, n, k0, w0);
+  const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
+  const float* xn = x + (int64_t)n * K * W;
+  const int w = w0 + 2 * l;
+  uint16_t* tile16 = reinterpret_cast<uint16_t*>(&tile[0][0]);
+  constexpr int TROW = 2 * (NT_T / 2 + 1);        // uint16 per tile row
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {                   // rows k, lanes along w (float2)
+    const int kk = r + 8 * i;
+    const int64_t k = k0 + kk;
+    const int c = (int)(k / H);
+    float2 v = make_float2(0.f, 0.f);
+    if (w < W) v = *reinterpret_cast<const float2*>(xn + k * W + w);
+    const float sc = scale[c], sh = shift[c];
+    const __bf16 a = (__bf16)fmaxf(fmaf(v.x, sc, sh), 0.f);
+    const __bf16 b = (__bf16)fmaxf(fmaf(v.y, sc, sh), 0.f);
+    const uint16_t ua = __builtin_bit_cast(uint16_t, a), ub = __builtin_bit_cast(uint16_t, b);
+    if (w < W)
+      *reinterpret_cast<uint32_t*>(outT + k * ld_t + (int64_t)n * W + w) =
+          (uint32_t)ua | ((uint32_t)ub << 16);
+    tile16[(2 * l) * TROW + kk] = ua;
+    tile16[(2 * l + 1) * TROW + kk] = ub;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {                   // rows w, lanes along k (bf16 pairs)
+    const int ww = r + 8 * i;
+    const int64_t wr = w0 + ww;
+    if (wr < W)
+      *reinterpret_cast<uint32_t*>(out + ((int64_t)n * W + wr) * K + k0 + 2 * l) =
+          *reinterpret_cast<const uint32_t*>(&tile16[ww * TROW + 2 * l]);
+  }
+}
+
 static bool ntcf2_ok(int C, int64_t H, int64_t W, std::initializer_list<const void*> ptrs) {
   if (((int64_t)C * H) % NT_T != 0 || W % 2 != 0) return false;
   for (const void* p : ptrs)
@@ -564,6 +610,20 @@ extern "C" int ainp_bn_relu_apply(const float* x, const float* scale,
     hipLaunchKernelGGL(bn_relu_apply_kernel<false>, dim3((unsigned)blocks),
                        dim3(256), 0, s, x, scale, shift, out, C, H, W);
   return check_launch("bn_relu_apply");
+}
+
+extern "C" int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale,
+                                            const float* shift, uint16_t* out, uint16_t* outT,
+                                            int64_t ld_t, int64_t N, int C, int64_t H, int64_t W,
+                                            void* stream) {
+  if (!x || !scale || !shift || !out || !outT || N < 1 || C < 1 || H < 1 || W < 1 ||
+      ld_t < N * W || !ntcf2_ok(C, H, W, {x}) || (reinterpret_cast<uintptr_t>(out) & 3) ||
+      (reinterpret_cast<uintptr_t>(outT) & 3) || (ld_t & 1))
+    return record_msg("ainp_bn_relu_apply_ntcf_bf16: bad argument (C*H % 64, even W and ld_t)");
+  hipLaunchKernelGGL(bn_relu_apply_ntcf_bf16,
+                     dim3((unsigned)(N * (C * H / NT_T) * cdiv(W, NT_T))), dim3(256), 0,
+                     as_stream(stream), x, scale, shift, out, outT, ld_t, C, H, W);
+  return check_launch("bn_relu_apply_ntcf_bf16");
 }
 
 extern "C" size_t ainp_bn_relu_bwd_workspace(int64_t N, int C, int64_t H,

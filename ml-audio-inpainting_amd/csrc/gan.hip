@@ -327,7 +327,6 @@ __global__ __launch_bounds__(256, 2) void conv_gen_fwd_kernel(ConvGenParams p, c
 // fragments: lane (row r, half h) reads k = 16s + 8h..+7).  The gather, the
 // one-tap-per-tile fast path and the epilogue are conv_gen_fwd_kernel's.
 namespace cgx {
-constexpr int RS = 80;                 // bytes per image row (32 bf16 + 16 pad)
 __device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
   uint32_t r;
   asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
@@ -368,7 +367,7 @@ __global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(Con
   constexpr int WN = BN / 64;                 // waves along pixels (2 or 4)
   constexpr int AR = XBK * BM / 256;          // consecutive k per thread, A
   constexpr int BR = XBK * BN / 256;          // consecutive k per thread, B
-  constexpr int RS = XBK == 16 ? 48 : cgx::RS;
+  constexpr int RS = XBK * 2 + 16;            // image row: XBK bf16 + 16-byte pad
   constexpr int APL = BM * RS, BPL = BN * RS;   // plane bytes
   constexpr int ESCR = WN * BM * 2 * (int)sizeof(double);   // epilogue scratch (in sA)
   __shared__ __attribute__((aligned(16))) unsigned char sA[NPL * APL > ESCR ? NPL * APL : ESCR];
@@ -381,10 +380,10 @@ __global__ __launch_bounds__(256, XBK == 16 ? 3 : 2) void conv_gen_x6_kernel(Con
   const int64_t NP = (int64_t)p.N * HWo;
   const int64_t px0 = (int64_t)blockIdx.x * BN;
   const int co0 = blockIdx.y * BM;
-  constexpr int TPB = CG_BK / XBK;            // x6 tiles per split-range tile
+  // split-K ranges are in CG_BK units (the host keeps them XBK-aligned)
   const int nkt_all = (K + XBK - 1) / XBK;
-  const int64_t kb = (int64_t)blockIdx.z * p.ktiles_per_split * TPB;
-  const int64_t ke = kb + (int64_t)p.ktiles_per_split * TPB;
+  const int64_t kb = (int64_t)blockIdx.z * p.ktiles_per_split * CG_BK / XBK;
+  const int64_t ke = kb + (int64_t)p.ktiles_per_split * CG_BK / XBK;
   const int kt_begin = (int)(kb < nkt_all ? kb : nkt_all);
   const int kt_end = (int)(ke < nkt_all ? ke : nkt_all);
 
@@ -1351,7 +1350,23 @@ extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, in
     const char* e = getenv("AINP_CONV_GEN_BK");
     return (e && e[0] == '3') ? 32 : 16;
   }();
-  if (b16 && BM == 128)   // bf16 operands: one plane, 32-deep K-tiles
+  // bf16 operands: one plane, 32-deep K-tiles (measured: 64-deep tiles at
+  // 184-212 VGPRs ran the C4 step's convs 1.6x slower); AINP_CONV_GEN_B16_BK
+  // = 16 / 64 selects the other depths
+  static const int b16bk = [] {
+    const char* e = getenv("AINP_CONV_GEN_B16_BK");
+    return (e && e[0] == '6') ? 64 : (e && e[0] == '1') ? 16 : 32;
+  }();
+  const int bk = !b16 ? 0 : (b16bk == 64 && nsplit > 1 && p.ktiles_per_split % 2) ? 32 : b16bk;
+  if (bk == 64 && BM == 128)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 64, 1>), grid, dim3(256), 0, s, p, wt, act);
+  else if (bk == 64)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 64, 1>), grid, dim3(256), 0, s, p, wt, act);
+  else if (bk == 16 && BM == 128)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<128, 16, 1>), grid, dim3(256), 0, s, p, wt, act);
+  else if (bk == 16)
+    hipLaunchKernelGGL((conv_gen_x6_kernel<64, 16, 1>), grid, dim3(256), 0, s, p, wt, act);
+  else if (b16 && BM == 128)
     hipLaunchKernelGGL((conv_gen_x6_kernel<128, 32, 1>), grid, dim3(256), 0, s, p, wt, act);
   else if (b16)
     hipLaunchKernelGGL((conv_gen_x6_kernel<64, 32, 1>), grid, dim3(256), 0, s, p, wt, act);

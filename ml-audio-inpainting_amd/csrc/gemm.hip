@@ -25,6 +25,8 @@
 //  x6: K-tile 16; three bf16 planes [row][16 k] per operand with 48-byte rows
 //    (conflict-free ds_read_b128 fragments: lane (r, h) reads k = 8h..8h+7 of
 //    row r, the 32x32x16 operand map, identical for A and B).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace ainp {
@@ -252,26 +254,27 @@ __device__ __forceinline__ bf16x8v frag(const unsigned char* img, int plane, int
 // bf16-operand / fp32-accumulate autocast arithmetic.  K-tile 32, one plane per
 // operand, 80-byte image rows (conflict-free ds_read_b128 fragments).
 namespace b16 {
-constexpr int KT = 32;
-constexpr int RS = 80;            // bytes per image row: 32 bf16 + 16 B pad
-constexpr int IMG = 128 * RS;
+template <int KT> constexpr int rs() { return KT * 2 + 16; }   // image row: KT bf16 + 16 B pad
+template <int KT> constexpr int img() { return 128 * rs<KT>(); }
 
-// 128 x 32 fp32 operand tile -> registers -> bf16 -> one LDS plane.
-//  KC: thread = one row x 4 consecutive k (four float4 per thread);
-//  MC: thread = 4 consecutive rows x k pairs {2p, 2p+1, 2p+16, 2p+17}.
-template <bool KC, bool VEC>
+// 128 x KT fp32 operand tile -> registers -> bf16 -> one LDS plane.
+//  KC: thread = one row x 4 consecutive k (KT/8 float4 per thread);
+//  MC: thread = 4 consecutive rows x k pairs {2p, 2p+1} + 16 g, g < KT/16.
+template <bool KC, bool VEC, int KT = 32>
 struct Loader {
-  float4 v[4];
+  static constexpr int NV = KT / 8;
+  static constexpr int RS = rs<KT>();
+  float4 v[NV];
 
   __device__ __forceinline__ void load(const float* __restrict__ p, int64_t ld, int64_t r0,
                                        int64_t k0, int64_t R, int64_t K) {
     const int tid = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NV; ++i) {
       float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
       if (KC) {
         const int idx = tid + i * GEMM_THREADS;
-        const int64_t gr = r0 + (idx >> 3), gk = k0 + (idx & 7) * 4;
+        const int64_t gr = r0 + idx / (KT / 4), gk = k0 + (idx % (KT / 4)) * 4;
         if (gr < R) {
           const float* q = p + gr * ld + gk;
           if (VEC) {
@@ -306,15 +309,15 @@ struct Loader {
     const int tid = threadIdx.x;
     if (KC) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < NV; ++i) {
         const int idx = tid + i * GEMM_THREADS;
-        unsigned char* q = img + (idx >> 3) * RS + (idx & 7) * 8;
+        unsigned char* q = img + (idx / (KT / 4)) * RS + (idx % (KT / 4)) * 8;
         *reinterpret_cast<uint2*>(q) =
             make_uint2(x6::cvt_pk_bf16(v[i].x, v[i].y), x6::cvt_pk_bf16(v[i].z, v[i].w));
       }
     } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < KT / 16; ++h) {
         const float* f0 = reinterpret_cast<const float*>(&v[2 * h]);
         const float* f1 = reinterpret_cast<const float*>(&v[2 * h + 1]);
 #pragma unroll
@@ -328,8 +331,9 @@ struct Loader {
 };
 
 // fragment of k-step ks (16 k): lane (row, half h) gets k = 16 ks + 8h .. +7
+template <int KT>
 __device__ __forceinline__ bf16x8v frag(const unsigned char* img, int row, int ks, int h) {
-  const uint4 u = *reinterpret_cast<const uint4*>(img + row * RS + 32 * ks + 16 * h);
+  const uint4 u = *reinterpret_cast<const uint4*>(img + row * rs<KT>() + 32 * ks + 16 * h);
   return __builtin_bit_cast(bf16x8v, u);
 }
 }  // namespace b16
@@ -408,26 +412,28 @@ struct PolX6 {
   }
 };
 
-// bf16 path: K-tile 32, one bf16 plane per operand, two 32x32x16 MFMAs per tile.
-template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+// bf16 path: K-tile KT (32, or 64 with AINP_GEMM_B16_KT=64), one bf16 plane
+// per operand, KT/16 rounds of four 32x32x16 MFMAs per tile.
+template <bool AKC, bool BKC, bool AVEC, bool BVEC, int KTB = 32>
 struct PolB16 {
-  static constexpr int KT = b16::KT;
-  static constexpr int SMEM = 2 * b16::IMG;
-  using LA = b16::Loader<AKC, AVEC>;
-  using LB = b16::Loader<BKC, BVEC>;
+  static constexpr int KT = KTB;
+  static constexpr int IMG = b16::img<KT>();
+  static constexpr int SMEM = 2 * IMG;
+  using LA = b16::Loader<AKC, AVEC, KT>;
+  using LB = b16::Loader<BKC, BVEC, KT>;
   __device__ static __forceinline__ void store(const LA& la, const LB& lb, unsigned char* sm) {
     la.store(sm);
-    lb.store(sm + b16::IMG);
+    lb.store(sm + IMG);
   }
   __device__ static __forceinline__ void compute(const unsigned char* sm, f32x16v (&acc)[2][2],
                                                  int wm, int wn, int li, int lh) {
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int ks = 0; ks < KT / 16; ++ks) {
       bf16x8v a[2], b[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        a[i] = b16::frag(sm, wm + i * 32 + li, ks, lh);
-        b[i] = b16::frag(sm + b16::IMG, wn + i * 32 + li, ks, lh);
+        a[i] = b16::frag<KT>(sm, wm + i * 32 + li, ks, lh);
+        b[i] = b16::frag<KT>(sm + IMG, wn + i * 32 + li, ks, lh);
       }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
@@ -438,7 +444,7 @@ struct PolB16 {
 };
 
 // main loop: PM_F32 exact f32, PM_X6 fp32-accurate split bf16, PM_B16 bf16 operands
-constexpr int PM_F32 = 0, PM_X6 = 1, PM_B16 = 2;
+constexpr int PM_F32 = 0, PM_X6 = 1, PM_B16 = 2, PM_B16K64 = 3;
 template <int PM, bool AKC, bool BKC, bool AVEC, bool BVEC>
 struct PolSel {
   using type = PolF32<AKC, BKC, AVEC, BVEC>;
@@ -449,14 +455,18 @@ struct PolSel<PM_X6, AKC, BKC, AVEC, BVEC> {
 };
 template <bool AKC, bool BKC, bool AVEC, bool BVEC>
 struct PolSel<PM_B16, AKC, BKC, AVEC, BVEC> {
-  using type = PolB16<AKC, BKC, AVEC, BVEC>;
+  using type = PolB16<AKC, BKC, AVEC, BVEC, 32>;
+};
+template <bool AKC, bool BKC, bool AVEC, bool BVEC>
+struct PolSel<PM_B16K64, AKC, BKC, AVEC, BVEC> {
+  using type = PolB16<AKC, BKC, AVEC, BVEC, 64>;
 };
 
 // ================================================================ tile grid
 // Single-buffered LDS + one K-tile of register prefetch: <= 37 KB of LDS and
 // <= 168 VGPRs -> 3 workgroups per CU (768 resident tiles on the chip).
 template <int PM, bool AKC, bool BKC, bool AVEC, bool BVEC>
-__global__ __launch_bounds__(GEMM_THREADS, 3) void gemm_f32_kernel(
+__global__ __launch_bounds__(GEMM_THREADS, PM == PM_B16K64 ? 2 : 3) void gemm_f32_kernel(
     int64_t M, int64_t N, int64_t K, float alpha, GemmPtrs ptrs, int64_t lda,
     int64_t ldb, float beta, int64_t scm, int64_t scn, int nseg, int tiles_n) {
   using Pol = typename PolSel<PM, AKC, BKC, AVEC, BVEC>::type;
@@ -905,7 +915,14 @@ extern "C" int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
   const unsigned gy = ksplit == 1 ? 1u : (ksplit == 2 ? (unsigned)nptr : (unsigned)nb);
   const dim3 grid((unsigned)(tiles_m * tiles_n), gy);
   float* ws = reinterpret_cast<float*>(workspace);
-  if (pm == PM_B16)
+  static const bool k64 = [] {
+    const char* e = getenv("AINP_GEMM_B16_KT");
+    return e && e[0] == '6';
+  }();
+  if (pm == PM_B16 && k64)
+    dispatch_gemm<PM_B16K64>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb,
+                             beta, scm, scn, nseg, (int)tiles_n, g, ws);
+  else if (pm == PM_B16)
     dispatch_gemm<PM_B16>(sk, akc, bkc, avec, bvec, grid, s, M, N, K, alpha, p, lda, ldb, beta,
                           scm, scn, nseg, (int)tiles_n, g, ws);
   else if (pm == PM_X6)

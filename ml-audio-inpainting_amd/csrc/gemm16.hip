@@ -1,0 +1,225 @@
+// gemm16.hip — bf16-operand GEMM for the bf16 configurations (BASELINE C3).
+//
+// C[m][n] = sum_k A[m][k] B[n][k] (+ bias) with A, B stored as bf16 in HBM,
+// both k-contiguous ("NT"), fp32 accumulation on v_mfma_f32_32x32x16_bf16.
+// Replaces, in the bf16 configuration, the three layer-0 GEMMs of nn.LSTM
+// (models/CNNBLSTM/model.py:46-47,77) -- the input projection and its data /
+// weight gradients -- whose producers write the bf16 operands directly in the
+// layouts this kernel wants (the encoder's last BN+ReLU writes X and X^T, the
+// BPTT gradient is cast to dg and dg^T, the weights to W and W^T once per
+// optimizer step), so every operand arrives k-contiguous at 2 bytes/element:
+// half the HBM/L2 bytes of the fp32-staged bf16 loop (gemm.hip PM_B16) and one
+// 16-byte load per 8 elements, no conversion in the main loop.
+//
+// Tile 128 x 128 x 64 per 256-thread workgroup (4 waves as 2 x 2, each wave
+// 64 x 64 = 2 x 2 MFMA 32x32 tiles); A and B images [row][64 k] with 144-byte
+// rows in LDS (conflict-free ds_read_b128 fragments), the next K-tile
+// prefetched in registers (4 x 16 B per operand per thread); <= 168 VGPRs so
+// three workgroups fit per CU.  XCD-aware block order as gemm.hip.  Split-K:
+// blockIdx.y = split s covers k in [s*kc, min(K, (s+1)*kc)) and writes slab
+// C + s*strideC (summed by ainp_sum_slabs in fixed order).
+#include "common.h"
+
+namespace ainp {
+namespace g16 {
+
+constexpr int BM = 128, BN = 128, BK = 64, THREADS = 256;
+constexpr int RS = BK * 2 + 16;      // image row bytes: 64 bf16 + 16 B pad
+constexpr int IMG = 128 * RS;        // one operand image
+
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
+
+// 128 rows x 64 k of a k-contiguous bf16 operand: chunk c = tid + 256 i
+// (i < 4) is row c / 8, 16-byte column c % 8 (8 threads read one 128-B row).
+struct Loader {
+  uint4 v[4];
+  __device__ __forceinline__ void load(const uint16_t* __restrict__ p, int64_t ld, int64_t r0,
+                                       int64_t k0, int64_t R, int64_t kend) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + i * THREADS;
+      const int64_t r = r0 + (c >> 3), k = k0 + (c & 7) * 8;
+      uint4 x = make_uint4(0u, 0u, 0u, 0u);
+      if (r < R && k < kend) x = *reinterpret_cast<const uint4*>(p + r * ld + k);
+      v[i] = x;
+    }
+  }
+  __device__ __forceinline__ void store(unsigned char* img) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c = tid + i * THREADS;
+      *reinterpret_cast<uint4*>(img + (c >> 3) * RS + (c & 7) * 16) = v[i];
+    }
+  }
+};
+
+__device__ __forceinline__ bf16x8v frag(const unsigned char* img, int row, int ks, int h) {
+  return __builtin_bit_cast(bf16x8v,
+                            *reinterpret_cast<const uint4*>(img + row * RS + 32 * ks + 16 * h));
+}
+
+struct Bias {
+  const float* a1;   // n in [0, nsplit): a1[n] + a2[n]
+  const float* a2;
+  const float* b1;   // n in [nsplit, N): b1[n - nsplit] + b2[n - nsplit]
+  const float* b2;
+  int64_t nsplit;
+};
+
+__global__ __launch_bounds__(THREADS, 3) void gemm_bf16nt_kernel(
+    int64_t M, int64_t N, int64_t K, const uint16_t* __restrict__ A, int64_t lda,
+    const uint16_t* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
+    int64_t kc, int64_t strideC, Bias bias, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * IMG];
+  // XCD-aware order (gemm.hip): each XCD owns a contiguous range of linear
+  // tiles; within it groups of 8 n-tiles walk down m (A panels shared in L2).
+  const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t first_n = (bid / per_group) * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+
+  const int64_t split = blockIdx.y;
+  const int64_t kbeg = split * kc;
+  const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
+  float* Cs = C + split * strideC;
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  Loader la, lb;
+  if (kbeg < kend) {
+    la.load(A, lda, m0, kbeg, M, kend);
+    lb.load(B, ldb, n0, kbeg, N, kend);
+  }
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    if (k0 > kbeg) __syncthreads();     // every wave is done with the images
+    la.store(smem);
+    lb.store(smem + IMG);
+    __syncthreads();
+    if (k0 + BK < kend) {               // next K-tile's loads fly during the MFMAs
+      la.load(A, lda, m0, k0 + BK, M, kend);
+      lb.load(B, ldb, n0, k0 + BK, N, kend);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8v a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = frag(smem, wm + i * 32 + li, ks, lh);
+        b[i] = frag(smem + IMG, wn + i * 32 + li, ks, lh);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: D[row=(r&3)+8*(r>>2)+4*lh][col=li] of each 32x32 tile
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t n = n0 + wn + j * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (n < bias.nsplit) {
+      if (bias.a1) bv += bias.a1[n];
+      if (bias.a2) bv += bias.a2[n];
+    } else {
+      if (bias.b1) bv += bias.b1[n - bias.nsplit];
+      if (bias.b2) bv += bias.b2[n - bias.nsplit];
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cs[m * ldc + n] = acc[i][j][r] + bv;
+      }
+  }
+}
+
+// fp32 [R][ld_in] -> bf16 out [R][ld_out] (optional) and its transpose
+// outT [C][ld_t] (optional); 64 x 64 tiles through LDS, round-to-nearest-even.
+__global__ __launch_bounds__(256) void cast_bf16_t_kernel(const float* __restrict__ x, int64_t R,
+                                                          int64_t Cc, int64_t ld_in,
+                                                          uint16_t* __restrict__ out,
+                                                          int64_t ld_out,
+                                                          uint16_t* __restrict__ outT,
+                                                          int64_t ld_t) {
+  __shared__ uint16_t tile[64][66];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    uint16_t b = 0;
+    if (r < R && c < Cc) {
+      const __bf16 h = (__bf16)x[r * ld_in + c];
+      b = __builtin_bit_cast(uint16_t, h);
+      if (out) out[r * ld_out + c] = b;
+    }
+    tile[i][tx] = b;
+  }
+  if (!outT) return;
+  __syncthreads();
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < Cc && r < R) outT[c * ld_t + r] = tile[tx][i];
+  }
+}
+
+}  // namespace g16
+}  // namespace ainp
+
+using namespace ainp;
+
+extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t* A, int64_t lda,
+                                const uint16_t* B, int64_t ldb, float* C, int64_t ldc,
+                                const float* bias_a1, const float* bias_a2, const float* bias_b1,
+                                const float* bias_b2, int64_t bias_nsplit, int nsplit, int64_t kc,
+                                int64_t strideC, void* stream) {
+  if (M < 0 || N < 0 || K < 0 || !A || !B || !C || nsplit < 1 || nsplit > 65535 ||
+      lda % 8 || ldb % 8 || lda < K || ldb < K || ldc < N || (K % 8) ||
+      ((uintptr_t)A & 15) || ((uintptr_t)B & 15))
+    return record_msg("ainp_gemm_bf16nt: bad argument (16-byte aligned rows, K % 8 == 0)");
+  if (nsplit > 1 && (kc < g16::BK || kc % g16::BK || (int64_t)nsplit * kc < K ||
+                     (int64_t)(nsplit - 1) * kc >= K || strideC < M * ldc))
+    return record_msg("ainp_gemm_bf16nt: split-K needs kc % 64 == 0 covering K, strideC >= M*ldc");
+  if (nsplit == 1) kc = K;
+  if (M == 0 || N == 0) return AINP_OK;
+  g16::Bias b{bias_a1, bias_a2, bias_b1, bias_b2, bias_nsplit};
+  const int64_t tiles_n = cdiv(N, g16::BN);
+  const dim3 grid((unsigned)(cdiv(M, g16::BM) * tiles_n), (unsigned)nsplit);
+  hipLaunchKernelGGL(g16::gemm_bf16nt_kernel, grid, dim3(g16::THREADS), 0, as_stream(stream), M, N,
+                     K, A, lda, B, ldb, C, ldc, kc, strideC, b, (int)tiles_n);
+  return check_launch("gemm_bf16nt");
+}
+
+extern "C" int ainp_cast_bf16_t(const float* x, int64_t R, int64_t C, int64_t ld_in,
+                                uint16_t* out, int64_t ld_out, uint16_t* outT, int64_t ld_t,
+                                void* stream) {
+  if (!x || R < 0 || C < 0 || ld_in < C || (!out && !outT) || (out && ld_out < C) ||
+      (outT && ld_t < R))
+    return record_msg("ainp_cast_bf16_t: bad argument");
+  if (R == 0 || C == 0) return AINP_OK;
+  hipLaunchKernelGGL(g16::cast_bf16_t_kernel, dim3((unsigned)cdiv(C, 64), (unsigned)cdiv(R, 64)),
+                     dim3(256), 0, as_stream(stream), x, R, C, ld_in, out, ld_out, outT, ld_t);
+  return check_launch("cast_bf16_t");
+}

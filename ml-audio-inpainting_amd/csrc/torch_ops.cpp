@@ -765,6 +765,74 @@ void channel_sum(const Tensor& m, const Tensor& out) {
       "channel_sum");
 }
 
+
+// ------------------------------------------------------------------- bf16 GEMM operands
+uint16_t* bf16p(const Tensor& t, const char* name, bool contig = true) {
+  return reinterpret_cast<uint16_t*>(dev<void>(t, name, at::kBFloat16, contig));
+}
+
+void bn_relu_apply_ntcf_bf16(const Tensor& x, const Tensor& scale, const Tensor& shift,
+                             const Tensor& out, const Tensor& outT) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  numel_is(scale, C, "scale");
+  numel_is(shift, C, "shift");
+  numel_is(out, x.numel(), "out");
+  TORCH_CHECK(outT.dim() == 2 && outT.size(0) == C * H && outT.size(1) >= N * W,
+              "outT must be [C*H, >= N*W]");
+  TORCH_CHECK(outT.stride(1) == 1, "outT rows must be contiguous");
+  chk(ainp_bn_relu_apply_ntcf_bf16(dev(x, "x"), dev(scale, "scale"), dev(shift, "shift"),
+                                   bf16p(out, "out"), bf16p(outT, "outT", false), outT.stride(0),
+                                   N, (int)C, H, W, stream_of(x)),
+      "bn_relu_apply_ntcf_bf16");
+}
+
+void gemm_bf16nt(const Tensor& A, const Tensor& B, const Tensor& C, int64_t K,
+                 const OptT& bias_a1, const OptT& bias_a2, const OptT& bias_b1,
+                 const OptT& bias_b2, int64_t bias_nsplit, int64_t nsplit, int64_t kc) {
+  GUARD(C);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1,
+              "gemm_bf16nt: A [M, >=K], B [N, >=K] with unit-stride rows");
+  TORCH_CHECK(A.size(1) >= K && B.size(1) >= K, "gemm_bf16nt: K exceeds the operand rows");
+  const int64_t M = A.size(0), N = B.size(0);
+  TORCH_CHECK((C.dim() == 2 && nsplit == 1) || (C.dim() == 3 && C.size(0) == nsplit),
+              "gemm_bf16nt: C [M, N] or split-K slabs [nsplit, M, N]");
+  TORCH_CHECK(C.size(-2) == M && C.size(-1) == N && C.stride(-1) == 1, "gemm_bf16nt: C shape");
+  same_device(A, C);
+  same_device(B, C);
+  chk(ainp_gemm_bf16nt(M, N, K, bf16p(A, "A", false), A.stride(0), bf16p(B, "B", false),
+                       B.stride(0), dev(C, "C", at::kFloat, false), C.stride(-2),
+                       opt(bias_a1, "bias_a1"), opt(bias_a2, "bias_a2"), opt(bias_b1, "bias_b1"),
+                       opt(bias_b2, "bias_b2"), bias_nsplit, (int)nsplit, kc,
+                       C.dim() == 3 ? C.stride(0) : 0, stream_of(C)),
+      "gemm_bf16nt");
+}
+
+void cast_bf16_t(const Tensor& x, const OptT& out, const OptT& outT) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D with unit-stride rows");
+  const int64_t R = x.size(0), Cc = x.size(1);
+  uint16_t* o = nullptr;
+  uint16_t* ot = nullptr;
+  int64_t ldo = Cc, ldt = R;
+  if (out.has_value() && out->defined()) {
+    TORCH_CHECK(out->dim() == 2 && out->size(0) == R && out->size(1) == Cc && out->stride(1) == 1,
+                "out must be [R, C]");
+    o = bf16p(*out, "out", false);
+    ldo = out->stride(0);
+  }
+  if (outT.has_value() && outT->defined()) {
+    TORCH_CHECK(outT->dim() == 2 && outT->size(0) == Cc && outT->size(1) == R &&
+                    outT->stride(1) == 1,
+                "outT must be [C, R]");
+    ot = bf16p(*outT, "outT", false);
+    ldt = outT->stride(0);
+  }
+  chk(ainp_cast_bf16_t(dev(x, "x", at::kFloat, false), R, Cc, x.stride(0), o, ldo, ot, ldt,
+                       stream_of(x)),
+      "cast_bf16_t");
+}
 }  // namespace
 
 TORCH_LIBRARY(ainp, m) {
@@ -842,6 +910,11 @@ TORCH_LIBRARY(ainp, m) {
   m.def("leaky_bwd_ld(Tensor g, Tensor y, int rows, float slope, int ldo, Tensor(a!) out) -> ()");
   m.def("mul(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("channel_sum(Tensor m, Tensor(a!) out) -> ()");
+  m.def("bn_relu_apply_ntcf_bf16(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, "
+        "Tensor(b!) outT) -> ()");
+  m.def("gemm_bf16nt(Tensor A, Tensor B, Tensor(a!) C, int K, Tensor? bias_a1, Tensor? bias_a2, "
+        "Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, int kc) -> ()");
+  m.def("cast_bf16_t(Tensor x, Tensor(a!)? out, Tensor(b!)? outT) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
@@ -889,6 +962,9 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("leaky_bwd_ld", &leaky_bwd_ld);
   m.impl("mul", &mul);
   m.impl("channel_sum", &channel_sum);
+  m.impl("bn_relu_apply_ntcf_bf16", &bn_relu_apply_ntcf_bf16);
+  m.impl("gemm_bf16nt", &gemm_bf16nt);
+  m.impl("cast_bf16_t", &cast_bf16_t);
 }
 
 // The ops write through raw device pointers like the C ABI; autograd is the
@@ -939,4 +1015,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("leaky_bwd_ld", torch::CppFunction::makeFallthrough());
   m.impl("mul", torch::CppFunction::makeFallthrough());
   m.impl("channel_sum", torch::CppFunction::makeFallthrough());
+  m.impl("bn_relu_apply_ntcf_bf16", torch::CppFunction::makeFallthrough());
+  m.impl("gemm_bf16nt", torch::CppFunction::makeFallthrough());
+  m.impl("cast_bf16_t", torch::CppFunction::makeFallthrough());
 }

@@ -570,3 +570,111 @@ def test_im2col_col2im(ops, N, C, H, W, k, s, pad, ones, pad4):
     want = Fnn.fold(dcol[:, :, :P].double(), (H, W), k, padding=pad, stride=s)
     assert dx.shape == (N, C, H, W)
     assert rel(dx, want) < 1e-6
+
+
+# ------------------------------------------------- bf16-operand GEMM (gemm16.hip)
+def _tobf16(x):
+    return x.to(torch.bfloat16)
+
+
+@pytest.mark.parametrize("M,N,K,S", [(300, 200, 520, 1), (128, 256, 1024, 1), (257, 130, 4096, 3),
+                                     (1000, 77, 5376, 2)])
+def test_gemm_bf16nt_matches_fp64_of_bf16_operands(M, N, K, S):
+    """ainp_gemm_bf16nt vs fp64 products of the same bf16 operands: bf16 x bf16
+    products are exact in fp32, so only the fp32 accumulation differs (<= 1e-5
+    relative); ragged M / N tiles, K % 64 != 0, split-K slabs, bias segments."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(M + N + K)
+    A = _tobf16(torch.randn(M, K, generator=g)).cuda()
+    B = _tobf16(torch.randn(N, K + 16, generator=g)).cuda()[:, :K]     # ld > K
+    ref = A.double().cpu() @ B.double().cpu().T
+    if S == 1:
+        nb = N // 2
+        bias = [torch.randn(n, generator=g).cuda() for n in (nb, nb, N - nb, N - nb)]
+        C = ops.gemm_bf16nt(A, B, K=K, bias=tuple(bias), bias_nsplit=nb)
+        bref = torch.cat([bias[0] + bias[1], bias[2] + bias[3]]).double().cpu()
+        ref = ref + bref
+    else:
+        C = torch.empty(M, N, device="cuda")
+        kc = -(-K // S // 64) * 64
+        slabs = torch.empty(S, M, N, device="cuda")
+        torch.ops.ainp.gemm_bf16nt(A, B, slabs, K, None, None, None, None, 0, S, kc)
+        ops.sum_slabs(slabs, S, out=C.view(-1))
+    torch.cuda.synchronize()
+    err = (C.double().cpu() - ref).norm() / ref.norm()
+    assert err < 1e-5, float(err)
+
+
+def test_cast_bf16_t_and_ntcf_bf16_bridge_bit_exact():
+    """The bf16 operand producers round to nearest-even exactly as torch's
+    .to(bfloat16): cast (+ transpose into a strided view) and the encoder's
+    BN+ReLU writing X [N, W, C*H] and X^T [C*H, N*W]."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(300, 200, generator=g).cuda()
+    out, outT = ops.cast_bf16_t(x, out=True, outT=True)
+    wide = torch.zeros(200, 640, device="cuda", dtype=torch.bfloat16)
+    ops.cast_bf16_t(x, outT=wide[:, 320:620])
+    ref = x.to(torch.bfloat16)
+    assert torch.equal(out, ref) and torch.equal(outT, ref.T)
+    assert torch.equal(wide[:, 320:620], ref.T) and not wide[:, :320].any()
+    N, C, H, W = 2, 64, 9, 12
+    y = torch.randn(N, C, H, W, generator=g).cuda()
+    sc = torch.rand(C, generator=g).cuda() + 0.5
+    sh = torch.randn(C, generator=g).cuda() * 0.1
+    X16, XT16 = ops.bn_relu_apply_ntcf_bf16(y, sc, sh)
+    z = torch.relu(y * sc[None, :, None, None] + sh[None, :, None, None])
+    # fmaf vs torch's separate mul+add can differ by one fp32 rounding: compare
+    # against both roundings of the fused value
+    zf = torch.relu(torch.addcmul(sh[None, :, None, None], y, sc[None, :, None, None]))
+    xr = z.permute(0, 3, 1, 2).reshape(N, W, C * H)
+    xf = zf.permute(0, 3, 1, 2).reshape(N, W, C * H)
+    ok = (X16 == xr.to(torch.bfloat16)) | (X16 == xf.to(torch.bfloat16))
+    assert bool(ok.all())
+    assert torch.equal(XT16, X16.reshape(N * W, C * H).T)
+
+
+def test_bf16_layer0_operand_path_matches_staged_bf16_path():
+    """The bf16 configuration's layer-0 path on bf16 operands in HBM (bridge +
+    cast + gemm_bf16nt) against the fp32-staged bf16 GEMM loop it replaces, on
+    a C2-shaped batch (N*T % 8 == 0): both round every operand to bf16 once, so
+    only the fp32 accumulation order differs -- output, loss and every
+    gradient within 1e-4 relative (ReLU-branch flips aside)."""
+    import ainp.cnnblstm as CB
+    from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
+    cfg = {"data": {"spectrogram": {"n_fft": 512}},
+           "model": {"in_channels": 1, "num_lstm_layers": 2, "lstm_hidden_dim": 128,
+                     "enc_filters": [16, 32], "dec_filters": [16, 32]},
+           "accel": {"dtype": "bf16"}}
+    g = torch.Generator().manual_seed(11)
+    N, F, T = 4, 257, 90
+    x = (torch.randn(N, F, T, generator=g) - 2).cuda()
+    m = torch.zeros(N, F, T)
+    m[:, :, 40:48] = 1
+    m = m.cuda()
+    tgt = torch.polar(torch.rand(N, F, T, generator=g) * 5, torch.rand(N, F, T, generator=g)).to(
+        torch.complex64).cuda()
+    res = []
+    for use16 in (True, False):
+        torch.manual_seed(0)
+        model = StackedBLSTMCNN(config=cfg).cuda().train()
+        orig = CB._l0_bf16_ok
+        if not use16:
+            CB._l0_bf16_ok = lambda y: False
+        try:
+            y = model(x.unsqueeze(1))
+            loss = l1_pow10_loss(y, m, tgt)
+            loss.backward()
+        finally:
+            CB._l0_bf16_ok = orig
+        res.append((y.detach().double().cpu(), float(loss),
+                    {k: p.grad.double().cpu() for k, p in model.named_parameters()}))
+    from ainp.smoke import BN_FED_BIASES
+    (y1, l1, g1), (y0, l0, g0) = res
+    assert (y1 - y0).norm() / y0.norm() < 1e-4
+    assert abs(l1 - l0) / abs(l0) < 1e-4
+    for k in g0:
+        if k in BN_FED_BIASES:
+            continue   # BN-fed conv biases: exact gradient 0 (SURVEY Q10)
+        e = float((g1[k] - g0[k]).norm() / max(g0[k].norm(), 1e-30))
+        assert e < 1e-3, (k, e)

@@ -26,8 +26,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--dtype", choices=("fp32", "bf16"), default="fp32")
-    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--workload", choices=("cnnblstm", "gan"), default="cnnblstm")
+    ap.add_argument("--clip-s", type=float, default=5.0)
     args = ap.parse_args()
+    if args.workload == "gan":
+        return gan(args)
+    args.batch = args.batch or 32
     from ainp import ops
     from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
     from ainp.optim import Adam
@@ -52,6 +57,35 @@ def main():
         opt.step()
     torch.cuda.synchronize()
     print(f"{args.dtype}: {1e3 * (time.perf_counter() - t0) / args.steps:.3f} ms/step "
+          f"over {args.steps} steps; kernel tables / {3 + args.steps} = per step")
+
+
+def gan(args):
+    """The bench's GAN step (C4: 5 s / T=626; --clip-s 8: C5, T=1001)."""
+    from ainp import ops
+    from ainp import gan as G
+    from ainp.gan_train import GanTrainer
+    dev = torch.device("cuda", 0)
+    B = args.batch or 8
+    S = int(16000 * args.clip_s)
+    g = 1600 if args.clip_s >= 8 else 3200
+    T = 1 + S // 128
+    torch.manual_seed(0)
+    tr = GanTrainer(dict(bench.GAN_CFG, accel={"dtype": args.dtype}), G.PConvUNet().to(dev),
+                    G.Discriminator().to(dev), G.VGGLoss(dev))
+    audio = torch.from_numpy(bench.synthetic_clips(B, S, 5)).to(dev)
+    rng = np.random.default_rng(2)
+    starts = torch.from_numpy(rng.integers(0, S - g + 1, size=(3 + args.steps, B))).to(dev)
+    t0 = None
+    for i in range(3 + args.steps):
+        if i == 3:
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+        o, im, _, m = ops.stft_features(audio, starts[i], g, 512, 128, 512, n_frames=T,
+                                        mode=ops.FEAT_GAN, outputs=(True, True, False, True))
+        tr.step(o.unsqueeze(1), im.unsqueeze(1), m.unsqueeze(1))
+    torch.cuda.synchronize()
+    print(f"gan {args.dtype} T={T}: {1e3 * (time.perf_counter() - t0) / args.steps:.3f} ms/step "
           f"over {args.steps} steps; kernel tables / {3 + args.steps} = per step")
 
 
