@@ -24,6 +24,8 @@ through `comm` (SyncBN), so a DP run matches the single-process reference.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import yaml
@@ -52,7 +54,7 @@ class _ConvStackFn(torch.autograd.Function):
     """
 
     @staticmethod
-    def forward(ctx, x, spec, training, out_ntcf, comm, bf16, l0_box, *params):
+    def forward(ctx, x, spec, training, out_ntcf, comm, bf16, l0_box, defer_wgrad, *params):
         N, _, H, W = x.shape
         saved_y = []
         affine = []          # per BN block: (scale, shift, save or None)
@@ -112,6 +114,7 @@ class _ConvStackFn(torch.autograd.Function):
             out = saved_y[-1]
         ctx.spec = spec
         ctx.bf16 = bf16
+        ctx.defer_wgrad = defer_wgrad
         ctx.out_ntcf = out_ntcf
         ctx.comm = comm
         ctx.count = count
@@ -160,13 +163,35 @@ class _ConvStackFn(torch.autograd.Function):
             else:
                 xin = x
                 pro = (None, None)
-            dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
+            if ctx.defer_wgrad == "queue":
+                # off the critical path: queued, launched on the side stream when
+                # the BPTT recurrence (64 workgroups) starts -- filling the CUs
+                # it leaves idle (see _Deferred)
+                Cout, Cin = w.shape[0], w.shape[1]
+                dw = torch.empty(Cout, Cin, 3, 3, device=gy.device)
+                db = torch.empty(Cout, device=gy.device)
+                # the queue holds aliases only: autograd's AccumulateGrad steals a
+                # gradient tensor nobody else references instead of cloning it
+                # (a clone would copy it before the side stream writes it)
+                dwv, dbv = _alias(dw), _alias(db)
+                pr, bf = pro, ctx.bf16
+                _Deferred.push(gy.device, lambda xin=xin, gy=gy, pr=pr, dwv=dwv, dbv=dbv, bf=bf:
+                               ops.conv3x3_wgrad(xin, gy, pr[0], pr[1], bf16=bf, out=(dwv, dbv)),
+                               (xin, gy) + tuple(t for t in pro if t is not None), (dwv, dbv))
+            elif ctx.defer_wgrad:
+                # off the critical path: on the side stream, overlapping the next
+                # (HBM-bound) BatchNorm backward passes
+                with _side_work(gy.device) as sw:
+                    dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
+                    sw.handoff((xin, gy) + tuple(t for t in pro if t is not None), (dw, db))
+            else:
+                dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
             grads[p0], grads[p0 + 1] = dw, db
             if bi > 0 or ctx.needs_input_grad[0]:
                 g = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16)
                 if bi == 0:
                     gx = g
-        return (gx, None, None, None, None, None, None, *grads)
+        return (gx, None, None, None, None, None, None, None, *grads)
 
 
 def _l0_bf16_ok(y):
@@ -246,6 +271,8 @@ class _BLSTMFn(torch.autograd.Function):
             l016 = ctx.l016 if l == 0 else None
             Il = inp.shape[1] if l016 is None else ctx.I
             dg = ops.lstm_rec_bwd(dh, gates, cell, hf, hr, H)          # [N,T,8H]
+            if l == L - 1:
+                _Deferred.flush(dh.device)   # decoder / projection weight gradients
             dg2 = dg.view(NT, 8 * H)
             if l016 is not None:
                 # bf16 operands of the layer-0 data / weight gradients
@@ -304,12 +331,28 @@ class _BLSTMFn(torch.autograd.Function):
                     dxi = ops.sum_slabs(sl, 4).view(NT, Il)
                 dh = dxi.view(N, T, Il)
                 dx = dh
-        done = torch.cuda.Event()
-        done.record(side)
-        main.wait_event(done)
         for gr in grads:
             if gr is not None:
                 gr.record_stream(main)    # side-stream memory handed to autograd
+        if ctx.sink is None:
+            # nothing on the current stream reads these gradients before the
+            # optimizer: join the side stream at the end of the backward pass
+            # (engine callback) so the layer-0 weight gradient overlaps the
+            # encoder backward.  Non-view aliases, so AccumulateGrad stores them
+            # instead of cloning (a clone would read them before they exist).
+            dev = dh.device
+
+            def join():
+                ev = torch.cuda.Event()
+                ev.record(_side_stream(dev))
+                torch.cuda.current_stream(dev).wait_event(ev)
+            torch.autograd.Variable._execution_engine.queue_callback(join)
+            grads = [_alias(gr) if gr is not None else None for gr in grads]
+        else:
+            # data parallel: the gradient hooks read them as autograd hands them over
+            done = torch.cuda.Event()
+            done.record(side)
+            main.wait_event(done)
         if ctx.early_done:
             for p in ctx.wih0:            # side-stream .grad buffers read by the optimizer
                 p.grad.record_stream(main)
@@ -358,6 +401,90 @@ def _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, sink, wih0, rows=None, l016=Non
 _SIDE_STREAMS: dict = {}
 
 
+def _alias(t):
+    """A second tensor object on the same storage that is NOT a view: a view
+    keeps its base alive, which raises the base's reference count and makes
+    autograd's AccumulateGrad clone the gradient instead of stealing it."""
+    return torch.empty(0, device=t.device, dtype=t.dtype).set_(
+        t.untyped_storage(), t.storage_offset(), t.shape, t.stride())
+
+
+class _Deferred:
+    """Weight-gradient launches queued during the backward (decoder convs,
+    projection) and released onto the side stream at a chosen point -- when
+    the first BPTT recurrence has been launched -- so they fill the CUs that
+    latency-bound kernel leaves idle instead of competing with the decoder's
+    data-gradient chain.  Their output tensors are handed to autograd at
+    queue time (written later); an engine callback releases anything left and
+    makes the current stream join the side stream before the backward ends."""
+
+    _queues: dict = {}
+
+    @classmethod
+    def push(cls, device, fn, inputs, outputs):
+        q = cls._queues.setdefault(device, [])
+        if not q:
+            torch.autograd.Variable._execution_engine.queue_callback(
+                lambda: cls.flush(device, join=True))
+        q.append((fn, inputs, outputs))
+
+    @classmethod
+    def flush(cls, device, join=False):
+        q = cls._queues.pop(device, [])
+        if q:
+            with _side_work(device, callback=False) as sw:
+                for fn, inputs, outputs in q:
+                    fn()
+                    sw.handoff(inputs, outputs)
+        if join and q is not None:
+            done = torch.cuda.Event()
+            done.record(_side_stream(device))
+            torch.cuda.current_stream(device).wait_event(done)
+
+
+class _side_work:
+    """Context: queue work on the device's side stream after everything the
+    current stream has issued so far; the current stream joins the side stream
+    at the end of the backward pass (autograd engine callback), before any
+    optimizer step can read what the side stream produced."""
+
+    def __init__(self, device, callback=True):
+        self.device = device
+        self.callback = callback
+
+    def __enter__(self):
+        dev = self.device
+        self.main = torch.cuda.current_stream(dev)
+        self.side = _side_stream(dev)
+        ev = torch.cuda.Event()
+        ev.record(self.main)
+        self.side.wait_event(ev)
+        self._ctx = torch.cuda.stream(self.side)
+        self._ctx.__enter__()
+
+        def join():
+            done = torch.cuda.Event()
+            done.record(_side_stream(dev))
+            torch.cuda.current_stream(dev).wait_event(done)
+        if self.callback:
+            torch.autograd.Variable._execution_engine.queue_callback(join)
+        return self
+
+    def handoff(self, inputs, outputs):
+        """Caching-allocator bookkeeping: inputs (made on the current stream)
+        are read on the side stream; outputs (made on the side stream) are
+        read later on the current one."""
+        for t in inputs:
+            t.record_stream(self.side)
+        for t in outputs:
+            if t is not None:
+                t.record_stream(self.main)
+
+    def __exit__(self, *exc):
+        self._ctx.__exit__(*exc)
+        return False
+
+
 def _side_stream(device):
     s = _SIDE_STREAMS.get(device)
     if s is None:
@@ -371,7 +498,7 @@ class _ProjFn(torch.autograd.Function):
     """nn.Linear(2H, C*F) + view(N,T,C,F).permute(0,2,3,1) -> [N, C, F, T]."""
 
     @staticmethod
-    def forward(ctx, h, w, b, C, F, bf16=False):
+    def forward(ctx, h, w, b, C, F, bf16=False, defer_wgrad=False):
         N, T, K = h.shape
         out = torch.empty(N, C, F, T, device=h.device, dtype=torch.float32)
         NO = C * F
@@ -381,6 +508,7 @@ class _ProjFn(torch.autograd.Function):
         ctx.save_for_backward(h, w)
         ctx.shape = (N, C, F, T)
         ctx.bf16 = bf16
+        ctx.defer_wgrad = defer_wgrad
         return out
 
     @staticmethod
@@ -404,16 +532,26 @@ class _ProjFn(torch.autograd.Function):
         # dw[col][k] = sum_{n,t} g_n[col][t] h_n[t][k]: split the example sum
         # over S pointer batches (S partial slabs, ksplit mode 2) so the small
         # [C*F, 2H] output still fills the chip, then combine in fixed order.
-        S = _split_count(N)
-        per = N // S
-        slabs = torch.empty(S, NO, K, device=h.device, dtype=torch.float32)
-        ops.gemm(NO, K, T, [g[i * per] for i in range(S)], T, 1,
-                 [h[i * per] for i in range(S)], K, 1, [slabs[i] for i in range(S)], K, 1,
-                 strideA=NO * T, strideB=T * K, nstrided=per, ksplit=2, bf16=ctx.bf16)
-        dw = ops.sum_slabs(slabs, S).view(NO, K)
-        # db[col] = sum_{n,t} g_n[col][t]
-        db = ops.rowsum_batched(g.view(N, NO, T))
-        return dh, dw, db, None, None, None
+        bf16 = ctx.bf16
+
+        def wgrad(dw, db, g=g, h=h):
+            S = _split_count(N)
+            per = N // S
+            slabs = torch.empty(S, NO, K, device=h.device, dtype=torch.float32)
+            ops.gemm(NO, K, T, [g[i * per] for i in range(S)], T, 1,
+                     [h[i * per] for i in range(S)], K, 1, [slabs[i] for i in range(S)], K, 1,
+                     strideA=NO * T, strideB=T * K, nstrided=per, ksplit=2, bf16=bf16)
+            ops.sum_slabs(slabs, S, out=dw.view(-1))
+            # db[col] = sum_{n,t} g_n[col][t]
+            ops.rowsum_batched(g.view(N, NO, T), out=db)
+        dw = torch.empty(NO, K, device=g.device)
+        db = torch.empty(NO, device=g.device)
+        if ctx.defer_wgrad:
+            dwv, dbv = _alias(dw), _alias(db)     # aliases only (see _ConvStackFn)
+            _Deferred.push(g.device, lambda: wgrad(dwv, dbv), (g, h), (dwv, dbv))
+        else:
+            wgrad(dw, db)
+        return dh, dw, db, None, None, None, None
 
 
 def _split_count(n):
@@ -501,6 +639,9 @@ class StackedBLSTMCNN(nn.Module):
         # set to an ainp.dist.GradAllReducer (data parallel): the layer-0 input
         # weight gradients are computed in chunks and all-reduced as they complete
         self.grad_reducer = None
+        # decoder / projection weight gradients overlap the BPTT on a side stream
+        self.defer_wgrad = os.environ.get("AINP_DEFER_WGRAD", "1") != "0"
+        self.defer_wgrad_encoder = os.environ.get("AINP_DEFER_ENC", "1") != "0"
 
     # -- helpers ----------------------------------------------------------
     @staticmethod
@@ -530,15 +671,27 @@ class StackedBLSTMCNN(nn.Module):
         x = x.contiguous()
         spec, params = self._stack(self.encoder)
         box = {} if self.bf16 else None       # layer-0 bf16 operands (encoder -> BLSTM)
-        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, box, *params)
+        defer_enc = (self.defer_wgrad_encoder and self.training and torch.is_grad_enabled()
+                     and self.grad_reducer is None and self.comm is None)
+        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, box, defer_enc,
+                               *params)
         sink = self.grad_reducer if (self.training and torch.is_grad_enabled()) else None
         z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, self.bf16, sink, box,
                            *self.lstm._flat_weights)
+        # decoder / projection weight gradients on the side stream, overlapping the
+        # BPTT recurrence (64 workgroups) -- not under data parallelism, whose
+        # gradient hooks read each gradient as soon as autograd hands it over
+        # (and only while the .grad buffers are empty: the deferred outputs are
+        # written after autograd receives them, so they cannot be accumulated into)
+        defer = (self.defer_wgrad and self.training and sink is None and self.comm is None
+                 and all(q.grad is None for m in (self.projection, self.decoder)
+                         for q in m.parameters()))
         # model.py:82 hard-codes 16 decoder channels
         p = _ProjFn.apply(z, self.projection.weight, self.projection.bias, 16, freq_bins,
-                          self.bf16)
+                          self.bf16, defer)
         spec, params = self._stack(self.decoder)
-        y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, self.bf16, None, *params)
+        y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, self.bf16, None,
+                               "queue" if defer else False, *params)
         return y.squeeze(1)
 
     def reconstruct_spectrogram(self, log_spectrogram_gap, gap_mask):

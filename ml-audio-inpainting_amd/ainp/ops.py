@@ -363,12 +363,16 @@ def conv3x3_dgrad(dy, w, bf16=False):
     return dx
 
 
-def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False):
+def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False, out=None):
+    """out: optional preallocated (dw, db) to write."""
     _req(x, "x"); _req(dy, "dy")
     N, Cin, H, W = x.shape
     Cout = dy.shape[1]
-    dw = torch.empty(Cout, Cin, 3, 3, device=x.device, dtype=torch.float32)
-    db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
+    if out is not None:
+        dw, db = out
+    else:
+        dw = torch.empty(Cout, Cin, 3, 3, device=x.device, dtype=torch.float32)
+        db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
     ws_bytes = _lib.lib.ainp_conv3x3_wgrad_workspace(N, Cin, Cout, H, W)
     ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
     _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws, CONV_BF16 if bf16 else 0)
@@ -503,9 +507,10 @@ def sum_slabs(x, nslabs, out=None):
     return out
 
 
-def rowsum_batched(x3d):
+def rowsum_batched(x3d, out=None):
     nb, rows, cols = x3d.shape
-    out = torch.empty(rows, device=x3d.device, dtype=torch.float32)
+    if out is None:
+        out = torch.empty(rows, device=x3d.device, dtype=torch.float32)
     _T.rowsum_batched(x3d, out)
     return out
 
