@@ -445,6 +445,24 @@ int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, int H0, int W
                          int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
                          int pad, int act, float slope, int crop_h, int crop_w, int flags,
                          void* workspace, void* stream);
+/* bf16 configurations (C4 / C5), channel-last variant for sources whose
+ * channel counts are multiples of 32: ainp_nchw_to_nhwc16 writes a source
+ * x [N][C][H][W] times its mask plane m [N][H][W] (may be NULL) as bf16
+ * (nearest-even) out [N][H][W][C]; ainp_conv_weight_nhwc16 writes the weights
+ * as bf16 wt16 [Cout][K] (k = tap*C0 + ci, then KK*C0 + tap*C1 + ci); then
+ * ainp_conv_gen_fwd_nhwc16 is ainp_conv_gen_fwd_ex(AINP_CONV_BF16) on those
+ * operands (same resampling of source 0, ratio / scale / bias / stats /
+ * activation epilogue and split-K workspace; no crop, Cout > 1).  16-byte
+ * aligned buffers. */
+int ainp_nchw_to_nhwc16(const float* x, const float* m, int64_t N, int C, int H, int W,
+                        uint16_t* out, void* stream);
+int ainp_conv_weight_nhwc16(const float* w, int Cout, int C0, int C1, int KH, int KW,
+                            uint16_t* wt16, void* stream);
+int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0, const uint16_t* x1,
+                             int C1, int H1, int W1, const uint16_t* wt16, const float* bias,
+                             const float* ratio, const float* scale, float* y, double* stats,
+                             int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
+                             int pad, int act, float slope, void* workspace, void* stream);
 /* PartialConv2d mask update (networks.py:83-104, multi_channel=False):
  * count = C0*window_sum(m0) + C1*window_sum(m1) over the conv's window (masks
  * are planes of integer counts -- 0/1, or a channel sum -- repeated over their

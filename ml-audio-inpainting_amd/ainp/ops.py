@@ -571,6 +571,34 @@ def conv_weight_kmajor(w, C0, C1):
     return wt
 
 
+_WT16_CACHE: dict = {}
+# bf16 convs whose sources have channel counts % 32 == 0 run channel-last
+# (ainp_conv_gen_fwd_nhwc16); AINP_CONV_NHWC16=0 keeps the NCHW gather
+CONV_NHWC16 = os.environ.get("AINP_CONV_NHWC16", "1") != "0"
+
+
+def conv_weight_nhwc16(w, C0, C1):
+    """bf16 [Cout][K] weights for ainp_conv_gen_fwd_nhwc16, cached like
+    conv_weight_kmajor (invalidated by in-place updates / reallocation)."""
+    key = (w._version, C0, C1, w.data_ptr())
+    ent = _WT16_CACHE.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == key:
+        return ent[2]
+    wt = torch.empty(w.shape[0], w[0].numel(), device=w.device, dtype=torch.bfloat16)
+    _T.conv_weight_nhwc16(w, int(C0), int(C1), wt)
+    wid = id(w)
+    _WT16_CACHE[wid] = (weakref.ref(w, lambda _r, wid=wid: _WT16_CACHE.pop(wid, None)), key, wt)
+    return wt
+
+
+def to_nhwc16(x, m=None):
+    """x [N,C,H,W] fp32 (x mask plane m) -> bf16 [N,H,W,C] (ainp_nchw_to_nhwc16)."""
+    N, C, H, W = x.shape
+    out = torch.empty(N, H, W, C, device=x.device, dtype=torch.bfloat16)
+    _T.nchw_to_nhwc16(x, m, out)
+    return out
+
+
 def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=None, ratio=None,
              scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None,
              bf16=False):
@@ -611,6 +639,17 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
         if t is not None:
             _req(t, nm)
     ws = wt = None
+    if (bf16 and CONV_NHWC16 and Cout > 1 and crop is None and C0 % 32 == 0
+            and C1 % 32 == 0):
+        nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, Ho, Wo))
+        if nb:
+            ws = torch.empty(-(-nb // 4), device=x0.device)
+        a16 = to_nhwc16(x0, m0)
+        b16 = to_nhwc16(x1, m1) if src1 is not None else None
+        _T.conv_gen_fwd_nhwc16(a16, b16, conv_weight_nhwc16(w, C0, C1), int(Cout), int(KH),
+                               int(KW), bias, ratio, scale, out, stats, int(Hin), int(Win),
+                               int(stride), int(pad), int(act), float(slope), ws)
+        return out, stats
     if Cout == 1:
         nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, ch or Ho, cw or Wo))
     else:

@@ -1200,7 +1200,267 @@ __global__ void channel_sum_kernel(const float* m, int64_t N, int C, int64_t HW,
   out[t] = s;
 }
 
+
+// ------------------------------------------------------- few input channels
+// The first layers (G's 7x7 encoder conv on the 1-channel spectrogram, D's
+// 4x4 conv on it, VGG's conv1_1 on 3 channels): K = Cin*KH*KW <= 256 and
+// Cout <= 64 (K <= 160 here), so the implicit GEMM is all gather and no MFMA work.  Direct
+// form: one thread per output pixel holds all Cout accumulators; per k it
+// gathers one input value (x * mask) and FMAs it against the k-th weight
+// column read from LDS as broadcast float4s; the epilogue writes each
+// channel's plane with lane-consecutive pixels.  bf16 (AINP_CONV_BF16): the
+// input value and the weights are rounded to bf16 first, so every product is
+// the exact bf16 x bf16 product the MFMA would form (fp32 accumulation).
+constexpr int SC_K = 160, SC_CO = 64;   // 40 KB of weights in LDS
+
+template <bool B16>
+__global__ __launch_bounds__(256) void conv_gen_smallcin_kernel(ConvGenParams p, int act) {
+  __shared__ __attribute__((aligned(16))) float sw[SC_K][SC_CO];   // [k][co]
+  const int KK = p.KH * p.KW, K = KK * p.Cin, Cout = p.Cout;
+  for (int i = threadIdx.x; i < K * SC_CO; i += 256) {
+    const int k = i / SC_CO, co = i - k * SC_CO;
+    float v = 0.f;
+    if (co < Cout) {
+      // k = tap * Cin + ci (the kmajor order of source 0)
+      const int tap = k / p.Cin, ci = k - tap * p.Cin;
+      v = p.w[((int64_t)co * p.Cin + ci) * KK + tap];
+      if (B16) v = (float)(__bf16)v;
+    }
+    sw[k][co] = v;
+  }
+  __syncthreads();
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pix >= NP) return;
+  const int n = (int)(pix / HWo);
+  const int r = (int)(pix - (int64_t)n * HWo);
+  const int oy = r / p.Wo, ox = r - oy * p.Wo;
+  const int by = oy * p.stride - p.pad, bx = ox * p.stride - p.pad;
+  const ConvSrcDev& s = p.s0;
+  const int64_t plane = (int64_t)s.Hs * s.Ws;
+  const float* xn = s.x + (int64_t)n * s.C * plane;
+  const float* mn = s.m ? s.m + (int64_t)n * plane : nullptr;
+  float acc[SC_CO];
+#pragma unroll
+  for (int c = 0; c < SC_CO; ++c) acc[c] = 0.f;
+  int k = 0;
+  for (int ky = 0; ky < p.KH; ++ky) {
+    const int iy = by + ky;
+    for (int kx = 0; kx < p.KW; ++kx) {
+      const int ix = bx + kx;
+      const bool inb = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const int64_t off = inb ? (int64_t)iy * s.Ws + ix : 0;
+      const float mv = (inb && mn) ? mn[off] : 1.f;
+      for (int ci = 0; ci < p.Cin; ++ci, ++k) {
+        float v = inb ? xn[ci * plane + off] * mv : 0.f;
+        if (B16) v = (float)(__bf16)v;
+        const float4* wk = reinterpret_cast<const float4*>(sw[k]);
+#pragma unroll
+        for (int c4 = 0; c4 < SC_CO / 4; ++c4) {
+          const float4 w4 = wk[c4];
+          acc[4 * c4 + 0] = fmaf(w4.x, v, acc[4 * c4 + 0]);
+          acc[4 * c4 + 1] = fmaf(w4.y, v, acc[4 * c4 + 1]);
+          acc[4 * c4 + 2] = fmaf(w4.z, v, acc[4 * c4 + 2]);
+          acc[4 * c4 + 3] = fmaf(w4.w, v, acc[4 * c4 + 3]);
+        }
+      }
+    }
+  }
+  const float sc = p.scale ? *p.scale : 1.f;
+  const float rt = p.ratio ? p.ratio[pix] : 1.f;
+  float* yb = p.y + (int64_t)n * Cout * HWo + r;
+#pragma unroll
+  for (int c = 0; c < SC_CO; ++c) {
+    if (c < Cout) {
+      float v = acc[c] * sc;
+      v *= rt;
+      if (p.bias) v += p.bias[c];
+      yb[(int64_t)c * HWo] = apply_act(v, act, p.slope);
+    }
+  }
+}
+
+// ------------------------------------------------------- bf16 NHWC variant
+// The bf16 configurations (C4 / C5) of every conv whose sources have
+// channel counts % 32 == 0: the sources are first written channel-last in bf16
+// with their partial-conv mask already applied (nchw_to_nhwc16_kernel: the
+// masks are channel-uniform per source, so x*m folds in exactly), the weights
+// as bf16 [Cout][K] (k = tap*C + ci per source, the fast path's order), so a
+// K-tile of 32 channels of ONE tap is, per pixel, 64 contiguous bytes: four
+// 16-byte loads per thread per tile instead of 16 scalar gathers and a mask
+// load each, at half the bytes.  Same tiles, LDS images (80-byte rows),
+// one-plane MFMA loop, split-K and epilogue as conv_gen_x6_kernel<BM, 32, 1>.
+struct Src16 {
+  const uint16_t* x;   // [N][Hs][Ws][C] bf16 (mask applied)
+  int C, Hs, Ws, up;
+};
+
+template <int BM>
+__global__ __launch_bounds__(256, 4) void conv_gen_nhwc16_kernel(ConvGenParams p, Src16 s0,
+                                                                 Src16 s1,
+                                                                 const uint16_t* __restrict__ wt16,
+                                                                 int act) {
+  constexpr int XBK = 32;
+  constexpr int BN = 16384 / BM;
+  constexpr int WN = BN / 64;
+  constexpr int AR = XBK * BM / 256;          // consecutive k per thread, A (16 / 8)
+  constexpr int BR = XBK * BN / 256;          // consecutive channels per thread, B (16 / 32)
+  constexpr int RS = XBK * 2 + 16;
+  constexpr int APL = BM * RS, BPL = BN * RS;
+  constexpr int ESCR = WN * BM * 2 * (int)sizeof(double);
+  __shared__ __attribute__((aligned(16))) unsigned char sA[APL > ESCR ? APL : ESCR];
+  __shared__ __attribute__((aligned(16))) unsigned char sB[BPL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int KK = p.KH * p.KW;
+  const int K0 = KK * s0.C;
+  const int K = KK * p.Cin;
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px0 = (int64_t)blockIdx.x * BN;
+  const int co0 = blockIdx.y * BM;
+  const int nkt_all = K / XBK;
+  const int64_t kb = (int64_t)blockIdx.z * p.ktiles_per_split;
+  const int64_t ke = kb + p.ktiles_per_split;
+  const int kt_begin = (int)(kb < nkt_all ? kb : nkt_all);
+  const int kt_end = (int)(ke < nkt_all ? ke : nkt_all);
+
+  const int bpx = tid % BN, bkq = tid / BN;
+  const int64_t pix = px0 + bpx;
+  const bool pv = pix < NP;
+  int n = 0, by = 0, bx = 0;
+  if (pv) {
+    n = (int)(pix / HWo);
+    const int r = (int)(pix - (int64_t)n * HWo);
+    const int oy = r / p.Wo, ox = r - oy * p.Wo;
+    by = oy * p.stride - p.pad;
+    bx = ox * p.stride - p.pad;
+  }
+  const int aco = tid % BM, akq = tid / BM;
+  const bool acok = co0 + aco < p.Cout;
+  const uint16_t* wrow = wt16 + (int64_t)(acok ? co0 + aco : 0) * K + akq * AR;
+
+  uint4 ra[AR / 8], rb[BR / 8];
+  auto fetch = [&](int kt) {
+    const int k0 = kt * XBK;
+#pragma unroll
+    for (int i = 0; i < AR / 8; ++i)
+      ra[i] = acok ? *reinterpret_cast<const uint4*>(wrow + k0 + 8 * i) : make_uint4(0, 0, 0, 0);
+    const bool first = k0 < K0;
+    const Src16& s = first ? s0 : s1;
+    const int kr = first ? k0 : k0 - K0;
+    const int tap = kr / s.C, ci0 = kr - tap * s.C;
+    const int ky = tap / p.KW, kx = tap - ky * p.KW;
+    const int iy = by + ky, ix = bx + kx;
+    const bool inb = pv && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+    const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
+    const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
+    const uint16_t* base =
+        s.x + (((int64_t)n * s.Hs + sy) * s.Ws + sx) * s.C + ci0 + bkq * BR;
+#pragma unroll
+    for (int i = 0; i < BR / 8; ++i)
+      rb[i] = inb ? *reinterpret_cast<const uint4*>(base + 8 * i) : make_uint4(0, 0, 0, 0);
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int i = 0; i < AR / 8; ++i)
+      *reinterpret_cast<uint4*>(sA + aco * RS + akq * AR * 2 + 16 * i) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BR / 8; ++i)
+      *reinterpret_cast<uint4*>(sB + bpx * RS + bkq * BR * 2 + 16 * i) = rb[i];
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, lh = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  if (kt_begin < kt_end) fetch(kt_begin);
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    commit();
+    __syncthreads();
+    if (kt + 1 < kt_end) fetch(kt + 1);
+#pragma unroll
+    for (int st = 0; st < XBK / 16; ++st) {
+      cgx::bf16x8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = cgx::frag(sA + (wm * 64 + i * 32 + l31) * RS + 32 * st + 16 * lh);
+        b[i] = cgx::frag(sB + (wn * 64 + i * 32 + l31) * RS + 32 * st + 16 * lh);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  conv_gen_epilogue<BM>(p, acc, act, reinterpret_cast<double*>(sA));
+}
+
+// x [N][C][H][W] fp32 (* mask plane m [N][H][W] if given) -> out [N][H][W][C]
+// bf16 (nearest-even): 64 channels x 64 columns of one row per block.
+__global__ __launch_bounds__(256) void nchw_to_nhwc16_kernel(const float* __restrict__ x,
+                                                             const float* __restrict__ m, int C,
+                                                             int H, int W,
+                                                             uint16_t* __restrict__ out) {
+  __shared__ uint16_t tile[64][66];   // [w][c]
+  const int w0 = blockIdx.x * 64, h = blockIdx.y;
+  const int cb = (C + 63) / 64;
+  const int n = blockIdx.z / cb, c0 = (blockIdx.z % cb) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int w = w0 + tx;
+  const float mv = (m && w < W) ? m[((int64_t)n * H + h) * W + w] : 1.f;
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i;
+    float v = 0.f;
+    if (c < C && w < W) v = x[(((int64_t)n * C + c) * H + h) * W + w] * mv;
+    tile[tx][i] = __builtin_bit_cast(uint16_t, (__bf16)v);
+  }
+  __syncthreads();
+  // rows w, lanes along c (bf16 pairs): 32 lanes cover one pixel's 64 channels
+  const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
+#pragma unroll
+  for (int i = r; i < 64; i += 8) {
+    const int ww = w0 + i, c = c0 + 2 * l;
+    if (ww >= W || c >= C) continue;
+    uint16_t* q = out + (((int64_t)n * H + h) * W + ww) * C + c;
+    if (c + 1 < C)
+      *reinterpret_cast<uint32_t*>(q) = (uint32_t)tile[i][2 * l] | ((uint32_t)tile[i][2 * l + 1] << 16);
+    else
+      q[0] = tile[i][2 * l];
+  }
+}
+
+// w [Cout][C0+C1][KH][KW] fp32 -> wt16 [Cout][K] bf16, k = tap*C0 + ci (source 0)
+// then KK*C0 + tap*C1 + ci (source 1)
+__global__ void conv_weight_nhwc16_kernel(const float* __restrict__ w, int Cout, int C0, int C1,
+                                          int KK, uint16_t* __restrict__ wt16) {
+  const int Cin = C0 + C1, K = KK * Cin;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= (int64_t)Cout * K) return;
+  const int co = (int)(t / K), k = (int)(t % K);
+  const int K0 = KK * C0;
+  int tap, c;
+  if (k < K0) {
+    tap = k / C0;
+    c = k - tap * C0;
+  } else {
+    tap = (k - K0) / C1;
+    c = C0 + (k - K0 - tap * C1);
+  }
+  wt16[t] = __builtin_bit_cast(uint16_t, (__bf16)w[((int64_t)co * Cin + c) * KK + tap]);
+}
+
 }  // namespace ainp
+
 
 // ============================================================== C ABI
 using namespace ainp;
@@ -1329,6 +1589,22 @@ extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, in
     return check_launch("conv_cout1");
   }
   if (crop_h > 0 || crop_w > 0) return record_msg("ainp_conv_gen_fwd: crop needs Cout=1");
+  // few input channels, one plain source, no BN statistics: the direct kernel
+  static const bool small_ok = [] {
+    const char* e = getenv("AINP_CONV_SMALLCIN");
+    return !(e && e[0] == '0');
+  }();
+  if (small_ok && C1 == 0 && p.s0.up == 0 && !stats && Cout <= SC_CO &&
+      (int64_t)C0 * KH * KW <= SC_K && C0 <= 4) {
+    const int64_t NPs = N * (int64_t)Ho * Wo;
+    if (b16)
+      hipLaunchKernelGGL(conv_gen_smallcin_kernel<true>, dim3((unsigned)cdiv(NPs, 256)), dim3(256),
+                         0, s, p, act);
+    else
+      hipLaunchKernelGGL(conv_gen_smallcin_kernel<false>, dim3((unsigned)cdiv(NPs, 256)), dim3(256),
+                         0, s, p, act);
+    return check_launch("conv_gen_smallcin");
+  }
   if (!wt) return record_msg("ainp_conv_gen_fwd: k-major weights (ainp_conv_weight_kmajor) required");
   const int BM = conv_gen_bm(Cout);
   const int64_t NP = N * (int64_t)Ho * Wo;
@@ -1383,6 +1659,91 @@ extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, in
   else
     hipLaunchKernelGGL(conv_gen_fwd_kernel<64>, grid, dim3(256), 0, s, p, wt, act);
   int rc = check_launch("conv_gen_fwd");
+  if (rc || nsplit == 1) return rc;
+  hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), Cout), dim3(256), 0,
+                     s, p, nsplit, act);
+  return check_launch("conv_gen_splitk_epilogue");
+}
+
+extern "C" int ainp_nchw_to_nhwc16(const float* x, const float* m, int64_t N, int C, int H, int W,
+                                   uint16_t* out, void* stream) {
+  if (!x || !out || N < 1 || C < 1 || H < 1 || W < 1 || N * ((C + 63) / 64) > 65535 || H > 65535)
+    return record_msg("ainp_nchw_to_nhwc16: bad argument");
+  hipLaunchKernelGGL(nchw_to_nhwc16_kernel, dim3((unsigned)cdiv(W, 64), (unsigned)H,
+                                                 (unsigned)(N * cdiv(C, 64))),
+                     dim3(256), 0, as_stream(stream), x, m, C, H, W, out);
+  return check_launch("nchw_to_nhwc16");
+}
+
+extern "C" int ainp_conv_weight_nhwc16(const float* w, int Cout, int C0, int C1, int KH, int KW,
+                                       uint16_t* wt16, void* stream) {
+  if (!w || !wt16 || Cout < 1 || C0 < 1 || C1 < 0 || KH < 1 || KW < 1)
+    return record_msg("ainp_conv_weight_nhwc16: bad argument");
+  const int64_t total = (int64_t)Cout * (C0 + C1) * KH * KW;
+  hipLaunchKernelGGL(conv_weight_nhwc16_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
+                     as_stream(stream), w, Cout, C0, C1, KH * KW, wt16);
+  return check_launch("conv_weight_nhwc16");
+}
+
+extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0,
+                                        const uint16_t* x1, int C1, int H1, int W1,
+                                        const uint16_t* wt16, const float* bias, const float* ratio,
+                                        const float* scale, float* y, double* stats, int64_t N,
+                                        int Cout, int Hin, int Win, int KH, int KW, int stride,
+                                        int pad, int act, float slope, void* workspace,
+                                        void* stream) {
+  if (!x0 || C0 < 32 || C0 % 32 || C1 < 0 || C1 % 32 || (C1 > 0 && !x1) || !wt16 || !y ||
+      N < 1 || Cout < 2 || Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 ||
+      act < 0 || act > 3 || ((uintptr_t)x0 & 15) || ((uintptr_t)x1 & 15) || ((uintptr_t)wt16 & 15))
+    return record_msg("ainp_conv_gen_fwd_nhwc16: bad argument (channels % 32, Cout > 1, 16-B aligned)");
+  const int Ho = (Hin + 2 * pad - KH) / stride + 1;
+  const int Wo = (Win + 2 * pad - KW) / stride + 1;
+  if (Ho < 1 || Wo < 1) return record_msg("ainp_conv_gen_fwd_nhwc16: empty output");
+  Src16 a{x0, C0, H0, W0, 0}, b{x1, C1, C1 ? H1 : Hin, C1 ? W1 : Win, 0};
+  const ConvSrcDev sa = make_src(nullptr, nullptr, C0, H0, W0, Hin, Win);
+  const ConvSrcDev sb = make_src(nullptr, nullptr, C1, b.Hs, b.Ws, Hin, Win);
+  a.up = sa.up;
+  b.up = sb.up;
+  if (a.up == 1 && H0 * 2 != Hin) return record_msg("ainp_conv_gen_fwd_nhwc16: bad source size");
+  ConvGenParams p;
+  p.s0 = sa;
+  p.s1 = sb;
+  p.w = nullptr;
+  p.bias = bias;
+  p.ratio = ratio;
+  p.scale = scale;
+  p.y = y;
+  p.stats = stats;
+  p.partial = nullptr;
+  p.ktiles_per_split = 1 << 30;
+  p.N = (int)N;
+  p.Cin = C0 + C1;
+  p.Cout = Cout;
+  p.Hin = Hin;
+  p.Win = Win;
+  p.Ho = Ho;
+  p.Wo = Wo;
+  p.KH = KH;
+  p.KW = KW;
+  p.stride = stride;
+  p.pad = pad;
+  p.slope = slope;
+  const int BM = conv_gen_bm(Cout);
+  const int64_t NP = N * (int64_t)Ho * Wo;
+  const int K = p.Cin * KH * KW;
+  const int nsplit = conv_gen_nsplit(NP, Cout, K);
+  if (nsplit > 1) {
+    if (!workspace) return record_msg("ainp_conv_gen_fwd_nhwc16: split-K needs ainp_conv_gen_workspace");
+    p.partial = reinterpret_cast<float*>(workspace);
+    p.ktiles_per_split = (int)cdiv(cdiv(K, CG_BK), nsplit);
+  }
+  hipStream_t s = as_stream(stream);
+  const dim3 grid((unsigned)cdiv(NP, 16384 / BM), (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
+  if (BM == 128)
+    hipLaunchKernelGGL(conv_gen_nhwc16_kernel<128>, grid, dim3(256), 0, s, p, a, b, wt16, act);
+  else
+    hipLaunchKernelGGL(conv_gen_nhwc16_kernel<64>, grid, dim3(256), 0, s, p, a, b, wt16, act);
+  int rc = check_launch("conv_gen_nhwc16");
   if (rc || nsplit == 1) return rc;
   hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), Cout), dim3(256), 0,
                      s, p, nsplit, act);

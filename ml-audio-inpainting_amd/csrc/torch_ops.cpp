@@ -833,6 +833,69 @@ void cast_bf16_t(const Tensor& x, const OptT& out, const OptT& outT) {
                        stream_of(x)),
       "cast_bf16_t");
 }
+
+void nchw_to_nhwc16(const Tensor& x, const OptT& m, const Tensor& out) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const float* mp = opt(m, "mask");
+  if (mp) numel_is(*m, N * H * W, "mask");
+  numel_is(out, x.numel(), "out");
+  chk(ainp_nchw_to_nhwc16(dev(x, "x"), mp, N, (int)C, (int)H, (int)W, bf16p(out, "out"),
+                          stream_of(x)),
+      "nchw_to_nhwc16");
+}
+
+void conv_weight_nhwc16(const Tensor& w, int64_t C0, int64_t C1, const Tensor& wt16) {
+  GUARD(w);
+  TORCH_CHECK(w.dim() == 4 && w.size(1) == C0 + C1, "w must be [Cout, C0+C1, KH, KW]");
+  numel_is(wt16, w.numel(), "wt16");
+  chk(ainp_conv_weight_nhwc16(dev(w, "w"), (int)w.size(0), (int)C0, (int)C1, (int)w.size(2),
+                              (int)w.size(3), bf16p(wt16, "wt16"), stream_of(w)),
+      "conv_weight_nhwc16");
+}
+
+void conv_gen_fwd_nhwc16(const Tensor& x0, const OptT& x1, const Tensor& wt16, int64_t Cout,
+                         int64_t KH, int64_t KW, const OptT& bias, const OptT& ratio,
+                         const OptT& scale, const Tensor& y, const OptT& stats, int64_t Hin,
+                         int64_t Win, int64_t stride, int64_t pad, int64_t act, double slope,
+                         const OptT& workspace) {
+  GUARD(x0);
+  TORCH_CHECK(x0.dim() == 4, "x0 must be [N,H0,W0,C0] (channel-last bf16)");
+  const int64_t N = x0.size(0), H0 = x0.size(1), W0 = x0.size(2), C0 = x0.size(3);
+  int64_t C1 = 0, H1 = 0, W1 = 0;
+  const uint16_t* p1 = nullptr;
+  if (x1.has_value() && x1->defined()) {
+    TORCH_CHECK(x1->dim() == 4 && x1->size(0) == N, "x1 must be [N,H1,W1,C1]");
+    H1 = x1->size(1);
+    W1 = x1->size(2);
+    C1 = x1->size(3);
+    p1 = bf16p(*x1, "x1");
+  }
+  numel_is(wt16, Cout * (C0 + C1) * KH * KW, "wt16");
+  const int64_t Ho = (Hin + 2 * pad - KH) / stride + 1, Wo = (Win + 2 * pad - KW) / stride + 1;
+  numel_is(y, N * Cout * Ho * Wo, "y");
+  double* st = opt<double>(stats, "stats", at::kDouble);
+  if (st)
+    numel_is(*stats,
+             (int64_t)ainp_conv_gen_stat_parts(N, (int)(C0 + C1), (int)KH, (int)KW, (int)Cout, Ho, Wo) *
+                 2 * Cout,
+             "stats");
+  const size_t need = ainp_conv_gen_workspace(N, (int)(C0 + C1), (int)KH, (int)KW, (int)Cout, Ho, Wo);
+  void* ws = nullptr;
+  if (workspace.has_value() && workspace->defined()) {
+    ws = dev<void>(*workspace, "workspace", workspace->scalar_type());
+    TORCH_CHECK((size_t)workspace->nbytes() >= need, "conv_gen workspace too small");
+  } else {
+    TORCH_CHECK(need == 0, "conv_gen needs a workspace of ", need, " bytes");
+  }
+  chk(ainp_conv_gen_fwd_nhwc16(bf16p(x0, "x0"), (int)C0, (int)H0, (int)W0, p1, (int)C1, (int)H1,
+                               (int)W1, bf16p(wt16, "wt16"), opt(bias, "bias"), opt(ratio, "ratio"),
+                               opt(scale, "scale"), dev(y, "y"), st, N, (int)Cout, (int)Hin,
+                               (int)Win, (int)KH, (int)KW, (int)stride, (int)pad, (int)act,
+                               (float)slope, ws, stream_of(x0)),
+      "conv_gen_fwd_nhwc16");
+}
 }  // namespace
 
 TORCH_LIBRARY(ainp, m) {
@@ -915,6 +978,11 @@ TORCH_LIBRARY(ainp, m) {
   m.def("gemm_bf16nt(Tensor A, Tensor B, Tensor(a!) C, int K, Tensor? bias_a1, Tensor? bias_a2, "
         "Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, int kc) -> ()");
   m.def("cast_bf16_t(Tensor x, Tensor(a!)? out, Tensor(b!)? outT) -> ()");
+  m.def("nchw_to_nhwc16(Tensor x, Tensor? m, Tensor(a!) out) -> ()");
+  m.def("conv_weight_nhwc16(Tensor w, int C0, int C1, Tensor(a!) wt16) -> ()");
+  m.def("conv_gen_fwd_nhwc16(Tensor x0, Tensor? x1, Tensor wt16, int Cout, int KH, int KW, "
+        "Tensor? bias, Tensor? ratio, Tensor? scale, Tensor(a!) y, Tensor(b!)? stats, int Hin, "
+        "int Win, int stride, int pad, int act, float slope, Tensor(c!)? workspace) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
@@ -965,6 +1033,9 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("bn_relu_apply_ntcf_bf16", &bn_relu_apply_ntcf_bf16);
   m.impl("gemm_bf16nt", &gemm_bf16nt);
   m.impl("cast_bf16_t", &cast_bf16_t);
+  m.impl("nchw_to_nhwc16", &nchw_to_nhwc16);
+  m.impl("conv_weight_nhwc16", &conv_weight_nhwc16);
+  m.impl("conv_gen_fwd_nhwc16", &conv_gen_fwd_nhwc16);
 }
 
 // The ops write through raw device pointers like the C ABI; autograd is the
@@ -1018,4 +1089,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("bn_relu_apply_ntcf_bf16", torch::CppFunction::makeFallthrough());
   m.impl("gemm_bf16nt", torch::CppFunction::makeFallthrough());
   m.impl("cast_bf16_t", torch::CppFunction::makeFallthrough());
+  m.impl("nchw_to_nhwc16", torch::CppFunction::makeFallthrough());
+  m.impl("conv_weight_nhwc16", torch::CppFunction::makeFallthrough());
+  m.impl("conv_gen_fwd_nhwc16", torch::CppFunction::makeFallthrough());
 }
