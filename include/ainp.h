@@ -445,11 +445,15 @@ int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, int H0, int W
                          int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
                          int pad, int act, float slope, int crop_h, int crop_w, int flags,
                          void* workspace, void* stream);
-/* bf16 configurations (C4 / C5), channel-last variant for sources whose
- * channel counts are multiples of 32: ainp_nchw_to_nhwc16 writes a source
- * x [N][C][H][W] times its mask plane m [N][H][W] (may be NULL) as bf16
- * (nearest-even) out [N][H][W][C]; ainp_conv_weight_nhwc16 writes the weights
- * as bf16 wt16 [Cout][K] (k = tap*C0 + ci, then KK*C0 + tap*C1 + ci); then
+/* bf16 configurations (C4 / C5), channel-last variant: ainp_nchw_to_nhwc16
+ * writes a source x [N][C][H][W] times its mask plane m [N][H][W] (may be
+ * NULL) as bf16 (nearest-even) out [N][H][W][C]; ainp_conv_weight_nhwc16
+ * writes the weights as bf16 wt16 [Cout][S0 + S1] (k = tap*C0 + ci, then
+ * S0 + tap*C1 + ci), where a source of C channels spans S = KK*C k-values,
+ * rounded up to a multiple of 32 (zero weights) when C % 32 != 0; such a
+ * source is passed expanded per output pixel by ainp_im2col_nhwc16
+ * (x [N][C][Hs][Ws] fp32 times its mask plane m, resampled to Hin x Win like
+ * source 0 -> bf16 rows [N*Ho*Wo][S], k = tap*C + ci, zero past KK*C); then
  * ainp_conv_gen_fwd_nhwc16 is ainp_conv_gen_fwd_ex(AINP_CONV_BF16) on those
  * operands (same resampling of source 0, ratio / scale / bias / stats /
  * activation epilogue and split-K workspace; no crop, Cout > 1).  16-byte
@@ -458,6 +462,8 @@ int ainp_nchw_to_nhwc16(const float* x, const float* m, int64_t N, int C, int H,
                         uint16_t* out, void* stream);
 int ainp_conv_weight_nhwc16(const float* w, int Cout, int C0, int C1, int KH, int KW,
                             uint16_t* wt16, void* stream);
+int ainp_im2col_nhwc16(const float* x, const float* m, int64_t N, int C, int Hs, int Ws, int Hin,
+                       int Win, int KH, int KW, int stride, int pad, uint16_t* out, void* stream);
 int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0, const uint16_t* x1,
                              int C1, int H1, int W1, const uint16_t* wt16, const float* bias,
                              const float* ratio, const float* scale, float* y, double* stats,
@@ -550,6 +556,32 @@ int ainp_leaky_bwd_ld(const float* g, const float* y, int64_t rows, int64_t P, f
                       int64_t ldo, float* out, void* stream);
 int ainp_col2im_ld(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW, int stride,
                    int pad, int64_t ldp, float* dx, void* stream);
+/* The Discriminator backward in the bf16 configurations (C4 / C5; the same
+ * networks.py:375-409 convs as the row-padded fp32 forms above).
+ * ainp_d_prep16: g = sum of nslab slabs [N][C][P] (slab_stride apart; the
+ * split-K partials of ainp_dgrad16), times LeakyReLU'(y) when y != NULL
+ * (y = the layer's activation output, y > 0 ? 1 : slope), cast to bf16 as
+ * gA [C][ldA] (q = n*P + p; zero for N*P <= q < ldA) and, when gT != NULL,
+ * gT [N*P][C].  ainp_im2col16: ainp_im2col_ld in bf16 with every image's
+ * pixels in one row: col [C*KH*KW (+1 ones row)][ldA], q = n*Ho*Wo + p, zero
+ * past N*Ho*Wo (ldA % 8 == 0, 16-byte aligned); the weight gradient is then
+ * ainp_gemm_bf16nt(gA, col) over K = ldA.  ainp_dgrad16_weight: the weights
+ * w [Cout][Cin][k][k] regrouped for the data gradient, bf16
+ * wd [s*s][Cin][Kc], Kc = taps*Cout rounded up to 32 when Cout % 32 != 0,
+ * taps = (k/s)^2 (k % s == 0).  ainp_dgrad16: dx [N][Cin][H][W] of the conv
+ * (k, stride s, pad) from gT [N][Ho][Wo][Cout] and wd, times *scale (1/sigma;
+ * NULL = 1), as stride^2 parity-class implicit GEMMs; nsplit > 1 writes nsplit
+ * partial slabs slab_stride apart (summed by ainp_d_prep16 or ainp_sum_slabs). */
+int ainp_d_prep16(const float* g, int nslab, int64_t slab_stride, const float* y, float slope,
+                  int64_t N, int C, int64_t P, uint16_t* gA, int64_t ldA, uint16_t* gT,
+                  void* stream);
+int ainp_im2col16(const float* x, int64_t N, int C, int H, int W, int KH, int KW, int stride,
+                  int pad, int ones_row, uint16_t* col, int64_t ldA, void* stream);
+int ainp_dgrad16_weight(const float* w, int Cout, int Cin, int k, int stride, int pad,
+                        uint16_t* wd, void* stream);
+int ainp_dgrad16(const uint16_t* gT, int64_t N, int Cout, int Ho, int Wo, const uint16_t* wd,
+                 int Cin, int H, int W, int k, int stride, int pad, const float* scale,
+                 float* out, int nsplit, int64_t slab_stride, void* stream);
 /* PartialConv2d called with a per-channel mask (networks.py:74-85 when
  * mask.shape[1] == C_in): out = a*b elementwise, and the channel sum of the
  * mask [N,C,HW] -> [N,HW] whose window sum is the mask_conv count. */

@@ -136,8 +136,17 @@ _SIGS = {
     "ainp_gemm_bf16nt": (c_int, [c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P, c_int64,
                                  P, P, P, P, c_int64, c_int, c_int64, c_int64, P]),
     "ainp_cast_bf16_t": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P]),
+    "ainp_d_prep16": (c_int, [P, c_int, c_int64, P, c_float, c_int64, c_int, c_int64, P, c_int64,
+                              P, P]),
+    "ainp_im2col16": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                              P, c_int64, P]),
+    "ainp_dgrad16_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "ainp_dgrad16": (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int,
+                             c_int, P, P, c_int, c_int64, P]),
     "ainp_nchw_to_nhwc16": (c_int, [P, P, c_int64, c_int, c_int, c_int, P, P]),
     "ainp_conv_weight_nhwc16": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
+    "ainp_im2col_nhwc16": (c_int, [P, P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                   c_int, c_int, P, P]),
     "ainp_conv_gen_fwd_nhwc16": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, P, P, P,
                                          P, P, P, c_int64, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_float, P, P]),

@@ -22,6 +22,7 @@ libainp (ainp.ops):
 """
 from __future__ import annotations
 
+import os
 import re
 from pathlib import Path
 from typing import Dict, List, Optional, Tuple
@@ -355,6 +356,8 @@ class _DiscriminatorFn(torch.autograd.Function):
         ins, outs = st[1:1 + L], st[1 + L:1 + 2 * L]
         us, vs = st[1 + 2 * L:1 + 3 * L], st[1 + 3 * L:1 + 4 * L]
         params = st[1 + 4 * L:]
+        if ctx.bf16 and D_BWD16:
+            return _d_backward16(ctx, g, inv, ins, outs, us, vs, params)
         grads = [None] * len(params)
         g = g.contiguous()
         gx = None
@@ -388,6 +391,46 @@ class _DiscriminatorFn(torch.autograd.Function):
                 if l == 0:
                     gx = g
         return (gx, None, None, None, None, None, *grads)
+
+
+# bf16 configurations: the D backward on bf16 operands in HBM (csrc/dconv16.hip);
+# AINP_D_BWD16=0 keeps the fp32-staged im2col / GEMM / col2im loop
+D_BWD16 = os.environ.get("AINP_D_BWD16", "1") != "0"
+
+
+def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
+    """_DiscriminatorFn.backward with bf16 operands: per layer the gradient is
+    cast once into a pixel-contiguous and a channel-last bf16 copy (LeakyReLU
+    backward and the split-K slabs of the layer above folded in), the weight
+    gradient is one bf16 GEMM over every image's pixels, the data gradient a
+    parity-class implicit GEMM (csrc/dconv16.hip)."""
+    L = ctx.nl
+    grads = [None] * len(params)
+    gsrc, nslab = g.contiguous(), 1
+    gx = None
+    for l in range(L - 1, -1, -1):
+        k, s, p, act = ctx.cfg[l]
+        w = params[2 * l]
+        N, Cout, Ho, Wo = outs[l].shape
+        P = Ho * Wo
+        ldA = -(-N * P // 64) * 64
+        need_dx = l > 0 or ctx.needs_input_grad[0]
+        gA, gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P, ldA,
+                              want_gT=need_dx)
+        h = ins[l]
+        Cin, H, W = h.shape[1:]
+        col = ops.im2col16(h, k, s, p, ldA)                      # [Cin*k*k + 1, ldA]
+        Gw = ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=512)
+        dw, db = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1], with_bias=True)
+        grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
+        if need_dx:
+            S = ops.dgrad16_nsplit(N, Cin, H, W, k, s, Cout)
+            gsrc = ops.dgrad16(gT.view(N, Ho, Wo, Cout), ops.dgrad16_weight(w, s, p), Cin, H, W,
+                               k, s, p, scale=inv[l:l + 1], nsplit=S)
+            nslab = S
+            if l == 0:
+                gx = gsrc[0] if S == 1 else ops.sum_slabs(gsrc, S).view(N, Cin, H, W)
+    return (gx, None, None, None, None, None, *grads)
 
 
 def _split_count(n):

@@ -268,6 +268,7 @@ _B16_TILE_RATE = 700e12 / 768
 _SLAB_RATE = 4e12
 
 
+@functools.lru_cache(maxsize=256)
 def _splitk_bf16(M, N, K, slots=768, max_split=16):
     """Split count S for a bf16 GEMM over a small M x N: minimise the wave-quantised
     MFMA time ceil(tiles*S/slots) * tile_time(K/S) plus the slab round trip."""
@@ -288,7 +289,7 @@ def _splitk_bf16(M, N, K, slots=768, max_split=16):
     return best
 
 
-def gemm_bf16nt_splitk(A, B, K, out=None):
+def gemm_bf16nt_splitk(A, B, K, out=None, max_split=16):
     """A [M, >=K] . B [N, >=K]^T (bf16, no bias) with the long K split over
     slabs summed in fixed order (ainp_sum_slabs) -- the weight gradients."""
     M, N = A.shape[0], B.shape[0]
@@ -296,7 +297,7 @@ def gemm_bf16nt_splitk(A, B, K, out=None):
         out = torch.empty(M, N, device=A.device, dtype=torch.float32)
     if not out.is_contiguous():
         raise ValueError("gemm_bf16nt_splitk: out must be contiguous")
-    S = _splitk_bf16(M, N, K)
+    S = _splitk_bf16(M, N, K, max_split=max_split)
     if S == 1:
         _T.gemm_bf16nt(A, B, out, int(K), None, None, None, None, 0, 1, int(K))
         return out
@@ -572,9 +573,30 @@ def conv_weight_kmajor(w, C0, C1):
 
 
 _WT16_CACHE: dict = {}
-# bf16 convs whose sources have channel counts % 32 == 0 run channel-last
-# (ainp_conv_gen_fwd_nhwc16); AINP_CONV_NHWC16=0 keeps the NCHW gather
+# bf16 convs run channel-last (ainp_conv_gen_fwd_nhwc16); AINP_CONV_NHWC16=0
+# keeps the NCHW gather.  Sources with C % 32 != 0 (the U-Net's 1-channel
+# planes) are gathered element-wise inside it unless AINP_CONV_NHWC16_SMALL=0;
+# the plain few-channel first layers (D's, VGG's) keep the direct kernel
+# (ainp_conv_gen_fwd_ex) unless AINP_CONV_NHWC16_SMALL=all.
 CONV_NHWC16 = os.environ.get("AINP_CONV_NHWC16", "1") != "0"
+CONV_NHWC16_SMALL = os.environ.get("AINP_CONV_NHWC16_SMALL", "1")
+
+
+def nhwc16_seg(C, KK):
+    """k-values a source contributes to an nhwc16 weight row (gan.hip)."""
+    return -(-KK * C // 32) * 32 if C % 32 else KK * C
+
+
+def _nhwc16_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats):
+    if not CONV_NHWC16:
+        return False
+    if C0 % 32 == 0 and C1 % 32 == 0:
+        return True
+    if CONV_NHWC16_SMALL == "0":
+        return False
+    direct = (C1 == 0 and (H0, W0) == (Hin, Win) and not want_stats and Cout <= 64
+              and C0 * KH * KW <= 160 and C0 <= 4)
+    return CONV_NHWC16_SMALL == "all" or not direct
 
 
 def conv_weight_nhwc16(w, C0, C1):
@@ -584,7 +606,9 @@ def conv_weight_nhwc16(w, C0, C1):
     ent = _WT16_CACHE.get(id(w))
     if ent is not None and ent[0]() is w and ent[1] == key:
         return ent[2]
-    wt = torch.empty(w.shape[0], w[0].numel(), device=w.device, dtype=torch.bfloat16)
+    KK = w.shape[2] * w.shape[3]
+    wt = torch.empty(w.shape[0], nhwc16_seg(C0, KK) + nhwc16_seg(C1, KK), device=w.device,
+                     dtype=torch.bfloat16)
     _T.conv_weight_nhwc16(w, int(C0), int(C1), wt)
     wid = id(w)
     _WT16_CACHE[wid] = (weakref.ref(w, lambda _r, wid=wid: _WT16_CACHE.pop(wid, None)), key, wt)
@@ -639,16 +663,25 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
         if t is not None:
             _req(t, nm)
     ws = wt = None
-    if (bf16 and CONV_NHWC16 and Cout > 1 and crop is None and C0 % 32 == 0
-            and C1 % 32 == 0):
+    if bf16 and Cout > 1 and crop is None and _nhwc16_route(C0, C1, H0, W0, Hin, Win, KH, KW,
+                                                             Cout, want_stats):
         nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, Ho, Wo))
         if nb:
             ws = torch.empty(-(-nb // 4), device=x0.device)
-        a16 = to_nhwc16(x0, m0)
-        b16 = to_nhwc16(x1, m1) if src1 is not None else None
+        def src16(x, m, C):
+            if C % 32:   # few channels: expanded per output pixel
+                e = torch.empty(N * Ho * Wo, nhwc16_seg(C, KH * KW), device=x.device,
+                                dtype=torch.bfloat16)
+                _T.im2col_nhwc16(x, m, int(Hin), int(Win), int(KH), int(KW), int(stride),
+                                 int(pad), e)
+                return e
+            return to_nhwc16(x, m)
+        a16 = src16(x0, m0, C0)
+        b16 = src16(x1, m1, C1) if src1 is not None else None
         _T.conv_gen_fwd_nhwc16(a16, b16, conv_weight_nhwc16(w, C0, C1), int(Cout), int(KH),
                                int(KW), bias, ratio, scale, out, stats, int(Hin), int(Win),
-                               int(stride), int(pad), int(act), float(slope), ws)
+                               int(stride), int(pad), int(act), float(slope), ws,
+                               [int(N), int(C0), int(H0), int(W0), int(C1), int(H1), int(W1)])
         return out, stats
     if Cout == 1:
         nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, ch or Ho, cw or Wo))
@@ -835,6 +868,54 @@ def gemm_batched_splitk(M, N, Kd, As, sam, sak, Bs, sbk, sbn, out, *, alpha=1.0,
         sum_slabs(slabs, S, out=out.reshape(-1))
     else:
         sum_slabs(slabs, nb * S, out=out.reshape(-1))
+    return out
+
+
+def d_prep16(g, nslab, y, slope, N, C, P, ldA, want_gT=True):
+    """ainp_d_prep16: sum of nslab slabs of g [N, C, P] (x LeakyReLU'(y)) ->
+    (gA bf16 [C, ldA] pixel-contiguous, gT bf16 [N*P, C] or None)."""
+    gA = torch.empty(C, ldA, device=g.device, dtype=torch.bfloat16)
+    gT = torch.empty(N * P, C, device=g.device, dtype=torch.bfloat16) if want_gT else None
+    _T.d_prep16(g, int(nslab), y, float(slope), int(N), int(C), int(P), gA, gT)
+    return gA, gT
+
+
+def im2col16(x, k, stride, pad, ldA, ones_row=True):
+    """ainp_im2col16: bf16 [C*k*k (+1), ldA] columns, all images' pixels in a row."""
+    C = x.shape[1]
+    col = torch.empty(C * k * k + int(ones_row), ldA, device=x.device, dtype=torch.bfloat16)
+    _T.im2col16(x, int(k), int(stride), int(pad), bool(ones_row), col)
+    return col
+
+
+def dgrad16_weight(w, stride, pad):
+    """ainp_dgrad16_weight: bf16 [s*s, Cin, Kc] parity-class weights."""
+    Cout, Cin, k, _ = w.shape
+    nt = k // stride
+    wd = torch.empty(stride * stride, Cin, nhwc16_seg(Cout, nt * nt), device=w.device,
+                     dtype=torch.bfloat16)
+    _T.dgrad16_weight(w, int(stride), int(pad), wd)
+    return wd
+
+
+def dgrad16_nsplit(N, Cin, H, W, k, stride, Cout):
+    """Split-K count of ainp_dgrad16: ~768 workgroups, >= 8 K-tiles a split."""
+    BM = 128 if Cin > 64 else 64
+    tiles = -(-(N * -(-H // stride) * -(-W // stride)) // (16384 // BM))
+    blocks = tiles * -(-Cin // BM) * stride * stride
+    nkt = nhwc16_seg(Cout, (k // stride) ** 2) // 32
+    if blocks >= 512 or nkt < 16:
+        return 1
+    return max(1, min(-(-768 // blocks), nkt // 8))
+
+
+def dgrad16(gT, wd, Cin, H, W, k, stride, pad, scale=None, nsplit=1):
+    """ainp_dgrad16: gT bf16 [N, Ho, Wo, Cout] -> dx fp32 [nsplit, N, Cin, H, W]
+    (split-K partial slabs; nsplit == 1: the data gradient itself)."""
+    N = gT.shape[0]
+    out = torch.empty(nsplit, N, Cin, H, W, device=gT.device, dtype=torch.float32)
+    _T.dgrad16(gT, wd, int(Cin), int(H), int(W), int(k), int(stride), int(pad), scale, out,
+               int(nsplit))
     return out
 
 

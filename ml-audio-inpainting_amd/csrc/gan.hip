@@ -1291,12 +1291,21 @@ __global__ __launch_bounds__(256) void conv_gen_smallcin_kernel(ConvGenParams p,
 // 16-byte loads per thread per tile instead of 16 scalar gathers and a mask
 // load each, at half the bytes.  Same tiles, LDS images (80-byte rows),
 // one-plane MFMA loop, split-K and epilogue as conv_gen_x6_kernel<BM, 32, 1>.
+// A source with C % 32 != 0 (the U-Net's 1-channel input and mask planes)
+// owns KK*C k-values padded up to whole 32-deep tiles (zero weights in the
+// pad) and arrives already expanded per output pixel (im2col_nhwc16_kernel:
+// [N*Ho*Wo][seg] bf16, mask applied), so its tiles are plain row loads too.
 struct Src16 {
-  const uint16_t* x;   // [N][Hs][Ws][C] bf16 (mask applied)
-  int C, Hs, Ws, up;
+  const uint16_t* x;   // [N][Hs][Ws][C] bf16 (mask applied), or [N*Ho*Wo][seg] if exp
+  int C, Hs, Ws, up, exp;
 };
 
-template <int BM>
+// k-values one source contributes to the nhwc16 weight rows
+__host__ __device__ inline int nhwc16_seg(int C, int KK) {
+  return (C & 31) ? (KK * C + 31) / 32 * 32 : KK * C;
+}
+
+template <int BM, bool EXP>
 __global__ __launch_bounds__(256, 4) void conv_gen_nhwc16_kernel(ConvGenParams p, Src16 s0,
                                                                  Src16 s1,
                                                                  const uint16_t* __restrict__ wt16,
@@ -1304,8 +1313,6 @@ __global__ __launch_bounds__(256, 4) void conv_gen_nhwc16_kernel(ConvGenParams p
   constexpr int XBK = 32;
   constexpr int BN = 16384 / BM;
   constexpr int WN = BN / 64;
-  constexpr int AR = XBK * BM / 256;          // consecutive k per thread, A (16 / 8)
-  constexpr int BR = XBK * BN / 256;          // consecutive channels per thread, B (16 / 32)
   constexpr int RS = XBK * 2 + 16;
   constexpr int APL = BM * RS, BPL = BN * RS;
   constexpr int ESCR = WN * BM * 2 * (int)sizeof(double);
@@ -1313,8 +1320,8 @@ __global__ __launch_bounds__(256, 4) void conv_gen_nhwc16_kernel(ConvGenParams p
   __shared__ __attribute__((aligned(16))) unsigned char sB[BPL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int KK = p.KH * p.KW;
-  const int K0 = KK * s0.C;
-  const int K = KK * p.Cin;
+  const int K0 = nhwc16_seg(s0.C, KK);
+  const int K = K0 + nhwc16_seg(s1.C, KK);
   const int HWo = p.Ho * p.Wo;
   const int64_t NP = (int64_t)p.N * HWo;
   const int64_t px0 = (int64_t)blockIdx.x * BN;
@@ -1325,49 +1332,66 @@ __global__ __launch_bounds__(256, 4) void conv_gen_nhwc16_kernel(ConvGenParams p
   const int kt_begin = (int)(kb < nkt_all ? kb : nkt_all);
   const int kt_end = (int)(ke < nkt_all ? ke : nkt_all);
 
-  const int bpx = tid % BN, bkq = tid / BN;
-  const int64_t pix = px0 + bpx;
-  const bool pv = pix < NP;
-  int n = 0, by = 0, bx = 0;
-  if (pv) {
-    n = (int)(pix / HWo);
-    const int r = (int)(pix - (int64_t)n * HWo);
-    const int oy = r / p.Wo, ox = r - oy * p.Wo;
-    by = oy * p.stride - p.pad;
-    bx = ox * p.stride - p.pad;
+  // loads: lanes 4r..4r+3 read the four 16-byte chunks of one row's 64-byte
+  // K-tile slice (a pixel's 32 channels of one tap, or a weight row), so a
+  // wave's load touches 16 rows, not 64; rows r + 64 i, i < BN/64 (BM/64)
+  constexpr int NBI = BN / 64, NAI = BM / 64;
+  const int ch = tid & 3, rr = tid >> 2;
+  // per pixel row: n (-1 past the end) and the packed window origin (by, bx)
+  int n_[NBI], byx_[NBI];
+#pragma unroll
+  for (int i = 0; i < NBI; ++i) {
+    const int64_t pix = px0 + rr + 64 * i;
+    n_[i] = -1;
+    byx_[i] = 0;
+    if (pix < NP) {
+      n_[i] = (int)(pix / HWo);
+      const int r = (int)(pix - (int64_t)n_[i] * HWo);
+      const int oy = r / p.Wo, ox = r - oy * p.Wo;
+      byx_[i] = ((oy * p.stride - p.pad) << 16) | ((ox * p.stride - p.pad) & 0xffff);
+    }
   }
-  const int aco = tid % BM, akq = tid / BM;
-  const bool acok = co0 + aco < p.Cout;
-  const uint16_t* wrow = wt16 + (int64_t)(acok ? co0 + aco : 0) * K + akq * AR;
-
-  uint4 ra[AR / 8], rb[BR / 8];
+  const uint16_t* wrow = wt16 + (int64_t)(co0 + rr) * K + 8 * ch;
+  const int arows = p.Cout - co0 - rr;     // row rr + 64 i is valid iff 64 i < arows
+  uint4 ra[NAI], rb[NBI];
   auto fetch = [&](int kt) {
     const int k0 = kt * XBK;
 #pragma unroll
-    for (int i = 0; i < AR / 8; ++i)
-      ra[i] = acok ? *reinterpret_cast<const uint4*>(wrow + k0 + 8 * i) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < NAI; ++i)
+      ra[i] = 64 * i < arows ? *reinterpret_cast<const uint4*>(wrow + (int64_t)64 * i * K + k0)
+                             : make_uint4(0, 0, 0, 0);
     const bool first = k0 < K0;
     const Src16& s = first ? s0 : s1;
     const int kr = first ? k0 : k0 - K0;
+    if (EXP && s.exp) {   // pre-expanded few-channel source: row pix, k-values kr...
+      const int seg = nhwc16_seg(s.C, KK);
+#pragma unroll
+      for (int i = 0; i < NBI; ++i)
+        rb[i] = n_[i] >= 0 ? *reinterpret_cast<const uint4*>(
+                                 s.x + (px0 + rr + 64 * i) * seg + kr + 8 * ch)
+                           : make_uint4(0, 0, 0, 0);
+      return;
+    }
     const int tap = kr / s.C, ci0 = kr - tap * s.C;
     const int ky = tap / p.KW, kx = tap - ky * p.KW;
-    const int iy = by + ky, ix = bx + kx;
-    const bool inb = pv && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
-    const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
-    const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
-    const uint16_t* base =
-        s.x + (((int64_t)n * s.Hs + sy) * s.Ws + sx) * s.C + ci0 + bkq * BR;
 #pragma unroll
-    for (int i = 0; i < BR / 8; ++i)
-      rb[i] = inb ? *reinterpret_cast<const uint4*>(base + 8 * i) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < NBI; ++i) {
+      const int iy = (byx_[i] >> 16) + ky, ix = (int)(short)(byx_[i] & 0xffff) + kx;
+      const bool inb = n_[i] >= 0 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
+      const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
+      const uint16_t* src =
+          s.x + (((int64_t)n_[i] * s.Hs + sy) * s.Ws + sx) * s.C + ci0 + 8 * ch;
+      rb[i] = inb ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+    }
   };
   auto commit = [&]() {
 #pragma unroll
-    for (int i = 0; i < AR / 8; ++i)
-      *reinterpret_cast<uint4*>(sA + aco * RS + akq * AR * 2 + 16 * i) = ra[i];
+    for (int i = 0; i < NAI; ++i)
+      *reinterpret_cast<uint4*>(sA + (rr + 64 * i) * RS + 16 * ch) = ra[i];
 #pragma unroll
-    for (int i = 0; i < BR / 8; ++i)
-      *reinterpret_cast<uint4*>(sB + bpx * RS + bkq * BR * 2 + 16 * i) = rb[i];
+    for (int i = 0; i < NBI; ++i)
+      *reinterpret_cast<uint4*>(sB + (rr + 64 * i) * RS + 16 * ch) = rb[i];
   };
 
   const int wm = wave / WN, wn = wave % WN;
@@ -1439,24 +1463,63 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc16_kernel(const float* __rest
   }
 }
 
+// few-channel source x [N][C][Hs][Ws] fp32 (x mask plane m [N][Hs][Ws]),
+// resampled to Hin x Win as src_coord -> bf16 rows out [N*Ho*Wo][seg],
+// k = tap*C + ci < KK*C, zero past it; one thread = 8 k-values of a pixel
+__global__ __launch_bounds__(256) void im2col_nhwc16_kernel(
+    const float* __restrict__ x, const float* __restrict__ m, int C, int Hs, int Ws, int up,
+    int Hin, int Win, int KH, int KW, int stride, int pad, int Ho, int Wo, int64_t NP, int seg,
+    uint16_t* __restrict__ out) {
+  const int chunks = seg / 8;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= NP * chunks) return;
+  const int64_t pix = t / chunks;
+  const int k0 = (int)(t - pix * chunks) * 8;
+  const int HWo = Ho * Wo;
+  const int n = (int)(pix / HWo);
+  const int r = (int)(pix - (int64_t)n * HWo);
+  const int oy = r / Wo, ox = r - oy * Wo;
+  const int KK = KH * KW;
+  uint32_t g[4];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = k0 + j;
+    const int tap = k / C, ci = k - tap * C;
+    const int ky = tap / KW, kx = tap - ky * KW;
+    const int iy = oy * stride - pad + ky, ix = ox * stride - pad + kx;
+    float v = 0.f;
+    if (tap < KK && iy >= 0 && iy < Hin && ix >= 0 && ix < Win) {
+      const int sy = src_coord(iy, Hs, Hin, up), sx = src_coord(ix, Ws, Win, up);
+      v = x[(((int64_t)n * C + ci) * Hs + sy) * Ws + sx];
+      if (m) v *= m[((int64_t)n * Hs + sy) * Ws + sx];
+    }
+    const uint32_t b = __builtin_bit_cast(uint16_t, (__bf16)v);
+    if (j & 1) g[j >> 1] |= b << 16;
+    else g[j >> 1] = b;
+  }
+  *reinterpret_cast<uint4*>(out + pix * seg + k0) = make_uint4(g[0], g[1], g[2], g[3]);
+}
+
 // w [Cout][C0+C1][KH][KW] fp32 -> wt16 [Cout][K] bf16, k = tap*C0 + ci (source 0)
-// then KK*C0 + tap*C1 + ci (source 1)
+// then seg0 + tap*C1 + ci (source 1), each source padded to nhwc16_seg k-values
+// with zeros
 __global__ void conv_weight_nhwc16_kernel(const float* __restrict__ w, int Cout, int C0, int C1,
                                           int KK, uint16_t* __restrict__ wt16) {
-  const int Cin = C0 + C1, K = KK * Cin;
+  const int Cin = C0 + C1;
+  const int S0 = nhwc16_seg(C0, KK), K = S0 + nhwc16_seg(C1, KK);
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= (int64_t)Cout * K) return;
   const int co = (int)(t / K), k = (int)(t % K);
-  const int K0 = KK * C0;
   int tap, c;
-  if (k < K0) {
+  if (k < S0) {
     tap = k / C0;
     c = k - tap * C0;
   } else {
-    tap = (k - K0) / C1;
-    c = C0 + (k - K0 - tap * C1);
+    tap = (k - S0) / C1;
+    c = C0 + (k - S0 - tap * C1);
   }
-  wt16[t] = __builtin_bit_cast(uint16_t, (__bf16)w[((int64_t)co * Cin + c) * KK + tap]);
+  const float v = tap < KK ? w[((int64_t)co * Cin + c) * KK + tap] : 0.f;
+  wt16[t] = __builtin_bit_cast(uint16_t, (__bf16)v);
 }
 
 }  // namespace ainp
@@ -1675,11 +1738,30 @@ extern "C" int ainp_nchw_to_nhwc16(const float* x, const float* m, int64_t N, in
   return check_launch("nchw_to_nhwc16");
 }
 
+extern "C" int ainp_im2col_nhwc16(const float* x, const float* m, int64_t N, int C, int Hs,
+                                  int Ws, int Hin, int Win, int KH, int KW, int stride, int pad,
+                                  uint16_t* out, void* stream) {
+  if (!x || !out || N < 1 || C < 1 || Hs < 1 || Ws < 1 || Hin < 1 || Win < 1 || KH < 1 ||
+      KW < 1 || stride < 1 || pad < 0 || ((uintptr_t)out & 15))
+    return record_msg("ainp_im2col_nhwc16: bad argument");
+  const int Ho = (Hin + 2 * pad - KH) / stride + 1, Wo = (Win + 2 * pad - KW) / stride + 1;
+  if (Ho < 1 || Wo < 1) return record_msg("ainp_im2col_nhwc16: empty output");
+  const ConvSrcDev sd = make_src(x, m, C, Hs, Ws, Hin, Win);
+  if (sd.up == 1 && Hs * 2 != Hin) return record_msg("ainp_im2col_nhwc16: bad source size");
+  const int seg = nhwc16_seg(C, KH * KW);
+  const int64_t NP = N * (int64_t)Ho * Wo;
+  hipLaunchKernelGGL(im2col_nhwc16_kernel, dim3((unsigned)cdiv(NP * (seg / 8), 256)), dim3(256), 0,
+                     as_stream(stream), x, m, C, Hs, Ws, sd.up, Hin, Win, KH, KW, stride, pad, Ho,
+                     Wo, NP, seg, out);
+  return check_launch("im2col_nhwc16");
+}
+
 extern "C" int ainp_conv_weight_nhwc16(const float* w, int Cout, int C0, int C1, int KH, int KW,
                                        uint16_t* wt16, void* stream) {
   if (!w || !wt16 || Cout < 1 || C0 < 1 || C1 < 0 || KH < 1 || KW < 1)
     return record_msg("ainp_conv_weight_nhwc16: bad argument");
-  const int64_t total = (int64_t)Cout * (C0 + C1) * KH * KW;
+  const int64_t total =
+      (int64_t)Cout * (nhwc16_seg(C0, KH * KW) + nhwc16_seg(C1, KH * KW));
   hipLaunchKernelGGL(conv_weight_nhwc16_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                      as_stream(stream), w, Cout, C0, C1, KH * KW, wt16);
   return check_launch("conv_weight_nhwc16");
@@ -1692,14 +1774,15 @@ extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int 
                                         int Cout, int Hin, int Win, int KH, int KW, int stride,
                                         int pad, int act, float slope, void* workspace,
                                         void* stream) {
-  if (!x0 || C0 < 32 || C0 % 32 || C1 < 0 || C1 % 32 || (C1 > 0 && !x1) || !wt16 || !y ||
-      N < 1 || Cout < 2 || Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 ||
-      act < 0 || act > 3 || ((uintptr_t)x0 & 15) || ((uintptr_t)x1 & 15) || ((uintptr_t)wt16 & 15))
-    return record_msg("ainp_conv_gen_fwd_nhwc16: bad argument (channels % 32, Cout > 1, 16-B aligned)");
+  if (!x0 || C0 < 1 || C1 < 0 || (C1 > 0 && !x1) || !wt16 || !y || N < 1 || Cout < 2 ||
+      Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 || act < 0 || act > 3 ||
+      (C0 % 32 == 0 && ((uintptr_t)x0 & 15)) || (C1 % 32 == 0 && ((uintptr_t)x1 & 15)) ||
+      ((uintptr_t)wt16 & 15))
+    return record_msg("ainp_conv_gen_fwd_nhwc16: bad argument (Cout > 1, 16-B aligned)");
   const int Ho = (Hin + 2 * pad - KH) / stride + 1;
   const int Wo = (Win + 2 * pad - KW) / stride + 1;
   if (Ho < 1 || Wo < 1) return record_msg("ainp_conv_gen_fwd_nhwc16: empty output");
-  Src16 a{x0, C0, H0, W0, 0}, b{x1, C1, C1 ? H1 : Hin, C1 ? W1 : Win, 0};
+  Src16 a{x0, C0, H0, W0, 0, C0 % 32 != 0}, b{x1, C1, C1 ? H1 : Hin, C1 ? W1 : Win, 0, C1 % 32 != 0};
   const ConvSrcDev sa = make_src(nullptr, nullptr, C0, H0, W0, Hin, Win);
   const ConvSrcDev sb = make_src(nullptr, nullptr, C1, b.Hs, b.Ws, Hin, Win);
   a.up = sa.up;
@@ -1730,19 +1813,26 @@ extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int 
   p.slope = slope;
   const int BM = conv_gen_bm(Cout);
   const int64_t NP = N * (int64_t)Ho * Wo;
-  const int K = p.Cin * KH * KW;
-  const int nsplit = conv_gen_nsplit(NP, Cout, K);
+  // the split count follows the unpadded K (ainp_conv_gen_workspace /
+  // _stat_parts); the padded tiles are spread over those splits
+  const int nsplit = conv_gen_nsplit(NP, Cout, p.Cin * KH * KW);
+  const int Kp = nhwc16_seg(C0, KH * KW) + nhwc16_seg(C1, KH * KW);
   if (nsplit > 1) {
     if (!workspace) return record_msg("ainp_conv_gen_fwd_nhwc16: split-K needs ainp_conv_gen_workspace");
     p.partial = reinterpret_cast<float*>(workspace);
-    p.ktiles_per_split = (int)cdiv(cdiv(K, CG_BK), nsplit);
+    p.ktiles_per_split = (int)cdiv(Kp / CG_BK, nsplit);
   }
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)cdiv(NP, 16384 / BM), (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
-  if (BM == 128)
-    hipLaunchKernelGGL(conv_gen_nhwc16_kernel<128>, grid, dim3(256), 0, s, p, a, b, wt16, act);
+  const bool exp = a.exp || b.exp;
+  if (BM == 128 && exp)
+    hipLaunchKernelGGL((conv_gen_nhwc16_kernel<128, true>), grid, dim3(256), 0, s, p, a, b, wt16, act);
+  else if (BM == 128)
+    hipLaunchKernelGGL((conv_gen_nhwc16_kernel<128, false>), grid, dim3(256), 0, s, p, a, b, wt16, act);
+  else if (exp)
+    hipLaunchKernelGGL((conv_gen_nhwc16_kernel<64, true>), grid, dim3(256), 0, s, p, a, b, wt16, act);
   else
-    hipLaunchKernelGGL(conv_gen_nhwc16_kernel<64>, grid, dim3(256), 0, s, p, a, b, wt16, act);
+    hipLaunchKernelGGL((conv_gen_nhwc16_kernel<64, false>), grid, dim3(256), 0, s, p, a, b, wt16, act);
   int rc = check_launch("conv_gen_nhwc16");
   if (rc || nsplit == 1) return rc;
   hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), Cout), dim3(256), 0,

@@ -834,6 +834,9 @@ void cast_bf16_t(const Tensor& x, const OptT& out, const OptT& outT) {
       "cast_bf16_t");
 }
 
+// k-values one source contributes to an nhwc16 weight row (gan.hip nhwc16_seg)
+int64_t nhwc16_seg(int64_t C, int64_t KK) { return (C % 32) ? (KK * C + 31) / 32 * 32 : KK * C; }
+
 void nchw_to_nhwc16(const Tensor& x, const OptT& m, const Tensor& out) {
   GUARD(x);
   TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
@@ -846,10 +849,25 @@ void nchw_to_nhwc16(const Tensor& x, const OptT& m, const Tensor& out) {
       "nchw_to_nhwc16");
 }
 
+void im2col_nhwc16(const Tensor& x, const OptT& m, int64_t Hin, int64_t Win, int64_t KH,
+                   int64_t KW, int64_t stride, int64_t pad, const Tensor& out) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,Hs,Ws]");
+  const int64_t N = x.size(0), C = x.size(1), Hs = x.size(2), Ws = x.size(3);
+  const float* mp = opt(m, "mask");
+  if (mp) numel_is(*m, N * Hs * Ws, "mask");
+  const int64_t Ho = (Hin + 2 * pad - KH) / stride + 1, Wo = (Win + 2 * pad - KW) / stride + 1;
+  numel_is(out, N * Ho * Wo * nhwc16_seg(C, KH * KW), "out");
+  chk(ainp_im2col_nhwc16(dev(x, "x"), mp, N, (int)C, (int)Hs, (int)Ws, (int)Hin, (int)Win, (int)KH,
+                         (int)KW, (int)stride, (int)pad, bf16p(out, "out"), stream_of(x)),
+      "im2col_nhwc16");
+}
+
 void conv_weight_nhwc16(const Tensor& w, int64_t C0, int64_t C1, const Tensor& wt16) {
   GUARD(w);
   TORCH_CHECK(w.dim() == 4 && w.size(1) == C0 + C1, "w must be [Cout, C0+C1, KH, KW]");
-  numel_is(wt16, w.numel(), "wt16");
+  const int64_t KK = w.size(2) * w.size(3);
+  numel_is(wt16, w.size(0) * (nhwc16_seg(C0, KK) + nhwc16_seg(C1, KK)), "wt16");
   chk(ainp_conv_weight_nhwc16(dev(w, "w"), (int)w.size(0), (int)C0, (int)C1, (int)w.size(2),
                               (int)w.size(3), bf16p(wt16, "wt16"), stream_of(w)),
       "conv_weight_nhwc16");
@@ -859,21 +877,35 @@ void conv_gen_fwd_nhwc16(const Tensor& x0, const OptT& x1, const Tensor& wt16, i
                          int64_t KH, int64_t KW, const OptT& bias, const OptT& ratio,
                          const OptT& scale, const Tensor& y, const OptT& stats, int64_t Hin,
                          int64_t Win, int64_t stride, int64_t pad, int64_t act, double slope,
-                         const OptT& workspace) {
+                         const OptT& workspace, at::IntArrayRef dims) {
+  // dims = [N, C0, H0, W0, C1, H1, W1] (required when a source has C % 32 != 0:
+  // such a source is the [N*Ho*Wo, seg] rows of im2col_nhwc16), else from the
+  // [N, Hs, Ws, C] channel-last tensors
   GUARD(x0);
-  TORCH_CHECK(x0.dim() == 4, "x0 must be [N,H0,W0,C0] (channel-last bf16)");
-  const int64_t N = x0.size(0), H0 = x0.size(1), W0 = x0.size(2), C0 = x0.size(3);
-  int64_t C1 = 0, H1 = 0, W1 = 0;
+  const int64_t Ho = (Hin + 2 * pad - KH) / stride + 1, Wo = (Win + 2 * pad - KW) / stride + 1;
+  int64_t N, C0, H0, W0, C1 = 0, H1 = 0, W1 = 0;
   const uint16_t* p1 = nullptr;
-  if (x1.has_value() && x1->defined()) {
-    TORCH_CHECK(x1->dim() == 4 && x1->size(0) == N, "x1 must be [N,H1,W1,C1]");
-    H1 = x1->size(1);
-    W1 = x1->size(2);
-    C1 = x1->size(3);
+  if (!dims.empty()) {
+    TORCH_CHECK(dims.size() == 7, "dims must be [N, C0, H0, W0, C1, H1, W1]");
+    N = dims[0]; C0 = dims[1]; H0 = dims[2]; W0 = dims[3]; C1 = dims[4]; H1 = dims[5]; W1 = dims[6];
+  } else {
+    TORCH_CHECK(x0.dim() == 4, "x0 must be [N,H0,W0,C0] (channel-last bf16)");
+    N = x0.size(0); H0 = x0.size(1); W0 = x0.size(2); C0 = x0.size(3);
+    if (x1.has_value() && x1->defined()) {
+      TORCH_CHECK(x1->dim() == 4 && x1->size(0) == N, "x1 must be [N,H1,W1,C1]");
+      H1 = x1->size(1); W1 = x1->size(2); C1 = x1->size(3);
+    }
+  }
+  auto src_numel = [&](int64_t C, int64_t H, int64_t W) {
+    return (C % 32) ? N * Ho * Wo * nhwc16_seg(C, KH * KW) : N * H * W * C;
+  };
+  numel_is(x0, src_numel(C0, H0, W0), "x0");
+  if (C1 > 0) {
+    TORCH_CHECK(x1.has_value() && x1->defined(), "x1 required for C1 > 0");
+    numel_is(*x1, src_numel(C1, H1, W1), "x1");
     p1 = bf16p(*x1, "x1");
   }
-  numel_is(wt16, Cout * (C0 + C1) * KH * KW, "wt16");
-  const int64_t Ho = (Hin + 2 * pad - KH) / stride + 1, Wo = (Win + 2 * pad - KW) / stride + 1;
+  numel_is(wt16, Cout * (nhwc16_seg(C0, KH * KW) + nhwc16_seg(C1, KH * KW)), "wt16");
   numel_is(y, N * Cout * Ho * Wo, "y");
   double* st = opt<double>(stats, "stats", at::kDouble);
   if (st)
@@ -895,6 +927,62 @@ void conv_gen_fwd_nhwc16(const Tensor& x0, const OptT& x1, const Tensor& wt16, i
                                (int)Win, (int)KH, (int)KW, (int)stride, (int)pad, (int)act,
                                (float)slope, ws, stream_of(x0)),
       "conv_gen_fwd_nhwc16");
+}
+
+void d_prep16(const Tensor& g, int64_t nslab, const OptT& y, double slope, int64_t N, int64_t C,
+              int64_t P, const Tensor& gA, const OptT& gT) {
+  GUARD(g);
+  numel_is(g, nslab * N * C * P, "g");
+  const float* yp = opt(y, "y");
+  if (yp) numel_is(*y, N * C * P, "y");
+  TORCH_CHECK(gA.dim() == 2 && gA.size(0) == C && gA.size(1) >= N * P, "gA must be [C, >= N*P]");
+  uint16_t* gt = nullptr;
+  if (gT.has_value() && gT->defined()) {
+    numel_is(*gT, N * P * C, "gT");
+    gt = bf16p(*gT, "gT");
+  }
+  chk(ainp_d_prep16(dev(g, "g"), (int)nslab, N * C * P, yp, (float)slope, N, (int)C, P,
+                    bf16p(gA, "gA"), gA.size(1), gt, stream_of(g)),
+      "d_prep16");
+}
+
+void im2col16(const Tensor& x, int64_t k, int64_t stride, int64_t pad, bool ones_row,
+              const Tensor& col) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(col.dim() == 2 && col.size(0) == C * k * k + (ones_row ? 1 : 0),
+              "col must be [C*k*k (+1), ldA]");
+  chk(ainp_im2col16(dev(x, "x"), N, (int)C, (int)H, (int)W, (int)k, (int)k, (int)stride, (int)pad,
+                    ones_row ? 1 : 0, bf16p(col, "col"), col.size(1), stream_of(x)),
+      "im2col16");
+}
+
+void dgrad16_weight(const Tensor& w, int64_t stride, int64_t pad, const Tensor& wd) {
+  GUARD(w);
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == w.size(3), "w must be [Cout, Cin, k, k]");
+  const int64_t Cout = w.size(0), Cin = w.size(1), k = w.size(2);
+  TORCH_CHECK(stride >= 1 && k % stride == 0, "dgrad16_weight: k % stride == 0");
+  const int64_t nt = k / stride;
+  numel_is(wd, stride * stride * Cin * nhwc16_seg(Cout, nt * nt), "wd");
+  chk(ainp_dgrad16_weight(dev(w, "w"), (int)Cout, (int)Cin, (int)k, (int)stride, (int)pad,
+                          bf16p(wd, "wd"), stream_of(w)),
+      "dgrad16_weight");
+}
+
+void dgrad16(const Tensor& gT, const Tensor& wd, int64_t Cin, int64_t H, int64_t W, int64_t k,
+             int64_t stride, int64_t pad, const OptT& scale, const Tensor& out, int64_t nsplit) {
+  GUARD(gT);
+  TORCH_CHECK(gT.dim() == 4, "gT must be [N, Ho, Wo, Cout] (channel-last bf16)");
+  const int64_t N = gT.size(0), Ho = gT.size(1), Wo = gT.size(2), Cout = gT.size(3);
+  TORCH_CHECK(stride >= 1 && k % stride == 0, "dgrad16: k % stride == 0");
+  const int64_t nt = k / stride;
+  numel_is(wd, stride * stride * Cin * nhwc16_seg(Cout, nt * nt), "wd");
+  numel_is(out, nsplit * N * Cin * H * W, "out");
+  chk(ainp_dgrad16(bf16p(gT, "gT"), N, (int)Cout, (int)Ho, (int)Wo, bf16p(wd, "wd"), (int)Cin,
+                   (int)H, (int)W, (int)k, (int)stride, (int)pad, opt(scale, "scale"),
+                   dev(out, "out"), (int)nsplit, N * Cin * H * W, stream_of(gT)),
+      "dgrad16");
 }
 }  // namespace
 
@@ -982,7 +1070,16 @@ TORCH_LIBRARY(ainp, m) {
   m.def("conv_weight_nhwc16(Tensor w, int C0, int C1, Tensor(a!) wt16) -> ()");
   m.def("conv_gen_fwd_nhwc16(Tensor x0, Tensor? x1, Tensor wt16, int Cout, int KH, int KW, "
         "Tensor? bias, Tensor? ratio, Tensor? scale, Tensor(a!) y, Tensor(b!)? stats, int Hin, "
-        "int Win, int stride, int pad, int act, float slope, Tensor(c!)? workspace) -> ()");
+        "int Win, int stride, int pad, int act, float slope, Tensor(c!)? workspace, "
+        "int[] dims=[]) -> ()");
+  m.def("im2col_nhwc16(Tensor x, Tensor? m, int Hin, int Win, int KH, int KW, int stride, "
+        "int pad, Tensor(a!) out) -> ()");
+  m.def("d_prep16(Tensor g, int nslab, Tensor? y, float slope, int N, int C, int P, "
+        "Tensor(a!) gA, Tensor(b!)? gT) -> ()");
+  m.def("im2col16(Tensor x, int k, int stride, int pad, bool ones_row, Tensor(a!) col) -> ()");
+  m.def("dgrad16_weight(Tensor w, int stride, int pad, Tensor(a!) wd) -> ()");
+  m.def("dgrad16(Tensor gT, Tensor wd, int Cin, int H, int W, int k, int stride, int pad, "
+        "Tensor? scale, Tensor(a!) out, int nsplit) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
@@ -1036,6 +1133,11 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("nchw_to_nhwc16", &nchw_to_nhwc16);
   m.impl("conv_weight_nhwc16", &conv_weight_nhwc16);
   m.impl("conv_gen_fwd_nhwc16", &conv_gen_fwd_nhwc16);
+  m.impl("im2col_nhwc16", &im2col_nhwc16);
+  m.impl("d_prep16", &d_prep16);
+  m.impl("im2col16", &im2col16);
+  m.impl("dgrad16_weight", &dgrad16_weight);
+  m.impl("dgrad16", &dgrad16);
 }
 
 // The ops write through raw device pointers like the C ABI; autograd is the
@@ -1092,4 +1194,9 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("nchw_to_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("conv_weight_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("conv_gen_fwd_nhwc16", torch::CppFunction::makeFallthrough());
+  m.impl("im2col_nhwc16", torch::CppFunction::makeFallthrough());
+  m.impl("d_prep16", torch::CppFunction::makeFallthrough());
+  m.impl("im2col16", torch::CppFunction::makeFallthrough());
+  m.impl("dgrad16_weight", torch::CppFunction::makeFallthrough());
+  m.impl("dgrad16", torch::CppFunction::makeFallthrough());
 }

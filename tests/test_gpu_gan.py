@@ -132,6 +132,52 @@ def test_conv_gen_bf16_matches_torch(case):
     assert rel(y, y32) > 1e-5          # a bf16 result, not the fp32-accurate one
 
 
+SMALL_C_CASES = [
+    # N, C0, C1, Hin, Win, up0, Cout, k, s, p, masks, bias, ratio, scale, act
+    (2, 1, 1, 33, 40, False, 64, 7, 2, 3, True, False, True, False, 0),       # U-Net enc1
+    (2, 64, 1, 24, 30, True, 64, 3, 1, 1, True, True, True, False, 2),        # final pc1
+    (2, 3, 0, 20, 22, False, 64, 3, 1, 1, False, True, False, False, 1),      # VGG conv1_1
+    (2, 2, 0, 30, 50, False, 16, 4, 2, 1, False, True, False, True, 2),       # D layer 1
+    (1, 5, 32, 9, 11, True, 130, 3, 1, 1, True, False, True, False, 2),       # C0 small + up
+    (2, 256, 1, 6, 10, True, 512, 3, 1, 1, True, False, True, False, 0),      # split-K, padded
+]
+
+
+@pytest.mark.parametrize("case", SMALL_C_CASES)
+def test_conv_gen_nhwc16_small_channel_sources(case, monkeypatch):
+    """bf16 channel-last conv with sources of C % 32 != 0 (k-values gathered
+    element-wise into zero-padded tiles), forced for every case, with BN
+    statistics: vs an fp64 convolution of the bf16-rounded operands."""
+    from ainp import ops
+    monkeypatch.setattr(ops, "CONV_NHWC16_SMALL", "all")
+    N, C0, C1, Hin, Win, up0, Cout, k, s, p, masks, hb, hr, hs, act = case
+    g = torch.Generator().manual_seed(hash(case) % 1000 + 11)
+    H0, W0 = (Hin // 2, Win // 2) if up0 else (Hin, Win)
+    x0 = torch.randn(N, C0, H0, W0, generator=g)
+    m0 = (torch.rand(N, H0, W0, generator=g) > 0.3).float() if masks else None
+    x1 = torch.randn(N, C1, Hin, Win, generator=g) if C1 else None
+    m1 = (torch.rand(N, Hin, Win, generator=g) > 0.3).float() if (masks and C1) else None
+    w = torch.randn(Cout, C0 + C1, k, k, generator=g) * 0.1
+    Ho, Wo = (Hin + 2 * p - k) // s + 1, (Win + 2 * p - k) // s + 1
+    bias = torch.randn(Cout, generator=g) if hb else None
+    ratio = torch.rand(N, Ho, Wo, generator=g) * 3 if hr else None
+    scale = torch.tensor([0.7]) if hs else None
+    d = lambda t: None if t is None else t.cuda()  # noqa: E731
+    y, stats = ops.conv_gen((d(x0), d(m0)), d(w), src1=(d(x1), d(m1)) if C1 else None, Hin=Hin,
+                            Win=Win, stride=s, pad=p, bias=d(bias), ratio=d(ratio),
+                            scale=d(scale), act=act, want_stats=True, bf16=True)
+    bf = lambda t: None if t is None else t.bfloat16().float()  # noqa: E731
+    yr, pre = _conv_ref(bf(x0), m0, bf(x1), m1, Hin, Win, bf(w), k, s, p, bias, ratio, scale, act)
+    assert y.shape == yr.shape
+    assert rel(y, yr) < 2e-5
+    st = stats.double().sum(0).cpu()
+    assert rel(st[0], pre.sum((0, 2, 3))) < 2e-5
+    assert rel(st[1], (pre * pre).sum((0, 2, 3))) < 2e-5
+    wt = ops.conv_weight_nhwc16(d(w), C0, C1)
+    assert wt.shape[1] == ops.nhwc16_seg(C0, k * k) + ops.nhwc16_seg(C1, k * k)
+    assert wt.shape[1] % 32 == 0
+
+
 @pytest.mark.parametrize("k,s,p,crop,act", [(3, 1, 1, (25, 30), 3), (4, 1, 1, None, 0),
                                              (4, 2, 1, None, 2)])
 def test_conv_gen_cout1(k, s, p, crop, act):
