@@ -578,19 +578,28 @@ def run_gan(args):
         out = torch.empty(B, 64, Hp, Wp, device=dev)
         kw = dict(src1=(x1, m1), Hin=Hp, Win=Wp, stride=1, pad=1, bias=bias, ratio=ratio,
                   act=ops.ACT_LEAKY, out=out, bf16=bf16)
-        avg_s = time_kernel(lambda: ops.conv_gen((x0, m0), w, **kw), args.roofline_reps, dev)
+        if bf16:   # the channel-last kernel alone, operands converted beforehand
+            launch = ops.conv_gen((x0, m0), w, launcher=True, **kw)
+            kname = "conv_gen_nhwc16_kernel<64, true>"
+        else:
+            launch = lambda: ops.conv_gen((x0, m0), w, **kw)  # noqa: E731
+            kname = "conv_gen_x6_kernel<64,16>"
+        avg_s = time_kernel(launch, args.roofline_reps, dev)
         flops = 2.0 * 64 * 65 * 9 * B * Hp * Wp
         ach = flops / avg_s / 1e12
         peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
         roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                "traffic": _traffic("traffic_conv_gen_final.json"),
-                "kernel": f"conv_gen_x6_kernel<64,16> (final PartialConv2d 65->64 3x3 at "
+                "traffic": _traffic("traffic_conv_gen_final_bf16.json" if bf16
+                                    else "traffic_conv_gen_final.json"),
+                "kernel": f"{kname} (final PartialConv2d 65->64 3x3 at "
                           f"{Hp}x{Wp}, B={B})", "avg_launch_ms": round(avg_s * 1e3, 4),
                 "flop_per_launch": flops}
         if bf16:
-            roof["main_loop"] = ("operands rounded to bf16 at LDS staging, "
+            roof["main_loop"] = ("channel-last bf16 operands (x*mask folded in; the 1-channel "
+                                 "skip source expanded per pixel, 9 -> 32 k-values), "
                                  "v_mfma_f32_32x32x16_bf16, f32 accumulate")
+            roof["executed_flop_per_launch"] = 2.0 * 64 * (64 * 9 + 32) * B * Hp * Wp
         else:
             roof.update({
                 "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross products "

@@ -28,8 +28,13 @@ class GanTrainer:
         self.cfg = cfg
         self.G, self.D, self.vgg = generator, discriminator, vgg
         betas = (tc.get("b1", 0.5), tc.get("b2", 0.999))
-        self.g_opt = Adam(generator.parameters(), lr=tc.get("g_lr", 2e-4), betas=betas)
-        self.d_opt = Adam(discriminator.parameters(), lr=tc.get("d_lr", 2e-4), betas=betas)
+        # accel.capturable: device-side Adam step counters, so the whole step
+        # can be captured in a HIP graph and replayed (tools/gan_graph.py)
+        cap = bool((cfg.get("accel") or {}).get("capturable", False))
+        self.g_opt = Adam(generator.parameters(), lr=tc.get("g_lr", 2e-4), betas=betas,
+                          capturable=cap)
+        self.d_opt = Adam(discriminator.parameters(), lr=tc.get("d_lr", 2e-4), betas=betas,
+                          capturable=cap)
         self.faithful = faithful_g_backward
         self.comm = comm
         dtype = (cfg.get("accel") or {}).get("dtype", "fp32")

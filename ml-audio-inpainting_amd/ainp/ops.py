@@ -625,7 +625,7 @@ def to_nhwc16(x, m=None):
 
 def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=None, ratio=None,
              scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None,
-             bf16=False):
+             bf16=False, launcher=False):
     """ainp_conv_gen_fwd.  src0/src1 = (x [N,C,Hs,Ws], mask plane [N,Hs,Ws] or None);
     the conv's input is cat(src0 nearest-resampled to (Hin, Win), src1) * masks.
     Returns (y [N,Cout,Ho,Wo] (or [N,crop_h,crop_w] for Cout=1 with crop), stats)."""
@@ -678,10 +678,16 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
             return to_nhwc16(x, m)
         a16 = src16(x0, m0, C0)
         b16 = src16(x1, m1, C1) if src1 is not None else None
-        _T.conv_gen_fwd_nhwc16(a16, b16, conv_weight_nhwc16(w, C0, C1), int(Cout), int(KH),
-                               int(KW), bias, ratio, scale, out, stats, int(Hin), int(Win),
-                               int(stride), int(pad), int(act), float(slope), ws,
-                               [int(N), int(C0), int(H0), int(W0), int(C1), int(H1), int(W1)])
+        wt16 = conv_weight_nhwc16(w, C0, C1)
+
+        def launch():
+            _T.conv_gen_fwd_nhwc16(a16, b16, wt16, int(Cout), int(KH), int(KW), bias, ratio,
+                                   scale, out, stats, int(Hin), int(Win), int(stride), int(pad),
+                                   int(act), float(slope), ws,
+                                   [int(N), int(C0), int(H0), int(W0), int(C1), int(H1), int(W1)])
+        if launcher:   # bench / profiling: the conv kernel alone on prepared operands
+            return launch
+        launch()
         return out, stats
     if Cout == 1:
         nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, ch or Ho, cw or Wo))
