@@ -622,8 +622,16 @@ class VGGLoss(nn.Module):
     @torch.no_grad()
     def forward(self, generated, target):
         _need_cuda(generated, "VGGLoss")
-        fg = self._extract_features(self._prepare(generated, True))
-        ft = self._extract_features(self._prepare(target, False))
+        xg, xt = self._prepare(generated, True), self._prepare(target, False)
+        if xg.shape == xt.shape:
+            # one VGG pass over both batches (no normalisation layers in
+            # vgg19.features: each image's features are those of its own pass)
+            B = xg.shape[0]
+            f = self._extract_features(torch.cat([xg, xt]))
+            fg = {i: v[:B] for i, v in f.items()}
+            ft = {i: v[B:] for i, v in f.items()}
+        else:
+            fg, ft = self._extract_features(xg), self._extract_features(xt)
         perc = torch.zeros((), device=generated.device, dtype=torch.float64)
         style = torch.zeros((), device=generated.device, dtype=torch.float64)
         n_p = n_s = 0
