@@ -1,6 +1,8 @@
 """Launch only the bench's roofline kernel (LSTM layer-0 input projection GEMM,
-M=N*T=10688, N=8H=1024, K=C*F=16448, fp32) a few times: the target of the
-rocprofv3 --pmc passes that give profiles/traffic_gemm_l0.json."""
+M=N*T=10688, N=8H=1024, K=C*F=16448) a few times: fp32 -> the x6 loop on fp32
+operands; bf16 (argv[2]) -> gemm_bf16nt on bf16 X / W_cat, as the bench times
+it.  The target of the rocprofv3 --pmc passes behind
+profiles/traffic_gemm_l0*.json."""
 import os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "ml-audio-inpainting_amd"))
@@ -8,13 +10,21 @@ import torch
 from ainp import ops
 H, F, B, T = 128, 257, 32, 334
 M, I = B * T, (H // 2) * F
+reps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+bf16 = len(sys.argv) > 2 and sys.argv[2] == "bf16"
 dev = "cuda"
 A = torch.randn(M, I, device=dev)
 W = [torch.randn(4 * H, I, device=dev) * 0.01 for _ in range(2)]
 b = [torch.zeros(4 * H, device=dev) for _ in range(4)]
 zx = torch.empty(M, 8 * H, device=dev)
-for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 5):
-    ops.gemm(M, 4 * H, I, [A, A], I, 1, W, 1, I, [zx, zx[:, 4 * H:]], 8 * H, 1,
-             bias1=b[:2], bias2=b[2:])
+if bf16:
+    A16 = A.bfloat16()
+    W16 = torch.cat(W).bfloat16()
+    for _ in range(reps):
+        ops.gemm_bf16nt(A16, W16, out=zx, bias=tuple(b), bias_nsplit=4 * H)
+else:
+    for _ in range(reps):
+        ops.gemm(M, 4 * H, I, [A, A], I, 1, W, 1, I, [zx, zx[:, 4 * H:]], 8 * H, 1,
+                 bias1=b[:2], bias2=b[2:])
 torch.cuda.synchronize()
 print("done")
