@@ -177,36 +177,40 @@ __global__ __launch_bounds__(256) void stft_features_kernel(
 
 // ---------------------------------------------------------------------------
 // n_fft = 512 fast path (every configuration of BASELINE.json): tiles of 16
-// consecutive frames of one example per workgroup, outputs staged in LDS and
-// written as contiguous runs along t (the [B][F][T] layout), so every store is
-// a coalesced 64-B (f32) / 128-B (complex64) row segment instead of one
-// 4-byte scatter per bin.
+// consecutive frames of one example per workgroup of 4 waves, one frame per
+// 16-lane group; outputs staged in LDS and written as contiguous runs along t
+// (the [B][F][T] layout), so every store is a coalesced 64-B (f32) / 128-B
+// (complex64) row segment instead of one 4-byte scatter per bin.
 //
 // FFT: the 512-point real FFT is a 256-point complex FFT of
 // z[m] = x[2m] + i x[2m+1], computed four-step as 16 x 16 in float64:
-// 16 lanes per FFT, lane j holds z[16 n1 + j] (n1 = 0..15; a coalesced 128-B
-// load per n1), a 16-point DFT in registers (radix 4 x 4), the twiddle
-// W256^{j k1} (per-lane registers, read once from an LDS table), a dword-wise
-// 16 x 16 transpose through the wave's own LDS slice (no block barrier), and a
-// second in-register 16-point DFT.  Lane j then holds Z[j + 16 k2]; the
-// real-FFT unpack takes Z[256 - k] from lane 16 - j by ds_bpermute.
+// lane j holds z[16 n1 + j] (n1 = 0..15), a 16-point DFT in registers
+// (radix 4 x 4), the twiddle W256^{j k1} (LDS table), a 16 x 16 transpose
+// through the group's own LDS slot (wave-local sync), a second 16-point DFT.
+// Lane j then holds Z[j + 16 k2]; the real-FFT unpack pairs bins k and 256 - k
+// (X[256 - k] = conj(Ze - W^k Zo)), so each lane forms 16 bins from 8 partner
+// values fetched from lane 16 - j -- half the fp64 work of one bin per value.
 //
 // Work: one clean FFT per frame; a gapped FFT only for frames whose window
 // [t*hop - 256, t*hop + 256) intersects the gap -- elsewhere the gapped and
 // clean signals are the same float64 values, so the clean FFT is bit-identical
-// to the gapped one and feeds the log-magnitude directly.
+// to the gapped one and feeds the log-magnitude directly.  The kernel is
+// fp64-VALU-bound (gfx950 issues a wave64 fp64 op at half the fp32 rate,
+// measured 30 T lane-ops/s, tools/fp64_rate.hip) and store-bound in turn;
+// tools/stft_lab.hip holds the measured alternatives.
 namespace f512 {
 constexpr int M = 256, F = 257, TF = 16, NW = 4, NT = 64 * NW;
 constexpr int XROW = 17;                 // transpose row stride (dwords)
 constexpr int XSLOT = 16 * XROW;         // per-FFT transpose buffer (dwords)
-constexpr int PROW = 17;                 // staging row stride (floats) per bin
-constexpr int PLANE = F * PROW;          // floats per staged output plane
-constexpr size_t LDS_WIN = 512 * sizeof(double);
-constexpr size_t LDS_XCH = (size_t)NW * 4 * XSLOT * sizeof(uint32_t);
-constexpr size_t LDS_STAGE = (size_t)3 * PLANE * sizeof(float);
-constexpr size_t LDS_TW = (size_t)M * 2 * sizeof(double);
-constexpr size_t LDS_BYTES = LDS_WIN + LDS_TW + LDS_XCH + LDS_STAGE;
-static_assert(LDS_BYTES * 2 <= 160 * 1024, "two workgroups per CU");
+// LDS: log-magnitude plane P0 [257][16] f32 | complex plane PC [257][16] float2
+// (during the FFT phase PC's bytes hold the transpose slots and the window) |
+// W256 twiddle table.  53.4 KB: two workgroups per CU (VGPR-limited).
+constexpr size_t LDS_P0 = (size_t)F * TF * sizeof(float);
+constexpr size_t LDS_PC = (size_t)F * TF * sizeof(float2);
+constexpr size_t LDS_TW = 256 * sizeof(double2);
+constexpr size_t LDS_BYTES = LDS_P0 + LDS_PC + LDS_TW;
+constexpr size_t XCH_BYTES = (size_t)NW * 4 * XSLOT * sizeof(uint32_t);
+static_assert(XCH_BYTES + 512 * sizeof(double) <= LDS_PC, "xch + window fit in PC");
 
 constexpr double C1 = 0.9807852804032304, S1 = 0.19509032201612825;  // cos/sin(pi/16)
 constexpr double C2 = 0.9238795325112867, S2 = 0.3826834323650898;   // cos/sin(pi/8)
@@ -283,7 +287,7 @@ __device__ __forceinline__ int64_t xcd_tile(int64_t b, int64_t n) {
 
 // Per-tile scalars (uniform over the workgroup).
 struct Tile {
-  int b, t0, ncomp, nvalid, ga, gb, njobs;
+  int b, t0, ncomp, nvalid, ga, gb;
   int64_t gs64, ge64;
   const float* x;
 };
@@ -314,240 +318,268 @@ __device__ __forceinline__ Tile make_tile(int v, int ntiles, int ntt, int NF, in
     T.ga = (int)max((int64_t)0, min((int64_t)T.ncomp, tlo - T.t0));
     T.gb = (int)max((int64_t)T.ga, min((int64_t)T.ncomp, thi - T.t0));
   }
-  T.njobs = want_fft ? T.ncomp + (T.gb - T.ga) : 0;
   return T;
 }
 
-// Job q of a tile: columns 0..ncomp-1 clean, then ga..gb-1 gapped.  Lane j of
-// the job's 16-lane group loads x[s0 + 32 n1 + {0,1}], s0 = t*hop - 256 + 2j;
-// samples outside the signal, and gap samples of gapped jobs, read as 0 (an
-// exact zero, as the reference's multiply / concatenate gives).
+// staged element (bin f, tile column c): columns XOR-swizzled by the bin's low
+// bits, so the unpack's 16 lanes (16 bins, one column) hit 16 banks and the
+// write-out's 16 lanes (one bin, 16 columns) read one contiguous row.
+__device__ __forceinline__ int sw(int f, int c) { return f * TF + (c ^ (f & 15)); }
+
 template <bool VEC2>
-__device__ __forceinline__ void load_raw(const Tile& T, int q, int j, int ns, int hop,
-                                         int64_t gap_len, float (&raw0)[16],
-                                         float (&raw1)[16]) {
-  q = min(q, max(T.njobs - 1, 0));
-  const int c = q < T.ncomp ? q : T.ga + (q - T.ncomp);
-  const int s0 = (T.t0 + c) * hop - 256 + 2 * j;
-  const int gs = (int)max((int64_t)-(1 << 30), min((int64_t)1 << 30, T.gs64));
-  const int gl = q >= T.ncomp ? (int)gap_len : 0;
+__device__ __forceinline__ void load_frame(const float* __restrict__ x, int s0, int ns, int gs,
+                                           int gl, bool check, float (&r0)[16],
+                                           float (&r1)[16]) {
+  if (!check) {
+#pragma unroll
+    for (int n1 = 0; n1 < 16; ++n1) {
+      if (VEC2) {
+        const float2 p = *reinterpret_cast<const float2*>(x + s0 + 32 * n1);
+        r0[n1] = p.x;
+        r1[n1] = p.y;
+      } else {
+        r0[n1] = x[s0 + 32 * n1];
+        r1[n1] = x[s0 + 32 * n1 + 1];
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int n1 = 0; n1 < 16; ++n1) {
     const int s = s0 + 32 * n1;
     const bool in0 = (unsigned)s < (unsigned)ns && (unsigned)(s - gs) >= (unsigned)gl;
     const bool in1 = (unsigned)(s + 1) < (unsigned)ns && (unsigned)(s + 1 - gs) >= (unsigned)gl;
     if (VEC2) {
-      const float2 p = *reinterpret_cast<const float2*>(T.x + min(max(s, 0), ns - 2));
-      raw0[n1] = in0 ? p.x : 0.f;
-      raw1[n1] = in1 ? p.y : 0.f;
+      const float2 p = *reinterpret_cast<const float2*>(x + min(max(s, 0), ns - 2));
+      r0[n1] = in0 ? p.x : 0.f;
+      r1[n1] = in1 ? p.y : 0.f;
     } else {
-      const float p0 = T.x[min(max(s, 0), ns - 1)];
-      const float p1 = T.x[min(max(s + 1, 0), ns - 1)];
-      raw0[n1] = in0 ? p0 : 0.f;
-      raw1[n1] = in1 ? p1 : 0.f;
+      const float p0 = x[min(max(s, 0), ns - 1)];
+      const float p1 = x[min(max(s + 1, 0), ns - 1)];
+      r0[n1] = in0 ? p0 : 0.f;
+      r1[n1] = in1 ? p1 : 0.f;
     }
   }
 }
 
-// Persistent: each workgroup walks tiles v = blockIdx.x, + gridDim.x, ...;
-// the next tile's samples are loaded while the current tile is written out.
+// window (x 1/2, exact), 16-point DFT over n1, twiddle W256^{j k1}, wave-local
+// 16 x 16 transpose (four dword planes, in place: each round moves one plane),
+// 16-point DFT over n2.  Lane j ends with Z[j + 16 k2] at pos(k2).
+__device__ __forceinline__ void fft256(const float (&r0)[16], const float (&r1)[16],
+                                       const double2* win2, int j,
+                                       const double2* tw256, uint32_t* xs, double (&re)[16],
+                                       double (&im)[16], int tstride = 1) {
+#pragma unroll
+  for (int n1 = 0; n1 < 16; ++n1) {
+    const double2 w = win2[16 * n1 + j];
+    re[n1] = (double)r0[n1] * w.x;
+    im[n1] = (double)r1[n1] * w.y;
+  }
+  __builtin_amdgcn_sched_barrier(0);  // keep the twiddle loads below the first DFT
+  dft16(re, im);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k1 = 1; k1 < 16; ++k1) {
+    const double2 w = tw256[((j * k1) & 255) * tstride];
+    cmul_c(re[pos(k1)], im[pos(k1)], w.x, w.y);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int hi = r & 1;
+#pragma unroll
+    for (int k1 = 0; k1 < 16; ++k1)
+      xs[k1 * XROW + j] = dw(r < 2 ? re[pos(k1)] : im[pos(k1)], hi);
+    wave_sync();
+#pragma unroll
+    for (int n2 = 0; n2 < 16; ++n2) {
+      const uint32_t u = xs[j * XROW + n2];
+      if (r < 2) re[n2] = set_dw(re[n2], hi, u);
+      else im[n2] = set_dw(im[n2], hi, u);
+    }
+    wave_sync();
+  }
+  dft16(re, im);
+}
+
+// Real-FFT unpack by conjugate pairs: lane j forms X[k] and X[256 - k] for
+// k = j + 16 k2, k2 = 0..7 (X[256 - k] = conj(Ze - W^k Zo)), and lane 0 also
+// X[128].  Z's partner Z[256 - k] lives in lane 16 - j (lane 0: itself).
+template <typename Out>
+__device__ __forceinline__ void unpack(const double (&re)[16], const double (&im)[16], int j,
+                                       int lane, double ujr, double uji, Out out,
+                                       const double2* Wt = nullptr) {
+  const int src = (lane & ~15) | ((16 - j) & 15);
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2) {
+    const double zr = re[pos(k2)], zi = im[pos(k2)];
+    const double sr = __shfl(re[pos(15 - k2)], src, 64);
+    const double si = __shfl(im[pos(15 - k2)], src, 64);
+    const double pr = j == 0 ? re[pos((16 - k2) & 15)] : sr;
+    const double pi = j == 0 ? im[pos((16 - k2) & 15)] : si;
+    const double er = zr + pr, ei = zi - pi;
+    double orr = zi + pi, oi = pr - zr;
+    double wr = ujr, wi = uji;
+    if (Wt) {
+      const double2 w = Wt[j + 16 * k2];
+      wr = w.x;
+      wi = w.y;
+    } else {
+      cmul_c(wr, wi, W32R[k2], W32I[k2]);
+    }
+    cmul_c(orr, oi, wr, wi);
+    out(j + 16 * k2, er + orr, ei + oi);
+    out(256 - j - 16 * k2, er - orr, oi - ei);
+  }
+  if (j == 0) {
+    const double zr = re[pos(8)], zi = im[pos(8)];
+    const double er = zr + zr, orr = zi + zi;
+    double wr = ujr, wi = uji, o_r = orr, o_i = zr - zr;
+    if (Wt) {
+      wr = Wt[128].x;
+      wi = Wt[128].y;
+    } else {
+      cmul_c(wr, wi, W32R[8], W32I[8]);
+    }
+    cmul_c(o_r, o_i, wr, wi);
+    out(128, er + o_r, (zi - zi) + o_i);
+  }
+}
+
+// log10(|X| + 1e-9) of the complex64-rounded bin: |X|^2 in fp32 (the
+// cancellation-prone arithmetic is the fp64 FFT before it); the argument of the
+// log is >= 1e-9, so the raw v_log_f32 needs no denormal scaling.
+__device__ __forceinline__ float lm_cnn(double Xr, double Xi) {
+  const float r = (float)Xr, i = (float)Xi;
+  return __builtin_amdgcn_logf(__builtin_amdgcn_sqrtf(r * r + i * i) + 1e-9f) *
+         0.30102999566398120f;
+}
+
 template <int MODE, bool VEC2>
 __global__ __launch_bounds__(NT, 2) void stft512_kernel(
-    const float* __restrict__ audio, int64_t n_samples,
-    const int32_t* __restrict__ clip_index, const int64_t* __restrict__ gap_start,
-    int64_t batch, int64_t gap_len, int64_t sample_rate,
+    const float* __restrict__ audio, int64_t n_samples, const int32_t* __restrict__ clip_index,
+    const int64_t* __restrict__ gap_start, int64_t batch, int64_t gap_len, int64_t sample_rate,
     const double* __restrict__ window, int hop, int64_t n_frames, int64_t n_tiles_t,
     float* __restrict__ out0, float* __restrict__ out1, float* __restrict__ out2,
     float* __restrict__ out3) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  double* win = reinterpret_cast<double*>(smem);
-  double2* tw256 = reinterpret_cast<double2*>(smem + LDS_WIN);  // W256^q
-  uint32_t* xch = reinterpret_cast<uint32_t*>(smem + LDS_WIN + LDS_TW);
-  float* stage = reinterpret_cast<float*>(smem + LDS_WIN + LDS_TW + LDS_XCH);
-  float* P0 = stage;
-  float* P1 = stage + PLANE;
-  float* P2 = stage + 2 * PLANE;
+  float* P0 = reinterpret_cast<float*>(smem);
+  float2* PC = reinterpret_cast<float2*>(smem + LDS_P0);
+  // FFT phase: transpose slots and the window (x 1/2) live in PC's bytes
+  uint32_t* xch = reinterpret_cast<uint32_t*>(smem + LDS_P0);
+  double2* win2 = reinterpret_cast<double2*>(smem + LDS_P0 + XCH_BYTES);
+  double2* tw256 = reinterpret_cast<double2*>(smem + LDS_P0 + LDS_PC);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int slot = lane >> 4, j = lane & 15;
-  // the launcher guarantees n_samples, n_frames * hop and gap_len < 2^30
+  const int j0 = lane & 15, myjob0 = wave * 4 + (lane >> 4);
   const int ntt = (int)n_tiles_t, NF = (int)n_frames, ns = (int)n_samples;
   const int ntiles = (int)(batch * n_tiles_t);
   const bool want_lm = MODE == AINP_FEAT_CNNBLSTM ? out0 != nullptr : out1 != nullptr;
   const bool want_fft = MODE == AINP_FEAT_CNNBLSTM ? (out0 || out1) : (out0 || out1 || out2);
   float* mask_out = MODE == AINP_FEAT_CNNBLSTM ? out2 : out3;
   const int n_avail = 1 + ns / hop;
-  const int myjob = wave * 4 + slot;
-
-  int v = blockIdx.x;
-  Tile T = make_tile<MODE>(v, ntiles, ntt, NF, ns, hop, audio, n_samples, clip_index,
-                           gap_start, gap_len, want_lm, want_fft);
-  float raw0[16], raw1[16];
-  load_raw<VEC2>(T, myjob, j, ns, hop, gap_len, raw0, raw1);
-
-  // window / 2 (the unpack's 1/2 factors, exact) and W256^q into LDS, once
-  for (int n = tid; n < 512; n += NT) win[n] = 0.5 * window[n];
   {
     double s, c;
     sincospi(-(double)tid / 128.0, &s, &c);
     tw256[tid] = make_double2(c, s);
   }
   double ujr, uji;  // W512^j
-  sincospi(-(double)j / 256.0, &uji, &ujr);
-  uint32_t* xs = xch + myjob * XSLOT;
+  sincospi(-(double)j0 / 256.0, &uji, &ujr);
+  double2 wreg = make_double2(window[2 * tid], window[2 * tid + 1]);
+  wreg.x *= 0.5;  // the unpack's 1/2 factors (exact)
+  wreg.y *= 0.5;
 
-  while (true) {
-    if (T.ncomp < TF) {  // frames past the end of the signal (t >= 1 + S//hop) are zero
-      for (int i = tid; i < F * TF; i += NT) {
-        const int c = i % TF, f = i / TF;
-        if (c >= T.ncomp) {
-          P0[f * PROW + c] = 0.f;
-          P1[f * PROW + c] = 0.f;
-          P2[f * PROW + c] = 0.f;
-        }
-      }
-    }
-    __syncthreads();  // tables ready / previous tile written out
-
-    for (int q0 = 0; q0 < T.njobs; q0 += 4 * NW) {
-      const int q = q0 + myjob;
-      const bool active = q < T.njobs;
-      const bool gapped = q >= T.ncomp;
-      if (q0 > 0) load_raw<VEC2>(T, q, j, ns, hop, gap_len, raw0, raw1);
-      const int c = active ? (gapped ? T.ga + (q - T.ncomp) : q) : 0;
+  for (int v = blockIdx.x; v < ntiles; v += gridDim.x) {
+    const Tile T = make_tile<MODE>(v, ntiles, ntt, NF, ns, hop, audio, n_samples,
+                                               clip_index, gap_start, gap_len, want_lm, want_fft);
+    if (want_fft) {
+      win2[tid] = wreg;  // the previous tile's unpack overwrote it
+      // lane indices laundered per tile: keeps the compiler from hoisting ~100
+      // per-lane LDS addresses out of the tile loop into registers
+      int j = j0, myjob = myjob0;
+      asm volatile("" : "+v"(j), "+v"(myjob));
+      __syncthreads();
+      const int cb = min(myjob, max(T.ncomp - 1, 0));
+      const bool act_b = myjob < T.ncomp;
+      const bool interior = T.ncomp == TF && T.t0 * hop >= 256 && (T.t0 + TF - 1) * hop + 256 <= ns;
       double re[16], im[16];
-      // 1. window: z[16 n1 + j] = w x[32 n1 + 2j] + i w x[32 n1 + 2j + 1]
-#pragma unroll
-      for (int n1 = 0; n1 < 16; ++n1) {
-        const double2 w = *reinterpret_cast<const double2*>(win + 32 * n1 + 2 * j);
-        re[n1] = (double)raw0[n1] * w.x;
-        im[n1] = (double)raw1[n1] * w.y;
-      }
-      // 2. DFT over n1, twiddle W256^{j k1}
-      dft16(re, im);
-      double br[16], bi[16];
-#pragma unroll
-      for (int k1 = 0; k1 < 16; ++k1) {
-        br[k1] = re[pos(k1)];
-        bi[k1] = im[pos(k1)];
-        if (k1) {
-          const double2 w = tw256[(j * k1) & 255];
-          cmul_c(br[k1], bi[k1], w.x, w.y);
-        }
-      }
-      // 3. transpose Y[k1][n2=j] -> lane j gets Y[k1=j][n2], one dword plane at a time
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int hi = r & 1;
-#pragma unroll
-        for (int k1 = 0; k1 < 16; ++k1) xs[k1 * XROW + j] = dw(r < 2 ? br[k1] : bi[k1], hi);
-        wave_sync();
-#pragma unroll
-        for (int n2 = 0; n2 < 16; ++n2) {
-          const uint32_t u = xs[j * XROW + n2];
-          if (r < 2) re[n2] = set_dw(re[n2], hi, u);
-          else im[n2] = set_dw(im[n2], hi, u);
-        }
-        wave_sync();
-      }
-      // 4. DFT over n2: lane j now holds Z[j + 16 k2] at pos(k2)
-      dft16(re, im);
-      // 5. real-FFT unpack; partner Z[(256 - k) & 255] lives in lane (16 - j) & 15.
-      // Stores are unconditional: a lane whose value is not wanted writes the
-      // padding column TF of its row.
-      const bool in_gap = c >= T.ga && c < T.gb;
-      const int c_clean = active && !gapped ? c : TF;           // target / orig / phase
-      const int c_lm = active && (gapped || !in_gap) ? c : TF;   // log-magnitude of X_gap
-      const int c_lm2 = MODE == AINP_FEAT_GAN && active && !gapped && !in_gap ? c : TF;
-      const int src = (lane & ~15) | ((16 - j) & 15);
-#pragma unroll
-      for (int k2 = 0; k2 < 16; ++k2) {
-        const double zr = re[pos(k2)], zi = im[pos(k2)];
-        const double sr = __shfl(re[pos(15 - k2)], src, 64);
-        const double si = __shfl(im[pos(15 - k2)], src, 64);
-        const double pr = j == 0 ? re[pos((16 - k2) & 15)] : sr;
-        const double pi = j == 0 ? im[pos((16 - k2) & 15)] : si;
-        // Z carries a factor 1/2 (window): Ze = Z + conj(Zp), Zo = -i (Z - conj(Zp))
-        const double er = zr + pr, ei = zi - pi;
-        double orr = zi + pi, oi = pr - zr;
-        double wr = ujr, wi = uji;  // W512^{j + 16 k2} = W512^j * W32^{k2}
-        cmul_c(wr, wi, W32R[k2], W32I[k2]);
-        cmul_c(orr, oi, wr, wi);
-        const double Xr = er + orr, Xi = ei + oi;
-        const int row = (j + 16 * k2) * PROW;
+      uint32_t* xs = xch + myjob * XSLOT;
+      // pass A: gapped FFTs of the columns whose window meets the gap (log-magnitude only)
+      if (T.gb > T.ga) {
+        const int ca = min(T.ga + myjob, T.gb - 1);
+        const bool act_a = T.ga + myjob < T.gb;
+        const int gs = (int)max((int64_t)-(1 << 30), min((int64_t)1 << 30, T.gs64));
+        float ra0[16], ra1[16];
+        load_frame<VEC2>(T.x, (T.t0 + ca) * hop - 256 + 2 * j, ns, gs, (int)gap_len, true, ra0,
+                         ra1);
+        fft256(ra0, ra1, win2, j, tw256, xs, re, im);
         if (MODE == AINP_FEAT_CNNBLSTM) {
-          P1[row + c_clean] = (float)Xr;
-          P2[row + c_clean] = (float)Xi;
-          P0[row + c_lm] = __log10f(__builtin_amdgcn_sqrtf((float)(Xr * Xr + Xi * Xi)) + 1e-9f);
+          unpack(re, im, j, lane, ujr, uji, [&](int f, double Xr, double Xi) {
+            if (act_a) P0[sw(f, ca)] = lm_cnn(Xr, Xi);
+          });
         } else {
+          unpack(re, im, j, lane, ujr, uji, [&](int f, double Xr, double Xi) {
+            if (act_a) P0[sw(f, ca)] = log1pf(hypotf((float)Xr, (float)Xi));
+          });
+        }
+      }
+      // pass B: clean FFTs
+      float rb0[16], rb1[16];
+      load_frame<VEC2>(T.x, (T.t0 + cb) * hop - 256 + 2 * j, ns, 0, 0, !interior, rb0, rb1);
+      fft256(rb0, rb1, win2, j, tw256, xs, re, im);
+      __syncthreads();  // every transpose slot is read (they alias PC)
+      const bool own_lm = act_b && !(myjob >= T.ga && myjob < T.gb);
+      const bool zero_lm = !act_b;
+      if (MODE == AINP_FEAT_CNNBLSTM) {
+        unpack(re, im, j, lane, ujr, uji, [&](int f, double Xr, double Xi) {
+          const int l = sw(f, myjob);
+          PC[l] = act_b ? make_float2((float)Xr, (float)Xi) : make_float2(0.f, 0.f);
+          if (own_lm || zero_lm) P0[l] = act_b ? lm_cnn(Xr, Xi) : 0.f;
+        });
+      } else {
+        unpack(re, im, j, lane, ujr, uji, [&](int f, double Xr, double Xi) {
+          const int l = sw(f, myjob);
           const float cr = (float)Xr, ci = (float)Xi;
           const float lm = log1pf(hypotf(cr, ci));
-          P0[row + c_clean] = lm;
-          P2[row + c_clean] = atan2f(ci, cr);
-          P1[row + (gapped ? c_lm : c_lm2)] = lm;
-        }
+          PC[l] = act_b ? make_float2(lm, atan2f(ci, cr)) : make_float2(0.f, 0.f);
+          if (own_lm || zero_lm) P0[l] = act_b ? lm : 0.f;
+        });
       }
-      // Nyquist bin 256 = Re Z0 - Im Z0 (lane j = 0)
-      if (j == 0) {
-        const double Xr = 2.0 * (re[0] - im[0]);
-        const int row = 256 * PROW;
-        if (MODE == AINP_FEAT_CNNBLSTM) {
-          P1[row + c_clean] = (float)Xr;
-          P2[row + c_clean] = 0.f;
-          P0[row + c_lm] = __log10f(fabsf((float)Xr) + 1e-9f);
-        } else {
-          const float cr = (float)Xr;
-          const float lm = log1pf(fabsf(cr));
-          P0[row + c_clean] = lm;
-          P2[row + c_clean] = atan2f(0.f, cr);
-          P1[row + (gapped ? c_lm : c_lm2)] = lm;
-        }
-      }
-    }
-
-    // next tile: its first-pass samples load while this tile is written out
-    const Tile cur = T;
-    v += gridDim.x;
-    const bool more = v < ntiles;
-    if (more) {
-      T = make_tile<MODE>(v, ntiles, ntt, NF, ns, hop, audio, n_samples, clip_index,
-                          gap_start, gap_len, want_lm, want_fft);
-      load_raw<VEC2>(T, myjob, j, ns, hop, gap_len, raw0, raw1);
     }
     __syncthreads();
 
-    // coalesced write-out: thread (row, col) -> rows of TF consecutive frames
-    const int col = tid % TF, row0 = tid / TF;
-    if (col < cur.nvalid) {
-      const int t = cur.t0 + col;
+    // coalesced write-out: thread (row, col) -> runs of TF consecutive frames
+    int col = tid % TF, row0 = tid / TF;
+    asm volatile("" : "+v"(col), "+v"(row0));
+    if (col < T.nvalid) {
+      const int t = T.t0 + col;
       float maskv;
       if (MODE == AINP_FEAT_CNNBLSTM) {
-        const int64_t fs = time_to_frame(cur.gs64, sample_rate, hop);
-        const int64_t fe = time_to_frame(cur.ge64, sample_rate, hop);
+        const int64_t fs = time_to_frame(T.gs64, sample_rate, hop);
+        const int64_t fe = time_to_frame(T.ge64, sample_rate, hop);
         maskv = (t >= fs && t < fe) ? 1.f : 0.f;
       } else {
-        int64_t fs = cur.gs64 / hop;
-        int64_t fe = (cur.ge64 + hop - 1) / hop;
+        int64_t fs = T.gs64 / hop;
+        int64_t fe = (T.ge64 + hop - 1) / hop;
         if (fs < 0) fs = 0;
         if (fe > n_avail) fe = n_avail;
         maskv = (fe > fs && t >= fs && t < fe) ? 0.f : 1.f;
       }
-      const size_t base = (size_t)cur.b * F * n_frames + t;
+      const size_t base = (size_t)T.b * F * n_frames + t;
       for (int f = row0; f < F; f += NT / TF) {
         const size_t o = base + (size_t)f * n_frames;
-        const int l = f * PROW + col;
+        const int l = sw(f, col);
         if (MODE == AINP_FEAT_CNNBLSTM) {
           if (out0) out0[o] = P0[l];
-          if (out1) reinterpret_cast<float2*>(out1)[o] = make_float2(P1[l], P2[l]);
+          if (out1) reinterpret_cast<float2*>(out1)[o] = PC[l];
         } else {
-          if (out0) out0[o] = P0[l];
-          if (out1) out1[o] = P1[l];
-          if (out2) out2[o] = P2[l];
+          const float2 p = PC[l];
+          if (out0) out0[o] = p.x;
+          if (out1) out1[o] = P0[l];
+          if (out2) out2[o] = p.y;
         }
         if (mask_out) mask_out[o] = maskv;
       }
     }
-    if (!more) break;
     __syncthreads();  // staging is rewritten by the next tile
   }
 }
@@ -663,10 +695,20 @@ extern "C" int ainp_stft_features(const float* audio, int64_t n_clips,
     const int64_t ntt = cdiv(n_frames, f512::TF);
     const int64_t ntiles = batch * ntt;
     if (ntiles > 0x7fffffff) return record_msg("ainp_stft_features: too many frames");
-    // persistent: at most two workgroups per CU (LDS-limited); pstride env for tuning
-    int64_t grid = ntiles;
+    // persistent: two workgroups per CU walk the tiles (more do not fit the
+    // VGPR budget); AINP_STFT_GRID overrides for tuning
+    static int n_cu = 0;
+    if (n_cu == 0) {
+      int dev = 0, cu = 0;
+      if (hipGetDevice(&dev) == hipSuccess &&
+          hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+        n_cu = cu > 0 ? cu : 256;
+      else
+        n_cu = 256;
+    }
+    int64_t grid = min(ntiles, (int64_t)2 * n_cu);
     const char* ps = getenv("AINP_STFT_GRID");
-    if (ps && atoi(ps) > 0) grid = min(grid, (int64_t)atoi(ps));
+    if (ps && atoi(ps) > 0) grid = min(ntiles, (int64_t)atoi(ps));
     const bool vec2 = (hop % 2 == 0) && (n_samples % 2 == 0) &&
                       ((reinterpret_cast<uintptr_t>(audio) & 7) == 0);
 #define AINP_F512(MODE, V)                                                              \
