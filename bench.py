@@ -381,12 +381,13 @@ def main():
         traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else "traffic_gemm_l0.json")
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": traffic, "kernel": ("g16::gemm_bf16nt_kernel" if bf16 else
+                "traffic": traffic, "kernel": ("g256::gemm_bf16nt_256_kernel" if bf16 else
                                                "gemm_f32_kernel<1,...>") + f" (LSTM l0 "
                 f"input projection, M={M} N={8 * H} K={I}, both directions)",
                 "avg_launch_ms": round(avg_s * 1e3, 4), "flop_per_launch": flops}
         if bf16:
-            roof["main_loop"] = ("bf16 operands in HBM (X, W_cat), 128x128x64 tiles, "
+            roof["main_loop"] = ("bf16 operands in HBM (X, W_cat), 256x256x32 tiles staged "
+                                 "by global_load_lds into a 4-stage LDS ring, "
                                  "v_mfma_f32_32x32x16_bf16, f32 accumulate")
         elif not ops.GEMM_EXACT:
             # fp32-accurate three-piece bf16 split: 6 bf16 MFMA products per fp32

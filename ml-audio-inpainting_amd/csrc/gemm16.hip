@@ -17,8 +17,12 @@
 // prefetched in registers (4 x 16 B per operand per thread); <= 168 VGPRs so
 // three workgroups fit per CU.  XCD-aware block order as gemm.hip.  Split-K:
 // blockIdx.y = split s covers k in [s*kc, min(K, (s+1)*kc)) and writes slab
-// C + s*strideC (summed by ainp_sum_slabs in fixed order).
+// C + s*strideC (summed by ainp_sum_slabs in fixed order).  GEMMs with M and
+// N >= 512 run on g256 below instead (256 x 256 tiles, LDS-DMA ring):
+// 596-651 -> 722-890 TF at the layer-0 shapes (tools/gemm256_lab.hip).
 #include "common.h"
+
+#include <stdlib.h>
 
 namespace ainp {
 namespace g16 {
@@ -186,6 +190,157 @@ __global__ __launch_bounds__(256) void cast_bf16_t_kernel(const float* __restric
 }
 
 }  // namespace g16
+
+// Large GEMMs (M, N >= 512): 256 x 256 x 32 tiles with LDS-DMA staging.
+//
+// 512 threads = 8 waves as 2 (m) x 4 (n); each wave owns 128 x 64 outputs =
+// 4 x 2 tiles of v_mfma_f32_32x32x16_bf16 (128 accumulator VGPRs).  Operand
+// tiles (256 rows x 32 k, 64-byte rows) arrive by global_load_lds_dwordx4
+// (16 B per lane, one 1-KB contiguous LDS block per wave instruction: 16 rows)
+// into a ring of 4 LDS stages (4 x 32 KB), two K-tiles kept in flight across
+// each barrier by a counted vmcnt; one raw s_barrier per K-tile.  The LDS
+// image is row-linear with the four 16-byte chunks of a row XOR-swizzled by
+// bits 2..3 of the row (applied on the global source address, since the DMA
+// destination is lane-linear), so the 16 lanes of a ds_read_b128 quarter
+// (16 consecutive rows, one k-chunk) hit 16 distinct 16-byte bank slots.
+namespace g256 {
+constexpr int BM = 256, BN = 256, BK = 32, THREADS = 512, NSTAGE = 4;
+constexpr int ROWB = BK * 2;             // 64 bytes per image row
+constexpr int IMG = BM * ROWB;           // 16 KB per operand per stage
+constexpr int STAGE = 2 * IMG;           // A + B
+constexpr int LDS_BYTES = NSTAGE * STAGE;  // 128 KB
+constexpr int GLDS_PER_TILE = 4;         // per wave: 2 for A, 2 for B
+
+using g16::bf16x8v;
+using g16::f32x16v;
+using g16::Bias;
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+
+// Stage one operand's 256 x 32 K-tile: wave w, instruction i covers image
+// rows 16 (2w + i) .. +16; lane L -> row + L/4, physical chunk L % 4.
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ P, int64_t ld, int64_t r0,
+                                      int64_t R, int64_t k0, unsigned char* img, int wave,
+                                      int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = 2 * wave + i;
+    const int row = 16 * blk + (lane >> 2);
+    const int c = swz(row, lane & 3);
+    int64_t gr = r0 + row;
+    gr = gr < R ? gr : R - 1;  // rows past the end: any valid row (never stored)
+    const uint16_t* src = P + gr * ld + k0 + 8 * c;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)src, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8v frag(const unsigned char* img, int row, int chunk) {
+  return __builtin_bit_cast(bf16x8v,
+                            *reinterpret_cast<const uint4*>(img + row * ROWB + 16 * swz(row, chunk)));
+}
+
+template <int N_INFLIGHT>
+__device__ __forceinline__ void wait_vm() {
+  if (N_INFLIGHT == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else if (N_INFLIGHT == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+__global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
+    int64_t M, int64_t N, int64_t K, const uint16_t* __restrict__ A, int64_t lda,
+    const uint16_t* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
+    int64_t kc, int64_t strideC, Bias bias, int tiles_n) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  // XCD-aware order: each XCD owns a contiguous range of linear tiles; within
+  // it groups of (up to) 8 n-tiles walk down m, sharing A panels in its L2
+  const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t first_n = (bid / per_group) * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+
+  const int64_t split = blockIdx.y;
+  const int64_t kbeg = split * kc;
+  const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
+  float* Cs = C + split * strideC;
+  const int nk = (int)((kend - kbeg) / BK);  // the launcher guarantees BK | kc, BK | K
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16v acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % NSTAGE) * STAGE;
+    stage(A, lda, m0, M, kbeg + (int64_t)kt * BK, st, wave, lane);
+    stage(B, ldb, n0, N, kbeg + (int64_t)kt * BK, st + IMG, wave, lane);
+  };
+  // prologue: tiles 0, 1, 2 in flight
+#pragma unroll
+  for (int q = 0; q < NSTAGE - 1; ++q)
+    if (q < nk) issue(q);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    // tile kt must have landed; tiles kt+1, kt+2 (if issued) may stay in flight
+    const int ahead = nk - 1 - kt;
+    if (ahead >= 2) wait_vm<2>();
+    else if (ahead == 1) wait_vm<1>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // all waves' DMAs for tile kt visible; stage kt-1 free
+    asm volatile("" ::: "memory");
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1);  // into the stage of tile kt-1
+    const unsigned char* sa = smem + (kt % NSTAGE) * STAGE;
+    const unsigned char* sb = sa + IMG;
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8v a[4], b[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = frag(sb, wn + j * 32 + li, 2 * ks + lh);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = frag(sa, wm + i * 32 + li, 2 * ks + lh);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  // epilogue: D[row=(r&3)+8*(r>>2)+4*lh][col=li] of each 32x32 tile
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t n = n0 + wn + j * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (n < bias.nsplit) {
+      if (bias.a1) bv += bias.a1[n];
+      if (bias.a2) bv += bias.a2[n];
+    } else {
+      if (bias.b1) bv += bias.b1[n - bias.nsplit];
+      if (bias.b2) bv += bias.b2[n - bias.nsplit];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cs[m * ldc + n] = acc[i][j][r] + bv;
+      }
+  }
+}
+}  // namespace g256
+
 }  // namespace ainp
 
 using namespace ainp;
@@ -205,6 +360,24 @@ extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t*
   if (nsplit == 1) kc = K;
   if (M == 0 || N == 0) return AINP_OK;
   g16::Bias b{bias_a1, bias_a2, bias_b1, bias_b2, bias_nsplit};
+  // large GEMMs on the 256 x 256 LDS-DMA kernel (bit-identical: same MFMA, same
+  // k order); ops._splitk_bf16 mirrors this rule for its split choice
+  static const bool use256 = [] {  // AINP_GEMM16_256=0 keeps every GEMM on g16 (A/B runs)
+    const char* e = getenv("AINP_GEMM16_256");
+    return !(e && e[0] == '0');
+  }();
+  if (use256 && M >= 512 && N >= 512 && K % g256::BK == 0 && kc % g256::BK == 0) {
+    static const bool lds_ok =
+        hipFuncSetAttribute((const void*)g256::gemm_bf16nt_256_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
+                            g256::LDS_BYTES) == hipSuccess;
+    if (!lds_ok) return record_msg("ainp_gemm_bf16nt: cannot reserve 128 KB of LDS");
+    const int64_t tn = cdiv(N, g256::BN);
+    const dim3 grid((unsigned)(cdiv(M, g256::BM) * tn), (unsigned)nsplit);
+    hipLaunchKernelGGL(g256::gemm_bf16nt_256_kernel, grid, dim3(g256::THREADS), g256::LDS_BYTES,
+                       as_stream(stream), M, N, K, A, lda, B, ldb, C, ldc, kc, strideC, b, (int)tn);
+    return check_launch("gemm_bf16nt_256");
+  }
   const int64_t tiles_n = cdiv(N, g16::BN);
   const dim3 grid((unsigned)(cdiv(M, g16::BM) * tiles_n), (unsigned)nsplit);
   hipLaunchKernelGGL(g16::gemm_bf16nt_kernel, grid, dim3(g16::THREADS), 0, as_stream(stream), M, N,
