@@ -268,21 +268,11 @@ _B16_TILE_RATE = 700e12 / 768
 _SLAB_RATE = 4e12
 
 
-# the 256 x 256 LDS-DMA kernel (one workgroup per CU) takes GEMMs with
-# M, N >= 512 and K, kc multiples of 32 (gemm16.hip ainp_gemm_bf16nt)
-_B16_TILE256_RATE = 800e12 / 256
-_GEMM16_256 = os.environ.get("AINP_GEMM16_256", "1") != "0"
-
-
 @functools.lru_cache(maxsize=256)
 def _splitk_bf16(M, N, K, slots=768, max_split=16):
     """Split count S for a bf16 GEMM over a small M x N: minimise the wave-quantised
     MFMA time ceil(tiles*S/slots) * tile_time(K/S) plus the slab round trip."""
-    big = M >= 512 and N >= 512 and K % 32 == 0 and _GEMM16_256
-    tile, rate = (256, _B16_TILE256_RATE) if big else (128, _B16_TILE_RATE)
-    if big:
-        slots = 256
-    tiles = -(-M // tile) * -(-N // tile)
+    tiles = -(-M // 128) * -(-N // 128)
     best, best_t = 1, None
     for S in range(1, max_split + 1):
         kc = -(-K // S // 64) * 64
@@ -291,7 +281,7 @@ def _splitk_bf16(M, N, K, slots=768, max_split=16):
         Sr = -(-K // kc)
         if Sr != S:
             continue
-        t = -(-tiles * S // slots) * 2.0 * tile * tile * kc / rate
+        t = -(-tiles * S // slots) * 2.0 * 128 * 128 * kc / _B16_TILE_RATE
         if S > 1:
             t += 2.0 * S * M * N * 4 / _SLAB_RATE
         if best_t is None or t < best_t:

@@ -17,9 +17,9 @@
 // prefetched in registers (4 x 16 B per operand per thread); <= 168 VGPRs so
 // three workgroups fit per CU.  XCD-aware block order as gemm.hip.  Split-K:
 // blockIdx.y = split s covers k in [s*kc, min(K, (s+1)*kc)) and writes slab
-// C + s*strideC (summed by ainp_sum_slabs in fixed order).  GEMMs with M and
-// N >= 512 run on g256 below instead (256 x 256 tiles, LDS-DMA ring):
-// 596-651 -> 722-890 TF at the layer-0 shapes (tools/gemm256_lab.hip).
+// C + s*strideC (summed by ainp_sum_slabs in fixed order).  Unsplit GEMMs
+// with M, N >= 512 and at most 1536 tiles of 128 x 128 run on g256 below
+// instead (256 x 256 tiles, LDS-DMA ring; routing rule at the launcher).
 #include "common.h"
 
 #include <stdlib.h>
@@ -366,7 +366,16 @@ extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t*
     const char* e = getenv("AINP_GEMM16_256");
     return !(e && e[0] == '0');
   }();
-  if (use256 && M >= 512 && N >= 512 && K % g256::BK == 0 && kc % g256::BK == 0) {
+  // Routing: the 256 x 256 tile (one workgroup per CU, 128 KB of LDS) only
+  // for unsplit GEMMs whose 128 x 128 grid is at most two rounds of its 768
+  // resident slots -- the layer-0 projection (672 tiles): 522 -> 482 us inside
+  // the step.  Measured inside the step it loses where another GEMM runs beside
+  // it on the side stream: the data gradient (10836 tiles) 706 -> 891 us, the
+  // split-K weight gradient 621 -> 1325 us (it cannot co-reside with the
+  // 3-workgroups-per-CU kernel next to it).
+  const int64_t tiles128 = cdiv(M, g16::BM) * cdiv(N, g16::BN);
+  if (use256 && nsplit == 1 && M >= 512 && N >= 512 && tiles128 <= 1536 &&
+      K % g256::BK == 0) {
     static const bool lds_ok =
         hipFuncSetAttribute((const void*)g256::gemm_bf16nt_256_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize,
