@@ -367,6 +367,12 @@ def main():
             W16 = torch.cat([lw.weight_ih_l0, lw.weight_ih_l0_reverse]).detach().to(torch.bfloat16)
             bias = (lw.bias_ih_l0, lw.bias_hh_l0, lw.bias_ih_l0_reverse, lw.bias_hh_l0_reverse)
             gfn = lambda: ops.gemm_bf16nt(X16, W16, out=zx, bias=bias, bias_nsplit=4 * H)  # noqa: E731
+        elif not ops.GEMM_EXACT and ops.x6_256_eligible(M, 8 * H, I, 4 * H):
+            # the path the step takes (cnnblstm._BLSTMFn): 256x256 LDS-DMA tile, split 3
+            A = torch.randn(M, I, device=dev)
+            bias = (lw.bias_ih_l0, lw.bias_hh_l0, lw.bias_ih_l0_reverse, lw.bias_hh_l0_reverse)
+            gfn = lambda: ops.gemm_x6nt_256(A, lw.weight_ih_l0, lw.weight_ih_l0_reverse,  # noqa: E731
+                                            zx, bias=bias, bias_nsplit=4 * H)
         else:
             A = torch.randn(M, I, device=dev)
             args_g = (M, 4 * H, I, [A, A], I, 1, [lw.weight_ih_l0, lw.weight_ih_l0_reverse], 1,
@@ -382,6 +388,9 @@ def main():
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "traffic": traffic, "kernel": ("g256::gemm_bf16nt_256_kernel" if bf16 else
+                                               "x6_256::gemm_x6nt_256_kernel, split 3 + slab sum"
+                                               if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
+                                               and not ops.GEMM_EXACT else
                                                "gemm_f32_kernel<1,...>") + f" (LSTM l0 "
                 f"input projection, M={M} N={8 * H} K={I}, both directions)",
                 "avg_launch_ms": round(avg_s * 1e3, 4), "flop_per_launch": flops}
@@ -394,7 +403,10 @@ def main():
             # product; its own instruction-stream ceiling is the dense bf16 peak / 6
             roof.update({
                 "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross "
-                             "products on v_mfma_f32_32x32x16_bf16, f32 accumulate",
+                             "products on v_mfma_f32_32x32x16_bf16, f32 accumulate"
+                             + ("; 256x256x16 tiles staged by global_load_lds, split at "
+                                "fragment-read time" if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
+                                else ""),
                 "executed_tflops": round(6 * achieved, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
                 "executed_frac": round(6 * achieved / BF16_MFMA_PEAK_TFLOPS, 4)})
 

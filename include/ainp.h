@@ -180,6 +180,24 @@ int ainp_gemm_f32_ex(int64_t M, int64_t N, int64_t K, float alpha,
                      int nptr, int64_t nstrided, int ksplit, int flags, void* workspace,
                      size_t ws_bytes, void* stream);
 
+/* fp32 layer-0 LSTM input projection (models/CNNBLSTM/model.py:46-47,77,
+ * nn.LSTM's x W_ih^T + b_ih + b_hh for both directions in one launch) on the
+ * 256x256 LDS-DMA tile: C[m][n] = sum_k A[m][k] B[n][k] + bias(n), A [M][lda]
+ * fp32 k-contiguous, B rows n < bsplit from B1 [bsplit][ldb], the rest from
+ * B2 [N - bsplit][ldb] (the two directions' W_ih), 16-byte aligned rows
+ * (lda, ldb % 4 == 0), K % 16 == 0, bsplit % 256 == 0; bias as
+ * ainp_gemm_bf16nt.  Arithmetic and summation order are those of
+ * ainp_gemm_f32's default main loop (the exact three-piece bf16 split, six
+ * cross products per 16-k step), so with nsplit == 1 C is bit-identical to
+ * it.  nsplit > 1: split-K, split s sums k in [s*kc, min(K, (s+1)*kc))
+ * (kc % 16 == 0) into slab C + s*strideC, the bias into slab 0 only (combine
+ * with ainp_sum_slabs). */
+int ainp_gemm_x6nt_256(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                       const float* B1, const float* B2, int64_t ldb, int64_t bsplit,
+                       float* C, int64_t ldc, const float* bias_a1, const float* bias_a2,
+                       const float* bias_b1, const float* bias_b2, int64_t bias_nsplit,
+                       int nsplit, int64_t kc, int64_t strideC, void* stream);
+
 /* bf16-operand GEMM (the bf16 configuration's layer-0 LSTM GEMMs,
  * models/CNNBLSTM/model.py:46-47,77: input projection, data and weight
  * gradients): C[m][n] (+ split s * strideC) = sum_k A[m][k] B[n][k] + bias(n),

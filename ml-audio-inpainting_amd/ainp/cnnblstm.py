@@ -233,6 +233,11 @@ class _BLSTMFn(torch.autograd.Function):
                 ops.gemm_bf16nt(X16.view(NT, I), W16, out=zx.view(NT, 8 * H),
                                 bias=(bif, bhf, bir, bhr), bias_nsplit=4 * H)
                 ctx.l016 = (XT16, WT16)
+            elif (l == 0 and not bf16 and not ops.GEMM_EXACT
+                  and ops.x6_256_eligible(NT, 8 * H, Il, 4 * H)):
+                # fp32 layer-0 projection (360 GFLOP at C2) on the 256 x 256 tile
+                ops.gemm_x6nt_256(inp, wf, wr, zx.view(NT, 8 * H), bias=(bif, bhf, bir, bhr),
+                                  bias_nsplit=4 * H)
             else:
                 ops.gemm(NT, 4 * H, Il, [inp, inp], Il, 1, [wf, wr], 1, Il,
                          [zx, zx[:, :, 4 * H:]], 8 * H, 1, bias1=[bif, bir], bias2=[bhf, bhr],

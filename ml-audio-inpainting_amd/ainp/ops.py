@@ -262,6 +262,33 @@ def gemm_bf16nt(A, B, K=None, out=None, bias=(None, None, None, None), bias_nspl
     return out
 
 
+# fp32 layer-0 projection on the 256 x 256 LDS-DMA tile (ainp_gemm_x6nt_256):
+# split 3 fills the 256 CUs with the 168 tiles of M = 10688, N = 1024
+# (2.28 -> 2.09 ms, tools/x6_256_lab.cpp); AINP_X6_256=0 keeps ainp_gemm_f32.
+X6_256 = os.environ.get("AINP_X6_256", "1") != "0"
+_X6_SPLIT = 3
+
+
+def x6_256_eligible(M, N, K, bsplit):
+    return X6_256 and M >= 2048 and K % 16 == 0 and bsplit % 256 == 0 and N >= 512
+
+
+def gemm_x6nt_256(A, B1, B2, out, bias=(None, None, None, None), bias_nsplit=0, nsplit=None):
+    """out [M, N1+N2] = A [M, K] . [B1; B2]^T + bias, fp32 on the three-piece
+    bf16 split (ainp_gemm_x6nt_256); split-K slabs summed in fixed order."""
+    M, K = A.shape
+    N = B1.shape[0] + B2.shape[0]
+    S = _X6_SPLIT if nsplit is None else int(nsplit)
+    if S == 1:
+        _T.gemm_x6nt_256(A, B1, B2, out, *bias, int(bias_nsplit), 1, K)
+        return out
+    kc = -(-K // S // 16) * 16
+    slabs = torch.empty(S, M, N, device=A.device, dtype=torch.float32)
+    _T.gemm_x6nt_256(A, B1, B2, slabs, *bias, int(bias_nsplit), S, kc)
+    sum_slabs(slabs, S, out=out.view(-1))
+    return out
+
+
 # bf16 MFMA rate per resident workgroup slot and the HBM rate, for the split-K
 # choice below (measured orders of magnitude, not limits)
 _B16_TILE_RATE = 700e12 / 768

@@ -341,6 +341,178 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
 }
 }  // namespace g256
 
+// ---------------------------------------------------------------------------
+// fp32-accurate ("x6") layer-0 projection on the same 256 x 256 LDS-DMA ring:
+// C[m][n] = sum_k A[m][k] B[n][k] + bias, A and B fp32 and k-contiguous, B
+// given as two halves (the two LSTM directions' W_ih: rows n < bsplit from B1,
+// the rest from B2).  K-tile 16 fp32 = the same 64-byte image rows as the
+// bf16 kernel; each lane reads its fragment's 8 fp32 (two ds_read_b128) and
+// splits them exactly into three bf16 pieces (x = x0 + x1 + x2, gemm.hip x6),
+// then accumulates the six cross products a2b0 + a1b1 + a0b2 + a1b0 + a0b1 +
+// a0b0 per 16-k step -- the same split, products and order as gemm.hip's x6
+// main loop, so the result is bit-identical to it.  The split is repeated by
+// the waves sharing a fragment (4 for A, 2 for B); the VALU work hides under
+// the 48 MFMAs per wave per K-tile.
+namespace x6_256 {
+using g256::BM;
+using g256::BN;
+using g256::NSTAGE;
+using g256::THREADS;
+constexpr int BK = 16;                   // fp32 k per tile: 64-byte rows
+constexpr int ROWB = BK * 4;
+constexpr int IMG = BM * ROWB;
+constexpr int STAGE = 2 * IMG;
+constexpr int LDS_BYTES = NSTAGE * STAGE;
+static_assert(ROWB == g256::ROWB && LDS_BYTES == g256::LDS_BYTES, "same image geometry");
+using g16::bf16x8v;
+using g16::f32x16v;
+using g16::Bias;
+
+__device__ __forceinline__ void stage(const float* __restrict__ P, int64_t ld, int64_t r0,
+                                      int64_t R, int64_t k0, unsigned char* img, int wave,
+                                      int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = 2 * wave + i;
+    const int row = 16 * blk + (lane >> 2);
+    const int c = g256::swz(row, lane & 3);
+    int64_t gr = r0 + row;
+    gr = gr < R ? gr : R - 1;
+    const float* src = P + gr * ld + k0 + 4 * c;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)src, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ uint32_t cvt_pk(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
+// the fragment (row, k = 8h .. 8h+7) as three bf16x8 pieces
+__device__ __forceinline__ void frag3(const unsigned char* img, int row, int h, bf16x8v& p0,
+                                      bf16x8v& p1, bf16x8v& p2) {
+  const float4 u = *reinterpret_cast<const float4*>(img + row * ROWB + 16 * g256::swz(row, 2 * h));
+  const float4 v = *reinterpret_cast<const float4*>(img + row * ROWB + 16 * g256::swz(row, 2 * h + 1));
+  const float x[8] = {u.x, u.y, u.z, u.w, v.x, v.y, v.z, v.w};
+  uint32_t q0[4], q1[4], q2[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float a = x[2 * e], b = x[2 * e + 1];
+    q0[e] = cvt_pk(a, b);
+    const float ra = a - __uint_as_float(q0[e] << 16), rb = b - __uint_as_float(q0[e] & 0xffff0000u);
+    q1[e] = cvt_pk(ra, rb);
+    const float sa = ra - __uint_as_float(q1[e] << 16), sb = rb - __uint_as_float(q1[e] & 0xffff0000u);
+    q2[e] = cvt_pk(sa, sb);
+  }
+  p0 = __builtin_bit_cast(bf16x8v, make_uint4(q0[0], q0[1], q0[2], q0[3]));
+  p1 = __builtin_bit_cast(bf16x8v, make_uint4(q1[0], q1[1], q1[2], q1[3]));
+  p2 = __builtin_bit_cast(bf16x8v, make_uint4(q2[0], q2[1], q2[2], q2[3]));
+}
+
+__global__ __launch_bounds__(THREADS, 1) void gemm_x6nt_256_kernel(
+    int64_t M, int64_t N, int64_t K, const float* __restrict__ A, int64_t lda,
+    const float* __restrict__ B1, const float* __restrict__ B2, int64_t ldb, int64_t bsplit,
+    float* __restrict__ C, int64_t ldc, int64_t kc, int64_t strideC, Bias bias, int tiles_n) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t first_n = (bid / per_group) * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+  // this n-tile's B half (the launcher guarantees bsplit % 256 == 0)
+  const bool hi = n0 >= bsplit;
+  const float* Bp = hi ? B2 : B1;
+  const int64_t nb0 = hi ? n0 - bsplit : n0, NB = hi ? N - bsplit : bsplit;
+  // split-K: blockIdx.y = split s sums k in [s*kc, min(K, (s+1)*kc)) into
+  // slab C + s*strideC; the bias goes into slab 0 only
+  const int64_t split = blockIdx.y;
+  const int64_t kbeg = split * kc;
+  const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
+  float* Cs = C + split * strideC;
+  const int nk = (int)((kend - kbeg) / BK);  // the launcher guarantees BK | K, BK | kc
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16v acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % NSTAGE) * STAGE;
+    stage(A, lda, m0, M, kbeg + (int64_t)kt * BK, st, wave, lane);
+    stage(Bp, ldb, nb0, NB, kbeg + (int64_t)kt * BK, st + IMG, wave, lane);
+  };
+#pragma unroll
+  for (int q = 0; q < NSTAGE - 1; ++q)
+    if (q < nk) issue(q);
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int ahead = nk - 1 - kt;
+    if (ahead >= 2) g256::wait_vm<2>();
+    else if (ahead == 1) g256::wait_vm<1>();
+    else g256::wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NSTAGE - 1 < nk) issue(kt + NSTAGE - 1);
+    const unsigned char* sa = smem + (kt % NSTAGE) * STAGE;
+    const unsigned char* sb = sa + IMG;
+    bf16x8v b0[2], b1[2], b2[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) frag3(sb, wn + j * 32 + li, lh, b0[j], b1[j], b2[j]);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      bf16x8v a0, a1, a2;
+      frag3(sa, wm + i * 32 + li, lh, a0, a1, a2);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        f32x16v c = acc[i][j];
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0[j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1[j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2[j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0[j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1[j], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0[j], c, 0, 0, 0);
+        acc[i][j] = c;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t n = n0 + wn + j * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (split == 0) {
+      if (n < bias.nsplit) {
+        if (bias.a1) bv += bias.a1[n];
+        if (bias.a2) bv += bias.a2[n];
+      } else {
+        if (bias.b1) bv += bias.b1[n - bias.nsplit];
+        if (bias.b2) bv += bias.b2[n - bias.nsplit];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cs[m * ldc + n] = acc[i][j][r] + bv;
+      }
+  }
+}
+}  // namespace x6_256
+
 }  // namespace ainp
 
 using namespace ainp;
@@ -392,6 +564,38 @@ extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t*
   hipLaunchKernelGGL(g16::gemm_bf16nt_kernel, grid, dim3(g16::THREADS), 0, as_stream(stream), M, N,
                      K, A, lda, B, ldb, C, ldc, kc, strideC, b, (int)tiles_n);
   return check_launch("gemm_bf16nt");
+}
+
+extern "C" int ainp_gemm_x6nt_256(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                  const float* B1, const float* B2, int64_t ldb, int64_t bsplit,
+                                  float* C, int64_t ldc, const float* bias_a1,
+                                  const float* bias_a2, const float* bias_b1,
+                                  const float* bias_b2, int64_t bias_nsplit, int nsplit,
+                                  int64_t kc, int64_t strideC, void* stream) {
+  if (nsplit < 1 || nsplit > 65535 ||
+      (nsplit > 1 && (kc < x6_256::BK || kc % x6_256::BK || (int64_t)nsplit * kc < K ||
+                      (int64_t)(nsplit - 1) * kc >= K || strideC < M * ldc)))
+    return record_msg("ainp_gemm_x6nt_256: split-K needs kc % 16 == 0 covering K, strideC >= M*ldc");
+  if (nsplit == 1) kc = K;
+  if (M < 0 || N < 0 || K < 0 || !A || !B1 || !C || lda % 4 || ldb % 4 || lda < K || ldb < K ||
+      ldc < N || K % x6_256::BK || ((uintptr_t)A & 15) || ((uintptr_t)B1 & 15) ||
+      bsplit < 0 || bsplit > N || bsplit % x6_256::BN ||
+      (bsplit < N && (!B2 || ((uintptr_t)B2 & 15))))
+    return record_msg("ainp_gemm_x6nt_256: bad argument (16-byte aligned k-contiguous rows, "
+                      "K % 16 == 0, bsplit % 256 == 0)");
+  if (M == 0 || N == 0) return AINP_OK;
+  static const bool lds_ok =
+      hipFuncSetAttribute((const void*)x6_256::gemm_x6nt_256_kernel,
+                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                          x6_256::LDS_BYTES) == hipSuccess;
+  if (!lds_ok) return record_msg("ainp_gemm_x6nt_256: cannot reserve 128 KB of LDS");
+  g16::Bias b{bias_a1, bias_a2, bias_b1, bias_b2, bias_nsplit};
+  const int64_t tn = cdiv(N, x6_256::BN);
+  hipLaunchKernelGGL(x6_256::gemm_x6nt_256_kernel,
+                     dim3((unsigned)(cdiv(M, x6_256::BM) * tn), (unsigned)nsplit),
+                     dim3(x6_256::THREADS), x6_256::LDS_BYTES, as_stream(stream), M, N, K, A, lda,
+                     B1, B2, ldb, bsplit, C, ldc, kc, strideC, b, (int)tn);
+  return check_launch("gemm_x6nt_256");
 }
 
 extern "C" int ainp_cast_bf16_t(const float* x, int64_t R, int64_t C, int64_t ld_in,

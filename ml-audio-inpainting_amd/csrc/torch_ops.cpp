@@ -809,6 +809,30 @@ void gemm_bf16nt(const Tensor& A, const Tensor& B, const Tensor& C, int64_t K,
       "gemm_bf16nt");
 }
 
+void gemm_x6nt_256(const Tensor& A, const Tensor& B1, const Tensor& B2, const Tensor& C,
+                   const OptT& bias_a1, const OptT& bias_a2, const OptT& bias_b1,
+                   const OptT& bias_b2, int64_t bias_nsplit, int64_t nsplit, int64_t kc) {
+  GUARD(C);
+  TORCH_CHECK(A.dim() == 2 && B1.dim() == 2 && B2.dim() == 2 && A.stride(1) == 1 &&
+                  B1.stride(1) == 1 && B2.stride(1) == 1 && B1.stride(0) == B2.stride(0),
+              "gemm_x6nt_256: A [M, K], B1 [N1, K], B2 [N2, K] with unit-stride rows");
+  const int64_t M = A.size(0), K = A.size(1), N1 = B1.size(0), N = N1 + B2.size(0);
+  TORCH_CHECK(B1.size(1) == K && B2.size(1) == K, "gemm_x6nt_256: operand K mismatch");
+  TORCH_CHECK((C.dim() == 2 && nsplit == 1) || (C.dim() == 3 && C.size(0) == nsplit),
+              "gemm_x6nt_256: C [M, N] or split-K slabs [nsplit, M, N]");
+  TORCH_CHECK(C.size(-2) == M && C.size(-1) == N && C.stride(-1) == 1, "gemm_x6nt_256: C shape");
+  same_device(A, C);
+  same_device(B1, C);
+  same_device(B2, C);
+  chk(ainp_gemm_x6nt_256(M, N, K, dev(A, "A", at::kFloat, false), A.stride(0),
+                         dev(B1, "B1", at::kFloat, false), dev(B2, "B2", at::kFloat, false),
+                         B1.stride(0), N1, dev(C, "C", at::kFloat, false), C.stride(-2),
+                         opt(bias_a1, "bias_a1"), opt(bias_a2, "bias_a2"), opt(bias_b1, "bias_b1"),
+                         opt(bias_b2, "bias_b2"), bias_nsplit, (int)nsplit, kc,
+                         C.dim() == 3 ? C.stride(0) : 0, stream_of(C)),
+      "gemm_x6nt_256");
+}
+
 void cast_bf16_t(const Tensor& x, const OptT& out, const OptT& outT) {
   GUARD(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D with unit-stride rows");
@@ -1066,6 +1090,9 @@ TORCH_LIBRARY(ainp, m) {
   m.def("gemm_bf16nt(Tensor A, Tensor B, Tensor(a!) C, int K, Tensor? bias_a1, Tensor? bias_a2, "
         "Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, int kc) -> ()");
   m.def("cast_bf16_t(Tensor x, Tensor(a!)? out, Tensor(b!)? outT) -> ()");
+  m.def("gemm_x6nt_256(Tensor A, Tensor B1, Tensor B2, Tensor(a!) C, Tensor? bias_a1, "
+        "Tensor? bias_a2, Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, "
+        "int kc) -> ()");
   m.def("nchw_to_nhwc16(Tensor x, Tensor? m, Tensor(a!) out) -> ()");
   m.def("conv_weight_nhwc16(Tensor w, int C0, int C1, Tensor(a!) wt16) -> ()");
   m.def("conv_gen_fwd_nhwc16(Tensor x0, Tensor? x1, Tensor wt16, int Cout, int KH, int KW, "
@@ -1130,6 +1157,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("bn_relu_apply_ntcf_bf16", &bn_relu_apply_ntcf_bf16);
   m.impl("gemm_bf16nt", &gemm_bf16nt);
   m.impl("cast_bf16_t", &cast_bf16_t);
+  m.impl("gemm_x6nt_256", &gemm_x6nt_256);
   m.impl("nchw_to_nhwc16", &nchw_to_nhwc16);
   m.impl("conv_weight_nhwc16", &conv_weight_nhwc16);
   m.impl("conv_gen_fwd_nhwc16", &conv_gen_fwd_nhwc16);
@@ -1191,6 +1219,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("bn_relu_apply_ntcf_bf16", torch::CppFunction::makeFallthrough());
   m.impl("gemm_bf16nt", torch::CppFunction::makeFallthrough());
   m.impl("cast_bf16_t", torch::CppFunction::makeFallthrough());
+  m.impl("gemm_x6nt_256", torch::CppFunction::makeFallthrough());
   m.impl("nchw_to_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("conv_weight_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("conv_gen_fwd_nhwc16", torch::CppFunction::makeFallthrough());

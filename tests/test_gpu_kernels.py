@@ -249,6 +249,37 @@ def test_gemm_x6_is_fp32_accurate(ops):
     assert errs[False] < 2 * errs[True] + 1e-7, errs
 
 
+@pytest.mark.parametrize("M,K,H", [(2304, 1024, 128), (700, 160, 64), (10688, 16448, 128)])
+def test_gemm_x6nt_256_matches_x6_path(ops, M, K, H):
+    """The fp32 layer-0 projection on the 256x256 LDS-DMA tile
+    (ainp_gemm_x6nt_256): unsplit it is bit-identical to ainp_gemm_f32's
+    default x6 loop (same split, products and order); split 3 (what the model
+    uses) is an fp32 GEMM against fp64 (models/CNNBLSTM/model.py:46-47,77:
+    x W_ih^T + b_ih + b_hh for both directions).  Row tails (M % 256) and the
+    C2 shape included."""
+    g = torch.Generator().manual_seed(11)
+    A = torch.relu(torch.randn(M, K, generator=g)).to(DEV)
+    wf = (torch.randn(4 * H, K, generator=g) * 0.02).to(DEV)
+    wr = (torch.randn(4 * H, K, generator=g) * 0.02).to(DEV)
+    b = [(torch.randn(4 * H, generator=g) * 0.1).to(DEV) for _ in range(4)]
+    ref = torch.empty(M, 8 * H, device=DEV)
+    ops.gemm(M, 4 * H, K, [A, A], K, 1, [wf, wr], 1, K, [ref, ref[:, 4 * H:]], 8 * H, 1,
+             bias1=[b[0], b[2]], bias2=[b[1], b[3]], exact=False)
+    y1 = torch.full((M, 8 * H), float("nan"), device=DEV)
+    ops.gemm_x6nt_256(A, wf, wr, y1, bias=(b[0], b[1], b[2], b[3]), bias_nsplit=4 * H, nsplit=1)
+    assert torch.equal(y1, ref)
+    y3 = torch.empty(M, 8 * H, device=DEV)
+    ops.gemm_x6nt_256(A, wf, wr, y3, bias=(b[0], b[1], b[2], b[3]), bias_nsplit=4 * H, nsplit=3)
+    W = torch.cat([wf, wr]).double().cpu()
+    bias = torch.cat([b[0] + b[1], b[2] + b[3]]).double().cpu()
+    r64 = A.double().cpu() @ W.T + bias
+    # an fp32 GEMM over K terms (~u*sqrt(K) relative): the split changes only
+    # the summation order, so its error stays at the unsplit loop's level
+    e3, e1 = rel(y3.cpu(), r64), rel(ref.cpu(), r64)
+    assert e3 < 1e-5 and e1 < 1e-5, (e3, e1)
+    assert e3 < 2 * e1 + 1e-7, (e3, e1)
+
+
 def _bf(t):
     """fp64 copy of t rounded to fp32, then to bf16 (nearest-even)."""
     return t.float().bfloat16().double()

@@ -28,7 +28,11 @@ if [ "$DT" = bf16 ]; then
   python3 tools/traffic_json.py "$OUT" gemm_bf16nt $(( 2 * (10688*16448 + 1024*16448) + 4 * 10688*1024 )) \
     "tools/pmc_gemm.sh bf16 over tools/roofline_probe.py" > "$OUT/traffic.json" && cat "$OUT/traffic.json"
 else
-  python3 tools/traffic_json.py "$OUT" > "$OUT/traffic.json" && cat "$OUT/traffic.json"
+  # the 256x256 x6 tile, split 3: X [10688][16448] + W_ih (both) [1024][16448]
+  # fp32 read once, three fp32 slabs [10688][1024] written (the slab sum is a
+  # separate launch)
+  python3 tools/traffic_json.py "$OUT" gemm_x6nt_256 $(( 4 * (10688*16448 + 1024*16448) + 3 * 4 * 10688*1024 )) \
+    "tools/pmc_gemm.sh fp32 over tools/roofline_probe.py" > "$OUT/traffic.json" && cat "$OUT/traffic.json"
 fi
 python3 tools/pmc_table.py "$OUT"/sq/run_counter_collection.csv gemm > "$OUT/sq_table.txt"
 cat "$OUT/sq_table.txt"
