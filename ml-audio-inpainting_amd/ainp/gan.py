@@ -259,7 +259,7 @@ class PConvUNet(nn.Module):
                           "SURVEY Q1): its output carries no gradient to G's parameters",
                           stacklevel=2)
             PConvUNet._warned_no_grad = True
-        with torch.no_grad():
+        with torch.no_grad(), ops.nhwc16_memo():
             return self._forward(x, mask)
 
     _warned_no_grad = False

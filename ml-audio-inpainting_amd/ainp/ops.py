@@ -642,11 +642,43 @@ def conv_weight_nhwc16(w, C0, C1):
     return wt
 
 
+_NHWC_MEMO = None   # dict while an nhwc16_memo scope is active
+
+
+class nhwc16_memo:
+    """Scope in which to_nhwc16 reuses its result for an unchanged (x, mask)
+    pair: PConvUNet converts each encoder output once for the next encoder
+    conv and finds it again as the decoder's skip source.  The memo holds the
+    sources, so their storage cannot be reused inside the scope; an in-place
+    update bumps the tensor version and misses."""
+
+    def __enter__(self):
+        global _NHWC_MEMO
+        self._prev = _NHWC_MEMO
+        _NHWC_MEMO = {}
+        return self
+
+    def __exit__(self, *exc):
+        global _NHWC_MEMO
+        _NHWC_MEMO = self._prev
+        return False
+
+
 def to_nhwc16(x, m=None):
     """x [N,C,H,W] fp32 (x mask plane m) -> bf16 [N,H,W,C] (ainp_nchw_to_nhwc16)."""
+    memo = _NHWC_MEMO
+    key = None
+    if memo is not None:
+        key = (x.data_ptr(), tuple(x.shape), x._version,
+               m.data_ptr() if m is not None else 0, m._version if m is not None else -1)
+        hit = memo.get(key)
+        if hit is not None:
+            return hit[0]
     N, C, H, W = x.shape
     out = torch.empty(N, H, W, C, device=x.device, dtype=torch.bfloat16)
     _T.nchw_to_nhwc16(x, m, out)
+    if memo is not None:
+        memo[key] = (out, x, m)
     return out
 
 

@@ -609,11 +609,14 @@ def _tobf16(x):
 
 
 @pytest.mark.parametrize("M,N,K,S", [(300, 200, 520, 1), (128, 256, 1024, 1), (257, 130, 4096, 3),
-                                     (1000, 77, 5376, 2)])
+                                     (1000, 77, 5376, 2), (1000, 1024, 2080, 1),
+                                     (777, 600, 1056, 1)])
 def test_gemm_bf16nt_matches_fp64_of_bf16_operands(M, N, K, S):
     """ainp_gemm_bf16nt vs fp64 products of the same bf16 operands: bf16 x bf16
     products are exact in fp32, so only the fp32 accumulation differs (<= 1e-5
-    relative); ragged M / N tiles, K % 64 != 0, split-K slabs, bias segments."""
+    relative); ragged M / N tiles, K % 64 != 0, split-K slabs, bias segments.
+    The last two shapes are routed to the 256x256 LDS-DMA tile (g256: unsplit,
+    M, N >= 512), ragged in M and N with ld > K."""
     from ainp import ops
     g = torch.Generator().manual_seed(M + N + K)
     A = _tobf16(torch.randn(M, K, generator=g)).cuda()
