@@ -505,6 +505,13 @@ int ainp_gan_pad_input(const float* x, const float* m, int64_t N, int H, int W,
  * Encoder/DecoderBlocks (networks.py:149-151, 165-167). */
 int ainp_affine_act(float* y, const float* scale, const float* shift, int64_t N, int C,
                     int64_t HW, int act, float slope, void* stream);
+/* ainp_affine_act on y [N][C][H][W] and, in the same pass, the bf16
+ * configurations' channel-last copy of the result times the mask plane
+ * m [N][H][W] (may be NULL): out [N][H][W][C] bf16, exactly what
+ * ainp_nchw_to_nhwc16(y, m) gives afterwards (the next PartialConv2d's source). */
+int ainp_affine_act_nhwc16(float* y, const float* scale, const float* shift, int64_t N, int C,
+                           int H, int W, int act, float slope, const float* m, uint16_t* out,
+                           void* stream);
 /* nn.MaxPool2d(2, 2) of VGG19.features (loss.py:21). */
 int ainp_maxpool2(const float* x, float* y, int64_t NC, int H, int W, void* stream);
 /* VGGLoss._prepare_input_for_vgg + weights.transforms() (loss.py:65-86,104-106):

@@ -160,6 +160,17 @@ class EncoderBlock(nn.Module):
 
     def run(self, srcs, Hin, Win):
         y, newm, stats = self.pconv.run(srcs, Hin, Win, want_stats=self._want_stats())
+        if (self.pconv.ainp_bf16 and ops._NHWC_MEMO is not None and ops.CONV_NHWC16
+                and y.shape[1] % 32 == 0):
+            # bf16 U-Net: the next conv's channel-last source in the same pass
+            N, C, Ho, Wo = y.shape
+            if isinstance(self.norm, nn.BatchNorm2d):
+                sc, sh = _bn_affine(self.norm, stats, N * Ho * Wo, C)
+            else:
+                sc = torch.ones(C, device=y.device)
+                sh = torch.zeros(C, device=y.device)
+            ops.affine_act_nhwc16_(y, sc, sh, ops.ACT_LEAKY, SLOPE, newm)
+            return y, newm
         return self._finish(y, stats), newm
 
     def forward(self, x, mask):

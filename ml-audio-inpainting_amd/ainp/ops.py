@@ -794,6 +794,22 @@ def affine_act_(y, scale, shift, act, slope=0.2):
     return y
 
 
+def affine_act_nhwc16_(y, scale, shift, act, slope=0.2, m=None):
+    """affine_act_ in place and, in the same pass, the bf16 channel-last copy of
+    the result times the mask plane m (ainp_affine_act_nhwc16); inside an
+    nhwc16_memo scope the copy is what to_nhwc16(y, m) returns afterwards."""
+    _req(y, "y")
+    N, C, H, W = y.shape
+    out = torch.empty(N, H, W, C, device=y.device, dtype=torch.bfloat16)
+    _T.affine_act_nhwc16(y, scale, shift, int(act), float(slope), m, out)
+    memo = _NHWC_MEMO
+    if memo is not None:
+        key = (y.data_ptr(), tuple(y.shape), y._version,
+               m.data_ptr() if m is not None else 0, m._version if m is not None else -1)
+        memo[key] = (out, y, m)
+    return y, out
+
+
 def maxpool2(x):
     _req(x, "x")
     N, C, H, W = x.shape

@@ -1463,6 +1463,47 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc16_kernel(const float* __rest
   }
 }
 
+// BatchNorm affine + activation in place (affine_act_kernel's arithmetic) and,
+// in the same pass, the channel-last bf16 copy of act(y) times the mask plane
+// (nchw_to_nhwc16_kernel's conversion): the bf16 U-Net's block outputs feed
+// the next conv without a separate conversion pass.
+__global__ __launch_bounds__(256) void affine_act_nhwc16_kernel(
+    float* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    int act, float slope, const float* __restrict__ m, int C, int H, int W,
+    uint16_t* __restrict__ out) {
+  __shared__ uint16_t tile[64][66];   // [w][c]
+  const int w0 = blockIdx.x * 64, h = blockIdx.y;
+  const int cb = (C + 63) / 64;
+  const int n = blockIdx.z / cb, c0 = (blockIdx.z % cb) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int w = w0 + tx;
+  const float mv = (m && w < W) ? m[((int64_t)n * H + h) * W + w] : 1.f;
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i;
+    float v = 0.f;
+    if (c < C && w < W) {
+      float* q = y + (((int64_t)n * C + c) * H + h) * W + w;
+      v = apply_act(fmaf(*q, scale[c], shift[c]), act, slope);
+      *q = v;
+      v *= mv;
+    }
+    tile[tx][i] = __builtin_bit_cast(uint16_t, (__bf16)v);
+  }
+  __syncthreads();
+  const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
+#pragma unroll
+  for (int i = r; i < 64; i += 8) {
+    const int ww = w0 + i, c = c0 + 2 * l;
+    if (ww >= W || c >= C) continue;
+    uint16_t* q = out + (((int64_t)n * H + h) * W + ww) * C + c;
+    if (c + 1 < C)
+      *reinterpret_cast<uint32_t*>(q) = (uint32_t)tile[i][2 * l] | ((uint32_t)tile[i][2 * l + 1] << 16);
+    else
+      q[0] = tile[i][2 * l];
+  }
+}
+
 // few-channel source x [N][C][Hs][Ws] fp32 (x mask plane m [N][Hs][Ws]),
 // resampled to Hin x Win as src_coord -> bf16 rows out [N*Ho*Wo][seg],
 // k = tap*C + ci < KK*C, zero past it; one thread = 8 k-values of a pixel
@@ -1736,6 +1777,19 @@ extern "C" int ainp_nchw_to_nhwc16(const float* x, const float* m, int64_t N, in
                                                  (unsigned)(N * cdiv(C, 64))),
                      dim3(256), 0, as_stream(stream), x, m, C, H, W, out);
   return check_launch("nchw_to_nhwc16");
+}
+
+extern "C" int ainp_affine_act_nhwc16(float* y, const float* scale, const float* shift,
+                                     int64_t N, int C, int H, int W, int act, float slope,
+                                     const float* m, uint16_t* out, void* stream) {
+  if (!y || !scale || !shift || !out || N < 1 || C < 1 || H < 1 || W < 1 ||
+      N * ((C + 63) / 64) > 65535 || H > 65535)
+    return record_msg("ainp_affine_act_nhwc16: bad argument");
+  hipLaunchKernelGGL(affine_act_nhwc16_kernel, dim3((unsigned)cdiv(W, 64), (unsigned)H,
+                                                    (unsigned)(N * cdiv(C, 64))),
+                     dim3(256), 0, as_stream(stream), y, scale, shift, act, slope, m, C, H, W,
+                     out);
+  return check_launch("affine_act_nhwc16");
 }
 
 extern "C" int ainp_im2col_nhwc16(const float* x, const float* m, int64_t N, int C, int Hs,

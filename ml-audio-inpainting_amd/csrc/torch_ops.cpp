@@ -873,6 +873,22 @@ void nchw_to_nhwc16(const Tensor& x, const OptT& m, const Tensor& out) {
       "nchw_to_nhwc16");
 }
 
+void affine_act_nhwc16(const Tensor& y, const Tensor& scale, const Tensor& shift, int64_t act,
+                       double slope, const OptT& m, const Tensor& out) {
+  GUARD(y);
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
+  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  numel_is(scale, C, "scale");
+  numel_is(shift, C, "shift");
+  const float* mp = opt(m, "mask");
+  if (mp) numel_is(*m, N * H * W, "mask");
+  numel_is(out, y.numel(), "out");
+  chk(ainp_affine_act_nhwc16(dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"), N, (int)C,
+                             (int)H, (int)W, (int)act, (float)slope, mp, bf16p(out, "out"),
+                             stream_of(y)),
+      "affine_act_nhwc16");
+}
+
 void im2col_nhwc16(const Tensor& x, const OptT& m, int64_t Hin, int64_t Win, int64_t KH,
                    int64_t KW, int64_t stride, int64_t pad, const Tensor& out) {
   GUARD(x);
@@ -1094,6 +1110,8 @@ TORCH_LIBRARY(ainp, m) {
         "Tensor? bias_a2, Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, "
         "int kc) -> ()");
   m.def("nchw_to_nhwc16(Tensor x, Tensor? m, Tensor(a!) out) -> ()");
+  m.def("affine_act_nhwc16(Tensor(a!) y, Tensor scale, Tensor shift, int act, float slope, "
+        "Tensor? m, Tensor(b!) out) -> ()");
   m.def("conv_weight_nhwc16(Tensor w, int C0, int C1, Tensor(a!) wt16) -> ()");
   m.def("conv_gen_fwd_nhwc16(Tensor x0, Tensor? x1, Tensor wt16, int Cout, int KH, int KW, "
         "Tensor? bias, Tensor? ratio, Tensor? scale, Tensor(a!) y, Tensor(b!)? stats, int Hin, "
@@ -1139,6 +1157,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("pconv_mask", &pconv_mask);
   m.impl("gan_pad_input", &gan_pad_input);
   m.impl("affine_act", &affine_act);
+  m.impl("affine_act_nhwc16", &affine_act_nhwc16);
   m.impl("maxpool2", &maxpool2);
   m.impl("absdiff_mean", &absdiff_mean);
   m.impl("bce_logits", &bce_logits);
@@ -1201,6 +1220,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("pconv_mask", torch::CppFunction::makeFallthrough());
   m.impl("gan_pad_input", torch::CppFunction::makeFallthrough());
   m.impl("affine_act", torch::CppFunction::makeFallthrough());
+  m.impl("affine_act_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("maxpool2", torch::CppFunction::makeFallthrough());
   m.impl("absdiff_mean", torch::CppFunction::makeFallthrough());
   m.impl("bce_logits", torch::CppFunction::makeFallthrough());

@@ -498,3 +498,29 @@ def test_full_size_gan_step_bf16_tracks_reference(golden_dir):
         errs[k] = abs(float(out[k]) - r) / abs(r)
     print("bf16 GAN step rel errs", errs)
     assert max(errs.values()) < 2e-2, errs
+
+
+@pytest.mark.parametrize("N,C,H,W,masked", [(2, 64, 17, 70, True), (1, 96, 5, 130, False),
+                                           (2, 512, 3, 5, True)])
+def test_affine_act_nhwc16_equals_affine_then_convert(N, C, H, W, masked):
+    """ainp_affine_act_nhwc16 (the bf16 U-Net blocks' BatchNorm + LeakyReLU with
+    the next conv's channel-last source in the same pass) against affine_act_
+    followed by to_nhwc16: the in-place fp32 result and the bf16 copy are both
+    bit-identical; inside an nhwc16_memo scope to_nhwc16 returns the copy."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(N * C + H * W)
+    y0 = torch.randn(N, C, H, W, generator=g).cuda()
+    sc = (torch.rand(C, generator=g) + 0.5).cuda()
+    sh = torch.randn(C, generator=g).cuda()
+    m = (torch.rand(N, H, W, generator=g) > 0.3).float().cuda() if masked else None
+    ya = y0.clone()
+    ops.affine_act_(ya, sc, sh, ops.ACT_LEAKY, 0.2)
+    ref16 = ops.to_nhwc16(ya, m)
+    yb = y0.clone()
+    with ops.nhwc16_memo():
+        _, out16 = ops.affine_act_nhwc16_(yb, sc, sh, ops.ACT_LEAKY, 0.2, m)
+        again = ops.to_nhwc16(yb, m)
+        assert again.data_ptr() == out16.data_ptr()
+    torch.cuda.synchronize()
+    assert torch.equal(ya, yb)
+    assert torch.equal(ref16.view(torch.int16), out16.view(torch.int16))
