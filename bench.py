@@ -388,7 +388,7 @@ def main():
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
                 "traffic": traffic, "kernel": ("g256::gemm_bf16nt_256_kernel" if bf16 else
-                                               "x6_256::gemm_x6nt_256_kernel, split 3 + slab sum"
+                                               "x6_256::gemm_x6nt_256s_kernel (split pass), split 3 + slab sum"
                                                if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
                                                and not ops.GEMM_EXACT else
                                                "gemm_f32_kernel<1,...>") + f" (LSTM l0 "
