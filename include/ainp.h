@@ -219,6 +219,13 @@ int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t* A, int64_t
 int ainp_cast_bf16_t(const float* x, int64_t R, int64_t C, int64_t ld_in, uint16_t* out,
                      int64_t ld_out, uint16_t* outT, int64_t ld_t, void* stream);
 
+/* fp32 x [R][ld_in] -> outT [C][ld_t] (64 x 64 LDS tiles).  Builds the
+ * k-contiguous W_ih^T operand of the fp32 layer-0 data gradient
+ * dX = dgates . W_ih (models/CNNBLSTM/model.py:46-47 backward, via
+ * ainp_gemm_x6nt_256 with bsplit == N). */
+int ainp_transpose_f32(const float* x, int64_t R, int64_t C, int64_t ld_in, float* outT,
+                       int64_t ld_t, void* stream);
+
 /* ------------------------------------------------------------------------ */
 /* 3x3 / stride 1 / pad 1 convolution over [N, C, F, T] spectrogram tiles    */
 /* ------------------------------------------------------------------------ */

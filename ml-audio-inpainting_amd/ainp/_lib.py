@@ -138,6 +138,7 @@ _SIGS = {
     "ainp_gemm_bf16nt": (c_int, [c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P, c_int64,
                                  P, P, P, P, c_int64, c_int, c_int64, c_int64, P]),
     "ainp_cast_bf16_t": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P]),
+    "ainp_transpose_f32": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P]),
     "ainp_gemm_x6nt_256": (c_int, [c_int64, c_int64, c_int64, P, c_int64, P, P, c_int64, c_int64,
                                    P, c_int64, P, P, P, P, c_int64, c_int, c_int64, c_int64, P]),
     "ainp_d_prep16": (c_int, [P, c_int, c_int64, P, c_float, c_int64, c_int, c_int64, P, c_int64,

@@ -323,6 +323,15 @@ class _BLSTMFn(torch.autograd.Function):
                 # 672 tiles) summed in fixed order.
                 if l016 is not None:
                     dxi = ops.gemm_bf16nt(dg16, l016[1])                 # dg [NT,8H] x W_cat
+                elif Il >= 1024 and ops.DX_X6_256 and not bf16 and not ops.GEMM_EXACT \
+                        and ops.x6_256_eligible(NT, Il, 8 * H, Il):
+                    # layer 0 fp32: dX = dg [NT, 8H] . [W_f; W_r] on the 256 x 256
+                    # split-pass tile with the k-contiguous W_cat^T [Il, 8H]
+                    wt = torch.empty(Il, 8 * H, device=dh.device)
+                    ops.transpose_f32(wf, out=wt[:, :4 * H])
+                    ops.transpose_f32(wr, out=wt[:, 4 * H:])
+                    dxi = torch.empty(NT, Il, device=dh.device)
+                    ops.gemm_x6nt_256(dg2.view(NT, 8 * H), wt, wt[:0], dxi, nsplit=1)
                 elif Il >= 1024:
                     dxi = torch.empty(NT, Il, device=dh.device)
                     ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,

@@ -266,11 +266,26 @@ def gemm_bf16nt(A, B, K=None, out=None, bias=(None, None, None, None), bias_nspl
 # split 3 fills the 256 CUs with the 168 tiles of M = 10688, N = 1024
 # (2.28 -> 2.09 ms, tools/x6_256_lab.cpp); AINP_X6_256=0 keeps ainp_gemm_f32.
 X6_256 = os.environ.get("AINP_X6_256", "1") != "0"
+# layer-0 fp32 data gradient on the same tile (W_ih^T transposed per step).  Off:
+# inside the step it ran 4.11 ms against the 128 x 128 x6 kernel's 3.10 ms, as
+# the side-stream weight-gradient GEMM cannot co-reside with its 144 KB of LDS
+# (profiles/r02_s11_dx_x6_256_ab.txt); AINP_DX_X6_256=1 turns it on.
+DX_X6_256 = os.environ.get("AINP_DX_X6_256", "0") == "1"
 _X6_SPLIT = 3
 
 
 def x6_256_eligible(M, N, K, bsplit):
-    return X6_256 and M >= 2048 and K % 16 == 0 and bsplit % 256 == 0 and N >= 512
+    return X6_256 and M >= 2048 and K % 16 == 0 and (bsplit % 256 == 0 or bsplit == N) \
+        and N >= 512
+
+
+def transpose_f32(x, out=None):
+    """ainp_transpose_f32: fp32 x [R, C] (unit-stride rows) -> out [C, R]."""
+    R, Cc = x.shape
+    if out is None:
+        out = torch.empty(Cc, R, device=x.device, dtype=torch.float32)
+    _T.transpose_f32(x, out)
+    return out
 
 
 def gemm_x6nt_256(A, B1, B2, out, bias=(None, None, None, None), bias_nsplit=0, nsplit=None):

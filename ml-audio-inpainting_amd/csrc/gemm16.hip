@@ -189,6 +189,29 @@ __global__ __launch_bounds__(256) void cast_bf16_t_kernel(const float* __restric
   }
 }
 
+
+// fp32 [R][ld_in] -> its transpose outT [C][ld_t]; 64 x 64 tiles through LDS
+// (the layer-0 data gradient's k-contiguous W_ih^T operand)
+__global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restrict__ x, int64_t R,
+                                                            int64_t Cc, int64_t ld_in,
+                                                            float* __restrict__ outT,
+                                                            int64_t ld_t) {
+  __shared__ float tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < Cc) ? x[r * ld_in + c] : 0.f;
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < Cc && r < R) outT[c * ld_t + r] = tile[tx][i];
+  }
+}
+
 }  // namespace g16
 
 // Large GEMMs (M, N >= 512): 256 x 256 x 32 tiles with LDS-DMA staging.
@@ -731,10 +754,10 @@ extern "C" int ainp_gemm_x6nt_256(int64_t M, int64_t N, int64_t K, const float* 
   if (nsplit == 1) kc = K;
   if (M < 0 || N < 0 || K < 0 || !A || !B1 || !C || lda % 4 || ldb % 4 || lda < K || ldb < K ||
       ldc < N || K % x6_256::BK || ((uintptr_t)A & 15) || ((uintptr_t)B1 & 15) ||
-      bsplit < 0 || bsplit > N || bsplit % x6_256::BN ||
+      bsplit < 0 || bsplit > N || (bsplit % x6_256::BN && bsplit != N) ||
       (bsplit < N && (!B2 || ((uintptr_t)B2 & 15))))
     return record_msg("ainp_gemm_x6nt_256: bad argument (16-byte aligned k-contiguous rows, "
-                      "K % 16 == 0, bsplit % 256 == 0)");
+                      "K % 16 == 0, bsplit % 256 == 0 or bsplit == N)");
   if (M == 0 || N == 0) return AINP_OK;
   // AINP_X6_SPLITPASS=0 keeps the per-fragment-split kernel (A/B runs)
   static const bool splitpass = [] {
@@ -773,4 +796,14 @@ extern "C" int ainp_cast_bf16_t(const float* x, int64_t R, int64_t C, int64_t ld
   hipLaunchKernelGGL(g16::cast_bf16_t_kernel, dim3((unsigned)cdiv(C, 64), (unsigned)cdiv(R, 64)),
                      dim3(256), 0, as_stream(stream), x, R, C, ld_in, out, ld_out, outT, ld_t);
   return check_launch("cast_bf16_t");
+}
+
+extern "C" int ainp_transpose_f32(const float* x, int64_t R, int64_t C, int64_t ld_in, float* outT,
+                                  int64_t ld_t, void* stream) {
+  if (R < 0 || C < 0 || !x || !outT || ld_in < C || ld_t < R)
+    return record_msg("ainp_transpose_f32: bad argument");
+  if (R == 0 || C == 0) return AINP_OK;
+  hipLaunchKernelGGL(g16::transpose_f32_kernel, dim3((unsigned)cdiv(C, 64), (unsigned)cdiv(R, 64)),
+                     dim3(256), 0, as_stream(stream), x, R, C, ld_in, outT, ld_t);
+  return check_launch("transpose_f32");
 }

@@ -833,6 +833,18 @@ void gemm_x6nt_256(const Tensor& A, const Tensor& B1, const Tensor& B2, const Te
       "gemm_x6nt_256");
 }
 
+void transpose_f32(const Tensor& x, const Tensor& outT) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D with unit-stride rows");
+  TORCH_CHECK(outT.dim() == 2 && outT.size(0) == x.size(1) && outT.size(1) == x.size(0) &&
+                  outT.stride(1) == 1,
+              "outT must be [C, R] with unit-stride rows");
+  same_device(x, outT);
+  chk(ainp_transpose_f32(dev(x, "x", at::kFloat, false), x.size(0), x.size(1), x.stride(0),
+                         dev(outT, "outT", at::kFloat, false), outT.stride(0), stream_of(x)),
+      "transpose_f32");
+}
+
 void cast_bf16_t(const Tensor& x, const OptT& out, const OptT& outT) {
   GUARD(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D with unit-stride rows");
@@ -1106,6 +1118,7 @@ TORCH_LIBRARY(ainp, m) {
   m.def("gemm_bf16nt(Tensor A, Tensor B, Tensor(a!) C, int K, Tensor? bias_a1, Tensor? bias_a2, "
         "Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, int kc) -> ()");
   m.def("cast_bf16_t(Tensor x, Tensor(a!)? out, Tensor(b!)? outT) -> ()");
+  m.def("transpose_f32(Tensor x, Tensor(a!) outT) -> ()");
   m.def("gemm_x6nt_256(Tensor A, Tensor B1, Tensor B2, Tensor(a!) C, Tensor? bias_a1, "
         "Tensor? bias_a2, Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, "
         "int kc) -> ()");
@@ -1176,6 +1189,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("bn_relu_apply_ntcf_bf16", &bn_relu_apply_ntcf_bf16);
   m.impl("gemm_bf16nt", &gemm_bf16nt);
   m.impl("cast_bf16_t", &cast_bf16_t);
+  m.impl("transpose_f32", &transpose_f32);
   m.impl("gemm_x6nt_256", &gemm_x6nt_256);
   m.impl("nchw_to_nhwc16", &nchw_to_nhwc16);
   m.impl("conv_weight_nhwc16", &conv_weight_nhwc16);
@@ -1239,6 +1253,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("bn_relu_apply_ntcf_bf16", torch::CppFunction::makeFallthrough());
   m.impl("gemm_bf16nt", torch::CppFunction::makeFallthrough());
   m.impl("cast_bf16_t", torch::CppFunction::makeFallthrough());
+  m.impl("transpose_f32", torch::CppFunction::makeFallthrough());
   m.impl("gemm_x6nt_256", torch::CppFunction::makeFallthrough());
   m.impl("nchw_to_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("conv_weight_nhwc16", torch::CppFunction::makeFallthrough());

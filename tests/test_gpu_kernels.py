@@ -280,6 +280,42 @@ def test_gemm_x6nt_256_matches_x6_path(ops, M, K, H):
     assert e3 < 2 * e1 + 1e-7, (e3, e1)
 
 
+@pytest.mark.parametrize("R,C", [(512, 16448), (77, 130), (1, 65)])
+def test_transpose_f32_exact(ops, R, C):
+    """ainp_transpose_f32 into a strided destination (the half of W_cat^T one
+    direction's W_ih fills) is an exact copy."""
+    g = torch.Generator().manual_seed(R + C)
+    x = torch.randn(R, C, generator=g).to(DEV)
+    out = torch.full((C, 2 * R), float("nan"), device=DEV)
+    ops.transpose_f32(x, out=out[:, R:])
+    assert torch.equal(out[:, R:], x.t())
+    assert torch.isnan(out[:, :R]).all()
+
+
+@pytest.mark.parametrize("M,N,H", [(2304, 1088, 128), (10688, 16448, 128)])
+def test_layer0_dx_on_x6_256(ops, M, N, H):
+    """The fp32 layer-0 data gradient dX = dg [M, 8H] . [W_f; W_r] (backward of
+    models/CNNBLSTM/model.py:46-47) on the 256x256 split-pass tile with the
+    transposed W_cat^T (bsplit == N, N % 256 != 0 tail tile) against fp64 and
+    within 2x the error of the 128x128 x6 path it replaces."""
+    g = torch.Generator().manual_seed(M + N)
+    dg = (torch.randn(M, 8 * H, generator=g) * 0.1).to(DEV)
+    wf = (torch.randn(4 * H, N, generator=g) * 0.02).to(DEV)
+    wr = (torch.randn(4 * H, N, generator=g) * 0.02).to(DEV)
+    wt = torch.empty(N, 8 * H, device=DEV)
+    ops.transpose_f32(wf, out=wt[:, :4 * H])
+    ops.transpose_f32(wr, out=wt[:, 4 * H:])
+    dx = torch.full((M, N), float("nan"), device=DEV)
+    ops.gemm_x6nt_256(dg, wt, wt[:0], dx, nsplit=1)
+    old = torch.empty(M, N, device=DEV)
+    ops.gemm(M, N, 4 * H, [dg, dg[:, 4 * H:]], 8 * H, 1, [wf, wr], N, 1, [old, old], N, 1,
+             ksplit=True)
+    r64 = dg.double().cpu() @ torch.cat([wf, wr]).double().cpu()
+    e_new, e_old = rel(dx.cpu(), r64), rel(old.cpu(), r64)
+    assert e_new < 1e-5 and e_old < 1e-5, (e_new, e_old)
+    assert e_new < 2 * e_old + 1e-7, (e_new, e_old)
+
+
 def _bf(t):
     """fp64 copy of t rounded to fp32, then to bf16 (nearest-even)."""
     return t.float().bfloat16().double()
