@@ -485,7 +485,10 @@ def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
 @pytest.mark.parametrize("ntcf,H,W", [(False, 37, 70), (True, 37, 70), (False, 37, 71),
                                        (False, 65, 130),
                                        # C*H % 64 == 0, even W: the flattened-k NTCF kernels
-                                       (True, 48, 70), (True, 16, 134), (True, 8, 6)])
+                                       (True, 48, 70), (True, 16, 134), (True, 8, 6),
+                                       # H >= 64 as well: the ntcf2 backward statistics
+                                       # (64-row k-tiles spanning two channels)
+                                       (True, 72, 70), (True, 264, 66)])
 def test_bn_relu_fwd_bwd(ops, ntcf, H, W):
     g = torch.Generator().manual_seed(9)
     N, C = 3, 8
