@@ -404,8 +404,8 @@ def main():
             roof.update({
                 "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross "
                              "products on v_mfma_f32_32x32x16_bf16, f32 accumulate"
-                             + ("; 256x256x16 tiles staged by global_load_lds, split at "
-                                "fragment-read time" if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
+                             + ("; 256x256x16 tiles staged by global_load_lds, each K-tile "
+                                "split once per workgroup into LDS bf16 planes" if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
                                 else ""),
                 "executed_tflops": round(6 * achieved, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
                 "executed_frac": round(6 * achieved / BF16_MFMA_PEAK_TFLOPS, 4)})
