@@ -251,14 +251,30 @@ def cast_bf16_t(x, out=None, outT=None):
     return out, outT
 
 
-def gemm_bf16nt(A, B, K=None, out=None, bias=(None, None, None, None), bias_nsplit=0):
+# bf16 layer-0 projection split count (M >= 8N, M,N >= 512: ainp_gemm_bf16nt runs
+# a split tall GEMM on the 256 x 256 tile, 168 -> 504 workgroups); 1 = unsplit
+B16_PROJ_SPLIT = int(os.environ.get("AINP_B16_PROJ_SPLIT", "1"))
+
+
+def gemm_bf16nt(A, B, K=None, out=None, bias=(None, None, None, None), bias_nsplit=0,
+                nsplit=1):
     """C [M, N] = A [M, >=K] . B [N, >=K]^T + bias on bf16 operands (ainp_gemm_bf16nt);
-    bias = (a1, a2, b1, b2): a1 + a2 for columns < bias_nsplit, b1 + b2 after."""
+    bias = (a1, a2, b1, b2): a1 + a2 for columns < bias_nsplit, b1 + b2 after.
+    nsplit > 1: K split over slabs (bias in slab 0) summed in fixed order."""
     M, N = A.shape[0], B.shape[0]
     K = A.shape[1] if K is None else int(K)
     if out is None:
         out = torch.empty(M, N, device=A.device, dtype=torch.float32)
-    _T.gemm_bf16nt(A, B, out, K, *bias, int(bias_nsplit), 1, K)
+    S = int(nsplit)
+    kc = -(-K // S // 64) * 64 if S > 1 else K
+    if S > 1 and (-(-K // kc) != S or not out.is_contiguous()):
+        S, kc = 1, K
+    if S == 1:
+        _T.gemm_bf16nt(A, B, out, K, *bias, int(bias_nsplit), 1, K)
+        return out
+    slabs = torch.empty(S, M, N, device=A.device, dtype=torch.float32)
+    _T.gemm_bf16nt(A, B, slabs, K, *bias, int(bias_nsplit), S, kc)
+    sum_slabs(slabs, S, out=out.view(-1))
     return out
 
 

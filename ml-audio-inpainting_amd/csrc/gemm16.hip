@@ -141,7 +141,8 @@ __global__ __launch_bounds__(THREADS, 3) void gemm_bf16nt_kernel(
     const int64_t n = n0 + wn + j * 32 + li;
     if (n >= N) continue;
     float bv = 0.f;
-    if (n < bias.nsplit) {
+    if (split != 0) {   // split-K: the bias goes into slab 0 only
+    } else if (n < bias.nsplit) {
       if (bias.a1) bv += bias.a1[n];
       if (bias.a2) bv += bias.a2[n];
     } else {
@@ -346,7 +347,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
     const int64_t n = n0 + wn + j * 32 + li;
     if (n >= N) continue;
     float bv = 0.f;
-    if (n < bias.nsplit) {
+    if (split != 0) {   // split-K: the bias goes into slab 0 only
+    } else if (n < bias.nsplit) {
       if (bias.a1) bv += bias.a1[n];
       if (bias.a2) bv += bias.a2[n];
     } else {
@@ -720,8 +722,10 @@ extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t*
   // it on the side stream: the data gradient (10836 tiles) 706 -> 891 us, the
   // split-K weight gradient 621 -> 1325 us (it cannot co-reside with the
   // 3-workgroups-per-CU kernel next to it).
+  // A split tall-and-narrow GEMM (M >= 8N: the layer-0 projection, 168 tiles
+  // of 256 x 256 -> 504 workgroups at split 3) also runs on g256.
   const int64_t tiles128 = cdiv(M, g16::BM) * cdiv(N, g16::BN);
-  if (use256 && nsplit == 1 && M >= 512 && N >= 512 && tiles128 <= 1536 &&
+  if (use256 && (nsplit == 1 || M >= 8 * N) && M >= 512 && N >= 512 && tiles128 <= 1536 &&
       K % g256::BK == 0) {
     static const bool lds_ok =
         hipFuncSetAttribute((const void*)g256::gemm_bf16nt_256_kernel,

@@ -678,6 +678,27 @@ def test_gemm_bf16nt_matches_fp64_of_bf16_operands(M, N, K, S):
     assert err < 1e-5, float(err)
 
 
+@pytest.mark.parametrize("M,N,K,S", [(10688, 1024, 16448, 3), (4100, 512, 1088, 2),
+                                     (4100, 300, 1088, 3)])
+def test_gemm_bf16nt_split_projection_with_bias(M, N, K, S):
+    """The bf16 layer-0 projection split over K (ops.gemm_bf16nt nsplit > 1;
+    M >= 8N runs split on the 256x256 tile, N < 512 on the 128 tile): the two
+    directions' biases land once (slab 0 only) and the result is the unsplit
+    one up to fp32 summation order (models/CNNBLSTM/model.py:46-47,77)."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(M + N + K + S)
+    A = _tobf16(torch.randn(M, K, generator=g)).cuda()
+    B = _tobf16(torch.randn(N, K, generator=g)).cuda()
+    nb = N // 2
+    bias = tuple(torch.randn(n, generator=g).cuda() for n in (nb, nb, N - nb, N - nb))
+    C1 = ops.gemm_bf16nt(A, B, bias=bias, bias_nsplit=nb)
+    CS = torch.full((M, N), float("nan"), device="cuda")
+    ops.gemm_bf16nt(A, B, out=CS, bias=bias, bias_nsplit=nb, nsplit=S)
+    torch.cuda.synchronize()
+    err = (CS.double() - C1.double()).norm() / C1.double().norm()
+    assert err < 1e-6, float(err)
+
+
 def test_cast_bf16_t_and_ntcf_bf16_bridge_bit_exact():
     """The bf16 operand producers round to nearest-even exactly as torch's
     .to(bfloat16): cast (+ transpose into a strided view) and the encoder's
