@@ -366,7 +366,8 @@ def main():
             X16 = torch.randn(M, I, device=dev).to(torch.bfloat16)
             W16 = torch.cat([lw.weight_ih_l0, lw.weight_ih_l0_reverse]).detach().to(torch.bfloat16)
             bias = (lw.bias_ih_l0, lw.bias_hh_l0, lw.bias_ih_l0_reverse, lw.bias_hh_l0_reverse)
-            gfn = lambda: ops.gemm_bf16nt(X16, W16, out=zx, bias=bias, bias_nsplit=4 * H)  # noqa: E731
+            gfn = lambda: ops.gemm_bf16nt(X16, W16, out=zx, bias=bias, bias_nsplit=4 * H,  # noqa: E731
+                                          nsplit=ops.b16_proj_split(M, 8 * H))
         elif not ops.GEMM_EXACT and ops.x6_256_eligible(M, 8 * H, I, 4 * H):
             # the path the step takes (cnnblstm._BLSTMFn): 256x256 LDS-DMA tile, split 3
             A = torch.randn(M, I, device=dev)
@@ -387,7 +388,9 @@ def main():
         traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else "traffic_gemm_l0.json")
         roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                 "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": traffic, "kernel": ("g256::gemm_bf16nt_256_kernel" if bf16 else
+                "traffic": traffic, "kernel": ("g256::gemm_bf16nt_256_kernel" + (
+                    f", split {ops.b16_proj_split(M, 8 * H)} + slab sum"
+                    if ops.b16_proj_split(M, 8 * H) > 1 else "") if bf16 else
                                                "x6_256::gemm_x6nt_256s_kernel (split pass), split 3 + slab sum"
                                                if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
                                                and not ops.GEMM_EXACT else

@@ -230,10 +230,9 @@ class _BLSTMFn(torch.autograd.Function):
                 WT16 = torch.empty(I, 8 * H, device=x.device, dtype=torch.bfloat16)
                 ops.cast_bf16_t(wf, out=W16[:4 * H], outT=WT16[:, :4 * H])
                 ops.cast_bf16_t(wr, out=W16[4 * H:], outT=WT16[:, 4 * H:])
-                tall = NT >= 8 * 8 * H and NT >= 512 and 8 * H >= 512
                 ops.gemm_bf16nt(X16.view(NT, I), W16, out=zx.view(NT, 8 * H),
                                 bias=(bif, bhf, bir, bhr), bias_nsplit=4 * H,
-                                nsplit=ops.B16_PROJ_SPLIT if tall else 1)
+                                nsplit=ops.b16_proj_split(NT, 8 * H))
                 ctx.l016 = (XT16, WT16)
             elif (l == 0 and not bf16 and not ops.GEMM_EXACT
                   and ops.x6_256_eligible(NT, 8 * H, Il, 4 * H)):

@@ -252,8 +252,15 @@ def cast_bf16_t(x, out=None, outT=None):
 
 
 # bf16 layer-0 projection split count (M >= 8N, M,N >= 512: ainp_gemm_bf16nt runs
-# a split tall GEMM on the 256 x 256 tile, 168 -> 504 workgroups); 1 = unsplit
-B16_PROJ_SPLIT = int(os.environ.get("AINP_B16_PROJ_SPLIT", "1"))
+# a split tall GEMM on the 256 x 256 tile, 168 -> 504 workgroups): inside the
+# C3-shape step 483 -> 368 us + a 22 us slab sum, 9.92 -> 9.83 ms/step
+# (profiles/r02_s14_b16_proj_split_ab.txt); AINP_B16_PROJ_SPLIT=1 = unsplit
+B16_PROJ_SPLIT = int(os.environ.get("AINP_B16_PROJ_SPLIT", "3"))
+
+
+def b16_proj_split(M, N):
+    """Split count the bf16 layer-0 projection [M, N] uses (cnnblstm, bench)."""
+    return B16_PROJ_SPLIT if (M >= 8 * N and M >= 512 and N >= 512) else 1
 
 
 def gemm_bf16nt(A, B, K=None, out=None, bias=(None, None, None, None), bias_nsplit=0,

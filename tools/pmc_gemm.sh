@@ -24,8 +24,9 @@ pass write WRITE_SIZE || exit 1
 pass sq GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
   SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES || exit 1
 if [ "$DT" = bf16 ]; then
-  # X [10688][16448] + W_cat [1024][16448] bf16, zx [10688][1024] fp32
-  python3 tools/traffic_json.py "$OUT" gemm_bf16nt $(( 2 * (10688*16448 + 1024*16448) + 4 * 10688*1024 )) \
+  # X [10688][16448] + W_cat [1024][16448] bf16 read once, three fp32 split-K
+  # slabs [10688][1024] written (the slab sum is a separate launch)
+  python3 tools/traffic_json.py "$OUT" gemm_bf16nt $(( 2 * (10688*16448 + 1024*16448) + 3 * 4 * 10688*1024 )) \
     "tools/pmc_gemm.sh bf16 over tools/roofline_probe.py" > "$OUT/traffic.json" && cat "$OUT/traffic.json"
 else
   # the 256x256 x6 tile, split 3: X [10688][16448] + W_ih (both) [1024][16448]
