@@ -215,6 +215,114 @@ def graph_replay(model, opt, audio, starts, g, n_fft, hop, win, T, args, dev, ea
                     "replayed per step after a D2D copy of the gap starts"}
 
 
+def executed_peak(bf16):
+    """TFLOP/s ceiling of the MFMA instruction stream a configuration issues:
+    bf16 -> dense bf16 peak; fp32 -> the x6 split (6 x v_mfma_f32_32x32x16_bf16
+    per fp32 product) = bf16 peak / 6, unless AINP_GEMM_EXACT runs the f32 MFMA."""
+    from ainp import ops
+    if bf16:
+        return BF16_MFMA_PEAK_TFLOPS
+    return FP32_MFMA_PEAK_TFLOPS if ops.GEMM_EXACT else BF16_MFMA_PEAK_TFLOPS / 6.0
+
+
+def _roof(flops, avg_s, bf16, kernel, **extra):
+    ach = flops / avg_s / 1e12
+    peak = executed_peak(bf16)
+    r = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 2), "unit": "TFLOP/s",
+         "frac": round(ach / peak, 4), "kernel": kernel, "avg_launch_ms": round(avg_s * 1e3, 4),
+         "flop_per_launch": flops,
+         "peak_def": ("dense bf16 MFMA (MI355X_MICROARCH.md)" if bf16 else
+                      "x6 instruction-stream ceiling = dense bf16 MFMA / 6 (6 bf16 MFMA "
+                      "products per fp32 product)")}
+    if not bf16:
+        r["f32_mfma_ratio"] = round(ach / FP32_MFMA_PEAK_TFLOPS, 4)
+    r.update(extra)
+    return r
+
+
+def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
+    """(projection, backward pair) roofline entries of the LSTM layer-0 GEMMs
+    (M = B*T frames, 8H = both directions' gate rows, K = I = 64*257):
+    the projection X W_cat^T, and the backward pair dX = dg W_cat (main
+    stream) beside dW_cat = dg^T X (side stream), launched as
+    cnnblstm._BLSTMFn.backward launches them (2 x 2*M*8H*I flop)."""
+    from ainp import ops
+    M = B * T
+    lw = model.lstm
+    bias = (lw.bias_ih_l0, lw.bias_hh_l0, lw.bias_ih_l0_reverse, lw.bias_hh_l0_reverse)
+    zx = torch.empty(M, 8 * H, device=dev)
+    flops = 2.0 * M * (8 * H) * I
+    g = torch.Generator(device=dev).manual_seed(5)
+    dg = torch.randn(M, 8 * H, device=dev, generator=g) * 1e-3
+    if bf16:
+        # bf16 X [M, I] (written by the encoder's BN+ReLU) x bf16 W_cat [8H, I]
+        X16 = torch.randn(M, I, device=dev, generator=g).to(torch.bfloat16)
+        XT16 = X16.t().contiguous()
+        W16 = torch.cat([lw.weight_ih_l0, lw.weight_ih_l0_reverse]).detach().to(torch.bfloat16)
+        WT16 = W16.t().contiguous()
+        dg16, dgT16 = dg.to(torch.bfloat16), dg.t().contiguous().to(torch.bfloat16)
+        ns = ops.b16_proj_split(M, 8 * H, I)
+        fwd = lambda: ops.gemm_bf16nt(X16, W16, out=zx, bias=bias, bias_nsplit=4 * H,  # noqa: E731
+                                      nsplit=ns)
+        kname = ("g256::gemm_bf16nt_256_kernel" if ops.GEMM16_256 else "g16::gemm_bf16nt_kernel") \
+            + (f", split {ns} + slab sum" if ns > 1 else "")
+        dx_fn = lambda: ops.gemm_bf16nt(dg16, WT16)                       # noqa: E731
+        dw_fn = lambda: ops.gemm_bf16nt_splitk(dgT16, XT16, M)            # noqa: E731
+        bname = "dX gemm_bf16nt (dg16 x W_cat) + dW gemm_bf16nt_splitk (dg^T x X^T, side stream)"
+        main_loop = ("bf16 operands in HBM (X, W_cat), 256x256x32 tiles staged by global_load_lds "
+                     "into a 4-stage LDS ring, v_mfma_f32_32x32x16_bf16, f32 accumulate")
+    else:
+        A = torch.randn(M, I, device=dev, generator=g)
+        if not ops.GEMM_EXACT and ops.x6_256_eligible(M, 8 * H, I, 4 * H):
+            fwd = lambda: ops.gemm_x6nt_256(A, lw.weight_ih_l0, lw.weight_ih_l0_reverse,  # noqa: E731
+                                            zx, bias=bias, bias_nsplit=4 * H)
+            kname = "x6_256::gemm_x6nt_256s_kernel (split pass), split 3 + slab sum"
+        else:
+            args_g = (M, 4 * H, I, [A, A], I, 1, [lw.weight_ih_l0, lw.weight_ih_l0_reverse], 1,
+                      I, [zx, zx[:, 4 * H:]], 8 * H, 1)
+            kw = dict(bias1=[lw.bias_ih_l0, lw.bias_ih_l0_reverse],
+                      bias2=[lw.bias_hh_l0, lw.bias_hh_l0_reverse])
+            fwd = lambda: ops.gemm(*args_g, **kw)  # noqa: E731
+            kname = "gemm_f32_kernel (x6 loop)"
+        wf, wr = lw.weight_ih_l0.detach(), lw.weight_ih_l0_reverse.detach()
+        dxo = torch.empty(M, I, device=dev)
+        dx_fn = lambda: ops.gemm(M, I, 4 * H, [dg, dg[:, 4 * H:]], 8 * H, 1, [wf, wr], I, 1,  # noqa: E731
+                                 [dxo, dxo], I, 1, ksplit=True)
+        dw_fn = lambda: ops.gemm_tn_splitk(dg, 8 * H, A, I, M, 4 * H, I, offsets_b=(0, 0))  # noqa: E731
+        bname = ("dX gemm_f32_kernel x6 (dg x [W_f; W_r], both directions summed in-tile) + dW "
+                 "gemm_tn_splitk x6 (dg^T x X, split-K slabs + fixed-order sum, side stream)")
+        main_loop = ("fp32 operands split exactly into 3 bf16 pieces, 6 cross products on "
+                     "v_mfma_f32_32x32x16_bf16, f32 accumulate; 256x256x16 tiles staged by "
+                     "global_load_lds, each K-tile split once per workgroup into LDS bf16 planes")
+    avg_s = time_kernel(fwd, reps, dev)
+    traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else "traffic_gemm_l0.json")
+    roof = _roof(flops, avg_s, bf16, kname + f" (LSTM l0 input projection, M={M} N={8 * H} "
+                 f"K={I}, both directions)", traffic=traffic, main_loop=main_loop)
+
+    side = torch.cuda.Stream(dev)
+    main = torch.cuda.current_stream(dev)
+
+    def pair():
+        ev = torch.cuda.Event()
+        ev.record(main)
+        side.wait_event(ev)
+        with torch.cuda.stream(side):
+            dw_fn()
+        dx_fn()
+        done = torch.cuda.Event()
+        done.record(side)
+        main.wait_event(done)
+    pair_s = time_kernel(pair, reps, dev)
+    dx_s = time_kernel(dx_fn, reps, dev)
+    dw_s = time_kernel(dw_fn, reps, dev)
+    roof_bwd = _roof(2 * flops, pair_s, bf16, bname + f" (M={M}, 8H={8 * H}, K={I})",
+                     dx_alone_ms=round(dx_s * 1e3, 4), dw_alone_ms=round(dw_s * 1e3, 4),
+                     what="dX on the current stream beside dW on a side stream, as "
+                          "cnnblstm._BLSTMFn.backward launches them; timed from the first "
+                          "launch to the join")
+    return roof, roof_bwd
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -352,66 +460,16 @@ def main():
         graph = graph_replay(model, opt, audio, starts, g, n_fft, hop, win, T, args, dev, med_ms)
     recon_l1 = eval_recon_l1(model, n_fft, hop, win, T, S, g, dev) if rank == 0 else None
 
-    # ---- roofline: dominant kernel (LSTM layer-0 input projection GEMM) timed live
-    roof = None
+    # ---- roofline: dominant kernel (LSTM layer-0 input projection GEMM) timed
+    # live, and the layer-0 backward pair (data + weight gradient) as the step
+    # runs them.  `peak` is the ceiling of the instruction stream the kernel
+    # issues, so frac <= 1 by construction: bf16 -> the dense bf16 MFMA peak;
+    # fp32 (x6: 6 bf16 MFMA products per fp32 product) -> bf16 peak / 6.
+    roof = roof_bwd = None
     if rank == 0:
         H = CFG["model"]["lstm_hidden_dim"]
         I = (H // 2) * (n_fft // 2 + 1)
-        M = B * T
-        lw = model.lstm
-        zx = torch.empty(M, 8 * H, device=dev)
-        if bf16:
-            # the bf16 configuration's layer-0 projection: bf16 X [M, I] (written
-            # by the encoder's BN+ReLU) x bf16 W_cat [8H, I] on gemm_bf16nt
-            X16 = torch.randn(M, I, device=dev).to(torch.bfloat16)
-            W16 = torch.cat([lw.weight_ih_l0, lw.weight_ih_l0_reverse]).detach().to(torch.bfloat16)
-            bias = (lw.bias_ih_l0, lw.bias_hh_l0, lw.bias_ih_l0_reverse, lw.bias_hh_l0_reverse)
-            gfn = lambda: ops.gemm_bf16nt(X16, W16, out=zx, bias=bias, bias_nsplit=4 * H,  # noqa: E731
-                                          nsplit=ops.b16_proj_split(M, 8 * H))
-        elif not ops.GEMM_EXACT and ops.x6_256_eligible(M, 8 * H, I, 4 * H):
-            # the path the step takes (cnnblstm._BLSTMFn): 256x256 LDS-DMA tile, split 3
-            A = torch.randn(M, I, device=dev)
-            bias = (lw.bias_ih_l0, lw.bias_hh_l0, lw.bias_ih_l0_reverse, lw.bias_hh_l0_reverse)
-            gfn = lambda: ops.gemm_x6nt_256(A, lw.weight_ih_l0, lw.weight_ih_l0_reverse,  # noqa: E731
-                                            zx, bias=bias, bias_nsplit=4 * H)
-        else:
-            A = torch.randn(M, I, device=dev)
-            args_g = (M, 4 * H, I, [A, A], I, 1, [lw.weight_ih_l0, lw.weight_ih_l0_reverse], 1,
-                      I, [zx, zx[:, 4 * H:]], 8 * H, 1)
-            kw = dict(bias1=[lw.bias_ih_l0, lw.bias_ih_l0_reverse],
-                      bias2=[lw.bias_hh_l0, lw.bias_hh_l0_reverse])
-            gfn = lambda: ops.gemm(*args_g, **kw)  # noqa: E731
-        avg_s = time_kernel(gfn, args.roofline_reps, dev)
-        flops = 2.0 * M * (8 * H) * I
-        achieved = flops / avg_s / 1e12
-        peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
-        traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else "traffic_gemm_l0.json")
-        roof = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(achieved / peak, 4),
-                "traffic": traffic, "kernel": ("g256::gemm_bf16nt_256_kernel" + (
-                    f", split {ops.b16_proj_split(M, 8 * H)} + slab sum"
-                    if ops.b16_proj_split(M, 8 * H) > 1 else "") if bf16 else
-                                               "x6_256::gemm_x6nt_256s_kernel (split pass), split 3 + slab sum"
-                                               if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
-                                               and not ops.GEMM_EXACT else
-                                               "gemm_f32_kernel<1,...>") + f" (LSTM l0 "
-                f"input projection, M={M} N={8 * H} K={I}, both directions)",
-                "avg_launch_ms": round(avg_s * 1e3, 4), "flop_per_launch": flops}
-        if bf16:
-            roof["main_loop"] = ("bf16 operands in HBM (X, W_cat), 256x256x32 tiles staged "
-                                 "by global_load_lds into a 4-stage LDS ring, "
-                                 "v_mfma_f32_32x32x16_bf16, f32 accumulate")
-        elif not ops.GEMM_EXACT:
-            # fp32-accurate three-piece bf16 split: 6 bf16 MFMA products per fp32
-            # product; its own instruction-stream ceiling is the dense bf16 peak / 6
-            roof.update({
-                "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross "
-                             "products on v_mfma_f32_32x32x16_bf16, f32 accumulate"
-                             + ("; 256x256x16 tiles staged by global_load_lds, each K-tile "
-                                "split once per workgroup into LDS bf16 planes" if ops.x6_256_eligible(M, 8 * H, I, 4 * H)
-                                else ""),
-                "executed_tflops": round(6 * achieved, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
-                "executed_frac": round(6 * achieved / BF16_MFMA_PEAK_TFLOPS, 4)})
+        roof, roof_bwd = l0_rooflines(model, B, T, H, I, bf16, args.roofline_reps, dev)
 
     # ---- STFT / feature / mask path (HBM-bound): 4880 B per frame
     roof_stft = None
@@ -453,9 +511,17 @@ def main():
                             "L1sum(10**y*m, |X|*m), model.eval() (train.py:128-150,192)",
             "train_loss_last": train_loss,
             "step_tflops": round(step_flops / (ms_step / 1e3) / 1e12, 2),
+            # against the ceiling of the MFMA stream the step issues (fp32 runs
+            # the x6 split: bf16 peak / 6); f32-MFMA ratio kept under its own name
             "mfma_util_step": round(step_flops / world / (ms_step / 1e3) / 1e12
-                                    / (BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS), 4),
+                                    / executed_peak(bf16), 4),
+            "mfma_util_step_def": ("step FLOPs (163.0 MFLOP/frame, SURVEY d4) / ms_per_step / "
+                                   + ("dense bf16 peak" if bf16 else
+                                      "x6 executed ceiling (bf16 peak / 6 = 416.7 TF)")),
+            **({} if bf16 else {"f32_mfma_ratio_step": round(
+                step_flops / world / (ms_step / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}),
             "roofline": roof,
+            "roofline_l0_bwd": roof_bwd,
             "roofline_stft": roof_stft,
             "dp": dp,
             "graph": graph,
@@ -602,26 +668,18 @@ def run_gan(args):
             kname = "conv_gen_x6_kernel<64,16>"
         avg_s = time_kernel(launch, args.roofline_reps, dev)
         flops = 2.0 * 64 * 65 * 9 * B * Hp * Wp
-        ach = flops / avg_s / 1e12
-        peak = BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS
-        roof = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak,
-                "unit": "TFLOP/s", "frac": round(ach / peak, 4),
-                "traffic": _traffic("traffic_conv_gen_final_bf16.json" if bf16
-                                    else "traffic_conv_gen_final.json"),
-                "kernel": f"{kname} (final PartialConv2d 65->64 3x3 at "
-                          f"{Hp}x{Wp}, B={B})", "avg_launch_ms": round(avg_s * 1e3, 4),
-                "flop_per_launch": flops}
+        roof = _roof(flops, avg_s, bf16, f"{kname} (final PartialConv2d 65->64 3x3 at "
+                     f"{Hp}x{Wp}, B={B})",
+                     traffic=_traffic("traffic_conv_gen_final_bf16.json" if bf16
+                                      else "traffic_conv_gen_final.json"))
         if bf16:
             roof["main_loop"] = ("channel-last bf16 operands (x*mask folded in; the 1-channel "
                                  "skip source expanded per pixel, 9 -> 32 k-values), "
                                  "v_mfma_f32_32x32x16_bf16, f32 accumulate")
             roof["executed_flop_per_launch"] = 2.0 * 64 * (64 * 9 + 32) * B * Hp * Wp
         else:
-            roof.update({
-                "main_loop": "fp32 operands split exactly into 3 bf16 pieces, 6 cross products "
-                             "on v_mfma_f32_32x32x16_bf16, f32 accumulate",
-                "executed_tflops": round(6 * ach, 1), "executed_peak": BF16_MFMA_PEAK_TFLOPS,
-                "executed_frac": round(6 * ach / BF16_MFMA_PEAK_TFLOPS, 4)})
+            roof["main_loop"] = ("fp32 operands split exactly into 3 bf16 pieces, 6 cross "
+                                 "products on v_mfma_f32_32x32x16_bf16, f32 accumulate")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = gan_cpu_baseline(T, S, g)
@@ -648,8 +706,7 @@ def run_gan(args):
             "step_tflops": (round(step_flops / (ms_step / 1e3) / 1e12, 2)
                             if step_flops else None),
             "mfma_util_step": (round(step_flops / world / (ms_step / 1e3) / 1e12
-                                     / (BF16_MFMA_PEAK_TFLOPS if bf16 else FP32_MFMA_PEAK_TFLOPS),
-                                     4) if step_flops else None),
+                                     / executed_peak(bf16), 4) if step_flops else None),
             "roofline": roof, "reconstruction": recon, "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

@@ -375,8 +375,12 @@ int ainp_lstm_hprev(const float* h_out, float* hprev, int64_t N, int64_t T,
 /* ------------------------------------------------------------------------ */
 /* CNNBLSTM training loss (models/CNNBLSTM/train.py:70,104):
  *   L = sum | 10^y * m - |target| * m |    (nn.L1Loss(reduction='sum'))
- * y, mask [n] f32; target [n] complex64 (interleaved). loss: double[1]
- * accumulated (caller zeroes). dy (may be NULL): dL/dy * grad_scale. */
+ * y, mask [n] f32; target [n] complex64 (interleaved).
+ * loss: double[ainp_l1_pow10_loss_slots(n)], caller-allocated (no zeroing):
+ * on completion loss[0] = L, loss[1..] is the per-workgroup partial scratch.
+ * Deterministic: fixed-order two-pass reduction, no atomics (bit-reproducible
+ * from run to run).  dy (may be NULL): dL/dy * grad_scale. */
+int64_t ainp_l1_pow10_loss_slots(int64_t n);
 int ainp_l1_pow10_loss(const float* y, const float* mask, const float* target,
                        int64_t n, double* loss, float* dy, float grad_scale,
                        void* stream);

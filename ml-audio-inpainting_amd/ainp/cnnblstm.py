@@ -232,7 +232,7 @@ class _BLSTMFn(torch.autograd.Function):
                 ops.cast_bf16_t(wr, out=W16[4 * H:], outT=WT16[:, 4 * H:])
                 ops.gemm_bf16nt(X16.view(NT, I), W16, out=zx.view(NT, 8 * H),
                                 bias=(bif, bhf, bir, bhr), bias_nsplit=4 * H,
-                                nsplit=ops.b16_proj_split(NT, 8 * H))
+                                nsplit=ops.b16_proj_split(NT, 8 * H, I))
                 ctx.l016 = (XT16, WT16)
             elif (l == 0 and not bf16 and not ops.GEMM_EXACT
                   and ops.x6_256_eligible(NT, 8 * H, Il, 4 * H)):
@@ -252,6 +252,7 @@ class _BLSTMFn(torch.autograd.Function):
         # gradient bytes, produced late) are handed to the reducer chunk by chunk
         ctx.sink = sink
         ctx.wih0 = (params[0], params[4])     # the Parameters themselves
+        ctx.param_objs = params
         ctx.save_for_backward(*saved, *params)
         return h
 
@@ -349,12 +350,14 @@ class _BLSTMFn(torch.autograd.Function):
         for gr in grads:
             if gr is not None:
                 gr.record_stream(main)    # side-stream memory handed to autograd
-        if ctx.sink is None:
+        if ctx.sink is None and all(p.grad is None for p in ctx.param_objs):
             # nothing on the current stream reads these gradients before the
             # optimizer: join the side stream at the end of the backward pass
             # (engine callback) so the layer-0 weight gradient overlaps the
             # encoder backward.  Non-view aliases, so AccumulateGrad stores them
             # instead of cloning (a clone would read them before they exist).
+            # Only while every .grad is empty: otherwise AccumulateGrad adds
+            # them into .grad on the current stream, which must wait (below).
             dev = dh.device
 
             def join():
@@ -364,7 +367,8 @@ class _BLSTMFn(torch.autograd.Function):
             torch.autograd.Variable._execution_engine.queue_callback(join)
             grads = [_alias(gr) if gr is not None else None for gr in grads]
         else:
-            # data parallel: the gradient hooks read them as autograd hands them over
+            # data parallel: the gradient hooks read them as autograd hands them
+            # over; accumulation into an existing .grad reads them too
             done = torch.cuda.Event()
             done.record(side)
             main.wait_event(done)
@@ -686,8 +690,11 @@ class StackedBLSTMCNN(nn.Module):
         x = x.contiguous()
         spec, params = self._stack(self.encoder)
         box = {} if self.bf16 else None       # layer-0 bf16 operands (encoder -> BLSTM)
+        # the deferred weight gradients are written after autograd receives
+        # them: only while the .grad buffers are empty (nothing accumulates)
         defer_enc = (self.defer_wgrad_encoder and self.training and torch.is_grad_enabled()
-                     and self.grad_reducer is None and self.comm is None)
+                     and self.grad_reducer is None and self.comm is None
+                     and all(q.grad is None for q in self.encoder.parameters()))
         z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, box, defer_enc,
                                *params)
         sink = self.grad_reducer if (self.training and torch.is_grad_enabled()) else None

@@ -15,6 +15,7 @@ the N>1 logic is tested without GPUs (tests/test_cpu_dist.py).
 """
 from __future__ import annotations
 
+import datetime
 import os
 
 import torch
@@ -258,6 +259,12 @@ def init_from_env(backend: str | None = None):
             ("nccl" if torch.cuda.is_available() else "gloo")
     if backend == "nccl" or torch.cuda.is_available():
         torch.cuda.set_device(local if backend == "nccl" else local % max(1, torch.cuda.device_count()))
+    if backend == "nccl":
+        # collective failures raise instead of hanging (RCCL async error
+        # handling: a failed/timed-out collective aborts the communicator)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
-        dist.init_process_group(backend=backend, rank=rank, world_size=ws)
+        # AINP_DIST_TIMEOUT_S bounds every collective (default 600 s)
+        timeout = datetime.timedelta(seconds=float(os.environ.get("AINP_DIST_TIMEOUT_S", "600")))
+        dist.init_process_group(backend=backend, rank=rank, world_size=ws, timeout=timeout)
     return rank, ws, local

@@ -23,8 +23,14 @@ from .optim import Adam
 
 class GanTrainer:
     def __init__(self, cfg, generator, discriminator, vgg=None, faithful_g_backward=False,
-                 comm=None):
+                 comm=None, fail_fast=False):
+        """fail_fast: read the D loss on the host before d_optimizer.step()
+        and raise ainp.failfast.NonFiniteLossError if it is NaN/inf on any
+        rank (models/GAN/train.py reads the losses every step anyway; off for
+        the bench, which must not add a mid-step sync)."""
         tc = cfg["training"]
+        self.fail_fast = fail_fast
+        self.nstep = 0
         self.cfg = cfg
         self.G, self.D, self.vgg = generator, discriminator, vgg
         betas = (tc.get("b1", 0.5), tc.get("b2", 0.999))
@@ -76,6 +82,10 @@ class GanTrainer:
             for p in self.D.parameters():
                 if p.grad is not None:
                     p.grad.div_(self.comm.world_size)
+        if self.fail_fast:
+            from .failfast import check_finite
+            check_finite(d_loss, "D loss", self.nstep, self.comm)
+        self.nstep += 1
         self.d_opt.step()
         # ---- generator step (train.py:366-378)
         self.g_opt.zero_grad()

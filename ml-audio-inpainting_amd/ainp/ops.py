@@ -22,9 +22,12 @@ import torch
 
 from . import _lib
 
-TORCH_OPS_PATH = os.path.join(os.path.dirname(_lib.LIB_PATH), "libainp_torch.so")
+# AINP_TORCH_OPS: another build of the same registration (e.g. the UBSan build
+# libainp_torch_ubsan.so that tests/test_gpu_sanitize.py loads)
+TORCH_OPS_PATH = os.environ.get("AINP_TORCH_OPS") or \
+    os.path.join(os.path.dirname(_lib.LIB_PATH), "libainp_torch.so")
 if not os.path.exists(TORCH_OPS_PATH):
-    raise ImportError(f"libainp_torch.so not found at {TORCH_OPS_PATH}; build it with "
+    raise ImportError(f"torch ops library not found at {TORCH_OPS_PATH}; build it with "
                       "`make -C ml-audio-inpainting_amd/csrc` (or __graft_entry__.build())")
 torch.ops.load_library(TORCH_OPS_PATH)
 _T = torch.ops.ainp
@@ -258,9 +261,18 @@ def cast_bf16_t(x, out=None, outT=None):
 B16_PROJ_SPLIT = int(os.environ.get("AINP_B16_PROJ_SPLIT", "3"))
 
 
-def b16_proj_split(M, N):
-    """Split count the bf16 layer-0 projection [M, N] uses (cnnblstm, bench)."""
-    return B16_PROJ_SPLIT if (M >= 8 * N and M >= 512 and N >= 512) else 1
+GEMM16_256 = os.environ.get("AINP_GEMM16_256", "1")[:1] != "0"
+
+
+def b16_proj_split(M, N, K):
+    """Split count the bf16 layer-0 projection [M, N] x K uses (cnnblstm,
+    bench): B16_PROJ_SPLIT only where ainp_gemm_bf16nt routes the split GEMM
+    to the 256 x 256 tile (gemm16.hip: M >= 8N, M, N >= 512, at most 1536
+    128 x 128 tiles, K % 32 == 0, AINP_GEMM16_256 on); else unsplit."""
+    tiles128 = -(-M // 128) * -(-N // 128)
+    ok = (GEMM16_256 and M >= 8 * N and M >= 512 and N >= 512 and tiles128 <= 1536
+          and K % 32 == 0)
+    return B16_PROJ_SPLIT if ok else 1
 
 
 def gemm_bf16nt(A, B, K=None, out=None, bias=(None, None, None, None), bias_nsplit=0,
@@ -547,14 +559,16 @@ def lstm_hprev(h_out, H):
 
 # --------------------------------------------------------------------- loss
 def l1_pow10_loss(y, mask, target, want_grad=True, grad_scale=1.0):
-    """sum |10^y*m - |target|*m| -> (loss float64 [1], dy or None)."""
+    """sum |10^y*m - |target|*m| -> (loss float64 [1], dy or None).  The sum
+    is a fixed-order two-pass reduction (bit-reproducible run to run)."""
     _req(y, "y"); _req(mask, "mask"); _req(target, "target", torch.complex64)
     n = y.numel()
     assert mask.numel() == n and target.numel() == n
-    loss = torch.zeros(1, device=y.device, dtype=torch.float64)
+    ws = torch.empty(int(_lib.lib.ainp_l1_pow10_loss_slots(n)), device=y.device,
+                     dtype=torch.float64)
     dy = torch.empty_like(y) if want_grad else None
-    _T.l1_pow10_loss(y, mask, target, loss, dy, float(grad_scale))
-    return loss, dy
+    _T.l1_pow10_loss(y, mask, target, ws, dy, float(grad_scale))
+    return ws[:1], dy
 
 
 def scale_by_scalar(x, s):

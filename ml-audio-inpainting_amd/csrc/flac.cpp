@@ -105,6 +105,14 @@ struct StreamInfo {
 
 int fail(const char* m) { return ainp::record_msg(m); }
 
+// Predictor / decorrelation arithmetic wraps modulo 2^64 like the hardware
+// does: a valid stream never leaves the sample range (so the results are the
+// same), and a corrupted one cannot hit signed-overflow UB (found by the UBSan
+// harness, tests/sanitize/flac_fuzz.cpp); its CRC-16 check rejects it later.
+inline int64_t wadd(int64_t a, int64_t b) { return (int64_t)((uint64_t)a + (uint64_t)b); }
+inline int64_t wsub(int64_t a, int64_t b) { return (int64_t)((uint64_t)a - (uint64_t)b); }
+inline int64_t wmul(int64_t a, int64_t b) { return (int64_t)((uint64_t)a * (uint64_t)b); }
+
 int parse_header(const uint8_t* d, size_t n, StreamInfo& si) {
   size_t at = 0;
   if (n >= 10 && d[0] == 'I' && d[1] == 'D' && d[2] == '3') {  // ID3v2 tag in front
@@ -193,12 +201,17 @@ bool subframe(Bits& b, int blocksize, int bps, int64_t* out) {
       int64_t pred = 0;
       switch (order) {
         case 1: pred = out[i - 1]; break;
-        case 2: pred = 2 * out[i - 1] - out[i - 2]; break;
-        case 3: pred = 3 * out[i - 1] - 3 * out[i - 2] + out[i - 3]; break;
-        case 4: pred = 4 * out[i - 1] - 6 * out[i - 2] + 4 * out[i - 3] - out[i - 4]; break;
+        case 2: pred = wsub(wmul(2, out[i - 1]), out[i - 2]); break;
+        case 3:
+          pred = wadd(wsub(wmul(3, out[i - 1]), wmul(3, out[i - 2])), out[i - 3]);
+          break;
+        case 4:
+          pred = wsub(wadd(wsub(wmul(4, out[i - 1]), wmul(6, out[i - 2])), wmul(4, out[i - 3])),
+                      out[i - 4]);
+          break;
         default: break;
       }
-      out[i] += pred;
+      out[i] = wadd(out[i], pred);
     }
   } else if (type >= 32) {  // LPC, order 1..32
     const int order = type - 31;
@@ -213,8 +226,8 @@ bool subframe(Bits& b, int blocksize, int bps, int64_t* out) {
     if (!residual(b, blocksize, order, out)) return false;
     for (int i = order; i < blocksize; ++i) {
       int64_t sum = 0;
-      for (int j = 0; j < order; ++j) sum += coef[j] * out[i - 1 - j];
-      out[i] += sum >> shift;
+      for (int j = 0; j < order; ++j) sum = wadd(sum, wmul(coef[j], out[i - 1 - j]));
+      out[i] = wadd(out[i], sum >> shift);
     }
   } else {
     return false;  // reserved
@@ -304,15 +317,15 @@ extern "C" int ainp_flac_decode(const uint8_t* data, size_t n, int32_t* out, int
       if (!subframe(b, blocksize, sbps, ch[c].data())) return fail("flac: bad subframe");
     }
     if (ch_code == 8) {
-      for (int i = 0; i < blocksize; ++i) ch[1][i] = ch[0][i] - ch[1][i];
+      for (int i = 0; i < blocksize; ++i) ch[1][i] = wsub(ch[0][i], ch[1][i]);
     } else if (ch_code == 9) {
-      for (int i = 0; i < blocksize; ++i) ch[0][i] += ch[1][i];
+      for (int i = 0; i < blocksize; ++i) ch[0][i] = wadd(ch[0][i], ch[1][i]);
     } else if (ch_code == 10) {
       for (int i = 0; i < blocksize; ++i) {
         const int64_t side = ch[1][i];
-        const int64_t mid = (ch[0][i] * 2) | (side & 1);
-        ch[0][i] = (mid + side) >> 1;
-        ch[1][i] = (mid - side) >> 1;
+        const int64_t mid = wmul(ch[0][i], 2) | (side & 1);
+        ch[0][i] = wadd(mid, side) >> 1;
+        ch[1][i] = wsub(mid, side) >> 1;
       }
     }
     b.align();
@@ -438,7 +451,7 @@ struct Md5 {
   }
 };
 
-inline uint32_t zigzag(int64_t r) { return (uint32_t)((r << 1) ^ (r >> 63)); }
+inline uint32_t zigzag(int64_t r) { return (uint32_t)(((uint64_t)r << 1) ^ (uint64_t)(r >> 63)); }
 
 // Exact bits of the Rice-coded residual r[0..n) with the best partition order
 // <= max_po (partition 0 shortened by `order` warm-up samples) and per-

@@ -6,9 +6,12 @@ namespace ainp {
 // L = sum |10^y*m - |target|*m|  (models/CNNBLSTM/train.py:70,104:
 // nn.L1Loss(reduction='sum') on (10 ** y) * mask vs abs(target) * mask)
 // dL/dy = sign(d) * m * 10^y * ln(10), sign(0) = 0 as in torch's L1 backward.
+// Deterministic: each workgroup writes its fp64 partial to partial[blockIdx.x]
+// (fixed grid-stride order, fixed wave/LDS combine); l1_sum_partials_kernel
+// adds the partials in a fixed order.  No atomics: the loss is bit-reproducible.
 __global__ __launch_bounds__(256) void l1_pow10_kernel(
     const float* __restrict__ y, const float* __restrict__ mask,
-    const float2* __restrict__ target, int64_t n, double* __restrict__ loss,
+    const float2* __restrict__ target, int64_t n, double* __restrict__ partial,
     float* __restrict__ dy, float grad_scale) {
   const float LN10 = 2.302585092994046f;
   double acc = 0.0;
@@ -30,7 +33,24 @@ __global__ __launch_bounds__(256) void l1_pow10_kernel(
   acc = wave_sum_d(acc);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(loss, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) partial[blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+// out[0] = sum of partial[0..np) in a fixed order (one workgroup of 256).
+__global__ __launch_bounds__(256) void l1_sum_partials_kernel(const double* __restrict__ partial,
+                                                              int64_t np, double* __restrict__ out) {
+  double acc = 0.0;
+  for (int64_t i = threadIdx.x; i < np; i += 256) acc += partial[i];
+  __shared__ double red[4];
+  acc = wave_sum_d(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) out[0] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+
+static int64_t l1_grid(int64_t n) {
+  int64_t grid = cdiv(n, 256 * 8);
+  return grid > 2048 ? 2048 : (grid < 1 ? 1 : grid);
 }
 
 // out[j] (+)= sum_i x[i*ld + j]; one thread per column, rows split over
@@ -179,18 +199,22 @@ extern "C" int ainp_scale_by_dev(const float* x, float* out, int64_t n,
   return check_launch("scale_by_dev");
 }
 
+extern "C" int64_t ainp_l1_pow10_loss_slots(int64_t n) { return 1 + l1_grid(n); }
+
 extern "C" int ainp_l1_pow10_loss(const float* y, const float* mask,
                                   const float* target, int64_t n, double* loss,
                                   float* dy, float grad_scale, void* stream) {
-  if (!y || !mask || !target || !loss || n < 0)
+  if (!loss || n < 0 || (n > 0 && (!y || !mask || !target)))
     return record_msg("ainp_l1_pow10_loss: bad argument");
-  if (n == 0) return AINP_OK;
-  int64_t grid = cdiv(n, 256 * 8);
-  if (grid > 2048) grid = 2048;
-  hipLaunchKernelGGL(l1_pow10_kernel, dim3((unsigned)grid), dim3(256), 0,
-                     as_stream(stream), y, mask,
-                     reinterpret_cast<const float2*>(target), n, loss, dy,
-                     grad_scale);
+  hipStream_t s = as_stream(stream);
+  if (n == 0) {
+    hipLaunchKernelGGL(l1_sum_partials_kernel, dim3(1), dim3(256), 0, s, loss + 1, 0, loss);
+    return check_launch("l1_pow10_loss");
+  }
+  const int64_t grid = l1_grid(n);
+  hipLaunchKernelGGL(l1_pow10_kernel, dim3((unsigned)grid), dim3(256), 0, s, y, mask,
+                     reinterpret_cast<const float2*>(target), n, loss + 1, dy, grad_scale);
+  hipLaunchKernelGGL(l1_sum_partials_kernel, dim3(1), dim3(256), 0, s, loss + 1, grid, loss);
   return check_launch("l1_pow10_loss");
 }
 

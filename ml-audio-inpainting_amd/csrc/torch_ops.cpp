@@ -375,6 +375,8 @@ void l1_pow10_loss(const Tensor& y, const Tensor& mask, const Tensor& target, co
   numel_is(target, n, "target");
   float* d = opt(dy, "dy");
   if (d) numel_is(*dy, n, "dy");
+  TORCH_CHECK(loss.numel() >= ainp_l1_pow10_loss_slots(n),
+              "l1_pow10_loss: loss needs ainp_l1_pow10_loss_slots(n) doubles");
   chk(ainp_l1_pow10_loss(dev(y, "y"), dev(mask, "mask"),
                          (const float*)dev<void>(target, "target", at::kComplexFloat), n,
                          dev<double>(loss, "loss", at::kDouble), d, (float)grad_scale,
@@ -788,6 +790,20 @@ void bn_relu_apply_ntcf_bf16(const Tensor& x, const Tensor& scale, const Tensor&
       "bn_relu_apply_ntcf_bf16");
 }
 
+// Split-column bias of the NT GEMMs: bias_a1/a2 cover columns [0, nsplit),
+// bias_b1/b2 columns [nsplit, N); every bias given must have that many entries.
+void check_nt_bias(const OptT& a1, const OptT& a2, const OptT& b1, const OptT& b2,
+                   int64_t nsplit, int64_t N, const char* op) {
+  const bool any = (a1.has_value() && a1->defined()) || (a2.has_value() && a2->defined()) ||
+                   (b1.has_value() && b1->defined()) || (b2.has_value() && b2->defined());
+  if (!any) return;
+  TORCH_CHECK(nsplit >= 0 && nsplit <= N, op, ": bias_nsplit must be in [0, N]");
+  if (a1.has_value() && a1->defined()) numel_is(*a1, nsplit, "bias_a1");
+  if (a2.has_value() && a2->defined()) numel_is(*a2, nsplit, "bias_a2");
+  if (b1.has_value() && b1->defined()) numel_is(*b1, N - nsplit, "bias_b1");
+  if (b2.has_value() && b2->defined()) numel_is(*b2, N - nsplit, "bias_b2");
+}
+
 void gemm_bf16nt(const Tensor& A, const Tensor& B, const Tensor& C, int64_t K,
                  const OptT& bias_a1, const OptT& bias_a2, const OptT& bias_b1,
                  const OptT& bias_b2, int64_t bias_nsplit, int64_t nsplit, int64_t kc) {
@@ -801,6 +817,7 @@ void gemm_bf16nt(const Tensor& A, const Tensor& B, const Tensor& C, int64_t K,
   TORCH_CHECK(C.size(-2) == M && C.size(-1) == N && C.stride(-1) == 1, "gemm_bf16nt: C shape");
   same_device(A, C);
   same_device(B, C);
+  check_nt_bias(bias_a1, bias_a2, bias_b1, bias_b2, bias_nsplit, N, "gemm_bf16nt");
   chk(ainp_gemm_bf16nt(M, N, K, bf16p(A, "A", false), A.stride(0), bf16p(B, "B", false),
                        B.stride(0), dev(C, "C", at::kFloat, false), C.stride(-2),
                        opt(bias_a1, "bias_a1"), opt(bias_a2, "bias_a2"), opt(bias_b1, "bias_b1"),
@@ -824,6 +841,7 @@ void gemm_x6nt_256(const Tensor& A, const Tensor& B1, const Tensor& B2, const Te
   same_device(A, C);
   same_device(B1, C);
   same_device(B2, C);
+  check_nt_bias(bias_a1, bias_a2, bias_b1, bias_b2, bias_nsplit, N, "gemm_x6nt_256");
   chk(ainp_gemm_x6nt_256(M, N, K, dev(A, "A", at::kFloat, false), A.stride(0),
                          dev(B1, "B1", at::kFloat, false), dev(B2, "B2", at::kFloat, false),
                          B1.stride(0), N1, dev(C, "C", at::kFloat, false), C.stride(-2),

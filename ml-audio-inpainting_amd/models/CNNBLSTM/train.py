@@ -40,6 +40,7 @@ from models.CNNBLSTM.dataset import LibriSpeechDataset  # noqa: E402
 from models.CNNBLSTM.model import StackedBLSTMCNN  # noqa: E402
 
 from ainp.cnnblstm import l1_pow10_loss  # noqa: E402
+from ainp.failfast import check_finite  # noqa: E402
 from ainp.dist import Comm, GradAllReducer, init_from_env  # noqa: E402
 from ainp.optim import Adam  # noqa: E402
 
@@ -156,8 +157,10 @@ def main(config_path="cnn_blstm.yaml"):
             loss.backward()
             if reducer is not None:
                 reducer.allreduce()
+            # the reference's per-step loss.item() (train.py:111), read before
+            # the optimizer step: a NaN/inf loss stops training (all DP ranks)
+            lv = check_finite(loss, "Train_Loss", global_step, comm)
             optimizer.step()
-            lv = loss.item()
             running_loss += lv
             if global_step % config["logging"]["metric_interval"] == 0:
                 writer.add_scalar("Train_Loss", lv, global_step)

@@ -201,7 +201,7 @@ def main(config_path="config.yaml"):
                                   use_spectral_norm=dcfg["use_spectral_norm"]).to(device)
     use_vgg = train_cfg["lambda_vgg_perceptual"] > 0 or train_cfg["lambda_vgg_style"] > 0
     vgg = VGGLoss(device=device, weights=train_cfg.get("vgg_weights")) if use_vgg else None
-    trainer = GanTrainer(cfg, generator, discriminator, vgg, comm=comm)
+    trainer = GanTrainer(cfg, generator, discriminator, vgg, comm=comm, fail_fast=True)
 
     start_epoch, global_step = 0, 0
     if resume_dir is not None and resume_dir.exists():

@@ -106,13 +106,15 @@ class Trainer:
     """One reference training step per call: zero_grad, forward, loss, backward,
     Adam step (train.py:96-108)."""
 
-    def __init__(self, params: dict, H: int, L: int, lr: float = 1e-4):
+    def __init__(self, params: dict, H: int, L: int, lr: float = 1e-4, frozen=()):
+        """frozen: parameter names left out of Adam (they still get .grad),
+        as tests/golden/gen_golden_r03.py does for the BN-fed conv biases."""
         self.p = params
         self.H, self.L = H, L
         self.keys = trainable_keys(params)
         for k in self.keys:
             self.p[k].requires_grad_(True)
-        self.opt = torch.optim.Adam([self.p[k] for k in self.keys], lr=lr)
+        self.opt = torch.optim.Adam([self.p[k] for k in self.keys if k not in frozen], lr=lr)
 
     def step(self, x, mask, target):
         self.opt.zero_grad()

@@ -1,0 +1,172 @@
+"""Round-3 golden fixtures.
+
+Run in the build container (where /root/reference exists):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden_r03.py [ganstep1001|curvefix ...]
+
+The reference's models/GAN/networks.py and models/CNNBLSTM/model.py are
+imported (never copied) and run on seeded inputs; only data is written:
+
+  gan_step_t1001.npz      one reference GAN step (models/GAN/train.py:341-378)
+                          at the C5 shape: B=2, 8 s clips (S=128000), hop 128,
+                          n_fft 512, 0.1 s gaps (g=1600), T=1001 (the U-Net pads
+                          W 1001 -> 1024, networks.py:255-261; D logits
+                          [2,1,30,123]).  Inputs are re-made in the test by the
+                          oracle's GAN data path (oracle/stft_ref.gan_item over
+                          ainp.synth clips) and checksummed.  Stored: generated
+                          sample/norm, D real/fake logits, D losses, every D
+                          gradient (norm + strided sample), D parameters after
+                          Adam, u/v after the third (G-step) D forward, G's BN
+                          running statistics, and the G-step losses from the
+                          oracle restatement with seeded VGG19 weights
+                          (oracle/gan_ref.vgg19_init: loss.py imports
+                          torchvision, absent here; pretrained values unpinned).
+  cnnblstm_curve_fixbias.npz
+                          the cnnblstm_curve.npz schedule (small config, 30
+                          Adam steps over 4 cycling batches, train.py:96-108)
+                          with the five conv biases that feed a BatchNorm
+                          (encoder.{0,3,6}.bias, decoder.{0,3}.bias) left out of
+                          the optimizer.  Their exact gradient is 0 (SURVEY
+                          Q10), so Adam would only move them on rounding noise;
+                          frozen, they stay at their initial values in the
+                          reference run and in the HIP run alike, and the BN
+                          running_mean they would shift can be compared at the
+                          1e-4 gate with no absolute allowance.
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "ml-audio-inpainting_amd"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from oracle import gan_ref, stft_ref  # noqa: E402
+from ainp import synth  # noqa: E402
+from golden.gen_golden_r02 import _load, _sample, checksum  # noqa: E402
+
+GSTEP1001 = dict(B=2, S=128000, g=1600, hop=128, n_fft=512, T=1001, clip_seed=51000,
+                 starts=(37000, 90000), g_seed=0, d_seed=1, vgg_seed=0)
+BN_FED = ("encoder.0.bias", "encoder.3.bias", "encoder.6.bias", "decoder.0.bias",
+          "decoder.3.bias")
+
+
+def gan_step1001_inputs():
+    """(orig, impaired, mask) [B,1,F,T] of the C5-shape GAN step."""
+    c = GSTEP1001
+    o, i, m = [], [], []
+    for b in range(c["B"]):
+        clip = synth.synthetic_clip(c["clip_seed"] + b, c["S"])
+        r0, r1, _, r3 = stft_ref.gan_item(clip, c["starts"][b], c["g"], c["n_fft"], c["hop"],
+                                          c["n_fft"])
+        o.append(r0); i.append(r1); m.append(r3)
+    f = lambda a: np.stack(a)[:, None].astype(np.float32)
+    return f(o), f(i), f(m)
+
+
+def gen_ganstep1001(net):
+    c = GSTEP1001
+    out = {}
+    orig, imp, mask = gan_step1001_inputs()
+    assert orig.shape == (c["B"], 1, 257, c["T"]), orig.shape
+    out["orig_check"], out["imp_check"], out["mask_check"] = (checksum(orig), checksum(imp),
+                                                              checksum(mask))
+    torch.manual_seed(c["g_seed"])
+    G = net.PConvUNet()
+    torch.manual_seed(c["d_seed"])
+    D = net.Discriminator()
+    G.train(); D.train()
+    O, I, M = (torch.from_numpy(a) for a in (orig, imp, mask))
+    bce = torch.nn.BCEWithLogitsLoss()
+    d_opt = torch.optim.Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    # ---- D step (train.py:348-363)
+    d_opt.zero_grad()
+    with torch.no_grad():
+        gen = G(I, M)
+    dr = D(O)
+    l_real = bce(dr, torch.ones_like(dr))
+    df = D(gen.detach())
+    l_fake = bce(df, torch.zeros_like(df))
+    d_loss = (l_real + l_fake) / 2
+    d_loss.backward()
+    gf = gen.numpy().reshape(-1)
+    out["gen_sample"] = gf[::97].copy()
+    out["gen_norm"] = np.array([np.linalg.norm(gf.astype(np.float64))])
+    out["d_real_logits"], out["d_fake_logits"] = dr.detach().numpy(), df.detach().numpy()
+    out["d_losses"] = np.array([d_loss.item(), l_real.item(), l_fake.item()])
+    for k, p in D.named_parameters():
+        g = p.grad.numpy()
+        out["d_gnorm/" + k] = np.array([np.linalg.norm(g.astype(np.float64))])
+        out["d_gsample/" + k] = _sample(g)
+    d_opt.step()
+    for k, v in D.state_dict().items():
+        out["d_after/" + k] = _sample(v.numpy())
+    for k, v in G.state_dict().items():
+        if "running" in k:
+            out["g_after/" + k] = v.numpy().copy()
+    # ---- G step forward (train.py:366-374): third D forward + losses
+    with torch.no_grad():
+        dfg = D(gen)
+    out["d_fake_g_logits"] = dfg.numpy()
+    for k, v in D.state_dict().items():
+        if k.endswith("weight_u") or k.endswith("weight_v"):
+            out["d_after_g/" + k] = v.numpy().copy()
+    pv = gan_ref.vgg19_init(c["vgg_seed"])
+    with torch.no_grad():
+        L = gan_ref.generator_losses(gen, O, M, dfg, pv)
+    for k, v in L.items():
+        out["oracle_loss/" + k] = np.array([float(v)])
+    out["config"] = np.array([c[k] for k in ("B", "S", "g", "hop", "n_fft", "T", "clip_seed")]
+                             + list(c["starts"]))
+    np.savez_compressed(os.path.join(HERE, "gan_step_t1001.npz"), **out)
+
+
+def gen_curvefix(mod, steps=30):
+    from golden.gen_golden import make_inputs, write_cfg
+    import tempfile
+    n_fft, hop, win, hidden, layers = 64, 16, 48, 32, 3
+    F, T, N = n_fft // 2 + 1, 24, 2
+    torch.manual_seed(4321)
+    with tempfile.TemporaryDirectory() as d:
+        cfgp = os.path.join(d, "cfg.yaml")
+        write_cfg(cfgp, n_fft, hidden, layers, [16, 32], [16, 32])
+        model = mod.StackedBLSTMCNN(cfgp)
+    model.train()
+    out = {"init/" + k: v.detach().numpy().copy() for k, v in model.state_dict().items()}
+    batches = [make_inputs(N, F, T, 30 + b, n_fft, hop, win) for b in range(4)]
+    for b, (x, m, t) in enumerate(batches):
+        out[f"x{b}"], out[f"mask{b}"], out[f"target{b}"] = x, m, t
+    crit = torch.nn.L1Loss(reduction="sum")
+    names = [k for k, _ in model.named_parameters()]
+    assert all(k in names for k in BN_FED)
+    opt = torch.optim.Adam([p for k, p in model.named_parameters() if k not in BN_FED], lr=1e-4)
+    losses = []
+    for s in range(steps):
+        x, m, t = (torch.from_numpy(a) for a in batches[s % 4])
+        opt.zero_grad()
+        y = model(x.unsqueeze(1))
+        loss = crit((10 ** y) * m, torch.abs(t) * m)
+        loss.backward()
+        opt.step()
+        losses.append(loss.item())
+    out["losses"] = np.array(losses)
+    for k, v in model.state_dict().items():
+        out["final/" + k] = v.detach().numpy().copy()
+    out["config"] = np.array([n_fft, hop, win, hidden, layers, N, T, steps])
+    out["frozen"] = np.array(BN_FED)
+    np.savez_compressed(os.path.join(HERE, "cnnblstm_curve_fixbias.npz"), **out)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1:] or ["ganstep1001", "curvefix"]
+    torch.set_num_threads(os.cpu_count() or 1)
+    if "curvefix" in what:
+        gen_curvefix(_load("models/CNNBLSTM/model.py", "ref_cnnblstm_model"))
+    if "ganstep1001" in what:
+        gen_ganstep1001(_load("models/GAN/networks.py", "ref_gan_networks"))
+    print("written:", what)

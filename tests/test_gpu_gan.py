@@ -412,31 +412,36 @@ def test_generator_and_discriminator_t1001_match_reference(golden_dir):
 
 
 # ------------------------------------------------------------- full-size GAN step
-@pytest.mark.timeout(600)
-def test_full_size_gan_step_matches_reference(golden_dir):
-    """One full-size GAN step (train.py:341-378) at B=2, T=626 on the GAN data
-    path (gan_step_full.npz from the reference's networks.py): generated
-    spectrogram, D logits and losses, every D gradient (norms and samples),
-    D parameters and u/v after Adam and after the G-step forward, G's
-    BatchNorm running statistics; the G-step losses (incl. VGG19 with seeded
-    weights, oracle/gan_ref.vgg19_init(0): pretrained weights parity-unpinned)
-    vs the oracle values stored with the fixture."""
+def _fixture_step(g, seeds, inputs, dtype=None):
+    """One GanTrainer step on a reference step fixture (gan_step_full.npz /
+    gan_step_t1001.npz) with the fixture's seeded G, D and VGG19 weights."""
     from ainp import gan as G
     from ainp.gan_train import GanTrainer
-    from golden.gen_golden_r02 import GSTEP, checksum, gan_step_inputs
-    g = np.load(os.path.join(golden_dir, "gan_step_full.npz"), allow_pickle=False)
-    orig, imp, mask = gan_step_inputs()
+    from golden.gen_golden_r02 import checksum
+    orig, imp, mask = inputs
     for a, k in ((orig, "orig_check"), (imp, "imp_check"), (mask, "mask_check")):
         assert np.allclose(checksum(a), g[k], rtol=1e-12, atol=0), k
-    torch.manual_seed(GSTEP["g_seed"])
+    torch.manual_seed(seeds["g_seed"])
     Gm = G.PConvUNet()
-    torch.manual_seed(GSTEP["d_seed"])
+    torch.manual_seed(seeds["d_seed"])
     Dm = G.Discriminator()
-    v, _ = _vgg_pair(GSTEP["vgg_seed"])
+    v, _ = _vgg_pair(seeds["vgg_seed"])
     cfg = {"training": dict(R.LAMBDAS, g_lr=2e-4, d_lr=2e-4, b1=0.5, b2=0.999)}
+    if dtype is not None:
+        cfg["accel"] = {"dtype": dtype}
     tr = GanTrainer(cfg, Gm.cuda(), Dm.cuda(), vgg=v)
+    if dtype == "bf16":
+        assert Dm.ainp_bf16 and v.ainp_bf16
     out = tr.step(torch.from_numpy(orig).cuda(), torch.from_numpy(imp).cuda(),
                   torch.from_numpy(mask).cuda())
+    return out, Gm, Dm
+
+
+def _check_fp32_step(g, out, Gm, Dm, param_tol=1e-5):
+    """param_tol: D parameters after Adam (samples).  Adam's first step moves
+    each weight by lr * g / (|g| + eps'), so weights whose gradient is within
+    a few eps of 0 carry most of the difference; 1e-5 holds at T=626, the
+    north-star 1e-4 gate at T=1001 (measured 6.3e-5 on layer 0)."""
     gf = out["generated"].cpu().numpy().reshape(-1)
     assert rel(gf[::97], g["gen_sample"]) < TOL
     assert abs(np.linalg.norm(gf.astype(np.float64)) - g["gen_norm"][0]) < TOL * g["gen_norm"][0]
@@ -461,11 +466,42 @@ def test_full_size_gan_step_matches_reference(golden_dir):
         elif k.startswith("d_after/") and "weight_u" not in k and "weight_v" not in k:
             t = sd[k[len("d_after/"):]].cpu().numpy()
             s = t.reshape(-1)[::max(1, t.size // 4096)]
-            assert rel(s, g[k]) < 1e-5, k
+            assert rel(s, g[k]) < param_tol, (k, rel(s, g[k]))
     for k in ("g_total", "g_adv", "g_l1_valid", "g_l1_hole", "g_mag_weighted",
               "g_vgg_perceptual", "g_vgg_style"):
         r = float(g["oracle_loss/" + k][0])
         assert abs(float(out[k]) - r) <= TOL * max(abs(r), 1e-6), (k, float(out[k]), r)
+
+
+# bf16 gate (bf16 cannot meet 1e-4): generated spectrogram, D loss
+# and the G-step losses within BF16_STEP_TOL relative of the fp32 reference.
+BF16_STEP_TOL = 2e-2
+
+
+def _check_bf16_step(g, out, tag):
+    gf = out["generated"].cpu().numpy().reshape(-1)
+    errs = {"generated": rel(gf[::97], g["gen_sample"]),
+            "d_loss": abs(float(out["d_loss"]) - g["d_losses"][0]) / abs(g["d_losses"][0])}
+    for k in ("g_total", "g_l1_valid", "g_l1_hole", "g_vgg_perceptual", "g_vgg_style"):
+        r = float(g["oracle_loss/" + k][0])
+        errs[k] = abs(float(out[k]) - r) / abs(r)
+    print(tag, "bf16 GAN step rel errs", errs)
+    assert max(errs.values()) < BF16_STEP_TOL, errs
+
+
+@pytest.mark.timeout(600)
+def test_full_size_gan_step_matches_reference(golden_dir):
+    """One full-size GAN step (train.py:341-378) at B=2, T=626 on the GAN data
+    path (gan_step_full.npz from the reference's networks.py): generated
+    spectrogram, D logits and losses, every D gradient (norms and samples),
+    D parameters and u/v after Adam and after the G-step forward, G's
+    BatchNorm running statistics; the G-step losses (incl. VGG19 with seeded
+    weights, oracle/gan_ref.vgg19_init(0): pretrained weights parity-unpinned)
+    vs the oracle values stored with the fixture."""
+    from golden.gen_golden_r02 import GSTEP, gan_step_inputs
+    g = np.load(os.path.join(golden_dir, "gan_step_full.npz"), allow_pickle=False)
+    out, Gm, Dm = _fixture_step(g, GSTEP, gan_step_inputs())
+    _check_fp32_step(g, out, Gm, Dm)
 
 
 @pytest.mark.timeout(600)
@@ -474,30 +510,32 @@ def test_full_size_gan_step_bf16_tracks_reference(golden_dir):
     (accel.dtype = bf16: bf16 conv / GEMM operands in G, D and VGG, fp32
     accumulation, BatchNorm statistics and weights): generated spectrogram,
     D losses and G-step losses within 2e-2 relative of the fp32 reference."""
-    from ainp import gan as G
-    from ainp.gan_train import GanTrainer
     from golden.gen_golden_r02 import GSTEP, gan_step_inputs
     g = np.load(os.path.join(golden_dir, "gan_step_full.npz"), allow_pickle=False)
-    orig, imp, mask = gan_step_inputs()
-    torch.manual_seed(GSTEP["g_seed"])
-    Gm = G.PConvUNet()
-    torch.manual_seed(GSTEP["d_seed"])
-    Dm = G.Discriminator()
-    v, _ = _vgg_pair(GSTEP["vgg_seed"])
-    cfg = {"training": dict(R.LAMBDAS, g_lr=2e-4, d_lr=2e-4, b1=0.5, b2=0.999),
-           "accel": {"dtype": "bf16"}}
-    tr = GanTrainer(cfg, Gm.cuda(), Dm.cuda(), vgg=v)
-    assert Dm.ainp_bf16 and v.ainp_bf16
-    out = tr.step(torch.from_numpy(orig).cuda(), torch.from_numpy(imp).cuda(),
-                  torch.from_numpy(mask).cuda())
-    gf = out["generated"].cpu().numpy().reshape(-1)
-    errs = {"generated": rel(gf[::97], g["gen_sample"]),
-            "d_loss": abs(float(out["d_loss"]) - g["d_losses"][0]) / abs(g["d_losses"][0])}
-    for k in ("g_total", "g_l1_valid", "g_l1_hole", "g_vgg_perceptual", "g_vgg_style"):
-        r = float(g["oracle_loss/" + k][0])
-        errs[k] = abs(float(out[k]) - r) / abs(r)
-    print("bf16 GAN step rel errs", errs)
-    assert max(errs.values()) < 2e-2, errs
+    out, _, _ = _fixture_step(g, GSTEP, gan_step_inputs(), dtype="bf16")
+    _check_bf16_step(g, out, "T=626")
+
+
+@pytest.mark.timeout(600)
+def test_c5_shape_gan_step_matches_reference(golden_dir):
+    """C5's own shape (8 s clips, T=1001, 0.1 s gaps, B=2; gan_step_t1001.npz
+    from the reference's networks.py): the same checks as the T=626 step at
+    the fp32 gate."""
+    from golden.gen_golden_r03 import GSTEP1001, gan_step1001_inputs
+    g = np.load(os.path.join(golden_dir, "gan_step_t1001.npz"), allow_pickle=False)
+    out, Gm, Dm = _fixture_step(g, GSTEP1001, gan_step1001_inputs())
+    assert tuple(out["generated"].shape) == (2, 1, 257, 1001)
+    _check_fp32_step(g, out, Gm, Dm, param_tol=TOL)
+
+
+@pytest.mark.timeout(600)
+def test_c5_shape_gan_step_bf16_tracks_reference(golden_dir):
+    """C5 in its own arithmetic: the bf16 configuration of the T=1001 step
+    within BF16_STEP_TOL of the reference's fp32 step."""
+    from golden.gen_golden_r03 import GSTEP1001, gan_step1001_inputs
+    g = np.load(os.path.join(golden_dir, "gan_step_t1001.npz"), allow_pickle=False)
+    out, _, _ = _fixture_step(g, GSTEP1001, gan_step1001_inputs(), dtype="bf16")
+    _check_bf16_step(g, out, "T=1001")
 
 
 @pytest.mark.parametrize("N,C,H,W,masked", [(2, 64, 17, 70, True), (1, 96, 5, 130, False),

@@ -92,3 +92,32 @@ def test_spectrogram_to_audio_paths():
     y4 = utils.spectrogram_to_audio(mag, n_fft=512, hop_length=128, n_iter=2, random_state=0)
     ref4 = stft_ref.griffinlim(mag.astype(np.float64), 2, 128, 512, 512, random_state=0)
     assert np.linalg.norm(y4 - ref4) / np.linalg.norm(ref4) < 1e-4
+
+
+@pytest.mark.timeout(300)
+def test_griffinlim_c5_shape_matches_oracle():
+    """BASELINE C5's on-GPU reconstruction at its own shape: a batch of 8
+    log1p-magnitude spectrograms of 8 s clips ([8, 257, 1001], n_fft 512,
+    hop 128, win 512), 64 Griffin-Lim iterations (GAN train.py sample audio,
+    utils.py:279-333) from supplied initial phases, against the float64
+    oracle.  Tolerance 1e-3 relative L2 per signal: the GPU iterates in fp32
+    (complex64 angles, float32 audio) over 64 momentum-0.99 iterations."""
+    from ainp import ops
+    B, S, hop, n_iter = 8, 128000, 128, 64
+    mags = np.stack([np.abs(stft_ref.stft(synth.synthetic_clip(700 + b, S).astype(np.float64),
+                                          512, hop, 512)) for b in range(B)]).astype(np.float32)
+    assert mags.shape == (B, 257, 1001)
+    rng = np.random.default_rng(5)
+    ph = 2 * np.pi * rng.random(mags.shape)
+    ang = (np.cos(ph) + 1j * np.sin(ph)).astype(np.complex64)
+    y = ops.griffinlim(torch.from_numpy(mags).cuda(), n_iter=n_iter, hop_length=hop,
+                       win_length=512, n_fft=512,
+                       init_angles=torch.from_numpy(ang).cuda()).cpu().numpy()
+    assert y.shape == (B, hop * 1000)
+    errs = []
+    for b in range(B):
+        ref = stft_ref.griffinlim(mags[b].astype(np.float64), n_iter, hop, 512, 512,
+                                  init_angles=ang[b].astype(np.complex128))
+        errs.append(np.linalg.norm(y[b] - ref) / np.linalg.norm(ref))
+    print("GL C5 rel errs", errs)
+    assert max(errs) < 1e-3, errs

@@ -576,6 +576,25 @@ def test_l1_pow10_loss(ops):
     assert rel(dy.cpu(), y.grad) < 1e-6
 
 
+def test_l1_pow10_loss_is_bit_reproducible(ops):
+    """The loss scalar is a fixed-order two-pass reduction (no fp64 atomics):
+    repeated evaluations at the C2 size (N=32, F=257, T=334; 2048 workgroup
+    partials) agree bit for bit; an empty input gives 0."""
+    g = torch.Generator().manual_seed(2)
+    n = (32, 257, 334)
+    y = (torch.randn(n, generator=g) * 0.5).to(DEV)
+    m = (torch.rand(n, generator=g) > 0.9).float().to(DEV)
+    t = torch.complex(torch.randn(n, generator=g), torch.randn(n, generator=g)).to(DEV)
+    vals = {ops.l1_pow10_loss(y, m, t, want_grad=False)[0].item() for _ in range(20)}
+    assert len(vals) == 1, vals
+    ref = ((10 ** y.double().cpu()) * m.double().cpu()
+           - t.abs().double().cpu() * m.double().cpu()).abs().sum().item()
+    assert abs(vals.pop() - ref) / ref < 1e-6
+    e = torch.empty(0, device=DEV)
+    l0, _ = ops.l1_pow10_loss(e, e, e.to(torch.complex64), want_grad=False)
+    assert l0.item() == 0.0
+
+
 @pytest.mark.parametrize("rows,cols,ld", [(10688, 1024, 1024), (10688, 512, 1024), (37, 130, 131),
                                            (5, 3, 3)])
 def test_colsum_fixed_order(ops, rows, cols, ld):
@@ -697,6 +716,18 @@ def test_gemm_bf16nt_split_projection_with_bias(M, N, K, S):
     torch.cuda.synchronize()
     err = (CS.double() - C1.double()).norm() / C1.double().norm()
     assert err < 1e-6, float(err)
+    # the slabs themselves: slab 0 = its K range + the bias, every other slab
+    # = the bias-free GEMM over its K range, bit for bit (same kernel, same k
+    # order), so the bias lands exactly once and exactly in slab 0
+    kc = -(-K // S // 64) * 64
+    slabs = torch.full((S, M, N), float("nan"), device="cuda")
+    torch.ops.ainp.gemm_bf16nt(A, B, slabs, K, *bias, nb, S, kc)
+    for s_ in range(S):
+        k0, k1 = s_ * kc, min(K, (s_ + 1) * kc)
+        part = ops.gemm_bf16nt(A[:, k0:], B[:, k0:], K=k1 - k0,
+                               bias=bias if s_ == 0 else (None,) * 4, bias_nsplit=nb)
+        torch.cuda.synchronize()
+        assert torch.equal(slabs[s_], part), s_
 
 
 def test_cast_bf16_t_and_ntcf_bf16_bridge_bit_exact():

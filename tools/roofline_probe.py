@@ -23,7 +23,7 @@ if bf16:
     W16 = torch.cat(W).bfloat16()
     for _ in range(reps):
         ops.gemm_bf16nt(A16, W16, out=zx, bias=tuple(b), bias_nsplit=4 * H,
-                        nsplit=ops.b16_proj_split(zx.shape[0], zx.shape[1]))
+                        nsplit=ops.b16_proj_split(zx.shape[0], zx.shape[1], A16.shape[1]))
 elif len(sys.argv) > 2 and sys.argv[2] == "fp32old":
     for _ in range(reps):
         ops.gemm(M, 4 * H, I, [A, A], I, 1, W, 1, I, [zx, zx[:, 4 * H:]], 8 * H, 1,
