@@ -349,6 +349,7 @@ def main():
     from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
     from ainp.dist import Comm, GradAllReducer, init_from_env
     from ainp.optim import Adam
+    from ainp.trace import phase
     import torch.distributed as dist
 
     rank, world, local = init_from_env()
@@ -382,14 +383,19 @@ def main():
     losses = torch.zeros(nsteps, device=dev)
 
     def step(i):
-        x, tgt, mask, _ = ops.stft_features(audio, starts[i], g, n_fft, hop, win, n_frames=T)
+        with phase("data"):
+            x, tgt, mask, _ = ops.stft_features(audio, starts[i], g, n_fft, hop, win, n_frames=T)
         opt.zero_grad()
-        y = model(x.unsqueeze(1))
-        loss = l1_pow10_loss(y, mask, tgt)
-        loss.backward()
+        with phase("fwd"):
+            y = model(x.unsqueeze(1))
+            loss = l1_pow10_loss(y, mask, tgt)
+        with phase("bwd"):
+            loss.backward()
         if reducer is not None:
-            reducer.allreduce()
-        opt.step()
+            with phase("allreduce"):
+                reducer.allreduce()
+        with phase("optimizer"):
+            opt.step()
         losses[i] = loss.detach()
 
     for i in range(args.warmup):
@@ -571,6 +577,7 @@ def run_gan(args):
     from ainp import gan as G
     from ainp.dist import Comm, init_from_env
     from ainp.gan_train import GanTrainer
+    from ainp.trace import phase
     import torch.distributed as dist
 
     rank, world, local = init_from_env()
@@ -598,8 +605,9 @@ def run_gan(args):
     last = {}
 
     def step(i):
-        o, im, ph, m = ops.stft_features(audio, starts[i], g, n_fft, hop, n_fft, n_frames=T,
-                                         mode=ops.FEAT_GAN, outputs=(True, True, c5, True))
+        with phase("data"):
+            o, im, ph, m = ops.stft_features(audio, starts[i], g, n_fft, hop, n_fft, n_frames=T,
+                                             mode=ops.FEAT_GAN, outputs=(True, True, c5, True))
         out = tr.step(o.unsqueeze(1), im.unsqueeze(1), m.unsqueeze(1))
         hole[i] = out["g_l1_hole"]
         last.update(orig=o, phase=ph, mask=m, gen=out["generated"])
@@ -640,9 +648,13 @@ def run_gan(args):
         ist_s = time_kernel(lambda: ops.istft(mag=mag, phase=last["phase"], n_fft=n_fft,
                                               hop_length=hop), 5, dev)
         gl_s = time_kernel(lambda: ops.griffinlim(mag, n_iter=64, hop_length=hop, n_fft=n_fft,
-                                                  random_state=0), 2, dev)
+                                                  random_state=0, init="device"), 3, dev)
         recon = {"istft_orig_phase_ms": round(ist_s * 1e3, 3),
                  "griffinlim64_ms": round(gl_s * 1e3, 3),
+                 "griffinlim_def": "64 iterations on the batch, initial phases drawn on the "
+                                   "device (init='device'), each iteration = ainp_istft + "
+                                   "ainp_gl_stft_update (n_fft=512 tiled STFT with the phase "
+                                   "update fused into its write-out)",
                  "batch": B, "samples_per_clip": hop * (T - 1)}
 
     roof = None

@@ -111,6 +111,16 @@ int ainp_istft(const void* in0, const void* in1, int mode, int64_t n_signals, in
 /* One Griffin-Lim phase update (librosa griffinlim, utils.py:330): a = rebuilt -
  * m/(1+m) * tprev (no tprev term when first != 0), angles = a / (|a| + tiny),
  * tprev = rebuilt; n complex64 elements (interleaved). */
+/* Griffin-Lim STFT + phase update in one launch (n_fft = 512, center, float32
+ * audio [n_signals][n_samples] -> n_frames frames; the tiled n_fft=512 STFT
+ * kernel with ainp_gl_update's arithmetic in its write-out): rebuilt =
+ * stft(audio); a = rebuilt - m/(1+m) * tprev (not when first != 0); angles =
+ * a / (|a| + tiny); tprev = rebuilt.  tprev / angles: complex64
+ * [n_signals][257][n_frames].  ainp_stft routes n_fft = 512 float32 center
+ * STFTs to the same kernel. */
+int ainp_gl_stft_update(const float* audio, int64_t n_signals, int64_t n_samples,
+                        const double* window, int hop, int64_t n_frames, float* tprev,
+                        float* angles, float momentum, int first, void* stream);
 int ainp_gl_update(const float* rebuilt, float* tprev, float* angles, int64_t n,
                    float momentum, int first, void* stream);
 
@@ -369,6 +379,14 @@ int ainp_lstm_rec_bwd(const float* dh_out, const float* gates,
  * sequence start): the right-hand operand of dW_hh = dgates^T * hprev. */
 int ainp_lstm_hprev(const float* h_out, float* hprev, int64_t N, int64_t T,
                     int H, void* stream);
+
+/* ------------------------------------------------------------------------ */
+/* Tracing: per-phase roctx ranges (data / fwd / bwd / all-reduce / */
+/* optimizer) for rocprofv3 --marker-trace.  push returns the nesting depth.  */
+/* ------------------------------------------------------------------------ */
+int ainp_range_push(const char* name);
+int ainp_range_pop(void);
+void ainp_mark(const char* name);
 
 /* ------------------------------------------------------------------------ */
 /* Loss, reductions, optimizer                                               */

@@ -35,6 +35,9 @@ _SIGS = {
     "ainp_abi_version": (c_int, []),
     "ainp_build_target": (c_char_p, []),
     "ainp_last_error": (c_char_p, []),
+    "ainp_range_push": (c_int, [c_char_p]),
+    "ainp_range_pop": (c_int, []),
+    "ainp_mark": (None, [c_char_p]),
     "ainp_stft_features": (c_int, [P, c_int64, c_int64, P, P, c_int64, c_int64, c_int64,
                                    P, c_int, c_int, c_int64, c_int, P, P, P, P, P]),
     "ainp_stft": (c_int, [P, c_int, c_int64, c_int64, P, c_int, c_int, c_int, c_int64, P, P]),
@@ -130,6 +133,8 @@ _SIGS = {
     "ainp_mul": (c_int, [P, P, c_int64, P, P]),
     "ainp_istft_workspace": (c_size_t, [c_int64, c_int64, c_int]),
     "ainp_l1_pow10_loss_slots": (c_int64, [c_int64]),
+    "ainp_gl_stft_update": (c_int, [P, c_int64, c_int64, P, c_int, c_int64, P, P, c_float, c_int,
+                                    P]),
     "ainp_istft": (c_int, [P, P, c_int, c_int64, c_int, c_int64, P, c_int, c_int, c_int, P, P,
                            P]),
     "ainp_gl_update": (c_int, [P, P, P, c_int64, c_float, c_int, P]),

@@ -19,6 +19,7 @@ import torch
 
 from . import gan as G
 from .optim import Adam
+from .trace import phase
 
 
 class GanTrainer:
@@ -68,25 +69,30 @@ class GanTrainer:
         self.D.train()
         # ---- discriminator step (train.py:348-363)
         self.d_opt.zero_grad()
-        with torch.no_grad():
-            generated = self.G(impaired_mag, mask)
-        d_real = self.D(original_mag)
-        l_real = G.bce_with_logits_const(d_real, 1.0)
-        d_fake = self.D(generated)
-        l_fake = G.bce_with_logits_const(d_fake, 0.0)
-        d_loss = (l_real + l_fake) / 2
-        d_loss.backward()
+        with phase("fwd_G"):
+            with torch.no_grad():
+                generated = self.G(impaired_mag, mask)
+        with phase("fwd_D"):
+            d_real = self.D(original_mag)
+            l_real = G.bce_with_logits_const(d_real, 1.0)
+            d_fake = self.D(generated)
+            l_fake = G.bce_with_logits_const(d_fake, 0.0)
+            d_loss = (l_real + l_fake) / 2
+        with phase("bwd_D"):
+            d_loss.backward()
         if self.reducer is not None:
-            # the reference loss is a per-rank mean: DP averages D's gradients
-            self.reducer.allreduce()
-            for p in self.D.parameters():
-                if p.grad is not None:
-                    p.grad.div_(self.comm.world_size)
+            with phase("allreduce"):
+                # the reference loss is a per-rank mean: DP averages D's gradients
+                self.reducer.allreduce()
+                for p in self.D.parameters():
+                    if p.grad is not None:
+                        p.grad.div_(self.comm.world_size)
         if self.fail_fast:
             from .failfast import check_finite
             check_finite(d_loss, "D loss", self.nstep, self.comm)
         self.nstep += 1
-        self.d_opt.step()
+        with phase("optimizer"):
+            self.d_opt.step()
         # ---- generator step (train.py:366-378)
         self.g_opt.zero_grad()
         if self.faithful:
@@ -103,7 +109,7 @@ class GanTrainer:
                 if self.reducer is not None:
                     self.reducer.paused = False
         else:
-            with torch.no_grad():
+            with torch.no_grad(), phase("g_losses"):
                 d_fake_g = self.D(generated)
                 losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g,
                                             self.vgg, comm=self.comm)

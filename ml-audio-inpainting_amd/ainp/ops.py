@@ -1188,12 +1188,16 @@ def istft(spec=None, *, mag=None, angles=None, phase=None, n_fft=None, hop_lengt
 
 
 def griffinlim(S, n_iter=32, hop_length=None, win_length=None, n_fft=None, window="hann",
-               center=True, momentum=0.99, random_state=None, init_angles=None):
+               center=True, momentum=0.99, random_state=None, init_angles=None, init="numpy"):
     """librosa>=0.10 griffinlim (init='random') on the GPU: S [F, T] or [B, F, T]
-    float32 magnitudes.  The initial phases come from
-    np.random.default_rng(random_state).random(S.shape) exactly as librosa draws
-    them (or pass init_angles, complex64).  Each iteration = ainp_istft (S *
-    angles) + ainp_stft + ainp_gl_update."""
+    float32 magnitudes.  Initial phases: init_angles (complex64, any device),
+    else init="numpy" draws them exactly as librosa does
+    (np.random.default_rng(random_state).random(S.shape), on the host, then one
+    copy), or init="device" draws them on the GPU (torch.rand with a
+    torch.Generator seeded by random_state: same distribution, different
+    stream -- no host work).  Each iteration = ainp_istft (S * angles) + the
+    STFT with the phase update fused into its write-out (ainp_gl_stft_update,
+    n_fft = 512 center float32; ainp_stft + ainp_gl_update otherwise)."""
     _req(S, "S")
     F, T = S.shape[-2:]
     n_fft = 2 * (F - 1) if n_fft is None else n_fft
@@ -1204,15 +1208,31 @@ def griffinlim(S, n_iter=32, hop_length=None, win_length=None, n_fft=None, windo
     if momentum < 0:
         raise ValueError("momentum must be non-negative")
     if init_angles is None:
-        rng = np.random.default_rng(seed=random_state)
-        ph = 2 * np.pi * rng.random(size=tuple(S.shape))
-        init_angles = torch.from_numpy((np.cos(ph) + 1j * np.sin(ph)).astype(np.complex64))
+        if init == "device":
+            gen = torch.Generator(device=S.device)
+            gen.manual_seed(0 if random_state is None else int(random_state))
+            ph = (2 * np.pi) * torch.rand(tuple(S.shape), device=S.device, generator=gen,
+                                          dtype=torch.float64)
+            init_angles = torch.polar(torch.ones_like(ph), ph).to(torch.complex64)
+        elif init == "numpy":
+            rng = np.random.default_rng(seed=random_state)
+            ph = 2 * np.pi * rng.random(size=tuple(S.shape))
+            init_angles = torch.from_numpy((np.cos(ph) + 1j * np.sin(ph)).astype(np.complex64))
+        else:
+            raise ValueError("init must be 'numpy' or 'device'")
     angles = init_angles.to(S.device, torch.complex64).contiguous().clone()
-    tprev = torch.zeros_like(angles)
+    tprev = torch.empty_like(angles)
+    fused = n_fft == 512 and center and window == "hann"
+    w = _device_window(window, win_length, n_fft, S.device) if fused else None
+    nsig = int(np.prod(S.shape[:-2])) if S.dim() > 2 else 1
     for it in range(n_iter):
         inv = istft(mag=S, angles=angles, n_fft=n_fft, hop_length=hop_length,
                     win_length=win_length, window=window, center=center)
-        rebuilt = stft(inv, n_fft, hop_length, win_length, window, center)
-        _T.gl_update(rebuilt, tprev, angles, float(momentum), it == 0)
+        if fused:
+            _T.gl_stft_update(inv.reshape(nsig, -1), w, int(hop_length), T, tprev, angles,
+                              float(momentum), it == 0)
+        else:
+            rebuilt = stft(inv, n_fft, hop_length, win_length, window, center)
+            _T.gl_update(rebuilt, tprev, angles, float(momentum), it == 0)
     return istft(mag=S, angles=angles, n_fft=n_fft, hop_length=hop_length,
                  win_length=win_length, window=window, center=center)

@@ -303,7 +303,7 @@ __device__ __forceinline__ Tile make_tile(int v, int ntiles, int ntt, int NF, in
   T.t0 = (tile - T.b * ntt) * TF;
   const int64_t clip = clip_index ? (int64_t)clip_index[T.b] : T.b;
   T.x = audio + clip * n_samples;
-  T.gs64 = gap_start[T.b];
+  T.gs64 = gap_start ? gap_start[T.b] : 0;
   T.ge64 = T.gs64 + gap_len;
   const int n_avail = 1 + ns / hop;
   T.nvalid = min(TF, NF - T.t0);
@@ -454,13 +454,23 @@ __device__ __forceinline__ float lm_cnn(double Xr, double Xi) {
          0.30102999566398120f;
 }
 
+// Modes beyond the two feature modes (include/ainp.h):
+//   F512_PLAIN  out0 = complex64 X [batch][257][n_frames] (librosa.stft, center,
+//               zero padding) -- ainp_stft for n_fft = 512 float32
+//   F512_GL     one Griffin-Lim phase update fused into the write-out
+//               (librosa griffinlim): rebuilt = X; a = rebuilt - m/(1+m) tprev
+//               (not on the first iteration); angles (out1) = a / (|a| + tiny);
+//               tprev (out0, read and written) = rebuilt
+constexpr int F512_PLAIN = 2, F512_GL = 3;
+
 template <int MODE, bool VEC2>
 __global__ __launch_bounds__(NT, 2) void stft512_kernel(
     const float* __restrict__ audio, int64_t n_samples, const int32_t* __restrict__ clip_index,
     const int64_t* __restrict__ gap_start, int64_t batch, int64_t gap_len, int64_t sample_rate,
     const double* __restrict__ window, int hop, int64_t n_frames, int64_t n_tiles_t,
     float* __restrict__ out0, float* __restrict__ out1, float* __restrict__ out2,
-    float* __restrict__ out3) {
+    float* __restrict__ out3, float gl_c = 0.f, int gl_first = 0) {
+  constexpr bool FEAT = MODE == AINP_FEAT_CNNBLSTM || MODE == AINP_FEAT_GAN;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* P0 = reinterpret_cast<float*>(smem);
   float2* PC = reinterpret_cast<float2*>(smem + LDS_P0);
@@ -473,9 +483,12 @@ __global__ __launch_bounds__(NT, 2) void stft512_kernel(
   const int j0 = lane & 15, myjob0 = wave * 4 + (lane >> 4);
   const int ntt = (int)n_tiles_t, NF = (int)n_frames, ns = (int)n_samples;
   const int ntiles = (int)(batch * n_tiles_t);
-  const bool want_lm = MODE == AINP_FEAT_CNNBLSTM ? out0 != nullptr : out1 != nullptr;
-  const bool want_fft = MODE == AINP_FEAT_CNNBLSTM ? (out0 || out1) : (out0 || out1 || out2);
-  float* mask_out = MODE == AINP_FEAT_CNNBLSTM ? out2 : out3;
+  const bool want_lm = !FEAT ? false
+                       : MODE == AINP_FEAT_CNNBLSTM ? out0 != nullptr : out1 != nullptr;
+  const bool want_fft = MODE == F512_GL ? true
+                        : MODE == F512_PLAIN ? out0 != nullptr
+                        : MODE == AINP_FEAT_CNNBLSTM ? (out0 || out1) : (out0 || out1 || out2);
+  float* mask_out = !FEAT ? nullptr : MODE == AINP_FEAT_CNNBLSTM ? out2 : out3;
   const int n_avail = 1 + ns / hop;
   {
     double s, c;
@@ -529,7 +542,11 @@ __global__ __launch_bounds__(NT, 2) void stft512_kernel(
       __syncthreads();  // every transpose slot is read (they alias PC)
       const bool own_lm = act_b && !(myjob >= T.ga && myjob < T.gb);
       const bool zero_lm = !act_b;
-      if (MODE == AINP_FEAT_CNNBLSTM) {
+      if (!FEAT) {
+        unpack(re, im, j, lane, ujr, uji, [&](int f, double Xr, double Xi) {
+          PC[sw(f, myjob)] = act_b ? make_float2((float)Xr, (float)Xi) : make_float2(0.f, 0.f);
+        });
+      } else if (MODE == AINP_FEAT_CNNBLSTM) {
         unpack(re, im, j, lane, ujr, uji, [&](int f, double Xr, double Xi) {
           const int l = sw(f, myjob);
           PC[l] = act_b ? make_float2((float)Xr, (float)Xi) : make_float2(0.f, 0.f);
@@ -550,7 +567,28 @@ __global__ __launch_bounds__(NT, 2) void stft512_kernel(
     // coalesced write-out: thread (row, col) -> runs of TF consecutive frames
     int col = tid % TF, row0 = tid / TF;
     asm volatile("" : "+v"(col), "+v"(row0));
-    if (col < T.nvalid) {
+    if (!FEAT && col < T.nvalid) {
+      const size_t base = (size_t)T.b * F * n_frames + T.t0 + col;
+      float2* o0 = reinterpret_cast<float2*>(out0);
+      float2* o1 = reinterpret_cast<float2*>(out1);
+      for (int f = row0; f < F; f += NT / TF) {
+        const size_t o = base + (size_t)f * n_frames;
+        const float2 x = PC[sw(f, col)];
+        if (MODE == F512_PLAIN) {
+          o0[o] = x;
+        } else {
+          float ar = x.x, ai = x.y;
+          if (!gl_first) {
+            const float2 tp = o0[o];
+            ar -= gl_c * tp.x;
+            ai -= gl_c * tp.y;
+          }
+          const float mag = sqrtf(ar * ar + ai * ai) + 1.17549435e-38f;
+          o1[o] = make_float2(ar / mag, ai / mag);
+          o0[o] = x;
+        }
+      }
+    } else if (FEAT && col < T.nvalid) {
       const int t = T.t0 + col;
       float maskv;
       if (MODE == AINP_FEAT_CNNBLSTM) {
@@ -671,6 +709,20 @@ __global__ __launch_bounds__(256) void stft_plain_kernel(
 
 using namespace ainp;
 
+// persistent grid of the n_fft = 512 kernel: two workgroups per CU
+static int64_t f512_grid(int64_t ntiles) {
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0, cu = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+      n_cu = cu > 0 ? cu : 256;
+    else
+      n_cu = 256;
+  }
+  return min(ntiles, (int64_t)2 * n_cu);
+}
+
 extern "C" int ainp_stft_features(const float* audio, int64_t n_clips,
                                   int64_t n_samples, const int32_t* clip_index,
                                   const int64_t* gap_start, int64_t batch,
@@ -697,16 +749,7 @@ extern "C" int ainp_stft_features(const float* audio, int64_t n_clips,
     if (ntiles > 0x7fffffff) return record_msg("ainp_stft_features: too many frames");
     // persistent: two workgroups per CU walk the tiles (more do not fit the
     // VGPR budget); AINP_STFT_GRID overrides for tuning
-    static int n_cu = 0;
-    if (n_cu == 0) {
-      int dev = 0, cu = 0;
-      if (hipGetDevice(&dev) == hipSuccess &&
-          hipDeviceGetAttribute(&cu, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-        n_cu = cu > 0 ? cu : 256;
-      else
-        n_cu = 256;
-    }
-    int64_t grid = min(ntiles, (int64_t)2 * n_cu);
+    int64_t grid = f512_grid(ntiles);
     const char* ps = getenv("AINP_STFT_GRID");
     if (ps && atoi(ps) > 0) grid = min(ntiles, (int64_t)atoi(ps));
     const bool vec2 = (hop % 2 == 0) && (n_samples % 2 == 0) &&
@@ -749,6 +792,45 @@ extern "C" int ainp_stft_features(const float* audio, int64_t n_clips,
   return check_launch("ainp_stft_features");
 }
 
+// n_fft = 512, center, float32 input on the tiled kernel (MODE F512_PLAIN or F512_GL)
+template <int MODE>
+static int f512_launch(const float* audio, int64_t n_signals, int64_t n_samples,
+                       const double* window, int hop, int64_t n_frames, float* out0, float* out1,
+                       float gl_c, int gl_first, hipStream_t s) {
+  if (n_samples >= (1 << 30) || n_frames * hop >= (1 << 30))
+    return record_msg("ainp_stft: signal too long for the n_fft=512 kernel");
+  const int64_t ntt = cdiv(n_frames, f512::TF);
+  const int64_t ntiles = n_signals * ntt;
+  if (ntiles > 0x7fffffff) return record_msg("ainp_stft: too many frames");
+  const int64_t grid = f512_grid(ntiles);
+  const bool vec2 = (hop % 2 == 0) && (n_samples % 2 == 0) &&
+                    ((reinterpret_cast<uintptr_t>(audio) & 7) == 0);
+  if (vec2)
+    hipLaunchKernelGGL((f512::stft512_kernel<MODE, true>), dim3(grid), dim3(f512::NT),
+                       f512::LDS_BYTES, s, audio, n_samples, nullptr, nullptr, n_signals,
+                       (int64_t)0, (int64_t)1, window, hop, n_frames, ntt, out0, out1, nullptr,
+                       nullptr, gl_c, gl_first);
+  else
+    hipLaunchKernelGGL((f512::stft512_kernel<MODE, false>), dim3(grid), dim3(f512::NT),
+                       f512::LDS_BYTES, s, audio, n_samples, nullptr, nullptr, n_signals,
+                       (int64_t)0, (int64_t)1, window, hop, n_frames, ntt, out0, out1, nullptr,
+                       nullptr, gl_c, gl_first);
+  return check_launch("ainp_stft (n_fft 512)");
+}
+
+extern "C" int ainp_gl_stft_update(const float* audio, int64_t n_signals, int64_t n_samples,
+                                   const double* window, int hop, int64_t n_frames,
+                                   float* tprev, float* angles, float momentum, int first,
+                                   void* stream) {
+  if (!audio || !window || !tprev || !angles || n_signals < 0 || n_samples <= 0 || hop <= 0 ||
+      n_frames < 0 || n_frames > 1 + n_samples / hop)
+    return record_msg("ainp_gl_stft_update: bad argument");
+  if (n_signals == 0 || n_frames == 0) return AINP_OK;
+  return f512_launch<f512::F512_GL>(audio, n_signals, n_samples, window, hop, n_frames, tprev,
+                                    angles, momentum / (1.f + momentum), first,
+                                    as_stream(stream));
+}
+
 extern "C" int ainp_stft(const void* audio, int dtype, int64_t n_signals,
                          int64_t n_samples, const double* window, int n_fft,
                          int hop, int center, int64_t n_frames, void* out,
@@ -759,6 +841,12 @@ extern "C" int ainp_stft(const void* audio, int dtype, int64_t n_signals,
   if (n_fft < 16 || n_fft > 2048 || (n_fft & (n_fft - 1)))
     return record_msg("ainp_stft: n_fft must be a power of two in [16,2048]");
   if (n_signals == 0 || n_frames == 0) return AINP_OK;
+  const char* gen = getenv("AINP_STFT_GENERIC");  // 1: force the generic kernel (tests)
+  if (n_fft == 512 && dtype == 0 && center && n_frames <= 1 + n_samples / hop &&
+      !(gen && gen[0] == '1'))
+    return f512_launch<f512::F512_PLAIN>((const float*)audio, n_signals, n_samples, window, hop,
+                                         n_frames, (float*)out, nullptr, 0.f, 0,
+                                         as_stream(stream));
   const int M = n_fft / 2;
   int log2m = 0;
   while ((1 << log2m) < M) ++log2m;

@@ -136,6 +136,22 @@ void istft(const Tensor& in0, const OptT& in1, int64_t mode, int64_t n_bins, int
       "istft");
 }
 
+void gl_stft_update(const Tensor& audio, const Tensor& window, int64_t hop, int64_t n_frames,
+                    const Tensor& tprev, const Tensor& angles, double momentum, bool first) {
+  GUARD(audio);
+  TORCH_CHECK(audio.dim() == 2, "audio must be [n_signals, n_samples]");
+  const int64_t n = audio.size(0) * 257 * n_frames;
+  numel_is(tprev, n, "tprev");
+  numel_is(angles, n, "angles");
+  numel_is(window, 512, "window");
+  chk(ainp_gl_stft_update(dev(audio, "audio"), audio.size(0), audio.size(1),
+                          dev<double>(window, "window", at::kDouble), (int)hop, n_frames,
+                          (float*)dev<void>(tprev, "tprev", at::kComplexFloat),
+                          (float*)dev<void>(angles, "angles", at::kComplexFloat), (float)momentum,
+                          first ? 1 : 0, stream_of(audio)),
+      "gl_stft_update");
+}
+
 void gl_update(const Tensor& rebuilt, const Tensor& tprev, const Tensor& angles, double momentum,
                bool first) {
   GUARD(rebuilt);
@@ -1066,6 +1082,8 @@ TORCH_LIBRARY(ainp, m) {
         "int n_fft, int hop, bool center, Tensor(a!) workspace, Tensor(b!) out) -> ()");
   m.def("gl_update(Tensor rebuilt, Tensor(a!) tprev, Tensor(b!) angles, float momentum, "
         "bool first) -> ()");
+  m.def("gl_stft_update(Tensor audio, Tensor window, int hop, int n_frames, Tensor(a!) tprev, "
+        "Tensor(b!) angles, float momentum, bool first) -> ()");
   m.def("gemm(int M, int N, int K, float alpha, Tensor[] A, int sam, int sak, int strideA, "
         "Tensor[] B, int sbk, int sbn, int strideB, float beta, Tensor(a!)[] C, int scm, int scn, "
         "int strideC, Tensor?[] bias1, Tensor?[] bias2, int nstrided, int ksplit, int flags, "
@@ -1163,6 +1181,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("stft", &stft);
   m.impl("istft", &istft);
   m.impl("gl_update", &gl_update);
+  m.impl("gl_stft_update", &gl_stft_update);
   m.impl("gemm", &gemm);
   m.impl("conv3x3_fwd", &conv3x3_fwd);
   m.impl("conv3x3_dgrad", &conv3x3_dgrad);
@@ -1227,6 +1246,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("stft", torch::CppFunction::makeFallthrough());
   m.impl("istft", torch::CppFunction::makeFallthrough());
   m.impl("gl_update", torch::CppFunction::makeFallthrough());
+  m.impl("gl_stft_update", torch::CppFunction::makeFallthrough());
   m.impl("gemm", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_fwd", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_dgrad", torch::CppFunction::makeFallthrough());

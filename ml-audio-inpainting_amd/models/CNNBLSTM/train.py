@@ -41,6 +41,7 @@ from models.CNNBLSTM.model import StackedBLSTMCNN  # noqa: E402
 
 from ainp.cnnblstm import l1_pow10_loss  # noqa: E402
 from ainp.failfast import check_finite  # noqa: E402
+from ainp.trace import phase  # noqa: E402
 from ainp.dist import Comm, GradAllReducer, init_from_env  # noqa: E402
 from ainp.optim import Adam  # noqa: E402
 
@@ -150,17 +151,22 @@ def main(config_path="cnn_blstm.yaml"):
         model.train()
         running_loss = 0.0
         for batch_idx, batch in enumerate(train_loader):
-            x, _, mask, target = _flatten(batch)
+            with phase("data"):
+                x, _, mask, target = _flatten(batch)
             optimizer.zero_grad()
-            y = model(x.unsqueeze(1))
-            loss = l1_pow10_loss(y, mask, target)
-            loss.backward()
+            with phase("fwd"):
+                y = model(x.unsqueeze(1))
+                loss = l1_pow10_loss(y, mask, target)
+            with phase("bwd"):
+                loss.backward()
             if reducer is not None:
-                reducer.allreduce()
+                with phase("allreduce"):
+                    reducer.allreduce()
             # the reference's per-step loss.item() (train.py:111), read before
             # the optimizer step: a NaN/inf loss stops training (all DP ranks)
             lv = check_finite(loss, "Train_Loss", global_step, comm)
-            optimizer.step()
+            with phase("optimizer"):
+                optimizer.step()
             running_loss += lv
             if global_step % config["logging"]["metric_interval"] == 0:
                 writer.add_scalar("Train_Loss", lv, global_step)

@@ -121,3 +121,44 @@ def test_griffinlim_c5_shape_matches_oracle():
         errs.append(np.linalg.norm(y[b] - ref) / np.linalg.norm(ref))
     print("GL C5 rel errs", errs)
     assert max(errs) < 1e-3, errs
+
+
+@pytest.mark.parametrize("hop,win,S", [(128, 512, 128000), (192, 384, 64000), (128, 512, 1000)])
+def test_stft512_plain_mode_matches_oracle_and_generic(hop, win, S, monkeypatch):
+    """ainp_stft at n_fft = 512 (float32, center) runs on the tiled n_fft=512
+    kernel (F512_PLAIN mode): complex64 spectrum vs the float64 oracle
+    (librosa>=0.10 stft restated) within 2e-6 of max|X|, and vs the generic
+    radix-2 kernel (AINP_STFT_GENERIC=1) to fp32 rounding."""
+    from ainp import ops
+    B = 3
+    xs = np.stack([synth.synthetic_clip(40 + b, S) for b in range(B)]).astype(np.float32)
+    X = ops.stft(torch.from_numpy(xs).cuda(), 512, hop, win).cpu().numpy()
+    ref = np.stack([stft_ref.stft(xs[b].astype(np.float64), 512, hop, win) for b in range(B)])
+    assert X.shape == ref.shape == (B, 257, 1 + S // hop)
+    assert np.abs(X - ref).max() <= 2e-6 * np.abs(ref).max()
+    monkeypatch.setenv("AINP_STFT_GENERIC", "1")
+    Xg = ops.stft(torch.from_numpy(xs).cuda(), 512, hop, win).cpu().numpy()
+    assert np.abs(X - Xg).max() <= 1e-6 * np.abs(ref).max()
+
+
+def test_gl_stft_update_equals_stft_then_update():
+    """ainp_gl_stft_update (the STFT with the Griffin-Lim phase update fused
+    into its write-out) == ainp_stft followed by ainp_gl_update, bit for bit,
+    on the first and on a later iteration."""
+    from ainp import ops
+    B, S, hop = 2, 16000, 128
+    x = torch.from_numpy(np.stack([synth.synthetic_clip(60 + b, S) for b in range(B)])
+                         .astype(np.float32)).cuda()
+    T = 1 + S // hop
+    w = ops._device_window("hann", 512, 512, x.device)
+    g = torch.Generator().manual_seed(3)
+    tp0 = torch.randn(B, 257, T, 2, generator=g).cuda()
+    tp0 = torch.view_as_complex(tp0).contiguous()
+    for first in (True, False):
+        tp_a, an_a = tp0.clone(), torch.empty_like(tp0)
+        rebuilt = ops.stft(x, 512, hop, 512)
+        torch.ops.ainp.gl_update(rebuilt, tp_a, an_a, 0.99, first)
+        tp_b, an_b = tp0.clone(), torch.empty_like(tp0)
+        torch.ops.ainp.gl_stft_update(x, w, hop, T, tp_b, an_b, 0.99, first)
+        torch.cuda.synchronize()
+        assert torch.equal(tp_a, tp_b) and torch.equal(an_a, an_b), first
