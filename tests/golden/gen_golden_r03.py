@@ -31,6 +31,20 @@ imported (never copied) and run on seeded inputs; only data is written:
                           reference run and in the HIP run alike, and the BN
                           running_mean they would shift can be compared at the
                           1e-4 gate with no absolute allowance.
+  cnnblstm_c2_bf16sens.npz
+                          conditioning of the C2 gradients (VERDICT r02 item 1:
+                          a stated bf16 bound for the bf16 C2 backward): the
+                          reference's model.py at the C2 batch (cnnblstm_c2.npz
+                          inputs and seed-0 weights) in fp32 on the CPU, once
+                          with every weight rounded to bf16 and once with the
+                          input spectrogram rounded to bf16 -- perturbations of
+                          the size bf16 operands make.  Stored per parameter:
+                          (norm rel err, sample rel err) of those gradients
+                          against the unperturbed reference gradients.  The
+                          layer-0 forward-direction LSTM and encoder gradients
+                          move by 10-40 % under such a perturbation: that is the
+                          model's conditioning, and the bound the bf16 GPU test
+                          applies to them.
 """
 from __future__ import annotations
 
@@ -162,9 +176,105 @@ def gen_curvefix(mod, steps=30):
     np.savez_compressed(os.path.join(HERE, "cnnblstm_curve_fixbias.npz"), **out)
 
 
+def gen_bf16sens(mod):
+    import tempfile
+    from golden.gen_golden_r02 import c2_config, c2_inputs, _write_cfg
+    g = np.load(os.path.join(HERE, "cnnblstm_c2.npz"), allow_pickle=False)
+    x, m, t, _ = c2_inputs()
+    out = {}
+
+    def grads(round_w, round_x):
+        with tempfile.TemporaryDirectory() as d:
+            cfgp = os.path.join(d, "cfg.yaml")
+            _write_cfg(cfgp, c2_config())
+            torch.manual_seed(0)
+            model = mod.StackedBLSTMCNN(cfgp)
+        model.train()
+        if round_w:
+            with torch.no_grad():
+                for p in model.parameters():
+                    p.copy_(p.bfloat16().float())
+        X = torch.from_numpy(x)
+        if round_x:
+            X = X.bfloat16().float()
+        y = model(X.unsqueeze(1))
+        loss = torch.nn.L1Loss(reduction="sum")((10 ** y) * torch.from_numpy(m),
+                                                torch.abs(torch.from_numpy(t)) * torch.from_numpy(m))
+        loss.backward()
+        return {k: p.grad.double().numpy() for k, p in model.named_parameters()}
+
+    def rel(a, b):
+        return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+    def emu_grads():
+        """The bf16 configuration's arithmetic emulated on the reference model:
+        every conv / Linear / LSTM input-projection operand (activation and
+        weight, and the gradients flowing back into them) rounded to bf16,
+        fp32 accumulation; LSTM recurrence, cell state, BatchNorm and loss in
+        fp32 (csrc/gemm16.hip, conv_x6.hip NP=1, lstm.hip)."""
+        import torch.nn.functional as F
+        with tempfile.TemporaryDirectory() as d:
+            cfgp = os.path.join(d, "cfg.yaml")
+            _write_cfg(cfgp, c2_config())
+            torch.manual_seed(0)
+            model = mod.StackedBLSTMCNN(cfgp)
+        model.train()
+        r = lambda a: a.bfloat16().float()      # noqa: E731  (grad rounded too)
+        for mm in model.modules():
+            if isinstance(mm, torch.nn.Conv2d):
+                mm.forward = (lambda c: lambda z: F.conv2d(r(z), r(c.weight), c.bias,
+                                                           padding=1))(mm)
+        lin = model.projection
+        lin.forward = lambda z: F.linear(r(z), r(lin.weight), lin.bias)
+        lstm = model.lstm
+        H = lstm.hidden_size
+
+        def lstm_fwd(z):
+            N, T, _ = z.shape
+            inp = z
+            for l in range(lstm.num_layers):
+                outs = []
+                for sfx in ("", "_reverse"):
+                    wi, wh = getattr(lstm, f"weight_ih_l{l}{sfx}"), getattr(lstm, f"weight_hh_l{l}{sfx}")
+                    bi, bh = getattr(lstm, f"bias_ih_l{l}{sfx}"), getattr(lstm, f"bias_hh_l{l}{sfx}")
+                    zx = F.linear(r(inp), r(wi), bi) + bh
+                    h = torch.zeros(N, H)
+                    c = torch.zeros(N, H)
+                    hs = [None] * T
+                    order = range(T) if sfx == "" else range(T - 1, -1, -1)
+                    for t in order:
+                        gt = zx[:, t] + h @ wh.t()
+                        i, f, gg, o = gt.chunk(4, 1)
+                        c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+                        h = torch.sigmoid(o) * torch.tanh(c)
+                        hs[t] = h
+                    outs.append(torch.stack(hs, 1))
+                inp = torch.cat(outs, 2)
+            return inp, None
+        lstm.forward = lstm_fwd
+        y = model(torch.from_numpy(x).unsqueeze(1))
+        loss = torch.nn.L1Loss(reduction="sum")((10 ** y) * torch.from_numpy(m),
+                                                torch.abs(torch.from_numpy(t)) * torch.from_numpy(m))
+        loss.backward()
+        return {k: p.grad.double().numpy() for k, p in model.named_parameters()}
+
+    for tag, rw, rx in (("w", True, False), ("x", False, True), ("emu", None, None)):
+        gr = emu_grads() if tag == "emu" else grads(rw, rx)
+        for k, v in gr.items():
+            e_n = abs(np.linalg.norm(v) - g["gnorm/" + k][0]) / g["gnorm/" + k][0]
+            e_s = rel(v.reshape(-1)[::max(1, v.size // 4096)], g["gsample/" + k])
+            out[f"{tag}/{k}"] = np.array([e_n, e_s])
+    np.savez_compressed(os.path.join(HERE, "cnnblstm_c2_bf16sens.npz"), **out)
+    for k in sorted(out):
+        if "_l0" in k or "encoder.0.w" in k or "_l1" in k:
+            print(k, np.round(out[k], 4))
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["ganstep1001", "curvefix"]
     torch.set_num_threads(os.cpu_count() or 1)
+    if "bf16sens" in what:
+        gen_bf16sens(_load("models/CNNBLSTM/model.py", "ref_cnnblstm_model"))
     if "curvefix" in what:
         gen_curvefix(_load("models/CNNBLSTM/model.py", "ref_cnnblstm_model"))
     if "ganstep1001" in what:

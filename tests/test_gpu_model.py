@@ -316,14 +316,17 @@ def test_bf16_loss_curve_30_steps_tracks_fp32_reference(golden_dir):
     assert (ref[-4:].mean() < ref[:4].mean())
 
 
-# bf16 gradient gate at the C3 per-GPU shape: every gradient's norm within
-# BF16_GNORM_TOL and its strided sample within BF16_GSAMPLE_TOL relative L2 of
-# the reference's fp32 gradient (cnnblstm_c2.npz).  bf16 operands carry 8
-# significant bits (rounding 2^-9 = 2e-3 per operand); the gradient of the
-# layer-0 input weights is a sum over 10,688 frames of such products, the
-# encoder's gradients come through 5 BatchNorm+ReLU layers, so the bound is
-# an order above the operand rounding.  BN-fed conv biases have exact
-# gradient 0: bounded by their weight gradient's norm instead.
+# bf16 gradient gate at the C3 per-GPU shape.  The reference model's own
+# gradients are ill-conditioned under bf16 arithmetic: the same model.py with
+# every conv / Linear / LSTM-projection operand rounded to bf16 (fp32
+# accumulate; tests/golden/gen_golden_r03.py bf16sens, "emu/") moves the
+# layer-0 forward-direction LSTM gradients by 27-47 % and the encoder's by up
+# to 63 % (saturated random-init gates: a few near-threshold units carry the
+# gradient), the layer-1/2, projection and decoder gradients by 1-9 %.  Each
+# gradient's norm and strided sample must stay within
+#   max(BF16_GNORM_TOL, 2 x emu norm err)  /  max(BF16_GSAMPLE_TOL, 2 x emu sample err)
+# of the reference's fp32 gradient (cnnblstm_c2.npz).  BN-fed conv biases have
+# exact gradient 0: bounded by their weight gradient's norm.
 BF16_GNORM_TOL = 2e-2
 BF16_GSAMPLE_TOL = 5e-2
 
@@ -361,8 +364,11 @@ def test_bf16_c2_batch32_forward_backward_tracks_reference(golden_dir):
         e_s = rel(gr.reshape(-1)[::max(1, gr.size // 4096)], g["gsample/" + k])
         errs[k] = (round(e_n, 5), round(e_s, 5))
     print("bf16 C2 grad errs (norm, sample)", errs)
+    sens = np.load(os.path.join(golden_dir, "cnnblstm_c2_bf16sens.npz"), allow_pickle=False)
     for k, (e_n, e_s) in errs.items():
-        assert e_n < BF16_GNORM_TOL and e_s < BF16_GSAMPLE_TOL, (k, e_n, e_s)
+        emu_n, emu_s = sens["emu/" + k]
+        bn, bs = max(BF16_GNORM_TOL, 2 * emu_n), max(BF16_GSAMPLE_TOL, 2 * emu_s)
+        assert e_n < bn and e_s < bs, (k, e_n, e_s, bn, bs)
 
 
 def test_hip_graph_replayed_curve_matches_reference(golden_dir):
