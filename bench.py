@@ -249,6 +249,7 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
     from ainp import ops
     M = B * T
     lw = model.lstm
+    fused = None
     bias = (lw.bias_ih_l0, lw.bias_hh_l0, lw.bias_ih_l0_reverse, lw.bias_hh_l0_reverse)
     zx = torch.empty(M, 8 * H, device=dev)
     flops = 2.0 * M * (8 * H) * I
@@ -291,6 +292,12 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
         dw_fn = lambda: ops.gemm_tn_splitk(dg, 8 * H, A, I, M, 4 * H, I, offsets_b=(0, 0))  # noqa: E731
         bname = ("dX gemm_f32_kernel x6 (dg x [W_f; W_r], both directions summed in-tile) + dW "
                  "gemm_tn_splitk x6 (dg^T x X, split-K slabs + fixed-order sum, side stream)")
+        if ops.l0_bwd_x6r_eligible(M, I, H):
+            # the step's path (cnnblstm._BLSTMFn): both GEMMs in one gemm_x6r launch
+            dwf, dwr = torch.empty(4 * H, I, device=dev), torch.empty(4 * H, I, device=dev)
+            fused = lambda: ops.lstm_l0_bwd_x6(dg, wf, wr, A, dxo, dwf, dwr)  # noqa: E731
+            bname = ("x6r::gemm_x6r_kernel, one launch: dW_cat = dg^T X (k-major operands, "
+                     "tiles first) + dX = dg W_cat (ops.lstm_l0_bwd_x6)")
         main_loop = ("fp32 operands split exactly into 3 bf16 pieces, 6 cross products on "
                      "v_mfma_f32_32x32x16_bf16, f32 accumulate; 256x256x16 tiles staged by "
                      "global_load_lds, each K-tile split once per workgroup into LDS bf16 planes")
@@ -303,6 +310,9 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
     main = torch.cuda.current_stream(dev)
 
     def pair():
+        if fused is not None:
+            fused()
+            return
         ev = torch.cuda.Event()
         ev.record(main)
         side.wait_event(ev)
@@ -316,10 +326,13 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
     dx_s = time_kernel(dx_fn, reps, dev)
     dw_s = time_kernel(dw_fn, reps, dev)
     roof_bwd = _roof(2 * flops, pair_s, bf16, bname + f" (M={M}, 8H={8 * H}, K={I})",
-                     dx_alone_ms=round(dx_s * 1e3, 4), dw_alone_ms=round(dw_s * 1e3, 4),
-                     what="dX on the current stream beside dW on a side stream, as "
-                          "cnnblstm._BLSTMFn.backward launches them; timed from the first "
-                          "launch to the join")
+                     two_stream_dx_alone_ms=round(dx_s * 1e3, 4),
+                     two_stream_dw_alone_ms=round(dw_s * 1e3, 4),
+                     what=("both GEMMs in one launch, as cnnblstm._BLSTMFn.backward runs them"
+                           if fused is not None else
+                           "dX on the current stream beside dW on a side stream, as "
+                           "cnnblstm._BLSTMFn.backward launches them; timed from the first "
+                           "launch to the join"))
     return roof, roof_bwd
 
 

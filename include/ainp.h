@@ -208,6 +208,37 @@ int ainp_gemm_x6nt_256(int64_t M, int64_t N, int64_t K, const float* A, int64_t 
                        const float* bias_b1, const float* bias_b2, int64_t bias_nsplit,
                        int nsplit, int64_t kc, int64_t strideC, void* stream);
 
+/* fp32-accurate ("x6") GEMMs on the 256 x 256 split-plane tile
+ * (csrc/gemm_x6r.hip): 1..3 problems in ONE launch (one grid, problem q's
+ * work items after problem q-1's), so e.g. the layer-0 LSTM data gradient and
+ * weight gradient (models/CNNBLSTM/model.py:46-47,77 backward) share the chip
+ * without a second stream.  Per problem:
+ *   C(m, n) = sum_k A(m, k) B(n, k) + bias(n)          m < M, n < N, k < K
+ *   A(m, k) = a_kmajor ? A[k*lda + m] : A[m*lda + k]; if A2, columns
+ *             k >= a_ksplit come from A2 at k - a_ksplit
+ *   B(n, k) = b_kmajor ? B[k*ldb + n] : B[n*ldb + k]; if B2 and b_ksplit > 0,
+ *             columns k >= b_ksplit come from B2 (k - b_ksplit); if B2 and
+ *             b_ksplit <= 0, rows n >= b_nsplit come from B2 (n - b_nsplit)
+ *   C rows m >= c_msplit go to C2 (m - c_msplit) when C2 != NULL; ldc for both
+ *   bias: (bias_a1 + bias_a2)[n] for n < bias_nsplit, (bias_b1 + bias_b2)
+ *         [n - bias_nsplit] after (any may be NULL), slab 0 only
+ *   nsplit > 1: split-K, split s sums k in [s*kc, min(K, (s+1)*kc)) into
+ *         C + s*strideC (and C2 + s*strideC)
+ * Requirements: K, kc, a_ksplit, b_ksplit % 16 == 0; b_nsplit, c_msplit %
+ * 256 == 0; operands 16-byte aligned with ld % 4 == 0; k-major operands have
+ * a row count % 4 == 0.  Arithmetic: the exact three-piece bf16 split, six
+ * cross products per 16-k step (ainp_gemm_f32's default main loop): with
+ * nsplit == 1 and k-contiguous operands bit-identical to ainp_gemm_x6nt_256. */
+typedef struct {
+  const float* A; const float* A2; int64_t lda; int64_t a_ksplit; int a_kmajor;
+  const float* B; const float* B2; int64_t ldb; int64_t b_nsplit; int64_t b_ksplit; int b_kmajor;
+  float* C; float* C2; int64_t ldc; int64_t c_msplit;
+  const float* bias_a1; const float* bias_a2; const float* bias_b1; const float* bias_b2;
+  int64_t bias_nsplit;
+  int64_t M, N, K; int nsplit; int64_t kc; int64_t strideC;
+} ainp_x6_problem;
+int ainp_gemm_x6_multi(const ainp_x6_problem* probs, int nprobs, void* stream);
+
 /* bf16-operand GEMM (the bf16 configuration's layer-0 LSTM GEMMs,
  * models/CNNBLSTM/model.py:46-47,77: input projection, data and weight
  * gradients): C[m][n] (+ split s * strideC) = sum_k A[m][k] B[n][k] + bias(n),

@@ -237,8 +237,8 @@ class _BLSTMFn(torch.autograd.Function):
             elif (l == 0 and not bf16 and not ops.GEMM_EXACT
                   and ops.x6_256_eligible(NT, 8 * H, Il, 4 * H)):
                 # fp32 layer-0 projection (360 GFLOP at C2) on the 256 x 256 tile
-                ops.gemm_x6nt_256(inp, wf, wr, zx.view(NT, 8 * H), bias=(bif, bhf, bir, bhr),
-                                  bias_nsplit=4 * H)
+                (ops.gemm_x6r_nt if ops.X6R_FWD else ops.gemm_x6nt_256)(
+                    inp, wf, wr, zx.view(NT, 8 * H), bias=(bif, bhf, bir, bhr), bias_nsplit=4 * H)
             else:
                 ops.gemm(NT, 4 * H, Il, [inp, inp], Il, 1, [wf, wr], 1, Il,
                          [zx, zx[:, :, 4 * H:]], 8 * H, 1, bias1=[bif, bir], bias2=[bhf, bhr],
@@ -292,12 +292,21 @@ class _BLSTMFn(torch.autograd.Function):
             side.wait_event(ready)
             early = (l == 0 and ctx.sink is not None and ctx.sink.early_ok
                      and all(p.grad is None for p in ctx.wih0))
+            # fp32 layer 0, no data parallelism: dX and dW_ih in ONE launch on
+            # the current stream (gemm_x6r.hip: the weight-gradient tiles first,
+            # the data-gradient tiles behind them), instead of dX here beside a
+            # split-K weight gradient on the side stream
+            pair = (l == 0 and l016 is None and not bf16 and not ops.GEMM_EXACT and not early
+                    and ctx.sink is None and (l > 0 or ctx.needs_input_grad[0])
+                    and ops.l0_bwd_x6r_eligible(NT, Il, H))
             with torch.cuda.stream(side):
                 # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
                 # for the recurrent / upper layers -> parallel split-K over row chunks
                 gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H),
                                          bf16=bf16)
-                if early:
+                if pair:
+                    gwi = None
+                elif early:
                     gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0,
                                             l016=(dgT16, l016[0]) if l016 is not None else None)
                 elif l016 is not None:
@@ -311,6 +320,10 @@ class _BLSTMFn(torch.autograd.Function):
             for t in (dg, hp, inp) + ((dgT16, l016[0]) if l016 is not None else ()):
                 t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l
+            if pair:
+                dxi = torch.empty(NT, Il, device=dh.device)
+                gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
+                ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
             if early:   # p.grad set and reduced by _wih_grad_chunked: nothing for autograd
                 gwi = [None, None]
                 ctx.early_done = True
@@ -323,7 +336,9 @@ class _BLSTMFn(torch.autograd.Function):
                 # tiles) sums both directions inside each tile; the upper layers
                 # (Il = 256: 168 tiles) write 4 K-slabs (two per direction,
                 # 672 tiles) summed in fixed order.
-                if l016 is not None:
+                if pair:
+                    pass                                                  # dxi from the pair
+                elif l016 is not None:
                     dxi = ops.gemm_bf16nt(dg16, l016[1])                 # dg [NT,8H] x W_cat
                 elif Il >= 1024 and ops.DX_X6_256 and not bf16 and not ops.GEMM_EXACT \
                         and ops.x6_256_eligible(NT, Il, 8 * H, Il):

@@ -366,6 +366,91 @@ def _splitk_bf16(M, N, K, slots=768, max_split=16):
     return best
 
 
+def x6_problem(A, B, C, M, N, K, lda, ldb, ldc, *, A2=None, a_ksplit=0, a_kmajor=False,
+               B2=None, b_nsplit=0, b_ksplit=0, b_kmajor=False, C2=None, c_msplit=0,
+               bias=(None, None, None, None), bias_nsplit=0, nsplit=1, kc=0, strideC=0):
+    """One problem of ainp_gemm_x6_multi (include/ainp.h: element maps, splits)."""
+    return {"ins": [A, A2, B, B2, *bias], "outs": [C, C2],
+            "ints": [int(a_ksplit), int(bool(a_kmajor)), int(b_nsplit), int(b_ksplit),
+                     int(bool(b_kmajor)), int(c_msplit), int(bias_nsplit), int(M), int(N), int(K),
+                     int(nsplit), int(kc), int(strideC), int(lda), int(ldb), int(ldc)]}
+
+
+_EMPTY = {}
+
+
+def gemm_x6_multi(problems):
+    """fp32-accurate GEMMs, 1..3 problems in one launch (ainp_gemm_x6_multi,
+    csrc/gemm_x6r.hip)."""
+    ins, outs, ints = [], [], []
+    for p in problems:
+        ins += p["ins"]
+        for t in p["outs"]:
+            if t is None:
+                dev = p["outs"][0].device
+                t = _EMPTY.get(dev)
+                if t is None:
+                    t = _EMPTY[dev] = torch.empty(0, device=dev)
+            outs.append(t)
+        ints += p["ints"]
+    _T.gemm_x6_multi(ins, outs, ints)
+
+
+# AINP_L0_BWD_X6R=0 keeps the layer-0 backward pair on two streams (128 x 128
+# x6 kernels: dX on the current stream, the split-K weight gradient beside it)
+L0_BWD_X6R = os.environ.get("AINP_L0_BWD_X6R", "1") != "0"
+# AINP_X6R_FWD=1: the fp32 layer-0 projection on the split-plane tile too
+# (bit-identical to gemm_x6nt_256)
+X6R_FWD = os.environ.get("AINP_X6R_FWD", "0") == "1"
+
+
+def l0_bwd_x6r_eligible(NT, I, H):
+    return L0_BWD_X6R and NT % 4 == 0 and I % 4 == 0 and (4 * H) % 256 == 0 and NT >= 256
+
+
+def lstm_l0_bwd_x6(dg, wf, wr, x, dx, dwf, dwr):
+    """The fp32 layer-0 LSTM backward pair in ONE launch (nn.LSTM backward,
+    models/CNNBLSTM/model.py:46-47,77):
+        dW_cat [8H, I] = dg^T [8H, NT] . X [NT, I]   (rows < 4H -> dwf, rest -> dwr)
+        dX [NT, I]     = dg [NT, 8H] . W_cat [8H, I] (k < 4H from wf, rest from wr)
+    dg [NT, 8H], x [NT, I] (row-major, read as they lie: k-major operands of the
+    weight gradient), wf / wr [4H, I]; the weight-gradient tiles (long K = NT)
+    are scheduled first, the data-gradient tiles fill in behind them."""
+    NT, G8 = dg.shape
+    I = x.shape[1]
+    G4 = G8 // 2
+    for t in (dg, x, wf, wr, dx, dwf, dwr):
+        _req(t, "operand")
+    pw = x6_problem(dg, x, dwf, M=G8, N=I, K=NT, lda=G8, ldb=I, ldc=I, a_kmajor=True,
+                    b_kmajor=True, C2=dwr, c_msplit=G4)
+    px = x6_problem(dg, wf, dx, M=NT, N=I, K=G8, lda=G8, ldb=I, ldc=I, B2=wr, b_ksplit=G4,
+                    b_kmajor=True)
+    gemm_x6_multi([pw, px])
+
+
+def gemm_x6r_nt(A, B1, B2, out, bias=(None, None, None, None), bias_nsplit=0, nsplit=None):
+    """The fp32 layer-0 projection on the split-plane tile: drop-in for
+    gemm_x6nt_256 (same split-K rule, bias in slab 0, bit-identical slabs)."""
+    M, K = A.shape
+    N1 = B1.shape[0]
+    N = N1 + B2.shape[0]
+    S = _X6_SPLIT if nsplit is None else int(nsplit)
+    kc = -(-K // S // 16) * 16 if S > 1 else K
+    if S > 1 and -(-K // kc) != S:
+        S, kc = 1, K
+    kw = dict(B2=B2 if B2.shape[0] else None, b_nsplit=N1 if B2.shape[0] else 0,
+              bias=bias, bias_nsplit=bias_nsplit)
+    if S == 1:
+        gemm_x6_multi([x6_problem(A, B1, out, M=M, N=N, K=K, lda=A.stride(0), ldb=B1.stride(0),
+                                  ldc=out.stride(0), **kw)])
+        return out
+    slabs = torch.empty(S, M, N, device=A.device, dtype=torch.float32)
+    gemm_x6_multi([x6_problem(A, B1, slabs, M=M, N=N, K=K, lda=A.stride(0), ldb=B1.stride(0),
+                              ldc=N, nsplit=S, kc=kc, strideC=M * N, **kw)])
+    sum_slabs(slabs, S, out=out.view(-1))
+    return out
+
+
 def gemm_bf16nt_splitk(A, B, K, out=None, max_split=16):
     """A [M, >=K] . B [N, >=K]^T (bf16, no bias) with the long K split over
     slabs summed in fixed order (ainp_sum_slabs) -- the weight gradients."""

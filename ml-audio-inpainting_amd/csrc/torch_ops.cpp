@@ -867,6 +867,76 @@ void gemm_x6nt_256(const Tensor& A, const Tensor& B1, const Tensor& B2, const Te
       "gemm_x6nt_256");
 }
 
+// ainp_gemm_x6_multi: per problem q, ins[8q .. 8q+7] = A, A2, B, B2, bias_a1,
+// bias_a2, bias_b1, bias_b2 (optional), outs[2q], outs[2q+1] = C, C2 (C2 with
+// no elements = none), ints[16q .. 16q+15] = a_ksplit, a_kmajor, b_nsplit,
+// b_ksplit, b_kmajor, c_msplit, bias_nsplit, M, N, K, nsplit, kc, strideC,
+// lda, ldb, ldc.  Every operand extent is checked against its tensor.
+void gemm_x6_multi(const std::vector<std::optional<Tensor>>& ins, const std::vector<Tensor>& outs,
+                   const std::vector<int64_t>& ints) {
+  const int64_t np = (int64_t)outs.size() / 2;
+  TORCH_CHECK(np >= 1 && np <= 3 && (int64_t)ins.size() == 8 * np && (int64_t)ints.size() == 16 * np,
+              "gemm_x6_multi: 1..3 problems of 8 inputs, 2 outputs, 16 ints");
+  GUARD(outs[0]);
+  std::vector<ainp_x6_problem> pr(np);
+  auto fp = [&](const std::optional<Tensor>& t, const char* nm) -> const float* {
+    if (!t.has_value() || !t->defined() || t->numel() == 0) return nullptr;
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat, nm, " must be a float32 GPU tensor");
+    same_device(*t, outs[0]);
+    return t->data_ptr<float>();
+  };
+  // an operand of R rows x Kx cols (k-major or not) with leading dim ld must fit t
+  auto fits = [](const std::optional<Tensor>& t, bool km, int64_t R, int64_t Kx, int64_t ld,
+                 const char* nm) {
+    if (!t.has_value() || !t->defined() || t->numel() == 0) return;
+    TORCH_CHECK(t->is_contiguous() || t->dim() == 2, nm, ": contiguous or 2-D strided");
+    const int64_t need = km ? (Kx - 1) * ld + R : (R - 1) * ld + Kx;
+    const int64_t have = t->dim() == 2 && !t->is_contiguous()
+                             ? (t->size(0) - 1) * t->stride(0) + t->size(1) : t->numel();
+    TORCH_CHECK(R > 0 && Kx > 0 && need <= have, nm, " is too small for its extent (", need,
+                " > ", have, ")");
+  };
+  for (int64_t q = 0; q < np; ++q) {
+    const int64_t* v = ints.data() + 16 * q;
+    const auto* in = ins.data() + 8 * q;
+    ainp_x6_problem& p = pr[q];
+    p.a_ksplit = v[0]; p.a_kmajor = (int)v[1]; p.b_nsplit = v[2]; p.b_ksplit = v[3];
+    p.b_kmajor = (int)v[4]; p.c_msplit = v[5]; p.bias_nsplit = v[6];
+    p.M = v[7]; p.N = v[8]; p.K = v[9]; p.nsplit = (int)v[10]; p.kc = v[11]; p.strideC = v[12];
+    p.lda = v[13]; p.ldb = v[14]; p.ldc = v[15];
+    p.A = fp(in[0], "A"); p.A2 = fp(in[1], "A2"); p.B = fp(in[2], "B"); p.B2 = fp(in[3], "B2");
+    p.bias_a1 = fp(in[4], "bias_a1"); p.bias_a2 = fp(in[5], "bias_a2");
+    p.bias_b1 = fp(in[6], "bias_b1"); p.bias_b2 = fp(in[7], "bias_b2");
+    const Tensor& C = outs[2 * q];
+    const Tensor& C2 = outs[2 * q + 1];
+    p.C = const_cast<float*>(fp(C, "C"));
+    p.C2 = const_cast<float*>(fp(C2, "C2"));
+    TORCH_CHECK(p.A && p.B && p.C, "gemm_x6_multi: A, B, C are required");
+    const bool a2 = p.A2 != nullptr, b2 = p.B2 != nullptr, c2 = p.C2 != nullptr;
+    TORCH_CHECK(!a2 || (p.a_ksplit > 0 && p.a_ksplit < p.K), "a_ksplit out of range");
+    TORCH_CHECK(!c2 || (p.c_msplit > 0 && p.c_msplit < p.M), "c_msplit out of range");
+    TORCH_CHECK(!b2 || (p.b_ksplit > 0 ? p.b_ksplit < p.K : (p.b_nsplit > 0 && p.b_nsplit < p.N)),
+                "B split out of range");
+    fits(in[0], p.a_kmajor, p.M, a2 ? p.a_ksplit : p.K, p.lda, "A");
+    if (a2) fits(in[1], p.a_kmajor, p.M, p.K - p.a_ksplit, p.lda, "A2");
+    const bool bk = b2 && p.b_ksplit > 0;
+    const int64_t nb1 = (b2 && !bk) ? p.b_nsplit : p.N;
+    fits(in[2], p.b_kmajor, nb1, bk ? p.b_ksplit : p.K, p.ldb, "B");
+    if (b2) fits(in[3], p.b_kmajor, bk ? p.N : p.N - p.b_nsplit, bk ? p.K - p.b_ksplit : p.K,
+                 p.ldb, "B2");
+    const int64_t ns = p.nsplit < 1 ? 1 : p.nsplit;
+    const int64_t m1 = c2 ? p.c_msplit : p.M;
+    fits(C, false, (ns - 1) * (p.strideC / std::max<int64_t>(p.ldc, 1)) + m1, p.N, p.ldc, "C");
+    if (c2) fits(C2, false, (ns - 1) * (p.strideC / std::max<int64_t>(p.ldc, 1)) + p.M - m1, p.N,
+                 p.ldc, "C2");
+    if (p.bias_a1) numel_is(*in[4], p.bias_nsplit, "bias_a1");
+    if (p.bias_a2) numel_is(*in[5], p.bias_nsplit, "bias_a2");
+    if (p.bias_b1) numel_is(*in[6], p.N - p.bias_nsplit, "bias_b1");
+    if (p.bias_b2) numel_is(*in[7], p.N - p.bias_nsplit, "bias_b2");
+  }
+  chk(ainp_gemm_x6_multi(pr.data(), (int)np, stream_of(outs[0])), "gemm_x6_multi");
+}
+
 void transpose_f32(const Tensor& x, const Tensor& outT) {
   GUARD(x);
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1, "x must be 2-D with unit-stride rows");
@@ -1082,6 +1152,7 @@ TORCH_LIBRARY(ainp, m) {
         "int n_fft, int hop, bool center, Tensor(a!) workspace, Tensor(b!) out) -> ()");
   m.def("gl_update(Tensor rebuilt, Tensor(a!) tprev, Tensor(b!) angles, float momentum, "
         "bool first) -> ()");
+  m.def("gemm_x6_multi(Tensor?[] ins, Tensor(a!)[] outs, int[] ints) -> ()");
   m.def("gl_stft_update(Tensor audio, Tensor window, int hop, int n_frames, Tensor(a!) tprev, "
         "Tensor(b!) angles, float momentum, bool first) -> ()");
   m.def("gemm(int M, int N, int K, float alpha, Tensor[] A, int sam, int sak, int strideA, "
@@ -1182,6 +1253,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("istft", &istft);
   m.impl("gl_update", &gl_update);
   m.impl("gl_stft_update", &gl_stft_update);
+  m.impl("gemm_x6_multi", &gemm_x6_multi);
   m.impl("gemm", &gemm);
   m.impl("conv3x3_fwd", &conv3x3_fwd);
   m.impl("conv3x3_dgrad", &conv3x3_dgrad);
@@ -1247,6 +1319,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("istft", torch::CppFunction::makeFallthrough());
   m.impl("gl_update", torch::CppFunction::makeFallthrough());
   m.impl("gl_stft_update", torch::CppFunction::makeFallthrough());
+  m.impl("gemm_x6_multi", torch::CppFunction::makeFallthrough());
   m.impl("gemm", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_fwd", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_dgrad", torch::CppFunction::makeFallthrough());

@@ -803,3 +803,116 @@ def test_bf16_layer0_operand_path_matches_staged_bf16_path():
             continue   # BN-fed conv biases: exact gradient 0
         e = float((g1[k] - g0[k]).norm() / max(g0[k].norm(), 1e-30))
         assert e < 1e-3, (k, e)
+
+
+# ------------------------------------------------------- x6r (csrc/gemm_x6r.hip)
+@pytest.mark.parametrize("M,K,H", [(2304, 1024, 128), (700, 160, 64), (10688, 16448, 128)])
+def test_gemm_x6r_projection_bit_identical_to_x6nt_256(ops, M, K, H):
+    """The layer-0 projection on the split-plane tile (ainp_gemm_x6_multi,
+    one problem, k-contiguous operands, B split by rows at 4H) is bit-identical
+    to ainp_gemm_x6nt_256 unsplit and split 3 (same split, products, k order;
+    bias in slab 0)."""
+    g = torch.Generator().manual_seed(12)
+    A = torch.relu(torch.randn(M, K, generator=g)).to(DEV)
+    wf = (torch.randn(4 * H, K, generator=g) * 0.02).to(DEV)
+    wr = (torch.randn(4 * H, K, generator=g) * 0.02).to(DEV)
+    b = tuple((torch.randn(4 * H, generator=g) * 0.1).to(DEV) for _ in range(4))
+    for S in (1, 3):
+        y0 = torch.full((M, 8 * H), float("nan"), device=DEV)
+        ops.gemm_x6nt_256(A, wf, wr, y0, bias=b, bias_nsplit=4 * H, nsplit=S)
+        y1 = torch.full((M, 8 * H), float("nan"), device=DEV)
+        ops.gemm_x6r_nt(A, wf, wr, y1, bias=b, bias_nsplit=4 * H, nsplit=S)
+        torch.cuda.synchronize()
+        assert torch.equal(y0, y1), S
+
+
+@pytest.mark.parametrize("NT,H,I", [(1200, 64, 1088), (2048, 128, 520), (10688, 128, 16448)])
+def test_lstm_l0_bwd_x6_pair(ops, NT, H, I):
+    """The fp32 layer-0 backward pair in one launch (ops.lstm_l0_bwd_x6:
+    dW_cat = dg^T X with both operands k-major, rows split into the two
+    directions; dX = dg W_cat with W_cat's k-halves from W_f / W_r): an fp32
+    GEMM against fp64 (within 1e-6 relative, a few times torch's blocked fp32
+    GEMM on the CPU, at the small shapes), and at the C2 shape within 1e-6 of the two-stream 128 x 128
+    x6 path it replaces (models/CNNBLSTM/model.py:46-47 backward)."""
+    g = torch.Generator().manual_seed(NT + I)
+    dg = (torch.randn(NT, 8 * H, generator=g) * 1e-2).to(DEV)
+    x = torch.relu(torch.randn(NT, I, generator=g)).to(DEV)
+    wf = (torch.randn(4 * H, I, generator=g) * 0.05).to(DEV)
+    wr = (torch.randn(4 * H, I, generator=g) * 0.05).to(DEV)
+    dx = torch.full((NT, I), float("nan"), device=DEV)
+    dwf = torch.full((4 * H, I), float("nan"), device=DEV)
+    dwr = torch.full((4 * H, I), float("nan"), device=DEV)
+    ops.lstm_l0_bwd_x6(dg, wf, wr, x, dx, dwf, dwr)
+    torch.cuda.synchronize()
+    dW = torch.cat([dwf, dwr]).cpu()
+    if NT * I <= 4 * 2 ** 20:
+        d64, x64 = dg.double().cpu(), x.double().cpu()
+        W64 = torch.cat([wf, wr]).double().cpu()
+        rw, rx = d64.T @ x64, d64 @ W64
+        fw = (dg.cpu().T @ x.cpu()).double()
+        fx = (dg.cpu() @ torch.cat([wf, wr]).cpu()).double()
+        # one fp32 accumulator per output over the whole K (no split-K slabs):
+        # within 1e-6, a few times the CPU's blocked fp32 sum
+        assert rel(dW, rw) < max(4 * rel(fw, rw), 1e-6), (rel(dW, rw), rel(fw, rw))
+        assert rel(dx.cpu(), rx) < max(4 * rel(fx, rx), 1e-6), (rel(dx.cpu(), rx), rel(fx, rx))
+    else:
+        # the two-stream path (cnnblstm._BLSTMFn with AINP_L0_BWD_X6R=0)
+        ox = torch.empty(NT, I, device=DEV)
+        dg2 = dg.contiguous()
+        ops.gemm(NT, I, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], I, 1, [ox, ox], I, 1,
+                 ksplit=True)
+        ow = ops.gemm_tn_splitk(dg2, 8 * H, x, I, NT, 4 * H, I, offsets_b=(0, 0))
+        torch.cuda.synchronize()
+        assert rel(dx.cpu(), ox.cpu()) < 1e-6
+        assert rel(dW, torch.cat([ow[0], ow[1]]).cpu()) < 1e-6
+
+
+def test_gemm_x6_multi_equals_separate_launches(ops):
+    """Problems launched together (one grid) give bit-identical results to the
+    same problems launched one by one; a split-K problem writes its slabs."""
+    g = torch.Generator().manual_seed(21)
+    NT, H, I = 1200, 64, 1088
+    dg = torch.randn(NT, 8 * H, generator=g).to(DEV)
+    x = torch.randn(NT, I, generator=g).to(DEV)
+    wf, wr = (torch.randn(4 * H, I, generator=g).to(DEV) for _ in range(2))
+
+    def probs(outs):
+        dx, dwf, dwr, sl = outs
+        return [ops.x6_problem(dg, x, dwf, M=8 * H, N=I, K=NT, lda=8 * H, ldb=I, ldc=I,
+                               a_kmajor=True, b_kmajor=True, C2=dwr, c_msplit=4 * H),
+                ops.x6_problem(dg, wf, dx, M=NT, N=I, K=8 * H, lda=8 * H, ldb=I, ldc=I, B2=wr,
+                               b_ksplit=4 * H, b_kmajor=True),
+                ops.x6_problem(x, wf, sl, M=NT, N=4 * H, K=I, lda=I, ldb=I, ldc=4 * H, nsplit=2,
+                               kc=544, strideC=NT * 4 * H)]
+
+    def fresh():
+        return (torch.full((NT, I), float("nan"), device=DEV),
+                torch.full((4 * H, I), float("nan"), device=DEV),
+                torch.full((4 * H, I), float("nan"), device=DEV),
+                torch.full((2, NT, 4 * H), float("nan"), device=DEV))
+    a, b = fresh(), fresh()
+    ops.gemm_x6_multi(probs(a))
+    for p in probs(b):
+        ops.gemm_x6_multi([p])
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert not torch.isnan(u).any()
+        assert torch.equal(u, v)
+    ref = (x.double().cpu() @ wf.double().cpu().T)
+    assert rel(a[3].sum(0).cpu(), ref) < 1e-6
+
+
+def test_gemm_x6_multi_rejects_bad_extents(ops):
+    """Host checks before the launch: an operand shorter than its extent, a
+    split off the tile grid, more than 3 problems."""
+    A = torch.randn(300, 64, device=DEV)
+    B = torch.randn(256, 64, device=DEV)
+    C = torch.empty(300, 256, device=DEV)
+    with pytest.raises(RuntimeError):
+        ops.gemm_x6_multi([ops.x6_problem(A, B, C, M=300, N=256, K=128, lda=64, ldb=64, ldc=256)])
+    with pytest.raises(RuntimeError):
+        ops.gemm_x6_multi([ops.x6_problem(A, B, C, M=300, N=256, K=64, lda=64, ldb=64, ldc=256,
+                                          C2=C, c_msplit=100)])
+    p = ops.x6_problem(A, B, C, M=300, N=256, K=64, lda=64, ldb=64, ldc=256)
+    with pytest.raises(RuntimeError):
+        ops.gemm_x6_multi([p] * 4)
