@@ -275,9 +275,11 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
     else:
         A = torch.randn(M, I, device=dev, generator=g)
         if not ops.GEMM_EXACT and ops.x6_256_eligible(M, 8 * H, I, 4 * H):
-            fwd = lambda: ops.gemm_x6nt_256(A, lw.weight_ih_l0, lw.weight_ih_l0_reverse,  # noqa: E731
-                                            zx, bias=bias, bias_nsplit=4 * H)
-            kname = "x6_256::gemm_x6nt_256s_kernel (split pass), split 3 + slab sum"
+            gx = ops.gemm_x6r_nt if ops.X6R_FWD else ops.gemm_x6nt_256
+            fwd = lambda: gx(A, lw.weight_ih_l0, lw.weight_ih_l0_reverse,  # noqa: E731
+                             zx, bias=bias, bias_nsplit=4 * H)
+            kname = ("x6r::gemm_x6r_kernel" if ops.X6R_FWD else
+                     "x6_256::gemm_x6nt_256s_kernel (split pass)") + ", split 3 + slab sum"
         else:
             args_g = (M, 4 * H, I, [A, A], I, 1, [lw.weight_ih_l0, lw.weight_ih_l0_reverse], 1,
                       I, [zx, zx[:, 4 * H:]], 8 * H, 1)
@@ -300,7 +302,9 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
                      "tiles first) + dX = dg W_cat (ops.lstm_l0_bwd_x6)")
         main_loop = ("fp32 operands split exactly into 3 bf16 pieces, 6 cross products on "
                      "v_mfma_f32_32x32x16_bf16, f32 accumulate; 256x256x16 tiles staged by "
-                     "global_load_lds, each K-tile split once per workgroup into LDS bf16 planes")
+                     "global_load_lds into a 2-stage fp32 ring, each K-tile split once per "
+                     "workgroup into double-buffered LDS bf16 planes while the previous "
+                     "tile's MFMAs run (one barrier per K-tile)")
     avg_s = time_kernel(fwd, reps, dev)
     traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else "traffic_gemm_l0.json")
     roof = _roof(flops, avg_s, bf16, kname + f" (LSTM l0 input projection, M={M} N={8 * H} "

@@ -114,7 +114,11 @@ class _ConvStackFn(torch.autograd.Function):
             out = saved_y[-1]
         ctx.spec = spec
         ctx.bf16 = bf16
-        ctx.defer_wgrad = defer_wgrad
+        # (mode, sink): mode False / True (side stream now) / "queue" (released at
+        # the first BPTT); sink = the data-parallel GradAllReducer or None
+        ctx.defer_wgrad, ctx.sink = defer_wgrad if isinstance(defer_wgrad, tuple) \
+            else (defer_wgrad, None)
+        ctx.param_objs = params
         ctx.out_ntcf = out_ntcf
         ctx.comm = comm
         ctx.count = count
@@ -177,13 +181,17 @@ class _ConvStackFn(torch.autograd.Function):
                 pr, bf = pro, ctx.bf16
                 _Deferred.push(gy.device, lambda xin=xin, gy=gy, pr=pr, dwv=dwv, dbv=dbv, bf=bf:
                                ops.conv3x3_wgrad(xin, gy, pr[0], pr[1], bf16=bf, out=(dwv, dbv)),
-                               (xin, gy) + tuple(t for t in pro if t is not None), (dwv, dbv))
+                               (xin, gy) + tuple(t for t in pro if t is not None), (dwv, dbv),
+                               params=ctx.param_objs[p0:p0 + 2], sink=ctx.sink)
             elif ctx.defer_wgrad:
                 # off the critical path: on the side stream, overlapping the next
                 # (HBM-bound) BatchNorm backward passes
                 with _side_work(gy.device) as sw:
                     dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
                     sw.handoff((xin, gy) + tuple(t for t in pro if t is not None), (dw, db))
+                    # data parallel: all-reduced from the side stream as soon as
+                    # they exist (the collective waits for this stream only)
+                    _reduce_side(ctx.sink, ctx.param_objs[p0:p0 + 2], (dw, db))
             else:
                 dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
             grads[p0], grads[p0 + 1] = dw, db
@@ -272,6 +280,11 @@ class _BLSTMFn(torch.autograd.Function):
         # on with dX and layer l-1's recurrence (64 workgroups: most CUs idle).
         main = torch.cuda.current_stream(dh.device)
         side = _side_stream(dh.device)
+        # data parallel: the side stream's weight / bias gradients are
+        # all-reduced from the side stream as they are produced, so the compute
+        # stream never waits for them (AccumulateGrad stores non-view aliases)
+        dp_side = ctx.sink is not None and ctx.sink.early_ok and \
+            getattr(ctx.sink, "side_ok", True) and all(p.grad is None for p in ctx.param_objs)
         for l in range(L - 1, -1, -1):
             inp, h, gates, cell = saved[4 * l:4 * l + 4]
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
@@ -317,6 +330,11 @@ class _BLSTMFn(torch.autograd.Function):
                                              offsets_b=(0, 0), bf16=bf16)
                 db_ih = ops.colsum(dg2)           # b_ih and b_hh get the same gradient
                 db_hh = db_ih.clone()
+                if dp_side:
+                    po = ctx.param_objs[8 * l:8 * l + 8]
+                    wi = [None, None] if (early or gwi is None) else gwi
+                    _reduce_side(ctx.sink, po, (wi[0], gwh[0], db_ih[:4 * H], db_hh[:4 * H],
+                                                wi[1], gwh[1], db_ih[4 * H:], db_hh[4 * H:]))
             for t in (dg, hp, inp) + ((dgT16, l016[0]) if l016 is not None else ()):
                 t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l
@@ -365,7 +383,7 @@ class _BLSTMFn(torch.autograd.Function):
         for gr in grads:
             if gr is not None:
                 gr.record_stream(main)    # side-stream memory handed to autograd
-        if ctx.sink is None and all(p.grad is None for p in ctx.param_objs):
+        if dp_side or (ctx.sink is None and all(p.grad is None for p in ctx.param_objs)):
             # nothing on the current stream reads these gradients before the
             # optimizer: join the side stream at the end of the backward pass
             # (engine callback) so the layer-0 weight gradient overlaps the
@@ -455,25 +473,49 @@ class _Deferred:
     _queues: dict = {}
 
     @classmethod
-    def push(cls, device, fn, inputs, outputs):
+    def push(cls, device, fn, inputs, outputs, params=(), sink=None):
+        """params / sink (data parallel): the Parameters the outputs are the
+        gradients of, and the GradAllReducer that all-reduces them from the side
+        stream once they are written (its hooks skip them meanwhile)."""
         q = cls._queues.setdefault(device, [])
         if not q:
             torch.autograd.Variable._execution_engine.queue_callback(
                 lambda: cls.flush(device, join=True))
-        q.append((fn, inputs, outputs))
+        if sink is not None and sink.early_ok:
+            for p in params:
+                sink.defer(p)
+        else:
+            sink = None
+        q.append((fn, inputs, outputs, params, sink))
 
     @classmethod
     def flush(cls, device, join=False):
         q = cls._queues.pop(device, [])
         if q:
             with _side_work(device, callback=False) as sw:
-                for fn, inputs, outputs in q:
+                for fn, inputs, outputs, params, sink in q:
                     fn()
                     sw.handoff(inputs, outputs)
+                    if sink is not None:
+                        for p, o in zip(params, outputs):
+                            sink.reduce_chunk(p, o, kind="side")
         if join and q is not None:
             done = torch.cuda.Event()
             done.record(_side_stream(device))
             torch.cuda.current_stream(device).wait_event(done)
+
+
+def _reduce_side(sink, params, grads):
+    """Data parallel: hand side-stream gradients to the reducer from the side
+    stream (call inside its context): the all-reduce waits for that stream's
+    work, not for the compute stream; the reducer's hooks skip them."""
+    if sink is None or not sink.early_ok:
+        return False
+    for p, g in zip(params, grads):
+        if p is not None and g is not None:
+            sink.defer(p)
+            sink.reduce_chunk(p, g, kind="side")
+    return True
 
 
 class _side_work:
@@ -532,7 +574,7 @@ class _ProjFn(torch.autograd.Function):
     """nn.Linear(2H, C*F) + view(N,T,C,F).permute(0,2,3,1) -> [N, C, F, T]."""
 
     @staticmethod
-    def forward(ctx, h, w, b, C, F, bf16=False, defer_wgrad=False):
+    def forward(ctx, h, w, b, C, F, bf16=False, defer_wgrad=False, sink=None):
         N, T, K = h.shape
         out = torch.empty(N, C, F, T, device=h.device, dtype=torch.float32)
         NO = C * F
@@ -543,6 +585,8 @@ class _ProjFn(torch.autograd.Function):
         ctx.shape = (N, C, F, T)
         ctx.bf16 = bf16
         ctx.defer_wgrad = defer_wgrad
+        ctx.sink = sink
+        ctx.param_objs = (w, b)
         return out
 
     @staticmethod
@@ -582,10 +626,11 @@ class _ProjFn(torch.autograd.Function):
         db = torch.empty(NO, device=g.device)
         if ctx.defer_wgrad:
             dwv, dbv = _alias(dw), _alias(db)     # aliases only (see _ConvStackFn)
-            _Deferred.push(g.device, lambda: wgrad(dwv, dbv), (g, h), (dwv, dbv))
+            _Deferred.push(g.device, lambda: wgrad(dwv, dbv), (g, h), (dwv, dbv),
+                           params=ctx.param_objs, sink=ctx.sink)
         else:
             wgrad(dw, db)
-        return dh, dw, db, None, None, None, None
+        return dh, dw, db, None, None, None, None, None
 
 
 def _split_count(n):
@@ -707,28 +752,31 @@ class StackedBLSTMCNN(nn.Module):
         box = {} if self.bf16 else None       # layer-0 bf16 operands (encoder -> BLSTM)
         # the deferred weight gradients are written after autograd receives
         # them: only while the .grad buffers are empty (nothing accumulates)
-        defer_enc = (self.defer_wgrad_encoder and self.training and torch.is_grad_enabled()
-                     and self.grad_reducer is None and self.comm is None
-                     and all(q.grad is None for q in self.encoder.parameters()))
-        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, box, defer_enc,
-                               *params)
         sink = self.grad_reducer if (self.training and torch.is_grad_enabled()) else None
+        if sink is not None:    # BLSTM side-stream reductions follow the same switch
+            sink.side_ok = self.defer_wgrad
+        # data parallel keeps these overlaps: the deferred gradients are
+        # all-reduced from the side stream once written (_reduce_side)
+        defer_enc = (self.defer_wgrad_encoder and self.training and torch.is_grad_enabled()
+                     and all(q.grad is None for q in self.encoder.parameters()))
+        z = _ConvStackFn.apply(x, spec, self.training, True, self.comm, self.bf16, box,
+                               (defer_enc, sink), *params)
         z = _BLSTMFn.apply(z, self.hidden_dim, self.n_layers, self.bf16, sink, box,
                            *self.lstm._flat_weights)
         # decoder / projection weight gradients on the side stream, overlapping the
-        # BPTT recurrence (64 workgroups) -- not under data parallelism, whose
-        # gradient hooks read each gradient as soon as autograd hands it over
-        # (and only while the .grad buffers are empty: the deferred outputs are
-        # written after autograd receives them, so they cannot be accumulated into)
-        defer = (self.defer_wgrad and self.training and sink is None and self.comm is None
+        # BPTT recurrence (64 workgroups); only while the .grad buffers are empty
+        # (the deferred outputs are written after autograd receives them, so
+        # they cannot be accumulated into); under data parallelism they are
+        # all-reduced from the side stream when written
+        defer = (self.defer_wgrad and self.training and torch.is_grad_enabled()
                  and all(q.grad is None for m in (self.projection, self.decoder)
                          for q in m.parameters()))
         # model.py:82 hard-codes 16 decoder channels
         p = _ProjFn.apply(z, self.projection.weight, self.projection.bias, 16, freq_bins,
-                          self.bf16, defer)
+                          self.bf16, defer, sink)
         spec, params = self._stack(self.decoder)
         y = _ConvStackFn.apply(p, spec, self.training, False, self.comm, self.bf16, None,
-                               "queue" if defer else False, *params)
+                               ("queue" if defer else False, sink), *params)
         return y.squeeze(1)
 
     def reconstruct_spectrogram(self, log_spectrogram_gap, gap_mask):

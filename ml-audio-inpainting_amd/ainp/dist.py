@@ -128,8 +128,15 @@ class GradAllReducer:
         """The model may hand gradient chunks over as they are computed."""
         return self.overlap and not self.paused
 
+    def defer(self, p):
+        """p's gradient will be handed over later through reduce_chunk (a
+        side-stream weight gradient): its accumulate hook must not launch a
+        collective on the buffer before the side stream has written it."""
+        self._seen.add(id(p))
+        self._chunked.add(id(p))
+
     @torch.no_grad()
-    def reduce_chunk(self, p, chunk: torch.Tensor):
+    def reduce_chunk(self, p, chunk: torch.Tensor, kind="early"):
         """All-reduce (SUM) one finished chunk of p's gradient now, from the
         caller's current stream: the collective waits for exactly the work
         queued on that stream (e.g. a side-stream weight-gradient GEMM) rather
@@ -143,9 +150,13 @@ class GradAllReducer:
         else:
             work = dist.all_reduce(chunk, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         self._inflight.append((work, [], None))
-        self.early_chunks += 1
+        if kind == "early":
+            self.early_chunks += 1
+        else:
+            self.side_reductions += 1
 
-    early_chunks = 0
+    early_chunks = 0        # layer-0 input-weight gradient chunks (reduce_chunk)
+    side_reductions = 0     # side-stream weight gradients (kind="side")
 
     # -- overlapped path ------------------------------------------------------
     def _ready(self, p):

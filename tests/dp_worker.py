@@ -40,7 +40,7 @@ def _cnnblstm_batch(n=4, F=33, T=24):
     return x, mask, tgt
 
 
-def run_cnnblstm(comm=None, rank=0, world=1, uneven=False, steps=1):
+def run_cnnblstm(comm=None, rank=0, world=1, uneven=False, steps=1, defer=True):
     """uneven: rank 0 takes 3 of the 4 examples, rank 1 one (SyncBN must use
     the global element count).  The ranks start from different seeds and get
     rank 0's weights by broadcast; the layer-0 input weights' gradients go to
@@ -51,6 +51,9 @@ def run_cnnblstm(comm=None, rank=0, world=1, uneven=False, steps=1):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0 if comm is None else 100 * rank)
     model = StackedBLSTMCNN(config=CNNBLSTM_CFG).to(dev).train()
+    # side-stream weight gradients (on by default; under DP they are
+    # all-reduced from the side stream as they are written)
+    model.defer_wgrad = model.defer_wgrad_encoder = defer
     if comm is not None:
         comm.broadcast_module_(model)
     model.comm = comm
@@ -64,13 +67,13 @@ def run_cnnblstm(comm=None, rank=0, world=1, uneven=False, steps=1):
         per = x.shape[0] // world
         sl = slice(rank * per, (rank + 1) * per)
     x, mask, tgt = x[sl].to(dev), mask[sl].to(dev), tgt[sl].to(dev)
-    early = 0
+    early = side = 0
     for _ in range(steps):
         opt.zero_grad()
         loss = l1_pow10_loss(model(x), mask, tgt)
         loss.backward()
         if red is not None:
-            early = red.early_chunks
+            early, side = red.early_chunks, red.side_reductions
             red.allreduce()
         opt.step()
     loss = loss.detach().double().reshape(1)
@@ -78,7 +81,7 @@ def run_cnnblstm(comm=None, rank=0, world=1, uneven=False, steps=1):
         comm.allreduce_sum_(loss)            # the reference loss is a batch SUM
     torch.cuda.synchronize()
     state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    return {"loss": loss.cpu(), "state": state, "early_chunks": early}
+    return {"loss": loss.cpu(), "state": state, "early_chunks": early, "side_reductions": side}
 
 
 def _gan_batch(n=2, F=257, T=100):
@@ -126,6 +129,8 @@ def main():
     assert comm.grad_group is not comm.group     # SyncBN and gradients: two communicators
     if mode == "cnnblstm":
         res = run_cnnblstm(comm, rank, world)
+    elif mode == "cnnblstm_nodefer":
+        res = run_cnnblstm(comm, rank, world, defer=False)
     elif mode == "cnnblstm_uneven":
         res = run_cnnblstm(comm, rank, world, uneven=True, steps=2)
     elif mode == "gan_faithful":

@@ -72,6 +72,24 @@ def test_cnnblstm_dp2_equals_single_process(tmp_path):
     # the layer-0 input weights' gradients went to the reducer in 4 gate chunks
     # per direction, all-reduced as they completed
     assert ranks[0]["early_chunks"] == 8
+    # the other side-stream weight gradients (encoder and decoder convs,
+    # projection, BLSTM W_hh / biases / upper W_ih) were all-reduced from the
+    # side stream as they were written -- the single-GPU overlaps kept under DP
+    assert ranks[0]["side_reductions"] > 0
+
+
+@pytest.mark.timeout(300)
+def test_cnnblstm_dp2_side_stream_reductions_bit_identical(tmp_path):
+    """Under DP, the deferred / side-stream weight gradients are handed to the
+    reducer from the side stream (no compute-stream join); the result is bit
+    for bit the one with every weight gradient synchronous (deferral off)."""
+    on = _run_ranks("cnnblstm", tmp_path)
+    off = _run_ranks("cnnblstm_nodefer", tmp_path)
+    assert off[0]["side_reductions"] == 0 < on[0]["side_reductions"]
+    assert torch.equal(on[0]["loss"], off[0]["loss"])
+    for k, v in off[0]["state"].items():
+        assert torch.equal(on[0]["state"][k], v), k
+        assert torch.equal(on[1]["state"][k], v), k
 
 
 def _check_state(ranks, ref, tol=1e-5):

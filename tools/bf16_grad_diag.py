@@ -32,7 +32,7 @@ if var in ("conv_bf16_only", "gemm_bf16_only"):
     C._ConvStackFn.apply = lambda x_, spec, tr, ntcf, comm, bf, box, dw, *p: oc(
         x_, spec, tr, ntcf, comm, conv_b, None, dw, *p)
     C._BLSTMFn.apply = lambda z, H, L, bf, sink, box, *p: ob(z, H, L, not conv_b, sink, None, *p)
-    C._ProjFn.apply = lambda z, w, b, c, f, bf, d: op(z, w, b, c, f, not conv_b, d)
+    C._ProjFn.apply = lambda z, w, b, c, f, bf, d, sk: op(z, w, b, c, f, not conv_b, d, sk)
 torch.manual_seed(0)
 model = StackedBLSTMCNN(config=cfg).cuda().train()
 X, M, Tg = torch.from_numpy(x).cuda(), torch.from_numpy(m).cuda(), torch.from_numpy(t).cuda()
