@@ -406,7 +406,10 @@ X6R_FWD = os.environ.get("AINP_X6R_FWD", "1") != "0"
 
 
 def l0_bwd_x6r_eligible(NT, I, H):
-    return L0_BWD_X6R and NT % 4 == 0 and I % 4 == 0 and (4 * H) % 256 == 0 and NT >= 256
+    """Shapes ops.lstm_l0_bwd_x6 takes: K of the weight gradient (= NT) and of
+    the data gradient (= 8H) in whole 16-deep K-tiles, the direction split on
+    the 256-row tile grid, 4-row groups of the k-major operands."""
+    return (L0_BWD_X6R and NT % 16 == 0 and I % 4 == 0 and (4 * H) % 256 == 0 and NT >= 256)
 
 
 def lstm_l0_bwd_x6(dg, wf, wr, x, dx, dwf, dwr):
