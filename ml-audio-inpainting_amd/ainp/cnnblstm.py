@@ -341,6 +341,13 @@ class _BLSTMFn(torch.autograd.Function):
             if pair:
                 dxi = torch.empty(NT, Il, device=dh.device)
                 gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
+                if ops.PAIR_JOIN:
+                    # the side stream's queued weight gradients finish first at
+                    # full width: the pair kernel (160 KB of LDS per workgroup)
+                    # cannot share a CU with them
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    main.wait_event(ev)
                 ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
             if early:   # p.grad set and reduced by _wih_grad_chunked: nothing for autograd
                 gwi = [None, None]

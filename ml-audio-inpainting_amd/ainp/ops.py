@@ -399,6 +399,8 @@ def gemm_x6_multi(problems):
 # AINP_L0_BWD_X6R=0 keeps the layer-0 backward pair on two streams (128 x 128
 # x6 kernels: dX on the current stream, the split-K weight gradient beside it)
 L0_BWD_X6R = os.environ.get("AINP_L0_BWD_X6R", "1") != "0"
+# AINP_PAIR_JOIN=1: the pair waits for the side stream's weight gradients
+PAIR_JOIN = os.environ.get("AINP_PAIR_JOIN", "0") == "1"
 # the fp32 layer-0 projection on the split-plane tile (AINP_X6R_FWD=0: on
 # gemm_x6nt_256; 1.73 vs 2.15 ms alone, profiles/r03_x6r_probe.log)
 # (bit-identical to gemm_x6nt_256)

@@ -1428,6 +1428,168 @@ __global__ __launch_bounds__(256, 4) void conv_gen_nhwc16_kernel(ConvGenParams p
   conv_gen_epilogue<BM>(p, acc, act, reinterpret_cast<double*>(sA));
 }
 
+// LDS-DMA ring variant (the default; AINP_CONV16_RING=0 keeps the kernel
+// above): the same tiles, K order, MFMA and epilogue, but the operand rows
+// (a weight row's or a pixel's 64-byte K-tile slice) go straight from global
+// memory into a 4-stage LDS ring by global_load_lds_dwordx4 -- lane l of a
+// wave instruction moves 16 bytes of row 16i + l/4, the chunk XOR-swizzled on
+// the source address (g256's image layout: conflict-free ds_read_b128
+// fragments) -- with two K-tiles in flight across each barrier (counted
+// vmcnt, raw s_barrier): one barrier per K-tile instead of two, and the
+// gathers' latency spread over three K-tiles instead of hidden by occupancy
+// alone.  Window taps outside the input read a 64-byte zero row.
+namespace cgr {
+constexpr int NST = 4, ROWB = 64;
+__device__ __attribute__((aligned(64))) uint16_t zero_row[32];   // zero-initialised
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+}  // namespace cgr
+
+template <int BM, bool EXP>
+__global__ __launch_bounds__(256, 2) void conv_gen_nhwc16_ring_kernel(ConvGenParams p, Src16 s0,
+                                                                      Src16 s1,
+                                                                      const uint16_t* __restrict__ wt16,
+                                                                      int act) {
+  constexpr int BN = 16384 / BM;
+  constexpr int WN = BN / 64;
+  constexpr int IMGA = BM * cgr::ROWB, STAGE = (BM + BN) * cgr::ROWB;   // 16 / 20 KB
+  constexpr int NA = BM / 64, NB = BN / 64;        // DMA instructions per wave per K-tile
+  constexpr int L = NA + NB;
+  static_assert(WN * BM * 2 * 8 <= cgr::NST * STAGE, "epilogue scratch fits the ring");
+  __shared__ __attribute__((aligned(1024))) unsigned char ring[cgr::NST * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int KK = p.KH * p.KW;
+  const int K0 = nhwc16_seg(s0.C, KK);
+  const int K = K0 + nhwc16_seg(s1.C, KK);
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px0 = (int64_t)blockIdx.x * BN;
+  const int co0 = blockIdx.y * BM;
+  const int nkt_all = K / CG_BK;
+  const int64_t kb = (int64_t)blockIdx.z * p.ktiles_per_split;
+  const int64_t ke = kb + p.ktiles_per_split;
+  const int kt_begin = (int)(kb < nkt_all ? kb : nkt_all);
+  const int kt_end = (int)(ke < nkt_all ? ke : nkt_all);
+
+  // this lane's rows: A (weights) rows 16 (NA wave + i) + lane/4, B (pixels)
+  // rows 16 (NB wave + i) + lane/4; physical chunk lane % 4 holds logical
+  // chunk swz(row, lane % 4)
+  const int cl = lane & 3;
+  const uint16_t* wsrc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = 16 * (NA * wave + i) + (lane >> 2);
+    int co = co0 + row;
+    co = co < p.Cout ? co : p.Cout - 1;          // rows past Cout: never stored
+    wsrc[i] = wt16 + (int64_t)co * K + 8 * cgr::swz(row, cl);
+  }
+  int n_[NB], byx_[NB], brow[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int row = 16 * (NB * wave + i) + (lane >> 2);
+    brow[i] = row;
+    const int64_t pix = px0 + row;
+    n_[i] = -1;
+    byx_[i] = 0;
+    if (pix < NP) {
+      n_[i] = (int)(pix / HWo);
+      const int r = (int)(pix - (int64_t)n_[i] * HWo);
+      const int oy = r / p.Wo, ox = r - oy * p.Wo;
+      byx_[i] = ((oy * p.stride - p.pad) << 16) | ((ox * p.stride - p.pad) & 0xffff);
+    }
+  }
+  const uint16_t* zero = cgr::zero_row + 8 * cl;
+
+  auto issue = [&](int kt) {
+    unsigned char* st = ring + (kt & (cgr::NST - 1)) * STAGE;
+    const int k0 = kt * CG_BK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
+                                       (__attribute__((address_space(3))) void*)(
+                                           st + (NA * wave + i) * 1024),
+                                       16, 0, 0);
+    const bool first = k0 < K0;
+    const Src16& s = first ? s0 : s1;
+    const int kr = first ? k0 : k0 - K0;
+    if (EXP && s.exp) {   // pre-expanded few-channel source: row pix, k-values kr...
+      const int seg = nhwc16_seg(s.C, KK);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const uint16_t* src = n_[i] >= 0 ? s.x + (px0 + brow[i]) * seg + kr +
+                                               8 * cgr::swz(brow[i], cl)
+                                         : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(
+                                             st + IMGA + (NB * wave + i) * 1024),
+                                         16, 0, 0);
+      }
+      return;
+    }
+    const int tap = kr / s.C, ci0 = kr - tap * s.C;
+    const int ky = tap / p.KW, kx = tap - ky * p.KW;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int iy = (byx_[i] >> 16) + ky, ix = (int)(short)(byx_[i] & 0xffff) + kx;
+      const bool inb = n_[i] >= 0 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
+      const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
+      const uint16_t* src = inb ? s.x + (((int64_t)n_[i] * s.Hs + sy) * s.Ws + sx) * s.C + ci0 +
+                                      8 * cgr::swz(brow[i], cl)
+                                : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(
+                                           st + IMGA + (NB * wave + i) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  const int wm = wave / WN, wn = wave % WN;
+  const int l31 = lane & 31, lh = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int q = 0; q < cgr::NST - 1; ++q)
+    if (kt_begin + q < kt_end) issue(kt_begin + q);
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    // tile kt landed (kt+1, kt+2 may stay in flight); stage of kt-1 free
+    const int ahead = kt_end - 1 - kt;
+    if (ahead >= 2) __builtin_amdgcn_s_waitcnt(0x0F70 | (2 * L));
+    else if (ahead == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | L);
+    else __builtin_amdgcn_s_waitcnt(0x0F70);
+    __builtin_amdgcn_s_waitcnt(0xC07F);              // lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    const unsigned char* sa = ring + (kt & (cgr::NST - 1)) * STAGE;
+    const unsigned char* sb = sa + IMGA;
+#pragma unroll
+    for (int st = 0; st < CG_BK / 16; ++st) {
+      // the next DMA's address arithmetic runs under the first MFMAs
+      if (st == 1 && kt + cgr::NST - 1 < kt_end) issue(kt + cgr::NST - 1);
+      cgx::bf16x8 a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int ra = wm * 64 + i * 32 + l31, rb = wn * 64 + i * 32 + l31;
+        a[i] = cgx::frag(sa + ra * cgr::ROWB + 16 * cgr::swz(ra, 2 * st + lh));
+        b[i] = cgx::frag(sb + rb * cgr::ROWB + 16 * cgr::swz(rb, 2 * st + lh));
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  __syncthreads();     // every wave done with the ring: the epilogue reuses it
+  conv_gen_epilogue<BM>(p, acc, act, reinterpret_cast<double*>(ring));
+}
+
 // x [N][C][H][W] fp32 (* mask plane m [N][H][W] if given) -> out [N][H][W][C]
 // bf16 (nearest-even): 64 channels x 64 columns of one row per block.
 __global__ __launch_bounds__(256) void nchw_to_nhwc16_kernel(const float* __restrict__ x,
@@ -1879,7 +2041,24 @@ extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int 
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)cdiv(NP, 16384 / BM), (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
   const bool exp = a.exp || b.exp;
-  if (BM == 128 && exp)
+  static const bool ring = [] {    // AINP_CONV16_RING=0: the register-staged kernel (A/B runs)
+    const char* e = getenv("AINP_CONV16_RING");
+    return !(e && e[0] == '0');
+  }();
+  if (ring) {
+    if (BM == 128 && exp)
+      hipLaunchKernelGGL((conv_gen_nhwc16_ring_kernel<128, true>), grid, dim3(256), 0, s, p, a, b,
+                         wt16, act);
+    else if (BM == 128)
+      hipLaunchKernelGGL((conv_gen_nhwc16_ring_kernel<128, false>), grid, dim3(256), 0, s, p, a,
+                         b, wt16, act);
+    else if (exp)
+      hipLaunchKernelGGL((conv_gen_nhwc16_ring_kernel<64, true>), grid, dim3(256), 0, s, p, a, b,
+                         wt16, act);
+    else
+      hipLaunchKernelGGL((conv_gen_nhwc16_ring_kernel<64, false>), grid, dim3(256), 0, s, p, a, b,
+                         wt16, act);
+  } else if (BM == 128 && exp)
     hipLaunchKernelGGL((conv_gen_nhwc16_kernel<128, true>), grid, dim3(256), 0, s, p, a, b, wt16, act);
   else if (BM == 128)
     hipLaunchKernelGGL((conv_gen_nhwc16_kernel<128, false>), grid, dim3(256), 0, s, p, a, b, wt16, act);

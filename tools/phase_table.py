@@ -7,8 +7,9 @@ training-step phase):
       -f csv -d <dir> -o run -- python3 bench.py --steps 5 --warmup 2 ...
   python3 tools/phase_table.py <dir>
 
-Each kernel dispatch is attributed to the innermost range that was open on
-the launching thread when its HIP launch call ran (kernel Correlation_Id ->
+Each kernel dispatch is attributed to the innermost range that was open
+(on any thread: autograd's engine thread launches the backward while the
+main thread sits in its "bwd" range) when its HIP launch call ran (kernel Correlation_Id ->
 HIP API row -> host timestamp -> marker ranges).  Prints, per phase, the
 number of dispatches, the summed kernel time and its share, and per-phase
 top kernels; kernels launched outside every range go to "(none)"."""
@@ -70,7 +71,9 @@ def main(d):
             th, t = li
             best = None
             for (rth, s, e, nm) in rs:
-                if s <= t <= e and (th is None or rth is None or rth == th):
+                # time containment only: the backward's kernels are launched by
+                # autograd's engine thread while the main thread sits in "bwd"
+                if s <= t <= e:
                     if best is None or (e - s) < best[0]:
                         best = (e - s, nm)
             if best:
