@@ -24,6 +24,7 @@ through `comm` (SyncBN), so a DP run matches the single-process reference.
 """
 from __future__ import annotations
 
+import atexit
 import os
 
 import torch
@@ -457,7 +458,8 @@ def _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, sink, wih0, rows=None, l016=Non
     return bufs
 
 
-_SIDE_STREAMS: dict = {}
+_SIDE_STREAMS: dict = {}   # torch pool streams (never destroyed by torch); cleared at exit
+atexit.register(_SIDE_STREAMS.clear)
 
 
 def _alias(t):
@@ -603,6 +605,8 @@ class _ProjFn(torch.autograd.Function):
         NO = C * F
         K = h.shape[2]
         g = g.contiguous()
+        if not ctx.bf16 and not ops.GEMM_EXACT and ops.proj_bwd_x6_eligible(N * T, NO, K):
+            return _ProjFn._backward_x6(ctx, g, h, w)
         # dh_n[t][k] = sum_col g_n[col][t] w[col][k]: only 6 output tiles per
         # example, so the col sum (K = C*F) is split over S pointer batches into
         # slabs (4x the workgroups) and combined in fixed order
@@ -637,6 +641,33 @@ class _ProjFn(torch.autograd.Function):
                            params=ctx.param_objs, sink=ctx.sink)
         else:
             wgrad(dw, db)
+        return dh, dw, db, None, None, None, None, None
+
+    @staticmethod
+    def _backward_x6(ctx, g, h, w):
+        """fp32: both gradients on the x6r MFMA tile (ops.proj_bwd_x6) from the
+        gradient permuted once to [C*F, N*T] -- every column of the reduction
+        then lies at one stride, where the [N][C*F][T] layout needs a pointer
+        batch per example."""
+        N, C, F, T = ctx.shape
+        NO, K = C * F, h.shape[2]
+        gp = g.view(N, NO, T).transpose(0, 1).contiguous().view(NO, N * T)
+        h2 = h.view(N * T, K)
+        dh = torch.empty(N, T, K, device=g.device, dtype=torch.float32)
+        dw = torch.empty(NO, K, device=g.device)
+        db = torch.empty(NO, device=g.device)
+        if ctx.defer_wgrad and not ops.PROJ_JOINT:
+            ops.proj_bwd_x6(gp, h2, w, dh=dh.view(N * T, K))
+
+            def wgrad(dw, db):
+                ops.proj_bwd_x6(gp, h2, w, dw=dw)
+                ops.rowsum_batched(gp.view(1, NO, N * T), out=db)
+            dwv, dbv = _alias(dw), _alias(db)
+            _Deferred.push(g.device, lambda: wgrad(dwv, dbv), (gp, h), (dwv, dbv),
+                           params=ctx.param_objs, sink=ctx.sink)
+        else:
+            ops.proj_bwd_x6(gp, h2, w, dh=dh.view(N * T, K), dw=dw)
+            ops.rowsum_batched(gp.view(1, NO, N * T), out=db)
         return dh, dw, db, None, None, None, None, None
 
 

@@ -12,9 +12,12 @@ this module fails when libainp_torch.so is missing.  Host-only queries
 """
 from __future__ import annotations
 
+import atexit
 import functools
-import os
+import heapq
+import itertools
 import math
+import os
 import weakref
 
 import numpy as np
@@ -31,6 +34,24 @@ if not os.path.exists(TORCH_OPS_PATH):
                       "`make -C ml-audio-inpainting_amd/csrc` (or __graft_entry__.build())")
 torch.ops.load_library(TORCH_OPS_PATH)
 _T = torch.ops.ainp
+
+
+def _release_device_caches():
+    """atexit: drop the module-level device tensors (windows, GEMM workspaces,
+    bf16 weight copies) while the HIP runtime is still up, so nothing of ours
+    is freed from a static destructor during __cxa_finalize, after the runtime
+    (and a profiler's tool library) has been torn down -- the failure mode of
+    round 2's dropped CU-masked-stream variant."""
+    try:
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except Exception:   # noqa: BLE001 -- best effort at interpreter exit
+        pass
+    for c in (_WIN_CACHE, _GEMM_WS, _EMPTY, _WT_CACHE):
+        c.clear()
+
+
+atexit.register(_release_device_caches)
 
 FEAT_CNNBLSTM = 0
 FEAT_GAN = 1
@@ -399,7 +420,7 @@ def gemm_x6_multi(problems):
 # AINP_L0_BWD_X6R=0 keeps the layer-0 backward pair on two streams (128 x 128
 # x6 kernels: dX on the current stream, the split-K weight gradient beside it)
 L0_BWD_X6R = os.environ.get("AINP_L0_BWD_X6R", "1") != "0"
-# AINP_PAIR_JOIN=1: the pair waits for the side stream's weight gradients
+# AINP_PAIR_JOIN=1 (measured slower, 16.6 vs 16.1 ms C2 step, profiles/r03_ab1_*): the pair waits for the side stream's weight gradients
 PAIR_JOIN = os.environ.get("AINP_PAIR_JOIN", "0") == "1"
 # the fp32 layer-0 projection on the split-plane tile (AINP_X6R_FWD=0: on
 # gemm_x6nt_256; 1.73 vs 2.15 ms alone, profiles/r03_x6r_probe.log)
@@ -455,6 +476,97 @@ def gemm_x6r_nt(A, B1, B2, out, bias=(None, None, None, None), bias_nsplit=0, ns
                               ldc=N, nsplit=S, kc=kc, strideC=M * N, **kw)])
     sum_slabs(slabs, S, out=out.view(-1))
     return out
+
+
+# AINP_PROJ_X6R=0 keeps the fp32 output-projection backward on gemm_f32
+# (pointer-batched FMA GEMMs over the [N, C*F, T] gradient as it lies)
+PROJ_X6R = os.environ.get("AINP_PROJ_X6R", "1") != "0"
+# AINP_PROJ_JOINT=1: dh and dW in one launch even when the weight gradient
+# could be deferred to the side stream (A/B)
+PROJ_JOINT = os.environ.get("AINP_PROJ_JOINT", "0") == "1"
+_X6R_SLOTS = 256        # one 160 KB-LDS workgroup per CU
+
+
+def _x6r_makespan(items_kt, slots=_X6R_SLOTS):
+    """Finish time (in K-tiles) of work items dispatched in grid order onto
+    `slots` CUs, each taking the next item when it frees (items_kt: K-tiles
+    per item)."""
+    free = [0] * slots
+    heapq.heapify(free)
+    end = 0
+    for kt in items_kt:
+        t = heapq.heappop(free) + kt
+        end = max(end, t)
+        heapq.heappush(free, t)
+    return end
+
+
+@functools.lru_cache(maxsize=64)
+def x6r_splits(shapes, max_split=16):
+    """Split-K counts for problems (M, N, K) launched together on the x6r tile:
+    minimise the estimated makespan plus the slab traffic (each split > 1 writes
+    S slabs that ainp_sum_slabs reads back).  Returns ((S, kc), ...)."""
+    def opts(M, N, K):
+        out = []
+        for S in range(1, max_split + 1):
+            kc = -(-K // S // 16) * 16 if S > 1 else K
+            if S > 1 and -(-K // kc) != S:
+                continue
+            out.append((S, kc))
+        return out
+    best, best_t = None, None
+    for combo in itertools.product(*(opts(*s) for s in shapes)):
+        items = []
+        slab = 0.0
+        for (M, N, K), (S, kc) in zip(shapes, combo):
+            tiles = -(-M // 256) * -(-N // 256)
+            items += [kc // 16] * (tiles * S)
+            if S > 1:
+                slab += (S + 1) * M * N * 4
+        # K-tile of a 256 x 256 x16 x6 item ~ 4.5 us at the measured rate
+        t = _x6r_makespan(items) * 4.5e-6 + slab / _SLAB_RATE
+        if best_t is None or t < best_t:
+            best, best_t = combo, t
+    return best
+
+
+def proj_bwd_x6_eligible(NT, NO, K):
+    """Output projection shapes the x6r backward takes: whole 16-deep K-tiles
+    (K of dW = N*T, of dh = C*F) and 4-row groups of the k-major operands."""
+    return PROJ_X6R and NT % 16 == 0 and NO % 16 == 0 and K % 4 == 0
+
+
+def proj_bwd_x6(gp, h, w, dh=None, dw=None):
+    """The fp32 output-projection gradients of nn.Linear(2H, C*F)
+    (models/CNNBLSTM/model.py:48,78) on the x6r tile, from the gradient
+    permuted to gp [C*F, N*T] (row c*... = output column, k = n*T + t):
+        dh [NT, K] = gp^T [NT, NO] . w [NO, K]   (both operands k-major)
+        dW [NO, K] = gp   [NO, NT] . h [NT, K]   (h k-major)
+    Either output may be None; both given -> ONE launch.  Rows of gp are the
+    C*F output columns, its columns k = n*T + t."""
+    NO, NT = gp.shape
+    K = h.shape[-1]
+    for t in (gp, h, w):
+        _req(t, "operand")
+    # each problem's split-K is chosen for it alone, so the joint launch and
+    # two separate ones (side-stream deferral) give bit-identical gradients
+    probs, outs = [], []
+    if dh is not None:
+        (S, kc), = x6r_splits(((NT, K, NO),))
+        C = dh if S == 1 else torch.empty(S, NT, K, device=gp.device)
+        probs.append(x6_problem(gp, w, C, M=NT, N=K, K=NO, lda=NT, ldb=K, ldc=K, a_kmajor=True,
+                                b_kmajor=True, nsplit=S, kc=kc, strideC=NT * K))
+        outs.append((dh, C, S))
+    if dw is not None:
+        (S, kc), = x6r_splits(((NO, K, NT),))
+        C = dw if S == 1 else torch.empty(S, NO, K, device=gp.device)
+        probs.append(x6_problem(gp, h, C, M=NO, N=K, K=NT, lda=NT, ldb=K, ldc=K, b_kmajor=True,
+                                nsplit=S, kc=kc, strideC=NO * K))
+        outs.append((dw, C, S))
+    gemm_x6_multi(probs)
+    for o, C, S in outs:
+        if S > 1:
+            sum_slabs(C, S, out=o.view(-1))
 
 
 def gemm_bf16nt_splitk(A, B, K, out=None, max_split=16):

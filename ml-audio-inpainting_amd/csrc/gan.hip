@@ -1428,8 +1428,8 @@ __global__ __launch_bounds__(256, 4) void conv_gen_nhwc16_kernel(ConvGenParams p
   conv_gen_epilogue<BM>(p, acc, act, reinterpret_cast<double*>(sA));
 }
 
-// LDS-DMA ring variant (the default; AINP_CONV16_RING=0 keeps the kernel
-// above): the same tiles, K order, MFMA and epilogue, but the operand rows
+// LDS-DMA ring variant (opt-in, AINP_CONV16_RING=1; measured slower than the
+// kernel above on the C4 bf16 step, 11.66 vs 10.59 ms, profiles/r03_ab1_*): the same tiles, K order, MFMA and epilogue, but the operand rows
 // (a weight row's or a pixel's 64-byte K-tile slice) go straight from global
 // memory into a 4-stage LDS ring by global_load_lds_dwordx4 -- lane l of a
 // wave instruction moves 16 bytes of row 16i + l/4, the chunk XOR-swizzled on
@@ -2041,9 +2041,9 @@ extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int 
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)cdiv(NP, 16384 / BM), (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
   const bool exp = a.exp || b.exp;
-  static const bool ring = [] {    // AINP_CONV16_RING=0: the register-staged kernel (A/B runs)
+  static const bool ring = [] {    // AINP_CONV16_RING=1: the LDS-DMA ring kernel (A/B runs)
     const char* e = getenv("AINP_CONV16_RING");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   if (ring) {
     if (BM == 128 && exp)

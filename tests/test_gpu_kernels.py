@@ -867,6 +867,37 @@ def test_lstm_l0_bwd_x6_pair(ops, NT, H, I):
         assert rel(dW, torch.cat([ow[0], ow[1]]).cpu()) < 1e-6
 
 
+@pytest.mark.parametrize("N,T,C,F,K", [(2, 48, 4, 20, 64), (3, 112, 16, 33, 256),
+                                       (32, 528, 16, 257, 256)])
+def test_proj_bwd_x6(ops, N, T, C, F, K):
+    """The fp32 output-projection backward on the x6r tile (ops.proj_bwd_x6,
+    nn.Linear(2H, C*F) of models/CNNBLSTM/model.py:48,78): dh = g^T w and
+    dW = g h from the gradient permuted to [C*F, N*T], against fp64 (a few
+    times torch's fp32 CPU GEMM, floor 2e-6: split-K slabs at the C2 shape),
+    and the joint launch bit-identical to the two separate ones."""
+    g = torch.Generator().manual_seed(N * T + K)
+    NO, NT = C * F, N * T
+    gr = (torch.randn(N, NO, T, generator=g) * 1e-2).to(DEV)
+    h = torch.tanh(torch.randn(NT, K, generator=g)).to(DEV)
+    w = (torch.randn(NO, K, generator=g) * 0.05).to(DEV)
+    gp = gr.transpose(0, 1).contiguous().view(NO, NT)
+    dh = torch.full((NT, K), float("nan"), device=DEV)
+    dw = torch.full((NO, K), float("nan"), device=DEV)
+    ops.proj_bwd_x6(gp, h, w, dh=dh, dw=dw)
+    dh1 = torch.full((NT, K), float("nan"), device=DEV)
+    dw1 = torch.full((NO, K), float("nan"), device=DEV)
+    ops.proj_bwd_x6(gp, h, w, dh=dh1)
+    ops.proj_bwd_x6(gp, h, w, dw=dw1)
+    torch.cuda.synchronize()
+    assert torch.equal(dh, dh1) and torch.equal(dw, dw1)
+    g64, h64, w64 = gp.double().cpu(), h.double().cpu(), w.double().cpu()
+    rh, rw = g64.T @ w64, g64 @ h64
+    fh = (gp.cpu().T @ w.cpu()).double()
+    fw = (gp.cpu() @ h.cpu()).double()
+    assert rel(dh.cpu(), rh) < max(4 * rel(fh, rh), 2e-6), (rel(dh.cpu(), rh), rel(fh, rh))
+    assert rel(dw.cpu(), rw) < max(4 * rel(fw, rw), 2e-6), (rel(dw.cpu(), rw), rel(fw, rw))
+
+
 def test_gemm_x6_multi_equals_separate_launches(ops):
     """Problems launched together (one grid) give bit-identical results to the
     same problems launched one by one; a split-K problem writes its slabs."""
