@@ -306,7 +306,10 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
                      "workgroup into double-buffered LDS bf16 planes while the previous "
                      "tile's MFMAs run (one barrier per K-tile)")
     avg_s = time_kernel(fwd, reps, dev)
-    traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else "traffic_gemm_l0.json")
+    # committed rocprofv3 FETCH/WRITE passes over the same kernel (tools/pmc_x6r.sh,
+    # tools/pmc_gemm.sh)
+    traffic = _traffic("traffic_gemm_l0_bf16.json" if bf16 else
+                       "traffic_gemm_l0_x6r.json" if ops.X6R_FWD else "traffic_gemm_l0.json")
     roof = _roof(flops, avg_s, bf16, kname + f" (LSTM l0 input projection, M={M} N={8 * H} "
                  f"K={I}, both directions)", traffic=traffic, main_loop=main_loop)
 
@@ -332,6 +335,7 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
     roof_bwd = _roof(2 * flops, pair_s, bf16, bname + f" (M={M}, 8H={8 * H}, K={I})",
                      two_stream_dx_alone_ms=round(dx_s * 1e3, 4),
                      two_stream_dw_alone_ms=round(dw_s * 1e3, 4),
+                     traffic=_traffic("traffic_l0_pair_x6r.json") if fused is not None else None,
                      what=("both GEMMs in one launch, as cnnblstm._BLSTMFn.backward runs them"
                            if fused is not None else
                            "dX on the current stream beside dW on a side stream, as "

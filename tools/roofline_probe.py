@@ -1,7 +1,8 @@
 """Launch only the bench's roofline kernel (LSTM layer-0 input projection GEMM,
 M=N*T=10688, N=8H=1024, K=C*F=16448) a few times: fp32 -> the x6 split on fp32
-operands (the 256x256 LDS-DMA tile, split 3 + slab sum, as the step runs it;
-argv[2] == fp32old: the 128x128 gemm_f32 loop); bf16 (argv[2]) -> gemm_bf16nt
+operands (the 256x256 x6r tile, split 3 + slab sum, as the step runs it;
+argv[2] == fp32old: the 128x128 gemm_f32 loop; pair: the fused layer-0
+backward dX + dW_ih launch); bf16 (argv[2]) -> gemm_bf16nt
 on bf16 X / W_cat, as the bench times it.  The target of the rocprofv3 --pmc passes behind
 profiles/traffic_gemm_l0*.json."""
 import os, sys
@@ -28,8 +29,19 @@ elif len(sys.argv) > 2 and sys.argv[2] == "fp32old":
     for _ in range(reps):
         ops.gemm(M, 4 * H, I, [A, A], I, 1, W, 1, I, [zx, zx[:, 4 * H:]], 8 * H, 1,
                  bias1=b[:2], bias2=b[2:])
+elif len(sys.argv) > 2 and sys.argv[2] == "pair":
+    # the fused layer-0 backward pair (dX + dW_ih in one x6r launch)
+    dg = torch.randn(M, 8 * H, device=dev) * 1e-3
+    dx = torch.empty(M, I, device=dev)
+    dw = [torch.empty(4 * H, I, device=dev) for _ in range(2)]
+    for _ in range(reps):
+        ops.lstm_l0_bwd_x6(dg, W[0], W[1], A, dx, dw[0], dw[1])
 else:
     for _ in range(reps):
-        ops.gemm_x6nt_256(A, W[0], W[1], zx, bias=(b[0], b[2], b[1], b[3]), bias_nsplit=4 * H)
+        if ops.X6R_FWD:   # the step's kernel (gemm_x6r.hip), as the bench times it
+            ops.gemm_x6r_nt(A, W[0], W[1], zx, bias=(b[0], b[2], b[1], b[3]), bias_nsplit=4 * H)
+        else:
+            ops.gemm_x6nt_256(A, W[0], W[1], zx, bias=(b[0], b[2], b[1], b[3]),
+                              bias_nsplit=4 * H)
 torch.cuda.synchronize()
 print("done")
