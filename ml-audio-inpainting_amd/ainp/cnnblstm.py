@@ -727,6 +727,14 @@ class StackedBLSTMCNN(nn.Module):
         if dtype not in ("fp32", "bf16"):
             raise ValueError(f"accel.dtype must be fp32 or bf16, got {dtype!r}")
         self.bf16 = dtype == "bf16"
+        # accel.deterministic (default true): every kernel on the path reduces in
+        # a fixed order, so runs are bit-reproducible; true also makes the one
+        # atomic-accumulating entry point (ops.colsum(accumulate=True)) raise
+        det = (full_cfg.get("accel") or {}).get("deterministic", True)
+        if not isinstance(det, bool):
+            raise ValueError(f"accel.deterministic must be true or false, got {det!r}")
+        self.deterministic = det
+        ops.set_deterministic(det)
         # identical construction order to model.py:34-61 (same init RNG draws)
         self.encoder = nn.Sequential(
             nn.Conv2d(self.in_channels, self.enc_filters[0], kernel_size=3, padding=1),

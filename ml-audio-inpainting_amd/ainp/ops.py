@@ -798,14 +798,28 @@ def rowsum_batched(x3d, out=None):
     return out
 
 
+_DETERMINISTIC = True
+
+
+def set_deterministic(on: bool) -> None:
+    """accel.deterministic: forbid the atomic-accumulating entry points (the
+    only non-fixed-order reductions; nothing on the training path uses them)."""
+    global _DETERMINISTIC
+    _DETERMINISTIC = bool(on)
+
+
 def colsum(x2d, out=None, accumulate=False):
     """Column sums of a row-major [rows, cols] view.  Default: fixed-order row
     slabs combined by sum_slabs (deterministic);
-    accumulate=True adds into `out` with float atomics."""
+    accumulate=True adds into `out` with float atomics (refused under
+    accel.deterministic)."""
     rows, cols = x2d.shape
     ld = x2d.stride(0)
     assert x2d.stride(1) == 1
     if accumulate:
+        if _DETERMINISTIC:
+            raise RuntimeError("ops.colsum(accumulate=True) uses float atomics; "
+                               "accel.deterministic is set")
         _T.colsum(x2d, rows, cols, ld, out, True)
         return out
     # ~256 workgroups of column sums; the slab combine then reads nslabs*cols

@@ -146,6 +146,23 @@ def test_init_parity_with_reference_construction(golden_dir):
         assert abs(float(sd[k].double().sum()) - chk[0]) <= 1e-6 * max(1, abs(chk[0])), k
 
 
+def test_accel_deterministic_flag():
+    """accel.deterministic: validated, default true, and under it the atomic
+    colsum entry point refuses before launching anything (host-side check)."""
+    from ainp import ops
+    from ainp.cnnblstm import StackedBLSTMCNN
+    cfg = {"data": {"spectrogram": {"n_fft": 64}},
+           "model": {"in_channels": 1, "num_lstm_layers": 1, "lstm_hidden_dim": 8,
+                     "enc_filters": [4, 8], "dec_filters": [4, 8]}}
+    assert StackedBLSTMCNN(config=cfg).deterministic is True
+    with pytest.raises(ValueError):
+        StackedBLSTMCNN(config=dict(cfg, accel={"deterministic": "yes"}))
+    assert StackedBLSTMCNN(config=dict(cfg, accel={"deterministic": False})).deterministic is False
+    StackedBLSTMCNN(config=dict(cfg, accel={"deterministic": True}))
+    with pytest.raises(RuntimeError, match="deterministic"):
+        ops.colsum(torch.zeros(4, 4), out=torch.zeros(4), accumulate=True)
+
+
 def test_state_dict_keys_match_reference_layout(golden_dir):
     g = np.load(os.path.join(golden_dir, "cnnblstm_small.npz"), allow_pickle=False)
     cfg, _, _ = _small_cfg(g)

@@ -267,6 +267,21 @@ def test_loss_curve_30_steps_matches_reference(golden_dir):
             assert rel(v, r) < 1e-3, (k, rel(v, r))
 
 
+def test_training_run_is_bit_reproducible(golden_dir):
+    """accel.deterministic: every reduction on the path is a
+    fixed-order slab / tree sum (no atomics, no stream-order-dependent
+    accumulation), so two runs of the same 8-step schedule -- side streams,
+    split-K slabs and the two-pass loss included -- give bit-identical losses,
+    parameters and BatchNorm statistics."""
+    g = np.load(os.path.join(golden_dir, "cnnblstm_curve.npz"), allow_pickle=False)
+    l1, m1 = run_curve(g, steps=8)
+    l2, m2 = run_curve(g, steps=8)
+    assert np.array_equal(l1, l2), (l1, l2)
+    s2 = m2.state_dict()
+    for k, v in m1.state_dict().items():
+        assert torch.equal(v, s2[k]), k
+
+
 def test_loss_curve_frozen_bn_biases_matches_reference_without_waiver(golden_dir):
     """cnnblstm_curve_fixbias.npz: the 30-step schedule with the five BN-fed
     conv biases out of Adam in the reference run and here.  With nothing
