@@ -547,6 +547,14 @@ int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0, const u
                              const float* ratio, const float* scale, float* y, double* stats,
                              int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
                              int pad, int act, float slope, void* workspace, void* stream);
+/* Main loop of ainp_conv_gen_fwd_nhwc16 (same sums, bit for bit, in every
+ * variant): 0 register-staged 128x128 / 64x256 tiles, 1 the same tiles on an
+ * LDS-DMA ring, 2 wide tiles (256x128 / 128x256 / 64x256) of 4 waves on a
+ * 3-stage LDS-DMA ring with XCD-major workgroup order, 3 the same tiles with 8
+ * waves of 64x64 (Cout > 64; variant 0 below; the default).  Returns the
+ * previous variant; an out-of-range v only queries.  Initial value: env
+ * AINP_CONV16. */
+int ainp_conv16_set_variant(int v);
 /* PartialConv2d mask update (networks.py:83-104, multi_channel=False):
  * count = C0*window_sum(m0) + C1*window_sum(m1) over the conv's window (masks
  * are planes of integer counts -- 0/1, or a channel sum -- repeated over their

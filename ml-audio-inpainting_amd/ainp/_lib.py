@@ -159,6 +159,7 @@ _SIGS = {
     "ainp_conv_weight_nhwc16": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "ainp_im2col_nhwc16": (c_int, [P, P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                    c_int, c_int, P, P]),
+    "ainp_conv16_set_variant": (c_int, [c_int]),
     "ainp_conv_gen_fwd_nhwc16": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, P, P, P,
                                          P, P, P, c_int64, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_float, P, P]),

@@ -951,6 +951,14 @@ def to_nhwc16(x, m=None):
     return out
 
 
+def conv16_set_variant(v):
+    """Main loop of the bf16 channel-last conv (ainp_conv16_set_variant): 0
+    register-staged tiles, 1 LDS-DMA ring, 2 / 3 wide-tile ring of 4 / 8 waves
+    (3: Cout > 64 only, else 0); same sums in all.  Returns the previous variant
+    (v outside 0..3 only queries)."""
+    return int(_lib.lib.ainp_conv16_set_variant(int(v)))
+
+
 def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=None, ratio=None,
              scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None,
              bf16=False, launcher=False):
@@ -1014,6 +1022,7 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
                                    int(act), float(slope), ws,
                                    [int(N), int(C0), int(H0), int(W0), int(C1), int(H1), int(W1)])
         if launcher:   # bench / profiling: the conv kernel alone on prepared operands
+            launch.out, launch.stats = out, stats
             return launch
         launch()
         return out, stats

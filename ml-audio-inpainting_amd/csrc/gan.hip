@@ -1590,6 +1590,288 @@ __global__ __launch_bounds__(256, 2) void conv_gen_nhwc16_ring_kernel(ConvGenPar
   conv_gen_epilogue<BM>(p, acc, act, reinterpret_cast<double*>(ring));
 }
 
+// ------------------------------------------------ bf16 NHWC, wide-tile ring
+// conv_gen_nhwc16 on twice the tile area (AINP_CONV16=2 / ainp_conv16_set_variant):
+// the kernels above stage 16 KB of operand rows per 1 MFLOP (128 x 128 or
+// 64 x 256 tiles, 32-deep K-tiles), so at the layers' re-use they are bound
+// by the L2 -> LDS row traffic and the latency of the gathers.  Here:
+//  * Cout > 128: 256 (co) x 128 (pixels); Cout 65..128: 128 x 256; both with
+//    four waves of 128 x 64 (4 x 2 v_mfma_f32_32x32x16_bf16: 16 MFMAs and 12
+//    ds_read_b128 per wave per K-tile), 8 KB of rows per MFLOP;
+//  * Cout <= 64: 64 x 256, waves of 64 x 64 (the previous kernels' tile);
+//  * rows go global -> LDS by global_load_lds_dwordx4 into a 3-stage ring
+//    (two K-tiles in flight across the one raw barrier per K-tile, counted
+//    vmcnt; g256's XOR-swizzled 64-byte row image), 60-72 KB: two
+//    workgroups (8 waves) per CU;
+//  * workgroups are numbered XCD-major (each XCD's L2 owns a contiguous range
+//    of pixel tiles) and, within it, co-tile fastest, so the co-tiles that
+//    gather the same pixel rows run side by side on one L2.
+// Same K order and per-output MFMA chain as conv_gen_nhwc16_kernel (so the
+// same sums, bit for bit); the BatchNorm partials keep that kernel's
+// per-128/256-pixel slot layout (ainp_conv_gen_stat_parts).
+namespace cgw {
+constexpr int NST = 3, ROWB = 64;
+// NW = 4: waves of 128 x 64 (64 x 64 for BM = 64); NW = 8 (BM >= 128): waves
+// of 64 x 64, two workgroups of 8 waves per CU.
+template <int BM, int NW>
+struct Cfg {
+  static constexpr int WM = (NW == 4 && BM >= 128) ? 128 : 64;   // wave tile (co)
+  static constexpr int WGM = BM / WM;                            // waves along co
+  static constexpr int WGN = NW / WGM;                           // waves along pixels
+  static constexpr int WNP = 64;                                 // wave tile (pixels)
+  static constexpr int BN = WGN * WNP;                           // tile pixels
+  static constexpr int MI = WM / 32, NJ = WNP / 32;
+  static constexpr int NA = BM / 16 / NW, NB = BN / 16 / NW;     // 1 KB DMA blocks per wave
+  static constexpr int L = NA + NB;
+  static constexpr int STAGE = (BM + BN) * ROWB;
+  static constexpr int OLD_BN = 16384 / (BM > 64 ? 128 : 64);   // stats slot width
+  static_assert(NA * NW * 16 == BM && NB * NW * 16 == BN, "whole DMA blocks per wave");
+};
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
+}  // namespace cgw
+
+template <int BM, int NW, bool EXP>
+__global__ __launch_bounds__(NW * 64, 2) void conv_gen_nhwc16_wide_kernel(ConvGenParams p, Src16 s0,
+                                                                      Src16 s1,
+                                                                      const uint16_t* __restrict__ wt16,
+                                                                      int act, int tiles_co,
+                                                                      int tiles_px) {
+  using C = cgw::Cfg<BM, NW>;
+  constexpr int BN = C::BN, MI = C::MI, NJ = C::NJ, NA = C::NA, NB = C::NB, L = C::L;
+  constexpr int IMGA = BM * cgw::ROWB;
+  static_assert(C::WGN * BM * 2 * 8 <= cgw::NST * C::STAGE, "epilogue scratch fits the ring");
+  __shared__ __attribute__((aligned(1024))) unsigned char ring[cgw::NST * C::STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-major numbering: hardware XCD = blockIdx.x % 8 owns a contiguous range
+  const int nwg = gridDim.x, b0 = blockIdx.x;
+  const int xcd = b0 & 7, slot = b0 >> 3, q8 = nwg >> 3, r8 = nwg & 7;
+  const int bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int co_t = bid % tiles_co, px_t = bid / tiles_co;
+  const int KK = p.KH * p.KW;
+  const int K0 = nhwc16_seg(s0.C, KK);
+  const int K = K0 + nhwc16_seg(s1.C, KK);
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px0 = (int64_t)px_t * BN;
+  const int co0 = co_t * BM;
+  const int nkt_all = K / CG_BK;
+  const int64_t kb = (int64_t)blockIdx.y * p.ktiles_per_split;
+  const int64_t ke = kb + p.ktiles_per_split;
+  const int kt_begin = (int)(kb < nkt_all ? kb : nkt_all);
+  const int kt_end = (int)(ke < nkt_all ? ke : nkt_all);
+
+  // DMA blocks of this wave: block 4i + wave (16 image rows); i < NA: weight
+  // rows, else pixel rows.  Lane: row 16 blk + lane/4, physical chunk lane%4
+  // holding logical chunk swz(row, lane%4).
+  const int cl = lane & 3;
+  const uint16_t* wsrc[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int row = 16 * (NW * i + wave) + (lane >> 2);
+    int co = co0 + row;
+    co = co < p.Cout ? co : p.Cout - 1;          // rows past Cout: never stored
+    wsrc[i] = wt16 + (int64_t)co * K + 8 * cgw::swz(row, cl);
+  }
+  int n_[NB], byx_[NB], brow[NB], bchunk[NB];
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    const int row = 16 * (NW * (NA + i) + wave) + (lane >> 2) - BM;   // pixel row in the tile
+    brow[i] = row;
+    bchunk[i] = 8 * cgw::swz(row + BM, cl);
+    const int64_t pix = px0 + row;
+    n_[i] = -1;
+    byx_[i] = 0;
+    if (pix < NP) {
+      n_[i] = (int)(pix / HWo);
+      const int r = (int)(pix - (int64_t)n_[i] * HWo);
+      const int oy = r / p.Wo, ox = r - oy * p.Wo;
+      byx_[i] = ((oy * p.stride - p.pad) << 16) | ((ox * p.stride - p.pad) & 0xffff);
+    }
+  }
+  const uint16_t* zero = cgr::zero_row + 8 * cl;
+
+  auto issue = [&](int kt) {
+    unsigned char* st = ring + (kt % cgw::NST) * C::STAGE;
+    const int k0 = kt * CG_BK;
+#pragma unroll
+    for (int i = 0; i < NA; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(wsrc[i] + k0),
+                                       (__attribute__((address_space(3))) void*)(
+                                           st + (NW * i + wave) * 1024),
+                                       16, 0, 0);
+    const bool first = k0 < K0;
+    const Src16& s = first ? s0 : s1;
+    const int kr = first ? k0 : k0 - K0;
+    if (EXP && s.exp) {   // pre-expanded few-channel source: row pix, k-values kr...
+      const int seg = nhwc16_seg(s.C, KK);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) {
+        const uint16_t* src = n_[i] >= 0 ? s.x + (px0 + brow[i]) * seg + kr + bchunk[i] : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)(
+                                             st + (NW * (NA + i) + wave) * 1024),
+                                         16, 0, 0);
+      }
+      return;
+    }
+    const int tap = kr / s.C, ci0 = kr - tap * s.C;
+    const int ky = tap / p.KW, kx = tap - ky * p.KW;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) {
+      const int iy = (byx_[i] >> 16) + ky, ix = (int)(short)(byx_[i] & 0xffff) + kx;
+      const bool inb = n_[i] >= 0 && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      const int sy = inb ? src_coord(iy, s.Hs, p.Hin, s.up) : 0;
+      const int sx = inb ? src_coord(ix, s.Ws, p.Win, s.up) : 0;
+      const uint16_t* src = inb ? s.x + (((int64_t)n_[i] * s.Hs + sy) * s.Ws + sx) * s.C + ci0 +
+                                      bchunk[i]
+                                : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(
+                                           st + (NW * (NA + i) + wave) * 1024),
+                                       16, 0, 0);
+    }
+  };
+
+  const int wm = wave / C::WGN, wn = wave % C::WGN;
+  const int l31 = lane & 31, lh = lane >> 5;
+  f32x16 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+#pragma unroll
+  for (int q = 0; q < cgw::NST - 1; ++q)
+    if (kt_begin + q < kt_end) issue(kt_begin + q);
+  for (int kt = kt_begin; kt < kt_end; ++kt) {
+    // tile kt landed (kt+1 may stay in flight); every wave is past tile kt-1,
+    // whose stage the DMA of kt+2 reuses
+    if (kt + 1 < kt_end) {
+      if (L == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if (L == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + cgw::NST - 1 < kt_end) issue(kt + cgw::NST - 1);
+    const unsigned char* sa = ring + (kt % cgw::NST) * C::STAGE;
+    const unsigned char* sb = sa + IMGA;
+#pragma unroll
+    for (int st = 0; st < CG_BK / 16; ++st) {
+      cgx::bf16x8 a[MI], b[NJ];
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int rb = wn * C::WNP + j * 32 + l31;
+        b[j] = cgx::frag(sb + rb * cgw::ROWB + 16 * cgw::swz(rb + BM, 2 * st + lh));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int ra = wm * C::WM + i * 32 + l31;
+        a[i] = cgx::frag(sa + ra * cgw::ROWB + 16 * cgw::swz(ra, 2 * st + lh));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();     // every wave done with the ring: the epilogue reuses it
+  double* red = reinterpret_cast<double*>(ring);
+
+  // ---------------- epilogue (conv_gen_epilogue's arithmetic on this tile)
+  if (p.partial) {   // split-K: raw partial sums, the epilogue kernel finishes
+    float* pb = p.partial + (int64_t)blockIdx.y * p.Cout * NP;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int64_t pg = px0 + wn * C::WNP + 32 * j + l31;
+      if (pg >= NP) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int co = co0 + wm * C::WM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (co < p.Cout) pb[(int64_t)co * NP + pg] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  const float sc = p.scale ? *p.scale : 1.f;
+  bool ok[NJ];
+  float rt[NJ];
+  float* yb[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int64_t pg = px0 + wn * C::WNP + 32 * j + l31;
+    ok[j] = pg < NP;
+    int pn = 0, prem = 0;
+    if (ok[j]) {
+      pn = (int)(pg / HWo);
+      prem = (int)(pg - (int64_t)pn * HWo);
+    }
+    rt[j] = (ok[j] && p.ratio) ? p.ratio[pg] : 1.f;
+    yb[j] = p.y + (int64_t)pn * p.Cout * HWo + prem;
+  }
+  // stats: one (sum, sumsq) per co per OLD_BN-pixel slot; a wave's 64 pixels
+  // lie in one slot (OLD_BN is 128 or 256)
+  constexpr int SPT = BN / C::OLD_BN > 1 ? BN / C::OLD_BN : 1;   // slots per tile
+  constexpr int WPS = C::WGN / SPT;                              // waves per slot
+#pragma unroll
+  for (int i = 0; i < MI; ++i) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int cll = wm * C::WM + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const int co = co0 + cll;
+      const bool cok = co < p.Cout;
+      const float bv = (cok && p.bias) ? p.bias[co] : 0.f;
+      double a = 0.0, b = 0.0;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (!ok[j] || !cok) continue;
+        float v = acc[i][j][r] * sc;
+        v *= rt[j];
+        v += bv;
+        a += (double)v;
+        b += (double)v * (double)v;
+        yb[j][(int64_t)co * HWo] = apply_act(v, act, p.slope);
+      }
+      if (p.stats) {
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          a += __shfl_xor(a, o, 64);
+          b += __shfl_xor(b, o, 64);
+        }
+        if (l31 == 0) {
+          red[(wn * BM + cll) * 2 + 0] = a;
+          red[(wn * BM + cll) * 2 + 1] = b;
+        }
+      }
+    }
+  }
+  if (p.stats) {
+    __syncthreads();
+    const int64_t nslots = (NP + C::OLD_BN - 1) / C::OLD_BN;
+    for (int e = tid; e < BM * SPT; e += NW * 64) {
+      const int cll = e % BM, sl = e / BM;
+      const int co = co0 + cll;
+      const int64_t slot = (int64_t)px_t * SPT + sl;
+      if (co >= p.Cout || slot >= nslots) continue;
+      double a = 0.0, b = 0.0;
+      for (int q = sl * WPS; q < (sl + 1) * WPS; ++q) {
+        a += red[(q * BM + cll) * 2];
+        b += red[(q * BM + cll) * 2 + 1];
+      }
+      p.stats[(slot * 2 + 0) * p.Cout + co] = a;
+      p.stats[(slot * 2 + 1) * p.Cout + co] = b;
+    }
+  }
+}
+
 // x [N][C][H][W] fp32 (* mask plane m [N][H][W] if given) -> out [N][H][W][C]
 // bf16 (nearest-even): 64 channels x 64 columns of one row per block.
 __global__ __launch_bounds__(256) void nchw_to_nhwc16_kernel(const float* __restrict__ x,
@@ -1983,6 +2265,27 @@ extern "C" int ainp_conv_weight_nhwc16(const float* w, int Cout, int C0, int C1,
   return check_launch("conv_weight_nhwc16");
 }
 
+// conv_gen_nhwc16 main loop: 0 register-staged, 1 LDS-DMA ring, 2 wide-tile
+// ring of 4 waves, 3 (default) wide-tile ring of 8 waves for Cout > 64 and the
+// register-staged kernel below (tools/conv16_lab.py, profiles/r03_c16b_*: the
+// C4 step's 30 launches 3.98 -> 3.59 ms, all bit-identical).  Initial value
+// from AINP_CONV16 (or AINP_CONV16_RING=1).
+static int g_conv16_variant = -1;
+static int conv16_variant() {
+  if (g_conv16_variant < 0) {
+    const char* e = getenv("AINP_CONV16");
+    const char* r = getenv("AINP_CONV16_RING");
+    g_conv16_variant = (e && e[0] >= '0' && e[0] <= '3') ? e[0] - '0' : ((r && r[0] == '1') ? 1 : 3);
+  }
+  return g_conv16_variant;
+}
+
+extern "C" int ainp_conv16_set_variant(int v) {
+  const int prev = conv16_variant();
+  if (v >= 0 && v <= 3) g_conv16_variant = v;
+  return prev;
+}
+
 extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0,
                                         const uint16_t* x1, int C1, int H1, int W1,
                                         const uint16_t* wt16, const float* bias, const float* ratio,
@@ -2041,11 +2344,23 @@ extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int 
   hipStream_t s = as_stream(stream);
   const dim3 grid((unsigned)cdiv(NP, 16384 / BM), (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
   const bool exp = a.exp || b.exp;
-  static const bool ring = [] {    // AINP_CONV16_RING=1: the LDS-DMA ring kernel (A/B runs)
-    const char* e = getenv("AINP_CONV16_RING");
-    return e && e[0] == '1';
-  }();
-  if (ring) {
+  const int variant = conv16_variant();
+  if (variant == 2 || (variant == 3 && Cout > 64)) {
+    const int BW = Cout > 128 ? 256 : (Cout > 64 ? 128 : 64);
+    const int BNW = BW == 256 ? 128 : 256;       // both NW: 256x128 / 128x256 / 64x256
+    const int tco = (int)cdiv(Cout, BW), tpx = (int)cdiv(NP, BNW);
+    const dim3 gw((unsigned)(tco * tpx), (unsigned)nsplit);
+#define AINP_CGW(BMV, NWV, EXPV)                                                                 \
+  hipLaunchKernelGGL((conv_gen_nhwc16_wide_kernel<BMV, NWV, EXPV>), gw, dim3(NWV * 64), 0, s, p, a, \
+                     b, wt16, act, tco, tpx)
+    if (variant == 3) {
+      if (BW == 256) { if (exp) AINP_CGW(256, 8, true); else AINP_CGW(256, 8, false); }
+      else { if (exp) AINP_CGW(128, 8, true); else AINP_CGW(128, 8, false); }
+    } else if (BW == 256) { if (exp) AINP_CGW(256, 4, true); else AINP_CGW(256, 4, false); }
+    else if (BW == 128) { if (exp) AINP_CGW(128, 4, true); else AINP_CGW(128, 4, false); }
+    else { if (exp) AINP_CGW(64, 4, true); else AINP_CGW(64, 4, false); }
+#undef AINP_CGW
+  } else if (variant == 1) {
     if (BM == 128 && exp)
       hipLaunchKernelGGL((conv_gen_nhwc16_ring_kernel<128, true>), grid, dim3(256), 0, s, p, a, b,
                          wt16, act);

@@ -75,7 +75,8 @@ def test_ops_refuse_cpu_tensors():
 
 HOST_ONLY = {"ainp_abi_version", "ainp_build_target", "ainp_last_error", "ainp_reduce_workspace",
              "ainp_flac_info", "ainp_flac_decode", "ainp_flac_encode_bound", "ainp_flac_encode",
-             "ainp_l1_pow10_loss_slots", "ainp_range_push", "ainp_range_pop", "ainp_mark"}
+             "ainp_l1_pow10_loss_slots", "ainp_range_push", "ainp_range_pop", "ainp_mark",
+             "ainp_conv16_set_variant"}
 
 
 def test_torch_library_registers_every_gpu_entry_point():

@@ -178,6 +178,56 @@ def test_conv_gen_nhwc16_small_channel_sources(case, monkeypatch):
     assert wt.shape[1] % 32 == 0
 
 
+VARIANT_CASES = [
+    # N, C0, C1, Hin, Win, up0, Cout, k, s, p, stats
+    (2, 64, 1, 24, 30, True, 64, 3, 1, 1, True),        # final pc1 (expanded source, Cout 64)
+    (2, 64, 64, 40, 52, True, 128, 3, 1, 1, True),      # decoder block, Cout 128
+    (2, 128, 0, 37, 45, False, 256, 5, 2, 2, True),     # encoder 5x5 stride 2, Cout 256
+    (2, 256, 256, 12, 20, True, 512, 3, 1, 1, True),    # decoder 512, two 256-row co tiles
+    (1, 512, 512, 6, 10, True, 512, 3, 1, 1, True),     # split-K bottleneck
+    (3, 96, 0, 19, 23, False, 100, 3, 1, 1, True),      # ragged Cout and pixel tails
+    (2, 3, 0, 20, 22, False, 64, 3, 1, 1, False),       # VGG conv1_1 (expanded)
+    (2, 64, 0, 28, 28, False, 200, 4, 2, 1, False),     # D-like 4x4 stride 2
+]
+
+
+@pytest.mark.parametrize("case", VARIANT_CASES)
+def test_conv_gen_nhwc16_variants_bit_identical(case, monkeypatch):
+    """The main loops of the bf16 channel-last conv (ainp_conv16_set_variant:
+    register-staged, LDS-DMA ring, wide-tile ring of 4 or 8 waves) run the same per-output MFMA
+    chain: outputs and BatchNorm partials are bit-identical."""
+    from ainp import ops
+    monkeypatch.setattr(ops, "CONV_NHWC16_SMALL", "all")
+    N, C0, C1, Hin, Win, up0, Cout, k, s, p, want = case
+    g = torch.Generator().manual_seed(hash(case) % 1000 + 3)
+    H0, W0 = (Hin // 2, Win // 2) if up0 else (Hin, Win)
+    d = lambda t: None if t is None else t.cuda()  # noqa: E731
+    x0 = d(torch.randn(N, C0, H0, W0, generator=g))
+    m0 = d((torch.rand(N, H0, W0, generator=g) > 0.3).float())
+    x1 = d(torch.randn(N, C1, Hin, Win, generator=g)) if C1 else None
+    m1 = d((torch.rand(N, Hin, Win, generator=g) > 0.3).float()) if C1 else None
+    w = d(torch.randn(Cout, C0 + C1, k, k, generator=g) * 0.1)
+    Ho, Wo = (Hin + 2 * p - k) // s + 1, (Win + 2 * p - k) // s + 1
+    bias = d(torch.randn(Cout, generator=g))
+    ratio = d(torch.rand(N, Ho, Wo, generator=g) * 3)
+    outs = {}
+    prev = ops.conv16_set_variant(-1)
+    try:
+        for v in (0, 1, 2, 3):
+            ops.conv16_set_variant(v)
+            y, st = ops.conv_gen((x0, m0), w, src1=(x1, m1) if C1 else None, Hin=Hin, Win=Win,
+                                 stride=s, pad=p, bias=bias, ratio=ratio, act=ops.ACT_LEAKY,
+                                 want_stats=want, bf16=True)
+            torch.cuda.synchronize()
+            outs[v] = (y.cpu(), st.cpu() if st is not None else None)
+    finally:
+        ops.conv16_set_variant(prev)
+    for v in (1, 2, 3):
+        assert torch.equal(outs[v][0], outs[0][0]), v
+        if want:
+            assert torch.equal(outs[v][1], outs[0][1]), v
+
+
 @pytest.mark.parametrize("k,s,p,crop,act", [(3, 1, 1, (25, 30), 3), (4, 1, 1, None, 0),
                                              (4, 2, 1, None, 2)])
 def test_conv_gen_cout1(k, s, p, crop, act):
