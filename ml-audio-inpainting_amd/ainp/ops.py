@@ -898,8 +898,7 @@ def _nhwc16_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats):
 def conv_weight_nhwc16(w, C0, C1):
     """bf16 [Cout][K] weights for ainp_conv_gen_fwd_nhwc16, cached like
     conv_weight_kmajor (invalidated by in-place updates / reallocation)."""
-    # the k order follows the conv's main-loop variant (tap-inner under 4)
-    key = (w._version, C0, C1, w.data_ptr(), conv16_set_variant(-1) == 4)
+    key = (w._version, C0, C1, w.data_ptr())
     ent = _WT16_CACHE.get(id(w))
     if ent is not None and ent[0]() is w and ent[1] == key:
         return ent[2]
@@ -955,10 +954,8 @@ def to_nhwc16(x, m=None):
 def conv16_set_variant(v):
     """Main loop of the bf16 channel-last conv (ainp_conv16_set_variant): 0
     register-staged tiles, 1 LDS-DMA ring, 2 / 3 wide-tile ring of 4 / 8 waves
-    (same sums in 0-3, bit for bit), 4 = 3 with the tap-inner K order (its own
-    weight layout from conv_weight_nhwc16; same products, another fp32
-    summation order).  Returns the previous variant (v outside 0..4 only
-    queries)."""
+    (3, the default: Cout > 64, else 0); same sums in all, bit for bit.  Returns
+    the previous variant (v outside 0..3 only queries)."""
     return int(_lib.lib.ainp_conv16_set_variant(int(v)))
 
 

@@ -1,6 +1,7 @@
-"""Per-op timing of one CNNBLSTM training step at C2 (B=32, T=334): every
-ainp.ops call is bracketed by HIP events (after warmup) and listed with its
-shapes; GEMM/conv lines also print TFLOP/s."""
+"""Per-op timing of one CNNBLSTM training step at C2 (B=32, T=334; argv[1] =
+bf16: the C3-shape bf16 configuration): every ainp.ops call is bracketed by HIP
+events and a synchronize (after warmup), so each op runs alone, and listed
+with its shapes; GEMM/conv lines also print TFLOP/s."""
 import os
 import sys
 
@@ -15,8 +16,9 @@ from ainp.optim import Adam  # noqa: E402
 import bench  # noqa: E402
 
 B = 32
+DT = sys.argv[1] if len(sys.argv) > 1 else "fp32"     # fp32 (C2) or bf16 (C3 shape)
 torch.manual_seed(0)
-model = CB.StackedBLSTMCNN(config=bench.CFG).cuda().train()
+model = CB.StackedBLSTMCNN(config=dict(bench.CFG, accel={"dtype": DT})).cuda().train()
 opt = Adam(model.parameters(), lr=1e-4)
 audio = torch.from_numpy(bench.synthetic_clips(B, 64000, 0)).cuda()
 starts = torch.randint(0, 64000 - 3200, (B,), dtype=torch.int64).cuda()
@@ -25,7 +27,9 @@ records = []
 names = ["stft_features", "gemm", "gemm_tn_splitk", "conv3x3_fwd", "conv3x3_dgrad",
          "conv3x3_wgrad", "bn_stats_reduce", "bn_finalize", "bn_relu_apply", "bn_relu_bwd_reduce",
          "bn_relu_bwd_apply", "lstm_rec_fwd", "lstm_rec_bwd", "lstm_hprev", "l1_pow10_loss",
-         "sum_slabs", "rowsum_batched", "colsum", "adam_step", "scale_by_scalar"]
+         "sum_slabs", "rowsum_batched", "colsum", "adam_step", "scale_by_scalar",
+         "gemm_bf16nt", "gemm_bf16nt_splitk", "bn_relu_apply_ntcf_bf16", "cast_bf16_t",
+         "gemm_x6r_nt", "lstm_l0_bwd_x6", "proj_bwd_x6"]
 active = [False]
 
 
@@ -69,7 +73,8 @@ def wrap(nm):
 
 
 for nm in names:
-    wrap(nm)
+    if hasattr(ops, nm):
+        wrap(nm)
 
 
 def step():

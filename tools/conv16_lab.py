@@ -2,9 +2,11 @@
 loop (ops.conv16_set_variant: 0 register-staged, 1 LDS-DMA ring, 2 / 3 wide-tile
 ring of 4 / 8 waves): the launches of one bf16 GAN step at the C4 (T=626) or C5 (--clip-s 8)
 shapes -- G forward, VGG19 over generated + target, one D forward -- recorded
-as prepared-operand launchers, then each timed alone (HIP events, median of
---reps) and checked bit-identical (output and BatchNorm partials) against
-variant 0.
+as prepared-operand launchers (re-recorded per variant), then each timed alone
+(HIP events, median of --reps) and compared with variant 0 (bit-identical
+output and BatchNorm partials, else the worst relative difference; the
+discriminator's spectral norm updates its weights in every forward, so its
+last three convs differ between recordings by construction).
 
   python tools/conv16_lab.py [--reps 7] [--variants 0,1,2] [--clip-s 5]
 """
@@ -22,7 +24,7 @@ from ainp import gan as G, ops  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=7)
-    ap.add_argument("--variants", default="0,1,2")
+    ap.add_argument("--variants", default="0,3")
     ap.add_argument("--clip-s", type=float, default=5.0)
     ap.add_argument("--batch", type=int, default=8)
     ap.add_argument("--only", type=int, default=-1,
@@ -42,30 +44,42 @@ def main():
     m[:, :, :, T // 2:T // 2 + 26] = 0
 
     orig = ops.conv_gen
-    recs = []
 
-    def rec(*a, **k):
-        res = orig(*a, **k)
-        if k.get("bf16"):
-            kk = dict(k)
-            kk["out"] = None
-            la = orig(*a, launcher=True, **kk)
-            if callable(la):
-                w = a[1]
-                Cout, Cin, KH, KW = w.shape
-                y = la.out
-                flops = 2.0 * Cout * Cin * KH * KW * y.shape[0] * y.shape[-2] * y.shape[-1]
-                recs.append((tuple(a[0][0].shape), tuple(w.shape), k.get("stride", 1),
-                             tuple(y.shape), flops, la))
-        return res
+    def collect(v):
+        """Run one G forward + VGG + D forward under variant v, recording every
+        bf16 channel-last conv as a launcher on its prepared operands (the
+        weights in v's k order)."""
+        recs = []
 
-    ops.conv_gen = rec
-    with torch.no_grad():
-        g = gen(x, m)
-        vgg(g, x)
-        disc(x)
-    ops.conv_gen = orig
-    torch.cuda.synchronize()
+        def rec(*a, **k):
+            res = orig(*a, **k)
+            if k.get("bf16"):
+                kk = dict(k)
+                kk["out"] = None
+                la = orig(*a, launcher=True, **kk)
+                if callable(la):
+                    w = a[1]
+                    Cout, Cin, KH, KW = w.shape
+                    y = la.out
+                    flops = 2.0 * Cout * Cin * KH * KW * y.shape[0] * y.shape[-2] * y.shape[-1]
+                    recs.append((tuple(a[0][0].shape), tuple(w.shape), k.get("stride", 1),
+                                 tuple(y.shape), flops, la))
+            return res
+
+        prev = ops.conv16_set_variant(v)
+        ops.conv_gen = rec
+        try:
+            with torch.no_grad():
+                g = gen(x, m)
+                vgg(g, x)
+                disc(x)
+        finally:
+            ops.conv_gen = orig
+            ops.conv16_set_variant(prev)
+        torch.cuda.synchronize()
+        return recs
+
+    recs = collect(variants[0])
     print(f"{len(recs)} nhwc16 launches, B={B} T={T}")
 
     def time_it(fn):
@@ -92,27 +106,31 @@ def main():
         print(f"layer {args.only}: {xs} w{ws} s{s} -> {ys} {fl / 1e9:.1f} GF x {args.reps}")
         return
     ref = {}
+    r0 = collect(0)
     ops.conv16_set_variant(0)
-    for i, r in enumerate(recs):
+    for i, r in enumerate(r0):
         la = r[5]
         la()
         ref[i] = (la.out.clone(), la.stats.clone() if la.stats is not None else None)
     torch.cuda.synchronize()
     res = {v: [] for v in variants}
     ident = {v: 0 for v in variants}
+    worst = {v: 0.0 for v in variants}
     for v in variants:
+        rv = collect(v)
+        assert len(rv) == len(r0)
         ops.conv16_set_variant(v)
-        for i, r in enumerate(recs):
+        for i, r in enumerate(rv):
             la = r[5]
             la.out.zero_()
             la()
             torch.cuda.synchronize()
-            o, s = ref[i]
-            same = torch.equal(la.out, o) and (s is None or torch.equal(la.stats, s))
+            o, st = ref[i]
+            same = torch.equal(la.out, o) and (st is None or torch.equal(la.stats, st))
             ident[v] += int(same)
             if not same:
-                d = (la.out - o).abs().max().item()
-                print(f"  variant {v} layer {i} differs: max |d| {d:.3e}")
+                d = ((la.out - o).abs().max() / o.abs().max().clamp_min(1e-30)).item()
+                worst[v] = max(worst[v], d)
             res[v].append(time_it(la))
     ops.conv16_set_variant(prev)
     hdr = "".join(f"  v{v} ms    TF" for v in variants)
@@ -124,7 +142,7 @@ def main():
     for v in variants:
         tot = sum(res[v])
         print(f"variant {v}: total {tot:.3f} ms, {tf / tot / 1e9:.0f} TF, bit-identical "
-              f"{ident[v]}/{len(recs)}")
+              f"{ident[v]}/{len(recs)}, worst max|d|/max|ref| {worst[v]:.2e}")
 
 
 if __name__ == "__main__":

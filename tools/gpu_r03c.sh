@@ -15,4 +15,8 @@ tail -1 "$OUT/bench_gan_c4_bf16.json" | cut -c1-200
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/cnn_bf16" -o run -- \
   python3 tools/step_prof.py --steps 10 --dtype bf16 > "$OUT/cnn_bf16.log" 2>&1 || exit 1
 grep "ms/step" "$OUT/cnn_bf16.log"
+for dt in fp32 bf16; do
+  timeout -k 10 300 python3 tools/cnnblstm_op_bench.py $dt > "$OUT/opbench_$dt.log" 2>&1 || exit 1
+  head -2 "$OUT/opbench_$dt.log" | tail -1
+done
 echo "all ok"
