@@ -713,6 +713,27 @@ def run_gan(args):
         else:
             roof["main_loop"] = ("fp32 operands split exactly into 3 bf16 pieces, 6 cross "
                                  "products on v_mfma_f32_32x32x16_bf16, f32 accumulate")
+    roof_wide = None
+    if rank == 0 and bf16:
+        # the kernel with the most time in the bf16 step (profiles/r03_ganprof1_*):
+        # the wide-tile conv on its largest launch, the U-Net decoder block
+        # cat(up(512 ch), skip 256 ch) -> 256 at 1/8 resolution, with BN partials
+        Hd, Wd = Hp // 8, Wp // 8
+        xa = torch.randn(B, 512, Hd // 2, Wd // 2, device=dev)
+        ma = (torch.rand(B, Hd // 2, Wd // 2, device=dev) > 0.1).float()
+        xb = torch.randn(B, 256, Hd, Wd, device=dev)
+        mb = (torch.rand(B, Hd, Wd, device=dev) > 0.1).float()
+        wd = torch.randn(256, 768, 3, 3, device=dev) * 0.02
+        launch_w = ops.conv_gen((xa, ma), wd, src1=(xb, mb), Hin=Hd, Win=Wd, stride=1, pad=1,
+                                bias=torch.zeros(256, device=dev),
+                                ratio=torch.ones(B, Hd, Wd, device=dev), want_stats=True,
+                                bf16=True, launcher=True)
+        avg_w = time_kernel(launch_w, args.roofline_reps, dev)
+        roof_wide = _roof(2.0 * 256 * 768 * 9 * B * Hd * Wd, avg_w, True,
+                          f"conv_gen_nhwc16_wide_kernel<256, 8, false> (U-Net decoder block "
+                          f"768->256 3x3 at {Hd}x{Wd}, B={B}, BN partials)")
+        roof_wide["main_loop"] = ("256x128 tiles, 8 waves of 64x64, 3-stage LDS-DMA ring "
+                                  "(global_load_lds_dwordx4), v_mfma_f32_32x32x16_bf16")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = gan_cpu_baseline(T, S, g)
@@ -740,7 +761,8 @@ def run_gan(args):
                             if step_flops else None),
             "mfma_util_step": (round(step_flops / world / (ms_step / 1e3) / 1e12
                                      / executed_peak(bf16), 4) if step_flops else None),
-            "roofline": roof, "reconstruction": recon, "cpu_baseline": cpu,
+            "roofline": roof, "roofline_wide": roof_wide, "reconstruction": recon,
+            "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

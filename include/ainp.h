@@ -547,6 +547,18 @@ int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0, const u
                              const float* ratio, const float* scale, float* y, double* stats,
                              int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
                              int pad, int act, float slope, void* workspace, void* stream);
+/* ainp_conv_gen_fwd_nhwc16 that also writes y16 (may be NULL): the result
+ * after the activation as a bf16 (nearest-even) channel-last copy
+ * [N][Ho][Wo][Cout] -- the next conv's channel-last source, written by this
+ * epilogue instead of a separate ainp_nchw_to_nhwc16 pass (VGG19 and the
+ * discriminator, whose convs have no partial-conv mask;
+ * models/GAN/loss.py:41-51, networks.py:352-409). */
+int ainp_conv_gen_fwd_nhwc16_ex(const uint16_t* x0, int C0, int H0, int W0, const uint16_t* x1,
+                                int C1, int H1, int W1, const uint16_t* wt16, const float* bias,
+                                const float* ratio, const float* scale, float* y, double* stats,
+                                int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
+                                int pad, int act, float slope, uint16_t* y16, void* workspace,
+                                void* stream);
 /* Main loop of ainp_conv_gen_fwd_nhwc16 (same sums, bit for bit, in every
  * variant): 0 register-staged 128x128 / 64x256 tiles, 1 the same tiles on an
  * LDS-DMA ring, 2 wide tiles (256x128 / 128x256 / 64x256) of 4 waves on a

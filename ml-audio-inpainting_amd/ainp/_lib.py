@@ -163,6 +163,9 @@ _SIGS = {
     "ainp_conv_gen_fwd_nhwc16": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, P, P, P,
                                          P, P, P, c_int64, c_int, c_int, c_int, c_int, c_int,
                                          c_int, c_int, c_int, c_float, P, P]),
+    "ainp_conv_gen_fwd_nhwc16_ex": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, P, P,
+                                            P, P, P, P, c_int64, c_int, c_int, c_int, c_int, c_int,
+                                            c_int, c_int, c_int, c_float, P, P, P]),
 }
 
 EXPORTED = tuple(_SIGS)

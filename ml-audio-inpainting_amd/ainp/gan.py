@@ -345,14 +345,19 @@ class _DiscriminatorFn(torch.autograd.Function):
     def forward(ctx, x, cfg, bf16, inv, us, vs, *params):
         h = x.contiguous()
         ins, outs = [], []
-        for l, (k, s, p, act) in enumerate(cfg):
-            w, b = params[2 * l], params[2 * l + 1]
-            y, _ = ops.conv_gen((h, None), w, stride=s, pad=p, bias=b, scale=inv[l:l + 1],
-                                act=ops.ACT_LEAKY if act else ops.ACT_NONE, slope=SLOPE,
-                                bf16=bf16)
-            ins.append(h)
-            outs.append(y)
-            h = y
+        L = len(cfg)
+        # bf16: each conv whose successor is a channel-last bf16 conv (Cout > 1)
+        # writes that conv's source itself (no separate nchw_to_nhwc16 pass)
+        with ops.nhwc16_memo():
+            for l, (k, s, p, act) in enumerate(cfg):
+                w, b = params[2 * l], params[2 * l + 1]
+                nxt16 = bf16 and l + 1 < L and params[2 * (l + 1)].shape[0] > 1
+                y, _ = ops.conv_gen((h, None), w, stride=s, pad=p, bias=b, scale=inv[l:l + 1],
+                                    act=ops.ACT_LEAKY if act else ops.ACT_NONE, slope=SLOPE,
+                                    bf16=bf16, out16=nxt16)
+                ins.append(h)
+                outs.append(y)
+                h = y
         ctx.cfg = cfg
         ctx.bf16 = bf16
         ctx.nl = len(cfg)
@@ -597,27 +602,33 @@ class VGGLoss(nn.Module):
         want = self.layer_indices_style | self.layer_indices_perceptual
         layers = list(self.vgg_layers)
         i = 0
-        while i < len(layers):
-            lay = layers[i]
-            if isinstance(lay, nn.Conv2d):
-                relu_next = (i < self.max_layer_idx and i + 1 < len(layers)
-                             and isinstance(layers[i + 1], nn.ReLU))
-                x, _ = ops.conv_gen((x, None), lay.weight, stride=1, pad=1, bias=lay.bias,
-                                    act=ops.ACT_RELU if relu_next else ops.ACT_NONE,
-                                    bf16=self.ainp_bf16)
-                if i in want:
-                    feats[i] = x
-                if relu_next:
-                    i += 1          # the ReLU ran inside the conv epilogue
+        with ops.nhwc16_memo():
+            while i < len(layers):
+                lay = layers[i]
+                if isinstance(lay, nn.Conv2d):
+                    relu_next = (i < self.max_layer_idx and i + 1 < len(layers)
+                                 and isinstance(layers[i + 1], nn.ReLU))
+                    # bf16: a conv feeding the next conv directly (no max-pool between)
+                    # also writes that conv's channel-last bf16 source
+                    j = i + 2 if relu_next else i + 1
+                    nxt16 = (self.ainp_bf16 and j <= self.max_layer_idx and j < len(layers)
+                             and isinstance(layers[j], nn.Conv2d))
+                    x, _ = ops.conv_gen((x, None), lay.weight, stride=1, pad=1, bias=lay.bias,
+                                        act=ops.ACT_RELU if relu_next else ops.ACT_NONE,
+                                        bf16=self.ainp_bf16, out16=nxt16)
                     if i in want:
                         feats[i] = x
-            elif isinstance(lay, nn.MaxPool2d):
-                x = ops.maxpool2(x)
-                if i in want:
-                    feats[i] = x
-            if i >= self.max_layer_idx:
-                break
-            i += 1
+                    if relu_next:
+                        i += 1          # the ReLU ran inside the conv epilogue
+                        if i in want:
+                            feats[i] = x
+                elif isinstance(lay, nn.MaxPool2d):
+                    x = ops.maxpool2(x)
+                    if i in want:
+                        feats[i] = x
+                if i >= self.max_layer_idx:
+                    break
+                i += 1
         return feats
 
     def _gram(self, x):

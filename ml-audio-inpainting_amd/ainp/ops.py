@@ -875,6 +875,9 @@ _WT16_CACHE: dict = {}
 # the plain few-channel first layers (D's, VGG's) keep the direct kernel
 # (ainp_conv_gen_fwd_ex) unless AINP_CONV_NHWC16_SMALL=all.
 CONV_NHWC16 = os.environ.get("AINP_CONV_NHWC16", "1") != "0"
+# conv_gen(out16=True): the epilogue writes the next conv's channel-last bf16
+# source (AINP_CONV_OUT16=0: a separate nchw_to_nhwc16 pass, as before)
+CONV_OUT16 = os.environ.get("AINP_CONV_OUT16", "1") != "0"
 CONV_NHWC16_SMALL = os.environ.get("AINP_CONV_NHWC16_SMALL", "1")
 
 
@@ -961,10 +964,13 @@ def conv16_set_variant(v):
 
 def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=None, ratio=None,
              scale=None, act=ACT_NONE, slope=0.2, want_stats=False, crop=None, out=None,
-             bf16=False, launcher=False):
+             bf16=False, launcher=False, out16=False):
     """ainp_conv_gen_fwd.  src0/src1 = (x [N,C,Hs,Ws], mask plane [N,Hs,Ws] or None);
     the conv's input is cat(src0 nearest-resampled to (Hin, Win), src1) * masks.
-    Returns (y [N,Cout,Ho,Wo] (or [N,crop_h,crop_w] for Cout=1 with crop), stats)."""
+    Returns (y [N,Cout,Ho,Wo] (or [N,crop_h,crop_w] for Cout=1 with crop), stats).
+    out16 (bf16 channel-last route, inside an nhwc16_memo scope): the epilogue
+    also writes y's bf16 channel-last copy (ainp_conv_gen_fwd_nhwc16_ex), which
+    to_nhwc16(y) then returns -- for a next conv with no mask plane."""
     x0, m0 = src0
     _req(x0, "x0"); _req(w, "w")
     N, C0, H0, W0 = x0.shape
@@ -1015,16 +1021,22 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
         a16 = src16(x0, m0, C0)
         b16 = src16(x1, m1, C1) if src1 is not None else None
         wt16 = conv_weight_nhwc16(w, C0, C1)
+        y16 = None
+        if out16 and CONV_OUT16 and _NHWC_MEMO is not None:
+            y16 = torch.empty(N, Ho, Wo, Cout, device=x0.device, dtype=torch.bfloat16)
 
         def launch():
             _T.conv_gen_fwd_nhwc16(a16, b16, wt16, int(Cout), int(KH), int(KW), bias, ratio,
                                    scale, out, stats, int(Hin), int(Win), int(stride), int(pad),
                                    int(act), float(slope), ws,
-                                   [int(N), int(C0), int(H0), int(W0), int(C1), int(H1), int(W1)])
+                                   [int(N), int(C0), int(H0), int(W0), int(C1), int(H1), int(W1)],
+                                   y16)
         if launcher:   # bench / profiling: the conv kernel alone on prepared operands
-            launch.out, launch.stats = out, stats
+            launch.out, launch.stats, launch.y16 = out, stats, y16
             return launch
         launch()
+        if y16 is not None:
+            _NHWC_MEMO[(out.data_ptr(), tuple(out.shape), out._version, 0, -1)] = (y16, out, None)
         return out, stats
     if Cout == 1:
         nb = int(_lib.lib.ainp_conv_gen_workspace(N, Cin, KH, KW, Cout, ch or Ho, cw or Wo))

@@ -38,6 +38,7 @@ struct ConvGenParams {
   float* y;                 // [N][Cout][Ho][Wo]
   double* stats;            // [px_tiles][2][Cout] (sum, sumsq of the stored y) or null
   float* partial;           // split-K: raw sums [gridDim.z][Cout][N*Ho*Wo], epilogue deferred
+  uint16_t* y16;            // optional bf16 channel-last copy of y: [N][Ho][Wo][Cout] (nhwc16 only)
   int ktiles_per_split;     // K tiles per blockIdx.z
   int N, Cin, Cout, Hin, Win, Ho, Wo, KH, KW, stride, pad;
   float slope;              // LeakyReLU negative slope (act == 2)
@@ -54,6 +55,103 @@ __device__ __forceinline__ float apply_act(float v, int act, float slope) {
   if (act == ACT_LEAKY) return v > 0.f ? v : v * slope;
   if (act == ACT_TANH) return tanhf(v);
   return v;
+}
+
+// The optional channel-last bf16 copy (nearest-even) of an MFMA epilogue's
+// outputs: register r of a 32x32 accumulator holds channel (r&3) + 8(r>>2) +
+// 4(lane>>5), so registers 4q..4q+3 are 4 consecutive channels of the lane's
+// pixel -- one 8-byte store each (Cout % 4 == 0; else element stores).  The
+// value is recomputed exactly as the fp32 store's (same operations, same order).
+__device__ __forceinline__ void store_y16_quad(const ConvGenParams& p, int64_t pg, int co,
+                                               const float (&o)[4]) {
+  uint16_t* d = p.y16 + pg * p.Cout + co;
+  if ((p.Cout & 3) == 0 && co + 3 < p.Cout) {
+    uint2 u;
+    u.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[0]) |
+          ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[1]) << 16);
+    u.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[2]) |
+          ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[3]) << 16);
+    *reinterpret_cast<uint2*>(d) = u;
+  } else {
+    for (int e = 0; e < 4; ++e)
+      if (co + e < p.Cout) d[e] = __builtin_bit_cast(uint16_t, (__bf16)o[e]);
+  }
+}
+template <int MI, int NJ>
+__device__ __forceinline__ void epilogue_y16(const ConvGenParams& p, const f32x16 (&acc)[MI][NJ],
+                                             int act, int64_t px_w, int co_w, const bool* ok,
+                                             const float* rt, int lh, int l31) {
+  const float sc = p.scale ? *p.scale : 1.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    if (!ok[j]) continue;
+    const int64_t pg = px_w + 32 * j + l31;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int co = co_w + 32 * i + 8 * q + 4 * lh;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float bv = (co + e < p.Cout && p.bias) ? p.bias[co + e] : 0.f;
+          float v = acc[i][j][4 * q + e] * sc;
+          v *= rt[j];
+          v += bv;
+          o[e] = apply_act(v, act, p.slope);
+        }
+        store_y16_quad(p, pg, co, o);
+      }
+  }
+}
+
+// The same copy through a wave-private LDS transpose (the wide kernel's free
+// ring): per 32-pixel group the wave stages [32 px][MI*32 co] bf16 (144-byte
+// rows) and stores whole 128-byte pixel rows, 16 bytes per lane, instead of
+// 8-byte pieces 2*Cout bytes apart.  Edge tiles (Cout % 8, last co tile) use
+// epilogue_y16.
+template <int MI, int NJ>
+__device__ __forceinline__ void epilogue_y16_lds(const ConvGenParams& p,
+                                                 const f32x16 (&acc)[MI][NJ], int act,
+                                                 int64_t px_w, int co_w, const bool* ok,
+                                                 const float* rt, int lh, int l31, int lane,
+                                                 uint16_t* stg, int64_t NP) {
+  constexpr int RS = MI * 32 + 8;                 // staging row stride (bf16)
+  constexpr int CPR = MI * 32 / 8;                // 16-byte chunks per pixel row
+  if ((p.Cout & 7) || co_w + MI * 32 > p.Cout) {
+    epilogue_y16<MI, NJ>(p, acc, act, px_w, co_w, ok, rt, lh, l31);
+    return;
+  }
+  const float sc = p.scale ? *p.scale : 1.f;
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int cl = 32 * i + 8 * q + 4 * lh;
+        uint32_t h[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float bv = p.bias ? p.bias[co_w + cl + e] : 0.f;
+          float v = acc[i][j][4 * q + e] * sc;
+          v *= rt[j];
+          v += bv;
+          h[e] = __builtin_bit_cast(uint16_t, (__bf16)apply_act(v, act, p.slope));
+        }
+        *reinterpret_cast<uint2*>(stg + l31 * RS + cl) =
+            make_uint2(h[0] | (h[1] << 16), h[2] | (h[3] << 16));
+      }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < 32 * CPR / 64; ++it) {
+      const int c = it * 64 + lane, px = c / CPR, cb = (c % CPR) * 8;
+      const uint4 v = *reinterpret_cast<const uint4*>(stg + px * RS + cb);
+      const int64_t pg = px_w + 32 * j + px;
+      if (pg < NP) *reinterpret_cast<uint4*>(p.y16 + pg * p.Cout + co_w + cb) = v;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
 }
 
 constexpr int CG_BK = 32;
@@ -167,6 +265,7 @@ __device__ __forceinline__ void conv_gen_epilogue(const ConvGenParams& p, f32x16
       }
     }
   }
+  if (p.y16) epilogue_y16<2, 2>(p, acc, act, px0 + wn * 64, co0 + wm * 64, ok, rt, lh, l31);
   if (p.stats) {
     __syncthreads();
     if (tid < BM) {
@@ -1853,6 +1952,19 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_gen_nhwc16_wide_kernel(ConvGe
       }
     }
   }
+  if (p.y16) {
+    // the ring past the statistics scratch (WGN * BM * 16 bytes): 32 rows of
+    // (MI*32 + 8) bf16 per wave
+    static_assert(C::WGN * BM * 16 + NW * 32 * (MI * 32 + 8) * 2 <= cgw::NST * C::STAGE,
+                  "y16 staging fits the ring");
+    uint16_t* stg = reinterpret_cast<uint16_t*>(ring + C::WGN * BM * 16) +
+                    wave * 32 * (MI * 32 + 8);
+    if (MI == 2)
+      epilogue_y16_lds<MI, NJ>(p, acc, act, px0 + wn * C::WNP, co0 + wm * C::WM, ok, rt, lh,
+                               l31, lane, stg, NP);
+    else
+      epilogue_y16<MI, NJ>(p, acc, act, px0 + wn * C::WNP, co0 + wm * C::WM, ok, rt, lh, l31);
+  }
   if (p.stats) {
     __syncthreads();
     const int64_t nslots = (NP + C::OLD_BN - 1) / C::OLD_BN;
@@ -2109,6 +2221,7 @@ extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, in
   p.y = y;
   p.stats = stats;
   p.partial = nullptr;
+  p.y16 = nullptr;
   p.ktiles_per_split = 1 << 30;
   p.N = (int)N;
   p.Cin = C0 + C1;
@@ -2286,12 +2399,12 @@ extern "C" int ainp_conv16_set_variant(int v) {
   return prev;
 }
 
-extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0,
+extern "C" int ainp_conv_gen_fwd_nhwc16_ex(const uint16_t* x0, int C0, int H0, int W0,
                                         const uint16_t* x1, int C1, int H1, int W1,
                                         const uint16_t* wt16, const float* bias, const float* ratio,
                                         const float* scale, float* y, double* stats, int64_t N,
                                         int Cout, int Hin, int Win, int KH, int KW, int stride,
-                                        int pad, int act, float slope, void* workspace,
+                                        int pad, int act, float slope, uint16_t* y16, void* workspace,
                                         void* stream) {
   if (!x0 || C0 < 1 || C1 < 0 || (C1 > 0 && !x1) || !wt16 || !y || N < 1 || Cout < 2 ||
       Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 || act < 0 || act > 3 ||
@@ -2317,6 +2430,7 @@ extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int 
   p.y = y;
   p.stats = stats;
   p.partial = nullptr;
+  p.y16 = y16;
   p.ktiles_per_split = 1 << 30;
   p.N = (int)N;
   p.Cin = C0 + C1;
@@ -2385,7 +2499,23 @@ extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int 
   if (rc || nsplit == 1) return rc;
   hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), Cout), dim3(256), 0,
                      s, p, nsplit, act);
-  return check_launch("conv_gen_splitk_epilogue");
+  rc = check_launch("conv_gen_splitk_epilogue");
+  if (rc || !y16) return rc;
+  // split-K layers are small: their bf16 copy by the coalesced transpose kernel
+  // (the per-channel epilogue blocks would store it 2 bytes at a time)
+  return ainp_nchw_to_nhwc16(y, nullptr, N, Cout, Ho, Wo, y16, stream);
+}
+
+extern "C" int ainp_conv_gen_fwd_nhwc16(const uint16_t* x0, int C0, int H0, int W0,
+                                        const uint16_t* x1, int C1, int H1, int W1,
+                                        const uint16_t* wt16, const float* bias, const float* ratio,
+                                        const float* scale, float* y, double* stats, int64_t N,
+                                        int Cout, int Hin, int Win, int KH, int KW, int stride,
+                                        int pad, int act, float slope, void* workspace,
+                                        void* stream) {
+  return ainp_conv_gen_fwd_nhwc16_ex(x0, C0, H0, W0, x1, C1, H1, W1, wt16, bias, ratio, scale, y,
+                                     stats, N, Cout, Hin, Win, KH, KW, stride, pad, act, slope,
+                                     nullptr, workspace, stream);
 }
 
 extern "C" int ainp_pconv_mask(const float* m0, int C0, int H0, int W0, const float* m1, int C1,

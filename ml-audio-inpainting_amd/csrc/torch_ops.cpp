@@ -1033,7 +1033,7 @@ void conv_gen_fwd_nhwc16(const Tensor& x0, const OptT& x1, const Tensor& wt16, i
                          int64_t KH, int64_t KW, const OptT& bias, const OptT& ratio,
                          const OptT& scale, const Tensor& y, const OptT& stats, int64_t Hin,
                          int64_t Win, int64_t stride, int64_t pad, int64_t act, double slope,
-                         const OptT& workspace, at::IntArrayRef dims) {
+                         const OptT& workspace, at::IntArrayRef dims, const OptT& y16) {
   // dims = [N, C0, H0, W0, C1, H1, W1] (required when a source has C % 32 != 0:
   // such a source is the [N*Ho*Wo, seg] rows of im2col_nhwc16), else from the
   // [N, Hs, Ws, C] channel-last tensors
@@ -1077,11 +1077,16 @@ void conv_gen_fwd_nhwc16(const Tensor& x0, const OptT& x1, const Tensor& wt16, i
   } else {
     TORCH_CHECK(need == 0, "conv_gen needs a workspace of ", need, " bytes");
   }
-  chk(ainp_conv_gen_fwd_nhwc16(bf16p(x0, "x0"), (int)C0, (int)H0, (int)W0, p1, (int)C1, (int)H1,
-                               (int)W1, bf16p(wt16, "wt16"), opt(bias, "bias"), opt(ratio, "ratio"),
-                               opt(scale, "scale"), dev(y, "y"), st, N, (int)Cout, (int)Hin,
-                               (int)Win, (int)KH, (int)KW, (int)stride, (int)pad, (int)act,
-                               (float)slope, ws, stream_of(x0)),
+  uint16_t* o16 = nullptr;
+  if (y16.has_value() && y16->defined()) {
+    numel_is(*y16, N * Cout * Ho * Wo, "y16");
+    o16 = bf16p(*y16, "y16");
+  }
+  chk(ainp_conv_gen_fwd_nhwc16_ex(bf16p(x0, "x0"), (int)C0, (int)H0, (int)W0, p1, (int)C1,
+                                  (int)H1, (int)W1, bf16p(wt16, "wt16"), opt(bias, "bias"),
+                                  opt(ratio, "ratio"), opt(scale, "scale"), dev(y, "y"), st, N,
+                                  (int)Cout, (int)Hin, (int)Win, (int)KH, (int)KW, (int)stride,
+                                  (int)pad, (int)act, (float)slope, o16, ws, stream_of(x0)),
       "conv_gen_fwd_nhwc16");
 }
 
@@ -1236,7 +1241,7 @@ TORCH_LIBRARY(ainp, m) {
   m.def("conv_gen_fwd_nhwc16(Tensor x0, Tensor? x1, Tensor wt16, int Cout, int KH, int KW, "
         "Tensor? bias, Tensor? ratio, Tensor? scale, Tensor(a!) y, Tensor(b!)? stats, int Hin, "
         "int Win, int stride, int pad, int act, float slope, Tensor(c!)? workspace, "
-        "int[] dims=[]) -> ()");
+        "int[] dims=[], Tensor(d!)? y16=None) -> ()");
   m.def("im2col_nhwc16(Tensor x, Tensor? m, int Hin, int Win, int KH, int KW, int stride, "
         "int pad, Tensor(a!) out) -> ()");
   m.def("d_prep16(Tensor g, int nslab, Tensor? y, float slope, int N, int C, int P, "

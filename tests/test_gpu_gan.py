@@ -228,6 +228,36 @@ def test_conv_gen_nhwc16_variants_bit_identical(case, monkeypatch):
             assert torch.equal(outs[v][1], outs[0][1]), v
 
 
+@pytest.mark.parametrize("case", [
+    (2, 64, 28, 28, 64, 3, 1, 1, 1),                  # VGG-like ReLU, Cout 64 (register-staged)
+    (2, 128, 30, 26, 256, 4, 2, 1, 2),                # D-like LeakyReLU 4x4 stride 2, wide tile
+    (1, 512, 6, 10, 512, 3, 1, 1, 1),                 # split-K epilogue kernel
+    (2, 64, 30, 22, 128, 3, 1, 1, 2),                 # wide tile, 128 channels
+    (1, 96, 17, 23, 200, 3, 1, 1, 1),                 # ragged last channel tile
+])
+def test_conv_gen_epilogue_nhwc16_copy(case):
+    """out16: the conv epilogue's bf16 channel-last copy of y equals
+    to_nhwc16(y) bit for bit, and inside an nhwc16_memo scope to_nhwc16(y)
+    returns it (the VGG19 / discriminator chains use it as the next conv's
+    source)."""
+    from ainp import ops
+    N, C, H, W, Cout, k, s, p, act = case
+    g = torch.Generator().manual_seed(17 + Cout)
+    x = torch.randn(N, C, H, W, generator=g).cuda()
+    w = (torch.randn(Cout, C, k, k, generator=g) * 0.05).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    with ops.nhwc16_memo():
+        y, st = ops.conv_gen((x, None), w, stride=s, pad=p, bias=b, act=act, want_stats=True,
+                             bf16=True, out16=True)
+        y16 = ops.to_nhwc16(y)
+    ref = ops.to_nhwc16(y)
+    torch.cuda.synchronize()
+    assert torch.equal(y16.view(torch.int16), ref.view(torch.int16))
+    y2, st2 = ops.conv_gen((x, None), w, stride=s, pad=p, bias=b, act=act, want_stats=True,
+                           bf16=True)
+    assert torch.equal(y, y2) and torch.equal(st, st2)   # y / stats unchanged by out16
+
+
 @pytest.mark.parametrize("k,s,p,crop,act", [(3, 1, 1, (25, 30), 3), (4, 1, 1, None, 0),
                                              (4, 2, 1, None, 2)])
 def test_conv_gen_cout1(k, s, p, crop, act):
