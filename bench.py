@@ -731,7 +731,9 @@ def run_gan(args):
         avg_w = time_kernel(launch_w, args.roofline_reps, dev)
         roof_wide = _roof(2.0 * 256 * 768 * 9 * B * Hd * Wd, avg_w, True,
                           f"conv_gen_nhwc16_wide_kernel<256, 8, false> (U-Net decoder block "
-                          f"768->256 3x3 at {Hd}x{Wd}, B={B}, BN partials)")
+                          f"768->256 3x3 at {Hd}x{Wd}, B={B}, BN partials)",
+                          traffic=(_traffic("traffic_conv_gen_wide_bf16.json")
+                                   if (not c5 and B == 8) else None))
         roof_wide["main_loop"] = ("256x128 tiles, 8 waves of 64x64, 3-stage LDS-DMA ring "
                                   "(global_load_lds_dwordx4), v_mfma_f32_32x32x16_bf16")
     cpu = None

@@ -29,6 +29,9 @@ f = per_dispatch("fetch", "FETCH_SIZE")
 w = per_dispatch("write", "WRITE_SIZE")
 fk = [v for _, v, _ in f][1:]
 wk = [v for _, v, _ in w][1:]
+if len(sys.argv) > 5:   # only the last N dispatches of that kernel (a probe's timed launches)
+    nlast = int(sys.argv[5])
+    fk, wk = fk[-nlast:], wk[-nlast:]
 M, N, K = 10688, 1024, 16448
 alg = int(sys.argv[3]) if len(sys.argv) > 3 else 4 * (M * K + N * K + M * N)
 probe = sys.argv[4] if len(sys.argv) > 4 else "tools/pmc_gemm.sh over tools/roofline_probe.py"
