@@ -258,12 +258,16 @@ def test_conv_gen_epilogue_nhwc16_copy(case):
     assert torch.equal(y, y2) and torch.equal(st, st2)   # y / stats unchanged by out16
 
 
-@pytest.mark.parametrize("k,s,p,crop,act", [(3, 1, 1, (25, 30), 3), (4, 1, 1, None, 0),
-                                             (4, 2, 1, None, 2)])
-def test_conv_gen_cout1(k, s, p, crop, act):
+@pytest.mark.parametrize("k,s,p,crop,act,C,H,W", [
+    (3, 1, 1, (25, 30), 3, 64, 32, 40), (4, 1, 1, None, 0, 64, 32, 40),
+    (4, 2, 1, None, 2, 64, 32, 40),
+    # LDS-tiled path (stride 1, 3x3 / 4x4): ragged channel chunks and tiles
+    (3, 1, 1, (37, 66), 3, 40, 37, 70), (4, 1, 1, None, 0, 200, 13, 35),
+    (3, 1, 1, None, 0, 7, 17, 33)])
+def test_conv_gen_cout1(k, s, p, crop, act, C, H, W):
     from ainp import ops
     g = torch.Generator().manual_seed(5)
-    N, C, H, W = 2, 64, 32, 40
+    N = 2
     x = torch.randn(N, C, H, W, generator=g)
     m = (torch.rand(N, H, W, generator=g) > 0.2).float()
     w = torch.randn(1, C, k, k, generator=g) * 0.1
