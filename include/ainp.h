@@ -682,6 +682,17 @@ int ainp_d_prep16(const float* g, int nslab, int64_t slab_stride, const float* y
                   void* stream);
 int ainp_im2col16(const float* x, int64_t N, int C, int H, int W, int KH, int KW, int stride,
                   int pad, int ones_row, uint16_t* col, int64_t ldA, void* stream);
+/* ainp_wgrad_cout1: the weight gradient of a Cout = 1 conv (k = 3 or 4; the
+ * discriminator's logit conv, networks.py:403-406) straight from the fp32
+ * input x [N][Cin][H][W] and g = sum of nslab slabs [N][1][Ho][Wo] (times
+ * LeakyReLU'(y) when y != NULL): gw [Cin*k*k + 1] = [dW | db], fp32 products,
+ * fixed-order reduction -- replaces ainp_im2col16 + ainp_gemm_bf16nt (a GEMV
+ * over materialised columns) for that layer.  ws: ainp_wgrad_cout1_workspace
+ * bytes (the per-pixel-slice partial rows). */
+int ainp_wgrad_cout1(const float* x, const float* g, int nslab, int64_t slab_stride,
+                     const float* y, float slope, int64_t N, int Cin, int H, int W, int k,
+                     int stride, int pad, float* gw, float* ws, void* stream);
+int64_t ainp_wgrad_cout1_workspace(int Cin, int k);
 int ainp_dgrad16_weight(const float* w, int Cout, int Cin, int k, int stride, int pad,
                         uint16_t* wd, void* stream);
 int ainp_dgrad16(const uint16_t* gT, int64_t N, int Cout, int Ho, int Wo, const uint16_t* wd,

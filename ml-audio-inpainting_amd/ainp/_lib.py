@@ -150,6 +150,9 @@ _SIGS = {
                                    P, c_int64, P, P, P, P, c_int64, c_int, c_int64, c_int64, P]),
     "ainp_d_prep16": (c_int, [P, c_int, c_int64, P, c_float, c_int64, c_int, c_int64, P, c_int64,
                               P, P]),
+    "ainp_wgrad_cout1": (c_int, [P, P, c_int, c_int64, P, c_float, c_int64, c_int, c_int, c_int,
+                                 c_int, c_int, c_int, P, P, P]),
+    "ainp_wgrad_cout1_workspace": (c_int64, [c_int, c_int]),
     "ainp_im2col16": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                               P, c_int64, P]),
     "ainp_dgrad16_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),

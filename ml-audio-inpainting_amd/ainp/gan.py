@@ -412,6 +412,8 @@ class _DiscriminatorFn(torch.autograd.Function):
 # bf16 configurations: the D backward on bf16 operands in HBM (csrc/dconv16.hip);
 # AINP_D_BWD16=0 keeps the fp32-staged im2col / GEMM / col2im loop
 D_BWD16 = os.environ.get("AINP_D_BWD16", "1") != "0"
+# the logit conv's weight gradient by ainp_wgrad_cout1 (0: im2col16 + GEMM, A/B)
+WGRAD_COUT1 = os.environ.get("AINP_WGRAD_COUT1", "1") != "0"
 
 
 def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
@@ -431,12 +433,18 @@ def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
         P = Ho * Wo
         ldA = -(-N * P // 64) * 64
         need_dx = l > 0 or ctx.needs_input_grad[0]
-        gA, gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P, ldA,
-                              want_gT=need_dx)
         h = ins[l]
         Cin, H, W = h.shape[1:]
-        col = ops.im2col16(h, k, s, p, ldA)                      # [Cin*k*k + 1, ldA]
-        Gw = ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=512)
+        if WGRAD_COUT1 and Cout == 1 and k in (3, 4):
+            # the logit conv: a GEMV, straight from h (no materialised columns)
+            Gw = ops.wgrad_cout1(h, gsrc, nslab, outs[l] if act else None, SLOPE, k, s, p)
+            gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P, ldA,
+                              want_gT=True)[1] if need_dx else None
+        else:
+            gA, gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P, ldA,
+                                  want_gT=need_dx)
+            col = ops.im2col16(h, k, s, p, ldA)                  # [Cin*k*k + 1, ldA]
+            Gw = ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=512)
         dw, db = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1], with_bias=True)
         grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
         if need_dx:

@@ -1251,6 +1251,16 @@ def d_prep16(g, nslab, y, slope, N, C, P, ldA, want_gT=True):
     return gA, gT
 
 
+def wgrad_cout1(x, g, nslab, y, slope, k, stride, pad):
+    """ainp_wgrad_cout1: [dW | db] [1, Cin*k*k + 1] of a Cout = 1 conv from the
+    fp32 input x [N, Cin, H, W] and nslab slabs of g [N, 1, Ho, Wo]."""
+    _req(x, "x"); _req(g, "g")
+    gw = torch.empty(1, x.shape[1] * k * k + 1, device=x.device)
+    ws = torch.empty(_lib.lib.ainp_wgrad_cout1_workspace(x.shape[1], k) // 4, device=x.device)
+    _T.wgrad_cout1(x, g, int(nslab), y, float(slope), int(k), int(stride), int(pad), gw, ws)
+    return gw
+
+
 def im2col16(x, k, stride, pad, ldA, ones_row=True):
     """ainp_im2col16: bf16 [C*k*k (+1), ldA] columns, all images' pixels in a row."""
     C = x.shape[1]

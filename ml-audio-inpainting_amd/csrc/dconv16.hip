@@ -337,6 +337,100 @@ __global__ __launch_bounds__(256, 4) void dgrad16_kernel(DgradArgs d) {
   }
 }
 
+// Weight gradient of a Cout = 1 conv (the discriminator's logit conv,
+// networks.py:403-406): [dW | db] [Cin*KK + 1] with
+//   dW[ci][ky][kx] = sum_q g[q] x[n][ci][oy*s+ky-p][ox*s+kx-p],  db = sum_q g[q],
+// g = sum of nslab slabs (x LeakyReLU'(y)) as in d_prep16_kernel.  With
+// Cout = 1 the im2col16 + GEMM route materialises Cin*KK*N*P bf16 columns
+// (299 MB at C4) for a GEMV; here block (ci, z) keeps its KK tap sums over
+// pixel slice z in registers (fp32 products, the input read once through L1,
+// WC1_U pixels' loads in flight per iteration) and writes them to partial row z;
+// wgrad_cout1_sum adds the WC1_S rows in fixed order (bit-reproducible).
+// Channel index Cin is the bias.
+constexpr int WC1_S = 8, WC1_U = 2;   // pixel slices per channel, pixels in flight per thread
+
+template <int K>
+__global__ __launch_bounds__(256) void wgrad_cout1_kernel(const float* __restrict__ x,
+                                                          const float* __restrict__ g, int nslab,
+                                                          int64_t slab_stride,
+                                                          const float* __restrict__ y, float slope,
+                                                          int Cin, int H, int W, int Ho, int Wo,
+                                                          int stride, int pad, int64_t NP,
+                                                          float* __restrict__ part) {
+  constexpr int KK = K * K;
+  __shared__ float red[4][KK];
+  const int ci = blockIdx.x, z = blockIdx.y;
+  const int P = Ho * Wo;   // NP < 2^31 (host check): 32-bit index arithmetic
+  const int chunk = (int)((NP + WC1_S - 1) / WC1_S);
+  const int qa = z * chunk, qb = min((int)NP, qa + chunk);
+  float acc[KK];
+#pragma unroll
+  for (int t = 0; t < KK; ++t) acc[t] = 0.f;
+  for (int q0 = qa + threadIdx.x; q0 < qb; q0 += 256 * WC1_U) {
+    float gv[WC1_U], xv[WC1_U][KK];
+#pragma unroll
+    for (int e = 0; e < WC1_U; ++e) {
+      const int q = q0 + 256 * e;
+      const bool vq = q < qb;
+      float gq = 0.f;
+      if (vq) {
+        for (int zz = 0; zz < nslab; ++zz) gq += g[zz * slab_stride + q];
+        if (y && !(y[q] > 0.f)) gq *= slope;
+      }
+      gv[e] = gq;
+      if (ci == Cin) continue;
+      const int n = vq ? q / P : 0;
+      const int r = vq ? q - n * P : 0;
+      const int oy = r / Wo, ox = r - oy * Wo;
+      const int by = vq ? oy * stride - pad : -(1 << 28), bx = ox * stride - pad;
+      const float* xp = x + ((int64_t)n * Cin + ci) * (int64_t)H * W;
+#pragma unroll
+      for (int ky = 0; ky < K; ++ky) {
+        const int iy = by + ky;
+        const bool vy = iy >= 0 && iy < H;
+#pragma unroll
+        for (int kx = 0; kx < K; ++kx) {
+          const int ix = bx + kx;
+          xv[e][ky * K + kx] = (vy && ix >= 0 && ix < W) ? xp[(int64_t)iy * W + ix] : 0.f;
+        }
+      }
+    }
+    if (ci == Cin) {
+#pragma unroll
+      for (int e = 0; e < WC1_U; ++e) acc[0] += gv[e];
+      continue;
+    }
+#pragma unroll
+    for (int e = 0; e < WC1_U; ++e)
+#pragma unroll
+      for (int t = 0; t < KK; ++t) acc[t] = fmaf(gv[e], xv[e][t], acc[t]);
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int t = 0; t < KK; ++t) {
+    const float v = wave_sum(acc[t]);
+    if (lane == 0) red[wv][t] = v;
+  }
+  __syncthreads();
+  const int64_t row = (int64_t)Cin * KK + 1;
+  if (threadIdx.x < KK) {
+    const int t = threadIdx.x;
+    const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    if (ci < Cin) part[z * row + (int64_t)ci * KK + t] = v;
+    else if (t == 0) part[z * row + (int64_t)Cin * KK] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void wgrad_cout1_sum(const float* __restrict__ part, int64_t row,
+                                                       float* __restrict__ gw) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= row) return;
+  float v = 0.f;
+#pragma unroll
+  for (int z = 0; z < WC1_S; ++z) v += part[z * row + i];
+  gw[i] = v;
+}
+
 }  // namespace d16
 }  // namespace ainp
 
@@ -370,6 +464,34 @@ extern "C" int ainp_im2col16(const float* x, int64_t N, int C, int H, int W, int
                      dim3(256), 0, as_stream(stream), x, C, H, W, KH, KW, stride, pad, Ho, Wo, NP,
                      ones_row, col, ldA);
   return check_launch("im2col16");
+}
+
+extern "C" int ainp_wgrad_cout1(const float* x, const float* g, int nslab, int64_t slab_stride,
+                                const float* y, float slope, int64_t N, int Cin, int H, int W,
+                                int k, int stride, int pad, float* gw, float* ws, void* stream) {
+  if (!x || !g || !gw || !ws || nslab < 1 || N < 1 || Cin < 1 || stride < 1 || pad < 0 ||
+      (k != 3 && k != 4) || Cin >= 65535)
+    return record_msg("ainp_wgrad_cout1: bad argument (k 3 or 4, workspace)");
+  const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  const int64_t NP = N * Ho * Wo;
+  if (Ho < 1 || Wo < 1 || (nslab > 1 && slab_stride < NP) || NP >= (int64_t)1 << 31)
+    return record_msg("ainp_wgrad_cout1: bad shape (N*Ho*Wo < 2^31)");
+  const dim3 grid((unsigned)(Cin + 1), d16::WC1_S);
+  hipStream_t s = as_stream(stream);
+  if (k == 4)
+    hipLaunchKernelGGL(d16::wgrad_cout1_kernel<4>, grid, dim3(256), 0, s, x, g, nslab,
+                       slab_stride, y, slope, Cin, H, W, Ho, Wo, stride, pad, NP, ws);
+  else
+    hipLaunchKernelGGL(d16::wgrad_cout1_kernel<3>, grid, dim3(256), 0, s, x, g, nslab,
+                       slab_stride, y, slope, Cin, H, W, Ho, Wo, stride, pad, NP, ws);
+  const int64_t row = (int64_t)Cin * k * k + 1;
+  hipLaunchKernelGGL(d16::wgrad_cout1_sum, dim3((unsigned)cdiv(row, 256)), dim3(256), 0, s, ws, row,
+                     gw);
+  return check_launch("wgrad_cout1");
+}
+
+extern "C" int64_t ainp_wgrad_cout1_workspace(int Cin, int k) {
+  return (int64_t)d16::WC1_S * ((int64_t)Cin * k * k + 1) * (int64_t)sizeof(float);
 }
 
 extern "C" int ainp_dgrad16_weight(const float* w, int Cout, int Cin, int k, int stride, int pad,

@@ -1107,6 +1107,24 @@ void d_prep16(const Tensor& g, int64_t nslab, const OptT& y, double slope, int64
       "d_prep16");
 }
 
+void wgrad_cout1(const Tensor& x, const Tensor& g, int64_t nslab, const OptT& y, double slope,
+                 int64_t k, int64_t stride, int64_t pad, const Tensor& gw, const Tensor& ws) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  numel_is(g, nslab * N * Ho * Wo, "g");
+  const float* yp = opt(y, "y");
+  if (yp) numel_is(*y, N * Ho * Wo, "y");
+  numel_is(gw, C * k * k + 1, "gw");
+  TORCH_CHECK(ws.numel() * 4 >= ainp_wgrad_cout1_workspace((int)C, (int)k),
+              "ws smaller than ainp_wgrad_cout1_workspace");
+  chk(ainp_wgrad_cout1(dev(x, "x"), dev(g, "g"), (int)nslab, N * Ho * Wo, yp, (float)slope, N,
+                       (int)C, (int)H, (int)W, (int)k, (int)stride, (int)pad, dev(gw, "gw"),
+                       dev(ws, "ws"), stream_of(x)),
+      "wgrad_cout1");
+}
+
 void im2col16(const Tensor& x, int64_t k, int64_t stride, int64_t pad, bool ones_row,
               const Tensor& col) {
   GUARD(x);
@@ -1246,6 +1264,8 @@ TORCH_LIBRARY(ainp, m) {
         "int pad, Tensor(a!) out) -> ()");
   m.def("d_prep16(Tensor g, int nslab, Tensor? y, float slope, int N, int C, int P, "
         "Tensor(a!) gA, Tensor(b!)? gT) -> ()");
+  m.def("wgrad_cout1(Tensor x, Tensor g, int nslab, Tensor? y, float slope, int k, int stride, "
+        "int pad, Tensor(a!) gw, Tensor(b!) ws) -> ()");
   m.def("im2col16(Tensor x, int k, int stride, int pad, bool ones_row, Tensor(a!) col) -> ()");
   m.def("dgrad16_weight(Tensor w, int stride, int pad, Tensor(a!) wd) -> ()");
   m.def("dgrad16(Tensor gT, Tensor wd, int Cin, int H, int W, int k, int stride, int pad, "
@@ -1310,6 +1330,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("conv_gen_fwd_nhwc16", &conv_gen_fwd_nhwc16);
   m.impl("im2col_nhwc16", &im2col_nhwc16);
   m.impl("d_prep16", &d_prep16);
+  m.impl("wgrad_cout1", &wgrad_cout1);
   m.impl("im2col16", &im2col16);
   m.impl("dgrad16_weight", &dgrad16_weight);
   m.impl("dgrad16", &dgrad16);
@@ -1376,6 +1397,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("conv_gen_fwd_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("im2col_nhwc16", torch::CppFunction::makeFallthrough());
   m.impl("d_prep16", torch::CppFunction::makeFallthrough());
+  m.impl("wgrad_cout1", torch::CppFunction::makeFallthrough());
   m.impl("im2col16", torch::CppFunction::makeFallthrough());
   m.impl("dgrad16_weight", torch::CppFunction::makeFallthrough());
   m.impl("dgrad16", torch::CppFunction::makeFallthrough());

@@ -47,7 +47,7 @@ def test_d_prep16_bit_exact(nslab, act, C, want_gT):
 
 
 @pytest.mark.parametrize("C,H,W,k,s,p", [(1, 21, 30, 4, 2, 1), (5, 11, 14, 4, 1, 1),
-                                         (3, 10, 9, 3, 2, 0)])
+                                         (3, 10, 9, 3, 2, 0), (2, 5, 5, 4, 2, 1)])
 def test_im2col16_bit_exact(C, H, W, k, s, p):
     from ainp import ops
     g = torch.Generator().manual_seed(H * W)

@@ -286,6 +286,31 @@ def test_conv_gen_cout1(k, s, p, crop, act, C, H, W):
     assert rel(y, yr) < 1e-5
 
 
+@pytest.mark.parametrize("k,s,p,C,H,W,nslab,leaky", [
+    (4, 1, 1, 512, 31, 77, 1, False),     # the C4 logit conv
+    (4, 2, 1, 64, 21, 33, 2, True),       # split-K slabs + LeakyReLU' folded in
+    (3, 1, 1, 7, 9, 13, 1, True)])
+def test_wgrad_cout1_matches_torch(k, s, p, C, H, W, nslab, leaky):
+    """ainp_wgrad_cout1 against torch's fp32 conv weight/bias gradient."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(11)
+    N = 3
+    x = torch.randn(N, C, H, W, generator=g)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    gs = torch.randn(nslab, N, 1, Ho, Wo, generator=g)
+    y = torch.randn(N, 1, Ho, Wo, generator=g) if leaky else None
+    gr = gs.sum(0)
+    if leaky:
+        gr = torch.where(y > 0, gr, gr * 0.2)
+    w = torch.zeros(1, C, k, k, requires_grad=True)
+    b = torch.zeros(1, requires_grad=True)
+    torch.nn.functional.conv2d(x, w, b, stride=s, padding=p).backward(gr)
+    gw = ops.wgrad_cout1(x.cuda(), gs.cuda().contiguous(), nslab,
+                         None if y is None else y.cuda(), 0.2, k, s, p).cpu()
+    assert rel(gw[0, :-1], w.grad.reshape(-1)) < 1e-5
+    assert abs(gw[0, -1] - b.grad[0]) <= 1e-4 * max(1.0, abs(b.grad[0]))
+
+
 # ------------------------------------------------------------- partial conv
 def test_partial_conv_fixture_cases(small):
     from ainp import gan as G
