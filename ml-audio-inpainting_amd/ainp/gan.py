@@ -409,6 +409,11 @@ class _DiscriminatorFn(torch.autograd.Function):
         return (gx, None, None, None, None, None, *grads)
 
 
+# Discriminator forward: the spectral-norm u / v snapshots for the backward as
+# one multi-tensor copy, none without autograd (AINP_SN_FOREACH=0: per-tensor
+# clones in every pass, A/B)
+SN_FOREACH = os.environ.get("AINP_SN_FOREACH", "1") != "0"
+
 # bf16 configurations: the D backward on bf16 operands in HBM (csrc/dconv16.hip);
 # AINP_D_BWD16=0 keeps the fp32-staged im2col / GEMM / col2im loop
 D_BWD16 = os.environ.get("AINP_D_BWD16", "1") != "0"
@@ -504,8 +509,17 @@ class Discriminator(nn.Module):
         training = convs[0].training
         inv = ops.sn_power(ws, [c.weight_u for c in convs], [c.weight_v for c in convs],
                            update=training)
-        us = [c.weight_u.clone() for c in convs]
-        vs = [c.weight_v.clone() for c in convs]
+        L = len(convs)
+        if SN_FOREACH and not (torch.is_grad_enabled() and any(w.requires_grad for w in ws)):
+            # no backward (the G step's D pass): nothing keeps u / v
+            us, vs = [c.weight_u for c in convs], [c.weight_v for c in convs]
+        elif SN_FOREACH:
+            # the 2L clones as one multi-tensor launch (x * 1.0 is an exact copy)
+            uv = torch._foreach_mul([c.weight_u for c in convs] + [c.weight_v for c in convs], 1.0)
+            us, vs = uv[:L], uv[L:]
+        else:
+            us = [c.weight_u.clone() for c in convs]
+            vs = [c.weight_v.clone() for c in convs]
         params = []
         for c in convs:
             params += [c.weight_orig, c.bias]

@@ -1,7 +1,6 @@
 #!/bin/bash
-# Generator mask chain on a side stream (AINP_MASK_SIDE): GAN GPU tests, C4 and
-# (AINP_MASK_SIDE was the experiment of profiles/r03_ms_summary.txt; dropped.)
-# C5 bf16 A/B on one box.
+# GAN step A/B on one box (AINP_SN_FOREACH; first used for AINP_MASK_SIDE,
+# profiles/r03_ms_summary.txt, dropped): GAN GPU tests, C4 and C5 bf16 benches.
 set -o pipefail
 OUT=gpurun_out/${1:-ms}
 mkdir -p "$OUT"
@@ -10,13 +9,13 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_gan.py tests/test_gpu_dist.
   --timeout-method thread > "$OUT/pytest.log" 2>&1 || { tail -30 "$OUT/pytest.log"; exit 1; }
 tail -1 "$OUT/pytest.log"
 for v in 0 1 0 1; do
-  AINP_MASK_SIDE=$v timeout -k 10 300 python bench.py --workload gan --dtype bf16 --steps 20 --warmup 5 \
+  AINP_SN_FOREACH=$v timeout -k 10 300 python bench.py --workload gan --dtype bf16 --steps 20 --warmup 5 \
     --no-cpu-baseline > "$OUT/c4_$v.json" 2> "$OUT/c4_$v.err" || { tail -5 "$OUT/c4_$v.err"; exit 1; }
-  python -c "import json;d=json.loads(open('$OUT/c4_$v.json').read().strip().splitlines()[-1]);print('C4 mask_side=$v',d['ms_per_step'],d['ms_per_step_median'])"
+  python -c "import json;d=json.loads(open('$OUT/c4_$v.json').read().strip().splitlines()[-1]);print('C4 sn_foreach=$v',d['ms_per_step'],d['ms_per_step_median'])"
 done
 for v in 0 1; do
-  AINP_MASK_SIDE=$v timeout -k 10 300 python bench.py --workload gan --clip-s 8 --dtype bf16 --steps 20 \
+  AINP_SN_FOREACH=$v timeout -k 10 300 python bench.py --workload gan --clip-s 8 --dtype bf16 --steps 20 \
     --warmup 5 --no-cpu-baseline > "$OUT/c5_$v.json" 2> "$OUT/c5_$v.err" || { tail -5 "$OUT/c5_$v.err"; exit 1; }
-  python -c "import json;d=json.loads(open('$OUT/c5_$v.json').read().strip().splitlines()[-1]);print('C5 mask_side=$v',d['ms_per_step'],d['ms_per_step_median'])"
+  python -c "import json;d=json.loads(open('$OUT/c5_$v.json').read().strip().splitlines()[-1]);print('C5 sn_foreach=$v',d['ms_per_step'],d['ms_per_step_median'])"
 done
 echo "all ok"
