@@ -344,6 +344,44 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
     return roof, roof_bwd
 
 
+def spawn_ranks(n):
+    """Launch this script as N ranks (torch.distributed.run, 127.0.0.1, one
+    process per GPU, RCCL unless AINP_DIST_BACKEND says otherwise) with the
+    same arguments, stream their output through, and check that rank 0's JSON
+    line reports n_gpus == N.  Returns the launcher's exit code."""
+    import socket
+    import subprocess
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={n}", "--master-addr=127.0.0.1", f"--master-port={port}",
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC only on this host
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True, bufsize=1)
+    line_out = None
+    for line in proc.stdout:
+        if line.lstrip().startswith("{"):
+            try:
+                rec = json.loads(line)
+            except ValueError:
+                rec = None
+            if isinstance(rec, dict) and "metric" in rec:
+                line_out = rec
+        sys.stdout.write(line)
+        sys.stdout.flush()
+    rc = proc.wait()
+    if rc == 0:
+        if line_out is None:
+            raise SystemExit("bench.py: the ranks printed no result line")
+        if line_out.get("n_gpus") != n:
+            raise SystemExit(f"bench.py: launched {n} ranks, result reports "
+                             f"n_gpus={line_out.get('n_gpus')}")
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -363,6 +401,13 @@ def main():
                     help="fp32 = C2 (headline); bf16 = the C3 per-GPU shape (bf16 GEMM/conv "
                          "operands, fp32 accumulate / cell state / BN statistics / weights)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N`: one rank per GPU, started here before this
+        # process touches the GPU (it never does); rank 0's line is passed on
+        return spawn_ranks(args.gpus)
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws != args.gpus and not (ws == 1 and args.gpus == 1):
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws}")
     if args.workload == "gan":
         return run_gan(args)
 
@@ -772,4 +817,4 @@ def run_gan(args):
 
 
 if __name__ == "__main__":
-    main()
+    raise SystemExit(main() or 0)

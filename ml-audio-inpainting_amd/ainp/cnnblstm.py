@@ -191,8 +191,14 @@ class _ConvStackFn(torch.autograd.Function):
                     dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
                     sw.handoff((xin, gy) + tuple(t for t in pro if t is not None), (dw, db))
                     # data parallel: all-reduced from the side stream as soon as
-                    # they exist (the collective waits for this stream only)
+                    # they exist (the collective waits for this stream only).
+                    # The collective's Work keeps a reference to what it reduces,
+                    # so autograd gets a separate non-view alias of the same
+                    # storage: AccumulateGrad then steals its tensor instead of
+                    # cloning it on the compute stream before the side stream
+                    # has written it (the BLSTM / _Deferred pattern)
                     _reduce_side(ctx.sink, ctx.param_objs[p0:p0 + 2], (dw, db))
+                    dw, db = _alias(dw), _alias(db)
             else:
                 dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
             grads[p0], grads[p0 + 1] = dw, db
@@ -304,15 +310,21 @@ class _BLSTMFn(torch.autograd.Function):
             ready = torch.cuda.Event()
             ready.record(main)
             side.wait_event(ready)
-            early = (l == 0 and ctx.sink is not None and ctx.sink.early_ok
-                     and all(p.grad is None for p in ctx.wih0))
-            # fp32 layer 0, no data parallelism: dX and dW_ih in ONE launch on
-            # the current stream (gemm_x6r.hip: the weight-gradient tiles first,
-            # the data-gradient tiles behind them), instead of dX here beside a
-            # split-K weight gradient on the side stream
-            pair = (l == 0 and l016 is None and not bf16 and not ops.GEMM_EXACT and not early
-                    and ctx.sink is None and (l > 0 or ctx.needs_input_grad[0])
+            # fp32 layer 0: dX and dW_ih in ONE launch on the current stream
+            # (gemm_x6r.hip: the weight-gradient tiles first, the data-gradient
+            # tiles behind them), instead of dX here beside a split-K weight
+            # gradient on the side stream
+            pair = (l == 0 and l016 is None and not bf16 and not ops.GEMM_EXACT
+                    and (l > 0 or ctx.needs_input_grad[0])
                     and ops.l0_bwd_x6r_eligible(NT, Il, H))
+            # data parallel: the layer-0 input weights' gradients go to the
+            # reducer as soon as they exist, bypassing autograd -- after the
+            # pair launch (the same kernels as one GPU: its all-reduce then
+            # overlaps the whole encoder backward), or chunk by chunk from the
+            # side stream where the pair does not run
+            to_sink = (l == 0 and ctx.sink is not None and ctx.sink.early_ok
+                       and all(p.grad is None for p in ctx.wih0))
+            early = to_sink and not pair
             with torch.cuda.stream(side):
                 # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
                 # for the recurrent / upper layers -> parallel split-K over row chunks
@@ -350,7 +362,13 @@ class _BLSTMFn(torch.autograd.Function):
                     ev.record(side)
                     main.wait_event(ev)
                 ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
-            if early:   # p.grad set and reduced by _wih_grad_chunked: nothing for autograd
+                if to_sink:
+                    # all-reduced from the current stream right behind the pair;
+                    # the reducer's Work holds these buffers, autograd gets None
+                    for d in range(2):
+                        ctx.sink.reduce_chunk(ctx.wih0[d], gwi[d], kind="pair")
+                        ctx.wih0[d].grad = gwi[d]
+            if to_sink:   # p.grad set and reduced above / by _wih_grad_chunked
                 gwi = [None, None]
                 ctx.early_done = True
             grads[base + 0], grads[base + 1] = gwi[0], gwh[0]

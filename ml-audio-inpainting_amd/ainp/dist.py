@@ -35,13 +35,20 @@ class Comm:
     compute stream waits on SyncBN.  With separate communicators the gradient
     all-reduce overlaps the rest of the backward."""
 
-    def __init__(self, group=None, grad_group="new"):
+    def __init__(self, group=None, grad_group="new", host_staging=None):
         self.group = group
         self.world_size = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         # gloo with GPU tensors (the multi-rank tests on a one-GPU box): stage
-        # through host memory; RCCL ("nccl") reduces device tensors directly
-        self.host_staging = dist.get_backend(group) == "gloo"
+        # through host memory; RCCL ("nccl") reduces device tensors directly.
+        # host_staging=False (or AINP_GLOO_DEVICE=1) hands device tensors to
+        # gloo's own async CUDA path instead: the collective then runs behind
+        # the issuing stream and its Work holds the reduced tensors until
+        # wait(), the RCCL semantics the side-stream hand-offs must survive
+        if host_staging is None:
+            host_staging = (dist.get_backend(group) == "gloo"
+                            and os.environ.get("AINP_GLOO_DEVICE", "0") != "1")
+        self.host_staging = bool(host_staging)
         if grad_group == "new":
             # collective call: every rank constructs its Comm at the same point
             ranks = dist.get_process_group_ranks(group) if group is not None else \
@@ -116,6 +123,7 @@ class GradAllReducer:
         self._inflight = []          # (work, params, flat or None)
         self._seen = set()           # params queued since the last allreduce()
         self._chunked = set()        # params reduced chunk by chunk since then
+        self.reduced_storage = {}    # id(p) -> storage pointers reduce_chunk reduced
         self._hooks = []
         self.paused = False          # hooks ignore gradients (e.g. a discarded backward)
         if self.overlap:
@@ -144,6 +152,9 @@ class GradAllReducer:
         (it sets it to the full buffer); allreduce() waits for the chunk."""
         self._seen.add(id(p))
         self._chunked.add(id(p))
+        # storage each hand-off reduced (checked against p.grad by the DP tests:
+        # the reduced buffer must be the one the optimizer reads)
+        self.reduced_storage.setdefault(id(p), set()).add(chunk.untyped_storage().data_ptr())
         if self.comm.host_staging and chunk.is_cuda:
             self.comm._allreduce(chunk, dist.ReduceOp.SUM, group=self.group)
             work = _Done()
@@ -152,10 +163,13 @@ class GradAllReducer:
         self._inflight.append((work, [], None))
         if kind == "early":
             self.early_chunks += 1
+        elif kind == "pair":
+            self.pair_reductions += 1
         else:
             self.side_reductions += 1
 
     early_chunks = 0        # layer-0 input-weight gradient chunks (reduce_chunk)
+    pair_reductions = 0     # layer-0 input-weight gradients from the fused pair launch
     side_reductions = 0     # side-stream weight gradients (kind="side")
 
     # -- overlapped path ------------------------------------------------------
@@ -249,6 +263,7 @@ class GradAllReducer:
             self._finish()
             self._seen.clear()
             self._chunked.clear()
+            self.reduced_storage = {}
             return
         for bucket in self._buckets():
             self._launch(bucket)

@@ -113,6 +113,11 @@ class GanTrainer:
                 d_fake_g = self.D(generated)
                 losses = G.calculate_losses(self.cfg, generated, original_mag, mask, d_fake_g,
                                             self.vgg, comm=self.comm)
+        if self.fail_fast:
+            # the reference reads both losses every step: a non-finite G loss
+            # stops every rank before g_optimizer.step() too
+            from .failfast import check_finite
+            check_finite(losses["g_total"], "G loss", self.nstep - 1, self.comm)
         self.g_opt.step()   # no-op: G has no gradients (Q1)
         out = {k: v.detach() for k, v in losses.items()}
         out.update(d_loss=d_loss.detach(), d_real=l_real.detach(), d_fake=l_fake.detach())

@@ -1,0 +1,196 @@
+"""Round-4 golden fixtures (bf16 gates that can fail).
+
+Run in the build container (where /root/reference exists):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden_r04.py [bf16emu]
+
+The reference's models/CNNBLSTM/model.py is imported (never copied) and run
+on the C2 batch of cnnblstm_c2.npz (seed-0 weights, the same inputs); only
+data is written:
+
+  cnnblstm_c2_bf16emu.npz
+      The reference model with the bf16 configuration's rounding points
+      emulated operand by operand -- the arithmetic the HIP bf16 path runs
+      (csrc/conv_x6.hip NP = 1 kernels, gemm16.hip, gemm.hip's one-plane loop),
+      fp32 everywhere else:
+        * every conv except the 1 <-> 16-channel pairs (encoder.0,
+          decoder.6: ainp's exact f32 kernels, conv.hip small_pair):
+            forward  y  = conv(bf16(act(x)), bf16(W)) + b
+            dgrad    dx = conv^T(bf16(dy), bf16(W))
+            wgrad    dW = bf16(act(x)) (*) bf16(dy);  db = sum dy (fp32)
+        * nn.Linear projection and every LSTM input projection (both
+          directions, all layers):
+            forward  z  = bf16(x) bf16(W)^T + b        (+ b_hh for the LSTM)
+            backward dx = bf16(dg) bf16(W);  dW = bf16(dg)^T bf16(x)
+        * LSTM recurrence h_{t-1} W_hh^T, cell state, gates: fp32; its weight
+          gradient dW_hh = bf16(dg)^T bf16(h_{t-1}) (ops.gemm_tn_splitk bf16)
+        * BatchNorm (statistics, affine, backward), ReLU, the L1(sum) of
+          10**y inside the gap: fp32.
+      Stored: output sample / loss and every parameter gradient's norm and
+      strided sample (the cnnblstm_c2.npz sampling), for the emulation in fp32
+      ("emu32/") and, with the same rounding points, in fp64 between them
+      ("emu64/").  |emu32 - emu64| is the emulation's own accumulation-order
+      floor: rounding points are discontinuous, so two exact restatements
+      that sum in different orders round a few operands differently.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "ml-audio-inpainting_amd"))
+sys.path.insert(0, os.path.dirname(HERE))
+
+from golden.gen_golden_r02 import _load, _sample, _write_cfg, c2_config, c2_inputs  # noqa: E402
+
+
+def _r(a):
+    """Round to bf16 (round to nearest even) and back to a's dtype."""
+    return a.to(torch.bfloat16).to(a.dtype)
+
+
+class _BLinear(torch.autograd.Function):
+    """z = bf16(x) bf16(W)^T + b; dx = bf16(g) bf16(W); dW = bf16(g)^T bf16(x)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xr, wr = _r(x), _r(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.has_b = b is not None
+        z = xr @ wr.t()
+        return z + b if b is not None else z
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, wr = ctx.saved_tensors
+        gr = _r(g)
+        dx = gr @ wr
+        dw = gr.reshape(-1, gr.shape[-1]).t() @ xr.reshape(-1, xr.shape[-1])
+        db = g.reshape(-1, g.shape[-1]).sum(0) if ctx.has_b else None
+        return dx, dw, db
+
+
+class _RecMM(torch.autograd.Function):
+    """h_{t-1} W_hh^T in full precision; dW_hh = bf16(g)^T bf16(h_{t-1})."""
+
+    @staticmethod
+    def forward(ctx, h, w):
+        ctx.save_for_backward(h, w)
+        return h @ w.t()
+
+    @staticmethod
+    def backward(ctx, g):
+        h, w = ctx.saved_tensors
+        return g @ w, _r(g).t() @ _r(h)
+
+
+class _BConv(torch.autograd.Function):
+    """3x3, padding 1: conv(bf16(x), bf16(W)) + b and the matching backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        xr, wr = _r(x), _r(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.xshape = x.shape
+        return F.conv2d(xr, wr, b, padding=1)
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, wr = ctx.saved_tensors
+        gr = _r(g)
+        dx = torch.nn.grad.conv2d_input(ctx.xshape, wr, gr, padding=1)
+        dw = torch.nn.grad.conv2d_weight(xr, wr.shape, gr, padding=1)
+        return dx, dw, g.sum((0, 2, 3))
+
+
+def _small_pair(conv):
+    a, b = conv.in_channels, conv.out_channels
+    return ((a in (1, 2)) and b == 16) or ((b in (1, 2)) and a == 16)
+
+
+def emulate(mod, dtype):
+    """Gradients, output and loss of the reference model on the C2 batch with
+    the bf16 configuration's rounding points (module docstring)."""
+    x, m, t, _ = c2_inputs()
+    with tempfile.TemporaryDirectory() as d:
+        cfgp = os.path.join(d, "cfg.yaml")
+        _write_cfg(cfgp, c2_config())
+        torch.manual_seed(0)
+        model = mod.StackedBLSTMCNN(cfgp)
+    model = model.to(dtype).train()
+    for mm in model.modules():
+        if isinstance(mm, torch.nn.Conv2d) and not _small_pair(mm):
+            mm.forward = (lambda c: lambda z: _BConv.apply(z, c.weight, c.bias))(mm)
+    lin = model.projection
+    lin.forward = lambda z: _BLinear.apply(z, lin.weight, lin.bias)
+    lstm = model.lstm
+    H = lstm.hidden_size
+
+    def lstm_fwd(z):
+        N, T, _ = z.shape
+        inp = z
+        for l in range(lstm.num_layers):
+            outs = []
+            for sfx in ("", "_reverse"):
+                wi, wh = getattr(lstm, f"weight_ih_l{l}{sfx}"), getattr(lstm, f"weight_hh_l{l}{sfx}")
+                bi, bh = getattr(lstm, f"bias_ih_l{l}{sfx}"), getattr(lstm, f"bias_hh_l{l}{sfx}")
+                zx = _BLinear.apply(inp, wi, bi) + bh
+                h = torch.zeros(N, H, dtype=dtype)
+                c = torch.zeros(N, H, dtype=dtype)
+                hs = [None] * T
+                order = range(T) if sfx == "" else range(T - 1, -1, -1)
+                for tt in order:
+                    gt = zx[:, tt] + _RecMM.apply(h, wh)
+                    i, f, gg, o = gt.chunk(4, 1)
+                    c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+                    h = torch.sigmoid(o) * torch.tanh(c)
+                    hs[tt] = h
+                outs.append(torch.stack(hs, 1))
+            inp = torch.cat(outs, 2)
+        return inp, None
+    lstm.forward = lstm_fwd
+    X = torch.from_numpy(x).to(dtype)
+    M = torch.from_numpy(m).to(dtype)
+    Tm = torch.from_numpy(np.abs(t)).to(dtype)
+    y = model(X.unsqueeze(1))
+    loss = torch.nn.L1Loss(reduction="sum")((10 ** y) * M, Tm * M)
+    loss.backward()
+    out = {"y_sample": y.detach().double().numpy().reshape(-1)[::97].copy(),
+           "loss": np.array([loss.item()])}
+    for k, p in model.named_parameters():
+        gr = p.grad.double().numpy()
+        out["gnorm/" + k] = np.array([np.linalg.norm(gr)])
+        out["gsample/" + k] = _sample(gr)
+    return out
+
+
+def gen_bf16emu(mod):
+    g = np.load(os.path.join(HERE, "cnnblstm_c2.npz"), allow_pickle=False)
+    out = {}
+    for tag, dt in (("emu32", torch.float32), ("emu64", torch.float64)):
+        res = emulate(mod, dt)
+        for k, v in res.items():
+            out[f"{tag}/{k}"] = v
+    # report: emulation floor and distance from the fp32 reference
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))  # noqa: E731
+    for k in sorted(x for x in out if x.startswith("emu32/gsample/")):
+        name = k[len("emu32/gsample/"):]
+        print(f"{name:28s} floor {rel(out[k], out['emu64/gsample/' + name]):.2e}  "
+              f"vs fp32 ref {rel(out[k], g['gsample/' + name]):.2e}")
+    print("loss", out["emu32/loss"], out["emu64/loss"], g["loss"])
+    np.savez_compressed(os.path.join(HERE, "cnnblstm_c2_bf16emu.npz"), **out)
+
+
+if __name__ == "__main__":
+    what = sys.argv[1:] or ["bf16emu"]
+    torch.set_num_threads(os.cpu_count() or 1)
+    if "bf16emu" in what:
+        gen_bf16emu(_load("models/CNNBLSTM/model.py", "ref_cnnblstm_model"))
+    print("written:", what)

@@ -76,6 +76,48 @@ def test_cnnblstm_dp2_equals_single_process(tmp_path):
     # projection, BLSTM W_hh / biases / upper W_ih) were all-reduced from the
     # side stream as they were written -- the single-GPU overlaps kept under DP
     assert ranks[0]["side_reductions"] > 0
+    assert ranks[0]["bad_storage"] == [] and ranks[1]["bad_storage"] == []
+
+
+@pytest.mark.timeout(300)
+def test_cnnblstm_dp2_device_collectives_keep_reduced_storage(tmp_path):
+    """Gradients handed to gloo's async CUDA collectives (no host staging):
+    the Work objects hold the reduced tensors until wait(), as RCCL's do, so a
+    gradient autograd received by reference would be cloned on the compute
+    stream before the side stream wrote it.  Every reduced buffer must be the
+    storage of p.grad, and the result equal the host-staged run bit for bit."""
+    dev = _run_ranks("cnnblstm:dev", tmp_path)
+    host = _run_ranks("cnnblstm", tmp_path)
+    for r in range(2):
+        assert dev[r]["bad_storage"] == [], dev[r]["bad_storage"]
+    assert dev[0]["side_reductions"] > 0 and dev[0]["early_chunks"] == 8
+    assert torch.equal(dev[0]["loss"], host[0]["loss"])
+    for k, v in host[0]["state"].items():
+        assert torch.equal(dev[0]["state"][k], v), k
+        assert torch.equal(dev[1]["state"][k], v), k
+
+
+@pytest.mark.timeout(300)
+def test_cnnblstm_dp2_fused_layer0_pair(tmp_path):
+    """H = 64 (4H = 256 gate rows): each rank runs the fp32 layer-0 backward
+    as the same single gemm_x6r launch as one GPU does and hands both
+    directions' W_ih gradients to the reducer right behind it (no chunked
+    side-stream GEMMs).  Matches the 1-process step on the whole batch, is
+    bit-identical with and without the other side-stream hand-offs, and keeps
+    the reduced buffers as the .grad storage under device collectives."""
+    import dp_worker
+    ref = dp_worker.run_cnnblstm(pair=True)
+    on = _run_ranks("cnnblstm_pair:dev", tmp_path)
+    off = _run_ranks("cnnblstm_pair_nodefer", tmp_path)
+    for res in (on, off):
+        assert res[0]["pair_reductions"] == 2 and res[0]["early_chunks"] == 0
+        assert res[0]["bad_storage"] == [] and res[1]["bad_storage"] == []
+    assert _rel(on[0]["loss"], ref["loss"]) < 1e-6
+    _check_state(on, ref)
+    assert torch.equal(on[0]["loss"], off[0]["loss"])
+    for k, v in off[0]["state"].items():
+        assert torch.equal(on[0]["state"][k], v), k
+        assert torch.equal(on[1]["state"][k], v), k
 
 
 @pytest.mark.timeout(300)
@@ -131,6 +173,15 @@ def test_gan_dp2_faithful_g_backward_two_steps(tmp_path):
     ranks = _run_ranks("gan_faithful", tmp_path)
     for k, v in ref["disc"].items():
         assert _rel(ranks[0]["disc"][k], v) < 1e-4, k
+
+
+@pytest.mark.timeout(300)
+def test_gan_dp2_nonfinite_g_loss_fails_fast_on_every_rank(tmp_path):
+    """faithful_g_backward with fail_fast: a NaN G-step loss on rank 1 stops
+    both ranks before g_optimizer.step() (MAX-all-reduced flag)."""
+    ranks = _run_ranks("gan_gnan", tmp_path)
+    assert "G loss" in ranks[1]["error"] and "on this rank" in ranks[1]["error"]
+    assert "G loss" in ranks[0]["error"] and "another DP rank" in ranks[0]["error"]
 
 
 @pytest.mark.timeout(300)

@@ -583,11 +583,18 @@ def _check_fp32_step(g, out, Gm, Dm, param_tol=1e-5):
 
 
 # bf16 gate (bf16 cannot meet 1e-4): generated spectrogram, D loss
-# and the G-step losses within BF16_STEP_TOL relative of the fp32 reference.
+# and the G-step losses within BF16_STEP_TOL relative of the fp32 reference;
+# every discriminator gradient (the bf16 D backward: csrc/dconv16.hip, the
+# logit conv's GEMV) within BF16_DGRAD_NORM_TOL (norm) / BF16_DGRAD_SAMPLE_TOL
+# (strided sample, relative L2) of the reference's fp32 gradient, and the D
+# parameters after the Adam step within BF16_DPARAM_TOL.
 BF16_STEP_TOL = 2e-2
+BF16_DGRAD_NORM_TOL = 5e-2
+BF16_DGRAD_SAMPLE_TOL = 1e-1
+BF16_DPARAM_TOL = 1e-2
 
 
-def _check_bf16_step(g, out, tag):
+def _check_bf16_step(g, out, tag, Dm=None):
     gf = out["generated"].cpu().numpy().reshape(-1)
     errs = {"generated": rel(gf[::97], g["gen_sample"]),
             "d_loss": abs(float(out["d_loss"]) - g["d_losses"][0]) / abs(g["d_losses"][0])}
@@ -595,7 +602,27 @@ def _check_bf16_step(g, out, tag):
         r = float(g["oracle_loss/" + k][0])
         errs[k] = abs(float(out[k]) - r) / abs(r)
     print(tag, "bf16 GAN step rel errs", errs)
+    gerrs, perrs = {}, {}
+    if Dm is not None:
+        for k, p in Dm.named_parameters():
+            gr = p.grad.detach().cpu().double().numpy()
+            assert np.isfinite(gr).all(), k
+            e_n = abs(np.linalg.norm(gr) - g["d_gnorm/" + k][0]) / g["d_gnorm/" + k][0]
+            e_s = rel(gr.reshape(-1)[::max(1, gr.size // 4096)], g["d_gsample/" + k])
+            gerrs[k] = (round(float(e_n), 5), round(float(e_s), 5))
+        sd = Dm.state_dict()
+        for k in g.files:
+            if k.startswith("d_after/") and "weight_u" not in k and "weight_v" not in k:
+                t = sd[k[len("d_after/"):]].cpu().numpy()
+                perrs[k] = round(float(rel(t.reshape(-1)[::max(1, t.size // 4096)], g[k])), 6)
+        print(tag, "bf16 D grad errs (norm, sample)", gerrs)
+        print(tag, "bf16 D params after Adam", perrs)
+        assert len(gerrs) == sum(1 for k in g.files if k.startswith("d_gnorm/"))
     assert max(errs.values()) < BF16_STEP_TOL, errs
+    for k, (e_n, e_s) in gerrs.items():
+        assert e_n < BF16_DGRAD_NORM_TOL and e_s < BF16_DGRAD_SAMPLE_TOL, (k, e_n, e_s)
+    for k, e in perrs.items():
+        assert e < BF16_DPARAM_TOL, (k, e)
 
 
 @pytest.mark.timeout(600)
@@ -618,11 +645,13 @@ def test_full_size_gan_step_bf16_tracks_reference(golden_dir):
     """The full-size B=2 step of gan_step_full.npz in the bf16 configuration
     (accel.dtype = bf16: bf16 conv / GEMM operands in G, D and VGG, fp32
     accumulation, BatchNorm statistics and weights): generated spectrogram,
-    D losses and G-step losses within 2e-2 relative of the fp32 reference."""
+    D losses and G-step losses within 2e-2 relative of the fp32 reference,
+    every D gradient and the D parameters after Adam at the BF16_DGRAD_* /
+    BF16_DPARAM_TOL gates."""
     from golden.gen_golden_r02 import GSTEP, gan_step_inputs
     g = np.load(os.path.join(golden_dir, "gan_step_full.npz"), allow_pickle=False)
-    out, _, _ = _fixture_step(g, GSTEP, gan_step_inputs(), dtype="bf16")
-    _check_bf16_step(g, out, "T=626")
+    out, _, Dm = _fixture_step(g, GSTEP, gan_step_inputs(), dtype="bf16")
+    _check_bf16_step(g, out, "T=626", Dm)
 
 
 @pytest.mark.timeout(600)
@@ -643,8 +672,8 @@ def test_c5_shape_gan_step_bf16_tracks_reference(golden_dir):
     within BF16_STEP_TOL of the reference's fp32 step."""
     from golden.gen_golden_r03 import GSTEP1001, gan_step1001_inputs
     g = np.load(os.path.join(golden_dir, "gan_step_t1001.npz"), allow_pickle=False)
-    out, _, _ = _fixture_step(g, GSTEP1001, gan_step1001_inputs(), dtype="bf16")
-    _check_bf16_step(g, out, "T=1001")
+    out, _, Dm = _fixture_step(g, GSTEP1001, gan_step1001_inputs(), dtype="bf16")
+    _check_bf16_step(g, out, "T=1001", Dm)
 
 
 @pytest.mark.parametrize("N,C,H,W,masked", [(2, 64, 17, 70, True), (1, 96, 5, 130, False),

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round 4, first pass: the DP tests (device collectives, fused layer-0 pair
+# under DP, G-loss fail-fast), `bench.py --gpus 2` spawning its own ranks
+# (gloo on the box's one GPU), and the C2 / C3-shape benches of this tree.
+#   gpurun -- bash tools/gpu_r04a.sh <tag>
+set -o pipefail
+OUT=gpurun_out/${1:-r04a}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {
+  local t=$1 log=$2; shift 2
+  echo "== $(date +%T) $*" | tee -a "$OUT/steps.log"
+  timeout -k 10 "$t" "$@" > "$OUT/$log" 2>&1
+  local rc=$?
+  echo "   rc=$rc" | tee -a "$OUT/steps.log"
+  tail -1 "$OUT/$log" | cut -c1-250
+  return $rc
+}
+step 900 pytest_dist.log python -u -m pytest tests/test_gpu_dist.py -x -v --timeout 300 --timeout-method thread || exit 1
+step 600 pytest_bf16gates.log python -u -m pytest tests/test_gpu_model.py tests/test_gpu_gan.py -v -s --timeout 300 --timeout-method thread -k "bf16_c2_batch32 or bf16_tracks_reference"
+AINP_DIST_BACKEND=gloo step 400 dp2_spawn.json python bench.py --gpus 2 --steps 6 --warmup 2 --no-cpu-baseline --no-graph || exit 1
+step 300 bench.json python bench.py --no-cpu-baseline --no-graph || exit 1
+step 300 bench_bf16.json python bench.py --dtype bf16 --no-cpu-baseline --no-graph || exit 1
+echo "all steps ok"
