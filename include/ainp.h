@@ -661,6 +661,77 @@ int ainp_leaky_bwd_ld(const float* g, const float* y, int64_t rows, int64_t P, f
                       int64_t ldo, float* out, void* stream);
 int ainp_col2im_ld(const float* dcol, int64_t N, int C, int H, int W, int KH, int KW, int stride,
                    int pad, int64_t ldp, float* dx, void* stream);
+/* ---- Generator backward (opt-in fix_generator_grad; csrc/gan_bwd.hip).
+ * The reference's PConvUNet / VGGLoss / calculate_losses are differentiable
+ * nn.Modules (networks.py:247-345, loss.py:89-131, train.py:33-88); only its
+ * loop's torch.no_grad() (train.py:349-350) keeps G untrained (Q1). */
+/* out = LeakyReLU(y * scale[c] + shift[c]) out of place (EncoderBlock /
+ * DecoderBlock BatchNorm + activation, networks.py:150-151; the pre-BN y is
+ * kept for the backward). */
+int ainp_affine_leaky_out(const float* y, const float* scale, const float* shift, int64_t N,
+                          int C, int64_t HW, float slope, float* out, void* stream);
+/* PartialConv2d's convolved input cat(nearest(x0) * nearest(m0), x1 * m1)
+ * [N, C0+C1, Hin, Win] (networks.py:79-82 with the decoder's x2 nearest
+ * upsample and torch.cat, networks.py:297-313); m0 / m1 [N, Hs, Ws] planes
+ * or NULL, x1 NULL when C1 == 0. */
+int ainp_pconv_src_materialize(const float* x0, const float* m0, int64_t N, int C0, int H0,
+                               int W0, const float* x1, const float* m1, int C1, int Hin, int Win,
+                               float* out, void* stream);
+/* Backward of the above for one source (channels [c_off, c_off+C) of dxin,
+ * resolution Hs x Ws, Hin % Hs == 0): dxs (+)= ms * block sum of dxin. */
+int ainp_pconv_src_grad(const float* dxin, int64_t N, int Cin, int Hin, int Win, int c_off, int C,
+                        int Hs, int Ws, const float* ms, float* dxs, int accumulate,
+                        void* stream);
+/* Activation (+crop) backward of a PartialConv2d output (act 0 none, 1 LeakyReLU,
+ * 3 Tanh; a = the activation's output, [N, C, gH, gW]): gz [N, C, H*W] =
+ * g * act'(a) (zero outside the gH x gW crop; may be NULL), gc [N, C, ldo] =
+ * gz * ratio[n][pixel] (ratio may be NULL), rows zero-padded to ldo. */
+int ainp_gen_act_bwd(const float* g, int gH, int gW, const float* a, int act, float slope,
+                     const float* ratio, int64_t N, int C, int H, int W, int64_t ldo, float* gz,
+                     float* gc, void* stream);
+/* BatchNorm2d (train mode) + LeakyReLU backward of a generator block
+ * (save = [mean | rstd] from ainp_bn_finalize; y the pre-BN conv output):
+ * reduce -> sums[0:C] = sum g', sums[C:2C] = sum g' xhat (fixed order, f64;
+ * all-reduce them for SyncBN); apply -> gc [N, C, ldo] = dy * ratio (the
+ * PartialConv2d window ratio, may be NULL), dgamma, dbeta.  count == 0: the
+ * element count is sums[2C] (ainp_bn_stats_reduce's DP form). */
+size_t ainp_bn_act_bwd_workspace(int64_t N, int C, int64_t P);
+int ainp_bn_act_bwd_reduce(const float* ga, const float* y, const float* scale, const float* shift,
+                           const float* save, float slope, int64_t N, int C, int64_t P,
+                           void* workspace, double* sums, void* stream);
+int ainp_bn_act_bwd_apply(const float* ga, const float* y, const float* scale, const float* shift,
+                          const float* save, const float* gamma, const double* sums, int64_t count,
+                          float slope, const float* ratio, int64_t N, int C, int64_t P,
+                          int64_t ldo, float* gc, float* dgamma, float* dbeta, void* stream);
+/* nn.MaxPool2d(2, 2) backward (torch's first-maximum rule), g [NC, H/2, W/2]. */
+int ainp_maxpool2_bwd(const float* g, const float* x, int64_t NC, int H, int W, float* gx,
+                      void* stream);
+/* VGG input preparation backward for the generated batch (loss.py:71,79-81 +
+ * ImageClassification): g [N, 3, S, S] -> gx [N, 1, H, W] through the
+ * normalisation, the x3 repeat, the antialiased resize + crop (the
+ * ainp_vgg_prep tables) and clamp((x+1)/2, 0, 1). */
+size_t ainp_vgg_prep_bwd_workspace(int64_t N, int W, int S);
+int ainp_vgg_prep_bwd(const float* g, const float* x, int64_t N, int H, int W, const int* ry0,
+                      const int* rn, const float* rw, int rtaps, const int* cx0, const int* cn,
+                      const float* cw, int ctaps, int S, void* workspace, float* gx,
+                      void* stream);
+/* nn.L1Loss backward: out (+)= (*gscale) * scale * sign(a - b) (gscale: a
+ * device float, e.g. autograd's incoming gradient, or NULL = 1). */
+int ainp_absdiff_grad(const float* a, const float* b, int64_t n, const float* gscale, float scale,
+                      float* out, int accumulate, void* stream);
+/* L1 of two Gram batches [B, C, C] backward, symmetrised for bmm(F, F^T):
+ * out = (*gscale) * scale * (sign(Ga - Gb) + sign(Ga - Gb)^T). */
+int ainp_gram_sign_sym(const float* Ga, const float* Gb, int64_t B, int C, const float* gscale,
+                       float scale, float* out, void* stream);
+/* calculate_losses' Lv / Lh / Lw (train.py:49-63) backward w.r.t. the
+ * generated magnitude, from the forward's sums (ainp_gan_recon_sums, after
+ * a DP all-reduce) and the three losses' incoming gradients gout3 (device). */
+int ainp_gan_recon_bwd(const float* g, const float* o, const float* m, int64_t n,
+                       const double* sums5, const float* gout3, double n_total, float* out,
+                       void* stream);
+/* out [Cin][Cout][K][K] = w[co][ci] flipped: a stride-1 'same' conv's data
+ * gradient as a forward conv (VGG19 input gradient). */
+int ainp_conv_weight_flip_t(const float* w, int Cout, int Cin, int K, float* out, void* stream);
 /* The Discriminator backward in the bf16 configurations (C4 / C5; the same
  * networks.py:375-409 convs as the row-padded fp32 forms above).
  * ainp_d_prep16: g = sum of nslab slabs [N][C][P] (slab_stride apart; the

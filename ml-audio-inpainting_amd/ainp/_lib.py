@@ -169,6 +169,26 @@ _SIGS = {
     "ainp_conv_gen_fwd_nhwc16_ex": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, P, P,
                                             P, P, P, P, c_int64, c_int, c_int, c_int, c_int, c_int,
                                             c_int, c_int, c_int, c_float, P, P, P]),
+    # generator backward (csrc/gan_bwd.hip)
+    "ainp_affine_leaky_out": (c_int, [P, P, P, c_int64, c_int, c_int64, c_float, P, P]),
+    "ainp_pconv_src_materialize": (c_int, [P, P, c_int64, c_int, c_int, c_int, P, P, c_int, c_int,
+                                           c_int, P, P]),
+    "ainp_pconv_src_grad": (c_int, [P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                    P, P, c_int, P]),
+    "ainp_gen_act_bwd": (c_int, [P, c_int, c_int, P, c_int, c_float, P, c_int64, c_int, c_int,
+                                 c_int, c_int64, P, P, P]),
+    "ainp_bn_act_bwd_workspace": (c_size_t, [c_int64, c_int, c_int64]),
+    "ainp_bn_act_bwd_reduce": (c_int, [P, P, P, P, P, c_float, c_int64, c_int, c_int64, P, P, P]),
+    "ainp_bn_act_bwd_apply": (c_int, [P, P, P, P, P, P, P, c_int64, c_float, P, c_int64, c_int,
+                                      c_int64, c_int64, P, P, P, P]),
+    "ainp_maxpool2_bwd": (c_int, [P, P, c_int64, c_int, c_int, P, P]),
+    "ainp_vgg_prep_bwd_workspace": (c_size_t, [c_int64, c_int, c_int]),
+    "ainp_vgg_prep_bwd": (c_int, [P, P, c_int64, c_int, c_int, P, P, P, c_int, P, P, P, c_int,
+                                  c_int, P, P, P]),
+    "ainp_absdiff_grad": (c_int, [P, P, c_int64, P, c_float, P, c_int, P]),
+    "ainp_gram_sign_sym": (c_int, [P, P, c_int64, c_int, P, c_float, P, P]),
+    "ainp_gan_recon_bwd": (c_int, [P, P, P, c_int64, P, P, c_double, P, P]),
+    "ainp_conv_weight_flip_t": (c_int, [P, c_int, c_int, c_int, P, P]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -6,8 +6,10 @@ so checkpoints move between the two unchanged; only the arithmetic moves onto
 libainp (ainp.ops):
 
   PartialConv2d / EncoderBlock / DecoderBlock  networks.py:10-168
-  PConvUNet       networks.py:173-345  forward-only (the reference trains G
-                  under torch.no_grad).  Every PartialConv2d is ONE
+  PConvUNet       networks.py:173-345  under torch.no_grad (the reference
+                  loop) the forward-only path; with autograd on
+                  (fix_generator_grad) _PConvUNetFn adds the generator
+                  backward (csrc/gan_bwd.hip).  Every PartialConv2d is ONE
                   implicit-GEMM launch whose gather reads the upsampled decoder
                   input and the skip directly (no torch.cat / nn.Upsample
                   tensors) times their 0/1 mask planes, plus one mask-count
@@ -17,7 +19,8 @@ libainp (ainp.ops):
                   forward = conv_gen with 1/sigma, bias and LeakyReLU fused;
                   backward = im2col + MFMA GEMMs + the spectral-norm weight-grad
                   correction.
-  VGGLoss         loss.py:6-131  VGG19.features[0..30] (frozen, forward only).
+  VGGLoss         loss.py:6-131  VGG19.features[0..30] (frozen); the input
+                  gradient of the generated batch under autograd (_VGGLossFn).
   calculate_losses train.py:33-88.
 """
 from __future__ import annotations
@@ -42,8 +45,9 @@ def _need_cuda(t, what):
         raise RuntimeError(f"ainp {what} runs on the MI355X kernels only; move it to a GPU")
 
 
-def _bn_affine(bn: nn.BatchNorm2d, stats, count, C):
-    """BatchNorm2d train (batch stats + running update) or eval -> (scale, shift).
+def _bn_affine(bn: nn.BatchNorm2d, stats, count, C, want_save=False):
+    """BatchNorm2d train (batch stats + running update) or eval -> (scale, shift)
+    (+ save = [mean | rstd] of the batch with want_save, for the backward).
     A data-parallel trainer sets `bn.ainp_comm`: the (sum, sum of squares)
     are then all-reduced (SyncBN), so every rank normalises with the statistics
     of the global batch, as the single-process reference does."""
@@ -58,10 +62,13 @@ def _bn_affine(bn: nn.BatchNorm2d, stats, count, C):
         rm = bn.running_mean if bn.track_running_stats else None
         rv = bn.running_var if bn.track_running_stats else None
         mom = bn.momentum if bn.momentum is not None else 0.1
-        sc, sh, _ = ops.bn_finalize(sums, count, bn.weight, bn.bias, rm, rv, mom, bn.eps)
+        sc, sh, save = ops.bn_finalize(sums, count, bn.weight, bn.bias, rm, rv, mom, bn.eps)
         if bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
-        return sc, sh
+        return (sc, sh, save) if want_save else (sc, sh)
+    if want_save:
+        raise NotImplementedError("generator backward through an eval-mode BatchNorm2d "
+                                  "(the reference trains G in train mode)")
     return ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
 
 
@@ -91,7 +98,8 @@ class PartialConv2d(nn.Module):
         self.ainp_bf16 = False   # set_compute_dtype(): bf16 conv operands (C4 / C5)
 
     # plane-level entry used by the U-Net: srcs = [(x, mask_plane [N,H,W]), ...]
-    def run(self, srcs, Hin, Win, act=ops.ACT_NONE, want_stats=False, crop=None):
+    def run(self, srcs, Hin, Win, act=ops.ACT_NONE, want_stats=False, crop=None,
+            with_ratio=False):
         k, s, p = self.kernel_size, self.stride, self.padding
         (x0, m0) = srcs[0]
         src1 = srcs[1] if len(srcs) > 1 else None
@@ -102,6 +110,8 @@ class PartialConv2d(nn.Module):
         y, stats = ops.conv_gen(srcs[0], self.conv.weight, src1=src1, Hin=Hin, Win=Win, stride=s,
                                 pad=p, bias=self.bias, ratio=ratio, act=act, slope=SLOPE,
                                 want_stats=want_stats, crop=crop, bf16=self.ainp_bf16)
+        if with_ratio:
+            return y, newm, stats, ratio
         return y, newm, stats
 
     def run_full_mask(self, x, mask, want_stats=False):
@@ -259,23 +269,21 @@ class PConvUNet(nn.Module):
             raise NotImplementedError("out_ch must be 1 (the reference's configuration)")
 
     def forward(self, x: torch.Tensor, mask: torch.Tensor) -> torch.Tensor:
-        """Forward only: the reference never back-propagates into G (its
-        optimizer step has no gradients), so there is no G backward
-        on this path.  Called with autograd enabled it warns once and returns a
-        tensor detached from G's parameters."""
-        if torch.is_grad_enabled() and not PConvUNet._warned_no_grad and \
-                any(p.requires_grad for p in self.parameters()):
-            import warnings
-            warnings.warn("ainp PConvUNet.forward is forward-only (no generator backward, "
-                          "SURVEY Q1): its output carries no gradient to G's parameters",
-                          stacklevel=2)
-            PConvUNet._warned_no_grad = True
+        """networks.py:247-345.  Under torch.no_grad() (the reference training
+        loop, train.py:349-350: G is never trained) the forward-only
+        path; with autograd on and trainable parameters (fix_generator_grad,
+        or any caller that back-propagates into G as the reference module
+        allows) the output carries G's gradient: _PConvUNetFn keeps each
+        block's pre-BN conv output, window ratio and batch statistics and its
+        backward runs the kernels of csrc/gan_bwd.hip plus the MFMA GEMMs."""
+        params = [p for p in self.parameters()]
+        if torch.is_grad_enabled() and any(p.requires_grad for p in params):
+            return _PConvUNetFn.apply(x.contiguous().float(), mask.contiguous().float(), self,
+                                      *params)
         with torch.no_grad(), ops.nhwc16_memo():
             return self._forward(x, mask)
 
-    _warned_no_grad = False
-
-    def _forward(self, x, mask):
+    def _check_inputs(self, x, mask):
         if x.shape[1] != self.input_channels:
             raise ValueError(f"Input x channels ({x.shape[1]}) != expected ({self.input_channels})")
         if mask.shape[1] != self.mask_channels:
@@ -283,6 +291,66 @@ class PConvUNet(nn.Module):
         if x.shape[2:] != mask.shape[2:]:
             raise ValueError("x and mask spatial dims must match")
         _need_cuda(x, "PConvUNet")
+
+    def _forward_tape(self, x, mask):
+        """The training forward of _PConvUNetFn: the same launches as _forward
+        (no channel-last memo: the pre-BN outputs must survive), recording what
+        the backward needs.  Returns (output [N,1,H,W], tape)."""
+        self._check_inputs(x, mask)
+        N, _, H, W = x.shape
+        f = self._total_downsampling
+        Hp, Wp = H + get_pad_size(H, f), W + get_pad_size(W, f)
+        xp, mp = ops.gan_pad_input(x, mask, Hp, Wp)
+        xp4, mp4 = xp.view(N, 1, Hp, Wp), mp.view(N, 1, Hp, Wp)
+        tape = {"Hp": Hp, "Wp": Wp, "H": H, "W": W, "blocks": []}
+
+        def block(blk, srcs, Hin, Win):
+            pc = blk.pconv
+            y, newm, stats, ratio = pc.run(srcs, Hin, Win, want_stats=blk._want_stats(),
+                                           with_ratio=True)
+            Nn, C, Ho, Wo = y.shape
+            if isinstance(blk.norm, nn.BatchNorm2d):
+                sc, sh, save = _bn_affine(blk.norm, stats, Nn * Ho * Wo, C, want_save=True)
+            else:
+                sc = torch.ones(C, device=y.device)
+                sh = torch.zeros(C, device=y.device)
+                save = None
+            a = ops.affine_leaky_out(y, sc, sh, SLOPE)
+            tape["blocks"].append({"blk": blk, "srcs": srcs, "Hin": Hin, "Win": Win, "y": y,
+                                   "ratio": ratio, "sc": sc, "sh": sh, "save": save, "a": a})
+            return a, newm
+
+        srcs = [(xp4, mp), (mp4, mp)]
+        Hc, Wc = Hp, Wp
+        feats, masks = [], []
+        for blk in self.encoder_blocks:
+            a, m = block(blk, srcs, Hc, Wc)
+            feats.append(a)
+            masks.append(m)
+            Hc, Wc = a.shape[2:]
+            srcs = [(a, m)]
+        d, dm = feats[-1], masks[-1]
+        for i, blk in enumerate(self.decoder_blocks):
+            j = len(feats) - 2 - i
+            Hs, Ws = feats[j].shape[2:]
+            if (2 * d.shape[2], 2 * d.shape[3]) != (Hs, Ws):
+                raise RuntimeError("decoder/skip size mismatch")
+            d, dm = block(blk, [(d, dm), (feats[j], masks[j])], Hs, Ws)
+        if (2 * d.shape[2], 2 * d.shape[3]) != (Hp, Wp):
+            raise RuntimeError(f"Size mismatch before final layer. Dec: {d.shape[2:]}, "
+                               f"Skip: {(Hp, Wp)}")
+        pc1, pc2 = self.final_decoder_layer[0], self.final_decoder_layer[2]
+        s1 = [(d, dm), (xp4, mp)]
+        y1, m1, _, r1 = pc1.run(s1, Hp, Wp, act=ops.ACT_LEAKY, with_ratio=True)
+        s2 = [(y1, m1)]
+        out, _, _, r2 = pc2.run(s2, Hp, Wp, act=ops.ACT_TANH, crop=(H, W), with_ratio=True)
+        tape["pc1"] = {"pc": pc1, "srcs": s1, "ratio": r1, "a": y1}
+        tape["pc2"] = {"pc": pc2, "srcs": s2, "ratio": r2, "a": out.view(N, 1, H, W)}
+        tape["n_enc"] = len(self.encoder_blocks)
+        return out.view(N, 1, H, W), tape
+
+    def _forward(self, x, mask):
+        self._check_inputs(x, mask)
         x = x.contiguous().float()
         mask = mask.contiguous().float()
         N, _, H, W = x.shape
@@ -316,6 +384,157 @@ class PConvUNet(nn.Module):
         # final PartialConv2d (Cout=1) + Tanh + crop to the input size in one launch
         out, _, _ = pc2.run([(y1, m1)], Hp, Wp, act=ops.ACT_TANH, crop=(H, W))
         return out.view(N, 1, H, W)
+
+
+def _ld4(P):
+    """Pixel rows padded to a multiple of 4 (16-byte GEMM loads)."""
+    return P + (-P) % 4
+
+
+def _pconv_weight_data_grads(pc, gc, srcs, Hin, Win, dsrcs):
+    """Weight gradient of a PartialConv2d's conv and the gradients of its
+    sources from gc [N, Cout, ldo] = d(conv output) (window ratio applied):
+      dW [Cout, Cin*k*k] = sum_n gc_n . im2col(input_n)^T   (MFMA GEMM, split-K)
+      dinput = col2im(W^T . gc),  dsrc (+)= mask * block-sum(dinput[channels])
+    input = cat(nearest(x0) * m0, x1 * m1) (networks.py:79-82,297-313).
+    dsrcs: per source a (tensor to accumulate into, accumulate flag) or None."""
+    w = pc.conv.weight
+    Cout, Cin, k, _ = w.shape
+    s, p = pc.stride, pc.padding
+    bf16 = pc.ainp_bf16
+    N, _, ldo = gc.shape
+    xin = ops.pconv_src_materialize(srcs[0], srcs[1] if len(srcs) > 1 else None, Hin, Win)
+    K = Cin * k * k
+    col = ops.im2col(xin, k, s, p, ldp=ldo)                       # [N, K, ldo]
+    dw = torch.empty(Cout, K, device=gc.device)
+    ops.gemm_batched_splitk(Cout, K, ldo, [gc[n] for n in range(N)], ldo, 1,
+                            [col[n] for n in range(N)], 1, ldo, dw, bf16=bf16)
+    del col
+    if any(d is not None for d in dsrcs):
+        dcol = torch.empty(N, K, ldo, device=gc.device)
+        ops.gemm(K, ldo, Cout, [w], 1, K, [gc], ldo, 1, [dcol], ldo, 1, strideB=Cout * ldo,
+                 strideC=K * ldo, nstrided=N, bf16=bf16)
+        dxin = ops.col2im(dcol, N, Cin, Hin, Win, k, s, p)
+        del dcol
+        c_off = 0
+        for (x, m), d in zip(srcs, dsrcs):
+            if d is not None:
+                dst, acc = d
+                ops.pconv_src_grad(dxin, c_off, m, dst, acc)
+            c_off += x.shape[1]
+    return dw.view_as(w)
+
+
+class _PConvUNetFn(torch.autograd.Function):
+    """PConvUNet forward with autograd (the opt-in generator training of
+    SURVEY §7, fix_generator_grad): forward = PConvUNet._forward_tape; backward
+    in reverse block order -- Tanh + crop, the final PartialConv2d pair with
+    their biases, then each decoder / encoder block: LeakyReLU + BatchNorm2d
+    backward (batch statistics; SyncBN sums all-reduced under DP) times the
+    window ratio, the conv's weight gradient and its sources' gradients (the
+    skip's added to the encoder block's output gradient, the upsampled
+    decoder input's 2x2-summed into the previous block's).  The input x and
+    the mask get no gradient (data)."""
+
+    @staticmethod
+    def forward(ctx, x, mask, unet, *params):
+        out, tape = unet._forward_tape(x, mask)
+        ctx.tape = tape
+        ctx.unet = unet
+        ctx.params = params
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        tape, unet = ctx.tape, ctx.unet
+        ctx.tape = None
+        grads = {}
+        Hp, Wp, H, W = tape["Hp"], tape["Wp"], tape["H"], tape["W"]
+        g = g.contiguous()
+        N = g.shape[0]
+        P = Hp * Wp
+        ldo = _ld4(P)
+        # ---- final PartialConv2d (Cout = 1) + Tanh + crop (networks.py:331-337)
+        t2 = tape["pc2"]
+        pc2 = t2["pc"]
+        gz, gc = ops.gen_act_bwd(g, t2["a"], ops.ACT_TANH, SLOPE, t2["ratio"], Hp, Wp, ldo)
+        grads[pc2.bias] = ops.rowsum_batched(gz.view(N, 1, P))
+        y1 = tape["pc1"]["a"]
+        dy1 = torch.empty_like(y1)
+        grads[pc2.conv.weight] = _pconv_weight_data_grads(pc2, gc, t2["srcs"], Hp, Wp,
+                                                          [(dy1, False)])
+        # ---- PartialConv2d(64+1 -> 64) + LeakyReLU (networks.py:327-329)
+        t1 = tape["pc1"]
+        pc1 = t1["pc"]
+        C1 = y1.shape[1]
+        gz, gc = ops.gen_act_bwd(dy1, y1, ops.ACT_LEAKY, SLOPE, t1["ratio"], Hp, Wp, ldo)
+        grads[pc1.bias] = ops.rowsum_batched(gz.view(N, C1, P))
+        del gz
+        blocks = tape["blocks"]
+        n_enc = tape["n_enc"]
+        # gradient accumulators of every block output (decoder inputs, skips)
+        ga = [None] * len(blocks)
+        last = len(blocks) - 1
+        ga[last] = torch.empty_like(blocks[last]["a"])
+        grads[pc1.conv.weight] = _pconv_weight_data_grads(pc1, gc, t1["srcs"], Hp, Wp,
+                                                          [(ga[last], False), None])
+        del gc
+        # ---- decoder blocks (reverse), then encoder blocks (reverse)
+        for bi in range(last, -1, -1):
+            rec = blocks[bi]
+            blk = rec["blk"]
+            y, a = rec["y"], rec["a"]
+            Nn, C, Ho, Wo = y.shape
+            Pb = Ho * Wo
+            ldb = _ld4(Pb)
+            gab = ga[bi]
+            if isinstance(blk.norm, nn.BatchNorm2d):
+                bn = blk.norm
+                comm = getattr(bn, "ainp_comm", None)
+                if comm is not None and comm.world_size > 1:
+                    sums = comm.allreduce_sum_(ops.bn_act_bwd_reduce(gab, y, rec["sc"], rec["sh"],
+                                                                     rec["save"], SLOPE,
+                                                                     count=Nn * Pb))
+                    cnt = 0
+                else:
+                    sums = ops.bn_act_bwd_reduce(gab, y, rec["sc"], rec["sh"], rec["save"], SLOPE)
+                    cnt = Nn * Pb
+                gc, dgam, dbet = ops.bn_act_bwd_apply(gab, y, rec["sc"], rec["sh"], rec["save"],
+                                                      bn.weight, sums, cnt, SLOPE, rec["ratio"],
+                                                      ldb)
+                grads[bn.weight], grads[bn.bias] = dgam, dbet
+            else:
+                _, gc = ops.gen_act_bwd(gab, a, ops.ACT_LEAKY, SLOPE, rec["ratio"], Ho, Wo, ldb,
+                                        want_gz=False)
+            srcs = rec["srcs"]
+            if bi == 0:
+                dsrcs = [None, None]                      # cat(x_pad, mask_pad): data
+            elif bi < n_enc:
+                if ga[bi - 1] is None:
+                    ga[bi - 1] = torch.empty_like(blocks[bi - 1]["a"])
+                    dsrcs = [(ga[bi - 1], False)]
+                else:
+                    dsrcs = [(ga[bi - 1], True)]
+            else:
+                # decoder block i = bi - n_enc: sources (previous output, skip j)
+                i = bi - n_enc
+                prev = bi - 1                              # the block whose output is upsampled
+                j = n_enc - 2 - i
+                dsrcs = []
+                for tgt in (prev, j):
+                    if ga[tgt] is None:
+                        ga[tgt] = torch.empty_like(blocks[tgt]["a"])
+                        dsrcs.append((ga[tgt], False))
+                    else:
+                        dsrcs.append((ga[tgt], True))
+            grads[blk.pconv.conv.weight] = _pconv_weight_data_grads(
+                blk.pconv, gc, srcs, rec["Hin"], rec["Win"], dsrcs)
+            ga[bi] = None
+            del gc
+        out = []
+        for p in ctx.params:
+            out.append(grads.get(p))
+        return (None, None, None, *out)
 
 
 # ------------------------------------------------------------ discriminator
@@ -617,16 +836,19 @@ class VGGLoss(nn.Module):
             return ops.vgg_prep(x, generated, tables, target_max=mx)
         return ops.vgg_prep(x, generated, tables)
 
-    def _extract_features(self, x) -> Dict[int, torch.Tensor]:
+    def _extract_features(self, x, tape=None) -> Dict[int, torch.Tensor]:
         """loss.py:41-51 incl. the inplace-ReLU effect: a collected conv output
-        is the post-ReLU value unless the loop stops right after it."""
+        is the post-ReLU value unless the loop stops right after it.  tape (the
+        generated batch's input gradient, _VGGLossFn): every executed layer as
+        (kind, layer, input, output, feature indices of its output)."""
         feats = {}
         want = self.layer_indices_style | self.layer_indices_perceptual
         layers = list(self.vgg_layers)
         i = 0
-        with ops.nhwc16_memo():
+        with ops.nhwc16_memo() if tape is None else _nullctx():
             while i < len(layers):
                 lay = layers[i]
+                xin = x
                 if isinstance(lay, nn.Conv2d):
                     relu_next = (i < self.max_layer_idx and i + 1 < len(layers)
                                  and isinstance(layers[i + 1], nn.ReLU))
@@ -634,20 +856,26 @@ class VGGLoss(nn.Module):
                     # also writes that conv's channel-last bf16 source
                     j = i + 2 if relu_next else i + 1
                     nxt16 = (self.ainp_bf16 and j <= self.max_layer_idx and j < len(layers)
-                             and isinstance(layers[j], nn.Conv2d))
+                             and isinstance(layers[j], nn.Conv2d) and tape is None)
                     x, _ = ops.conv_gen((x, None), lay.weight, stride=1, pad=1, bias=lay.bias,
                                         act=ops.ACT_RELU if relu_next else ops.ACT_NONE,
                                         bf16=self.ainp_bf16, out16=nxt16)
+                    idx = [i]
                     if i in want:
                         feats[i] = x
                     if relu_next:
                         i += 1          # the ReLU ran inside the conv epilogue
+                        idx.append(i)
                         if i in want:
                             feats[i] = x
+                    if tape is not None:
+                        tape.append(("conv", lay, xin, x, relu_next, [q for q in idx if q in want]))
                 elif isinstance(lay, nn.MaxPool2d):
                     x = ops.maxpool2(x)
                     if i in want:
                         feats[i] = x
+                    if tape is not None:
+                        tape.append(("pool", lay, xin, x, False, [i] if i in want else []))
                 if i >= self.max_layer_idx:
                     break
                 i += 1
@@ -663,35 +891,133 @@ class VGGLoss(nn.Module):
                                 per_batch_out=True, bf16=self.ainp_bf16)
         return g
 
-    @torch.no_grad()
     def forward(self, generated, target):
+        """loss.py:89-131 -> (perceptual, style).  With autograd on and a
+        generated batch that requires grad (the generator training of
+        fix_generator_grad) the losses carry its input gradient through VGG19
+        (_VGGLossFn); otherwise no graph is built (the reference's loop)."""
         _need_cuda(generated, "VGGLoss")
+        if torch.is_grad_enabled() and generated.requires_grad:
+            return _VGGLossFn.apply(generated, target, self)
+        with torch.no_grad():
+            return self._losses(generated, target)
+
+    def _losses(self, generated, target, keep=None):
+        """keep (dict, _VGGLossFn): the generated batch's layer tape, features,
+        Gram matrices and prepared input for the backward."""
         xg, xt = self._prepare(generated, True), self._prepare(target, False)
+        tape = [] if keep is not None else None
+        B = xg.shape[0]
         if xg.shape == xt.shape:
             # one VGG pass over both batches (no normalisation layers in
             # vgg19.features: each image's features are those of its own pass)
-            B = xg.shape[0]
-            f = self._extract_features(torch.cat([xg, xt]))
+            f = self._extract_features(torch.cat([xg, xt]), tape)
             fg = {i: v[:B] for i, v in f.items()}
             ft = {i: v[B:] for i, v in f.items()}
+            split = True
         else:
-            fg, ft = self._extract_features(xg), self._extract_features(xt)
+            fg, ft = self._extract_features(xg, tape), self._extract_features(xt)
+            split = False
         perc = torch.zeros((), device=generated.device, dtype=torch.float64)
         style = torch.zeros((), device=generated.device, dtype=torch.float64)
         n_p = n_s = 0
+        grams = {}
         for i in self.layer_indices_perceptual:
             if i in fg and i in ft:
                 perc = perc + ops.absdiff_mean(fg[i], ft[i])
                 n_p += 1
         for i in self.layer_indices_style:
             if i in fg and i in ft:
-                style = style + ops.absdiff_mean(self._gram(fg[i]), self._gram(ft[i]))
+                gg, gt = self._gram(fg[i]), self._gram(ft[i])
+                style = style + ops.absdiff_mean(gg, gt)
+                grams[i] = (gg, gt)
                 n_s += 1
         if n_p:
             perc = perc / n_p
         if n_s:
             style = style / n_s
+        if keep is not None:
+            keep.update(tape=tape, fg=fg, ft=ft, grams=grams, n_p=n_p, n_s=n_s, B=B, split=split,
+                        xg_shape=tuple(generated.shape))
         return perc.to(torch.float32), style.to(torch.float32)
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False
+
+
+class _VGGLossFn(torch.autograd.Function):
+    """VGGLoss.forward with the generated batch's input gradient (loss.py:
+    89-131 under autograd; VGG19 frozen, the target needs no gradient):
+    perceptual L1 backward sign(fg - ft) / numel, style through the Gram L1
+    (sign symmetrised, times F / (c h w): bmm's backward), then back through
+    the executed layers -- max-pool (first-maximum rule), ReLU (output > 0),
+    conv data gradient as a conv with the flipped transposed weights -- and
+    the input preparation (normalisation, repeat, antialiased resize + crop,
+    clamp((x+1)/2))."""
+
+    @staticmethod
+    def forward(ctx, generated, target, vgg):
+        keep = {}
+        perc, style = vgg._losses(generated, target, keep)
+        ctx.keep, ctx.vgg = keep, vgg
+        ctx.gen = generated.detach()
+        return perc, style
+
+    @staticmethod
+    def backward(ctx, gp, gs):
+        keep, vgg = ctx.keep, ctx.vgg
+        ctx.keep = None
+        B = keep["B"]
+        fg, ft = keep["fg"], keep["ft"]
+        gp = gp.reshape(1).float().contiguous()
+        gs = gs.reshape(1).float().contiguous()
+        grams = keep["grams"]
+
+        def feature_grad(q, g):
+            """g (+)= d loss / d feature q (g: a tensor this backward owns)."""
+            if keep["n_p"] and q in vgg.layer_indices_perceptual and q in fg and q in ft:
+                g = ops.absdiff_grad(fg[q], ft[q], gp, 1.0 / (keep["n_p"] * fg[q].numel()),
+                                     out=g, accumulate=g is not None)
+            if keep["n_s"] and q in grams:
+                gg, gt = grams[q]
+                b, c, h, w = fg[q].shape
+                sg = ops.gram_sign_sym(gg, gt, gs, 1.0 / (keep["n_s"] * gg.numel()))
+                beta = 1.0 if g is not None else 0.0
+                if g is None:
+                    g = torch.empty_like(fg[q])
+                # dF_b = (dG + dG^T)_b F_b / (c h w)   (bmm(F, F^T)'s backward)
+                ops.gemm(c, h * w, c, [sg], c, 1, [fg[q]], h * w, 1, [g], h * w, 1,
+                         alpha=1.0 / (c * h * w), beta=beta, strideA=c * c, strideB=c * h * w,
+                         strideC=c * h * w, nstrided=b, bf16=vgg.ainp_bf16)
+            return g
+
+        g = None
+        for kind, lay, xin, xout, relu, idx in reversed(keep["tape"]):
+            for q in idx:
+                g = feature_grad(q, g)
+            if g is None:
+                continue
+            if keep["split"]:
+                xin, xout = xin[:B], xout[:B]
+            if kind == "pool":
+                g = ops.maxpool2_bwd(g, xin.contiguous())
+            else:
+                if relu:                 # ReLU backward: the output's sign
+                    g = ops.leaky_bwd(g, xout.contiguous(), 0.0)
+                wt = ops.conv_weight_flip_t(lay.weight)
+                g, _ = ops.conv_gen((g, None), wt, stride=1, pad=1, bf16=vgg.ainp_bf16)
+        gen = ctx.gen
+        if g is None:
+            return torch.zeros_like(gen), None, None
+        x = gen.unsqueeze(1) if gen.dim() == 3 else gen
+        tables = vgg._prep_tables(x.shape[2], x.shape[3], x.device)
+        gx = ops.vgg_prep_bwd(g, x.contiguous().float(), tables)
+        return gx.view_as(gen), None, None
 
 
 def set_compute_dtype(module: nn.Module, dtype: str = "fp32") -> nn.Module:
@@ -723,7 +1049,12 @@ def calculate_losses(cfg, generated_mag, original_mag, mask, d_fake_pred,
         generated_mag = generated_mag[:, :1]
     if original_mag.shape[1] != 1:
         original_mag = original_mag[:, :1]
-    if comm is not None and comm.world_size > 1:
+    if torch.is_grad_enabled() and generated_mag.requires_grad:
+        # generator training (fix_generator_grad): the three terms carry the
+        # gradient w.r.t. the generated magnitude (train.py:49-63 under autograd)
+        rec = _ReconFn.apply(generated_mag.contiguous().float(), original_mag.contiguous().float(),
+                             mask.contiguous().float(), comm)
+    elif comm is not None and comm.world_size > 1:
         sums = comm.allreduce_sum_(ops.gan_recon_sums(generated_mag.contiguous().float(),
                                                       original_mag.contiguous().float(),
                                                       mask.contiguous().float()))
@@ -744,6 +1075,30 @@ def calculate_losses(cfg, generated_mag, original_mag, mask, d_fake_pred,
              + lc["lambda_vgg_style"] * style)
     return {"g_total": total, "g_adv": adv, "g_l1_valid": l1v, "g_l1_hole": l1h,
             "g_mag_weighted": lw, "g_vgg_perceptual": perc, "g_vgg_style": style}
+
+
+class _ReconFn(torch.autograd.Function):
+    """calculate_losses' (Lv, Lh, Lw) (train.py:49-63) as float32 [3] with the
+    gradient w.r.t. the generated magnitude (ainp_gan_recon_bwd).  Under DP the
+    normalisers and numerators are the all-reduced global sums."""
+
+    @staticmethod
+    def forward(ctx, g, o, m, comm):
+        sums = ops.gan_recon_sums(g, o, m)
+        ws = 1
+        if comm is not None and comm.world_size > 1:
+            comm.allreduce_sum_(sums)
+            ws = comm.world_size
+        n_total = g.numel() * ws
+        ctx.save_for_backward(g, o, m, sums)
+        ctx.n_total = n_total
+        return ops.gan_recon_from_sums(sums, n_total).to(torch.float32)
+
+    @staticmethod
+    def backward(ctx, gout):
+        g, o, m, sums = ctx.saved_tensors
+        return (ops.gan_recon_bwd(g, o, m, sums, gout.float().contiguous(), ctx.n_total),
+                None, None, None)
 
 
 def find_latest_checkpoint(checkpoint_dir: Path):

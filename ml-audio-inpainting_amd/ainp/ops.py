@@ -1392,6 +1392,124 @@ def channel_sum(m):
     return out
 
 
+# ============================================================ generator backward
+# (csrc/gan_bwd.hip; the opt-in fix_generator_grad path of ainp.gan)
+def affine_leaky_out(y, scale, shift, slope=0.2):
+    """LeakyReLU(y * scale[c] + shift[c]) into a new tensor (y kept)."""
+    _req(y, "y")
+    out = torch.empty_like(y)
+    _T.affine_leaky_out(y, scale, shift, float(slope), out)
+    return out
+
+
+def pconv_src_materialize(src0, src1, Hin, Win):
+    """cat(nearest(x0) * m0, x1 * m1) [N, C0+C1, Hin, Win]: the input a
+    PartialConv2d convolves (src = (x, mask plane or None))."""
+    x0, m0 = src0
+    _req(x0, "x0")
+    x1, m1 = src1 if src1 is not None else (None, None)
+    C1 = x1.shape[1] if x1 is not None else 0
+    out = torch.empty(x0.shape[0], x0.shape[1] + C1, int(Hin), int(Win), device=x0.device)
+    _T.pconv_src_materialize(x0, m0, x1, m1, int(Hin), int(Win), out)
+    return out
+
+
+def pconv_src_grad(dxin, c_off, ms, dxs, accumulate):
+    """dxs (+)= ms * block-sum of dxin[:, c_off:c_off+C] (the gradient of one
+    PartialConv2d source from that of the materialised input)."""
+    _req(dxin, "dxin"); _req(dxs, "dxs")
+    _T.pconv_src_grad(dxin, int(c_off), ms, bool(accumulate), dxs)
+    return dxs
+
+
+def gen_act_bwd(g, a, act, slope, ratio, H, W, ldo, want_gz=True):
+    """(gz [N,C,H*W] = g * act'(a) on the conv grid, gc [N,C,ldo] = gz * ratio)."""
+    _req(g, "g")
+    N, C = g.shape[:2]
+    gz = torch.empty(N, C, H * W, device=g.device) if want_gz else None
+    gc = torch.empty(N, C, int(ldo), device=g.device)
+    _T.gen_act_bwd(g, a, int(act), float(slope), ratio, int(H), int(W), int(ldo), gz, gc)
+    return gz, gc
+
+
+def bn_act_bwd_reduce(ga, y, scale, shift, save, slope=0.2, count=None):
+    """[sum g' | sum g' xhat] (f64; + the element count when `count` is given,
+    for a SyncBN all-reduce, see bn_stats_reduce)."""
+    _req(ga, "ga"); _req(y, "y")
+    N, C = y.shape[:2]
+    P = y.shape[2] * y.shape[3]
+    ws = torch.empty(-(-int(_lib.lib.ainp_bn_act_bwd_workspace(N, C, P)) // 8),
+                     device=y.device, dtype=torch.float64)
+    sums = torch.empty(2 * C + (1 if count is not None else 0), device=y.device,
+                       dtype=torch.float64)
+    _T.bn_act_bwd_reduce(ga, y, scale, shift, save, float(slope), ws, sums)
+    if count is not None:
+        sums[2 * C:].fill_(float(count))
+    return sums
+
+
+def bn_act_bwd_apply(ga, y, scale, shift, save, gamma, sums, count, slope, ratio, ldo):
+    """(gc [N, C, ldo] = BN(+LeakyReLU) data gradient x ratio, dgamma, dbeta)."""
+    N, C = y.shape[:2]
+    gc = torch.empty(N, C, int(ldo), device=y.device)
+    dgamma = torch.empty(C, device=y.device) if gamma is not None else None
+    dbeta = torch.empty(C, device=y.device)
+    _T.bn_act_bwd_apply(ga, y, scale, shift, save, gamma, sums, int(count), float(slope), ratio,
+                        int(ldo), gc, dgamma, dbeta)
+    return gc, dgamma, dbeta
+
+
+def maxpool2_bwd(g, x):
+    _req(g, "g"); _req(x, "x")
+    gx = torch.empty_like(x)
+    _T.maxpool2_bwd(g, x, gx)
+    return gx
+
+
+def vgg_prep_bwd(g, x, tables, S=224):
+    """Gradient of vgg_prep(x, generated=True) w.r.t. x [N,1,H,W]."""
+    _req(g, "g"); _req(x, "x")
+    N, _, H, W = x.shape
+    ry0, rn, rw, cx0, cn, cw = tables
+    ws = torch.empty(-(-int(_lib.lib.ainp_vgg_prep_bwd_workspace(N, W, S)) // 4),
+                     device=x.device)
+    gx = torch.empty_like(x)
+    _T.vgg_prep_bwd(g, x, ry0, rn, rw, cx0, cn, cw, int(S), ws, gx)
+    return gx
+
+
+def absdiff_grad(a, b, gscale=None, scale=1.0, out=None, accumulate=False):
+    """nn.L1Loss backward: out (+)= gscale * scale * sign(a - b)."""
+    _req(a, "a"); _req(b, "b")
+    if out is None:
+        out = torch.empty_like(a)
+        accumulate = False
+    _T.absdiff_grad(a, b, gscale, float(scale), bool(accumulate), out)
+    return out
+
+
+def gram_sign_sym(Ga, Gb, gscale=None, scale=1.0):
+    out = torch.empty_like(Ga)
+    _T.gram_sign_sym(Ga, Gb, gscale, float(scale), out)
+    return out
+
+
+def gan_recon_bwd(g, o, m, sums5, gout3, n_total):
+    """d(Lv, Lh, Lw) . gout3 / d generated (ainp_gan_recon_bwd)."""
+    out = torch.empty_like(g)
+    _T.gan_recon_bwd(g, o, m, sums5, gout3, float(n_total), out)
+    return out
+
+
+def conv_weight_flip_t(w):
+    """w [Cout, Cin, K, K] -> [Cin, Cout, K, K] spatially flipped."""
+    _req(w, "w")
+    Cout, Cin, K, _ = w.shape
+    out = torch.empty(Cin, Cout, K, K, device=w.device)
+    _T.conv_weight_flip_t(w, out)
+    return out
+
+
 # ============================================================ ISTFT / Griffin-Lim
 IST_C64, IST_C128, IST_MAG_ANGLES, IST_MAG_PHASE = 0, 1, 2, 3
 

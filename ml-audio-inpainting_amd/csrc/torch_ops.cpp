@@ -1163,6 +1163,188 @@ void dgrad16(const Tensor& gT, const Tensor& wd, int64_t Cin, int64_t H, int64_t
                    dev(out, "out"), (int)nsplit, N * Cin * H * W, stream_of(gT)),
       "dgrad16");
 }
+// ---------------------------------------------------------------- generator backward
+// (csrc/gan_bwd.hip; opt-in fix_generator_grad)
+void affine_leaky_out(const Tensor& y, const Tensor& scale, const Tensor& shift, double slope,
+                      const Tensor& out) {
+  GUARD(y);
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
+  const int64_t N = y.size(0), C = y.size(1), HW = y.size(2) * y.size(3);
+  numel_is(scale, C, "scale");
+  numel_is(shift, C, "shift");
+  numel_is(out, y.numel(), "out");
+  chk(ainp_affine_leaky_out(dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"), N, (int)C, HW,
+                            (float)slope, dev(out, "out"), stream_of(y)),
+      "affine_leaky_out");
+}
+
+void pconv_src_materialize(const Tensor& x0, const OptT& m0, const OptT& x1, const OptT& m1,
+                           int64_t Hin, int64_t Win, const Tensor& out) {
+  GUARD(x0);
+  TORCH_CHECK(x0.dim() == 4, "x0 must be [N,C0,H0,W0]");
+  const int64_t N = x0.size(0), C0 = x0.size(1), H0 = x0.size(2), W0 = x0.size(3);
+  int64_t C1 = 0;
+  if (x1.has_value() && x1->defined()) {
+    TORCH_CHECK(x1->dim() == 4 && x1->size(0) == N && x1->size(2) == Hin && x1->size(3) == Win,
+                "x1 must be [N,C1,Hin,Win]");
+    C1 = x1->size(1);
+  }
+  if (m0.has_value() && m0->defined()) numel_is(*m0, N * H0 * W0, "m0");
+  if (m1.has_value() && m1->defined()) numel_is(*m1, N * Hin * Win, "m1");
+  numel_is(out, N * (C0 + C1) * Hin * Win, "out");
+  chk(ainp_pconv_src_materialize(dev(x0, "x0"), opt(m0, "m0"), N, (int)C0, (int)H0, (int)W0,
+                                 opt(x1, "x1"), opt(m1, "m1"), (int)C1, (int)Hin, (int)Win,
+                                 dev(out, "out"), stream_of(x0)),
+      "pconv_src_materialize");
+}
+
+void pconv_src_grad(const Tensor& dxin, int64_t c_off, const OptT& ms, bool accumulate,
+                    const Tensor& dxs) {
+  GUARD(dxin);
+  TORCH_CHECK(dxin.dim() == 4 && dxs.dim() == 4, "dxin / dxs must be 4-d");
+  const int64_t N = dxin.size(0), Cin = dxin.size(1), Hin = dxin.size(2), Win = dxin.size(3);
+  const int64_t C = dxs.size(1), Hs = dxs.size(2), Ws = dxs.size(3);
+  TORCH_CHECK(dxs.size(0) == N && c_off >= 0 && c_off + C <= Cin, "pconv_src_grad: channels");
+  if (ms.has_value() && ms->defined()) numel_is(*ms, N * Hs * Ws, "ms");
+  chk(ainp_pconv_src_grad(dev(dxin, "dxin"), N, (int)Cin, (int)Hin, (int)Win, (int)c_off, (int)C,
+                          (int)Hs, (int)Ws, opt(ms, "ms"), dev(dxs, "dxs"), accumulate ? 1 : 0,
+                          stream_of(dxin)),
+      "pconv_src_grad");
+}
+
+void gen_act_bwd(const Tensor& g, const OptT& a, int64_t act, double slope, const OptT& ratio,
+                 int64_t H, int64_t W, int64_t ldo, const OptT& gz, const Tensor& gc) {
+  GUARD(g);
+  TORCH_CHECK(g.dim() == 4, "g must be [N,C,gH,gW]");
+  const int64_t N = g.size(0), C = g.size(1), gH = g.size(2), gW = g.size(3);
+  if (a.has_value() && a->defined()) numel_is(*a, g.numel(), "a");
+  if (ratio.has_value() && ratio->defined()) numel_is(*ratio, N * H * W, "ratio");
+  if (gz.has_value() && gz->defined()) numel_is(*gz, N * C * H * W, "gz");
+  numel_is(gc, N * C * ldo, "gc");
+  chk(ainp_gen_act_bwd(dev(g, "g"), (int)gH, (int)gW, opt(a, "a"), (int)act, (float)slope,
+                       opt(ratio, "ratio"), N, (int)C, (int)H, (int)W, ldo, opt(gz, "gz"),
+                       dev(gc, "gc"), stream_of(g)),
+      "gen_act_bwd");
+}
+
+void bn_act_bwd_reduce(const Tensor& ga, const Tensor& y, const Tensor& scale,
+                       const Tensor& shift, const Tensor& save, double slope,
+                       const Tensor& workspace, const Tensor& sums) {
+  GUARD(ga);
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
+  const int64_t N = y.size(0), C = y.size(1), P = y.size(2) * y.size(3);
+  numel_is(ga, y.numel(), "ga");
+  numel_is(save, 2 * C, "save");
+  TORCH_CHECK(sums.numel() >= 2 * C, "sums");
+  TORCH_CHECK(workspace.numel() * workspace.element_size() >=
+                  (int64_t)ainp_bn_act_bwd_workspace(N, (int)C, P), "workspace too small");
+  chk(ainp_bn_act_bwd_reduce(dev(ga, "ga"), dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"),
+                             dev(save, "save"), (float)slope, N, (int)C, P, workspace.data_ptr(),
+                             dev<double>(sums, "sums", at::kDouble), stream_of(ga)),
+      "bn_act_bwd_reduce");
+}
+
+void bn_act_bwd_apply(const Tensor& ga, const Tensor& y, const Tensor& scale, const Tensor& shift,
+                      const Tensor& save, const OptT& gamma, const Tensor& sums, int64_t count,
+                      double slope, const OptT& ratio, int64_t ldo, const Tensor& gc,
+                      const OptT& dgamma, const OptT& dbeta) {
+  GUARD(ga);
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
+  const int64_t N = y.size(0), C = y.size(1), P = y.size(2) * y.size(3);
+  numel_is(ga, y.numel(), "ga");
+  numel_is(save, 2 * C, "save");
+  TORCH_CHECK(sums.numel() >= 2 * C + (count == 0 ? 1 : 0), "sums");
+  if (ratio.has_value() && ratio->defined()) numel_is(*ratio, N * P, "ratio");
+  numel_is(gc, N * C * ldo, "gc");
+  chk(ainp_bn_act_bwd_apply(dev(ga, "ga"), dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"),
+                            dev(save, "save"), opt(gamma, "gamma"),
+                            dev<double>(sums, "sums", at::kDouble), count, (float)slope,
+                            opt(ratio, "ratio"), N, (int)C, P, ldo, dev(gc, "gc"),
+                            opt(dgamma, "dgamma"), opt(dbeta, "dbeta"), stream_of(ga)),
+      "bn_act_bwd_apply");
+}
+
+void maxpool2_bwd(const Tensor& g, const Tensor& x, const Tensor& gx) {
+  GUARD(g);
+  TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
+  const int64_t NC = x.size(0) * x.size(1), H = x.size(2), W = x.size(3);
+  numel_is(g, NC * (H / 2) * (W / 2), "g");
+  numel_is(gx, x.numel(), "gx");
+  chk(ainp_maxpool2_bwd(dev(g, "g"), dev(x, "x"), NC, (int)H, (int)W, dev(gx, "gx"),
+                        stream_of(g)),
+      "maxpool2_bwd");
+}
+
+void vgg_prep_bwd(const Tensor& g, const Tensor& x, const Tensor& ry0, const Tensor& rn,
+                  const Tensor& rw, const Tensor& cx0, const Tensor& cn, const Tensor& cw,
+                  int64_t S, const Tensor& workspace, const Tensor& gx) {
+  GUARD(g);
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 1, "x must be [N,1,H,W]");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  numel_is(g, N * 3 * S * S, "g");
+  numel_is(gx, x.numel(), "gx");
+  TORCH_CHECK(rw.dim() == 2 && cw.dim() == 2 && rw.size(0) == S && cw.size(0) == S,
+              "vgg_prep_bwd: weight tables [S, taps]");
+  numel_is(ry0, S, "ry0");
+  numel_is(rn, S, "rn");
+  numel_is(cx0, S, "cx0");
+  numel_is(cn, S, "cn");
+  TORCH_CHECK(workspace.numel() * workspace.element_size() >=
+                  (int64_t)ainp_vgg_prep_bwd_workspace(N, (int)W, (int)S), "workspace too small");
+  chk(ainp_vgg_prep_bwd(dev(g, "g"), dev(x, "x"), N, (int)H, (int)W,
+                        dev<int32_t>(ry0, "ry0", at::kInt), dev<int32_t>(rn, "rn", at::kInt),
+                        dev(rw, "rw"), (int)rw.size(1), dev<int32_t>(cx0, "cx0", at::kInt),
+                        dev<int32_t>(cn, "cn", at::kInt), dev(cw, "cw"), (int)cw.size(1), (int)S,
+                        workspace.data_ptr(), dev(gx, "gx"), stream_of(g)),
+      "vgg_prep_bwd");
+}
+
+void absdiff_grad(const Tensor& a, const Tensor& b, const OptT& gscale, double scale,
+                  bool accumulate, const Tensor& out) {
+  GUARD(a);
+  numel_is(b, a.numel(), "b");
+  numel_is(out, a.numel(), "out");
+  if (gscale.has_value() && gscale->defined()) numel_is(*gscale, 1, "gscale");
+  chk(ainp_absdiff_grad(dev(a, "a"), dev(b, "b"), a.numel(), opt(gscale, "gscale"), (float)scale,
+                        dev(out, "out"), accumulate ? 1 : 0, stream_of(a)),
+      "absdiff_grad");
+}
+
+void gram_sign_sym(const Tensor& Ga, const Tensor& Gb, const OptT& gscale, double scale,
+                   const Tensor& out) {
+  GUARD(Ga);
+  TORCH_CHECK(Ga.dim() == 3 && Ga.size(1) == Ga.size(2), "Ga must be [B,C,C]");
+  numel_is(Gb, Ga.numel(), "Gb");
+  numel_is(out, Ga.numel(), "out");
+  if (gscale.has_value() && gscale->defined()) numel_is(*gscale, 1, "gscale");
+  chk(ainp_gram_sign_sym(dev(Ga, "Ga"), dev(Gb, "Gb"), Ga.size(0), (int)Ga.size(1),
+                         opt(gscale, "gscale"), (float)scale, dev(out, "out"), stream_of(Ga)),
+      "gram_sign_sym");
+}
+
+void gan_recon_bwd(const Tensor& g, const Tensor& o, const Tensor& m, const Tensor& sums5,
+                   const Tensor& gout3, double n_total, const Tensor& out) {
+  GUARD(g);
+  numel_is(o, g.numel(), "original");
+  numel_is(m, g.numel(), "mask");
+  numel_is(sums5, 5, "sums5");
+  numel_is(gout3, 3, "gout3");
+  numel_is(out, g.numel(), "out");
+  chk(ainp_gan_recon_bwd(dev(g, "generated"), dev(o, "original"), dev(m, "mask"), g.numel(),
+                         dev<double>(sums5, "sums5", at::kDouble), dev(gout3, "gout3"), n_total,
+                         dev(out, "out"), stream_of(g)),
+      "gan_recon_bwd");
+}
+
+void conv_weight_flip_t(const Tensor& w, const Tensor& out) {
+  GUARD(w);
+  TORCH_CHECK(w.dim() == 4 && w.size(2) == w.size(3), "w must be [Cout,Cin,K,K]");
+  numel_is(out, w.numel(), "out");
+  chk(ainp_conv_weight_flip_t(dev(w, "w"), (int)w.size(0), (int)w.size(1), (int)w.size(2),
+                              dev(out, "out"), stream_of(w)),
+      "conv_weight_flip_t");
+}
+
 }  // namespace
 
 TORCH_LIBRARY(ainp, m) {
@@ -1270,6 +1452,26 @@ TORCH_LIBRARY(ainp, m) {
   m.def("dgrad16_weight(Tensor w, int stride, int pad, Tensor(a!) wd) -> ()");
   m.def("dgrad16(Tensor gT, Tensor wd, int Cin, int H, int W, int k, int stride, int pad, "
         "Tensor? scale, Tensor(a!) out, int nsplit) -> ()");
+  m.def("affine_leaky_out(Tensor y, Tensor scale, Tensor shift, float slope, Tensor(a!) out) -> ()");
+  m.def("pconv_src_materialize(Tensor x0, Tensor? m0, Tensor? x1, Tensor? m1, int Hin, int Win, "
+        "Tensor(a!) out) -> ()");
+  m.def("pconv_src_grad(Tensor dxin, int c_off, Tensor? ms, bool accumulate, Tensor(a!) dxs) -> ()");
+  m.def("gen_act_bwd(Tensor g, Tensor? a, int act, float slope, Tensor? ratio, int H, int W, "
+        "int ldo, Tensor(a!)? gz, Tensor(b!) gc) -> ()");
+  m.def("bn_act_bwd_reduce(Tensor ga, Tensor y, Tensor scale, Tensor shift, Tensor save, "
+        "float slope, Tensor(a!) workspace, Tensor(b!) sums) -> ()");
+  m.def("bn_act_bwd_apply(Tensor ga, Tensor y, Tensor scale, Tensor shift, Tensor save, "
+        "Tensor? gamma, Tensor sums, int count, float slope, Tensor? ratio, int ldo, "
+        "Tensor(a!) gc, Tensor(b!)? dgamma, Tensor(c!)? dbeta) -> ()");
+  m.def("maxpool2_bwd(Tensor g, Tensor x, Tensor(a!) gx) -> ()");
+  m.def("vgg_prep_bwd(Tensor g, Tensor x, Tensor ry0, Tensor rn, Tensor rw, Tensor cx0, Tensor cn, "
+        "Tensor cw, int S, Tensor(a!) workspace, Tensor(b!) gx) -> ()");
+  m.def("absdiff_grad(Tensor a, Tensor b, Tensor? gscale, float scale, bool accumulate, "
+        "Tensor(a!) out) -> ()");
+  m.def("gram_sign_sym(Tensor Ga, Tensor Gb, Tensor? gscale, float scale, Tensor(a!) out) -> ()");
+  m.def("gan_recon_bwd(Tensor g, Tensor o, Tensor m, Tensor sums5, Tensor gout3, float n_total, "
+        "Tensor(a!) out) -> ()");
+  m.def("conv_weight_flip_t(Tensor w, Tensor(a!) out) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
@@ -1334,6 +1536,18 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("im2col16", &im2col16);
   m.impl("dgrad16_weight", &dgrad16_weight);
   m.impl("dgrad16", &dgrad16);
+  m.impl("affine_leaky_out", &affine_leaky_out);
+  m.impl("pconv_src_materialize", &pconv_src_materialize);
+  m.impl("pconv_src_grad", &pconv_src_grad);
+  m.impl("gen_act_bwd", &gen_act_bwd);
+  m.impl("bn_act_bwd_reduce", &bn_act_bwd_reduce);
+  m.impl("bn_act_bwd_apply", &bn_act_bwd_apply);
+  m.impl("maxpool2_bwd", &maxpool2_bwd);
+  m.impl("vgg_prep_bwd", &vgg_prep_bwd);
+  m.impl("absdiff_grad", &absdiff_grad);
+  m.impl("gram_sign_sym", &gram_sign_sym);
+  m.impl("gan_recon_bwd", &gan_recon_bwd);
+  m.impl("conv_weight_flip_t", &conv_weight_flip_t);
 }
 
 // The ops write through raw device pointers like the C ABI; autograd is the
@@ -1401,4 +1615,16 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("im2col16", torch::CppFunction::makeFallthrough());
   m.impl("dgrad16_weight", torch::CppFunction::makeFallthrough());
   m.impl("dgrad16", torch::CppFunction::makeFallthrough());
+  m.impl("affine_leaky_out", torch::CppFunction::makeFallthrough());
+  m.impl("pconv_src_materialize", torch::CppFunction::makeFallthrough());
+  m.impl("pconv_src_grad", torch::CppFunction::makeFallthrough());
+  m.impl("gen_act_bwd", torch::CppFunction::makeFallthrough());
+  m.impl("bn_act_bwd_reduce", torch::CppFunction::makeFallthrough());
+  m.impl("bn_act_bwd_apply", torch::CppFunction::makeFallthrough());
+  m.impl("maxpool2_bwd", torch::CppFunction::makeFallthrough());
+  m.impl("vgg_prep_bwd", torch::CppFunction::makeFallthrough());
+  m.impl("absdiff_grad", torch::CppFunction::makeFallthrough());
+  m.impl("gram_sign_sym", torch::CppFunction::makeFallthrough());
+  m.impl("gan_recon_bwd", torch::CppFunction::makeFallthrough());
+  m.impl("conv_weight_flip_t", torch::CppFunction::makeFallthrough());
 }

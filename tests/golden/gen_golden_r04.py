@@ -31,6 +31,19 @@ data is written:
       ("emu64/").  |emu32 - emu64| is the emulation's own accumulation-order
       floor: rounding points are discontinuous, so two exact restatements
       that sum in different orders round a few operands differently.
+
+  gan_gstep_small.npz
+      One GAN step with the generator trained (SURVEY §7 fix_generator_grad:
+      models/GAN/train.py:341-378 without the torch.no_grad() around G): the
+      reference's reduced-channel PConvUNet and Discriminator (the gan_small
+      configuration of gen_golden_gan.py, seeds 2 / 3) on x, mask
+      [2,1,129,100]; D step on generated.detach(), then the G step: D(gen),
+      calculate_losses through the oracle restatement (oracle/gan_ref.
+      generator_losses, VGG19 with seeded weights vgg19_init(0): loss.py
+      imports torchvision, absent here), g_total.backward(), Adam(2e-4,
+      (0.5, 0.999)) on G.  Stored: initial G / D state dicts, inputs, the
+      generated output, every G gradient, G's state after its Adam step, the
+      G-step losses.
 """
 from __future__ import annotations
 
@@ -188,9 +201,62 @@ def gen_bf16emu(mod):
     np.savez_compressed(os.path.join(HERE, "cnnblstm_c2_bf16emu.npz"), **out)
 
 
+def gen_gstep_small(net):
+    from golden.gen_golden_gan import SMALL_D, SMALL_DEC, SMALL_ENC, SMALL_FINAL, spec_inputs
+    from oracle import gan_ref
+    out = {}
+    torch.manual_seed(2)
+    G = net.PConvUNet(enc_layer_cfg=SMALL_ENC, dec_layer_cfg=SMALL_DEC, final_dec_cfg=SMALL_FINAL)
+    torch.manual_seed(3)
+    D = net.Discriminator(layer_cfg=SMALL_D)
+    G.train(); D.train()
+    for k, v in G.state_dict().items():
+        out["g_init/" + k] = v.detach().clone().numpy()
+    for k, v in D.state_dict().items():
+        out["d_init/" + k] = v.detach().clone().numpy()
+    x, m = spec_inputs(2, 129, 100, seed=500)
+    imp = x * m
+    out["orig"], out["imp"], out["mask"] = x, imp, m
+    O, I, M = (torch.from_numpy(a) for a in (x, imp, m))
+    bce = torch.nn.BCEWithLogitsLoss()
+    d_opt = torch.optim.Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    g_opt = torch.optim.Adam(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
+    d_opt.zero_grad()
+    gen = G(I, M)                                # autograd on: the fixed loop
+    dr = D(O)
+    l_real = bce(dr, torch.ones_like(dr))
+    df = D(gen.detach())
+    l_fake = bce(df, torch.zeros_like(df))
+    d_loss = (l_real + l_fake) / 2
+    d_loss.backward()
+    d_opt.step()
+    g_opt.zero_grad()
+    dfg = D(gen)
+    pv = gan_ref.vgg19_init(0)
+    L = gan_ref.generator_losses(gen, O, M, dfg, pv)
+    L["g_total"].backward()
+    out["gen"] = gen.detach().numpy()
+    out["d_loss"] = np.array([d_loss.item()])
+    for k, v in L.items():
+        out["loss/" + k] = np.array([float(v.detach())])
+    for k, p in G.named_parameters():
+        if p.requires_grad:
+            assert p.grad is not None, k
+            out["g_grad/" + k] = p.grad.detach().clone().numpy()
+    g_opt.step()
+    for k, v in G.state_dict().items():
+        out["g_after/" + k] = v.detach().clone().numpy()
+    np.savez_compressed(os.path.join(HERE, "gan_gstep_small.npz"), **out)
+    for k in sorted(x for x in out if x.startswith("g_grad/")):
+        print(k, out[k].shape, float(np.linalg.norm(out[k])))
+    print({k: float(out[k][0]) for k in out if k.startswith("loss/")})
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["bf16emu"]
     torch.set_num_threads(os.cpu_count() or 1)
     if "bf16emu" in what:
         gen_bf16emu(_load("models/CNNBLSTM/model.py", "ref_cnnblstm_model"))
+    if "gstep" in what:
+        gen_gstep_small(_load("models/GAN/networks.py", "ref_gan_networks"))
     print("written:", what)

@@ -64,6 +64,13 @@ def test_bad_arguments_fail_without_launching():
     assert b"bad argument" in _lib.lib.ainp_last_error()
     rc = _lib.lib.ainp_lstm_rec_fwd(None, None, None, None, None, 1, 1, 128, None)
     assert rc == -1
+    # generator backward (csrc/gan_bwd.hip): shapes checked before any launch
+    rc = _lib.lib.ainp_pconv_src_grad(None, 1, 4, 8, 8, 0, 2, 3, 3, None, None, 0, None)
+    assert rc == -1 and b"pconv_src_grad" in _lib.lib.ainp_last_error()
+    rc = _lib.lib.ainp_gen_act_bwd(None, 4, 4, None, 2, 0.2, None, 1, 1, 4, 4, 16, None, None,
+                                   None)
+    assert rc == -1 and b"gen_act_bwd" in _lib.lib.ainp_last_error()
+    assert _lib.lib.ainp_bn_act_bwd_workspace(2, 64, 10000) == 2 * 64 * 3 * 16
 
 
 def test_ops_refuse_cpu_tensors():

@@ -700,3 +700,183 @@ def test_affine_act_nhwc16_equals_affine_then_convert(N, C, H, W, masked):
     torch.cuda.synchronize()
     assert torch.equal(ya, yb)
     assert torch.equal(ref16.view(torch.int16), out16.view(torch.int16))
+
+
+# ------------------------------------------------------------- generator backward
+# (opt-in fix_generator_grad; csrc/gan_bwd.hip + ainp.gan._PConvUNetFn,
+# _VGGLossFn, _ReconFn)
+def test_gen_bwd_kernels_match_torch_autograd():
+    """The generator-backward building blocks against torch autograd (fp64 CPU):
+    PartialConv2d source materialisation and its gradient (nearest x2 upsample
+    + masks), BatchNorm2d(train) + LeakyReLU backward x window ratio, Tanh +
+    crop backward, MaxPool2d backward, the Gram / L1 sign gradients and the
+    reconstruction-loss gradient."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(42)
+    N, C0, C1, Hs, Ws = 2, 3, 2, 5, 7
+    x0 = torch.randn(N, C0, Hs, Ws, generator=g, dtype=torch.float64, requires_grad=True)
+    m0 = (torch.rand(N, Hs, Ws, generator=g) > 0.3).double()
+    x1 = torch.randn(N, C1, 2 * Hs, 2 * Ws, generator=g, dtype=torch.float64, requires_grad=True)
+    m1 = (torch.rand(N, 2 * Hs, 2 * Ws, generator=g) > 0.3).double()
+    up = F.interpolate(x0 * m0.unsqueeze(1), scale_factor=2, mode="nearest")
+    ref = torch.cat([up, x1 * m1.unsqueeze(1)], 1)
+    d = lambda t: t.detach().float().contiguous().cuda()  # noqa: E731
+    xin = ops.pconv_src_materialize((d(x0), d(m0)), (d(x1), d(m1)), 2 * Hs, 2 * Ws)
+    assert rel(xin, ref) < 1e-7
+    gout = torch.randn(ref.shape, generator=g, dtype=torch.float64)
+    ref.backward(gout)
+    dx0 = torch.full((N, C0, Hs, Ws), 0.5, device="cuda")
+    ops.pconv_src_grad(d(gout), 0, d(m0), dx0, True)
+    dx1 = torch.empty(N, C1, 2 * Hs, 2 * Ws, device="cuda")
+    ops.pconv_src_grad(d(gout), C0, d(m1), dx1, False)
+    assert rel(dx0 - 0.5, x0.grad) < 1e-6 and rel(dx1, x1.grad) < 1e-6
+
+    # BatchNorm2d (train) + LeakyReLU(0.2) backward, times a window ratio
+    C, H, W = 4, 6, 9
+    y = torch.randn(N, C, H, W, generator=g, dtype=torch.float64, requires_grad=True)
+    gam = torch.rand(C, generator=g, dtype=torch.float64) + 0.5
+    bet = torch.randn(C, generator=g, dtype=torch.float64) * 0.1
+    gam.requires_grad_(True); bet.requires_grad_(True)
+    a = F.leaky_relu(F.batch_norm(y, None, None, gam, bet, True, 0.1, 1e-5), 0.2)
+    ga = torch.randn(a.shape, generator=g, dtype=torch.float64)
+    a.backward(ga)
+    mean = y.detach().mean((0, 2, 3))
+    rstd = 1.0 / torch.sqrt(y.detach().var((0, 2, 3), unbiased=False) + 1e-5)
+    sc, sh = gam.detach() * rstd, bet.detach() - mean * gam.detach() * rstd
+    save = torch.cat([mean, rstd])
+    ratio = torch.rand(N, H, W, generator=g, dtype=torch.float64) * 3
+    sums = ops.bn_act_bwd_reduce(d(ga), d(y), d(sc), d(sh), d(save), 0.2)
+    ld = H * W + 2
+    gc, dg_, db_ = ops.bn_act_bwd_apply(d(ga), d(y), d(sc), d(sh), d(save), d(gam), sums,
+                                        N * H * W, 0.2, d(ratio), ld)
+    want = (y.grad * ratio.unsqueeze(1)).reshape(N, C, H * W)
+    assert rel(gc[:, :, :H * W], want) < 1e-5 and float(gc[:, :, H * W:].abs().max()) == 0.0
+    assert rel(dg_, gam.grad) < 1e-5 and rel(db_, bet.grad) < 1e-5
+
+    # Tanh + crop backward on the padded grid
+    z = torch.randn(N, 1, H, W, generator=g, dtype=torch.float64, requires_grad=True)
+    o = torch.tanh(z)[:, :, :H - 2, :W - 3]
+    go = torch.randn(o.shape, generator=g, dtype=torch.float64)
+    o.backward(go)
+    gz, gc = ops.gen_act_bwd(d(go), d(o), ops.ACT_TANH, 0.2, d(ratio), H, W, H * W)
+    assert rel(gz.view(N, 1, H, W), z.grad) < 1e-5
+    assert rel(gc.view(N, 1, H, W), z.grad * ratio.unsqueeze(1)) < 1e-5
+
+    # MaxPool2d(2, 2) backward (ties broken like torch CPU: first maximum)
+    xp = torch.randn(N, C, 8, 10, generator=g, dtype=torch.float64)
+    xp[0, 0, 0, :2] = 1.5                    # a tie inside one window
+    xp.requires_grad_(True)
+    yp = F.max_pool2d(xp, 2, 2)
+    gp = torch.randn(yp.shape, generator=g, dtype=torch.float64)
+    yp.backward(gp)
+    assert rel(ops.maxpool2_bwd(d(gp), d(xp)), xp.grad) < 1e-6
+
+    # L1 of Gram matrices: dF = (dG + dG^T) F / (c h w) and the L1 sign gradient
+    Fm = torch.randn(N, C, 5, 6, generator=g, dtype=torch.float64, requires_grad=True)
+    Ft = torch.randn(N, C, 5, 6, generator=g, dtype=torch.float64)
+    gram = lambda t: torch.bmm(t.reshape(N, C, -1), t.reshape(N, C, -1).transpose(1, 2)) / (C * 30)  # noqa: E731,E501
+    loss = torch.mean(torch.abs(gram(Fm) - gram(Ft))) * 3.0 + torch.mean(torch.abs(Fm - Ft))
+    loss.backward()
+    gs = torch.tensor([3.0], device="cuda")
+    sg = ops.gram_sign_sym(d(gram(Fm)), d(gram(Ft)), gs, 1.0 / (N * C * C))
+    dF = torch.empty(N, C, 5, 6, device="cuda")
+    ops.gemm(C, 30, C, [sg], C, 1, [d(Fm)], 30, 1, [dF], 30, 1, alpha=1.0 / (C * 30),
+             strideA=C * C, strideB=C * 30, strideC=C * 30, nstrided=N)
+    ops.absdiff_grad(d(Fm), d(Ft), None, 1.0 / Fm.numel(), out=dF, accumulate=True)
+    assert rel(dF, Fm.grad) < 1e-5
+
+    # reconstruction losses Lv / Lh / Lw (train.py:49-63)
+    gen = torch.tanh(torch.randn(N, 1, H, W, generator=g, dtype=torch.float64)).requires_grad_(True)
+    org = torch.rand(N, 1, H, W, generator=g, dtype=torch.float64)
+    msk = (torch.rand(N, 1, H, W, generator=g) > 0.4).double()
+    lv = torch.sum(torch.abs(gen * msk - org * msk)) / (msk.sum() + 1e-8)
+    lh = torch.sum(torch.abs(gen * (1 - msk) - org * (1 - msk))) / ((1 - msk).sum() + 1e-8)
+    lw = torch.mean(torch.abs(gen - org) * torch.abs(org))
+    (1.0 * lv + 2.0 * lh + 0.2 * lw).backward()
+    sums = ops.gan_recon_sums(d(gen), d(org), d(msk))
+    gr = ops.gan_recon_bwd(d(gen), d(org), d(msk), sums,
+                           torch.tensor([1.0, 2.0, 0.2], device="cuda"), gen.numel())
+    assert rel(gr, gen.grad) < 1e-6
+
+
+def test_vgg_loss_input_gradient_matches_oracle():
+    """d(lambda_p perceptual + lambda_s style) / d generated through VGG19
+    (seeded weights; loss.py:89-131 incl. the inplace-ReLU feature quirk) and
+    the input preparation, against torch autograd of the oracle restatement
+    in fp64 on the CPU."""
+    g = torch.Generator().manual_seed(9)
+    gen = torch.tanh(torch.randn(2, 1, 129, 100, generator=g))
+    tgt = torch.rand(2, 1, 129, 100, generator=g) * 3
+    v, pv = _vgg_pair(0)
+    gg = gen.cuda().requires_grad_(True)
+    perc, style = v(gg, tgt.cuda())
+    (4.0 * perc + 500.0 * style).backward()
+    p64 = {k: t.double() for k, t in pv.items()}
+    g64 = gen.double().requires_grad_(True)
+    rp, rs = R.vgg_losses(p64, g64, tgt.double())
+    (4.0 * rp + 500.0 * rs).backward()
+    assert abs(float(perc) - float(rp)) < 1e-4 * abs(float(rp))
+    assert abs(float(style) - float(rs)) < 1e-4 * abs(float(rs))
+    e = rel(gg.grad, g64.grad)
+    print("VGG input gradient rel err", e)
+    assert e < 1e-4
+
+
+@pytest.mark.timeout(600)
+def test_generator_training_step_matches_reference(golden_dir):
+    """fix_generator_grad: one GAN step with G trained, on the
+    reference's reduced-channel PConvUNet / Discriminator (gan_gstep_small.npz
+    from networks.py, losses through the oracle restatement with seeded VGG19):
+    the G-step losses, every G parameter gradient (PartialConv2d weights and
+    biases, BatchNorm gamma / beta) at the fp32 gate 1e-4, and G's parameters
+    and BatchNorm statistics after its Adam step.  The default loop keeps Q1
+    (G untouched), checked on the same fixture."""
+    from ainp import gan as G
+    from ainp.gan_train import GanTrainer
+    from golden.gen_golden_gan import SMALL_D, SMALL_DEC, SMALL_ENC, SMALL_FINAL
+    f = np.load(os.path.join(golden_dir, "gan_gstep_small.npz"), allow_pickle=False)
+
+    def make(fix):
+        Gm = G.PConvUNet(enc_layer_cfg=SMALL_ENC, dec_layer_cfg=SMALL_DEC,
+                         final_dec_cfg=SMALL_FINAL)
+        Gm.load_state_dict(_sd(f, "g_init/"))
+        Dm = G.Discriminator(layer_cfg=SMALL_D)
+        Dm.load_state_dict(_sd(f, "d_init/"))
+        v, _ = _vgg_pair(0)
+        cfg = {"training": dict(R.LAMBDAS, g_lr=2e-4, d_lr=2e-4, b1=0.5, b2=0.999,
+                                fix_generator_grad=fix)}
+        tr = GanTrainer(cfg, Gm.cuda(), Dm.cuda(), vgg=v)
+        assert tr.fix_g == fix
+        out = tr.step(*(torch.from_numpy(f[k]).cuda() for k in ("orig", "imp", "mask")))
+        return out, Gm
+    out, Gm = make(True)
+    assert rel(out["generated"], f["gen"]) < TOL
+    assert abs(float(out["d_loss"]) - f["d_loss"][0]) <= TOL * abs(f["d_loss"][0])
+    for k in ("g_total", "g_adv", "g_l1_valid", "g_l1_hole", "g_mag_weighted",
+              "g_vgg_perceptual", "g_vgg_style"):
+        r = float(f["loss/" + k][0])
+        assert abs(float(out[k]) - r) <= TOL * max(abs(r), 1e-6), (k, float(out[k]), r)
+    errs = {}
+    for k, p in Gm.named_parameters():
+        if not p.requires_grad:
+            continue
+        assert p.grad is not None, k
+        errs[k] = rel(p.grad, f["g_grad/" + k])
+    print("G grad rel errs", sorted(errs.items(), key=lambda kv: -kv[1])[:6])
+    assert len(errs) == sum(1 for k in f.files if k.startswith("g_grad/"))
+    for k, e in errs.items():
+        assert e < TOL, (k, e)
+    sd = Gm.state_dict()
+    for k in f.files:
+        if k.startswith("g_after/"):
+            name = k[len("g_after/"):]
+            if name.endswith("num_batches_tracked"):
+                assert int(sd[name]) == int(f[k])
+            else:
+                assert rel(sd[name], f[k]) < TOL, name
+    # default loop (fix_generator_grad off): G's parameters do not move (Q1)
+    _, G0 = make(False)
+    sd0 = G0.state_dict()
+    for k in f.files:
+        if k.startswith("g_init/") and "running" not in k and "num_batches" not in k:
+            assert np.array_equal(sd0[k[len("g_init/"):]].cpu().numpy(), f[k]), k
