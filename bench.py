@@ -382,6 +382,86 @@ def spawn_ranks(n):
     return rc
 
 
+# ------------------------------------------------------------- in-step kernels
+# Committed rocprofv3 kernel-stats tables of the step alone (tools/step_prof.py:
+# 3 warm-up + 10 timed steps, nothing else launched; per step = total / 13),
+# regenerated by tools/gpu_r04f.sh.  The bench reports the dominant in-step
+# kernels from them with their own roofline fractions (per-step algorithmic
+# work / per-step kernel time / peak), next to the live stand-alone launches.
+STEP_TABLES = {
+    ("cnnblstm", "fp32"): "profiles/r04_cnn_fp32_step_kernel_stats.csv",
+    ("cnnblstm", "bf16"): "profiles/r04_cnn_bf16_step_kernel_stats.csv",
+    ("gan", "bf16", 626): "profiles/r04_gan_c4_bf16_step_kernel_stats.csv",
+    ("gan", "bf16", 1001): "profiles/r04_gan_c5_bf16_step_kernel_stats.csv",
+}
+STEP_TABLE_DIV = 13
+
+
+def _cnn_step_work(B=32, F=257, T=334, H=128):
+    """(name substring, kind, per-step algorithmic work) of the CNNBLSTM step's
+    kernels at the C2 / C3 per-GPU shape: FLOP for MFMA kernels, HBM bytes
+    for the BatchNorm passes (every operand read / written once)."""
+    P = B * F * T                       # pixels per channel plane set
+    conv = lambda ci, co: 2.0 * 9 * ci * co * P          # noqa: E731
+    l0 = 2.0 * B * T * 8 * H * 64 * F                     # one layer-0 GEMM
+    bn_small = (16 + 32 + 32 + 16) * P                    # BN-ReLU elements of the 16/32-ch layers
+    big = 64 * P
+    return [
+        ("gemm_x6r_kernel", "mfma", 3 * l0),              # projection + backward pair
+        ("gemm_bf16nt_256_kernel", "mfma", l0),           # bf16 projection
+        ("g16::gemm_bf16nt_kernel", "mfma", 2 * l0),      # bf16 dX + dW
+        ("conv3x3_x6p_kernel<32, 64", "mfma", conv(32, 64)),
+        ("conv3x3_x6_kernel<64, 32", "mfma", conv(64, 32)),
+        ("conv3x3_wgrad_x6<64", "mfma", conv(32, 64)),
+        ("conv3x3_x6p_kernel<16, 32, false", "mfma", 2 * conv(16, 32)),
+        ("conv3x3_x6q_kernel<32, true", "mfma", 2 * conv(16, 32)),
+        ("conv3x3_wgrad_x6s<16, 32", "mfma", 2 * conv(16, 32)),
+        ("conv3x3_wgrad_x6s<32, 16", "mfma", conv(32, 16)),
+        ("conv3x3_x6q_kernel<32, false", "mfma", conv(32, 16)),
+        ("conv3x3_x6p_kernel<16, 32, true", "mfma", conv(32, 16)),
+        ("bn_relu_bwd_reduce_flat", "hbm", 8.0 * bn_small),
+        ("bn_relu_bwd_apply_flat", "hbm", 12.0 * bn_small),
+        ("bn_relu_bwd_apply_ntcf2", "hbm", 12.0 * big),
+        ("bn_relu_bwd_ntcf", "hbm", 8.0 * big),
+        ("bn_relu_apply_ntcf2", "hbm", 8.0 * big),
+        ("bn_relu_apply_ntcf_bf16", "hbm", 8.0 * big),
+    ]
+
+
+def in_step_table(key, bf16, top=8):
+    """Dominant in-step kernels of the committed step table for `key` (None
+    if absent): per-step ms, share of the step's kernel time, and for the
+    kernels with a known per-step work their roofline fraction."""
+    path = STEP_TABLES.get(key)
+    if not path or not os.path.exists(os.path.join(ROOT, path)):
+        return None
+    import csv
+    rows = list(csv.DictReader(open(os.path.join(ROOT, path))))
+    total = sum(float(r["TotalDurationNs"]) for r in rows)
+    work = _cnn_step_work() if key[0] == "cnnblstm" else []
+    out = []
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
+        ms = float(r["TotalDurationNs"]) / 1e6 / STEP_TABLE_DIV
+        e = {"kernel": r["Name"].split("(")[0][:120], "ms_per_step": round(ms, 4),
+             "launches_per_step": round(int(r["Calls"]) / STEP_TABLE_DIV, 2),
+             "share_of_kernel_time": round(float(r["TotalDurationNs"]) / total, 4)}
+        for sub, kind, amount in work:
+            if sub in r["Name"]:
+                if kind == "mfma":
+                    tf = amount / (ms / 1e3) / 1e12
+                    peak = executed_peak(bf16)
+                    e.update(bound="mfma", achieved_tflops=round(tf, 1), peak=round(peak, 1),
+                             frac=round(tf / peak, 4), flop_per_step=amount)
+                else:
+                    gbs = amount / (ms / 1e3) / 1e9
+                    e.update(bound="hbm", achieved_gbs=round(gbs, 1), peak=HBM_PEAK_GBS,
+                             frac=round(gbs / HBM_PEAK_GBS, 4), bytes_per_step=amount)
+                break
+        out.append(e)
+    return {"table": path, "per_step": f"rocprofv3 --kernel-trace --stats of tools/step_prof.py "
+                                       f"(totals / {STEP_TABLE_DIV})", "top": out}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -594,6 +674,7 @@ def main():
                 step_flops / world / (ms_step / 1e3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 4)}),
             "roofline": roof,
             "roofline_l0_bwd": roof_bwd,
+            "in_step_kernels": in_step_table(("cnnblstm", args.dtype), bf16),
             "roofline_stft": roof_stft,
             "dp": dp,
             "graph": graph,
@@ -638,6 +719,45 @@ def gan_cpu_baseline(T, S, g, steps=1):
                       f"{steps} timed step after 1 warmup; features precomputed"}
 
 
+def gan_roofline_operands(gen, imp, mask):
+    """Sources of the final PartialConv2d and of U-Net decoder block 3 as a G
+    forward launches them (ainp.gan.PConvUNet.capture), on the batch given."""
+    from ainp import gan as G
+    from ainp import ops
+    G.PConvUNet.capture = {"decoder": (3,)}
+    try:
+        with torch.no_grad(), ops.nhwc16_memo():
+            gen._forward(imp.unsqueeze(1), mask.unsqueeze(1))
+        cap = G.PConvUNet.capture
+    finally:
+        G.PConvUNet.capture = None
+    return cap["final"], cap["decoder3"]
+
+
+def gan_roofline_launch(mod, operands, bf16, stats=False):
+    """(launch, flop per launch, Hout, Wout) of one PartialConv2d conv (mod:
+    a PartialConv2d or an Encoder/DecoderBlock) on captured sources, with its
+    own window ratio; bf16 -> the channel-last kernel alone (operands converted
+    beforehand), fp32 -> the conv_gen call."""
+    from ainp import ops
+    pc = getattr(mod, "pconv", mod)
+    srcs, Hin, Win = operands
+    (x0, m0), (x1, m1) = srcs
+    N = x0.shape[0]
+    k, st, pd = pc.kernel_size, pc.stride, pc.padding
+    ratio, _ = ops.pconv_mask((m0, x0.shape[1]), (m1, x1.shape[1]), N, Hin, Win, k, st, pd)
+    w = pc.conv.weight
+    Cout, Cin = w.shape[:2]
+    kw = dict(src1=(x1, m1), Hin=Hin, Win=Win, stride=st, pad=pd, bias=pc.bias, ratio=ratio,
+              act=ops.ACT_NONE if stats else ops.ACT_LEAKY, want_stats=stats, bf16=bf16)
+    if bf16:
+        launch = ops.conv_gen((x0, m0), w, launcher=True, **kw)
+    else:
+        launch = lambda: ops.conv_gen((x0, m0), w, **kw)  # noqa: E731
+    Ho, Wo = ops.conv_out_size(Hin, k, st, pd), ops.conv_out_size(Win, k, st, pd)
+    return launch, 2.0 * Cout * Cin * k * k * N * Ho * Wo, Ho, Wo
+
+
 def run_gan(args):
     from ainp import ops
     from ainp import gan as G
@@ -676,7 +796,7 @@ def run_gan(args):
                                              mode=ops.FEAT_GAN, outputs=(True, True, c5, True))
         out = tr.step(o.unsqueeze(1), im.unsqueeze(1), m.unsqueeze(1))
         hole[i] = out["g_l1_hole"]
-        last.update(orig=o, phase=ph, mask=m, gen=out["generated"])
+        last.update(orig=o, imp=im, phase=ph, mask=m, gen=out["generated"])
 
     for i in range(args.warmup):
         step(i)
@@ -723,33 +843,25 @@ def run_gan(args):
                                    "update fused into its write-out)",
                  "batch": B, "samples_per_clip": hop * (T - 1)}
 
-    roof = None
+    roof = roof_wide = None
     if rank == 0:
-        # dominant kernel: the final PartialConv2d (65 -> 64, 3x3) at the padded
-        # 384 x 640 resolution, B examples: conv_gen generic path
-        Hp, Wp = 384, (1024 if c5 else 640)
-        x0 = torch.randn(B, 64, Hp // 2, Wp // 2, device=dev)
-        m0 = torch.ones(B, Hp // 2, Wp // 2, device=dev)
-        x1 = torch.randn(B, 1, Hp, Wp, device=dev)
-        m1 = torch.ones(B, Hp, Wp, device=dev)
-        w = torch.randn(64, 65, 3, 3, device=dev) * 0.05
-        ratio = torch.ones(B, Hp, Wp, device=dev)
-        bias = torch.zeros(64, device=dev)
-        out = torch.empty(B, 64, Hp, Wp, device=dev)
-        kw = dict(src1=(x1, m1), Hin=Hp, Win=Wp, stride=1, pad=1, bias=bias, ratio=ratio,
-                  act=ops.ACT_LEAKY, out=out, bf16=bf16)
-        if bf16:   # the channel-last kernel alone, operands converted beforehand
-            launch = ops.conv_gen((x0, m0), w, launcher=True, **kw)
-            kname = "conv_gen_nhwc16_kernel<64, true>"
-        else:
-            launch = lambda: ops.conv_gen((x0, m0), w, **kw)  # noqa: E731
-            kname = "conv_gen_x6_kernel<64,16>"
+        # the in-step launches of the two dominant conv kernels, on operands
+        # captured from a G forward over the last timed batch (real masks and
+        # window ratios): the final PartialConv2d (65 -> 64, 3x3) at the padded
+        # 384 x 640 / 1024 resolution, and the U-Net decoder block 768 -> 256 at
+        # 1/8 resolution (the wide-tile kernel's largest launch)
+        ops_fin, ops_wide = gan_roofline_operands(gen, last["imp"], last["mask"])
+        launch, flops, Hp, Wp = gan_roofline_launch(gen.final_decoder_layer[0], ops_fin, bf16)
         avg_s = time_kernel(launch, args.roofline_reps, dev)
-        flops = 2.0 * 64 * 65 * 9 * B * Hp * Wp
+        tsuf = "_c5" if c5 else ""
+        kname = "conv_gen_nhwc16_kernel<64, true>" if bf16 else "conv_gen_x6_kernel<64,16>"
         roof = _roof(flops, avg_s, bf16, f"{kname} (final PartialConv2d 65->64 3x3 at "
-                     f"{Hp}x{Wp}, B={B})",
-                     traffic=_traffic("traffic_conv_gen_final_bf16.json" if bf16
-                                      else "traffic_conv_gen_final.json"))
+                     f"{Hp}x{Wp}, B={B}, in-step operands)",
+                     traffic=_traffic(f"traffic_conv_gen_final_bf16{tsuf}.json" if bf16
+                                      else f"traffic_conv_gen_final{tsuf}.json"))
+        roof["operands"] = ("captured from a G forward over the last timed batch (real mask "
+                            "planes and window ratios; tools/roofline_probe_gan.py replays the "
+                            "first batch for the PMC passes)")
         if bf16:
             roof["main_loop"] = ("channel-last bf16 operands (x*mask folded in; the 1-channel "
                                  "skip source expanded per pixel, 9 -> 32 k-values), "
@@ -758,29 +870,16 @@ def run_gan(args):
         else:
             roof["main_loop"] = ("fp32 operands split exactly into 3 bf16 pieces, 6 cross "
                                  "products on v_mfma_f32_32x32x16_bf16, f32 accumulate")
-    roof_wide = None
-    if rank == 0 and bf16:
-        # the kernel with the most time in the bf16 step (profiles/r03_ganprof1_*):
-        # the wide-tile conv on its largest launch, the U-Net decoder block
-        # cat(up(512 ch), skip 256 ch) -> 256 at 1/8 resolution, with BN partials
-        Hd, Wd = Hp // 8, Wp // 8
-        xa = torch.randn(B, 512, Hd // 2, Wd // 2, device=dev)
-        ma = (torch.rand(B, Hd // 2, Wd // 2, device=dev) > 0.1).float()
-        xb = torch.randn(B, 256, Hd, Wd, device=dev)
-        mb = (torch.rand(B, Hd, Wd, device=dev) > 0.1).float()
-        wd = torch.randn(256, 768, 3, 3, device=dev) * 0.02
-        launch_w = ops.conv_gen((xa, ma), wd, src1=(xb, mb), Hin=Hd, Win=Wd, stride=1, pad=1,
-                                bias=torch.zeros(256, device=dev),
-                                ratio=torch.ones(B, Hd, Wd, device=dev), want_stats=True,
-                                bf16=True, launcher=True)
-        avg_w = time_kernel(launch_w, args.roofline_reps, dev)
-        roof_wide = _roof(2.0 * 256 * 768 * 9 * B * Hd * Wd, avg_w, True,
-                          f"conv_gen_nhwc16_wide_kernel<256, 8, false> (U-Net decoder block "
-                          f"768->256 3x3 at {Hd}x{Wd}, B={B}, BN partials)",
-                          traffic=(_traffic("traffic_conv_gen_wide_bf16.json")
-                                   if (not c5 and B == 8) else None))
-        roof_wide["main_loop"] = ("256x128 tiles, 8 waves of 64x64, 3-stage LDS-DMA ring "
-                                  "(global_load_lds_dwordx4), v_mfma_f32_32x32x16_bf16")
+        if bf16:
+            launch_w, flops_w, Hd, Wd = gan_roofline_launch(gen.decoder_blocks[3], ops_wide, True,
+                                                            stats=True)
+            avg_w = time_kernel(launch_w, args.roofline_reps, dev)
+            roof_wide = _roof(flops_w, avg_w, True,
+                              f"conv_gen_nhwc16_wide_kernel<256, 8, false> (U-Net decoder block "
+                              f"768->256 3x3 at {Hd}x{Wd}, B={B}, BN partials, in-step operands)",
+                              traffic=_traffic(f"traffic_conv_gen_wide_bf16{tsuf}.json"))
+            roof_wide["main_loop"] = ("256x128 tiles, 8 waves of 64x64, 3-stage LDS-DMA ring "
+                                      "(global_load_lds_dwordx4), v_mfma_f32_32x32x16_bf16")
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = gan_cpu_baseline(T, S, g)
@@ -809,6 +908,7 @@ def run_gan(args):
             "mfma_util_step": (round(step_flops / world / (ms_step / 1e3) / 1e12
                                      / executed_peak(bf16), 4) if step_flops else None),
             "roofline": roof, "roofline_wide": roof_wide, "reconstruction": recon,
+            "in_step_kernels": in_step_table(("gan", args.dtype, T), bf16),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

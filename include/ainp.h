@@ -682,8 +682,8 @@ int ainp_pconv_src_materialize(const float* x0, const float* m0, int64_t N, int 
 int ainp_pconv_src_grad(const float* dxin, int64_t N, int Cin, int Hin, int Win, int c_off, int C,
                         int Hs, int Ws, const float* ms, float* dxs, int accumulate,
                         void* stream);
-/* Activation (+crop) backward of a PartialConv2d output (act 0 none, 1 LeakyReLU,
- * 3 Tanh; a = the activation's output, [N, C, gH, gW]): gz [N, C, H*W] =
+/* Activation (+crop) backward of a PartialConv2d output (act 0 none, 1 ReLU,
+ * 2 LeakyReLU, 3 Tanh; a = the activation's output, [N, C, gH, gW]): gz [N, C, H*W] =
  * g * act'(a) (zero outside the gH x gW crop; may be NULL), gc [N, C, ldo] =
  * gz * ratio[n][pixel] (ratio may be NULL), rows zero-padded to ldo. */
 int ainp_gen_act_bwd(const float* g, int gH, int gW, const float* a, int act, float slope,
@@ -694,7 +694,8 @@ int ainp_gen_act_bwd(const float* g, int gH, int gW, const float* a, int act, fl
  * reduce -> sums[0:C] = sum g', sums[C:2C] = sum g' xhat (fixed order, f64;
  * all-reduce them for SyncBN); apply -> gc [N, C, ldo] = dy * ratio (the
  * PartialConv2d window ratio, may be NULL), dgamma, dbeta.  count == 0: the
- * element count is sums[2C] (ainp_bn_stats_reduce's DP form). */
+ * element count is sums[2C] (ainp_bn_stats_reduce's DP form); count == -1:
+ * eval mode (save = [running_mean | 1/sqrt(running_var + eps)]). */
 size_t ainp_bn_act_bwd_workspace(int64_t N, int C, int64_t P);
 int ainp_bn_act_bwd_reduce(const float* ga, const float* y, const float* scale, const float* shift,
                            const float* save, float slope, int64_t N, int C, int64_t P,

@@ -66,10 +66,14 @@ def _bn_affine(bn: nn.BatchNorm2d, stats, count, C, want_save=False):
         if bn.track_running_stats:
             bn.num_batches_tracked.add_(1)
         return (sc, sh, save) if want_save else (sc, sh)
+    sc, sh = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
     if want_save:
-        raise NotImplementedError("generator backward through an eval-mode BatchNorm2d "
-                                  "(the reference trains G in train mode)")
-    return ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
+        # eval mode under autograd: the running statistics are constants
+        # (ainp_bn_act_bwd_apply count = -1); [mean | rstd] for xhat
+        save = torch.cat([bn.running_mean.float(),
+                          torch.rsqrt(bn.running_var.float() + bn.eps)])
+        return sc, sh, save
+    return sc, sh
 
 
 # ------------------------------------------------------------ partial conv
@@ -283,6 +287,11 @@ class PConvUNet(nn.Module):
         with torch.no_grad(), ops.nhwc16_memo():
             return self._forward(x, mask)
 
+    # profiling hook: a dict set here collects the sources of the final
+    # PartialConv2d ("final") and of the decoder blocks listed under "decoder"
+    # during the next no-grad forward (bench.py's in-step roofline launches)
+    capture = None
+
     def _check_inputs(self, x, mask):
         if x.shape[1] != self.input_channels:
             raise ValueError(f"Input x channels ({x.shape[1]}) != expected ({self.input_channels})")
@@ -316,8 +325,11 @@ class PConvUNet(nn.Module):
                 sh = torch.zeros(C, device=y.device)
                 save = None
             a = ops.affine_leaky_out(y, sc, sh, SLOPE)
+            ev = isinstance(blk.norm, nn.BatchNorm2d) and not (
+                blk.norm.training or not blk.norm.track_running_stats)
             tape["blocks"].append({"blk": blk, "srcs": srcs, "Hin": Hin, "Win": Win, "y": y,
-                                   "ratio": ratio, "sc": sc, "sh": sh, "save": save, "a": a})
+                                   "ratio": ratio, "sc": sc, "sh": sh, "save": save, "a": a,
+                                   "eval": ev})
             return a, newm
 
         srcs = [(xp4, mp), (mp4, mp)]
@@ -375,11 +387,18 @@ class PConvUNet(nn.Module):
             if (2 * d.shape[2], 2 * d.shape[3]) != (Hs, Ws):
                 raise RuntimeError("decoder/skip size mismatch (cannot happen after padding to "
                                    "the total downsampling factor)")
+            cap = PConvUNet.capture
+            if cap is not None and i in cap.get("decoder", ()):
+                # profiling hook (bench.py's in-step roofline operands): this
+                # block's sources as the step launches them
+                cap[f"decoder{i}"] = ([(d, dm), (feats[j], masks[j])], Hs, Ws)
             d, dm = blk.run([(d, dm), (feats[j], masks[j])], Hs, Ws)
         if (2 * d.shape[2], 2 * d.shape[3]) != (Hp, Wp):
             raise RuntimeError(f"Size mismatch before final layer. Dec: {d.shape[2:]}, "
                                f"Skip: {(Hp, Wp)}")
         pc1, pc2 = self.final_decoder_layer[0], self.final_decoder_layer[2]
+        if PConvUNet.capture is not None:
+            PConvUNet.capture["final"] = ([(d, dm), (xp4, mp)], Hp, Wp)
         y1, m1, _ = pc1.run([(d, dm), (xp4, mp)], Hp, Wp, act=ops.ACT_LEAKY)
         # final PartialConv2d (Cout=1) + Tanh + crop to the input size in one launch
         out, _, _ = pc2.run([(y1, m1)], Hp, Wp, act=ops.ACT_TANH, crop=(H, W))
@@ -491,7 +510,10 @@ class _PConvUNetFn(torch.autograd.Function):
             if isinstance(blk.norm, nn.BatchNorm2d):
                 bn = blk.norm
                 comm = getattr(bn, "ainp_comm", None)
-                if comm is not None and comm.world_size > 1:
+                if rec["eval"]:
+                    sums = ops.bn_act_bwd_reduce(gab, y, rec["sc"], rec["sh"], rec["save"], SLOPE)
+                    cnt = -1
+                elif comm is not None and comm.world_size > 1:
                     sums = comm.allreduce_sum_(ops.bn_act_bwd_reduce(gab, y, rec["sc"], rec["sh"],
                                                                      rec["save"], SLOPE,
                                                                      count=Nn * Pb))

@@ -70,8 +70,9 @@ __global__ void pconv_src_grad_kernel(const float* __restrict__ dxin, int Cin, i
 }
 
 // ------------------------------------------------------------ activation (+crop) backward
-// act: 0 none, 1 LeakyReLU(slope) (derivative from the output's sign, as
-// torch's inplace LeakyReLU backward), 3 Tanh (1 - a^2).  g / a are
+// act (ainp's ACT_* codes): 0 none, 1 ReLU, 2 LeakyReLU(slope) (derivative
+// from the output's sign, as torch's inplace ReLU / LeakyReLU backward),
+// 3 Tanh (1 - a^2).  g / a are
 // [N, C, gH, gW] (the cropped output for the generator's last layer); the
 // result lives on the conv grid [N, C, H, W] (zero outside the crop):
 // gz = g * act'(a) and gc = gz * ratio[n][pixel] in rows of ldo.
@@ -95,6 +96,8 @@ __global__ void gen_act_bwd_kernel(const float* __restrict__ g, int gH, int gW,
     const int64_t i = row * gH * gW + (int64_t)y * gW + x;
     v = g[i];
     if (act == 1) {
+      v = a[i] > 0.f ? v : 0.f;
+    } else if (act == 2) {
       v = a[i] > 0.f ? v : v * slope;
     } else if (act == 3) {
       const float o = a[i];
@@ -181,7 +184,7 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(
     const float* __restrict__ ga, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ save,
     const float* __restrict__ gamma, const double* __restrict__ sums, double inv_count,
-    float slope, const float* __restrict__ ratio, int C, int64_t P, int64_t ldo,
+    int eval, float slope, const float* __restrict__ ratio, int C, int64_t P, int64_t ldo,
     int64_t total, float* __restrict__ gc, float* __restrict__ dgamma,
     float* __restrict__ dbeta) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -199,7 +202,9 @@ __global__ __launch_bounds__(256) void bn_act_bwd_apply_kernel(
   const int c = (int)(row % C);
   const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
   const float k = (gamma ? gamma[c] : 1.f) * rstd;
-  const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C];
+  // eval mode (running statistics): the statistics are constants, so the
+  // batch-mean terms vanish
+  const double ic = eval ? 0.0 : (inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C]);
   const float m1 = (float)(sums[c] * ic);
   const float m2 = (float)(sums[C + c] * ic);
   const float yv = y[row * P + p];
@@ -418,7 +423,7 @@ extern "C" int ainp_gen_act_bwd(const float* g, int gH, int gW, const float* a, 
                                 float slope, const float* ratio, int64_t N, int C, int H, int W,
                                 int64_t ldo, float* gz, float* gc, void* stream) {
   if (!g || !gc || N < 1 || C < 1 || gH < 1 || gW < 1 || gH > H || gW > W ||
-      ldo < (int64_t)H * W || !(act == 0 || act == 1 || act == 3) || (act && !a))
+      ldo < (int64_t)H * W || act < 0 || act > 3 || (act && !a))
     return record_msg("ainp_gen_act_bwd: bad argument");
   const int64_t total = N * C * ldo;
   hipLaunchKernelGGL(gen_act_bwd_kernel, grid1(total), dim3(256), 0, as_stream(stream), g, gH,
@@ -454,13 +459,17 @@ extern "C" int ainp_bn_act_bwd_apply(const float* ga, const float* y, const floa
                                      const float* ratio, int64_t N, int C, int64_t P, int64_t ldo,
                                      float* gc, float* dgamma, float* dbeta, void* stream) {
   if (!ga || !y || !scale || !shift || !save || !sums || !gc || N < 1 || C < 1 || P < 1 ||
-      ldo < P || count < 0)
+      ldo < P || count < -1)
     return record_msg("ainp_bn_act_bwd_apply: bad argument");
   const int64_t total = N * C * ldo;
-  const double inv = count > 0 ? 1.0 / (double)count : 0.0;   // 0: the count is sums[2C]
+  // count: > 0 batch statistics over count elements; 0: the count is sums[2C];
+  // -1: eval mode (save = running mean | rstd)
+  const double inv = count > 0 ? 1.0 / (double)count : 0.0;
+  const int eval = count < 0 ? 1 : 0;
   const int64_t launch = total > C ? total : C;
   hipLaunchKernelGGL(bn_act_bwd_apply_kernel, grid1(launch), dim3(256), 0, as_stream(stream), ga,
-                     y, scale, shift, save, gamma, sums, inv, slope, ratio, C, P, ldo, total, gc,
+                     y, scale, shift, save, gamma, sums, inv, eval, slope, ratio, C, P, ldo, total,
+                     gc,
                      dgamma, dbeta);
   return check_launch("bn_act_bwd_apply");
 }

@@ -360,7 +360,7 @@ def test_generator_full_matches_reference(golden_dir):
     torch.manual_seed(0)
     m = G.PConvUNet().cuda().train()
     y = m(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["mask"]).cuda())
-    yf = y.cpu().numpy().reshape(-1)
+    yf = y.detach().cpu().numpy().reshape(-1)
     assert rel(yf[::97], g["y_sample"]) < TOL
     assert abs(np.linalg.norm(yf.astype(np.float64)) - g["y_norm"][0]) < TOL * g["y_norm"][0]
 
@@ -589,8 +589,10 @@ def _check_fp32_step(g, out, Gm, Dm, param_tol=1e-5):
 # (strided sample, relative L2) of the reference's fp32 gradient, and the D
 # parameters after the Adam step within BF16_DPARAM_TOL.
 BF16_STEP_TOL = 2e-2
-BF16_DGRAD_NORM_TOL = 5e-2
-BF16_DGRAD_SAMPLE_TOL = 1e-1
+# measured at T=626 / T=1001: norms <= 1.9e-3, samples <= 9.1e-3, parameters
+# <= 3.4e-3 (profiles/r04a_pytest_bf16gates.log)
+BF16_DGRAD_NORM_TOL = 1e-2
+BF16_DGRAD_SAMPLE_TOL = 3e-2
 BF16_DPARAM_TOL = 1e-2
 
 

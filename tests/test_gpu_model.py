@@ -343,7 +343,7 @@ def test_bf16_loss_curve_30_steps_tracks_fp32_reference(golden_dir):
 # have exact gradient 0: bounded by their weight gradient's norm.
 BF16_GNORM_TOL = 2e-2
 BF16_GSAMPLE_TOL = 5e-2
-BF16_EMU_TOL = 5e-2
+BF16_EMU_TOL = 2e-2
 
 
 def test_bf16_c2_batch32_forward_backward_tracks_reference(golden_dir):
@@ -385,7 +385,8 @@ def test_bf16_c2_batch32_forward_backward_tracks_reference(golden_dir):
     # elsewhere).  Every gradient within BF16_EMU_TOL of the emulated one --
     # a bound that a wrong or zero gradient fails; the emulation's own
     # accumulation-order floor (fp32 vs fp64 between identical rounding
-    # points) is 2e-4 .. 7e-3 per tensor.
+    # points) is 2e-4 .. 7e-3 per tensor; measured HIP vs emulation: <= 4.6e-3
+    # (norms) / 8.6e-3 (samples), profiles/r04a_pytest_bf16gates.log.
     emu = np.load(os.path.join(golden_dir, "cnnblstm_c2_bf16emu.npz"), allow_pickle=False)
     e_y = rel(yf[::97], emu["emu32/y_sample"])
     e_l = abs(loss.item() - emu["emu32/loss"][0]) / emu["emu32/loss"][0]
