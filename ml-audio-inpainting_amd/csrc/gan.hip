@@ -950,14 +950,29 @@ __global__ void gan_recon_partial_kernel(const float* g, const float* o, const f
         red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
 }
 
-__global__ void gan_recon_final_kernel(const double* partial, int np, int64_t n, double* out3) {
-  __shared__ double tot[5];
-  if (threadIdx.x < 5) {
-    double s = 0.0;
-    for (int b = 0; b < np; ++b) s += partial[(int64_t)b * 5 + threadIdx.x];
-    tot[threadIdx.x] = s;
+// The 5 sums over the block partials in a fixed order: thread t adds partials
+// t, t+256, ... (one load in flight per iteration of 256 threads, not one
+// thread walking all np rows), then a fixed wave / cross-wave tree.
+__device__ __forceinline__ void recon_reduce5(const double* partial, int np, double (&tot)[5]) {
+  double s[5] = {0, 0, 0, 0, 0};
+  for (int b = threadIdx.x; b < np; b += blockDim.x)
+#pragma unroll
+    for (int q = 0; q < 5; ++q) s[q] += partial[(int64_t)b * 5 + q];
+  __shared__ double red[5][4];
+#pragma unroll
+  for (int q = 0; q < 5; ++q) {
+    const double v = wave_sum_d(s[q]);
+    if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = v;
   }
   __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 5; ++q) tot[q] = red[q][0] + red[q][1] + red[q][2] + red[q][3];
+}
+
+__global__ __launch_bounds__(256) void gan_recon_final_kernel(const double* partial, int np,
+                                                              int64_t n, double* out3) {
+  double tot[5];
+  recon_reduce5(partial, np, tot);
   if (threadIdx.x == 0) {
     // torch: fp32 sums / (fp32 sum + 1e-8); the fp64 sums are rounded once
     const float nv = (float)tot[1] + 1e-8f, nh = (float)tot[3] + 1e-8f;
@@ -2630,16 +2645,15 @@ extern "C" int ainp_gan_recon_losses(const float* g, const float* o, const float
   hipStream_t s = as_stream(stream);
   double* part = reinterpret_cast<double*>(workspace);
   hipLaunchKernelGGL(gan_recon_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, g, o, m, n, part);
-  hipLaunchKernelGGL(gan_recon_final_kernel, dim3(1), dim3(64), 0, s, part, kRedBlocks, n, out3);
+  hipLaunchKernelGGL(gan_recon_final_kernel, dim3(1), dim3(256), 0, s, part, kRedBlocks, n, out3);
   return check_launch("gan_recon_losses");
 }
 
-__global__ void gan_recon_sums_kernel(const double* partial, int np, double* out5) {
-  if (threadIdx.x < 5) {
-    double s = 0.0;
-    for (int b = 0; b < np; ++b) s += partial[(int64_t)b * 5 + threadIdx.x];
-    out5[threadIdx.x] = s;
-  }
+__global__ __launch_bounds__(256) void gan_recon_sums_kernel(const double* partial, int np,
+                                                             double* out5) {
+  double tot[5];
+  recon_reduce5(partial, np, tot);
+  if (threadIdx.x < 5) out5[threadIdx.x] = tot[threadIdx.x];
 }
 
 extern "C" int ainp_gan_recon_sums(const float* g, const float* o, const float* m, int64_t n,
@@ -2649,7 +2663,7 @@ extern "C" int ainp_gan_recon_sums(const float* g, const float* o, const float* 
   hipStream_t s = as_stream(stream);
   double* part = reinterpret_cast<double*>(workspace);
   hipLaunchKernelGGL(gan_recon_partial_kernel, dim3(kRedBlocks), dim3(256), 0, s, g, o, m, n, part);
-  hipLaunchKernelGGL(gan_recon_sums_kernel, dim3(1), dim3(64), 0, s, part, kRedBlocks, out5);
+  hipLaunchKernelGGL(gan_recon_sums_kernel, dim3(1), dim3(256), 0, s, part, kRedBlocks, out5);
   return check_launch("gan_recon_sums");
 }
 

@@ -41,9 +41,12 @@ data is written:
       calculate_losses through the oracle restatement (oracle/gan_ref.
       generator_losses, VGG19 with seeded weights vgg19_init(0): loss.py
       imports torchvision, absent here), g_total.backward(), Adam(2e-4,
-      (0.5, 0.999)) on G.  Stored: initial G / D state dicts, inputs, the
-      generated output, every G gradient, G's state after its Adam step, the
-      G-step losses.
+      (0.5, 0.999)) on G.  Run twice, in fp32 ("r32/") and with the same
+      modules in fp64 ("r64/"): the L1 terms of the VGG losses make the input
+      gradient a sum of sign() functions, so fp32 and fp64 differ by ~1e-3
+      (the conditioning floor the GPU test's bound is derived from).  Stored:
+      initial G / D state dicts, inputs, the generated output, every G
+      gradient, G's state after its Adam step, the G-step losses.
 """
 from __future__ import annotations
 
@@ -201,23 +204,28 @@ def gen_bf16emu(mod):
     np.savez_compressed(os.path.join(HERE, "cnnblstm_c2_bf16emu.npz"), **out)
 
 
-def gen_gstep_small(net):
+def _gstep(net, dtype, out, tag):
+    """One fix_generator_grad step of the reduced reference G / D in `dtype`;
+    stores under tag/ the generated output, D loss, G-step losses, G grads and
+    G's state after Adam."""
     from golden.gen_golden_gan import SMALL_D, SMALL_DEC, SMALL_ENC, SMALL_FINAL, spec_inputs
     from oracle import gan_ref
-    out = {}
     torch.manual_seed(2)
     G = net.PConvUNet(enc_layer_cfg=SMALL_ENC, dec_layer_cfg=SMALL_DEC, final_dec_cfg=SMALL_FINAL)
     torch.manual_seed(3)
     D = net.Discriminator(layer_cfg=SMALL_D)
+    if tag == "r32":
+        for k, v in G.state_dict().items():
+            out["g_init/" + k] = v.detach().clone().numpy()
+        for k, v in D.state_dict().items():
+            out["d_init/" + k] = v.detach().clone().numpy()
+    G, D = G.to(dtype), D.to(dtype)
     G.train(); D.train()
-    for k, v in G.state_dict().items():
-        out["g_init/" + k] = v.detach().clone().numpy()
-    for k, v in D.state_dict().items():
-        out["d_init/" + k] = v.detach().clone().numpy()
     x, m = spec_inputs(2, 129, 100, seed=500)
     imp = x * m
-    out["orig"], out["imp"], out["mask"] = x, imp, m
-    O, I, M = (torch.from_numpy(a) for a in (x, imp, m))
+    if tag == "r32":
+        out["orig"], out["imp"], out["mask"] = x, imp, m
+    O, I, M = (torch.from_numpy(a).to(dtype) for a in (x, imp, m))
     bce = torch.nn.BCEWithLogitsLoss()
     d_opt = torch.optim.Adam(D.parameters(), lr=2e-4, betas=(0.5, 0.999))
     g_opt = torch.optim.Adam(G.parameters(), lr=2e-4, betas=(0.5, 0.999))
@@ -232,24 +240,33 @@ def gen_gstep_small(net):
     d_opt.step()
     g_opt.zero_grad()
     dfg = D(gen)
-    pv = gan_ref.vgg19_init(0)
+    pv = {k: v.to(dtype) for k, v in gan_ref.vgg19_init(0).items()}
     L = gan_ref.generator_losses(gen, O, M, dfg, pv)
     L["g_total"].backward()
-    out["gen"] = gen.detach().numpy()
-    out["d_loss"] = np.array([d_loss.item()])
+    out[tag + "/gen"] = gen.detach().float().numpy()
+    out[tag + "/d_loss"] = np.array([d_loss.item()])
     for k, v in L.items():
-        out["loss/" + k] = np.array([float(v.detach())])
+        out[tag + "/loss/" + k] = np.array([float(v.detach())])
     for k, p in G.named_parameters():
         if p.requires_grad:
             assert p.grad is not None, k
-            out["g_grad/" + k] = p.grad.detach().clone().numpy()
+            out[tag + "/g_grad/" + k] = p.grad.detach().double().numpy()
     g_opt.step()
     for k, v in G.state_dict().items():
-        out["g_after/" + k] = v.detach().clone().numpy()
+        out[tag + "/g_after/" + k] = v.detach().clone().numpy()
+
+
+def gen_gstep_small(net):
+    out = {}
+    _gstep(net, torch.float32, out, "r32")
+    _gstep(net, torch.float64, out, "r64")
     np.savez_compressed(os.path.join(HERE, "gan_gstep_small.npz"), **out)
-    for k in sorted(x for x in out if x.startswith("g_grad/")):
-        print(k, out[k].shape, float(np.linalg.norm(out[k])))
-    print({k: float(out[k][0]) for k in out if k.startswith("loss/")})
+    rel = lambda a, b: float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))  # noqa: E731
+    for k in sorted(x for x in out if x.startswith("r32/g_grad/")):
+        name = k[len("r32/g_grad/"):]
+        print(f"{name:45s} |g| {np.linalg.norm(out[k]):.4e}  fp32 vs fp64 "
+              f"{rel(out[k], out['r64/g_grad/' + name]):.2e}")
+    print({k: float(out[k][0]) for k in out if "/loss/" in k and k.startswith("r32")})
 
 
 if __name__ == "__main__":

@@ -38,3 +38,17 @@ def test_bf16emu_fixture_covers_c2_and_floor_is_small(golden_dir):
     assert worst < 1e-2, worst
     assert abs(emu["emu32/loss"][0] - ref["loss"][0]) / ref["loss"][0] < 2e-3
     assert abs(emu["emu64/loss"][0] - emu["emu32/loss"][0]) / emu["emu64/loss"][0] < 1e-4
+
+
+def test_gstep_fixture_fp32_and_fp64_runs_agree(golden_dir):
+    """gan_gstep_small.npz (tests/golden/gen_golden_r04.py gstep): the
+    reference G-step in fp32 and fp64 agree to 1e-4 on every G gradient (so
+    the GPU test's 1e-4 gate against the fp64 run is meaningful), and every
+    trainable G parameter of the reduced generator has a gradient."""
+    f = np.load(os.path.join(golden_dir, "gan_gstep_small.npz"), allow_pickle=False)
+    names = [k[len("r32/g_grad/"):] for k in f.files if k.startswith("r32/g_grad/")]
+    assert len(names) == 43   # 7 + 6 blocks x (conv W, BN gamma, beta) + 2 x (W, b)
+    for k in names:
+        assert rel(f["r32/g_grad/" + k], f["r64/g_grad/" + k]) < 1e-4, k
+        assert np.linalg.norm(f["r64/g_grad/" + k]) > 0, k
+    assert abs(f["r32/loss/g_total"][0] - f["r64/loss/g_total"][0]) < 1e-5

@@ -805,23 +805,33 @@ def test_vgg_loss_input_gradient_matches_oracle():
     """d(lambda_p perceptual + lambda_s style) / d generated through VGG19
     (seeded weights; loss.py:89-131 incl. the inplace-ReLU feature quirk) and
     the input preparation, against torch autograd of the oracle restatement
-    in fp64 on the CPU."""
+    in fp64 on the CPU.  The L1 terms make the gradient a sum of sign()
+    functions of feature / Gram differences, so two correct fp32
+    implementations already differ by ~2e-3 (sign flips where fg ~ ft): the
+    bound is 1.5 x the oracle's own fp32-vs-fp64 distance (+1e-5), i.e. the
+    GPU path must be as accurate as an fp32 restatement of the reference."""
     g = torch.Generator().manual_seed(9)
     gen = torch.tanh(torch.randn(2, 1, 129, 100, generator=g))
     tgt = torch.rand(2, 1, 129, 100, generator=g) * 3
     v, pv = _vgg_pair(0)
-    gg = gen.cuda().requires_grad_(True)
-    perc, style = v(gg, tgt.cuda())
-    (4.0 * perc + 500.0 * style).backward()
-    p64 = {k: t.double() for k, t in pv.items()}
-    g64 = gen.double().requires_grad_(True)
-    rp, rs = R.vgg_losses(p64, g64, tgt.double())
-    (4.0 * rp + 500.0 * rs).backward()
-    assert abs(float(perc) - float(rp)) < 1e-4 * abs(float(rp))
-    assert abs(float(style) - float(rs)) < 1e-4 * abs(float(rs))
-    e = rel(gg.grad, g64.grad)
-    print("VGG input gradient rel err", e)
-    assert e < 1e-4
+    for lp, ls in ((4.0, 0.0), (0.0, 500.0)):
+        gg = gen.cuda().requires_grad_(True)
+        perc, style = v(gg, tgt.cuda())
+        (lp * perc + ls * style).backward()
+        ref = {}
+        for dt in (torch.float64, torch.float32):
+            p = {k: t.to(dt) for k, t in pv.items()}
+            gr = gen.to(dt).requires_grad_(True)
+            rp, rs = R.vgg_losses(p, gr, tgt.to(dt))
+            (lp * rp + ls * rs).backward()
+            ref[dt] = (gr.grad, float(rp), float(rs))
+        g64, rp, rs = ref[torch.float64]
+        assert abs(float(perc) - rp) < 1e-4 * abs(rp)
+        assert abs(float(style) - rs) < 1e-4 * abs(rs)
+        e = rel(gg.grad, g64)
+        floor = rel(ref[torch.float32][0], g64)
+        print(f"VGG input gradient (lp={lp}, ls={ls}): rel err {e:.3e}, fp32 floor {floor:.3e}")
+        assert e < 1.5 * floor + 1e-5, (e, floor)
 
 
 @pytest.mark.timeout(600)
@@ -852,26 +862,28 @@ def test_generator_training_step_matches_reference(golden_dir):
         out = tr.step(*(torch.from_numpy(f[k]).cuda() for k in ("orig", "imp", "mask")))
         return out, Gm
     out, Gm = make(True)
-    assert rel(out["generated"], f["gen"]) < TOL
-    assert abs(float(out["d_loss"]) - f["d_loss"][0]) <= TOL * abs(f["d_loss"][0])
+    assert rel(out["generated"], f["r32/gen"]) < TOL
+    assert abs(float(out["d_loss"]) - f["r32/d_loss"][0]) <= TOL * abs(f["r32/d_loss"][0])
     for k in ("g_total", "g_adv", "g_l1_valid", "g_l1_hole", "g_mag_weighted",
               "g_vgg_perceptual", "g_vgg_style"):
-        r = float(f["loss/" + k][0])
+        r = float(f["r32/loss/" + k][0])
         assert abs(float(out[k]) - r) <= TOL * max(abs(r), 1e-6), (k, float(out[k]), r)
+    # every G gradient vs the reference module run in fp64 (the fp32 reference
+    # itself sits 4e-7 .. 1.2e-5 from it), and vs the fp32 reference run
     errs = {}
     for k, p in Gm.named_parameters():
         if not p.requires_grad:
             continue
         assert p.grad is not None, k
-        errs[k] = rel(p.grad, f["g_grad/" + k])
-    print("G grad rel errs", sorted(errs.items(), key=lambda kv: -kv[1])[:6])
-    assert len(errs) == sum(1 for k in f.files if k.startswith("g_grad/"))
-    for k, e in errs.items():
-        assert e < TOL, (k, e)
+        errs[k] = (rel(p.grad, f["r64/g_grad/" + k]), rel(p.grad, f["r32/g_grad/" + k]))
+    print("G grad rel errs (vs fp64, vs fp32)", sorted(errs.items(), key=lambda kv: -kv[1][0])[:6])
+    assert len(errs) == sum(1 for k in f.files if k.startswith("r32/g_grad/"))
+    for k, (e64, e32) in errs.items():
+        assert e64 < TOL and e32 < TOL, (k, e64, e32)
     sd = Gm.state_dict()
     for k in f.files:
-        if k.startswith("g_after/"):
-            name = k[len("g_after/"):]
+        if k.startswith("r32/g_after/"):
+            name = k[len("r32/g_after/"):]
             if name.endswith("num_batches_tracked"):
                 assert int(sd[name]) == int(f[k])
             else:
