@@ -389,10 +389,10 @@ def spawn_ranks(n):
 # kernels from them with their own roofline fractions (per-step algorithmic
 # work / per-step kernel time / peak), next to the live stand-alone launches.
 STEP_TABLES = {
-    ("cnnblstm", "fp32"): "profiles/r04_cnn_fp32_step_kernel_stats.csv",
-    ("cnnblstm", "bf16"): "profiles/r04_cnn_bf16_step_kernel_stats.csv",
-    ("gan", "bf16", 626): "profiles/r04_gan_c4_bf16_step_kernel_stats.csv",
-    ("gan", "bf16", 1001): "profiles/r04_gan_c5_bf16_step_kernel_stats.csv",
+    ("cnnblstm", "fp32"): "profiles/r04d_cnn_fp32_step_kernel_stats.csv",
+    ("cnnblstm", "bf16"): "profiles/r04d_cnn_bf16_step_kernel_stats.csv",
+    ("gan", "bf16", 626): "profiles/r04d_gan_c4_step_kernel_stats.csv",
+    ("gan", "bf16", 1001): "profiles/r04d_gan_c5_step_kernel_stats.csv",
 }
 STEP_TABLE_DIV = 13
 
