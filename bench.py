@@ -404,10 +404,13 @@ def _cnn_step_work(B=32, F=257, T=334, H=128):
     P = B * F * T                       # pixels per channel plane set
     conv = lambda ci, co: 2.0 * 9 * ci * co * P          # noqa: E731
     l0 = 2.0 * B * T * 8 * H * 64 * F                     # one layer-0 GEMM
+    proj = 2.0 * B * T * 16 * F * 2 * H                   # one output-projection GEMM
     bn_small = (16 + 32 + 32 + 16) * P                    # BN-ReLU elements of the 16/32-ch layers
     big = 64 * P
     return [
-        ("gemm_x6r_kernel", "mfma", 3 * l0),              # projection + backward pair
+        # fp32: layer-0 projection + backward pair + the output projection's
+        # dh and dW (proj_bwd_x6)
+        ("gemm_x6r_kernel", "mfma", 3 * l0 + 2 * proj),
         ("gemm_bf16nt_256_kernel", "mfma", l0),           # bf16 projection
         ("g16::gemm_bf16nt_kernel", "mfma", 2 * l0),      # bf16 dX + dW
         ("conv3x3_x6p_kernel<32, 64", "mfma", conv(32, 64)),

@@ -283,6 +283,10 @@ int ainp_transpose_f32(const float* x, int64_t R, int64_t C, int64_t ld_in, floa
  * rows a kernel does not produce are zeroed. */
 int ainp_conv3x3_fwd_stat_parts(int64_t N, int64_t H, int64_t W);
 int64_t ainp_conv3x3_fwd_stat_rows(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
+/* The rows for a given ainp_conv3x3_fwd_ex `flags` (AINP_CONV_BF16: the bf16
+ * kernels run a larger persistent grid, one row per workgroup). */
+int64_t ainp_conv3x3_fwd_stat_rows_ex(int64_t N, int Cin, int Cout, int64_t H, int64_t W,
+                                      int flags);
 int ainp_conv3x3_fwd(const float* x, const float* w, const float* bias,
                      const float* in_scale, const float* in_shift, float* y,
                      double* stats, int64_t N, int Cin, int Cout, int64_t H,

@@ -55,6 +55,7 @@ _SIGS = {
                                  c_int, P, c_size_t, P]),
     "ainp_conv3x3_fwd_stat_parts": (c_int, [c_int64, c_int64, c_int64]),
     "ainp_conv3x3_fwd_stat_rows": (c_int64, [c_int64, c_int, c_int, c_int64, c_int64]),
+    "ainp_conv3x3_fwd_stat_rows_ex": (c_int64, [c_int64, c_int, c_int, c_int64, c_int64, c_int]),
     "ainp_conv3x3_fwd": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
                                  c_int64, P]),
     "ainp_conv3x3_dgrad": (c_int, [P, P, P, P, c_int64, c_int, c_int, c_int64, c_int64, P]),

@@ -629,7 +629,9 @@ def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf
     y = torch.empty(N, Cout, H, W, device=x.device, dtype=torch.float32)
     stats = None
     if want_stats:
-        stats = torch.empty(_lib.lib.ainp_conv3x3_fwd_stat_rows(N, Cin, Cout, H, W), 2 * Cout,
+        stats = torch.empty(_lib.lib.ainp_conv3x3_fwd_stat_rows_ex(N, Cin, Cout, H, W,
+                                                                   CONV_BF16 if bf16 else 0),
+                            2 * Cout,
                             device=x.device, dtype=torch.float64)
     _T.conv3x3_fwd(x, w, b, in_scale, in_shift, y, stats, CONV_BF16 if bf16 else 0)
     return y, stats

@@ -21,6 +21,12 @@ inline int check_launch(const char* where) {
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
+// Upper bound of the persistent-grid multiplier of the bf16 (NP = 1) 3x3 conv
+// kernels (conv_x6.hip conv_x6_occ16): BatchNorm partial rows and weight-
+// gradient slabs are sized for it.
+constexpr int X6_OCC_MAX = 4;
+int conv_x6_occ16();
+
 // Wave-level (64-lane) reductions.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

@@ -909,7 +909,8 @@ using namespace ainp;
 
 namespace ainp {
 int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W);
-int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W);
+int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W,
+                          bool b16);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
                          int ci0, int cp, int grid, hipStream_t s, bool b16);
@@ -942,12 +943,18 @@ extern "C" int ainp_conv3x3_fwd_stat_parts(int64_t N, int64_t H, int64_t W) {
 // The BatchNorm partial rows ainp_conv3x3_fwd writes for this shape (the
 // kernel the dispatch below selects; fewer than the bound above when a
 // persistent kernel serves it).
-extern "C" int64_t ainp_conv3x3_fwd_stat_rows(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+extern "C" int64_t ainp_conv3x3_fwd_stat_rows_ex(int64_t N, int Cin, int Cout, int64_t H,
+                                                 int64_t W, int flags) {
   if (!small_pair(Cin, Cout) && !conv_exact_env()) {
-    const int64_t r = conv_x6_stat_rows(false, Cin, Cout, N, H, W);
+    const int64_t r =
+        conv_x6_stat_rows(false, Cin, Cout, N, H, W, (flags & AINP_CONV_BF16) != 0);
     if (r) return r;
   }
   return exact_stat_parts(N, H, W);
+}
+
+extern "C" int64_t ainp_conv3x3_fwd_stat_rows(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+  return ainp_conv3x3_fwd_stat_rows_ex(N, Cin, Cout, H, W, 0);
 }
 
 template <bool DG>
@@ -958,7 +965,8 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
   // partials [used, rows) of the BatchNorm statistics are zero
   auto zero_tail = [&](int64_t used) -> int {
     if (!stats) return AINP_OK;
-    const int64_t bound = ainp_conv3x3_fwd_stat_rows(N, Cin, Cout, H, W);
+    const int64_t bound =
+        ainp_conv3x3_fwd_stat_rows_ex(N, Cin, Cout, H, W, b16 ? AINP_CONV_BF16 : 0);
     if (used >= bound) return AINP_OK;
     hipError_t e = hipMemsetAsync(stats + used * 2 * Cout, 0,
                                   (size_t)(bound - used) * 2 * Cout * sizeof(double), s);
@@ -1057,7 +1065,9 @@ extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
   const int cp = wgrad_pass(Cin);
   int ct = wgrad_ct(Cout);
   if (ct == 3) ct = 4;
-  return (size_t)(WG_BLOCKS + 2 * WG_GROUPS) * ct * 16 * (9 * cp + 1) * sizeof(float);
+  // slabs for the largest grid (the bf16 x6 kernels' multiplier, conv_x6_occ16)
+  return (size_t)(WG_BLOCKS * X6_OCC_MAX + 2 * WG_GROUPS) * ct * 16 * (9 * cp + 1) *
+         sizeof(float);
 }
 
 extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
@@ -1113,10 +1123,12 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
                      in_scale, in_shift, dy, partial, (int)N, Cin, (int)H, (int)W, ci0)
     // split-bf16 kernel where it is instantiated (conv_x6.hip), unless
     // AINP_CONV_EXACT=1; same slab format
+    const int nblk_x6 = b16 ? WG_BLOCKS * conv_x6_occ16() : WG_BLOCKS;
     int rc = (fits && !conv_exact_env())
                  ? conv_wgrad_x6_launch(x, in_scale, in_shift, dy, partial, N, Cin, Cout, H, W,
-                                        ci0, cp, WG_BLOCKS, s, b16)
+                                        ci0, cp, nblk_x6, s, b16)
                  : 1;
+    const int nblk = rc == 0 ? nblk_x6 : WG_BLOCKS;   // slabs the launch writes
     if (rc == 1) switch (key) {
       case 1616: AINP_WGT(16, 16); break;
       case 1632: AINP_WGT(16, 32); break;
@@ -1137,9 +1149,9 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
     if (rc) return rc;
     const int J = 9 * cp;
     const int per = CTp * 16 * (J + 1);
-    double* tmp = reinterpret_cast<double*>(partial + (size_t)WG_BLOCKS * per);
+    double* tmp = reinterpret_cast<double*>(partial + (size_t)nblk * per);
     hipLaunchKernelGGL(wgrad_reduce1, dim3((per + 255) / 256, WG_GROUPS), dim3(256), 0, s,
-                       partial, WG_BLOCKS, per, WG_BLOCKS / WG_GROUPS, tmp);
+                       partial, nblk, per, nblk / WG_GROUPS, tmp);
     rc = check_launch("wgrad_reduce1");
     if (rc) return rc;
     hipLaunchKernelGGL(wgrad_reduce, dim3((per + 255) / 256), dim3(256), 0, s,

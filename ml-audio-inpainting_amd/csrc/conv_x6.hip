@@ -305,20 +305,37 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16);
 
+// Persistent-grid multiplier of the bf16 (NP = 1) kernels: their LDS (21-50
+// KB) and VGPR (48-80) footprints let 2-4x the fp32 kernels' workgroups stay
+// resident, and they are bound by the loads a CU keeps in flight (SQ passes:
+// MFMA busy 0.05-0.10, waves parked on s_waitcnt 0.5-0.67 of their cycles,
+// profiles/r04e_*).  AINP_X6_OCC16 overrides (1 .. X6_OCC_MAX).
+int conv_x6_occ16() {
+  static const int v = [] {
+    const char* e = getenv("AINP_X6_OCC16");
+    const int o = e ? atoi(e) : 1;
+    return o < 1 ? 1 : (o > X6_OCC_MAX ? X6_OCC_MAX : o);
+  }();
+  return v;
+}
+
 // Launch if (Cin, Cout) has an x6 instantiation; returns 1 if not handled.
 // *parts = the number of BatchNorm partials written.  The persistent kernel
 // serves every pair it has (32-bit buffer offsets permitting); the tiled one
 // is kept for AINP_CONV_X6_TILED=1.
 // BatchNorm partial rows the x6 launch below writes for this shape (0: no x6
 // kernel serves it); mirrors conv_x6_launch / conv_x6p_launch.
-int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W) {
+int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W,
+                          bool b16) {
+  const int occ = b16 ? conv_x6_occ16() : 1;
   if (Cout > 64 || Cout < 16) return 0;
   const int cop = Cout <= 32 ? 32 : 64;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
-    if (!dgrad && Cin == 32 && cop == 64) return 256;
-    if (Cin == 16 && cop == 32) return 512;
-    if (Cin == 32 && Cout == 16) return 512;
+    // one row per persistent workgroup (bf16: the multiplied grid)
+    if (!dgrad && Cin == 32 && cop == 64) return 256 * occ;
+    if (Cin == 16 && cop == 32) return 512 * occ;
+    if (Cin == 32 && Cout == 16) return 512 * occ;
   }
   if (((Cin == 32 && cop == 64) || (Cin == 64 && cop == 32)) &&
       (int64_t)Cin * H * W * 4 < ((int64_t)1 << 31))    // 32-bit buffer offsets
@@ -329,7 +346,7 @@ int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, i
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16) {
-  if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W) == 0) return 1;
+  if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W, b16) == 0) return 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
@@ -1259,20 +1276,22 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
 #define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                      \
   if (dgrad == DG && Cin == CIV && cop == COV) {                                                 \
+    const int g2 = b16 ? (G) * conv_x6_occ16() : (G);                                            \
     if (b16)                                                                                     \
-      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 1>), dim3(G), dim3(NTV), 0, \
+      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 1>), dim3(g2), dim3(NTV), 0, \
                          s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);         \
     else                                                                                         \
-      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 3>), dim3(G), dim3(NTV), 0, \
+      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 3>), dim3(g2), dim3(NTV), 0, \
                          s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);         \
-    *parts = G;                                                                                  \
+    *parts = g2;                                                                                 \
     return check_launch("conv3x3_x6p");                                                          \
   }
   AINP_X6P(32, 64, false, 256, 1024, 8)
   AINP_X6P(16, 32, false, 512, 512, 8) AINP_X6P(16, 32, true, 512, 512, 8)
-  if (Cin == 32 && Cout == 16) {   // two workgroups per CU (65 KB of LDS)
+  if (Cin == 32 && Cout == 16) {   // two workgroups per CU (65 KB of LDS; bf16: more)
+    const int gq = b16 ? 512 * conv_x6_occ16() : 512;
 #define AINP_X6Q(DG, NPV)                                                                        \
-  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV>), dim3(512), dim3(512), 0, s, x, w, bias,  \
+  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV>), dim3(gq), dim3(512), 0, s, x, w, bias,   \
                      sc, sh, y, stats, (int)N, Cout, (int)H, (int)W)
     if (dgrad) {
       if (b16) AINP_X6Q(true, 1);
@@ -1282,7 +1301,7 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
       else AINP_X6Q(false, 3);
     }
 #undef AINP_X6Q
-    *parts = 512;
+    *parts = gq;
     return check_launch("conv3x3_x6q");
   }
 

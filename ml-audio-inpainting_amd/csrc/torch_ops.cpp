@@ -216,7 +216,10 @@ void conv3x3_fwd(const Tensor& x, const Tensor& w, const OptT& bias, const OptT&
   const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = w.size(0);
   numel_is(y, N * Cout * H * W, "y");
   double* st = opt<double>(stats, "stats", at::kDouble);
-  if (st) numel_is(*stats, ainp_conv3x3_fwd_stat_rows(N, (int)Cin, (int)Cout, H, W) * 2 * Cout, "stats");
+  if (st)
+    numel_is(*stats,
+             ainp_conv3x3_fwd_stat_rows_ex(N, (int)Cin, (int)Cout, H, W, (int)flags) * 2 * Cout,
+             "stats");
   chk(ainp_conv3x3_fwd_ex(dev(x, "x"), dev(w, "w"), opt(bias, "bias"), opt(in_scale, "in_scale"),
                           opt(in_shift, "in_shift"), dev(y, "y"), st, N, (int)Cin, (int)Cout, H, W,
                           (int)flags, stream_of(x)),

@@ -815,14 +815,14 @@ def test_vgg_loss_input_gradient_matches_oracle():
     tgt = torch.rand(2, 1, 129, 100, generator=g) * 3
     v, pv = _vgg_pair(0)
     for lp, ls in ((4.0, 0.0), (0.0, 500.0)):
-        gg = gen.cuda().requires_grad_(True)
+        gg = gen.clone().cuda().requires_grad_(True)
         perc, style = v(gg, tgt.cuda())
         (lp * perc if lp else ls * style).backward()     # one term at a time
         assert torch.isfinite(gg.grad).all()
         ref = {}
         for dt in (torch.float64, torch.float32):
             p = {k: t.to(dt) for k, t in pv.items()}
-            gr = gen.to(dt).requires_grad_(True)
+            gr = gen.clone().to(dt).requires_grad_(True)      # a fresh leaf per run
             rp, rs = R.vgg_losses(p, gr, tgt.to(dt))
             (lp * rp if lp else ls * rs).backward()
             assert torch.isfinite(gr.grad).all(), dt
