@@ -150,6 +150,30 @@ def test_stft512_tiled_vs_generic_and_oracle(ops, mode, S, hop, win, n_frames, g
         assert torch.equal(part[3], new[3])
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+@pytest.mark.parametrize("grid", [1, 7, 64])
+def test_stft512_persistent_walk_bit_identical(ops, mode, grid, monkeypatch):
+    """The persistent n_fft=512 kernel loads a tile's clean frames before the
+    previous tile's write-out: with a grid of 1, 7 or 64 workgroups every
+    workgroup walks many tiles (edge, gap and interior ones, odd tile counts),
+    and the result must equal the one-tile-per-workgroup launch bit for bit."""
+    S, hop, win, T, g, B = 64000, 192, 384, 334, 3200, 6
+    clips = np.stack([synth.synthetic_clip(90 + i, S) for i in range(B)])
+    starts = np.array([0, S - g - 1, 5000, 17001, 40000, 33333], np.int64)
+    a = torch.from_numpy(clips).to(DEV)
+    gs = torch.from_numpy(starts).to(DEV)
+    kw = dict(n_frames=T, mode=mode)
+    ref = ops.stft_features(a, gs, g, 512, hop, win, **kw)
+    monkeypatch.setenv("AINP_STFT_GRID", str(grid))
+    got = ops.stft_features(a, gs, g, 512, hop, win, **kw)
+    part = ops.stft_features(a, gs, g, 512, hop, win, outputs=(True, False, False, True), **kw)
+    torch.cuda.synchronize()
+    for i, (x, y) in enumerate(zip(got, ref)):
+        if x is not None:
+            assert torch.equal(x, y), (mode, grid, i)
+    assert torch.equal(part[0], ref[0])
+
+
 def test_gap_frames_known_answers_n512(ops, golden_dir):
     """The Q3 known answers through the tiled n_fft=512 kernel (mask-only launch)."""
     cases = json.load(open(os.path.join(golden_dir, "gap_frames.json")))["cases"]
