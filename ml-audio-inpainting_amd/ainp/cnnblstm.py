@@ -292,6 +292,62 @@ class _BLSTMFn(torch.autograd.Function):
         # stream never waits for them (AccumulateGrad stores non-view aliases)
         dp_side = ctx.sink is not None and ctx.sink.early_ok and \
             getattr(ctx.sink, "side_ok", True) and all(p.grad is None for p in ctx.param_objs)
+        main_first = ops.MAIN_FIRST
+
+        def main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink, dg16):
+            """Layer l's data gradient (and, for the fp32 layer-0 pair, dW_ih) on
+            the current stream; (dxi or None, [gW_ih, gW_ih_rev] or None)."""
+            gwi = None
+            dxi = None
+            if pair:
+                dxi = torch.empty(NT, Il, device=dh.device)
+                gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
+                if ops.PAIR_JOIN:
+                    # the side stream's queued weight gradients finish first at
+                    # full width: the pair kernel (160 KB of LDS per workgroup)
+                    # cannot share a CU with them
+                    ev = torch.cuda.Event()
+                    ev.record(side)
+                    main.wait_event(ev)
+                ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
+                if to_sink:
+                    # all-reduced from the current stream right behind the pair;
+                    # the reducer's Work holds these buffers, autograd gets None
+                    for d in range(2):
+                        ctx.sink.reduce_chunk(ctx.wih0[d], gwi[d], kind="pair")
+                        ctx.wih0[d].grad = gwi[d]
+            if not (l > 0 or ctx.needs_input_grad[0]):
+                return dxi, gwi
+            # dX = dg_f W_ih + dg_r W_ih_rev.  Layer 0 (Il = 16448: 10836
+            # tiles) sums both directions inside each tile; the upper layers
+            # (Il = 256: 168 tiles) write 4 K-slabs (two per direction,
+            # 672 tiles) summed in fixed order.
+            if pair:
+                pass                                                  # dxi from the pair
+            elif l016 is not None:
+                dxi = ops.gemm_bf16nt(dg16, l016[1])                 # dg [NT,8H] x W_cat
+            elif Il >= 1024 and ops.DX_X6_256 and not bf16 and not ops.GEMM_EXACT \
+                    and ops.x6_256_eligible(NT, Il, 8 * H, Il):
+                # layer 0 fp32: dX = dg [NT, 8H] . [W_f; W_r] on the 256 x 256
+                # split-pass tile with the k-contiguous W_cat^T [Il, 8H]
+                wt = torch.empty(Il, 8 * H, device=dh.device)
+                ops.transpose_f32(wf, out=wt[:, :4 * H])
+                ops.transpose_f32(wr, out=wt[:, 4 * H:])
+                dxi = torch.empty(NT, Il, device=dh.device)
+                ops.gemm_x6nt_256(dg2.view(NT, 8 * H), wt, wt[:0], dxi, nsplit=1)
+            elif Il >= 1024:
+                dxi = torch.empty(NT, Il, device=dh.device)
+                ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,
+                         [dxi, dxi], Il, 1, ksplit=True, bf16=bf16)
+            else:
+                hk = 2 * H                      # half of a direction's 4H gate columns
+                sl = torch.empty(4, NT, Il, device=dh.device)
+                ops.gemm(NT, Il, hk, [dg2[:, q * hk:] for q in range(4)], 8 * H, 1,
+                         [(wf if q < 2 else wr)[(q % 2) * hk:] for q in range(4)], Il, 1,
+                         [sl[q] for q in range(4)], Il, 1, bf16=bf16)
+                dxi = ops.sum_slabs(sl, 4).view(NT, Il)
+            return dxi, gwi
+
         for l in range(L - 1, -1, -1):
             inp, h, gates, cell = saved[4 * l:4 * l + 4]
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
@@ -325,6 +381,13 @@ class _BLSTMFn(torch.autograd.Function):
             to_sink = (l == 0 and ctx.sink is not None and ctx.sink.early_ok
                        and all(p.grad is None for p in ctx.wih0))
             early = to_sink and not pair
+            if main_first:
+                # the data gradient (the critical path: the next BPTT / the
+                # encoder backward wait for it) is issued before the side
+                # stream's weight-gradient launches, whose host-side issue
+                # would otherwise leave the current stream idle
+                dxi, gwi_pair = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
+                                        dg16 if l016 is not None else None)
             with torch.cuda.stream(side):
                 # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
                 # for the recurrent / upper layers -> parallel split-K over row chunks
@@ -351,23 +414,11 @@ class _BLSTMFn(torch.autograd.Function):
             for t in (dg, hp, inp) + ((dgT16, l016[0]) if l016 is not None else ()):
                 t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l
+            if not main_first:
+                dxi, gwi_pair = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
+                                        dg16 if l016 is not None else None)
             if pair:
-                dxi = torch.empty(NT, Il, device=dh.device)
-                gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
-                if ops.PAIR_JOIN:
-                    # the side stream's queued weight gradients finish first at
-                    # full width: the pair kernel (160 KB of LDS per workgroup)
-                    # cannot share a CU with them
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    main.wait_event(ev)
-                ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
-                if to_sink:
-                    # all-reduced from the current stream right behind the pair;
-                    # the reducer's Work holds these buffers, autograd gets None
-                    for d in range(2):
-                        ctx.sink.reduce_chunk(ctx.wih0[d], gwi[d], kind="pair")
-                        ctx.wih0[d].grad = gwi[d]
+                gwi = gwi_pair
             if to_sink:   # p.grad set and reduced above / by _wih_grad_chunked
                 gwi = [None, None]
                 ctx.early_done = True
@@ -376,34 +427,6 @@ class _BLSTMFn(torch.autograd.Function):
             grads[base + 4], grads[base + 5] = gwi[1], gwh[1]
             grads[base + 6], grads[base + 7] = db_ih[4 * H:], db_hh[4 * H:]
             if l > 0 or ctx.needs_input_grad[0]:
-                # dX = dg_f W_ih + dg_r W_ih_rev.  Layer 0 (Il = 16448: 10836
-                # tiles) sums both directions inside each tile; the upper layers
-                # (Il = 256: 168 tiles) write 4 K-slabs (two per direction,
-                # 672 tiles) summed in fixed order.
-                if pair:
-                    pass                                                  # dxi from the pair
-                elif l016 is not None:
-                    dxi = ops.gemm_bf16nt(dg16, l016[1])                 # dg [NT,8H] x W_cat
-                elif Il >= 1024 and ops.DX_X6_256 and not bf16 and not ops.GEMM_EXACT \
-                        and ops.x6_256_eligible(NT, Il, 8 * H, Il):
-                    # layer 0 fp32: dX = dg [NT, 8H] . [W_f; W_r] on the 256 x 256
-                    # split-pass tile with the k-contiguous W_cat^T [Il, 8H]
-                    wt = torch.empty(Il, 8 * H, device=dh.device)
-                    ops.transpose_f32(wf, out=wt[:, :4 * H])
-                    ops.transpose_f32(wr, out=wt[:, 4 * H:])
-                    dxi = torch.empty(NT, Il, device=dh.device)
-                    ops.gemm_x6nt_256(dg2.view(NT, 8 * H), wt, wt[:0], dxi, nsplit=1)
-                elif Il >= 1024:
-                    dxi = torch.empty(NT, Il, device=dh.device)
-                    ops.gemm(NT, Il, 4 * H, [dg2, dg2[:, 4 * H:]], 8 * H, 1, [wf, wr], Il, 1,
-                             [dxi, dxi], Il, 1, ksplit=True, bf16=bf16)
-                else:
-                    hk = 2 * H                      # half of a direction's 4H gate columns
-                    sl = torch.empty(4, NT, Il, device=dh.device)
-                    ops.gemm(NT, Il, hk, [dg2[:, q * hk:] for q in range(4)], 8 * H, 1,
-                             [(wf if q < 2 else wr)[(q % 2) * hk:] for q in range(4)], Il, 1,
-                             [sl[q] for q in range(4)], Il, 1, bf16=bf16)
-                    dxi = ops.sum_slabs(sl, 4).view(NT, Il)
                 dh = dxi.view(N, T, Il)
                 dx = dh
         for gr in grads:

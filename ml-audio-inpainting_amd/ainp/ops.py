@@ -422,6 +422,9 @@ def gemm_x6_multi(problems):
 L0_BWD_X6R = os.environ.get("AINP_L0_BWD_X6R", "1") != "0"
 # AINP_PAIR_JOIN=1 (measured slower, 16.6 vs 16.1 ms C2 step, profiles/r03_ab1_*): the pair waits for the side stream's weight gradients
 PAIR_JOIN = os.environ.get("AINP_PAIR_JOIN", "0") == "1"
+# AINP_MAIN_FIRST=0: the BLSTM backward issues each layer's data gradient after
+# the side stream's weight-gradient launches (the round-3 order); default: before
+MAIN_FIRST = os.environ.get("AINP_MAIN_FIRST", "1") != "0"
 # the fp32 layer-0 projection on the split-plane tile (AINP_X6R_FWD=0: on
 # gemm_x6nt_256; 1.73 vs 2.15 ms alone, profiles/r03_x6r_probe.log)
 # (bit-identical to gemm_x6nt_256)

@@ -767,20 +767,28 @@ def test_cast_bf16_t_and_ntcf_bf16_bridge_bit_exact():
     ref = x.to(torch.bfloat16)
     assert torch.equal(out, ref) and torch.equal(outT, ref.T)
     assert torch.equal(wide[:, 320:620], ref.T) and not wide[:, :320].any()
-    N, C, H, W = 2, 64, 9, 12
-    y = torch.randn(N, C, H, W, generator=g).cuda()
-    sc = torch.rand(C, generator=g).cuda() + 0.5
-    sh = torch.randn(C, generator=g).cuda() * 0.1
-    X16, XT16 = ops.bn_relu_apply_ntcf_bf16(y, sc, sh)
-    z = torch.relu(y * sc[None, :, None, None] + sh[None, :, None, None])
-    # fmaf vs torch's separate mul+add can differ by one fp32 rounding: compare
-    # against both roundings of the fused value
-    zf = torch.relu(torch.addcmul(sh[None, :, None, None], y, sc[None, :, None, None]))
-    xr = z.permute(0, 3, 1, 2).reshape(N, W, C * H)
-    xf = zf.permute(0, 3, 1, 2).reshape(N, W, C * H)
-    ok = (X16 == xr.to(torch.bfloat16)) | (X16 == xf.to(torch.bfloat16))
-    assert bool(ok.all())
-    assert torch.equal(XT16, X16.reshape(N * W, C * H).T)
+    # k / w tails of both tilings (64 x 64 and 128 x 128): C*H = 576 and 320,
+    # W = 12 and 134, odd N (X^T rows start at odd multiples of W)
+    for N, C, H, W in ((2, 64, 9, 12), (3, 64, 5, 134)):
+        y = torch.randn(N, C, H, W, generator=g).cuda()
+        sc = torch.rand(C, generator=g).cuda() + 0.5
+        sh = torch.randn(C, generator=g).cuda() * 0.1
+        X16, XT16 = ops.bn_relu_apply_ntcf_bf16(y, sc, sh)
+        z = torch.relu(y * sc[None, :, None, None] + sh[None, :, None, None])
+        # fmaf vs torch's separate mul+add can differ by one fp32 rounding: compare
+        # against both roundings of the fused value
+        zf = torch.relu(torch.addcmul(sh[None, :, None, None], y, sc[None, :, None, None]))
+        # and the single rounding of fmaf itself (the fp32 product is exact in
+        # float64): near-cancelling y*sc + sh differ by more than one ulp
+        zd = torch.relu(y.double() * sc.double()[None, :, None, None]
+                        + sh.double()[None, :, None, None]).float()
+        xr = z.permute(0, 3, 1, 2).reshape(N, W, C * H)
+        xf = zf.permute(0, 3, 1, 2).reshape(N, W, C * H)
+        xd = zd.permute(0, 3, 1, 2).reshape(N, W, C * H)
+        ok = ((X16 == xr.to(torch.bfloat16)) | (X16 == xf.to(torch.bfloat16))
+              | (X16 == xd.to(torch.bfloat16)))
+        assert bool(ok.all())
+        assert torch.equal(XT16, X16.reshape(N * W, C * H).T)
 
 
 def test_bf16_layer0_operand_path_matches_staged_bf16_path():
@@ -971,3 +979,4 @@ def test_gemm_x6_multi_rejects_bad_extents(ops):
     p = ops.x6_problem(A, B, C, M=300, N=256, K=64, lda=64, ldb=64, ldc=256)
     with pytest.raises(RuntimeError):
         ops.gemm_x6_multi([p] * 4)
+
