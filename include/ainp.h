@@ -314,6 +314,14 @@ int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
  * models/CNNBLSTM/model.py:35-60); BatchNorm statistics, biases and outputs
  * stay fp32.  The 1 <-> 16 channel convs stay fp32 (HBM-bound). */
 #define AINP_CONV_BF16 2
+/* With AINP_CONV_BF16, data / weight gradients only: dy holds bf16 values
+ * (uint16 storage, passed through the float* argument) -- the bf16
+ * configuration's BatchNorm-backward outputs (ainp_bn_relu_bwd_apply_ex with
+ * AINP_BN_GY16), which these kernels round to bf16 anyway, so dx and dw are
+ * those of fp32 dy (dbias sums the stored bf16 values).  Supported by the
+ * pairs with split-bf16 kernels (16/32/64 channels); other pairs return an
+ * error. */
+#define AINP_CONV_DY16 4
 int ainp_conv3x3_fwd_ex(const float* x, const float* w, const float* bias,
                         const float* in_scale, const float* in_shift, float* y,
                         double* stats, int64_t N, int Cin, int Cout, int64_t H,
@@ -325,6 +333,9 @@ int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
                           const float* in_shift, const float* dy, float* dw,
                           float* dbias, void* workspace, int64_t N, int Cin,
                           int Cout, int64_t H, int64_t W, int flags, void* stream);
+/* 1 if both ainp_conv3x3_dgrad_ex and ainp_conv3x3_wgrad_ex of this
+ * nn.Conv2d(Cin, Cout) accept AINP_CONV_BF16 | AINP_CONV_DY16 (host-only). */
+int ainp_conv3x3_dy16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
 
 /* ------------------------------------------------------------------------ */
 /* BatchNorm2d (training statistics) + ReLU                                   */
@@ -378,6 +389,17 @@ int ainp_bn_relu_bwd_apply(const float* g, const float* y, const float* scale,
                            int64_t count, float* gy, float* dgamma,
                            float* dbeta, int64_t N, int C, int64_t H,
                            int64_t W, int g_ntcf, void* stream);
+/* Step 2 with flags: AINP_BN_GY16 writes gy as bf16 (nearest-even, uint16
+ * storage) -- the bf16 configuration, whose data / weight gradient kernels
+ * round gy to bf16 when staging it (ainp_conv3x3_dgrad_ex / _wgrad_ex with
+ * AINP_CONV_DY16 read that storage; see ainp_conv3x3_dy16_ok). */
+#define AINP_BN_GY16 1
+int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale,
+                              const float* shift, const float* gamma,
+                              const float* save_mean_rstd, const double* sums,
+                              int64_t count, void* gy, float* dgamma, float* dbeta,
+                              int64_t N, int C, int64_t H, int64_t W, int g_ntcf, int flags,
+                              void* stream);
 
 /* bf16 configuration (BASELINE C3): the encoder's last BN+ReLU writes the
  * layer-0 LSTM input directly as bf16 (nearest-even) in both layouts the

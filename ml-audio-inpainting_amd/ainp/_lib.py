@@ -77,6 +77,9 @@ _SIGS = {
                                         c_int64, c_int, P]),
     "ainp_bn_relu_bwd_apply": (c_int, [P, P, P, P, P, P, P, c_int64, P, P, P, c_int64, c_int,
                                        c_int64, c_int64, c_int, P]),
+    "ainp_bn_relu_bwd_apply_ex": (c_int, [P, P, P, P, P, P, P, c_int64, P, P, P, c_int64, c_int,
+                                          c_int64, c_int64, c_int, c_int, P]),
+    "ainp_conv3x3_dy16_ok": (c_int, [c_int64, c_int, c_int, c_int64, c_int64]),
     "ainp_lstm_rec_fwd": (c_int, [P, PP, P, P, P, c_int64, c_int64, c_int, P]),
     "ainp_lstm_rec_bwd": (c_int, [P, P, P, PP, P, c_int64, c_int64, c_int, P]),
     "ainp_lstm_hprev": (c_int, [P, P, c_int64, c_int64, c_int, P]),

@@ -156,8 +156,12 @@ class _ConvStackFn(torch.autograd.Function):
                 cnt = ctx.count
                 if ctx.count_dev is not None:
                     sums, cnt = torch.cat([sums, ctx.count_dev]), 0
+                # bf16 configuration: gy in bf16 storage where this conv's data
+                # and weight gradients take it (they round it to bf16 anyway)
+                gy16 = ctx.bf16 and GY16 and ops.dy16_ok(y.shape[0], w.shape[1], w.shape[0],
+                                                         y.shape[2], y.shape[3])
                 gy, dgam, dbet = ops.bn_relu_bwd_apply(g, y, sc, sh, params[p0 + 2], sv, sums,
-                                                       cnt, ntcf)
+                                                       cnt, ntcf, gy16=gy16)
                 grads[p0 + 2], grads[p0 + 3] = dgam, dbet
             else:
                 gy = g.view_as(y) if g.shape != y.shape else g
@@ -207,6 +211,11 @@ class _ConvStackFn(torch.autograd.Function):
                 if bi == 0:
                     gx = g
         return (gx, None, None, None, None, None, None, None, *grads)
+
+
+# bf16 configuration: BatchNorm-backward outputs in bf16 storage (AINP_GY16=0:
+# fp32, as before; the conv results are the same bit for bit)
+GY16 = os.environ.get("AINP_GY16", "1") != "0"
 
 
 def _l0_bf16_ok(y):

@@ -178,6 +178,8 @@ GEMM_EXACT = os.environ.get("AINP_GEMM_EXACT", "0") == "1"
 GEMM_EXACT_F32 = 1
 GEMM_BF16 = 2          # include/ainp.h AINP_GEMM_BF16
 CONV_BF16 = 2          # include/ainp.h AINP_CONV_BF16
+CONV_DY16 = 4          # AINP_CONV_DY16: dy in bf16 storage (data / weight gradients)
+BN_GY16 = 1            # AINP_BN_GY16: BatchNorm-backward output gy in bf16 storage
 
 
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
@@ -640,18 +642,30 @@ def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf
     return y, stats
 
 
+def _dy_flags(dy, bf16):
+    if dy.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError(f"dy must be float32 or bfloat16, got {dy.dtype}")
+    if dy.dtype == torch.bfloat16:
+        if not bf16:
+            raise ValueError("a bf16 dy needs the bf16 conv arithmetic (bf16=True)")
+        return CONV_BF16 | CONV_DY16
+    return CONV_BF16 if bf16 else 0
+
+
 def conv3x3_dgrad(dy, w, bf16=False):
-    _req(dy, "dy"); _req(w, "w")
+    """dy fp32, or bf16 storage with bf16=True (AINP_CONV_DY16)."""
+    _req(dy, "dy", None); _req(w, "w")
     N, Cout, H, W = dy.shape
     Cin = w.shape[1]
     dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=torch.float32)
-    _T.conv3x3_dgrad(dy, w, dx, CONV_BF16 if bf16 else 0)
+    _T.conv3x3_dgrad(dy, w, dx, _dy_flags(dy, bf16))
     return dx
 
 
 def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False, out=None):
-    """out: optional preallocated (dw, db) to write."""
-    _req(x, "x"); _req(dy, "dy")
+    """out: optional preallocated (dw, db) to write.  dy fp32, or bf16 storage
+    with bf16=True (AINP_CONV_DY16)."""
+    _req(x, "x"); _req(dy, "dy", None)
     N, Cin, H, W = x.shape
     Cout = dy.shape[1]
     if out is not None:
@@ -661,7 +675,7 @@ def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=Fals
         db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
     ws_bytes = _lib.lib.ainp_conv3x3_wgrad_workspace(N, Cin, Cout, H, W)
     ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
-    _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws, CONV_BF16 if bf16 else 0)
+    _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws, _dy_flags(dy, bf16))
     return dw, db
 
 
@@ -721,14 +735,23 @@ def bn_relu_bwd_reduce(g, y, scale, shift, save, ntcf=False):
     return sums
 
 
-def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False):
+def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False, gy16=False):
+    """gy16: gy in bf16 storage (AINP_BN_GY16) -- for the bf16 configuration's
+    data / weight gradients, which round gy to bf16 anyway (conv3x3_dgrad /
+    conv3x3_wgrad take it with bf16=True; dy16_ok says for which convs)."""
     N, C, H, W = y.shape
-    gy = torch.empty_like(y)
+    gy = torch.empty(y.shape, device=y.device, dtype=torch.bfloat16 if gy16 else torch.float32)
     dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
     _T.bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, int(count), gy, dgamma, dbeta,
-                         bool(ntcf))
+                         bool(ntcf), BN_GY16 if gy16 else 0)
     return gy, dgamma, dbeta
+
+
+def dy16_ok(N, Cin, Cout, H, W) -> bool:
+    """ainp_conv3x3_dy16_ok: the data and weight gradients of Conv2d(Cin, Cout)
+    take a bf16 dy (bf16 configuration)."""
+    return bool(_lib.lib.ainp_conv3x3_dy16_ok(N, Cin, Cout, H, W))
 
 
 def bn_relu_bwd(g, y, scale, shift, gamma, save, ntcf=False):

@@ -170,6 +170,26 @@ __global__ void bn_bwd_sum_kernel(const double* __restrict__ partial, int N,
   }
 }
 
+// BatchNorm-backward output stores: fp32, or bf16 (GY16, nearest-even: the
+// bf16 configuration's gy, which its consumers round to bf16 anyway)
+template <bool GY16>
+__device__ __forceinline__ void gy_st2(void* gy, int64_t e, float a, float b) {   // e even
+  if constexpr (GY16) {
+    const uint32_t lo = __builtin_bit_cast(uint16_t, (__bf16)a);
+    const uint32_t hi = __builtin_bit_cast(uint16_t, (__bf16)b);
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<uint16_t*>(gy) + e) = lo | (hi << 16);
+  } else {
+    *reinterpret_cast<float2*>(reinterpret_cast<float*>(gy) + e) = make_float2(a, b);
+  }
+}
+template <bool GY16>
+__device__ __forceinline__ void gy_st1(void* gy, int64_t e, float a) {
+  if constexpr (GY16)
+    reinterpret_cast<uint16_t*>(gy)[e] = __builtin_bit_cast(uint16_t, (__bf16)a);
+  else
+    reinterpret_cast<float*>(gy)[e] = a;
+}
+
 // ---------------------------------------------------------- flat NCHW path
 // g and y both NCHW: a block owns BN_CHUNK contiguous elements of one (n, c)
 // plane -- float2 loads/stores straight from HBM, no LDS staging.  The
@@ -225,11 +245,11 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_flat(
   }
 }
 
-template <bool VEC>
+template <bool VEC, bool GY16 = false>
 __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
-    const float* __restrict__ save, const double* __restrict__ sums, float* __restrict__ gy,
+    const float* __restrict__ save, const double* __restrict__ sums, void* __restrict__ gy,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int C, int64_t HW, int chunks,
     double inv_count) {
   if (blockIdx.x < (unsigned)C && threadIdx.x == 0) {
@@ -250,7 +270,6 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
   if (VEC) {
     const float2* g2 = reinterpret_cast<const float2*>(g + off);
     const float2* y2 = reinterpret_cast<const float2*>(y + off);
-    float2* o2 = reinterpret_cast<float2*>(gy + off);
 #pragma unroll
     for (int i = 0; i < BN_CHUNK / 512; ++i) {
       const int e = threadIdx.x + 256 * i;
@@ -258,17 +277,15 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
         const float2 gv = g2[e], yv = y2[e];
         const float gz0 = fmaf(yv.x, sc, sh) > 0.f ? gv.x : 0.f;
         const float gz1 = fmaf(yv.y, sc, sh) > 0.f ? gv.y : 0.f;
-        float2 r;
-        r.x = k * (gz0 - m1 - ((yv.x - mean) * rstd) * m2);
-        r.y = k * (gz1 - m1 - ((yv.y - mean) * rstd) * m2);
-        o2[e] = r;
+        gy_st2<GY16>(gy, off + 2 * e, k * (gz0 - m1 - ((yv.x - mean) * rstd) * m2),
+                     k * (gz1 - m1 - ((yv.y - mean) * rstd) * m2));
       }
     }
   } else {
     for (int e = threadIdx.x; e < len; e += 256) {
       const float yv = y[off + e];
       const float gz = fmaf(yv, sc, sh) > 0.f ? g[off + e] : 0.f;
-      gy[off + e] = k * (gz - m1 - ((yv - mean) * rstd) * m2);
+      gy_st1<GY16>(gy, off + e, k * (gz - m1 - ((yv - mean) * rstd) * m2));
     }
   }
 }
@@ -318,12 +335,12 @@ __global__ __launch_bounds__(256) void bn_relu_apply_ntcf(const float* __restric
   }
 }
 
-template <bool APPLY>
+template <bool APPLY, bool GY16 = false>
 __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
     const float* __restrict__ save, const double* __restrict__ sums, double* __restrict__ partial,
-    float* __restrict__ gy, float* __restrict__ dgamma, float* __restrict__ dbeta, int C,
+    void* __restrict__ gy, float* __restrict__ dgamma, float* __restrict__ dbeta, int C,
     int64_t H, int64_t W, double inv_count) {
   __shared__ float tile[NT_T][NT_T + 1];   // g as [w][h]
   __shared__ double red[2][4];
@@ -361,7 +378,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
       const int64_t h = h0 + q + 4 * i, w = w0 + lane;
       if (h < H && w < W) {
         const float gz = fmaf(yv[i], sc, sh) > 0.f ? tile[lane][q + 4 * i] : 0.f;
-        gy[off + h * W + w] = k * (gz - m1 - ((yv[i] - mean) * rstd) * m2);
+        gy_st1<GY16>(gy, off + h * W + w, k * (gz - m1 - ((yv[i] - mean) * rstd) * m2));
       }
     }
   } else {
@@ -435,10 +452,11 @@ __global__ __launch_bounds__(256) void bn_relu_apply_ntcf2(const float* __restri
   }
 }
 
+template <bool GY16 = false>
 __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
-    const float* __restrict__ save, const double* __restrict__ sums, float* __restrict__ gy,
+    const float* __restrict__ save, const double* __restrict__ sums, void* __restrict__ gy,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int C, int64_t H, int64_t W,
     double inv_count, int64_t ntiles) {
   __shared__ float tile[NT_T][NT_T + 1];   // g as [w][k]
@@ -469,7 +487,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
     yv[i] = w < W ? *reinterpret_cast<const float2*>(yn + k * W + w) : make_float2(0.f, 0.f);
   }
   __syncthreads();
-  float* gn = gy + (int64_t)n * K * W;
+  const int64_t gn = (int64_t)n * K * W;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     const int kk = r + 8 * i;
@@ -484,10 +502,8 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
     const float m2 = (float)(sums[C + c] * ic);
     const float gz0 = fmaf(yv[i].x, sc, sh) > 0.f ? tile[2 * l][kk] : 0.f;
     const float gz1 = fmaf(yv[i].y, sc, sh) > 0.f ? tile[2 * l + 1][kk] : 0.f;
-    float2 o;
-    o.x = kc * (gz0 - m1 - ((yv[i].x - mean) * rstd) * m2);
-    o.y = kc * (gz1 - m1 - ((yv[i].y - mean) * rstd) * m2);
-    *reinterpret_cast<float2*>(gn + k * W + w) = o;
+    gy_st2<GY16>(gy, gn + k * W + w, kc * (gz0 - m1 - ((yv[i].x - mean) * rstd) * m2),
+                 kc * (gz1 - m1 - ((yv[i].y - mean) * rstd) * m2));
   }
 }
 
@@ -688,6 +704,29 @@ extern "C" int ainp_bn_relu_bwd_reduce(const float* g, const float* y,
   return check_launch("bn_bwd_sum");
 }
 
+template <bool GY16>
+static int bn_bwd_apply_launch(const float* g, const float* y, const float* scale,
+                               const float* shift, const float* gamma,
+                               const float* save_mean_rstd, const double* sums, int64_t count,
+                               void* gy, float* dgamma, float* dbeta, int64_t N, int C, int64_t H,
+                               int64_t W, int g_ntcf, hipStream_t s);
+
+extern "C" int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale,
+                                         const float* shift, const float* gamma,
+                                         const float* save_mean_rstd, const double* sums,
+                                         int64_t count, void* gy, float* dgamma, float* dbeta,
+                                         int64_t N, int C, int64_t H, int64_t W, int g_ntcf,
+                                         int flags, void* stream) {
+  if (!g || !y || !scale || !shift || !save_mean_rstd || !sums || !gy ||
+      N < 1 || C < 1 || H < 1 || W < 1 || count < 0 || (flags & ~AINP_BN_GY16))
+    return record_msg("ainp_bn_relu_bwd_apply: bad argument");
+  if (flags & AINP_BN_GY16)
+    return bn_bwd_apply_launch<true>(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy,
+                                     dgamma, dbeta, N, C, H, W, g_ntcf, as_stream(stream));
+  return bn_bwd_apply_launch<false>(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy,
+                                    dgamma, dbeta, N, C, H, W, g_ntcf, as_stream(stream));
+}
+
 extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
                                       const float* scale, const float* shift,
                                       const float* gamma,
@@ -696,12 +735,18 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
                                       float* gy, float* dgamma, float* dbeta,
                                       int64_t N, int C, int64_t H, int64_t W,
                                       int g_ntcf, void* stream) {
-  if (!g || !y || !scale || !shift || !save_mean_rstd || !sums || !gy ||
-      N < 1 || C < 1 || H < 1 || W < 1 || count < 0)
-    return record_msg("ainp_bn_relu_bwd_apply: bad argument");
+  return ainp_bn_relu_bwd_apply_ex(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy,
+                                   dgamma, dbeta, N, C, H, W, g_ntcf, 0, stream);
+}
+
+template <bool GY16>
+static int bn_bwd_apply_launch(const float* g, const float* y, const float* scale,
+                               const float* shift, const float* gamma,
+                               const float* save_mean_rstd, const double* sums, int64_t count,
+                               void* gy, float* dgamma, float* dbeta, int64_t N, int C, int64_t H,
+                               int64_t W, int g_ntcf, hipStream_t s) {
   const int64_t blocks = N * C * tiles_per_plane(H, W);
   const double inv_count = count > 0 ? 1.0 / (double)count : 0.0;   // 0: sums[2C]
-  hipStream_t s = as_stream(stream);
   if (!g_ntcf) {
     const int64_t HW = H * W;
     const int chunks = (int)cdiv(HW, BN_CHUNK);
@@ -710,11 +755,11 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
     int64_t nb = N * C * chunks;
     if (nb < C) nb = C;   // the dgamma / dbeta writers
     if (vec)
-      hipLaunchKernelGGL(bn_relu_bwd_apply_flat<true>, dim3((unsigned)nb), dim3(256), 0, s, g, y,
+      hipLaunchKernelGGL((bn_relu_bwd_apply_flat<true, GY16>), dim3((unsigned)nb), dim3(256), 0, s, g, y,
                          scale, shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, HW,
                          chunks, inv_count);
     else
-      hipLaunchKernelGGL(bn_relu_bwd_apply_flat<false>, dim3((unsigned)nb), dim3(256), 0, s, g, y,
+      hipLaunchKernelGGL((bn_relu_bwd_apply_flat<false, GY16>), dim3((unsigned)nb), dim3(256), 0, s, g, y,
                          scale, shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, HW,
                          chunks, inv_count);
     return check_launch("bn_relu_bwd_apply_flat");
@@ -723,14 +768,14 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
   if (ntcf2_ok(C, H, W, {g, y, gy})) {
     const int64_t nt2 = N * (C * H / NT_T) * cdiv(W, NT_T);
     const int64_t nb2 = nt2 < C ? C : nt2;   // >= C blocks: the dgamma / dbeta writers
-    hipLaunchKernelGGL(bn_relu_bwd_apply_ntcf2, dim3((unsigned)nb2), dim3(256), 0, s, g, y, scale,
+    hipLaunchKernelGGL(bn_relu_bwd_apply_ntcf2<GY16>, dim3((unsigned)nb2), dim3(256), 0, s, g, y, scale,
                        shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W, inv_count,
                        nt2);
     return check_launch("bn_relu_bwd_apply_ntcf2");
   }
   int64_t nb = N * C * cdiv(H, NT_T) * cdiv(W, NT_T);
   if (nb < C) nb = C;
-  hipLaunchKernelGGL(bn_relu_bwd_ntcf<true>, dim3((unsigned)nb), dim3(256), 0, s, g, y, scale,
+  hipLaunchKernelGGL((bn_relu_bwd_ntcf<true, GY16>), dim3((unsigned)nb), dim3(256), 0, s, g, y, scale,
                      shift, gamma, save_mean_rstd, sums, nullptr, gy, dgamma, dbeta, C, H, W,
                      inv_count);
   return check_launch("bn_relu_bwd_apply_ntcf");

@@ -911,12 +911,14 @@ namespace ainp {
 int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W);
 int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W,
                           bool b16);
+bool conv_x6_dgrad16_ok(int Cin, int Cout, int64_t H, int64_t W);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s, bool b16);
+                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16);
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16);
+                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
+                   bool x16);
 
 // conv_x6.hip (fp32-accurate split-bf16 MFMA) serves every pair it has an
 // instantiation for unless AINP_CONV_EXACT=1 selects the exact f32 kernels.
@@ -961,7 +963,7 @@ template <bool DG>
 static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y,
                              double* stats, int64_t N, int Cin, int Cout,
-                             int64_t H, int64_t W, hipStream_t s, bool b16) {
+                             int64_t H, int64_t W, hipStream_t s, bool b16, bool x16 = false) {
   // partials [used, rows) of the BatchNorm statistics are zero
   auto zero_tail = [&](int64_t used) -> int {
     if (!stats) return AINP_OK;
@@ -972,16 +974,21 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                                   (size_t)(bound - used) * 2 * Cout * sizeof(double), s);
     return e == hipSuccess ? AINP_OK : record_error(e, "conv3x3 stats tail");
   };
+  static const char* kNo16 =
+      "conv3x3: AINP_CONV_DY16 needs a split-bf16 data-gradient kernel for this pair";
   if (small_pair(Cin, Cout)) {
+    if (x16) return record_msg(kNo16);
     const int rc = small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
     return rc ? rc : zero_tail(exact_stat_parts(N, H, W));
   }
   if (!conv_exact_env()) {
     int64_t parts = 0;
-    const int rc =
-        conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s, &parts, b16);
+    const int rc = conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
+                                  &parts, b16, x16);
+    if (rc == 2) return record_msg(kNo16);
     if (rc != 1) return rc ? rc : zero_tail(parts);
   }
+  if (x16) return record_msg(kNo16);
   {
     const int rc = zero_tail(exact_stat_parts(N, H, W));
     if (rc) return rc;
@@ -1011,6 +1018,11 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
 }
 
 static bool conv_flags_ok(int flags) { return (flags & ~AINP_CONV_BF16) == 0; }
+// data / weight gradients: dy may be bf16 storage (with the bf16 arithmetic)
+static bool conv_grad_flags_ok(int flags) {
+  return (flags & ~(AINP_CONV_BF16 | AINP_CONV_DY16)) == 0 &&
+         (!(flags & AINP_CONV_DY16) || (flags & AINP_CONV_BF16));
+}
 
 extern "C" int ainp_conv3x3_fwd_ex(const float* x, const float* w,
                                    const float* bias, const float* in_scale,
@@ -1043,13 +1055,13 @@ extern "C" int ainp_conv3x3_dgrad_ex(const float* dy, const float* w, float* dx,
                                      void* stream) {
   (void)workspace;
   if (!dy || !w || !dx || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
-      N > 65535 || !conv_flags_ok(flags))
+      N > 65535 || !conv_grad_flags_ok(flags))
     return record_msg("ainp_conv3x3_dgrad: bad argument");
   if (N == 0) return AINP_OK;
   // conv over dy (Cout channels) producing Cin channels, flipped weights
   return conv_fwd_dispatch<true>(dy, w, nullptr, nullptr, nullptr, dx, nullptr,
                                  N, Cout, Cin, H, W, as_stream(stream),
-                                 (flags & AINP_CONV_BF16) != 0);
+                                 (flags & AINP_CONV_BF16) != 0, (flags & AINP_CONV_DY16) != 0);
 }
 
 extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
@@ -1057,6 +1069,21 @@ extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
                                   int Cout, int64_t H, int64_t W,
                                   void* stream) {
   return ainp_conv3x3_dgrad_ex(dy, w, dx, workspace, N, Cin, Cout, H, W, 0, stream);
+}
+
+extern "C" int ainp_conv3x3_dy16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+  (void)N;
+  if (Cin < 1 || Cout < 1 || H < 1 || W < 1 || small_pair(Cin, Cout) || conv_exact_env())
+    return 0;
+  // weight gradient: one 32-channel pass on conv3x3_wgrad_x6(s) (conv_wgrad_x6_launch)
+  const bool fits =
+      (int64_t)H * W * 4 * (Cout > WG_CIMAX ? Cout : WG_CIMAX) < ((int64_t)1 << 31);
+  const int cp = wgrad_pass(Cin);
+  if (!fits || Cin > WG_CIMAX ||
+      !((cp == 32 && Cout == 16) || (cp == 16 && Cout == 32) || (cp == 32 && Cout == 64)))
+    return 0;
+  // data gradient: the conv over dy (Cout channels) producing Cin
+  return conv_x6_dgrad16_ok(Cout, Cin, H, W) ? 1 : 0;
 }
 
 extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
@@ -1085,14 +1112,19 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
                                      int64_t N, int Cin, int Cout, int64_t H,
                                      int64_t W, int flags, void* stream) {
   if (!x || !dy || !dw || !workspace || N < 1 || Cin < 1 || Cout < 1 ||
-      H < 1 || W < 1 || !conv_flags_ok(flags))
+      H < 1 || W < 1 || !conv_grad_flags_ok(flags))
     return record_msg("ainp_conv3x3_wgrad: bad argument");
   const bool b16 = (flags & AINP_CONV_BF16) != 0;
+  const bool g16 = (flags & AINP_CONV_DY16) != 0;
+  static const char* kNo16 =
+      "ainp_conv3x3_wgrad: AINP_CONV_DY16 needs a split-bf16 weight-gradient kernel for this pair";
   if ((in_scale == nullptr) != (in_shift == nullptr))
     return record_msg("ainp_conv3x3_wgrad: in_scale/in_shift must both be set");
-  if (small_pair(Cin, Cout))
+  if (small_pair(Cin, Cout)) {
+    if (g16) return record_msg(kNo16);
     return small_wgrad(x, in_scale, in_shift, dy, dw, dbias, workspace, N, Cin, Cout, H, W,
                        as_stream(stream));
+  }
   const int CT = wgrad_ct(Cout);
   if (CT > 4) return record_msg("ainp_conv3x3_wgrad: Cout > 64 unsupported");
   const int CTp = CT == 3 ? 4 : CT;  // kernel co-tiles (waves split evenly)
@@ -1126,8 +1158,9 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
     const int nblk_x6 = b16 ? WG_BLOCKS * conv_x6_occ16() : WG_BLOCKS;
     int rc = (fits && !conv_exact_env())
                  ? conv_wgrad_x6_launch(x, in_scale, in_shift, dy, partial, N, Cin, Cout, H, W,
-                                        ci0, cp, nblk_x6, s, b16)
+                                        ci0, cp, nblk_x6, s, b16, g16)
                  : 1;
+    if (rc == 1 && g16) return record_msg(kNo16);
     const int nblk = rc == 0 ? nblk_x6 : WG_BLOCKS;   // slabs the launch writes
     if (rc == 1) switch (key) {
       case 1616: AINP_WGT(16, 16); break;

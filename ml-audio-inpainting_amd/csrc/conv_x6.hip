@@ -56,6 +56,24 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wx6_rsrc(const float* p) {
 __device__ __forceinline__ float wx6_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
 }
+// Activation / gradient operands stored as fp32 or, G16, as bf16 (the bf16
+// configuration's BatchNorm-backward outputs, AINP_CONV_DY16): element size,
+// the buffer over element e0 of p, and one element load at byte offsets.
+template <bool G16>
+constexpr int act_es() { return G16 ? 2 : 4; }
+template <bool G16>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t act_rsrc(const float* p, int64_t e0) {
+  const char* b = reinterpret_cast<const char*>(p) + e0 * act_es<G16>();
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(b), (short)0, 0x7fffffff,
+                                           0x00020000);
+}
+template <bool G16>
+__device__ __forceinline__ float act_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+  if constexpr (G16)
+    return __uint_as_float((uint32_t)__builtin_amdgcn_raw_buffer_load_b16(r, voff, soff, 0) << 16);
+  else
+    return wx6_ld(r, voff, soff);
+}
 typedef __bf16 bf16x4c __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ uint32_t cx6_cvt_pk(float lo, float hi) {
@@ -113,7 +131,7 @@ __device__ __forceinline__ bf16x8c cx6_ld(const unsigned char* p) {
 
 // RPW output rows per wave: 2 (16-row tiles, one workgroup per CU) or 1
 // (8-row tiles: half the halo LDS, two workgroups per CU).
-template <int CI, int COP, bool DGRAD, int RPW, int NP>
+template <int CI, int COP, bool DGRAD, int RPW, int NP, bool G16 = false>
 __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -139,23 +157,23 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int64_t HW = (int64_t)H * W;
-  const float* xn = x + (int64_t)n * CI * HW;
+  constexpr int ES = act_es<G16>();
 
   float px[XI][8];
   // clamped-address buffer loads (selected to zero at commit); valid while a
   // sample's CI planes span < 2^31 bytes (the launcher checks)
   auto fetch = [&](int ci0) {
-    int plane = (int)(HW * 4);
+    int plane = (int)(HW * ES);
     asm volatile("" : "+s"(plane));
-    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(xn + (int64_t)ci0 * HW);
+    const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ci0) * HW);
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
       const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
-      const int vo = 8 * half * plane + (gr * W + gc) * 4;
+      const int vo = 8 * half * plane + (gr * W + gc) * ES;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
     }
   };
   auto commit = [&](int ci0) {
@@ -303,7 +321,8 @@ int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W) {
 
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16);
+                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
+                    bool x16);
 
 // Persistent-grid multiplier of the bf16 (NP = 1) kernels: their LDS (21-50
 // KB) and VGPR (48-80) footprints let 2-4x the fp32 kernels' workgroups stay
@@ -343,17 +362,32 @@ int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, i
   return 0;
 }
 
+// 1 if conv_x6_launch(dgrad = true, stats = nullptr, b16, x16) takes bf16 dy
+// for this (dy channels, dx channels) pair; mirrors its routing.
+bool conv_x6_dgrad16_ok(int Cin, int Cout, int64_t H, int64_t W) {
+  const int cop = Cout <= 32 ? 32 : 64;
+  static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
+  if (Cout > 64 || Cout < 16) return false;
+  if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31) &&
+      ((Cin == 16 && cop == 32) || (Cin == 32 && Cout == 16)))
+    return true;   // persistent x6p / x6q
+  return ((Cin == 32 && cop == 64) || (Cin == 64 && cop == 32)) &&
+         (int64_t)Cin * H * W * 4 < ((int64_t)1 << 31);   // tiled, 8-row tiles
+}
+
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16) {
+                   int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
+                   bool x16) {
   if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W, b16) == 0) return 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                   parts, b16);
+                                   parts, b16, x16);
     if (rc != 1) return rc;
   }
   if ((int64_t)Cin * H * W * 4 >= ((int64_t)1 << 31)) return 1;   // 32-bit buffer offsets
+  if (x16 && !(dgrad && !stats && b16)) return 2;   // bf16 operand storage: no such kernel
   *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
@@ -361,8 +395,12 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
   if (Cin == CIV && cop == COV) {                                                               \
     if (dgrad && !stats) {   /* 8-row tiles, two workgroups per CU (no BN partials) */           \
       const dim3 g8((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, 8), (unsigned)N);             \
-      hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV>), g8, dim3(cx6::NT), 0, s,  \
-                         x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                   \
+      if (NPV == 1 && x16)                                                                      \
+        hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV, true>), g8, dim3(cx6::NT), \
+                           0, s, x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);           \
+      else                                                                                      \
+        hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV>), g8, dim3(cx6::NT), 0, s, \
+                           x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                 \
     } else if (dgrad)                                                                           \
       hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 2, NPV>), grid, dim3(cx6::NT), 0, s, \
                          x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                   \
@@ -431,7 +469,7 @@ __device__ __forceinline__ int wx6_gswz(int px) {
   return (((px >> 1) & 1) << 2) | (((px >> 2) & 1) << 1) | (px & 1);
 }
 
-template <int CO, int NP>
+template <int CO, int NP, bool G16 = false>
 __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -514,14 +552,18 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
 #pragma unroll
       for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
     }
-    const __amdgpu_buffer_rsrc_t rg = wx6_rsrc(dy + (int64_t)n * CO * HW);
+    // dy: fp32 or bf16 storage (G16)
+    constexpr int GES = act_es<G16>();
+    int gplane = (int)(HW * GES);
+    asm volatile("" : "+s"(gplane));
+    const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * CO * HW);
     const int gr = wx6_clamp(f0 + gpx / TT, 0, H - 1), gc = wx6_clamp(t0 + gpx % TT, 0, W - 1);
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
       const int grp = (tid + NT * i) / NPX;
-      const int vo = 8 * grp * plane + (gr * W + gc) * 4;
+      const int vo = 8 * grp * gplane + (gr * W + gc) * GES;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) pg[i][c] = wx6_ld(rg, vo, c * plane);
+      for (int c = 0; c < 8; ++c) pg[i][c] = act_ld<G16>(rg, vo, c * gplane);
     }
   };
   auto commit = [&](int64_t tile) {
@@ -644,7 +686,7 @@ __device__ __forceinline__ int wx6s_swz(int px) {
   return ((px >> 1) & 1) | ((((px >> 2) ^ (px >> 3)) & 1) << 1);
 }
 
-template <int CP, int CO, int NP>
+template <int CP, int CO, int NP, bool G16 = false>
 __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -711,11 +753,15 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
 #pragma unroll
       for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
     }
-    const __amdgpu_buffer_rsrc_t rg = wx6_rsrc(dy + (int64_t)n * CO * HW);
+    // dy: fp32 or bf16 storage (G16)
+    constexpr int GES = act_es<G16>();
+    int gplane = (int)(HW * GES);
+    asm volatile("" : "+s"(gplane));
+    const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * CO * HW);
     const int gr = wx6_clamp(f0 + gpx / TT, 0, H - 1), gc = wx6_clamp(t0 + gpx % TT, 0, W - 1);
-    const int vo = 8 * (ggrp < GG ? ggrp : GG - 1) * plane + (gr * W + gc) * 4;
+    const int vo = 8 * (ggrp < GG ? ggrp : GG - 1) * gplane + (gr * W + gc) * GES;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) pg[c] = wx6_ld(rg, vo, c * plane);
+    for (int c = 0; c < 8; ++c) pg[c] = act_ld<G16>(rg, vo, c * gplane);
   };
   auto commit = [&](int64_t tile) {
     int n, f0, t0;
@@ -833,7 +879,7 @@ constexpr int XROW = HC * 32;            // halo row bytes per plane (16 bf16 pe
 constexpr int WROW = 9 * 32 + 16;        // weight row bytes per chunk and plane
 }  // namespace cxp
 
-template <int CI, int COP, bool DGRAD, int NT, int TR, int NP>
+template <int CI, int COP, bool DGRAD, int NT, int TR, int NP, bool G16 = false>
 __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -888,17 +934,18 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
   auto fetch = [&](int64_t tile, int ch) {
     int n, r0, c0;
     tile_coords(tile, n, r0, c0);
-    int plane = (int)(HW * 4);
+    constexpr int ES = act_es<G16>();
+    int plane = (int)(HW * ES);
     asm volatile("" : "+s"(plane));  // keep c * plane out of the loop
-    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * CI + ch * CK) * HW);
+    const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ch * CK) * HW);
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
       const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
-      const int vo = 8 * half * plane + (gr * W + gc) * 4;
+      const int vo = 8 * half * plane + (gr * W + gc) * ES;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
     }
   };
   auto commit = [&](int64_t tile, int ch) {
@@ -1066,7 +1113,7 @@ constexpr int XPLANE = HR * cxp::XROW;
 constexpr int XU = 2 * HR * cxp::HC;
 }  // namespace cxq
 
-template <int CI, bool DGRAD, int NP>
+template <int CI, bool DGRAD, int NP, bool G16 = false>
 __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -1116,17 +1163,18 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
   auto fetch = [&](int64_t tile, int ch) {
     int n, r0, c0;
     tile_coords(tile, n, r0, c0);
-    int plane = (int)(HW * 4);
+    constexpr int ES = act_es<G16>();
+    int plane = (int)(HW * ES);
     asm volatile("" : "+s"(plane));
-    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * CI + ch * CK) * HW);
+    const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ch * CK) * HW);
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
       const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
-      const int vo = 8 * half * plane + (gr * W + gc) * 4;
+      const int vo = 8 * half * plane + (gr * W + gc) * ES;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
     }
   };
   auto commit = [&](int64_t tile, int ch) {
@@ -1271,13 +1319,18 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
 // has no instantiation.
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
-                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16) {
+                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
+                    bool x16) {
   const int cop = Cout <= 32 ? 32 : 64;
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
 #define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                      \
   if (dgrad == DG && Cin == CIV && cop == COV) {                                                 \
     const int g2 = b16 ? (G) * conv_x6_occ16() : (G);                                            \
-    if (b16)                                                                                     \
+    if (b16 && x16 && DG)                                                                        \
+      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 1, true>), dim3(g2),       \
+                         dim3(NTV), 0, s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H,   \
+                         (int)W);                                                                \
+    else if (b16)                                                                                \
       hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 1>), dim3(g2), dim3(NTV), 0, \
                          s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);         \
     else                                                                                         \
@@ -1290,15 +1343,16 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
   AINP_X6P(16, 32, false, 512, 512, 8) AINP_X6P(16, 32, true, 512, 512, 8)
   if (Cin == 32 && Cout == 16) {   // two workgroups per CU (65 KB of LDS; bf16: more)
     const int gq = b16 ? 512 * conv_x6_occ16() : 512;
-#define AINP_X6Q(DG, NPV)                                                                        \
-  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV>), dim3(gq), dim3(512), 0, s, x, w, bias,   \
-                     sc, sh, y, stats, (int)N, Cout, (int)H, (int)W)
+#define AINP_X6Q(DG, NPV, X16V)                                                                  \
+  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV, X16V>), dim3(gq), dim3(512), 0, s, x, w,   \
+                     bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W)
     if (dgrad) {
-      if (b16) AINP_X6Q(true, 1);
-      else AINP_X6Q(true, 3);
+      if (b16 && x16) AINP_X6Q(true, 1, true);
+      else if (b16) AINP_X6Q(true, 1, false);
+      else AINP_X6Q(true, 3, false);
     } else {
-      if (b16) AINP_X6Q(false, 1);
-      else AINP_X6Q(false, 3);
+      if (b16) AINP_X6Q(false, 1, false);
+      else AINP_X6Q(false, 3, false);
     }
 #undef AINP_X6Q
     *parts = gq;
@@ -1314,10 +1368,13 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
 // instantiation; returns 1 if not handled.  grid = persistent workgroups.
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s, bool b16) {
+                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16) {
 #define AINP_WX6S(CPV, COV)                                                                 \
   do {                                                                                      \
-    if (b16)                                                                                \
+    if (b16 && g16)                                                                         \
+      hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, 1, true>), dim3(grid), dim3(384), 0, s, \
+                         x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);         \
+    else if (b16)                                                                           \
       hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, 1>), dim3(grid), dim3(384), 0, s, x, sc, \
                          sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);                \
     else                                                                                    \
@@ -1329,7 +1386,10 @@ int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const
   if (cp == 16 && Cout == 32) AINP_WX6S(16, 32);
 #undef AINP_WX6S
   if (cp != 32 || Cout != 64) return 1;
-  if (b16)
+  if (b16 && g16)
+    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 1, true>), dim3(grid), dim3(384), 0, s, x, sc, sh,
+                       dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+  else if (b16)
     hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 1>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
                        partial, (int)N, Cin, (int)H, (int)W, ci0);
   else

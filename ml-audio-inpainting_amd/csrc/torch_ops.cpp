@@ -232,7 +232,10 @@ void conv3x3_dgrad(const Tensor& dy, const Tensor& w, const Tensor& dx, int64_t 
               "conv3x3_dgrad: dy [N,Cout,H,W], w [Cout,Cin,3,3]");
   const int64_t N = dy.size(0), Cout = dy.size(1), H = dy.size(2), W = dy.size(3), Cin = w.size(1);
   numel_is(dx, N * Cin * H * W, "dx");
-  chk(ainp_conv3x3_dgrad_ex(dev(dy, "dy"), dev(w, "w"), dev(dx, "dx"), nullptr, N, (int)Cin,
+  const float* dyp = (flags & AINP_CONV_DY16)
+                         ? reinterpret_cast<const float*>(dev<c10::BFloat16>(dy, "dy", at::kBFloat16))
+                         : dev(dy, "dy");
+  chk(ainp_conv3x3_dgrad_ex(dyp, dev(w, "w"), dev(dx, "dx"), nullptr, N, (int)Cin,
                             (int)Cout, H, W, (int)flags, stream_of(dy)),
       "conv3x3_dgrad_ex");
 }
@@ -247,8 +250,11 @@ void conv3x3_wgrad(const Tensor& x, const OptT& in_scale, const OptT& in_shift, 
   numel_is(dw, Cout * Cin * 9, "dw");
   TORCH_CHECK((size_t)workspace.nbytes() >= ainp_conv3x3_wgrad_workspace(N, (int)Cin, (int)Cout, H, W),
               "conv3x3_wgrad workspace too small");
+  const float* dyp = (flags & AINP_CONV_DY16)
+                         ? reinterpret_cast<const float*>(dev<c10::BFloat16>(dy, "dy", at::kBFloat16))
+                         : dev(dy, "dy");
   chk(ainp_conv3x3_wgrad_ex(dev(x, "x"), opt(in_scale, "in_scale"), opt(in_shift, "in_shift"),
-                            dev(dy, "dy"), dev(dw, "dw"), opt(dbias, "dbias"),
+                            dyp, dev(dw, "dw"), opt(dbias, "dbias"),
                             workspace.data_ptr(), N, (int)Cin, (int)Cout, H, W, (int)flags,
                             stream_of(x)),
       "conv3x3_wgrad_ex");
@@ -327,19 +333,23 @@ void bn_relu_bwd_reduce(const Tensor& g, const Tensor& y, const Tensor& scale, c
 
 void bn_relu_bwd_apply(const Tensor& g, const Tensor& y, const Tensor& scale, const Tensor& shift,
                        const OptT& gamma, const Tensor& save, const Tensor& sums, int64_t count,
-                       const Tensor& gy, const OptT& dgamma, const OptT& dbeta, bool ntcf) {
+                       const Tensor& gy, const OptT& dgamma, const OptT& dbeta, bool ntcf,
+                       int64_t flags) {
   GUARD(y);
   TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
   numel_is(g, y.numel(), "g");
   numel_is(gy, y.numel(), "gy");
   TORCH_CHECK(sums.numel() >= 2 * C + (count == 0 ? 1 : 0), "sums too short");
-  chk(ainp_bn_relu_bwd_apply(dev(g, "g"), dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"),
-                             opt(gamma, "gamma"), dev(save, "save"),
-                             dev<double>(sums, "sums", at::kDouble), count, dev(gy, "gy"),
-                             opt(dgamma, "dgamma"), opt(dbeta, "dbeta"), N, (int)C, H, W,
-                             ntcf ? 1 : 0, stream_of(y)),
-      "bn_relu_bwd_apply");
+  // AINP_BN_GY16: gy is bf16 storage
+  void* gyp = (flags & AINP_BN_GY16) ? (void*)dev<c10::BFloat16>(gy, "gy", at::kBFloat16)
+                                     : (void*)dev(gy, "gy");
+  chk(ainp_bn_relu_bwd_apply_ex(dev(g, "g"), dev(y, "y"), dev(scale, "scale"),
+                                dev(shift, "shift"), opt(gamma, "gamma"), dev(save, "save"),
+                                dev<double>(sums, "sums", at::kDouble), count, gyp,
+                                opt(dgamma, "dgamma"), opt(dbeta, "dbeta"), N, (int)C, H, W,
+                                ntcf ? 1 : 0, (int)flags, stream_of(y)),
+      "bn_relu_bwd_apply_ex");
 }
 
 // ------------------------------------------------------------------- BLSTM
@@ -1383,7 +1393,7 @@ TORCH_LIBRARY(ainp, m) {
         "Tensor(a!) workspace, Tensor(b!) sums, bool ntcf) -> ()");
   m.def("bn_relu_bwd_apply(Tensor g, Tensor y, Tensor scale, Tensor shift, Tensor? gamma, "
         "Tensor save, Tensor sums, int count, Tensor(a!) gy, Tensor(b!)? dgamma, "
-        "Tensor(c!)? dbeta, bool ntcf) -> ()");
+        "Tensor(c!)? dbeta, bool ntcf, int flags=0) -> ()");
   m.def("lstm_rec_fwd(Tensor zx, Tensor whh_f, Tensor whh_r, Tensor(a!) h_out, "
         "Tensor(b!)? gates, Tensor(c!)? cell, int H) -> ()");
   m.def("lstm_rec_bwd(Tensor dh_out, Tensor gates, Tensor cell, Tensor whh_f, Tensor whh_r, "

@@ -71,6 +71,24 @@ def test_bad_arguments_fail_without_launching():
                                    None)
     assert rc == -1 and b"gen_act_bwd" in _lib.lib.ainp_last_error()
     assert _lib.lib.ainp_bn_act_bwd_workspace(2, 64, 10000) == 2 * 64 * 3 * 16
+    # bf16 dy storage: refused without the bf16 arithmetic flag, before any launch
+    rc = _lib.lib.ainp_conv3x3_dgrad_ex(1, 1, 1, None, 1, 16, 32, 8, 8, 4, None)
+    assert rc == -1 and b"bad argument" in _lib.lib.ainp_last_error()
+    rc = _lib.lib.ainp_bn_relu_bwd_apply_ex(None, None, None, None, None, None, None, 1, None,
+                                            None, None, 1, 1, 1, 1, 0, 1, None)
+    assert rc == -1
+
+
+def test_dy16_routing_query():
+    """ainp_conv3x3_dy16_ok (host-only): the CNNBLSTM's 16/32/64-channel convs
+    take a bf16 dy in both gradients; the 1 <-> 16 channel ones (exact fp32
+    kernels) and passes wider than 32 input channels do not."""
+    from ainp import _lib
+    q = _lib.lib.ainp_conv3x3_dy16_ok
+    for cin, cout in ((16, 32), (32, 16), (32, 64)):
+        assert q(32, cin, cout, 257, 334) == 1, (cin, cout)
+    for cin, cout in ((1, 16), (16, 1), (64, 32), (8, 24)):
+        assert q(32, cin, cout, 257, 334) == 0, (cin, cout)
 
 
 def test_ops_refuse_cpu_tensors():
@@ -83,7 +101,7 @@ def test_ops_refuse_cpu_tensors():
 HOST_ONLY = {"ainp_abi_version", "ainp_build_target", "ainp_last_error", "ainp_reduce_workspace",
              "ainp_flac_info", "ainp_flac_decode", "ainp_flac_encode_bound", "ainp_flac_encode",
              "ainp_l1_pow10_loss_slots", "ainp_range_push", "ainp_range_pop", "ainp_mark",
-             "ainp_conv16_set_variant"}
+             "ainp_conv16_set_variant", "ainp_conv3x3_dy16_ok"}
 
 
 def test_torch_library_registers_every_gpu_entry_point():

@@ -501,7 +501,8 @@ def test_generator_and_discriminator_t1001_match_reference(golden_dir):
     m = G.PConvUNet().cuda().train()
     y = m(torch.from_numpy(g["x"]).cuda(), torch.from_numpy(g["mask"]).cuda())
     assert tuple(y.shape) == tuple(int(v) for v in g["y_shape"])
-    yf = y.cpu().numpy().reshape(-1)
+    # (with autograd on this is the generator's training forward, _PConvUNetFn)
+    yf = y.detach().cpu().numpy().reshape(-1)
     assert rel(yf[::97], g["y_sample"]) < TOL
     assert abs(np.linalg.norm(yf.astype(np.float64)) - g["y_norm"][0]) < TOL * g["y_norm"][0]
     sd = m.state_dict()

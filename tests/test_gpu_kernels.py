@@ -980,3 +980,58 @@ def test_gemm_x6_multi_rejects_bad_extents(ops):
     with pytest.raises(RuntimeError):
         ops.gemm_x6_multi([p] * 4)
 
+
+
+@pytest.mark.parametrize("Cin,Cout,H,W", [(16, 32, 37, 70), (32, 16, 37, 70), (32, 64, 37, 70)])
+def test_conv3x3_grads_take_bf16_dy_bit_exact(ops, Cin, Cout, H, W):
+    """bf16 configuration: the data / weight gradients read a bf16-stored dy
+    (AINP_CONV_DY16) and give exactly what they give for the same values in
+    fp32 (they round dy to bf16 when staging it), incl. the bias gradient."""
+    N = 3
+    g = torch.Generator(device=DEV).manual_seed(Cin + 7 * Cout)
+    dy16 = torch.randn(N, Cout, H, W, device=DEV, generator=g).to(torch.bfloat16)
+    dy32 = dy16.float()
+    x = torch.randn(N, Cin, H, W, device=DEV, generator=g)
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV, generator=g) * 0.2
+    sc = torch.rand(Cin, device=DEV, generator=g) + 0.5
+    sh = torch.randn(Cin, device=DEV, generator=g) * 0.3
+    assert ops.dy16_ok(N, Cin, Cout, H, W)
+    assert torch.equal(ops.conv3x3_dgrad(dy16, w, bf16=True), ops.conv3x3_dgrad(dy32, w, bf16=True))
+    dw16, db16 = ops.conv3x3_wgrad(x, dy16, sc, sh, bf16=True)
+    dw32, db32 = ops.conv3x3_wgrad(x, dy32, sc, sh, bf16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dw16, dw32) and torch.equal(db16, db32)
+    with pytest.raises(ValueError):
+        ops.conv3x3_dgrad(dy16, w)          # bf16 storage needs the bf16 arithmetic
+
+
+def test_conv3x3_bf16_dy_refused_where_no_kernel_reads_it(ops):
+    """The exact fp32 small-channel kernels have no bf16-dy path: an error, not
+    a silent misread."""
+    dy16 = torch.zeros(1, 16, 8, 8, device=DEV, dtype=torch.bfloat16)
+    w = torch.zeros(16, 1, 3, 3, device=DEV)
+    assert not ops.dy16_ok(1, 1, 16, 8, 8)
+    with pytest.raises(RuntimeError, match="DY16"):
+        ops.conv3x3_dgrad(dy16, w, bf16=True)
+
+
+@pytest.mark.parametrize("ntcf,C,H,W", [(False, 8, 37, 70), (True, 64, 37, 70), (True, 8, 37, 70)])
+def test_bn_relu_bwd_apply_bf16_output_is_rounded_fp32(ops, ntcf, C, H, W):
+    """AINP_BN_GY16: gy written as bf16 equals the fp32 gy rounded to nearest
+    even (flat, NTCF v2 (C*H % 64 == 0) and NTCF tile paths)."""
+    N = 2
+    g = torch.Generator(device=DEV).manual_seed(H + W)
+    y = torch.randn(N, C, H, W, device=DEV, generator=g) * 2 + 0.5
+    gg = torch.randn((N, W, C * H) if ntcf else (N, C, H, W), device=DEV, generator=g)
+    sc = torch.rand(C, device=DEV, generator=g) + 0.5
+    sh = torch.randn(C, device=DEV, generator=g) * 0.1
+    gam = torch.rand(C, device=DEV, generator=g) + 0.5
+    save = torch.cat([y.mean((0, 2, 3)), 1.0 / (y.var((0, 2, 3)) + 1e-5).sqrt()])
+    sums = ops.bn_relu_bwd_reduce(gg, y, sc, sh, save, ntcf)
+    gy32, dg32, db32 = ops.bn_relu_bwd_apply(gg, y, sc, sh, gam, save, sums, N * H * W, ntcf)
+    gy16, dg16, db16 = ops.bn_relu_bwd_apply(gg, y, sc, sh, gam, save, sums, N * H * W, ntcf,
+                                             gy16=True)
+    torch.cuda.synchronize()
+    assert gy16.dtype == torch.bfloat16
+    assert torch.equal(gy16, gy32.to(torch.bfloat16))
+    assert torch.equal(dg16, dg32) and torch.equal(db16, db32)

@@ -412,6 +412,43 @@ def test_bf16_c2_batch32_forward_backward_tracks_reference(golden_dir):
         assert e_n < bn and e_s < bs, (k, e_n, e_s, bn, bs)
 
 
+def test_bf16_gy_storage_is_bit_identical(monkeypatch):
+    """bf16 configuration: the BatchNorm-backward outputs stored as bf16
+    (cnnblstm.GY16, AINP_BN_GY16 / AINP_CONV_DY16) give the same step bit for
+    bit as fp32 storage -- their consumers, the 16/32/64-channel data and
+    weight gradients, round them to bf16 when staging them -- except the
+    bias gradients of those convs (sum of dy, now of the stored bf16 values):
+    BatchNorm-fed biases, whose exact gradient is 0."""
+    from ainp import cnnblstm
+    from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
+    from ainp.smoke import BN_FED_BIASES
+    cfg, (x, m, t, _) = _c2()
+    cfg = dict(cfg, accel={"dtype": "bf16"})
+    X, M, Tg = (torch.from_numpy(a[:8]).cuda() for a in (x, m, t))
+    runs, names = [], None
+    for gy16 in (False, True, False):
+        monkeypatch.setattr(cnnblstm, "GY16", gy16)
+        torch.manual_seed(0)
+        model = StackedBLSTMCNN(config=cfg).cuda().train()
+        loss = l1_pow10_loss(model(X.unsqueeze(1)), M, Tg)
+        loss.backward()
+        torch.cuda.synchronize()
+        names = ["loss"] + [k for k, _ in model.named_parameters()]
+        runs.append([loss.detach()] + [p.grad.detach().clone() for p in model.parameters()])
+    # the fp32-storage step is bit-reproducible (same inputs, same seed) ...
+    rep = [k for k, a, c in zip(names, runs[0], runs[2]) if not torch.equal(a, c)]
+    assert not rep, f"bf16 step not bit-reproducible: {rep}"
+    # ... and bf16 storage of gy does not change a bit of it
+    diff = [k for k, a, b in zip(names, runs[0], runs[1])
+            if k not in BN_FED_BIASES and not torch.equal(a, b)]
+    assert not diff, f"bf16 gy storage changed: {diff}"
+    grads = dict(zip(names, runs[1]))
+    for k in BN_FED_BIASES:
+        if k in grads:
+            wn = float(grads[k.replace("bias", "weight")].norm())
+            assert float(grads[k].abs().max()) <= 1e-2 * wn, k
+
+
 def test_hip_graph_replayed_curve_matches_reference(golden_dir):
     """The cnnblstm_curve.npz schedule with the training step captured once in
     a HIP graph (torch.cuda.CUDAGraph over the torch.ops.ainp launches) and
