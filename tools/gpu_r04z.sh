@@ -22,6 +22,7 @@ if [ "$PART" = A ]; then
   step 1100 pytest_gpu.log python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread; ok $? || exit 1
   step 300 smoke.log python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" || exit 1
 else
+  step 300 pytest_gy16.log python -u -m pytest tests/test_gpu_model.py -v -s --timeout 300 --timeout-method thread -k "gy_storage"; ok $? || exit 1
   step 400 bench.json python bench.py || exit 1
   step 300 bench_bf16.json python bench.py --dtype bf16 --no-cpu-baseline || exit 1
   step 300 bench_gan_c4.json python bench.py --workload gan --dtype bf16 --no-cpu-baseline || exit 1
