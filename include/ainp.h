@@ -322,6 +322,14 @@ int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
  * pairs with split-bf16 kernels (16/32/64 channels); other pairs return an
  * error. */
 #define AINP_CONV_DY16 4
+/* With AINP_CONV_BF16: forward, and the weight gradient's act(x) source: x
+ * holds bf16 values (uint16 storage through the float* argument) -- the bf16
+ * configuration's pre-BatchNorm activations, written by a forward with
+ * AINP_CONV_Y16 (y as bf16, nearest-even; its BatchNorm partials sum the
+ * stored values).  Supported by the pairs with persistent split-bf16
+ * forwards and split-bf16 weight gradients (ainp_conv3x3_io16_ok). */
+#define AINP_CONV_X16 8
+#define AINP_CONV_Y16 16
 int ainp_conv3x3_fwd_ex(const float* x, const float* w, const float* bias,
                         const float* in_scale, const float* in_shift, float* y,
                         double* stats, int64_t N, int Cin, int Cout, int64_t H,
@@ -336,6 +344,10 @@ int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
 /* 1 if both ainp_conv3x3_dgrad_ex and ainp_conv3x3_wgrad_ex of this
  * nn.Conv2d(Cin, Cout) accept AINP_CONV_BF16 | AINP_CONV_DY16 (host-only). */
 int ainp_conv3x3_dy16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
+/* 1 if ainp_conv3x3_fwd_ex of this nn.Conv2d(Cin, Cout) accepts AINP_CONV_X16
+ * and AINP_CONV_Y16 and its ainp_conv3x3_wgrad_ex accepts AINP_CONV_X16
+ * (host-only; with AINP_CONV_BF16). */
+int ainp_conv3x3_io16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
 
 /* ------------------------------------------------------------------------ */
 /* BatchNorm2d (training statistics) + ReLU                                   */
@@ -394,6 +406,14 @@ int ainp_bn_relu_bwd_apply(const float* g, const float* y, const float* scale,
  * round gy to bf16 when staging it (ainp_conv3x3_dgrad_ex / _wgrad_ex with
  * AINP_CONV_DY16 read that storage; see ainp_conv3x3_dy16_ok). */
 #define AINP_BN_GY16 1
+/* AINP_BN_Y16 (reduce / apply / the bf16 NTCF bridge): the pre-BN input y holds
+ * bf16 values (uint16 storage through the float* argument; a forward with
+ * AINP_CONV_Y16 wrote it). */
+#define AINP_BN_Y16 2
+int ainp_bn_relu_bwd_reduce_ex(const float* g, const float* y, const float* scale,
+                               const float* shift, const float* save_mean_rstd, void* workspace,
+                               double* sums, int64_t N, int C, int64_t H, int64_t W, int g_ntcf,
+                               int flags, void* stream);
 int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale,
                               const float* shift, const float* gamma,
                               const float* save_mean_rstd, const double* sums,
@@ -409,6 +429,10 @@ int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale
 int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale, const float* shift,
                                  uint16_t* out, uint16_t* outT, int64_t ld_t, int64_t N, int C,
                                  int64_t H, int64_t W, void* stream);
+/* flags: AINP_BN_Y16 (x in bf16 storage) */
+int ainp_bn_relu_apply_ntcf_bf16_ex(const float* x, const float* scale, const float* shift,
+                                    uint16_t* out, uint16_t* outT, int64_t ld_t, int64_t N,
+                                    int C, int64_t H, int64_t W, int flags, void* stream);
 
 /* ------------------------------------------------------------------------ */
 /* BLSTM recurrence (one layer, both directions), batch_first                */

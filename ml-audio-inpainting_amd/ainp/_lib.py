@@ -80,6 +80,9 @@ _SIGS = {
     "ainp_bn_relu_bwd_apply_ex": (c_int, [P, P, P, P, P, P, P, c_int64, P, P, P, c_int64, c_int,
                                           c_int64, c_int64, c_int, c_int, P]),
     "ainp_conv3x3_dy16_ok": (c_int, [c_int64, c_int, c_int, c_int64, c_int64]),
+    "ainp_conv3x3_io16_ok": (c_int, [c_int64, c_int, c_int, c_int64, c_int64]),
+    "ainp_bn_relu_bwd_reduce_ex": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int64, c_int64,
+                                           c_int, c_int, P]),
     "ainp_lstm_rec_fwd": (c_int, [P, PP, P, P, P, c_int64, c_int64, c_int, P]),
     "ainp_lstm_rec_bwd": (c_int, [P, P, P, PP, P, c_int64, c_int64, c_int, P]),
     "ainp_lstm_hprev": (c_int, [P, P, c_int64, c_int64, c_int, P]),
@@ -146,6 +149,8 @@ _SIGS = {
     "ainp_channel_sum": (c_int, [P, c_int64, c_int, c_int64, P, P]),
     "ainp_bn_relu_apply_ntcf_bf16": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, c_int64,
                                              c_int64, P]),
+    "ainp_bn_relu_apply_ntcf_bf16_ex": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, c_int64,
+                                                c_int64, c_int, P]),
     "ainp_gemm_bf16nt": (c_int, [c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P, c_int64,
                                  P, P, P, P, c_int64, c_int, c_int64, c_int64, P]),
     "ainp_cast_bf16_t": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P]),

@@ -66,11 +66,28 @@ class _ConvStackFn(torch.autograd.Function):
         # so ranks with uneven shards still normalise with the global count
         count = N * H * W
         count_dev = None
+        # bf16 configuration: pre-BN outputs in bf16 storage (the next conv's
+        # forward / weight gradient and the BatchNorm passes read them) where
+        # this conv and its consumer have the kernels for it
+        ws_, q = [], 0
+        for has_bn, _ in spec:
+            ws_.append(params[q])
+            q += 4 if has_bn else 2
+        l0_path = bool(spec) and l0_box is not None and _l0_bf16_ok(
+            (N, ws_[-1].shape[0], H, W))
         for bi, (has_bn, bn) in enumerate(spec):
             w, b = params[pi], params[pi + 1]
             pi += 2
             want_stats = has_bn and training
-            y, stats = ops.conv3x3_fwd(h, w, b, act[0], act[1], want_stats=want_stats, bf16=bf16)
+            y16 = False
+            if bf16 and Y16 and has_bn and ops.io16_ok(N, w.shape[1], w.shape[0], H, W):
+                if bi + 1 < len(spec):
+                    wn = ws_[bi + 1]
+                    y16 = ops.io16_ok(N, wn.shape[1], wn.shape[0], H, W)
+                else:
+                    y16 = l0_path          # the bf16 bridge to the LSTM reads it
+            y, stats = ops.conv3x3_fwd(h, w, b, act[0], act[1], want_stats=want_stats, bf16=bf16,
+                                       y16=y16)
             saved_y.append(y)
             if has_bn:
                 gamma, beta = params[pi], params[pi + 1]
@@ -216,14 +233,20 @@ class _ConvStackFn(torch.autograd.Function):
 # bf16 configuration: BatchNorm-backward outputs in bf16 storage (AINP_GY16=0:
 # fp32, as before; the conv results are the same bit for bit)
 GY16 = os.environ.get("AINP_GY16", "1") != "0"
+# bf16 configuration: pre-BatchNorm conv outputs in bf16 storage (AINP_Y16=0:
+# fp32, as before).  Unlike gy this is a rounding point of its own: the
+# BatchNorm statistics and the BatchNorm+ReLU that feeds the next conv see the
+# bf16 values (autocast's bf16 conv output); tests/golden/gen_golden_r04.py's
+# emulation rounds there too.
+Y16 = os.environ.get("AINP_Y16", "1") != "0"
 
 
 def _l0_bf16_ok(y):
     """Shapes the bf16 layer-0 operand path supports (ainp_bn_relu_apply_ntcf_bf16,
     ainp_gemm_bf16nt): C*F % 64 == 0, even T, N*T % 8 == 0 (k-contiguous rows
     of 16 bytes for the weight-gradient GEMM).  Otherwise the fp32-staged bf16
-    GEMM loop runs."""
-    N, C, F, T = y.shape
+    GEMM loop runs.  y: the encoder output or its (N, C, F, T) shape."""
+    N, C, F, T = y if isinstance(y, tuple) else y.shape
     return (C * F) % 64 == 0 and T % 2 == 0 and (N * T) % 8 == 0
 
 

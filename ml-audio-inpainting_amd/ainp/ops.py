@@ -179,7 +179,10 @@ GEMM_EXACT_F32 = 1
 GEMM_BF16 = 2          # include/ainp.h AINP_GEMM_BF16
 CONV_BF16 = 2          # include/ainp.h AINP_CONV_BF16
 CONV_DY16 = 4          # AINP_CONV_DY16: dy in bf16 storage (data / weight gradients)
+CONV_X16 = 8           # AINP_CONV_X16: the act(x) source in bf16 storage (fwd / wgrad)
+CONV_Y16 = 16          # AINP_CONV_Y16: forward output y in bf16 storage
 BN_GY16 = 1            # AINP_BN_GY16: BatchNorm-backward output gy in bf16 storage
+BN_Y16 = 2             # AINP_BN_Y16: the pre-BN input y in bf16 storage
 
 
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
@@ -255,13 +258,13 @@ def bn_relu_apply_ntcf_bf16(y, scale, shift):
     """ainp_bn_relu_apply_ntcf_bf16: relu(y*scale+shift) of the encoder's last
     block as bf16 X [N, W, C*H] and X^T [C*H, N*W] (row stride rounded up to 8
     elements, so every row starts 16-byte aligned)."""
-    _req(y, "y")
+    _req(y, "y", None)
     N, C, H, W = y.shape
     K, NW = C * H, N * W
     out = torch.empty(N, W, K, device=y.device, dtype=torch.bfloat16)
     ldt = -(-NW // 8) * 8
     outT = torch.empty(K, ldt, device=y.device, dtype=torch.bfloat16)[:, :NW]
-    _T.bn_relu_apply_ntcf_bf16(y, scale, shift, out, outT)
+    _T.bn_relu_apply_ntcf_bf16(y, scale, shift, out, outT, _y_flag(y))
     return out, outT
 
 
@@ -626,20 +629,44 @@ def conv_stat_parts(N, H, W) -> int:
     return _lib.lib.ainp_conv3x3_fwd_stat_parts(N, H, W)
 
 
-def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf16=False):
-    _req(x, "x"); _req(w, "w")
+def _x_flag(x, bf16, name="x"):
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError(f"{name} must be float32 or bfloat16, got {x.dtype}")
+    if x.dtype == torch.bfloat16 and not bf16:
+        raise ValueError(f"a bf16 {name} needs the bf16 conv arithmetic (bf16=True)")
+    return CONV_X16 if x.dtype == torch.bfloat16 else 0
+
+
+def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf16=False,
+                y16=False):
+    """x fp32, or bf16 storage with bf16=True (AINP_CONV_X16); y16: y written
+    as bf16 (AINP_CONV_Y16, BatchNorm partials of the stored values).  Both
+    where io16_ok says so (the bf16 configuration's pre-BN activations)."""
+    _req(x, "x", None); _req(w, "w")
     N, Cin, H, W = x.shape
     Cout = w.shape[0]
     assert tuple(w.shape) == (Cout, Cin, 3, 3)
-    y = torch.empty(N, Cout, H, W, device=x.device, dtype=torch.float32)
+    flags = (CONV_BF16 if bf16 else 0) | _x_flag(x, bf16)
+    if y16:
+        if not bf16:
+            raise ValueError("y16 needs the bf16 conv arithmetic (bf16=True)")
+        flags |= CONV_Y16
+    y = torch.empty(N, Cout, H, W, device=x.device,
+                    dtype=torch.bfloat16 if y16 else torch.float32)
     stats = None
     if want_stats:
         stats = torch.empty(_lib.lib.ainp_conv3x3_fwd_stat_rows_ex(N, Cin, Cout, H, W,
                                                                    CONV_BF16 if bf16 else 0),
                             2 * Cout,
                             device=x.device, dtype=torch.float64)
-    _T.conv3x3_fwd(x, w, b, in_scale, in_shift, y, stats, CONV_BF16 if bf16 else 0)
+    _T.conv3x3_fwd(x, w, b, in_scale, in_shift, y, stats, flags)
     return y, stats
+
+
+def io16_ok(N, Cin, Cout, H, W) -> bool:
+    """ainp_conv3x3_io16_ok: Conv2d(Cin, Cout)'s forward takes a bf16 act(x)
+    source and writes a bf16 y, and its weight gradient takes the bf16 source."""
+    return bool(_lib.lib.ainp_conv3x3_io16_ok(N, Cin, Cout, H, W))
 
 
 def _dy_flags(dy, bf16):
@@ -665,7 +692,7 @@ def conv3x3_dgrad(dy, w, bf16=False):
 def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False, out=None):
     """out: optional preallocated (dw, db) to write.  dy fp32, or bf16 storage
     with bf16=True (AINP_CONV_DY16)."""
-    _req(x, "x"); _req(dy, "dy", None)
+    _req(x, "x", None); _req(dy, "dy", None)
     N, Cin, H, W = x.shape
     Cout = dy.shape[1]
     if out is not None:
@@ -675,7 +702,7 @@ def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=Fals
         db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
     ws_bytes = _lib.lib.ainp_conv3x3_wgrad_workspace(N, Cin, Cout, H, W)
     ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
-    _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws, _dy_flags(dy, bf16))
+    _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws, _dy_flags(dy, bf16) | _x_flag(x, bf16))
     return dw, db
 
 
@@ -725,13 +752,20 @@ def bn_relu_apply(x, scale, shift, ntcf=False):
     return out
 
 
+def _y_flag(y):
+    if y.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError(f"y must be float32 or bfloat16, got {y.dtype}")
+    return BN_Y16 if y.dtype == torch.bfloat16 else 0
+
+
 def bn_relu_bwd_reduce(g, y, scale, shift, save, ntcf=False):
-    _req(g, "g"); _req(y, "y")
+    """y fp32 or bf16 storage (AINP_BN_Y16)."""
+    _req(g, "g"); _req(y, "y", None)
     N, C, H, W = y.shape
     ws = torch.empty(_lib.lib.ainp_bn_relu_bwd_workspace(N, C, H, W), device=y.device,
                      dtype=torch.uint8)
     sums = torch.empty(2 * C, device=y.device, dtype=torch.float64)
-    _T.bn_relu_bwd_reduce(g, y, scale, shift, save, ws, sums, bool(ntcf))
+    _T.bn_relu_bwd_reduce(g, y, scale, shift, save, ws, sums, bool(ntcf), _y_flag(y))
     return sums
 
 
@@ -744,7 +778,7 @@ def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False, 
     dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
     _T.bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, int(count), gy, dgamma, dbeta,
-                         bool(ntcf), BN_GY16 if gy16 else 0)
+                         bool(ntcf), (BN_GY16 if gy16 else 0) | _y_flag(y))
     return gy, dgamma, dbeta
 
 

@@ -170,6 +170,26 @@ __global__ void bn_bwd_sum_kernel(const double* __restrict__ partial, int N,
   }
 }
 
+// Pre-BatchNorm input y in fp32 or bf16 storage (YB16, AINP_BN_Y16: the bf16
+// configuration's conv outputs, AINP_CONV_Y16); e = element index (even for
+// the pair load).
+template <bool YB16>
+__device__ __forceinline__ float2 ld_y2(const float* y, int64_t e) {
+  if constexpr (YB16) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(y) + e);
+    return make_float2(__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u));
+  } else {
+    return *reinterpret_cast<const float2*>(y + e);
+  }
+}
+template <bool YB16>
+__device__ __forceinline__ float ld_y1(const float* y, int64_t e) {
+  if constexpr (YB16)
+    return __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(y)[e] << 16);
+  else
+    return y[e];
+}
+
 // BatchNorm-backward output stores: fp32, or bf16 (GY16, nearest-even: the
 // bf16 configuration's gy, which its consumers round to bf16 anyway)
 template <bool GY16>
@@ -196,7 +216,7 @@ __device__ __forceinline__ void gy_st1(void* gy, int64_t e, float a) {
 // partial layout [n][c][chunk] is what bn_bwd_sum_kernel reduces.
 constexpr int BN_CHUNK = 4096;
 
-template <bool VEC>
+template <bool VEC, bool YB16 = false>
 __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_flat(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ save, double* __restrict__ partial,
@@ -208,17 +228,16 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_flat(
   const int64_t o0 = (int64_t)ch * BN_CHUNK;
   const int len = (int)((HW - o0) < BN_CHUNK ? (HW - o0) : BN_CHUNK);
   const float* gp = g + plane * HW + o0;
-  const float* yp = y + plane * HW + o0;
+  const int64_t yo = plane * HW + o0;
   const float sc = scale[c], sh = shift[c], mean = save[c], rstd = save[C + c];
   float s1 = 0.f, s2 = 0.f;
   if (VEC) {
     const float2* g2 = reinterpret_cast<const float2*>(gp);
-    const float2* y2 = reinterpret_cast<const float2*>(yp);
 #pragma unroll
     for (int i = 0; i < BN_CHUNK / 512; ++i) {
       const int e = threadIdx.x + 256 * i;
       if (2 * e < len) {
-        const float2 gv = g2[e], yv = y2[e];
+        const float2 gv = g2[e], yv = ld_y2<YB16>(y, yo + 2 * e);
         const float gz0 = fmaf(yv.x, sc, sh) > 0.f ? gv.x : 0.f;
         const float gz1 = fmaf(yv.y, sc, sh) > 0.f ? gv.y : 0.f;
         s1 += gz0 + gz1;
@@ -227,7 +246,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_flat(
     }
   } else {
     for (int e = threadIdx.x; e < len; e += 256) {
-      const float yv = yp[e];
+      const float yv = ld_y1<YB16>(y, yo + e);
       const float gz = fmaf(yv, sc, sh) > 0.f ? gp[e] : 0.f;
       s1 += gz;
       s2 += gz * ((yv - mean) * rstd);
@@ -245,7 +264,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_flat(
   }
 }
 
-template <bool VEC, bool GY16 = false>
+template <bool VEC, bool GY16 = false, bool YB16 = false>
 __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
@@ -269,12 +288,11 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
   const float m2 = (float)(sums[C + c] * ic);
   if (VEC) {
     const float2* g2 = reinterpret_cast<const float2*>(g + off);
-    const float2* y2 = reinterpret_cast<const float2*>(y + off);
 #pragma unroll
     for (int i = 0; i < BN_CHUNK / 512; ++i) {
       const int e = threadIdx.x + 256 * i;
       if (2 * e < len) {
-        const float2 gv = g2[e], yv = y2[e];
+        const float2 gv = g2[e], yv = ld_y2<YB16>(y, off + 2 * e);
         const float gz0 = fmaf(yv.x, sc, sh) > 0.f ? gv.x : 0.f;
         const float gz1 = fmaf(yv.y, sc, sh) > 0.f ? gv.y : 0.f;
         gy_st2<GY16>(gy, off + 2 * e, k * (gz0 - m1 - ((yv.x - mean) * rstd) * m2),
@@ -283,7 +301,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
     }
   } else {
     for (int e = threadIdx.x; e < len; e += 256) {
-      const float yv = y[off + e];
+      const float yv = ld_y1<YB16>(y, off + e);
       const float gz = fmaf(yv, sc, sh) > 0.f ? g[off + e] : 0.f;
       gy_st1<GY16>(gy, off + e, k * (gz - m1 - ((yv - mean) * rstd) * m2));
     }
@@ -335,7 +353,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_ntcf(const float* __restric
   }
 }
 
-template <bool APPLY, bool GY16 = false>
+template <bool APPLY, bool GY16 = false, bool YB16 = false>
 __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
@@ -362,7 +380,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
 #pragma unroll
   for (int i = 0; i < 16; ++i) {            // y: lanes along w (NCHW rows)
     const int64_t h = h0 + q + 4 * i, w = w0 + lane;
-    yv[i] = (h < H && w < W) ? y[off + h * W + w] : 0.f;
+    yv[i] = (h < H && w < W) ? ld_y1<YB16>(y, off + h * W + w) : 0.f;
   }
 #pragma unroll
   for (int i = 0; i < 16; ++i) tile[q + 4 * i][lane] = gv[i];
@@ -452,7 +470,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_ntcf2(const float* __restri
   }
 }
 
-template <bool GY16 = false>
+template <bool GY16 = false, bool YB16 = false>
 __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
     const float* __restrict__ g, const float* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
@@ -479,12 +497,12 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
     tile[ww][2 * l] = v.x;
     tile[ww][2 * l + 1] = v.y;
   }
-  const float* yn = y + (int64_t)n * K * W;
+  const int64_t yn = (int64_t)n * K * W;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {                 // y: rows k, lanes along w
     const int64_t k = k0 + r + 8 * i;
     const int w = w0 + 2 * l;
-    yv[i] = w < W ? *reinterpret_cast<const float2*>(yn + k * W + w) : make_float2(0.f, 0.f);
+    yv[i] = w < W ? ld_y2<YB16>(y, yn + k * W + w) : make_float2(0.f, 0.f);
   }
   __syncthreads();
   const int64_t gn = (int64_t)n * K * W;
@@ -518,6 +536,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
 // (w, w+1) pairs of each row, the LDS tile the (k, k+1) pairs of each column,
 // packed bf16x2 both ways.
 constexpr int B2K = 128, B2W = 128;
+template <bool YB16 = false>
 __global__ __launch_bounds__(256) void bn_relu_apply_ntcf_bf16(
     const float* __restrict__ x, const float* __restrict__ scale, const float* __restrict__ shift,
     uint16_t* __restrict__ out, uint16_t* __restrict__ outT, int64_t ld_t, int C, int64_t H,
@@ -530,7 +549,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_ntcf_bf16(
   const int64_t k0 = ((b / tw) % tk) * B2K;
   const int n = (int)(b / ((int64_t)tw * tk));
   const int l = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const float* xn = x + (int64_t)n * K * W;
+  const int64_t xn = (int64_t)n * K * W;
   const int w = w0 + 2 * l;
   const bool wok = w < W;
   float2 v[16][2];
@@ -539,8 +558,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_ntcf_bf16(
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int64_t k = k0 + 2 * (q + 4 * i) + e;
-      v[i][e] = (wok && k < K) ? *reinterpret_cast<const float2*>(xn + k * W + w)
-                               : make_float2(0.f, 0.f);
+      v[i][e] = (wok && k < K) ? ld_y2<YB16>(x, xn + k * W + w) : make_float2(0.f, 0.f);
     }
   }
 #pragma unroll
@@ -647,23 +665,82 @@ extern "C" int ainp_bn_relu_apply(const float* x, const float* scale,
   return check_launch("bn_relu_apply");
 }
 
+extern "C" int ainp_bn_relu_apply_ntcf_bf16_ex(const float* x, const float* scale,
+                                               const float* shift, uint16_t* out, uint16_t* outT,
+                                               int64_t ld_t, int64_t N, int C, int64_t H,
+                                               int64_t W, int flags, void* stream) {
+  if (!x || !scale || !shift || !out || !outT || N < 1 || C < 1 || H < 1 || W < 1 ||
+      ld_t < N * W || !ntcf2_ok(C, H, W, {x}) || (reinterpret_cast<uintptr_t>(out) & 3) ||
+      (reinterpret_cast<uintptr_t>(outT) & 3) || (ld_t & 1) || (flags & ~AINP_BN_Y16))
+    return record_msg("ainp_bn_relu_apply_ntcf_bf16: bad argument (C*H % 64, even W and ld_t)");
+  const dim3 grid((unsigned)(N * cdiv(C * H, B2K) * cdiv(W, B2W)));
+  if (flags & AINP_BN_Y16)
+    hipLaunchKernelGGL(bn_relu_apply_ntcf_bf16<true>, grid, dim3(256), 0, as_stream(stream), x,
+                       scale, shift, out, outT, ld_t, C, H, W);
+  else
+    hipLaunchKernelGGL(bn_relu_apply_ntcf_bf16<false>, grid, dim3(256), 0, as_stream(stream), x,
+                       scale, shift, out, outT, ld_t, C, H, W);
+  return check_launch("bn_relu_apply_ntcf_bf16");
+}
+
 extern "C" int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale,
                                             const float* shift, uint16_t* out, uint16_t* outT,
                                             int64_t ld_t, int64_t N, int C, int64_t H, int64_t W,
                                             void* stream) {
-  if (!x || !scale || !shift || !out || !outT || N < 1 || C < 1 || H < 1 || W < 1 ||
-      ld_t < N * W || !ntcf2_ok(C, H, W, {x}) || (reinterpret_cast<uintptr_t>(out) & 3) ||
-      (reinterpret_cast<uintptr_t>(outT) & 3) || (ld_t & 1))
-    return record_msg("ainp_bn_relu_apply_ntcf_bf16: bad argument (C*H % 64, even W and ld_t)");
-  hipLaunchKernelGGL(bn_relu_apply_ntcf_bf16,
-                     dim3((unsigned)(N * cdiv(C * H, B2K) * cdiv(W, B2W))), dim3(256), 0,
-                     as_stream(stream), x, scale, shift, out, outT, ld_t, C, H, W);
-  return check_launch("bn_relu_apply_ntcf_bf16");
+  return ainp_bn_relu_apply_ntcf_bf16_ex(x, scale, shift, out, outT, ld_t, N, C, H, W, 0, stream);
 }
 
 extern "C" size_t ainp_bn_relu_bwd_workspace(int64_t N, int C, int64_t H,
                                              int64_t W) {
   return (size_t)(N * C * tiles_per_plane(H, W) * 2) * sizeof(double);
+}
+
+template <bool YB16>
+static int bn_bwd_reduce_launch(const float* g, const float* y, const float* scale,
+                                const float* shift, const float* save_mean_rstd, void* workspace,
+                                double* sums, int64_t N, int C, int64_t H, int64_t W, int g_ntcf,
+                                hipStream_t s) {
+  double* partial = reinterpret_cast<double*>(workspace);
+  if (!g_ntcf) {
+    const int64_t HW = H * W;
+    const int chunks = (int)cdiv(HW, BN_CHUNK);   // <= tiles_per_plane: fits the workspace
+    const bool vec = (HW % 2 == 0) && ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(y)) % 8 == 0);
+    const dim3 grid((unsigned)(N * C * chunks));
+    if (vec)
+      hipLaunchKernelGGL((bn_relu_bwd_reduce_flat<true, YB16>), grid, dim3(256), 0, s, g, y,
+                         scale, shift, save_mean_rstd, partial, C, HW, chunks);
+    else
+      hipLaunchKernelGGL((bn_relu_bwd_reduce_flat<false, YB16>), grid, dim3(256), 0, s, g, y,
+                         scale, shift, save_mean_rstd, partial, C, HW, chunks);
+    int rc = check_launch("bn_relu_bwd_reduce_flat");
+    if (rc) return rc;
+    hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial, (int)N, C, chunks, sums);
+    return check_launch("bn_bwd_sum");
+  }
+  const int64_t tpp = cdiv(H, NT_T) * cdiv(W, NT_T);   // <= tiles_per_plane: fits
+  hipLaunchKernelGGL((bn_relu_bwd_ntcf<false, false, YB16>), dim3((unsigned)(N * C * tpp)),
+                     dim3(256), 0, s, g, y, scale, shift, nullptr, save_mean_rstd, nullptr,
+                     partial, nullptr, nullptr, nullptr, C, H, W, 0.0);
+  int rc = check_launch("bn_relu_bwd_reduce_ntcf");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial,
+                     (int)N, C, (int)tpp, sums);
+  return check_launch("bn_bwd_sum");
+}
+
+extern "C" int ainp_bn_relu_bwd_reduce_ex(const float* g, const float* y, const float* scale,
+                                          const float* shift, const float* save_mean_rstd,
+                                          void* workspace, double* sums, int64_t N, int C,
+                                          int64_t H, int64_t W, int g_ntcf, int flags,
+                                          void* stream) {
+  if (!g || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
+      N < 1 || C < 1 || H < 1 || W < 1 || (flags & ~AINP_BN_Y16))
+    return record_msg("ainp_bn_relu_bwd_reduce: bad argument");
+  if (flags & AINP_BN_Y16)
+    return bn_bwd_reduce_launch<true>(g, y, scale, shift, save_mean_rstd, workspace, sums, N, C,
+                                      H, W, g_ntcf, as_stream(stream));
+  return bn_bwd_reduce_launch<false>(g, y, scale, shift, save_mean_rstd, workspace, sums, N, C, H,
+                                     W, g_ntcf, as_stream(stream));
 }
 
 extern "C" int ainp_bn_relu_bwd_reduce(const float* g, const float* y,
@@ -672,39 +749,11 @@ extern "C" int ainp_bn_relu_bwd_reduce(const float* g, const float* y,
                                        void* workspace, double* sums,
                                        int64_t N, int C, int64_t H, int64_t W,
                                        int g_ntcf, void* stream) {
-  if (!g || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
-      N < 1 || C < 1 || H < 1 || W < 1)
-    return record_msg("ainp_bn_relu_bwd_reduce: bad argument");
-  double* partial = reinterpret_cast<double*>(workspace);
-  hipStream_t s = as_stream(stream);
-  if (!g_ntcf) {
-    const int64_t HW = H * W;
-    const int chunks = (int)cdiv(HW, BN_CHUNK);   // <= tiles_per_plane: fits the workspace
-    const bool vec = (HW % 2 == 0) && ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(y)) % 8 == 0);
-    const dim3 grid((unsigned)(N * C * chunks));
-    if (vec)
-      hipLaunchKernelGGL(bn_relu_bwd_reduce_flat<true>, grid, dim3(256), 0, s, g, y, scale, shift,
-                         save_mean_rstd, partial, C, HW, chunks);
-    else
-      hipLaunchKernelGGL(bn_relu_bwd_reduce_flat<false>, grid, dim3(256), 0, s, g, y, scale, shift,
-                         save_mean_rstd, partial, C, HW, chunks);
-    int rc = check_launch("bn_relu_bwd_reduce_flat");
-    if (rc) return rc;
-    hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial, (int)N, C, chunks, sums);
-    return check_launch("bn_bwd_sum");
-  }
-  const int64_t tpp = cdiv(H, NT_T) * cdiv(W, NT_T);   // <= tiles_per_plane: fits
-  hipLaunchKernelGGL(bn_relu_bwd_ntcf<false>, dim3((unsigned)(N * C * tpp)), dim3(256), 0, s, g,
-                     y, scale, shift, nullptr, save_mean_rstd, nullptr, partial, nullptr, nullptr,
-                     nullptr, C, H, W, 0.0);
-  int rc = check_launch("bn_relu_bwd_reduce_ntcf");
-  if (rc) return rc;
-  hipLaunchKernelGGL(bn_bwd_sum_kernel, dim3(C), dim3(256), 0, s, partial,
-                     (int)N, C, (int)tpp, sums);
-  return check_launch("bn_bwd_sum");
+  return ainp_bn_relu_bwd_reduce_ex(g, y, scale, shift, save_mean_rstd, workspace, sums, N, C, H,
+                                    W, g_ntcf, 0, stream);
 }
 
-template <bool GY16>
+template <bool GY16, bool YB16>
 static int bn_bwd_apply_launch(const float* g, const float* y, const float* scale,
                                const float* shift, const float* gamma,
                                const float* save_mean_rstd, const double* sums, int64_t count,
@@ -718,13 +767,18 @@ extern "C" int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const f
                                          int64_t N, int C, int64_t H, int64_t W, int g_ntcf,
                                          int flags, void* stream) {
   if (!g || !y || !scale || !shift || !save_mean_rstd || !sums || !gy ||
-      N < 1 || C < 1 || H < 1 || W < 1 || count < 0 || (flags & ~AINP_BN_GY16))
+      N < 1 || C < 1 || H < 1 || W < 1 || count < 0 || (flags & ~(AINP_BN_GY16 | AINP_BN_Y16)))
     return record_msg("ainp_bn_relu_bwd_apply: bad argument");
-  if (flags & AINP_BN_GY16)
-    return bn_bwd_apply_launch<true>(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy,
-                                     dgamma, dbeta, N, C, H, W, g_ntcf, as_stream(stream));
-  return bn_bwd_apply_launch<false>(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy,
-                                    dgamma, dbeta, N, C, H, W, g_ntcf, as_stream(stream));
+  hipStream_t s = as_stream(stream);
+#define AINP_BNA(GV, YV)                                                                       \
+  return bn_bwd_apply_launch<GV, YV>(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy, \
+                                     dgamma, dbeta, N, C, H, W, g_ntcf, s)
+  const bool g16 = flags & AINP_BN_GY16, y16 = flags & AINP_BN_Y16;
+  if (g16 && y16) AINP_BNA(true, true);
+  if (g16) AINP_BNA(true, false);
+  if (y16) AINP_BNA(false, true);
+  AINP_BNA(false, false);
+#undef AINP_BNA
 }
 
 extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
@@ -739,7 +793,7 @@ extern "C" int ainp_bn_relu_bwd_apply(const float* g, const float* y,
                                    dgamma, dbeta, N, C, H, W, g_ntcf, 0, stream);
 }
 
-template <bool GY16>
+template <bool GY16, bool YB16>
 static int bn_bwd_apply_launch(const float* g, const float* y, const float* scale,
                                const float* shift, const float* gamma,
                                const float* save_mean_rstd, const double* sums, int64_t count,
@@ -755,11 +809,11 @@ static int bn_bwd_apply_launch(const float* g, const float* y, const float* scal
     int64_t nb = N * C * chunks;
     if (nb < C) nb = C;   // the dgamma / dbeta writers
     if (vec)
-      hipLaunchKernelGGL((bn_relu_bwd_apply_flat<true, GY16>), dim3((unsigned)nb), dim3(256), 0, s, g, y,
+      hipLaunchKernelGGL((bn_relu_bwd_apply_flat<true, GY16, YB16>), dim3((unsigned)nb), dim3(256), 0, s, g, y,
                          scale, shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, HW,
                          chunks, inv_count);
     else
-      hipLaunchKernelGGL((bn_relu_bwd_apply_flat<false, GY16>), dim3((unsigned)nb), dim3(256), 0, s, g, y,
+      hipLaunchKernelGGL((bn_relu_bwd_apply_flat<false, GY16, YB16>), dim3((unsigned)nb), dim3(256), 0, s, g, y,
                          scale, shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, HW,
                          chunks, inv_count);
     return check_launch("bn_relu_bwd_apply_flat");
@@ -768,14 +822,14 @@ static int bn_bwd_apply_launch(const float* g, const float* y, const float* scal
   if (ntcf2_ok(C, H, W, {g, y, gy})) {
     const int64_t nt2 = N * (C * H / NT_T) * cdiv(W, NT_T);
     const int64_t nb2 = nt2 < C ? C : nt2;   // >= C blocks: the dgamma / dbeta writers
-    hipLaunchKernelGGL(bn_relu_bwd_apply_ntcf2<GY16>, dim3((unsigned)nb2), dim3(256), 0, s, g, y, scale,
+    hipLaunchKernelGGL((bn_relu_bwd_apply_ntcf2<GY16, YB16>), dim3((unsigned)nb2), dim3(256), 0, s, g, y, scale,
                        shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W, inv_count,
                        nt2);
     return check_launch("bn_relu_bwd_apply_ntcf2");
   }
   int64_t nb = N * C * cdiv(H, NT_T) * cdiv(W, NT_T);
   if (nb < C) nb = C;
-  hipLaunchKernelGGL((bn_relu_bwd_ntcf<true, GY16>), dim3((unsigned)nb), dim3(256), 0, s, g, y, scale,
+  hipLaunchKernelGGL((bn_relu_bwd_ntcf<true, GY16, YB16>), dim3((unsigned)nb), dim3(256), 0, s, g, y, scale,
                      shift, gamma, save_mean_rstd, sums, nullptr, gy, dgamma, dbeta, C, H, W,
                      inv_count);
   return check_launch("bn_relu_bwd_apply_ntcf");

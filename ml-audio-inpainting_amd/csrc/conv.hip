@@ -912,13 +912,14 @@ int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W);
 int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, int64_t W,
                           bool b16);
 bool conv_x6_dgrad16_ok(int Cin, int Cout, int64_t H, int64_t W);
+bool conv_x6_fwd16_ok(int Cin, int Cout, int64_t H, int64_t W);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16);
+                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16);
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                   bool x16);
+                   bool x16, bool y16);
 
 // conv_x6.hip (fp32-accurate split-bf16 MFMA) serves every pair it has an
 // instantiation for unless AINP_CONV_EXACT=1 selects the exact f32 kernels.
@@ -963,7 +964,8 @@ template <bool DG>
 static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y,
                              double* stats, int64_t N, int Cin, int Cout,
-                             int64_t H, int64_t W, hipStream_t s, bool b16, bool x16 = false) {
+                             int64_t H, int64_t W, hipStream_t s, bool b16, bool x16 = false,
+                             bool y16 = false) {
   // partials [used, rows) of the BatchNorm statistics are zero
   auto zero_tail = [&](int64_t used) -> int {
     if (!stats) return AINP_OK;
@@ -975,20 +977,20 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
     return e == hipSuccess ? AINP_OK : record_error(e, "conv3x3 stats tail");
   };
   static const char* kNo16 =
-      "conv3x3: AINP_CONV_DY16 needs a split-bf16 data-gradient kernel for this pair";
+      "conv3x3: bf16 storage (AINP_CONV_DY16 / _X16 / _Y16) needs a split-bf16 kernel for this pair";
   if (small_pair(Cin, Cout)) {
-    if (x16) return record_msg(kNo16);
+    if (x16 || y16) return record_msg(kNo16);
     const int rc = small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
     return rc ? rc : zero_tail(exact_stat_parts(N, H, W));
   }
   if (!conv_exact_env()) {
     int64_t parts = 0;
     const int rc = conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                  &parts, b16, x16);
+                                  &parts, b16, x16, y16);
     if (rc == 2) return record_msg(kNo16);
     if (rc != 1) return rc ? rc : zero_tail(parts);
   }
-  if (x16) return record_msg(kNo16);
+  if (x16 || y16) return record_msg(kNo16);
   {
     const int rc = zero_tail(exact_stat_parts(N, H, W));
     if (rc) return rc;
@@ -1018,10 +1020,16 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
 }
 
 static bool conv_flags_ok(int flags) { return (flags & ~AINP_CONV_BF16) == 0; }
+// forward: the act(x) source and / or y in bf16 storage (with the bf16 arithmetic)
+static bool conv_fwd_flags_ok(int flags) {
+  return (flags & ~(AINP_CONV_BF16 | AINP_CONV_X16 | AINP_CONV_Y16)) == 0 &&
+         (!(flags & (AINP_CONV_X16 | AINP_CONV_Y16)) || (flags & AINP_CONV_BF16));
+}
 // data / weight gradients: dy may be bf16 storage (with the bf16 arithmetic)
-static bool conv_grad_flags_ok(int flags) {
-  return (flags & ~(AINP_CONV_BF16 | AINP_CONV_DY16)) == 0 &&
-         (!(flags & AINP_CONV_DY16) || (flags & AINP_CONV_BF16));
+static bool conv_grad_flags_ok(int flags, bool wgrad) {
+  const int extra = AINP_CONV_DY16 | (wgrad ? AINP_CONV_X16 : 0);
+  return (flags & ~(AINP_CONV_BF16 | extra)) == 0 &&
+         (!(flags & extra) || (flags & AINP_CONV_BF16));
 }
 
 extern "C" int ainp_conv3x3_fwd_ex(const float* x, const float* w,
@@ -1030,14 +1038,15 @@ extern "C" int ainp_conv3x3_fwd_ex(const float* x, const float* w,
                                    int64_t N, int Cin, int Cout, int64_t H,
                                    int64_t W, int flags, void* stream) {
   if (!x || !w || !y || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
-      N > 65535 || H > (1 << 24) || W > (1 << 24) || !conv_flags_ok(flags))
+      N > 65535 || H > (1 << 24) || W > (1 << 24) || !conv_fwd_flags_ok(flags))
     return record_msg("ainp_conv3x3_fwd: bad argument");
   if ((in_scale == nullptr) != (in_shift == nullptr))
     return record_msg("ainp_conv3x3_fwd: in_scale/in_shift must both be set");
   if (N == 0) return AINP_OK;
   return conv_fwd_dispatch<false>(x, w, bias, in_scale, in_shift, y, stats, N,
                                   Cin, Cout, H, W, as_stream(stream),
-                                  (flags & AINP_CONV_BF16) != 0);
+                                  (flags & AINP_CONV_BF16) != 0, (flags & AINP_CONV_X16) != 0,
+                                  (flags & AINP_CONV_Y16) != 0);
 }
 
 extern "C" int ainp_conv3x3_fwd(const float* x, const float* w,
@@ -1055,7 +1064,7 @@ extern "C" int ainp_conv3x3_dgrad_ex(const float* dy, const float* w, float* dx,
                                      void* stream) {
   (void)workspace;
   if (!dy || !w || !dx || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
-      N > 65535 || !conv_grad_flags_ok(flags))
+      N > 65535 || !conv_grad_flags_ok(flags, false))
     return record_msg("ainp_conv3x3_dgrad: bad argument");
   if (N == 0) return AINP_OK;
   // conv over dy (Cout channels) producing Cin channels, flipped weights
@@ -1086,6 +1095,19 @@ extern "C" int ainp_conv3x3_dy16_ok(int64_t N, int Cin, int Cout, int64_t H, int
   return conv_x6_dgrad16_ok(Cout, Cin, H, W) ? 1 : 0;
 }
 
+extern "C" int ainp_conv3x3_io16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+  (void)N;
+  if (Cin < 1 || Cout < 1 || H < 1 || W < 1 || small_pair(Cin, Cout) || conv_exact_env())
+    return 0;
+  const bool fits =
+      (int64_t)H * W * 4 * (Cout > WG_CIMAX ? Cout : WG_CIMAX) < ((int64_t)1 << 31);
+  const int cp = wgrad_pass(Cin);
+  if (!fits || Cin > WG_CIMAX ||
+      !((cp == 32 && Cout == 16) || (cp == 16 && Cout == 32) || (cp == 32 && Cout == 64)))
+    return 0;
+  return conv_x6_fwd16_ok(Cin, Cout, H, W) ? 1 : 0;
+}
+
 extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
                                                int64_t H, int64_t W) {
   if (small_pair(Cin, Cout)) return small_wgrad_ws(N, Cin, Cout, H, W);
@@ -1112,16 +1134,18 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
                                      int64_t N, int Cin, int Cout, int64_t H,
                                      int64_t W, int flags, void* stream) {
   if (!x || !dy || !dw || !workspace || N < 1 || Cin < 1 || Cout < 1 ||
-      H < 1 || W < 1 || !conv_grad_flags_ok(flags))
+      H < 1 || W < 1 || !conv_grad_flags_ok(flags, true))
     return record_msg("ainp_conv3x3_wgrad: bad argument");
   const bool b16 = (flags & AINP_CONV_BF16) != 0;
   const bool g16 = (flags & AINP_CONV_DY16) != 0;
+  const bool x16 = (flags & AINP_CONV_X16) != 0;
   static const char* kNo16 =
-      "ainp_conv3x3_wgrad: AINP_CONV_DY16 needs a split-bf16 weight-gradient kernel for this pair";
+      "ainp_conv3x3_wgrad: bf16 storage (AINP_CONV_DY16 / _X16) needs a split-bf16 "
+      "weight-gradient kernel for this pair";
   if ((in_scale == nullptr) != (in_shift == nullptr))
     return record_msg("ainp_conv3x3_wgrad: in_scale/in_shift must both be set");
   if (small_pair(Cin, Cout)) {
-    if (g16) return record_msg(kNo16);
+    if (g16 || x16) return record_msg(kNo16);
     return small_wgrad(x, in_scale, in_shift, dy, dw, dbias, workspace, N, Cin, Cout, H, W,
                        as_stream(stream));
   }
@@ -1158,9 +1182,9 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
     const int nblk_x6 = b16 ? WG_BLOCKS * conv_x6_occ16() : WG_BLOCKS;
     int rc = (fits && !conv_exact_env())
                  ? conv_wgrad_x6_launch(x, in_scale, in_shift, dy, partial, N, Cin, Cout, H, W,
-                                        ci0, cp, nblk_x6, s, b16, g16)
+                                        ci0, cp, nblk_x6, s, b16, g16, x16)
                  : 1;
-    if (rc == 1 && g16) return record_msg(kNo16);
+    if (rc == 1 && (g16 || x16)) return record_msg(kNo16);
     const int nblk = rc == 0 ? nblk_x6 : WG_BLOCKS;   // slabs the launch writes
     if (rc == 1) switch (key) {
       case 1616: AINP_WGT(16, 16); break;

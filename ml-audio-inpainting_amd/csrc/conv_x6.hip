@@ -67,6 +67,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t act_rsrc(const float* p, int64
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(b), (short)0, 0x7fffffff,
                                            0x00020000);
 }
+// Forward output y in bf16 storage (Y16, AINP_CONV_Y16: the bf16
+// configuration's pre-BatchNorm activations): the value as stored, whose
+// BatchNorm partials the epilogue then sums.
+__device__ __forceinline__ float y16_round(float v) { return (float)(__bf16)v; }
+__device__ __forceinline__ void y16_st(float* y, int64_t e, float vr) {
+  reinterpret_cast<uint16_t*>(y)[e] = __builtin_bit_cast(uint16_t, (__bf16)vr);
+}
 template <bool G16>
 __device__ __forceinline__ float act_ld(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
   if constexpr (G16)
@@ -322,7 +329,7 @@ int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W) {
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                    bool x16);
+                    bool x16, bool y16);
 
 // Persistent-grid multiplier of the bf16 (NP = 1) kernels: their LDS (21-50
 // KB) and VGPR (48-80) footprints let 2-4x the fp32 kernels' workgroups stay
@@ -375,19 +382,30 @@ bool conv_x6_dgrad16_ok(int Cin, int Cout, int64_t H, int64_t W) {
          (int64_t)Cin * H * W * 4 < ((int64_t)1 << 31);   // tiled, 8-row tiles
 }
 
+// 1 if conv_x6_launch(dgrad = false, b16) serves this pair on a persistent
+// kernel, the only forwards with bf16-storage input / output (x16 / y16)
+bool conv_x6_fwd16_ok(int Cin, int Cout, int64_t H, int64_t W) {
+  const int cop = Cout <= 32 ? 32 : 64;
+  static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
+  if (Cout > 64 || Cout < 16 || tiled_env ||
+      (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 >= ((int64_t)1 << 31))
+    return false;
+  return (Cin == 32 && cop == 64) || (Cin == 16 && cop == 32) || (Cin == 32 && Cout == 16);
+}
+
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                   bool x16) {
+                   bool x16, bool y16) {
   if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W, b16) == 0) return 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                   parts, b16, x16);
+                                   parts, b16, x16, y16);
     if (rc != 1) return rc;
   }
   if ((int64_t)Cin * H * W * 4 >= ((int64_t)1 << 31)) return 1;   // 32-bit buffer offsets
-  if (x16 && !(dgrad && !stats && b16)) return 2;   // bf16 operand storage: no such kernel
+  if (y16 || (x16 && !(dgrad && !stats && b16))) return 2;   // bf16 storage: no such kernel
   *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
@@ -469,7 +487,7 @@ __device__ __forceinline__ int wx6_gswz(int px) {
   return (((px >> 1) & 1) << 2) | (((px >> 2) & 1) << 1) | (px & 1);
 }
 
-template <int CO, int NP, bool G16 = false>
+template <int CO, int NP, bool G16 = false, bool XG16 = false>
 __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -539,18 +557,20 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
   auto fetch = [&](int64_t tile) {
     int n, f0, t0;
     tile_coords(tile, n, f0, t0);
-    int plane = (int)(HW * 4);
+    // act(x) input: fp32 or bf16 storage (XG16)
+    constexpr int XES = act_es<XG16>();
+    int plane = (int)(HW * XES);
     asm volatile("" : "+s"(plane));  // keep c * plane out of the tile loop
-    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * Cin + ci0) * HW);
+    const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, ((int64_t)n * Cin + ci0) * HW);
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : 3;
       const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
       const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
-      const int vo = 8 * grp * plane + (gr * W + gc) * 4;
+      const int vo = 8 * grp * plane + (gr * W + gc) * XES;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<XG16>(rx, vo, c * plane);
     }
     // dy: fp32 or bf16 storage (G16)
     constexpr int GES = act_es<G16>();
@@ -686,7 +706,7 @@ __device__ __forceinline__ int wx6s_swz(int px) {
   return ((px >> 1) & 1) | ((((px >> 2) ^ (px >> 3)) & 1) << 1);
 }
 
-template <int CP, int CO, int NP, bool G16 = false>
+template <int CP, int CO, int NP, bool G16 = false, bool XG16 = false>
 __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -740,18 +760,20 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
   auto fetch = [&](int64_t tile) {
     int n, f0, t0;
     tile_coords(tile, n, f0, t0);
-    int plane = (int)(HW * 4);
+    // act(x) input: fp32 or bf16 storage (XG16)
+    constexpr int XES = act_es<XG16>();
+    int plane = (int)(HW * XES);
     asm volatile("" : "+s"(plane));
-    const __amdgpu_buffer_rsrc_t rx = wx6_rsrc(x + ((int64_t)n * Cin + ci0) * HW);
+    const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, ((int64_t)n * Cin + ci0) * HW);
 #pragma unroll
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : XG - 1;
       const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
       const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
-      const int vo = 8 * grp * plane + (gr * W + gc) * 4;
+      const int vo = 8 * grp * plane + (gr * W + gc) * XES;
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = wx6_ld(rx, vo, c * plane);
+      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<XG16>(rx, vo, c * plane);
     }
     // dy: fp32 or bf16 storage (G16)
     constexpr int GES = act_es<G16>();
@@ -879,7 +901,7 @@ constexpr int XROW = HC * 32;            // halo row bytes per plane (16 bf16 pe
 constexpr int WROW = 9 * 32 + 16;        // weight row bytes per chunk and plane
 }  // namespace cxp
 
-template <int CI, int COP, bool DGRAD, int NT, int TR, int NP, bool G16 = false>
+template <int CI, int COP, bool DGRAD, int NT, int TR, int NP, bool G16 = false, bool Y16 = false>
 __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -1005,7 +1027,7 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     tile_coords(tile, n, r0, c0);
     const int row = r0 + wrow, col = c0 + li;
     const bool pok = row < H && col < W;
-    float* yn = y + (int64_t)n * Cout * HW + (int64_t)row * W + col;
+    const int64_t yo = (int64_t)n * Cout * HW + (int64_t)row * W + col;
 #pragma unroll
     for (int i = 0; i < NIW; ++i) {
       float s[16], q[16];
@@ -1013,8 +1035,13 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
       for (int r = 0; r < 16; ++r) {
         const int co = 32 * (wco + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
         const bool ok = pok && co < Cout;
-        const float v = acc[i][r] + ((bias && co < Cout) ? bias[co] : 0.f);
-        if (ok) yn[(int64_t)co * HW] = v;
+        float v = acc[i][r] + ((bias && co < Cout) ? bias[co] : 0.f);
+        if constexpr (Y16) {
+          v = y16_round(v);
+          if (ok) y16_st(y, yo + (int64_t)co * HW, v);
+        } else {
+          if (ok) y[yo + (int64_t)co * HW] = v;
+        }
         s[r] = ok ? v : 0.f;
         q[r] = s[r] * s[r];
       }
@@ -1113,7 +1140,7 @@ constexpr int XPLANE = HR * cxp::XROW;
 constexpr int XU = 2 * HR * cxp::HC;
 }  // namespace cxq
 
-template <int CI, bool DGRAD, int NP, bool G16 = false>
+template <int CI, bool DGRAD, int NP, bool G16 = false, bool Y16 = false>
 __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -1224,7 +1251,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     int n, r0, c0;
     tile_coords(tile, n, r0, c0);
     const int row = r0 + wave;
-    float* yn = y + (int64_t)n * Cout * HW + (int64_t)row * W;
+    const int64_t yo = (int64_t)n * Cout * HW + (int64_t)row * W;
     float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -1234,8 +1261,13 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
       for (int r = 0; r < 4; ++r) {
         const int co = 4 * g + r;
         const bool ok = pok && co < Cout;
-        const float v = acc[j][r] + ((bias && co < Cout) ? bias[co] : 0.f);
-        if (ok) yn[(int64_t)co * HW + col] = v;
+        float v = acc[j][r] + ((bias && co < Cout) ? bias[co] : 0.f);
+        if constexpr (Y16) {
+          v = y16_round(v);
+          if (ok) y16_st(y, yo + (int64_t)co * HW + col, v);
+        } else {
+          if (ok) y[yo + (int64_t)co * HW + col] = v;
+        }
         const float sv = ok ? v : 0.f;
         s[r] += sv;
         q[r] += sv * sv;
@@ -1316,26 +1348,62 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
 }
 
 // Persistent launcher (conv_x6_launch routes here); returns 1 if (CI, COP)
-// has no instantiation.
+// has no instantiation.  x16 / y16 (bf16 configuration, NP = 1 only): the
+// input (dy of a data gradient, act(x) source of a forward) / the forward
+// output in bf16 storage.
+template <int CIV, int COV, bool DG, int NTV, int TRV>
+static void x6p_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, const float* x,
+                   const float* w, const float* bias, const float* sc, const float* sh, float* y,
+                   double* stats, int N, int Cout, int H, int W) {
+#define AINP_X6PK(NPV, GV, YV)                                                                \
+  hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, NPV, GV, YV>), g, dim3(NTV), \
+                     0, s, x, w, bias, sc, sh, y, stats, N, Cout, H, W)
+  if (!b16) {
+    AINP_X6PK(3, false, false);
+  } else if constexpr (DG) {
+    if (x16) AINP_X6PK(1, true, false);
+    else AINP_X6PK(1, false, false);
+  } else {
+    if (x16 && y16) AINP_X6PK(1, true, true);
+    else if (x16) AINP_X6PK(1, true, false);
+    else if (y16) AINP_X6PK(1, false, true);
+    else AINP_X6PK(1, false, false);
+  }
+#undef AINP_X6PK
+}
+
+template <bool DG>
+static void x6q_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, const float* x,
+                   const float* w, const float* bias, const float* sc, const float* sh, float* y,
+                   double* stats, int N, int Cout, int H, int W) {
+#define AINP_X6QK(NPV, GV, YV)                                                                \
+  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV, GV, YV>), g, dim3(512), 0, s, x, w,     \
+                     bias, sc, sh, y, stats, N, Cout, H, W)
+  if (!b16) {
+    AINP_X6QK(3, false, false);
+  } else if constexpr (DG) {
+    if (x16) AINP_X6QK(1, true, false);
+    else AINP_X6QK(1, false, false);
+  } else {
+    if (x16 && y16) AINP_X6QK(1, true, true);
+    else if (x16) AINP_X6QK(1, true, false);
+    else if (y16) AINP_X6QK(1, false, true);
+    else AINP_X6QK(1, false, false);
+  }
+#undef AINP_X6QK
+}
+
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                    bool x16) {
+                    bool x16, bool y16) {
   const int cop = Cout <= 32 ? 32 : 64;
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
 #define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                      \
   if (dgrad == DG && Cin == CIV && cop == COV) {                                                 \
     const int g2 = b16 ? (G) * conv_x6_occ16() : (G);                                            \
-    if (b16 && x16 && DG)                                                                        \
-      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 1, true>), dim3(g2),       \
-                         dim3(NTV), 0, s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H,   \
-                         (int)W);                                                                \
-    else if (b16)                                                                                \
-      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 1>), dim3(g2), dim3(NTV), 0, \
-                         s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);         \
-    else                                                                                         \
-      hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, 3>), dim3(g2), dim3(NTV), 0, \
-                         s, x, w, bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W);         \
+    x6p_go<CIV, COV, DG, NTV, TRV>(dim3(g2), s, b16, x16, y16, x, w, bias, sc, sh, y, stats,    \
+                                   (int)N, Cout, (int)H, (int)W);                                \
     *parts = g2;                                                                                 \
     return check_launch("conv3x3_x6p");                                                          \
   }
@@ -1343,58 +1411,66 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
   AINP_X6P(16, 32, false, 512, 512, 8) AINP_X6P(16, 32, true, 512, 512, 8)
   if (Cin == 32 && Cout == 16) {   // two workgroups per CU (65 KB of LDS; bf16: more)
     const int gq = b16 ? 512 * conv_x6_occ16() : 512;
-#define AINP_X6Q(DG, NPV, X16V)                                                                  \
-  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV, X16V>), dim3(gq), dim3(512), 0, s, x, w,   \
-                     bias, sc, sh, y, stats, (int)N, Cout, (int)H, (int)W)
-    if (dgrad) {
-      if (b16 && x16) AINP_X6Q(true, 1, true);
-      else if (b16) AINP_X6Q(true, 1, false);
-      else AINP_X6Q(true, 3, false);
-    } else {
-      if (b16) AINP_X6Q(false, 1, false);
-      else AINP_X6Q(false, 3, false);
-    }
-#undef AINP_X6Q
+    if (dgrad)
+      x6q_go<true>(dim3(gq), s, b16, x16, y16, x, w, bias, sc, sh, y, stats, (int)N, Cout,
+                   (int)H, (int)W);
+    else
+      x6q_go<false>(dim3(gq), s, b16, x16, y16, x, w, bias, sc, sh, y, stats, (int)N, Cout,
+                    (int)H, (int)W);
     *parts = gq;
     return check_launch("conv3x3_x6q");
   }
-
-
 #undef AINP_X6P
+  return 1;
+}
+
+template <bool G16, bool XG16>
+static int wgrad_x6_go(const float* x, const float* sc, const float* sh, const float* dy,
+                       float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
+                       int ci0, int cp, int grid, hipStream_t s) {
+  if (cp == 32 && Cout == 16) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16, 1, G16, XG16>), dim3(grid), dim3(384), 0, s, x,
+                       sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+    return check_launch("conv3x3_wgrad_x6s");
+  }
+  if (cp == 16 && Cout == 32) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32, 1, G16, XG16>), dim3(grid), dim3(384), 0, s, x,
+                       sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+    return check_launch("conv3x3_wgrad_x6s");
+  }
+  if (cp == 32 && Cout == 64) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 1, G16, XG16>), dim3(grid), dim3(384), 0, s, x, sc,
+                       sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+    return check_launch("conv3x3_wgrad_x6");
+  }
   return 1;
 }
 
 // Launch the split-bf16 weight gradient of one 32-channel pass if Cout has an
 // instantiation; returns 1 if not handled.  grid = persistent workgroups.
+// g16 / x16 (bf16 configuration): dy / act(x)'s source in bf16 storage.
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16) {
-#define AINP_WX6S(CPV, COV)                                                                 \
-  do {                                                                                      \
-    if (b16 && g16)                                                                         \
-      hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, 1, true>), dim3(grid), dim3(384), 0, s, \
-                         x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);         \
-    else if (b16)                                                                           \
-      hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, 1>), dim3(grid), dim3(384), 0, s, x, sc, \
-                         sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);                \
-    else                                                                                    \
-      hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, 3>), dim3(grid), dim3(384), 0, s, x, sc, \
-                         sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);                \
-    return check_launch("conv3x3_wgrad_x6s");                                               \
-  } while (0)
-  if (cp == 32 && Cout == 16) AINP_WX6S(32, 16);
-  if (cp == 16 && Cout == 32) AINP_WX6S(16, 32);
-#undef AINP_WX6S
+                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16) {
+  if (b16) {
+    if (g16 && x16) return wgrad_x6_go<true, true>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
+    if (g16) return wgrad_x6_go<true, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
+    if (x16) return wgrad_x6_go<false, true>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
+    return wgrad_x6_go<false, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
+  }
+  if (cp == 32 && Cout == 16) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
+                       partial, (int)N, Cin, (int)H, (int)W, ci0);
+    return check_launch("conv3x3_wgrad_x6s");
+  }
+  if (cp == 16 && Cout == 32) {
+    hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
+                       partial, (int)N, Cin, (int)H, (int)W, ci0);
+    return check_launch("conv3x3_wgrad_x6s");
+  }
   if (cp != 32 || Cout != 64) return 1;
-  if (b16 && g16)
-    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 1, true>), dim3(grid), dim3(384), 0, s, x, sc, sh,
-                       dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
-  else if (b16)
-    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 1>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
-                       partial, (int)N, Cin, (int)H, (int)W, ci0);
-  else
-    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
-                       partial, (int)N, Cin, (int)H, (int)W, ci0);
+  hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
+                     partial, (int)N, Cin, (int)H, (int)W, ci0);
   return check_launch("conv3x3_wgrad_x6");
 }
 

@@ -206,6 +206,18 @@ void gemm(int64_t M, int64_t N, int64_t K, double alpha, at::TensorList A, int64
       "gemm_f32_ex");
 }
 
+// An fp32 tensor's data, or (bf16 = the flag bit is set) a bf16 tensor's uint16
+// storage passed through the ABI's float* argument (AINP_CONV_X16 / _Y16 /
+// _DY16, AINP_BN_Y16 / _GY16).
+const float* f32_or_16(const Tensor& t, const char* name, bool bf16) {
+  return bf16 ? reinterpret_cast<const float*>(dev<c10::BFloat16>(t, name, at::kBFloat16))
+              : dev(t, name);
+}
+float* f32_or_16_mut(const Tensor& t, const char* name, bool bf16) {
+  return bf16 ? reinterpret_cast<float*>(dev<c10::BFloat16>(t, name, at::kBFloat16))
+              : dev(t, name);
+}
+
 // ------------------------------------------------------------------- conv3x3
 void conv3x3_fwd(const Tensor& x, const Tensor& w, const OptT& bias, const OptT& in_scale,
                  const OptT& in_shift, const Tensor& y, const OptT& stats, int64_t flags) {
@@ -220,9 +232,10 @@ void conv3x3_fwd(const Tensor& x, const Tensor& w, const OptT& bias, const OptT&
     numel_is(*stats,
              ainp_conv3x3_fwd_stat_rows_ex(N, (int)Cin, (int)Cout, H, W, (int)flags) * 2 * Cout,
              "stats");
-  chk(ainp_conv3x3_fwd_ex(dev(x, "x"), dev(w, "w"), opt(bias, "bias"), opt(in_scale, "in_scale"),
-                          opt(in_shift, "in_shift"), dev(y, "y"), st, N, (int)Cin, (int)Cout, H, W,
-                          (int)flags, stream_of(x)),
+  chk(ainp_conv3x3_fwd_ex(f32_or_16(x, "x", flags & AINP_CONV_X16), dev(w, "w"),
+                          opt(bias, "bias"), opt(in_scale, "in_scale"), opt(in_shift, "in_shift"),
+                          f32_or_16_mut(y, "y", flags & AINP_CONV_Y16), st, N, (int)Cin,
+                          (int)Cout, H, W, (int)flags, stream_of(x)),
       "conv3x3_fwd_ex");
 }
 
@@ -232,9 +245,7 @@ void conv3x3_dgrad(const Tensor& dy, const Tensor& w, const Tensor& dx, int64_t 
               "conv3x3_dgrad: dy [N,Cout,H,W], w [Cout,Cin,3,3]");
   const int64_t N = dy.size(0), Cout = dy.size(1), H = dy.size(2), W = dy.size(3), Cin = w.size(1);
   numel_is(dx, N * Cin * H * W, "dx");
-  const float* dyp = (flags & AINP_CONV_DY16)
-                         ? reinterpret_cast<const float*>(dev<c10::BFloat16>(dy, "dy", at::kBFloat16))
-                         : dev(dy, "dy");
+  const float* dyp = f32_or_16(dy, "dy", flags & AINP_CONV_DY16);
   chk(ainp_conv3x3_dgrad_ex(dyp, dev(w, "w"), dev(dx, "dx"), nullptr, N, (int)Cin,
                             (int)Cout, H, W, (int)flags, stream_of(dy)),
       "conv3x3_dgrad_ex");
@@ -250,10 +261,9 @@ void conv3x3_wgrad(const Tensor& x, const OptT& in_scale, const OptT& in_shift, 
   numel_is(dw, Cout * Cin * 9, "dw");
   TORCH_CHECK((size_t)workspace.nbytes() >= ainp_conv3x3_wgrad_workspace(N, (int)Cin, (int)Cout, H, W),
               "conv3x3_wgrad workspace too small");
-  const float* dyp = (flags & AINP_CONV_DY16)
-                         ? reinterpret_cast<const float*>(dev<c10::BFloat16>(dy, "dy", at::kBFloat16))
-                         : dev(dy, "dy");
-  chk(ainp_conv3x3_wgrad_ex(dev(x, "x"), opt(in_scale, "in_scale"), opt(in_shift, "in_shift"),
+  const float* dyp = f32_or_16(dy, "dy", flags & AINP_CONV_DY16);
+  chk(ainp_conv3x3_wgrad_ex(f32_or_16(x, "x", flags & AINP_CONV_X16), opt(in_scale, "in_scale"),
+                            opt(in_shift, "in_shift"),
                             dyp, dev(dw, "dw"), opt(dbias, "dbias"),
                             workspace.data_ptr(), N, (int)Cin, (int)Cout, H, W, (int)flags,
                             stream_of(x)),
@@ -316,7 +326,8 @@ void bn_relu_apply(const Tensor& x, const Tensor& scale, const Tensor& shift, co
 }
 
 void bn_relu_bwd_reduce(const Tensor& g, const Tensor& y, const Tensor& scale, const Tensor& shift,
-                        const Tensor& save, const Tensor& workspace, const Tensor& sums, bool ntcf) {
+                        const Tensor& save, const Tensor& workspace, const Tensor& sums, bool ntcf,
+                        int64_t flags) {
   GUARD(y);
   TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -324,11 +335,11 @@ void bn_relu_bwd_reduce(const Tensor& g, const Tensor& y, const Tensor& scale, c
   TORCH_CHECK(sums.numel() >= 2 * C, "sums needs 2C entries");
   TORCH_CHECK((size_t)workspace.nbytes() >= ainp_bn_relu_bwd_workspace(N, (int)C, H, W),
               "bn_relu_bwd workspace too small");
-  chk(ainp_bn_relu_bwd_reduce(dev(g, "g"), dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"),
-                              dev(save, "save"), workspace.data_ptr(),
-                              dev<double>(sums, "sums", at::kDouble), N, (int)C, H, W, ntcf ? 1 : 0,
-                              stream_of(y)),
-      "bn_relu_bwd_reduce");
+  chk(ainp_bn_relu_bwd_reduce_ex(dev(g, "g"), f32_or_16(y, "y", flags & AINP_BN_Y16),
+                                 dev(scale, "scale"), dev(shift, "shift"), dev(save, "save"),
+                                 workspace.data_ptr(), dev<double>(sums, "sums", at::kDouble), N,
+                                 (int)C, H, W, ntcf ? 1 : 0, (int)flags, stream_of(y)),
+      "bn_relu_bwd_reduce_ex");
 }
 
 void bn_relu_bwd_apply(const Tensor& g, const Tensor& y, const Tensor& scale, const Tensor& shift,
@@ -344,7 +355,8 @@ void bn_relu_bwd_apply(const Tensor& g, const Tensor& y, const Tensor& scale, co
   // AINP_BN_GY16: gy is bf16 storage
   void* gyp = (flags & AINP_BN_GY16) ? (void*)dev<c10::BFloat16>(gy, "gy", at::kBFloat16)
                                      : (void*)dev(gy, "gy");
-  chk(ainp_bn_relu_bwd_apply_ex(dev(g, "g"), dev(y, "y"), dev(scale, "scale"),
+  chk(ainp_bn_relu_bwd_apply_ex(dev(g, "g"), f32_or_16(y, "y", flags & AINP_BN_Y16),
+                                dev(scale, "scale"),
                                 dev(shift, "shift"), opt(gamma, "gamma"), dev(save, "save"),
                                 dev<double>(sums, "sums", at::kDouble), count, gyp,
                                 opt(dgamma, "dgamma"), opt(dbeta, "dbeta"), N, (int)C, H, W,
@@ -803,7 +815,7 @@ uint16_t* bf16p(const Tensor& t, const char* name, bool contig = true) {
 }
 
 void bn_relu_apply_ntcf_bf16(const Tensor& x, const Tensor& scale, const Tensor& shift,
-                             const Tensor& out, const Tensor& outT) {
+                             const Tensor& out, const Tensor& outT, int64_t flags) {
   GUARD(x);
   TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
@@ -813,10 +825,11 @@ void bn_relu_apply_ntcf_bf16(const Tensor& x, const Tensor& scale, const Tensor&
   TORCH_CHECK(outT.dim() == 2 && outT.size(0) == C * H && outT.size(1) >= N * W,
               "outT must be [C*H, >= N*W]");
   TORCH_CHECK(outT.stride(1) == 1, "outT rows must be contiguous");
-  chk(ainp_bn_relu_apply_ntcf_bf16(dev(x, "x"), dev(scale, "scale"), dev(shift, "shift"),
-                                   bf16p(out, "out"), bf16p(outT, "outT", false), outT.stride(0),
-                                   N, (int)C, H, W, stream_of(x)),
-      "bn_relu_apply_ntcf_bf16");
+  chk(ainp_bn_relu_apply_ntcf_bf16_ex(f32_or_16(x, "x", flags & AINP_BN_Y16), dev(scale, "scale"),
+                                      dev(shift, "shift"), bf16p(out, "out"),
+                                      bf16p(outT, "outT", false), outT.stride(0), N, (int)C, H, W,
+                                      (int)flags, stream_of(x)),
+      "bn_relu_apply_ntcf_bf16_ex");
 }
 
 // Split-column bias of the NT GEMMs: bias_a1/a2 cover columns [0, nsplit),
@@ -1390,7 +1403,7 @@ TORCH_LIBRARY(ainp, m) {
         "float eps, Tensor(a!) scale, Tensor(b!) shift) -> ()");
   m.def("bn_relu_apply(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, bool ntcf) -> ()");
   m.def("bn_relu_bwd_reduce(Tensor g, Tensor y, Tensor scale, Tensor shift, Tensor save, "
-        "Tensor(a!) workspace, Tensor(b!) sums, bool ntcf) -> ()");
+        "Tensor(a!) workspace, Tensor(b!) sums, bool ntcf, int flags=0) -> ()");
   m.def("bn_relu_bwd_apply(Tensor g, Tensor y, Tensor scale, Tensor shift, Tensor? gamma, "
         "Tensor save, Tensor sums, int count, Tensor(a!) gy, Tensor(b!)? dgamma, "
         "Tensor(c!)? dbeta, bool ntcf, int flags=0) -> ()");
@@ -1439,7 +1452,7 @@ TORCH_LIBRARY(ainp, m) {
   m.def("mul(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("channel_sum(Tensor m, Tensor(a!) out) -> ()");
   m.def("bn_relu_apply_ntcf_bf16(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, "
-        "Tensor(b!) outT) -> ()");
+        "Tensor(b!) outT, int flags=0) -> ()");
   m.def("gemm_bf16nt(Tensor A, Tensor B, Tensor(a!) C, int K, Tensor? bias_a1, Tensor? bias_a2, "
         "Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, int kc) -> ()");
   m.def("cast_bf16_t(Tensor x, Tensor(a!)? out, Tensor(b!)? outT) -> ()");

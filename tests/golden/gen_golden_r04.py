@@ -17,6 +17,13 @@ data is written:
             forward  y  = conv(bf16(act(x)), bf16(W)) + b
             dgrad    dx = conv^T(bf16(dy), bf16(W))
             wgrad    dW = bf16(act(x)) (*) bf16(dy);  db = sum dy (fp32)
+          and the pre-BatchNorm outputs stored as bf16 (ainp cnnblstm.Y16:
+          encoder.3, encoder.6, decoder.0 -- the BatchNorm'd convs whose
+          consumers read bf16 storage): y -> bf16(y), straight-through in the
+          backward (BatchNorm statistics, normalisation and its backward see
+          bf16(y)); the BatchNorm-backward outputs gy of encoder.3/.6 and
+          decoder.0/.3 are bf16 as well, which only the fp32 bias gradient sum
+          db = sum(dy) sees (the convs round dy anyway)
         * nn.Linear projection and every LSTM input projection (both
           directions, all layers):
             forward  z  = bf16(x) bf16(W)^T + b        (+ b_hh for the LSTM)
@@ -108,7 +115,31 @@ class _RecMM(torch.autograd.Function):
 
 
 class _BConv(torch.autograd.Function):
-    """3x3, padding 1: conv(bf16(x), bf16(W)) + b and the matching backward."""
+    """3x3, padding 1: conv(bf16(x), bf16(W)) + b and the matching backward.
+    y16: the output rounded to bf16 (straight-through), and dy taken as
+    stored bf16 (db sums the rounded values: the BatchNorm-fed convs)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, y16=False):
+        xr, wr = _r(x), _r(w)
+        ctx.save_for_backward(xr, wr)
+        ctx.xshape = x.shape
+        ctx.y16 = y16
+        y = F.conv2d(xr, wr, b, padding=1)
+        return _r(y) if y16 else y
+
+    @staticmethod
+    def backward(ctx, g):
+        xr, wr = ctx.saved_tensors
+        gr = _r(g)
+        dx = torch.nn.grad.conv2d_input(ctx.xshape, wr, gr, padding=1)
+        dw = torch.nn.grad.conv2d_weight(xr, wr.shape, gr, padding=1)
+        return dx, dw, (gr if ctx.y16 else g).sum((0, 2, 3)), None
+
+
+class _BConvG16(torch.autograd.Function):
+    """_BConv with dy taken as stored bf16 (db sums the rounded values) and an
+    fp32 output: decoder.3, whose output feeds the fp32 16 -> 1 conv."""
 
     @staticmethod
     def forward(ctx, x, w, b):
@@ -123,7 +154,7 @@ class _BConv(torch.autograd.Function):
         gr = _r(g)
         dx = torch.nn.grad.conv2d_input(ctx.xshape, wr, gr, padding=1)
         dw = torch.nn.grad.conv2d_weight(xr, wr.shape, gr, padding=1)
-        return dx, dw, g.sum((0, 2, 3))
+        return dx, dw, gr.sum((0, 2, 3))
 
 
 def _small_pair(conv):
@@ -141,9 +172,16 @@ def emulate(mod, dtype):
         torch.manual_seed(0)
         model = mod.StackedBLSTMCNN(cfgp)
     model = model.to(dtype).train()
+    # the convs whose pre-BN output the HIP bf16 path stores as bf16 (and whose
+    # gy it stores as bf16: db then sums bf16 values) -- cnnblstm.Y16 / GY16
+    y16_convs = {id(model.encoder[3]), id(model.encoder[6]), id(model.decoder[0])}
+    gy16_convs = y16_convs | {id(model.decoder[3])}
     for mm in model.modules():
         if isinstance(mm, torch.nn.Conv2d) and not _small_pair(mm):
-            mm.forward = (lambda c: lambda z: _BConv.apply(z, c.weight, c.bias))(mm)
+            mm.forward = (lambda c, yy: lambda z: _BConv.apply(z, c.weight, c.bias, yy))(
+                mm, id(mm) in y16_convs)
+            if id(mm) in gy16_convs and id(mm) not in y16_convs:
+                mm.forward = (lambda c: lambda z: _BConvG16.apply(z, c.weight, c.bias))(mm)
     lin = model.projection
     lin.forward = lambda z: _BLinear.apply(z, lin.weight, lin.bias)
     lstm = model.lstm

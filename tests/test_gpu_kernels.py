@@ -1035,3 +1035,76 @@ def test_bn_relu_bwd_apply_bf16_output_is_rounded_fp32(ops, ntcf, C, H, W):
     assert gy16.dtype == torch.bfloat16
     assert torch.equal(gy16, gy32.to(torch.bfloat16))
     assert torch.equal(dg16, dg32) and torch.equal(db16, db32)
+
+
+@pytest.mark.parametrize("Cin,Cout,H,W", [(16, 32, 37, 70), (32, 16, 37, 70), (32, 64, 37, 70)])
+def test_conv3x3_bf16_activation_storage(ops, Cin, Cout, H, W):
+    """bf16 configuration, pre-BN activations in bf16 storage: a forward with
+    AINP_CONV_Y16 writes round(y) of the fp32-output forward bit for bit, its
+    BatchNorm partials sum the stored values; a forward / weight gradient
+    reading a bf16 act(x) source (AINP_CONV_X16) equals the one reading the
+    same values in fp32; BatchNorm backward and the NTCF bridge likewise."""
+    N = 3
+    g = torch.Generator(device=DEV).manual_seed(3 * Cin + Cout)
+    x16 = (torch.randn(N, Cin, H, W, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    x32 = x16.float()
+    w = torch.randn(Cout, Cin, 3, 3, device=DEV, generator=g) * 0.2
+    b = torch.randn(Cout, device=DEV, generator=g) * 0.1
+    sc = torch.rand(Cin, device=DEV, generator=g) + 0.5
+    sh = torch.randn(Cin, device=DEV, generator=g) * 0.3
+    assert ops.io16_ok(N, Cin, Cout, H, W)
+    y32, st32 = ops.conv3x3_fwd(x32, w, b, sc, sh, want_stats=True, bf16=True)
+    y16, st16 = ops.conv3x3_fwd(x16, w, b, sc, sh, want_stats=True, bf16=True, y16=True)
+    y32b, _ = ops.conv3x3_fwd(x16, w, b, sc, sh, want_stats=True, bf16=True)
+    torch.cuda.synchronize()
+    assert y16.dtype == torch.bfloat16
+    assert torch.equal(y32b, y32)                       # X16 read == fp32 read of the values
+    assert torch.equal(y16, y32.to(torch.bfloat16))     # Y16 == round(fp32 output)
+    s = st16.sum(0).double().cpu()
+    yd = y16.double().cpu()
+    assert rel(s[:Cout], yd.sum((0, 2, 3))) < 1e-6
+    assert rel(s[Cout:], (yd ** 2).sum((0, 2, 3))) < 1e-6
+    dy = torch.randn(N, Cout, H, W, device=DEV, generator=g)
+    dw16, db16 = ops.conv3x3_wgrad(x16, dy, sc, sh, bf16=True)
+    dw32, db32 = ops.conv3x3_wgrad(x32, dy, sc, sh, bf16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(dw16, dw32) and torch.equal(db16, db32)
+    # BatchNorm backward over the bf16-stored y (same values as fp32)
+    scb = torch.rand(Cout, device=DEV, generator=g) + 0.5
+    shb = torch.randn(Cout, device=DEV, generator=g) * 0.1
+    save = torch.cat([yd.float().mean((0, 2, 3)), 1.0 / (yd.float().var((0, 2, 3)) + 1e-5).sqrt()]).cuda()
+    gam = torch.rand(Cout, device=DEV, generator=g) + 0.5
+    gg = torch.randn(N, Cout, H, W, device=DEV, generator=g)
+    r16 = ops.bn_relu_bwd_reduce(gg, y16, scb, shb, save)
+    r32 = ops.bn_relu_bwd_reduce(gg, y16.float(), scb, shb, save)
+    a16 = ops.bn_relu_bwd_apply(gg, y16, scb, shb, gam, save, r32, N * H * W, gy16=True)
+    a32 = ops.bn_relu_bwd_apply(gg, y16.float(), scb, shb, gam, save, r32, N * H * W, gy16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(r16, r32)
+    for u, v in zip(a16, a32):
+        assert torch.equal(u, v)
+
+
+def test_ntcf_bridge_and_backward_read_bf16_y(ops):
+    """The encoder's last block with its pre-BN output in bf16 storage: the
+    bf16 X / X^T bridge and the NTCF BatchNorm backward (reduce + apply) give
+    what they give for the same values in fp32."""
+    N, C, H, W = 2, 64, 37, 70
+    g = torch.Generator(device=DEV).manual_seed(11)
+    y16 = (torch.randn(N, C, H, W, device=DEV, generator=g) * 2).to(torch.bfloat16)
+    sc = torch.rand(C, device=DEV, generator=g) + 0.5
+    sh = torch.randn(C, device=DEV, generator=g) * 0.1
+    X16, XT16 = ops.bn_relu_apply_ntcf_bf16(y16, sc, sh)
+    X32, XT32 = ops.bn_relu_apply_ntcf_bf16(y16.float(), sc, sh)
+    gg = torch.randn(N, W, C * H, device=DEV, generator=g)
+    save = torch.cat([y16.float().mean((0, 2, 3)), 1.0 / (y16.float().var((0, 2, 3)) + 1e-5).sqrt()])
+    gam = torch.rand(C, device=DEV, generator=g) + 0.5
+    r16 = ops.bn_relu_bwd_reduce(gg, y16, sc, sh, save, ntcf=True)
+    r32 = ops.bn_relu_bwd_reduce(gg, y16.float(), sc, sh, save, ntcf=True)
+    a16 = ops.bn_relu_bwd_apply(gg, y16, sc, sh, gam, save, r32, N * H * W, ntcf=True, gy16=True)
+    a32 = ops.bn_relu_bwd_apply(gg, y16.float(), sc, sh, gam, save, r32, N * H * W, ntcf=True,
+                                gy16=True)
+    torch.cuda.synchronize()
+    assert torch.equal(X16, X32) and torch.equal(XT16, XT32) and torch.equal(r16, r32)
+    for u, v in zip(a16, a32):
+        assert torch.equal(u, v)
