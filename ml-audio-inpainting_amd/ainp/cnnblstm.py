@@ -543,6 +543,10 @@ def _alias(t):
         t.untyped_storage(), t.storage_offset(), t.shape, t.stride())
 
 
+# AINP_DEFER_LIFO=1: release the deferred weight gradients in reverse order
+DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "0") == "1"
+
+
 class _Deferred:
     """Weight-gradient launches queued during the backward (decoder convs,
     projection) and released onto the side stream at a chosen point -- when
@@ -573,6 +577,11 @@ class _Deferred:
     @classmethod
     def flush(cls, device, join=False):
         q = cls._queues.pop(device, [])
+        if DEFER_LIFO:
+            # last queued first: the output projection's weight gradient (a
+            # short full-width GEMM) ahead of the decoder convs' (persistent
+            # kernels), so it does not run starved beside the layer-0 pair
+            q = q[::-1]
         if q:
             with _side_work(device, callback=False) as sw:
                 for fn, inputs, outputs, params, sink in q:

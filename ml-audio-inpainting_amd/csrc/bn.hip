@@ -428,23 +428,37 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
 // bridge is a batched 2-D transpose tiled 64 (k) x 64 (w) -- no 1-row h
 // tiles, 8-byte vectors on both sides (a wave moves two 256-byte rows per
 // instruction); the channel of row k is k / H.
+// kfirst: consecutive workgroups walk k (the NTCF rows' contiguous dimension)
+// rather than w (AINP_NTCF_KFIRST, A/B)
 __device__ __forceinline__ void ntcf2_tile(int64_t b, int64_t K, int64_t W, int& n, int& k0,
-                                           int& w0) {
+                                           int& w0, int kfirst = 0) {
   const int tw = (int)((W + NT_T - 1) / NT_T), tk = (int)(K / NT_T);
-  w0 = (int)(b % tw) * NT_T;
-  k0 = (int)((b / tw) % tk) * NT_T;
+  if (kfirst) {
+    k0 = (int)(b % tk) * NT_T;
+    w0 = (int)((b / tk) % tw) * NT_T;
+  } else {
+    w0 = (int)(b % tw) * NT_T;
+    k0 = (int)((b / tw) % tk) * NT_T;
+  }
   n = (int)(b / ((int64_t)tw * tk));
+}
+static int ntcf_kfirst() {
+  static const int v = [] {
+    const char* e = getenv("AINP_NTCF_KFIRST");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v;
 }
 
 __global__ __launch_bounds__(256) void bn_relu_apply_ntcf2(const float* __restrict__ x,
                                                            const float* __restrict__ scale,
                                                            const float* __restrict__ shift,
                                                            float* __restrict__ out, int C, int64_t H,
-                                                           int64_t W) {
+                                                           int64_t W, int kfirst) {
   __shared__ float tile[NT_T][NT_T + 1];   // [w][k]
   const int64_t K = (int64_t)C * H;
   int n, k0, w0;
-  ntcf2_tile(blockIdx.x, K, W, n, k0, w0);
+  ntcf2_tile(blockIdx.x, K, W, n, k0, w0, kfirst);
   const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
   const float* xn = x + (int64_t)n * K * W;
 #pragma unroll
@@ -476,7 +490,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
     const float* __restrict__ shift, const float* __restrict__ gamma,
     const float* __restrict__ save, const double* __restrict__ sums, void* __restrict__ gy,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int C, int64_t H, int64_t W,
-    double inv_count, int64_t ntiles) {
+    double inv_count, int64_t ntiles, int kfirst) {
   __shared__ float tile[NT_T][NT_T + 1];   // g as [w][k]
   if (blockIdx.x < (unsigned)C && threadIdx.x == 0) {
     if (dbeta) dbeta[blockIdx.x] = (float)sums[blockIdx.x];
@@ -485,7 +499,7 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_ntcf2(
   if (blockIdx.x >= ntiles) return;         // a dgamma / dbeta writer only
   const int64_t K = (int64_t)C * H;
   int n, k0, w0;
-  ntcf2_tile(blockIdx.x, K, W, n, k0, w0);
+  ntcf2_tile(blockIdx.x, K, W, n, k0, w0, kfirst);
   const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
   float2 yv[8];
 #pragma unroll
@@ -655,7 +669,7 @@ extern "C" int ainp_bn_relu_apply(const float* x, const float* scale,
   if (out_ntcf && ntcf2_ok(C, H, W, {x, out}))
     hipLaunchKernelGGL(bn_relu_apply_ntcf2,
                        dim3((unsigned)(N * (C * H / NT_T) * cdiv(W, NT_T))), dim3(256), 0, s, x,
-                       scale, shift, out, C, H, W);
+                       scale, shift, out, C, H, W, ntcf_kfirst());
   else if (out_ntcf)
     hipLaunchKernelGGL(bn_relu_apply_ntcf, dim3((unsigned)(N * C * cdiv(H, NT_T) * cdiv(W, NT_T))),
                        dim3(256), 0, s, x, scale, shift, out, C, H, W);
@@ -824,7 +838,7 @@ static int bn_bwd_apply_launch(const float* g, const float* y, const float* scal
     const int64_t nb2 = nt2 < C ? C : nt2;   // >= C blocks: the dgamma / dbeta writers
     hipLaunchKernelGGL((bn_relu_bwd_apply_ntcf2<GY16, YB16>), dim3((unsigned)nb2), dim3(256), 0, s, g, y, scale,
                        shift, gamma, save_mean_rstd, sums, gy, dgamma, dbeta, C, H, W, inv_count,
-                       nt2);
+                       nt2, ntcf_kfirst());
     return check_launch("bn_relu_bwd_apply_ntcf2");
   }
   int64_t nb = N * C * cdiv(H, NT_T) * cdiv(W, NT_T);

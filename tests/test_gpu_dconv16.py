@@ -47,7 +47,10 @@ def test_d_prep16_bit_exact(nslab, act, C, want_gT):
 
 
 @pytest.mark.parametrize("C,H,W,k,s,p", [(1, 21, 30, 4, 2, 1), (5, 11, 14, 4, 1, 1),
-                                         (3, 10, 9, 3, 2, 0), (2, 5, 5, 4, 2, 1)])
+                                         (3, 10, 9, 3, 2, 0), (2, 5, 5, 4, 2, 1),
+                                         (3, 41, 700, 4, 2, 1),   # Wo > 256 (row-staged)
+                                         (2, 7, 600, 3, 1, 1),
+                                         (1, 9, 3000, 4, 2, 1)])  # rows too wide: per-pixel
 def test_im2col16_bit_exact(C, H, W, k, s, p):
     from ainp import ops
     g = torch.Generator().manual_seed(H * W)
