@@ -233,12 +233,13 @@ class _ConvStackFn(torch.autograd.Function):
 # bf16 configuration: BatchNorm-backward outputs in bf16 storage (AINP_GY16=0:
 # fp32, as before; the conv results are the same bit for bit)
 GY16 = os.environ.get("AINP_GY16", "1") != "0"
-# bf16 configuration: pre-BatchNorm conv outputs in bf16 storage (AINP_Y16=0:
-# fp32, as before).  Unlike gy this is a rounding point of its own: the
-# BatchNorm statistics and the BatchNorm+ReLU that feeds the next conv see the
-# bf16 values (autocast's bf16 conv output); tests/golden/gen_golden_r04.py's
-# emulation rounds there too.
-Y16 = os.environ.get("AINP_Y16", "1") != "0"
+# bf16 configuration: pre-BatchNorm conv outputs in bf16 storage (AINP_Y16=1;
+# off by default: the C3-shape step measured 9.60 -> 9.67 ms/step with it,
+# profiles/r04kl_summary.txt).  Unlike gy this is a rounding point of its own:
+# the BatchNorm statistics and the BatchNorm+ReLU that feeds the next conv see
+# the bf16 values (autocast's bf16 conv output); tests/golden/gen_golden_r04.py
+# rounds there too when run with AINP_Y16=1.
+Y16 = os.environ.get("AINP_Y16", "0") == "1"
 
 
 def _l0_bf16_ok(y):
@@ -543,8 +544,10 @@ def _alias(t):
         t.untyped_storage(), t.storage_offset(), t.shape, t.stride())
 
 
-# AINP_DEFER_LIFO=1: release the deferred weight gradients in reverse order
-DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "0") == "1"
+# release the deferred weight gradients in reverse order (the output
+# projection's last, behind the layer-0 pair: C2 16.07 -> 15.96 ms/step,
+# profiles/r04kl_summary.txt); AINP_DEFER_LIFO=0: issue order
+DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "1") != "0"
 
 
 class _Deferred:

@@ -429,7 +429,8 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf(
 // tiles, 8-byte vectors on both sides (a wave moves two 256-byte rows per
 // instruction); the channel of row k is k / H.
 // kfirst: consecutive workgroups walk k (the NTCF rows' contiguous dimension)
-// rather than w (AINP_NTCF_KFIRST, A/B)
+// rather than w (default; AINP_NTCF_KFIRST=0: w first.  bwd_apply 0.609 ->
+// 0.588 ms in tools/bn_probe.py, profiles/r04kl_summary.txt)
 __device__ __forceinline__ void ntcf2_tile(int64_t b, int64_t K, int64_t W, int& n, int& k0,
                                            int& w0, int kfirst = 0) {
   const int tw = (int)((W + NT_T - 1) / NT_T), tk = (int)(K / NT_T);
@@ -445,7 +446,7 @@ __device__ __forceinline__ void ntcf2_tile(int64_t b, int64_t K, int64_t W, int&
 static int ntcf_kfirst() {
   static const int v = [] {
     const char* e = getenv("AINP_NTCF_KFIRST");
-    return (e && e[0] == '1') ? 1 : 0;
+    return (e && e[0] == '0') ? 0 : 1;
   }();
   return v;
 }

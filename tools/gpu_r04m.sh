@@ -8,6 +8,9 @@ export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
   tests/test_gpu_dconv16.py > "$OUT/pytest_dconv16.log" 2>&1 || { tail -30 "$OUT/pytest_dconv16.log"; exit 1; }
 tail -3 "$OUT/pytest_dconv16.log"
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+  tests/test_gpu_kernels.py -k "ntcf or bn_relu" > "$OUT/pytest_ntcf.log" 2>&1 || { tail -30 "$OUT/pytest_ntcf.log"; exit 1; }
+tail -3 "$OUT/pytest_ntcf.log"
 for rep in 1 2 3; do
   for rows in 0 1; do
     AINP_IM2COL16_ROWS=$rows timeout -k 10 300 python bench.py --workload gan --dtype bf16 \
