@@ -123,56 +123,6 @@ __global__ __launch_bounds__(256) void im2col16_kernel(const float* __restrict__
     }
 }
 
-// Row-staged variant: a workgroup owns IM_R output rows oy of one (image n,
-// input channel ci); the (IM_R-1)*stride + KH input rows they read are staged
-// zero-padded in LDS with coalesced loads, and each tap's column row segment
-// [q0, q0 + Wo) is written from LDS (consecutive lanes = consecutive ox: one
-// 128-byte run per wave instruction).  The window reads then hit LDS, not
-// the strided L1 traffic of im2col16_kernel.  blockIdx.z == C: the ones row.
-// Workgroups of the last (n, row block) also zero the tail [NP, ldA) of their
-// rows.  Same values as im2col16_kernel bit for bit.
-constexpr int IM_R = 4, IM_LDS_FLOATS = 6144;
-__global__ __launch_bounds__(256) void im2col16_rows_kernel(
-    const float* __restrict__ x, int C, int H, int W, int KH, int KW, int stride, int pad, int Ho,
-    int Wo, int64_t NP, int ones_row, uint16_t* __restrict__ col, int64_t ldA) {
-  __shared__ float rows[IM_LDS_FLOATS];
-  const int oy0 = blockIdx.x * IM_R, n = blockIdx.y, ci = blockIdx.z;
-  const int KK = KH * KW, t = threadIdx.x;
-  const int nr = min(IM_R, Ho - oy0);
-  const int64_t P = (int64_t)Ho * Wo;
-  const bool last = n == (int)gridDim.y - 1 && blockIdx.x == gridDim.x - 1;
-  if (ci == C) {   // ones row (bias gradient)
-    uint16_t* cp = col + (int64_t)C * KK * ldA;
-    for (int r = 0; r < nr; ++r)
-      for (int ox = t; ox < Wo; ox += 256) cp[n * P + (int64_t)(oy0 + r) * Wo + ox] = 0x3F80u;
-    if (last)
-      for (int64_t q = NP + t; q < ldA; q += 256) cp[q] = 0;
-    return;
-  }
-  const int LW = W + 2 * pad + stride;            // staged row length (zero borders)
-  const int SR = (nr - 1) * stride + KH;          // staged rows
-  const int iy0 = oy0 * stride - pad;
-  const float* xp = x + ((int64_t)n * C + ci) * H * W;
-  for (int e = t; e < SR * LW; e += 256) {
-    const int r = e / LW, c = e - r * LW;
-    const int iy = iy0 + r, ix = c - pad;
-    rows[e] = (iy >= 0 && iy < H && ix >= 0 && ix < W) ? xp[(int64_t)iy * W + ix] : 0.f;
-  }
-  __syncthreads();
-  uint16_t* cp = col + (int64_t)ci * KK * ldA;
-  for (int tap = 0; tap < KK; ++tap) {
-    const int ky = tap / KW, kx = tap - ky * KW;
-    uint16_t* cr = cp + (int64_t)tap * ldA;
-    for (int r = 0; r < nr; ++r) {
-      const float* lr = rows + (r * stride + ky) * LW + kx;
-      const int64_t q0 = n * P + (int64_t)(oy0 + r) * Wo;
-      for (int ox = t; ox < Wo; ox += 256) cr[q0 + ox] = to_bf16(lr[ox * stride]);
-    }
-    if (last)
-      for (int64_t q = NP + t; q < ldA; q += 256) cr[q] = 0;
-  }
-}
-
 // Parity class (py, px) of a stride-s transposed conv: output rows y = s*i + py
 // read gradient rows i + dy0 + a, a < nt = k/s, through kernel row
 // ky = ky0 + s*(nt-1-a), ky0 = (py+pad) % s.
@@ -509,21 +459,6 @@ extern "C" int ainp_im2col16(const float* x, int64_t N, int C, int H, int W, int
   const int64_t NP = N * Ho * Wo;
   const int Kr = C * KH * KW + (ones_row ? 1 : 0);
   if (Ho < 1 || Wo < 1 || ldA < NP || Kr > 65535) return record_msg("ainp_im2col16: bad shape");
-  // row-staged kernel where the staged rows fit its LDS (AINP_IM2COL16_ROWS=0:
-  // the per-pixel kernel)
-  static const bool rows_env = [] {
-    const char* e = getenv("AINP_IM2COL16_ROWS");
-    return !(e && e[0] == '0');
-  }();
-  const int LW = W + 2 * pad + stride, SR = (d16::IM_R - 1) * stride + KH;
-  if (rows_env && (int64_t)SR * LW <= d16::IM_LDS_FLOATS && N <= 65535) {
-    hipLaunchKernelGGL(d16::im2col16_rows_kernel,
-                       dim3((unsigned)cdiv(Ho, d16::IM_R), (unsigned)N,
-                            (unsigned)(C + (ones_row ? 1 : 0))),
-                       dim3(256), 0, as_stream(stream), x, C, H, W, KH, KW, stride, pad, Ho, Wo,
-                       NP, ones_row, col, ldA);
-    return check_launch("im2col16_rows");
-  }
   hipLaunchKernelGGL(d16::im2col16_kernel,
                      dim3((unsigned)cdiv(ldA / 2, 256), (unsigned)(C + (ones_row ? 1 : 0))),
                      dim3(256), 0, as_stream(stream), x, C, H, W, KH, KW, stride, pad, Ho, Wo, NP,

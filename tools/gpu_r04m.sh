@@ -32,4 +32,6 @@ done
 find "$OUT" -name '*kernel_stats.csv' | while read f; do
   echo "== $f"; grep -i "im2col\|gemm_bf16" "$f" | cut -d, -f1-5
 done
+timeout -k 10 300 python tools/glue_sites.py > "$OUT/glue_sites.log" 2>&1 || { tail -20 "$OUT/glue_sites.log"; exit 1; }
+grep -v amdgpu.ids "$OUT/glue_sites.log"
 echo "all steps ok"
