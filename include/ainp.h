@@ -573,6 +573,21 @@ int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, int H0, int W
                          int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
                          int pad, int act, float slope, int crop_h, int crop_w, int flags,
                          void* workspace, void* stream);
+/* ainp_conv_gen_fwd_ex that also writes y16 (may be NULL; Cout % 8 == 0,
+ * 16-byte aligned): the result after the activation as a bf16 (nearest-even)
+ * channel-last copy [N][Ho][Wo][Cout], the next conv's channel-last source
+ * (what ainp_nchw_to_nhwc16 would write from y).  Only the direct
+ * few-input-channel route writes it (one plain source of <= 4 channels,
+ * C0*KH*KW <= 160, Cout <= 64, no statistics: the discriminator's first conv
+ * on the spectrogram, networks.py:359-373, and VGG19's conv1_1, loss.py:41-51);
+ * any other route returns an error when y16 is given. */
+int ainp_conv_gen_fwd_out16(const float* x0, const float* m0, int C0, int H0, int W0,
+                            const float* x1, const float* m1, int C1, int H1, int W1,
+                            const float* w, const float* wt, const float* bias,
+                            const float* ratio, const float* scale, float* y, double* stats,
+                            int64_t N, int Cout, int Hin, int Win, int KH, int KW, int stride,
+                            int pad, int act, float slope, int crop_h, int crop_w, int flags,
+                            uint16_t* y16, void* workspace, void* stream);
 /* bf16 configurations (C4 / C5), channel-last variant: ainp_nchw_to_nhwc16
  * writes a source x [N][C][H][W] times its mask plane m [N][H][W] (may be
  * NULL) as bf16 (nearest-even) out [N][H][W][C]; ainp_conv_weight_nhwc16
@@ -644,6 +659,11 @@ int ainp_affine_act_nhwc16(float* y, const float* scale, const float* shift, int
                            void* stream);
 /* nn.MaxPool2d(2, 2) of VGG19.features (loss.py:21). */
 int ainp_maxpool2(const float* x, float* y, int64_t NC, int H, int W, void* stream);
+/* ainp_maxpool2 on x [N][C][H][W] that also writes the pooled values' bf16
+ * (nearest-even) channel-last copy out [N][H/2][W/2][C] (4-byte aligned): the
+ * next VGG19 conv's source (loss.py:41-51), as ainp_nchw_to_nhwc16 would. */
+int ainp_maxpool2_nhwc16(const float* x, float* y, int64_t N, int C, int H, int W,
+                         uint16_t* out, void* stream);
 /* VGGLoss._prepare_input_for_vgg + weights.transforms() (loss.py:65-86,104-106):
  * generated: (x+1)/2; target: clamp(x,0)/(max+1e-6) with the batch max found on
  * the device (max_ws: 1 uint scratch); clamp to [0,1]; antialiased bilinear

@@ -106,6 +106,10 @@ _SIGS = {
                                      P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int, c_int,
                                      c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int, P,
                                      P]),
+    "ainp_conv_gen_fwd_out16": (c_int, [P, P, c_int, c_int, c_int, P, P, c_int, c_int, c_int,
+                                        P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int, c_int,
+                                        c_int, c_int, c_int, c_int, c_float, c_int, c_int, c_int,
+                                        P, P, P]),
     "ainp_pconv_mask": (c_int, [P, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int64,
                                 c_int, c_int, c_int, c_int, c_int, c_int, c_float, P, P, P]),
     "ainp_gan_pad_input": (c_int, [P, P, c_int64, c_int, c_int, c_int, c_int, P, P, P]),
@@ -113,6 +117,7 @@ _SIGS = {
     "ainp_affine_act_nhwc16": (c_int, [P, P, P, c_int64, c_int, c_int, c_int, c_int, c_float, P,
                                        P, P]),
     "ainp_maxpool2": (c_int, [P, P, c_int64, c_int, c_int, P]),
+    "ainp_maxpool2_nhwc16": (c_int, [P, P, c_int64, c_int, c_int, c_int, P, P]),
     "ainp_vgg_prep": (c_int, [P, c_int64, c_int, c_int, c_int, P, P, P, P, c_int, P, P, P,
                               c_int, c_int, P, P]),
     "ainp_reduce_workspace": (c_size_t, []),

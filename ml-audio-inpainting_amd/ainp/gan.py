@@ -893,7 +893,10 @@ class VGGLoss(nn.Module):
                     if tape is not None:
                         tape.append(("conv", lay, xin, x, relu_next, [q for q in idx if q in want]))
                 elif isinstance(lay, nn.MaxPool2d):
-                    x = ops.maxpool2(x)
+                    # bf16: the pooled plane's channel-last copy for the next conv
+                    nxt16 = (self.ainp_bf16 and tape is None and i + 1 <= self.max_layer_idx
+                             and i + 1 < len(layers) and isinstance(layers[i + 1], nn.Conv2d))
+                    x = ops.maxpool2(x, out16=nxt16)
                     if i in want:
                         feats[i] = x
                     if tape is not None:

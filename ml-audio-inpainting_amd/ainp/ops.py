@@ -941,11 +941,22 @@ CONV_NHWC16 = os.environ.get("AINP_CONV_NHWC16", "1") != "0"
 # source (AINP_CONV_OUT16=0: a separate nchw_to_nhwc16 pass, as before)
 CONV_OUT16 = os.environ.get("AINP_CONV_OUT16", "1") != "0"
 CONV_NHWC16_SMALL = os.environ.get("AINP_CONV_NHWC16_SMALL", "1")
+# the same copy from the few-input-channel direct conv and from the max-pool
+# (AINP_OUT16_DIRECT=0: separate nchw_to_nhwc16 passes for those, A/B)
+OUT16_DIRECT = os.environ.get("AINP_OUT16_DIRECT", "1") != "0"
 
 
 def nhwc16_seg(C, KK):
     """k-values a source contributes to an nhwc16 weight row (gan.hip)."""
     return -(-KK * C // 32) * 32 if C % 32 else KK * C
+
+
+def _direct_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats):
+    """ainp_conv_gen_fwd_ex's few-input-channel kernel (gan.hip
+    conv_gen_smallcin_kernel) takes this conv (AINP_CONV_SMALLCIN unset)."""
+    return (os.environ.get("AINP_CONV_SMALLCIN", "1") != "0" and C1 == 0
+            and (H0, W0) == (Hin, Win) and not want_stats and 1 < Cout <= 64
+            and C0 * KH * KW <= 160 and C0 <= 4)
 
 
 def _nhwc16_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats):
@@ -1107,9 +1118,16 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
         wt = conv_weight_kmajor(w, C0, C1)
     if nb:
         ws = torch.empty(-(-nb // 4), device=x0.device)
+    y16 = None
+    if (out16 and bf16 and CONV_OUT16 and OUT16_DIRECT and _NHWC_MEMO is not None
+            and Cout % 8 == 0 and _direct_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats)):
+        # the few-input-channel kernel writes the next conv's channel-last source
+        y16 = torch.empty(N, Ho, Wo, Cout, device=x0.device, dtype=torch.bfloat16)
     _T.conv_gen_fwd(x0, m0, x1, m1, w, wt, bias, ratio, scale, out, stats, int(Hin), int(Win),
                     int(stride), int(pad), int(act), float(slope), int(ch), int(cw),
-                    CONV_BF16 if bf16 else 0, ws)
+                    CONV_BF16 if bf16 else 0, ws, y16)
+    if y16 is not None:
+        _NHWC_MEMO[(out.data_ptr(), tuple(out.shape), out._version, 0, -1)] = (y16, out, None)
     return out, stats
 
 
@@ -1162,11 +1180,19 @@ def affine_act_nhwc16_(y, scale, shift, act, slope=0.2, m=None):
     return y, out
 
 
-def maxpool2(x):
+def maxpool2(x, out16=False):
+    """2x2 / stride-2 max-pool.  out16 (inside an nhwc16_memo scope): the same
+    pass writes y's bf16 channel-last copy (ainp_maxpool2_nhwc16), which
+    to_nhwc16(y) then returns -- the next VGG19 conv's source."""
     _req(x, "x")
     N, C, H, W = x.shape
     y = torch.empty(N, C, H // 2, W // 2, device=x.device)
-    _T.maxpool2(x, y)
+    y16 = None
+    if out16 and CONV_OUT16 and OUT16_DIRECT and _NHWC_MEMO is not None:
+        y16 = torch.empty(N, H // 2, W // 2, C, device=x.device, dtype=torch.bfloat16)
+    _T.maxpool2(x, y, y16)
+    if y16 is not None:
+        _NHWC_MEMO[(y.data_ptr(), tuple(y.shape), y._version, 0, -1)] = (y16, y, None)
     return y
 
 

@@ -38,7 +38,8 @@ struct ConvGenParams {
   float* y;                 // [N][Cout][Ho][Wo]
   double* stats;            // [px_tiles][2][Cout] (sum, sumsq of the stored y) or null
   float* partial;           // split-K: raw sums [gridDim.z][Cout][N*Ho*Wo], epilogue deferred
-  uint16_t* y16;            // optional bf16 channel-last copy of y: [N][Ho][Wo][Cout] (nhwc16 only)
+  uint16_t* y16;            // optional bf16 channel-last copy of y: [N][Ho][Wo][Cout] (nhwc16
+                            // and few-input-channel kernels)
   int ktiles_per_split;     // K tiles per blockIdx.z
   int N, Cin, Cout, Hin, Win, Ho, Wo, KH, KW, stride, pad;
   float slope;              // LeakyReLU negative slope (act == 2)
@@ -823,6 +824,50 @@ __global__ void maxpool2_kernel(const float* x, float* y, int64_t NC, int H, int
   y[t] = fmaxf(fmaxf(b[0], b[1]), fmaxf(b[W], b[W + 1]));
 }
 
+// maxpool2_kernel's values plus, in the same pass, their channel-last bf16
+// copy out [N][Ho][Wo][C] (nchw_to_nhwc16_kernel's conversion and write-out):
+// the VGG19 conv after each max-pool (loss.py:41-51) reads that copy, so no
+// separate nchw_to_nhwc16 pass re-reads the pooled plane.  Block (64 output
+// columns, output row, image x 64-channel chunk).
+__global__ __launch_bounds__(256) void maxpool2_nhwc16_kernel(const float* __restrict__ x,
+                                                              float* __restrict__ y, int C,
+                                                              int H, int W,
+                                                              uint16_t* __restrict__ out) {
+  __shared__ uint16_t tile[64][66];   // [w][c]
+  const int Ho = H / 2, Wo = W / 2;
+  const int w0 = blockIdx.x * 64, h = blockIdx.y;
+  const int cb = (C + 63) / 64;
+  const int n = blockIdx.z / cb, c0 = (blockIdx.z % cb) * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int w = w0 + tx;
+#pragma unroll 4
+  for (int i = ty; i < 64; i += 4) {
+    const int c = c0 + i;
+    float v = 0.f;
+    if (c < C && w < Wo) {
+      const int64_t nc = (int64_t)n * C + c;
+      const float* b = x + nc * H * W + (int64_t)(2 * h) * W + 2 * w;
+      v = fmaxf(fmaxf(b[0], b[1]), fmaxf(b[W], b[W + 1]));
+      y[(nc * Ho + h) * Wo + w] = v;
+    }
+    tile[tx][i] = __builtin_bit_cast(uint16_t, (__bf16)v);
+  }
+  __syncthreads();
+  const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
+#pragma unroll
+  for (int i = r; i < 64; i += 8) {
+    const int ww = w0 + i, c = c0 + 2 * l;
+    if (ww >= Wo || c >= C) continue;
+    uint16_t* q = out + (((int64_t)n * Ho + h) * Wo + ww) * C + c;
+    if (c + 1 < C && !(C & 1)) {
+      *reinterpret_cast<uint32_t*>(q) = (uint32_t)tile[i][2 * l] | ((uint32_t)tile[i][2 * l + 1] << 16);
+    } else {   // odd C: 2-byte stores keep every access aligned
+      q[0] = tile[i][2 * l];
+      if (c + 1 < C) q[1] = tile[i][2 * l + 1];
+    }
+  }
+}
+
 // ---------------------------------------------------------------- VGG input
 // max(clamp(x, 0)) over the whole batch (loss.py:77-78).  Values are >= 0,
 // so the float ordering equals the uint ordering of their bit patterns.
@@ -1390,7 +1435,24 @@ __global__ __launch_bounds__(256) void conv_gen_smallcin_kernel(ConvGenParams p,
       float v = acc[c] * sc;
       v *= rt;
       if (p.bias) v += p.bias[c];
-      yb[(int64_t)c * HWo] = apply_act(v, act, p.slope);
+      acc[c] = apply_act(v, act, p.slope);
+      yb[(int64_t)c * HWo] = acc[c];
+    }
+  }
+  // the next conv's channel-last bf16 source (Cout % 8 == 0): this pixel's
+  // Cout values as one contiguous run of 16-byte stores
+  if (p.y16) {
+    uint16_t* o = p.y16 + pix * Cout;
+#pragma unroll
+    for (int c = 0; c < SC_CO; c += 8) {
+      if (c < Cout) {
+        uint32_t h[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          h[j] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)acc[c + 2 * j]) |
+                 ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)acc[c + 2 * j + 1]) << 16);
+        *reinterpret_cast<uint4*>(o + c) = make_uint4(h[0], h[1], h[2], h[3]);
+      }
     }
   }
 }
@@ -2112,6 +2174,59 @@ __global__ __launch_bounds__(256) void im2col_nhwc16_kernel(
   *reinterpret_cast<uint4*>(out + pix * seg + k0) = make_uint4(g[0], g[1], g[2], g[3]);
 }
 
+// Row-staged im2col_nhwc16_kernel (same values bit for bit): a workgroup owns
+// IMN_P consecutive output pixels of one output row; the KH input rows x C
+// channels they read (x * m, resampled, zero outside) are staged in LDS with
+// coalesced loads, a per-k LDS offset table replaces the per-element tap /
+// channel divisions, and each thread writes 16-byte chunks of the [pix][seg]
+// rows (consecutive threads: consecutive chunks, one contiguous run per block).
+constexpr int IMN_P = 64, IMN_LDS = 4096, IMN_SEG = 256;
+__global__ __launch_bounds__(256) void im2col_nhwc16_rows_kernel(
+    const float* __restrict__ x, const float* __restrict__ m, int C, int Hs, int Ws, int up,
+    int Hin, int Win, int KH, int KW, int stride, int pad, int Ho, int Wo, int seg,
+    uint16_t* __restrict__ out) {
+  __shared__ float patch[IMN_LDS];   // [ci][ky][PW]
+  __shared__ int koff[IMN_SEG];      // k -> patch offset of pixel 0, or -1 past KK*C
+  const int ox0 = blockIdx.x * IMN_P, oy = blockIdx.y, n = blockIdx.z;
+  const int np = min(IMN_P, Wo - ox0);
+  const int PW = (np - 1) * stride + KW;
+  const int KK = KH * KW;
+  const int iy0 = oy * stride - pad, ix0 = ox0 * stride - pad;
+  for (int k = threadIdx.x; k < seg; k += 256) {
+    const int tap = k / C, ci = k - tap * C;
+    const int ky = tap / KW, kx = tap - ky * KW;
+    koff[k] = tap < KK ? (ci * KH + ky) * PW + kx : -1;
+  }
+  for (int e = threadIdx.x; e < C * KH * PW; e += 256) {
+    const int ci = e / (KH * PW), rem = e - ci * KH * PW;
+    const int ky = rem / PW, c = rem - ky * PW;
+    const int iy = iy0 + ky, ix = ix0 + c;
+    float v = 0.f;
+    if (iy >= 0 && iy < Hin && ix >= 0 && ix < Win) {
+      const int sy = src_coord(iy, Hs, Hin, up), sx = src_coord(ix, Ws, Win, up);
+      v = x[(((int64_t)n * C + ci) * Hs + sy) * Ws + sx];
+      if (m) v *= m[((int64_t)n * Hs + sy) * Ws + sx];
+    }
+    patch[e] = v;
+  }
+  __syncthreads();
+  const int chunks = seg / 8;
+  uint16_t* ob = out + (((int64_t)n * Ho + oy) * Wo + ox0) * seg;
+  for (int t = threadIdx.x; t < np * chunks; t += 256) {
+    const int p = t / chunks, k0 = (t - p * chunks) * 8;
+    uint32_t g[4];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int o = koff[k0 + j];
+      const float v = o >= 0 ? patch[o + p * stride] : 0.f;
+      const uint32_t b = __builtin_bit_cast(uint16_t, (__bf16)v);
+      if (j & 1) g[j >> 1] |= b << 16;
+      else g[j >> 1] = b;
+    }
+    *reinterpret_cast<uint4*>(ob + (int64_t)p * seg + k0) = make_uint4(g[0], g[1], g[2], g[3]);
+  }
+}
+
 // w [Cout][C0+C1][KH][KW] fp32 -> wt16 [Cout][K] bf16, k = tap*C0 + ci (source 0)
 // then seg0 + tap*C1 + ci (source 1), each source padded to nhwc16_seg k-values
 // with zeros
@@ -2216,10 +2331,23 @@ extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, in
                                     double* stats, int64_t N, int Cout, int Hin, int Win, int KH,
                                     int KW, int stride, int pad, int act, float slope, int crop_h,
                                     int crop_w, int flags, void* workspace, void* stream) {
+  return ainp_conv_gen_fwd_out16(x0, m0, C0, H0, W0, x1, m1, C1, H1, W1, w, wt, bias, ratio,
+                                 scale, y, stats, N, Cout, Hin, Win, KH, KW, stride, pad, act,
+                                 slope, crop_h, crop_w, flags, nullptr, workspace, stream);
+}
+
+extern "C" int ainp_conv_gen_fwd_out16(const float* x0, const float* m0, int C0, int H0, int W0,
+                                       const float* x1, const float* m1, int C1, int H1, int W1,
+                                       const float* w, const float* wt, const float* bias,
+                                       const float* ratio, const float* scale, float* y,
+                                       double* stats, int64_t N, int Cout, int Hin, int Win,
+                                       int KH, int KW, int stride, int pad, int act, float slope,
+                                       int crop_h, int crop_w, int flags, uint16_t* y16,
+                                       void* workspace, void* stream) {
   if (!x0 || C0 < 1 || C1 < 0 || (C1 > 0 && !x1) || !w || !y || N < 1 || Cout < 1 ||
       Hin < 1 || Win < 1 || KH < 1 || KW < 1 || stride < 1 || pad < 0 || act < 0 || act > 3 ||
-      (flags & ~AINP_CONV_BF16))
-    return record_msg("ainp_conv_gen_fwd: bad argument");
+      (flags & ~AINP_CONV_BF16) || (y16 && (Cout % 8 || ((uintptr_t)y16 & 15))))
+    return record_msg("ainp_conv_gen_fwd: bad argument (y16: Cout % 8 == 0, 16-byte aligned)");
   const bool b16 = (flags & AINP_CONV_BF16) != 0;
   const int Ho = (Hin + 2 * pad - KH) / stride + 1;
   const int Wo = (Win + 2 * pad - KW) / stride + 1;
@@ -2273,6 +2401,7 @@ extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, in
   if (small_ok && C1 == 0 && p.s0.up == 0 && !stats && Cout <= SC_CO &&
       (int64_t)C0 * KH * KW <= SC_K && C0 <= 4) {
     const int64_t NPs = N * (int64_t)Ho * Wo;
+    p.y16 = y16;
     if (b16)
       hipLaunchKernelGGL(conv_gen_smallcin_kernel<true>, dim3((unsigned)cdiv(NPs, 256)), dim3(256),
                          0, s, p, act);
@@ -2281,6 +2410,7 @@ extern "C" int ainp_conv_gen_fwd_ex(const float* x0, const float* m0, int C0, in
                          0, s, p, act);
     return check_launch("conv_gen_smallcin");
   }
+  if (y16) return record_msg("ainp_conv_gen_fwd: y16 is written by the few-input-channel kernel only");
   if (!wt) return record_msg("ainp_conv_gen_fwd: k-major weights (ainp_conv_weight_kmajor) required");
   const int BM = conv_gen_bm(Cout);
   const int64_t NP = N * (int64_t)Ho * Wo;
@@ -2376,6 +2506,21 @@ extern "C" int ainp_im2col_nhwc16(const float* x, const float* m, int64_t N, int
   if (sd.up == 1 && Hs * 2 != Hin) return record_msg("ainp_im2col_nhwc16: bad source size");
   const int seg = nhwc16_seg(C, KH * KW);
   const int64_t NP = N * (int64_t)Ho * Wo;
+  // row-staged kernel where its LDS holds the patch (AINP_IM2COL_NHWC16_ROWS=0:
+  // the per-chunk kernel)
+  static const bool rows_env = [] {
+    const char* e = getenv("AINP_IM2COL_NHWC16_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  const int PWmax = (IMN_P - 1) * stride + KW;
+  if (rows_env && (int64_t)C * KH * PWmax <= IMN_LDS && seg <= IMN_SEG && N <= 65535 &&
+      Ho <= 65535) {
+    hipLaunchKernelGGL(im2col_nhwc16_rows_kernel,
+                       dim3((unsigned)cdiv(Wo, IMN_P), (unsigned)Ho, (unsigned)N), dim3(256), 0,
+                       as_stream(stream), x, m, C, Hs, Ws, sd.up, Hin, Win, KH, KW, stride, pad,
+                       Ho, Wo, seg, out);
+    return check_launch("im2col_nhwc16_rows");
+  }
   hipLaunchKernelGGL(im2col_nhwc16_kernel, dim3((unsigned)cdiv(NP * (seg / 8), 256)), dim3(256), 0,
                      as_stream(stream), x, m, C, Hs, Ws, sd.up, Hin, Win, KH, KW, stride, pad, Ho,
                      Wo, NP, seg, out);
@@ -2569,6 +2714,17 @@ extern "C" int ainp_affine_act(float* y, const float* scale, const float* shift,
   hipLaunchKernelGGL(affine_act_kernel, dim3((unsigned)cdiv(total, 256)), dim3(256), 0,
                      as_stream(stream), y, scale, shift, C, HW, total, act, slope);
   return check_launch("affine_act");
+}
+
+extern "C" int ainp_maxpool2_nhwc16(const float* x, float* y, int64_t N, int C, int H, int W,
+                                    uint16_t* out, void* stream) {
+  if (!x || !y || !out || N < 1 || C < 1 || H < 2 || W < 2 || ((uintptr_t)out & 3) ||
+      N * ((C + 63) / 64) > 65535 || H / 2 > 65535)
+    return record_msg("ainp_maxpool2_nhwc16: bad argument");
+  hipLaunchKernelGGL(maxpool2_nhwc16_kernel, dim3((unsigned)cdiv(W / 2, 64), (unsigned)(H / 2),
+                                                  (unsigned)(N * cdiv(C, 64))),
+                     dim3(256), 0, as_stream(stream), x, y, C, H, W, out);
+  return check_launch("maxpool2_nhwc16");
 }
 
 extern "C" int ainp_maxpool2(const float* x, float* y, int64_t NC, int H, int W, void* stream) {

@@ -507,11 +507,13 @@ void conv_weight_kmajor(const Tensor& w, int64_t C0, int64_t C1, const Tensor& w
       "conv_weight_kmajor");
 }
 
+uint16_t* bf16p(const Tensor& t, const char* name, bool contig);
+
 void conv_gen_fwd(const Tensor& x0, const OptT& m0, const OptT& x1, const OptT& m1,
                   const Tensor& w, const OptT& wt, const OptT& bias, const OptT& ratio,
                   const OptT& scale, const Tensor& y, const OptT& stats, int64_t Hin, int64_t Win,
                   int64_t stride, int64_t pad, int64_t act, double slope, int64_t crop_h,
-                  int64_t crop_w, int64_t flags, const OptT& workspace) {
+                  int64_t crop_w, int64_t flags, const OptT& workspace, const OptT& y16) {
   GUARD(x0);
   TORCH_CHECK(x0.dim() == 4 && w.dim() == 4, "conv_gen: x0 [N,C0,H0,W0], w [Cout,Cin,KH,KW]");
   const int64_t N = x0.size(0), C0 = x0.size(1), H0 = x0.size(2), W0 = x0.size(3);
@@ -551,12 +553,18 @@ void conv_gen_fwd(const Tensor& x0, const OptT& m0, const OptT& x1, const OptT& 
   } else {
     TORCH_CHECK(need == 0, "conv_gen needs a workspace of ", need, " bytes");
   }
-  chk(ainp_conv_gen_fwd_ex(dev(x0, "x0"), pm0, (int)C0, (int)H0, (int)W0, px1, pm1, (int)C1,
-                           (int)H1, (int)W1, dev(w, "w"), pwt, opt(bias, "bias"), opt(ratio, "ratio"),
-                           opt(scale, "scale"), dev(y, "y"), st, N, (int)Cout, (int)Hin, (int)Win,
-                           (int)KH, (int)KW, (int)stride, (int)pad, (int)act, (float)slope,
-                           (int)crop_h, (int)crop_w, (int)flags, ws, stream_of(x0)),
-      "conv_gen_fwd_ex");
+  uint16_t* o16 = nullptr;
+  if (y16.has_value() && y16->defined()) {
+    numel_is(*y16, N * Cout * Ho * Wo, "y16");
+    o16 = bf16p(*y16, "y16", true);
+  }
+  chk(ainp_conv_gen_fwd_out16(dev(x0, "x0"), pm0, (int)C0, (int)H0, (int)W0, px1, pm1, (int)C1,
+                              (int)H1, (int)W1, dev(w, "w"), pwt, opt(bias, "bias"),
+                              opt(ratio, "ratio"), opt(scale, "scale"), dev(y, "y"), st, N,
+                              (int)Cout, (int)Hin, (int)Win, (int)KH, (int)KW, (int)stride,
+                              (int)pad, (int)act, (float)slope, (int)crop_h, (int)crop_w,
+                              (int)flags, o16, ws, stream_of(x0)),
+      "conv_gen_fwd_out16");
 }
 
 void pconv_mask(const Tensor& m0, int64_t C0, const OptT& m1, int64_t C1, int64_t N, int64_t Hin,
@@ -607,10 +615,18 @@ void affine_act(const Tensor& y, const Tensor& scale, const Tensor& shift, int64
       "affine_act");
 }
 
-void maxpool2(const Tensor& x, const Tensor& y) {
+void maxpool2(const Tensor& x, const Tensor& y, const OptT& out16) {
   GUARD(x);
   TORCH_CHECK(x.dim() == 4, "x must be [N,C,H,W]");
   numel_is(y, x.size(0) * x.size(1) * (x.size(2) / 2) * (x.size(3) / 2), "y");
+  if (out16.has_value() && out16->defined()) {
+    numel_is(*out16, y.numel(), "out16");
+    chk(ainp_maxpool2_nhwc16(dev(x, "x"), dev(y, "y"), x.size(0), (int)x.size(1),
+                             (int)x.size(2), (int)x.size(3), bf16p(*out16, "out16", true),
+                             stream_of(x)),
+        "maxpool2_nhwc16");
+    return;
+  }
   chk(ainp_maxpool2(dev(x, "x"), dev(y, "y"), x.size(0) * x.size(1), (int)x.size(2),
                     (int)x.size(3), stream_of(x)),
       "maxpool2");
@@ -1426,12 +1442,12 @@ TORCH_LIBRARY(ainp, m) {
   m.def("conv_gen_fwd(Tensor x0, Tensor? m0, Tensor? x1, Tensor? m1, Tensor w, Tensor? wt, "
         "Tensor? bias, Tensor? ratio, Tensor? scale, Tensor(a!) y, Tensor(b!)? stats, int Hin, "
         "int Win, int stride, int pad, int act, float slope, int crop_h, int crop_w, int flags, "
-        "Tensor(c!)? workspace) -> ()");
+        "Tensor(c!)? workspace, Tensor(d!)? y16=None) -> ()");
   m.def("pconv_mask(Tensor m0, int C0, Tensor? m1, int C1, int N, int Hin, int Win, int k, "
         "int stride, int pad, float winsize, Tensor(a!)? ratio, Tensor(b!)? newmask) -> ()");
   m.def("gan_pad_input(Tensor x, Tensor m, Tensor(a!) xp, Tensor(b!) mp) -> ()");
   m.def("affine_act(Tensor(a!) y, Tensor scale, Tensor shift, int act, float slope) -> ()");
-  m.def("maxpool2(Tensor x, Tensor(a!) y) -> ()");
+  m.def("maxpool2(Tensor x, Tensor(a!) y, Tensor(b!)? out16=None) -> ()");
   m.def("absdiff_mean(Tensor a, Tensor b, Tensor(a!) workspace, Tensor(b!) out) -> ()");
   m.def("bce_logits(Tensor x, float target, Tensor(a!)? grad, float grad_scale, "
         "Tensor(b!) workspace, Tensor(c!) out) -> ()");

@@ -114,7 +114,7 @@ HOST_ONLY = {"ainp_abi_version", "ainp_build_target", "ainp_last_error", "ainp_r
 
 def test_torch_library_registers_every_gpu_entry_point():
     """b2: torch.ops.ainp.* (csrc/torch_ops.cpp) covers every launching entry
-    point of include/ainp.h -- the newest form of each (_ex / _ld variants);
+    point of include/ainp.h -- the newest form of each (_ex / _ld / _out16 variants);
     the remaining symbols are host-only queries or older forms of the same
     launch."""
     import torch
@@ -124,7 +124,7 @@ def test_torch_library_registers_every_gpu_entry_point():
     declared = set(declared_symbols())
     covered = set()
     for n in names:
-        cands = [f"ainp_{n}{suf}" for suf in ("", "_ex", "_f32_ex")]
+        cands = [f"ainp_{n}{suf}" for suf in ("", "_ex", "_f32_ex", "_out16", "_nhwc16")]
         hit = [c for c in cands if c in declared]
         assert hit, n
         covered.update(hit)

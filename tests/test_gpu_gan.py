@@ -258,6 +258,85 @@ def test_conv_gen_epilogue_nhwc16_copy(case):
     assert torch.equal(y, y2) and torch.equal(st, st2)   # y / stats unchanged by out16
 
 
+@pytest.mark.parametrize("case", [
+    (2, 1, 37, 70, 64, 4, 2, 1, 2),     # the discriminator's first conv (LeakyReLU)
+    (2, 3, 20, 26, 64, 3, 1, 1, 1),     # VGG19 conv1_1 (ReLU)
+    (1, 2, 9, 13, 16, 3, 1, 1, 0),      # 16 channels, no activation
+])
+def test_conv_gen_direct_kernel_nhwc16_copy(case):
+    """out16 on the few-input-channel direct kernel (ainp_conv_gen_fwd_out16):
+    its bf16 channel-last copy equals to_nhwc16(y) bit for bit, to_nhwc16
+    finds it in the memo, and y is unchanged."""
+    from ainp import ops
+    N, C, H, W, Cout, k, s, p, act = case
+    g = torch.Generator().manual_seed(5 + Cout + C)
+    x = torch.randn(N, C, H, W, generator=g).cuda()
+    w = (torch.randn(Cout, C, k, k, generator=g) * 0.2).cuda()
+    b = torch.randn(Cout, generator=g).cuda()
+    assert ops._direct_route(C, 0, H, W, H, W, k, k, Cout, False)
+    with ops.nhwc16_memo():
+        y, _ = ops.conv_gen((x, None), w, stride=s, pad=p, bias=b, act=act, bf16=True, out16=True)
+        key = (y.data_ptr(), tuple(y.shape), y._version, 0, -1)
+        assert key in ops._NHWC_MEMO
+        y16 = ops.to_nhwc16(y)
+        assert y16 is ops._NHWC_MEMO[key][0]
+    ref = ops.to_nhwc16(y)
+    torch.cuda.synchronize()
+    assert torch.equal(y16.view(torch.int16), ref.view(torch.int16))
+    y2, _ = ops.conv_gen((x, None), w, stride=s, pad=p, bias=b, act=act, bf16=True)
+    assert torch.equal(y, y2)
+
+
+@pytest.mark.parametrize("case", [
+    # N, C, Hs, Ws, Hin, Win, k, stride, pad, mask
+    (2, 1, 40, 150, 40, 150, 7, 2, 3, True),     # the U-Net's first conv (7x7 / 2)
+    (2, 1, 21, 70, 21, 70, 3, 1, 1, True),       # the final PartialConv's input source
+    (1, 2, 10, 33, 20, 66, 3, 1, 1, True),       # nearest x2 resampling, 2 channels
+    (1, 3, 9, 14, 20, 30, 5, 2, 2, False),       # general nearest resampling, no mask
+    (1, 4, 12, 300, 12, 300, 7, 2, 3, False),    # wide rows (several pixel blocks)
+])
+def test_im2col_nhwc16_matches_unfold(case):
+    """ainp_im2col_nhwc16: bf16 rows [N*Ho*Wo][seg], k = tap*C + ci, of the
+    source times its mask plane resampled to Hin x Win (index i*Hs//Hin), zero
+    past KK*C -- equal bit for bit to torch's unfold of the same values."""
+    from ainp import ops
+    N, C, Hs, Ws, Hin, Win, k, st, pd, use_m = case
+    g = torch.Generator().manual_seed(Hs * Ws + C)
+    x = torch.randn(N, C, Hs, Ws, generator=g)
+    m = (torch.rand(N, Hs, Ws, generator=g) > 0.3).float() if use_m else None
+    Ho, Wo = (Hin + 2 * pd - k) // st + 1, (Win + 2 * pd - k) // st + 1
+    KK = k * k
+    seg = ops.nhwc16_seg(C, KK)
+    out = torch.empty(N * Ho * Wo, seg, dtype=torch.bfloat16, device="cuda")
+    ops._T.im2col_nhwc16(x.cuda(), m.cuda() if use_m else None, Hin, Win, k, k, st, pd, out)
+    xm = x * m[:, None] if use_m else x
+    sy, sx = (torch.arange(Hin) * Hs) // Hin, (torch.arange(Win) * Ws) // Win
+    xr = xm[:, :, sy][:, :, :, sx]
+    u = torch.nn.functional.unfold(xr, k, padding=pd, stride=st)       # [N, C*KK, L]
+    u = u.view(N, C, KK, Ho * Wo).permute(0, 3, 2, 1).reshape(N * Ho * Wo, KK * C)
+    exp = torch.zeros(N * Ho * Wo, seg, dtype=torch.bfloat16)
+    exp[:, :KK * C] = u.bfloat16()
+    assert torch.equal(out.cpu().view(torch.int16), exp.view(torch.int16))
+
+
+@pytest.mark.parametrize("shape", [(2, 64, 24, 30), (1, 200, 9, 131), (3, 3, 5, 7)])
+def test_maxpool2_nhwc16_copy(shape):
+    """ainp_maxpool2_nhwc16: y equals ainp_maxpool2's, the copy equals
+    to_nhwc16(y) bit for bit and is what to_nhwc16 finds in the memo (odd H / W:
+    the last row / column dropped; C not a multiple of 64 / 2)."""
+    from ainp import ops
+    x = torch.randn(*shape, generator=torch.Generator().manual_seed(shape[1])).cuda()
+    with ops.nhwc16_memo():
+        y = ops.maxpool2(x, out16=True)
+        y16 = ops.to_nhwc16(y)
+        key = (y.data_ptr(), tuple(y.shape), y._version, 0, -1)
+        assert y16 is ops._NHWC_MEMO[key][0]
+    assert torch.equal(y, ops.maxpool2(x))
+    assert torch.equal(y, torch.nn.functional.max_pool2d(x, 2))
+    torch.cuda.synchronize()
+    assert torch.equal(y16.view(torch.int16), ops.to_nhwc16(y).view(torch.int16))
+
+
 @pytest.mark.parametrize("k,s,p,crop,act,C,H,W", [
     (3, 1, 1, (25, 30), 3, 64, 32, 40), (4, 1, 1, None, 0, 64, 32, 40),
     (4, 2, 1, None, 2, 64, 32, 40),
