@@ -824,6 +824,17 @@ int ainp_d_prep16(const float* g, int nslab, int64_t slab_stride, const float* y
                   void* stream);
 int ainp_im2col16(const float* x, int64_t N, int C, int H, int W, int KH, int KW, int stride,
                   int pad, int ones_row, uint16_t* col, int64_t ldA, void* stream);
+/* ainp_wgrad16_nhwc: the weight gradient ainp_im2col16 + ainp_gemm_bf16nt
+ * compute, [dW | db] = gA . [col ; 1]^T over K = ldA, without materialising
+ * the columns: the GEMM's B operand is gathered from the layer input's
+ * channel-last bf16 copy x16 [N][H][W][Cin] (Cin % 8 == 0; the copy the
+ * forward conv read).  G [nsplit][Cout][Cin*k*k + 1] (column ci*k*k + tap,
+ * then the bias), split-K slabs kc apart in K as ainp_gemm_bf16nt's (kc % 64
+ * == 0; nsplit 1: kc ignored); bit-identical to the two-call route with the
+ * same split. */
+int ainp_wgrad16_nhwc(const uint16_t* gA, int64_t ldA, int Cout, const uint16_t* x16, int64_t N,
+                      int Cin, int H, int W, int k, int stride, int pad, float* G, int nsplit,
+                      int64_t kc, void* stream);
 /* ainp_wgrad_cout1: the weight gradient of a Cout = 1 conv (k = 3 or 4; the
  * discriminator's logit conv, networks.py:403-406) straight from the fp32
  * input x [N][Cin][H][W] and g = sum of nslab slabs [N][1][Ho][Wo] (times
@@ -840,6 +851,17 @@ int ainp_dgrad16_weight(const float* w, int Cout, int Cin, int k, int stride, in
 int ainp_dgrad16(const uint16_t* gT, int64_t N, int Cout, int Ho, int Wo, const uint16_t* wd,
                  int Cin, int H, int W, int k, int stride, int pad, const float* scale,
                  float* out, int nsplit, int64_t slab_stride, void* stream);
+/* ainp_dgrad16 (nsplit 1) followed by ainp_d_prep16 of its dx, in one pass:
+ * the data-gradient epilogue multiplies by LeakyReLU'(y) (y [N][Cin][H][W],
+ * NULL = none), rounds to bf16 and writes gA [Cin][ldA] (q = n*H*W + pixel,
+ * zero for N*H*W <= q < ldA) and, when gTo != NULL, gTo [N*H*W][Cin] -- the
+ * next (lower) discriminator layer's two gradient operands, bit for bit what
+ * the two calls give, without the fp32 dx round trip.  Cin % 4 == 0,
+ * gTo 8-byte aligned. */
+int ainp_dgrad16_prep(const uint16_t* gT, int64_t N, int Cout, int Ho, int Wo,
+                      const uint16_t* wd, int Cin, int H, int W, int k, int stride, int pad,
+                      const float* scale, const float* y, float slope, uint16_t* gA,
+                      int64_t ldA, uint16_t* gTo, void* stream);
 /* PartialConv2d called with a per-channel mask (networks.py:74-85 when
  * mask.shape[1] == C_in): out = a*b elementwise, and the channel sum of the
  * mask [N,C,HW] -> [N,HW] whose window sum is the mask_conv count. */

@@ -172,6 +172,10 @@ _SIGS = {
     "ainp_dgrad16_weight": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "ainp_dgrad16": (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int, c_int,
                              c_int, P, P, c_int, c_int64, P]),
+    "ainp_wgrad16_nhwc": (c_int, [P, c_int64, c_int, P, c_int64, c_int, c_int, c_int, c_int,
+                                  c_int, c_int, P, c_int, c_int64, P]),
+    "ainp_dgrad16_prep": (c_int, [P, c_int64, c_int, c_int, c_int, P, c_int, c_int, c_int, c_int,
+                                  c_int, c_int, P, P, c_float, P, c_int64, P, P]),
     "ainp_nchw_to_nhwc16": (c_int, [P, P, c_int64, c_int, c_int, c_int, P, P]),
     "ainp_conv_weight_nhwc16": (c_int, [P, c_int, c_int, c_int, c_int, c_int, P, P]),
     "ainp_im2col_nhwc16": (c_int, [P, P, c_int64, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

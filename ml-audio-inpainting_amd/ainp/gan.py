@@ -599,6 +599,9 @@ class _DiscriminatorFn(torch.autograd.Function):
                 ins.append(h)
                 outs.append(y)
                 h = y
+            # the channel-last bf16 inputs the convs read: the bf16 backward's
+            # weight gradients gather from them (ainp_wgrad16_nhwc)
+            ctx.h16 = [ops.nhwc16_memo_get(t) if bf16 else None for t in ins]
         ctx.cfg = cfg
         ctx.bf16 = bf16
         ctx.nl = len(cfg)
@@ -658,6 +661,12 @@ SN_FOREACH = os.environ.get("AINP_SN_FOREACH", "1") != "0"
 # bf16 configurations: the D backward on bf16 operands in HBM (csrc/dconv16.hip);
 # AINP_D_BWD16=0 keeps the fp32-staged im2col / GEMM / col2im loop
 D_BWD16 = os.environ.get("AINP_D_BWD16", "1") != "0"
+# weight gradients of layers with a channel-last bf16 input copy as implicit
+# GEMMs over it (ainp_wgrad16_nhwc; 0: im2col16 + gemm_bf16nt, A/B)
+WGRAD16_NHWC = os.environ.get("AINP_WGRAD16_NHWC", "1") != "0"
+# the data gradient of a layer writes the lower layer's bf16 gradient operands
+# itself where it runs unsplit (ainp_dgrad16_prep; 0: dgrad16 + d_prep16, A/B)
+D_PREP_FUSED = os.environ.get("AINP_D_PREP_FUSED", "1") != "0"
 # the logit conv's weight gradient by ainp_wgrad_cout1 (0: im2col16 + GEMM, A/B)
 WGRAD_COUT1 = os.environ.get("AINP_WGRAD_COUT1", "1") != "0"
 
@@ -665,13 +674,15 @@ WGRAD_COUT1 = os.environ.get("AINP_WGRAD_COUT1", "1") != "0"
 def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
     """_DiscriminatorFn.backward with bf16 operands: per layer the gradient is
     cast once into a pixel-contiguous and a channel-last bf16 copy (LeakyReLU
-    backward and the split-K slabs of the layer above folded in), the weight
+    backward and the split-K slabs of the layer above folded in; written by
+    the layer above's data-gradient epilogue where that runs unsplit), the weight
     gradient is one bf16 GEMM over every image's pixels, the data gradient a
     parity-class implicit GEMM (csrc/dconv16.hip)."""
     L = ctx.nl
     grads = [None] * len(params)
     gsrc, nslab = g.contiguous(), 1
     gx = None
+    pre = None    # this layer's (gA, gT), written by the layer above's data gradient
     for l in range(L - 1, -1, -1):
         k, s, p, act = ctx.cfg[l]
         w = params[2 * l]
@@ -687,15 +698,34 @@ def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
             gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P, ldA,
                               want_gT=True)[1] if need_dx else None
         else:
-            gA, gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P, ldA,
-                                  want_gT=need_dx)
-            col = ops.im2col16(h, k, s, p, ldA)                  # [Cin*k*k + 1, ldA]
-            Gw = ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=512)
+            if pre is not None:
+                gA, gT = pre
+            else:
+                gA, gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P,
+                                      ldA, want_gT=need_dx)
+            h16 = ctx.h16[l] if WGRAD16_NHWC else None
+            if h16 is not None and Cin % 8 == 0:
+                # implicit GEMM over the forward's channel-last input copy
+                Gw = ops.wgrad16_nhwc(gA, h16, k, s, p, max_split=512)
+            else:
+                col = ops.im2col16(h, k, s, p, ldA)              # [Cin*k*k + 1, ldA]
+                Gw = ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=512)
         dw, db = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1], with_bias=True)
         grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
+        pre = None
         if need_dx:
             S = ops.dgrad16_nsplit(N, Cin, H, W, k, s, Cout)
-            gsrc = ops.dgrad16(gT.view(N, Ho, Wo, Cout), ops.dgrad16_weight(w, s, p), Cin, H, W,
+            wd = ops.dgrad16_weight(w, s, p)
+            if D_PREP_FUSED and l > 0 and S == 1 and Cin % 4 == 0:
+                # the lower layer's gA / gT straight from this data gradient's
+                # epilogue (no fp32 dx, no d_prep16 pass)
+                act_lo = ctx.cfg[l - 1][3]
+                pre = ops.dgrad16_prep(gT.view(N, Ho, Wo, Cout), wd, Cin, H, W, k, s, p,
+                                       outs[l - 1] if act_lo else None, SLOPE,
+                                       -(-N * H * W // 64) * 64, scale=inv[l:l + 1],
+                                       want_gT=l - 1 > 0 or ctx.needs_input_grad[0])
+                continue
+            gsrc = ops.dgrad16(gT.view(N, Ho, Wo, Cout), wd, Cin, H, W,
                                k, s, p, scale=inv[l:l + 1], nsplit=S)
             nslab = S
             if l == 0:

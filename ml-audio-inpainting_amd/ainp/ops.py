@@ -1388,6 +1388,47 @@ def dgrad16(gT, wd, Cin, H, W, k, stride, pad, scale=None, nsplit=1):
     return out
 
 
+def wgrad16_nhwc(gA, x16, k, stride, pad, max_split=512):
+    """ainp_wgrad16_nhwc: [dW | db] [Cout, Cin*k*k + 1] from gA bf16 [Cout, ldA]
+    and the layer input's channel-last bf16 copy x16 [N, H, W, Cin] -- what
+    gemm_bf16nt_splitk(gA, im2col16(x, ...), ldA) gives, bit for bit."""
+    Cout, ldA = gA.shape[0], gA.shape[1]
+    Cin = x16.shape[3]
+    Ncol = Cin * k * k + 1
+    S = _splitk_bf16(Cout, Ncol, ldA, max_split=max_split)
+    kc = -(-ldA // S // 64) * 64 if S > 1 else ldA
+    G = torch.empty(S, Cout, Ncol, device=gA.device, dtype=torch.float32)
+    _T.wgrad16_nhwc(gA, x16, int(k), int(stride), int(pad), G, int(S), int(kc))
+    if S == 1:
+        return G[0]
+    out = torch.empty(Cout, Ncol, device=gA.device, dtype=torch.float32)
+    sum_slabs(G, S, out=out.view(-1))
+    return out
+
+
+def nhwc16_memo_get(x):
+    """The channel-last bf16 copy of x (no mask plane) held by the active
+    nhwc16_memo scope, or None."""
+    memo = _NHWC_MEMO
+    if memo is None:
+        return None
+    hit = memo.get((x.data_ptr(), tuple(x.shape), x._version, 0, -1))
+    return hit[0] if hit is not None else None
+
+
+def dgrad16_prep(gT, wd, Cin, H, W, k, stride, pad, y, slope, ldA, scale=None, want_gT=True):
+    """ainp_dgrad16_prep: dgrad16 (nsplit 1) then d_prep16 of its dx in one
+    pass -> (gA bf16 [Cin, ldA], gT bf16 [N*H*W, Cin] or None), the lower
+    layer's gradient operands, bit for bit those of the two calls."""
+    N = gT.shape[0]
+    gA = torch.empty(Cin, ldA, device=gT.device, dtype=torch.bfloat16)
+    gTo = (torch.empty(N * H * W, Cin, device=gT.device, dtype=torch.bfloat16)
+           if want_gT else None)
+    _T.dgrad16_prep(gT, wd, int(Cin), int(H), int(W), int(k), int(stride), int(pad), scale, y,
+                    float(slope), gA, gTo)
+    return gA, gTo
+
+
 def col2im(dcol, N, C, H, W, k, stride, pad):
     """dcol [N, C*k*k, ldp] (ldp >= Ho*Wo) -> dx [N, C, H, W]."""
     _req(dcol, "dcol")

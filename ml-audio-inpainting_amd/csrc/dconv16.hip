@@ -169,10 +169,18 @@ struct DgradArgs {
   float* out;           // [nsplit][N][Cin][H][W]
   int64_t slab;         // elements per split slab
   int N, Cout, Ho, Wo, Cin, H, W, k, s, pad, ktiles_per_split;
+  // PREP epilogue (ainp_dgrad16_prep, nsplit 1): d_prep16_kernel's outputs of
+  // dx instead of dx -- times LeakyReLU'(y) (y == null: none), bf16 gA
+  // [Cin][ldA] (q = n*H*W + pixel) and, if gTo, gTo [N*H*W][Cin]
+  const float* y;
+  float slope;
+  uint16_t* gA;
+  int64_t ldA;
+  uint16_t* gTo;
 };
 
 // grid (pixel tiles of the largest class, Cin / BM, s*s * nsplit)
-template <int BM, bool GATHER>
+template <int BM, bool GATHER, bool PREP = false>
 __global__ __launch_bounds__(256, 4) void dgrad16_kernel(DgradArgs d) {
   constexpr int XBK = 32;
   constexpr int BN = 16384 / BM;
@@ -319,6 +327,40 @@ __global__ __launch_bounds__(256, 4) void dgrad16_kernel(DgradArgs d) {
   const float sc = d.scale ? *d.scale : 1.f;
   float* ob = d.out + (int64_t)split * d.slab;
   const int64_t HW = (int64_t)d.H * d.W;
+  if (PREP) {
+    // rows ci0 .. ci0+3 of a lane's accumulators are 4 consecutive channels:
+    // one 8-byte gTo store per 4 values (Cin % 4 == 0, checked on the host)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t pg = px0 + wn * 64 + 32 * j + l31;
+      if (pg >= NPc) continue;
+      const int pn = (int)(pg / HWc);
+      const int r = (int)(pg - (int64_t)pn * HWc);
+      const int i = r / Wc, jj = r - i * Wc;
+      const int64_t pix = (int64_t)(d.s * i + c.py) * d.W + d.s * jj + c.px;
+      const int64_t q = (int64_t)pn * HW + pix;
+      const float* yb = d.y ? d.y + (int64_t)pn * d.Cin * HW + pix : nullptr;
+#pragma unroll
+      for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+        for (int r4 = 0; r4 < 4; ++r4) {
+          const int ci0 = co0 + wm * 64 + 32 * ii + 8 * r4 + 4 * lh;
+          if (ci0 >= d.Cin) continue;
+          uint32_t h[2];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float v = acc[ii][j][4 * r4 + e] * sc;
+            if (yb && !(yb[(int64_t)(ci0 + e) * HW] > 0.f)) v *= d.slope;
+            const uint16_t b = to_bf16(v);
+            d.gA[(int64_t)(ci0 + e) * d.ldA + q] = b;
+            if (e & 1) h[e >> 1] |= (uint32_t)b << 16;
+            else h[e >> 1] = b;
+          }
+          if (d.gTo) *reinterpret_cast<uint2*>(d.gTo + q * d.Cin + ci0) = make_uint2(h[0], h[1]);
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t pg = px0 + wn * 64 + 32 * j + l31;
@@ -494,6 +536,17 @@ extern "C" int64_t ainp_wgrad_cout1_workspace(int Cin, int k) {
   return (int64_t)d16::WC1_S * ((int64_t)Cin * k * k + 1) * (int64_t)sizeof(float);
 }
 
+// the grid of ainp_dgrad16 / ainp_dgrad16_prep
+static int dgrad16_grid(int64_t N, int Cin, int H, int W, int stride, int nsplit, int BM,
+                        dim3* grid) {
+  const int64_t Hc = cdiv(H, stride), Wc = cdiv(W, stride);   // class (0, 0): the largest
+  const int64_t tiles = cdiv(N * Hc * Wc, 16384 / BM);
+  const int64_t gz = (int64_t)stride * stride * nsplit;
+  if (tiles > 0x7fffffff || gz > 65535) return record_msg("ainp_dgrad16: grid too large");
+  *grid = dim3((unsigned)tiles, (unsigned)cdiv(Cin, BM), (unsigned)gz);
+  return AINP_OK;
+}
+
 extern "C" int ainp_dgrad16_weight(const float* w, int Cout, int Cin, int k, int stride, int pad,
                                    uint16_t* wd, void* stream) {
   if (!w || !wd || Cout < 1 || Cin < 1 || k < 1 || stride < 1 || k % stride || pad < 0 ||
@@ -521,13 +574,10 @@ extern "C" int ainp_dgrad16(const uint16_t* gT, int64_t N, int Cout, int Ho, int
   const int nkt = d16::seg32(Cout, nt * nt) / 32;
   const int per = (int)cdiv(nkt, nsplit);
   d16::DgradArgs a{gT, wd, scale, out, slab_stride, (int)N, Cout, Ho, Wo, Cin, H, W, k, stride,
-                   pad, per};
+                   pad, per, nullptr, 0.f, nullptr, 0, nullptr};
   const int BM = Cin > 64 ? 128 : 64;
-  const int64_t Hc = cdiv(H, stride), Wc = cdiv(W, stride);   // class (0, 0): the largest
-  const int64_t tiles = cdiv(N * Hc * Wc, 16384 / BM);
-  const int64_t gz = (int64_t)stride * stride * nsplit;
-  if (tiles > 0x7fffffff || gz > 65535) return record_msg("ainp_dgrad16: grid too large");
-  const dim3 grid((unsigned)tiles, (unsigned)cdiv(Cin, BM), (unsigned)gz);
+  dim3 grid;
+  if (const int rc = dgrad16_grid(N, Cin, H, W, stride, nsplit, BM, &grid)) return rc;
   const bool gather = Cout % 32 != 0;
   if (BM == 128 && gather)
     hipLaunchKernelGGL((d16::dgrad16_kernel<128, true>), grid, dim3(256), 0, as_stream(stream), a);
@@ -538,4 +588,39 @@ extern "C" int ainp_dgrad16(const uint16_t* gT, int64_t N, int Cout, int Ho, int
   else
     hipLaunchKernelGGL((d16::dgrad16_kernel<64, false>), grid, dim3(256), 0, as_stream(stream), a);
   return check_launch("dgrad16");
+}
+
+extern "C" int ainp_dgrad16_prep(const uint16_t* gT, int64_t N, int Cout, int Ho, int Wo,
+                                 const uint16_t* wd, int Cin, int H, int W, int k, int stride,
+                                 int pad, const float* scale, const float* y, float slope,
+                                 uint16_t* gA, int64_t ldA, uint16_t* gTo, void* stream) {
+  const int64_t NP = N * (int64_t)H * W;
+  if (!gT || !wd || !gA || N < 1 || Cout < 1 || Cin < 1 || Cin % 4 || k < 1 || stride < 1 ||
+      k % stride || pad < 0 || pad >= k || ((uintptr_t)wd & 15) ||
+      ((Cout % 32 == 0) && ((uintptr_t)gT & 15)) || ldA < NP || ((uintptr_t)gTo & 7))
+    return record_msg("ainp_dgrad16_prep: bad argument (Cin % 4 == 0, ldA >= N*H*W)");
+  if ((H + 2 * pad - k) / stride + 1 != Ho || (W + 2 * pad - k) / stride + 1 != Wo)
+    return record_msg("ainp_dgrad16_prep: Ho/Wo do not match the forward conv of H/W");
+  const int nkt = d16::seg32(Cout, (k / stride) * (k / stride)) / 32;
+  d16::DgradArgs a{gT, wd, scale, nullptr, 0, (int)N, Cout, Ho, Wo, Cin, H, W, k, stride,
+                   pad, nkt, y, slope, gA, ldA, gTo};
+  const int BM = Cin > 64 ? 128 : 64;
+  dim3 grid;
+  if (const int rc = dgrad16_grid(N, Cin, H, W, stride, 1, BM, &grid)) return rc;
+  hipStream_t s = as_stream(stream);
+  if (ldA > NP) {   // the zero tail of every gA row
+    const hipError_t e = hipMemset2DAsync(gA + NP, (size_t)ldA * 2, 0, (size_t)(ldA - NP) * 2,
+                                          (size_t)Cin, s);
+    if (e != hipSuccess) return record_error(e, "dgrad16_prep tail");
+  }
+  const bool gather = Cout % 32 != 0;
+  if (BM == 128 && gather)
+    hipLaunchKernelGGL((d16::dgrad16_kernel<128, true, true>), grid, dim3(256), 0, s, a);
+  else if (BM == 128)
+    hipLaunchKernelGGL((d16::dgrad16_kernel<128, false, true>), grid, dim3(256), 0, s, a);
+  else if (gather)
+    hipLaunchKernelGGL((d16::dgrad16_kernel<64, true, true>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((d16::dgrad16_kernel<64, false, true>), grid, dim3(256), 0, s, a);
+  return check_launch("dgrad16_prep");
 }

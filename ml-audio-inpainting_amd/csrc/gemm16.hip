@@ -213,6 +213,163 @@ __global__ __launch_bounds__(256) void transpose_f32_kernel(const float* __restr
   }
 }
 
+// ------------------------------------------------- implicit-GEMM weight gradient
+// Weight gradient of a k x k / stride s conv with the layer input x in
+// channel-last bf16 (x16 [N][H][W][Cin], the copy the forward conv read):
+//   G[m][ci*KK + tap] = sum_q A[m][q] * x16[n][oy*s+ky-pad][ox*s+kx-pad][ci],
+//   G[m][Cin*KK]      = sum_q A[m][q]          (the bias: a ones row),
+// q = n*Ho*Wo + oy*Wo + ox, A = the bf16 output gradient [M][lda] (d_prep16's
+// gA).  gemm_bf16nt_kernel's tiles, MFMA loop, K order and split-K, with the
+// B operand built from x16 instead of materialised im2col16 columns: GEMM
+// column n = tap*Cin + ci (a 16-byte chunk of 8 channels of one tap per load),
+// the tile's rows gathered for four consecutive q per thread and transposed in
+// registers to the k-contiguous LDS image; the epilogue stores column n at
+// ci*KK + tap.  Same products, same order: bit-identical to im2col16 + GEMM.
+struct WgGeom {
+  const uint16_t* x16;
+  int N, Cin, H, W, KW, KK, stride, pad, Ho, Wo;
+  int64_t NP;
+};
+
+__global__ __launch_bounds__(THREADS, 3) void wgrad16_nhwc_kernel(
+    int64_t M, int64_t Ncol, int64_t K, const uint16_t* __restrict__ A, int64_t lda, WgGeom g,
+    float* __restrict__ C, int64_t ldc, int64_t kc, int64_t strideC, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * IMG];
+  const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t first_n = (bid / per_group) * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+
+  const int64_t split = blockIdx.y;
+  const int64_t kbeg = split * kc;
+  const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
+  float* Cs = C + split * strideC;
+
+  // this thread's B chunk: rows n0 + 8c .. +7 (one tap, 8 channels), q group qg
+  const int tid = threadIdx.x;
+  const int c = tid & 15, qg = tid >> 4;
+  const int64_t nb = n0 + 8 * c;
+  const int64_t KC = (int64_t)g.KK * g.Cin;
+  const int kind = nb < KC ? 0 : (nb == KC ? 1 : 2);   // channels / ones row / past N
+  const int tap = kind == 0 ? (int)(nb / g.Cin) : 0;
+  const int ci0 = kind == 0 ? (int)(nb - (int64_t)tap * g.Cin) : 0;
+  const int ky = tap / g.KW, kx = tap - ky * g.KW;
+  const int64_t HWo = (int64_t)g.Ho * g.Wo;
+
+  uint4 vb[4];
+  auto load_b = [&](int64_t k0) {
+    int64_t q = k0 + 4 * qg;
+    int img = 0, oy = 0, ox = 0;
+    if (q < g.NP) {
+      img = (int)(q / HWo);
+      const int r = (int)(q - (int64_t)img * HWo);
+      oy = r / g.Wo;
+      ox = r - oy * g.Wo;
+    }
+#pragma unroll
+    for (int m = 0; m < 4; ++m, ++q) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (q < kend && q < g.NP) {
+        if (kind == 0) {
+          const int iy = oy * g.stride - g.pad + ky, ix = ox * g.stride - g.pad + kx;
+          if (iy >= 0 && iy < g.H && ix >= 0 && ix < g.W)
+            v = *reinterpret_cast<const uint4*>(
+                g.x16 + (((int64_t)img * g.H + iy) * g.W + ix) * g.Cin + ci0);
+        } else if (kind == 1) {
+          v.x = 0x3F80u;   // 1.0 in row n0 + 8c, zero in the rows after it
+        }
+      }
+      vb[m] = v;
+      if (++ox == g.Wo) {
+        ox = 0;
+        if (++oy == g.Ho) {
+          oy = 0;
+          ++img;
+        }
+      }
+    }
+  };
+  // 4 q x 8 channels -> 8 rows of 4 q (8 bytes each) in the B image
+  auto store_b = [&](unsigned char* img) {
+    const uint32_t w[4][4] = {{vb[0].x, vb[0].y, vb[0].z, vb[0].w},
+                              {vb[1].x, vb[1].y, vb[1].z, vb[1].w},
+                              {vb[2].x, vb[2].y, vb[2].z, vb[2].w},
+                              {vb[3].x, vb[3].y, vb[3].z, vb[3].w}};
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const uint2 lo = make_uint2((w[0][p] & 0xffffu) | (w[1][p] << 16),
+                                  (w[2][p] & 0xffffu) | (w[3][p] << 16));
+      const uint2 hi = make_uint2((w[0][p] >> 16) | (w[1][p] & 0xffff0000u),
+                                  (w[2][p] >> 16) | (w[3][p] & 0xffff0000u));
+      *reinterpret_cast<uint2*>(img + (8 * c + 2 * p) * RS + 8 * qg) = lo;
+      *reinterpret_cast<uint2*>(img + (8 * c + 2 * p + 1) * RS + 8 * qg) = hi;
+    }
+  };
+
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16v acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  Loader la;
+  if (kbeg < kend) {
+    la.load(A, lda, m0, kbeg, M, kend);
+    load_b(kbeg);
+  }
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    if (k0 > kbeg) __syncthreads();
+    la.store(smem);
+    store_b(smem + IMG);
+    __syncthreads();
+    if (k0 + BK < kend) {
+      la.load(A, lda, m0, k0 + BK, M, kend);
+      load_b(k0 + BK);
+    }
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      bf16x8v a[2], b[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        a[i] = frag(smem, wm + i * 32 + li, ks, lh);
+        b[i] = frag(smem + IMG, wn + i * 32 + li, ks, lh);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t n = n0 + wn + j * 32 + li;
+    if (n >= Ncol) continue;
+    int64_t col = n;   // the ones row stays last
+    if (n < KC) {
+      const int t = (int)(n / g.Cin);
+      col = (n - (int64_t)t * g.Cin) * g.KK + t;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cs[m * ldc + col] = acc[i][j][r];
+      }
+  }
+}
+
 }  // namespace g16
 
 // Large GEMMs (M, N >= 512): 256 x 256 x 32 tiles with LDS-DMA staging.
@@ -743,6 +900,31 @@ extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t*
   hipLaunchKernelGGL(g16::gemm_bf16nt_kernel, grid, dim3(g16::THREADS), 0, as_stream(stream), M, N,
                      K, A, lda, B, ldb, C, ldc, kc, strideC, b, (int)tiles_n);
   return check_launch("gemm_bf16nt");
+}
+
+extern "C" int ainp_wgrad16_nhwc(const uint16_t* gA, int64_t ldA, int Cout, const uint16_t* x16,
+                                 int64_t N, int Cin, int H, int W, int k, int stride, int pad,
+                                 float* G, int nsplit, int64_t kc, void* stream) {
+  if (!gA || !x16 || !G || Cout < 1 || N < 1 || Cin < 8 || Cin % 8 || k < 1 || stride < 1 ||
+      pad < 0 || ldA % 8 || ((uintptr_t)gA & 15) || ((uintptr_t)x16 & 15) || nsplit < 1 ||
+      nsplit > 65535)
+    return record_msg("ainp_wgrad16_nhwc: bad argument (Cin % 8 == 0, 16-byte aligned)");
+  const int Ho = (H + 2 * pad - k) / stride + 1, Wo = (W + 2 * pad - k) / stride + 1;
+  const int64_t NP = N * (int64_t)Ho * Wo;
+  if (Ho < 1 || Wo < 1 || ldA < NP) return record_msg("ainp_wgrad16_nhwc: bad shape (ldA >= N*Ho*Wo)");
+  const int64_t K = ldA;   // gA is zero past N*Ho*Wo, as im2col16's columns
+  if (nsplit > 1 && (kc < g16::BK || kc % g16::BK || (int64_t)nsplit * kc < K ||
+                     (int64_t)(nsplit - 1) * kc >= K))
+    return record_msg("ainp_wgrad16_nhwc: split-K needs kc % 64 == 0 covering ldA");
+  if (nsplit == 1) kc = K;
+  const int64_t Ncol = (int64_t)Cin * k * k + 1;
+  g16::WgGeom geo{x16, (int)N, Cin, H, W, k, k * k, stride, pad, Ho, Wo, NP};
+  const int64_t tiles_n = cdiv(Ncol, g16::BN);
+  const dim3 grid((unsigned)(cdiv(Cout, g16::BM) * tiles_n), (unsigned)nsplit);
+  hipLaunchKernelGGL(g16::wgrad16_nhwc_kernel, grid, dim3(g16::THREADS), 0, as_stream(stream),
+                     (int64_t)Cout, Ncol, K, gA, ldA, geo, G, Ncol, kc, (int64_t)Cout * Ncol,
+                     (int)tiles_n);
+  return check_launch("wgrad16_nhwc");
 }
 
 extern "C" int ainp_gemm_x6nt_256(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,

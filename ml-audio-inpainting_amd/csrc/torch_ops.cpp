@@ -1205,6 +1205,43 @@ void dgrad16(const Tensor& gT, const Tensor& wd, int64_t Cin, int64_t H, int64_t
                    dev(out, "out"), (int)nsplit, N * Cin * H * W, stream_of(gT)),
       "dgrad16");
 }
+void wgrad16_nhwc(const Tensor& gA, const Tensor& x16, int64_t k, int64_t stride, int64_t pad,
+                  const Tensor& G, int64_t nsplit, int64_t kc) {
+  GUARD(gA);
+  TORCH_CHECK(gA.dim() == 2 && x16.dim() == 4, "wgrad16_nhwc: gA [Cout, ldA], x16 [N, H, W, Cin]");
+  const int64_t Cout = gA.size(0), N = x16.size(0), H = x16.size(1), W = x16.size(2),
+                Cin = x16.size(3);
+  numel_is(G, nsplit * Cout * (Cin * k * k + 1), "G");
+  chk(ainp_wgrad16_nhwc(bf16p(gA, "gA", false), gA.stride(0), (int)Cout, bf16p(x16, "x16"), N,
+                        (int)Cin, (int)H, (int)W, (int)k, (int)stride, (int)pad, dev(G, "G"),
+                        (int)nsplit, kc, stream_of(gA)),
+      "wgrad16_nhwc");
+}
+
+void dgrad16_prep(const Tensor& gT, const Tensor& wd, int64_t Cin, int64_t H, int64_t W,
+                  int64_t k, int64_t stride, int64_t pad, const OptT& scale, const OptT& y,
+                  double slope, const Tensor& gA, const OptT& gTo) {
+  GUARD(gT);
+  TORCH_CHECK(gT.dim() == 4, "gT must be [N, Ho, Wo, Cout] (channel-last bf16)");
+  const int64_t N = gT.size(0), Ho = gT.size(1), Wo = gT.size(2), Cout = gT.size(3);
+  TORCH_CHECK(stride >= 1 && k % stride == 0, "dgrad16_prep: k % stride == 0");
+  const int64_t nt = k / stride;
+  numel_is(wd, stride * stride * Cin * nhwc16_seg(Cout, nt * nt), "wd");
+  TORCH_CHECK(gA.dim() == 2 && gA.size(0) == Cin && gA.size(1) >= N * H * W,
+              "gA must be [Cin, ldA >= N*H*W]");
+  const float* py = opt(y, "y");
+  if (py) numel_is(*y, N * Cin * H * W, "y");
+  uint16_t* pt = nullptr;
+  if (gTo.has_value() && gTo->defined()) {
+    numel_is(*gTo, N * H * W * Cin, "gTo");
+    pt = bf16p(*gTo, "gTo");
+  }
+  chk(ainp_dgrad16_prep(bf16p(gT, "gT"), N, (int)Cout, (int)Ho, (int)Wo, bf16p(wd, "wd"),
+                        (int)Cin, (int)H, (int)W, (int)k, (int)stride, (int)pad,
+                        opt(scale, "scale"), py, (float)slope, bf16p(gA, "gA"), gA.size(1), pt,
+                        stream_of(gT)),
+      "dgrad16_prep");
+}
 // ---------------------------------------------------------------- generator backward
 // (csrc/gan_bwd.hip; opt-in fix_generator_grad)
 void affine_leaky_out(const Tensor& y, const Tensor& scale, const Tensor& shift, double slope,
@@ -1494,6 +1531,10 @@ TORCH_LIBRARY(ainp, m) {
   m.def("dgrad16_weight(Tensor w, int stride, int pad, Tensor(a!) wd) -> ()");
   m.def("dgrad16(Tensor gT, Tensor wd, int Cin, int H, int W, int k, int stride, int pad, "
         "Tensor? scale, Tensor(a!) out, int nsplit) -> ()");
+  m.def("wgrad16_nhwc(Tensor gA, Tensor x16, int k, int stride, int pad, Tensor(a!) G, "
+        "int nsplit, int kc) -> ()");
+  m.def("dgrad16_prep(Tensor gT, Tensor wd, int Cin, int H, int W, int k, int stride, int pad, "
+        "Tensor? scale, Tensor? y, float slope, Tensor(a!) gA, Tensor(b!)? gTo) -> ()");
   m.def("affine_leaky_out(Tensor y, Tensor scale, Tensor shift, float slope, Tensor(a!) out) -> ()");
   m.def("pconv_src_materialize(Tensor x0, Tensor? m0, Tensor? x1, Tensor? m1, int Hin, int Win, "
         "Tensor(a!) out) -> ()");
@@ -1578,6 +1619,8 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("im2col16", &im2col16);
   m.impl("dgrad16_weight", &dgrad16_weight);
   m.impl("dgrad16", &dgrad16);
+  m.impl("dgrad16_prep", &dgrad16_prep);
+  m.impl("wgrad16_nhwc", &wgrad16_nhwc);
   m.impl("affine_leaky_out", &affine_leaky_out);
   m.impl("pconv_src_materialize", &pconv_src_materialize);
   m.impl("pconv_src_grad", &pconv_src_grad);
@@ -1657,6 +1700,8 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("im2col16", torch::CppFunction::makeFallthrough());
   m.impl("dgrad16_weight", torch::CppFunction::makeFallthrough());
   m.impl("dgrad16", torch::CppFunction::makeFallthrough());
+  m.impl("dgrad16_prep", torch::CppFunction::makeFallthrough());
+  m.impl("wgrad16_nhwc", torch::CppFunction::makeFallthrough());
   m.impl("affine_leaky_out", torch::CppFunction::makeFallthrough());
   m.impl("pconv_src_materialize", torch::CppFunction::makeFallthrough());
   m.impl("pconv_src_grad", torch::CppFunction::makeFallthrough());

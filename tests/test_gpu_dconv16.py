@@ -162,3 +162,108 @@ def test_d_backward16_input_gradient(monkeypatch):
     e_new, e_old = rel(grads[True], h.grad), rel(grads[False], h.grad)
     print("bf16 D input grad rel err (dconv16, fp32-staged):", e_new, e_old)
     assert e_new < 2 * e_old + 5e-3, (e_new, e_old)
+
+
+@pytest.mark.parametrize("case", [c for c in DGRAD_CASES if c[-1] == 1 and c[2] % 4 == 0])
+@pytest.mark.parametrize("act", [True, False])
+def test_dgrad16_prep_equals_dgrad16_then_d_prep16(case, act):
+    """ainp_dgrad16_prep: the lower layer's gA / gT from the data gradient's
+    epilogue, bit for bit what ainp_dgrad16 (nsplit 1) + ainp_d_prep16 give
+    (LeakyReLU' of y, bf16 rounding, zero gA tail, gT optional)."""
+    from ainp import ops
+    N, Cout, Cin, H, W, k, s, p, _ = case
+    g = torch.Generator().manual_seed(sum(case) + act)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.1).cuda()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    gT = torch.randn(N, Ho, Wo, Cout, generator=g).bfloat16().cuda()
+    y = torch.randn(N, Cin, H, W, generator=g).cuda() if act else None
+    scale = torch.tensor([0.37]).cuda()
+    wd = ops.dgrad16_weight(w, s, p)
+    P = H * W
+    ldA = -(-N * P // 64) * 64 + 64          # a tail past N*P
+    dx = ops.dgrad16(gT, wd, Cin, H, W, k, s, p, scale=scale, nsplit=1)
+    eA, eT = ops.d_prep16(dx, 1, y, 0.2, N, Cin, P, ldA, want_gT=True)
+    for want in (True, False):
+        gA, gTo = ops.dgrad16_prep(gT, wd, Cin, H, W, k, s, p, y, 0.2, ldA, scale=scale,
+                                   want_gT=want)
+        torch.cuda.synchronize()
+        assert torch.equal(gA.view(torch.int16), eA.view(torch.int16))
+        if want:
+            assert torch.equal(gTo.view(torch.int16), eT.view(torch.int16))
+        else:
+            assert gTo is None
+
+
+def test_d_backward16_prep_fused_is_bit_identical(monkeypatch):
+    """The bf16 D backward with the fused data-gradient epilogue
+    (AINP_D_PREP_FUSED) gives the same parameter and input gradients, bit for
+    bit, as dgrad16 + d_prep16."""
+    from ainp import gan as G
+    torch.manual_seed(5)
+    D = G.Discriminator().cuda().eval()
+    D.ainp_bf16 = True
+    x0 = torch.randn(2, 1, 64, 96, device="cuda")
+
+    def run(fused):
+        monkeypatch.setattr(G, "D_PREP_FUSED", fused)
+        for q in D.parameters():
+            q.grad = None
+        x = x0.clone().requires_grad_(True)
+        out = D(x)
+        out.backward(torch.ones_like(out))
+        return [q.grad.clone() for q in D.parameters()] + [x.grad.clone()]
+
+    a, b = run(True), run(False)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("case", [
+    # N, Cin, H, W, Cout, k, s, p, max_split
+    (2, 64, 21, 30, 128, 4, 2, 1, 512),     # D layer 1-like, split-K
+    (1, 128, 17, 26, 256, 4, 2, 1, 1),      # odd sizes, unsplit
+    (2, 256, 9, 12, 200, 4, 1, 1, 512),     # stride 1, ragged Cout tile
+    (1, 8, 7, 9, 64, 3, 1, 1, 4),           # 3x3, 8 channels (one chunk per tap)
+])
+def test_wgrad16_nhwc_equals_im2col16_gemm(case):
+    """ainp_wgrad16_nhwc (implicit GEMM over the channel-last bf16 input) is
+    bit-identical to im2col16 + gemm_bf16nt_splitk with the same split."""
+    from ainp import ops
+    N, Cin, H, W, Cout, k, s, p, ms = case
+    g = torch.Generator().manual_seed(sum(case))
+    x = torch.randn(N, Cin, H, W, generator=g).cuda()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    NP = N * Ho * Wo
+    ldA = -(-NP // 64) * 64
+    gy = torch.randn(N, Cout, Ho, Wo, generator=g).cuda()
+    gA, _ = ops.d_prep16(gy, 1, None, 0.2, N, Cout, Ho * Wo, ldA, want_gT=False)
+    col = ops.im2col16(x, k, s, p, ldA)
+    ref = ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=ms)
+    got = ops.wgrad16_nhwc(gA, ops.to_nhwc16(x), k, s, p, max_split=ms)
+    torch.cuda.synchronize()
+    assert got.shape == ref.shape
+    assert torch.equal(got, ref)
+
+
+def test_d_backward16_wgrad_nhwc_is_bit_identical(monkeypatch):
+    """The bf16 D backward with implicit-GEMM weight gradients
+    (AINP_WGRAD16_NHWC) gives the same gradients, bit for bit, as im2col16 +
+    gemm_bf16nt."""
+    from ainp import gan as G
+    torch.manual_seed(6)
+    D = G.Discriminator().cuda().eval()
+    D.ainp_bf16 = True
+    x0 = torch.randn(2, 1, 64, 96, device="cuda")
+
+    def run(nhwc):
+        monkeypatch.setattr(G, "WGRAD16_NHWC", nhwc)
+        for q in D.parameters():
+            q.grad = None
+        x = x0.clone().requires_grad_(True)
+        out = D(x)
+        out.backward(torch.ones_like(out))
+        return [q.grad.clone() for q in D.parameters()] + [x.grad.clone()]
+
+    a, b = run(True), run(False)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
