@@ -601,7 +601,8 @@ class _DiscriminatorFn(torch.autograd.Function):
                 h = y
             # the channel-last bf16 inputs the convs read: the bf16 backward's
             # weight gradients gather from them (ainp_wgrad16_nhwc)
-            ctx.h16 = [ops.nhwc16_memo_get(t) if bf16 else None for t in ins]
+            keep = bf16 and WGRAD16_NHWC
+            ctx.h16 = [ops.nhwc16_memo_get(t) if keep else None for t in ins]
         ctx.cfg = cfg
         ctx.bf16 = bf16
         ctx.nl = len(cfg)
@@ -661,9 +662,12 @@ SN_FOREACH = os.environ.get("AINP_SN_FOREACH", "1") != "0"
 # bf16 configurations: the D backward on bf16 operands in HBM (csrc/dconv16.hip);
 # AINP_D_BWD16=0 keeps the fp32-staged im2col / GEMM / col2im loop
 D_BWD16 = os.environ.get("AINP_D_BWD16", "1") != "0"
-# weight gradients of layers with a channel-last bf16 input copy as implicit
-# GEMMs over it (ainp_wgrad16_nhwc; 0: im2col16 + gemm_bf16nt, A/B)
-WGRAD16_NHWC = os.environ.get("AINP_WGRAD16_NHWC", "1") != "0"
+# AINP_WGRAD16_NHWC=1: weight gradients of layers with a channel-last bf16
+# input copy as implicit GEMMs over it (ainp_wgrad16_nhwc, bit-identical).  Off:
+# in the C4 step 9.35 -> 9.54 ms/step; standalone it wins only at layer 1 (119
+# vs 157 us) and loses at layers 2 / 3 (122 vs 100, 311 vs 184 us): the 128 x
+# 128 tiles re-gather the input per Cout tile (profiles/r04p_summary.txt)
+WGRAD16_NHWC = os.environ.get("AINP_WGRAD16_NHWC", "0") == "1"
 # the data gradient of a layer writes the lower layer's bf16 gradient operands
 # itself where it runs unsplit (ainp_dgrad16_prep; 0: dgrad16 + d_prep16, A/B)
 D_PREP_FUSED = os.environ.get("AINP_D_PREP_FUSED", "1") != "0"

@@ -235,17 +235,16 @@ __global__ __launch_bounds__(THREADS, 3) void wgrad16_nhwc_kernel(
     int64_t M, int64_t Ncol, int64_t K, const uint16_t* __restrict__ A, int64_t lda, WgGeom g,
     float* __restrict__ C, int64_t ldc, int64_t kc, int64_t strideC, int tiles_n) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * IMG];
+  // one linear grid of tiles x splits, numbered XCD-major: each XCD owns a
+  // contiguous run of splits with all their tiles, so the tiles that gather
+  // the same input pixels (same K range, other taps / channels) share its L2
   const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
   const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
   const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
   const int64_t tiles_m = (M + BM - 1) / BM;
-  const int64_t per_group = 8 * tiles_m;
-  const int64_t first_n = (bid / per_group) * 8;
-  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
-  const int64_t in_g = bid % per_group;
-  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
-
-  const int64_t split = blockIdx.y;
+  const int64_t tiles = tiles_m * tiles_n;
+  const int64_t split = bid / tiles, t = bid - split * tiles;
+  const int64_t m0 = (t % tiles_m) * BM, n0 = (t / tiles_m) * BN;
   const int64_t kbeg = split * kc;
   const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
   float* Cs = C + split * strideC;
@@ -920,7 +919,9 @@ extern "C" int ainp_wgrad16_nhwc(const uint16_t* gA, int64_t ldA, int Cout, cons
   const int64_t Ncol = (int64_t)Cin * k * k + 1;
   g16::WgGeom geo{x16, (int)N, Cin, H, W, k, k * k, stride, pad, Ho, Wo, NP};
   const int64_t tiles_n = cdiv(Ncol, g16::BN);
-  const dim3 grid((unsigned)(cdiv(Cout, g16::BM) * tiles_n), (unsigned)nsplit);
+  const int64_t nwg = cdiv(Cout, g16::BM) * tiles_n * nsplit;
+  if (nwg > 0x7fffffff) return record_msg("ainp_wgrad16_nhwc: grid too large");
+  const dim3 grid((unsigned)nwg);
   hipLaunchKernelGGL(g16::wgrad16_nhwc_kernel, grid, dim3(g16::THREADS), 0, as_stream(stream),
                      (int64_t)Cout, Ncol, K, gA, ldA, geo, G, Ncol, kc, (int64_t)Cout * Ncol,
                      (int)tiles_n);

@@ -256,7 +256,7 @@ def test_d_backward16_wgrad_nhwc_is_bit_identical(monkeypatch):
     x0 = torch.randn(2, 1, 64, 96, device="cuda")
 
     def run(nhwc):
-        monkeypatch.setattr(G, "WGRAD16_NHWC", nhwc)
+        monkeypatch.setattr(G, "WGRAD16_NHWC", nhwc)   # read by the forward too
         for q in D.parameters():
             q.grad = None
         x = x0.clone().requires_grad_(True)

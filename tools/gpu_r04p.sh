@@ -1,0 +1,33 @@
+#!/bin/bash
+# Round 4: implicit-GEMM discriminator weight gradient (AINP_WGRAD16_NHWC):
+# parity tests, C4 A/B, per-step kernel table.
+set -o pipefail
+OUT=gpurun_out/${1:-r04p}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+  tests/test_gpu_dconv16.py > "$OUT/pytest_dconv16.log" 2>&1 || { tail -30 "$OUT/pytest_dconv16.log"; exit 1; }
+tail -3 "$OUT/pytest_dconv16.log"
+run() {  # tag env...
+  local tag=$1; shift
+  env "$@" timeout -k 10 300 python bench.py --workload gan --dtype bf16 \
+    --no-cpu-baseline --steps 20 > "$OUT/c4_$tag.json" 2> "$OUT/c4_$tag.err" || return 1
+  python - "$OUT/c4_$tag.json" "$tag" <<'PY'
+import json, sys
+for l in open(sys.argv[1]):
+    if l.startswith("{"):
+        d = json.loads(l)
+        print(sys.argv[2], d["ms_per_step"], "ms/step median", d.get("ms_per_step_median"), flush=True)
+PY
+}
+for rep in 1 2 3; do
+  run nhwc1_$rep AINP_WGRAD16_NHWC=1 || exit 1
+  run nhwc0_$rep AINP_WGRAD16_NHWC=0 || exit 1
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -f csv -d "$OUT/step" -o run -- \
+  python3 tools/step_prof.py --workload gan --steps 6 --dtype bf16 > "$OUT/step.log" 2>&1 || exit 1
+grep "ms/step" "$OUT/step.log"
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu \
+  tests/test_gpu_gan.py > "$OUT/pytest_gan.log" 2>&1 || { tail -30 "$OUT/pytest_gan.log"; exit 1; }
+tail -3 "$OUT/pytest_gan.log"
+echo "all steps ok"
