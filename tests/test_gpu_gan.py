@@ -342,11 +342,13 @@ def test_maxpool2_nhwc16_copy(shape):
     (4, 2, 1, None, 2, 64, 32, 40),
     # LDS-tiled path (stride 1, 3x3 / 4x4): ragged channel chunks and tiles
     (3, 1, 1, (37, 66), 3, 40, 37, 70), (4, 1, 1, None, 0, 200, 13, 35),
-    (3, 1, 1, None, 0, 7, 17, 33)])
+    (3, 1, 1, None, 0, 7, 17, 33),
+    # large planes: the LDS-tiled kernel (>= 2048 output tiles of 4 x 64)
+    (3, 1, 1, (257, 590), 3, 9, 260, 600), (4, 1, 1, None, 2, 12, 200, 700)])
 def test_conv_gen_cout1(k, s, p, crop, act, C, H, W):
     from ainp import ops
     g = torch.Generator().manual_seed(5)
-    N = 2
+    N = 2 if H < 100 else 4
     x = torch.randn(N, C, H, W, generator=g)
     m = (torch.rand(N, H, W, generator=g) > 0.2).float()
     w = torch.randn(1, C, k, k, generator=g) * 0.1
