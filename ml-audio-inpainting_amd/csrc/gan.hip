@@ -755,67 +755,6 @@ __global__ void conv_cout1_finish_kernel(ConvGenParams p, int act, int Hc, int W
   p.y[t] = apply_act(v, act, p.slope);
 }
 
-// Stride-1 Cout == 1 conv on large planes (the generator's last PartialConv2d,
-// networks.py:334-339): a workgroup owns a C1T_H x C1T_W output tile and
-// loops over the input channels in chunks of C1T_CC, staging each chunk's
-// (C1T_H + KH - 1) x (C1T_W + KW - 1) input window (x times its mask plane,
-// resampled, zero outside) and weights in LDS with coalesced loads; each
-// thread sums its pixel from LDS and applies the epilogue itself (no partial
-// planes).  The window values are read once from HBM instead of KH*KW times
-// through L1.  Same products as conv_cout1_partial_kernel (binary partial-conv
-// masks: x*m == the masked sum), summed in another order (fp32).
-constexpr int C1T_H = 4, C1T_W = 64, C1T_CC = 8, C1T_KMAX = 8;
-__global__ __launch_bounds__(256) void conv_cout1_tiled_kernel(ConvGenParams p, int act, int Hc,
-                                                               int Wc) {
-  __shared__ float win[C1T_CC * (C1T_H + C1T_KMAX - 1) * (C1T_W + C1T_KMAX - 1)];
-  __shared__ float sw[C1T_CC * C1T_KMAX * C1T_KMAX];
-  const int KH = p.KH, KW = p.KW, KK = KH * KW;
-  const int TH = C1T_H + KH - 1, TW = C1T_W + KW - 1, PL = TH * TW;
-  const int tiles_w = (Wc + C1T_W - 1) / C1T_W;
-  const int ox0 = (blockIdx.x % tiles_w) * C1T_W, oy0 = (blockIdx.x / tiles_w) * C1T_H;
-  const int n = blockIdx.y;
-  const int tx = threadIdx.x % C1T_W, ty = threadIdx.x / C1T_W;
-  float acc = 0.f;
-  for (int c0 = 0; c0 < p.Cin; c0 += C1T_CC) {
-    __syncthreads();   // the previous chunk's window is consumed
-    for (int e = threadIdx.x; e < C1T_CC * PL; e += 256) {
-      const int cc = e / PL, rem = e - cc * PL;
-      const int r = rem / TW, col = rem - r * TW;
-      const int c = c0 + cc;
-      const int iy = oy0 - p.pad + r, ix = ox0 - p.pad + col;
-      float v = 0.f;
-      if (c < p.Cin && iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win) {
-        const bool first = c < p.s0.C;
-        const ConvSrcDev& sd = first ? p.s0 : p.s1;
-        const int ci = first ? c : c - p.s0.C;
-        const int sy = src_coord(iy, sd.Hs, p.Hin, sd.up), sx = src_coord(ix, sd.Ws, p.Win, sd.up);
-        const int64_t off = (int64_t)sy * sd.Ws + sx;
-        v = sd.x[((int64_t)n * sd.C + ci) * sd.Hs * sd.Ws + off];
-        if (sd.m) v *= sd.m[(int64_t)n * sd.Hs * sd.Ws + off];
-      }
-      win[e] = v;
-    }
-    for (int e = threadIdx.x; e < C1T_CC * KK; e += 256) {
-      const int c = c0 + e / KK;
-      sw[e] = c < p.Cin ? p.w[(int64_t)c0 * KK + e] : 0.f;
-    }
-    __syncthreads();
-    const int cn = min(C1T_CC, p.Cin - c0);
-    for (int cc = 0; cc < cn; ++cc) {
-      const float* wp = win + cc * PL + ty * TW + tx;
-      const float* wk = sw + cc * KK;
-      for (int ky = 0; ky < KH; ++ky)
-        for (int kx = 0; kx < KW; ++kx) acc = fmaf(wk[ky * KW + kx], wp[ky * TW + kx], acc);
-    }
-  }
-  const int oy = oy0 + ty, ox = ox0 + tx;
-  if (oy >= Hc || ox >= Wc) return;
-  float v = acc * (p.scale ? *p.scale : 1.f);
-  if (p.ratio) v *= p.ratio[((int64_t)n * p.Ho + oy) * p.Wo + ox];
-  if (p.bias) v += p.bias[0];
-  p.y[((int64_t)n * Hc + oy) * Wc + ox] = apply_act(v, act, p.slope);
-}
-
 // Partial-conv mask update (networks.py:83-104): count = sum over the window
 // of the channel-repeated masks = C0 * win(m0) + C1 * win(m1) (exact integers
 // in fp32), ratio = (Cin*k*k) / (count + 1e-8), new mask = clamp(count, 0, 1).
@@ -2445,19 +2384,6 @@ extern "C" int ainp_conv_gen_fwd_out16(const float* x0, const float* m0, int C0,
     if (stats || Hc > Ho || Wc > Wo || !workspace || KH * KW > 64)
       return record_msg("ainp_conv_gen_fwd: Cout=1 options (workspace, kernel <= 8x8)");
     const int64_t np = N * (int64_t)Hc * Wc;
-    // large stride-1 planes: the LDS-tiled kernel (AINP_COUT1_TILED=0: the
-    // channel-chunked kernel below)
-    static const bool tiled_env = [] {
-      const char* e = getenv("AINP_COUT1_TILED");
-      return !(e && e[0] == '0');
-    }();
-    const int64_t tiles = cdiv(Hc, C1T_H) * cdiv(Wc, C1T_W);
-    if (tiled_env && stride == 1 && KH <= C1T_KMAX && KW <= C1T_KMAX && N <= 65535 &&
-        tiles * N >= 2048 && tiles <= 0x7fffffff) {
-      hipLaunchKernelGGL(conv_cout1_tiled_kernel, dim3((unsigned)tiles, (unsigned)N), dim3(256), 0,
-                         s, p, act, Hc, Wc);
-      return check_launch("conv_cout1_tiled");
-    }
     const int nchunk = (int)cdiv(p.Cin, C1_CC);
     float* part = reinterpret_cast<float*>(workspace);
     hipLaunchKernelGGL(conv_cout1_partial_kernel, dim3((unsigned)cdiv(np, 256), nchunk), dim3(256),

@@ -343,7 +343,7 @@ def test_maxpool2_nhwc16_copy(shape):
     # LDS-tiled path (stride 1, 3x3 / 4x4): ragged channel chunks and tiles
     (3, 1, 1, (37, 66), 3, 40, 37, 70), (4, 1, 1, None, 0, 200, 13, 35),
     (3, 1, 1, None, 0, 7, 17, 33),
-    # large planes: the LDS-tiled kernel (>= 2048 output tiles of 4 x 64)
+    # large planes (the generator's last PartialConv2d is 64 x 384 x 640)
     (3, 1, 1, (257, 590), 3, 9, 260, 600), (4, 1, 1, None, 2, 12, 200, 700)])
 def test_conv_gen_cout1(k, s, p, crop, act, C, H, W):
     from ainp import ops
