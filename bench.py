@@ -388,13 +388,15 @@ def spawn_ranks(n):
 # regenerated by tools/gpu_r04f.sh.  The bench reports the dominant in-step
 # kernels from them with their own roofline fractions (per-step algorithmic
 # work / per-step kernel time / peak), next to the live stand-alone launches.
+# (table, steps it covers: tools/step_prof.py's "kernel tables / N"); under
+# profiles/steps/ so they travel with gpurun / the driver's snapshot
+# (.gpurunignore drops profiles/r0*)
 STEP_TABLES = {
-    ("cnnblstm", "fp32"): "profiles/r04d_cnn_fp32_step_kernel_stats.csv",
-    ("cnnblstm", "bf16"): "profiles/r04d_cnn_bf16_step_kernel_stats.csv",
-    ("gan", "bf16", 626): "profiles/r04d_gan_c4_step_kernel_stats.csv",
-    ("gan", "bf16", 1001): "profiles/r04d_gan_c5_step_kernel_stats.csv",
+    ("cnnblstm", "fp32"): ("profiles/steps/r04zB_cnn_fp32_step_kernel_stats.csv", 13),
+    ("cnnblstm", "bf16"): ("profiles/steps/r04zB_cnn_bf16_step_kernel_stats.csv", 13),
+    ("gan", "bf16", 626): ("profiles/steps/r04zB_gan_c4_step_kernel_stats.csv", 9),
+    ("gan", "bf16", 1001): ("profiles/steps/r04d_gan_c5_step_kernel_stats.csv", 13),
 }
-STEP_TABLE_DIV = 13
 
 
 def _cnn_step_work(B=32, F=257, T=334, H=128):
@@ -435,7 +437,7 @@ def in_step_table(key, bf16, top=8):
     """Dominant in-step kernels of the committed step table for `key` (None
     if absent): per-step ms, share of the step's kernel time, and for the
     kernels with a known per-step work their roofline fraction."""
-    path = STEP_TABLES.get(key)
+    path, div = STEP_TABLES.get(key, (None, 1))
     if not path or not os.path.exists(os.path.join(ROOT, path)):
         return None
     import csv
@@ -444,9 +446,9 @@ def in_step_table(key, bf16, top=8):
     work = _cnn_step_work() if key[0] == "cnnblstm" else []
     out = []
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
-        ms = float(r["TotalDurationNs"]) / 1e6 / STEP_TABLE_DIV
+        ms = float(r["TotalDurationNs"]) / 1e6 / div
         e = {"kernel": r["Name"].split("(")[0][:120], "ms_per_step": round(ms, 4),
-             "launches_per_step": round(int(r["Calls"]) / STEP_TABLE_DIV, 2),
+             "launches_per_step": round(int(r["Calls"]) / div, 2),
              "share_of_kernel_time": round(float(r["TotalDurationNs"]) / total, 4)}
         for sub, kind, amount in work:
             if sub in r["Name"]:
@@ -462,7 +464,7 @@ def in_step_table(key, bf16, top=8):
                 break
         out.append(e)
     return {"table": path, "per_step": f"rocprofv3 --kernel-trace --stats of tools/step_prof.py "
-                                       f"(totals / {STEP_TABLE_DIV})", "top": out}
+                                       f"(totals / {div})", "top": out}
 
 
 def main():

@@ -33,5 +33,7 @@ else
     python3 tools/step_prof.py --steps 10 || exit 1
   step 300 cnn_bf16.log rocprofv3 --kernel-trace --stats -f csv -d "$OUT/cnn_bf16" -o run -- \
     python3 tools/step_prof.py --steps 10 --dtype bf16 || exit 1
+  step 300 gan_bf16.log rocprofv3 --kernel-trace --stats -f csv -d "$OUT/gan_bf16" -o run -- \
+    python3 tools/step_prof.py --workload gan --steps 6 --dtype bf16 || exit 1
 fi
 echo "all steps ok"
