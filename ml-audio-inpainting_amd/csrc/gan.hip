@@ -2273,11 +2273,29 @@ static int conv_gen_bm(int Cout) { return Cout > 64 ? 128 : 64; }
 
 // K splits for a launch: small tile grids with long K (the U-Net bottleneck,
 // VGG's last blocks) are split so ~768 workgroups run; >= 8 K tiles per split.
+// For Cout > 64 count the workgroups of the bf16 wide-tile kernel (256 x 128 /
+// 128 x 256 tiles, two per CU) and split grids under 384 of them to ~512: the
+// U-Net decoder's 240-tile layers ran on half the CUs' slots (C4 9.34-9.37 ->
+// 9.24-9.25, C5 11.98-12.00 -> 11.78-11.80 ms/step, profiles/r04t_summary.txt).
+// AINP_CONV_SPLIT_WIDE=0: the old-tile count for every Cout; =3: ~768.
 static int conv_gen_nsplit(int64_t NP, int Cout, int K) {
   if (Cout == 1) return 1;
   const int BM = conv_gen_bm(Cout);
   const int64_t blocks = cdiv(NP, 16384 / BM) * cdiv(Cout, BM);
   const int nkt = (int)cdiv(K, CG_BK);
+  static const int wide_target = [] {
+    const char* e = getenv("AINP_CONV_SPLIT_WIDE");
+    return (e && e[0] == '0') ? 0 : (e && e[0] == '3') ? 768 : 512;
+  }();
+  if (wide_target && Cout > 64) {
+    const int64_t bw = Cout > 128 ? cdiv(NP, 128) * cdiv(Cout, 256) : cdiv(NP, 256) * cdiv(Cout, 128);
+    if (bw >= 384 || nkt < 16) return 1;
+    int64_t sw = wide_target / bw;
+    if (sw > nkt / 8) sw = nkt / 8;
+    if (sw < 1) sw = 1;
+    const int per = (int)cdiv(nkt, sw);
+    return (int)cdiv(nkt, per);
+  }
   if (blocks >= 384 || nkt < 16) return 1;
   int64_t s = cdiv(768, blocks);
   if (s > nkt / 8) s = nkt / 8;
