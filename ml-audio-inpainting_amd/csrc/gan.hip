@@ -2637,7 +2637,13 @@ extern "C" int ainp_conv_gen_fwd_nhwc16_ex(const uint16_t* x0, int C0, int H0, i
   const dim3 grid((unsigned)cdiv(NP, 16384 / BM), (unsigned)cdiv(Cout, BM), (unsigned)nsplit);
   const bool exp = a.exp || b.exp;
   const int variant = conv16_variant();
-  if (variant == 2 || (variant == 3 && Cout > 64)) {
+  // AINP_CONV16_SMALLCO=2: Cout <= 64 on the 4-wave 64 x 256 wide ring under
+  // the default variant too (A/B)
+  static const bool small_wide = [] {
+    const char* e = getenv("AINP_CONV16_SMALLCO");
+    return e && e[0] == '2';
+  }();
+  if (variant == 2 || (variant == 3 && (Cout > 64 || small_wide))) {
     const int BW = Cout > 128 ? 256 : (Cout > 64 ? 128 : 64);
     const int BNW = BW == 256 ? 128 : 256;       // both NW: 256x128 / 128x256 / 64x256
     const int tco = (int)cdiv(Cout, BW), tpx = (int)cdiv(NP, BNW);
@@ -2645,7 +2651,7 @@ extern "C" int ainp_conv_gen_fwd_nhwc16_ex(const uint16_t* x0, int C0, int H0, i
 #define AINP_CGW(BMV, NWV, EXPV)                                                                 \
   hipLaunchKernelGGL((conv_gen_nhwc16_wide_kernel<BMV, NWV, EXPV>), gw, dim3(NWV * 64), 0, s, p, a, \
                      b, wt16, act, tco, tpx)
-    if (variant == 3) {
+    if (variant == 3 && BW > 64) {
       if (BW == 256) { if (exp) AINP_CGW(256, 8, true); else AINP_CGW(256, 8, false); }
       else { if (exp) AINP_CGW(128, 8, true); else AINP_CGW(128, 8, false); }
     } else if (BW == 256) { if (exp) AINP_CGW(256, 4, true); else AINP_CGW(256, 4, false); }
