@@ -75,6 +75,7 @@ class _ConvStackFn(torch.autograd.Function):
             q += 4 if has_bn else 2
         l0_path = bool(spec) and l0_box is not None and _l0_bf16_ok(
             (N, ws_[-1].shape[0], H, W))
+        nbt = []             # num_batches_tracked += 1, applied by one multi-tensor add
         for bi, (has_bn, bn) in enumerate(spec):
             w, b = params[pi], params[pi + 1]
             pi += 2
@@ -105,7 +106,7 @@ class _ConvStackFn(torch.autograd.Function):
                     sc, sh, sv = ops.bn_finalize(sums, 0 if comm is not None else count, gamma,
                                                  beta, rm, rv, mom, bn.eps)
                     if bn.track_running_stats:
-                        bn.num_batches_tracked.add_(1)
+                        nbt.append(bn.num_batches_tracked)
                 else:
                     sc, sh = ops.bn_eval_affine(gamma, beta, bn.running_mean,
                                                 bn.running_var, bn.eps)
@@ -116,6 +117,8 @@ class _ConvStackFn(torch.autograd.Function):
                 affine.append(None)
                 act = (None, None)
             h = y
+        if nbt:
+            torch._foreach_add_(nbt, 1)
         last = affine[-1]
         if last is not None and l0_box is not None and _l0_bf16_ok(saved_y[-1]):
             # bf16 configuration: the LSTM's layer-0 operands are written as bf16

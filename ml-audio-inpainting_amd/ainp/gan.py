@@ -45,6 +45,30 @@ def _need_cuda(t, what):
         raise RuntimeError(f"ainp {what} runs on the MI355X kernels only; move it to a GPU")
 
 
+_NBT_PENDING = None   # list while a _nbt_batch scope is active
+
+
+class _nbt_batch:
+    """Scope in which the BatchNorm layers' num_batches_tracked += 1 are
+    collected and applied by one multi-tensor add at exit (the U-Net's 13
+    BatchNorms: one launch instead of 13 single-element kernels)."""
+
+    def __enter__(self):
+        global _NBT_PENDING
+        self._prev = _NBT_PENDING
+        if self._prev is None:
+            _NBT_PENDING = []
+        return self
+
+    def __exit__(self, *exc):
+        global _NBT_PENDING
+        if self._prev is None:
+            pend, _NBT_PENDING = _NBT_PENDING, None
+            if pend:
+                torch._foreach_add_(pend, 1)
+        return False
+
+
 def _bn_affine(bn: nn.BatchNorm2d, stats, count, C, want_save=False):
     """BatchNorm2d train (batch stats + running update) or eval -> (scale, shift)
     (+ save = [mean | rstd] of the batch with want_save, for the backward).
@@ -64,7 +88,10 @@ def _bn_affine(bn: nn.BatchNorm2d, stats, count, C, want_save=False):
         mom = bn.momentum if bn.momentum is not None else 0.1
         sc, sh, save = ops.bn_finalize(sums, count, bn.weight, bn.bias, rm, rv, mom, bn.eps)
         if bn.track_running_stats:
-            bn.num_batches_tracked.add_(1)
+            if _NBT_PENDING is not None:
+                _NBT_PENDING.append(bn.num_batches_tracked)
+            else:
+                bn.num_batches_tracked.add_(1)
         return (sc, sh, save) if want_save else (sc, sh)
     sc, sh = ops.bn_eval_affine(bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps)
     if want_save:
@@ -282,9 +309,10 @@ class PConvUNet(nn.Module):
         backward runs the kernels of csrc/gan_bwd.hip plus the MFMA GEMMs."""
         params = [p for p in self.parameters()]
         if torch.is_grad_enabled() and any(p.requires_grad for p in params):
-            return _PConvUNetFn.apply(x.contiguous().float(), mask.contiguous().float(), self,
-                                      *params)
-        with torch.no_grad(), ops.nhwc16_memo():
+            with _nbt_batch():
+                return _PConvUNetFn.apply(x.contiguous().float(), mask.contiguous().float(),
+                                          self, *params)
+        with torch.no_grad(), ops.nhwc16_memo(), _nbt_batch():
             return self._forward(x, mask)
 
     # profiling hook: a dict set here collects the sources of the final
@@ -977,24 +1005,21 @@ class VGGLoss(nn.Module):
         else:
             fg, ft = self._extract_features(xg, tape), self._extract_features(xt)
             split = False
-        perc = torch.zeros((), device=generated.device, dtype=torch.float64)
-        style = torch.zeros((), device=generated.device, dtype=torch.float64)
-        n_p = n_s = 0
+        # each L1 term written into its slot of one float64 vector, summed in
+        # order by one reduction per loss (no per-term scalar adds)
+        p_idx = [i for i in self.layer_indices_perceptual if i in fg and i in ft]
+        s_idx = [i for i in self.layer_indices_style if i in fg and i in ft]
+        n_p, n_s = len(p_idx), len(s_idx)
+        terms = torch.zeros(max(1, n_p + n_s), device=generated.device, dtype=torch.float64)
         grams = {}
-        for i in self.layer_indices_perceptual:
-            if i in fg and i in ft:
-                perc = perc + ops.absdiff_mean(fg[i], ft[i])
-                n_p += 1
-        for i in self.layer_indices_style:
-            if i in fg and i in ft:
-                gg, gt = self._gram(fg[i]), self._gram(ft[i])
-                style = style + ops.absdiff_mean(gg, gt)
-                grams[i] = (gg, gt)
-                n_s += 1
-        if n_p:
-            perc = perc / n_p
-        if n_s:
-            style = style / n_s
+        for k, i in enumerate(p_idx):
+            ops.absdiff_mean(fg[i], ft[i], out=terms[k])
+        for k, i in enumerate(s_idx):
+            gg, gt = self._gram(fg[i]), self._gram(ft[i])
+            ops.absdiff_mean(gg, gt, out=terms[n_p + k])
+            grams[i] = (gg, gt)
+        perc = terms[:n_p].sum() / n_p if n_p else terms.new_zeros(())
+        style = terms[n_p:n_p + n_s].sum() / n_s if n_s else terms.new_zeros(())
         if keep is not None:
             keep.update(tape=tape, fg=fg, ft=ft, grams=grams, n_p=n_p, n_s=n_s, B=B, split=split,
                         xg_shape=tuple(generated.shape))

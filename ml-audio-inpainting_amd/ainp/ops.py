@@ -1209,11 +1209,13 @@ def _reduce_ws(device):
     return ws
 
 
-def absdiff_mean(a, b):
-    """mean |a - b| as a float64 device scalar (nn.L1Loss())."""
+def absdiff_mean(a, b, out=None):
+    """mean |a - b| as a float64 device scalar (nn.L1Loss()); out: a float64
+    0-d tensor (e.g. one element of a loss vector) to write it to."""
     _req(a, "a"); _req(b, "b")
     assert a.numel() == b.numel()
-    out = torch.empty((), device=a.device, dtype=torch.float64)
+    if out is None:
+        out = torch.empty((), device=a.device, dtype=torch.float64)
     _T.absdiff_mean(a, b, _reduce_ws(a.device), out)
     return out
 

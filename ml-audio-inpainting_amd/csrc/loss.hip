@@ -147,6 +147,41 @@ __global__ void sum_slabs_kernel(const float* __restrict__ x, int64_t nslabs,
   }
 }
 
+// sum_slabs for few elements over many slabs (a split-K GEMM with a tiny
+// output: the discriminator's first-layer weight gradient, 64 x 17 over 512
+// slabs): a workgroup owns SS_E elements, its SS_G slab groups each sum the
+// slabs g, g + SS_G, ... in order, and the group partials are added in
+// fixed order g = 0 .. SS_G-1 (deterministic; a different order than
+// sum_slabs_kernel's, so only taken where that kernel would run a handful of
+// workgroups through hundreds of dependent loads).
+constexpr int SS_E = 8, SS_G = 32;
+__global__ __launch_bounds__(256) void sum_slabs_groups_kernel(const float* __restrict__ x,
+                                                               int64_t nslabs, int64_t n,
+                                                               float* __restrict__ out) {
+  __shared__ float part[SS_G][SS_E];
+  const int e = threadIdx.x % SS_E, g = threadIdx.x / SS_E;
+  const int64_t i = (int64_t)blockIdx.x * SS_E + e;
+  float a = 0.f;
+  if (i < n) {
+    int64_t s = g;
+    for (; s + 3 * SS_G < nslabs; s += 4 * SS_G) {
+      float b[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) b[u] = x[(s + u * SS_G) * n + i];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a += b[u];
+    }
+    for (; s < nslabs; s += SS_G) a += x[s * n + i];
+  }
+  part[g][e] = a;
+  __syncthreads();
+  if (g == 0 && i < n) {
+    float t = part[0][e];
+    for (int q = 1; q < SS_G; ++q) t += part[q][e];
+    out[i] = t;
+  }
+}
+
 // out[r] = sum_b sum_c x[(b*rows + r)*cols + c]; one wave per row.
 __global__ __launch_bounds__(256) void rowsum_batched_kernel(
     const float* __restrict__ x, int64_t nb, int64_t rows, int64_t cols,
@@ -173,6 +208,11 @@ extern "C" int ainp_sum_slabs(const float* x, int64_t nslabs, int64_t n,
   if (n == 0) return AINP_OK;
   int64_t grid = cdiv(cdiv(n, 4), 256);
   if (grid > 4096) grid = 4096;
+  if (grid < 16 && nslabs >= 64) {
+    hipLaunchKernelGGL(sum_slabs_groups_kernel, dim3((unsigned)cdiv(n, SS_E)), dim3(256), 0,
+                       as_stream(stream), x, nslabs, n, out);
+    return check_launch("sum_slabs_groups");
+  }
   hipLaunchKernelGGL(sum_slabs_kernel, dim3((unsigned)grid), dim3(256), 0,
                      as_stream(stream), x, nslabs, n, out);
   return check_launch("sum_slabs");

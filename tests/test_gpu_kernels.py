@@ -1108,3 +1108,30 @@ def test_ntcf_bridge_and_backward_read_bf16_y(ops):
     assert torch.equal(X16, X32) and torch.equal(XT16, XT32) and torch.equal(r16, r32)
     for u, v in zip(a16, a32):
         assert torch.equal(u, v)
+
+
+@pytest.mark.parametrize("nslabs,n", [(512, 1088), (100, 37), (64, 4000), (3, 10), (70, 4096 * 4 + 3)])
+def test_sum_slabs_orders(nslabs, n):
+    """ainp_sum_slabs: sequential slab order on its main kernel; for few
+    elements over >= 64 slabs, 32 slab groups (g, g+32, ...) each summed in
+    order and the group partials added in order -- both reproduced exactly."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(nslabs + n)
+    x = torch.randn(nslabs, n, generator=g)
+    out = ops.sum_slabs(x.cuda().contiguous(), nslabs).cpu()
+    grid = -(-(-(-n // 4)) // 256)
+    if grid < 16 and nslabs >= 64:
+        parts = []
+        for q in range(32):
+            a = torch.zeros(n)
+            for s in range(q, nslabs, 32):
+                a = a + x[s]
+            parts.append(a)
+        ref = parts[0].clone()
+        for q in range(1, 32):
+            ref = ref + parts[q]
+    else:
+        ref = x[0].clone()
+        for s in range(1, nslabs):
+            ref = ref + x[s]
+    assert torch.equal(out, ref)
