@@ -357,6 +357,13 @@ int ainp_conv3x3_io16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
  * ainp_bn_finalize a data-parallel caller all-reduces `sums` (SyncBN). */
 int ainp_bn_stats_reduce(const double* stats, int nparts, double* sums, int C,
                          void* stream);
+/* ainp_bn_stats_reduce followed by ainp_bn_finalize (count > 0) in one
+ * launch, for a single process (no all-reduce of the sums between them):
+ * the same scale / shift / save / running statistics, bit for bit. */
+int ainp_bn_reduce_finalize(const double* stats, int nparts, int64_t count, const float* gamma,
+                            const float* beta, float* running_mean, float* running_var,
+                            float momentum, float eps, float* scale, float* shift,
+                            float* save_mean_rstd, int C, void* stream);
 /* Finalise batch statistics into the affine form used by the next kernel:
  * scale = gamma*rstd, shift = beta-mean*scale; save_mean_rstd (float[2*C])
  * keeps mean / rstd for the backward; running stats updated in place with

@@ -69,6 +69,8 @@ _SIGS = {
     "ainp_conv3x3_wgrad_ex": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
                                       c_int64, c_int, P]),
     "ainp_bn_stats_reduce": (c_int, [P, c_int, P, c_int, P]),
+    "ainp_bn_reduce_finalize": (c_int, [P, c_int, c_int64, P, P, P, P, c_float, c_float, P, P,
+                                        P, c_int, P]),
     "ainp_bn_finalize": (c_int, [P, c_int64, P, P, P, P, c_float, c_float, P, P, P, c_int, P]),
     "ainp_bn_eval_affine": (c_int, [P, P, P, P, c_float, P, P, c_int, P]),
     "ainp_bn_relu_apply": (c_int, [P, P, P, P, c_int64, c_int, c_int64, c_int64, c_int, P]),

@@ -95,16 +95,17 @@ class _ConvStackFn(torch.autograd.Function):
                 pi += 2
                 if training:
                     C = y.shape[1]
-                    if comm is not None:
-                        sums = _allreduce(comm, ops.bn_stats_reduce(stats, C, count=count))
-                        count_dev = sums[2 * C:]
-                    else:
-                        sums = ops.bn_stats_reduce(stats, C)
                     rm = bn.running_mean if bn.track_running_stats else None
                     rv = bn.running_var if bn.track_running_stats else None
                     mom = bn.momentum if bn.momentum is not None else 0.1
-                    sc, sh, sv = ops.bn_finalize(sums, 0 if comm is not None else count, gamma,
-                                                 beta, rm, rv, mom, bn.eps)
+                    if comm is not None:
+                        sums = _allreduce(comm, ops.bn_stats_reduce(stats, C, count=count))
+                        count_dev = sums[2 * C:]
+                        sc, sh, sv = ops.bn_finalize(sums, 0, gamma, beta, rm, rv, mom, bn.eps)
+                    else:
+                        # one launch: partials -> scale / shift / running statistics
+                        sc, sh, sv = ops.bn_reduce_finalize(stats, C, count, gamma, beta, rm, rv,
+                                                            mom, bn.eps)
                     if bn.track_running_stats:
                         nbt.append(bn.num_batches_tracked)
                 else:

@@ -77,16 +77,17 @@ def _bn_affine(bn: nn.BatchNorm2d, stats, count, C, want_save=False):
     of the global batch, as the single-process reference does."""
     if bn.training or not bn.track_running_stats:
         comm = getattr(bn, "ainp_comm", None)
-        if comm is not None and comm.world_size > 1:
-            # the local count rides in sums[2C]: uneven shards get the true global count
-            sums = comm.allreduce_sum_(ops.bn_stats_reduce(stats, C, count=count))
-            count = 0
-        else:
-            sums = ops.bn_stats_reduce(stats, C)
         rm = bn.running_mean if bn.track_running_stats else None
         rv = bn.running_var if bn.track_running_stats else None
         mom = bn.momentum if bn.momentum is not None else 0.1
-        sc, sh, save = ops.bn_finalize(sums, count, bn.weight, bn.bias, rm, rv, mom, bn.eps)
+        if comm is not None and comm.world_size > 1:
+            # the local count rides in sums[2C]: uneven shards get the true global count
+            sums = comm.allreduce_sum_(ops.bn_stats_reduce(stats, C, count=count))
+            sc, sh, save = ops.bn_finalize(sums, 0, bn.weight, bn.bias, rm, rv, mom, bn.eps)
+        else:
+            # one launch: partials -> sums -> scale / shift / running statistics
+            sc, sh, save = ops.bn_reduce_finalize(stats, C, count, bn.weight, bn.bias, rm, rv,
+                                                  mom, bn.eps)
         if bn.track_running_stats:
             if _NBT_PENDING is not None:
                 _NBT_PENDING.append(bn.num_batches_tracked)

@@ -732,6 +732,18 @@ def bn_finalize(sums, count, gamma, beta, running_mean, running_var, momentum, e
     return scale, shift, save
 
 
+def bn_reduce_finalize(stats, C, count, gamma, beta, running_mean, running_var, momentum, eps):
+    """bn_stats_reduce + bn_finalize in one launch (single process, count > 0):
+    (scale, shift, save), bit for bit those of the two calls."""
+    dev = stats.device
+    scale = torch.empty(C, device=dev, dtype=torch.float32)
+    shift = torch.empty(C, device=dev, dtype=torch.float32)
+    save = torch.empty(2, C, device=dev, dtype=torch.float32)
+    _T.bn_reduce_finalize(stats, int(count), gamma, beta, running_mean, running_var,
+                          float(momentum), float(eps), scale, shift, save)
+    return scale, shift, save
+
+
 def bn_eval_affine(gamma, beta, running_mean, running_var, eps):
     C = running_mean.numel()
     dev = running_mean.device
@@ -1359,13 +1371,27 @@ def im2col16(x, k, stride, pad, ldA, ones_row=True):
     return col
 
 
+_WD16_CACHE: dict = {}
+
+
 def dgrad16_weight(w, stride, pad):
-    """ainp_dgrad16_weight: bf16 [s*s, Cin, Kc] parity-class weights."""
+    """ainp_dgrad16_weight: bf16 [s*s, Cin, Kc] parity-class weights; reused
+    while w's storage and version are unchanged (the discriminator's real and
+    fake backward passes of one step share them)."""
+    key = (w.data_ptr(), w._version, tuple(w.shape), int(stride), int(pad), w.device)
+    hit = _WD16_CACHE.get(key)
+    if hit is not None:
+        return hit[1]
     Cout, Cin, k, _ = w.shape
     nt = k // stride
     wd = torch.empty(stride * stride, Cin, nhwc16_seg(Cout, nt * nt), device=w.device,
                      dtype=torch.bfloat16)
     _T.dgrad16_weight(w, int(stride), int(pad), wd)
+    if len(_WD16_CACHE) >= 64:
+        _WD16_CACHE.clear()
+    # the entry holds w: its storage cannot be freed and its address reused by
+    # another tensor while the entry exists
+    _WD16_CACHE[key] = (w, wd)
     return wd
 
 

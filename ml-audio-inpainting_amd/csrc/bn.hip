@@ -39,6 +39,16 @@ __global__ void bn_stats_reduce_kernel(const double* __restrict__ stats,
 
 // Per channel: mean/var (biased) from the (possibly all-reduced) sums;
 // running stats with the unbiased variance (torch BatchNorm2d train mode).
+__device__ __forceinline__ void bn_finalize_channel(double sum, double sumsq, int c,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta,
+                                                    float* __restrict__ running_mean,
+                                                    float* __restrict__ running_var,
+                                                    float momentum, float eps, int64_t count,
+                                                    float* __restrict__ scale,
+                                                    float* __restrict__ shift,
+                                                    float* __restrict__ save, int C);
+
 __global__ void bn_finalize_kernel(const double* __restrict__ sums,
                                    const float* __restrict__ gamma,
                                    const float* __restrict__ beta,
@@ -53,8 +63,52 @@ __global__ void bn_finalize_kernel(const double* __restrict__ sums,
   // count <= 0: the element count travels with the sums (sums[2C], all-reduced
   // with them by a data-parallel caller, so uneven shards normalise correctly)
   if (count <= 0) count = (int64_t)sums[2 * C];
-  const double mean = sums[c] / (double)count;
-  double var = sums[C + c] / (double)count - mean * mean;
+  bn_finalize_channel(sums[c], sums[C + c], c, gamma, beta, running_mean, running_var, momentum,
+                      eps, count, scale, shift, save, C);
+}
+
+// bn_stats_reduce_kernel + bn_finalize_kernel in one launch (single process:
+// no all-reduce between them): workgroup c reduces channel c's partials and
+// its thread 0 finalises the channel -- the same arithmetic, bit for bit.
+__global__ void bn_reduce_finalize_kernel(const double* __restrict__ stats, int nparts,
+                                          const float* __restrict__ gamma,
+                                          const float* __restrict__ beta,
+                                          float* __restrict__ running_mean,
+                                          float* __restrict__ running_var, float momentum,
+                                          float eps, int64_t count, float* __restrict__ scale,
+                                          float* __restrict__ shift, float* __restrict__ save,
+                                          int C) {
+  const int c = blockIdx.x;
+  double s = 0.0, q = 0.0;
+  for (int p = threadIdx.x; p < nparts; p += blockDim.x) {
+    s += stats[(int64_t)p * 2 * C + c];
+    q += stats[(int64_t)p * 2 * C + C + c];
+  }
+  __shared__ double rs[4], rq[4];
+  s = wave_sum_d(s);
+  q = wave_sum_d(q);
+  if ((threadIdx.x & 63) == 0) {
+    rs[threadIdx.x >> 6] = s;
+    rq[threadIdx.x >> 6] = q;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    bn_finalize_channel(rs[0] + rs[1] + rs[2] + rs[3], rq[0] + rq[1] + rq[2] + rq[3], c, gamma,
+                        beta, running_mean, running_var, momentum, eps, count, scale, shift,
+                        save, C);
+}
+
+__device__ __forceinline__ void bn_finalize_channel(double sum, double sumsq, int c,
+                                                    const float* __restrict__ gamma,
+                                                    const float* __restrict__ beta,
+                                                    float* __restrict__ running_mean,
+                                                    float* __restrict__ running_var,
+                                                    float momentum, float eps, int64_t count,
+                                                    float* __restrict__ scale,
+                                                    float* __restrict__ shift,
+                                                    float* __restrict__ save, int C) {
+  const double mean = sum / (double)count;
+  double var = sumsq / (double)count - mean * mean;
   if (var < 0.0) var = 0.0;
   const float rstd = (float)(1.0 / sqrt(var + (double)eps));
   const float g = gamma ? gamma[c] : 1.f;
@@ -627,6 +681,20 @@ extern "C" int ainp_bn_stats_reduce(const double* stats, int nparts,
   hipLaunchKernelGGL(bn_stats_reduce_kernel, dim3(C), dim3(256), 0,
                      as_stream(stream), stats, nparts, sums, C);
   return check_launch("bn_stats_reduce");
+}
+
+extern "C" int ainp_bn_reduce_finalize(const double* stats, int nparts, int64_t count,
+                                       const float* gamma, const float* beta,
+                                       float* running_mean, float* running_var, float momentum,
+                                       float eps, float* scale, float* shift,
+                                       float* save_mean_rstd, int C, void* stream) {
+  if (!stats || nparts < 1 || !scale || !shift || !save_mean_rstd || C < 1 || count < 1 ||
+      ((running_mean == nullptr) != (running_var == nullptr)))
+    return record_msg("ainp_bn_reduce_finalize: bad argument");
+  hipLaunchKernelGGL(bn_reduce_finalize_kernel, dim3(C), dim3(256), 0, as_stream(stream), stats,
+                     nparts, gamma, beta, running_mean, running_var, momentum, eps, count, scale,
+                     shift, save_mean_rstd, C);
+  return check_launch("bn_reduce_finalize");
 }
 
 extern "C" int ainp_bn_finalize(const double* sums, int64_t count,

@@ -298,6 +298,25 @@ void bn_finalize(const Tensor& sums, int64_t count, const OptT& gamma, const Opt
       "bn_finalize");
 }
 
+void bn_reduce_finalize(const Tensor& stats, int64_t count, const OptT& gamma, const OptT& beta,
+                        const OptT& running_mean, const OptT& running_var, double momentum,
+                        double eps, const Tensor& scale, const Tensor& shift, const Tensor& save) {
+  GUARD(stats);
+  const int64_t C = scale.numel();
+  TORCH_CHECK(C > 0 && stats.numel() % (2 * C) == 0 &&
+                  stats.size(-1) * (stats.dim() == 3 ? 2 : 1) == 2 * C,
+              "stats must be [parts, 2C] or [parts, 2, C]");
+  numel_is(shift, C, "shift");
+  numel_is(save, 2 * C, "save");
+  chk(ainp_bn_reduce_finalize(dev<double>(stats, "stats", at::kDouble),
+                              (int)(stats.numel() / (2 * C)), count, opt(gamma, "gamma"),
+                              opt(beta, "beta"), opt(running_mean, "running_mean"),
+                              opt(running_var, "running_var"), (float)momentum, (float)eps,
+                              dev(scale, "scale"), dev(shift, "shift"), dev(save, "save"),
+                              (int)C, stream_of(stats)),
+      "bn_reduce_finalize");
+}
+
 void bn_eval_affine(const OptT& gamma, const OptT& beta, const Tensor& running_mean,
                     const Tensor& running_var, double eps, const Tensor& scale,
                     const Tensor& shift) {
@@ -1449,6 +1468,9 @@ TORCH_LIBRARY(ainp, m) {
   m.def("conv3x3_wgrad(Tensor x, Tensor? in_scale, Tensor? in_shift, Tensor dy, Tensor(a!) dw, "
         "Tensor(b!)? dbias, Tensor(c!) workspace, int flags) -> ()");
   m.def("bn_stats_reduce(Tensor stats, Tensor(a!) sums, int C) -> ()");
+  m.def("bn_reduce_finalize(Tensor stats, int count, Tensor? gamma, Tensor? beta, "
+        "Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, float eps, "
+        "Tensor(c!) scale, Tensor(d!) shift, Tensor(e!) save) -> ()");
   m.def("bn_finalize(Tensor sums, int count, Tensor? gamma, Tensor? beta, "
         "Tensor(a!)? running_mean, Tensor(b!)? running_var, float momentum, float eps, "
         "Tensor(c!) scale, Tensor(d!) shift, Tensor(e!) save) -> ()");
@@ -1570,6 +1592,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("conv3x3_wgrad", &conv3x3_wgrad);
   m.impl("bn_stats_reduce", &bn_stats_reduce);
   m.impl("bn_finalize", &bn_finalize);
+  m.impl("bn_reduce_finalize", &bn_reduce_finalize);
   m.impl("bn_eval_affine", &bn_eval_affine);
   m.impl("bn_relu_apply", &bn_relu_apply);
   m.impl("bn_relu_bwd_reduce", &bn_relu_bwd_reduce);
@@ -1651,6 +1674,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("conv3x3_wgrad", torch::CppFunction::makeFallthrough());
   m.impl("bn_stats_reduce", torch::CppFunction::makeFallthrough());
   m.impl("bn_finalize", torch::CppFunction::makeFallthrough());
+  m.impl("bn_reduce_finalize", torch::CppFunction::makeFallthrough());
   m.impl("bn_eval_affine", torch::CppFunction::makeFallthrough());
   m.impl("bn_relu_apply", torch::CppFunction::makeFallthrough());
   m.impl("bn_relu_bwd_reduce", torch::CppFunction::makeFallthrough());

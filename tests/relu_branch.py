@@ -19,22 +19,27 @@ def recording(model):
     names = [n for n, m in model.named_modules() if isinstance(m, nn.BatchNorm2d)]
     masks = {}
     last = {}
-    f_conv, f_fin = ops.conv3x3_fwd, ops.bn_finalize
+    f_conv, f_fin, f_rfin = ops.conv3x3_fwd, ops.bn_finalize, ops.bn_reduce_finalize
 
     def conv(*a, **k):
         out = f_conv(*a, **k)
         last["y"] = out[0]
         return out
 
-    def fin(*a, **k):
-        out = f_fin(*a, **k)
+    def record(out):
         sc, sh = out[0], out[1]
         name = names[len(masks)]
         masks[name] = (ops.bn_relu_apply(last["y"], sc, sh) > 0).cpu()
         return out
 
-    ops.conv3x3_fwd, ops.bn_finalize = conv, fin
+    def fin(*a, **k):          # data parallel: bn_finalize of the all-reduced sums
+        return record(f_fin(*a, **k))
+
+    def rfin(*a, **k):         # single process: the fused reduce + finalize
+        return record(f_rfin(*a, **k))
+
+    ops.conv3x3_fwd, ops.bn_finalize, ops.bn_reduce_finalize = conv, fin, rfin
     try:
         yield masks
     finally:
-        ops.conv3x3_fwd, ops.bn_finalize = f_conv, f_fin
+        ops.conv3x3_fwd, ops.bn_finalize, ops.bn_reduce_finalize = f_conv, f_fin, f_rfin

@@ -1135,3 +1135,41 @@ def test_sum_slabs_orders(nslabs, n):
         for s in range(1, nslabs):
             ref = ref + x[s]
     assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("C,parts,running", [(64, 300, True), (16, 7, False), (512, 1, True)])
+def test_bn_reduce_finalize_equals_two_calls(C, parts, running):
+    """ainp_bn_reduce_finalize: scale / shift / save and the running statistics
+    bit for bit those of ainp_bn_stats_reduce + ainp_bn_finalize."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(C + parts)
+    stats = (torch.randn(parts, 2 * C, generator=g, dtype=torch.float64).abs() * 50).cuda()
+    gamma = torch.randn(C, generator=g).cuda()
+    beta = torch.randn(C, generator=g).cuda()
+    rm1 = torch.randn(C, generator=g).cuda() if running else None
+    rv1 = torch.rand(C, generator=g).cuda() + 0.5 if running else None
+    rm2 = rm1.clone() if running else None
+    rv2 = rv1.clone() if running else None
+    count = 1000 * parts
+    sums = ops.bn_stats_reduce(stats, C)
+    a = ops.bn_finalize(sums, count, gamma, beta, rm1, rv1, 0.1, 1e-5)
+    b = ops.bn_reduce_finalize(stats, C, count, gamma, beta, rm2, rv2, 0.1, 1e-5)
+    torch.cuda.synchronize()
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+    if running:
+        assert torch.equal(rm1, rm2) and torch.equal(rv1, rv2)
+
+
+def test_adam_bumps_parameter_versions():
+    """The device weight caches keyed on tensor._version (conv_weight_nhwc16,
+    dgrad16_weight) see every ainp Adam update: the op's mutable-argument
+    schema makes the dispatcher bump the parameters' version counters."""
+    from ainp.optim import Adam
+    p = torch.nn.Parameter(torch.randn(64, 32, 3, 3, device=DEV))
+    opt = Adam([p], lr=1e-3)
+    p.grad = torch.randn_like(p)
+    v0 = p._version
+    opt.step()
+    torch.cuda.synchronize()
+    assert p._version > v0
