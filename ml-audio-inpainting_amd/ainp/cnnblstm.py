@@ -193,7 +193,14 @@ class _ConvStackFn(torch.autograd.Function):
             else:
                 xin = x
                 pro = (None, None)
-            if ctx.defer_wgrad == "queue":
+            # the first conv's weight gradient is the backward's last work: with no
+            # input gradient to compute, the main stream would only wait for it,
+            # so it runs there, beside the side stream's tail (single process)
+            last_main = (WGRAD_LAST_MAIN and bi == 0 and not ctx.needs_input_grad[0]
+                         and ctx.sink is None)
+            if last_main:
+                dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
+            elif ctx.defer_wgrad == "queue":
                 # off the critical path: queued, launched on the side stream when
                 # the BPTT recurrence (64 workgroups) starts -- filling the CUs
                 # it leaves idle (see _Deferred)
@@ -234,6 +241,9 @@ class _ConvStackFn(torch.autograd.Function):
         return (gx, None, None, None, None, None, None, None, *grads)
 
 
+# the encoder's first-conv weight gradient on the main stream when nothing
+# else is left there (AINP_WGRAD_LAST_MAIN=0: on the side stream, A/B)
+WGRAD_LAST_MAIN = os.environ.get("AINP_WGRAD_LAST_MAIN", "1") != "0"
 # bf16 configuration: BatchNorm-backward outputs in bf16 storage (AINP_GY16=0:
 # fp32, as before; the conv results are the same bit for bit)
 GY16 = os.environ.get("AINP_GY16", "1") != "0"
