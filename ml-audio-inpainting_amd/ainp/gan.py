@@ -704,18 +704,40 @@ D_PREP_FUSED = os.environ.get("AINP_D_PREP_FUSED", "1") != "0"
 WGRAD_COUT1 = os.environ.get("AINP_WGRAD_COUT1", "1") != "0"
 
 
+# the discriminator's weight gradients (im2col16 + GEMM + spectral-norm
+# gradient) on a side stream, overlapping the data-gradient chain of the
+# layers below (AINP_D_WGRAD_SIDE=0: in line, A/B)
+D_WGRAD_SIDE = os.environ.get("AINP_D_WGRAD_SIDE", "1") != "0"
+_D_SIDE: dict = {}
+
+
+def _d_side(device):
+    """(side stream, its own reduction workspace) of the device."""
+    key = str(device)
+    ent = _D_SIDE.get(key)
+    if ent is None:
+        st = torch.cuda.Stream(device=device)
+        with torch.cuda.stream(st):
+            ws = torch.empty_like(ops._reduce_ws(device))
+        ent = _D_SIDE[key] = (st, ws)
+    return ent
+
+
 def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
     """_DiscriminatorFn.backward with bf16 operands: per layer the gradient is
     cast once into a pixel-contiguous and a channel-last bf16 copy (LeakyReLU
     backward and the split-K slabs of the layer above folded in; written by
     the layer above's data-gradient epilogue where that runs unsplit), the weight
-    gradient is one bf16 GEMM over every image's pixels, the data gradient a
-    parity-class implicit GEMM (csrc/dconv16.hip)."""
+    gradient is one bf16 GEMM over every image's pixels (on a side stream),
+    the data gradient a parity-class implicit GEMM (csrc/dconv16.hip)."""
     L = ctx.nl
     grads = [None] * len(params)
     gsrc, nslab = g.contiguous(), 1
     gx = None
     pre = None    # this layer's (gA, gT), written by the layer above's data gradient
+    dev = g.device
+    side, side_ws = _d_side(dev) if D_WGRAD_SIDE else (None, None)
+    main = torch.cuda.current_stream(dev)
     for l in range(L - 1, -1, -1):
         k, s, p, act = ctx.cfg[l]
         w = params[2 * l]
@@ -725,25 +747,45 @@ def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
         need_dx = l > 0 or ctx.needs_input_grad[0]
         h = ins[l]
         Cin, H, W = h.shape[1:]
+        y_act = outs[l] if act else None
         if WGRAD_COUT1 and Cout == 1 and k in (3, 4):
             # the logit conv: a GEMV, straight from h (no materialised columns)
-            Gw = ops.wgrad_cout1(h, gsrc, nslab, outs[l] if act else None, SLOPE, k, s, p)
-            gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P, ldA,
+            def wgrad(h=h, gsrc=gsrc, nslab=nslab, y_act=y_act, k=k, s=s, p=p):
+                return ops.wgrad_cout1(h, gsrc, nslab, y_act, SLOPE, k, s, p)
+            deps = [h, gsrc] + ([y_act] if act else [])
+            gT = ops.d_prep16(gsrc, nslab, y_act, SLOPE, N, Cout, P, ldA,
                               want_gT=True)[1] if need_dx else None
         else:
             if pre is not None:
                 gA, gT = pre
             else:
-                gA, gT = ops.d_prep16(gsrc, nslab, outs[l] if act else None, SLOPE, N, Cout, P,
-                                      ldA, want_gT=need_dx)
+                gA, gT = ops.d_prep16(gsrc, nslab, y_act, SLOPE, N, Cout, P, ldA,
+                                      want_gT=need_dx)
             h16 = ctx.h16[l] if WGRAD16_NHWC else None
             if h16 is not None and Cin % 8 == 0:
                 # implicit GEMM over the forward's channel-last input copy
-                Gw = ops.wgrad16_nhwc(gA, h16, k, s, p, max_split=512)
+                def wgrad(gA=gA, h16=h16, k=k, s=s, p=p):
+                    return ops.wgrad16_nhwc(gA, h16, k, s, p, max_split=512)
+                deps = [gA, h16]
             else:
-                col = ops.im2col16(h, k, s, p, ldA)              # [Cin*k*k + 1, ldA]
-                Gw = ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=512)
-        dw, db = ops.sn_weight_grad(Gw, w, us[l], vs[l], inv[l:l + 1], with_bias=True)
+                def wgrad(gA=gA, h=h, k=k, s=s, p=p, ldA=ldA):
+                    col = ops.im2col16(h, k, s, p, ldA)          # [Cin*k*k + 1, ldA]
+                    return ops.gemm_bf16nt_splitk(gA, col, ldA, max_split=512)
+                deps = [gA, h]
+        sn = (w, us[l], vs[l], inv[l:l + 1])
+        if side is not None:
+            # the operands are complete on the main stream at this point
+            ready = torch.cuda.Event()
+            ready.record(main)
+            with torch.cuda.stream(side):
+                side.wait_event(ready)
+                dw, db = ops.sn_weight_grad(wgrad(), *sn, with_bias=True, ws=side_ws)
+            for t in deps + list(sn):
+                t.record_stream(side)     # not reused while the side stream reads it
+            for t in (dw, db):
+                t.record_stream(main)     # consumed by autograd on the main stream
+        else:
+            dw, db = ops.sn_weight_grad(wgrad(), *sn, with_bias=True)
         grads[2 * l], grads[2 * l + 1] = dw.view_as(w), db
         pre = None
         if need_dx:
@@ -763,6 +805,8 @@ def _d_backward16(ctx, g, inv, ins, outs, us, vs, params):
             nslab = S
             if l == 0:
                 gx = gsrc[0] if S == 1 else ops.sum_slabs(gsrc, S).view(N, Cin, H, W)
+    if side is not None:
+        main.wait_stream(side)            # the weight gradients are complete
     return (gx, None, None, None, None, None, *grads)
 
 

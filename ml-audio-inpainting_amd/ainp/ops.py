@@ -1287,13 +1287,16 @@ def sn_power(weights, us, vs, update=True, eps=1e-12):
     return inv
 
 
-def sn_weight_grad(G, w_orig, u, v, inv_sigma, with_bias=False):
-    """G [h, ldg] (ldg >= wd, +1 with the bias column) -> (dW_orig, dbias or None)."""
+def sn_weight_grad(G, w_orig, u, v, inv_sigma, with_bias=False, ws=None):
+    """G [h, ldg] (ldg >= wd, +1 with the bias column) -> (dW_orig, dbias or None).
+    ws: a reduction workspace (default: the device's shared one; a side stream
+    passes its own)."""
     _req(G, "G"); _req(w_orig, "w_orig")
     out = torch.empty_like(w_orig)
     h = w_orig.shape[0]
     ob = torch.empty(h, device=G.device) if with_bias else None
-    _T.sn_weight_grad(G, w_orig, u, v, inv_sigma, _reduce_ws(G.device), out, ob)
+    _T.sn_weight_grad(G, w_orig, u, v, inv_sigma, _reduce_ws(G.device) if ws is None else ws,
+                      out, ob)
     return out, ob
 
 

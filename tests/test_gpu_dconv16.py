@@ -267,3 +267,27 @@ def test_d_backward16_wgrad_nhwc_is_bit_identical(monkeypatch):
     a, b = run(True), run(False)
     for u, v in zip(a, b):
         assert torch.equal(u, v)
+
+
+def test_d_backward16_side_stream_weight_grads_bit_identical(monkeypatch):
+    """The discriminator's weight gradients on the side stream
+    (AINP_D_WGRAD_SIDE) equal the in-line ones bit for bit, with the data
+    gradient chain running beside them."""
+    from ainp import gan as G
+    torch.manual_seed(9)
+    D = G.Discriminator().cuda().eval()
+    D.ainp_bf16 = True
+    x0 = torch.randn(3, 1, 80, 120, device="cuda")
+
+    def run(side):
+        monkeypatch.setattr(G, "D_WGRAD_SIDE", side)
+        for q in D.parameters():
+            q.grad = None
+        x = x0.clone().requires_grad_(True)
+        out = D(x)
+        out.backward(torch.ones_like(out))
+        return [q.grad.clone() for q in D.parameters()] + [x.grad.clone()]
+
+    a, b = run(True), run(False)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
