@@ -704,10 +704,11 @@ D_PREP_FUSED = os.environ.get("AINP_D_PREP_FUSED", "1") != "0"
 WGRAD_COUT1 = os.environ.get("AINP_WGRAD_COUT1", "1") != "0"
 
 
-# the discriminator's weight gradients (im2col16 + GEMM + spectral-norm
-# gradient) on a side stream, overlapping the data-gradient chain of the
-# layers below (AINP_D_WGRAD_SIDE=0: in line, A/B)
-D_WGRAD_SIDE = os.environ.get("AINP_D_WGRAD_SIDE", "1") != "0"
+# AINP_D_WGRAD_SIDE=1: the discriminator's weight gradients (im2col16 + GEMM +
+# spectral-norm gradient) on a side stream beside the data-gradient chain of
+# the layers below (bit-identical).  Off: C4 9.12-9.15 -> 9.32-9.36 ms/step
+# with it, the two chains' kernels slow each other (profiles/r04z4_summary.txt)
+D_WGRAD_SIDE = os.environ.get("AINP_D_WGRAD_SIDE", "0") == "1"
 _D_SIDE: dict = {}
 
 

@@ -271,8 +271,8 @@ def test_d_backward16_wgrad_nhwc_is_bit_identical(monkeypatch):
 
 def test_d_backward16_side_stream_weight_grads_bit_identical(monkeypatch):
     """The discriminator's weight gradients on the side stream
-    (AINP_D_WGRAD_SIDE) equal the in-line ones bit for bit, with the data
-    gradient chain running beside them."""
+    (AINP_D_WGRAD_SIDE=1, opt-in) equal the in-line ones bit for bit, with the
+    data gradient chain running beside them."""
     from ainp import gan as G
     torch.manual_seed(9)
     D = G.Discriminator().cuda().eval()
