@@ -739,74 +739,6 @@ __global__ __launch_bounds__(256) void conv_cout1_partial_kernel(ConvGenParams p
   partial[(int64_t)blockIdx.y * np + t] = acc;
 }
 
-// Stride-1 variant: a thread owns C1S_TX consecutive output pixels of a row,
-// so each input row segment it loads (C1S_TX + KW - 1 values, times the mask)
-// serves KW taps of all C1S_TX pixels: about KW-fold fewer L1 loads per
-// output than one pixel per thread.  Same chunks and partial planes.
-constexpr int C1S_TX = 4;
-template <int KW>
-__global__ __launch_bounds__(256) void conv_cout1_strip_kernel(ConvGenParams p, int Hc, int Wc,
-                                                               float* partial) {
-  __shared__ float sw[C1_CC * 64];
-  const int KK = p.KH * KW;
-  const int c0 = blockIdx.y * C1_CC;
-  const int cn = min(C1_CC, p.Cin - c0);
-  for (int i = threadIdx.x; i < cn * KK; i += blockDim.x) sw[i] = p.w[(int64_t)c0 * KK + i];
-  __syncthreads();
-  const int sxn = (Wc + C1S_TX - 1) / C1S_TX;
-  const int64_t nstrip = (int64_t)p.N * Hc * sxn;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= nstrip) return;
-  const int n = (int)(t / ((int64_t)Hc * sxn));
-  const int r = (int)(t - (int64_t)n * Hc * sxn);
-  const int oy = r / sxn, ox0 = (r - oy * sxn) * C1S_TX;
-  const int by = oy - p.pad, bx = ox0 - p.pad;
-  constexpr int NV = C1S_TX + KW - 1;
-  float acc[C1S_TX];
-#pragma unroll
-  for (int j = 0; j < C1S_TX; ++j) acc[j] = 0.f;
-  for (int src = 0; src < 2; ++src) {
-    const ConvSrcDev& s = src == 0 ? p.s0 : p.s1;
-    const int sc0 = src == 0 ? 0 : p.s0.C;
-    const int lo = max(c0, sc0), hi = min(c0 + cn, sc0 + s.C);
-    if (lo >= hi) continue;
-    const int64_t plane = (int64_t)s.Hs * s.Ws;
-    for (int ky = 0; ky < p.KH; ++ky) {
-      const int iy = by + ky;
-      if (iy < 0 || iy >= p.Hin) continue;
-      const int sy = src_coord(iy, s.Hs, p.Hin, s.up);
-      int64_t off[NV];
-      float mv[NV];
-#pragma unroll
-      for (int j = 0; j < NV; ++j) {
-        const int ix = bx + j;
-        const bool ok = ix >= 0 && ix < p.Win;
-        off[j] = ok ? (int64_t)sy * s.Ws + src_coord(ix, s.Ws, p.Win, s.up) : -1;
-        mv[j] = !ok ? 0.f : (s.m ? s.m[(int64_t)n * plane + off[j]] : 1.f);
-      }
-#pragma unroll 4
-      for (int c = lo; c < hi; ++c) {
-        const float* xb = s.x + ((int64_t)n * s.C + (c - sc0)) * plane;
-        float v[NV];
-#pragma unroll
-        for (int j = 0; j < NV; ++j) v[j] = off[j] >= 0 ? xb[off[j]] * mv[j] : 0.f;
-        const float* wk = sw + (c - c0) * KK + ky * KW;
-#pragma unroll
-        for (int kx = 0; kx < KW; ++kx) {
-          const float wv = wk[kx];
-#pragma unroll
-          for (int j = 0; j < C1S_TX; ++j) acc[j] = fmaf(wv, v[j + kx], acc[j]);
-        }
-      }
-    }
-  }
-  const int64_t np = (int64_t)p.N * Hc * Wc;
-  float* pp = partial + (int64_t)blockIdx.y * np + ((int64_t)n * Hc + oy) * Wc + ox0;
-#pragma unroll
-  for (int j = 0; j < C1S_TX; ++j)
-    if (ox0 + j < Wc) pp[j] = acc[j];
-}
-
 __global__ void conv_cout1_finish_kernel(ConvGenParams p, int act, int Hc, int Wc, int nchunk,
                                          const float* partial) {
   const int64_t np = (int64_t)p.N * Hc * Wc;
@@ -2472,24 +2404,8 @@ extern "C" int ainp_conv_gen_fwd_out16(const float* x0, const float* m0, int C0,
     const int64_t np = N * (int64_t)Hc * Wc;
     const int nchunk = (int)cdiv(p.Cin, C1_CC);
     float* part = reinterpret_cast<float*>(workspace);
-    // stride 1, 3 x 3 / 4 x 4: strips of C1S_TX pixels per thread
-    // (AINP_COUT1_STRIP=0: one pixel per thread)
-    static const bool strip_env = [] {
-      const char* e = getenv("AINP_COUT1_STRIP");
-      return !(e && e[0] == '0');
-    }();
-    const int64_t nstrip = N * (int64_t)Hc * cdiv(Wc, C1S_TX);
-    if (strip_env && stride == 1 && (KW == 3 || KW == 4)) {
-      if (KW == 3)
-        hipLaunchKernelGGL(conv_cout1_strip_kernel<3>, dim3((unsigned)cdiv(nstrip, 256), nchunk),
-                           dim3(256), 0, s, p, Hc, Wc, part);
-      else
-        hipLaunchKernelGGL(conv_cout1_strip_kernel<4>, dim3((unsigned)cdiv(nstrip, 256), nchunk),
-                           dim3(256), 0, s, p, Hc, Wc, part);
-    } else {
-      hipLaunchKernelGGL(conv_cout1_partial_kernel, dim3((unsigned)cdiv(np, 256), nchunk),
-                         dim3(256), 0, s, p, Hc, Wc, part);
-    }
+    hipLaunchKernelGGL(conv_cout1_partial_kernel, dim3((unsigned)cdiv(np, 256), nchunk), dim3(256),
+                       0, s, p, Hc, Wc, part);
     hipLaunchKernelGGL(conv_cout1_finish_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, s, p,
                        act, Hc, Wc, nchunk, part);
     return check_launch("conv_cout1");
