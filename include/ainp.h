@@ -664,6 +664,13 @@ int ainp_affine_act(float* y, const float* scale, const float* shift, int64_t N,
 int ainp_affine_act_nhwc16(float* y, const float* scale, const float* shift, int64_t N, int C,
                            int H, int W, int act, float slope, const float* m, uint16_t* out,
                            void* stream);
+/* ainp_affine_act_nhwc16 with flags: AINP_AFFINE_NO_Y leaves y unchanged (only
+ * the channel-last copy is written) for a caller whose consumers all read the
+ * copy -- the bf16 U-Net's no-grad forward (networks.py:139-152, 247-345). */
+#define AINP_AFFINE_NO_Y 1
+int ainp_affine_act_nhwc16_ex(float* y, const float* scale, const float* shift, int64_t N, int C,
+                              int H, int W, int act, float slope, const float* m, uint16_t* out,
+                              int flags, void* stream);
 /* nn.MaxPool2d(2, 2) of VGG19.features (loss.py:21). */
 int ainp_maxpool2(const float* x, float* y, int64_t NC, int H, int W, void* stream);
 /* ainp_maxpool2 on x [N][C][H][W] that also writes the pooled values' bf16

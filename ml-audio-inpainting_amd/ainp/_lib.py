@@ -118,6 +118,8 @@ _SIGS = {
     "ainp_affine_act": (c_int, [P, P, P, c_int64, c_int, c_int64, c_int, c_float, P]),
     "ainp_affine_act_nhwc16": (c_int, [P, P, P, c_int64, c_int, c_int, c_int, c_int, c_float, P,
                                        P, P]),
+    "ainp_affine_act_nhwc16_ex": (c_int, [P, P, P, c_int64, c_int, c_int, c_int, c_int, c_float, P,
+                                          P, c_int, P]),
     "ainp_maxpool2": (c_int, [P, P, c_int64, c_int, c_int, P]),
     "ainp_maxpool2_nhwc16": (c_int, [P, P, c_int64, c_int, c_int, c_int, P, P]),
     "ainp_vgg_prep": (c_int, [P, c_int64, c_int, c_int, c_int, P, P, P, P, c_int, P, P, P,

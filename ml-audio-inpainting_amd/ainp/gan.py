@@ -175,6 +175,12 @@ class PartialConv2d(nn.Module):
         return y, newm.reshape(N, 1, Ho, Wo).expand(N, self.out_channels, Ho, Wo).contiguous()
 
 
+# bf16 no-grad U-Net: the BatchNorm + LeakyReLU pass writes only the next
+# convs' channel-last bf16 copy, not the fp32 block output back
+# (AINP_AFFINE_NO_Y=0: both, A/B)
+AFFINE_NO_Y = os.environ.get("AINP_AFFINE_NO_Y", "1") != "0"
+
+
 class EncoderBlock(nn.Module):
     """networks.py:139-152: PartialConv -> BatchNorm2d -> LeakyReLU(0.2)."""
 
@@ -200,7 +206,10 @@ class EncoderBlock(nn.Module):
         return isinstance(self.norm, nn.BatchNorm2d) and (
             self.norm.training or not self.norm.track_running_stats)
 
-    def run(self, srcs, Hin, Win):
+    def run(self, srcs, Hin, Win, keep_y=True):
+        """keep_y=False (the U-Net's own no-grad forward): in the channel-last
+        bf16 path the fp32 block output is not written back -- its consumers
+        read the copy."""
         y, newm, stats = self.pconv.run(srcs, Hin, Win, want_stats=self._want_stats())
         if (self.pconv.ainp_bf16 and ops._NHWC_MEMO is not None and ops.CONV_NHWC16
                 and y.shape[1] % 32 == 0):
@@ -211,7 +220,13 @@ class EncoderBlock(nn.Module):
             else:
                 sc = torch.ones(C, device=y.device)
                 sh = torch.zeros(C, device=y.device)
-            ops.affine_act_nhwc16_(y, sc, sh, ops.ACT_LEAKY, SLOPE, newm)
+            # the block output's consumers (the next encoder conv, the decoder's
+            # skip / upsampled sources) read the channel-last copy: in the U-Net's
+            # forward the fp32 write-back is skipped unless a profiling capture
+            # reads the planes
+            ops.affine_act_nhwc16_(y, sc, sh, ops.ACT_LEAKY, SLOPE, newm,
+                                   keep_y=keep_y or not AFFINE_NO_Y
+                                   or PConvUNet.capture is not None)
             return y, newm
         return self._finish(y, stats), newm
 
@@ -404,7 +419,7 @@ class PConvUNet(nn.Module):
         Hc, Wc = Hp, Wp
         feats, masks = [], []
         for blk in self.encoder_blocks:
-            y, m = blk.run(srcs, Hc, Wc)
+            y, m = blk.run(srcs, Hc, Wc, keep_y=False)
             feats.append(y)
             masks.append(m)
             Hc, Wc = y.shape[2:]
@@ -421,7 +436,7 @@ class PConvUNet(nn.Module):
                 # profiling hook (bench.py's in-step roofline operands): this
                 # block's sources as the step launches them
                 cap[f"decoder{i}"] = ([(d, dm), (feats[j], masks[j])], Hs, Ws)
-            d, dm = blk.run([(d, dm), (feats[j], masks[j])], Hs, Ws)
+            d, dm = blk.run([(d, dm), (feats[j], masks[j])], Hs, Ws, keep_y=False)
         if (2 * d.shape[2], 2 * d.shape[3]) != (Hp, Wp):
             raise RuntimeError(f"Size mismatch before final layer. Dec: {d.shape[2:]}, "
                                f"Skip: {(Hp, Wp)}")

@@ -1176,14 +1176,16 @@ def affine_act_(y, scale, shift, act, slope=0.2):
     return y
 
 
-def affine_act_nhwc16_(y, scale, shift, act, slope=0.2, m=None):
+def affine_act_nhwc16_(y, scale, shift, act, slope=0.2, m=None, keep_y=True):
     """affine_act_ in place and, in the same pass, the bf16 channel-last copy of
     the result times the mask plane m (ainp_affine_act_nhwc16); inside an
-    nhwc16_memo scope the copy is what to_nhwc16(y, m) returns afterwards."""
+    nhwc16_memo scope the copy is what to_nhwc16(y, m) returns afterwards.
+    keep_y=False: y keeps its input values (AINP_AFFINE_NO_Y) -- only for
+    callers whose every consumer reads the copy."""
     _req(y, "y")
     N, C, H, W = y.shape
     out = torch.empty(N, H, W, C, device=y.device, dtype=torch.bfloat16)
-    _T.affine_act_nhwc16(y, scale, shift, int(act), float(slope), m, out)
+    _T.affine_act_nhwc16(y, scale, shift, int(act), float(slope), m, out, bool(keep_y))
     memo = _NHWC_MEMO
     if memo is not None:
         key = (y.data_ptr(), tuple(y.shape), y._version,

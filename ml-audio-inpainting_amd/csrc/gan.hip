@@ -2100,6 +2100,9 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc16_kernel(const float* __rest
 // in the same pass, the channel-last bf16 copy of act(y) times the mask plane
 // (nchw_to_nhwc16_kernel's conversion): the bf16 U-Net's block outputs feed
 // the next conv without a separate conversion pass.
+// KEEP_Y = false: y is only read (a caller whose consumers all take the
+// channel-last copy skips the fp32 write-back, a third of the pass's bytes).
+template <bool KEEP_Y>
 __global__ __launch_bounds__(256) void affine_act_nhwc16_kernel(
     float* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
     int act, float slope, const float* __restrict__ m, int C, int H, int W,
@@ -2118,7 +2121,7 @@ __global__ __launch_bounds__(256) void affine_act_nhwc16_kernel(
     if (c < C && w < W) {
       float* q = y + (((int64_t)n * C + c) * H + h) * W + w;
       v = apply_act(fmaf(*q, scale[c], shift[c]), act, slope);
-      *q = v;
+      if (KEEP_Y) *q = v;
       v *= mv;
     }
     tile[tx][i] = __builtin_bit_cast(uint16_t, (__bf16)v);
@@ -2502,13 +2505,22 @@ extern "C" int ainp_nchw_to_nhwc16(const float* x, const float* m, int64_t N, in
 extern "C" int ainp_affine_act_nhwc16(float* y, const float* scale, const float* shift,
                                      int64_t N, int C, int H, int W, int act, float slope,
                                      const float* m, uint16_t* out, void* stream) {
+  return ainp_affine_act_nhwc16_ex(y, scale, shift, N, C, H, W, act, slope, m, out, 0, stream);
+}
+
+extern "C" int ainp_affine_act_nhwc16_ex(float* y, const float* scale, const float* shift,
+                                        int64_t N, int C, int H, int W, int act, float slope,
+                                        const float* m, uint16_t* out, int flags, void* stream) {
   if (!y || !scale || !shift || !out || N < 1 || C < 1 || H < 1 || W < 1 ||
-      N * ((C + 63) / 64) > 65535 || H > 65535)
+      N * ((C + 63) / 64) > 65535 || H > 65535 || (flags & ~AINP_AFFINE_NO_Y))
     return record_msg("ainp_affine_act_nhwc16: bad argument");
-  hipLaunchKernelGGL(affine_act_nhwc16_kernel, dim3((unsigned)cdiv(W, 64), (unsigned)H,
-                                                    (unsigned)(N * cdiv(C, 64))),
-                     dim3(256), 0, as_stream(stream), y, scale, shift, act, slope, m, C, H, W,
-                     out);
+  const dim3 grid((unsigned)cdiv(W, 64), (unsigned)H, (unsigned)(N * cdiv(C, 64)));
+  if (flags & AINP_AFFINE_NO_Y)
+    hipLaunchKernelGGL(affine_act_nhwc16_kernel<false>, grid, dim3(256), 0, as_stream(stream), y,
+                       scale, shift, act, slope, m, C, H, W, out);
+  else
+    hipLaunchKernelGGL(affine_act_nhwc16_kernel<true>, grid, dim3(256), 0, as_stream(stream), y,
+                       scale, shift, act, slope, m, C, H, W, out);
   return check_launch("affine_act_nhwc16");
 }
 

@@ -1051,7 +1051,7 @@ void nchw_to_nhwc16(const Tensor& x, const OptT& m, const Tensor& out) {
 }
 
 void affine_act_nhwc16(const Tensor& y, const Tensor& scale, const Tensor& shift, int64_t act,
-                       double slope, const OptT& m, const Tensor& out) {
+                       double slope, const OptT& m, const Tensor& out, bool keep_y) {
   GUARD(y);
   TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
   const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
@@ -1060,9 +1060,10 @@ void affine_act_nhwc16(const Tensor& y, const Tensor& scale, const Tensor& shift
   const float* mp = opt(m, "mask");
   if (mp) numel_is(*m, N * H * W, "mask");
   numel_is(out, y.numel(), "out");
-  chk(ainp_affine_act_nhwc16(dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"), N, (int)C,
-                             (int)H, (int)W, (int)act, (float)slope, mp, bf16p(out, "out"),
-                             stream_of(y)),
+  chk(ainp_affine_act_nhwc16_ex(dev(y, "y"), dev(scale, "scale"), dev(shift, "shift"), N,
+                                (int)C, (int)H, (int)W, (int)act, (float)slope, mp,
+                                bf16p(out, "out", true), keep_y ? 0 : AINP_AFFINE_NO_Y,
+                                stream_of(y)),
       "affine_act_nhwc16");
 }
 
@@ -1537,7 +1538,7 @@ TORCH_LIBRARY(ainp, m) {
         "int kc) -> ()");
   m.def("nchw_to_nhwc16(Tensor x, Tensor? m, Tensor(a!) out) -> ()");
   m.def("affine_act_nhwc16(Tensor(a!) y, Tensor scale, Tensor shift, int act, float slope, "
-        "Tensor? m, Tensor(b!) out) -> ()");
+        "Tensor? m, Tensor(b!) out, bool keep_y=True) -> ()");
   m.def("conv_weight_nhwc16(Tensor w, int C0, int C1, Tensor(a!) wt16) -> ()");
   m.def("conv_gen_fwd_nhwc16(Tensor x0, Tensor? x1, Tensor wt16, int Cout, int KH, int KW, "
         "Tensor? bias, Tensor? ratio, Tensor? scale, Tensor(a!) y, Tensor(b!)? stats, int Hin, "

@@ -978,3 +978,20 @@ def test_generator_training_step_matches_reference(golden_dir):
     for k in f.files:
         if k.startswith("g_init/") and "running" not in k and "num_batches" not in k:
             assert np.array_equal(sd0[k[len("g_init/"):]].cpu().numpy(), f[k]), k
+
+
+def test_unet_bf16_forward_without_fp32_writeback_is_bit_identical(monkeypatch):
+    """bf16 U-Net no-grad forward: the BatchNorm + LeakyReLU pass that writes
+    only the channel-last copy (AINP_AFFINE_NO_Y) gives the same output, bit
+    for bit -- no consumer reads the fp32 block outputs."""
+    from ainp import gan as G
+    torch.manual_seed(4)
+    net = G.set_compute_dtype(G.PConvUNet().cuda().eval(), "bf16")
+    x = torch.randn(2, 1, 129, 250, device="cuda")
+    m = (torch.rand(2, 1, 129, 250, device="cuda") > 0.2).float()
+    outs = []
+    for flag in (True, False):
+        monkeypatch.setattr(G, "AFFINE_NO_Y", flag)
+        with torch.no_grad():
+            outs.append(net(x, m).clone())
+    assert torch.equal(outs[0], outs[1])
