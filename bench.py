@@ -392,9 +392,9 @@ def spawn_ranks(n):
 # profiles/steps/ so they travel with gpurun / the driver's snapshot
 # (.gpurunignore drops profiles/r0*)
 STEP_TABLES = {
-    ("cnnblstm", "fp32"): ("profiles/steps/r04zB3_cnn_fp32_step_kernel_stats.csv", 13),
-    ("cnnblstm", "bf16"): ("profiles/steps/r04zB3_cnn_bf16_step_kernel_stats.csv", 13),
-    ("gan", "bf16", 626): ("profiles/steps/r04zB3_gan_c4_step_kernel_stats.csv", 9),
+    ("cnnblstm", "fp32"): ("profiles/steps/r04zB4_cnn_fp32_step_kernel_stats.csv", 13),
+    ("cnnblstm", "bf16"): ("profiles/steps/r04zB4_cnn_bf16_step_kernel_stats.csv", 13),
+    ("gan", "bf16", 626): ("profiles/steps/r04zB4_gan_c4_step_kernel_stats.csv", 9),
     ("gan", "bf16", 1001): ("profiles/steps/r04d_gan_c5_step_kernel_stats.csv", 13),
 }
 
