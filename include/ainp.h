@@ -330,6 +330,18 @@ int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
  * forwards and split-bf16 weight gradients (ainp_conv3x3_io16_ok). */
 #define AINP_CONV_X16 8
 #define AINP_CONV_Y16 16
+/* Round 5: channel-last activations, [N][H][W][C] (a pixel's channels
+ * contiguous; 1-2-channel tensors are the same in either layout).  The
+ * input (forward: x; data gradient: dy; weight gradient: x) is channel-last
+ * with AINP_CONV_XCL, the output (forward: y; data gradient: dx) with
+ * AINP_CONV_YCL, the weight gradient's dy with AINP_CONV_GCL.  Every
+ * combination with the bf16 flags above; served for the pairs
+ * ainp_conv3x3_cl_ok accepts (the model's 1/16/32/64-channel convs).
+ * Replaces the NCHW convs of models/CNNBLSTM/model.py:34-61. */
+#define AINP_CONV_XCL 32
+#define AINP_CONV_YCL 64
+#define AINP_CONV_GCL 128
+int ainp_conv3x3_cl_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
 int ainp_conv3x3_fwd_ex(const float* x, const float* w, const float* bias,
                         const float* in_scale, const float* in_shift, float* y,
                         double* stats, int64_t N, int Cin, int Cout, int64_t H,
@@ -417,6 +429,11 @@ int ainp_bn_relu_bwd_apply(const float* g, const float* y, const float* scale,
  * bf16 values (uint16 storage through the float* argument; a forward with
  * AINP_CONV_Y16 wrote it). */
 #define AINP_BN_Y16 2
+/* Round 5: g, y and gy channel-last ([N][H][W][C], C = 16 / 32 / 64, 16-byte
+ * aligned; g_ntcf must be 0) -- the layout the AINP_CONV_XCL / _YCL convs
+ * read and write.  AINP_BN_G16 (with AINP_BN_CL): g in bf16 storage. */
+#define AINP_BN_CL 4
+#define AINP_BN_G16 8
 int ainp_bn_relu_bwd_reduce_ex(const float* g, const float* y, const float* scale,
                                const float* shift, const float* save_mean_rstd, void* workspace,
                                double* sums, int64_t N, int C, int64_t H, int64_t W, int g_ntcf,

@@ -75,6 +75,8 @@ class _ConvStackFn(torch.autograd.Function):
             q += 4 if has_bn else 2
         l0_path = bool(spec) and l0_box is not None and _l0_bf16_ok(
             (N, ws_[-1].shape[0], H, W))
+        # activation layout per block: (input channel-last, output channel-last)
+        lays = _cl_layouts(ws_, N, H, W, out_ntcf, x.shape[1])
         nbt = []             # num_batches_tracked += 1, applied by one multi-tensor add
         for bi, (has_bn, bn) in enumerate(spec):
             w, b = params[pi], params[pi + 1]
@@ -87,8 +89,9 @@ class _ConvStackFn(torch.autograd.Function):
                     y16 = ops.io16_ok(N, wn.shape[1], wn.shape[0], H, W)
                 else:
                     y16 = l0_path          # the bf16 bridge to the LSTM reads it
+            xcl, ycl = lays[bi]
             y, stats = ops.conv3x3_fwd(h, w, b, act[0], act[1], want_stats=want_stats, bf16=bf16,
-                                       y16=y16)
+                                       y16=y16, xcl=xcl, ycl=ycl)
             saved_y.append(y)
             if has_bn:
                 gamma, beta = params[pi], params[pi + 1]
@@ -135,6 +138,7 @@ class _ConvStackFn(torch.autograd.Function):
         else:
             out = saved_y[-1]
         ctx.spec = spec
+        ctx.lays = lays
         ctx.bf16 = bf16
         # (mode, sink): mode False / True (side stream now) / "queue" (released at
         # the first BPTT); sink = the data-parallel GradAllReducer or None
@@ -165,24 +169,26 @@ class _ConvStackFn(torch.autograd.Function):
         grads = [None] * len(params)
         g = g.contiguous()
         gx = None
+        N, H, W = x.shape[0], x.shape[2], x.shape[3]
         for bi in range(nb - 1, -1, -1):
             has_bn, _ = ctx.spec[bi]
             p0 = idx[bi]
             w = params[p0]
             y = ys[bi]
+            xcl, ycl = ctx.lays[bi]
             if has_bn:
                 sc, sh, sv = ctx.affine[bi]
                 ntcf = ctx.out_ntcf and bi == nb - 1
-                sums = _allreduce(ctx.comm, ops.bn_relu_bwd_reduce(g, y, sc, sh, sv, ntcf))
+                sums = _allreduce(ctx.comm, ops.bn_relu_bwd_reduce(g, y, sc, sh, sv, ntcf,
+                                                                   cl=ycl))
                 cnt = ctx.count
                 if ctx.count_dev is not None:
                     sums, cnt = torch.cat([sums, ctx.count_dev]), 0
                 # bf16 configuration: gy in bf16 storage where this conv's data
                 # and weight gradients take it (they round it to bf16 anyway)
-                gy16 = ctx.bf16 and GY16 and ops.dy16_ok(y.shape[0], w.shape[1], w.shape[0],
-                                                         y.shape[2], y.shape[3])
+                gy16 = ctx.bf16 and GY16 and ops.dy16_ok(N, w.shape[1], w.shape[0], H, W)
                 gy, dgam, dbet = ops.bn_relu_bwd_apply(g, y, sc, sh, params[p0 + 2], sv, sums,
-                                                       cnt, ntcf, gy16=gy16)
+                                                       cnt, ntcf, gy16=gy16, cl=ycl)
                 grads[p0 + 2], grads[p0 + 3] = dgam, dbet
             else:
                 gy = g.view_as(y) if g.shape != y.shape else g
@@ -193,13 +199,15 @@ class _ConvStackFn(torch.autograd.Function):
             else:
                 xin = x
                 pro = (None, None)
+            # layouts: the conv's input xin (xcl), its output / gy (ycl)
+            lw = dict(xcl=xcl, gcl=ycl)
             # the first conv's weight gradient is the backward's last work: with no
             # input gradient to compute, the main stream would only wait for it,
             # so it runs there, beside the side stream's tail (single process)
             last_main = (WGRAD_LAST_MAIN and bi == 0 and not ctx.needs_input_grad[0]
                          and ctx.sink is None)
             if last_main:
-                dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
+                dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16, **lw)
             elif ctx.defer_wgrad == "queue":
                 # off the critical path: queued, launched on the side stream when
                 # the BPTT recurrence (64 workgroups) starts -- filling the CUs
@@ -212,15 +220,16 @@ class _ConvStackFn(torch.autograd.Function):
                 # (a clone would copy it before the side stream writes it)
                 dwv, dbv = _alias(dw), _alias(db)
                 pr, bf = pro, ctx.bf16
-                _Deferred.push(gy.device, lambda xin=xin, gy=gy, pr=pr, dwv=dwv, dbv=dbv, bf=bf:
-                               ops.conv3x3_wgrad(xin, gy, pr[0], pr[1], bf16=bf, out=(dwv, dbv)),
+                _Deferred.push(gy.device, lambda xin=xin, gy=gy, pr=pr, dwv=dwv, dbv=dbv, bf=bf,
+                               lw=lw: ops.conv3x3_wgrad(xin, gy, pr[0], pr[1], bf16=bf,
+                                                        out=(dwv, dbv), **lw),
                                (xin, gy) + tuple(t for t in pro if t is not None), (dwv, dbv),
                                params=ctx.param_objs[p0:p0 + 2], sink=ctx.sink)
             elif ctx.defer_wgrad:
                 # off the critical path: on the side stream, overlapping the next
                 # (HBM-bound) BatchNorm backward passes
                 with _side_work(gy.device) as sw:
-                    dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
+                    dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16, **lw)
                     sw.handoff((xin, gy) + tuple(t for t in pro if t is not None), (dw, db))
                     # data parallel: all-reduced from the side stream as soon as
                     # they exist (the collective waits for this stream only).
@@ -232,13 +241,43 @@ class _ConvStackFn(torch.autograd.Function):
                     _reduce_side(ctx.sink, ctx.param_objs[p0:p0 + 2], (dw, db))
                     dw, db = _alias(dw), _alias(db)
             else:
-                dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16)
+                dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16, **lw)
             grads[p0], grads[p0 + 1] = dw, db
             if bi > 0 or ctx.needs_input_grad[0]:
-                g = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16)
+                # dx in this conv's input layout (the previous block's y)
+                g = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16, xcl=ycl, ycl=xcl)
                 if bi == 0:
                     gx = g
         return (gx, None, None, None, None, None, None, None, *grads)
+
+
+# Round 5: channel-last activations ([N, F, T, C]) between the 16/32-channel
+# convs of both conv stacks (AINP_CL=0: NCHW everywhere, as before).  The
+# 64-channel encoder output stays NCHW (the NTCF bridge to the LSTM and its
+# BatchNorm backward read it), so does the projection's 16-channel decoder
+# input; 1-channel tensors are the same in either layout.
+CL = os.environ.get("AINP_CL", "1") != "0"
+
+
+def _cl_layouts(ws, N, H, W, out_ntcf, cin0):
+    """[(input channel-last, output channel-last)] per conv of a stack whose
+    weights are ws: block i's output layout is block i+1's input layout."""
+    nb = len(ws)
+    if not (CL and nb and all(ops.cl_ok(N, w.shape[1], w.shape[0], H, W) for w in ws)):
+        return [(False, False)] * nb
+    outs = []
+    for i, w in enumerate(ws):
+        cout = w.shape[0]
+        last = i == nb - 1
+        # channel-last where a consumer conv reads it; NCHW for the bridge /
+        # the stack's 1-channel output
+        outs.append(not last and cout > 1)
+    lays = []
+    for i in range(nb):
+        xin_cl = outs[i - 1] if i > 0 else False   # stack input: NCHW (or 1 channel)
+        lays.append((xin_cl, outs[i]))
+    del out_ntcf, cin0
+    return lays
 
 
 # the encoder's first-conv weight gradient on the main stream when nothing

@@ -86,6 +86,11 @@ class Comm:
                         t.copy_(h)
                     else:
                         dist.broadcast(t.data, src, group=self.group)
+                    # the write went through storage (t.data / a host copy) that
+                    # does not bump t._version: bump it, so every weight cache
+                    # keyed on (data_ptr, _version) -- the k-major / bf16 weight
+                    # copies of ainp.ops -- rebuilds from the broadcast values
+                    torch.autograd.graph.increment_version(t)
         return module
 
 

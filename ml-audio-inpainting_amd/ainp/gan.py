@@ -181,6 +181,17 @@ class PartialConv2d(nn.Module):
 AFFINE_NO_Y = os.environ.get("AINP_AFFINE_NO_Y", "1") != "0"
 
 
+def _affine_no_y_safe():
+    """The fp32 write-back may be skipped only while every consumer of a U-Net
+    block output reads the channel-last copy: the 32-multiple-channel convs
+    always take the nhwc16 route, but the final PartialConv2d's (64 + 1 -> 64)
+    second source is the 1-channel padded input, which reaches that route only
+    through the CONV_NHWC16_SMALL branch (ops._nhwc16_route); with
+    AINP_CONV_NHWC16_SMALL=0 it runs the NCHW fp32 gather, which reads the
+    block output's fp32 planes, so they must be written."""
+    return AFFINE_NO_Y and ops.CONV_NHWC16 and ops.CONV_NHWC16_SMALL != "0"
+
+
 class EncoderBlock(nn.Module):
     """networks.py:139-152: PartialConv -> BatchNorm2d -> LeakyReLU(0.2)."""
 
@@ -225,7 +236,7 @@ class EncoderBlock(nn.Module):
             # forward the fp32 write-back is skipped unless a profiling capture
             # reads the planes
             ops.affine_act_nhwc16_(y, sc, sh, ops.ACT_LEAKY, SLOPE, newm,
-                                   keep_y=keep_y or not AFFINE_NO_Y
+                                   keep_y=keep_y or not _affine_no_y_safe()
                                    or PConvUNet.capture is not None)
             return y, newm
         return self._finish(y, stats), newm
@@ -510,6 +521,10 @@ class _PConvUNetFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         tape, unet = ctx.tape, ctx.unet
+        if tape is None:
+            raise RuntimeError("PConvUNet backward ran twice through the same graph: its saved "
+                               "activations are released after the first backward "
+                               "(retain_graph=True is not supported); run the forward again")
         ctx.tape = None
         grads = {}
         Hp, Wp, H, W = tape["Hp"], tape["Wp"], tape["H"], tape["W"]
@@ -568,6 +583,14 @@ class _PConvUNetFn(torch.autograd.Function):
                 gc, dgam, dbet = ops.bn_act_bwd_apply(gab, y, rec["sc"], rec["sh"], rec["save"],
                                                       bn.weight, sums, cnt, SLOPE, rec["ratio"],
                                                       ldb)
+                if cnt == 0:
+                    # SyncBN: dgamma / dbeta came from the all-reduced sums, so every
+                    # rank already holds the global sum; the trainer's reducer SUMs
+                    # over ranks and divides by world_size, so hand it the per-rank
+                    # share (torch SyncBN uses the local sums here; for equal
+                    # per-rank batches the two are the same, exactly for 2^k ranks)
+                    dgam.div_(comm.world_size)
+                    dbet.div_(comm.world_size)
                 grads[bn.weight], grads[bn.bias] = dgam, dbet
             else:
                 _, gc = ops.gen_act_bwd(gab, a, ops.ACT_LEAKY, SLOPE, rec["ratio"], Ho, Wo, ldb,
@@ -1116,6 +1139,10 @@ class _VGGLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gp, gs):
         keep, vgg = ctx.keep, ctx.vgg
+        if keep is None:
+            raise RuntimeError("VGGLoss backward ran twice through the same graph: its saved "
+                               "features are released after the first backward "
+                               "(retain_graph=True is not supported)")
         ctx.keep = None
         B = keep["B"]
         fg, ft = keep["fg"], keep["ft"]
@@ -1237,12 +1264,21 @@ class _ReconFn(torch.autograd.Function):
         n_total = g.numel() * ws
         ctx.save_for_backward(g, o, m, sums)
         ctx.n_total = n_total
+        ctx.ws = ws
         return ops.gan_recon_from_sums(sums, n_total).to(torch.float32)
 
     @staticmethod
     def backward(ctx, gout):
         g, o, m, sums = ctx.saved_tensors
-        return (ops.gan_recon_bwd(g, o, m, sums, gout.float().contiguous(), ctx.n_total),
+        # Under DP the three terms are global-batch values, so this rank's
+        # gradient is already its full share of d(global loss); the trainer's
+        # reducer then SUMs over ranks and divides by world_size (the averaging
+        # the per-rank-mean terms need).  Pre-scaling by world_size here makes
+        # that average return exactly d(global L1 terms)/d(theta).
+        gout = gout.float()
+        if ctx.ws > 1:
+            gout = gout * float(ctx.ws)
+        return (ops.gan_recon_bwd(g, o, m, sums, gout.contiguous(), ctx.n_total),
                 None, None, None)
 
 

@@ -183,6 +183,12 @@ CONV_X16 = 8           # AINP_CONV_X16: the act(x) source in bf16 storage (fwd /
 CONV_Y16 = 16          # AINP_CONV_Y16: forward output y in bf16 storage
 BN_GY16 = 1            # AINP_BN_GY16: BatchNorm-backward output gy in bf16 storage
 BN_Y16 = 2             # AINP_BN_Y16: the pre-BN input y in bf16 storage
+# round 5: channel-last activations [N, H, W, C] (include/ainp.h)
+CONV_XCL = 32          # AINP_CONV_XCL: input channel-last (fwd x, dgrad dy, wgrad x)
+CONV_YCL = 64          # AINP_CONV_YCL: output channel-last (fwd y, dgrad dx)
+CONV_GCL = 128         # AINP_CONV_GCL: the weight gradient's dy channel-last
+BN_CL = 4              # AINP_BN_CL: g / y / gy channel-last
+BN_G16 = 8             # AINP_BN_G16: g in bf16 storage (with BN_CL)
 
 
 def gemm(M, N, K, A, sam, sak, B, sbk, sbn, C, scm, scn, *, alpha=1.0, beta=0.0,
@@ -638,21 +644,27 @@ def _x_flag(x, bf16, name="x"):
 
 
 def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf16=False,
-                y16=False):
+                y16=False, xcl=False, ycl=False):
     """x fp32, or bf16 storage with bf16=True (AINP_CONV_X16); y16: y written
     as bf16 (AINP_CONV_Y16, BatchNorm partials of the stored values).  Both
-    where io16_ok says so (the bf16 configuration's pre-BN activations)."""
+    where io16_ok says so (the bf16 configuration's pre-BN activations).
+    xcl / ycl (round 5): x given / y returned channel-last, [N, H, W, C]
+    (AINP_CONV_XCL / _YCL; cl_ok says for which convs)."""
     _req(x, "x", None); _req(w, "w")
-    N, Cin, H, W = x.shape
+    if xcl:
+        N, H, W, Cin = x.shape
+    else:
+        N, Cin, H, W = x.shape
     Cout = w.shape[0]
     assert tuple(w.shape) == (Cout, Cin, 3, 3)
     flags = (CONV_BF16 if bf16 else 0) | _x_flag(x, bf16)
+    flags |= (CONV_XCL if xcl else 0) | (CONV_YCL if ycl else 0)
     if y16:
         if not bf16:
             raise ValueError("y16 needs the bf16 conv arithmetic (bf16=True)")
         flags |= CONV_Y16
-    y = torch.empty(N, Cout, H, W, device=x.device,
-                    dtype=torch.bfloat16 if y16 else torch.float32)
+    shape = (N, H, W, Cout) if ycl else (N, Cout, H, W)
+    y = torch.empty(shape, device=x.device, dtype=torch.bfloat16 if y16 else torch.float32)
     stats = None
     if want_stats:
         stats = torch.empty(_lib.lib.ainp_conv3x3_fwd_stat_rows_ex(N, Cin, Cout, H, W,
@@ -661,6 +673,12 @@ def conv3x3_fwd(x, w, b=None, in_scale=None, in_shift=None, want_stats=False, bf
                             device=x.device, dtype=torch.float64)
     _T.conv3x3_fwd(x, w, b, in_scale, in_shift, y, stats, flags)
     return y, stats
+
+
+def cl_ok(N, Cin, Cout, H, W) -> bool:
+    """ainp_conv3x3_cl_ok: every entry point of Conv2d(Cin, Cout) takes
+    channel-last activations."""
+    return bool(_lib.lib.ainp_conv3x3_cl_ok(N, Cin, Cout, H, W))
 
 
 def io16_ok(N, Cin, Cout, H, W) -> bool:
@@ -679,22 +697,32 @@ def _dy_flags(dy, bf16):
     return CONV_BF16 if bf16 else 0
 
 
-def conv3x3_dgrad(dy, w, bf16=False):
-    """dy fp32, or bf16 storage with bf16=True (AINP_CONV_DY16)."""
+def conv3x3_dgrad(dy, w, bf16=False, xcl=False, ycl=False):
+    """dy fp32, or bf16 storage with bf16=True (AINP_CONV_DY16).  xcl / ycl:
+    dy given / dx returned channel-last [N, H, W, C]."""
     _req(dy, "dy", None); _req(w, "w")
-    N, Cout, H, W = dy.shape
+    if xcl:
+        N, H, W, Cout = dy.shape
+    else:
+        N, Cout, H, W = dy.shape
     Cin = w.shape[1]
-    dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=torch.float32)
-    _T.conv3x3_dgrad(dy, w, dx, _dy_flags(dy, bf16))
+    dx = torch.empty((N, H, W, Cin) if ycl else (N, Cin, H, W), device=dy.device,
+                     dtype=torch.float32)
+    _T.conv3x3_dgrad(dy, w, dx, _dy_flags(dy, bf16) | (CONV_XCL if xcl else 0)
+                     | (CONV_YCL if ycl else 0))
     return dx
 
 
-def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False, out=None):
+def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False, out=None,
+                  xcl=False, gcl=False):
     """out: optional preallocated (dw, db) to write.  dy fp32, or bf16 storage
-    with bf16=True (AINP_CONV_DY16)."""
+    with bf16=True (AINP_CONV_DY16).  xcl / gcl: x / dy channel-last."""
     _req(x, "x", None); _req(dy, "dy", None)
-    N, Cin, H, W = x.shape
-    Cout = dy.shape[1]
+    if xcl:
+        N, H, W, Cin = x.shape
+    else:
+        N, Cin, H, W = x.shape
+    Cout = dy.shape[3] if gcl else dy.shape[1]
     if out is not None:
         dw, db = out
     else:
@@ -702,7 +730,9 @@ def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=Fals
         db = torch.empty(Cout, device=x.device, dtype=torch.float32) if want_bias else None
     ws_bytes = _lib.lib.ainp_conv3x3_wgrad_workspace(N, Cin, Cout, H, W)
     ws = torch.empty(ws_bytes, device=x.device, dtype=torch.uint8)
-    _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws, _dy_flags(dy, bf16) | _x_flag(x, bf16))
+    _T.conv3x3_wgrad(x, in_scale, in_shift, dy, dw, db, ws,
+                     _dy_flags(dy, bf16) | _x_flag(x, bf16) | (CONV_XCL if xcl else 0)
+                     | (CONV_GCL if gcl else 0))
     return dw, db
 
 
@@ -770,27 +800,41 @@ def _y_flag(y):
     return BN_Y16 if y.dtype == torch.bfloat16 else 0
 
 
-def bn_relu_bwd_reduce(g, y, scale, shift, save, ntcf=False):
-    """y fp32 or bf16 storage (AINP_BN_Y16)."""
-    _req(g, "g"); _req(y, "y", None)
-    N, C, H, W = y.shape
+def bn_relu_bwd_reduce(g, y, scale, shift, save, ntcf=False, cl=False):
+    """y fp32 or bf16 storage (AINP_BN_Y16).  cl (round 5): g and y
+    channel-last [N, H, W, C] (AINP_BN_CL), g fp32 or bf16 (AINP_BN_G16)."""
+    _req(y, "y", None)
+    if cl:
+        N, H, W, C = y.shape
+        flags = BN_CL | (BN_G16 if g.dtype == torch.bfloat16 else 0)
+    else:
+        _req(g, "g")
+        N, C, H, W = y.shape
+        flags = 0
     ws = torch.empty(_lib.lib.ainp_bn_relu_bwd_workspace(N, C, H, W), device=y.device,
                      dtype=torch.uint8)
     sums = torch.empty(2 * C, device=y.device, dtype=torch.float64)
-    _T.bn_relu_bwd_reduce(g, y, scale, shift, save, ws, sums, bool(ntcf), _y_flag(y))
+    _T.bn_relu_bwd_reduce(g, y, scale, shift, save, ws, sums, bool(ntcf), _y_flag(y) | flags)
     return sums
 
 
-def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False, gy16=False):
+def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False, gy16=False,
+                      cl=False):
     """gy16: gy in bf16 storage (AINP_BN_GY16) -- for the bf16 configuration's
     data / weight gradients, which round gy to bf16 anyway (conv3x3_dgrad /
-    conv3x3_wgrad take it with bf16=True; dy16_ok says for which convs)."""
-    N, C, H, W = y.shape
+    conv3x3_wgrad take it with bf16=True; dy16_ok says for which convs).
+    cl: g, y and gy channel-last [N, H, W, C]."""
+    if cl:
+        N, H, W, C = y.shape
+        flags = BN_CL | (BN_G16 if g.dtype == torch.bfloat16 else 0)
+    else:
+        N, C, H, W = y.shape
+        flags = 0
     gy = torch.empty(y.shape, device=y.device, dtype=torch.bfloat16 if gy16 else torch.float32)
     dgamma = torch.empty(C, device=y.device, dtype=torch.float32)
     dbeta = torch.empty(C, device=y.device, dtype=torch.float32)
     _T.bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, int(count), gy, dgamma, dbeta,
-                         bool(ntcf), (BN_GY16 if gy16 else 0) | _y_flag(y))
+                         bool(ntcf), (BN_GY16 if gy16 else 0) | _y_flag(y) | flags)
     return gy, dgamma, dbeta
 
 

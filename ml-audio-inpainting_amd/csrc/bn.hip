@@ -363,6 +363,172 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_flat(
 }
 
 
+
+// ---------------------------------------------------- channel-last path
+// Round 5: g, y and gy channel-last ([N][H][W][C], C a multiple of 8): a
+// thread owns 8 consecutive channels (one or two 16-byte loads per operand)
+// of every (256 / (C/8))-th pixel of its block's range, so its per-channel
+// constants stay in registers.  Partials [block][2C] (sum gz, sum gz*xhat),
+// summed in fixed order by bn_cl_partials_sum.
+constexpr int BNC_PIX = 2048;   // pixels per reduce block
+
+template <bool B16>
+__device__ __forceinline__ void bnc_ld8(const void* p, int64_t e, float (&v)[8]) {
+  if constexpr (B16) {
+    const uint4 q = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(p) + e);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(w[j] << 16);
+      v[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+    }
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + e);
+    const float4 b = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + e + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+}
+
+template <int C, bool GB16, bool YB16>
+__global__ __launch_bounds__(256) void bn_relu_bwd_reduce_cl(
+    const void* __restrict__ g, const void* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ save, double* __restrict__ partial,
+    int64_t P) {
+  constexpr int G = C / 8, PPI = 256 / G;
+  __shared__ double red[4][2 * C];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, grp = tid % G;
+  float sc[8], sh[8], mu[8], rs[8], s1[8], s2[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int ch = 8 * grp + c;
+    sc[c] = scale[ch];
+    sh[c] = shift[ch];
+    mu[c] = save[ch];
+    rs[c] = save[C + ch];
+    s1[c] = s2[c] = 0.f;
+  }
+  const int64_t p0 = (int64_t)blockIdx.x * BNC_PIX + tid / G;
+#pragma unroll 4
+  for (int it = 0; it < BNC_PIX / PPI; ++it) {
+    const int64_t p = p0 + (int64_t)it * PPI;
+    if (p < P) {
+      float gv[8], yv[8];
+      bnc_ld8<GB16>(g, p * C + 8 * grp, gv);
+      bnc_ld8<YB16>(y, p * C + 8 * grp, yv);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float gz = fmaf(yv[c], sc[c], sh[c]) > 0.f ? gv[c] : 0.f;
+        s1[c] += gz;
+        s2[c] += gz * ((yv[c] - mu[c]) * rs[c]);
+      }
+    }
+  }
+  // lanes of one channel group: xor offsets G, 2G, .. 32 (fixed order)
+#pragma unroll
+  for (int o = G; o < 64; o <<= 1)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      s1[c] += __shfl_xor(s1[c], o, 64);
+      s2[c] += __shfl_xor(s2[c], o, 64);
+    }
+  if (lane < G) {
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      red[wave][8 * lane + c] = s1[c];
+      red[wave][C + 8 * lane + c] = s2[c];
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * C)
+    partial[(int64_t)blockIdx.x * 2 * C + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+
+// sums[o] = sum over blocks of partial[block][o], o < 2C: 256 / (2C) threads
+// per output over strided block subsets, then combined in fixed order
+__global__ __launch_bounds__(256) void bn_cl_partials_sum(const double* __restrict__ partial,
+                                                          int nblk, int C2,
+                                                          double* __restrict__ sums) {
+  __shared__ double red[256];
+  const int tid = threadIdx.x, per = 256 / C2, o = tid % C2, sub = tid / C2;
+  double a = 0.0;
+  if (sub < per)
+    for (int b = sub; b < nblk; b += per) a += partial[(int64_t)b * C2 + o];
+  red[tid] = a;
+  __syncthreads();
+  if (tid < C2) {
+    double t = 0.0;
+    for (int k = 0; k < per; ++k) t += red[k * C2 + tid];
+    sums[tid] = t;
+  }
+}
+
+template <int C, bool GB16, bool YB16, bool OB16>
+__global__ __launch_bounds__(256) void bn_relu_bwd_apply_cl(
+    const void* __restrict__ g, const void* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ gamma,
+    const float* __restrict__ save, const double* __restrict__ sums, void* __restrict__ gy,
+    float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t P, double inv_count) {
+  constexpr int G = C / 8, PPI = 256 / G, UNR = 4;
+  const int tid = threadIdx.x, grp = tid % G;
+  if (blockIdx.x == 0 && tid < C) {
+    if (dbeta) dbeta[tid] = (float)sums[tid];
+    if (dgamma) dgamma[tid] = (float)sums[C + tid];
+  }
+  const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C];   // see bn_finalize
+  float sc[8], sh[8], mu[8], rs[8], kk[8], m1[8], m2[8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const int ch = 8 * grp + c;
+    sc[c] = scale[ch];
+    sh[c] = shift[ch];
+    mu[c] = save[ch];
+    rs[c] = save[C + ch];
+    kk[c] = (gamma ? gamma[ch] : 1.f) * rs[c];
+    m1[c] = (float)(sums[ch] * ic);
+    m2[c] = (float)(sums[C + ch] * ic);
+  }
+  for (int64_t pb = (int64_t)blockIdx.x * PPI * UNR; pb < P; pb += (int64_t)gridDim.x * PPI * UNR) {
+    float gv[UNR][8], yv[UNR][8];
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = pb + u * PPI + tid / G;
+      if (p < P) {
+        bnc_ld8<GB16>(g, p * C + 8 * grp, gv[u]);
+        bnc_ld8<YB16>(y, p * C + 8 * grp, yv[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int64_t p = pb + u * PPI + tid / G;
+      if (p >= P) continue;
+      float o[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float gz = fmaf(yv[u][c], sc[c], sh[c]) > 0.f ? gv[u][c] : 0.f;
+        o[c] = kk[c] * (gz - m1[c] - ((yv[u][c] - mu[c]) * rs[c]) * m2[c]);
+      }
+      const int64_t e = p * C + 8 * grp;
+      if constexpr (OB16) {
+        uint4 q;
+        q.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[0]) |
+              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[1]) << 16);
+        q.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[2]) |
+              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[3]) << 16);
+        q.z = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[4]) |
+              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[5]) << 16);
+        q.w = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[6]) |
+              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[7]) << 16);
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(gy) + e) = q;
+      } else {
+        float* d = reinterpret_cast<float*>(gy) + e;
+        *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
+        *reinterpret_cast<float4*>(d + 4) = make_float4(o[4], o[5], o[6], o[7]);
+      }
+    }
+  }
+}
+
 // ----------------------------------------------------------- NTCF path
 // The encoder's last BatchNorm+ReLU reads / writes the LSTM layout
 // [n][w][c*H + h] (model.py:73-74) while y is NCHW: 64(h) x 64(w) tiles of one
@@ -775,7 +941,9 @@ extern "C" int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale,
 
 extern "C" size_t ainp_bn_relu_bwd_workspace(int64_t N, int C, int64_t H,
                                              int64_t W) {
-  return (size_t)(N * C * tiles_per_plane(H, W) * 2) * sizeof(double);
+  const int64_t tiled = N * C * tiles_per_plane(H, W) * 2;
+  const int64_t cl = cdiv(N * H * W, BNC_PIX) * 2 * C;   // channel-last partials
+  return (size_t)(tiled > cl ? tiled : cl) * sizeof(double);
 }
 
 template <bool YB16>
@@ -811,14 +979,79 @@ static int bn_bwd_reduce_launch(const float* g, const float* y, const float* sca
   return check_launch("bn_bwd_sum");
 }
 
+// channel-last launchers (AINP_BN_CL; AINP_BN_G16: g in bf16 storage)
+static bool bn_cl_ok(int C, std::initializer_list<const void*> ptrs) {
+  if (C % 8 != 0 || C > 64) return false;
+  for (const void* p : ptrs)
+    if (reinterpret_cast<uintptr_t>(p) % 16 != 0) return false;
+  return true;
+}
+
+static int bn_cl_reduce(const float* g, const float* y, const float* scale, const float* shift,
+                        const float* save, void* workspace, double* sums, int64_t P, int C,
+                        int g_ntcf, int flags, hipStream_t s) {
+  if (!(flags & AINP_BN_CL) || g_ntcf || !bn_cl_ok(C, {g, y}))
+    return record_msg("ainp_bn_relu_bwd_reduce: AINP_BN_CL needs C % 8 == 0 (<= 64), 16-byte "
+                      "aligned g / y and no NTCF layout (AINP_BN_G16 needs AINP_BN_CL)");
+  const int64_t nblk = cdiv(P, BNC_PIX);
+  double* partial = reinterpret_cast<double*>(workspace);
+  const bool g16 = flags & AINP_BN_G16, y16 = flags & AINP_BN_Y16;
+#define AINP_BNCR(CV, GV, YV)                                                                   \
+  if (C == CV && g16 == GV && y16 == YV)                                                        \
+    hipLaunchKernelGGL((bn_relu_bwd_reduce_cl<CV, GV, YV>), dim3((unsigned)nblk), dim3(256), 0, s, \
+                       g, y, scale, shift, save, partial, P);
+#define AINP_BNCR4(CV) AINP_BNCR(CV, false, false) AINP_BNCR(CV, true, false) \
+  AINP_BNCR(CV, false, true) AINP_BNCR(CV, true, true)
+  AINP_BNCR4(16) AINP_BNCR4(32) AINP_BNCR4(64)
+  if (C != 16 && C != 32 && C != 64)
+    return record_msg("ainp_bn_relu_bwd_reduce: AINP_BN_CL serves C = 16, 32, 64");
+#undef AINP_BNCR4
+#undef AINP_BNCR
+  int rc = check_launch("bn_relu_bwd_reduce_cl");
+  if (rc) return rc;
+  hipLaunchKernelGGL(bn_cl_partials_sum, dim3(1), dim3(256), 0, s, partial, (int)nblk, 2 * C, sums);
+  return check_launch("bn_cl_partials_sum");
+}
+
+static int bn_cl_apply(const float* g, const float* y, const float* scale, const float* shift,
+                       const float* gamma, const float* save, const double* sums, int64_t count,
+                       void* gy, float* dgamma, float* dbeta, int64_t P, int C, int g_ntcf,
+                       int flags, hipStream_t s) {
+  if (!(flags & AINP_BN_CL) || g_ntcf || !bn_cl_ok(C, {g, y, gy}))
+    return record_msg("ainp_bn_relu_bwd_apply: AINP_BN_CL needs C % 8 == 0 (<= 64), 16-byte "
+                      "aligned g / y / gy and no NTCF layout (AINP_BN_G16 needs AINP_BN_CL)");
+  const double inv_count = count > 0 ? 1.0 / (double)count : 0.0;   // 0: sums[2C]
+  const int ppb = 256 / (C / 8) * 4;                                 // pixels per block pass
+  int64_t nb = cdiv(P, ppb);
+  if (nb > 2048) nb = 2048;
+  const bool g16 = flags & AINP_BN_G16, y16 = flags & AINP_BN_Y16, o16 = flags & AINP_BN_GY16;
+#define AINP_BNCA(CV, GV, YV, OV)                                                              \
+  if (C == CV && g16 == GV && y16 == YV && o16 == OV)                                          \
+    hipLaunchKernelGGL((bn_relu_bwd_apply_cl<CV, GV, YV, OV>), dim3((unsigned)nb), dim3(256), 0, \
+                       s, g, y, scale, shift, gamma, save, sums, gy, dgamma, dbeta, P, inv_count);
+#define AINP_BNCA8(CV) AINP_BNCA(CV, false, false, false) AINP_BNCA(CV, false, false, true) \
+  AINP_BNCA(CV, true, false, false) AINP_BNCA(CV, true, false, true)                        \
+  AINP_BNCA(CV, false, true, false) AINP_BNCA(CV, false, true, true)                        \
+  AINP_BNCA(CV, true, true, false) AINP_BNCA(CV, true, true, true)
+  AINP_BNCA8(16) AINP_BNCA8(32) AINP_BNCA8(64)
+  if (C != 16 && C != 32 && C != 64)
+    return record_msg("ainp_bn_relu_bwd_apply: AINP_BN_CL serves C = 16, 32, 64");
+#undef AINP_BNCA8
+#undef AINP_BNCA
+  return check_launch("bn_relu_bwd_apply_cl");
+}
+
 extern "C" int ainp_bn_relu_bwd_reduce_ex(const float* g, const float* y, const float* scale,
                                           const float* shift, const float* save_mean_rstd,
                                           void* workspace, double* sums, int64_t N, int C,
                                           int64_t H, int64_t W, int g_ntcf, int flags,
                                           void* stream) {
   if (!g || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
-      N < 1 || C < 1 || H < 1 || W < 1 || (flags & ~AINP_BN_Y16))
+      N < 1 || C < 1 || H < 1 || W < 1 || (flags & ~(AINP_BN_Y16 | AINP_BN_CL | AINP_BN_G16)))
     return record_msg("ainp_bn_relu_bwd_reduce: bad argument");
+  if (flags & (AINP_BN_CL | AINP_BN_G16))
+    return bn_cl_reduce(g, y, scale, shift, save_mean_rstd, workspace, sums, N * H * W, C,
+                        g_ntcf, flags, as_stream(stream));
   if (flags & AINP_BN_Y16)
     return bn_bwd_reduce_launch<true>(g, y, scale, shift, save_mean_rstd, workspace, sums, N, C,
                                       H, W, g_ntcf, as_stream(stream));
@@ -850,9 +1083,13 @@ extern "C" int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const f
                                          int64_t N, int C, int64_t H, int64_t W, int g_ntcf,
                                          int flags, void* stream) {
   if (!g || !y || !scale || !shift || !save_mean_rstd || !sums || !gy ||
-      N < 1 || C < 1 || H < 1 || W < 1 || count < 0 || (flags & ~(AINP_BN_GY16 | AINP_BN_Y16)))
+      N < 1 || C < 1 || H < 1 || W < 1 || count < 0 ||
+      (flags & ~(AINP_BN_GY16 | AINP_BN_Y16 | AINP_BN_CL | AINP_BN_G16)))
     return record_msg("ainp_bn_relu_bwd_apply: bad argument");
   hipStream_t s = as_stream(stream);
+  if (flags & (AINP_BN_CL | AINP_BN_G16))
+    return bn_cl_apply(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy, dgamma, dbeta,
+                       N * H * W, C, g_ntcf, flags, s);
 #define AINP_BNA(GV, YV)                                                                       \
   return bn_bwd_apply_launch<GV, YV>(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy, \
                                      dgamma, dbeta, N, C, H, W, g_ntcf, s)

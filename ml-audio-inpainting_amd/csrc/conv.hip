@@ -639,7 +639,10 @@ static int wgrad_pass(int Cin) { return Cin < WG_CIMAX ? Cin : WG_CIMAX; }
 // numbering as conv3x3_fwd_mfma), 128 threads = 8 rows x 16 x 3 pixels, input
 // tile + weights in LDS.  The tile is staged with every global load issued
 // before the first LDS store (no per-element load->store latency chain).
-template <int CIN, bool PRO, int NT>
+// XL (round 5): x channel-last [N][H][W][CIN]; element e then walks the
+// channels of a pixel fastest (contiguous loads) and lands in the same
+// [c][row][col] LDS image.
+template <int CIN, bool PRO, int NT, bool XL = false>
 __device__ __forceinline__ void stage_small_tile(const float* __restrict__ x,
                                                  const float* __restrict__ in_scale,
                                                  const float* __restrict__ in_shift,
@@ -648,29 +651,44 @@ __device__ __forceinline__ void stage_small_tile(const float* __restrict__ x,
   constexpr int PER = (E + NT - 1) / NT;
   constexpr int BATCH = PER < 16 ? PER : 16;      // loads in flight per thread
   const int64_t HW = (int64_t)H * W;
+  auto decode = [&](int e, int& c, int& rr, int& cc) {
+    if constexpr (XL) {
+      c = e % CIN;
+      rr = (e / CIN) / LR;
+      cc = (e / CIN) % LR;
+    } else {
+      c = e / (ROWS * LR);
+      rr = (e / LR) % ROWS;
+      cc = e % LR;
+    }
+  };
 #pragma unroll
   for (int b0 = 0; b0 < PER; b0 += BATCH) {
     float v[BATCH];
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
       const int e = threadIdx.x + NT * (b0 + i);
-      const int c = e / (ROWS * LR), rr = (e / LR) % ROWS, cc = e % LR;
+      int c, rr, cc;
+      decode(e, c, rr, cc);
       const int f = f0 - 1 + rr, t = t0 - 1 + cc;
       const bool ok = b0 + i < PER && e < E && f >= 0 && f < H && t >= 0 && t < W;
-      v[i] = ok ? x[((int64_t)n * CIN + c) * HW + (int64_t)f * W + t] : 0.f;
+      const int64_t off = XL ? ((int64_t)n * HW + (int64_t)f * W + t) * CIN + c
+                             : ((int64_t)n * CIN + c) * HW + (int64_t)f * W + t;
+      v[i] = ok ? x[off] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < BATCH; ++i) {
       const int e = threadIdx.x + NT * (b0 + i);
       if (b0 + i >= PER || e >= E) break;
+      int c, rr, cc;
+      decode(e, c, rr, cc);
       float a = v[i];
       if (PRO) {
-        const int c = e / (ROWS * LR), rr = (e / LR) % ROWS, cc = e % LR;
         const int f = f0 - 1 + rr, t = t0 - 1 + cc;
         // BatchNorm+ReLU of the previous layer; zero padding stays zero
         if (f >= 0 && f < H && t >= 0 && t < W) a = fmaxf(fmaf(a, in_scale[c], in_shift[c]), 0.f);
       }
-      sx[e] = a;
+      sx[(c * ROWS + rr) * LR + cc] = a;
     }
   }
 }
@@ -678,7 +696,7 @@ __device__ __forceinline__ void stage_small_tile(const float* __restrict__ x,
 // PX pixels per thread: 3 (128 threads) when COUT is wide (per-thread outputs
 // amortise the stats reduction), 1 (384 threads) when it is 1-2 (more waves
 // in flight for the 16-channel staging).
-template <int CIN, int COUT, bool DGRAD, bool PRO, int PX>
+template <int CIN, int COUT, bool DGRAD, bool PRO, int PX, bool XL = false, bool YL = false>
 __global__ __launch_bounds__(384 / PX) void conv3x3_small_fwd(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -690,7 +708,7 @@ __global__ __launch_bounds__(384 / PX) void conv3x3_small_fwd(
   const int n = blockIdx.z, f0 = blockIdx.y * TR, t0 = blockIdx.x * TC;
   const int tid = threadIdx.x;
   const int64_t HW = (int64_t)H * W;
-  stage_small_tile<CIN, PRO, NT>(x, in_scale, in_shift, sx, n, f0, t0, H, W);
+  stage_small_tile<CIN, PRO, NT, XL>(x, in_scale, in_shift, sx, n, f0, t0, H, W);
   for (int i = tid; i < COUT * CIN * 9; i += blockDim.x) {
     const int co = i / (CIN * 9), ci = (i / 9) % CIN, tap = i % 9;
     sw[co][ci][tap] = DGRAD ? w[(ci * COUT + co) * 9 + 8 - tap] : w[(co * CIN + ci) * 9 + tap];
@@ -725,9 +743,18 @@ __global__ __launch_bounds__(384 / PX) void conv3x3_small_fwd(
     const int t = t0 + c0 + TPR * q;
     ok[q] = f < H && t < W;
     if (ok[q]) {
+      if constexpr (YL && COUT % 4 == 0) {   // channel-last: a pixel's COUT channels
+        float4* yp = reinterpret_cast<float4*>(y + ((int64_t)n * HW + (int64_t)f * W + t) * COUT);
 #pragma unroll
-      for (int co = 0; co < COUT; ++co)
-        y[((int64_t)n * COUT + co) * HW + (int64_t)f * W + t] = acc[q][co];
+        for (int c4 = 0; c4 < COUT / 4; ++c4)
+          yp[c4] = make_float4(acc[q][4 * c4], acc[q][4 * c4 + 1], acc[q][4 * c4 + 2],
+                               acc[q][4 * c4 + 3]);
+      } else {
+#pragma unroll
+        for (int co = 0; co < COUT; ++co)
+          y[YL ? ((int64_t)n * HW + (int64_t)f * W + t) * COUT + co
+               : ((int64_t)n * COUT + co) * HW + (int64_t)f * W + t] = acc[q][co];
+      }
     }
   }
   if (stats) {
@@ -815,6 +842,256 @@ __global__ __launch_bounds__(256) void conv3x3_small_wgrad(
   }
 }
 
+// wgrad of the 1-2-channel-sided convs as row strips (round 5): one wave per
+// (input channel ca, output channel cg) pair walks a strip of SW_RS rows of
+// one image; its 64 lanes cover columns t0-1 .. t0+62 and lanes 1..62 own the
+// output columns t0 .. t0+61.  Each loaded row of act(x)[ca] is shifted by one
+// lane both ways (the kx = 0 / 2 taps), the last three rows stay in registers
+// (the ky taps), so every input element is read from HBM once per pair and
+// every lane does 9 FMAs per pixel -- no LDS, no partially idle threads (the
+// 8x48-tile kernel above keeps 145 of 256 threads busy and re-stages the
+// halo per tile; in the C2 step its 16->1 instance ran 1.8 ms beside the
+// layer-0 GEMM pair on the side stream).  Rows are loaded SW_RB at a time.
+// Partial slabs: [tile][NOUT] with the old kernel's output order, reduced by
+// the same fixed-order wgrad_reduce1 + small_wgrad_final.
+constexpr int SW_RS = 32;          // rows per strip
+constexpr int SW_TW = 62;          // output columns per wave
+constexpr int SW_RB = 8;           // rows loaded per batch
+
+template <int CA, int CG, bool PRO>
+__global__ __launch_bounds__(256) void conv3x3_strip_wgrad(
+    const float* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const float* __restrict__ dy,
+    float* __restrict__ partial, int H, int W, int ntf, int ntt) {
+  constexpr int NOUT = CG * CA * 9 + CG;
+  const int lane = threadIdx.x & 63;
+  const int pair = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (pair >= CA * CG) return;                 // whole waves only: no barrier below
+  const int ca = pair % CA, cg = pair / CA;
+  const int tile = blockIdx.x;                 // (n, strip, column block)
+  const int tt = tile % ntt, fs = (tile / ntt) % ntf, n = tile / (ntt * ntf);
+  const int f0 = fs * SW_RS, t = tt * SW_TW - 1 + lane;
+  const bool tin = t >= 0 && t < W;
+  const bool own = lane >= 1 && lane <= SW_TW && tin;
+  const int64_t HW = (int64_t)H * W;
+  const float* xa = x + ((int64_t)n * CA + ca) * HW + t;
+  const float* gg = dy + ((int64_t)n * CG + cg) * HW + t;
+  float sc = 1.f, sh = 0.f;
+  if (PRO) {
+    sc = in_scale[ca];
+    sh = in_shift[ca];
+  }
+  float acc[9], accb = 0.f;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) acc[i] = 0.f;
+  // window rows f-1, f, f+1 of act(x): (left, centre, right) per lane
+  float w0l = 0.f, w0c = 0.f, w0r = 0.f, w1l = 0.f, w1c = 0.f, w1r = 0.f;
+  // row f0-1 and f0 prime the window
+  {
+    const int f = f0 - 1;
+    float a = (f >= 0 && tin) ? xa[(int64_t)f * W] : 0.f;
+    if (PRO && f >= 0 && tin) a = fmaxf(fmaf(a, sc, sh), 0.f);
+    w1c = a;
+    w1l = __shfl_up(a, 1, 64);
+    w1r = __shfl_down(a, 1, 64);
+  }
+  {
+    const int f = f0;
+    float a = (f < H && tin) ? xa[(int64_t)f * W] : 0.f;
+    if (PRO && f < H && tin) a = fmaxf(fmaf(a, sc, sh), 0.f);
+    w0l = w1l; w0c = w1c; w0r = w1r;
+    w1c = a;
+    w1l = __shfl_up(a, 1, 64);
+    w1r = __shfl_down(a, 1, 64);
+  }
+  const int rows = (H - f0) < SW_RS ? (H - f0) : SW_RS;
+  for (int r0 = 0; r0 < rows; r0 += SW_RB) {
+    float va[SW_RB], vg[SW_RB];
+#pragma unroll
+    for (int i = 0; i < SW_RB; ++i) {
+      const int f = f0 + r0 + i;              // output row; a needs row f+1
+      const bool rok = r0 + i < rows;
+      va[i] = (rok && f + 1 < H && tin) ? xa[(int64_t)(f + 1) * W] : 0.f;
+      vg[i] = (rok && own) ? gg[(int64_t)f * W] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < SW_RB; ++i) {
+      const int f = f0 + r0 + i;
+      float a = va[i];
+      if (PRO && f + 1 < H && tin) a = fmaxf(fmaf(a, sc, sh), 0.f);
+      const float al = __shfl_up(a, 1, 64), ar = __shfl_down(a, 1, 64);
+      const float g = vg[i];
+      // rows f-1 (w0), f (w1), f+1 (a)
+      acc[0] = fmaf(g, w0l, acc[0]);
+      acc[1] = fmaf(g, w0c, acc[1]);
+      acc[2] = fmaf(g, w0r, acc[2]);
+      acc[3] = fmaf(g, w1l, acc[3]);
+      acc[4] = fmaf(g, w1c, acc[4]);
+      acc[5] = fmaf(g, w1r, acc[5]);
+      acc[6] = fmaf(g, al, acc[6]);
+      acc[7] = fmaf(g, a, acc[7]);
+      acc[8] = fmaf(g, ar, acc[8]);
+      accb += g;
+      w0l = w1l; w0c = w1c; w0r = w1r;
+      w1l = al; w1c = a; w1r = ar;
+    }
+  }
+  float* out = partial + (int64_t)tile * NOUT;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    const float s = wave_sum(acc[i]);
+    if (lane == 0) out[(cg * CA + ca) * 9 + i] = s;
+  }
+  if (ca == 0) {
+    const float s = wave_sum(accb);
+    if (lane == 0) out[CG * CA * 9 + cg] = s;
+  }
+}
+
+// The same row strips with the 16-channel side channel-last (round 5): a lane
+// holds 4 consecutive channels (one 16-byte load) of one pixel, a wave 16
+// pixels (columns t0-1 .. t0+14; lanes of pixels 1..14 own outputs) x 4
+// channel quads; the column shifts are lane shifts by 4.  ACL: act(x) is the
+// 16-channel side (16 -> 1 conv, dy one plane); else dy is (1 -> 16).
+constexpr int SWC_TW = 14;         // output columns per wave
+
+template <bool ACL, bool PRO>
+__global__ __launch_bounds__(256) void conv3x3_strip_wgrad_cl(
+    const float* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const float* __restrict__ dy,
+    float* __restrict__ partial, int H, int W, int ntf, int ntt, int ntiles) {
+  constexpr int NOUT = 16 * 9 + (ACL ? 1 : 16);
+  const int lane = threadIdx.x & 63, q = lane & 3, pj = lane >> 2;
+  const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);     // one tile per wave
+  if (tile >= ntiles) return;                               // whole waves: no barrier below
+  const int tt = tile % ntt, fs = (tile / ntt) % ntf, n = tile / (ntt * ntf);
+  const int f0 = fs * SW_RS, t = tt * SWC_TW - 1 + pj;
+  const bool tin = t >= 0 && t < W;
+  const bool own = pj >= 1 && pj <= SWC_TW && tin;
+  const int64_t HW = (int64_t)H * W;
+  // the 16-channel side: element (pixel, 4q..4q+3); the 1-channel side: pixel
+  const float* vsrc = (ACL ? x : dy) + ((int64_t)n * HW + t) * 16 + 4 * q;
+  const float* ssrc = (ACL ? dy : x) + (int64_t)n * HW + t;
+  float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
+  float ssc = 1.f, ssh = 0.f;
+  if (PRO) {
+    if (ACL) {
+      sc = *reinterpret_cast<const float4*>(in_scale + 4 * q);
+      sh = *reinterpret_cast<const float4*>(in_shift + 4 * q);
+    } else {
+      ssc = in_scale[0];
+      ssh = in_shift[0];
+    }
+  }
+  // act(x) of row f (zero outside the image): 4 channels (ACL) or 1 (x 4 lanes)
+  auto load_a = [&](int f, float (&a)[4]) {
+    const bool ok = f >= 0 && f < H && tin;
+    if (ACL) {
+      float4 v = ok ? *reinterpret_cast<const float4*>(vsrc + (int64_t)f * W * 16)
+                    : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (PRO && ok) {
+        v.x = fmaxf(fmaf(v.x, sc.x, sh.x), 0.f);
+        v.y = fmaxf(fmaf(v.y, sc.y, sh.y), 0.f);
+        v.z = fmaxf(fmaf(v.z, sc.z, sh.z), 0.f);
+        v.w = fmaxf(fmaf(v.w, sc.w, sh.w), 0.f);
+      }
+      a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+    } else {
+      float v = ok ? ssrc[(int64_t)f * W] : 0.f;
+      if (PRO && ok) v = fmaxf(fmaf(v, ssc, ssh), 0.f);
+      a[0] = a[1] = a[2] = a[3] = v;
+    }
+  };
+  auto load_g = [&](int f, float (&g)[4]) {
+    const bool ok = f < H && own;
+    if (ACL) {
+      const float v = ok ? ssrc[(int64_t)f * W] : 0.f;
+      g[0] = g[1] = g[2] = g[3] = v;
+    } else {
+      const float4 v = ok ? *reinterpret_cast<const float4*>(vsrc + (int64_t)f * W * 16)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
+      g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+    }
+  };
+  float acc[9][4], accb[4];
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) acc[i][e] = 0.f;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) accb[e] = 0.f;
+  // window rows f-1 (w0) and f (w1): (left, centre, right) per channel
+  float w0l[4], w0c[4], w0r[4], w1l[4], w1c[4], w1r[4];
+  auto shift = [&](const float (&a)[4], float (&l)[4], float (&r)[4]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      l[e] = __shfl_up(a[e], 4, 64);
+      r[e] = __shfl_down(a[e], 4, 64);
+    }
+  };
+  load_a(f0 - 1, w0c);
+  shift(w0c, w0l, w0r);
+  load_a(f0, w1c);
+  shift(w1c, w1l, w1r);
+  const int rows = (H - f0) < SW_RS ? (H - f0) : SW_RS;
+  for (int r0 = 0; r0 < rows; r0 += 4) {
+    float va[4][4], vg[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int f = f0 + r0 + i;
+      const bool rok = r0 + i < rows;
+      load_a(rok ? f + 1 : H, va[i]);
+      load_g(rok ? f : H, vg[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float al[4], ar[4];
+      shift(va[i], al, ar);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float g = vg[i][e];
+        acc[0][e] = fmaf(g, w0l[e], acc[0][e]);
+        acc[1][e] = fmaf(g, w0c[e], acc[1][e]);
+        acc[2][e] = fmaf(g, w0r[e], acc[2][e]);
+        acc[3][e] = fmaf(g, w1l[e], acc[3][e]);
+        acc[4][e] = fmaf(g, w1c[e], acc[4][e]);
+        acc[5][e] = fmaf(g, w1r[e], acc[5][e]);
+        acc[6][e] = fmaf(g, al[e], acc[6][e]);
+        acc[7][e] = fmaf(g, va[i][e], acc[7][e]);
+        acc[8][e] = fmaf(g, ar[e], acc[8][e]);
+        accb[e] += g;
+        w0l[e] = w1l[e]; w0c[e] = w1c[e]; w0r[e] = w1r[e];
+        w1l[e] = al[e]; w1c[e] = va[i][e]; w1r[e] = ar[e];
+      }
+    }
+  }
+  // sum the 16 pixels of each channel quad (lanes == q mod 4), fixed order
+  auto qsum = [&](float v) {
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  };
+  float* out = partial + (int64_t)tile * NOUT;
+#pragma unroll
+  for (int i = 0; i < 9; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float s = qsum(acc[i][e]);
+      // (16 -> 1): o = ci*9 + tap; (1 -> 16): o = co*9 + tap -- channel 4q + e
+      if (pj == 0) out[(4 * q + e) * 9 + i] = s;
+    }
+  if (ACL) {
+    const float s = qsum(accb[0]);
+    if (lane == 0) out[144] = s;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float s = qsum(accb[e]);
+      if (pj == 0) out[144 + 4 * q + e] = s;
+    }
+  }
+}
+
 // dw[o] (o < COUT*CIN*9, [co][ci][tap] order) and dbias from the group sums
 __global__ void small_wgrad_final(const double* __restrict__ tmp, int ngroups, int nw, int nout,
                                   float* __restrict__ dw, float* __restrict__ dbias) {
@@ -831,54 +1108,121 @@ static bool small_pair(int a, int b) {
   return ((a == 1 || a == 2) && b == 16) || ((b == 1 || b == 2) && a == 16);
 }
 
-template <int CIN, int COUT>
-static void launch_small_fwd(bool dgrad, const float* x, const float* w, const float* bias,
-                             const float* sc, const float* sh, float* y, double* stats,
-                             int64_t N, int64_t H, int64_t W, hipStream_t s) {
+template <int CIN, int COUT, bool XL, bool YL>
+static void launch_small_fwd_l(bool dgrad, const float* x, const float* w, const float* bias,
+                               const float* sc, const float* sh, float* y, double* stats,
+                               int64_t N, int64_t H, int64_t W, hipStream_t s) {
   dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
   constexpr int PX = COUT >= 16 ? 3 : 1;
   const dim3 block(384 / PX);
   if (dgrad)
-    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, true, false, PX>), grid, block, 0, s, x, w,
-                       bias, sc, sh, y, stats, (int)H, (int)W);
+    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, true, false, PX, XL, YL>), grid, block, 0, s,
+                       x, w, bias, sc, sh, y, stats, (int)H, (int)W);
   else if (sc)
-    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, true, PX>), grid, block, 0, s, x, w,
-                       bias, sc, sh, y, stats, (int)H, (int)W);
+    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, true, PX, XL, YL>), grid, block, 0, s,
+                       x, w, bias, sc, sh, y, stats, (int)H, (int)W);
   else
-    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, false, PX>), grid, block, 0, s, x, w,
-                       bias, sc, sh, y, stats, (int)H, (int)W);
+    hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, false, PX, XL, YL>), grid, block, 0,
+                       s, x, w, bias, sc, sh, y, stats, (int)H, (int)W);
+}
+
+// lay (round 5): bit 0 = input channel-last (a 16-channel input), bit 1 =
+// output channel-last (a 16-channel output); 1-2-channel tensors are the
+// same in both layouts
+template <int CIN, int COUT>
+static void launch_small_fwd(bool dgrad, const float* x, const float* w, const float* bias,
+                             const float* sc, const float* sh, float* y, double* stats,
+                             int64_t N, int64_t H, int64_t W, hipStream_t s, int lay = 0) {
+  const bool xl = (lay & 1) && CIN >= 16, yl = (lay & 2) && COUT >= 16;
+  if (xl) launch_small_fwd_l<CIN, COUT, true, false>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s);
+  else if (yl) launch_small_fwd_l<CIN, COUT, false, true>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s);
+  else launch_small_fwd_l<CIN, COUT, false, false>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s);
 }
 
 static int small_fwd_dispatch(bool dgrad, const float* x, const float* w, const float* bias,
                               const float* sc, const float* sh, float* y, double* stats,
-                              int64_t N, int Cin, int Cout, int64_t H, int64_t W, hipStream_t s) {
+                              int64_t N, int Cin, int Cout, int64_t H, int64_t W, hipStream_t s,
+                              int lay = 0) {
 #define AINP_SF(A, B) \
-  if (Cin == A && Cout == B) { launch_small_fwd<A, B>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s); return check_launch("conv3x3_small_fwd"); }
+  if (Cin == A && Cout == B) { launch_small_fwd<A, B>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, lay); return check_launch("conv3x3_small_fwd"); }
   AINP_SF(1, 16) AINP_SF(2, 16) AINP_SF(16, 1) AINP_SF(16, 2)
 #undef AINP_SF
   return record_msg("conv3x3: no small-channel kernel for this pair");
 }
 
+// AINP_SMALL_WGRAD_TILE=1: the 8x48-tile kernel for every small pair (A/B)
+static bool small_wgrad_tile_env() {
+  const char* e = getenv("AINP_SMALL_WGRAD_TILE");
+  return e && e[0] == '1';
+}
+
+static int64_t strip_tiles(int64_t N, int64_t H, int64_t W) {
+  return N * cdiv(H, SW_RS) * cdiv(W, SW_TW);
+}
+
 static size_t small_wgrad_ws(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
-  const int64_t nblk = N * cdiv(H, CV_FT) * cdiv(W, CV_TT);
+  int64_t nblk = N * cdiv(H, CV_FT) * cdiv(W, CV_TT);
+  const int64_t ns = strip_tiles(N, H, W), nc = N * cdiv(H, SW_RS) * cdiv(W, SWC_TW);
+  if (ns > nblk) nblk = ns;
+  if (nc > nblk) nblk = nc;
   const int nout = Cout * Cin * 9 + Cout;
   return (size_t)nblk * nout * sizeof(float) + (size_t)WG_GROUPS * nout * sizeof(double) + 16;
 }
 
+static int64_t strip_cl_tiles(int64_t N, int64_t H, int64_t W) {
+  return N * cdiv(H, SW_RS) * cdiv(W, SWC_TW);
+}
+
+// lay (round 5): bit 0 = x channel-last (its 16 channels: the 16 -> 1 conv),
+// bit 2 = dy channel-last (the 1 -> 16 conv); 1-channel tensors are the same
+// in both layouts
 static int small_wgrad(const float* x, const float* sc, const float* sh, const float* dy,
                        float* dw, float* dbias, void* workspace, int64_t N, int Cin, int Cout,
-                       int64_t H, int64_t W, hipStream_t s) {
-  dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
-  const int64_t nblk = (int64_t)grid.x * grid.y * grid.z;
+                       int64_t H, int64_t W, hipStream_t s, int lay = 0) {
   const int nout = Cout * Cin * 9 + Cout;
   float* partial = reinterpret_cast<float*>(workspace);
+  int64_t nblk;
+  const bool acl = (lay & 1) && Cin == 16, gcl = (lay & 4) && Cout == 16;
+  if ((acl && Cout == 1) || (gcl && Cin == 1)) {
+    const int ntf = (int)cdiv(H, SW_RS), ntt = (int)cdiv(W, SWC_TW);
+    nblk = strip_cl_tiles(N, H, W);
+    const dim3 grid((unsigned)cdiv(nblk, 4));
+    if (acl && sc)
+      hipLaunchKernelGGL((conv3x3_strip_wgrad_cl<true, true>), grid, dim3(256), 0, s, x, sc, sh,
+                         dy, partial, (int)H, (int)W, ntf, ntt, (int)nblk);
+    else if (acl)
+      hipLaunchKernelGGL((conv3x3_strip_wgrad_cl<true, false>), grid, dim3(256), 0, s, x, sc, sh,
+                         dy, partial, (int)H, (int)W, ntf, ntt, (int)nblk);
+    else if (sc)
+      hipLaunchKernelGGL((conv3x3_strip_wgrad_cl<false, true>), grid, dim3(256), 0, s, x, sc, sh,
+                         dy, partial, (int)H, (int)W, ntf, ntt, (int)nblk);
+    else
+      hipLaunchKernelGGL((conv3x3_strip_wgrad_cl<false, false>), grid, dim3(256), 0, s, x, sc, sh,
+                         dy, partial, (int)H, (int)W, ntf, ntt, (int)nblk);
+  } else if (acl || gcl) {
+    return record_msg("conv3x3_wgrad: no channel-last small-channel kernel for this pair");
+  } else if (!small_wgrad_tile_env() && H * W < ((int64_t)1 << 31)) {
+    const int ntf = (int)cdiv(H, SW_RS), ntt = (int)cdiv(W, SW_TW);
+    nblk = strip_tiles(N, H, W);
+    const dim3 grid((unsigned)nblk, (unsigned)cdiv(Cin * Cout, 4));
+#define AINP_SW(A, B) \
+  else if (Cin == A && Cout == B && sc) hipLaunchKernelGGL((conv3x3_strip_wgrad<A, B, true>), grid, dim3(256), 0, s, x, sc, sh, dy, partial, (int)H, (int)W, ntf, ntt); \
+  else if (Cin == A && Cout == B) hipLaunchKernelGGL((conv3x3_strip_wgrad<A, B, false>), grid, dim3(256), 0, s, x, sc, sh, dy, partial, (int)H, (int)W, ntf, ntt);
+    if (false) {}
+    AINP_SW(1, 16) AINP_SW(2, 16) AINP_SW(16, 1) AINP_SW(16, 2)
+    else return record_msg("conv3x3_wgrad: no small-channel kernel for this pair");
+#undef AINP_SW
+  } else {
+    dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
+    nblk = (int64_t)grid.x * grid.y * grid.z;
 #define AINP_SW(A, B) \
   else if (Cin == A && Cout == B && sc) hipLaunchKernelGGL((conv3x3_small_wgrad<A, B, true>), grid, dim3(256), 0, s, x, sc, sh, dy, partial, (int)H, (int)W); \
   else if (Cin == A && Cout == B) hipLaunchKernelGGL((conv3x3_small_wgrad<A, B, false>), grid, dim3(256), 0, s, x, sc, sh, dy, partial, (int)H, (int)W);
-  if (false) {}
-  AINP_SW(1, 16) AINP_SW(2, 16) AINP_SW(16, 1) AINP_SW(16, 2)
-  else return record_msg("conv3x3_wgrad: no small-channel kernel for this pair");
+    if (false) {}
+    AINP_SW(1, 16) AINP_SW(2, 16) AINP_SW(16, 1) AINP_SW(16, 2)
+    else return record_msg("conv3x3_wgrad: no small-channel kernel for this pair");
 #undef AINP_SW
+  }
   int rc = check_launch("conv3x3_small_wgrad");
   if (rc) return rc;
   uintptr_t tp = reinterpret_cast<uintptr_t>(partial + nblk * nout);
@@ -915,11 +1259,12 @@ bool conv_x6_dgrad16_ok(int Cin, int Cout, int64_t H, int64_t W);
 bool conv_x6_fwd16_ok(int Cin, int Cout, int64_t H, int64_t W);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16);
+                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16,
+                         int lay);
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                   bool x16, bool y16);
+                   bool x16, bool y16, int lay);
 
 // conv_x6.hip (fp32-accurate split-bf16 MFMA) serves every pair it has an
 // instantiation for unless AINP_CONV_EXACT=1 selects the exact f32 kernels.
@@ -965,7 +1310,7 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y,
                              double* stats, int64_t N, int Cin, int Cout,
                              int64_t H, int64_t W, hipStream_t s, bool b16, bool x16 = false,
-                             bool y16 = false) {
+                             bool y16 = false, int lay = 0) {
   // partials [used, rows) of the BatchNorm statistics are zero
   auto zero_tail = [&](int64_t used) -> int {
     if (!stats) return AINP_OK;
@@ -980,17 +1325,20 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
       "conv3x3: bf16 storage (AINP_CONV_DY16 / _X16 / _Y16) needs a split-bf16 kernel for this pair";
   if (small_pair(Cin, Cout)) {
     if (x16 || y16) return record_msg(kNo16);
-    const int rc = small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s);
+    const int rc = small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
+                                      lay);
     return rc ? rc : zero_tail(exact_stat_parts(N, H, W));
   }
   if (!conv_exact_env()) {
     int64_t parts = 0;
     const int rc = conv_x6_launch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                  &parts, b16, x16, y16);
-    if (rc == 2) return record_msg(kNo16);
+                                  &parts, b16, x16, y16, lay);
+    if (rc == 2) return record_msg(lay ? "conv3x3: no channel-last / bf16-storage kernel for this pair"
+                                       : kNo16);
     if (rc != 1) return rc ? rc : zero_tail(parts);
   }
   if (x16 || y16) return record_msg(kNo16);
+  if (lay) return record_msg("conv3x3: channel-last activations need a split-bf16 kernel for this pair");
   {
     const int rc = zero_tail(exact_stat_parts(N, H, W));
     if (rc) return rc;
@@ -1020,16 +1368,28 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
 }
 
 static bool conv_flags_ok(int flags) { return (flags & ~AINP_CONV_BF16) == 0; }
-// forward: the act(x) source and / or y in bf16 storage (with the bf16 arithmetic)
+// forward: the act(x) source and / or y in bf16 storage (with the bf16 arithmetic);
+// either may be channel-last
 static bool conv_fwd_flags_ok(int flags) {
+  const int cl = flags & (AINP_CONV_XCL | AINP_CONV_YCL);
+  flags &= ~cl;
   return (flags & ~(AINP_CONV_BF16 | AINP_CONV_X16 | AINP_CONV_Y16)) == 0 &&
          (!(flags & (AINP_CONV_X16 | AINP_CONV_Y16)) || (flags & AINP_CONV_BF16));
 }
-// data / weight gradients: dy may be bf16 storage (with the bf16 arithmetic)
+// data / weight gradients: dy may be bf16 storage (with the bf16 arithmetic);
+// data gradient: dy / dx channel-last; weight gradient: x / dy channel-last
 static bool conv_grad_flags_ok(int flags, bool wgrad) {
+  const int cl = flags & (wgrad ? (AINP_CONV_XCL | AINP_CONV_GCL) : (AINP_CONV_XCL | AINP_CONV_YCL));
+  flags &= ~cl;
   const int extra = AINP_CONV_DY16 | (wgrad ? AINP_CONV_X16 : 0);
   return (flags & ~(AINP_CONV_BF16 | extra)) == 0 &&
          (!(flags & extra) || (flags & AINP_CONV_BF16));
+}
+// ABI layout flags -> the kernels' layout bits (bit 0 input, bit 1 output,
+// bit 2 the weight gradient's dy)
+static int conv_lay(int flags) {
+  return ((flags & AINP_CONV_XCL) ? 1 : 0) | ((flags & AINP_CONV_YCL) ? 2 : 0) |
+         ((flags & AINP_CONV_GCL) ? 4 : 0);
 }
 
 extern "C" int ainp_conv3x3_fwd_ex(const float* x, const float* w,
@@ -1046,7 +1406,7 @@ extern "C" int ainp_conv3x3_fwd_ex(const float* x, const float* w,
   return conv_fwd_dispatch<false>(x, w, bias, in_scale, in_shift, y, stats, N,
                                   Cin, Cout, H, W, as_stream(stream),
                                   (flags & AINP_CONV_BF16) != 0, (flags & AINP_CONV_X16) != 0,
-                                  (flags & AINP_CONV_Y16) != 0);
+                                  (flags & AINP_CONV_Y16) != 0, conv_lay(flags));
 }
 
 extern "C" int ainp_conv3x3_fwd(const float* x, const float* w,
@@ -1070,7 +1430,8 @@ extern "C" int ainp_conv3x3_dgrad_ex(const float* dy, const float* w, float* dx,
   // conv over dy (Cout channels) producing Cin channels, flipped weights
   return conv_fwd_dispatch<true>(dy, w, nullptr, nullptr, nullptr, dx, nullptr,
                                  N, Cout, Cin, H, W, as_stream(stream),
-                                 (flags & AINP_CONV_BF16) != 0, (flags & AINP_CONV_DY16) != 0);
+                                 (flags & AINP_CONV_BF16) != 0, (flags & AINP_CONV_DY16) != 0,
+                                 false, conv_lay(flags));
 }
 
 extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
@@ -1106,6 +1467,23 @@ extern "C" int ainp_conv3x3_io16_ok(int64_t N, int Cin, int Cout, int64_t H, int
       !((cp == 32 && Cout == 16) || (cp == 16 && Cout == 32) || (cp == 32 && Cout == 64)))
     return 0;
   return conv_x6_fwd16_ok(Cin, Cout, H, W) ? 1 : 0;
+}
+
+// Round 5: 1 if every conv3x3 entry point of this nn.Conv2d(Cin, Cout) takes
+// channel-last activations (AINP_CONV_XCL / _YCL / _GCL; host-only)
+extern "C" int ainp_conv3x3_cl_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+  (void)N;
+  if (Cin < 1 || Cout < 1 || H < 1 || W < 1 || conv_exact_env()) return 0;
+  const int64_t cmax = Cin > Cout ? Cin : Cout;
+  if (H * W * cmax * 4 >= ((int64_t)1 << 31)) return 0;
+  if (small_pair(Cin, Cout)) return (Cin == 16 && Cout == 1) || (Cin == 1 && Cout == 16);
+  // forward (persistent x6p / x6q), data gradient (x6p / x6q / 8-row tiled),
+  // weight gradient (one 32-channel pass on wgrad_x6 / x6s)
+  const bool fwd = (Cin == 16 && Cout == 32) || (Cin == 32 && Cout == 64) ||
+                   (Cin == 32 && Cout == 16);
+  const bool dgr = (Cout == 32 && Cin == 16) || (Cout == 16 && Cin == 32) ||
+                   (Cout == 64 && Cin == 32);
+  return fwd && dgr ? 1 : 0;
 }
 
 extern "C" size_t ainp_conv3x3_wgrad_workspace(int64_t N, int Cin, int Cout,
@@ -1144,10 +1522,11 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
       "weight-gradient kernel for this pair";
   if ((in_scale == nullptr) != (in_shift == nullptr))
     return record_msg("ainp_conv3x3_wgrad: in_scale/in_shift must both be set");
+  const int lay = conv_lay(flags);
   if (small_pair(Cin, Cout)) {
     if (g16 || x16) return record_msg(kNo16);
     return small_wgrad(x, in_scale, in_shift, dy, dw, dbias, workspace, N, Cin, Cout, H, W,
-                       as_stream(stream));
+                       as_stream(stream), lay);
   }
   const int CT = wgrad_ct(Cout);
   if (CT > 4) return record_msg("ainp_conv3x3_wgrad: Cout > 64 unsupported");
@@ -1182,9 +1561,11 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
     const int nblk_x6 = b16 ? WG_BLOCKS * conv_x6_occ16() : WG_BLOCKS;
     int rc = (fits && !conv_exact_env())
                  ? conv_wgrad_x6_launch(x, in_scale, in_shift, dy, partial, N, Cin, Cout, H, W,
-                                        ci0, cp, nblk_x6, s, b16, g16, x16)
+                                        ci0, cp, nblk_x6, s, b16, g16, x16, lay)
                  : 1;
     if (rc == 1 && (g16 || x16)) return record_msg(kNo16);
+    if (rc == 1 && lay)
+      return record_msg("ainp_conv3x3_wgrad: channel-last activations need a split-bf16 kernel");
     const int nblk = rc == 0 ? nblk_x6 : WG_BLOCKS;   // slabs the launch writes
     if (rc == 1) switch (key) {
       case 1616: AINP_WGT(16, 16); break;

@@ -27,6 +27,7 @@
 // dgrad is the same kernel over dy with w'[ci][co][tap] = w[co][ci][8 - tap].
 #include "common.h"
 #include <stdlib.h>
+#include <type_traits>
 
 namespace ainp {
 
@@ -43,6 +44,9 @@ constexpr int XI = (XU + NT - 1) / NT;   // units per thread (3)
 }  // namespace cx6
 
 typedef __bf16 bf16x8c __attribute__((ext_vector_type(8)));
+
+// activation layouts of a launch (bitmask): input / output / dy channel-last
+constexpr int CL_X = 1, CL_Y = 2, CL_G = 4;
 
 __device__ __forceinline__ int wx6_clamp(int v, int lo, int hi) {
   return v < lo ? lo : (v > hi ? hi : v);
@@ -87,6 +91,43 @@ __device__ __forceinline__ uint32_t cx6_cvt_pk(float lo, float hi) {
   uint32_t r;
   asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
   return r;
+}
+
+// Channel-last activations (round 5): [N][H][W][C], a pixel's channels
+// contiguous.  8 consecutive channels are one 16-byte (bf16 storage) or two
+// 16-byte (fp32) buffer loads at byte offset voff -- the staging units of
+// the kernels below are (pixel, 8-channel group), so a unit is one or two
+// vector loads instead of 8 plane-strided scalar ones, and consecutive lanes
+// read consecutive bytes.
+template <bool G16>
+__device__ __forceinline__ void cl_ld8(__amdgpu_buffer_rsrc_t r, int voff, float (&v)[8]) {
+  if constexpr (G16) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[2 * j] = __uint_as_float(q[j] << 16);
+      v[2 * j + 1] = __uint_as_float(q[j] & 0xffff0000u);
+    }
+  } else {
+    const auto a = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+    const auto b = __builtin_amdgcn_raw_buffer_load_b128(r, voff + 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = __uint_as_float(a[j]);
+      v[4 + j] = __uint_as_float(b[j]);
+    }
+  }
+}
+// 4 consecutive channels of one channel-last pixel: fp32 (16 B) or bf16
+// (8 B, round-to-nearest-even; exact for values already rounded by y16_round)
+template <bool Y16>
+__device__ __forceinline__ void cl_st4(float* y, int64_t e, float a, float b, float c, float d) {
+  if constexpr (Y16) {
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(y) + e) =
+        make_uint2(cx6_cvt_pk(a, b), cx6_cvt_pk(c, d));
+  } else {
+    *reinterpret_cast<float4*>(y + e) = make_float4(a, b, c, d);
+  }
 }
 
 // split 8 floats into three packed bf16 vectors (8 x bf16 each), exactly
@@ -138,7 +179,8 @@ __device__ __forceinline__ bf16x8c cx6_ld(const unsigned char* p) {
 
 // RPW output rows per wave: 2 (16-row tiles, one workgroup per CU) or 1
 // (8-row tiles: half the halo LDS, two workgroups per CU).
-template <int CI, int COP, bool DGRAD, int RPW, int NP, bool G16 = false>
+template <int CI, int COP, bool DGRAD, int RPW, int NP, bool G16 = false, bool XL = false,
+          bool YL = false>
 __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -167,20 +209,46 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
   constexpr int ES = act_es<G16>();
 
   float px[XI][8];
+  // staging unit -> (halo column, halo row, channel half); channel-last (XL):
+  // the two lanes of a pixel read its chunk's channels as contiguous bytes
+  auto unit = [&](int u, int& col, int& row, int& half) {
+    if constexpr (XL) {
+      half = u & 1;
+      const int hp = u >> 1;
+      col = hp % HC;
+      row = hp / HC;
+    } else {
+      col = u % HC;
+      row = (u / HC) % HR;
+      half = u / (HR * HC);
+    }
+  };
   // clamped-address buffer loads (selected to zero at commit); valid while a
   // sample's CI planes span < 2^31 bytes (the launcher checks)
   auto fetch = [&](int ci0) {
-    int plane = (int)(HW * ES);
-    asm volatile("" : "+s"(plane));
-    const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ci0) * HW);
+    if constexpr (XL) {
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, (int64_t)n * HW * CI + ci0);
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = tid + NT * i;
-      const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
-      const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
-      const int vo = 8 * half * plane + (gr * W + gc) * ES;
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        int col, row, half;
+        unit(u < XU ? u : XU - 1, col, row, half);
+        const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+        cl_ld8<G16>(rx, ((gr * W + gc) * CI + 8 * half) * ES, px[i]);
+      }
+    } else {
+      int plane = (int)(HW * ES);
+      asm volatile("" : "+s"(plane));
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ci0) * HW);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
+        const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+        const int vo = 8 * half * plane + (gr * W + gc) * ES;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
+      }
     }
   };
   auto commit = [&](int ci0) {
@@ -188,7 +256,8 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       if (u < XU) {
-        const int col = u % HC, row = (u / HC) % HR, half = u / (HR * HC);
+        int col, row, half;
+        unit(u, col, row, half);
         const int gr = r0 - 1 + row, gc = c0 - 1 + col;
         const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
         float v[8];
@@ -273,6 +342,26 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
   // set), then over the 8 waves in fixed order
   float* yn = y + (int64_t)n * Cout * HW;
   const int col = c0 + li;
+  if constexpr (YL) {   // channel-last: 4 consecutive channels per store (Cout % 4 == 0)
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < RPW; ++j) {
+        const int row = r0 + RPW * wave + j;
+        if (row < H && col < W) {
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            const int co0 = 32 * i + 8 * rb + 4 * lh;
+            if (co0 < Cout) {
+              float v[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) v[e] = acc[i][j][4 * rb + e] + (bias ? bias[co0 + e] : 0.f);
+              cl_st4<false>(yn, ((int64_t)row * W + col) * Cout + co0, v[0], v[1], v[2], v[3]);
+            }
+          }
+        }
+      }
+  }
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -286,7 +375,7 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
         const int row = r0 + RPW * wave + j;
         if (cok && row < H && col < W) {
           const float v = acc[i][j][r] + bv;
-          yn[(int64_t)co * HW + (int64_t)row * W + col] = v;
+          if constexpr (!YL) yn[(int64_t)co * HW + (int64_t)row * W + col] = v;
           s += v;
           q += v * v;
         }
@@ -329,7 +418,7 @@ int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W) {
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                    bool x16, bool y16);
+                    bool x16, bool y16, int lay);
 
 // Persistent-grid multiplier of the bf16 (NP = 1) kernels: their LDS (21-50
 // KB) and VGPR (48-80) footprints let 2-4x the fp32 kernels' workgroups stay
@@ -393,19 +482,31 @@ bool conv_x6_fwd16_ok(int Cin, int Cout, int64_t H, int64_t W) {
   return (Cin == 32 && cop == 64) || (Cin == 16 && cop == 32) || (Cin == 32 && Cout == 16);
 }
 
+// Instantiate f for the run-time layout bits: f(xl, yl) with integral-constant
+// booleans (input / output channel-last)
+template <typename F>
+static void cl_dispatch(int lay, F&& f) {
+  if ((lay & CL_X) && (lay & CL_Y)) f(std::true_type{}, std::true_type{});
+  else if (lay & CL_X) f(std::true_type{}, std::false_type{});
+  else if (lay & CL_Y) f(std::false_type{}, std::true_type{});
+  else f(std::false_type{}, std::false_type{});
+}
+
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                   bool x16, bool y16) {
+                   bool x16, bool y16, int lay) {
   if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W, b16) == 0) return 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                   parts, b16, x16, y16);
+                                   parts, b16, x16, y16, lay);
     if (rc != 1) return rc;
   }
   if ((int64_t)Cin * H * W * 4 >= ((int64_t)1 << 31)) return 1;   // 32-bit buffer offsets
   if (y16 || (x16 && !(dgrad && !stats && b16))) return 2;   // bf16 storage: no such kernel
+  // channel-last: only the stat-free data gradient (8-row tiles) has it
+  if (lay && !(dgrad && !stats)) return 2;
   *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
@@ -413,12 +514,17 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
   if (Cin == CIV && cop == COV) {                                                               \
     if (dgrad && !stats) {   /* 8-row tiles, two workgroups per CU (no BN partials) */           \
       const dim3 g8((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, 8), (unsigned)N);             \
-      if (NPV == 1 && x16)                                                                      \
-        hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV, true>), g8, dim3(cx6::NT), \
-                           0, s, x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);           \
-      else                                                                                      \
-        hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV>), g8, dim3(cx6::NT), 0, s, \
-                           x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                 \
+      cl_dispatch(lay, [&](auto xl, auto yl) {                                                  \
+        constexpr bool XL = decltype(xl)::value, YL = decltype(yl)::value;                      \
+        if (NPV == 1 && x16)                                                                    \
+          hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV, true, XL, YL>), g8,     \
+                             dim3(cx6::NT), 0, s, x, w, bias, sc, sh, y, stats, Cout, (int)H,   \
+                             (int)W);                                                           \
+        else                                                                                    \
+          hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV, false, XL, YL>), g8,    \
+                             dim3(cx6::NT), 0, s, x, w, bias, sc, sh, y, stats, Cout, (int)H,   \
+                             (int)W);                                                           \
+      });                                                                                       \
     } else if (dgrad)                                                                           \
       hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 2, NPV>), grid, dim3(cx6::NT), 0, s, \
                          x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                   \
@@ -487,7 +593,10 @@ __device__ __forceinline__ int wx6_gswz(int px) {
   return (((px >> 1) & 1) << 2) | (((px >> 2) & 1) << 1) | (px & 1);
 }
 
-template <int CO, int NP, bool G16 = false, bool XG16 = false>
+// XL / GL (round 5): act(x)'s source / dy channel-last ([N][H][W][C]): a unit
+// (pixel, 8-channel group) is one or two vector loads, consecutive lanes on
+// consecutive groups of a pixel.
+template <int CO, int NP, bool G16 = false, bool XG16 = false, bool XL = false, bool GL = false>
 __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -550,8 +659,28 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     f0 = (int)((tile / tiles_t) % tiles_f) * FT;
     n = (int)(tile / ((int64_t)tiles_t * tiles_f));
   };
-  // the staging pixel of dy units (the same for all of a thread's units)
-  const int gpx = tid % NPX;
+  // dy unit i of this thread: staging pixel and 8-channel group (NCHW: one
+  // pixel for all of a thread's units; channel-last: consecutive groups)
+  auto gunit = [&](int i, int& px_, int& grp_) {
+    const int gu = tid + NT * i;
+    if constexpr (GL) {
+      px_ = gu / NG;
+      grp_ = gu % NG;
+    } else {
+      px_ = tid % NPX;
+      grp_ = gu / NPX;
+    }
+  };
+  // x unit -> (halo pixel, 8-channel group)
+  auto xunit = [&](int u, int& hp_, int& grp_) {
+    if constexpr (XL) {
+      hp_ = u >> 2;
+      grp_ = u & 3;
+    } else {
+      hp_ = u % (HR * HC);
+      grp_ = u / (HR * HC);
+    }
+  };
 
   float px[XI][8], pg[GI][8];
   auto fetch = [&](int64_t tile) {
@@ -559,31 +688,56 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     tile_coords(tile, n, f0, t0);
     // act(x) input: fp32 or bf16 storage (XG16)
     constexpr int XES = act_es<XG16>();
-    int plane = (int)(HW * XES);
-    asm volatile("" : "+s"(plane));  // keep c * plane out of the tile loop
-    const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, ((int64_t)n * Cin + ci0) * HW);
+    if constexpr (XL) {
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, (int64_t)n * HW * Cin + ci0);
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = tid + NT * i;
-      const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : 3;
-      const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
-      const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
-      const int vo = 8 * grp * plane + (gr * W + gc) * XES;
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        int hp, grp;
+        xunit(u < XU ? u : XU - 1, hp, grp);
+        const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
+        const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
+        cl_ld8<XG16>(rx, ((gr * W + gc) * Cin + 8 * grp) * XES, px[i]);
+      }
+    } else {
+      int plane = (int)(HW * XES);
+      asm volatile("" : "+s"(plane));  // keep c * plane out of the tile loop
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, ((int64_t)n * Cin + ci0) * HW);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<XG16>(rx, vo, c * plane);
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : 3;
+        const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
+        const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
+        const int vo = 8 * grp * plane + (gr * W + gc) * XES;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) px[i][c] = act_ld<XG16>(rx, vo, c * plane);
+      }
     }
     // dy: fp32 or bf16 storage (G16)
     constexpr int GES = act_es<G16>();
-    int gplane = (int)(HW * GES);
-    asm volatile("" : "+s"(gplane));
-    const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * CO * HW);
-    const int gr = wx6_clamp(f0 + gpx / TT, 0, H - 1), gc = wx6_clamp(t0 + gpx % TT, 0, W - 1);
+    if constexpr (GL) {
+      const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * HW * CO);
 #pragma unroll
-    for (int i = 0; i < GI; ++i) {
-      const int grp = (tid + NT * i) / NPX;
-      const int vo = 8 * grp * gplane + (gr * W + gc) * GES;
+      for (int i = 0; i < GI; ++i) {
+        int gp, grp;
+        gunit(i, gp, grp);
+        const int gr = wx6_clamp(f0 + gp / TT, 0, H - 1), gc = wx6_clamp(t0 + gp % TT, 0, W - 1);
+        cl_ld8<G16>(rg, ((gr * W + gc) * CO + 8 * grp) * GES, pg[i]);
+      }
+    } else {
+      int gplane = (int)(HW * GES);
+      asm volatile("" : "+s"(gplane));
+      const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * CO * HW);
+      const int gpx = tid % NPX;
+      const int gr = wx6_clamp(f0 + gpx / TT, 0, H - 1), gc = wx6_clamp(t0 + gpx % TT, 0, W - 1);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) pg[i][c] = act_ld<G16>(rg, vo, c * gplane);
+      for (int i = 0; i < GI; ++i) {
+        const int grp = (tid + NT * i) / NPX;
+        const int vo = 8 * grp * gplane + (gr * W + gc) * GES;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) pg[i][c] = act_ld<G16>(rg, vo, c * gplane);
+      }
     }
   };
   auto commit = [&](int64_t tile) {
@@ -593,7 +747,8 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       if (u < XU) {
-        const int hp = u % (HR * HC), grp = u / (HR * HC);
+        int hp, grp;
+        xunit(u, hp, grp);
         const int hr = hp / HC, hc = hp % HC;
         const int gr = f0 - 1 + hr, gc = t0 - 1 + hc;
         const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
@@ -608,10 +763,11 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
         cx6_stage<NP>(v, sx + sp * 64 + 16 * (grp ^ ((sp >> 1) & 3)), XPL);
       }
     }
-    const bool pok = f0 + gpx / TT < H && t0 + gpx % TT < W;
 #pragma unroll
     for (int i = 0; i < GI; ++i) {
-      const int grp = (tid + NT * i) / NPX;
+      int gpx, grp;
+      gunit(i, gpx, grp);
+      const bool pok = f0 + gpx / TT < H && t0 + gpx % TT < W;
       float v[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
@@ -671,7 +827,8 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
   float* red = reinterpret_cast<float*>(sx);
 #pragma unroll
   for (int i = 0; i < GI; ++i) {
-    const int grp = (tid + NT * i) / NPX;
+    int gpx, grp;
+    gunit(i, gpx, grp);
 #pragma unroll
     for (int c = 0; c < 8; ++c) red[(8 * grp + c) * NPX + gpx] = bsum[i][c];
   }
@@ -706,7 +863,8 @@ __device__ __forceinline__ int wx6s_swz(int px) {
   return ((px >> 1) & 1) | ((((px >> 2) ^ (px >> 3)) & 1) << 1);
 }
 
-template <int CP, int CO, int NP, bool G16 = false, bool XG16 = false>
+template <int CP, int CO, int NP, bool G16 = false, bool XG16 = false, bool XL = false,
+          bool GL = false>
 __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
@@ -754,7 +912,18 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     f0 = (int)((tile / tiles_t) % tiles_f) * FT;
     n = (int)(tile / ((int64_t)tiles_t * tiles_f));
   };
-  const int gpx = tid % NPX, ggrp = tid / NPX;   // this thread's dy unit (if tid < GU)
+  // this thread's dy unit (if tid < GU): pixel and 8-channel group; the
+  // channel-last order puts a pixel's groups on consecutive lanes
+  const int gpx = GL ? tid / GG : tid % NPX, ggrp = GL ? tid % GG : tid / NPX;
+  auto xunit = [&](int u, int& hp_, int& grp_) {
+    if constexpr (XL) {
+      hp_ = u / XG;
+      grp_ = u % XG;
+    } else {
+      hp_ = u % (HR * HC);
+      grp_ = u / (HR * HC);
+    }
+  };
 
   float px[XI][8], pg[8];
   auto fetch = [&](int64_t tile) {
@@ -762,28 +931,47 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     tile_coords(tile, n, f0, t0);
     // act(x) input: fp32 or bf16 storage (XG16)
     constexpr int XES = act_es<XG16>();
-    int plane = (int)(HW * XES);
-    asm volatile("" : "+s"(plane));
-    const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, ((int64_t)n * Cin + ci0) * HW);
+    if constexpr (XL) {
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, (int64_t)n * HW * Cin + ci0);
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = tid + NT * i;
-      const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : XG - 1;
-      const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
-      const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
-      const int vo = 8 * grp * plane + (gr * W + gc) * XES;
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        int hp, grp;
+        xunit(u < XU ? u : XU - 1, hp, grp);
+        const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
+        const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
+        cl_ld8<XG16>(rx, ((gr * W + gc) * Cin + 8 * grp) * XES, px[i]);
+      }
+    } else {
+      int plane = (int)(HW * XES);
+      asm volatile("" : "+s"(plane));
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<XG16>(x, ((int64_t)n * Cin + ci0) * HW);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<XG16>(rx, vo, c * plane);
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        const int hp = u % (HR * HC), grp = u < XU ? u / (HR * HC) : XG - 1;
+        const int gr = wx6_clamp(f0 - 1 + hp / HC, 0, H - 1);
+        const int gc = wx6_clamp(t0 - 1 + hp % HC, 0, W - 1);
+        const int vo = 8 * grp * plane + (gr * W + gc) * XES;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) px[i][c] = act_ld<XG16>(rx, vo, c * plane);
+      }
     }
     // dy: fp32 or bf16 storage (G16)
     constexpr int GES = act_es<G16>();
-    int gplane = (int)(HW * GES);
-    asm volatile("" : "+s"(gplane));
-    const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * CO * HW);
-    const int gr = wx6_clamp(f0 + gpx / TT, 0, H - 1), gc = wx6_clamp(t0 + gpx % TT, 0, W - 1);
-    const int vo = 8 * (ggrp < GG ? ggrp : GG - 1) * gplane + (gr * W + gc) * GES;
+    const int gpc = gpx < NPX ? gpx : NPX - 1;
+    const int gr = wx6_clamp(f0 + gpc / TT, 0, H - 1), gc = wx6_clamp(t0 + gpc % TT, 0, W - 1);
+    if constexpr (GL) {
+      const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * HW * CO);
+      cl_ld8<G16>(rg, ((gr * W + gc) * CO + 8 * (ggrp < GG ? ggrp : GG - 1)) * GES, pg);
+    } else {
+      int gplane = (int)(HW * GES);
+      asm volatile("" : "+s"(gplane));
+      const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * CO * HW);
+      const int vo = 8 * (ggrp < GG ? ggrp : GG - 1) * gplane + (gr * W + gc) * GES;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) pg[c] = act_ld<G16>(rg, vo, c * gplane);
+      for (int c = 0; c < 8; ++c) pg[c] = act_ld<G16>(rg, vo, c * gplane);
+    }
   };
   auto commit = [&](int64_t tile) {
     int n, f0, t0;
@@ -792,7 +980,8 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       if (u < XU) {
-        const int hp = u % (HR * HC), grp = u / (HR * HC);
+        int hp, grp;
+        xunit(u, hp, grp);
         const int hr = hp / HC, hc = hp % HC;
         const int gr = f0 - 1 + hr, gc = t0 - 1 + hc;
         const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
@@ -901,7 +1090,11 @@ constexpr int XROW = HC * 32;            // halo row bytes per plane (16 bf16 pe
 constexpr int WROW = 9 * 32 + 16;        // weight row bytes per chunk and plane
 }  // namespace cxp
 
-template <int CI, int COP, bool DGRAD, int NT, int TR, int NP, bool G16 = false, bool Y16 = false>
+// XL / YL (round 5): input / output channel-last ([N][H][W][C]) instead of
+// NCHW.  A channel-last staging unit u is (pixel u >> 1, 8-channel half u & 1):
+// the two lanes of a pixel read its chunk's 16 channels as contiguous bytes.
+template <int CI, int COP, bool DGRAD, int NT, int TR, int NP, bool G16 = false, bool Y16 = false,
+          bool XL = false, bool YL = false>
 __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -953,21 +1146,46 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
   };
 
   float px[XI][8];
+  // staging unit -> (halo column, halo row, channel half)
+  auto unit = [&](int u, int& col, int& row, int& half) {
+    if constexpr (XL) {
+      half = u & 1;
+      const int hp = u >> 1;
+      col = hp % HC;
+      row = hp / HC;
+    } else {
+      col = u % HC;
+      row = (u / HC) % HR;
+      half = u / (HR * HC);
+    }
+  };
   auto fetch = [&](int64_t tile, int ch) {
     int n, r0, c0;
     tile_coords(tile, n, r0, c0);
     constexpr int ES = act_es<G16>();
-    int plane = (int)(HW * ES);
-    asm volatile("" : "+s"(plane));  // keep c * plane out of the loop
-    const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ch * CK) * HW);
+    if constexpr (XL) {
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, (int64_t)n * HW * CI + ch * CK);
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = tid + NT * i;
-      const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
-      const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
-      const int vo = 8 * half * plane + (gr * W + gc) * ES;
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        int col, row, half;
+        unit(u < XU ? u : XU - 1, col, row, half);
+        const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+        cl_ld8<G16>(rx, ((gr * W + gc) * CI + 8 * half) * ES, px[i]);
+      }
+    } else {
+      int plane = (int)(HW * ES);
+      asm volatile("" : "+s"(plane));  // keep c * plane out of the loop
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ch * CK) * HW);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
+        const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+        const int vo = 8 * half * plane + (gr * W + gc) * ES;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
+      }
     }
   };
   auto commit = [&](int64_t tile, int ch) {
@@ -977,7 +1195,8 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       if (u < XU) {
-        const int col = u % HC, row = (u / HC) % HR, half = u / (HR * HC);
+        int col, row, half;
+        unit(u, col, row, half);
         const int gr = r0 - 1 + row, gc = c0 - 1 + col;
         const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
         float v[8];
@@ -1028,22 +1247,34 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     const int row = r0 + wrow, col = c0 + li;
     const bool pok = row < H && col < W;
     const int64_t yo = (int64_t)n * Cout * HW + (int64_t)row * W + col;
+    const int64_t ycl = ((int64_t)n * HW + (int64_t)row * W + col) * Cout;
 #pragma unroll
     for (int i = 0; i < NIW; ++i) {
-      float s[16], q[16];
+      float s[16], q[16], vv[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int co = 32 * (wco + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
         const bool ok = pok && co < Cout;
         float v = acc[i][r] + ((bias && co < Cout) ? bias[co] : 0.f);
-        if constexpr (Y16) {
-          v = y16_round(v);
-          if (ok) y16_st(y, yo + (int64_t)co * HW, v);
-        } else {
-          if (ok) y[yo + (int64_t)co * HW] = v;
+        if constexpr (Y16) v = y16_round(v);
+        if constexpr (!YL) {
+          if constexpr (Y16) {
+            if (ok) y16_st(y, yo + (int64_t)co * HW, v);
+          } else {
+            if (ok) y[yo + (int64_t)co * HW] = v;
+          }
         }
+        vv[r] = v;
         s[r] = ok ? v : 0.f;
         q[r] = s[r] * s[r];
+      }
+      if constexpr (YL) {   // 4 consecutive channels per store (Cout % 4 == 0)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const int co0 = 32 * (wco + i) + 8 * rb + 4 * lh;
+          if (pok && co0 < Cout)
+            cl_st4<Y16>(y, ycl + co0, vv[4 * rb], vv[4 * rb + 1], vv[4 * rb + 2], vv[4 * rb + 3]);
+        }
       }
       if (stats) {
         bs[i] += (double)reduce16(s);
@@ -1140,7 +1371,8 @@ constexpr int XPLANE = HR * cxp::XROW;
 constexpr int XU = 2 * HR * cxp::HC;
 }  // namespace cxq
 
-template <int CI, bool DGRAD, int NP, bool G16 = false, bool Y16 = false>
+template <int CI, bool DGRAD, int NP, bool G16 = false, bool Y16 = false, bool XL = false,
+          bool YL = false>
 __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -1187,21 +1419,47 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
   };
 
   float px[XI][8];
+  // staging unit -> (halo column, halo row, channel half); channel-last: the
+  // two lanes of a pixel read its chunk's channels as contiguous bytes
+  auto unit = [&](int u, int& col, int& row, int& half) {
+    if constexpr (XL) {
+      half = u & 1;
+      const int hp = u >> 1;
+      col = hp % HC;
+      row = hp / HC;
+    } else {
+      col = u % HC;
+      row = (u / HC) % HR;
+      half = u / (HR * HC);
+    }
+  };
   auto fetch = [&](int64_t tile, int ch) {
     int n, r0, c0;
     tile_coords(tile, n, r0, c0);
     constexpr int ES = act_es<G16>();
-    int plane = (int)(HW * ES);
-    asm volatile("" : "+s"(plane));
-    const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ch * CK) * HW);
+    if constexpr (XL) {
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, (int64_t)n * HW * CI + ch * CK);
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = tid + NT * i;
-      const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
-      const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
-      const int vo = 8 * half * plane + (gr * W + gc) * ES;
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        int col, row, half;
+        unit(u < XU ? u : XU - 1, col, row, half);
+        const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+        cl_ld8<G16>(rx, ((gr * W + gc) * CI + 8 * half) * ES, px[i]);
+      }
+    } else {
+      int plane = (int)(HW * ES);
+      asm volatile("" : "+s"(plane));
+      const __amdgpu_buffer_rsrc_t rx = act_rsrc<G16>(x, ((int64_t)n * CI + ch * CK) * HW);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
+      for (int i = 0; i < XI; ++i) {
+        const int u = tid + NT * i;
+        const int col = u % HC, row = (u / HC) % HR, half = u < XU ? u / (HR * HC) : 1;
+        const int gr = wx6_clamp(r0 - 1 + row, 0, H - 1), gc = wx6_clamp(c0 - 1 + col, 0, W - 1);
+        const int vo = 8 * half * plane + (gr * W + gc) * ES;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) px[i][c] = act_ld<G16>(rx, vo, c * plane);
+      }
     }
   };
   auto commit = [&](int64_t tile, int ch) {
@@ -1211,7 +1469,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     for (int i = 0; i < XI; ++i) {
       const int u = tid + NT * i;
       if (u < XU) {
-        const int col = u % HC, row = (u / HC) % HR, half = u / (HR * HC);
+        int col, row, half;
+        unit(u, col, row, half);
         const int gr = r0 - 1 + row, gc = c0 - 1 + col;
         const bool inb = gr >= 0 && gr < H && gc >= 0 && gc < W;
         float v[8];
@@ -1257,20 +1516,29 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     for (int j = 0; j < 2; ++j) {
       const int col = c0 + 16 * j + l16;
       const bool pok = row < H && col < W;
+      float vv[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = 4 * g + r;
         const bool ok = pok && co < Cout;
         float v = acc[j][r] + ((bias && co < Cout) ? bias[co] : 0.f);
-        if constexpr (Y16) {
-          v = y16_round(v);
-          if (ok) y16_st(y, yo + (int64_t)co * HW + col, v);
-        } else {
-          if (ok) y[yo + (int64_t)co * HW + col] = v;
+        if constexpr (Y16) v = y16_round(v);
+        if constexpr (!YL) {
+          if constexpr (Y16) {
+            if (ok) y16_st(y, yo + (int64_t)co * HW + col, v);
+          } else {
+            if (ok) y[yo + (int64_t)co * HW + col] = v;
+          }
         }
+        vv[r] = v;
         const float sv = ok ? v : 0.f;
         s[r] += sv;
         q[r] += sv * sv;
+      }
+      if constexpr (YL) {   // channels 4g .. 4g+3 of pixel (row, col)
+        if (pok && 4 * g < Cout)
+          cl_st4<Y16>(y, ((int64_t)n * HW + (int64_t)row * W + col) * Cout + 4 * g, vv[0], vv[1],
+                      vv[2], vv[3]);
       }
     }
     if (stats) {
@@ -1350,60 +1618,67 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
 // Persistent launcher (conv_x6_launch routes here); returns 1 if (CI, COP)
 // has no instantiation.  x16 / y16 (bf16 configuration, NP = 1 only): the
 // input (dy of a data gradient, act(x) source of a forward) / the forward
-// output in bf16 storage.
+// output in bf16 storage.  lay: CL_X (input channel-last) | CL_Y (output
+// channel-last).
 template <int CIV, int COV, bool DG, int NTV, int TRV>
-static void x6p_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, const float* x,
+static void x6p_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, int lay, const float* x,
                    const float* w, const float* bias, const float* sc, const float* sh, float* y,
                    double* stats, int N, int Cout, int H, int W) {
-#define AINP_X6PK(NPV, GV, YV)                                                                \
-  hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, NPV, GV, YV>), g, dim3(NTV), \
-                     0, s, x, w, bias, sc, sh, y, stats, N, Cout, H, W)
-  if (!b16) {
-    AINP_X6PK(3, false, false);
-  } else if constexpr (DG) {
-    if (x16) AINP_X6PK(1, true, false);
-    else AINP_X6PK(1, false, false);
-  } else {
-    if (x16 && y16) AINP_X6PK(1, true, true);
-    else if (x16) AINP_X6PK(1, true, false);
-    else if (y16) AINP_X6PK(1, false, true);
-    else AINP_X6PK(1, false, false);
-  }
+  cl_dispatch(lay, [&](auto xl, auto yl) {
+    constexpr bool XL = decltype(xl)::value, YL = decltype(yl)::value;
+#define AINP_X6PK(NPV, GV, YV)                                                                   \
+  hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, NPV, GV, YV, XL, YL>), g,       \
+                     dim3(NTV), 0, s, x, w, bias, sc, sh, y, stats, N, Cout, H, W)
+    if (!b16) {
+      AINP_X6PK(3, false, false);
+    } else if constexpr (DG) {
+      if (x16) AINP_X6PK(1, true, false);
+      else AINP_X6PK(1, false, false);
+    } else {
+      if (x16 && y16) AINP_X6PK(1, true, true);
+      else if (x16) AINP_X6PK(1, true, false);
+      else if (y16) AINP_X6PK(1, false, true);
+      else AINP_X6PK(1, false, false);
+    }
 #undef AINP_X6PK
+  });
 }
 
 template <bool DG>
-static void x6q_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, const float* x,
+static void x6q_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, int lay, const float* x,
                    const float* w, const float* bias, const float* sc, const float* sh, float* y,
                    double* stats, int N, int Cout, int H, int W) {
+  cl_dispatch(lay, [&](auto xl, auto yl) {
+    constexpr bool XL = decltype(xl)::value, YL = decltype(yl)::value;
 #define AINP_X6QK(NPV, GV, YV)                                                                \
-  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV, GV, YV>), g, dim3(512), 0, s, x, w,     \
-                     bias, sc, sh, y, stats, N, Cout, H, W)
-  if (!b16) {
-    AINP_X6QK(3, false, false);
-  } else if constexpr (DG) {
-    if (x16) AINP_X6QK(1, true, false);
-    else AINP_X6QK(1, false, false);
-  } else {
-    if (x16 && y16) AINP_X6QK(1, true, true);
-    else if (x16) AINP_X6QK(1, true, false);
-    else if (y16) AINP_X6QK(1, false, true);
-    else AINP_X6QK(1, false, false);
-  }
+  hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV, GV, YV, XL, YL>), g, dim3(512), 0, s, x, \
+                     w, bias, sc, sh, y, stats, N, Cout, H, W)
+    if (!b16) {
+      AINP_X6QK(3, false, false);
+    } else if constexpr (DG) {
+      if (x16) AINP_X6QK(1, true, false);
+      else AINP_X6QK(1, false, false);
+    } else {
+      if (x16 && y16) AINP_X6QK(1, true, true);
+      else if (x16) AINP_X6QK(1, true, false);
+      else if (y16) AINP_X6QK(1, false, true);
+      else AINP_X6QK(1, false, false);
+    }
 #undef AINP_X6QK
+  });
 }
 
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                    bool x16, bool y16) {
+                    bool x16, bool y16, int lay) {
   const int cop = Cout <= 32 ? 32 : 64;
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
 #define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                      \
   if (dgrad == DG && Cin == CIV && cop == COV) {                                                 \
     const int g2 = b16 ? (G) * conv_x6_occ16() : (G);                                            \
-    x6p_go<CIV, COV, DG, NTV, TRV>(dim3(g2), s, b16, x16, y16, x, w, bias, sc, sh, y, stats,    \
-                                   (int)N, Cout, (int)H, (int)W);                                \
+    x6p_go<CIV, COV, DG, NTV, TRV>(dim3(g2), s, b16, x16, y16, lay, x, w, bias, sc, sh, y,      \
+                                   stats, (int)N, Cout, (int)H, (int)W);                         \
     *parts = g2;                                                                                 \
     return check_launch("conv3x3_x6p");                                                          \
   }
@@ -1412,10 +1687,10 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
   if (Cin == 32 && Cout == 16) {   // two workgroups per CU (65 KB of LDS; bf16: more)
     const int gq = b16 ? 512 * conv_x6_occ16() : 512;
     if (dgrad)
-      x6q_go<true>(dim3(gq), s, b16, x16, y16, x, w, bias, sc, sh, y, stats, (int)N, Cout,
+      x6q_go<true>(dim3(gq), s, b16, x16, y16, lay, x, w, bias, sc, sh, y, stats, (int)N, Cout,
                    (int)H, (int)W);
     else
-      x6q_go<false>(dim3(gq), s, b16, x16, y16, x, w, bias, sc, sh, y, stats, (int)N, Cout,
+      x6q_go<false>(dim3(gq), s, b16, x16, y16, lay, x, w, bias, sc, sh, y, stats, (int)N, Cout,
                     (int)H, (int)W);
     *parts = gq;
     return check_launch("conv3x3_x6q");
@@ -1424,54 +1699,53 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
   return 1;
 }
 
-template <bool G16, bool XG16>
+// the split-bf16 weight-gradient kernels of one pass (NP planes, storage
+// G16 / XG16) for the (cp, Cout) pair; returns 1 if it has none
+template <int NP, bool G16, bool XG16>
 static int wgrad_x6_go(const float* x, const float* sc, const float* sh, const float* dy,
                        float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                       int ci0, int cp, int grid, hipStream_t s) {
-  if (cp == 32 && Cout == 16) {
-    hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16, 1, G16, XG16>), dim3(grid), dim3(384), 0, s, x,
-                       sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
-    return check_launch("conv3x3_wgrad_x6s");
-  }
-  if (cp == 16 && Cout == 32) {
-    hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32, 1, G16, XG16>), dim3(grid), dim3(384), 0, s, x,
-                       sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
-    return check_launch("conv3x3_wgrad_x6s");
-  }
-  if (cp == 32 && Cout == 64) {
-    hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 1, G16, XG16>), dim3(grid), dim3(384), 0, s, x, sc,
-                       sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
-    return check_launch("conv3x3_wgrad_x6");
-  }
-  return 1;
+                       int ci0, int cp, int grid, hipStream_t s, int lay) {
+  int rc = 1;
+  auto go = [&](auto xlc, auto glc) {
+    constexpr bool XL = decltype(xlc)::value, GL = decltype(glc)::value;
+    if (cp == 32 && Cout == 16) {
+      hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16, NP, G16, XG16, XL, GL>), dim3(grid),
+                         dim3(384), 0, s, x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+      rc = check_launch("conv3x3_wgrad_x6s");
+    } else if (cp == 16 && Cout == 32) {
+      hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32, NP, G16, XG16, XL, GL>), dim3(grid),
+                         dim3(384), 0, s, x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+      rc = check_launch("conv3x3_wgrad_x6s");
+    } else if (cp == 32 && Cout == 64) {
+      hipLaunchKernelGGL((conv3x3_wgrad_x6<64, NP, G16, XG16, XL, GL>), dim3(grid), dim3(384), 0,
+                         s, x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+      rc = check_launch("conv3x3_wgrad_x6");
+    }
+  };
+  const bool xl = (lay & CL_X) != 0, gl = (lay & CL_G) != 0;
+  if (xl && gl) go(std::true_type{}, std::true_type{});
+  else if (xl) go(std::true_type{}, std::false_type{});
+  else if (gl) go(std::false_type{}, std::true_type{});
+  else go(std::false_type{}, std::false_type{});
+  return rc;
 }
 
 // Launch the split-bf16 weight gradient of one 32-channel pass if Cout has an
 // instantiation; returns 1 if not handled.  grid = persistent workgroups.
 // g16 / x16 (bf16 configuration): dy / act(x)'s source in bf16 storage.
+// lay: CL_X (act(x) source channel-last) | CL_G (dy channel-last).
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
-                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16) {
+                         int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16,
+                         int lay) {
   if (b16) {
-    if (g16 && x16) return wgrad_x6_go<true, true>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
-    if (g16) return wgrad_x6_go<true, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
-    if (x16) return wgrad_x6_go<false, true>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
-    return wgrad_x6_go<false, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s);
+    if (g16 && x16) return wgrad_x6_go<1, true, true>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s, lay);
+    if (g16) return wgrad_x6_go<1, true, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s, lay);
+    if (x16) return wgrad_x6_go<1, false, true>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s, lay);
+    return wgrad_x6_go<1, false, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s, lay);
   }
-  if (cp == 32 && Cout == 16) {
-    hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
-                       partial, (int)N, Cin, (int)H, (int)W, ci0);
-    return check_launch("conv3x3_wgrad_x6s");
-  }
-  if (cp == 16 && Cout == 32) {
-    hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
-                       partial, (int)N, Cin, (int)H, (int)W, ci0);
-    return check_launch("conv3x3_wgrad_x6s");
-  }
-  if (cp != 32 || Cout != 64) return 1;
-  hipLaunchKernelGGL((conv3x3_wgrad_x6<64, 3>), dim3(grid), dim3(384), 0, s, x, sc, sh, dy,
-                     partial, (int)N, Cin, (int)H, (int)W, ci0);
-  return check_launch("conv3x3_wgrad_x6");
+  return wgrad_x6_go<3, false, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s,
+                                      lay);
 }
 
 }  // namespace ainp

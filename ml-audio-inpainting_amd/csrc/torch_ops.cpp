@@ -222,10 +222,13 @@ float* f32_or_16_mut(const Tensor& t, const char* name, bool bf16) {
 void conv3x3_fwd(const Tensor& x, const Tensor& w, const OptT& bias, const OptT& in_scale,
                  const OptT& in_shift, const Tensor& y, const OptT& stats, int64_t flags) {
   GUARD(x);
-  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(1) == x.size(1) && w.size(2) == 3 &&
+  // channel-last activations (AINP_CONV_XCL): x [N,H,W,Cin]
+  const bool xcl = flags & AINP_CONV_XCL;
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 4 && w.size(1) == x.size(xcl ? 3 : 1) && w.size(2) == 3 &&
                   w.size(3) == 3,
-              "conv3x3_fwd: x [N,Cin,H,W], w [Cout,Cin,3,3]");
-  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = w.size(0);
+              "conv3x3_fwd: x [N,Cin,H,W] (channel-last: [N,H,W,Cin]), w [Cout,Cin,3,3]");
+  const int64_t N = x.size(0), Cin = w.size(1), H = x.size(xcl ? 1 : 2), W = x.size(xcl ? 2 : 3),
+                Cout = w.size(0);
   numel_is(y, N * Cout * H * W, "y");
   double* st = opt<double>(stats, "stats", at::kDouble);
   if (st)
@@ -241,9 +244,11 @@ void conv3x3_fwd(const Tensor& x, const Tensor& w, const OptT& bias, const OptT&
 
 void conv3x3_dgrad(const Tensor& dy, const Tensor& w, const Tensor& dx, int64_t flags) {
   GUARD(dy);
-  TORCH_CHECK(dy.dim() == 4 && w.dim() == 4 && w.size(0) == dy.size(1),
-              "conv3x3_dgrad: dy [N,Cout,H,W], w [Cout,Cin,3,3]");
-  const int64_t N = dy.size(0), Cout = dy.size(1), H = dy.size(2), W = dy.size(3), Cin = w.size(1);
+  const bool gcl = flags & AINP_CONV_XCL;   // dy [N,H,W,Cout]
+  TORCH_CHECK(dy.dim() == 4 && w.dim() == 4 && w.size(0) == dy.size(gcl ? 3 : 1),
+              "conv3x3_dgrad: dy [N,Cout,H,W] (channel-last: [N,H,W,Cout]), w [Cout,Cin,3,3]");
+  const int64_t N = dy.size(0), Cout = w.size(0), H = dy.size(gcl ? 1 : 2),
+                W = dy.size(gcl ? 2 : 3), Cin = w.size(1);
   numel_is(dx, N * Cin * H * W, "dx");
   const float* dyp = f32_or_16(dy, "dy", flags & AINP_CONV_DY16);
   chk(ainp_conv3x3_dgrad_ex(dyp, dev(w, "w"), dev(dx, "dx"), nullptr, N, (int)Cin,
@@ -254,10 +259,13 @@ void conv3x3_dgrad(const Tensor& dy, const Tensor& w, const Tensor& dx, int64_t 
 void conv3x3_wgrad(const Tensor& x, const OptT& in_scale, const OptT& in_shift, const Tensor& dy,
                    const Tensor& dw, const OptT& dbias, const Tensor& workspace, int64_t flags) {
   GUARD(x);
-  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == x.size(0) && dy.size(2) == x.size(2) &&
-                  dy.size(3) == x.size(3),
-              "conv3x3_wgrad: x [N,Cin,H,W], dy [N,Cout,H,W]");
-  const int64_t N = x.size(0), Cin = x.size(1), H = x.size(2), W = x.size(3), Cout = dy.size(1);
+  // channel-last: x [N,H,W,Cin] (AINP_CONV_XCL), dy [N,H,W,Cout] (AINP_CONV_GCL)
+  const bool xcl = flags & AINP_CONV_XCL, gcl = flags & AINP_CONV_GCL;
+  const int64_t N = x.size(0), Cin = x.size(xcl ? 3 : 1), H = x.size(xcl ? 1 : 2),
+                W = x.size(xcl ? 2 : 3), Cout = dy.size(gcl ? 3 : 1);
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4 && dy.size(0) == N && dy.size(gcl ? 1 : 2) == H &&
+                  dy.size(gcl ? 2 : 3) == W,
+              "conv3x3_wgrad: x [N,Cin,H,W], dy [N,Cout,H,W] (or channel-last [N,H,W,C])");
   numel_is(dw, Cout * Cin * 9, "dw");
   TORCH_CHECK((size_t)workspace.nbytes() >= ainp_conv3x3_wgrad_workspace(N, (int)Cin, (int)Cout, H, W),
               "conv3x3_wgrad workspace too small");
@@ -348,13 +356,17 @@ void bn_relu_bwd_reduce(const Tensor& g, const Tensor& y, const Tensor& scale, c
                         const Tensor& save, const Tensor& workspace, const Tensor& sums, bool ntcf,
                         int64_t flags) {
   GUARD(y);
-  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
-  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  // AINP_BN_CL: y (and g) channel-last [N,H,W,C]; AINP_BN_G16: g bf16 storage
+  const bool cl = flags & AINP_BN_CL;
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W] (channel-last: [N,H,W,C])");
+  const int64_t N = y.size(0), C = y.size(cl ? 3 : 1), H = y.size(cl ? 1 : 2),
+                W = y.size(cl ? 2 : 3);
   numel_is(g, y.numel(), "g");
   TORCH_CHECK(sums.numel() >= 2 * C, "sums needs 2C entries");
   TORCH_CHECK((size_t)workspace.nbytes() >= ainp_bn_relu_bwd_workspace(N, (int)C, H, W),
               "bn_relu_bwd workspace too small");
-  chk(ainp_bn_relu_bwd_reduce_ex(dev(g, "g"), f32_or_16(y, "y", flags & AINP_BN_Y16),
+  chk(ainp_bn_relu_bwd_reduce_ex(f32_or_16(g, "g", flags & AINP_BN_G16),
+                                 f32_or_16(y, "y", flags & AINP_BN_Y16),
                                  dev(scale, "scale"), dev(shift, "shift"), dev(save, "save"),
                                  workspace.data_ptr(), dev<double>(sums, "sums", at::kDouble), N,
                                  (int)C, H, W, ntcf ? 1 : 0, (int)flags, stream_of(y)),
@@ -366,15 +378,18 @@ void bn_relu_bwd_apply(const Tensor& g, const Tensor& y, const Tensor& scale, co
                        const Tensor& gy, const OptT& dgamma, const OptT& dbeta, bool ntcf,
                        int64_t flags) {
   GUARD(y);
-  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W]");
-  const int64_t N = y.size(0), C = y.size(1), H = y.size(2), W = y.size(3);
+  const bool cl = flags & AINP_BN_CL;
+  TORCH_CHECK(y.dim() == 4, "y must be [N,C,H,W] (channel-last: [N,H,W,C])");
+  const int64_t N = y.size(0), C = y.size(cl ? 3 : 1), H = y.size(cl ? 1 : 2),
+                W = y.size(cl ? 2 : 3);
   numel_is(g, y.numel(), "g");
   numel_is(gy, y.numel(), "gy");
   TORCH_CHECK(sums.numel() >= 2 * C + (count == 0 ? 1 : 0), "sums too short");
   // AINP_BN_GY16: gy is bf16 storage
   void* gyp = (flags & AINP_BN_GY16) ? (void*)dev<c10::BFloat16>(gy, "gy", at::kBFloat16)
                                      : (void*)dev(gy, "gy");
-  chk(ainp_bn_relu_bwd_apply_ex(dev(g, "g"), f32_or_16(y, "y", flags & AINP_BN_Y16),
+  chk(ainp_bn_relu_bwd_apply_ex(f32_or_16(g, "g", flags & AINP_BN_G16),
+                                f32_or_16(y, "y", flags & AINP_BN_Y16),
                                 dev(scale, "scale"),
                                 dev(shift, "shift"), opt(gamma, "gamma"), dev(save, "save"),
                                 dev<double>(sums, "sums", at::kDouble), count, gyp,

@@ -115,7 +115,7 @@ def _gan_batch(n=2, F=257, T=100):
     return orig, imp, mask
 
 
-def run_gan(comm=None, rank=0, world=1, faithful=False, steps=1, g_nan_rank=None):
+def run_gan(comm=None, rank=0, world=1, faithful=False, steps=1, g_nan_rank=None, fix_g=False):
     """faithful: GanTrainer(faithful_g_backward=True), whose G-step backward
     fills D grads that must not reach the gradient reducer.  g_nan_rank: that
     rank's G-step total loss is made NaN (fail_fast on): every rank must stop
@@ -129,7 +129,7 @@ def run_gan(comm=None, rank=0, world=1, faithful=False, steps=1, g_nan_rank=None
     disc = G.Discriminator().to(dev)
     vgg = G.VGGLoss(dev)
     tr = GanTrainer(GAN_CFG, gen, disc, vgg, comm=comm, faithful_g_backward=faithful,
-                    fail_fast=g_nan_rank is not None)
+                    fail_fast=g_nan_rank is not None, fix_generator_grad=fix_g)
     if g_nan_rank == rank:
         calc = G.calculate_losses
 
@@ -153,7 +153,15 @@ def run_gan(comm=None, rank=0, world=1, faithful=False, steps=1, g_nan_rank=None
     dstate = {k: v.detach().cpu().clone() for k, v in disc.state_dict().items()}
     gbn = {k: v.detach().cpu().clone() for k, v in gen.state_dict().items()
            if "running" in k}
-    return {"losses": losses, "disc": dstate, "gen_bn": gbn}
+    res = {"losses": losses, "disc": dstate, "gen_bn": gbn}
+    if fix_g:
+        # G's gradients as g_optimizer.step() consumed them (after the
+        # reducer's exchange; Adam's update itself is nearly scale-free, so
+        # the gradients are what pins the DP scaling)
+        res["gen_grad"] = {n: p.grad.detach().cpu().clone() for n, p in gen.named_parameters()
+                           if p.grad is not None}
+        res["gen"] = {k: v.detach().cpu().clone() for k, v in gen.state_dict().items()}
+    return res
 
 
 def main():
@@ -181,6 +189,8 @@ def main():
         res = run_cnnblstm(comm, rank, world, uneven=True, steps=2)
     elif mode == "gan_gnan":
         res = run_gan(comm, rank, world, faithful=True, g_nan_rank=1)
+    elif mode == "gan_fixg":
+        res = run_gan(comm, rank, world, fix_g=True)
     elif mode == "gan_faithful":
         res = run_gan(comm, rank, world, faithful=True, steps=2)
     else:

@@ -97,6 +97,15 @@ def test_dy16_routing_query():
         assert q(32, cin, cout, 257, 334) == 0, (cin, cout)
     rc = _lib.lib.ainp_conv3x3_fwd_ex(1, 1, None, None, None, 1, None, 1, 16, 32, 8, 8, 16, None)
     assert rc == -1          # AINP_CONV_Y16 without the bf16 arithmetic
+    # channel-last activations (round 5): every conv of the model, none other
+    q = _lib.lib.ainp_conv3x3_cl_ok
+    for cin, cout in ((1, 16), (16, 32), (32, 64), (32, 16), (16, 1)):
+        assert q(32, cin, cout, 257, 334) == 1, (cin, cout)
+    for cin, cout in ((2, 16), (16, 2), (64, 32), (8, 24), (16, 16)):
+        assert q(32, cin, cout, 257, 334) == 0, (cin, cout)
+    # an unknown flag bit is refused before any launch
+    rc = _lib.lib.ainp_conv3x3_fwd_ex(1, 1, None, None, None, 1, None, 1, 16, 32, 8, 8, 256, None)
+    assert rc == -1
 
 
 def test_ops_refuse_cpu_tensors():
@@ -109,7 +118,8 @@ def test_ops_refuse_cpu_tensors():
 HOST_ONLY = {"ainp_abi_version", "ainp_build_target", "ainp_last_error", "ainp_reduce_workspace",
              "ainp_flac_info", "ainp_flac_decode", "ainp_flac_encode_bound", "ainp_flac_encode",
              "ainp_l1_pow10_loss_slots", "ainp_range_push", "ainp_range_pop", "ainp_mark",
-             "ainp_conv16_set_variant", "ainp_conv3x3_dy16_ok", "ainp_conv3x3_io16_ok"}
+             "ainp_conv16_set_variant", "ainp_conv3x3_dy16_ok", "ainp_conv3x3_io16_ok",
+             "ainp_conv3x3_cl_ok"}
 
 
 def test_torch_library_registers_every_gpu_entry_point():

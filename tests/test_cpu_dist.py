@@ -206,7 +206,10 @@ def _groups_worker(rank, world, port, q):
     # broadcast from rank 0 over the sync group
     m = torch.nn.Linear(2, 2)
     torch.nn.init.constant_(m.weight, float(rank))
+    v0 = m.weight._version
     comm.broadcast_module_(m)
+    # the broadcast bumps the version the device weight caches are keyed on
+    bumped = m.weight._version > v0
     # paused reducer ignores gradients
     red.paused = True
     red._ready(p)
@@ -217,7 +220,7 @@ def _groups_worker(rank, world, port, q):
     from models.GAN.train import train_subset
     random.seed(100 + rank)
     idx = train_subset(1000, 30, rank, world)
-    q.put((rank, distinct, p.grad.tolist(), float(m.weight.sum()), ignored, idx))
+    q.put((rank, distinct and bumped, p.grad.tolist(), float(m.weight.sum()), ignored, idx))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -1,0 +1,189 @@
+"""Channel-last activations (round 5): the CNNBLSTM conv / BatchNorm kernels
+reading and writing [N, F, T, C] tensors (AINP_CONV_XCL / _YCL / _GCL,
+AINP_BN_CL) against the NCHW kernels they replace.
+
+The split-bf16 conv kernels stage the same values into the same LDS images
+and run the same MFMA chains whichever layout they load from, so their
+outputs, BatchNorm partials and weight gradients are bit-identical to the
+NCHW launches.  The channel-last BatchNorm backward and the small-channel
+row-strip weight gradient sum in another order (checked at 1e-6).  The model
+test runs a CNNBLSTM step with AINP_CL on / off (models/CNNBLSTM/model.py:
+34-61 is the reference either way)."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "ml-audio-inpainting_amd"))
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _cl(t):
+    return t.permute(0, 2, 3, 1).contiguous()
+
+
+def _nchw(t):
+    return t.permute(0, 3, 1, 2).contiguous()
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _data(N, cin, cout, H, W, seed):
+    g = torch.Generator(device=DEV).manual_seed(seed)
+    x = torch.randn(N, cin, H, W, device=DEV, generator=g)
+    dy = torch.randn(N, cout, H, W, device=DEV, generator=g) * 0.1
+    w = torch.randn(cout, cin, 3, 3, device=DEV, generator=g) * 0.2
+    b = torch.randn(cout, device=DEV, generator=g)
+    sc = torch.rand(cin, device=DEV, generator=g) + 0.5
+    sh = torch.randn(cin, device=DEV, generator=g) * 0.3
+    return x, dy, w, b, sc, sh
+
+
+PAIRS = [(16, 32), (32, 64), (32, 16)]
+SHAPES = [(2, 257, 334), (1, 19, 47)]
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("N,H,W", SHAPES)
+@pytest.mark.parametrize("cin,cout", PAIRS)
+def test_cl_fwd_bit_identical(cin, cout, N, H, W, bf16):
+    from ainp import ops
+    x, dy, w, b, sc, sh = _data(N, cin, cout, H, W, cin * 100 + cout)
+    y0, st0 = ops.conv3x3_fwd(x, w, b, sc, sh, want_stats=True, bf16=bf16)
+    for xcl, ycl in ((True, True), (True, False), (False, True)):
+        y, st = ops.conv3x3_fwd(_cl(x) if xcl else x, w, b, sc, sh, want_stats=True, bf16=bf16,
+                                xcl=xcl, ycl=ycl)
+        assert torch.equal(_nchw(y) if ycl else y, y0), (xcl, ycl)
+        assert torch.equal(st, st0), (xcl, ycl)
+    if bf16:   # bf16 storage of the source and of y (AINP_CONV_X16 / _Y16)
+        x16 = x.to(torch.bfloat16)
+        y0, st0 = ops.conv3x3_fwd(x16, w, b, sc, sh, want_stats=True, bf16=True, y16=True)
+        y, st = ops.conv3x3_fwd(_cl(x16), w, b, sc, sh, want_stats=True, bf16=True, y16=True,
+                                xcl=True, ycl=True)
+        assert torch.equal(_nchw(y), y0) and torch.equal(st, st0)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("N,H,W", SHAPES)
+@pytest.mark.parametrize("cin,cout", PAIRS)
+def test_cl_dgrad_wgrad_bit_identical(cin, cout, N, H, W, bf16):
+    from ainp import ops
+    x, dy, w, b, sc, sh = _data(N, cin, cout, H, W, cin * 7 + cout)
+    dys = [dy] + ([dy.to(torch.bfloat16)] if bf16 else [])
+    for d in dys:
+        dx0 = ops.conv3x3_dgrad(d, w, bf16=bf16)
+        for xcl, ycl in ((True, True), (True, False), (False, True)):
+            dx = ops.conv3x3_dgrad(_cl(d) if xcl else d, w, bf16=bf16, xcl=xcl, ycl=ycl)
+            assert torch.equal(_nchw(dx) if ycl else dx, dx0), (d.dtype, xcl, ycl)
+        dw0, db0 = ops.conv3x3_wgrad(x, d, sc, sh, bf16=bf16)
+        for xcl, gcl in ((True, True), (True, False), (False, True)):
+            dw, db = ops.conv3x3_wgrad(_cl(x) if xcl else x, _cl(d) if gcl else d, sc, sh,
+                                       bf16=bf16, xcl=xcl, gcl=gcl)
+            assert torch.equal(dw, dw0) and torch.equal(db, db0), (d.dtype, xcl, gcl)
+
+
+@pytest.mark.parametrize("N,H,W", SHAPES)
+@pytest.mark.parametrize("pro", [True, False])
+def test_cl_small_channel_convs(N, H, W, pro):
+    """1 -> 16 and 16 -> 1 (encoder.0, decoder.6): forward and data gradient
+    bit-identical, the channel-last row-strip weight gradient within 1e-6 of
+    the NCHW one (another summation order) and run-to-run identical."""
+    from ainp import ops
+    for cin, cout in ((1, 16), (16, 1)):
+        x, dy, w, b, sc, sh = _data(N, cin, cout, H, W, 5 + cin)
+        s_, h_ = (sc, sh) if pro else (None, None)
+        y0, st0 = ops.conv3x3_fwd(x, w, b, s_, h_, want_stats=True)
+        xcl, ycl = cin == 16, cout == 16
+        y, st = ops.conv3x3_fwd(_cl(x) if xcl else x, w, b, s_, h_, want_stats=True, xcl=xcl,
+                                ycl=ycl)
+        # y bit-identical; the BatchNorm partials of the two template instances
+        # may contract the sum of squares differently (fp32 rounding level)
+        assert torch.equal(_nchw(y) if ycl else y, y0) and rel(st, st0) < 1e-6
+        dx0 = ops.conv3x3_dgrad(dy, w)
+        dx = ops.conv3x3_dgrad(_cl(dy) if ycl else dy, w, xcl=ycl, ycl=xcl)
+        assert torch.equal(_nchw(dx) if xcl else dx, dx0)
+        dw0, db0 = ops.conv3x3_wgrad(x, dy, s_, h_)
+        args = (_cl(x) if xcl else x, _cl(dy) if ycl else dy, s_, h_)
+        dw, db = ops.conv3x3_wgrad(*args, xcl=xcl, gcl=ycl)
+        dw2, db2 = ops.conv3x3_wgrad(*args, xcl=xcl, gcl=ycl)
+        assert torch.equal(dw, dw2) and torch.equal(db, db2)
+        assert rel(dw, dw0) < 1e-6 and rel(db, db0) < 1e-6, (cin, cout)
+
+
+@pytest.mark.parametrize("C", [16, 32, 64])
+@pytest.mark.parametrize("store", ["f32", "y16", "g16", "gy16"])
+def test_cl_bn_relu_backward(C, store):
+    """Channel-last BatchNorm+ReLU backward (reduce + apply) against the NCHW
+    kernels: sums within 1e-6 (fixed-order partials of another grouping),
+    gy within 1e-6, dgamma / dbeta the sums; bf16 storage of y / g / gy."""
+    from ainp import ops
+    N, H, W = 3, 57, 110
+    g = torch.Generator(device=DEV).manual_seed(C)
+    y = torch.randn(N, C, H, W, device=DEV, generator=g)
+    gr = torch.randn(N, C, H, W, device=DEV, generator=g)
+    sc = torch.rand(C, device=DEV, generator=g) + 0.5
+    sh = torch.randn(C, device=DEV, generator=g) * 0.3
+    save = torch.stack([torch.randn(C, device=DEV, generator=g) * 0.1,
+                        torch.rand(C, device=DEV, generator=g) + 0.5])
+    gamma = torch.rand(C, device=DEV, generator=g) + 0.5
+    if store == "y16":
+        y = y.to(torch.bfloat16)
+    gin = gr.to(torch.bfloat16).float() if store == "g16" else gr
+    s0 = ops.bn_relu_bwd_reduce(gin, y, sc, sh, save)
+    gy0, dg0, db0 = ops.bn_relu_bwd_apply(gin, y, sc, sh, gamma, save, s0, N * H * W,
+                                          gy16=store == "gy16")
+    gcl = _cl(gr.to(torch.bfloat16)) if store == "g16" else _cl(gr)
+    s1 = ops.bn_relu_bwd_reduce(gcl, _cl(y), sc, sh, save, cl=True)
+    assert rel(s1, s0) < 1e-6
+    gy1, dg1, db1 = ops.bn_relu_bwd_apply(gcl, _cl(y), sc, sh, gamma, save, s0, N * H * W,
+                                          gy16=store == "gy16", cl=True)
+    assert gy1.dtype == gy0.dtype
+    if store == "gy16":   # the same fp32 values rounded once
+        assert rel(_nchw(gy1).float(), gy0.float()) < 4e-3
+    else:
+        assert rel(_nchw(gy1), gy0) < 1e-6
+    assert torch.equal(dg1, dg0) and torch.equal(db1, db0)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cnnblstm_step_channel_last_matches_nchw(monkeypatch, dtype):
+    """One training step of the CNNBLSTM at the C2 plane (N=4) with the
+    channel-last conv stacks (default) and with NCHW (AINP_CL=0): every
+    gradient within 1e-5 (the BatchNorm backward sums in another order)."""
+    from ainp import cnnblstm
+    cfg = {"data": {"sample_rate": 16000, "spectrogram": {"n_fft": 512, "hop_length": 192,
+                                                          "win_length": 384}},
+           "model": {"in_channels": 1, "num_lstm_layers": 2, "lstm_hidden_dim": 128,
+                     "enc_filters": [16, 32], "dec_filters": [16, 32]},
+           "accel": {"dtype": dtype}}
+    g = torch.Generator().manual_seed(3)
+    N, F, T = 4, 257, 334
+    x = (torch.randn(N, 1, F, T, generator=g) - 2.0).to(DEV)
+    mask = torch.zeros(N, F, T)
+    for i in range(N):
+        mask[i, :, 40 + 30 * i:57 + 30 * i] = 1.0
+    mask = mask.to(DEV)
+    tgt = torch.complex(torch.rand(N, F, T, generator=g), torch.rand(N, F, T, generator=g)).to(DEV)
+    res = []
+    for cl in (True, False):
+        monkeypatch.setattr(cnnblstm, "CL", cl)
+        torch.manual_seed(0)
+        m = cnnblstm.StackedBLSTMCNN(config=cfg).to(DEV).train()
+        loss = cnnblstm.l1_pow10_loss(m(x), mask, tgt)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    tol = 1e-5 if dtype == "fp32" else 2e-3
+    assert abs(res[0][0] - res[1][0]) <= 1e-6 * abs(res[1][0])
+    for n, g1 in res[1][1].items():
+        if n in ("encoder.0.bias", "encoder.3.bias", "encoder.6.bias", "decoder.0.bias",
+                 "decoder.3.bias"):
+            continue   # BatchNorm-fed conv biases: exact gradient 0
+        assert rel(res[0][1][n], g1) < tol, n

@@ -176,6 +176,26 @@ def test_gan_dp2_faithful_g_backward_two_steps(tmp_path):
 
 
 @pytest.mark.timeout(300)
+def test_gan_dp2_fix_generator_grad_equals_single_process(tmp_path):
+    """fix_generator_grad under DP: G's exchanged gradients equal the
+    1-process gradients of the whole batch.  Pins the two scale conventions
+    of the DP generator backward: the L1 terms are global-batch
+    values (their per-rank gradient is pre-scaled for the reducer's average)
+    and SyncBN's dgamma / dbeta come from all-reduced sums (handed over as the
+    per-rank share)."""
+    import dp_worker
+    ref = dp_worker.run_gan(fix_g=True)
+    ranks = _run_ranks("gan_fixg", tmp_path)
+    assert set(ranks[0]["gen_grad"]) == set(ref["gen_grad"])
+    for k, v in ref["gen_grad"].items():
+        assert _rel(ranks[0]["gen_grad"][k], v) < 1e-3, k
+        assert torch.equal(ranks[0]["gen_grad"][k], ranks[1]["gen_grad"][k]), k
+    for k, v in ref["gen"].items():
+        if v.is_floating_point():
+            assert _rel(ranks[0]["gen"][k], v) < 1e-4, k
+
+
+@pytest.mark.timeout(300)
 def test_gan_dp2_nonfinite_g_loss_fails_fast_on_every_rank(tmp_path):
     """faithful_g_backward with fail_fast: a NaN G-step loss on rank 1 stops
     both ranks before g_optimizer.step() (MAX-all-reduced flag)."""

@@ -995,3 +995,18 @@ def test_unet_bf16_forward_without_fp32_writeback_is_bit_identical(monkeypatch):
         with torch.no_grad():
             outs.append(net(x, m).clone())
     assert torch.equal(outs[0], outs[1])
+    # AINP_CONV_NHWC16_SMALL=0: the final PartialConv2d's 1-channel source
+    # sends it down the fp32 NCHW gather, which reads the block output's fp32
+    # planes -- the write-back must then stay on, same output
+    # as with every consumer channel-last
+    from ainp import ops
+    monkeypatch.setattr(ops, "CONV_NHWC16_SMALL", "0")
+    monkeypatch.setattr(G, "AFFINE_NO_Y", True)
+    assert not G._affine_no_y_safe()
+    with torch.no_grad():
+        small0 = net(x, m).clone()
+    monkeypatch.setattr(G, "AFFINE_NO_Y", False)
+    with torch.no_grad():
+        small0_y = net(x, m).clone()
+    assert torch.equal(small0, small0_y)
+    assert (small0 - outs[0]).abs().max().item() < 1e-1

@@ -474,6 +474,8 @@ def _act(x, sc, sh):
     # small-channel kernels (1-2 channels on one side, 16 on the other), multi-tile
     (2, 1, 16, 41, 100, False), (3, 16, 1, 19, 97, True), (1, 2, 16, 12, 50, True),
     (1, 16, 2, 25, 60, False),
+    # the row-strip weight gradient: several 32-row strips and 62-column blocks
+    (2, 16, 1, 70, 130, True), (1, 1, 16, 65, 125, False),
     # split-bf16 weight gradient (32-channel passes x 64 outputs): the model's
     # plane, two passes without a prologue, tiles smaller than one 2 x 48 tile
     (2, 32, 64, 257, 334, True), (1, 64, 64, 19, 47, False), (3, 32, 64, 5, 3, True),
@@ -503,6 +505,27 @@ def test_conv3x3_fwd_dgrad_wgrad(ops, N, Cin, Cout, H, W, pro):
     dw, db = ops.conv3x3_wgrad(d(x), d(dy), d(sc), d(sh))
     assert rel(dw.cpu(), wr.grad) < 1e-5
     assert rel(db.cpu(), br.grad) < 1e-5
+
+
+@pytest.mark.parametrize("Cin,Cout,pro", [(16, 1, True), (1, 16, False), (2, 16, True),
+                                           (16, 2, False)])
+def test_small_wgrad_strip_matches_tile_kernel(ops, monkeypatch, Cin, Cout, pro):
+    """The row-strip weight gradient of the 1-2-channel-sided convs against
+    the 8 x 48-tile kernel it replaced (AINP_SMALL_WGRAD_TILE=1), at the C2
+    plane: the same sums in another order, and run-to-run bit-identical."""
+    g = torch.Generator().manual_seed(Cin * 7 + Cout)
+    N, H, W = 3, 257, 334
+    x = torch.randn(N, Cin, H, W, generator=g).to(DEV)
+    dy = torch.randn(N, Cout, H, W, generator=g).to(DEV)
+    sc = (torch.rand(Cin, generator=g) + 0.5).to(DEV) if pro else None
+    sh = (torch.randn(Cin, generator=g) * 0.3).to(DEV) if pro else None
+    dw, db = ops.conv3x3_wgrad(x, dy, sc, sh)
+    dw2, db2 = ops.conv3x3_wgrad(x, dy, sc, sh)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    monkeypatch.setenv("AINP_SMALL_WGRAD_TILE", "1")
+    tw, tb = ops.conv3x3_wgrad(x, dy, sc, sh)
+    assert rel(dw.cpu().double(), tw.cpu().double()) < 1e-6
+    assert rel(db.cpu().double(), tb.cpu().double()) < 1e-6
 
 
 # ------------------------------------------------------------------ BN
