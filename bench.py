@@ -433,10 +433,14 @@ def _cnn_step_work(B=32, F=257, T=334, H=128):
     ]
 
 
-def in_step_table(key, bf16, top=8):
+def in_step_table(key, bf16, top=8, families=None):
     """Dominant in-step kernels of the committed step table for `key` (None
     if absent): per-step ms, share of the step's kernel time, and for the
-    kernels with a known per-step work their roofline fraction."""
+    kernels with a known per-step work their roofline fraction.
+    families (the GAN step): {kernel-name substring: FLOP per step} measured
+    by ops.WORK_TRACE over one live step; every table row whose name holds
+    the substring belongs to the family (template instances of one kernel),
+    whose fraction is its FLOP over the family's summed per-step time."""
     path, div = STEP_TABLES.get(key, (None, 1))
     if not path or not os.path.exists(os.path.join(ROOT, path)):
         return None
@@ -444,6 +448,20 @@ def in_step_table(key, bf16, top=8):
     rows = list(csv.DictReader(open(os.path.join(ROOT, path))))
     total = sum(float(r["TotalDurationNs"]) for r in rows)
     work = _cnn_step_work() if key[0] == "cnnblstm" else []
+    fam = None
+    if families:
+        peak = executed_peak(bf16)
+        fam = []
+        for sub, flop in sorted(families.items(), key=lambda kv: -kv[1]):
+            ns = sum(float(r["TotalDurationNs"]) for r in rows if sub in r["Name"])
+            if ns <= 0:
+                continue
+            ms = ns / 1e6 / div
+            tf = flop / (ms / 1e3) / 1e12
+            fam.append({"family": sub, "ms_per_step": round(ms, 4), "flop_per_step": flop,
+                        "achieved_tflops": round(tf, 1), "peak": round(peak, 1),
+                        "frac": round(tf / peak, 4),
+                        "instances": sum(1 for r in rows if sub in r["Name"])})
     out = []
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:top]:
         ms = float(r["TotalDurationNs"]) / 1e6 / div
@@ -462,9 +480,19 @@ def in_step_table(key, bf16, top=8):
                     e.update(bound="hbm", achieved_gbs=round(gbs, 1), peak=HBM_PEAK_GBS,
                              frac=round(gbs / HBM_PEAK_GBS, 4), bytes_per_step=amount)
                 break
+        for f in fam or ():
+            if f["family"] in r["Name"]:
+                e.update(family=f["family"], family_frac=f["frac"])
+                break
         out.append(e)
-    return {"table": path, "per_step": f"rocprofv3 --kernel-trace --stats of tools/step_prof.py "
-                                       f"(totals / {div})", "top": out}
+    res = {"table": path, "per_step": f"rocprofv3 --kernel-trace --stats of tools/step_prof.py "
+                                      f"(totals / {div})", "top": out}
+    if fam is not None:
+        res["families"] = fam
+        res["family_work"] = ("FLOP per step of each kernel family from ops.WORK_TRACE over one "
+                              "live step (2 * outputs * Cin * k * k per conv launch, by the "
+                              "kernel the launch routes to; D weight gradients as GEMM FLOP)")
+    return res
 
 
 def main():
@@ -885,6 +913,16 @@ def run_gan(args):
                               traffic=_traffic(f"traffic_conv_gen_wide_bf16{tsuf}.json"))
             roof_wide["main_loop"] = ("256x128 tiles, 8 waves of 64x64, 3-stage LDS-DMA ring "
                                       "(global_load_lds_dwordx4), v_mfma_f32_32x32x16_bf16")
+    families = None
+    if rank == 0 and world == 1:
+        # per-family algorithmic work of one step, as the step routes it
+        ops.WORK_TRACE = []
+        step(nsteps - 1)
+        torch.cuda.synchronize()
+        families = {}
+        for nm, fl in ops.WORK_TRACE:
+            families[nm] = families.get(nm, 0.0) + fl
+        ops.WORK_TRACE = None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = gan_cpu_baseline(T, S, g)
@@ -913,7 +951,7 @@ def run_gan(args):
             "mfma_util_step": (round(step_flops / world / (ms_step / 1e3) / 1e12
                                      / executed_peak(bf16), 4) if step_flops else None),
             "roofline": roof, "roofline_wide": roof_wide, "reconstruction": recon,
-            "in_step_kernels": in_step_table(("gan", args.dtype, T), bf16),
+            "in_step_kernels": in_step_table(("gan", args.dtype, T), bf16, families=families),
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

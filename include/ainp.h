@@ -453,6 +453,15 @@ int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale
 int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale, const float* shift,
                                  uint16_t* out, uint16_t* outT, int64_t ld_t, int64_t N, int C,
                                  int64_t H, int64_t W, void* stream);
+/* Round 5: the same bridge from a channel-last y [N][H][W][64] (AINP_BN_Y16:
+ * bf16 storage): out (fp32) and / or out16 (bf16) = relu(y*scale+shift) as
+ * [N][W][64*H], outT (bf16) as [64*H][ld_t] (element (k, n*W + w)); NULL
+ * outputs are skipped.  With AINP_BN_CL, ainp_bn_relu_bwd_reduce_ex /
+ * _apply_ex take g_ntcf = 1 for this block: g [N,W,64*H] fp32, y and gy
+ * channel-last. */
+int ainp_bn_relu_apply_ntcf_cl(const float* y, const float* scale, const float* shift,
+                               float* out, uint16_t* out16, uint16_t* outT, int64_t ld_t,
+                               int64_t N, int C, int64_t H, int64_t W, int flags, void* stream);
 /* flags: AINP_BN_Y16 (x in bf16 storage) */
 int ainp_bn_relu_apply_ntcf_bf16_ex(const float* x, const float* scale, const float* shift,
                                     uint16_t* out, uint16_t* outT, int64_t ld_t, int64_t N,

@@ -161,6 +161,8 @@ _SIGS = {
                                              c_int64, P]),
     "ainp_bn_relu_apply_ntcf_bf16_ex": (c_int, [P, P, P, P, P, c_int64, c_int64, c_int, c_int64,
                                                 c_int64, c_int, P]),
+    "ainp_bn_relu_apply_ntcf_cl": (c_int, [P, P, P, P, P, P, c_int64, c_int64, c_int, c_int64,
+                                           c_int64, c_int, P]),
     "ainp_gemm_bf16nt": (c_int, [c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P, c_int64,
                                  P, P, P, P, c_int64, c_int, c_int64, c_int64, P]),
     "ainp_cast_bf16_t": (c_int, [P, c_int64, c_int64, c_int64, P, c_int64, P, c_int64, P]),

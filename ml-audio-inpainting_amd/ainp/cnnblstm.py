@@ -97,7 +97,7 @@ class _ConvStackFn(torch.autograd.Function):
                 gamma, beta = params[pi], params[pi + 1]
                 pi += 2
                 if training:
-                    C = y.shape[1]
+                    C = w.shape[0]
                     rm = bn.running_mean if bn.track_running_stats else None
                     rv = bn.running_var if bn.track_running_stats else None
                     mom = bn.momentum if bn.momentum is not None else 0.1
@@ -124,19 +124,27 @@ class _ConvStackFn(torch.autograd.Function):
         if nbt:
             torch._foreach_add_(nbt, 1)
         last = affine[-1]
-        if last is not None and l0_box is not None and _l0_bf16_ok(saved_y[-1]):
+        yl = saved_y[-1]
+        ylcl = lays[-1][1] if lays else False        # the last block's y channel-last
+        yshape = (N, ws_[-1].shape[0], H, W)
+        if last is not None and l0_box is not None and _l0_bf16_ok(yshape):
             # bf16 configuration: the LSTM's layer-0 operands are written as bf16
             # X / X^T for the bf16-operand GEMMs (gemm16.hip); the fp32 NTCF
             # tensor is never materialised -- autograd gets a stride-0
             # placeholder of its shape, and its gradient (dX, fp32) as usual
-            yl = saved_y[-1]
-            l0_box["x16"] = ops.bn_relu_apply_ntcf_bf16(yl, last[0], last[1])
-            Nl, Cl, Hl, Wl = yl.shape
+            if ylcl:
+                l0_box["x16"] = ops.bn_relu_apply_ntcf_cl(yl, last[0], last[1], out32=False,
+                                                          out16=True)[1]
+            else:
+                l0_box["x16"] = ops.bn_relu_apply_ntcf_bf16(yl, last[0], last[1])
+            Nl, Cl, Hl, Wl = yshape
             out = torch.zeros((), device=yl.device).expand(Nl, Wl, Cl * Hl)
+        elif last is not None and ylcl:
+            out = ops.bn_relu_apply_ntcf_cl(yl, last[0], last[1])[0]
         elif last is not None:
-            out = ops.bn_relu_apply(saved_y[-1], last[0], last[1], ntcf=out_ntcf)
+            out = ops.bn_relu_apply(yl, last[0], last[1], ntcf=out_ntcf)
         else:
-            out = saved_y[-1]
+            out = yl
         ctx.spec = spec
         ctx.lays = lays
         ctx.bf16 = bf16
@@ -251,12 +259,14 @@ class _ConvStackFn(torch.autograd.Function):
         return (gx, None, None, None, None, None, None, None, *grads)
 
 
-# Round 5: channel-last activations ([N, F, T, C]) between the 16/32-channel
-# convs of both conv stacks (AINP_CL=0: NCHW everywhere, as before).  The
-# 64-channel encoder output stays NCHW (the NTCF bridge to the LSTM and its
-# BatchNorm backward read it), so does the projection's 16-channel decoder
-# input; 1-channel tensors are the same in either layout.
+# Round 5: channel-last activations ([N, F, T, C]) between the convs of both
+# conv stacks (AINP_CL=0: NCHW everywhere, as before).  The projection's
+# 16-channel decoder input stays NCHW (the GEMM writes it); 1-channel tensors
+# are the same in either layout.
 CL = os.environ.get("AINP_CL", "1") != "0"
+# the encoder's 64-channel output channel-last too (AINP_CL_BRIDGE=0: NCHW,
+# bridged by the NCHW <-> NTCF kernels)
+CL_BRIDGE = os.environ.get("AINP_CL_BRIDGE", "1") != "0"
 
 
 def _cl_layouts(ws, N, H, W, out_ntcf, cin0):
@@ -269,9 +279,10 @@ def _cl_layouts(ws, N, H, W, out_ntcf, cin0):
     for i, w in enumerate(ws):
         cout = w.shape[0]
         last = i == nb - 1
-        # channel-last where a consumer conv reads it; NCHW for the bridge /
-        # the stack's 1-channel output
-        outs.append(not last and cout > 1)
+        # channel-last where a consumer conv reads it, and for the encoder's
+        # 64-channel output (the channel-last NTCF bridge, bn.hip); the
+        # decoder's 1-channel output is the same either way
+        outs.append((not last and cout > 1) or (last and out_ntcf and cout == 64 and CL_BRIDGE))
     lays = []
     for i in range(nb):
         xin_cl = outs[i - 1] if i > 0 else False   # stack input: NCHW (or 1 channel)

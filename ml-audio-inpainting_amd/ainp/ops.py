@@ -170,6 +170,20 @@ def stft(audio: torch.Tensor, n_fft: int = 2048, hop_length: int = 512,
     return out.reshape(*lead, F, n_frames)
 
 
+# ------------------------------------------------------------ work accounting
+# bench.py's in-step roofline table for the GAN step: while WORK_TRACE is a
+# list, the GAN conv / D-backward launches below append (kernel-name
+# substring, algorithmic FLOP) -- the name of the kernel the C side routes the
+# launch to (include/ainp.h; default variants), the FLOP of the layer's
+# product (2 * outputs * Cin * k * k).  Off (None) otherwise.
+WORK_TRACE = None
+
+
+def _work(name, flop):
+    if WORK_TRACE is not None:
+        WORK_TRACE.append((name, float(flop)))
+
+
 # --------------------------------------------------------------------- GEMM
 # ainp_gemm_f32_ex precision: False (default) = fp32-accurate three-piece bf16
 # split on the bf16 MFMA (include/ainp.h); True = exact f32 MFMA.  The
@@ -272,6 +286,24 @@ def bn_relu_apply_ntcf_bf16(y, scale, shift):
     outT = torch.empty(K, ldt, device=y.device, dtype=torch.bfloat16)[:, :NW]
     _T.bn_relu_apply_ntcf_bf16(y, scale, shift, out, outT, _y_flag(y))
     return out, outT
+
+
+def bn_relu_apply_ntcf_cl(y, scale, shift, out32=True, out16=False):
+    """ainp_bn_relu_apply_ntcf_cl (round 5): relu(y*scale+shift) of a
+    channel-last y [N, H, W, 64] as the LSTM input: fp32 X [N, W, 64*H]
+    (out32) and / or the bf16 X [N, W, 64*H] and X^T [64*H, N*W] (out16, row
+    stride rounded up to 8 elements).  Returns (X or None, (X16, XT16) or None)."""
+    _req(y, "y", None)
+    N, H, W, C = y.shape
+    K, NW = C * H, N * W
+    out = torch.empty(N, W, K, device=y.device, dtype=torch.float32) if out32 else None
+    o16 = oT = None
+    if out16:
+        o16 = torch.empty(N, W, K, device=y.device, dtype=torch.bfloat16)
+        ldt = -(-NW // 8) * 8
+        oT = torch.empty(K, ldt, device=y.device, dtype=torch.bfloat16)[:, :NW]
+    _T.bn_relu_apply_ntcf_cl(y, scale, shift, out, o16, oT, _y_flag(y))
+    return out, ((o16, oT) if out16 else None)
 
 
 def cast_bf16_t(x, out=None, outT=None):
@@ -592,6 +624,7 @@ def gemm_bf16nt_splitk(A, B, K, out=None, max_split=16):
     if not out.is_contiguous():
         raise ValueError("gemm_bf16nt_splitk: out must be contiguous")
     S = _splitk_bf16(M, N, K, max_split=max_split)
+    _work("gemm_bf16nt", 2.0 * M * N * K)
     if S == 1:
         _T.gemm_bf16nt(A, B, out, int(K), None, None, None, None, 0, 1, int(K))
         return out
@@ -1121,6 +1154,19 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
                 raise ValueError("conv_gen: mask plane must be [N, Hs, Ws] of its source")
     Ho, Wo = conv_out_size(Hin, KH, stride, pad), conv_out_size(Win, KW, stride, pad)
     ch, cw = (0, 0) if crop is None else crop
+    if WORK_TRACE is not None and not launcher:
+        flop = 2.0 * N * Cout * Cin * KH * KW * ((ch * cw) if (Cout == 1 and crop) else Ho * Wo)
+        if bf16 and Cout > 1 and crop is None and _nhwc16_route(C0, C1, H0, W0, Hin, Win, KH, KW,
+                                                                 Cout, want_stats):
+            nm = ("conv_gen_nhwc16_wide_kernel<256" if Cout > 128 else
+                  "conv_gen_nhwc16_wide_kernel<128" if Cout > 64 else "conv_gen_nhwc16_kernel<64")
+        elif Cout == 1:
+            nm = "conv_cout1_partial_kernel"
+        elif _direct_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats):
+            nm = "conv_gen_smallcin_kernel"
+        else:
+            nm = "conv_gen_x6_kernel" if not bf16 else "conv_gen"
+        _work(nm, flop)
     if out is None:
         if Cout == 1 and crop is not None:
             out = torch.empty(N, ch, cw, device=x0.device, dtype=torch.float32)
@@ -1406,6 +1452,7 @@ def wgrad_cout1(x, g, nslab, y, slope, k, stride, pad):
     """ainp_wgrad_cout1: [dW | db] [1, Cin*k*k + 1] of a Cout = 1 conv from the
     fp32 input x [N, Cin, H, W] and nslab slabs of g [N, 1, Ho, Wo]."""
     _req(x, "x"); _req(g, "g")
+    _work("wgrad_cout1_kernel", 2.0 * x.shape[0] * g.shape[-2] * g.shape[-1] * x.shape[1] * k * k)
     gw = torch.empty(1, x.shape[1] * k * k + 1, device=x.device)
     ws = torch.empty(_lib.lib.ainp_wgrad_cout1_workspace(x.shape[1], k) // 4, device=x.device)
     _T.wgrad_cout1(x, g, int(nslab), y, float(slope), int(k), int(stride), int(pad), gw, ws)
@@ -1459,6 +1506,7 @@ def dgrad16(gT, wd, Cin, H, W, k, stride, pad, scale=None, nsplit=1):
     """ainp_dgrad16: gT bf16 [N, Ho, Wo, Cout] -> dx fp32 [nsplit, N, Cin, H, W]
     (split-K partial slabs; nsplit == 1: the data gradient itself)."""
     N = gT.shape[0]
+    _work("dgrad16_kernel", 2.0 * gT.numel() * Cin * k * k)
     out = torch.empty(nsplit, N, Cin, H, W, device=gT.device, dtype=torch.float32)
     _T.dgrad16(gT, wd, int(Cin), int(H), int(W), int(k), int(stride), int(pad), scale, out,
                int(nsplit))
@@ -1498,6 +1546,7 @@ def dgrad16_prep(gT, wd, Cin, H, W, k, stride, pad, y, slope, ldA, scale=None, w
     pass -> (gA bf16 [Cin, ldA], gT bf16 [N*H*W, Cin] or None), the lower
     layer's gradient operands, bit for bit those of the two calls."""
     N = gT.shape[0]
+    _work("dgrad16_kernel", 2.0 * gT.numel() * Cin * k * k)
     gA = torch.empty(Cin, ldA, device=gT.device, dtype=torch.bfloat16)
     gTo = (torch.empty(N * H * W, Cin, device=gT.device, dtype=torch.bfloat16)
            if want_gT else None)

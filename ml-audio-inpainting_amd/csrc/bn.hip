@@ -529,6 +529,229 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_cl(
   }
 }
 
+
+// Channel-last <-> NTCF (round 5): the encoder's last block with y channel-
+// last [N][H][W][64] and the LSTM side in [N][W][64*H] (feature c*H + h,
+// model.py:73-74).  Tiles of 64 pixels x 64 channels transposed through LDS
+// ([c][pixel], rows padded to 65 floats): a thread owns 16 consecutive
+// channels of one pixel (4 threads per pixel, 64- / 32-byte loads), a wave
+// then writes 16 channel rows of 64 pixels (256 / 128-byte runs).
+//  * bridge, X role: tile (n, t, 64 rows h): X[n][t][c*H + h] fp32 and / or
+//    bf16 -- 64 consecutive h per channel;
+//  * bridge, XT role (bf16): tile (n, h, 64 columns t): XT[c*H + h][n*W + t]
+//    -- 64 consecutive t per channel (the weight gradient's k-contiguous
+//    operand, gemm16.hip);
+//  * backward: tile (n, t, 64 rows h); g (NTCF) into LDS, y (channel-last)
+//    in registers; reduce accumulates per channel across a persistent
+//    block's tiles, apply writes gy channel-last.  The next tile's loads are
+//    issued before the current tile is processed.
+constexpr int CLN_C = 64;
+
+template <bool YB16>
+__device__ __forceinline__ void cln_ld16(const void* y, int64_t e, float (&v)[16]) {
+  if constexpr (YB16) {
+    const uint4* p = reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(y) + e);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint4 q = p[h];
+      const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[8 * h + 2 * j] = __uint_as_float(w[j] << 16);
+        v[8 * h + 2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      }
+    }
+  } else {
+    const float4* p = reinterpret_cast<const float4*>(reinterpret_cast<const float*>(y) + e);
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const float4 a = p[h];
+      v[4 * h] = a.x; v[4 * h + 1] = a.y; v[4 * h + 2] = a.z; v[4 * h + 3] = a.w;
+    }
+  }
+}
+
+template <bool YB16>
+__global__ __launch_bounds__(256) void bn_relu_apply_ntcf_cl(
+    const void* __restrict__ y, const float* __restrict__ scale, const float* __restrict__ shift,
+    float* __restrict__ out, uint16_t* __restrict__ out16, uint16_t* __restrict__ outT,
+    int64_t ld_t, int H, int W, int64_t nx, int ntf, int ntt) {
+  __shared__ float tile[CLN_C][65];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, pr = tid >> 2, q = tid & 3;
+  int64_t b = blockIdx.x;
+  const bool xt = b >= nx;
+  int n, h0, t0;
+  if (!xt) {                       // (n, t, 64 rows)
+    t0 = (int)(b % W);
+    h0 = (int)((b / W) % ntf) * 64;
+    n = (int)(b / ((int64_t)W * ntf));
+  } else {                         // (n, h, 64 columns)
+    b -= nx;
+    t0 = (int)(b % ntt) * 64;
+    h0 = (int)((b / ntt) % H);
+    n = (int)(b / ((int64_t)ntt * H));
+  }
+  const int h = xt ? h0 : h0 + pr, t = xt ? t0 + pr : t0;
+  float v[16];
+  if (h < H && t < W) {
+    cln_ld16<YB16>(y, (((int64_t)n * H + h) * W + t) * CLN_C + 16 * q, v);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = fmaxf(fmaf(v[j], scale[16 * q + j], shift[16 * q + j]), 0.f);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) v[j] = 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) tile[16 * q + j][pr] = v[j];
+  __syncthreads();
+  if (!xt) {
+    const int hh = h0 + lane;
+    if (hh < H) {
+      const int64_t row = ((int64_t)n * W + t0) * CLN_C * H + hh;
+#pragma unroll 4
+      for (int it = 0; it < 16; ++it) {
+        const int c = 16 * wave + it;
+        const float val = tile[c][lane];
+        if (out) out[row + (int64_t)c * H] = val;
+        if (out16) out16[row + (int64_t)c * H] = __builtin_bit_cast(uint16_t, (__bf16)val);
+      }
+    }
+  } else {
+    const int tt = t0 + lane;
+    if (tt < W) {
+#pragma unroll 4
+      for (int it = 0; it < 16; ++it) {
+        const int c = 16 * wave + it;
+        outT[((int64_t)c * H + h0) * ld_t + (int64_t)n * W + tt] =
+            __builtin_bit_cast(uint16_t, (__bf16)tile[c][lane]);
+      }
+    }
+  }
+}
+
+template <bool APPLY, bool YB16, bool GY16>
+__global__ __launch_bounds__(256) void bn_relu_bwd_ntcf_cl(
+    const float* __restrict__ g, const void* __restrict__ y, const float* __restrict__ scale,
+    const float* __restrict__ shift, const float* __restrict__ gamma,
+    const float* __restrict__ save, const double* __restrict__ sums, double* __restrict__ partial,
+    void* __restrict__ gy, float* __restrict__ dgamma, float* __restrict__ dbeta, int H, int W,
+    int ntf, int64_t ntiles, double inv_count) {
+  __shared__ float tile[CLN_C][65];
+  __shared__ double red[4][2 * CLN_C];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, pr = tid >> 2, q = tid & 3;
+  if (APPLY && blockIdx.x == 0 && tid < CLN_C) {
+    if (dbeta) dbeta[tid] = (float)sums[tid];
+    if (dgamma) dgamma[tid] = (float)sums[CLN_C + tid];
+  }
+  float sc[16], sh[16], mu[16], rs[16], a1[16], a2[16];
+  double ic = 0.0;
+  if (APPLY) ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * CLN_C];   // see bn_finalize
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int c = 16 * q + j;
+    sc[j] = scale[c];
+    sh[j] = shift[c];
+    mu[j] = save[c];
+    rs[j] = save[CLN_C + c];
+    if (APPLY) {
+      a1[j] = (float)(sums[c] * ic);                              // m1
+      a2[j] = (float)(sums[CLN_C + c] * ic);                      // m2
+    } else {
+      a1[j] = a2[j] = 0.f;                                        // s1, s2
+    }
+  }
+  auto coords = [&](int64_t b, int& n, int& h0, int& t) {
+    t = (int)(b % W);
+    h0 = (int)((b / W) % ntf) * 64;
+    n = (int)(b / ((int64_t)W * ntf));
+  };
+  float gr[16], yr[16];
+  auto load = [&](int64_t b) {
+    int n, h0, t;
+    coords(b, n, h0, t);
+    const int hh = h0 + lane;
+    const float* gp = g + ((int64_t)n * W + t) * CLN_C * H + hh;
+#pragma unroll
+    for (int it = 0; it < 16; ++it) gr[it] = hh < H ? gp[(int64_t)(16 * wave + it) * H] : 0.f;
+    const int h = h0 + pr;
+    if (h < H) {
+      cln_ld16<YB16>(y, (((int64_t)n * H + h) * W + t) * CLN_C + 16 * q, yr);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) yr[j] = 0.f;
+    }
+  };
+  int64_t b = blockIdx.x;
+  if (b < ntiles) load(b);
+  for (; b < ntiles; b += gridDim.x) {
+#pragma unroll
+    for (int it = 0; it < 16; ++it) tile[16 * wave + it][lane] = gr[it];
+    float yc[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) yc[j] = yr[j];
+    int n, h0, t;
+    coords(b, n, h0, t);
+    __syncthreads();
+    if (b + gridDim.x < ntiles) load(b + gridDim.x);   // in flight during this tile
+    const int h = h0 + pr;
+    float o[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const float gz = fmaf(yc[j], sc[j], sh[j]) > 0.f ? tile[16 * q + j][pr] : 0.f;
+      const float xh = (yc[j] - mu[j]) * rs[j];
+      if (APPLY) {
+        const float k = (gamma ? gamma[16 * q + j] : 1.f) * rs[j];
+        o[j] = k * (gz - a1[j] - xh * a2[j]);
+      } else if (h < H) {
+        a1[j] += gz;
+        a2[j] += gz * xh;
+      }
+    }
+    if (APPLY && h < H) {
+      const int64_t e = (((int64_t)n * H + h) * W + t) * CLN_C + 16 * q;
+      if constexpr (GY16) {
+        uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(gy) + e);
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          uint32_t w[4];
+#pragma unroll
+          for (int jj = 0; jj < 4; ++jj)
+            w[jj] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[8 * hh + 2 * jj]) |
+                    ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[8 * hh + 2 * jj + 1]) << 16);
+          d[hh] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+      } else {
+        float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(gy) + e);
+#pragma unroll
+        for (int hh = 0; hh < 4; ++hh)
+          d[hh] = make_float4(o[4 * hh], o[4 * hh + 1], o[4 * hh + 2], o[4 * hh + 3]);
+      }
+    }
+    __syncthreads();   // the tile is re-written next iteration
+  }
+  if (APPLY) return;
+  // lanes of one channel quarter (== q mod 4): xor 4 .. 32, fixed order
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      a1[j] += __shfl_xor(a1[j], o, 64);
+      a2[j] += __shfl_xor(a2[j], o, 64);
+    }
+  if (lane < 4) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      red[wave][16 * lane + j] = a1[j];
+      red[wave][CLN_C + 16 * lane + j] = a2[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * CLN_C)
+    partial[(int64_t)blockIdx.x * 2 * CLN_C + tid] =
+        red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
+}
+constexpr int CLN_BLOCKS = 1024;   // persistent blocks of the backward passes
+
 // ----------------------------------------------------------- NTCF path
 // The encoder's last BatchNorm+ReLU reads / writes the LSTM layout
 // [n][w][c*H + h] (model.py:73-74) while y is NCHW: 64(h) x 64(w) tiles of one
@@ -932,6 +1155,30 @@ extern "C" int ainp_bn_relu_apply_ntcf_bf16_ex(const float* x, const float* scal
   return check_launch("bn_relu_apply_ntcf_bf16");
 }
 
+// Round 5: the bridge from a channel-last y ([N][H][W][64], AINP_BN_Y16: bf16
+// storage): out (fp32) / out16 (bf16) = relu(y*scale+shift) as [N][W][64*H],
+// outT (bf16) as [64*H][ld_t] (column n*W + w); NULL outputs are skipped.
+extern "C" int ainp_bn_relu_apply_ntcf_cl(const float* y, const float* scale, const float* shift,
+                                          float* out, uint16_t* out16, uint16_t* outT,
+                                          int64_t ld_t, int64_t N, int C, int64_t H, int64_t W,
+                                          int flags, void* stream) {
+  if (!y || !scale || !shift || (!out && !out16 && !outT) || N < 1 || C != CLN_C || H < 1 ||
+      W < 1 || (outT && ld_t < N * W) || (reinterpret_cast<uintptr_t>(y) & 15) ||
+      (flags & ~AINP_BN_Y16) || H * W * C >= ((int64_t)1 << 31))
+    return record_msg("ainp_bn_relu_apply_ntcf_cl: bad argument (C = 64, 16-byte aligned y)");
+  const int ntf = (int)cdiv(H, 64), ntt = (int)cdiv(W, 64);
+  const int64_t nx = (out || out16) ? N * W * ntf : 0;
+  const int64_t nxt = outT ? N * H * ntt : 0;
+  const dim3 grid((unsigned)(nx + nxt));
+  if (flags & AINP_BN_Y16)
+    hipLaunchKernelGGL(bn_relu_apply_ntcf_cl<true>, grid, dim3(256), 0, as_stream(stream), y,
+                       scale, shift, out, out16, outT, ld_t, (int)H, (int)W, nx, ntf, ntt);
+  else
+    hipLaunchKernelGGL(bn_relu_apply_ntcf_cl<false>, grid, dim3(256), 0, as_stream(stream), y,
+                       scale, shift, out, out16, outT, ld_t, (int)H, (int)W, nx, ntf, ntt);
+  return check_launch("bn_relu_apply_ntcf_cl");
+}
+
 extern "C" int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale,
                                             const float* shift, uint16_t* out, uint16_t* outT,
                                             int64_t ld_t, int64_t N, int C, int64_t H, int64_t W,
@@ -942,7 +1189,8 @@ extern "C" int ainp_bn_relu_apply_ntcf_bf16(const float* x, const float* scale,
 extern "C" size_t ainp_bn_relu_bwd_workspace(int64_t N, int C, int64_t H,
                                              int64_t W) {
   const int64_t tiled = N * C * tiles_per_plane(H, W) * 2;
-  const int64_t cl = cdiv(N * H * W, BNC_PIX) * 2 * C;   // channel-last partials
+  int64_t cl = cdiv(N * H * W, BNC_PIX) * 2 * C;   // channel-last partials
+  if (cl < (int64_t)CLN_BLOCKS * 2 * C) cl = (int64_t)CLN_BLOCKS * 2 * C;
   return (size_t)(tiled > cl ? tiled : cl) * sizeof(double);
 }
 
@@ -988,14 +1236,33 @@ static bool bn_cl_ok(int C, std::initializer_list<const void*> ptrs) {
 }
 
 static int bn_cl_reduce(const float* g, const float* y, const float* scale, const float* shift,
-                        const float* save, void* workspace, double* sums, int64_t P, int C,
-                        int g_ntcf, int flags, hipStream_t s) {
+                        const float* save, void* workspace, double* sums, int64_t N, int64_t H,
+                        int64_t W, int C, int g_ntcf, int flags, hipStream_t s) {
+  const int64_t P = N * H * W;
+  double* partial = reinterpret_cast<double*>(workspace);
+  const bool g16 = flags & AINP_BN_G16, y16 = flags & AINP_BN_Y16;
+  if ((flags & AINP_BN_CL) && g_ntcf) {   // g NTCF fp32, y channel-last (64 channels)
+    if (C != CLN_C || g16 || !bn_cl_ok(C, {y}) || H * W * C >= ((int64_t)1 << 31))
+      return record_msg("ainp_bn_relu_bwd_reduce: NTCF g with channel-last y needs C = 64, "
+                        "fp32 g, 16-byte aligned y");
+    const int ntf = (int)cdiv(H, 64);
+    const int64_t ntiles = N * W * ntf;
+#define AINP_BNN(YV)                                                                             \
+    hipLaunchKernelGGL((bn_relu_bwd_ntcf_cl<false, YV, false>), dim3(CLN_BLOCKS), dim3(256), 0, s, \
+                       g, y, scale, shift, nullptr, save, nullptr, partial, nullptr, nullptr,     \
+                       nullptr, (int)H, (int)W, ntf, ntiles, 0.0)
+    if (y16) AINP_BNN(true); else AINP_BNN(false);
+#undef AINP_BNN
+    int rc = check_launch("bn_relu_bwd_ntcf_cl");
+    if (rc) return rc;
+    hipLaunchKernelGGL(bn_cl_partials_sum, dim3(1), dim3(256), 0, s, partial, CLN_BLOCKS, 2 * C,
+                       sums);
+    return check_launch("bn_cl_partials_sum");
+  }
   if (!(flags & AINP_BN_CL) || g_ntcf || !bn_cl_ok(C, {g, y}))
     return record_msg("ainp_bn_relu_bwd_reduce: AINP_BN_CL needs C % 8 == 0 (<= 64), 16-byte "
                       "aligned g / y and no NTCF layout (AINP_BN_G16 needs AINP_BN_CL)");
   const int64_t nblk = cdiv(P, BNC_PIX);
-  double* partial = reinterpret_cast<double*>(workspace);
-  const bool g16 = flags & AINP_BN_G16, y16 = flags & AINP_BN_Y16;
 #define AINP_BNCR(CV, GV, YV)                                                                   \
   if (C == CV && g16 == GV && y16 == YV)                                                        \
     hipLaunchKernelGGL((bn_relu_bwd_reduce_cl<CV, GV, YV>), dim3((unsigned)nblk), dim3(256), 0, s, \
@@ -1015,12 +1282,32 @@ static int bn_cl_reduce(const float* g, const float* y, const float* scale, cons
 
 static int bn_cl_apply(const float* g, const float* y, const float* scale, const float* shift,
                        const float* gamma, const float* save, const double* sums, int64_t count,
-                       void* gy, float* dgamma, float* dbeta, int64_t P, int C, int g_ntcf,
-                       int flags, hipStream_t s) {
+                       void* gy, float* dgamma, float* dbeta, int64_t N, int64_t H, int64_t W,
+                       int C, int g_ntcf, int flags, hipStream_t s) {
+  const int64_t P = N * H * W;
+  const double inv_count = count > 0 ? 1.0 / (double)count : 0.0;   // 0: sums[2C]
+  if ((flags & AINP_BN_CL) && g_ntcf) {   // g NTCF fp32, y / gy channel-last (64 channels)
+    if (C != CLN_C || (flags & AINP_BN_G16) || !bn_cl_ok(C, {y, gy}) ||
+        H * W * C >= ((int64_t)1 << 31))
+      return record_msg("ainp_bn_relu_bwd_apply: NTCF g with channel-last y needs C = 64, "
+                        "fp32 g, 16-byte aligned y / gy");
+    const int ntf = (int)cdiv(H, 64);
+    const int64_t ntiles = N * W * ntf;
+    const bool y16 = flags & AINP_BN_Y16, o16 = flags & AINP_BN_GY16;
+#define AINP_BNN(YV, OV)                                                                         \
+    hipLaunchKernelGGL((bn_relu_bwd_ntcf_cl<true, YV, OV>), dim3(CLN_BLOCKS), dim3(256), 0, s, g, \
+                       y, scale, shift, gamma, save, sums, nullptr, gy, dgamma, dbeta, (int)H,    \
+                       (int)W, ntf, ntiles, inv_count)
+    if (y16 && o16) AINP_BNN(true, true);
+    else if (y16) AINP_BNN(true, false);
+    else if (o16) AINP_BNN(false, true);
+    else AINP_BNN(false, false);
+#undef AINP_BNN
+    return check_launch("bn_relu_bwd_ntcf_cl");
+  }
   if (!(flags & AINP_BN_CL) || g_ntcf || !bn_cl_ok(C, {g, y, gy}))
     return record_msg("ainp_bn_relu_bwd_apply: AINP_BN_CL needs C % 8 == 0 (<= 64), 16-byte "
                       "aligned g / y / gy and no NTCF layout (AINP_BN_G16 needs AINP_BN_CL)");
-  const double inv_count = count > 0 ? 1.0 / (double)count : 0.0;   // 0: sums[2C]
   const int ppb = 256 / (C / 8) * 4;                                 // pixels per block pass
   int64_t nb = cdiv(P, ppb);
   if (nb > 2048) nb = 2048;
@@ -1050,7 +1337,7 @@ extern "C" int ainp_bn_relu_bwd_reduce_ex(const float* g, const float* y, const 
       N < 1 || C < 1 || H < 1 || W < 1 || (flags & ~(AINP_BN_Y16 | AINP_BN_CL | AINP_BN_G16)))
     return record_msg("ainp_bn_relu_bwd_reduce: bad argument");
   if (flags & (AINP_BN_CL | AINP_BN_G16))
-    return bn_cl_reduce(g, y, scale, shift, save_mean_rstd, workspace, sums, N * H * W, C,
+    return bn_cl_reduce(g, y, scale, shift, save_mean_rstd, workspace, sums, N, H, W, C,
                         g_ntcf, flags, as_stream(stream));
   if (flags & AINP_BN_Y16)
     return bn_bwd_reduce_launch<true>(g, y, scale, shift, save_mean_rstd, workspace, sums, N, C,
@@ -1089,7 +1376,7 @@ extern "C" int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const f
   hipStream_t s = as_stream(stream);
   if (flags & (AINP_BN_CL | AINP_BN_G16))
     return bn_cl_apply(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy, dgamma, dbeta,
-                       N * H * W, C, g_ntcf, flags, s);
+                       N, H, W, C, g_ntcf, flags, s);
 #define AINP_BNA(GV, YV)                                                                       \
   return bn_bwd_apply_launch<GV, YV>(g, y, scale, shift, gamma, save_mean_rstd, sums, count, gy, \
                                      dgamma, dbeta, N, C, H, W, g_ntcf, s)

@@ -766,7 +766,7 @@ __global__ __launch_bounds__(384 / PX) void conv3x3_small_fwd(
       for (int q = 0; q < PX; ++q)
         if (ok[q]) {
           a += acc[q][co];
-          b += acc[q][co] * acc[q][co];
+          b = fmaf(acc[q][co], acc[q][co], b);   // explicit: every instance rounds alike
         }
       a = wave_sum(a);
       b = wave_sum(b);

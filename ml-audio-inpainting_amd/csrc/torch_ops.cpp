@@ -864,6 +864,40 @@ uint16_t* bf16p(const Tensor& t, const char* name, bool contig = true) {
   return reinterpret_cast<uint16_t*>(dev<void>(t, name, at::kBFloat16, contig));
 }
 
+// Round 5: the bridge from a channel-last y [N,H,W,64]; any of out (fp32
+// [N,W,64*H]), out16 (bf16, same), outT (bf16 [64*H, >= N*W]) may be absent.
+void bn_relu_apply_ntcf_cl(const Tensor& y, const Tensor& scale, const Tensor& shift,
+                           const OptT& out, const OptT& out16, const OptT& outT, int64_t flags) {
+  GUARD(y);
+  TORCH_CHECK(y.dim() == 4, "y must be channel-last [N,H,W,C]");
+  const int64_t N = y.size(0), H = y.size(1), W = y.size(2), C = y.size(3);
+  numel_is(scale, C, "scale");
+  numel_is(shift, C, "shift");
+  float* o = nullptr;
+  if (out.has_value() && out->defined()) {
+    numel_is(*out, y.numel(), "out");
+    o = dev(*out, "out");
+  }
+  uint16_t* o16 = nullptr;
+  if (out16.has_value() && out16->defined()) {
+    numel_is(*out16, y.numel(), "out16");
+    o16 = bf16p(*out16, "out16");
+  }
+  uint16_t* oT = nullptr;
+  int64_t ld_t = 0;
+  if (outT.has_value() && outT->defined()) {
+    TORCH_CHECK(outT->dim() == 2 && outT->size(0) == C * H && outT->size(1) >= N * W &&
+                    outT->stride(1) == 1,
+                "outT must be [C*H, >= N*W] with contiguous rows");
+    oT = bf16p(*outT, "outT", false);
+    ld_t = outT->stride(0);
+  }
+  chk(ainp_bn_relu_apply_ntcf_cl(f32_or_16(y, "y", flags & AINP_BN_Y16), dev(scale, "scale"),
+                                 dev(shift, "shift"), o, o16, oT, ld_t, N, (int)C, H, W,
+                                 (int)flags, stream_of(y)),
+      "bn_relu_apply_ntcf_cl");
+}
+
 void bn_relu_apply_ntcf_bf16(const Tensor& x, const Tensor& scale, const Tensor& shift,
                              const Tensor& out, const Tensor& outT, int64_t flags) {
   GUARD(x);
@@ -1542,6 +1576,8 @@ TORCH_LIBRARY(ainp, m) {
   m.def("leaky_bwd_ld(Tensor g, Tensor y, int rows, float slope, int ldo, Tensor(a!) out) -> ()");
   m.def("mul(Tensor a, Tensor b, Tensor(a!) out) -> ()");
   m.def("channel_sum(Tensor m, Tensor(a!) out) -> ()");
+  m.def("bn_relu_apply_ntcf_cl(Tensor y, Tensor scale, Tensor shift, Tensor(a!)? out, "
+        "Tensor(b!)? out16, Tensor(c!)? outT, int flags) -> ()");
   m.def("bn_relu_apply_ntcf_bf16(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, "
         "Tensor(b!) outT, int flags=0) -> ()");
   m.def("gemm_bf16nt(Tensor A, Tensor B, Tensor(a!) C, int K, Tensor? bias_a1, Tensor? bias_a2, "
@@ -1645,6 +1681,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("mul", &mul);
   m.impl("channel_sum", &channel_sum);
   m.impl("bn_relu_apply_ntcf_bf16", &bn_relu_apply_ntcf_bf16);
+  m.impl("bn_relu_apply_ntcf_cl", &bn_relu_apply_ntcf_cl);
   m.impl("gemm_bf16nt", &gemm_bf16nt);
   m.impl("cast_bf16_t", &cast_bf16_t);
   m.impl("transpose_f32", &transpose_f32);
@@ -1727,6 +1764,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("mul", torch::CppFunction::makeFallthrough());
   m.impl("channel_sum", torch::CppFunction::makeFallthrough());
   m.impl("bn_relu_apply_ntcf_bf16", torch::CppFunction::makeFallthrough());
+  m.impl("bn_relu_apply_ntcf_cl", torch::CppFunction::makeFallthrough());
   m.impl("gemm_bf16nt", torch::CppFunction::makeFallthrough());
   m.impl("cast_bf16_t", torch::CppFunction::makeFallthrough());
   m.impl("transpose_f32", torch::CppFunction::makeFallthrough());

@@ -103,9 +103,7 @@ def test_cl_small_channel_convs(N, H, W, pro):
         xcl, ycl = cin == 16, cout == 16
         y, st = ops.conv3x3_fwd(_cl(x) if xcl else x, w, b, s_, h_, want_stats=True, xcl=xcl,
                                 ycl=ycl)
-        # y bit-identical; the BatchNorm partials of the two template instances
-        # may contract the sum of squares differently (fp32 rounding level)
-        assert torch.equal(_nchw(y) if ycl else y, y0) and rel(st, st0) < 1e-6
+        assert torch.equal(_nchw(y) if ycl else y, y0) and torch.equal(st, st0)
         dx0 = ops.conv3x3_dgrad(dy, w)
         dx = ops.conv3x3_dgrad(_cl(dy) if ycl else dy, w, xcl=ycl, ycl=xcl)
         assert torch.equal(_nchw(dx) if xcl else dx, dx0)
@@ -155,8 +153,8 @@ def test_cl_bn_relu_backward(C, store):
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_cnnblstm_step_channel_last_matches_nchw(monkeypatch, dtype):
     """One training step of the CNNBLSTM at the C2 plane (N=4) with the
-    channel-last conv stacks (default) and with NCHW (AINP_CL=0): every
-    gradient within 1e-5 (the BatchNorm backward sums in another order)."""
+    channel-last conv stacks (default) and with NCHW (AINP_CL=0): the same
+    loss, every gradient within 2e-4 (fp32) / 2e-3 (bf16)."""
     from ainp import cnnblstm
     cfg = {"data": {"sample_rate": 16000, "spectrogram": {"n_fft": 512, "hop_length": 192,
                                                           "win_length": 384}},
@@ -179,11 +177,55 @@ def test_cnnblstm_step_channel_last_matches_nchw(monkeypatch, dtype):
         loss = cnnblstm.l1_pow10_loss(m(x), mask, tgt)
         loss.backward()
         torch.cuda.synchronize()
-        res.append((float(loss), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
-    tol = 1e-5 if dtype == "fp32" else 2e-3
-    assert abs(res[0][0] - res[1][0]) <= 1e-6 * abs(res[1][0])
+        res.append((float(loss.detach()),
+                    {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    # the forward is bit-identical (same conv staging and MFMA chains, same
+    # BatchNorm partials); the BatchNorm backward sums in another order, which
+    # the cancellation in gamma*rstd*(gz - mean(gz) - xhat*mean(gz*xhat))
+    # amplifies towards the encoder's first conv (5e-5 there in fp32)
+    tol = 2e-4 if dtype == "fp32" else 2e-3
+    assert res[0][0] == res[1][0]
+    errs = {}
     for n, g1 in res[1][1].items():
         if n in ("encoder.0.bias", "encoder.3.bias", "encoder.6.bias", "decoder.0.bias",
                  "decoder.3.bias"):
             continue   # BatchNorm-fed conv biases: exact gradient 0
-        assert rel(res[0][1][n], g1) < tol, n
+        errs[n] = rel(res[0][1][n], g1)
+    bad = {n: e for n, e in errs.items() if e >= tol}
+    assert not bad, (bad, max(errs.values()))
+
+
+@pytest.mark.parametrize("y16", [False, True])
+@pytest.mark.parametrize("H,W", [(257, 334), (130, 70)])
+def test_cl_ntcf_bridge_and_backward(y16, H, W):
+    """The encoder's last block with y channel-last: the bridge to the LSTM
+    layout (fp32 X, bf16 X / X^T) bit-identical to the NCHW bridges; the
+    BatchNorm backward from the NTCF gradient within 1e-6 (sums) / bit-level
+    (apply of the same sums)."""
+    from ainp import ops
+    N, C = 2, 64
+    g = torch.Generator(device=DEV).manual_seed(H + W)
+    y = torch.randn(N, C, H, W, device=DEV, generator=g)
+    if y16:
+        y = y.to(torch.bfloat16)
+    sc = torch.rand(C, device=DEV, generator=g) + 0.5
+    sh = torch.randn(C, device=DEV, generator=g) * 0.3
+    save = torch.stack([torch.randn(C, device=DEV, generator=g) * 0.1,
+                        torch.rand(C, device=DEV, generator=g) + 0.5])
+    gamma = torch.rand(C, device=DEV, generator=g) + 0.5
+    X0 = ops.bn_relu_apply(y.float(), sc, sh, ntcf=True)
+    X1, x16 = ops.bn_relu_apply_ntcf_cl(_cl(y), sc, sh, out32=True, out16=True)
+    assert torch.equal(X1, X0)
+    X16_0, XT16_0 = ops.bn_relu_apply_ntcf_bf16(y, sc, sh)
+    assert torch.equal(x16[0], X16_0) and torch.equal(x16[1], XT16_0)
+    gr = torch.randn(N, W, C * H, device=DEV, generator=g)
+    s0 = ops.bn_relu_bwd_reduce(gr, y, sc, sh, save, ntcf=True)
+    s1 = ops.bn_relu_bwd_reduce(gr, _cl(y), sc, sh, save, ntcf=True, cl=True)
+    assert rel(s1, s0) < 1e-6
+    for gy16 in (False, True):
+        gy0, dg0, db0 = ops.bn_relu_bwd_apply(gr, y, sc, sh, gamma, save, s0, N * H * W,
+                                              ntcf=True, gy16=gy16)
+        gy1, dg1, db1 = ops.bn_relu_bwd_apply(gr, _cl(y), sc, sh, gamma, save, s0, N * H * W,
+                                              ntcf=True, gy16=gy16, cl=True)
+        assert rel(_nchw(gy1).float(), gy0.float()) < (4e-3 if gy16 else 1e-6)
+        assert torch.equal(dg1, dg0) and torch.equal(db1, db0)

@@ -525,7 +525,9 @@ def test_small_wgrad_strip_matches_tile_kernel(ops, monkeypatch, Cin, Cout, pro)
     monkeypatch.setenv("AINP_SMALL_WGRAD_TILE", "1")
     tw, tb = ops.conv3x3_wgrad(x, dy, sc, sh)
     assert rel(dw.cpu().double(), tw.cpu().double()) < 1e-6
-    assert rel(db.cpu().double(), tb.cpu().double()) < 1e-6
+    # the bias: a sum of 2.7M random terms with heavy cancellation -- against fp64
+    ref = dy.double().sum((0, 2, 3)).cpu()
+    assert rel(db.cpu().double(), ref) < 1e-5 and rel(tb.cpu().double(), ref) < 1e-5
 
 
 # ------------------------------------------------------------------ BN
