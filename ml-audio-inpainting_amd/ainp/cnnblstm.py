@@ -232,7 +232,8 @@ class _ConvStackFn(torch.autograd.Function):
                                lw=lw: ops.conv3x3_wgrad(xin, gy, pr[0], pr[1], bf16=bf,
                                                         out=(dwv, dbv), **lw),
                                (xin, gy) + tuple(t for t in pro if t is not None), (dwv, dbv),
-                               params=ctx.param_objs[p0:p0 + 2], sink=ctx.sink)
+                               params=ctx.param_objs[p0:p0 + 2], sink=ctx.sink,
+                               first=min(Cout, Cin) <= 2)
             elif ctx.defer_wgrad:
                 # off the critical path: on the side stream, overlapping the next
                 # (HBM-bound) BatchNorm backward passes
@@ -297,13 +298,14 @@ WGRAD_LAST_MAIN = os.environ.get("AINP_WGRAD_LAST_MAIN", "1") != "0"
 # bf16 configuration: BatchNorm-backward outputs in bf16 storage (AINP_GY16=0:
 # fp32, as before; the conv results are the same bit for bit)
 GY16 = os.environ.get("AINP_GY16", "1") != "0"
-# bf16 configuration: pre-BatchNorm conv outputs in bf16 storage (AINP_Y16=1;
-# off by default: the C3-shape step measured 9.60 -> 9.67 ms/step with it,
-# profiles/r04kl_summary.txt).  Unlike gy this is a rounding point of its own:
-# the BatchNorm statistics and the BatchNorm+ReLU that feeds the next conv see
-# the bf16 values (autocast's bf16 conv output); tests/golden/gen_golden_r04.py
-# rounds there too when run with AINP_Y16=1.
-Y16 = os.environ.get("AINP_Y16", "0") == "1"
+# bf16 configuration: pre-BatchNorm conv outputs in bf16 storage (AINP_Y16,
+# on by default since round 5: with channel-last activations the C3-shape
+# step measured 8.92 -> 8.48 ms/step with it; round 4's NCHW kernels had
+# measured it slower, 9.60 -> 9.67).  Unlike gy this is a rounding point of
+# its own: the BatchNorm statistics and the BatchNorm+ReLU that feeds the next
+# conv see the bf16 values (autocast's bf16 conv output);
+# tests/golden/gen_golden_r04.py rounds there too (meta/emu_y16 in its fixture).
+Y16 = os.environ.get("AINP_Y16", "1") == "1"
 
 
 def _l0_bf16_ok(y):
@@ -626,10 +628,12 @@ class _Deferred:
     _queues: dict = {}
 
     @classmethod
-    def push(cls, device, fn, inputs, outputs, params=(), sink=None):
+    def push(cls, device, fn, inputs, outputs, params=(), sink=None, first=False):
         """params / sink (data parallel): the Parameters the outputs are the
         gradients of, and the GradAllReducer that all-reduces them from the side
-        stream once they are written (its hooks skip them meanwhile)."""
+        stream once they are written (its hooks skip them meanwhile).
+        first: released ahead of the others (a short job that must not be
+        left to run starved beside the layer-0 GEMM pair)."""
         q = cls._queues.setdefault(device, [])
         if not q:
             torch.autograd.Variable._execution_engine.queue_callback(
@@ -639,7 +643,7 @@ class _Deferred:
                 sink.defer(p)
         else:
             sink = None
-        q.append((fn, inputs, outputs, params, sink))
+        q.append((fn, inputs, outputs, params, sink, first))
 
     @classmethod
     def flush(cls, device, join=False):
@@ -649,9 +653,13 @@ class _Deferred:
             # short full-width GEMM) ahead of the decoder convs' (persistent
             # kernels), so it does not run starved beside the layer-0 pair
             q = q[::-1]
+        # the short 1-channel-side weight gradients first: behind the others
+        # they met the layer-0 GEMM pair, whose 160 KB / full-VGPR workgroups
+        # leave no room on a CU (16 -> 1: 1.6 ms there against 0.05 ms)
+        q = [j for j in q if j[5]] + [j for j in q if not j[5]]
         if q:
             with _side_work(device, callback=False) as sw:
-                for fn, inputs, outputs, params, sink in q:
+                for fn, inputs, outputs, params, sink, _first in q:
                     fn()
                     sw.handoff(inputs, outputs)
                     if sink is not None:

@@ -444,23 +444,24 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_reduce_cl(
     partial[(int64_t)blockIdx.x * 2 * C + tid] = red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
 }
 
-// sums[o] = sum over blocks of partial[block][o], o < 2C: 256 / (2C) threads
-// per output over strided block subsets, then combined in fixed order
+// sums[o] = sum over blocks of partial[block][o], o < C2: one 256-thread
+// block per output, each thread a strided subset of the blocks (in flight
+// together), then a fixed-order tree over the 256 per-thread sums
 __global__ __launch_bounds__(256) void bn_cl_partials_sum(const double* __restrict__ partial,
                                                           int nblk, int C2,
                                                           double* __restrict__ sums) {
   __shared__ double red[256];
-  const int tid = threadIdx.x, per = 256 / C2, o = tid % C2, sub = tid / C2;
+  const int tid = threadIdx.x, o = blockIdx.x;
   double a = 0.0;
-  if (sub < per)
-    for (int b = sub; b < nblk; b += per) a += partial[(int64_t)b * C2 + o];
+  for (int b = tid; b < nblk; b += 256) a += partial[(int64_t)b * C2 + o];
   red[tid] = a;
   __syncthreads();
-  if (tid < C2) {
-    double t = 0.0;
-    for (int k = 0; k < per; ++k) t += red[k * C2 + tid];
-    sums[tid] = t;
+#pragma unroll
+  for (int w = 128; w > 0; w >>= 1) {
+    if (tid < w) red[tid] += red[tid + w];
+    __syncthreads();
   }
+  if (tid == 0) sums[o] = red[0];
 }
 
 template <int C, bool GB16, bool YB16, bool OB16>
@@ -1255,8 +1256,8 @@ static int bn_cl_reduce(const float* g, const float* y, const float* scale, cons
 #undef AINP_BNN
     int rc = check_launch("bn_relu_bwd_ntcf_cl");
     if (rc) return rc;
-    hipLaunchKernelGGL(bn_cl_partials_sum, dim3(1), dim3(256), 0, s, partial, CLN_BLOCKS, 2 * C,
-                       sums);
+    hipLaunchKernelGGL(bn_cl_partials_sum, dim3(2 * C), dim3(256), 0, s, partial, CLN_BLOCKS,
+                       2 * C, sums);
     return check_launch("bn_cl_partials_sum");
   }
   if (!(flags & AINP_BN_CL) || g_ntcf || !bn_cl_ok(C, {g, y}))
@@ -1276,7 +1277,8 @@ static int bn_cl_reduce(const float* g, const float* y, const float* scale, cons
 #undef AINP_BNCR
   int rc = check_launch("bn_relu_bwd_reduce_cl");
   if (rc) return rc;
-  hipLaunchKernelGGL(bn_cl_partials_sum, dim3(1), dim3(256), 0, s, partial, (int)nblk, 2 * C, sums);
+  hipLaunchKernelGGL(bn_cl_partials_sum, dim3(2 * C), dim3(256), 0, s, partial, (int)nblk, 2 * C,
+                     sums);
   return check_launch("bn_cl_partials_sum");
 }
 

@@ -816,13 +816,16 @@ def test_cast_bf16_t_and_ntcf_bf16_bridge_bit_exact():
         assert torch.equal(XT16, X16.reshape(N * W, C * H).T)
 
 
-def test_bf16_layer0_operand_path_matches_staged_bf16_path():
+def test_bf16_layer0_operand_path_matches_staged_bf16_path(monkeypatch):
     """The bf16 configuration's layer-0 path on bf16 operands in HBM (bridge +
     cast + gemm_bf16nt) against the fp32-staged bf16 GEMM loop it replaces, on
     a C2-shaped batch (N*T % 8 == 0): both round every operand to bf16 once, so
     only the fp32 accumulation order differs -- output, loss and every
-    gradient within 1e-4 relative (ReLU-branch flips aside)."""
+    gradient within 1e-4 relative (ReLU-branch flips aside).  The pre-BN bf16
+    storage point (cnnblstm.Y16) of the encoder's last block exists only on
+    the bf16-operand path (its bridge reads bf16 y), so it is off for both."""
     import ainp.cnnblstm as CB
+    monkeypatch.setattr(CB, "Y16", False)
     from ainp.cnnblstm import StackedBLSTMCNN, l1_pow10_loss
     cfg = {"data": {"spectrogram": {"n_fft": 512}},
            "model": {"in_channels": 1, "num_lstm_layers": 2, "lstm_hidden_dim": 128,

@@ -388,6 +388,10 @@ def test_bf16_c2_batch32_forward_backward_tracks_reference(golden_dir):
     # points) is 2e-4 .. 7e-3 per tensor; measured HIP vs emulation: <= 4.6e-3
     # (norms) / 8.6e-3 (samples), profiles/r04a_pytest_bf16gates.log.
     emu = np.load(os.path.join(golden_dir, "cnnblstm_c2_bf16emu.npz"), allow_pickle=False)
+    # the fixture emulates the pre-BatchNorm bf16 storage point iff the run has it
+    from ainp import cnnblstm
+    assert int(emu["meta/emu_y16"][0]) == int(cnnblstm.Y16), \
+        "regenerate cnnblstm_c2_bf16emu.npz with this AINP_Y16 (tests/golden/gen_golden_r04.py)"
     e_y = rel(yf[::97], emu["emu32/y_sample"])
     e_l = abs(loss.item() - emu["emu32/loss"][0]) / emu["emu32/loss"][0]
     eerrs = {}
