@@ -399,6 +399,30 @@ STEP_TABLES = {
 }
 
 
+# One step of the same profiled runs as a kernel trace (tools/step_timeline.py
+# --extract): the main stream's critical path per phase and each stream's busy
+# time -- the in-step kernel times above add up to more than the step, because
+# the side stream's weight gradients overlap the main stream.
+STEP_TRACES = {
+    ("cnnblstm", "fp32"): "profiles/steps/r05_cnn_fp32_step_trace.csv",
+    ("cnnblstm", "bf16"): "profiles/steps/r05_cnn_bf16_step_trace.csv",
+}
+
+
+def step_critical_path(key):
+    """tools/step_timeline.critical_path of the committed one-step trace."""
+    path = STEP_TRACES.get(key)
+    if not path or not os.path.exists(os.path.join(ROOT, path)):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import step_timeline
+    cp = step_timeline.critical_path(step_timeline.load_step(os.path.join(ROOT, path)))
+    cp["trace"] = path
+    cp["critical_path_sum_ms"] = round(sum(cp["critical_path_ms"].values()), 3)
+    cp["span_ms"] = round(cp["span_ms"], 3)
+    return cp
+
+
 def _cnn_step_work(B=32, F=257, T=334, H=128):
     """(name substring, kind, per-step algorithmic work) of the CNNBLSTM step's
     kernels at the C2 / C3 per-GPU shape: FLOP for MFMA kernels, HBM bytes
@@ -487,6 +511,9 @@ def in_step_table(key, bf16, top=8, families=None):
         out.append(e)
     res = {"table": path, "per_step": f"rocprofv3 --kernel-trace --stats of tools/step_prof.py "
                                       f"(totals / {div})", "top": out}
+    cp = step_critical_path(key[:2])
+    if cp is not None:
+        res["timeline"] = cp
     if fam is not None:
         res["families"] = fam
         res["family_work"] = ("FLOP per step of each kernel family from ops.WORK_TRACE over one "

@@ -54,6 +54,7 @@ struct Prob {
   int64_t bias_nsplit;
   int64_t M, N, K, kc, strideC;
   int nsplit, tiles_m, tiles_n;
+  int mfast;                 // groups of 8 tiles walk m first (see gemm_x6r_kernel)
   int64_t items, first;      // work items (tiles x splits), first blockIdx (multiple of 8)
 };
 struct Job {
@@ -291,11 +292,26 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_x6r_kernel(Job job) {
   if (loc >= P.items) return;
   const int64_t tiles = (int64_t)P.tiles_m * P.tiles_n;
   const int64_t split = loc / tiles, t = loc - split * tiles;
-  const int64_t per_group = 8 * (int64_t)P.tiles_m;
-  const int64_t first_n = (t / per_group) * 8;
-  const int64_t gsize = (P.tiles_n - first_n) < 8 ? (P.tiles_n - first_n) : 8;
-  const int64_t in_g = t % per_group;
-  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+  int64_t m0, n0;
+  if (P.mfast) {
+    // few m-tiles (the layer-0 weight gradient dW = dg^T X: 4 gate-row tiles):
+    // a group of 8 consecutive items on one XCD = all tiles_m m-tiles of
+    // 8 / tiles_m n-tiles, so every X panel is streamed into that XCD's L2
+    // once for its 4 m-tiles instead of once per m-tile (the small dg panels
+    // are re-read from the Infinity Cache)
+    const int64_t gn = 8 / P.tiles_m;
+    const int64_t per = (int64_t)P.tiles_m * gn;
+    const int64_t in_g = t % per;
+    m0 = (in_g % P.tiles_m) * BM;
+    n0 = ((t / per) * gn + in_g / P.tiles_m) * BN;
+  } else {
+    const int64_t per_group = 8 * (int64_t)P.tiles_m;
+    const int64_t first_n = (t / per_group) * 8;
+    const int64_t gsize = (P.tiles_n - first_n) < 8 ? (P.tiles_n - first_n) : 8;
+    const int64_t in_g = t % per_group;
+    m0 = (in_g / gsize) * BM;
+    n0 = (first_n + in_g % gsize) * BN;
+  }
   const int64_t kbeg = split * P.kc;
   const int64_t kend = (kbeg + P.kc) < P.K ? (kbeg + P.kc) : P.K;
   // this n-tile's B half (b_nsplit % 256 == 0)
@@ -423,6 +439,14 @@ extern "C" int ainp_gemm_x6_multi(const ainp_x6_problem* probs, int nprobs, void
     d.M = M; d.N = N; d.K = K; d.kc = kc; d.strideC = s.strideC; d.nsplit = nsplit;
     d.tiles_m = (int)cdiv(M, x6r::BM);
     d.tiles_n = (int)cdiv(N, x6r::BN);
+    // m-first groups where 8 / tiles_m n-tiles x tiles_m tiles fill a group of
+    // 8 exactly (AINP_X6R_MFAST=0: n-first everywhere, A/B)
+    static const bool mfast_env = [] {
+      const char* e = getenv("AINP_X6R_MFAST");
+      return !(e && e[0] == '0');
+    }();
+    d.mfast = (mfast_env && (d.tiles_m == 2 || d.tiles_m == 4 || d.tiles_m == 8) &&
+               d.tiles_n >= 8) ? 1 : 0;
     d.items = (int64_t)d.tiles_m * d.tiles_n * nsplit;
     d.first = first;
     first += (d.items + 7) / 8 * 8;

@@ -23,7 +23,10 @@ def recording(model):
 
     def conv(*a, **k):
         out = f_conv(*a, **k)
-        last["y"] = out[0]
+        y = out[0]
+        if k.get("ycl"):                   # channel-last y [N, H, W, C] -> NCHW
+            y = y.permute(0, 3, 1, 2)
+        last["y"] = y.float().contiguous()     # bf16 storage: exact widening
         return out
 
     def record(out):
