@@ -452,9 +452,15 @@ class _BLSTMFn(torch.autograd.Function):
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
             l016 = ctx.l016 if l == 0 else None
             Il = inp.shape[1] if l016 is None else ctx.I
+            if l == L - 1 and DEFER_EARLY:
+                pre = torch.cuda.Event()      # the decoder backward is done here
+                pre.record(main)
             dg = ops.lstm_rec_bwd(dh, gates, cell, hf, hr, H)          # [N,T,8H]
             if l == L - 1:
-                _Deferred.flush(dh.device)   # decoder / projection weight gradients
+                # decoder / projection weight gradients, released behind the
+                # first BPTT launch (DEFER_EARLY: waiting only for the decoder
+                # backward, so they run beside that recurrence too)
+                _Deferred.flush(dh.device, after=pre if DEFER_EARLY else None)
             dg2 = dg.view(NT, 8 * H)
             if l016 is not None:
                 # bf16 operands of the layer-0 data / weight gradients
@@ -614,6 +620,14 @@ def _alias(t):
 # projection's last, behind the layer-0 pair: C2 16.07 -> 15.96 ms/step,
 # profiles/r04kl_summary.txt); AINP_DEFER_LIFO=0: issue order
 DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "1") != "0"
+# the deferred decoder / projection weight gradients wait only for the decoder
+# backward (an event recorded before the first BPTT launch), not for that
+# recurrence as well, so they run beside it on the CUs it leaves idle
+# (AINP_DEFER_EARLY=0: behind it; C2 14.54 -> 13.89, C3-shape 8.55 -> 8.39
+# ms/step on one box, profiles/r05i_ab_defer_early.txt).  A CU-masked side
+# stream (hipExtStreamCreateWithCUMask, 8 of 32 CUs kept free for the
+# recurrence) measured +3.3 ms/step on both and was dropped.
+DEFER_EARLY = os.environ.get("AINP_DEFER_EARLY", "1") != "0"
 
 
 class _Deferred:
@@ -646,7 +660,9 @@ class _Deferred:
         q.append((fn, inputs, outputs, params, sink, first))
 
     @classmethod
-    def flush(cls, device, join=False):
+    def flush(cls, device, join=False, after=None):
+        """after: an event recorded earlier on the current stream for the side
+        stream to wait on instead of everything issued so far."""
         q = cls._queues.pop(device, [])
         if DEFER_LIFO:
             # last queued first: the output projection's weight gradient (a
@@ -658,7 +674,7 @@ class _Deferred:
         # leave no room on a CU (16 -> 1: 1.6 ms there against 0.05 ms)
         q = [j for j in q if j[5]] + [j for j in q if not j[5]]
         if q:
-            with _side_work(device, callback=False) as sw:
+            with _side_work(device, callback=False, after=after) as sw:
                 for fn, inputs, outputs, params, sink, _first in q:
                     fn()
                     sw.handoff(inputs, outputs)
@@ -690,16 +706,19 @@ class _side_work:
     at the end of the backward pass (autograd engine callback), before any
     optimizer step can read what the side stream produced."""
 
-    def __init__(self, device, callback=True):
+    def __init__(self, device, callback=True, after=None):
         self.device = device
         self.callback = callback
+        self.after = after
 
     def __enter__(self):
         dev = self.device
         self.main = torch.cuda.current_stream(dev)
         self.side = _side_stream(dev)
-        ev = torch.cuda.Event()
-        ev.record(self.main)
+        ev = self.after
+        if ev is None:
+            ev = torch.cuda.Event()
+            ev.record(self.main)
         self.side.wait_event(ev)
         self._ctx = torch.cuda.stream(self.side)
         self._ctx.__enter__()

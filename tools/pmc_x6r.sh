@@ -19,7 +19,7 @@ pass() {  # pass <name> <probe-mode> <counters...>
   return $rc
 }
 SQ="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES"
-for mode in fp32 pair; do
+for mode in ${MODES:-fp32 pair}; do
   mkdir -p "$OUT/$mode"
   pass $mode/fetch $mode FETCH_SIZE || exit 1
   pass $mode/write $mode WRITE_SIZE || exit 1
@@ -31,6 +31,10 @@ done
 # [1024][16448] fp32 read once + three fp32 slabs [10688][1024] written;
 # pair = dg [10688][1024] + X + W_ih read once, dX [10688][16448] + dW_ih
 # [1024][16448] written
+if [ -n "$MODES" ]; then
+  for mode in $MODES; do python3 tools/traffic_json.py "$OUT/$mode" gemm_x6r $(( 4 * (10688*1024 + 10688*16448 + 1024*16448) )) "tools/pmc_x6r.sh over tools/roofline_probe.py 5 $mode" > "$OUT/traffic_$mode.json"; done
+  echo "all steps ok"; exit 0
+fi
 python3 tools/traffic_json.py "$OUT/fp32" gemm_x6r $(( 4 * (10688*16448 + 1024*16448) + 3 * 4 * 10688*1024 )) \
   "tools/pmc_x6r.sh over tools/roofline_probe.py 5 fp32" > "$OUT/traffic_fwd.json" && cat "$OUT/traffic_fwd.json" || exit 1
 python3 tools/traffic_json.py "$OUT/pair" gemm_x6r $(( 4 * (10688*1024 + 2 * 10688*16448 + 2 * 1024*16448) )) \

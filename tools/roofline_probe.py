@@ -36,6 +36,20 @@ elif len(sys.argv) > 2 and sys.argv[2] == "pair":
     dw = [torch.empty(4 * H, I, device=dev) for _ in range(2)]
     for _ in range(reps):
         ops.lstm_l0_bwd_x6(dg, W[0], W[1], A, dx, dw[0], dw[1])
+elif len(sys.argv) > 2 and sys.argv[2] in ("pair_dw", "pair_dx"):
+    # one half of the pair alone (its traffic apart from the other's)
+    dg = torch.randn(M, 8 * H, device=dev) * 1e-3
+    G4 = 4 * H
+    if sys.argv[2] == "pair_dw":
+        dw = [torch.empty(4 * H, I, device=dev) for _ in range(2)]
+        p = ops.x6_problem(dg, A, dw[0], M=8 * H, N=I, K=M, lda=8 * H, ldb=I, ldc=I,
+                           a_kmajor=True, b_kmajor=True, C2=dw[1], c_msplit=G4)
+    else:
+        dx = torch.empty(M, I, device=dev)
+        p = ops.x6_problem(dg, W[0], dx, M=M, N=I, K=8 * H, lda=8 * H, ldb=I, ldc=I,
+                           B2=W[1], b_ksplit=G4, b_kmajor=True)
+    for _ in range(reps):
+        ops.gemm_x6_multi([p])
 else:
     for _ in range(reps):
         if ops.X6R_FWD:   # the step's kernel (gemm_x6r.hip), as the bench times it
