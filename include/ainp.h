@@ -254,6 +254,23 @@ int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t* A, int64_t
                      const float* bias_a1, const float* bias_a2, const float* bias_b1,
                      const float* bias_b2, int64_t bias_nsplit, int nsplit, int64_t kc,
                      int64_t strideC, void* stream);
+/* Up to 3 bf16-operand GEMMs in ONE launch on the 256 x 256 LDS-DMA tile
+ * (csrc/gemm16.hip gemm_bf16nt_256_multi_kernel): the bf16 configuration's
+ * layer-0 LSTM backward pair dW_cat = dg^T X beside dX = dg W_cat
+ * (models/CNNBLSTM/model.py:46-47,77), the long-K weight-gradient items first.
+ * Per problem C[m][n] (+ split s * strideC) = sum_k A[m][k] B[n][k], A [M][lda]
+ * and B [N][ldb] bf16 bit patterns (k-contiguous, 16-byte aligned rows, lda,
+ * ldb % 8 == 0), K % 32 == 0, fp32 C row-major; nsplit > 1: split s sums k in
+ * [s*kc, min(K, (s+1)*kc)) (kc % 32 == 0) into slab C + s*strideC (combine
+ * with ainp_sum_slabs).  Same MFMA and k order as ainp_gemm_bf16nt: with equal
+ * splits the results are bit-identical. */
+typedef struct {
+  const uint16_t* A; int64_t lda;
+  const uint16_t* B; int64_t ldb;
+  float* C; int64_t ldc;
+  int64_t M, N, K; int nsplit; int64_t kc; int64_t strideC;
+} ainp_bf16_problem;
+int ainp_gemm_bf16nt_multi(const ainp_bf16_problem* probs, int nprobs, void* stream);
 /* fp32 x [R][ld_in] -> bf16 (nearest-even) out [R][ld_out] and/or its
  * transpose outT [C][ld_t] (either may be NULL): the BPTT gradient and the
  * layer-0 weights as bf16 GEMM operands. */

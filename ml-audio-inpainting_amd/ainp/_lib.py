@@ -151,6 +151,7 @@ _SIGS = {
     "ainp_istft_workspace": (c_size_t, [c_int64, c_int64, c_int]),
     "ainp_l1_pow10_loss_slots": (c_int64, [c_int64]),
     "ainp_gemm_x6_multi": (c_int, [P, c_int, P]),
+    "ainp_gemm_bf16nt_multi": (c_int, [P, c_int, P]),
     "ainp_gl_stft_update": (c_int, [P, c_int64, c_int64, P, c_int, c_int64, P, P, c_float, c_int,
                                     P]),
     "ainp_istft": (c_int, [P, P, c_int, c_int64, c_int, c_int64, P, c_int, c_int, c_int, P, P,

@@ -393,14 +393,15 @@ class _BLSTMFn(torch.autograd.Function):
             getattr(ctx.sink, "side_ok", True) and all(p.grad is None for p in ctx.param_objs)
         main_first = ops.MAIN_FIRST
 
-        def main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink, dg16):
-            """Layer l's data gradient (and, for the fp32 layer-0 pair, dW_ih) on
-            the current stream; (dxi or None, [gW_ih, gW_ih_rev] or None)."""
+        def main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink, dg16, dgT16=None,
+                    pair16=False):
+            """Layer l's data gradient (and, for the layer-0 pair -- fp32 x6r or
+            bf16 -- dW_ih) on the current stream; (dxi or None, [gW_ih,
+            gW_ih_rev] or None)."""
             gwi = None
             dxi = None
-            if pair:
+            if pair or pair16:
                 dxi = torch.empty(NT, Il, device=dh.device)
-                gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
                 if ops.PAIR_JOIN:
                     # the side stream's queued weight gradients finish first at
                     # full width: the pair kernel (160 KB of LDS per workgroup)
@@ -408,7 +409,14 @@ class _BLSTMFn(torch.autograd.Function):
                     ev = torch.cuda.Event()
                     ev.record(side)
                     main.wait_event(ev)
-                ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
+                if pair:
+                    gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
+                    ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
+                else:
+                    # bf16: dW_cat beside dX on the 256 x 256 tile, one launch
+                    gcat = torch.empty(8 * H, Il, device=dh.device)
+                    ops.lstm_l0_bwd_bf16(dg16, dgT16, l016[1], l016[0], dxi, gcat)
+                    gwi = [gcat[:4 * H], gcat[4 * H:]]
                 if to_sink:
                     # all-reduced from the current stream right behind the pair;
                     # the reducer's Work holds these buffers, autograd gets None
@@ -421,7 +429,7 @@ class _BLSTMFn(torch.autograd.Function):
             # tiles) sums both directions inside each tile; the upper layers
             # (Il = 256: 168 tiles) write 4 K-slabs (two per direction,
             # 672 tiles) summed in fixed order.
-            if pair:
+            if pair or pair16:
                 pass                                                  # dxi from the pair
             elif l016 is not None:
                 dxi = ops.gemm_bf16nt(dg16, l016[1])                 # dg [NT,8H] x W_cat
@@ -478,6 +486,8 @@ class _BLSTMFn(torch.autograd.Function):
             pair = (l == 0 and l016 is None and not bf16 and not ops.GEMM_EXACT
                     and (l > 0 or ctx.needs_input_grad[0])
                     and ops.l0_bwd_x6r_eligible(NT, Il, H))
+            pair16 = (l == 0 and l016 is not None and not ops.GEMM_EXACT
+                      and ctx.needs_input_grad[0] and ops.l0_bwd_bf16_eligible(NT, Il, H))
             # data parallel: the layer-0 input weights' gradients go to the
             # reducer as soon as they exist, bypassing autograd -- after the
             # pair launch (the same kernels as one GPU: its all-reduce then
@@ -485,20 +495,21 @@ class _BLSTMFn(torch.autograd.Function):
             # side stream where the pair does not run
             to_sink = (l == 0 and ctx.sink is not None and ctx.sink.early_ok
                        and all(p.grad is None for p in ctx.wih0))
-            early = to_sink and not pair
+            early = to_sink and not (pair or pair16)
             if main_first:
                 # the data gradient (the critical path: the next BPTT / the
                 # encoder backward wait for it) is issued before the side
                 # stream's weight-gradient launches, whose host-side issue
                 # would otherwise leave the current stream idle
                 dxi, gwi_pair = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
-                                        dg16 if l016 is not None else None)
+                                        dg16 if l016 is not None else None,
+                                        dgT16 if l016 is not None else None, pair16)
             with torch.cuda.stream(side):
                 # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
                 # for the recurrent / upper layers -> parallel split-K over row chunks
                 gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H),
                                          bf16=bf16)
-                if pair:
+                if pair or pair16:
                     gwi = None
                 elif early:
                     gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0,
@@ -521,8 +532,9 @@ class _BLSTMFn(torch.autograd.Function):
             base = 8 * l
             if not main_first:
                 dxi, gwi_pair = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
-                                        dg16 if l016 is not None else None)
-            if pair:
+                                        dg16 if l016 is not None else None,
+                                        dgT16 if l016 is not None else None, pair16)
+            if pair or pair16:
                 gwi = gwi_pair
             if to_sink:   # p.grad set and reduced above / by _wih_grad_chunked
                 gwi = [None, None]

@@ -615,6 +615,79 @@ def proj_bwd_x6(gp, h, w, dh=None, dw=None):
             sum_slabs(C, S, out=o.view(-1))
 
 
+# AINP_B16_PAIR=0: the bf16 layer-0 backward keeps dX (128 x 128 tiles) on the
+# current stream beside a split-K dW on the side stream, instead of the pair in
+# one 256 x 256 launch (ops.lstm_l0_bwd_bf16)
+B16_PAIR = os.environ.get("AINP_B16_PAIR", "1") != "0"
+
+
+@functools.lru_cache(maxsize=64)
+def g256_splits(shapes, max_split=16):
+    """Split-K counts for bf16 problems (M, N, K) launched together by
+    ainp_gemm_bf16nt_multi (256 x 256 tiles, 32-deep K-tiles, one workgroup per
+    CU): minimise the estimated makespan plus the slab round trip, as
+    x6r_splits does for the x6r tile.  Returns ((S, kc), ...)."""
+    def opts(M, N, K):
+        out = []
+        for S in range(1, max_split + 1):
+            kc = -(-K // S // 32) * 32 if S > 1 else K
+            if S > 1 and -(-K // kc) != S:
+                continue
+            out.append((S, kc))
+        return out
+    best, best_t = None, None
+    for combo in itertools.product(*(opts(*sh) for sh in shapes)):
+        items = []
+        slab = 0.0
+        for (M, N, K), (S, kc) in zip(shapes, combo):
+            tiles = -(-M // 256) * -(-N // 256)
+            items += [kc // 32] * (tiles * S)
+            if S > 1:
+                slab += (S + 1) * M * N * 4
+        # a 256 x 256 x 32 bf16 K-tile ~ 1.1 us at the measured per-CU rate
+        t = _x6r_makespan(items) * 1.1e-6 + slab / _SLAB_RATE
+        if best_t is None or t < best_t:
+            best, best_t = combo, t
+    return best
+
+
+def gemm_bf16nt_multi(problems):
+    """Up to 3 bf16 GEMMs C = A . B^T in ONE launch (ainp_gemm_bf16nt_multi,
+    256 x 256 tiles): problems = [(A [M, >=K], B [N, >=K], C, K, nsplit, kc)],
+    C [M, N] (nsplit 1) or slabs [nsplit, M, N]."""
+    ints = []
+    for A, B, C, K, S, kc in problems:
+        _work("gemm_bf16nt", 2.0 * A.shape[0] * B.shape[0] * K)
+        ints += [int(K), int(S), int(kc)]
+    _T.gemm_bf16nt_multi([p[0] for p in problems], [p[1] for p in problems],
+                         [p[2] for p in problems], ints)
+
+
+def l0_bwd_bf16_eligible(NT, I, H):
+    """Shapes ops.lstm_l0_bwd_bf16 takes: both reductions (N*T, 8H) in whole
+    32-deep K-tiles, 16-byte operand rows."""
+    return B16_PAIR and NT % 32 == 0 and (8 * H) % 32 == 0 and I % 8 == 0
+
+
+def lstm_l0_bwd_bf16(dg16, dgT16, wT16, xT16, dx, gcat):
+    """The bf16 layer-0 LSTM backward pair in ONE launch (nn.LSTM backward,
+    models/CNNBLSTM/model.py:46-47,77):
+        dW_cat [8H, I] = dg^T . X   from dgT16 [8H, >=NT] and xT16 [I, >=NT]
+        dX [NT, I]     = dg . W_cat from dg16 [NT, 8H] and wT16 = W_cat^T [I, 8H]
+    the weight-gradient items (long K = N*T) first, the data-gradient items
+    behind them; dW split over K only where the makespan model asks for it."""
+    NT, G8 = dg16.shape
+    I = xT16.shape[0]
+    (Sw, kcw), (Sx, kcx) = g256_splits(((G8, I, NT), (NT, I, G8)))
+    Cw = gcat if Sw == 1 else torch.empty(Sw, G8, I, device=dg16.device)
+    Cx = dx if Sx == 1 else torch.empty(Sx, NT, I, device=dg16.device)
+    gemm_bf16nt_multi([(dgT16, xT16, Cw, NT, Sw, kcw), (dg16, wT16, Cx, G8, Sx, kcx)])
+    if Sw > 1:
+        sum_slabs(Cw, Sw, out=gcat.view(-1))
+    if Sx > 1:
+        sum_slabs(Cx, Sx, out=dx.view(-1))
+
+
 def gemm_bf16nt_splitk(A, B, K, out=None, max_split=16):
     """A [M, >=K] . B [N, >=K]^T (bf16, no bias) with the long K split over
     slabs summed in fixed order (ainp_sum_slabs) -- the weight gradients."""

@@ -427,29 +427,14 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-__global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
-    int64_t M, int64_t N, int64_t K, const uint16_t* __restrict__ A, int64_t lda,
-    const uint16_t* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
-    int64_t kc, int64_t strideC, Bias bias, int tiles_n) {
-  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
-  // XCD-aware order: each XCD owns a contiguous range of linear tiles; within
-  // it groups of (up to) 8 n-tiles walk down m, sharing A panels in its L2
-  const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
-  const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
-  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
-  const int64_t tiles_m = (M + BM - 1) / BM;
-  const int64_t per_group = 8 * tiles_m;
-  const int64_t first_n = (bid / per_group) * 8;
-  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
-  const int64_t in_g = bid % per_group;
-  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
-
-  const int64_t split = blockIdx.y;
-  const int64_t kbeg = split * kc;
-  const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
-  float* Cs = C + split * strideC;
-  const int nk = (int)((kend - kbeg) / BK);  // the launcher guarantees BK | kc, BK | K
-
+// Tile (m0, n0) of Cs over k in [kbeg, kbeg + nk*BK): the 4-stage LDS-DMA ring
+// main loop and the store epilogue shared by the single- and multi-problem
+// kernels (bias only in split 0).
+__device__ __forceinline__ void tile256(int64_t M, int64_t N, const uint16_t* __restrict__ A,
+                                        int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+                                        float* __restrict__ Cs, int64_t ldc, int64_t m0,
+                                        int64_t n0, int64_t kbeg, int nk, int64_t split,
+                                        const Bias& bias, unsigned char* smem) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
   const int li = lane & 31, lh = lane >> 5;
@@ -519,6 +504,74 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
         if (m < M) Cs[m * ldc + n] = acc[i][j][r] + bv;
       }
   }
+}
+
+__global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
+    int64_t M, int64_t N, int64_t K, const uint16_t* __restrict__ A, int64_t lda,
+    const uint16_t* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
+    int64_t kc, int64_t strideC, Bias bias, int tiles_n) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  // XCD-aware order: each XCD owns a contiguous range of linear tiles; within
+  // it groups of (up to) 8 n-tiles walk down m, sharing A panels in its L2
+  const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t first_n = (bid / per_group) * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+
+  const int64_t split = blockIdx.y;
+  const int64_t kbeg = split * kc;
+  const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
+  const int nk = (int)((kend - kbeg) / BK);  // the launcher guarantees BK | kc, BK | K
+  tile256(M, N, A, lda, B, ldb, C + split * strideC, ldc, m0, n0, kbeg, nk, split, bias, smem);
+}
+
+// Several bf16 GEMMs in ONE grid (ainp_gemm_bf16nt_multi): problem q's work
+// items (tiles x splits) follow problem q-1's, each problem starting on a
+// multiple of 8 blocks.  Per problem the items are spread over the XCDs in
+// contiguous ranges (the single-problem kernel's order), so the long-K weight
+// gradient's items issue first and the short data-gradient items fill in
+// behind them -- the bf16 layer-0 backward pair without a second stream.
+constexpr int MAXP = 3;
+struct MProb {
+  const uint16_t* A; const uint16_t* B; float* C;
+  int64_t lda, ldb, ldc, M, N, K, kc, strideC;
+  int tiles_m, tiles_n, nsplit;
+  int64_t items, first;
+};
+struct MJob {
+  MProb p[MAXP];
+  int np;
+};
+
+__global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_multi_kernel(MJob job) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int64_t bid0 = blockIdx.x;
+  int pi = 0;
+#pragma unroll
+  for (int q = 1; q < MAXP; ++q)
+    if (q < job.np && bid0 >= job.p[q].first) pi = q;
+  const MProb& P = job.p[pi];
+  const int64_t n8 = (P.items + 7) / 8 * 8;
+  const int64_t loc0 = bid0 - P.first;
+  const int64_t loc = (loc0 % 8) * (n8 / 8) + loc0 / 8;   // contiguous range per XCD
+  if (loc >= P.items) return;
+  const int64_t tiles = (int64_t)P.tiles_m * P.tiles_n;
+  const int64_t split = loc / tiles, t = loc - split * tiles;
+  const int64_t per_group = 8 * (int64_t)P.tiles_m;
+  const int64_t first_n = (t / per_group) * 8;
+  const int64_t gsize = (P.tiles_n - first_n) < 8 ? (P.tiles_n - first_n) : 8;
+  const int64_t in_g = t % per_group;
+  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+  const int64_t kbeg = split * P.kc;
+  const int64_t kend = (kbeg + P.kc) < P.K ? (kbeg + P.kc) : P.K;
+  const Bias nob{nullptr, nullptr, nullptr, nullptr, 0};
+  tile256(P.M, P.N, P.A, P.lda, P.B, P.ldb, P.C + split * P.strideC, P.ldc, m0, n0, kbeg,
+          (int)((kend - kbeg) / BK), split, nob, smem);
 }
 }  // namespace g256
 
@@ -899,6 +952,44 @@ extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t*
   hipLaunchKernelGGL(g16::gemm_bf16nt_kernel, grid, dim3(g16::THREADS), 0, as_stream(stream), M, N,
                      K, A, lda, B, ldb, C, ldc, kc, strideC, b, (int)tiles_n);
   return check_launch("gemm_bf16nt");
+}
+
+extern "C" int ainp_gemm_bf16nt_multi(const ainp_bf16_problem* probs, int nprobs, void* stream) {
+  if (!probs || nprobs < 1 || nprobs > g256::MAXP)
+    return record_msg("ainp_gemm_bf16nt_multi: 1..3 problems");
+  g256::MJob job{};
+  job.np = nprobs;
+  int64_t first = 0;
+  for (int q = 0; q < nprobs; ++q) {
+    const ainp_bf16_problem& s = probs[q];
+    const int nsplit = s.nsplit < 1 ? 1 : s.nsplit;
+    const int64_t kc = nsplit == 1 ? s.K : s.kc;
+    if (!s.A || !s.B || !s.C || s.M < 1 || s.N < 1 || s.K < g256::BK || s.K % g256::BK ||
+        s.lda % 8 || s.ldb % 8 || s.lda < s.K || s.ldb < s.K || s.ldc < s.N ||
+        ((uintptr_t)s.A & 15) || ((uintptr_t)s.B & 15) || nsplit > 65535 ||
+        (nsplit > 1 && (kc < g256::BK || kc % g256::BK || (int64_t)nsplit * kc < s.K ||
+                        (int64_t)(nsplit - 1) * kc >= s.K || s.strideC < s.M * s.ldc)))
+      return record_msg("ainp_gemm_bf16nt_multi: bad problem (K, kc % 32 == 0 covering K; "
+                        "16-byte aligned k-contiguous rows; strideC >= M*ldc when split)");
+    g256::MProb& d = job.p[q];
+    d.A = s.A; d.B = s.B; d.C = s.C;
+    d.lda = s.lda; d.ldb = s.ldb; d.ldc = s.ldc;
+    d.M = s.M; d.N = s.N; d.K = s.K; d.kc = kc; d.strideC = s.strideC;
+    d.tiles_m = (int)cdiv(s.M, g256::BM);
+    d.tiles_n = (int)cdiv(s.N, g256::BN);
+    d.nsplit = nsplit;
+    d.items = (int64_t)d.tiles_m * d.tiles_n * nsplit;
+    d.first = first;
+    first += (d.items + 7) / 8 * 8;
+  }
+  static const bool lds_ok =
+      hipFuncSetAttribute((const void*)g256::gemm_bf16nt_256_multi_kernel,
+                          hipFuncAttributeMaxDynamicSharedMemorySize, g256::LDS_BYTES) == hipSuccess;
+  if (!lds_ok) return record_msg("ainp_gemm_bf16nt_multi: cannot reserve 128 KB of LDS");
+  if (first > 0x7fffffff) return record_msg("ainp_gemm_bf16nt_multi: grid too large");
+  hipLaunchKernelGGL(g256::gemm_bf16nt_256_multi_kernel, dim3((unsigned)first), dim3(g256::THREADS),
+                     g256::LDS_BYTES, as_stream(stream), job);
+  return check_launch("gemm_bf16nt_256_multi");
 }
 
 extern "C" int ainp_wgrad16_nhwc(const uint16_t* gA, int64_t ldA, int Cout, const uint16_t* x16,

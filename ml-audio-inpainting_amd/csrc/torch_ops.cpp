@@ -930,6 +930,45 @@ void check_nt_bias(const OptT& a1, const OptT& a2, const OptT& b1, const OptT& b
   if (b2.has_value() && b2->defined()) numel_is(*b2, N - nsplit, "bias_b2");
 }
 
+// ainp_gemm_bf16nt_multi: problem q = A[q] [M, >=K], B[q] [N, >=K] (bf16,
+// unit-stride rows), C[q] [M, N] or split-K slabs [nsplit, M, N];
+// ints[3q .. 3q+2] = K, nsplit, kc.
+void gemm_bf16nt_multi(const std::vector<Tensor>& A, const std::vector<Tensor>& B,
+                       const std::vector<Tensor>& C, const std::vector<int64_t>& ints) {
+  const int64_t np = (int64_t)C.size();
+  TORCH_CHECK(np >= 1 && np <= 3 && (int64_t)A.size() == np && (int64_t)B.size() == np &&
+                  (int64_t)ints.size() == 3 * np,
+              "gemm_bf16nt_multi: 1..3 problems (A, B, C each, 3 ints)");
+  GUARD(C[0]);
+  std::vector<ainp_bf16_problem> pr(np);
+  for (int64_t q = 0; q < np; ++q) {
+    const int64_t K = ints[3 * q], nsplit = ints[3 * q + 1], kc = ints[3 * q + 2];
+    const Tensor &a = A[q], &b = B[q], &c = C[q];
+    TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
+                "gemm_bf16nt_multi: A [M, >=K], B [N, >=K] with unit-stride rows");
+    TORCH_CHECK(a.size(1) >= K && b.size(1) >= K, "gemm_bf16nt_multi: K exceeds the operand rows");
+    const int64_t M = a.size(0), N = b.size(0);
+    TORCH_CHECK((c.dim() == 2 && nsplit == 1) || (c.dim() == 3 && c.size(0) == nsplit),
+                "gemm_bf16nt_multi: C [M, N] or split-K slabs [nsplit, M, N]");
+    TORCH_CHECK(c.size(-2) == M && c.size(-1) == N && c.stride(-1) == 1,
+                "gemm_bf16nt_multi: C shape");
+    same_device(a, C[0]);
+    same_device(b, C[0]);
+    same_device(c, C[0]);
+    ainp_bf16_problem& p = pr[q];
+    p.A = bf16p(a, "A", false);
+    p.lda = a.stride(0);
+    p.B = bf16p(b, "B", false);
+    p.ldb = b.stride(0);
+    p.C = dev(c, "C", at::kFloat, false);
+    p.ldc = c.stride(-2);
+    p.M = M; p.N = N; p.K = K;
+    p.nsplit = (int)nsplit; p.kc = kc;
+    p.strideC = c.dim() == 3 ? c.stride(0) : 0;
+  }
+  chk(ainp_gemm_bf16nt_multi(pr.data(), (int)np, stream_of(C[0])), "gemm_bf16nt_multi");
+}
+
 void gemm_bf16nt(const Tensor& A, const Tensor& B, const Tensor& C, int64_t K,
                  const OptT& bias_a1, const OptT& bias_a2, const OptT& bias_b1,
                  const OptT& bias_b2, int64_t bias_nsplit, int64_t nsplit, int64_t kc) {
@@ -1580,6 +1619,7 @@ TORCH_LIBRARY(ainp, m) {
         "Tensor(b!)? out16, Tensor(c!)? outT, int flags) -> ()");
   m.def("bn_relu_apply_ntcf_bf16(Tensor x, Tensor scale, Tensor shift, Tensor(a!) out, "
         "Tensor(b!) outT, int flags=0) -> ()");
+  m.def("gemm_bf16nt_multi(Tensor[] A, Tensor[] B, Tensor(a!)[] C, int[] ints) -> ()");
   m.def("gemm_bf16nt(Tensor A, Tensor B, Tensor(a!) C, int K, Tensor? bias_a1, Tensor? bias_a2, "
         "Tensor? bias_b1, Tensor? bias_b2, int bias_nsplit, int nsplit, int kc) -> ()");
   m.def("cast_bf16_t(Tensor x, Tensor(a!)? out, Tensor(b!)? outT) -> ()");
@@ -1638,6 +1678,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("gl_update", &gl_update);
   m.impl("gl_stft_update", &gl_stft_update);
   m.impl("gemm_x6_multi", &gemm_x6_multi);
+  m.impl("gemm_bf16nt_multi", &gemm_bf16nt_multi);
   m.impl("gemm", &gemm);
   m.impl("conv3x3_fwd", &conv3x3_fwd);
   m.impl("conv3x3_dgrad", &conv3x3_dgrad);
@@ -1721,6 +1762,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("gl_update", torch::CppFunction::makeFallthrough());
   m.impl("gl_stft_update", torch::CppFunction::makeFallthrough());
   m.impl("gemm_x6_multi", torch::CppFunction::makeFallthrough());
+  m.impl("gemm_bf16nt_multi", torch::CppFunction::makeFallthrough());
   m.impl("gemm", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_fwd", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_dgrad", torch::CppFunction::makeFallthrough());

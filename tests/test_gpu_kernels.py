@@ -779,6 +779,71 @@ def test_gemm_bf16nt_split_projection_with_bias(M, N, K, S):
         assert torch.equal(slabs[s_], part), s_
 
 
+def test_gemm_bf16nt_multi_problems_match_single_launches():
+    """ainp_gemm_bf16nt_multi: three problems in one grid (ragged tiles, one
+    split-K with slabs, ld > K) give exactly what each gives alone on the
+    256 x 256 tile / the 128 x 128 tile (same MFMA, same k order), and the
+    products of the bf16 operands to fp32 accumulation order."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(7)
+    shapes = [(1024, 700, 2112, 3), (777, 600, 1056, 1), (300, 520, 96, 1)]
+    probs, refs, outs = [], [], []
+    for M, N, K, S in shapes:
+        A = _tobf16(torch.randn(M, K + 8, generator=g)).cuda()[:, :K]
+        B = _tobf16(torch.randn(N, K, generator=g)).cuda()
+        kc = -(-K // S // 32) * 32 if S > 1 else K
+        C = torch.full((S, M, N) if S > 1 else (M, N), float("nan"), device="cuda")
+        probs.append((A, B, C, K, S, kc))
+        refs.append(A.double().cpu() @ B.double().cpu().T)
+    ops.gemm_bf16nt_multi(probs)
+    for (A, B, C, K, S, kc), ref in zip(probs, refs):
+        if S > 1:
+            for s_ in range(S):
+                k0, k1 = s_ * kc, min(K, (s_ + 1) * kc)
+                part = ops.gemm_bf16nt(A[:, k0:], B[:, k0:], K=k1 - k0)
+                torch.cuda.synchronize()
+                assert torch.equal(C[s_], part), s_
+            C = C.sum(0)
+        else:
+            alone = ops.gemm_bf16nt(A, B, K=K)
+            torch.cuda.synchronize()
+            assert torch.equal(C, alone)
+        err = (C.double().cpu() - ref).norm() / ref.norm()
+        assert err < 1e-5, float(err)
+
+
+@pytest.mark.parametrize("NT,H,I", [(10688, 128, 16448), (1024, 64, 520)])
+def test_lstm_l0_bwd_bf16_pair(NT, H, I):
+    """The bf16 layer-0 backward pair in one launch (ops.lstm_l0_bwd_bf16,
+    models/CNNBLSTM/model.py:46-47,77 backward) equals dX and dW_cat from
+    separate ainp_gemm_bf16nt launches with the same splits, bit for bit."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(NT + H)
+    dg = torch.randn(NT, 8 * H, generator=g).cuda() * 1e-3
+    x = torch.randn(NT, I, generator=g).cuda()
+    w = torch.randn(8 * H, I, generator=g).cuda() * 0.01
+    dg16, dgT16, xT16, wT16 = _tobf16(dg), _tobf16(dg.T.contiguous()), _tobf16(x.T.contiguous()), \
+        _tobf16(w.T.contiguous())
+    dx = torch.full((NT, I), float("nan"), device="cuda")
+    gcat = torch.full((8 * H, I), float("nan"), device="cuda")
+    ops.lstm_l0_bwd_bf16(dg16, dgT16, wT16, xT16, dx, gcat)
+    (Sw, kcw), (Sx, kcx) = ops.g256_splits(((8 * H, I, NT), (NT, I, 8 * H)))
+
+    def alone(A, B, K, S, kc):
+        if S == 1:
+            return ops.gemm_bf16nt(A, B)
+        slabs = torch.empty(S, A.shape[0], B.shape[0], device="cuda")
+        torch.ops.ainp.gemm_bf16nt(A, B, slabs, K, None, None, None, None, 0, S, kc)
+        return ops.sum_slabs(slabs, S).view(A.shape[0], B.shape[0])
+    want_dx = alone(dg16, wT16, 8 * H, Sx, kcx)
+    want_dw = alone(dgT16, xT16, NT, Sw, kcw)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, want_dx)
+    assert torch.equal(gcat, want_dw)
+    ref = dg16.double() @ wT16.double().T
+    assert float((dx.double() - ref).norm() / ref.norm()) < 1e-5
+
+
 def test_cast_bf16_t_and_ntcf_bf16_bridge_bit_exact():
     """The bf16 operand producers round to nearest-even exactly as torch's
     .to(bfloat16): cast (+ transpose into a strided view) and the encoder's
