@@ -385,17 +385,17 @@ def spawn_ranks(n):
 # ------------------------------------------------------------- in-step kernels
 # Committed rocprofv3 kernel-stats tables of the step alone (tools/step_prof.py:
 # 3 warm-up + 10 timed steps, nothing else launched; per step = total / 13),
-# regenerated by tools/gpu_r04f.sh.  The bench reports the dominant in-step
+# regenerated by tools/gpu_stepprof.sh / tools/gpu_stepprof_gan.sh.  The bench reports the dominant in-step
 # kernels from them with their own roofline fractions (per-step algorithmic
 # work / per-step kernel time / peak), next to the live stand-alone launches.
 # (table, steps it covers: tools/step_prof.py's "kernel tables / N"); under
 # profiles/steps/ so they travel with gpurun / the driver's snapshot
 # (.gpurunignore drops profiles/r0*)
 STEP_TABLES = {
-    ("cnnblstm", "fp32"): ("profiles/steps/r04zB4_cnn_fp32_step_kernel_stats.csv", 13),
-    ("cnnblstm", "bf16"): ("profiles/steps/r04zB4_cnn_bf16_step_kernel_stats.csv", 13),
-    ("gan", "bf16", 626): ("profiles/steps/r04zB4_gan_c4_step_kernel_stats.csv", 9),
-    ("gan", "bf16", 1001): ("profiles/steps/r04d_gan_c5_step_kernel_stats.csv", 13),
+    ("cnnblstm", "fp32"): ("profiles/steps/r05_cnn_fp32_step_kernel_stats.csv", 13),
+    ("cnnblstm", "bf16"): ("profiles/steps/r05_cnn_bf16_step_kernel_stats.csv", 13),
+    ("gan", "bf16", 626): ("profiles/steps/r05_gan_c4_step_kernel_stats.csv", 13),
+    ("gan", "bf16", 1001): ("profiles/steps/r05_gan_c5_step_kernel_stats.csv", 13),
 }
 
 
@@ -423,22 +423,25 @@ def step_critical_path(key):
     return cp
 
 
-def _cnn_step_work(B=32, F=257, T=334, H=128):
+def _cnn_step_work(B=32, F=257, T=334, H=128, bf16=False):
     """(name substring, kind, per-step algorithmic work) of the CNNBLSTM step's
     kernels at the C2 / C3 per-GPU shape: FLOP for MFMA kernels, HBM bytes
-    for the BatchNorm passes (every operand read / written once)."""
+    for the BatchNorm passes (every operand read / written once, at the
+    storage width of the configuration: bf16 pre-BN y and BN-backward outputs
+    in the bf16 step, fp32 otherwise; the incoming gradient is fp32 in both)."""
     P = B * F * T                       # pixels per channel plane set
     conv = lambda ci, co: 2.0 * 9 * ci * co * P          # noqa: E731
     l0 = 2.0 * B * T * 8 * H * 64 * F                     # one layer-0 GEMM
     proj = 2.0 * B * T * 16 * F * 2 * H                   # one output-projection GEMM
-    bn_small = (16 + 32 + 32 + 16) * P                    # BN-ReLU elements of the 16/32-ch layers
     big = 64 * P
+    y = 2.0 if bf16 else 4.0            # pre-BN y storage
+    gy = 2.0 if bf16 else 4.0           # BN-backward output storage
     return [
         # fp32: layer-0 projection + backward pair + the output projection's
         # dh and dW (proj_bwd_x6)
         ("gemm_x6r_kernel", "mfma", 3 * l0 + 2 * proj),
+        ("gemm_bf16nt_256_multi_kernel", "mfma", 2 * l0),  # bf16 dX + dW pair
         ("gemm_bf16nt_256_kernel", "mfma", l0),           # bf16 projection
-        ("g16::gemm_bf16nt_kernel", "mfma", 2 * l0),      # bf16 dX + dW
         ("conv3x3_x6p_kernel<32, 64", "mfma", conv(32, 64)),
         ("conv3x3_x6_kernel<64, 32", "mfma", conv(64, 32)),
         ("conv3x3_wgrad_x6<64", "mfma", conv(32, 64)),
@@ -448,12 +451,18 @@ def _cnn_step_work(B=32, F=257, T=334, H=128):
         ("conv3x3_wgrad_x6s<32, 16", "mfma", conv(32, 16)),
         ("conv3x3_x6q_kernel<32, false", "mfma", conv(32, 16)),
         ("conv3x3_x6p_kernel<16, 32, true", "mfma", conv(32, 16)),
-        ("bn_relu_bwd_reduce_flat", "hbm", 8.0 * bn_small),
-        ("bn_relu_bwd_apply_flat", "hbm", 12.0 * bn_small),
-        ("bn_relu_bwd_apply_ntcf2", "hbm", 12.0 * big),
-        ("bn_relu_bwd_ntcf", "hbm", 8.0 * big),
-        ("bn_relu_apply_ntcf2", "hbm", 8.0 * big),
-        ("bn_relu_apply_ntcf_bf16", "hbm", 8.0 * big),
+        # channel-last BatchNorm + ReLU backward of the 16/32-channel layers:
+        # reduce reads y and dy, apply reads both and writes gy
+        # (one instance per channel count: encoder + decoder layer each)
+        ("bn_relu_bwd_reduce_cl<16", "hbm", (y + 4.0) * 32 * P),
+        ("bn_relu_bwd_reduce_cl<32", "hbm", (y + 4.0) * 64 * P),
+        ("bn_relu_bwd_apply_cl<16", "hbm", (y + 4.0 + gy) * 32 * P),
+        ("bn_relu_bwd_apply_cl<32", "hbm", (y + 4.0 + gy) * 64 * P),
+        # the encoder's last block against the NTCF gradient of the LSTM input
+        ("bn_relu_bwd_ntcf_cl<false", "hbm", (y + 4.0) * big),
+        ("bn_relu_bwd_ntcf_cl<true", "hbm", (y + 4.0 + gy) * big),
+        # the bridge: y -> fp32 X [N, T, 64F], or bf16 X and X^T
+        ("bn_relu_apply_ntcf_cl", "hbm", (2.0 + 4.0 if bf16 else 8.0) * big),
     ]
 
 
@@ -471,7 +480,7 @@ def in_step_table(key, bf16, top=8, families=None):
     import csv
     rows = list(csv.DictReader(open(os.path.join(ROOT, path))))
     total = sum(float(r["TotalDurationNs"]) for r in rows)
-    work = _cnn_step_work() if key[0] == "cnnblstm" else []
+    work = _cnn_step_work(bf16=bf16) if key[0] == "cnnblstm" else []
     fam = None
     if families:
         peak = executed_peak(bf16)
