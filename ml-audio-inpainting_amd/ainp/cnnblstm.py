@@ -385,7 +385,10 @@ class _BLSTMFn(torch.autograd.Function):
         # gradients, so they run on a side stream while the main stream goes
         # on with dX and layer l-1's recurrence (64 workgroups: most CUs idle).
         main = torch.cuda.current_stream(dh.device)
-        side = _side_stream(dh.device)
+        # the BLSTM's weight gradients: on their own side stream (BLSTM_SIDE2),
+        # so they start right behind their recurrence instead of queueing
+        # behind the deferred decoder weight gradients
+        side = _side_stream(dh.device, 1 if BLSTM_SIDE2 else 0)
         # data parallel: the side stream's weight / bias gradients are
         # all-reduced from the side stream as they are produced, so the compute
         # stream never waits for them (AccumulateGrad stores non-view aliases)
@@ -559,11 +562,7 @@ class _BLSTMFn(torch.autograd.Function):
             # them into .grad on the current stream, which must wait (below).
             dev = dh.device
 
-            def join():
-                ev = torch.cuda.Event()
-                ev.record(_side_stream(dev))
-                torch.cuda.current_stream(dev).wait_event(ev)
-            torch.autograd.Variable._execution_engine.queue_callback(join)
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_side(dev))
             grads = [_alias(gr) if gr is not None else None for gr in grads]
         else:
             # data parallel: the gradient hooks read them as autograd hands them
@@ -640,6 +639,8 @@ DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "1") != "0"
 # stream (hipExtStreamCreateWithCUMask, 8 of 32 CUs kept free for the
 # recurrence) measured +3.3 ms/step on both and was dropped.
 DEFER_EARLY = os.environ.get("AINP_DEFER_EARLY", "1") != "0"
+# (C2 14.65 -> 14.43 / 14.79 -> 14.55 ms/step A/B, profiles/r05o_ab_x6r_apf_side2.txt)
+BLSTM_SIDE2 = os.environ.get("AINP_BLSTM_SIDE2", "1") != "0"
 
 
 class _Deferred:
@@ -694,9 +695,7 @@ class _Deferred:
                         for p, o in zip(params, outputs):
                             sink.reduce_chunk(p, o, kind="side")
         if join and q is not None:
-            done = torch.cuda.Event()
-            done.record(_side_stream(device))
-            torch.cuda.current_stream(device).wait_event(done)
+            _join_side(device)
 
 
 def _reduce_side(sink, params, grads):
@@ -735,12 +734,8 @@ class _side_work:
         self._ctx = torch.cuda.stream(self.side)
         self._ctx.__enter__()
 
-        def join():
-            done = torch.cuda.Event()
-            done.record(_side_stream(dev))
-            torch.cuda.current_stream(dev).wait_event(done)
         if self.callback:
-            torch.autograd.Variable._execution_engine.queue_callback(join)
+            torch.autograd.Variable._execution_engine.queue_callback(lambda: _join_side(dev))
         return self
 
     def handoff(self, inputs, outputs):
@@ -758,12 +753,25 @@ class _side_work:
         return False
 
 
-def _side_stream(device):
-    s = _SIDE_STREAMS.get(device)
+def _side_stream(device, k=0):
+    """Side stream k of the device (0: deferred conv / projection weight
+    gradients; 1: the BLSTM's weight gradients under BLSTM_SIDE2)."""
+    s = _SIDE_STREAMS.get((device, k))
     if s is None:
         s = torch.cuda.Stream(device=device)
-        _SIDE_STREAMS[device] = s
+        _SIDE_STREAMS[(device, k)] = s
     return s
+
+
+def _join_side(device):
+    """The current stream waits for everything issued so far on the device's
+    side streams."""
+    cur = torch.cuda.current_stream(device)
+    for (d, _k), s in list(_SIDE_STREAMS.items()):
+        if d == device:
+            ev = torch.cuda.Event()
+            ev.record(s)
+            cur.wait_event(ev)
 
 
 # ------------------------------------------------------------------ projection

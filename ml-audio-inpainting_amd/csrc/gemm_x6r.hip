@@ -214,7 +214,7 @@ __device__ __forceinline__ void issue_tile(const Ctx& c, int kt) {   // kt & 1 =
 
 // one K-tile kt (kt & 1 == PAR): MFMAs on planes PAR; meanwhile tile kt+2's
 // DMA into stage PAR and the split of tile kt+1 (stage PAR^1 -> planes PAR^1)
-template <int PAR, int AKM, int BKM>
+template <int PAR, int AKM, int BKM, bool APF>
 __device__ __forceinline__ void ktile(const Ctx& c, int kt, f32x16v (&acc)[4][2]) {
   // tile kt+1's DMA landed (every wave), planes PAR complete, every wave done
   // with tile kt-1 (planes PAR^1) and with the split of tile kt (stage PAR)
@@ -226,7 +226,11 @@ __device__ __forceinline__ void ktile(const Ctx& c, int kt, f32x16v (&acc)[4][2]
   const unsigned char* ps = planes_of<PAR>();
   const unsigned char* st = stage_of<PAR ^ 1>();
   unsigned char* pn = planes_of<PAR ^ 1>();
-  const bool nxt = kt + 1 < c.nk;
+  // APF: the split runs on every tile, the last included (it then reads a
+  // stale stage and writes planes nobody reads again -- every wave is past
+  // tile kt-1): the LDS op counts agree on every path, so the compiler's
+  // waits before the MFMA groups stay partial instead of lgkmcnt(0)
+  const bool nxt = APF || kt + 1 < c.nk;
   bf16x8v b0[2], b1[2], b2[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -237,15 +241,40 @@ __device__ __forceinline__ void ktile(const Ctx& c, int kt, f32x16v (&acc)[4][2]
   }
   float xa[8], xb[8];
   int ra = 0, ha = 0, rb = 0, hb = 0;
+  // APF: the A fragments of row group i+1 are read before group i's MFMAs,
+  // so their LDS latency hides under those MFMAs
+  bf16x8v a0, a1, a2;
+  if (APF) {
+    const int row = c.wm + c.li;
+    a0 = pfrag(ps, row, c.lh);
+    a1 = pfrag(ps + PLANE, row, c.lh);
+    a2 = pfrag(ps + 2 * PLANE, row, c.lh);
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int row = c.wm + i * 32 + c.li;
-    const bf16x8v a0 = pfrag(ps, row, c.lh), a1 = pfrag(ps + PLANE, row, c.lh),
-                  a2 = pfrag(ps + 2 * PLANE, row, c.lh);
+    bf16x8v n0, n1, n2;
+    if (APF) {
+      if (i < 3) {
+        const int row = c.wm + (i + 1) * 32 + c.li;
+        n0 = pfrag(ps, row, c.lh);
+        n1 = pfrag(ps + PLANE, row, c.lh);
+        n2 = pfrag(ps + 2 * PLANE, row, c.lh);
+      }
+    } else {
+      const int row = c.wm + i * 32 + c.li;
+      a0 = pfrag(ps, row, c.lh);
+      a1 = pfrag(ps + PLANE, row, c.lh);
+      a2 = pfrag(ps + 2 * PLANE, row, c.lh);
+    }
     __builtin_amdgcn_s_setprio(1);
     mfma6(acc[i][0], a0, a1, a2, b0[0], b1[0], b2[0]);
     mfma6(acc[i][1], a0, a1, a2, b0[1], b1[1], b2[1]);
     __builtin_amdgcn_s_setprio(0);
+    if (APF && i < 3) {
+      a0 = n0;
+      a1 = n1;
+      a2 = n2;
+    }
     if (i == 0 && kt + 2 < c.nk) issue_tile<PAR>(c, kt + 2);
     if (nxt) {
       if (i == 0) split_read<AKM>(st, c.tid, xa, ra, ha);
@@ -256,7 +285,7 @@ __device__ __forceinline__ void ktile(const Ctx& c, int kt, f32x16v (&acc)[4][2]
   }
 }
 
-template <int AKM, int BKM>
+template <int AKM, int BKM, bool APF>
 __device__ __forceinline__ void kloop(const Ctx& c, f32x16v (&acc)[4][2]) {
   // prologue: tile 0 landed and split into planes 0, tile 1 in flight
   if (c.nk > 0) {
@@ -273,11 +302,12 @@ __device__ __forceinline__ void kloop(const Ctx& c, f32x16v (&acc)[4][2]) {
     split_write(x, row, h, ps_a + 3 * PLANE);
   }
   for (int kt = 0; kt < c.nk; kt += 2) {
-    ktile<0, AKM, BKM>(c, kt, acc);
-    if (kt + 1 < c.nk) ktile<1, AKM, BKM>(c, kt + 1, acc);
+    ktile<0, AKM, BKM, APF>(c, kt, acc);
+    if (kt + 1 < c.nk) ktile<1, AKM, BKM, APF>(c, kt + 1, acc);
   }
 }
 
+template <bool APF>
 __global__ __launch_bounds__(THREADS, 1) void gemm_x6r_kernel(Job job) {
   // ---- which problem / tile / split (uniform per workgroup)
   const int64_t bid0 = blockIdx.x;
@@ -348,11 +378,11 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_x6r_kernel(Job job) {
   // operand layouts as template parameters: no runtime branch (and no merged
   // LDS address the compiler cannot attribute) inside the K loop
   if (c.a_km) {
-    if (c.b_km) kloop<1, 1>(c, acc);
-    else kloop<1, 0>(c, acc);
+    if (c.b_km) kloop<1, 1, APF>(c, acc);
+    else kloop<1, 0, APF>(c, acc);
   } else {
-    if (c.b_km) kloop<0, 1>(c, acc);
-    else kloop<0, 0>(c, acc);
+    if (c.b_km) kloop<0, 1, APF>(c, acc);
+    else kloop<0, 0, APF>(c, acc);
   }
   // ---- epilogue: D[row=(r&3)+8*(r>>2)+4*lh][col=li] of each 32x32 tile
   float* Cs = P.C;
@@ -452,7 +482,17 @@ extern "C" int ainp_gemm_x6_multi(const ainp_x6_problem* probs, int nprobs, void
     first += (d.items + 7) / 8 * 8;
   }
   if (first > 0x7fffffff) return record_msg("ainp_gemm_x6_multi: grid too large");
-  hipLaunchKernelGGL(x6r::gemm_x6r_kernel, dim3((unsigned)first), dim3(x6r::THREADS), 0,
-                     as_stream(stream), job);
+  // AINP_X6R_APF=0: A fragments read right before their MFMA group and the
+  // split skipped past the last tile (the round-4 main loop), for A/B
+  static const bool apf = [] {
+    const char* e = getenv("AINP_X6R_APF");
+    return !(e && e[0] == '0');
+  }();
+  if (apf)
+    hipLaunchKernelGGL(x6r::gemm_x6r_kernel<true>, dim3((unsigned)first), dim3(x6r::THREADS), 0,
+                       as_stream(stream), job);
+  else
+    hipLaunchKernelGGL(x6r::gemm_x6r_kernel<false>, dim3((unsigned)first), dim3(x6r::THREADS), 0,
+                       as_stream(stream), job);
   return check_launch("gemm_x6_multi");
 }
