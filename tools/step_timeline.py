@@ -82,7 +82,31 @@ def critical_path(step, phases=CNN_PHASES):
         s = int(ms[bounds[k]]["Start_Timestamp"])
         e = int(ms[nxt]["Start_Timestamp"]) if nxt is not None else t_end
         out.append((name, (e - s) / 1e6))
+    # how much of the BLSTM recurrences' time other streams' kernels run
+    # beside them (the recurrence holds 64 CUs; the rest are free for
+    # weight gradients): overlapped ms / recurrence ms, forward and BPTT
+    others = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]))
+                    for r in step if r["Queue_Id"] != main)
+    rec = {}
+    for kind, key in (("lstm_fwd_kernel", "fwd"), ("lstm_bwd_kernel", "bptt")):
+        tot = ov = 0
+        for r in ms:
+            if kind not in r["Kernel_Name"]:
+                continue
+            a, b = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            tot += b - a
+            cov, cur = 0, a         # union of the other streams' intervals inside [a, b]
+            for s0, e0 in others:
+                s1, e1 = max(s0, cur), min(e0, b)
+                if e1 > s1:
+                    cov += e1 - s1
+                    cur = e1
+            ov += cov
+        if tot:
+            rec[key] = {"ms": round(tot / 1e6, 3), "overlapped_ms": round(ov / 1e6, 3),
+                        "overlap_frac": round(ov / tot, 3)}
     return {"span_ms": (t_end - t0) / 1e6,
+            "recurrence_overlap": rec,
             "busy_ms": {("main" if q == main else f"queue_{q}"): round(v, 3)
                         for q, v in busy.items()},
             "critical_path_ms": {n: round(v, 3) for n, v in out}}
@@ -126,6 +150,7 @@ def main():
     for n, v in cp["critical_path_ms"].items():
         print(f"  {n:22s} {v:7.3f} ms")
     print(f"  {'sum':22s} {sum(cp['critical_path_ms'].values()):7.3f} ms  (span {cp['span_ms']:.3f})")
+    print("recurrence overlap:", cp["recurrence_overlap"])
 
 
 if __name__ == "__main__":
