@@ -262,13 +262,17 @@ int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t* A, int64_t
  * and B [N][ldb] bf16 bit patterns (k-contiguous, 16-byte aligned rows, lda,
  * ldb % 8 == 0), K % 32 == 0, fp32 C row-major; nsplit > 1: split s sums k in
  * [s*kc, min(K, (s+1)*kc)) (kc % 32 == 0) into slab C + s*strideC (combine
- * with ainp_sum_slabs).  Same MFMA and k order as ainp_gemm_bf16nt: with equal
- * splits the results are bit-identical. */
+ * with ainp_sum_slabs).  a_kmajor / b_kmajor: the operand is given k-major
+ * ([K][ld], ld >= M or N; rows transposed in LDS by ds_read_b64_tr_b16), e.g.
+ * dW_cat = dg^T X straight from dg [NT, 8H] and X [NT, I].  Same MFMA and k
+ * order as ainp_gemm_bf16nt in every layout: with equal splits the results
+ * are bit-identical. */
 typedef struct {
   const uint16_t* A; int64_t lda;
   const uint16_t* B; int64_t ldb;
   float* C; int64_t ldc;
   int64_t M, N, K; int nsplit; int64_t kc; int64_t strideC;
+  int a_kmajor, b_kmajor;   /* 1: A(m, k) = A[k*lda + m] (M % 8 == 0), likewise B */
 } ainp_bf16_problem;
 int ainp_gemm_bf16nt_multi(const ainp_bf16_problem* probs, int nprobs, void* stream);
 /* fp32 x [R][ld_in] -> bf16 (nearest-even) out [R][ld_out] and/or its

@@ -133,8 +133,11 @@ class _ConvStackFn(torch.autograd.Function):
             # tensor is never materialised -- autograd gets a stride-0
             # placeholder of its shape, and its gradient (dX, fp32) as usual
             if ylcl:
+                # B16_KM: the backward reads X k-major, so no X^T is written
+                km = ops.B16_KM and (N * W) % 32 == 0
                 l0_box["x16"] = ops.bn_relu_apply_ntcf_cl(yl, last[0], last[1], out32=False,
-                                                          out16=True)[1]
+                                                          out16=True, outT=not km)[1]
+                l0_box["km"] = km
             else:
                 l0_box["x16"] = ops.bn_relu_apply_ntcf_bf16(yl, last[0], last[1])
             Nl, Cl, Hl, Wl = yshape
@@ -332,6 +335,7 @@ class _BLSTMFn(torch.autograd.Function):
         saved = []
         h = None
         ctx.l016 = None
+        ctx.l016_km = False
         for l in range(L):
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
             Il = inp.shape[1] if (l > 0 or x16 is None) else I
@@ -340,6 +344,7 @@ class _BLSTMFn(torch.autograd.Function):
                 # bf16-operand layer-0 projection: X (bf16 [NT, I]) x W_cat^T, both
                 # directions in one GEMM (W_cat = [W_ih; W_ih_rev] as bf16)
                 X16, XT16 = x16
+                ctx.l016_km = bool(l0_box.get("km", False))
                 W16 = torch.empty(8 * H, I, device=x.device, dtype=torch.bfloat16)
                 WT16 = torch.empty(I, 8 * H, device=x.device, dtype=torch.bfloat16)
                 ops.cast_bf16_t(wf, out=W16[:4 * H], outT=WT16[:, :4 * H])
@@ -347,7 +352,8 @@ class _BLSTMFn(torch.autograd.Function):
                 ops.gemm_bf16nt(X16.view(NT, I), W16, out=zx.view(NT, 8 * H),
                                 bias=(bif, bhf, bir, bhr), bias_nsplit=4 * H,
                                 nsplit=ops.b16_proj_split(NT, 8 * H, I))
-                ctx.l016 = (XT16, WT16)
+                # the weight gradient's X operand: X^T [I, NT], or X [NT, I] k-major
+                ctx.l016 = (X16.view(NT, I) if ctx.l016_km else XT16, WT16)
             elif (l == 0 and not bf16 and not ops.GEMM_EXACT
                   and ops.x6_256_eligible(NT, 8 * H, Il, 4 * H)):
                 # fp32 layer-0 projection (360 GFLOP at C2) on the 256 x 256 tile
@@ -418,7 +424,8 @@ class _BLSTMFn(torch.autograd.Function):
                 else:
                     # bf16: dW_cat beside dX on the 256 x 256 tile, one launch
                     gcat = torch.empty(8 * H, Il, device=dh.device)
-                    ops.lstm_l0_bwd_bf16(dg16, dgT16, l016[1], l016[0], dxi, gcat)
+                    ops.lstm_l0_bwd_bf16(dg16, dgT16, l016[1], l016[0], dxi, gcat,
+                                         km=ctx.l016_km)
                     gwi = [gcat[:4 * H], gcat[4 * H:]]
                 if to_sink:
                     # all-reduced from the current stream right behind the pair;
@@ -474,9 +481,11 @@ class _BLSTMFn(torch.autograd.Function):
                 _Deferred.flush(dh.device, after=pre if DEFER_EARLY else None)
             dg2 = dg.view(NT, 8 * H)
             if l016 is not None:
-                # bf16 operands of the layer-0 data / weight gradients
+                # bf16 operands of the layer-0 data / weight gradients (k-major
+                # weight gradient: dg16 serves both, no dg^T copy)
                 dg16 = torch.empty(NT, 8 * H, device=dh.device, dtype=torch.bfloat16)
-                dgT16 = torch.empty(8 * H, NT, device=dh.device, dtype=torch.bfloat16)
+                dgT16 = None if ctx.l016_km else torch.empty(8 * H, NT, device=dh.device,
+                                                             dtype=torch.bfloat16)
                 ops.cast_bf16_t(dg2, out=dg16, outT=dgT16)
             hp = ops.lstm_hprev(h, H).view(NT, 2 * H)
             ready = torch.cuda.Event()
@@ -516,9 +525,14 @@ class _BLSTMFn(torch.autograd.Function):
                     gwi = None
                 elif early:
                     gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0,
-                                            l016=(dgT16, l016[0]) if l016 is not None else None)
+                                            l016=((dg16 if ctx.l016_km else dgT16), l016[0],
+                                                  ctx.l016_km) if l016 is not None else None)
                 elif l016 is not None:
-                    gcat = ops.gemm_bf16nt_splitk(dgT16, l016[0], NT)     # [8H, I]
+                    if ctx.l016_km:
+                        gcat = ops.wgrad_bf16_km(dg16, l016[0], NT,
+                                                 torch.empty(8 * H, Il, device=dh.device))
+                    else:
+                        gcat = ops.gemm_bf16nt_splitk(dgT16, l016[0], NT)     # [8H, I]
                     gwi = [gcat[:4 * H], gcat[4 * H:]]
                 else:
                     gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il,
@@ -530,8 +544,9 @@ class _BLSTMFn(torch.autograd.Function):
                     wi = [None, None] if (early or gwi is None) else gwi
                     _reduce_side(ctx.sink, po, (wi[0], gwh[0], db_ih[:4 * H], db_hh[:4 * H],
                                                 wi[1], gwh[1], db_ih[4 * H:], db_hh[4 * H:]))
-            for t in (dg, hp, inp) + ((dgT16, l016[0]) if l016 is not None else ()):
-                t.record_stream(side)     # main-stream memory read on the side stream
+            for t in (dg, hp, inp) + ((dg16, dgT16, l016[0]) if l016 is not None else ()):
+                if t is not None:
+                    t.record_stream(side)     # main-stream memory read on the side stream
             base = 8 * l
             if not main_first:
                 dxi, gwi_pair = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
@@ -587,13 +602,16 @@ def _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, sink, wih0, rows=None, l016=Non
     G4 = 4 * H
     rows = H if rows is None else rows       # one gate (i, f, g, o) per chunk
     bufs = [torch.empty(G4, Il, device=dg2.device, dtype=torch.float32) for _ in range(2)]
-    if l016 is not None:   # bf16 operands: dg^T [8H, NT], X^T [I, NT]
-        dgT16, XT16 = l016
+    if l016 is not None:   # bf16 operands: dg^T [8H, NT], X^T [I, NT] (or k-major dg, X)
+        dgT16, XT16, km = l016
         for r0 in range(0, G4, rows):
             for d in range(2):
                 chunk = bufs[d][r0:r0 + rows]
-                ops.gemm_bf16nt_splitk(dgT16[d * G4 + r0:d * G4 + r0 + rows], XT16, NT,
-                                       out=chunk)
+                if km:
+                    ops.wgrad_bf16_km(dgT16[:, d * G4 + r0:d * G4 + r0 + rows], XT16, NT, chunk)
+                else:
+                    ops.gemm_bf16nt_splitk(dgT16[d * G4 + r0:d * G4 + r0 + rows], XT16, NT,
+                                           out=chunk)
                 sink.reduce_chunk(wih0[d], chunk)
         for d in range(2):
             wih0[d].grad = bufs[d]

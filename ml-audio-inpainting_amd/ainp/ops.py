@@ -288,11 +288,12 @@ def bn_relu_apply_ntcf_bf16(y, scale, shift):
     return out, outT
 
 
-def bn_relu_apply_ntcf_cl(y, scale, shift, out32=True, out16=False):
+def bn_relu_apply_ntcf_cl(y, scale, shift, out32=True, out16=False, outT=True):
     """ainp_bn_relu_apply_ntcf_cl (round 5): relu(y*scale+shift) of a
     channel-last y [N, H, W, 64] as the LSTM input: fp32 X [N, W, 64*H]
-    (out32) and / or the bf16 X [N, W, 64*H] and X^T [64*H, N*W] (out16, row
-    stride rounded up to 8 elements).  Returns (X or None, (X16, XT16) or None)."""
+    (out32) and / or the bf16 X [N, W, 64*H] and (outT) X^T [64*H, N*W] (out16,
+    row stride rounded up to 8 elements).  Returns (X or None, (X16, XT16 or
+    None) or None)."""
     _req(y, "y", None)
     N, H, W, C = y.shape
     K, NW = C * H, N * W
@@ -300,8 +301,9 @@ def bn_relu_apply_ntcf_cl(y, scale, shift, out32=True, out16=False):
     o16 = oT = None
     if out16:
         o16 = torch.empty(N, W, K, device=y.device, dtype=torch.bfloat16)
-        ldt = -(-NW // 8) * 8
-        oT = torch.empty(K, ldt, device=y.device, dtype=torch.bfloat16)[:, :NW]
+        if outT:
+            ldt = -(-NW // 8) * 8
+            oT = torch.empty(K, ldt, device=y.device, dtype=torch.bfloat16)[:, :NW]
     _T.bn_relu_apply_ntcf_cl(y, scale, shift, out, o16, oT, _y_flag(y))
     return out, ((o16, oT) if out16 else None)
 
@@ -619,6 +621,11 @@ def proj_bwd_x6(gp, h, w, dh=None, dw=None):
 # current stream beside a split-K dW on the side stream, instead of the pair in
 # one 256 x 256 launch (ops.lstm_l0_bwd_bf16)
 B16_PAIR = os.environ.get("AINP_B16_PAIR", "1") != "0"
+# AINP_B16_KM=1: the pair's weight gradient reads dg [NT, 8H] and X [NT, I] as
+# they lie (k-major operands, ds_read_b64_tr_b16), so the bridge writes no X^T
+# and the BPTT gradient no dg^T copy
+# (C3-shape 8.21 -> 7.90 ms/step A/B, profiles/r05s_ab_b16_kmajor.txt)
+B16_KM = os.environ.get("AINP_B16_KM", "1") != "0"
 
 
 @functools.lru_cache(maxsize=64)
@@ -653,14 +660,30 @@ def g256_splits(shapes, max_split=16):
 
 def gemm_bf16nt_multi(problems):
     """Up to 3 bf16 GEMMs C = A . B^T in ONE launch (ainp_gemm_bf16nt_multi,
-    256 x 256 tiles): problems = [(A [M, >=K], B [N, >=K], C, K, nsplit, kc)],
-    C [M, N] (nsplit 1) or slabs [nsplit, M, N]."""
+    256 x 256 tiles): problems = [(A, B, C, K, nsplit, kc[, a_kmajor, b_kmajor])],
+    A [M, >=K] or k-major [>=K, M], B [N, >=K] or k-major [>=K, N], C [M, N]
+    (nsplit 1) or slabs [nsplit, M, N]."""
     ints = []
-    for A, B, C, K, S, kc in problems:
-        _work("gemm_bf16nt", 2.0 * A.shape[0] * B.shape[0] * K)
-        ints += [int(K), int(S), int(kc)]
+    for pr in problems:
+        A, B, C, K, S, kc = pr[:6]
+        akm, bkm = (pr[6], pr[7]) if len(pr) > 6 else (False, False)
+        _work("gemm_bf16nt", 2.0 * C.shape[-2] * C.shape[-1] * K)
+        ints += [int(K), int(S), int(kc), int(bool(akm)), int(bool(bkm))]
     _T.gemm_bf16nt_multi([p[0] for p in problems], [p[1] for p in problems],
                          [p[2] for p in problems], ints)
+
+
+def wgrad_bf16_km(dg16_cols, x16, NT, out):
+    """out [rows, I] = dg16_cols^T . X on the 256 x 256 tile from k-major
+    operands (dg16_cols: [NT, rows] column view of dg [NT, 8H]; x16 [NT, I]),
+    split over K by the makespan model, slabs summed in fixed order."""
+    rows, I = out.shape
+    (S, kc), = g256_splits(((rows, I, NT),))
+    C = out if S == 1 else torch.empty(S, rows, I, device=out.device)
+    gemm_bf16nt_multi([(dg16_cols, x16, C, NT, S, kc, True, True)])
+    if S > 1:
+        sum_slabs(C, S, out=out.view(-1))
+    return out
 
 
 def l0_bwd_bf16_eligible(NT, I, H):
@@ -669,19 +692,21 @@ def l0_bwd_bf16_eligible(NT, I, H):
     return B16_PAIR and NT % 32 == 0 and (8 * H) % 32 == 0 and I % 8 == 0
 
 
-def lstm_l0_bwd_bf16(dg16, dgT16, wT16, xT16, dx, gcat):
+def lstm_l0_bwd_bf16(dg16, dgT16, wT16, xB16, dx, gcat, km=False):
     """The bf16 layer-0 LSTM backward pair in ONE launch (nn.LSTM backward,
     models/CNNBLSTM/model.py:46-47,77):
-        dW_cat [8H, I] = dg^T . X   from dgT16 [8H, >=NT] and xT16 [I, >=NT]
+        dW_cat [8H, I] = dg^T . X   from dgT16 [8H, >=NT] and xB16 = X^T [I, >=NT]
+                                    (km: from dg16 and xB16 = X [NT, I], k-major)
         dX [NT, I]     = dg . W_cat from dg16 [NT, 8H] and wT16 = W_cat^T [I, 8H]
     the weight-gradient items (long K = N*T) first, the data-gradient items
     behind them; dW split over K only where the makespan model asks for it."""
     NT, G8 = dg16.shape
-    I = xT16.shape[0]
+    I = xB16.shape[1] if km else xB16.shape[0]
     (Sw, kcw), (Sx, kcx) = g256_splits(((G8, I, NT), (NT, I, G8)))
     Cw = gcat if Sw == 1 else torch.empty(Sw, G8, I, device=dg16.device)
     Cx = dx if Sx == 1 else torch.empty(Sx, NT, I, device=dg16.device)
-    gemm_bf16nt_multi([(dgT16, xT16, Cw, NT, Sw, kcw), (dg16, wT16, Cx, G8, Sx, kcx)])
+    pw = (dg16, xB16, Cw, NT, Sw, kcw, True, True) if km else (dgT16, xB16, Cw, NT, Sw, kcw)
+    gemm_bf16nt_multi([pw, (dg16, wT16, Cx, G8, Sx, kcx)])
     if Sw > 1:
         sum_slabs(Cw, Sw, out=gcat.view(-1))
     if Sx > 1:

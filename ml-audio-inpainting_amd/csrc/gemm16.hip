@@ -420,6 +420,54 @@ __device__ __forceinline__ bf16x8v frag(const unsigned char* img, int row, int c
                             *reinterpret_cast<const uint4*>(img + row * ROWB + 16 * swz(row, chunk)));
 }
 
+// k-major ("T") operand: element (r, k) at P[k*ld + r] -- the layer-0 weight
+// gradient's dg [NT, 8H] and X [NT, I] as they lie, no transposed copies.
+// Image: 32 k-rows of 256 elements (512 B), 16-byte chunk c of k-row kr at
+// physical chunk c ^ 4(kr & 3), so the transposed fragment reads below hit 64
+// distinct banks per half-wave.  Stage: wave w, instruction i covers k-rows
+// 2(2w+i), +1 (1 KB); lane L: k-row + L/32, physical chunk L % 32, fetching
+// the logical chunk it holds (columns past R clamp to R - 8: R % 8 == 0,
+// never stored).
+__device__ __forceinline__ int kswz(int kr, int c) { return c ^ (4 * (kr & 3)); }
+
+__device__ __forceinline__ void stage_km(const uint16_t* __restrict__ P, int64_t ld, int64_t r0,
+                                         int64_t R, int64_t k0, unsigned char* img, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int blk = 2 * wave + i;
+    const int kr = 2 * blk + (lane >> 5);
+    const int c = kswz(kr, lane & 31);
+    int64_t col = r0 + 8 * c;
+    col = col + 8 <= R ? col : R - 8;
+    const uint16_t* src = P + (k0 + kr) * ld + col;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)src, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16, 0, 0);
+  }
+}
+
+// The 32x32x16 operand of rows row0 .. row0+31, k = 16 ks + 8 (lane / 32) + 0..7,
+// from a k-major image by two ds_read_b64_tr_b16 (cdna_hip_programming.md
+// T10): lane 4q+p of each 16-lane group supplies k-row kb + q, columns
+// 4p .. 4p+3 of its group's 16; lane i of the group receives column i, rows
+// kb .. kb+3 -- the same (row, k) values frag() gives from a k-contiguous image.
+typedef short v4s16 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ bf16x8v frag_km(const unsigned char* img, int row0, int ks, int lane) {
+  const int g = (lane & 31) >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int col = row0 + 16 * g + 4 * p;
+  v4s16 h[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int kr = 16 * ks + 8 * (lane >> 5) + 4 * t + q;
+    const unsigned char* a = img + kr * 512 + 16 * kswz(kr, col >> 3) + 2 * (col & 7);
+    h[t] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (__attribute__((address_space(3))) v4s16*)(const_cast<unsigned char*>(a)));
+  }
+  typedef short v8s16 __attribute__((ext_vector_type(8)));
+  const v8s16 r = __builtin_shufflevector(h[0], h[1], 0, 1, 2, 3, 4, 5, 6, 7);
+  return __builtin_bit_cast(bf16x8v, r);
+}
+
 template <int N_INFLIGHT>
 __device__ __forceinline__ void wait_vm() {
   if (N_INFLIGHT == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
@@ -430,6 +478,7 @@ __device__ __forceinline__ void wait_vm() {
 // Tile (m0, n0) of Cs over k in [kbeg, kbeg + nk*BK): the 4-stage LDS-DMA ring
 // main loop and the store epilogue shared by the single- and multi-problem
 // kernels (bias only in split 0).
+template <bool AKM, bool BKM>
 __device__ __forceinline__ void tile256(int64_t M, int64_t N, const uint16_t* __restrict__ A,
                                         int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
                                         float* __restrict__ Cs, int64_t ldc, int64_t m0,
@@ -448,8 +497,10 @@ __device__ __forceinline__ void tile256(int64_t M, int64_t N, const uint16_t* __
 
   auto issue = [&](int kt) {
     unsigned char* st = smem + (kt % NSTAGE) * STAGE;
-    stage(A, lda, m0, M, kbeg + (int64_t)kt * BK, st, wave, lane);
-    stage(B, ldb, n0, N, kbeg + (int64_t)kt * BK, st + IMG, wave, lane);
+    if (AKM) stage_km(A, lda, m0, M, kbeg + (int64_t)kt * BK, st, wave, lane);
+    else stage(A, lda, m0, M, kbeg + (int64_t)kt * BK, st, wave, lane);
+    if (BKM) stage_km(B, ldb, n0, N, kbeg + (int64_t)kt * BK, st + IMG, wave, lane);
+    else stage(B, ldb, n0, N, kbeg + (int64_t)kt * BK, st + IMG, wave, lane);
   };
   // prologue: tiles 0, 1, 2 in flight
 #pragma unroll
@@ -472,9 +523,11 @@ __device__ __forceinline__ void tile256(int64_t M, int64_t N, const uint16_t* __
     for (int ks = 0; ks < BK / 16; ++ks) {
       bf16x8v a[4], b[2];
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = frag(sb, wn + j * 32 + li, 2 * ks + lh);
+      for (int j = 0; j < 2; ++j)
+        b[j] = BKM ? frag_km(sb, wn + j * 32, ks, lane) : frag(sb, wn + j * 32 + li, 2 * ks + lh);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = frag(sa, wm + i * 32 + li, 2 * ks + lh);
+      for (int i = 0; i < 4; ++i)
+        a[i] = AKM ? frag_km(sa, wm + i * 32, ks, lane) : frag(sa, wm + i * 32 + li, 2 * ks + lh);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -527,7 +580,8 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
   const int64_t kbeg = split * kc;
   const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
   const int nk = (int)((kend - kbeg) / BK);  // the launcher guarantees BK | kc, BK | K
-  tile256(M, N, A, lda, B, ldb, C + split * strideC, ldc, m0, n0, kbeg, nk, split, bias, smem);
+  tile256<false, false>(M, N, A, lda, B, ldb, C + split * strideC, ldc, m0, n0, kbeg, nk, split,
+                        bias, smem);
 }
 
 // Several bf16 GEMMs in ONE grid (ainp_gemm_bf16nt_multi): problem q's work
@@ -540,7 +594,7 @@ constexpr int MAXP = 3;
 struct MProb {
   const uint16_t* A; const uint16_t* B; float* C;
   int64_t lda, ldb, ldc, M, N, K, kc, strideC;
-  int tiles_m, tiles_n, nsplit;
+  int tiles_m, tiles_n, nsplit, a_km, b_km;
   int64_t items, first;
 };
 struct MJob {
@@ -570,8 +624,20 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_multi_kernel(MJob 
   const int64_t kbeg = split * P.kc;
   const int64_t kend = (kbeg + P.kc) < P.K ? (kbeg + P.kc) : P.K;
   const Bias nob{nullptr, nullptr, nullptr, nullptr, 0};
-  tile256(P.M, P.N, P.A, P.lda, P.B, P.ldb, P.C + split * P.strideC, P.ldc, m0, n0, kbeg,
-          (int)((kend - kbeg) / BK), split, nob, smem);
+  const int nk = (int)((kend - kbeg) / BK);
+  float* Cs = P.C + split * P.strideC;
+  if (P.a_km && P.b_km)
+    tile256<true, true>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split, nob,
+                        smem);
+  else if (P.a_km)
+    tile256<true, false>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split, nob,
+                         smem);
+  else if (P.b_km)
+    tile256<false, true>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split, nob,
+                         smem);
+  else
+    tile256<false, false>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split,
+                          nob, smem);
 }
 }  // namespace g256
 
@@ -965,7 +1031,9 @@ extern "C" int ainp_gemm_bf16nt_multi(const ainp_bf16_problem* probs, int nprobs
     const int nsplit = s.nsplit < 1 ? 1 : s.nsplit;
     const int64_t kc = nsplit == 1 ? s.K : s.kc;
     if (!s.A || !s.B || !s.C || s.M < 1 || s.N < 1 || s.K < g256::BK || s.K % g256::BK ||
-        s.lda % 8 || s.ldb % 8 || s.lda < s.K || s.ldb < s.K || s.ldc < s.N ||
+        s.lda % 8 || s.ldb % 8 || s.lda < (s.a_kmajor ? s.M : s.K) ||
+        s.ldb < (s.b_kmajor ? s.N : s.K) || s.ldc < s.N || (s.a_kmajor && s.M % 8) ||
+        (s.b_kmajor && s.N % 8) ||
         ((uintptr_t)s.A & 15) || ((uintptr_t)s.B & 15) || nsplit > 65535 ||
         (nsplit > 1 && (kc < g256::BK || kc % g256::BK || (int64_t)nsplit * kc < s.K ||
                         (int64_t)(nsplit - 1) * kc >= s.K || s.strideC < s.M * s.ldc)))
@@ -978,6 +1046,8 @@ extern "C" int ainp_gemm_bf16nt_multi(const ainp_bf16_problem* probs, int nprobs
     d.tiles_m = (int)cdiv(s.M, g256::BM);
     d.tiles_n = (int)cdiv(s.N, g256::BN);
     d.nsplit = nsplit;
+    d.a_km = s.a_kmajor ? 1 : 0;
+    d.b_km = s.b_kmajor ? 1 : 0;
     d.items = (int64_t)d.tiles_m * d.tiles_n * nsplit;
     d.first = first;
     first += (d.items + 7) / 8 * 8;

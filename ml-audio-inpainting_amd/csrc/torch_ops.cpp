@@ -930,28 +930,31 @@ void check_nt_bias(const OptT& a1, const OptT& a2, const OptT& b1, const OptT& b
   if (b2.has_value() && b2->defined()) numel_is(*b2, N - nsplit, "bias_b2");
 }
 
-// ainp_gemm_bf16nt_multi: problem q = A[q] [M, >=K], B[q] [N, >=K] (bf16,
-// unit-stride rows), C[q] [M, N] or split-K slabs [nsplit, M, N];
-// ints[3q .. 3q+2] = K, nsplit, kc.
+// ainp_gemm_bf16nt_multi: problem q = A[q] [M, >=K] (or k-major [>=K, >=M]),
+// B[q] [N, >=K] (or k-major [>=K, >=N]) (bf16, unit-stride rows), C[q] [M, N] or
+// split-K slabs [nsplit, M, N]; ints[5q .. 5q+4] = K, nsplit, kc, a_kmajor, b_kmajor.
 void gemm_bf16nt_multi(const std::vector<Tensor>& A, const std::vector<Tensor>& B,
                        const std::vector<Tensor>& C, const std::vector<int64_t>& ints) {
   const int64_t np = (int64_t)C.size();
   TORCH_CHECK(np >= 1 && np <= 3 && (int64_t)A.size() == np && (int64_t)B.size() == np &&
-                  (int64_t)ints.size() == 3 * np,
-              "gemm_bf16nt_multi: 1..3 problems (A, B, C each, 3 ints)");
+                  (int64_t)ints.size() == 5 * np,
+              "gemm_bf16nt_multi: 1..3 problems (A, B, C each, 5 ints)");
   GUARD(C[0]);
   std::vector<ainp_bf16_problem> pr(np);
   for (int64_t q = 0; q < np; ++q) {
-    const int64_t K = ints[3 * q], nsplit = ints[3 * q + 1], kc = ints[3 * q + 2];
+    const int64_t K = ints[5 * q], nsplit = ints[5 * q + 1], kc = ints[5 * q + 2];
+    const bool akm = ints[5 * q + 3] != 0, bkm = ints[5 * q + 4] != 0;
     const Tensor &a = A[q], &b = B[q], &c = C[q];
     TORCH_CHECK(a.dim() == 2 && b.dim() == 2 && a.stride(1) == 1 && b.stride(1) == 1,
-                "gemm_bf16nt_multi: A [M, >=K], B [N, >=K] with unit-stride rows");
-    TORCH_CHECK(a.size(1) >= K && b.size(1) >= K, "gemm_bf16nt_multi: K exceeds the operand rows");
-    const int64_t M = a.size(0), N = b.size(0);
+                "gemm_bf16nt_multi: 2-D operands with unit-stride rows");
     TORCH_CHECK((c.dim() == 2 && nsplit == 1) || (c.dim() == 3 && c.size(0) == nsplit),
                 "gemm_bf16nt_multi: C [M, N] or split-K slabs [nsplit, M, N]");
-    TORCH_CHECK(c.size(-2) == M && c.size(-1) == N && c.stride(-1) == 1,
-                "gemm_bf16nt_multi: C shape");
+    TORCH_CHECK(c.stride(-1) == 1, "gemm_bf16nt_multi: C rows must be unit-stride");
+    const int64_t M = c.size(-2), N = c.size(-1);
+    TORCH_CHECK(akm ? (a.size(0) >= K && a.size(1) == M) : (a.size(0) == M && a.size(1) >= K),
+                "gemm_bf16nt_multi: A must be [M, >=K] (or k-major [>=K, M])");
+    TORCH_CHECK(bkm ? (b.size(0) >= K && b.size(1) == N) : (b.size(0) == N && b.size(1) >= K),
+                "gemm_bf16nt_multi: B must be [N, >=K] (or k-major [>=K, N])");
     same_device(a, C[0]);
     same_device(b, C[0]);
     same_device(c, C[0]);
@@ -965,6 +968,8 @@ void gemm_bf16nt_multi(const std::vector<Tensor>& A, const std::vector<Tensor>& 
     p.M = M; p.N = N; p.K = K;
     p.nsplit = (int)nsplit; p.kc = kc;
     p.strideC = c.dim() == 3 ? c.stride(0) : 0;
+    p.a_kmajor = akm ? 1 : 0;
+    p.b_kmajor = bkm ? 1 : 0;
   }
   chk(ainp_gemm_bf16nt_multi(pr.data(), (int)np, stream_of(C[0])), "gemm_bf16nt_multi");
 }

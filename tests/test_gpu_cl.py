@@ -229,3 +229,37 @@ def test_cl_ntcf_bridge_and_backward(y16, H, W):
                                               ntcf=True, gy16=gy16, cl=True)
         assert rel(_nchw(gy1).float(), gy0.float()) < (4e-3 if gy16 else 1e-6)
         assert torch.equal(dg1, dg0) and torch.equal(db1, db0)
+
+
+def test_cnnblstm_bf16_step_kmajor_weight_gradient_bit_identical(monkeypatch):
+    """bf16 CNNBLSTM step with the layer-0 weight gradient read from k-major
+    dg / X (ops.B16_KM: no X^T from the bridge, no dg^T copy) against the
+    transposed-copy path: the same MFMAs in the same k order, so the loss and
+    every gradient are bit-identical (models/CNNBLSTM/model.py:46-47,77)."""
+    from ainp import cnnblstm, ops
+    cfg = {"data": {"sample_rate": 16000, "spectrogram": {"n_fft": 512, "hop_length": 192,
+                                                          "win_length": 384}},
+           "model": {"in_channels": 1, "num_lstm_layers": 2, "lstm_hidden_dim": 128,
+                     "enc_filters": [16, 32], "dec_filters": [16, 32]},
+           "accel": {"dtype": "bf16"}}
+    g = torch.Generator().manual_seed(5)
+    N, F, T = 4, 257, 336            # N*T % 32 == 0: the pair's k-major operand rule
+    x = (torch.randn(N, 1, F, T, generator=g) - 2.0).to(DEV)
+    mask = torch.zeros(N, F, T)
+    for i in range(N):
+        mask[i, :, 40 + 30 * i:57 + 30 * i] = 1.0
+    mask = mask.to(DEV)
+    tgt = torch.complex(torch.rand(N, F, T, generator=g), torch.rand(N, F, T, generator=g)).to(DEV)
+    res = []
+    for km in (True, False):
+        monkeypatch.setattr(ops, "B16_KM", km)
+        torch.manual_seed(0)
+        m = cnnblstm.StackedBLSTMCNN(config=cfg).to(DEV).train()
+        loss = cnnblstm.l1_pow10_loss(m(x), mask, tgt)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((float(loss.detach()),
+                    {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    assert res[0][0] == res[1][0]
+    for n, g1 in res[1][1].items():
+        assert torch.equal(res[0][1][n], g1), n

@@ -812,6 +812,55 @@ def test_gemm_bf16nt_multi_problems_match_single_launches():
         assert err < 1e-5, float(err)
 
 
+@pytest.mark.parametrize("akm,bkm", [(True, True), (True, False), (False, True)])
+def test_gemm_bf16nt_multi_kmajor_operands_bit_identical(akm, bkm):
+    """ainp_gemm_bf16nt_multi with k-major A and / or B (the operand read as it
+    lies, [K][ld], transposed in LDS by ds_read_b64_tr_b16) equals the
+    k-contiguous launch on the transposed copies bit for bit: ragged M / N
+    tiles, ld > M / N, split-K slabs."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(11)
+    for M, N, K, S in ((1024, 520, 2112, 3), (264, 776, 1056, 1), (40, 1000, 96, 1)):
+        A = _tobf16(torch.randn(M, K, generator=g)).cuda()
+        B = _tobf16(torch.randn(N, K, generator=g)).cuda()
+        Akm = torch.zeros(K, M + 16, dtype=torch.bfloat16, device="cuda")[:, :M]
+        Akm.copy_(A.T)
+        Bkm = torch.zeros(K, N + 8, dtype=torch.bfloat16, device="cuda")[:, :N]
+        Bkm.copy_(B.T)
+        kc = -(-K // S // 32) * 32 if S > 1 else K
+        shape = (S, M, N) if S > 1 else (M, N)
+        C0 = torch.full(shape, float("nan"), device="cuda")
+        C1 = torch.full(shape, float("nan"), device="cuda")
+        ops.gemm_bf16nt_multi([(A, B, C0, K, S, kc)])
+        ops.gemm_bf16nt_multi([(Akm if akm else A, Bkm if bkm else B, C1, K, S, kc, akm, bkm)])
+        torch.cuda.synchronize()
+        assert torch.equal(C0, C1), (M, N, K, S)
+        ref = A.double() @ B.double().T
+        got = C1.sum(0) if S > 1 else C1
+        assert float((got.double() - ref).norm() / ref.norm()) < 1e-5
+
+
+def test_lstm_l0_bwd_bf16_pair_kmajor_bit_identical():
+    """ops.lstm_l0_bwd_bf16(km=True) -- dW_cat from dg [NT, 8H] and X [NT, I]
+    k-major -- equals the transposed-copy pair bit for bit."""
+    from ainp import ops
+    NT, H, I = 10688, 128, 16448
+    g = torch.Generator().manual_seed(13)
+    dg16 = _tobf16(torch.randn(NT, 8 * H, generator=g) * 1e-3).cuda()
+    x16 = _tobf16(torch.randn(NT, I, generator=g)).cuda()
+    wT16 = _tobf16(torch.randn(I, 8 * H, generator=g) * 0.01).cuda()
+    out = []
+    for km in (False, True):
+        dx = torch.full((NT, I), float("nan"), device="cuda")
+        gcat = torch.full((8 * H, I), float("nan"), device="cuda")
+        ops.lstm_l0_bwd_bf16(dg16, None if km else dg16.T.contiguous(), wT16,
+                             x16 if km else x16.T.contiguous(), dx, gcat, km=km)
+        torch.cuda.synchronize()
+        out.append((dx, gcat))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize("NT,H,I", [(10688, 128, 16448), (1024, 64, 520)])
 def test_lstm_l0_bwd_bf16_pair(NT, H, I):
     """The bf16 layer-0 backward pair in one launch (ops.lstm_l0_bwd_bf16,
