@@ -272,6 +272,18 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
         bname = "dX gemm_bf16nt (dg16 x W_cat) + dW gemm_bf16nt_splitk (dg^T x X^T, side stream)"
         main_loop = ("bf16 operands in HBM (X, W_cat), 256x256x32 tiles staged by global_load_lds "
                      "into a 4-stage LDS ring, v_mfma_f32_32x32x16_bf16, f32 accumulate")
+        if ops.l0_bwd_bf16_eligible(M, I, H):
+            # the step's path (cnnblstm._BLSTMFn, round 5): both GEMMs in one
+            # gemm_bf16nt_256_multi launch, dW from k-major dg / X (B16_KM)
+            dxo16 = torch.empty(M, I, device=dev)
+            gcat = torch.empty(8 * H, I, device=dev)
+            km = ops.B16_KM
+            fused = lambda: ops.lstm_l0_bwd_bf16(dg16, None if km else dgT16, WT16,  # noqa: E731
+                                                 X16 if km else XT16, dxo16, gcat, km=km)
+            bname = ("g256::gemm_bf16nt_256_multi_kernel, one launch: dW_cat = dg^T X (weight-"
+                     "gradient items first" + (", k-major dg / X via ds_read_b64_tr_b16" if km
+                                               else "") + ") + dX = dg W_cat "
+                     "(ops.lstm_l0_bwd_bf16)")
     else:
         A = torch.randn(M, I, device=dev, generator=g)
         if not ops.GEMM_EXACT and ops.x6_256_eligible(M, 8 * H, I, 4 * H):
@@ -335,7 +347,8 @@ def l0_rooflines(model, B, T, H, I, bf16, reps, dev):
     roof_bwd = _roof(2 * flops, pair_s, bf16, bname + f" (M={M}, 8H={8 * H}, K={I})",
                      two_stream_dx_alone_ms=round(dx_s * 1e3, 4),
                      two_stream_dw_alone_ms=round(dw_s * 1e3, 4),
-                     traffic=_traffic("traffic_l0_pair_x6r.json") if fused is not None else None,
+                     traffic=(_traffic("traffic_l0_pair_x6r.json") if fused is not None
+                              and not bf16 else None),
                      what=("both GEMMs in one launch, as cnnblstm._BLSTMFn.backward runs them"
                            if fused is not None else
                            "dX on the current stream beside dW on a side stream, as "
