@@ -177,6 +177,126 @@ __device__ __forceinline__ bf16x8c cx6_ld(const unsigned char* p) {
   return __builtin_bit_cast(bf16x8c, *reinterpret_cast<const uint4*>(p));
 }
 
+// bf16 channel-last data gradient fed by LDS-DMA (round 5): the 64 -> 32
+// channel data gradient of the bf16 configuration (dy = the BatchNorm-backward
+// output gy, bf16 channel-last, no prologue: nothing to transform on the way
+// into LDS).  The conv3x3_x6_kernel<64, 32, dgrad, RPW 1, NP 1> instance
+// stages each 16-channel chunk's halo through registers and waits for it
+// once per chunk (SQ: MFMA busy 0.14, waits 0.69); here one persistent
+// workgroup per CU keeps the chunk images of the whole 64-channel halo in
+// LDS, double-buffered: global_load_lds_dwordx4 brings tile i+1's halo while
+// tile i's 36 MFMA steps run.  Same LDS image layout (per 16-channel plane:
+// [row][col][16], halves swizzled by column bit 3), same weights image, same
+// chunk -> tap MFMA order as the register-staged kernel: bit-identical.
+namespace cdd {
+constexpr int CI = 64, COP = 32, TR = 8, TC = 32, HR = TR + 2, HC = TC + 2;
+constexpr int XROW = HC * 32, XPLANE = HR * XROW;           // 1088, 10880
+constexpr int NPIX = HR * HC;                                // 340 halo pixels
+constexpr int XBLK = (NPIX * 32 + 1023) / 1024;              // 11 DMA blocks per plane
+constexpr int XPP = XBLK * 1024;                             // padded plane
+constexpr int NCK = CI / 16;                                 // 4 planes
+constexpr int XBUF = NCK * XPP;                              // 45056 per halo buffer
+constexpr int WROW = 9 * 32 + 16, WPLANE = COP * WROW;       // 304, 9728
+constexpr int NT = 512;
+}  // namespace cdd
+__device__ __attribute__((aligned(64))) uint16_t cdd_zero[8];   // zero-initialised
+
+__global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
+    const uint16_t* __restrict__ gy, const float* __restrict__ w, float* __restrict__ dx, int N,
+    int H, int W, int ntr, int ntc, int64_t ntiles) {
+  using namespace cdd;
+  __shared__ __attribute__((aligned(1024))) unsigned char sxa[XBUF];
+  __shared__ __attribute__((aligned(1024))) unsigned char sxb[XBUF];
+  __shared__ __attribute__((aligned(16))) unsigned char sw[NCK * WPLANE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  // weights once: plane kc, row co, tap, half -> w'[co][kc*16 + 8h + c][tap]
+  // = w[kc*16 + 8h + c][co][8 - tap] (the forward weight [64][32][3][3])
+  for (int u = tid; u < NCK * COP * 18; u += NT) {
+    const int half = u & 1, tap = (u >> 1) % 9, co = (u / 18) % COP, kc = u / (18 * COP);
+    float pw[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int ci = kc * 16 + 8 * half + c;
+      pw[c] = w[((int64_t)ci * COP + co) * 9 + (8 - tap)];
+    }
+    cx6_stage<1>(pw, sw + kc * WPLANE + co * WROW + tap * 32 + 16 * half, WPLANE);
+  }
+  // halo DMA of tile t into buffer buf: plane kc, block j (32 linear halo
+  // pixels, 1 KB); lane L -> pixel 32 j + L/2, physical half L % 2 holding
+  // the logical half (L % 2) ^ (col bit 3)
+  auto issue = [&](int64_t t, unsigned char* buf) {
+    const int tc = (int)(t % ntc), tr = (int)((t / ntc) % ntr), n = (int)(t / ((int64_t)ntc * ntr));
+    const int r0 = tr * TR, c0 = tc * TC;
+    for (int q = wave; q < NCK * XBLK; q += NT / 64) {
+      const int kc = q / XBLK, j = q % XBLK;
+      const int lp = 32 * j + (lane >> 1);
+      const uint16_t* src = cdd_zero;
+      if (lp < NPIX) {
+        const int row = lp / HC, col = lp % HC;
+        const int gr = r0 - 1 + row, gc = c0 - 1 + col;
+        const int hl = (lane & 1) ^ ((col >> 3) & 1);
+        if (gr >= 0 && gr < H && gc >= 0 && gc < W)
+          src = gy + (((int64_t)n * H + gr) * W + gc) * CI + kc * 16 + 8 * hl;
+      }
+      __builtin_amdgcn_global_load_lds((const void*)src,
+                                       (__attribute__((address_space(3))) void*)(
+                                           buf + kc * XPP + j * 1024),
+                                       16, 0, 0);
+    }
+  };
+  int64_t t = blockIdx.x;
+  if (t < ntiles) issue(t, sxa);
+  bool cur_a = true;
+  for (; t < ntiles; t += gridDim.x) {
+    unsigned char* sx = cur_a ? sxa : sxb;
+    // this tile's halo landed (every wave's DMA), the weights are staged
+    __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
+    __syncthreads();
+    const int64_t tn = t + gridDim.x;
+    if (tn < ntiles) issue(tn, cur_a ? sxb : sxa);   // lands during this tile
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < NCK; ++kc) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3, dxx = tap % 3;
+        const int hcol = li + dxx;
+        const bf16x8c a = cx6_ld(sw + kc * WPLANE + li * WROW + tap * 32 + 16 * lh);
+        const bf16x8c b = cx6_ld(sx + kc * XPP + (wave + dy) * XROW + hcol * 32 +
+                                 16 * (lh ^ ((hcol >> 3) & 1)));
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+      }
+    }
+    // epilogue: D[co = (r&3) + 8(r>>2) + 4lh][pixel col li] of output row
+    // r0 + wave; channel-last, 4 consecutive channels per 16-byte store
+    const int tc = (int)(t % ntc), tr = (int)((t / ntc) % ntr), n = (int)(t / ((int64_t)ntc * ntr));
+    const int row = tr * TR + wave, col = tc * TC + li;
+    if (row < H && col < W) {
+      float* d = dx + (((int64_t)n * H + row) * W + col) * COP;
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int co0 = 8 * rb + 4 * lh;
+        *reinterpret_cast<float4*>(d + co0) =
+            make_float4(acc[4 * rb], acc[4 * rb + 1], acc[4 * rb + 2], acc[4 * rb + 3]);
+      }
+    }
+    __syncthreads();   // every wave is done with sx before it is re-filled
+    cur_a = !cur_a;
+  }
+}
+
+// AINP_DGRAD16_DMA=0: the register-staged kernel for that data gradient (A/B)
+static bool dgrad16_dma() {
+  static const bool v = [] {
+    const char* e = getenv("AINP_DGRAD16_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // RPW output rows per wave: 2 (16-row tiles, one workgroup per CU) or 1
 // (8-row tiles: half the halo LDS, two workgroups per CU).
 template <int CI, int COP, bool DGRAD, int RPW, int NP, bool G16 = false, bool XL = false,
@@ -507,6 +627,17 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
   if (y16 || (x16 && !(dgrad && !stats && b16))) return 2;   // bf16 storage: no such kernel
   // channel-last: only the stat-free data gradient (8-row tiles) has it
   if (lay && !(dgrad && !stats)) return 2;
+  if (dgrad && !stats && b16 && x16 && lay == (CL_X | CL_Y) && Cin == cdd::CI &&
+      Cout == cdd::COP && !bias && !sc && dgrad16_dma()) {
+    const int ntr = (int)cdiv(H, cdd::TR), ntc = (int)cdiv(W, cdd::TC);
+    const int64_t nt = N * (int64_t)ntr * ntc;
+    *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
+    const int grid = (int)(nt < 256 ? nt : 256);   // one persistent workgroup per CU
+    hipLaunchKernelGGL(conv3x3_dgrad_b16dma_kernel, dim3(grid), dim3(cdd::NT), 0, s,
+                       reinterpret_cast<const uint16_t*>(x), w, y, (int)N, (int)H, (int)W, ntr,
+                       ntc, nt);
+    return check_launch("conv3x3_dgrad_b16dma");
+  }
   *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
