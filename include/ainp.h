@@ -465,6 +465,24 @@ int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale
                               int64_t count, void* gy, float* dgamma, float* dbeta,
                               int64_t N, int C, int64_t H, int64_t W, int g_ntcf, int flags,
                               void* stream);
+/* Round 5: ainp_conv3x3_dgrad_ex followed by the step-1 reduce of the
+ * BatchNorm+ReLU the data gradient feeds, in one pass where a split-bf16
+ * data-gradient kernel serves the pair: its epilogue sums (gz, gz*xhat) of
+ * the dx it just computed (y = that BatchNorm's pre-BN input, channel-last,
+ * AINP_BN_Y16: bf16 storage), so dx and y are not read again.  dx is written
+ * as ainp_conv3x3_dgrad_ex writes it; sums as ainp_bn_relu_bwd_reduce_ex
+ * with AINP_BN_CL would (same terms, another fixed summation order).  flags:
+ * ainp_conv3x3_dgrad_ex's, AINP_CONV_YCL required; Cin % 8 == 0, <= 64;
+ * dx / y / scale / shift / save 16-byte aligned.  Pairs without a fused
+ * kernel (or AINP_DGRAD_BNR=0) run the two passes.  Replaces the
+ * conv-backward + BatchNorm2d-backward pair of autograd on
+ * models/CNNBLSTM/model.py:35-60.  workspace:
+ * ainp_conv3x3_dgrad_bnr_workspace(...) bytes. */
+int64_t ainp_conv3x3_dgrad_bnr_workspace(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
+int ainp_conv3x3_dgrad_bnr(const float* dy, const float* w, float* dx, int64_t N, int Cin,
+                           int Cout, int64_t H, int64_t W, int flags, const void* y,
+                           const float* scale, const float* shift, const float* save_mean_rstd,
+                           void* workspace, double* sums, int bn_flags, void* stream);
 
 /* bf16 configuration (BASELINE C3): the encoder's last BN+ReLU writes the
  * layer-0 LSTM input directly as bf16 (nearest-even) in both layouts the

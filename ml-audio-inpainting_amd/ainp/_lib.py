@@ -64,6 +64,9 @@ _SIGS = {
                                    c_int64, P]),
     "ainp_conv3x3_fwd_ex": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,
                                     c_int64, c_int, P]),
+    "ainp_conv3x3_dgrad_bnr_workspace": (c_int64, [c_int64, c_int, c_int, c_int64, c_int64]),
+    "ainp_conv3x3_dgrad_bnr": (c_int, [P, P, P, c_int64, c_int, c_int, c_int64, c_int64, c_int,
+                                       P, P, P, P, P, P, c_int, P]),
     "ainp_conv3x3_dgrad_ex": (c_int, [P, P, P, P, c_int64, c_int, c_int, c_int64, c_int64, c_int,
                                       P]),
     "ainp_conv3x3_wgrad_ex": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int, c_int64,

@@ -180,6 +180,7 @@ class _ConvStackFn(torch.autograd.Function):
         grads = [None] * len(params)
         g = g.contiguous()
         gx = None
+        pre_sums = None   # the next block's BatchNorm reduce, fused into this dgrad
         N, H, W = x.shape[0], x.shape[2], x.shape[3]
         for bi in range(nb - 1, -1, -1):
             has_bn, _ = ctx.spec[bi]
@@ -190,8 +191,9 @@ class _ConvStackFn(torch.autograd.Function):
             if has_bn:
                 sc, sh, sv = ctx.affine[bi]
                 ntcf = ctx.out_ntcf and bi == nb - 1
-                sums = _allreduce(ctx.comm, ops.bn_relu_bwd_reduce(g, y, sc, sh, sv, ntcf,
-                                                                   cl=ycl))
+                if pre_sums is None:
+                    pre_sums = ops.bn_relu_bwd_reduce(g, y, sc, sh, sv, ntcf, cl=ycl)
+                sums, pre_sums = _allreduce(ctx.comm, pre_sums), None
                 cnt = ctx.count
                 if ctx.count_dev is not None:
                     sums, cnt = torch.cat([sums, ctx.count_dev]), 0
@@ -255,12 +257,25 @@ class _ConvStackFn(torch.autograd.Function):
             else:
                 dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16, **lw)
             grads[p0], grads[p0 + 1] = dw, db
-            if bi > 0 or ctx.needs_input_grad[0]:
+            if (bi > 0 and xcl and DGRAD_BNR and ctx.spec[bi - 1][0]
+                    and ctx.affine[bi - 1][2] is not None):
+                # dx channel-last into a BatchNorm+ReLU: its backward reduce
+                # is summed by the data gradient's epilogue
+                psc, psh, psv = ctx.affine[bi - 1]
+                g, pre_sums = ops.conv3x3_dgrad_bnr(gy, w, ys[bi - 1], psc, psh, psv,
+                                                    bf16=ctx.bf16, xcl=ycl)
+            elif bi > 0 or ctx.needs_input_grad[0]:
                 # dx in this conv's input layout (the previous block's y)
                 g = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16, xcl=ycl, ycl=xcl)
                 if bi == 0:
                     gx = g
         return (gx, None, None, None, None, None, None, None, *grads)
+
+
+# Round 5: a data gradient feeding a BatchNorm+ReLU with channel-last
+# activations also sums that BatchNorm's backward reduce in its epilogue
+# (ops.conv3x3_dgrad_bnr; AINP_DGRAD_BNR=0: the separate reduce pass)
+DGRAD_BNR = os.environ.get("AINP_DGRAD_BNR", "1") != "0"
 
 
 # Round 5: channel-last activations ([N, F, T, C]) between the convs of both

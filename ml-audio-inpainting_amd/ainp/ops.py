@@ -844,6 +844,26 @@ def conv3x3_dgrad(dy, w, bf16=False, xcl=False, ycl=False):
     return dx
 
 
+def conv3x3_dgrad_bnr(dy, w, y, scale, shift, save, bf16=False, xcl=False):
+    """The data gradient (dx channel-last [N, H, W, Cin]) and the reduce step
+    of the BatchNorm+ReLU backward it feeds (ainp_conv3x3_dgrad_bnr): y is that
+    layer's pre-BatchNorm output [N, H, W, Cin] (fp32 or bf16 storage).
+    Returns (dx, sums) -- sums as bn_relu_bwd_reduce(dx, y, ..., cl=True)."""
+    _req(dy, "dy", None); _req(w, "w"); _req(y, "y", None)
+    if xcl:
+        N, H, W, Cout = dy.shape
+    else:
+        N, Cout, H, W = dy.shape
+    Cin = w.shape[1]
+    dx = torch.empty((N, H, W, Cin), device=dy.device, dtype=torch.float32)
+    ws = torch.empty(_lib.lib.ainp_conv3x3_dgrad_bnr_workspace(N, Cin, Cout, H, W),
+                     device=dy.device, dtype=torch.uint8)
+    sums = torch.empty(2 * Cin, device=dy.device, dtype=torch.float64)
+    _T.conv3x3_dgrad_bnr(dy, w, dx, _dy_flags(dy, bf16) | (CONV_XCL if xcl else 0) | CONV_YCL,
+                         y, scale, shift, save, ws, sums, _y_flag(y))
+    return dx, sums
+
+
 def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False, out=None,
                   xcl=False, gcl=False):
     """out: optional preallocated (dw, db) to write.  dy fp32, or bf16 storage

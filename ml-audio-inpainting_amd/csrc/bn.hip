@@ -464,6 +464,11 @@ __global__ __launch_bounds__(256) void bn_cl_partials_sum(const double* __restri
   if (tid == 0) sums[o] = red[0];
 }
 
+int bn_cl_sum_partials(const double* partial, int nblk, int C2, double* sums, hipStream_t s) {
+  hipLaunchKernelGGL(bn_cl_partials_sum, dim3(C2), dim3(256), 0, s, partial, nblk, C2, sums);
+  return check_launch("bn_cl_partials_sum");
+}
+
 template <int C, bool GB16, bool YB16, bool OB16>
 __global__ __launch_bounds__(256) void bn_relu_bwd_apply_cl(
     const void* __restrict__ g, const void* __restrict__ y, const float* __restrict__ scale,

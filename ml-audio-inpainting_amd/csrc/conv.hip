@@ -700,14 +700,35 @@ template <int CIN, int COUT, bool DGRAD, bool PRO, int PX, bool XL = false, bool
 __global__ __launch_bounds__(384 / PX) void conv3x3_small_fwd(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
-    float* __restrict__ y, double* __restrict__ stats, int H, int W) {
+    float* __restrict__ y, double* __restrict__ stats, int H, int W, Bnr bnr) {
   constexpr int TR = CV_FT, TC = CV_TT, LR = TC + 2, NT = 384 / PX, TPR = TC / PX, NWV = NT / 64;
   __shared__ float sx[CIN * (TR + 2) * LR];
   __shared__ float sw[COUT][CIN][9];
   __shared__ double sred[2][NWV][COUT];
+  // fused BatchNorm-backward reduce of a channel-last dx (Bnr): the (gz,
+  // gz * xhat) terms replace (v, v^2); y is loaded before the tile is staged
+  // and the constants sit in LDS
+  constexpr bool FZ = DGRAD && YL && COUT % 4 == 0;
+  __shared__ float sbn[FZ ? 4 * COUT : 1];
   const int n = blockIdx.z, f0 = blockIdx.y * TR, t0 = blockIdx.x * TC;
   const int tid = threadIdx.x;
   const int64_t HW = (int64_t)H * W;
+  const bool fused = FZ && stats && bnr.y != nullptr;
+  uint4 yr[FZ ? PX : 1][FZ ? COUT / 4 : 1];
+  if constexpr (FZ) {
+    if (fused) {
+      bnr_stage(bnr, sbn, COUT, COUT, tid, NT);
+      const int f = f0 + tid / TPR;
+#pragma unroll
+      for (int q = 0; q < PX; ++q) {
+        const int t = t0 + tid % TPR + TPR * q;
+        const bool ok = f < H && t < W;
+#pragma unroll
+        for (int c4 = 0; c4 < COUT / 4; ++c4)
+          yr[q][c4] = bnr_ld4(bnr, ok ? ((int64_t)n * HW + (int64_t)f * W + t) * COUT + 4 * c4 : 0);
+      }
+    }
+  }
   stage_small_tile<CIN, PRO, NT, XL>(x, in_scale, in_shift, sx, n, f0, t0, H, W);
   for (int i = tid; i < COUT * CIN * 9; i += blockDim.x) {
     const int co = i / (CIN * 9), ci = (i / 9) % CIN, tap = i % 9;
@@ -759,12 +780,30 @@ __global__ __launch_bounds__(384 / PX) void conv3x3_small_fwd(
   }
   if (stats) {
     const int wave = tid >> 6;
+    float ts[FZ ? PX : 1][FZ ? COUT : 1], tq[FZ ? PX : 1][FZ ? COUT : 1];
+    if constexpr (FZ) {
+      if (fused) {
+#pragma unroll
+        for (int q = 0; q < PX; ++q)
+#pragma unroll
+          for (int c4 = 0; c4 < COUT / 4; ++c4) {
+            const float v4[4] = {acc[q][4 * c4], acc[q][4 * c4 + 1], acc[q][4 * c4 + 2],
+                                 acc[q][4 * c4 + 3]};
+            float yv[4];
+            bnr_dec4(bnr.y16, yr[q][c4], yv);
+            bnr_terms4<COUT>(sbn, 4 * c4, yv, v4, ok[q], &ts[q][4 * c4], &tq[q][4 * c4]);
+          }
+      }
+    }
 #pragma unroll
     for (int co = 0; co < COUT; ++co) {
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int q = 0; q < PX; ++q)
-        if (ok[q]) {
+        if (FZ && fused) {
+          a += ts[FZ ? q : 0][FZ ? co : 0];
+          b += tq[FZ ? q : 0][FZ ? co : 0];
+        } else if (ok[q]) {
           a += acc[q][co];
           b = fmaf(acc[q][co], acc[q][co], b);   // explicit: every instance rounds alike
         }
@@ -1111,19 +1150,19 @@ static bool small_pair(int a, int b) {
 template <int CIN, int COUT, bool XL, bool YL>
 static void launch_small_fwd_l(bool dgrad, const float* x, const float* w, const float* bias,
                                const float* sc, const float* sh, float* y, double* stats,
-                               int64_t N, int64_t H, int64_t W, hipStream_t s) {
+                               int64_t N, int64_t H, int64_t W, hipStream_t s, const Bnr& bnr) {
   dim3 grid((unsigned)cdiv(W, CV_TT), (unsigned)cdiv(H, CV_FT), (unsigned)N);
   constexpr int PX = COUT >= 16 ? 3 : 1;
   const dim3 block(384 / PX);
   if (dgrad)
     hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, true, false, PX, XL, YL>), grid, block, 0, s,
-                       x, w, bias, sc, sh, y, stats, (int)H, (int)W);
+                       x, w, bias, sc, sh, y, stats, (int)H, (int)W, bnr);
   else if (sc)
     hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, true, PX, XL, YL>), grid, block, 0, s,
-                       x, w, bias, sc, sh, y, stats, (int)H, (int)W);
+                       x, w, bias, sc, sh, y, stats, (int)H, (int)W, Bnr{});
   else
     hipLaunchKernelGGL((conv3x3_small_fwd<CIN, COUT, false, false, PX, XL, YL>), grid, block, 0,
-                       s, x, w, bias, sc, sh, y, stats, (int)H, (int)W);
+                       s, x, w, bias, sc, sh, y, stats, (int)H, (int)W, Bnr{});
 }
 
 // lay (round 5): bit 0 = input channel-last (a 16-channel input), bit 1 =
@@ -1132,19 +1171,20 @@ static void launch_small_fwd_l(bool dgrad, const float* x, const float* w, const
 template <int CIN, int COUT>
 static void launch_small_fwd(bool dgrad, const float* x, const float* w, const float* bias,
                              const float* sc, const float* sh, float* y, double* stats,
-                             int64_t N, int64_t H, int64_t W, hipStream_t s, int lay = 0) {
+                             int64_t N, int64_t H, int64_t W, hipStream_t s, int lay,
+                             const Bnr& bnr) {
   const bool xl = (lay & 1) && CIN >= 16, yl = (lay & 2) && COUT >= 16;
-  if (xl) launch_small_fwd_l<CIN, COUT, true, false>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s);
-  else if (yl) launch_small_fwd_l<CIN, COUT, false, true>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s);
-  else launch_small_fwd_l<CIN, COUT, false, false>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s);
+  if (xl) launch_small_fwd_l<CIN, COUT, true, false>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, bnr);
+  else if (yl) launch_small_fwd_l<CIN, COUT, false, true>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, bnr);
+  else launch_small_fwd_l<CIN, COUT, false, false>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, bnr);
 }
 
 static int small_fwd_dispatch(bool dgrad, const float* x, const float* w, const float* bias,
                               const float* sc, const float* sh, float* y, double* stats,
                               int64_t N, int Cin, int Cout, int64_t H, int64_t W, hipStream_t s,
-                              int lay = 0) {
+                              int lay = 0, const Bnr& bnr = Bnr{}) {
 #define AINP_SF(A, B) \
-  if (Cin == A && Cout == B) { launch_small_fwd<A, B>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, lay); return check_launch("conv3x3_small_fwd"); }
+  if (Cin == A && Cout == B) { launch_small_fwd<A, B>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, lay, bnr); return check_launch("conv3x3_small_fwd"); }
   AINP_SF(1, 16) AINP_SF(2, 16) AINP_SF(16, 1) AINP_SF(16, 2)
 #undef AINP_SF
   return record_msg("conv3x3: no small-channel kernel for this pair");
@@ -1264,7 +1304,7 @@ int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                   bool x16, bool y16, int lay);
+                   bool x16, bool y16, int lay, const Bnr* bnr = nullptr);
 
 // conv_x6.hip (fp32-accurate split-bf16 MFMA) serves every pair it has an
 // instantiation for unless AINP_CONV_EXACT=1 selects the exact f32 kernels.
@@ -1439,6 +1479,71 @@ extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,
                                   int Cout, int64_t H, int64_t W,
                                   void* stream) {
   return ainp_conv3x3_dgrad_ex(dy, w, dx, workspace, N, Cin, Cout, H, W, 0, stream);
+}
+
+// Round 5: the data gradient with the consuming BatchNorm's backward reduce
+// fused into its epilogue (conv_x6.hip Bnr): the split-bf16 data-gradient
+// kernels with a channel-last dx sum (gz, gz * xhat) of the value they just
+// computed into per-workgroup partials, so the separate reduce pass over dx
+// and y disappears.  Pairs without such a kernel run the data gradient and
+// then the channel-last reduce (same results, two passes).
+static bool dgrad_bnr_env() {
+  static const bool v = [] {
+    const char* e = getenv("AINP_DGRAD_BNR");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+extern "C" int64_t ainp_conv3x3_dgrad_bnr_workspace(int64_t N, int Cin, int Cout, int64_t H,
+                                                    int64_t W) {
+  (void)Cout;
+  if (N < 0 || Cin < 1 || H < 1 || W < 1) return 0;
+  int64_t rows = N * cdiv(H, 8) * cdiv(W, 32);            // 8-row tiles
+  const int64_t pers = 512 * (int64_t)X6_OCC_MAX;         // persistent grids
+  if (rows < pers) rows = pers;
+  if (rows < exact_stat_parts(N, H, W)) rows = exact_stat_parts(N, H, W);   // small convs
+  const int64_t fused = rows * 2 * Cin * (int64_t)sizeof(double);
+  const int64_t sep = (int64_t)ainp_bn_relu_bwd_workspace(N, Cin, H, W);
+  return fused > sep ? fused : sep;
+}
+
+extern "C" int ainp_conv3x3_dgrad_bnr(const float* dy, const float* w, float* dx, int64_t N,
+                                      int Cin, int Cout, int64_t H, int64_t W, int flags,
+                                      const void* y, const float* scale, const float* shift,
+                                      const float* save_mean_rstd, void* workspace, double* sums,
+                                      int bn_flags, void* stream) {
+  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  if (!dy || !w || !dx || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
+      N < 1 || Cin < 1 || Cout < 1 || H < 1 || W < 1 || N > 65535 ||
+      !conv_grad_flags_ok(flags, false) || !(flags & AINP_CONV_YCL) ||
+      (bn_flags & ~AINP_BN_Y16) || Cin % 8 != 0 || Cin > 64 ||
+      !al16(dx) || !al16(y) || !al16(scale) || !al16(shift) || !al16(save_mean_rstd))
+    return record_msg("ainp_conv3x3_dgrad_bnr: bad argument (channel-last dx and y, C % 8 == 0 "
+                      "and <= 64, 16-byte aligned dx / y / scale / shift / save)");
+  const hipStream_t s = as_stream(stream);
+  const Bnr bnr{y, scale, shift, save_mean_rstd, (bn_flags & AINP_BN_Y16) ? 1 : 0};
+  double* partial = reinterpret_cast<double*>(workspace);
+  if (dgrad_bnr_env() && small_pair(Cout, Cin) && Cin % 4 == 0 && !(flags & AINP_CONV_DY16)) {
+    // 1 -> 16 channels: the small kernel's channel-last epilogue
+    const int rc = small_fwd_dispatch(true, dy, w, nullptr, nullptr, nullptr, dx, partial, N,
+                                      Cout, Cin, H, W, s, conv_lay(flags), bnr);
+    if (rc) return rc;
+    return bn_cl_sum_partials(partial, (int)exact_stat_parts(N, H, W), 2 * Cin, sums, s);
+  }
+  if (dgrad_bnr_env() && !small_pair(Cout, Cin) && !conv_exact_env()) {
+    int64_t parts = 0;
+    const int rc = conv_x6_launch(true, dy, w, nullptr, nullptr, nullptr, dx, partial, N, Cout,
+                                  Cin, H, W, s, &parts, (flags & AINP_CONV_BF16) != 0,
+                                  (flags & AINP_CONV_DY16) != 0, false, conv_lay(flags), &bnr);
+    if (rc == AINP_OK) return bn_cl_sum_partials(partial, (int)parts, 2 * Cin, sums, s);
+    if (rc < 0) return rc;
+  }
+  const int rc = ainp_conv3x3_dgrad_ex(dy, w, dx, nullptr, N, Cin, Cout, H, W, flags, stream);
+  if (rc) return rc;
+  return ainp_bn_relu_bwd_reduce_ex(dx, reinterpret_cast<const float*>(y), scale, shift,
+                                    save_mean_rstd, workspace, sums, N, Cin, H, W, 0,
+                                    AINP_BN_CL | (bn_flags & AINP_BN_Y16), stream);
 }
 
 extern "C" int ainp_conv3x3_dy16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {

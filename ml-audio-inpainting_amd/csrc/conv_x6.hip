@@ -130,6 +130,32 @@ __device__ __forceinline__ void cl_st4(float* y, int64_t e, float a, float b, fl
   }
 }
 
+// Round 5: the BatchNorm-backward reduce of the layer a data gradient feeds
+// (bn.hip bn_relu_bwd_reduce_cl), fused into the data gradient's epilogue.
+// With y = that layer's pre-BatchNorm output (channel-last, fp32 or bf16
+// storage) and v the dx value just computed, the epilogue sums
+//   gz = v if y * scale + shift > 0 else 0   and   gz * (y - mean) * rstd
+// in the (sum, sum of squares) slots of the forward's BatchNorm partials --
+// the [part][2C] rows bn_cl_partials_sum reduces -- so the separate reduce
+// pass (a full re-read of dx and y) goes away.  Bnr: common.h.
+// 16 values per lane of a 32x32 MFMA accumulator -> lane li (of its 32-lane
+// half) holds the sum over the half of value li >> 1 (fixed butterfly order)
+__device__ __forceinline__ float x6_reduce16(const float (&v)[16], int li) {
+  float t8[8], t4[4], t2[2];
+  const bool b4 = li & 16, b3 = li & 8, b2 = li & 4, b1 = li & 2;
+#pragma unroll
+  for (int k = 0; k < 8; ++k)
+    t8[k] = (b4 ? v[k + 8] : v[k]) + __shfl_xor(b4 ? v[k] : v[k + 8], 16, 64);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    t4[k] = (b3 ? t8[k + 4] : t8[k]) + __shfl_xor(b3 ? t8[k] : t8[k + 4], 8, 64);
+#pragma unroll
+  for (int k = 0; k < 2; ++k)
+    t2[k] = (b2 ? t4[k + 2] : t4[k]) + __shfl_xor(b2 ? t4[k] : t4[k + 2], 4, 64);
+  const float t1 = (b1 ? t2[1] : t2[0]) + __shfl_xor(b1 ? t2[0] : t2[1], 2, 64);
+  return t1 + __shfl_xor(t1, 1, 64);
+}
+
 // split 8 floats into three packed bf16 vectors (8 x bf16 each), exactly
 __device__ __forceinline__ void cx6_split8(const float (&v)[8], uint4& p0, uint4& p1, uint4& p2) {
   uint32_t q0[4], q1[4], q2[4];
@@ -198,18 +224,27 @@ constexpr int NCK = CI / 16;                                 // 4 planes
 constexpr int XBUF = NCK * XPP;                              // 45056 per halo buffer
 constexpr int WROW = 9 * 32 + 16, WPLANE = COP * WROW;       // 304, 9728
 constexpr int NT = 512;
+constexpr int YBLK = TR * TC * COP * 2 / 1024;              // 16 blocks: bf16 y of a tile
 }  // namespace cdd
 __device__ __attribute__((aligned(64))) uint16_t cdd_zero[8];   // zero-initialised
 
 __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
-    const uint16_t* __restrict__ gy, const float* __restrict__ w, float* __restrict__ dx, int N,
-    int H, int W, int ntr, int ntc, int64_t ntiles) {
+    const uint16_t* __restrict__ gy, const float* __restrict__ w, float* __restrict__ dx,
+    double* __restrict__ stats, Bnr bnr, int N, int H, int W, int ntr, int ntc, int64_t ntiles) {
   using namespace cdd;
   __shared__ __attribute__((aligned(1024))) unsigned char sxa[XBUF];
   __shared__ __attribute__((aligned(1024))) unsigned char sxb[XBUF];
   __shared__ __attribute__((aligned(16))) unsigned char sw[NCK * WPLANE];
+  // fused BatchNorm-backward reduce (stats != nullptr, bf16 y): the tile's y
+  // [8 x 32 pixels][32 channels] rides the halo DMA into a second double
+  // buffer, the layer's constants sit in sbn -- the epilogue waits on LDS only
+  __shared__ __attribute__((aligned(1024))) unsigned char sya[YBLK * 1024];
+  __shared__ __attribute__((aligned(1024))) unsigned char syb[YBLK * 1024];
+  __shared__ float sbn[4 * COP];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
+  const bool fz = stats != nullptr;
+  if (fz) bnr_stage(bnr, sbn, COP, COP, tid, NT);
   // weights once: plane kc, row co, tap, half -> w'[co][kc*16 + 8h + c][tap]
   // = w[kc*16 + 8h + c][co][8 - tap] (the forward weight [64][32][3][3])
   for (int u = tid; u < NCK * COP * 18; u += NT) {
@@ -225,36 +260,50 @@ __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
   // halo DMA of tile t into buffer buf: plane kc, block j (32 linear halo
   // pixels, 1 KB); lane L -> pixel 32 j + L/2, physical half L % 2 holding
   // the logical half (L % 2) ^ (col bit 3)
-  auto issue = [&](int64_t t, unsigned char* buf) {
+  // y block j of the tile (fz): lane L -> pixel 16 j + L/4, channels 8 (L % 4) ..
+  const uint16_t* yg = reinterpret_cast<const uint16_t*>(bnr.y);
+  auto issue = [&](int64_t t, unsigned char* buf, unsigned char* ybuf) {
     const int tc = (int)(t % ntc), tr = (int)((t / ntc) % ntr), n = (int)(t / ((int64_t)ntc * ntr));
     const int r0 = tr * TR, c0 = tc * TC;
-    for (int q = wave; q < NCK * XBLK; q += NT / 64) {
-      const int kc = q / XBLK, j = q % XBLK;
-      const int lp = 32 * j + (lane >> 1);
+    const int nblk = NCK * XBLK + (fz ? YBLK : 0);
+    for (int q = wave; q < nblk; q += NT / 64) {
       const uint16_t* src = cdd_zero;
-      if (lp < NPIX) {
-        const int row = lp / HC, col = lp % HC;
-        const int gr = r0 - 1 + row, gc = c0 - 1 + col;
-        const int hl = (lane & 1) ^ ((col >> 3) & 1);
-        if (gr >= 0 && gr < H && gc >= 0 && gc < W)
-          src = gy + (((int64_t)n * H + gr) * W + gc) * CI + kc * 16 + 8 * hl;
+      unsigned char* dst;
+      if (q < NCK * XBLK) {
+        const int kc = q / XBLK, j = q % XBLK;
+        const int lp = 32 * j + (lane >> 1);
+        if (lp < NPIX) {
+          const int row = lp / HC, col = lp % HC;
+          const int gr = r0 - 1 + row, gc = c0 - 1 + col;
+          const int hl = (lane & 1) ^ ((col >> 3) & 1);
+          if (gr >= 0 && gr < H && gc >= 0 && gc < W)
+            src = gy + (((int64_t)n * H + gr) * W + gc) * CI + kc * 16 + 8 * hl;
+        }
+        dst = buf + kc * XPP + j * 1024;
+      } else {
+        const int j = q - NCK * XBLK, p = 16 * j + (lane >> 2);
+        const int gr = r0 + (p >> 5), gc = c0 + (p & 31);
+        if (gr < H && gc < W) src = yg + (((int64_t)n * H + gr) * W + gc) * COP + 8 * (lane & 3);
+        dst = ybuf + j * 1024;
       }
       __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(
-                                           buf + kc * XPP + j * 1024),
-                                       16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
     }
   };
+  // fused BatchNorm-backward reduce (stats != nullptr): lane li of half lh
+  // ends up holding channel row li >> 1's sums (x6p's butterfly)
+  double bs = 0.0, bq = 0.0;
   int64_t t = blockIdx.x;
-  if (t < ntiles) issue(t, sxa);
+  if (t < ntiles) issue(t, sxa, sya);
   bool cur_a = true;
   for (; t < ntiles; t += gridDim.x) {
     unsigned char* sx = cur_a ? sxa : sxb;
+    const unsigned char* sy = cur_a ? sya : syb;
     // this tile's halo landed (every wave's DMA), the weights are staged
     __builtin_amdgcn_s_waitcnt(0x0F70);      // vmcnt(0)
     __syncthreads();
     const int64_t tn = t + gridDim.x;
-    if (tn < ntiles) issue(tn, cur_a ? sxb : sxa);   // lands during this tile
+    if (tn < ntiles) issue(tn, cur_a ? sxb : sxa, cur_a ? syb : sya);   // lands during this tile
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
@@ -274,8 +323,10 @@ __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
     // r0 + wave; channel-last, 4 consecutive channels per 16-byte store
     const int tc = (int)(t % ntc), tr = (int)((t / ntc) % ntr), n = (int)(t / ((int64_t)ntc * ntr));
     const int row = tr * TR + wave, col = tc * TC + li;
-    if (row < H && col < W) {
-      float* d = dx + (((int64_t)n * H + row) * W + col) * COP;
+    const bool pok = row < H && col < W;
+    const int64_t e0 = (((int64_t)n * H + row) * W + col) * COP;
+    if (pok) {
+      float* d = dx + e0;
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         const int co0 = 8 * rb + 4 * lh;
@@ -283,8 +334,39 @@ __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
             make_float4(acc[4 * rb], acc[4 * rb + 1], acc[4 * rb + 2], acc[4 * rb + 3]);
       }
     }
+    if (fz) {
+      float s1[16], s2[16];
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int co0 = 8 * rb + 4 * lh;
+        const uint2 u = *reinterpret_cast<const uint2*>(sy + (wave * 32 + li) * 64 + co0 * 2);
+        float yv[4];
+        bnr_dec4(1, make_uint4(u.x, u.y, 0u, 0u), yv);
+        const float v4[4] = {acc[4 * rb], acc[4 * rb + 1], acc[4 * rb + 2], acc[4 * rb + 3]};
+        bnr_terms4<COP>(sbn, co0, yv, v4, pok, s1 + 4 * rb, s2 + 4 * rb);
+      }
+      bs += (double)x6_reduce16(s1, li);
+      bq += (double)x6_reduce16(s2, li);
+    }
     __syncthreads();   // every wave is done with sx before it is re-filled
     cur_a = !cur_a;
+  }
+  if (!fz) return;
+  // [wave][sum, sum of products][32] in the (now free) halo buffer, then the
+  // 8 waves in fixed order
+  double* red = reinterpret_cast<double*>(sxa);
+  if ((li & 1) == 0) {
+    const int r = li >> 1;
+    const int co = (r & 3) + 8 * (r >> 2) + 4 * lh;
+    red[(wave * 2 + 0) * COP + co] = bs;
+    red[(wave * 2 + 1) * COP + co] = bq;
+  }
+  __syncthreads();
+  if (tid < 2 * COP) {
+    const int k = tid / COP, co = tid % COP;
+    double a = 0.0;
+    for (int wv = 0; wv < NT / 64; ++wv) a += red[(wv * 2 + k) * COP + co];
+    stats[(int64_t)blockIdx.x * 2 * COP + tid] = a;
   }
 }
 
@@ -304,7 +386,7 @@ template <int CI, int COP, bool DGRAD, int RPW, int NP, bool G16 = false, bool X
 __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
-    float* __restrict__ y, double* __restrict__ stats, int Cout, int H, int W) {
+    float* __restrict__ y, double* __restrict__ stats, int Cout, int H, int W, Bnr bnr) {
   using cx6::HC;
   using cx6::TC;
   using cx6::CK;
@@ -321,12 +403,34 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char sx[NP * XPLANE];
   __shared__ __attribute__((aligned(16))) unsigned char sw[NP * WPLANE];
   __shared__ double red[8 * 2 * COP];          // BatchNorm partials per wave
+  // fused BatchNorm-backward reduce (Bnr, the 8-row channel-last data
+  // gradient): the layer's constants in LDS, this lane's y loaded up front
+  constexpr bool FZ = DGRAD && YL && RPW == 1 && COP == 32;
+  __shared__ float sbn[FZ ? 4 * COP : 1];
 
   const int n = blockIdx.z, r0 = blockIdx.y * TR, c0 = blockIdx.x * TC;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int64_t HW = (int64_t)H * W;
   constexpr int ES = act_es<G16>();
+  const bool fused = FZ && bnr.y != nullptr;
+  uint4 yr[FZ ? NI : 1][4];
+  if constexpr (FZ) {
+    if (fused) {
+      bnr_stage(bnr, sbn, Cout, COP, tid, NT);
+      const int row = r0 + wave, col = c0 + li;
+      const bool pok = row < H && col < W;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const int co0 = 32 * i + 8 * rb + 4 * lh;
+          yr[i][rb] = bnr_ld4(bnr, (pok && co0 < Cout)
+                                       ? ((int64_t)n * HW + (int64_t)row * W + col) * Cout + co0
+                                       : 0);
+        }
+    }
+  }
 
   float px[XI][8];
   // staging unit -> (halo column, halo row, channel half); channel-last (XL):
@@ -482,8 +586,35 @@ __global__ __launch_bounds__(cx6::NT, RPW == 1 ? 4 : 2) void conv3x3_x6_kernel(
         }
       }
   }
+  if constexpr (FZ) {
+    // fused BatchNorm-backward reduce (Bnr): (gz, gz * xhat) per channel,
+    // summed over the wave's 32 pixels by a float butterfly
+    if (fused) {
+      const int row = r0 + wave;
+      const bool pok = row < H && col < W;
 #pragma unroll
-  for (int i = 0; i < NI; ++i)
+      for (int i = 0; i < NI; ++i) {
+        float s1[16], s2[16];
+#pragma unroll
+        for (int rb = 0; rb < 4; ++rb) {
+          const int co0 = 32 * i + 8 * rb + 4 * lh;
+          const float v4[4] = {acc[i][0][4 * rb], acc[i][0][4 * rb + 1], acc[i][0][4 * rb + 2],
+                               acc[i][0][4 * rb + 3]};
+          float yv[4];
+          bnr_dec4(bnr.y16, yr[FZ ? i : 0][rb], yv);
+          bnr_terms4<COP>(sbn, co0, yv, v4, pok && co0 < Cout, s1 + 4 * rb, s2 + 4 * rb);
+        }
+        const float t1 = x6_reduce16(s1, li), t2 = x6_reduce16(s2, li);
+        const int r = li >> 1, co = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if ((li & 1) == 0 && co < Cout) {
+          red[(wave * 2 + 0) * COP + co] = t1;
+          red[(wave * 2 + 1) * COP + co] = t2;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NI && !fused; ++i)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int co = 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
@@ -538,7 +669,7 @@ int64_t conv_x6_stat_parts(int64_t N, int64_t H, int64_t W) {
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                    bool x16, bool y16, int lay);
+                    bool x16, bool y16, int lay, const Bnr& bnr);
 
 // Persistent-grid multiplier of the bf16 (NP = 1) kernels: their LDS (21-50
 // KB) and VGPR (48-80) footprints let 2-4x the fp32 kernels' workgroups stay
@@ -615,53 +746,61 @@ static void cl_dispatch(int lay, F&& f) {
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                   bool x16, bool y16, int lay) {
+                   bool x16, bool y16, int lay, const Bnr* bnrp) {
+  const Bnr bnr = bnrp ? *bnrp : Bnr{};
+  // fused BatchNorm-backward reduce: a data gradient writing channel-last dx,
+  // whose partials are the (sum gz, sum gz * xhat) rows
+  const bool fused = bnr.y != nullptr;
+  // (dx of at most 32 channels: the fused instances)
+  if (fused && !(dgrad && stats && (lay & CL_Y) && !bias && Cout <= 32)) return 2;
   if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W, b16) == 0) return 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                   parts, b16, x16, y16, lay);
+                                   parts, b16, x16, y16, lay, bnr);
     if (rc != 1) return rc;
   }
   if ((int64_t)Cin * H * W * 4 >= ((int64_t)1 << 31)) return 1;   // 32-bit buffer offsets
-  if (y16 || (x16 && !(dgrad && !stats && b16))) return 2;   // bf16 storage: no such kernel
-  // channel-last: only the stat-free data gradient (8-row tiles) has it
-  if (lay && !(dgrad && !stats)) return 2;
-  if (dgrad && !stats && b16 && x16 && lay == (CL_X | CL_Y) && Cin == cdd::CI &&
-      Cout == cdd::COP && !bias && !sc && dgrad16_dma()) {
+  // the data gradient without forward statistics: 8-row tiles (channel-last,
+  // bf16 dy, the fused reduce)
+  const bool dg8 = dgrad && (!stats || fused);
+  if (y16 || (x16 && !(dg8 && b16))) return 2;   // bf16 storage: no such kernel
+  if (lay && !dg8) return 2;
+  if (dg8 && b16 && x16 && lay == (CL_X | CL_Y) && Cin == cdd::CI && Cout == cdd::COP && !bias &&
+      !sc && (!fused || bnr.y16) && dgrad16_dma()) {
     const int ntr = (int)cdiv(H, cdd::TR), ntc = (int)cdiv(W, cdd::TC);
     const int64_t nt = N * (int64_t)ntr * ntc;
-    *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
     const int grid = (int)(nt < 256 ? nt : 256);   // one persistent workgroup per CU
+    *parts = grid;
     hipLaunchKernelGGL(conv3x3_dgrad_b16dma_kernel, dim3(grid), dim3(cdd::NT), 0, s,
-                       reinterpret_cast<const uint16_t*>(x), w, y, (int)N, (int)H, (int)W, ntr,
-                       ntc, nt);
+                       reinterpret_cast<const uint16_t*>(x), w, y, stats, bnr, (int)N, (int)H,
+                       (int)W, ntr, ntc, nt);
     return check_launch("conv3x3_dgrad_b16dma");
   }
-  *parts = N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
+  *parts = dg8 ? N * cdiv(H, 8) * cdiv(W, cx6::TC) : N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
   const dim3 grid((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, cx6::TR), (unsigned)N);
   const int cop = Cout <= 32 ? 32 : 64;
 #define AINP_X6N(CIV, COV, NPV)                                                                \
   if (Cin == CIV && cop == COV) {                                                               \
-    if (dgrad && !stats) {   /* 8-row tiles, two workgroups per CU (no BN partials) */           \
+    if (dg8) {   /* 8-row tiles, two workgroups per CU */                                       \
       const dim3 g8((unsigned)cdiv(W, cx6::TC), (unsigned)cdiv(H, 8), (unsigned)N);             \
       cl_dispatch(lay, [&](auto xl, auto yl) {                                                  \
         constexpr bool XL = decltype(xl)::value, YL = decltype(yl)::value;                      \
         if (NPV == 1 && x16)                                                                    \
           hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV, true, XL, YL>), g8,     \
                              dim3(cx6::NT), 0, s, x, w, bias, sc, sh, y, stats, Cout, (int)H,   \
-                             (int)W);                                                           \
+                             (int)W, bnr);                                                      \
         else                                                                                    \
           hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 1, NPV, false, XL, YL>), g8,    \
                              dim3(cx6::NT), 0, s, x, w, bias, sc, sh, y, stats, Cout, (int)H,   \
-                             (int)W);                                                           \
+                             (int)W, bnr);                                                      \
       });                                                                                       \
     } else if (dgrad)                                                                           \
       hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, true, 2, NPV>), grid, dim3(cx6::NT), 0, s, \
-                         x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                   \
+                         x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W, bnr);              \
     else                                                                                        \
       hipLaunchKernelGGL((conv3x3_x6_kernel<CIV, COV, false, 2, NPV>), grid, dim3(cx6::NT), 0,  \
-                         s, x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W);                \
+                         s, x, w, bias, sc, sh, y, stats, Cout, (int)H, (int)W, bnr);           \
     return check_launch("conv3x3_x6");                                                          \
   }
 #define AINP_X6(CIV, COV)                                                                     \
@@ -1229,7 +1368,7 @@ template <int CI, int COP, bool DGRAD, int NT, int TR, int NP, bool G16 = false,
 __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
-    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W) {
+    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W, Bnr bnr) {
   using namespace cxp;
   static_assert(CI % CK == 0 && (COP == 32 || COP == 64), "shape");
   constexpr int NI = COP / 32, NCH = CI / CK;
@@ -1247,11 +1386,18 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char sx[NP * XPLANE];
   __shared__ float s_ss[2 * CI];
   static_assert(NP * XPLANE >= TR * 2 * COP * 8, "BatchNorm row sums reuse the halo image");
+  // fused BatchNorm-backward reduce (Bnr): constants in LDS; the tile's y
+  // is loaded in one batch at the top of the epilogue (holding it across the
+  // MFMA loop would cost this kernel its second workgroup per CU)
+  constexpr bool FZ = DGRAD && YL;
+  __shared__ float sbn[FZ ? 4 * COP : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int li = lane & 31, lh = lane >> 5;
   const int wrow = wave % TR, wco = (wave / TR) * NIW;  // output row, first 32-channel tile
   const int64_t HW = (int64_t)H * W;
+  const bool fused = FZ && bnr.y != nullptr;
+  if (fused) bnr_stage(bnr, sbn, Cout, COP, tid, NT);
 
   for (int u = tid; u < WU; u += NT) {
     const int half = u & 1, tap = (u >> 1) % 9, co = (u / 18) % COP, ch = u / (18 * COP);
@@ -1267,6 +1413,10 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
   }
   if (tid < 2 * CI)
     s_ss[tid] = in_scale ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
+  // bias from LDS: a global load in the epilogue would make it wait for the
+  // next tile's halo prefetch (vmcnt is in order)
+  __shared__ float s_b[COP];
+  if (tid < COP) s_b[tid] = (bias && tid < Cout) ? bias[tid] : 0.f;
 
   const int tiles_c = (W + TC - 1) / TC, tiles_r = (H + TR - 1) / TR;
   const int64_t ntiles = (int64_t)N * tiles_r * tiles_c;
@@ -1379,6 +1529,18 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
     const bool pok = row < H && col < W;
     const int64_t yo = (int64_t)n * Cout * HW + (int64_t)row * W + col;
     const int64_t ycl = ((int64_t)n * HW + (int64_t)row * W + col) * Cout;
+    uint4 yr[FZ ? NIW : 1][4];
+    if constexpr (FZ) {
+      if (fused) {
+#pragma unroll
+        for (int i = 0; i < NIW; ++i)
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            const int co0 = 32 * (wco + i) + 8 * rb + 4 * lh;
+            yr[i][rb] = bnr_ld4(bnr, (pok && co0 < Cout) ? ycl + co0 : 0);
+          }
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NIW; ++i) {
       float s[16], q[16], vv[16];
@@ -1386,7 +1548,7 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
       for (int r = 0; r < 16; ++r) {
         const int co = 32 * (wco + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
         const bool ok = pok && co < Cout;
-        float v = acc[i][r] + ((bias && co < Cout) ? bias[co] : 0.f);
+        float v = acc[i][r] + s_b[co];
         if constexpr (Y16) v = y16_round(v);
         if constexpr (!YL) {
           if constexpr (Y16) {
@@ -1398,6 +1560,18 @@ __global__ __launch_bounds__(NT, NT / 256) void conv3x3_x6p_kernel(
         vv[r] = v;
         s[r] = ok ? v : 0.f;
         q[r] = s[r] * s[r];
+      }
+      if constexpr (FZ) {   // fused BatchNorm-backward reduce (Bnr)
+        if (fused) {
+#pragma unroll
+          for (int rb = 0; rb < 4; ++rb) {
+            const int co0 = 32 * (wco + i) + 8 * rb + 4 * lh;
+            const float v4[4] = {vv[4 * rb], vv[4 * rb + 1], vv[4 * rb + 2], vv[4 * rb + 3]};
+            float yv[4];
+            bnr_dec4(bnr.y16, yr[FZ ? i : 0][rb], yv);
+            bnr_terms4<COP>(sbn, co0, yv, v4, pok && co0 < Cout, s + 4 * rb, q + 4 * rb);
+          }
+        }
       }
       if constexpr (YL) {   // 4 consecutive channels per store (Cout % 4 == 0)
 #pragma unroll
@@ -1507,7 +1681,7 @@ template <int CI, bool DGRAD, int NP, bool G16 = false, bool Y16 = false, bool X
 __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
-    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W) {
+    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W, Bnr bnr) {
   using cxp::CK;
   using cxp::HC;
   using cxp::TC;
@@ -1521,10 +1695,16 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
   __shared__ __attribute__((aligned(16))) unsigned char sx[NP * XPLANE];
   __shared__ float s_ss[2 * CI];
   static_assert(NP * XPLANE >= TR * 2 * CO * 8, "BatchNorm row sums reuse the halo image");
+  // fused BatchNorm-backward reduce (Bnr): as in conv3x3_x6p_kernel
+  constexpr bool FZ = DGRAD && YL;
+  __shared__ float sbn[FZ ? 4 * CO : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int l16 = lane & 15, g = lane >> 4;
   const int64_t HW = (int64_t)H * W;
+  const bool fused = FZ && bnr.y != nullptr;
+  if (fused) bnr_stage(bnr, sbn, Cout, CO, tid, NT);
+  uint4 yr[2];
 
   for (int u = tid; u < WU; u += NT) {
     const int half = u & 1, tap = (u >> 1) % 10, co = (u / 20) % CO, ch = u / (20 * CO);
@@ -1540,6 +1720,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
   }
   if (tid < 2 * CI)
     s_ss[tid] = in_scale ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
+  // bias from LDS (see conv3x3_x6p_kernel)
+  __shared__ float s_b[CO];
+  if (tid < CO) s_b[tid] = (bias && tid < Cout) ? bias[tid] : 0.f;
 
   const int tiles_c = (W + TC - 1) / TC, tiles_r = (H + TR - 1) / TR;
   const int64_t ntiles = (int64_t)N * tiles_r * tiles_c;
@@ -1647,12 +1830,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     for (int j = 0; j < 2; ++j) {
       const int col = c0 + 16 * j + l16;
       const bool pok = row < H && col < W;
-      float vv[4];
+      float vv[4], ts[4], tq[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int co = 4 * g + r;
         const bool ok = pok && co < Cout;
-        float v = acc[j][r] + ((bias && co < Cout) ? bias[co] : 0.f);
+        float v = acc[j][r] + s_b[co];
         if constexpr (Y16) v = y16_round(v);
         if constexpr (!YL) {
           if constexpr (Y16) {
@@ -1663,8 +1846,20 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
         }
         vv[r] = v;
         const float sv = ok ? v : 0.f;
-        s[r] += sv;
-        q[r] += sv * sv;
+        ts[r] = sv;
+        tq[r] = sv * sv;
+      }
+      if constexpr (FZ) {   // fused BatchNorm-backward reduce (Bnr)
+        if (fused) {
+          float yv[4];
+          bnr_dec4(bnr.y16, yr[j], yv);
+          bnr_terms4<CO>(sbn, 4 * g, yv, vv, pok && 4 * g < Cout, ts, tq);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        s[r] += ts[r];
+        q[r] += tq[r];
       }
       if constexpr (YL) {   // channels 4g .. 4g+3 of pixel (row, col)
         if (pok && 4 * g < Cout)
@@ -1691,7 +1886,23 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
       nch = 0;
       ntile += gridDim.x;
     }
-    if (ntile < ntiles) fetch(ntile, nch);
+    if constexpr (FZ) {
+      if (fused && nch == 0) {   // this tile's y (its last chunk)
+        int n, r0, c0;
+        tile_coords(tile, n, r0, c0);
+        const int row = r0 + wave;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int col = c0 + 16 * j + l16;
+          const bool ok = row < H && col < W && 4 * g < Cout;
+          yr[j] = bnr_ld4(bnr, ok ? ((int64_t)n * HW + (int64_t)row * W + col) * Cout + 4 * g : 0);
+        }
+      }
+      // unconditional (see conv3x3_x6p_kernel)
+      fetch(ntile < ntiles ? ntile : tile, nch);
+    } else {
+      if (ntile < ntiles) fetch(ntile, nch);
+    }
     const unsigned char* wb0 = sw + ch * WCH + l16 * WROW + 16 * (g & 1);
 #pragma unroll
     for (int ks = 0; ks < 5; ++ks) {
@@ -1754,12 +1965,12 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
 template <int CIV, int COV, bool DG, int NTV, int TRV>
 static void x6p_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, int lay, const float* x,
                    const float* w, const float* bias, const float* sc, const float* sh, float* y,
-                   double* stats, int N, int Cout, int H, int W) {
+                   double* stats, int N, int Cout, int H, int W, const Bnr& bnr) {
   cl_dispatch(lay, [&](auto xl, auto yl) {
     constexpr bool XL = decltype(xl)::value, YL = decltype(yl)::value;
 #define AINP_X6PK(NPV, GV, YV)                                                                   \
   hipLaunchKernelGGL((conv3x3_x6p_kernel<CIV, COV, DG, NTV, TRV, NPV, GV, YV, XL, YL>), g,       \
-                     dim3(NTV), 0, s, x, w, bias, sc, sh, y, stats, N, Cout, H, W)
+                     dim3(NTV), 0, s, x, w, bias, sc, sh, y, stats, N, Cout, H, W, bnr)
     if (!b16) {
       AINP_X6PK(3, false, false);
     } else if constexpr (DG) {
@@ -1778,12 +1989,12 @@ static void x6p_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, int lay,
 template <bool DG>
 static void x6q_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, int lay, const float* x,
                    const float* w, const float* bias, const float* sc, const float* sh, float* y,
-                   double* stats, int N, int Cout, int H, int W) {
+                   double* stats, int N, int Cout, int H, int W, const Bnr& bnr) {
   cl_dispatch(lay, [&](auto xl, auto yl) {
     constexpr bool XL = decltype(xl)::value, YL = decltype(yl)::value;
 #define AINP_X6QK(NPV, GV, YV)                                                                \
   hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV, GV, YV, XL, YL>), g, dim3(512), 0, s, x, \
-                     w, bias, sc, sh, y, stats, N, Cout, H, W)
+                     w, bias, sc, sh, y, stats, N, Cout, H, W, bnr)
     if (!b16) {
       AINP_X6QK(3, false, false);
     } else if constexpr (DG) {
@@ -1802,14 +2013,14 @@ static void x6q_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, int lay,
 int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bias,
                     const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
-                    bool x16, bool y16, int lay) {
+                    bool x16, bool y16, int lay, const Bnr& bnr) {
   const int cop = Cout <= 32 ? 32 : 64;
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
 #define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                      \
   if (dgrad == DG && Cin == CIV && cop == COV) {                                                 \
     const int g2 = b16 ? (G) * conv_x6_occ16() : (G);                                            \
     x6p_go<CIV, COV, DG, NTV, TRV>(dim3(g2), s, b16, x16, y16, lay, x, w, bias, sc, sh, y,      \
-                                   stats, (int)N, Cout, (int)H, (int)W);                         \
+                                   stats, (int)N, Cout, (int)H, (int)W, bnr);                    \
     *parts = g2;                                                                                 \
     return check_launch("conv3x3_x6p");                                                          \
   }
@@ -1819,10 +2030,10 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
     const int gq = b16 ? 512 * conv_x6_occ16() : 512;
     if (dgrad)
       x6q_go<true>(dim3(gq), s, b16, x16, y16, lay, x, w, bias, sc, sh, y, stats, (int)N, Cout,
-                   (int)H, (int)W);
+                   (int)H, (int)W, bnr);
     else
       x6q_go<false>(dim3(gq), s, b16, x16, y16, lay, x, w, bias, sc, sh, y, stats, (int)N, Cout,
-                    (int)H, (int)W);
+                    (int)H, (int)W, bnr);
     *parts = gq;
     return check_launch("conv3x3_x6q");
   }

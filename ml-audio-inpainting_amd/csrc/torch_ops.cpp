@@ -256,6 +256,33 @@ void conv3x3_dgrad(const Tensor& dy, const Tensor& w, const Tensor& dx, int64_t 
       "conv3x3_dgrad_ex");
 }
 
+// dx channel-last [N,H,W,Cin] (AINP_CONV_YCL) + the BatchNorm-backward sums
+// of the layer it feeds (y [N,H,W,Cin], AINP_BN_Y16: bf16 storage)
+void conv3x3_dgrad_bnr(const Tensor& dy, const Tensor& w, const Tensor& dx, int64_t flags,
+                       const Tensor& y, const Tensor& scale, const Tensor& shift,
+                       const Tensor& save, const Tensor& workspace, const Tensor& sums,
+                       int64_t bn_flags) {
+  GUARD(dy);
+  const bool gcl = flags & AINP_CONV_XCL;   // dy [N,H,W,Cout]
+  TORCH_CHECK(dy.dim() == 4 && w.dim() == 4 && w.size(0) == dy.size(gcl ? 3 : 1),
+              "conv3x3_dgrad_bnr: dy [N,Cout,H,W] (channel-last: [N,H,W,Cout]), w [Cout,Cin,3,3]");
+  const int64_t N = dy.size(0), Cout = w.size(0), H = dy.size(gcl ? 1 : 2),
+                W = dy.size(gcl ? 2 : 3), Cin = w.size(1);
+  numel_is(dx, N * Cin * H * W, "dx");
+  numel_is(y, N * Cin * H * W, "y");
+  TORCH_CHECK(sums.numel() >= 2 * Cin, "sums needs 2C entries");
+  TORCH_CHECK((int64_t)workspace.nbytes() >=
+                  ainp_conv3x3_dgrad_bnr_workspace(N, (int)Cin, (int)Cout, H, W),
+              "conv3x3_dgrad_bnr workspace too small");
+  chk(ainp_conv3x3_dgrad_bnr(f32_or_16(dy, "dy", flags & AINP_CONV_DY16), dev(w, "w"),
+                             dev(dx, "dx"), N, (int)Cin, (int)Cout, H, W, (int)flags,
+                             f32_or_16(y, "y", bn_flags & AINP_BN_Y16), dev(scale, "scale"),
+                             dev(shift, "shift"), dev(save, "save"), workspace.data_ptr(),
+                             dev<double>(sums, "sums", at::kDouble), (int)bn_flags,
+                             stream_of(dy)),
+      "conv3x3_dgrad_bnr");
+}
+
 void conv3x3_wgrad(const Tensor& x, const OptT& in_scale, const OptT& in_shift, const Tensor& dy,
                    const Tensor& dw, const OptT& dbias, const Tensor& workspace, int64_t flags) {
   GUARD(x);
@@ -1559,6 +1586,8 @@ TORCH_LIBRARY(ainp, m) {
   m.def("conv3x3_fwd(Tensor x, Tensor w, Tensor? bias, Tensor? in_scale, Tensor? in_shift, "
         "Tensor(a!) y, Tensor(b!)? stats, int flags) -> ()");
   m.def("conv3x3_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int flags) -> ()");
+  m.def("conv3x3_dgrad_bnr(Tensor dy, Tensor w, Tensor(a!) dx, int flags, Tensor y, Tensor scale, "
+        "Tensor shift, Tensor save, Tensor(b!) workspace, Tensor(c!) sums, int bn_flags) -> ()");
   m.def("conv3x3_wgrad(Tensor x, Tensor? in_scale, Tensor? in_shift, Tensor dy, Tensor(a!) dw, "
         "Tensor(b!)? dbias, Tensor(c!) workspace, int flags) -> ()");
   m.def("bn_stats_reduce(Tensor stats, Tensor(a!) sums, int C) -> ()");
@@ -1687,6 +1716,7 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("gemm", &gemm);
   m.impl("conv3x3_fwd", &conv3x3_fwd);
   m.impl("conv3x3_dgrad", &conv3x3_dgrad);
+  m.impl("conv3x3_dgrad_bnr", &conv3x3_dgrad_bnr);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad);
   m.impl("bn_stats_reduce", &bn_stats_reduce);
   m.impl("bn_finalize", &bn_finalize);
@@ -1771,6 +1801,7 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("gemm", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_fwd", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_dgrad", torch::CppFunction::makeFallthrough());
+  m.impl("conv3x3_dgrad_bnr", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_wgrad", torch::CppFunction::makeFallthrough());
   m.impl("bn_stats_reduce", torch::CppFunction::makeFallthrough());
   m.impl("bn_finalize", torch::CppFunction::makeFallthrough());

@@ -263,3 +263,82 @@ def test_cnnblstm_bf16_step_kmajor_weight_gradient_bit_identical(monkeypatch):
     assert res[0][0] == res[1][0]
     for n, g1 in res[1][1].items():
         assert torch.equal(res[0][1][n], g1), n
+
+
+# (conv Cin, Cout) whose data gradient feeds a BatchNorm+ReLU in the model:
+# encoder 32 -> 64 (64 -> 32 dgrad, 8-row tiles / the bf16 LDS-DMA kernel),
+# encoder 16 -> 32 and decoder 32 -> 16 (persistent x6q / x6p), decoder
+# 16 -> 1 (small conv: the unfused two-pass path)
+BNR_PAIRS = [(32, 64), (16, 32), (32, 16), (16, 1)]
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("N,H,W", SHAPES)
+@pytest.mark.parametrize("cin,cout", BNR_PAIRS)
+def test_dgrad_bnr_fused_reduce(cin, cout, N, H, W, bf16):
+    """ops.conv3x3_dgrad_bnr (round 5): dx bit-identical to the channel-last
+    data gradient, and the fused BatchNorm-backward sums within 1e-6 of the
+    separate channel-last reduce over that dx (the same fp32 terms
+    gz = dx * [y*scale+shift > 0], gz * (y - mean) * rstd, summed in another
+    fixed order); y in fp32 and in bf16 storage; run-to-run identical."""
+    from ainp import ops
+    x, dy, w, b, sc, sh = _data(N, cin, cout, H, W, cin * 11 + cout)
+    g = torch.Generator(device=DEV).manual_seed(cin + cout + H)
+    y = torch.randn(N, H, W, cin, device=DEV, generator=g)
+    bsc = torch.rand(cin, device=DEV, generator=g) + 0.5
+    bsh = torch.randn(cin, device=DEV, generator=g) * 0.3
+    save = torch.stack([torch.randn(cin, device=DEV, generator=g) * 0.1,
+                        torch.rand(cin, device=DEV, generator=g) + 0.5])
+    small = cout == 1
+    dys = [_cl(dy)] + ([_cl(dy).to(torch.bfloat16)] if bf16 and not small else [])
+    for d in dys:
+        dx0 = ops.conv3x3_dgrad(d, w, bf16=bf16, xcl=True, ycl=True)
+        for yy in (y, y.to(torch.bfloat16)):
+            dx, s = ops.conv3x3_dgrad_bnr(d, w, yy, bsc, bsh, save, bf16=bf16, xcl=True)
+            assert torch.equal(dx, dx0), (d.dtype, yy.dtype)
+            s0 = ops.bn_relu_bwd_reduce(dx0, yy, bsc, bsh, save, cl=True)
+            assert rel(s, s0) < 1e-6, (d.dtype, yy.dtype, rel(s, s0))
+            dx2, s2 = ops.conv3x3_dgrad_bnr(d, w, yy, bsc, bsh, save, bf16=bf16, xcl=True)
+            assert torch.equal(dx2, dx) and torch.equal(s2, s)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cnnblstm_step_dgrad_bnr_matches_two_pass(monkeypatch, dtype):
+    """A CNNBLSTM step with the fused data-gradient + BatchNorm reduce
+    (cnnblstm.DGRAD_BNR, default) against the two-pass backward: the same
+    loss, every gradient within 2e-4 (fp32) / 2e-3 (bf16) -- only the
+    summation order of the BatchNorm-backward sums differs."""
+    from ainp import cnnblstm
+    cfg = {"data": {"sample_rate": 16000, "spectrogram": {"n_fft": 512, "hop_length": 192,
+                                                          "win_length": 384}},
+           "model": {"in_channels": 1, "num_lstm_layers": 2, "lstm_hidden_dim": 128,
+                     "enc_filters": [16, 32], "dec_filters": [16, 32]},
+           "accel": {"dtype": dtype}}
+    g = torch.Generator().manual_seed(7)
+    N, F, T = 4, 257, 334
+    x = (torch.randn(N, 1, F, T, generator=g) - 2.0).to(DEV)
+    mask = torch.zeros(N, F, T)
+    for i in range(N):
+        mask[i, :, 40 + 30 * i:57 + 30 * i] = 1.0
+    mask = mask.to(DEV)
+    tgt = torch.complex(torch.rand(N, F, T, generator=g), torch.rand(N, F, T, generator=g)).to(DEV)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(cnnblstm, "DGRAD_BNR", fused)
+        torch.manual_seed(0)
+        m = cnnblstm.StackedBLSTMCNN(config=cfg).to(DEV).train()
+        loss = cnnblstm.l1_pow10_loss(m(x), mask, tgt)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((float(loss.detach()),
+                    {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    tol = 2e-4 if dtype == "fp32" else 2e-3
+    assert res[0][0] == res[1][0]
+    errs = {}
+    for n, g1 in res[1][1].items():
+        if n in ("encoder.0.bias", "encoder.3.bias", "encoder.6.bias", "decoder.0.bias",
+                 "decoder.3.bias"):
+            continue   # BatchNorm-fed conv biases: exact gradient 0 (SURVEY Q10)
+        errs[n] = rel(res[0][1][n], g1)
+    bad = {n: e for n, e in errs.items() if e >= tol}
+    assert not bad, (bad, max(errs.values()))
