@@ -469,32 +469,39 @@ int bn_cl_sum_partials(const double* partial, int nblk, int C2, double* sums, hi
   return check_launch("bn_cl_partials_sum");
 }
 
+constexpr int BNA_UNR = 2;   // pixels per thread per pass of bn_relu_bwd_apply_cl
+
 template <int C, bool GB16, bool YB16, bool OB16>
-__global__ __launch_bounds__(256) void bn_relu_bwd_apply_cl(
+__global__ __launch_bounds__(256, 4) void bn_relu_bwd_apply_cl(
     const void* __restrict__ g, const void* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
     const float* __restrict__ save, const double* __restrict__ sums, void* __restrict__ gy,
     float* __restrict__ dgamma, float* __restrict__ dbeta, int64_t P, double inv_count) {
-  constexpr int G = C / 8, PPI = 256 / G, UNR = 4;
+  constexpr int G = C / 8, PPI = 256 / G, UNR = BNA_UNR;
   const int tid = threadIdx.x, grp = tid % G;
   if (blockIdx.x == 0 && tid < C) {
     if (dbeta) dbeta[tid] = (float)sums[tid];
     if (dgamma) dgamma[tid] = (float)sums[C + tid];
   }
-  const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C];   // see bn_finalize
-  float sc[8], sh[8], mu[8], rs[8], kk[8], m1[8], m2[8];
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    const int ch = 8 * grp + c;
-    sc[c] = scale[ch];
-    sh[c] = shift[ch];
-    mu[c] = save[ch];
-    rs[c] = save[C + ch];
-    kk[c] = (gamma ? gamma[ch] : 1.f) * rs[c];
-    m1[c] = (float)(sums[ch] * ic);
-    m2[c] = (float)(sums[C + ch] * ic);
+  // per-channel constants in LDS (7 x 8 registers per thread would cost the
+  // pass its occupancy): scale, shift, mean, rstd, k = gamma * rstd, m1, m2
+  __shared__ float cst[7][C];
+  if (tid < C) {
+    const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * C];   // see bn_finalize
+    cst[0][tid] = scale[tid];
+    cst[1][tid] = shift[tid];
+    cst[2][tid] = save[tid];
+    cst[3][tid] = save[C + tid];
+    cst[4][tid] = (gamma ? gamma[tid] : 1.f) * save[C + tid];
+    cst[5][tid] = (float)(sums[tid] * ic);
+    cst[6][tid] = (float)(sums[C + tid] * ic);
   }
+  __syncthreads();
   for (int64_t pb = (int64_t)blockIdx.x * PPI * UNR; pb < P; pb += (int64_t)gridDim.x * PPI * UNR) {
+    // re-read the constants per iteration (an opaque base keeps the compiler
+    // from hoisting 56 of them into registers for the whole loop)
+    int cb = 8 * grp;
+    asm volatile("" : "+v"(cb));
     float gv[UNR][8], yv[UNR][8];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
@@ -511,21 +518,15 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_apply_cl(
       float o[8];
 #pragma unroll
       for (int c = 0; c < 8; ++c) {
-        const float gz = fmaf(yv[u][c], sc[c], sh[c]) > 0.f ? gv[u][c] : 0.f;
-        o[c] = kk[c] * (gz - m1[c] - ((yv[u][c] - mu[c]) * rs[c]) * m2[c]);
+        const int ch = cb + c;
+        const float gz = fmaf(yv[u][c], cst[0][ch], cst[1][ch]) > 0.f ? gv[u][c] : 0.f;
+        o[c] = cst[4][ch] * (gz - cst[5][ch] - ((yv[u][c] - cst[2][ch]) * cst[3][ch]) * cst[6][ch]);
       }
       const int64_t e = p * C + 8 * grp;
       if constexpr (OB16) {
-        uint4 q;
-        q.x = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[0]) |
-              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[1]) << 16);
-        q.y = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[2]) |
-              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[3]) << 16);
-        q.z = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[4]) |
-              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[5]) << 16);
-        q.w = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[6]) |
-              ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[7]) << 16);
-        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(gy) + e) = q;
+        *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(gy) + e) =
+            make_uint4(cvt_pk_bf16(o[0], o[1]), cvt_pk_bf16(o[2], o[3]), cvt_pk_bf16(o[4], o[5]),
+                       cvt_pk_bf16(o[6], o[7]));
       } else {
         float* d = reinterpret_cast<float*>(gy) + e;
         *reinterpret_cast<float4*>(d) = make_float4(o[0], o[1], o[2], o[3]);
@@ -636,7 +637,7 @@ __global__ __launch_bounds__(256) void bn_relu_apply_ntcf_cl(
 }
 
 template <bool APPLY, bool YB16, bool GY16>
-__global__ __launch_bounds__(256) void bn_relu_bwd_ntcf_cl(
+__global__ __launch_bounds__(256, 4) void bn_relu_bwd_ntcf_cl(
     const float* __restrict__ g, const void* __restrict__ y, const float* __restrict__ scale,
     const float* __restrict__ shift, const float* __restrict__ gamma,
     const float* __restrict__ save, const double* __restrict__ sums, double* __restrict__ partial,
@@ -644,109 +645,131 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf_cl(
     int ntf, int64_t ntiles, double inv_count) {
   __shared__ float tile[CLN_C][65];
   __shared__ double red[4][2 * CLN_C];
+  // per-channel constants in LDS (registers would hold 6 x 16 of them per
+  // thread and cap the pass at two workgroups per CU): scale, shift, mean,
+  // rstd and, for the apply, k = gamma * rstd, m1, m2
+  __shared__ float cst[7][CLN_C];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, pr = tid >> 2, q = tid & 3;
   if (APPLY && blockIdx.x == 0 && tid < CLN_C) {
     if (dbeta) dbeta[tid] = (float)sums[tid];
     if (dgamma) dgamma[tid] = (float)sums[CLN_C + tid];
   }
-  float sc[16], sh[16], mu[16], rs[16], a1[16], a2[16];
-  double ic = 0.0;
-  if (APPLY) ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * CLN_C];   // see bn_finalize
-#pragma unroll
-  for (int j = 0; j < 16; ++j) {
-    const int c = 16 * q + j;
-    sc[j] = scale[c];
-    sh[j] = shift[c];
-    mu[j] = save[c];
-    rs[j] = save[CLN_C + c];
+  if (tid < CLN_C) {
+    const int c = tid;
+    cst[0][c] = scale[c];
+    cst[1][c] = shift[c];
+    cst[2][c] = save[c];
+    cst[3][c] = save[CLN_C + c];
     if (APPLY) {
-      a1[j] = (float)(sums[c] * ic);                              // m1
-      a2[j] = (float)(sums[CLN_C + c] * ic);                      // m2
-    } else {
-      a1[j] = a2[j] = 0.f;                                        // s1, s2
+      const double ic = inv_count > 0.0 ? inv_count : 1.0 / sums[2 * CLN_C];   // see bn_finalize
+      cst[4][c] = (gamma ? gamma[c] : 1.f) * save[CLN_C + c];
+      cst[5][c] = (float)(sums[c] * ic);                          // m1
+      cst[6][c] = (float)(sums[CLN_C + c] * ic);                  // m2
     }
   }
-  auto coords = [&](int64_t b, int& n, int& h0, int& t) {
-    t = (int)(b % W);
-    h0 = (int)((b / W) % ntf) * 64;
-    n = (int)(b / ((int64_t)W * ntf));
+  float a1[APPLY ? 1 : 16], a2[APPLY ? 1 : 16];                   // s1, s2
+#pragma unroll
+  for (int j = 0; j < (APPLY ? 1 : 16); ++j) a1[j] = a2[j] = 0.f;
+  // 32-bit tile coordinates (the launcher checks ntiles < 2^31); clamped,
+  // branch-free loads selected to zero past H.  g through a buffer resource
+  // per tile (one VGPR offset, the channel rows as scalar offsets); y kept as
+  // raw words until used -- the pass is held to 128 VGPRs (4 workgroups / CU)
+  constexpr int YW = YB16 ? 2 : 4;               // 16-byte words of y per thread
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  auto coords = [&](int b, int& n, int& h0, int& t) {
+    const int bw = b / W;
+    t = b - bw * W;
+    n = bw / ntf;
+    h0 = (bw - n * ntf) * 64;
   };
-  float gr[16], yr[16];
-  auto load = [&](int64_t b) {
+  float gr[16];
+  uint4 yr[YW];
+  auto load = [&](int b) {
     int n, h0, t;
     coords(b, n, h0, t);
     const int hh = h0 + lane;
-    const float* gp = g + ((int64_t)n * W + t) * CLN_C * H + hh;
+    const bool hok = hh < H;
+    const __amdgpu_buffer_rsrc_t rg = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(g + ((int64_t)n * W + t) * CLN_C * H + (int64_t)16 * wv * H), (short)0,
+        0x7fffffff, 0x00020000);
+    const int vo = (hok ? hh : H - 1) * 4;
 #pragma unroll
-    for (int it = 0; it < 16; ++it) gr[it] = hh < H ? gp[(int64_t)(16 * wave + it) * H] : 0.f;
-    const int h = h0 + pr;
-    if (h < H) {
-      cln_ld16<YB16>(y, (((int64_t)n * H + h) * W + t) * CLN_C + 16 * q, yr);
-    } else {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) yr[j] = 0.f;
+    for (int it = 0; it < 16; ++it) {
+      const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rg, vo, it * H * 4, 0));
+      gr[it] = hok ? v : 0.f;
     }
+    const int h = h0 + pr;
+    const int64_t e = (((int64_t)n * H + (h < H ? h : H - 1)) * W + t) * CLN_C + 16 * q;
+    const uint4* yp = YB16 ? reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(y) + e)
+                           : reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(y) + e);
+#pragma unroll
+    for (int k = 0; k < YW; ++k) yr[k] = yp[k];
   };
-  int64_t b = blockIdx.x;
-  if (b < ntiles) load(b);
-  for (; b < ntiles; b += gridDim.x) {
+  auto ydec = [&](const uint4 (&w)[YW], int j) -> float {   // channel 16 q + j
+    const uint4 u = w[YB16 ? j / 8 : j / 4];
+    const int k = YB16 ? (j % 8) / 2 : j % 4;
+    const uint32_t x = k == 0 ? u.x : k == 1 ? u.y : k == 2 ? u.z : u.w;
+    if constexpr (YB16) return __uint_as_float((j & 1) ? (x & 0xffff0000u) : (x << 16));
+    return __uint_as_float(x);
+  };
+  const int nt32 = (int)ntiles;
+  int b = blockIdx.x;
+  if (b < nt32) load(b);
+  for (; b < nt32; b += gridDim.x) {
 #pragma unroll
     for (int it = 0; it < 16; ++it) tile[16 * wave + it][lane] = gr[it];
-    float yc[16];
+    uint4 yc[YW];
 #pragma unroll
-    for (int j = 0; j < 16; ++j) yc[j] = yr[j];
+    for (int k = 0; k < YW; ++k) yc[k] = yr[k];
     int n, h0, t;
     coords(b, n, h0, t);
     __syncthreads();
-    if (b + gridDim.x < ntiles) load(b + gridDim.x);   // in flight during this tile
+    if (b + (int)gridDim.x < nt32) load(b + gridDim.x);   // in flight during this tile
     const int h = h0 + pr;
-    float o[16];
+    const int64_t e = (((int64_t)n * H + h) * W + t) * CLN_C + 16 * q;
+    // two halves of 8 channels: computed, then stored
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const float gz = fmaf(yc[j], sc[j], sh[j]) > 0.f ? tile[16 * q + j][pr] : 0.f;
-      const float xh = (yc[j] - mu[j]) * rs[j];
-      if (APPLY) {
-        const float k = (gamma ? gamma[16 * q + j] : 1.f) * rs[j];
-        o[j] = k * (gz - a1[j] - xh * a2[j]);
-      } else if (h < H) {
-        a1[j] += gz;
-        a2[j] += gz * xh;
-      }
-    }
-    if (APPLY && h < H) {
-      const int64_t e = (((int64_t)n * H + h) * W + t) * CLN_C + 16 * q;
-      if constexpr (GY16) {
-        uint4* d = reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(gy) + e);
+    for (int hf = 0; hf < 2; ++hf) {
+      float o[8];
 #pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          uint32_t w[4];
-#pragma unroll
-          for (int jj = 0; jj < 4; ++jj)
-            w[jj] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[8 * hh + 2 * jj]) |
-                    ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)o[8 * hh + 2 * jj + 1]) << 16);
-          d[hh] = make_uint4(w[0], w[1], w[2], w[3]);
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = 8 * hf + jj, c = 16 * q + j;
+        const float yv = ydec(yc, j);
+        const float gz = fmaf(yv, cst[0][c], cst[1][c]) > 0.f ? tile[c][pr] : 0.f;
+        const float xh = (yv - cst[2][c]) * cst[3][c];
+        if constexpr (APPLY) {
+          o[jj] = cst[4][c] * (gz - cst[5][c] - xh * cst[6][c]);
+        } else if (h < H) {
+          a1[j] += gz;
+          a2[j] += gz * xh;
         }
-      } else {
-        float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(gy) + e);
-#pragma unroll
-        for (int hh = 0; hh < 4; ++hh)
-          d[hh] = make_float4(o[4 * hh], o[4 * hh + 1], o[4 * hh + 2], o[4 * hh + 3]);
+      }
+      if (APPLY && h < H) {
+        if constexpr (GY16) {
+          reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(gy) + e)[hf] =
+              make_uint4(cvt_pk_bf16(o[0], o[1]), cvt_pk_bf16(o[2], o[3]),
+                         cvt_pk_bf16(o[4], o[5]), cvt_pk_bf16(o[6], o[7]));
+        } else {
+          float4* d = reinterpret_cast<float4*>(reinterpret_cast<float*>(gy) + e) + 2 * hf;
+          d[0] = make_float4(o[0], o[1], o[2], o[3]);
+          d[1] = make_float4(o[4], o[5], o[6], o[7]);
+        }
       }
     }
     __syncthreads();   // the tile is re-written next iteration
   }
-  if (APPLY) return;
+  if constexpr (APPLY) return;
   // lanes of one channel quarter (== q mod 4): xor 4 .. 32, fixed order
 #pragma unroll
   for (int o = 4; o < 64; o <<= 1)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < (APPLY ? 1 : 16); ++j) {
       a1[j] += __shfl_xor(a1[j], o, 64);
       a2[j] += __shfl_xor(a2[j], o, 64);
     }
   if (lane < 4) {
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
+    for (int j = 0; j < (APPLY ? 1 : 16); ++j) {
       red[wave][16 * lane + j] = a1[j];
       red[wave][CLN_C + 16 * lane + j] = a2[j];
     }
@@ -756,7 +779,17 @@ __global__ __launch_bounds__(256) void bn_relu_bwd_ntcf_cl(
     partial[(int64_t)blockIdx.x * 2 * CLN_C + tid] =
         red[0][tid] + red[1][tid] + red[2][tid] + red[3][tid];
 }
-constexpr int CLN_BLOCKS = 1024;   // persistent blocks of the backward passes
+// persistent blocks of the NTCF backward passes (AINP_CLN_BLOCKS, <= the
+// CLN_BLOCKS_MAX partial rows the workspace holds)
+constexpr int CLN_BLOCKS_MAX = 2048;
+static int cln_blocks() {
+  static const int v = [] {
+    const char* e = getenv("AINP_CLN_BLOCKS");
+    const int b = e ? atoi(e) : 1024;
+    return b < 256 ? 256 : (b > CLN_BLOCKS_MAX ? CLN_BLOCKS_MAX : b);
+  }();
+  return v;
+}
 
 // ----------------------------------------------------------- NTCF path
 // The encoder's last BatchNorm+ReLU reads / writes the LSTM layout
@@ -1196,7 +1229,7 @@ extern "C" size_t ainp_bn_relu_bwd_workspace(int64_t N, int C, int64_t H,
                                              int64_t W) {
   const int64_t tiled = N * C * tiles_per_plane(H, W) * 2;
   int64_t cl = cdiv(N * H * W, BNC_PIX) * 2 * C;   // channel-last partials
-  if (cl < (int64_t)CLN_BLOCKS * 2 * C) cl = (int64_t)CLN_BLOCKS * 2 * C;
+  if (cl < (int64_t)CLN_BLOCKS_MAX * 2 * C) cl = (int64_t)CLN_BLOCKS_MAX * 2 * C;
   return (size_t)(tiled > cl ? tiled : cl) * sizeof(double);
 }
 
@@ -1248,20 +1281,21 @@ static int bn_cl_reduce(const float* g, const float* y, const float* scale, cons
   double* partial = reinterpret_cast<double*>(workspace);
   const bool g16 = flags & AINP_BN_G16, y16 = flags & AINP_BN_Y16;
   if ((flags & AINP_BN_CL) && g_ntcf) {   // g NTCF fp32, y channel-last (64 channels)
-    if (C != CLN_C || g16 || !bn_cl_ok(C, {y}) || H * W * C >= ((int64_t)1 << 31))
+    if (C != CLN_C || g16 || !bn_cl_ok(C, {y}) || H * W * C >= ((int64_t)1 << 31) ||
+        N * W * cdiv(H, 64) >= ((int64_t)1 << 31))
       return record_msg("ainp_bn_relu_bwd_reduce: NTCF g with channel-last y needs C = 64, "
                         "fp32 g, 16-byte aligned y");
     const int ntf = (int)cdiv(H, 64);
     const int64_t ntiles = N * W * ntf;
 #define AINP_BNN(YV)                                                                             \
-    hipLaunchKernelGGL((bn_relu_bwd_ntcf_cl<false, YV, false>), dim3(CLN_BLOCKS), dim3(256), 0, s, \
+    hipLaunchKernelGGL((bn_relu_bwd_ntcf_cl<false, YV, false>), dim3(cln_blocks()), dim3(256), 0, s, \
                        g, y, scale, shift, nullptr, save, nullptr, partial, nullptr, nullptr,     \
                        nullptr, (int)H, (int)W, ntf, ntiles, 0.0)
     if (y16) AINP_BNN(true); else AINP_BNN(false);
 #undef AINP_BNN
     int rc = check_launch("bn_relu_bwd_ntcf_cl");
     if (rc) return rc;
-    hipLaunchKernelGGL(bn_cl_partials_sum, dim3(2 * C), dim3(256), 0, s, partial, CLN_BLOCKS,
+    hipLaunchKernelGGL(bn_cl_partials_sum, dim3(2 * C), dim3(256), 0, s, partial, cln_blocks(),
                        2 * C, sums);
     return check_launch("bn_cl_partials_sum");
   }
@@ -1295,14 +1329,14 @@ static int bn_cl_apply(const float* g, const float* y, const float* scale, const
   const double inv_count = count > 0 ? 1.0 / (double)count : 0.0;   // 0: sums[2C]
   if ((flags & AINP_BN_CL) && g_ntcf) {   // g NTCF fp32, y / gy channel-last (64 channels)
     if (C != CLN_C || (flags & AINP_BN_G16) || !bn_cl_ok(C, {y, gy}) ||
-        H * W * C >= ((int64_t)1 << 31))
+        H * W * C >= ((int64_t)1 << 31) || N * W * cdiv(H, 64) >= ((int64_t)1 << 31))
       return record_msg("ainp_bn_relu_bwd_apply: NTCF g with channel-last y needs C = 64, "
                         "fp32 g, 16-byte aligned y / gy");
     const int ntf = (int)cdiv(H, 64);
     const int64_t ntiles = N * W * ntf;
     const bool y16 = flags & AINP_BN_Y16, o16 = flags & AINP_BN_GY16;
 #define AINP_BNN(YV, OV)                                                                         \
-    hipLaunchKernelGGL((bn_relu_bwd_ntcf_cl<true, YV, OV>), dim3(CLN_BLOCKS), dim3(256), 0, s, g, \
+    hipLaunchKernelGGL((bn_relu_bwd_ntcf_cl<true, YV, OV>), dim3(cln_blocks()), dim3(256), 0, s, g, \
                        y, scale, shift, gamma, save, sums, nullptr, gy, dgamma, dbeta, (int)H,    \
                        (int)W, ntf, ntiles, inv_count)
     if (y16 && o16) AINP_BNN(true, true);
@@ -1315,7 +1349,7 @@ static int bn_cl_apply(const float* g, const float* y, const float* scale, const
   if (!(flags & AINP_BN_CL) || g_ntcf || !bn_cl_ok(C, {g, y, gy}))
     return record_msg("ainp_bn_relu_bwd_apply: AINP_BN_CL needs C % 8 == 0 (<= 64), 16-byte "
                       "aligned g / y / gy and no NTCF layout (AINP_BN_G16 needs AINP_BN_CL)");
-  const int ppb = 256 / (C / 8) * 4;                                 // pixels per block pass
+  const int ppb = 256 / (C / 8) * BNA_UNR;                           // pixels per block pass
   int64_t nb = cdiv(P, ppb);
   if (nb > 2048) nb = 2048;
   const bool g16 = flags & AINP_BN_G16, y16 = flags & AINP_BN_Y16, o16 = flags & AINP_BN_GY16;

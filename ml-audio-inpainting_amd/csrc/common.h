@@ -87,6 +87,14 @@ __device__ __forceinline__ void bnr_terms4(const float* sbn, int c0, const float
 // sums[o] = fixed-order sum of partial[0 .. nblk)[o], o < C2 (bn.hip)
 int bn_cl_sum_partials(const double* partial, int nblk, int C2, double* sums, hipStream_t s);
 
+// Two fp32 -> packed bf16 (round-to-nearest-even, lo in the low half): the
+// gfx950 conversion instruction (a software rounding sequence otherwise)
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float lo, float hi) {
+  uint32_t r;
+  asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
+
 // Wave-level (64-lane) reductions.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
