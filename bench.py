@@ -457,6 +457,7 @@ def _cnn_step_work(B=32, F=257, T=334, H=128, bf16=False):
         ("gemm_bf16nt_256_kernel", "mfma", l0),           # bf16 projection
         ("conv3x3_x6p_kernel<32, 64", "mfma", conv(32, 64)),
         ("conv3x3_x6_kernel<64, 32", "mfma", conv(64, 32)),
+        ("conv3x3_dgrad_b16dma_kernel", "mfma", conv(64, 32)),   # bf16 64 -> 32 dgrad
         ("conv3x3_wgrad_x6<64", "mfma", conv(32, 64)),
         ("conv3x3_x6p_kernel<16, 32, false", "mfma", 2 * conv(16, 32)),
         ("conv3x3_x6q_kernel<32, true", "mfma", 2 * conv(16, 32)),
