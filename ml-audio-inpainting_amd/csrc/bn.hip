@@ -785,7 +785,7 @@ constexpr int CLN_BLOCKS_MAX = 2048;
 static int cln_blocks() {
   static const int v = [] {
     const char* e = getenv("AINP_CLN_BLOCKS");
-    const int b = e ? atoi(e) : 1024;
+    const int b = e ? atoi(e) : 768;
     return b < 256 ? 256 : (b > CLN_BLOCKS_MAX ? CLN_BLOCKS_MAX : b);
   }();
   return v;
