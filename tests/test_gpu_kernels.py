@@ -238,18 +238,29 @@ def test_gap_frames_known_answers(ops, golden_dir):
 @pytest.mark.parametrize("M,N,K", [(333, 130, 77), (256, 512, 1024), (1, 5, 3), (129, 4112, 256)])
 @pytest.mark.parametrize("ta,tb", [(False, True), (False, False), (True, False), (True, True)])
 @pytest.mark.parametrize("exact", [False, True])
-def test_gemm_layouts(ops, M, N, K, ta, tb, exact):
+@pytest.mark.parametrize("ccol", [False, True])
+def test_gemm_layouts(ops, M, N, K, ta, tb, exact, ccol):
+    """Every operand layout; ccol: C column-major (computed as C^T = B^T A^T
+    since round 5, the bias moving to the rows), with a bias and beta."""
     g = torch.Generator().manual_seed(M * 7 + N)
     A = torch.randn(M, K, generator=g, dtype=torch.float64)
     B = torch.randn(K, N, generator=g, dtype=torch.float64)
+    bias = torch.randn(N, generator=g, dtype=torch.float64)
+    C0 = torch.randn(M, N, generator=g, dtype=torch.float64)
     ref = A @ B
     Ad = (A.t().contiguous() if ta else A).float().to(DEV)
     Bd = (B.t().contiguous() if tb else B).float().to(DEV)
-    C = torch.empty(M, N, device=DEV)
     sam, sak = (1, M) if ta else (K, 1)
     sbk, sbn = (1, K) if tb else (N, 1)
-    ops.gemm(M, N, K, [Ad], sam, sak, [Bd], sbk, sbn, [C], N, 1, exact=exact)
-    assert rel(C.cpu(), ref) < 1e-5
+    if not ccol:
+        C = torch.empty(M, N, device=DEV)
+        ops.gemm(M, N, K, [Ad], sam, sak, [Bd], sbk, sbn, [C], N, 1, exact=exact)
+        assert rel(C.cpu(), ref) < 1e-5
+        return
+    Ct = C0.t().contiguous().float().to(DEV)       # [N, M]: C[m][n] at n*M + m
+    ops.gemm(M, N, K, [Ad], sam, sak, [Bd], sbk, sbn, [Ct], 1, M, exact=exact, beta=0.5,
+             bias1=[bias.float().to(DEV)])
+    assert rel(Ct.cpu().t(), ref + bias + 0.5 * C0) < 1e-5
 
 
 def test_gemm_x6_is_fp32_accurate(ops):
