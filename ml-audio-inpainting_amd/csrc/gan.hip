@@ -679,6 +679,142 @@ __global__ __launch_bounds__(256) void conv_gen_splitk_epilogue(ConvGenParams p,
   }
 }
 
+// Split-K epilogue over 64-pixel x 64-channel tiles (the default; the
+// per-channel kernel above under AINP_SPLITK_TILE=0): 16 lanes per channel
+// row each own four consecutive pixels, so the nsplit partial rows arrive as
+// 16-byte loads issued together (the per-pixel kernel's serial loads were
+// latency bound), and the same per-pixel sums in the same z order -- y is
+// bit-identical.  The BatchNorm partials are per (64-pixel block, channel);
+// Y16: the bf16 channel-last copy of act(y) from an LDS transpose of the tile,
+// replacing the nchw_to_nhwc16 pass after the split layers.
+constexpr int SKT_P = 64, SKT_C = 64;
+template <bool Y16>
+__global__ __launch_bounds__(256) void conv_gen_splitk_tile_epilogue(ConvGenParams p, int nsplit,
+                                                                     int act) {
+  __shared__ uint16_t tile[Y16 ? SKT_P : 1][SKT_C + 2];
+  const int HWo = p.Ho * p.Wo;
+  const int64_t NP = (int64_t)p.N * HWo;
+  const int64_t px0 = (int64_t)blockIdx.x * SKT_P;
+  const int co0 = blockIdx.y * SKT_C;
+  const int pl = threadIdx.x & 15, rr = threadIdx.x >> 4;
+  const int64_t px = px0 + 4 * pl;
+  const bool vec = (NP & 3) == 0 && px + 3 < NP;
+  const float sc = p.scale ? *p.scale : 1.f;
+  float rat[4] = {1.f, 1.f, 1.f, 1.f};
+  if (p.ratio)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) rat[e] = px + e < NP ? p.ratio[px + e] : 1.f;
+  int nn[4], rq[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    nn[e] = (int)((px + e) / HWo);
+    rq[e] = (int)(px + e - (int64_t)nn[e] * HWo);
+  }
+#pragma unroll 1
+  for (int j = 0; j < SKT_C / 16; ++j) {
+    const int cl = rr + 16 * j, co = co0 + cl;
+    double a = 0.0, b = 0.0;
+    if (co < p.Cout && px < NP) {
+      float v[4] = {0.f, 0.f, 0.f, 0.f};
+      const float* src = p.partial + (int64_t)co * NP + px;
+      const int64_t zs = (int64_t)p.Cout * NP;
+      if (vec) {
+        int z = 0;
+        for (; z + 4 <= nsplit; z += 4) {
+          float4 q[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) q[u] = *reinterpret_cast<const float4*>(src + (z + u) * zs);
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            v[0] += q[u].x;
+            v[1] += q[u].y;
+            v[2] += q[u].z;
+            v[3] += q[u].w;
+          }
+        }
+        for (; z < nsplit; ++z) {
+          const float4 q = *reinterpret_cast<const float4*>(src + z * zs);
+          v[0] += q.x;
+          v[1] += q.y;
+          v[2] += q.z;
+          v[3] += q.w;
+        }
+      } else {
+        for (int z = 0; z < nsplit; ++z)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (px + e < NP) v[e] += src[z * zs + e];
+      }
+      const float bias = p.bias ? p.bias[co] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (px + e >= NP) continue;
+        float t = v[e] * sc;
+        if (p.ratio) t *= rat[e];
+        if (p.bias) t += bias;
+        a += t;
+        b += (double)t * (double)t;
+        const float o = apply_act(t, act, p.slope);
+        p.y[((int64_t)nn[e] * p.Cout + co) * HWo + rq[e]] = o;
+        if (Y16) tile[4 * pl + e][cl] = __builtin_bit_cast(uint16_t, (__bf16)o);
+      }
+    }
+    if (p.stats) {
+#pragma unroll
+      for (int m = 1; m < 16; m <<= 1) {
+        a += __shfl_xor(a, m, 16);
+        b += __shfl_xor(b, m, 16);
+      }
+      if (pl == 0 && co < p.Cout) {
+        p.stats[((int64_t)blockIdx.x * 2 + 0) * p.Cout + co] = a;
+        p.stats[((int64_t)blockIdx.x * 2 + 1) * p.Cout + co] = b;
+      }
+    }
+  }
+  if (!Y16) return;
+  __syncthreads();
+  // rows = pixels, lanes along the channels (bf16 pairs): 32 lanes per pixel
+  const int l = threadIdx.x & 31, r = threadIdx.x >> 5;
+  const int c = co0 + 2 * l;
+#pragma unroll
+  for (int i = r; i < SKT_P; i += 8) {
+    const int64_t q = px0 + i;
+    if (q >= NP || c >= p.Cout) continue;
+    uint16_t* d = p.y16 + q * p.Cout + c;
+    if (c + 1 < p.Cout && (p.Cout & 1) == 0)
+      *reinterpret_cast<uint32_t*>(d) = (uint32_t)tile[i][2 * l] | ((uint32_t)tile[i][2 * l + 1] << 16);
+    else {
+      d[0] = tile[i][2 * l];
+      if (c + 1 < p.Cout) d[1] = tile[i][2 * l + 1];
+    }
+  }
+}
+
+static bool splitk_tile() {
+  static const bool on = [] {
+    const char* e = getenv("AINP_SPLITK_TILE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+static int splitk_epilogue_launch(const ConvGenParams& p, int64_t NP, int nsplit, int act,
+                                  hipStream_t s) {
+  if (!splitk_tile()) {
+    hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), p.Cout), dim3(256),
+                       0, s, p, nsplit, act);
+  } else if (p.y16) {
+    hipLaunchKernelGGL(conv_gen_splitk_tile_epilogue<true>,
+                       dim3((unsigned)cdiv(NP, SKT_P), (unsigned)cdiv(p.Cout, SKT_C)), dim3(256), 0,
+                       s, p, nsplit, act);
+  } else {
+    hipLaunchKernelGGL(conv_gen_splitk_tile_epilogue<false>,
+                       dim3((unsigned)cdiv(NP, SKT_P), (unsigned)cdiv(p.Cout, SKT_C)), dim3(256), 0,
+                       s, p, nsplit, act);
+  }
+  return check_launch("conv_gen_splitk_epilogue");
+}
+
 // Direct convolution for Cout == 1 (the generator's last PartialConv2d and
 // the discriminator's logit conv).  Stage 1: grid (pixel blocks, channel
 // chunks of C1_CC) -- each thread sums its pixel over one chunk of the
@@ -2310,7 +2446,8 @@ static int conv_gen_nsplit(int64_t NP, int Cout, int K) {
 extern "C" int ainp_conv_gen_stat_parts(int64_t N, int Cin, int KH, int KW, int Cout, int64_t Ho,
                                         int64_t Wo) {
   const int64_t NP = N * Ho * Wo;
-  if (conv_gen_nsplit(NP, Cout, Cin * KH * KW) > 1) return (int)cdiv(NP, 256);
+  if (conv_gen_nsplit(NP, Cout, Cin * KH * KW) > 1)
+    return (int)cdiv(NP, splitk_tile() ? SKT_P : 256);
   return (int)cdiv(NP, 16384 / conv_gen_bm(Cout));
 }
 
@@ -2487,9 +2624,7 @@ extern "C" int ainp_conv_gen_fwd_out16(const float* x0, const float* m0, int C0,
     hipLaunchKernelGGL(conv_gen_fwd_kernel<64>, grid, dim3(256), 0, s, p, wt, act);
   int rc = check_launch("conv_gen_fwd");
   if (rc || nsplit == 1) return rc;
-  hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), Cout), dim3(256), 0,
-                     s, p, nsplit, act);
-  return check_launch("conv_gen_splitk_epilogue");
+  return splitk_epilogue_launch(p, NP, nsplit, act, s);
 }
 
 extern "C" int ainp_nchw_to_nhwc16(const float* x, const float* m, int64_t N, int C, int H, int W,
@@ -2693,10 +2828,8 @@ extern "C" int ainp_conv_gen_fwd_nhwc16_ex(const uint16_t* x0, int C0, int H0, i
     hipLaunchKernelGGL((conv_gen_nhwc16_kernel<64, false>), grid, dim3(256), 0, s, p, a, b, wt16, act);
   int rc = check_launch("conv_gen_nhwc16");
   if (rc || nsplit == 1) return rc;
-  hipLaunchKernelGGL(conv_gen_splitk_epilogue, dim3((unsigned)cdiv(NP, 256), Cout), dim3(256), 0,
-                     s, p, nsplit, act);
-  rc = check_launch("conv_gen_splitk_epilogue");
-  if (rc || !y16) return rc;
+  rc = splitk_epilogue_launch(p, NP, nsplit, act, s);
+  if (rc || !y16 || splitk_tile()) return rc;
   // split-K layers are small: their bf16 copy by the coalesced transpose kernel
   // (the per-channel epilogue blocks would store it 2 bytes at a time)
   return ainp_nchw_to_nhwc16(y, nullptr, N, Cout, Ho, Wo, y16, stream);

@@ -43,6 +43,7 @@ CONV_CASES = [
     (2, 64, 0, 12, 14, False, 32, 3, 1, 1, False, True, False, False, 1),     # VGG-like
     (2, 512, 512, 6, 10, True, 512, 3, 1, 1, True, False, True, False, 0),    # U-Net bottleneck: split-K
     (3, 256, 0, 7, 9, False, 64, 3, 2, 1, True, True, True, False, 2),        # BM=64, split-K
+    (1, 512, 0, 5, 7, False, 200, 3, 1, 1, True, True, True, True, 2),        # split-K, odd NP, Cout%64
 ]
 
 
@@ -234,6 +235,8 @@ def test_conv_gen_nhwc16_variants_bit_identical(case, monkeypatch):
     (1, 512, 6, 10, 512, 3, 1, 1, 1),                 # split-K epilogue kernel
     (2, 64, 30, 22, 128, 3, 1, 1, 2),                 # wide tile, 128 channels
     (1, 96, 17, 23, 200, 3, 1, 1, 1),                 # ragged last channel tile
+    (1, 512, 5, 7, 200, 3, 1, 1, 2),                  # split-K, odd pixel count, Cout % 64
+    (3, 256, 7, 9, 96, 3, 1, 1, 0),                   # split-K, Cout % 64, three images
 ])
 def test_conv_gen_epilogue_nhwc16_copy(case):
     """out16: the conv epilogue's bf16 channel-last copy of y equals
