@@ -1013,3 +1013,17 @@ def test_unet_bf16_forward_without_fp32_writeback_is_bit_identical(monkeypatch):
         small0_y = net(x, m).clone()
     assert torch.equal(small0, small0_y)
     assert (small0 - outs[0]).abs().max().item() < 1e-1
+
+
+@pytest.mark.parametrize("n,off", [(1, 0), (1003, 0), (4096 * 37 + 3, 0), (524288 * 9, 0), (70001, 1)])
+def test_absdiff_mean_matches_fp64(n, off):
+    """ainp_absdiff_mean (the perceptual / style L1 terms): mean |a - b| in
+    double against numpy's, over vector-loaded, ragged-tail and unaligned
+    (off = 1 float: the scalar loop) operands."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(n)
+    a = torch.randn(n + off, generator=g)
+    b = torch.randn(n + off, generator=g)
+    out = ops.absdiff_mean(a.cuda()[off:], b.cuda()[off:])
+    ref = np.abs(a[off:].numpy() - b[off:].numpy()).astype(np.float64).mean()
+    assert abs(out.item() - ref) <= 1e-12 * max(1.0, abs(ref))
