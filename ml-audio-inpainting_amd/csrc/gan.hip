@@ -894,9 +894,16 @@ __global__ void conv_cout1_finish_kernel(ConvGenParams p, int act, int Hc, int W
 // Partial-conv mask update (networks.py:83-104): count = sum over the window
 // of the channel-repeated masks = C0 * win(m0) + C1 * win(m1) (exact integers
 // in fp32), ratio = (Cin*k*k) / (count + 1e-8), new mask = clamp(count, 0, 1).
-__global__ void pconv_mask_kernel(ConvSrcDev s0, ConvSrcDev s1, int N, int Hin, int Win,
-                                  int KH, int KW, int stride, int pad, int Ho, int Wo,
-                                  float winsize, float* ratio, float* newmask) {
+// KT > 0: a KT x KT window, unrolled, with every tap's load issued
+// unconditionally from a clamped in-image position (zero weight outside), so a
+// thread's window loads are in flight together (the runtime-bounds loop waited
+// out one load latency per tap: 30-34 us for the generator's two largest).
+template <int KT>
+__global__ __launch_bounds__(256) void pconv_mask_kernel(ConvSrcDev s0, ConvSrcDev s1, int N,
+                                                         int Hin, int Win, int KH, int KW,
+                                                         int stride, int pad, int Ho, int Wo,
+                                                         float winsize, float* ratio,
+                                                         float* newmask) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t np = (int64_t)N * Ho * Wo;
   if (t >= np) return;
@@ -904,19 +911,43 @@ __global__ void pconv_mask_kernel(ConvSrcDev s0, ConvSrcDev s1, int N, int Hin, 
   const int r = (int)(t - (int64_t)n * Ho * Wo);
   const int oy = r / Wo, ox = r - oy * Wo;
   int c0 = 0, c1 = 0;
-  for (int ky = 0; ky < KH; ++ky) {
-    const int iy = oy * stride - pad + ky;
-    if (iy < 0 || iy >= Hin) continue;
-    for (int kx = 0; kx < KW; ++kx) {
-      const int ix = ox * stride - pad + kx;
-      if (ix < 0 || ix >= Win) continue;
-      if (s0.C) {
-        const int sy = src_coord(iy, s0.Hs, Hin, s0.up), sx = src_coord(ix, s0.Ws, Win, s0.up);
-        c0 += (int)s0.m[((int64_t)n * s0.Hs + sy) * s0.Ws + sx];
+  if (KT > 0) {
+    const float* m0 = s0.m + (int64_t)n * s0.Hs * s0.Ws;
+    const float* m1 = s1.C ? s1.m + (int64_t)n * s1.Hs * s1.Ws : m0;
+#pragma unroll
+    for (int ky = 0; ky < KT; ++ky) {
+      const int iy = oy * stride - pad + ky;
+      const bool oky = iy >= 0 && iy < Hin;
+      const int cy = min(max(iy, 0), Hin - 1);
+      const int sy0 = src_coord(cy, s0.Hs, Hin, s0.up), sy1 = src_coord(cy, s1.Hs, Hin, s1.up);
+#pragma unroll
+      for (int kx = 0; kx < KT; ++kx) {
+        const int ix = ox * stride - pad + kx;
+        const bool ok = oky && ix >= 0 && ix < Win;
+        const int cx = min(max(ix, 0), Win - 1);
+        const float v0 = m0[sy0 * s0.Ws + src_coord(cx, s0.Ws, Win, s0.up)];
+        c0 += ok ? (int)v0 : 0;
+        if (s1.C) {
+          const float v1 = m1[sy1 * s1.Ws + src_coord(cx, s1.Ws, Win, s1.up)];
+          c1 += ok ? (int)v1 : 0;
+        }
       }
-      if (s1.C) {
-        const int sy = src_coord(iy, s1.Hs, Hin, s1.up), sx = src_coord(ix, s1.Ws, Win, s1.up);
-        c1 += (int)s1.m[((int64_t)n * s1.Hs + sy) * s1.Ws + sx];
+    }
+  } else {
+    for (int ky = 0; ky < KH; ++ky) {
+      const int iy = oy * stride - pad + ky;
+      if (iy < 0 || iy >= Hin) continue;
+      for (int kx = 0; kx < KW; ++kx) {
+        const int ix = ox * stride - pad + kx;
+        if (ix < 0 || ix >= Win) continue;
+        if (s0.C) {
+          const int sy = src_coord(iy, s0.Hs, Hin, s0.up), sx = src_coord(ix, s0.Ws, Win, s0.up);
+          c0 += (int)s0.m[((int64_t)n * s0.Hs + sy) * s0.Ws + sx];
+        }
+        if (s1.C) {
+          const int sy = src_coord(iy, s1.Hs, Hin, s1.up), sx = src_coord(ix, s1.Ws, Win, s1.up);
+          c1 += (int)s1.m[((int64_t)n * s1.Hs + sy) * s1.Ws + sx];
+        }
       }
     }
   }
@@ -2891,9 +2922,22 @@ extern "C" int ainp_pconv_mask(const float* m0, int C0, int H0, int W0, const fl
   ConvSrcDev s1 = make_src(nullptr, m1, C1, C1 ? H1 : Hin, C1 ? W1 : Win, Hin, Win);
   if (winsize <= 0.f) winsize = (float)((C0 + C1) * KH * KW);
   const int64_t np = N * (int64_t)Ho * Wo;
-  hipLaunchKernelGGL(pconv_mask_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0,
-                     as_stream(stream), s0, s1, (int)N, Hin, Win, KH, KW, stride, pad, Ho, Wo,
-                     winsize, ratio, newmask);
+  const dim3 grid((unsigned)cdiv(np, 256));
+  hipStream_t st = as_stream(stream);
+#define AINP_PCM(KT)                                                                          \
+  hipLaunchKernelGGL(pconv_mask_kernel<KT>, grid, dim3(256), 0, st, s0, s1, (int)N, Hin, Win, KH, \
+                     KW, stride, pad, Ho, Wo, winsize, ratio, newmask)
+  static const bool unroll = [] {   // AINP_PCONV_MASK_UNROLL=0: the loop kernel (A/B)
+    const char* e = getenv("AINP_PCONV_MASK_UNROLL");
+    return !(e && e[0] == '0');
+  }();
+  const int kt = unroll && KH == KW ? KH : 0;
+  if (kt == 3) AINP_PCM(3);
+  else if (kt == 4) AINP_PCM(4);
+  else if (kt == 5) AINP_PCM(5);
+  else if (kt == 7) AINP_PCM(7);
+  else AINP_PCM(0);
+#undef AINP_PCM
   return check_launch("pconv_mask");
 }
 

@@ -1027,3 +1027,37 @@ def test_absdiff_mean_matches_fp64(n, off):
     out = ops.absdiff_mean(a.cuda()[off:], b.cuda()[off:])
     ref = np.abs(a[off:].numpy() - b[off:].numpy()).astype(np.float64).mean()
     assert abs(out.item() - ref) <= 1e-12 * max(1.0, abs(ref))
+
+
+@pytest.mark.parametrize("k,st,pd,N,H0,W0,C0,H1,W1,C1,Hin,Win", [
+    (3, 1, 1, 2, 20, 33, 64, 40, 66, 1, 40, 66),     # final PartialConv: x2 source + input mask
+    (7, 2, 3, 2, 37, 70, 2, 0, 0, 0, 37, 70),        # the U-Net's first conv (7x7 / 2)
+    (5, 2, 2, 1, 19, 23, 64, 0, 0, 0, 19, 23),       # 5x5 / 2
+    (4, 2, 1, 3, 9, 14, 3, 18, 28, 5, 18, 28),       # 4x4, two sources, x2
+    (3, 1, 1, 1, 7, 10, 8, 0, 0, 0, 20, 30),         # general nearest resampling
+    (2, 1, 0, 1, 9, 11, 4, 9, 11, 2, 9, 11),         # window size without an unrolled kernel
+])
+def test_pconv_mask_matches_window_counts(k, st, pd, N, H0, W0, C0, H1, W1, C1, Hin, Win):
+    """ainp_pconv_mask (networks.py:83-104): count = C0 * win(m0) + C1 * win(m1)
+    of the nearest-resampled masks, ratio = (Cin k^2) / (count + 1e-8), new
+    mask = clamp(count, 0, 1) -- exact against an fp64 ones-kernel conv."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(k * 100 + Hin)
+    m0 = (torch.rand(N, H0, W0, generator=g) > 0.4).float()
+    m1 = (torch.rand(N, H1, W1, generator=g) > 0.4).float() if C1 else None
+
+    def up(m):
+        Hs, Ws = m.shape[-2:]
+        sy, sx = (torch.arange(Hin) * Hs) // Hin, (torch.arange(Win) * Ws) // Win
+        return m[:, sy][:, :, sx].double().unsqueeze(1)
+
+    ones = torch.ones(1, 1, k, k, dtype=torch.float64)
+    cnt = C0 * F.conv2d(up(m0), ones, stride=st, padding=pd)
+    if C1:
+        cnt = cnt + C1 * F.conv2d(up(m1), ones, stride=st, padding=pd)
+    cnt = cnt[:, 0].float()
+    ratio, newm = ops.pconv_mask((m0.cuda(), C0), (m1.cuda(), C1) if C1 else None, N, Hin, Win,
+                                 k, st, pd)
+    exp_ratio = float((C0 + C1) * k * k) / (cnt + 1e-8)
+    assert torch.equal(newm.cpu(), cnt.clamp(0, 1))
+    assert torch.allclose(ratio.cpu(), exp_ratio, rtol=1e-6, atol=0)
