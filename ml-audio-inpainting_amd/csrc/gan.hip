@@ -1571,7 +1571,7 @@ __global__ void channel_sum_kernel(const float* m, int64_t N, int C, int64_t HW,
 // the exact bf16 x bf16 product the MFMA would form (fp32 accumulation).
 constexpr int SC_K = 160, SC_CO = 64;   // 40 KB of weights in LDS
 
-template <bool B16>
+template <bool B16, bool L16>
 __global__ __launch_bounds__(256) void conv_gen_smallcin_kernel(ConvGenParams p, int act) {
   __shared__ __attribute__((aligned(16))) float sw[SC_K][SC_CO];   // [k][co]
   const int KK = p.KH * p.KW, K = KK * p.Cin, Cout = p.Cout;
@@ -1589,10 +1589,14 @@ __global__ __launch_bounds__(256) void conv_gen_smallcin_kernel(ConvGenParams p,
   __syncthreads();
   const int HWo = p.Ho * p.Wo;
   const int64_t NP = (int64_t)p.N * HWo;
-  const int64_t pix = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (pix >= NP) return;
-  const int n = (int)(pix / HWo);
-  const int r = (int)(pix - (int64_t)n * HWo);
+  const int64_t pix0 = (int64_t)blockIdx.x * 256;
+  const int64_t pix = pix0 + threadIdx.x;
+  // y16 (bf16) is written through LDS below, so every thread reaches its barriers
+  if (pix >= NP && !(p.y16 && L16)) return;
+  const bool valid = pix < NP;
+  const int64_t pixc = valid ? pix : NP - 1;
+  const int n = (int)(pixc / HWo);
+  const int r = (int)(pixc - (int64_t)n * HWo);
   const int oy = r / p.Wo, ox = r - oy * p.Wo;
   const int by = oy * p.stride - p.pad, bx = ox * p.stride - p.pad;
   const ConvSrcDev& s = p.s0;
@@ -1626,7 +1630,7 @@ __global__ __launch_bounds__(256) void conv_gen_smallcin_kernel(ConvGenParams p,
     }
   }
   const float sc = p.scale ? *p.scale : 1.f;
-  const float rt = p.ratio ? p.ratio[pix] : 1.f;
+  const float rt = p.ratio ? p.ratio[pixc] : 1.f;
   float* yb = p.y + (int64_t)n * Cout * HWo + r;
 #pragma unroll
   for (int c = 0; c < SC_CO; ++c) {
@@ -1635,8 +1639,38 @@ __global__ __launch_bounds__(256) void conv_gen_smallcin_kernel(ConvGenParams p,
       v *= rt;
       if (p.bias) v += p.bias[c];
       acc[c] = apply_act(v, act, p.slope);
-      yb[(int64_t)c * HWo] = acc[c];
+      if (valid) yb[(int64_t)c * HWo] = acc[c];
     }
+  }
+  if (p.y16 && L16) {
+    // the block's [256 pixels][Cout] bf16 run staged in the weights' LDS (rows
+    // padded by 16 bytes against bank conflicts), then copied out as
+    // consecutive 16-byte chunks: fully coalesced stores (each lane's own
+    // 128-byte row store touched 8 lines per instruction at 16 bytes each)
+    constexpr int RS = SC_CO * 2 + 16;   // bytes per staged pixel row
+    static_assert(256 * RS <= (int)sizeof(sw), "y16 staging fits the weight LDS");
+    __syncthreads();                     // every wave done with the weights
+    unsigned char* st = reinterpret_cast<unsigned char*>(&sw[0][0]);
+#pragma unroll
+    for (int c = 0; c < SC_CO; c += 8) {
+      if (c < Cout) {
+        uint32_t h[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          h[j] = (uint32_t)__builtin_bit_cast(uint16_t, (__bf16)acc[c + 2 * j]) |
+                 ((uint32_t)__builtin_bit_cast(uint16_t, (__bf16)acc[c + 2 * j + 1]) << 16);
+        *reinterpret_cast<uint4*>(st + threadIdx.x * RS + 2 * c) = make_uint4(h[0], h[1], h[2], h[3]);
+      }
+    }
+    __syncthreads();
+    const int cpp = Cout / 8;            // 16-byte chunks per pixel
+    const int nblk = (int)min<int64_t>(256, NP - pix0);
+    uint4* o = reinterpret_cast<uint4*>(p.y16 + pix0 * Cout);
+    for (int q = threadIdx.x; q < nblk * cpp; q += 256) {
+      const int pl = q / cpp, part = q - pl * cpp;
+      o[q] = *reinterpret_cast<const uint4*>(st + pl * RS + 16 * part);
+    }
+    return;
   }
   // the next conv's channel-last bf16 source (Cout % 8 == 0): this pixel's
   // Cout values as one contiguous run of 16-byte stores
@@ -2623,12 +2657,20 @@ extern "C" int ainp_conv_gen_fwd_out16(const float* x0, const float* m0, int C0,
       (int64_t)C0 * KH * KW <= SC_K && C0 <= 4) {
     const int64_t NPs = N * (int64_t)Ho * Wo;
     p.y16 = y16;
-    if (b16)
-      hipLaunchKernelGGL(conv_gen_smallcin_kernel<true>, dim3((unsigned)cdiv(NPs, 256)), dim3(256),
-                         0, s, p, act);
+    // AINP_SMALLCIN_LDS16=0: each thread stores its own pixel's bf16 row (A/B)
+    static const bool l16 = [] {
+      const char* e = getenv("AINP_SMALLCIN_LDS16");
+      return !(e && e[0] == '0');
+    }();
+    const dim3 g((unsigned)cdiv(NPs, 256));
+    if (b16 && l16 && y16 && Cout % 8 == 0)
+      hipLaunchKernelGGL((conv_gen_smallcin_kernel<true, true>), g, dim3(256), 0, s, p, act);
+    else if (b16)
+      hipLaunchKernelGGL((conv_gen_smallcin_kernel<true, false>), g, dim3(256), 0, s, p, act);
+    else if (l16 && y16 && Cout % 8 == 0)
+      hipLaunchKernelGGL((conv_gen_smallcin_kernel<false, true>), g, dim3(256), 0, s, p, act);
     else
-      hipLaunchKernelGGL(conv_gen_smallcin_kernel<false>, dim3((unsigned)cdiv(NPs, 256)), dim3(256),
-                         0, s, p, act);
+      hipLaunchKernelGGL((conv_gen_smallcin_kernel<false, false>), g, dim3(256), 0, s, p, act);
     return check_launch("conv_gen_smallcin");
   }
   if (y16) return record_msg("ainp_conv_gen_fwd: y16 is written by the few-input-channel kernel only");
