@@ -541,7 +541,10 @@ def in_step_table(key, bf16, top=8, families=None):
         res["families"] = fam
         res["family_work"] = ("FLOP per step of each kernel family from ops.WORK_TRACE over one "
                               "live step (2 * outputs * Cin * k * k per conv launch, by the "
-                              "kernel the launch routes to; D weight gradients as GEMM FLOP)")
+                              "kernel the launch routes to; D weight gradients as GEMM FLOP). The split-K "
+                              "epilogues (conv_gen_splitk_*) belong to no family: their time is "
+                              "not in any family's ms_per_step, so a split-K layer's family "
+                              "fraction excludes it (see the top table)")
     return res
 
 

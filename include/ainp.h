@@ -472,7 +472,8 @@ int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale
  * AINP_BN_Y16: bf16 storage), so dx and y are not read again.  dx is written
  * as ainp_conv3x3_dgrad_ex writes it; sums as ainp_bn_relu_bwd_reduce_ex
  * with AINP_BN_CL would (same terms, another fixed summation order).  flags:
- * ainp_conv3x3_dgrad_ex's, AINP_CONV_YCL required; Cin % 8 == 0, <= 64;
+ * ainp_conv3x3_dgrad_ex's, AINP_CONV_YCL required; Cin in {16, 32, 64}
+ * (the channel-last BatchNorm reduce's instances; others are refused up front);
  * dx / y / scale / shift / save 16-byte aligned.  Pairs without a fused
  * kernel (or AINP_DGRAD_BNR=0) run the two passes.  Replaces the
  * conv-backward + BatchNorm2d-backward pair of autograd on

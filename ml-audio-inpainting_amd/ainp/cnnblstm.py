@@ -134,7 +134,9 @@ class _ConvStackFn(torch.autograd.Function):
             # placeholder of its shape, and its gradient (dX, fp32) as usual
             if ylcl:
                 # B16_KM: the backward reads X k-major, so no X^T is written
-                km = ops.B16_KM and (N * W) % 32 == 0
+                # and H % 8 == 0: the chunked (data-parallel) weight gradient
+                # reads 16-byte aligned gate-column views dg16[:, d*4H + r0:]
+                km = ops.B16_KM and (N * W) % 32 == 0 and l0_box.get("H", 0) % 8 == 0
                 l0_box["x16"] = ops.bn_relu_apply_ntcf_cl(yl, last[0], last[1], out32=False,
                                                           out16=True, outT=not km)[1]
                 l0_box["km"] = km
@@ -427,12 +429,13 @@ class _BLSTMFn(torch.autograd.Function):
             if pair or pair16:
                 dxi = torch.empty(NT, Il, device=dh.device)
                 if ops.PAIR_JOIN:
-                    # the side stream's queued weight gradients finish first at
-                    # full width: the pair kernel (160 KB of LDS per workgroup)
-                    # cannot share a CU with them
-                    ev = torch.cuda.Event()
-                    ev.record(side)
-                    main.wait_event(ev)
+                    # (A/B switch, off by default) the work queued on BOTH side
+                    # streams -- the BLSTM's weight gradients and the deferred
+                    # decoder / projection ones -- finishes first at full width:
+                    # the pair kernel (160 KB of LDS per workgroup) cannot share a
+                    # CU with them.  Off, the deferred jobs run beside the pair
+                    # (C2 faster that way)
+                    _join_side(dh.device)
                 if pair:
                     gwi = [torch.empty(4 * H, Il, device=dh.device) for _ in range(2)]
                     ops.lstm_l0_bwd_x6(dg2, wf, wr, inp, dxi, gwi[0], gwi[1])
@@ -1024,7 +1027,8 @@ class StackedBLSTMCNN(nn.Module):
         batch_size, _, freq_bins, timeframes = x.shape
         x = x.contiguous()
         spec, params = self._stack(self.encoder)
-        box = {} if self.bf16 else None       # layer-0 bf16 operands (encoder -> BLSTM)
+        # layer-0 bf16 operands (encoder -> BLSTM)
+        box = {"H": self.hidden_dim} if self.bf16 else None
         # the deferred weight gradients are written after autograd receives
         # them: only while the .grad buffers are empty (nothing accumulates)
         sink = self.grad_reducer if (self.training and torch.is_grad_enabled()) else None

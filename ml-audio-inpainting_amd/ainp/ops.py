@@ -1283,7 +1283,9 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
         elif _direct_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats):
             nm = "conv_gen_smallcin_kernel"
         else:
-            nm = "conv_gen_x6_kernel" if not bf16 else "conv_gen"
+            # exact kernel names: a bare "conv_gen" would also match the nhwc16,
+            # few-channel, wide and split-K epilogue rows of the step table
+            nm = "conv_gen_x6_kernel" if not bf16 else "conv_gen_fwd_kernel"
         _work(nm, flop)
     if out is None:
         if Cout == 1 and crop is not None:

@@ -270,6 +270,12 @@ void conv3x3_dgrad_bnr(const Tensor& dy, const Tensor& w, const Tensor& dx, int6
                 W = dy.size(gcl ? 2 : 3), Cin = w.size(1);
   numel_is(dx, N * Cin * H * W, "dx");
   numel_is(y, N * Cin * H * W, "y");
+  // the kernels stage 4*Cin BatchNorm constants (scale, shift, mean, rstd)
+  numel_is(scale, Cin, "scale");
+  numel_is(shift, Cin, "shift");
+  numel_is(save, 2 * Cin, "save");
+  for (const Tensor* t : {&w, &dx, &y, &scale, &shift, &save, &workspace, &sums})
+    same_device(*t, dy);
   TORCH_CHECK(sums.numel() >= 2 * Cin, "sums needs 2C entries");
   TORCH_CHECK((int64_t)workspace.nbytes() >=
                   ainp_conv3x3_dgrad_bnr_workspace(N, (int)Cin, (int)Cout, H, W),

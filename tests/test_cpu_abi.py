@@ -77,6 +77,12 @@ def test_bad_arguments_fail_without_launching():
     rc = _lib.lib.ainp_bn_relu_bwd_apply_ex(None, None, None, None, None, None, None, 1, None,
                                             None, None, 1, 1, 1, 1, 0, 1, None)
     assert rc == -1
+    # fused data gradient + BatchNorm reduce: a channel count the channel-last
+    # reduce has no instance for (24) is refused up front, not in the fallback
+    for cin in (8, 24, 48):
+        rc = _lib.lib.ainp_conv3x3_dgrad_bnr(16, 16, 16, 1, cin, 2 * cin, 8, 8, 64, 16, 16, 16,
+                                             16, 16, 16, 0, None)
+        assert rc == -1 and b"C in {16, 32, 64}" in _lib.lib.ainp_last_error(), cin
 
 
 def test_dy16_routing_query():

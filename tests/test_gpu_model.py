@@ -15,6 +15,12 @@ import torch
 pytestmark = pytest.mark.gpu
 
 TOL = 1e-4
+# C2 fp32 gradients element-wise (strided samples) against the reference's own
+# fp32 gradients: the fp32-vs-fp32 ReLU-branch floor (a BN output within fp32
+# rounding of 0 flips in one run and not the other; ~1e-3 upstream, below).
+# Measured (gpurun_out r06a): max 7.4e-4 (encoder.0.weight), the LSTM and
+# decoder tensors 1e-7 .. 1.7e-4; the gate is 2x the measured max.
+GSAMPLE_FP32_TOL = 1.5e-3
 
 
 def rel(a, b):
@@ -170,6 +176,21 @@ def test_c2_batch32_forward_backward_adam_match_reference(golden_dir):
             continue
         gn = float(gr.norm())
         assert abs(gn - g["gnorm/" + k][0]) <= 5e-3 * g["gnorm/" + k][0] + 1e-6, (k, gn)
+    # element-wise against the reference's OWN fp32 gradients (the strided
+    # gsample/* of cnnblstm_c2.npz, written by the reference's model.py): the
+    # only freedom left is the ReLU branch of activations within fp32 rounding
+    # of 0, which both fp32 runs take independently (GSAMPLE_FP32_TOL, the
+    # measured floor recorded above the constant)
+    serr = {}
+    for k, gr in grads.items():
+        if k in BN_FED_BIASES:
+            continue
+        a = gr.numpy().reshape(-1)
+        serr[k] = rel(a[::max(1, a.size // 4096)], g["gsample/" + k])
+    print("fp32 C2 grad sample errs vs the reference's fp32 gradients",
+          {k: round(v, 7) for k, v in serr.items()})
+    bad = {k: v for k, v in serr.items() if v >= GSAMPLE_FP32_TOL}
+    assert not bad, bad
     # fp64 oracle on the kernels' ReLU branch
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
     p = {k: (v.double() if v.is_floating_point() else v) for k, v in R.init_params(cfg, 0).items()}
@@ -344,6 +365,10 @@ def test_bf16_loss_curve_30_steps_tracks_fp32_reference(golden_dir):
 BF16_GNORM_TOL = 2e-2
 BF16_GSAMPLE_TOL = 5e-2
 BF16_EMU_TOL = 2e-2
+# absolute cap on the bf16 gradients' distance from the fp32 reference (norm and
+# sample), independent of the emulation fixture; measured max 0.433 (the sample
+# of encoder.0.weight, gpurun_out r05d), the rest <= 0.40
+BF16_FP32_CAP = 0.5
 
 
 def test_bf16_c2_batch32_forward_backward_tracks_reference(golden_dir):
@@ -414,6 +439,9 @@ def test_bf16_c2_batch32_forward_backward_tracks_reference(golden_dir):
         emu_s = rel(emu["emu32/gsample/" + k], g["gsample/" + k])
         bn, bs = max(BF16_GNORM_TOL, 2 * emu_n), max(BF16_GSAMPLE_TOL, 2 * emu_s)
         assert e_n < bn and e_s < bs, (k, e_n, e_s, bn, bs)
+        # a cap that does not follow the emulation: a rounding point added to
+        # the implementation (and to the fixture) cannot widen it silently
+        assert e_n < BF16_FP32_CAP and e_s < BF16_FP32_CAP, (k, e_n, e_s, BF16_FP32_CAP)
 
 
 def test_bf16_gy_storage_is_bit_identical(monkeypatch):
