@@ -1300,7 +1300,7 @@ bool conv_x6_fwd16_ok(int Cin, int Cout, int64_t H, int64_t W);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
                          int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16,
-                         int lay);
+                         int lay, int* grid_used);
 int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias,
                    const float* sc, const float* sh, float* y, double* stats, int64_t N, int Cin,
                    int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
@@ -1517,10 +1517,10 @@ extern "C" int ainp_conv3x3_dgrad_bnr(const float* dy, const float* w, float* dx
   if (!dy || !w || !dx || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
       N < 1 || Cin < 1 || Cout < 1 || H < 1 || W < 1 || N > 65535 ||
       !conv_grad_flags_ok(flags, false) || !(flags & AINP_CONV_YCL) ||
-      (bn_flags & ~AINP_BN_Y16) || Cin % 8 != 0 || Cin > 64 ||
+      (bn_flags & ~AINP_BN_Y16) || !(Cin == 16 || Cin == 32 || Cin == 64) ||
       !al16(dx) || !al16(y) || !al16(scale) || !al16(shift) || !al16(save_mean_rstd))
-    return record_msg("ainp_conv3x3_dgrad_bnr: bad argument (channel-last dx and y, C % 8 == 0 "
-                      "and <= 64, 16-byte aligned dx / y / scale / shift / save)");
+    return record_msg("ainp_conv3x3_dgrad_bnr: bad argument (channel-last dx and y, C in "
+                      "{16, 32, 64}, 16-byte aligned dx / y / scale / shift / save)");
   const hipStream_t s = as_stream(stream);
   const Bnr bnr{y, scale, shift, save_mean_rstd, (bn_flags & AINP_BN_Y16) ? 1 : 0};
   double* partial = reinterpret_cast<double*>(workspace);
@@ -1663,10 +1663,10 @@ extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
                      in_scale, in_shift, dy, partial, (int)N, Cin, (int)H, (int)W, ci0)
     // split-bf16 kernel where it is instantiated (conv_x6.hip), unless
     // AINP_CONV_EXACT=1; same slab format
-    const int nblk_x6 = b16 ? WG_BLOCKS * conv_x6_occ16() : WG_BLOCKS;
+    int nblk_x6 = b16 ? WG_BLOCKS * conv_x6_occ16() : WG_BLOCKS;
     int rc = (fits && !conv_exact_env())
                  ? conv_wgrad_x6_launch(x, in_scale, in_shift, dy, partial, N, Cin, Cout, H, W,
-                                        ci0, cp, nblk_x6, s, b16, g16, x16, lay)
+                                        ci0, cp, nblk_x6, s, b16, g16, x16, lay, &nblk_x6)
                  : 1;
     if (rc == 1 && (g16 || x16)) return record_msg(kNo16);
     if (rc == 1 && lay)

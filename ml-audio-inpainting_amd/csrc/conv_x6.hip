@@ -1110,6 +1110,351 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
   }
 }
 
+// Round 6: the bf16 configuration's 32 -> 64 weight gradient fed by LDS-DMA
+// (models/CNNBLSTM/model.py:40-42 backward).  conv3x3_wgrad_x6<64, NP = 1>
+// stages each 96-pixel tile through registers behind two barriers and runs
+// only 18 MFMAs per wave per tile (SQ: MFMA busy 0.06, waits 0.7).  Here both
+// bf16 channel-last operands go global -> LDS by global_load_lds_dwordx4
+// into a 3-stage ring (one tile in flight across each barrier, counted
+// vmcnt, raw s_barrier), in the register kernel's LDS images (same swizzles,
+// same transposing fragment reads), on 192-pixel tiles (8 x 24) walked
+// down the frequency axis so consecutive tiles share two halo rows in L2:
+//  * the BatchNorm+ReLU prologue act(x) = relu(x*scale+shift) (zero outside
+//    the image) is applied once per tile in place, an LDS pass between the
+//    two barriers of the tile -- the same fp32 fmaf/max and RNE rounding as
+//    the register kernel's staging, so the staged operands are identical;
+//  * the 18 output tiles (2 co tiles x 9 taps) plus the bias: 8 waves = 4
+//    groups of 5 accumulator tiles (co tile x taps 0-4 / taps 5-8 + bias)
+//    x 2 k-halves of the tile, 2 waves per SIMD, one A (dy) fragment per
+//    k-step shared by a wave's 5 MFMAs;
+//  * db[co] = sum dy on the MFMA: A times a ones B fragment (fp32
+//    accumulation of the bf16 dy);
+//  * epilogue: the k-halves combined through LDS, one slab per workgroup in
+//    conv.hip's [CO][9*32 + 1] slab format (wgrad_reduce1 / wgrad_reduce).
+// The per-pixel work is HBM-bound (2*9*32*64 FLOP per 192 B of bf16 x + dy).
+// global_load_lds_dwordx4 issued from inline asm (the recipe of
+// cdna_hip_programming.md, M0 saved and restored in the statement): hipcc does
+// not track it, so it neither drains it with vmcnt(0) before the LDS reads of
+// other ring stages nor counts it -- the kernel's own counted vmcnt waits do.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, const unsigned char* lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+
+namespace wdm {
+constexpr int TT = 24;                             // tile columns (3 row segments of 8)
+constexpr int HS = 32;                             // halo row stride (pixels)
+constexpr int NT = 512;                            // 8 waves
+constexpr int NW = NT / 64;
+constexpr int CP = 32, CO = 64, J = 9 * CP;
+constexpr int NA = 5;                              // accumulator tiles per wave
+// tile geometry / ring depth per variant (FT tile rows, NS ring stages)
+template <int FT, int NS>
+struct Geo {
+  static constexpr int NPX = FT * TT;                      // pixels per tile (k)
+  static constexpr int HR = FT + 2, HC = TT + 2;           // halo
+  static constexpr int XPIX = (HR - 1) * HS + HC;          // halo pixel slots
+  static constexpr int XBLK = (XPIX * 64 + 1023) / 1024;   // DMA blocks (16 pixels each)
+  static constexpr int GBLK = NPX * 128 / 1024;            // DMA blocks (8 pixels each)
+  static constexpr int XB = XBLK * 1024;
+  static constexpr int STAGE = XB + GBLK * 1024;
+  static constexpr int NBLK = XBLK + GBLK;                 // DMA blocks per tile
+  static constexpr int QMAX = (NBLK + NW - 1) / NW;        // DMA instructions per wave
+  static constexpr int QFULL = NBLK - (QMAX - 1) * NW;     // waves < QFULL issue QMAX
+  static constexpr int LDS = NS * STAGE + 2 * CP * 4;
+  static_assert(FT % 4 == 0 && NPX % 32 == 0, "two k-halves of whole k-steps");
+  static_assert(LDS <= 160 * 1024, "LDS");
+  static_assert(4 * NA * 16 * 64 * 4 <= NS * STAGE, "k-half reduction buffer");
+};
+}  // namespace wdm
+
+// s_waitcnt vmcnt(n * Q), n = DMA tiles left in flight (0..4), Q = this
+// wave's DMA instructions per tile
+template <int Q>
+__device__ __forceinline__ void wdm_wait(int n) {
+  switch (n) {
+    case 0: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(Q) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * Q) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * Q) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * Q) : "memory"); break;
+  }
+}
+
+// dbg (measurement only, AINP_WDM_DBG; wrong results): 1 = no MFMAs,
+// 2 = no prologue pass -- what the DMA ring / the pass alone cost
+template <int FT, int NS>
+__global__ __launch_bounds__(wdm::NT, 1) void conv3x3_wgrad_b16dma_kernel(
+    const uint16_t* __restrict__ x, const float* __restrict__ in_scale,
+    const float* __restrict__ in_shift, const uint16_t* __restrict__ dy,
+    float* __restrict__ partial, int N, int H, int W, int dbg) {
+  using namespace wdm;
+  using G = Geo<FT, NS>;
+  constexpr int NPX = G::NPX, HC = G::HC, XPIX = G::XPIX, XBLK = G::XBLK, XB = G::XB;
+  constexpr int STAGE = G::STAGE, NBLK = G::NBLK, QMAX = G::QMAX, QFULL = G::QFULL;
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[G::LDS];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int ct = wave & 1, th = (wave >> 1) & 1, kh = wave >> 2;   // co tile, tap half, k-half
+  const bool pro = in_scale != nullptr;
+  // transposing-read offsets: the register kernel's (conv3x3_wgrad_x6); slot
+  // j of tap half th is tap 5 th + j (th = 1, j = 4: the bias, no B read)
+  const int g = lane >> 4, q = (lane >> 2) & 3, pp = lane & 3;
+  int bx[NA][2];
+#pragma unroll
+  for (int j = 0; j < NA; ++j)
+#pragma unroll
+    for (int sh = 0; sh < 2; ++sh) {
+      const int tap = 5 * th + j < 9 ? 5 * th + j : 8;
+      const int hp = (tap / 3) * HS + tap % 3 + q + 4 * sh;
+      bx[j][sh] = hp * 64 + 16 * ((2 * (g & 1) + (pp >> 1)) ^ ((hp >> 1) & 3)) + 8 * (pp & 1);
+    }
+  int ba[2];   // pixel q + 4 sh of the lane's segment (segment offsets added below)
+#pragma unroll
+  for (int sh = 0; sh < 2; ++sh) {
+    const int px = q + 4 * sh;
+    ba[sh] = px * 128 + 16 * ((4 * ct + 2 * (g & 1) + (pp >> 1)) ^ wx6_gswz(px)) + 8 * (pp & 1);
+  }
+  const int tg = tid & 3;
+  // prologue constants [scale 32 | shift 32] behind the ring
+  float* sss = reinterpret_cast<float*>(smem + NS * STAGE);
+  if (pro && tid < 2 * CP) {
+    float v = tid < CP ? in_scale[tid] : in_shift[tid - CP];
+    asm volatile("" : "+v"(v));
+    sss[tid] = v;
+  }
+  __syncthreads();   // sss, before any DMA is in flight
+
+  // 32-bit tile arithmetic (the launcher checks N * tiles < 2^31)
+  const unsigned tiles_t = (W + TT - 1) / TT, tiles_f = (H + FT - 1) / FT;
+  const unsigned ntiles = (unsigned)N * tiles_f * tiles_t;
+  // contiguous tile ranges per workgroup, frequency tiles fastest
+  const unsigned per = ntiles / gridDim.x, rem = ntiles % gridDim.x;
+  const unsigned tbeg = blockIdx.x * per + (blockIdx.x < rem ? blockIdx.x : rem);
+  const int cnt = (int)(per + (blockIdx.x < rem ? 1 : 0));
+  auto coords = [&](unsigned t, int& n, int& f0, int& t0) {
+    const unsigned qd = t / tiles_f;
+    f0 = (int)(t - qd * tiles_f) * FT;
+    n = (int)(qd / tiles_t);
+    t0 = (int)(qd - (unsigned)n * tiles_t) * TT;
+  };
+  // lane unit k of this wave's DMAs: the pixel's (row, col) relative to the
+  // tile origin and its byte offset from the origin's pixel.  hole: one of
+  // the halo image's unused columns (never read by the MFMAs)
+  auto unit = [&](int k, int& rr, int& cc, int& off, bool& hole) {
+    const int qb = wave + NW * k;
+    if (qb < XBLK) {
+      // halo pixel slot sp = 16 qb + lane/4, physical 16-byte group lane % 4
+      const int sp = 16 * qb + (lane >> 2), hc = sp & 31;
+      const int grp = (lane & 3) ^ ((sp >> 1) & 3);
+      hole = hc >= HC;
+      rr = (sp >> 5) - 1;
+      cc = hole ? 0 : hc - 1;
+      off = (rr * W + cc) * (CP * 2) + 16 * grp;
+    } else {
+      // dy pixel px = 8 j + lane/8, physical 16-byte group lane % 8
+      const int px = 8 * (qb - XBLK) + (lane >> 3);
+      const int grp = (lane & 7) ^ wx6_gswz(px);
+      hole = false;
+      rr = px / TT;
+      cc = px - rr * TT;
+      off = (rr * W + cc) * (CO * 2) + 16 * grp;
+    }
+  };
+  // interior tiles (halo inside the image, the large majority): the source
+  // is the tile origin plus a per-lane offset fixed across tiles
+  int loff[QMAX];
+#pragma unroll
+  for (int k = 0; k < QMAX; ++k) {
+    int rr, cc;
+    bool hole;
+    unit(k, rr, cc, loff[k], hole);
+  }
+  auto interior = [&](int f0, int t0) {
+    return f0 >= 1 && f0 + FT + 1 <= H && t0 >= 1 && t0 + TT + 1 <= W;
+  };
+  auto issue = [&](int i) {
+    int n, f0, t0;
+    coords(tbeg + i, n, f0, t0);
+    const int64_t org = ((int64_t)n * H + f0) * W + t0;
+    const char* xo = reinterpret_cast<const char*>(x) + org * (CP * 2);
+    const char* go = reinterpret_cast<const char*>(dy) + org * (CO * 2);
+    unsigned char* st = smem + (i % NS) * STAGE;
+    if (interior(f0, t0)) {
+#pragma unroll
+      for (int k = 0; k < QMAX; ++k) {
+        const int qb = wave + NW * k;
+        if (qb >= NBLK) break;
+        glds16_asm((qb < XBLK ? xo : go) + loff[k], st + qb * 1024);
+      }
+      return;
+    }
+#pragma unroll
+    for (int k = 0; k < QMAX; ++k) {
+      const int qb = wave + NW * k;
+      if (qb >= NBLK) break;
+      int rr, cc, off;
+      bool hole;
+      unit(k, rr, cc, off, hole);
+      const bool ok = !hole && (unsigned)(f0 + rr) < (unsigned)H && (unsigned)(t0 + cc) < (unsigned)W;
+      glds16_asm(ok ? (qb < XBLK ? xo : go) + off : reinterpret_cast<const char*>(cdd_zero),
+                 st + qb * 1024);
+    }
+  };
+
+  f32x16 acc[NA];
+#pragma unroll
+  for (int t = 0; t < NA; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+  bf16x8c ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < cnt) issue(i);
+  for (int i = 0; i < cnt; ++i) {
+    // tile i landed (this wave's DMAs); tiles i+1 .. i+NS-2 may stay in flight
+    const int ahead = cnt - 1 - i < NS - 2 ? cnt - 1 - i : NS - 2;
+    if (wave < QFULL) wdm_wait<QMAX>(ahead);
+    else wdm_wait<QMAX - 1>(ahead);
+    unsigned char* sx = smem + (i % NS) * STAGE;
+    const unsigned char* sg = sx + XB;
+    if (pro && !(dbg & 2)) {
+      // act(x) in place, before the tile's barrier: each lane rewrites the 16
+      // bytes its own DMA wrote (its vmcnt wait above retired them), so no
+      // other wave's data is read here and the pass overlaps the other waves'
+      // MFMAs of the previous tile.  Outside the image the DMA wrote zeros,
+      // which stay (nn.Conv2d pads after the ReLU).
+      int n, f0, t0;
+      coords(tbeg + i, n, f0, t0);
+      const bool inner = interior(f0, t0);   // every lane's pixel in the image
+#pragma unroll
+      for (int k = 0; k < QMAX; ++k) {
+        const int qb = wave + NW * k;
+        if (qb >= XBLK) break;
+        const int sp = 16 * qb + (lane >> 2), hr = sp >> 5, hc = sp & 31;
+        const int grp = (lane & 3) ^ ((sp >> 1) & 3);
+        const int gr = f0 - 1 + hr, gc = t0 - 1 + hc;
+        if (inner || (hc < HC && (unsigned)gr < (unsigned)H && (unsigned)gc < (unsigned)W)) {
+          uint4* p = reinterpret_cast<uint4*>(sx + qb * 1024 + 16 * lane);
+          const uint4 v = *p;
+          const float4 c0 = reinterpret_cast<const float4*>(sss)[2 * grp];
+          const float4 c1 = reinterpret_cast<const float4*>(sss)[2 * grp + 1];
+          const float4 h0 = reinterpret_cast<const float4*>(sss + CP)[2 * grp];
+          const float4 h1 = reinterpret_cast<const float4*>(sss + CP)[2 * grp + 1];
+          const float ssc[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+          const float ssh[8] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w};
+          const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+          uint32_t o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float a = fmaxf(fmaf(__uint_as_float(w4[e] << 16), ssc[2 * e], ssh[2 * e]), 0.f);
+            const float b = fmaxf(fmaf(__uint_as_float(w4[e] & 0xffff0000u), ssc[2 * e + 1],
+                                       ssh[2 * e + 1]), 0.f);
+            o[e] = cx6_cvt_pk(a, b);
+          }
+          *p = make_uint4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // tile i (DMAs + prologue) visible; stage i-1 free
+    asm volatile("" ::: "memory");
+    if (i + NS - 1 < cnt) issue(i + NS - 1);
+    if (dbg & 1) continue;
+    // fragments of k-step ks+1 are read while the MFMAs of ks run (two
+    // register sets); the bias slot's ones fragment is selected, not branched
+    constexpr int KS = NPX / 32;
+    // per-lane fragment bases of this stage, once per tile; the k-step and
+    // segment offsets below are compile-time (ds_read offset fields)
+    // k-step kk takes 8-pixel row segment G = kk (lanes 0-31) and
+    // G = kk + NG/2 (lanes 32-63, NG/2 segments = whole tile rows later), so
+    // the lane-half part of every fragment address is a per-lane constant
+    // folded into these bases and the k-step part is compile-time
+    // (the k-half kh likewise: its KS k-steps are KS / 3 whole tile rows)
+    constexpr int NG = NPX / 8, HROWS = NG / 2 / 3;
+    static_assert((NPX / 32) % 3 == 0, "k-half = whole tile rows");
+    const int ao = (lh * (NG / 2) + kh * (NPX / 32)) * 8 * 128;
+    const int bo = (lh * HROWS + kh * (NPX / 32) / 3) * HS * 64;
+    const unsigned char* pa0 = sg + ba[0] + ao;
+    const unsigned char* pa1 = sg + ba[1] + ao;
+    const unsigned char* pb[NA][2];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      pb[j][0] = sx + bx[j][0] + bo;
+      pb[j][1] = sx + bx[j][1] + bo;
+    }
+    auto frag_a = [&](int kk) {
+      return wx6_cat(wx6_tr(pa0 + kk * 8 * 128), wx6_tr(pa1 + kk * 8 * 128));
+    };
+    auto frag_b = [&](int kk, int j) {
+      const int seg = (kk / 3) * HS + (kk % 3) * 8;
+      return wx6_cat(wx6_tr(pb[j][0] + seg * 64), wx6_tr(pb[j][1] + seg * 64));
+    };
+    bf16x8c fa[2], fb[2][NA];
+    fa[0] = frag_a(0);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) fb[0][j] = frag_b(0, j);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < KS) {
+        fa[cur ^ 1] = frag_a(ks + 1);
+#pragma unroll
+        for (int j = 0; j < NA; ++j) fb[cur ^ 1][j] = frag_b(ks + 1, j);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMAs
+#pragma unroll
+      for (int j = 0; j < NA - 1; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur], fb[cur][j], acc[j], 0, 0, 0);
+      acc[NA - 1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur], th ? ones : fb[cur][NA - 1],
+                                                            acc[NA - 1], 0, 0, 0);
+    }
+  }
+  // combine the k-halves through the (now idle) ring, then one slab
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem);
+  const int wg = wave & 3;
+  if (kh == 1) {
+#pragma unroll
+    for (int t = 0; t < NA; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[((wg * NA + t) * 16 + r) * 64 + lane] = acc[t][r];
+  }
+  __syncthreads();
+  if (kh == 1) return;
+  float* slab = partial + (int64_t)blockIdx.x * CO * (J + 1);
+#pragma unroll
+  for (int j = 0; j < NA; ++j) {
+    const int tap = 5 * th + j;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int co = ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const float v = acc[j][r] + red[((wg * NA + j) * 16 + r) * 64 + lane];
+      if (tap < 9) slab[co * (J + 1) + tap * CP + li] = v;
+      else if (li == 0) slab[co * (J + 1) + J] = v;    // the ones column: db
+    }
+  }
+}
+
+// AINP_WGRAD16_DMA=0: the register-staged kernel for that weight gradient (A/B)
+static bool wgrad16_dma() {
+  static const bool v = [] {
+    const char* e = getenv("AINP_WGRAD16_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 // Small-channel variant for (Cin pass, Cout) = (32, 16) and (16, 32): one of
 // the two GEMM dimensions is 16, so the 32x32 tiles above would be half
 // empty.  Same tiles, staging, slabs and bias as conv3x3_wgrad_x6, on
@@ -2079,7 +2424,43 @@ static int wgrad_x6_go(const float* x, const float* sc, const float* sh, const f
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
                          int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16,
-                         int lay) {
+                         int lay, int* grid_used) {
+  *grid_used = grid;
+  // bf16 channel-last 32 -> 64 (the bf16 configuration's encoder conv): the
+  // LDS-DMA kernel, one workgroup per CU (its slabs: grid_used)
+  if (b16 && g16 && x16 && lay == (CL_X | CL_G) && Cin == 32 && cp == 32 && ci0 == 0 &&
+      Cout == 64 && wgrad16_dma()) {
+    int dev = 0, ncu = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int g = ncu >= 16 ? ncu / 16 * 16 : 16;   // a multiple of WG_GROUPS (16)
+    if (N * ((H + 3) / 4) * ((W + wdm::TT - 1) / wdm::TT) >= ((int64_t)1 << 31))
+      return record_msg("conv3x3_wgrad_b16dma: too many tiles");
+    *grid_used = g;
+    static const int var = [] {
+      const char* e = getenv("AINP_WDM_VARIANT");
+      return e ? atoi(e) : 0;
+    }();
+    static const int dbg = [] {
+      const char* e = getenv("AINP_WDM_DBG");
+      return e ? atoi(e) : 0;
+    }();
+#define AINP_WDM(FTV, NSV)                                                                   \
+  hipLaunchKernelGGL((conv3x3_wgrad_b16dma_kernel<FTV, NSV>), dim3(g), dim3(wdm::NT), 0, s, \
+                     reinterpret_cast<const uint16_t*>(x), sc, sh,                          \
+                     reinterpret_cast<const uint16_t*>(dy), partial, (int)N, (int)H, (int)W, dbg)
+    // default: 8-row tiles, 2 stages (r06h sweep, standalone at the C3 shape:
+    // <8,2> 174 us, <4,4> 218, <4,5> 230, <4,6> 232; <8,3> needs more than
+    // 256 VGPRs with the fragment double buffer and spills)
+    switch (var) {
+      case 1: AINP_WDM(4, 5); break;
+      case 2: AINP_WDM(4, 6); break;
+      case 3: AINP_WDM(4, 4); break;
+      default: AINP_WDM(8, 2); break;
+    }
+#undef AINP_WDM
+    return check_launch("conv3x3_wgrad_b16dma");
+  }
   if (b16) {
     if (g16 && x16) return wgrad_x6_go<1, true, true>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s, lay);
     if (g16) return wgrad_x6_go<1, true, false>(x, sc, sh, dy, partial, N, Cin, Cout, H, W, ci0, cp, grid, s, lay);

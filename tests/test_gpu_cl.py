@@ -342,3 +342,32 @@ def test_cnnblstm_step_dgrad_bnr_matches_two_pass(monkeypatch, dtype):
         errs[n] = rel(res[0][1][n], g1)
     bad = {n: e for n, e in errs.items() if e >= tol}
     assert not bad, (bad, max(errs.values()))
+
+
+@pytest.mark.parametrize("pro", [True, False])
+@pytest.mark.parametrize("N,H,W", SHAPES + [(3, 70, 50)])
+def test_wgrad16_dma_matches_register_kernel(N, H, W, pro):
+    """Round 6: the bf16 channel-last 32 -> 64 weight gradient on the LDS-DMA
+    kernel (conv3x3_wgrad_b16dma_kernel: bf16 x and dy channel-last, the
+    BatchNorm+ReLU prologue applied in LDS) stages the same bf16 operands as
+    the register kernel (conv3x3_wgrad_x6, NCHW launch of the same tensors) and
+    sums the same products in another fixed order: dw / db within 1e-6 of it,
+    within 2e-5 of an fp64 weight gradient of the bf16-rounded operands, and
+    run-to-run identical."""
+    from ainp import ops
+    import torch.nn.functional as Fnn  # noqa: F401
+    x, dy, w, b, sc, sh = _data(N, 32, 64, H, W, 321 + H)
+    x16, dy16 = x.to(torch.bfloat16), dy.to(torch.bfloat16)
+    s_, h_ = (sc, sh) if pro else (None, None)
+    dw0, db0 = ops.conv3x3_wgrad(x16, dy16, s_, h_, bf16=True)                 # register kernel
+    dw, db = ops.conv3x3_wgrad(_cl(x16), _cl(dy16), s_, h_, bf16=True, xcl=True, gcl=True)
+    dw2, db2 = ops.conv3x3_wgrad(_cl(x16), _cl(dy16), s_, h_, bf16=True, xcl=True, gcl=True)
+    assert torch.equal(dw, dw2) and torch.equal(db, db2)
+    assert rel(dw, dw0) < 1e-6 and rel(db, db0) < 1e-6, (rel(dw, dw0), rel(db, db0))
+    xa = x16.double()
+    if pro:   # the kernels' fp32 prologue, rounded to bf16 once
+        xa = torch.relu(torch.addcmul(sh.view(1, -1, 1, 1).float(), x16.float(),
+                                      sc.view(1, -1, 1, 1))).to(torch.bfloat16).double()
+    dwr = torch.nn.grad.conv2d_weight(xa, w.shape, dy16.double(), padding=1)
+    assert rel(dw, dwr) < 2e-5, rel(dw, dwr)
+    assert rel(db, dy16.double().sum((0, 2, 3))) < 1e-6
