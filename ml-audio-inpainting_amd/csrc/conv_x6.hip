@@ -228,6 +228,22 @@ constexpr int YBLK = TR * TC * COP * 2 / 1024;              // 16 blocks: bf16 y
 }  // namespace cdd
 __device__ __attribute__((aligned(64))) uint16_t cdd_zero[8];   // zero-initialised
 
+// global_load_lds_dwordx4 issued from inline asm (the recipe of
+// cdna_hip_programming.md, M0 saved and restored in the statement): hipcc does
+// not track it, so it neither drains it with vmcnt(0) before the LDS reads of
+// other ring stages nor counts it -- the kernel's own counted vmcnt waits do.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, const unsigned char* lds) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane(
+      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)lds);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
+               "s_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+
+
 __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
     const uint16_t* __restrict__ gy, const float* __restrict__ w, float* __restrict__ dx,
     double* __restrict__ stats, Bnr bnr, int N, int H, int W, int ntr, int ntc, int64_t ntiles) {
@@ -368,6 +384,236 @@ __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
     for (int wv = 0; wv < NT / 64; ++wv) a += red[(wv * 2 + k) * COP + co];
     stats[(int64_t)blockIdx.x * 2 * COP + tid] = a;
   }
+}
+
+// Round 6: the bf16 configuration's forward convs (encoder 16 -> 32 and
+// 32 -> 64, decoder 16 -> 32; models/CNNBLSTM/model.py:35-43,53-55) on the
+// same LDS-DMA structure: one persistent grid as conv3x3_x6p_kernel's (same
+// tiles, same tile order per workgroup, same wave -> (output row, 32-channel
+// tile) map), the tile's whole CI-channel halo brought by
+// global_load_lds_dwordx4 into one of two LDS buffers while the previous
+// tile's MFMAs run, the weights staged once.  The input is the previous
+// layer's pre-BatchNorm y (bf16 channel-last): its BatchNorm+ReLU is applied
+// in LDS before the tile's barrier, each lane rewriting the 16 bytes its own
+// DMA wrote (the same fmaf / max / RNE rounding as x6p's staging; zeros
+// outside the image stay zero).  Same LDS images, the same chunk -> tap ->
+// channel-tile MFMA order, the same epilogue (bias, bf16 rounding, channel-
+// last store, fixed-order BatchNorm partials): bit-identical to x6p<CI, COP,
+// NP = 1, G16, Y16, XL, YL>.  (The DMA is issued from inline asm, so hipcc
+// adds no vmcnt(0) before the LDS reads; the loop's own vmcnt(0) at the top
+// retires the tile's DMA and the previous epilogue's stores.)
+namespace cdf {
+constexpr int TR = 8, TC = 32, HR = TR + 2, HC = TC + 2;
+constexpr int XROW = HC * 32;                                // 1088
+constexpr int NPIX = HR * HC;                                // 340 halo pixels
+constexpr int XBLK = (NPIX * 32 + 1023) / 1024;              // 11 DMA blocks per plane
+constexpr int XPP = XBLK * 1024;                             // padded plane
+constexpr int WROW = 9 * 32 + 16;                            // 304
+}  // namespace cdf
+
+template <int CI, int COP, int NT>
+__global__ __launch_bounds__(NT, 1) void conv3x3_fwd_b16dma_kernel(
+    const uint16_t* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+    uint16_t* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W) {
+  using namespace cdf;
+  constexpr int NCK = CI / 16, NI = COP / 32, NW = NT / 64, NIW = NI * TR / NW;
+  static_assert(CI % 16 == 0 && (COP == 32 || COP == 64) && NIW >= 1 && NIW * NW == NI * TR,
+                "shape");
+  constexpr int XBUF = NCK * XPP, WPLANE = COP * WROW;
+  constexpr int NBLK = NCK * XBLK;                         // DMA blocks per tile
+  constexpr int QMAX = (NBLK + NW - 1) / NW;
+  constexpr int OFF_W = 2 * XBUF, OFF_SS = OFF_W + NCK * WPLANE, OFF_B = OFF_SS + 2 * CI * 4;
+  constexpr int LDS = OFF_B + COP * 4;
+  static_assert(2 * XBUF >= TR * 2 * COP * 8, "BatchNorm row sums reuse the halo buffers");
+  // one LDS object: [halo buffer 0 | halo buffer 1 | weights | scale, shift | bias]
+  __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
+  unsigned char* sw = smem + OFF_W;
+  float* sss = reinterpret_cast<float*>(smem + OFF_SS);
+  float* s_b = reinterpret_cast<float*>(smem + OFF_B);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const int wrow = wave % TR, wco = (wave / TR) * NIW;
+  const bool pro = in_scale != nullptr;
+
+  for (int u = tid; u < NCK * COP * 18; u += NT) {
+    const int half = u & 1, tap = (u >> 1) % 9, co = (u / 18) % COP, ch = u / (18 * COP);
+    float pw[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int ci = ch * 16 + 8 * half + c;
+      pw[c] = co < Cout ? w[((int64_t)co * CI + ci) * 9 + tap] : 0.f;
+    }
+    cx6_stage<1>(pw, sw + ch * WPLANE + co * WROW + tap * 32 + 16 * half, WPLANE);
+  }
+  if (tid < 2 * CI) sss[tid] = pro ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
+  if (tid < COP) s_b[tid] = (bias && tid < Cout) ? bias[tid] : 0.f;
+  __syncthreads();   // weights and constants, before any DMA is in flight
+
+  const int tiles_c = (W + TC - 1) / TC, tiles_r = (H + TR - 1) / TR;
+  const int64_t ntiles = (int64_t)N * tiles_r * tiles_c;
+  auto coords = [&](int64_t t, int& n, int& r0, int& c0) {
+    c0 = (int)(t % tiles_c) * TC;
+    r0 = (int)((t / tiles_c) % tiles_r) * TR;
+    n = (int)(t / ((int64_t)tiles_c * tiles_r));
+  };
+  // DMA unit k of this wave: block qb = wave + NW k (plane qb / XBLK, block
+  // qb % XBLK); lane L -> halo pixel 32 j + L/2, physical half L % 2 holding
+  // the logical half (L % 2) ^ (column bit 3)
+  auto issue = [&](int64_t t, unsigned char* buf) {
+    int n, r0, c0;
+    coords(t, n, r0, c0);
+#pragma unroll
+    for (int k = 0; k < QMAX; ++k) {
+      const int qb = wave + NW * k;
+      if (qb >= NBLK) break;
+      const int kc = qb / XBLK, j = qb % XBLK;
+      const int lp = 32 * j + (lane >> 1);
+      const uint16_t* src = cdd_zero;
+      if (lp < NPIX) {
+        const int row = lp / HC, col = lp % HC;
+        const int gr = r0 - 1 + row, gc = c0 - 1 + col;
+        const int hl = (lane & 1) ^ ((col >> 3) & 1);
+        if ((unsigned)gr < (unsigned)H && (unsigned)gc < (unsigned)W)
+          src = x + (((int64_t)n * H + gr) * W + gc) * CI + kc * 16 + 8 * hl;
+      }
+      glds16_asm(src, buf + kc * XPP + j * 1024);
+    }
+  };
+  // BatchNorm+ReLU of the lane's own DMA units, in place
+  auto prologue = [&](int64_t t, unsigned char* buf) {
+    int n, r0, c0;
+    coords(t, n, r0, c0);
+#pragma unroll
+    for (int k = 0; k < QMAX; ++k) {
+      const int qb = wave + NW * k;
+      if (qb >= NBLK) break;
+      const int kc = qb / XBLK, j = qb % XBLK;
+      const int lp = 32 * j + (lane >> 1);
+      const int row = lp / HC, col = lp % HC;
+      const int gr = r0 - 1 + row, gc = c0 - 1 + col;
+      if (lp < NPIX && (unsigned)gr < (unsigned)H && (unsigned)gc < (unsigned)W) {
+        const int ci0 = kc * 16 + 8 * ((lane & 1) ^ ((col >> 3) & 1));
+        uint4* p = reinterpret_cast<uint4*>(buf + kc * XPP + j * 1024 + 16 * lane);
+        const uint4 v = *p;
+        const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+        uint32_t o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = ci0 + 2 * e;
+          const float a = fmaxf(fmaf(__uint_as_float(w4[e] << 16), sss[c], sss[CI + c]), 0.f);
+          const float b = fmaxf(fmaf(__uint_as_float(w4[e] & 0xffff0000u), sss[c + 1],
+                                     sss[CI + c + 1]), 0.f);
+          o[e] = cx6_cvt_pk(a, b);
+        }
+        *p = make_uint4(o[0], o[1], o[2], o[3]);
+      }
+    }
+  };
+
+  f32x16 acc[NIW];
+  double bs[NIW], bq[NIW];
+#pragma unroll
+  for (int i = 0; i < NIW; ++i) bs[i] = bq[i] = 0.0;
+  int64_t t = blockIdx.x;
+  if (t < ntiles) issue(t, smem);
+  bool cur_a = true;
+  for (; t < ntiles; t += gridDim.x) {
+    unsigned char* sx = cur_a ? smem : smem + XBUF;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile t
+    if (pro) prologue(t, sx);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // tile t complete in LDS; the other buffer is free
+    asm volatile("" ::: "memory");
+    const int64_t tn = t + gridDim.x;
+    if (tn < ntiles) issue(tn, cur_a ? smem + XBUF : smem);
+#pragma unroll
+    for (int i = 0; i < NIW; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll
+    for (int kc = 0; kc < NCK; ++kc) {
+      const unsigned char* wb0 = sw + kc * WPLANE + li * WROW + 16 * lh;
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3, dxx = tap % 3;
+        const int hcol = li + dxx;
+        const bf16x8c b = cx6_ld(sx + kc * XPP + (wrow + dy) * XROW + hcol * 32 +
+                                 16 * (lh ^ ((hcol >> 3) & 1)));
+        bf16x8c a[NIW];
+#pragma unroll
+        for (int i = 0; i < NIW; ++i) a[i] = cx6_ld(wb0 + (wco + i) * 32 * WROW + tap * 32);
+#pragma unroll
+        for (int i = 0; i < NIW; ++i)
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b, acc[i], 0, 0, 0);
+      }
+    }
+    // epilogue (conv3x3_x6p_kernel's, Y16 + YL): bias, bf16 rounding,
+    // channel-last stores of 4 channels, BatchNorm sums of the stored values
+    int n, r0, c0;
+    coords(t, n, r0, c0);
+    const int row = r0 + wrow, col = c0 + li;
+    const bool pok = row < H && col < W;
+    const int64_t ycl = (((int64_t)n * H + row) * W + col) * Cout;
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) {
+      float s[16], q[16], vv[16];
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = 32 * (wco + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        const bool ok = pok && co < Cout;
+        const float v = y16_round(acc[i][r] + s_b[co]);
+        vv[r] = v;
+        s[r] = ok ? v : 0.f;
+        q[r] = s[r] * s[r];
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; ++rb) {
+        const int co0 = 32 * (wco + i) + 8 * rb + 4 * lh;
+        if (pok && co0 < Cout)
+          cl_st4<true>(reinterpret_cast<float*>(y), ycl + co0, vv[4 * rb], vv[4 * rb + 1],
+                       vv[4 * rb + 2], vv[4 * rb + 3]);
+      }
+      if (stats) {
+        bs[i] += (double)x6_reduce16(s, li);
+        bq[i] += (double)x6_reduce16(q, li);
+      }
+    }
+    cur_a = !cur_a;
+  }
+  if (!stats) return;
+  // per-row sums -> [row][sum, sum of squares][COP] (the halo buffers are free)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  double* red = reinterpret_cast<double*>(smem);
+  if ((li & 1) == 0) {
+#pragma unroll
+    for (int i = 0; i < NIW; ++i) {
+      const int r = li >> 1;
+      const int co = 32 * (wco + i) + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      red[(wrow * 2 + 0) * COP + co] = bs[i];
+      red[(wrow * 2 + 1) * COP + co] = bq[i];
+    }
+  }
+  __syncthreads();
+  for (int co = tid; co < Cout; co += NT) {
+    double sm = 0.0, sq = 0.0;
+    for (int wv = 0; wv < TR; ++wv) {
+      sm += red[(wv * 2 + 0) * COP + co];
+      sq += red[(wv * 2 + 1) * COP + co];
+    }
+    stats[(int64_t)blockIdx.x * 2 * Cout + co] = sm;
+    stats[(int64_t)blockIdx.x * 2 * Cout + Cout + co] = sq;
+  }
+}
+
+// AINP_CONV16_DMA=0: the register-staged x6p forwards (A/B)
+static bool conv16_dma() {
+  static const bool v = [] {
+    const char* e = getenv("AINP_CONV16_DMA");
+    return !(e && e[0] == '0');
+  }();
+  return v;
 }
 
 // AINP_DGRAD16_DMA=0: the register-staged kernel for that data gradient (A/B)
@@ -1132,21 +1378,6 @@ __global__ __launch_bounds__(CO / 32 * 3 * 64, 3) void conv3x3_wgrad_x6(
 //  * epilogue: the k-halves combined through LDS, one slab per workgroup in
 //    conv.hip's [CO][9*32 + 1] slab format (wgrad_reduce1 / wgrad_reduce).
 // The per-pixel work is HBM-bound (2*9*32*64 FLOP per 192 B of bf16 x + dy).
-// global_load_lds_dwordx4 issued from inline asm (the recipe of
-// cdna_hip_programming.md, M0 saved and restored in the statement): hipcc does
-// not track it, so it neither drains it with vmcnt(0) before the LDS reads of
-// other ring stages nor counts it -- the kernel's own counted vmcnt waits do.
-__device__ __forceinline__ void glds16_asm(const void* gsrc, const unsigned char* lds) {
-  const uint32_t dst = __builtin_amdgcn_readfirstlane(
-      (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) unsigned char*)lds);
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\t"
-               "s_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(dst)
-               : "memory");
-}
-
 namespace wdm {
 constexpr int TT = 24;                             // tile columns (3 row segments of 8)
 constexpr int HS = 32;                             // halo row stride (pixels)
@@ -2360,6 +2591,22 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
                     bool x16, bool y16, int lay, const Bnr& bnr) {
   const int cop = Cout <= 32 ? 32 : 64;
+  // bf16 channel-last forward with bf16 source and output: the LDS-DMA
+  // kernel, on x6p's grid (the same BatchNorm partial rows, bit-identical)
+  if (!dgrad && b16 && x16 && y16 && lay == (CL_X | CL_Y) && Cout % 4 == 0 && conv16_dma() &&
+      ((Cin == 32 && cop == 64) || (Cin == 16 && cop == 32))) {
+    const int g = (Cin == 32 ? 256 : 512) * conv_x6_occ16();
+    *parts = g;
+    const uint16_t* x16p = reinterpret_cast<const uint16_t*>(x);
+    uint16_t* y16p = reinterpret_cast<uint16_t*>(y);
+    if (Cin == 32)
+      hipLaunchKernelGGL((conv3x3_fwd_b16dma_kernel<32, 64, 1024>), dim3(g), dim3(1024), 0, s,
+                         x16p, w, bias, sc, sh, y16p, stats, (int)N, Cout, (int)H, (int)W);
+    else
+      hipLaunchKernelGGL((conv3x3_fwd_b16dma_kernel<16, 32, 512>), dim3(g), dim3(512), 0, s,
+                         x16p, w, bias, sc, sh, y16p, stats, (int)N, Cout, (int)H, (int)W);
+    return check_launch("conv3x3_fwd_b16dma");
+  }
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
 #define AINP_X6P(CIV, COV, DG, G, NTV, TRV)                                                      \
   if (dgrad == DG && Cin == CIV && cop == COV) {                                                 \
