@@ -244,7 +244,11 @@ class _ConvStackFn(torch.autograd.Function):
             elif ctx.defer_wgrad:
                 # off the critical path: on the side stream, overlapping the next
                 # (HBM-bound) BatchNorm backward passes
-                with _side_work(gy.device) as sw:
+                # ENC_SIDE2: the encoder's inner weight gradients (all but the
+                # last block's) on the second side stream, so they do not queue
+                # behind the 32 -> 64 one on the first
+                k = 1 if (_enc_side2(ctx.bf16) and bi < nb - 1) else 0
+                with _side_work(gy.device, k=k) as sw:
                     dw, db = ops.conv3x3_wgrad(xin, gy, pro[0], pro[1], bf16=ctx.bf16, **lw)
                     sw.handoff((xin, gy) + tuple(t for t in pro if t is not None), (dw, db))
                     # data parallel: all-reduced from the side stream as soon as
@@ -677,6 +681,16 @@ DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "1") != "0"
 DEFER_EARLY = os.environ.get("AINP_DEFER_EARLY", "1") != "0"
 # (C2 14.65 -> 14.43 / 14.79 -> 14.55 ms/step A/B, profiles/r05o_ab_x6r_apf_side2.txt)
 BLSTM_SIDE2 = os.environ.get("AINP_BLSTM_SIDE2", "1") != "0"
+# Round 6: AINP_ENC_SIDE2 = 0 / 1 / fp32 / bf16: in which configurations the
+# encoder's inner weight gradients use the second side stream (idle by then),
+# so the 16 -> 32 one starts behind its own data gradient instead of behind
+# the 32 -> 64 one, which ends the C2 backward (profiles/r06m_ab_enc_side2.txt:
+# C2 14.82 / 14.86 -> 14.70 / 14.79 ms/step, C3 mixed +-0.06: fp32 only)
+ENC_SIDE2 = os.environ.get("AINP_ENC_SIDE2", "fp32")
+
+
+def _enc_side2(bf16):
+    return ENC_SIDE2 == "1" or ENC_SIDE2 == ("bf16" if bf16 else "fp32")
 
 
 class _Deferred:
@@ -753,15 +767,16 @@ class _side_work:
     at the end of the backward pass (autograd engine callback), before any
     optimizer step can read what the side stream produced."""
 
-    def __init__(self, device, callback=True, after=None):
+    def __init__(self, device, callback=True, after=None, k=0):
         self.device = device
         self.callback = callback
         self.after = after
+        self.k = k
 
     def __enter__(self):
         dev = self.device
         self.main = torch.cuda.current_stream(dev)
-        self.side = _side_stream(dev)
+        self.side = _side_stream(dev, self.k)
         ev = self.after
         if ev is None:
             ev = torch.cuda.Event()
