@@ -411,7 +411,26 @@ constexpr int XPP = XBLK * 1024;                             // padded plane
 constexpr int WROW = 9 * 32 + 16;                            // 304
 }  // namespace cdf
 
-template <int CI, int COP, int NT>
+// s_waitcnt vmcnt(n) for a run-time n (immediates 0..15; larger: 0, which
+// waits for more than needed)
+__device__ __forceinline__ void vm_wait_rt(int n) {
+  switch (n) {
+#define AINP_VMW(K) \
+  case K: asm volatile("s_waitcnt vmcnt(" #K ")" ::: "memory"); break;
+    AINP_VMW(1) AINP_VMW(2) AINP_VMW(3) AINP_VMW(4) AINP_VMW(5) AINP_VMW(6) AINP_VMW(7)
+    AINP_VMW(8) AINP_VMW(9) AINP_VMW(10) AINP_VMW(11) AINP_VMW(12) AINP_VMW(13) AINP_VMW(14)
+    AINP_VMW(15)
+#undef AINP_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// NS = 2: one tile's DMA in flight beside the MFMAs, vmcnt(0) at the top of
+// each tile; NS = 3: two, with the epilogue's stores issued as buffer stores
+// by every lane (masked lanes write past the buffer's end, which drops them)
+// so each wave's vmcnt counts are exact and the top-of-tile wait leaves the
+// younger DMA and the stores in flight
+template <int CI, int COP, int NT, int NS = 2, int NKREG = -1>
 __global__ __launch_bounds__(NT, 1) void conv3x3_fwd_b16dma_kernel(
     const uint16_t* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
@@ -423,10 +442,12 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_fwd_b16dma_kernel(
   constexpr int XBUF = NCK * XPP, WPLANE = COP * WROW;
   constexpr int NBLK = NCK * XBLK;                         // DMA blocks per tile
   constexpr int QMAX = (NBLK + NW - 1) / NW;
-  constexpr int OFF_W = 2 * XBUF, OFF_SS = OFF_W + NCK * WPLANE, OFF_B = OFF_SS + 2 * CI * 4;
+  constexpr int QFULL = NBLK - (QMAX - 1) * NW;            // waves < QFULL issue QMAX
+  constexpr int OFF_W = NS * XBUF, OFF_SS = OFF_W + NCK * WPLANE, OFF_B = OFF_SS + 2 * CI * 4;
   constexpr int LDS = OFF_B + COP * 4;
+  static_assert(NS == 2 || NS == 3, "ring");
   static_assert(2 * XBUF >= TR * 2 * COP * 8, "BatchNorm row sums reuse the halo buffers");
-  // one LDS object: [halo buffer 0 | halo buffer 1 | weights | scale, shift | bias]
+  // one LDS object: [halo buffers 0 .. NS-1 | weights | scale, shift | bias]
   __shared__ __attribute__((aligned(1024))) unsigned char smem[LDS];
   unsigned char* sw = smem + OFF_W;
   float* sss = reinterpret_cast<float*>(smem + OFF_SS);
@@ -449,18 +470,35 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_fwd_b16dma_kernel(
   if (tid < 2 * CI) sss[tid] = pro ? (tid < CI ? in_scale[tid] : in_shift[tid - CI]) : 0.f;
   if (tid < COP) s_b[tid] = (bias && tid < Cout) ? bias[tid] : 0.f;
   __syncthreads();   // weights and constants, before any DMA is in flight
+  // the wave's A (weight) fragments stay in VGPRs for the whole kernel
+  // (NCK x 9 x NIW x 4 VGPRs): per tile only the activations are read from LDS
+  // (the first NKR chunks, NKREG < 0: all; the rest read from LDS per tile.
+  // 32 -> 64: 16 waves reading every weight fragment from LDS measured faster
+  // than 8 waves holding half of them, r06o: 0.264 vs 0.277 ms)
+  constexpr int NKR = NKREG < 0 ? NCK : NKREG;
+  bf16x8c wa[NKR > 0 ? NKR : 1][9][NIW];
+#pragma unroll
+  for (int kc = 0; kc < NKR; ++kc)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int i = 0; i < NIW; ++i)
+        wa[kc][tap][i] = cx6_ld(sw + kc * WPLANE + li * WROW + 16 * lh + (wco + i) * 32 * WROW +
+                                tap * 32);
 
   const int tiles_c = (W + TC - 1) / TC, tiles_r = (H + TR - 1) / TR;
-  const int64_t ntiles = (int64_t)N * tiles_r * tiles_c;
-  auto coords = [&](int64_t t, int& n, int& r0, int& c0) {
-    c0 = (int)(t % tiles_c) * TC;
-    r0 = (int)((t / tiles_c) % tiles_r) * TR;
-    n = (int)(t / ((int64_t)tiles_c * tiles_r));
+  // 32-bit tile arithmetic (the launcher checks N * tiles < 2^31)
+  const int ntiles = N * tiles_r * tiles_c;
+  auto coords = [&](int t, int& n, int& r0, int& c0) {
+    const unsigned q = (unsigned)t / (unsigned)tiles_c;
+    c0 = (int)((unsigned)t - q * (unsigned)tiles_c) * TC;
+    n = (int)(q / (unsigned)tiles_r);
+    r0 = (int)(q - (unsigned)n * (unsigned)tiles_r) * TR;
   };
   // DMA unit k of this wave: block qb = wave + NW k (plane qb / XBLK, block
   // qb % XBLK); lane L -> halo pixel 32 j + L/2, physical half L % 2 holding
   // the logical half (L % 2) ^ (column bit 3)
-  auto issue = [&](int64_t t, unsigned char* buf) {
+  auto issue = [&](int t, unsigned char* buf) {
     int n, r0, c0;
     coords(t, n, r0, c0);
 #pragma unroll
@@ -481,7 +519,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_fwd_b16dma_kernel(
     }
   };
   // BatchNorm+ReLU of the lane's own DMA units, in place
-  auto prologue = [&](int64_t t, unsigned char* buf) {
+  auto prologue = [&](int t, unsigned char* buf) {
     int n, r0, c0;
     coords(t, n, r0, c0);
 #pragma unroll
@@ -515,37 +553,53 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_fwd_b16dma_kernel(
   double bs[NIW], bq[NIW];
 #pragma unroll
   for (int i = 0; i < NIW; ++i) bs[i] = bq[i] = 0.0;
-  int64_t t = blockIdx.x;
-  if (t < ntiles) issue(t, smem);
-  bool cur_a = true;
-  for (; t < ntiles; t += gridDim.x) {
-    unsigned char* sx = cur_a ? smem : smem + XBUF;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's DMAs of tile t
+  // this workgroup's tiles: blockIdx.x + i * gridDim.x, i < cnt
+  const int cnt = (int)blockIdx.x < ntiles ? (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  constexpr int S = NIW * 4;                               // stores per tile per wave
+  const int Q = wave < QFULL ? QMAX : QMAX - 1;            // DMAs per tile per wave
+  const __amdgpu_buffer_rsrc_t ry = __builtin_amdgcn_make_buffer_rsrc(
+      y, (short)0, (int)((int64_t)N * H * W * Cout * 2), 0x00020000);
+#pragma unroll
+  for (int i = 0; i < NS - 1; ++i)
+    if (i < cnt) issue((int)blockIdx.x + i * (int)gridDim.x, smem + i * XBUF);
+  for (int it = 0; it < cnt; ++it) {
+    const int t = (int)blockIdx.x + it * (int)gridDim.x;
+    unsigned char* sx = smem + (it % NS) * XBUF;
+    // this wave's DMAs of tile t retired; NS = 3: what was issued after them
+    // (the next tile's DMA, the last two epilogues' stores) may stay in flight
+    if constexpr (NS == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      const int younger = it == 0 ? (cnt > 1 ? Q : 0)
+                        : it == 1 ? S + (cnt > 2 ? Q : 0)
+                                  : 2 * S + (it + 1 < cnt ? Q : 0);
+      vm_wait_rt(younger);
+    }
     if (pro) prologue(t, sx);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();   // tile t complete in LDS; the other buffer is free
+    __builtin_amdgcn_s_barrier();   // tile t complete in LDS; the oldest buffer is free
     asm volatile("" ::: "memory");
-    const int64_t tn = t + gridDim.x;
-    if (tn < ntiles) issue(tn, cur_a ? smem + XBUF : smem);
+    if (it + NS - 1 < cnt)
+      issue((int)blockIdx.x + (it + NS - 1) * (int)gridDim.x, smem + ((it + NS - 1) % NS) * XBUF);
 #pragma unroll
     for (int i = 0; i < NIW; ++i)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 #pragma unroll
     for (int kc = 0; kc < NCK; ++kc) {
-      const unsigned char* wb0 = sw + kc * WPLANE + li * WROW + 16 * lh;
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int dy = tap / 3, dxx = tap % 3;
         const int hcol = li + dxx;
         const bf16x8c b = cx6_ld(sx + kc * XPP + (wrow + dy) * XROW + hcol * 32 +
                                  16 * (lh ^ ((hcol >> 3) & 1)));
-        bf16x8c a[NIW];
 #pragma unroll
-        for (int i = 0; i < NIW; ++i) a[i] = cx6_ld(wb0 + (wco + i) * 32 * WROW + tap * 32);
-#pragma unroll
-        for (int i = 0; i < NIW; ++i)
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b, acc[i], 0, 0, 0);
+        for (int i = 0; i < NIW; ++i) {
+          const bf16x8c a = kc < NKR ? wa[kc < NKR ? kc : 0][tap][i]
+                                     : cx6_ld(sw + kc * WPLANE + li * WROW + 16 * lh +
+                                              (wco + i) * 32 * WROW + tap * 32);
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
+        }
       }
     }
     // epilogue (conv3x3_x6p_kernel's, Y16 + YL): bias, bf16 rounding,
@@ -570,16 +624,24 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_fwd_b16dma_kernel(
 #pragma unroll
       for (int rb = 0; rb < 4; ++rb) {
         const int co0 = 32 * (wco + i) + 8 * rb + 4 * lh;
-        if (pok && co0 < Cout)
-          cl_st4<true>(reinterpret_cast<float*>(y), ycl + co0, vv[4 * rb], vv[4 * rb + 1],
-                       vv[4 * rb + 2], vv[4 * rb + 3]);
+        if constexpr (NS == 2) {
+          if (pok && co0 < Cout)
+            cl_st4<true>(reinterpret_cast<float*>(y), ycl + co0, vv[4 * rb], vv[4 * rb + 1],
+                         vv[4 * rb + 2], vv[4 * rb + 3]);
+        } else {
+          typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+          u32x2 d;
+          d[0] = cx6_cvt_pk(vv[4 * rb], vv[4 * rb + 1]);
+          d[1] = cx6_cvt_pk(vv[4 * rb + 2], vv[4 * rb + 3]);
+          const int vo = (pok && co0 < Cout) ? (int)((ycl + co0) * 2) : 0x7ffffff0;
+          __builtin_amdgcn_raw_buffer_store_b64(d, ry, vo, 0, 0);
+        }
       }
       if (stats) {
         bs[i] += (double)x6_reduce16(s, li);
         bq[i] += (double)x6_reduce16(q, li);
       }
     }
-    cur_a = !cur_a;
   }
   if (!stats) return;
   // per-row sums -> [row][sum, sum of squares][COP] (the halo buffers are free)
@@ -2599,12 +2661,29 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
     *parts = g;
     const uint16_t* x16p = reinterpret_cast<const uint16_t*>(x);
     uint16_t* y16p = reinterpret_cast<uint16_t*>(y);
-    if (Cin == 32)
-      hipLaunchKernelGGL((conv3x3_fwd_b16dma_kernel<32, 64, 1024>), dim3(g), dim3(1024), 0, s,
-                         x16p, w, bias, sc, sh, y16p, stats, (int)N, Cout, (int)H, (int)W);
-    else
-      hipLaunchKernelGGL((conv3x3_fwd_b16dma_kernel<16, 32, 512>), dim3(g), dim3(512), 0, s,
-                         x16p, w, bias, sc, sh, y16p, stats, (int)N, Cout, (int)H, (int)W);
+    // AINP_CONV16_RING=3: three halo buffers (exact-count buffer stores), A/B;
+    // default two (r06n / r06o: equal or faster, the DMA is not the limit)
+    static const int ring = [] {
+      const char* e = getenv("AINP_CONV16_RING");
+      return (e && e[0] == '3') ? 3 : 2;
+    }();
+    if (N * cdiv(H, cdf::TR) * cdiv(W, cdf::TC) >= ((int64_t)1 << 31))
+      return record_msg("conv3x3_fwd_b16dma: too many tiles");
+    const bool r3 = ring == 3 && N * H * W * Cout * 2 < ((int64_t)1 << 31) - 64;
+#define AINP_CF(CIV, COV, NTV, KR)                                                             \
+  do {                                                                                         \
+    if (r3)                                                                                    \
+      hipLaunchKernelGGL((conv3x3_fwd_b16dma_kernel<CIV, COV, NTV, 3, KR>), dim3(g), dim3(NTV), \
+                         0, s, x16p, w, bias, sc, sh, y16p, stats, (int)N, Cout, (int)H,        \
+                         (int)W);                                                               \
+    else                                                                                       \
+      hipLaunchKernelGGL((conv3x3_fwd_b16dma_kernel<CIV, COV, NTV, 2, KR>), dim3(g), dim3(NTV), \
+                         0, s, x16p, w, bias, sc, sh, y16p, stats, (int)N, Cout, (int)H,        \
+                         (int)W);                                                               \
+  } while (0)
+    if (Cin == 32) AINP_CF(32, 64, 1024, 0);
+    else AINP_CF(16, 32, 512, -1);
+#undef AINP_CF
     return check_launch("conv3x3_fwd_b16dma");
   }
   // two workgroups per CU where the LDS allows it (one 16-channel chunk)
