@@ -449,22 +449,28 @@ def _cnn_step_work(B=32, F=257, T=334, H=128, bf16=False):
     big = 64 * P
     y = 2.0 if bf16 else 4.0            # pre-BN y storage
     gy = 2.0 if bf16 else 4.0           # BN-backward output storage
+    # conv kernels: work PER LAUNCH (a template instance serves the encoder's
+    # and the decoder's layer of its shape as separate table rows, or one row
+    # of two launches): in_step_table multiplies by the row's launches per step
     return [
         # fp32: layer-0 projection + backward pair + the output projection's
         # dh and dW (proj_bwd_x6)
         ("gemm_x6r_kernel", "mfma", 3 * l0 + 2 * proj),
         ("gemm_bf16nt_256_multi_kernel", "mfma", 2 * l0),  # bf16 dX + dW pair
         ("gemm_bf16nt_256_kernel", "mfma", l0),           # bf16 projection
-        ("conv3x3_x6p_kernel<32, 64", "mfma", conv(32, 64)),
-        ("conv3x3_x6_kernel<64, 32", "mfma", conv(64, 32)),
-        ("conv3x3_dgrad_b16dma_kernel", "mfma", conv(64, 32)),   # bf16 64 -> 32 dgrad
-        ("conv3x3_wgrad_x6<64", "mfma", conv(32, 64)),
-        ("conv3x3_x6p_kernel<16, 32, false", "mfma", 2 * conv(16, 32)),
-        ("conv3x3_x6q_kernel<32, true", "mfma", 2 * conv(16, 32)),
-        ("conv3x3_wgrad_x6s<16, 32", "mfma", 2 * conv(16, 32)),
-        ("conv3x3_wgrad_x6s<32, 16", "mfma", conv(32, 16)),
-        ("conv3x3_x6q_kernel<32, false", "mfma", conv(32, 16)),
-        ("conv3x3_x6p_kernel<16, 32, true", "mfma", conv(32, 16)),
+        ("conv3x3_x6p_kernel<32, 64", "mfma/launch", conv(32, 64)),
+        ("conv3x3_fwd_b16dma_kernel<32, 64", "mfma/launch", conv(32, 64)),   # round 6
+        ("conv3x3_fwd_b16dma_kernel<16, 32", "mfma/launch", conv(16, 32)),   # round 6
+        ("conv3x3_x6_kernel<64, 32", "mfma/launch", conv(64, 32)),
+        ("conv3x3_dgrad_b16dma_kernel", "mfma/launch", conv(64, 32)),   # bf16 64 -> 32 dgrad
+        ("conv3x3_wgrad_x6<64", "mfma/launch", conv(32, 64)),
+        ("conv3x3_wgrad_b16dma_kernel", "mfma/launch", conv(32, 64)),   # round 6
+        ("conv3x3_x6p_kernel<16, 32, false", "mfma/launch", conv(16, 32)),
+        ("conv3x3_x6q_kernel<32, true", "mfma/launch", conv(16, 32)),
+        ("conv3x3_wgrad_x6s<16, 32", "mfma/launch", conv(16, 32)),
+        ("conv3x3_wgrad_x6s<32, 16", "mfma/launch", conv(32, 16)),
+        ("conv3x3_x6q_kernel<32, false", "mfma/launch", conv(32, 16)),
+        ("conv3x3_x6p_kernel<16, 32, true", "mfma/launch", conv(32, 16)),
         # channel-last BatchNorm + ReLU backward of the 16/32-channel layers:
         # reduce reads y and dy, apply reads both and writes gy
         # (one instance per channel count: encoder + decoder layer each)
@@ -517,6 +523,8 @@ def in_step_table(key, bf16, top=8, families=None):
              "share_of_kernel_time": round(float(r["TotalDurationNs"]) / total, 4)}
         for sub, kind, amount in work:
             if sub in r["Name"]:
+                if kind == "mfma/launch":   # per-launch work x this row's launches per step
+                    kind, amount = "mfma", amount * int(r["Calls"]) / div
                 if kind == "mfma":
                     tf = amount / (ms / 1e3) / 1e12
                     peak = executed_peak(bf16)

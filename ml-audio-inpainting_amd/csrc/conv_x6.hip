@@ -244,7 +244,12 @@ __device__ __forceinline__ void glds16_asm(const void* gsrc, const unsigned char
 }
 
 
-__global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
+// WREG (round 6): the wave's 36 weight fragments held in VGPRs (144) for the
+// whole kernel instead of re-read from LDS per tile -- half the LDS read
+// traffic of the MFMA loop (the LDS, 162 KB, allows one workgroup per CU
+// either way)
+template <bool WREG>
+__global__ __launch_bounds__(cdd::NT, WREG ? 1 : 2) void conv3x3_dgrad_b16dma_kernel(
     const uint16_t* __restrict__ gy, const float* __restrict__ w, float* __restrict__ dx,
     double* __restrict__ stats, Bnr bnr, int N, int H, int W, int ntr, int ntc, int64_t ntiles) {
   using namespace cdd;
@@ -309,6 +314,15 @@ __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
   // fused BatchNorm-backward reduce (stats != nullptr): lane li of half lh
   // ends up holding channel row li >> 1's sums (x6p's butterfly)
   double bs = 0.0, bq = 0.0;
+  bf16x8c wa[WREG ? NCK : 1][WREG ? 9 : 1];
+  if constexpr (WREG) {
+    __syncthreads();   // the staged weights
+#pragma unroll
+    for (int kc = 0; kc < NCK; ++kc)
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
+        wa[kc][tap] = cx6_ld(sw + kc * WPLANE + li * WROW + tap * 32 + 16 * lh);
+  }
   int64_t t = blockIdx.x;
   if (t < ntiles) issue(t, sxa, sya);
   bool cur_a = true;
@@ -329,7 +343,8 @@ __global__ __launch_bounds__(cdd::NT, 2) void conv3x3_dgrad_b16dma_kernel(
       for (int tap = 0; tap < 9; ++tap) {
         const int dy = tap / 3, dxx = tap % 3;
         const int hcol = li + dxx;
-        const bf16x8c a = cx6_ld(sw + kc * WPLANE + li * WROW + tap * 32 + 16 * lh);
+        const bf16x8c a = WREG ? wa[WREG ? kc : 0][WREG ? tap : 0]
+                               : cx6_ld(sw + kc * WPLANE + li * WROW + tap * 32 + 16 * lh);
         const bf16x8c b = cx6_ld(sx + kc * XPP + (wave + dy) * XROW + hcol * 32 +
                                  16 * (lh ^ ((hcol >> 3) & 1)));
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
@@ -1080,9 +1095,19 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
     const int64_t nt = N * (int64_t)ntr * ntc;
     const int grid = (int)(nt < 256 ? nt : 256);   // one persistent workgroup per CU
     *parts = grid;
-    hipLaunchKernelGGL(conv3x3_dgrad_b16dma_kernel, dim3(grid), dim3(cdd::NT), 0, s,
-                       reinterpret_cast<const uint16_t*>(x), w, y, stats, bnr, (int)N, (int)H,
-                       (int)W, ntr, ntc, nt);
+    // AINP_DGRAD16_WREG=0: weight fragments re-read from LDS per tile (A/B)
+    static const bool wreg = [] {
+      const char* e = getenv("AINP_DGRAD16_WREG");
+      return !(e && e[0] == '0');
+    }();
+    if (wreg)
+      hipLaunchKernelGGL(conv3x3_dgrad_b16dma_kernel<true>, dim3(grid), dim3(cdd::NT), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), w, y, stats, bnr, (int)N, (int)H,
+                         (int)W, ntr, ntc, nt);
+    else
+      hipLaunchKernelGGL(conv3x3_dgrad_b16dma_kernel<false>, dim3(grid), dim3(cdd::NT), 0, s,
+                         reinterpret_cast<const uint16_t*>(x), w, y, stats, bnr, (int)N, (int)H,
+                         (int)W, ntr, ntc, nt);
     return check_launch("conv3x3_dgrad_b16dma");
   }
   *parts = dg8 ? N * cdiv(H, 8) * cdiv(W, cx6::TC) : N * cdiv(H, cx6::TR) * cdiv(W, cx6::TC);
