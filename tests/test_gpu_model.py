@@ -470,10 +470,18 @@ def test_bf16_gy_storage_is_bit_identical(monkeypatch):
     # the fp32-storage step is bit-reproducible (same inputs, same seed) ...
     rep = [k for k, a, c in zip(names, runs[0], runs[2]) if not torch.equal(a, c)]
     assert not rep, f"bf16 step not bit-reproducible: {rep}"
-    # ... and bf16 storage of gy does not change a bit of it
+    # ... and bf16 storage of gy does not change a bit of it, except the
+    # 32 -> 64 weight gradient: with a bf16 dy it runs on the LDS-DMA kernel
+    # (round 6, conv3x3_wgrad_b16dma_kernel) -- the same staged bf16 operands,
+    # another fixed fp32 summation order -- checked at 1e-5
+    dma = {"encoder.6.weight"}
     diff = [k for k, a, b in zip(names, runs[0], runs[1])
-            if k not in BN_FED_BIASES and not torch.equal(a, b)]
+            if k not in BN_FED_BIASES and k not in dma and not torch.equal(a, b)]
     assert not diff, f"bf16 gy storage changed: {diff}"
+    for k, a, b in zip(names, runs[0], runs[1]):
+        if k in dma:
+            e = float((a.double() - b.double()).norm() / b.double().norm())
+            assert e < 1e-5, (k, e)
     grads = dict(zip(names, runs[1]))
     for k in BN_FED_BIASES:
         if k in grads:
