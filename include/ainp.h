@@ -362,6 +362,15 @@ int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
 #define AINP_CONV_XCL 32
 #define AINP_CONV_YCL 64
 #define AINP_CONV_GCL 128
+/* Round 6, data gradient only (not with AINP_CONV_YCL): dx written
+ * [Cin][H][N][W] -- for the decoder input, the [C*F, N*T] k-major operand of
+ * the fp32 output projection's backward GEMMs (nn.Linear + view/permute of
+ * models/CNNBLSTM/model.py:51-53,79-80), which otherwise needs a transposing
+ * copy of the whole gradient.  Served for the 32 -> 16 channel data gradient
+ * (dy 32 channels, dx 16) only; ainp_conv3x3_dgrad_cfnt_ok says when
+ * (host-only), and ainp_conv3x3_dgrad_ex refuses it otherwise. */
+#define AINP_CONV_YCFNT 256
+int ainp_conv3x3_dgrad_cfnt_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
 int ainp_conv3x3_cl_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
 int ainp_conv3x3_fwd_ex(const float* x, const float* w, const float* bias,
                         const float* in_scale, const float* in_shift, float* y,

@@ -153,6 +153,9 @@ class _ConvStackFn(torch.autograd.Function):
         ctx.spec = spec
         ctx.lays = lays
         ctx.bf16 = bf16
+        # the stack input is the fp32 output projection's result, whose x6r
+        # backward reads its gradient as [C*F, N*T]: dx written that way
+        ctx.gx_cfnt = bool(getattr(x, "_ainp_cfnt_grad", False))
         # (mode, sink): mode False / True (side stream now) / "queue" (released at
         # the first BPTT); sink = the data-parallel GradAllReducer or None
         ctx.defer_wgrad, ctx.sink = defer_wgrad if isinstance(defer_wgrad, tuple) \
@@ -270,12 +273,23 @@ class _ConvStackFn(torch.autograd.Function):
                 psc, psh, psv = ctx.affine[bi - 1]
                 g, pre_sums = ops.conv3x3_dgrad_bnr(gy, w, ys[bi - 1], psc, psh, psv,
                                                     bf16=ctx.bf16, xcl=ycl)
+            elif (bi == 0 and ctx.needs_input_grad[0] and ctx.gx_cfnt and not xcl
+                  and ops.dgrad_cfnt_ok(N, w.shape[1], w.shape[0], H, W)):
+                # round 6: dx as [C, F, N, T] (an [N, C, F, T] view of it) --
+                # _ProjFn._backward_x6's operand without the transposing copy
+                gx = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16, xcl=ycl, cfnt=True)
             elif bi > 0 or ctx.needs_input_grad[0]:
                 # dx in this conv's input layout (the previous block's y)
                 g = ops.conv3x3_dgrad(gy, w, bf16=ctx.bf16, xcl=ycl, ycl=xcl)
                 if bi == 0:
                     gx = g
         return (gx, None, None, None, None, None, None, None, *grads)
+
+
+# Round 6: the decoder's input gradient written [C, F, N, T] by its first
+# conv's data gradient, the layout the fp32 projection backward reads
+# (AINP_PROJ_CFNT=0: NCHW, transposed by a copy there)
+PROJ_CFNT = os.environ.get("AINP_PROJ_CFNT", "1") != "0"
 
 
 # Round 5: a data gradient feeding a BatchNorm+ReLU with channel-last
@@ -843,6 +857,9 @@ class _ProjFn(torch.autograd.Function):
         ctx.defer_wgrad = defer_wgrad
         ctx.sink = sink
         ctx.param_objs = (w, b)
+        # the consumer's data gradient may hand back [C, F, N, T] storage (see
+        # _ConvStackFn.backward, AINP_PROJ_CFNT=0: NCHW and the copy below)
+        out._ainp_cfnt_grad = PROJ_CFNT and _ProjFn._x6(bf16, N * T, NO, K)
         return out
 
     @staticmethod
@@ -851,9 +868,9 @@ class _ProjFn(torch.autograd.Function):
         N, C, F, T = ctx.shape
         NO = C * F
         K = h.shape[2]
-        g = g.contiguous()
-        if not ctx.bf16 and not ops.GEMM_EXACT and ops.proj_bwd_x6_eligible(N * T, NO, K):
+        if _ProjFn._x6(ctx.bf16, N * T, NO, K):
             return _ProjFn._backward_x6(ctx, g, h, w)
+        g = g.contiguous()
         # dh_n[t][k] = sum_col g_n[col][t] w[col][k]: only 6 output tiles per
         # example, so the col sum (K = C*F) is split over S pointer batches into
         # slabs (4x the workgroups) and combined in fixed order
@@ -891,6 +908,10 @@ class _ProjFn(torch.autograd.Function):
         return dh, dw, db, None, None, None, None, None
 
     @staticmethod
+    def _x6(bf16, NT, NO, K):
+        return not bf16 and not ops.GEMM_EXACT and ops.proj_bwd_x6_eligible(NT, NO, K)
+
+    @staticmethod
     def _backward_x6(ctx, g, h, w):
         """fp32: both gradients on the x6r MFMA tile (ops.proj_bwd_x6) from the
         gradient permuted once to [C*F, N*T] -- every column of the reduction
@@ -898,7 +919,11 @@ class _ProjFn(torch.autograd.Function):
         batch per example."""
         N, C, F, T = ctx.shape
         NO, K = C * F, h.shape[2]
-        gp = g.view(N, NO, T).transpose(0, 1).contiguous().view(NO, N * T)
+        gq = g.permute(1, 2, 0, 3)
+        if gq.is_contiguous():   # [C, F, N, T] storage (the decoder's dgrad wrote it)
+            gp = gq.view(NO, N * T)
+        else:
+            gp = g.contiguous().view(N, NO, T).transpose(0, 1).contiguous().view(NO, N * T)
         h2 = h.view(N * T, K)
         dh = torch.empty(N, T, K, device=g.device, dtype=torch.float32)
         dw = torch.empty(NO, K, device=g.device)

@@ -201,6 +201,7 @@ BN_Y16 = 2             # AINP_BN_Y16: the pre-BN input y in bf16 storage
 CONV_XCL = 32          # AINP_CONV_XCL: input channel-last (fwd x, dgrad dy, wgrad x)
 CONV_YCL = 64          # AINP_CONV_YCL: output channel-last (fwd y, dgrad dx)
 CONV_GCL = 128         # AINP_CONV_GCL: the weight gradient's dy channel-last
+CONV_YCFNT = 256       # AINP_CONV_YCFNT: the data gradient's dx as [C][H][N][W]
 BN_CL = 4              # AINP_BN_CL: g / y / gy channel-last
 BN_G16 = 8             # AINP_BN_G16: g in bf16 storage (with BN_CL)
 
@@ -828,20 +829,34 @@ def _dy_flags(dy, bf16):
     return CONV_BF16 if bf16 else 0
 
 
-def conv3x3_dgrad(dy, w, bf16=False, xcl=False, ycl=False):
+def conv3x3_dgrad(dy, w, bf16=False, xcl=False, ycl=False, cfnt=False):
     """dy fp32, or bf16 storage with bf16=True (AINP_CONV_DY16).  xcl / ycl:
-    dy given / dx returned channel-last [N, H, W, C]."""
+    dy given / dx returned channel-last [N, H, W, C].  cfnt (AINP_CONV_YCFNT,
+    see dgrad_cfnt_ok): dx written [C, H, N, W], returned as its [N, C, H, W]
+    view (permute(2, 0, 1, 3) of that buffer)."""
     _req(dy, "dy", None); _req(w, "w")
     if xcl:
         N, H, W, Cout = dy.shape
     else:
         N, Cout, H, W = dy.shape
     Cin = w.shape[1]
+    if cfnt:
+        if ycl:
+            raise ValueError("conv3x3_dgrad: cfnt and ycl are exclusive")
+        buf = torch.empty((Cin, H, N, W), device=dy.device, dtype=torch.float32)
+        _T.conv3x3_dgrad(dy, w, buf, _dy_flags(dy, bf16) | (CONV_XCL if xcl else 0) | CONV_YCFNT)
+        return buf.permute(2, 0, 1, 3)
     dx = torch.empty((N, H, W, Cin) if ycl else (N, Cin, H, W), device=dy.device,
                      dtype=torch.float32)
     _T.conv3x3_dgrad(dy, w, dx, _dy_flags(dy, bf16) | (CONV_XCL if xcl else 0)
                      | (CONV_YCL if ycl else 0))
     return dx
+
+
+def dgrad_cfnt_ok(N, Cin, Cout, H, W) -> bool:
+    """ainp_conv3x3_dgrad_cfnt_ok: the data gradient of Conv2d(Cin, Cout) can
+    write dx as [Cin, H, N, W] (conv3x3_dgrad(cfnt=True))."""
+    return bool(_lib.lib.ainp_conv3x3_dgrad_cfnt_ok(N, Cin, Cout, H, W))
 
 
 def conv3x3_dgrad_bnr(dy, w, y, scale, shift, save, bf16=False, xcl=False):

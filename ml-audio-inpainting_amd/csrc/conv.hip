@@ -649,8 +649,20 @@ __device__ __forceinline__ void stage_small_tile(const float* __restrict__ x,
                                                  float* sx, int n, int f0, int t0, int H, int W) {
   constexpr int LR = CV_TT + 2, ROWS = CV_FT + 2, E = CIN * ROWS * LR;
   constexpr int PER = (E + NT - 1) / NT;
-  constexpr int BATCH = PER < 16 ? PER : 16;      // loads in flight per thread
+  // loads in flight per thread: the whole tile in one round trip up to 32
+  constexpr int BATCH = PER <= 32 ? PER : 16;
   const int64_t HW = (int64_t)H * W;
+  // a thread's channel is the same for all its elements when CIN = 1 or, channel-
+  // last, when NT is a multiple of CIN: the prologue constants are then loaded
+  // once (round 6: per-element loads of in_scale[c] / in_shift[c] cost the
+  // 16 -> 1 forward 40 % of its time)
+  constexpr bool CFIX = CIN == 1 || (XL && NT % CIN == 0);
+  float fsc = 1.f, fsh = 0.f;
+  if (PRO && CFIX) {
+    const int c = CIN == 1 ? 0 : (int)(threadIdx.x % CIN);
+    fsc = in_scale[c];
+    fsh = in_shift[c];
+  }
   auto decode = [&](int e, int& c, int& rr, int& cc) {
     if constexpr (XL) {
       c = e % CIN;
@@ -686,7 +698,8 @@ __device__ __forceinline__ void stage_small_tile(const float* __restrict__ x,
       if (PRO) {
         const int f = f0 - 1 + rr, t = t0 - 1 + cc;
         // BatchNorm+ReLU of the previous layer; zero padding stays zero
-        if (f >= 0 && f < H && t >= 0 && t < W) a = fmaxf(fmaf(a, in_scale[c], in_shift[c]), 0.f);
+        if (f >= 0 && f < H && t >= 0 && t < W)
+          a = fmaxf(fmaf(a, CFIX ? fsc : in_scale[c], CFIX ? fsh : in_shift[c]), 0.f);
       }
       sx[(c * ROWS + rr) * LR + cc] = a;
     }
@@ -1297,6 +1310,7 @@ int64_t conv_x6_stat_rows(bool dgrad, int Cin, int Cout, int64_t N, int64_t H, i
                           bool b16);
 bool conv_x6_dgrad16_ok(int Cin, int Cout, int64_t H, int64_t W);
 bool conv_x6_fwd16_ok(int Cin, int Cout, int64_t H, int64_t W);
+bool conv_x6_dgrad_cfnt_ok(int Cin, int Cout, int64_t N, int64_t H, int64_t W);
 int conv_wgrad_x6_launch(const float* x, const float* sc, const float* sh, const float* dy,
                          float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
                          int ci0, int cp, int grid, hipStream_t s, bool b16, bool g16, bool x16,
@@ -1419,6 +1433,9 @@ static bool conv_fwd_flags_ok(int flags) {
 // data / weight gradients: dy may be bf16 storage (with the bf16 arithmetic);
 // data gradient: dy / dx channel-last; weight gradient: x / dy channel-last
 static bool conv_grad_flags_ok(int flags, bool wgrad) {
+  // data gradient: dx [C][H][N][W] (AINP_CONV_YCFNT) instead of channel-last
+  if ((flags & AINP_CONV_YCFNT) && (wgrad || (flags & AINP_CONV_YCL))) return false;
+  if (!wgrad) flags &= ~AINP_CONV_YCFNT;
   const int cl = flags & (wgrad ? (AINP_CONV_XCL | AINP_CONV_GCL) : (AINP_CONV_XCL | AINP_CONV_YCL));
   flags &= ~cl;
   const int extra = AINP_CONV_DY16 | (wgrad ? AINP_CONV_X16 : 0);
@@ -1429,7 +1446,7 @@ static bool conv_grad_flags_ok(int flags, bool wgrad) {
 // bit 2 the weight gradient's dy)
 static int conv_lay(int flags) {
   return ((flags & AINP_CONV_XCL) ? 1 : 0) | ((flags & AINP_CONV_YCL) ? 2 : 0) |
-         ((flags & AINP_CONV_GCL) ? 4 : 0);
+         ((flags & AINP_CONV_GCL) ? 4 : 0) | ((flags & AINP_CONV_YCFNT) ? 8 : 0);
 }
 
 extern "C" int ainp_conv3x3_fwd_ex(const float* x, const float* w,
@@ -1466,12 +1483,20 @@ extern "C" int ainp_conv3x3_dgrad_ex(const float* dy, const float* w, float* dx,
   if (!dy || !w || !dx || N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 ||
       N > 65535 || !conv_grad_flags_ok(flags, false))
     return record_msg("ainp_conv3x3_dgrad: bad argument");
+  if ((flags & AINP_CONV_YCFNT) && ainp_conv3x3_dgrad_cfnt_ok(N, Cin, Cout, H, W) != 1)
+    return record_msg("ainp_conv3x3_dgrad: AINP_CONV_YCFNT serves the 32 -> 16 channel data "
+                      "gradient only (see ainp_conv3x3_dgrad_cfnt_ok)");
   if (N == 0) return AINP_OK;
   // conv over dy (Cout channels) producing Cin channels, flipped weights
   return conv_fwd_dispatch<true>(dy, w, nullptr, nullptr, nullptr, dx, nullptr,
                                  N, Cout, Cin, H, W, as_stream(stream),
                                  (flags & AINP_CONV_BF16) != 0, (flags & AINP_CONV_DY16) != 0,
                                  false, conv_lay(flags));
+}
+
+extern "C" int ainp_conv3x3_dgrad_cfnt_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
+  if (N < 0 || Cin < 1 || Cout < 1 || H < 1 || W < 1 || conv_exact_env()) return 0;
+  return conv_x6_dgrad_cfnt_ok(Cout, Cin, N, H, W) ? 1 : 0;
 }
 
 extern "C" int ainp_conv3x3_dgrad(const float* dy, const float* w, float* dx,

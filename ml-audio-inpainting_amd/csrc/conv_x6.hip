@@ -47,6 +47,10 @@ typedef __bf16 bf16x8c __attribute__((ext_vector_type(8)));
 
 // activation layouts of a launch (bitmask): input / output / dy channel-last
 constexpr int CL_X = 1, CL_Y = 2, CL_G = 4;
+// round 6: a data gradient's dx written [C][H][N][W] (AINP_CONV_YCFNT) -- the
+// [C*F, N*T] operand of the fp32 output projection's backward GEMMs, so the
+// transposing copy of the decoder input gradient disappears (x6q only)
+constexpr int CL_CF = 8;
 
 __device__ __forceinline__ int wx6_clamp(int v, int lo, int hi) {
   return v < lo ? lo : (v > hi ? hi : v);
@@ -1045,6 +1049,14 @@ bool conv_x6_dgrad16_ok(int Cin, int Cout, int64_t H, int64_t W) {
          (int64_t)Cin * H * W * 4 < ((int64_t)1 << 31);   // tiled, 8-row tiles
 }
 
+// 1 if conv_x6_launch(dgrad = true, lay with CL_CF) serves this (dy channels,
+// dx channels) pair: the persistent 32 -> 16 data gradient (x6q)
+bool conv_x6_dgrad_cfnt_ok(int Cin, int Cout, int64_t N, int64_t H, int64_t W) {
+  static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
+  return !tiled_env && Cin == 32 && Cout == 16 && N * H * W * 16 < ((int64_t)1 << 40) &&
+         (int64_t)Cin * H * W * 4 < ((int64_t)1 << 31);
+}
+
 // 1 if conv_x6_launch(dgrad = false, b16) serves this pair on a persistent
 // kernel, the only forwards with bf16-storage input / output (x16 / y16)
 bool conv_x6_fwd16_ok(int Cin, int Cout, int64_t H, int64_t W) {
@@ -1076,13 +1088,14 @@ int conv_x6_launch(bool dgrad, const float* x, const float* w, const float* bias
   const bool fused = bnr.y != nullptr;
   // (dx of at most 32 channels: the fused instances)
   if (fused && !(dgrad && stats && (lay & CL_Y) && !bias && Cout <= 32)) return 2;
-  if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W, b16) == 0) return 1;
+  if (conv_x6_stat_rows(dgrad, Cin, Cout, N, H, W, b16) == 0) return (lay & CL_CF) ? 2 : 1;
   static const bool tiled_env = getenv("AINP_CONV_X6_TILED") != nullptr;
   if (!tiled_env && (int64_t)(Cin > Cout ? Cin : Cout) * H * W * 4 < ((int64_t)1 << 31)) {
     const int rc = conv_x6p_launch(dgrad, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
                                    parts, b16, x16, y16, lay, bnr);
     if (rc != 1) return rc;
   }
+  if (lay & CL_CF) return 2;   // only the persistent x6q writes [C][H][N][W]
   if ((int64_t)Cin * H * W * 4 >= ((int64_t)1 << 31)) return 1;   // 32-bit buffer offsets
   // the data gradient without forward statistics: 8-row tiles (channel-last,
   // bf16 dy, the fused reduce)
@@ -2344,7 +2357,8 @@ template <int CI, bool DGRAD, int NP, bool G16 = false, bool Y16 = false, bool X
 __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
-    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W, Bnr bnr) {
+    float* __restrict__ y, double* __restrict__ stats, int N, int Cout, int H, int W, Bnr bnr,
+    int ycf) {
   using cxp::CK;
   using cxp::HC;
   using cxp::TC;
@@ -2487,7 +2501,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
     int n, r0, c0;
     tile_coords(tile, n, r0, c0);
     const int row = r0 + wave;
-    const int64_t yo = (int64_t)n * Cout * HW + (int64_t)row * W;
+    // NCHW, or (ycf) [C][H][N][W]: the same contiguous rows of W, other strides
+    const int64_t yo = ycf ? ((int64_t)row * N + n) * W : (int64_t)n * Cout * HW + (int64_t)row * W;
+    const int64_t cs = ycf ? (int64_t)N * HW : HW;
     float s[4] = {0.f, 0.f, 0.f, 0.f}, q[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -2502,9 +2518,9 @@ __global__ __launch_bounds__(512, 2) void conv3x3_x6q_kernel(
         if constexpr (Y16) v = y16_round(v);
         if constexpr (!YL) {
           if constexpr (Y16) {
-            if (ok) y16_st(y, yo + (int64_t)co * HW + col, v);
+            if (ok) y16_st(y, yo + (int64_t)co * cs + col, v);
           } else {
-            if (ok) y[yo + (int64_t)co * HW + col] = v;
+            if (ok) y[yo + (int64_t)co * cs + col] = v;
           }
         }
         vv[r] = v;
@@ -2653,11 +2669,12 @@ template <bool DG>
 static void x6q_go(dim3 g, hipStream_t s, bool b16, bool x16, bool y16, int lay, const float* x,
                    const float* w, const float* bias, const float* sc, const float* sh, float* y,
                    double* stats, int N, int Cout, int H, int W, const Bnr& bnr) {
+  const int ycf = (lay & CL_CF) ? 1 : 0;
   cl_dispatch(lay, [&](auto xl, auto yl) {
     constexpr bool XL = decltype(xl)::value, YL = decltype(yl)::value;
 #define AINP_X6QK(NPV, GV, YV)                                                                \
   hipLaunchKernelGGL((conv3x3_x6q_kernel<32, DG, NPV, GV, YV, XL, YL>), g, dim3(512), 0, s, x, \
-                     w, bias, sc, sh, y, stats, N, Cout, H, W, bnr)
+                     w, bias, sc, sh, y, stats, N, Cout, H, W, bnr, ycf)
     if (!b16) {
       AINP_X6QK(3, false, false);
     } else if constexpr (DG) {
@@ -2678,6 +2695,8 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
                     int Cout, int64_t H, int64_t W, hipStream_t s, int64_t* parts, bool b16,
                     bool x16, bool y16, int lay, const Bnr& bnr) {
   const int cop = Cout <= 32 ? 32 : 64;
+  if ((lay & CL_CF) && !(dgrad && Cin == 32 && Cout == 16 && !(lay & CL_Y)))
+    return 2;   // [C][H][N][W] dx: the 32 -> 16 data gradient (x6q) only
   // bf16 channel-last forward with bf16 source and output: the LDS-DMA
   // kernel, on x6p's grid (the same BatchNorm partial rows, bit-identical)
   if (!dgrad && b16 && x16 && y16 && lay == (CL_X | CL_Y) && Cout % 4 == 0 && conv16_dma() &&

@@ -109,9 +109,19 @@ def test_dy16_routing_query():
         assert q(32, cin, cout, 257, 334) == 1, (cin, cout)
     for cin, cout in ((2, 16), (16, 2), (64, 32), (8, 24), (16, 16)):
         assert q(32, cin, cout, 257, 334) == 0, (cin, cout)
-    # an unknown flag bit is refused before any launch
+    # an unknown flag bit is refused before any launch (256 = AINP_CONV_YCFNT:
+    # data gradients only)
     rc = _lib.lib.ainp_conv3x3_fwd_ex(1, 1, None, None, None, 1, None, 1, 16, 32, 8, 8, 256, None)
     assert rc == -1
+    # round 6: dx as [C][H][N][W] -- the decoder's 16 -> 32 conv (dy 32, dx 16) only
+    q = _lib.lib.ainp_conv3x3_dgrad_cfnt_ok
+    assert q(32, 16, 32, 257, 334) == 1
+    for cin, cout in ((32, 16), (32, 64), (1, 16), (16, 1), (16, 64)):
+        assert q(32, cin, cout, 257, 334) == 0, (cin, cout)
+    rc = _lib.lib.ainp_conv3x3_dgrad_ex(1, 1, 1, None, 1, 32, 16, 8, 8, 256, None)
+    assert rc == -1 and b"YCFNT" in _lib.lib.ainp_last_error()
+    rc = _lib.lib.ainp_conv3x3_dgrad_ex(1, 1, 1, None, 1, 16, 32, 8, 8, 256 | 64, None)
+    assert rc == -1 and b"bad argument" in _lib.lib.ainp_last_error()
 
 
 def test_ops_refuse_cpu_tensors():
@@ -125,7 +135,7 @@ HOST_ONLY = {"ainp_abi_version", "ainp_build_target", "ainp_last_error", "ainp_r
              "ainp_flac_info", "ainp_flac_decode", "ainp_flac_encode_bound", "ainp_flac_encode",
              "ainp_l1_pow10_loss_slots", "ainp_range_push", "ainp_range_pop", "ainp_mark",
              "ainp_conv16_set_variant", "ainp_conv3x3_dy16_ok", "ainp_conv3x3_io16_ok",
-             "ainp_conv3x3_cl_ok"}
+             "ainp_conv3x3_cl_ok", "ainp_conv3x3_dgrad_cfnt_ok"}
 
 
 def test_torch_library_registers_every_gpu_entry_point():

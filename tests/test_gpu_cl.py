@@ -89,6 +89,32 @@ def test_cl_dgrad_wgrad_bit_identical(cin, cout, N, H, W, bf16):
             assert torch.equal(dw, dw0) and torch.equal(db, db0), (d.dtype, xcl, gcl)
 
 
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("N,H,W", SHAPES + [(3, 20, 70)])
+def test_dgrad_cfnt_bit_identical(N, H, W, bf16):
+    """Round 6, AINP_CONV_YCFNT: the decoder's 16 -> 32 conv data gradient
+    writing dx as [C, F, N, T] (the fp32 projection backward's operand) --
+    the same values as the NCHW launch, bit for bit, from NCHW and channel-last
+    dy; every element written (NaN-filled buffer)."""
+    from ainp import ops
+    assert ops.dgrad_cfnt_ok(N, 16, 32, H, W)
+    x, dy, w, b, sc, sh = _data(N, 16, 32, H, W, 11)
+    dys = [dy] + ([dy.to(torch.bfloat16)] if bf16 else [])
+    for d in dys:
+        dx0 = ops.conv3x3_dgrad(d, w, bf16=bf16)
+        for xcl in (False, True):
+            dx = ops.conv3x3_dgrad(_cl(d) if xcl else d, w, bf16=bf16, xcl=xcl, cfnt=True)
+            assert dx.shape == dx0.shape and dx.permute(1, 2, 0, 3).is_contiguous()
+            assert torch.equal(dx, dx0), (d.dtype, xcl)
+    buf = torch.full((16, H, N, W), float("nan"), device=DEV)
+    flags = ops.CONV_XCL | ops.CONV_YCFNT
+    ops._T.conv3x3_dgrad(_cl(dy), w, buf, flags)
+    assert torch.equal(buf.permute(2, 0, 1, 3), ops.conv3x3_dgrad(dy, w))
+    with pytest.raises(RuntimeError, match="YCFNT"):
+        ops.conv3x3_dgrad(_cl(torch.randn(N, 16, H, W, device=DEV)), w.transpose(0, 1).contiguous(),
+                          xcl=True, cfnt=True)
+
+
 @pytest.mark.parametrize("N,H,W", SHAPES)
 @pytest.mark.parametrize("pro", [True, False])
 def test_cl_small_channel_convs(N, H, W, pro):
