@@ -637,8 +637,10 @@ def g256_splits(shapes, max_split=16):
     x6r_splits does for the x6r tile.  Returns ((S, kc), ...)."""
     def opts(M, N, K):
         out = []
+        # 64-deep K-tiles where K allows (gemm16.hip tile256b needs 64 | kc)
+        g = 64 if K % 64 == 0 else 32
         for S in range(1, max_split + 1):
-            kc = -(-K // S // 32) * 32 if S > 1 else K
+            kc = -(-K // S // g) * g if S > 1 else K
             if S > 1 and -(-K // kc) != S:
                 continue
             out.append((S, kc))

@@ -1144,6 +1144,294 @@ __global__ __launch_bounds__(256) void conv3x3_strip_wgrad_cl(
   }
 }
 
+// Round 6: the 16 -> 1 forward (decoder.6, models/CNNBLSTM/model.py:59-60)
+// on row strips, its 16-channel input channel-last.  conv3x3_small_fwd stages
+// a 16 x 10 x 50 halo per 8 x 48 tile (32 KB of LDS: four workgroups per CU)
+// and reads it back 144 times per pixel: 106 us at the C2 shape (1.7 TB/s of
+// its 176 MB input).  Here a wave walks a strip of R1_RS rows x R1_TW output
+// columns.  Lane 4p + q holds pixel column t0 - 1 + p (p < 16; p = 1 .. 14
+// own outputs) and channels 4q .. 4q+3: one 16-byte load per row (a wave: 1
+// KB contiguous; rows prefetched three ahead), its 36 weights in VGPRs.  Per
+// input row it forms the nine tap partials u[ky][dx] = sum over its four
+// channels of w[c][ky][dx] act(x)[c] and adds them to the three output rows
+// the row feeds; a finished output row is summed over the four channel
+// quads (two DPP steps) and over its three columns (two one-pixel lane
+// shifts).  Every input element comes from HBM once per strip (halo: 16/14
+// columns, (R1_RS+2)/R1_RS rows).  BatchNorm partials: one [sum y, sum y^2]
+// row per workgroup of four strips (fp32 per lane and wave, fp64 across
+// waves).  Another summation order than conv3x3_small_fwd (within 1e-6).
+constexpr int R1_TW = 14;   // output columns per wave
+constexpr int R1_RS = 16;   // rows per strip
+
+template <bool PRO>
+__global__ __launch_bounds__(256) void conv3x3_rows_16to1(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+    float* __restrict__ y, double* __restrict__ stats, int H, int W, int nfs, int nts,
+    int nstrips) {
+  __shared__ double red[4][2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, p = lane >> 2, q = lane & 3;
+  const int strip = blockIdx.x * 4 + wave;
+  float s1 = 0.f, s2 = 0.f;
+  if (strip < nstrips) {
+    const int ts = strip % nts, fs = (strip / nts) % nfs, n = strip / (nts * nfs);
+    const int f0 = fs * R1_RS, t = ts * R1_TW - 1 + p;
+    const bool tin = t >= 0 && t < W;
+    const bool own = p >= 1 && p <= R1_TW && tin;
+    const int64_t HW = (int64_t)H * W;
+    const float4* src =
+        reinterpret_cast<const float4*>(x + ((int64_t)n * HW + (tin ? t : 0)) * 16 + 4 * q);
+    const int rows = (H - f0) < R1_RS ? (H - f0) : R1_RS;
+    const float bv = bias ? bias[0] : 0.f;
+    float wr[4][9];
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int k = 0; k < 9; ++k) wr[c][k] = w[(4 * q + c) * 9 + k];
+    float4 sc4 = make_float4(1.f, 1.f, 1.f, 1.f), sh4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (PRO) {
+      sc4 = *reinterpret_cast<const float4*>(in_scale + 4 * q);
+      sh4 = *reinterpret_cast<const float4*>(in_shift + 4 * q);
+    }
+    auto load = [&](int r) -> float4 {
+      return (r >= 0 && r < H && tin) ? src[(int64_t)r * W * 4] : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    float A[3][3];   // output rows r-1, r, r+1 of input row r: per dx, unshifted
+#pragma unroll
+    for (int k = 0; k < 3; ++k) A[0][k] = A[1][k] = A[2][k] = 0.f;
+    const int nrow = rows + 2;
+    float4 b0 = load(f0 - 1), b1 = load(f0), b2 = load(f0 + 1);   // three rows in flight
+    auto step = [&](int i, float4& buf) {
+      const int r = f0 - 1 + i;
+      float a[4] = {buf.x, buf.y, buf.z, buf.w};
+      if (i + 3 < nrow) buf = load(r + 3);
+      if (PRO && r >= 0 && r < H && tin) {   // zero padding stays zero
+        a[0] = fmaxf(fmaf(a[0], sc4.x, sh4.x), 0.f);
+        a[1] = fmaxf(fmaf(a[1], sc4.y, sh4.y), 0.f);
+        a[2] = fmaxf(fmaf(a[2], sc4.z, sh4.z), 0.f);
+        a[3] = fmaxf(fmaf(a[3], sc4.w, sh4.w), 0.f);
+      }
+      float u[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        float v = wr[0][k] * a[0];
+        v = fmaf(wr[1][k], a[1], v);
+        v = fmaf(wr[2][k], a[2], v);
+        u[k] = fmaf(wr[3][k], a[3], v);
+      }
+      // ky = 0 feeds output row r+1, ky = 1 row r, ky = 2 row r-1
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        A[2][dx] += u[dx];
+        A[1][dx] += u[3 + dx];
+        A[0][dx] += u[6 + dx];
+      }
+      if (i >= 2) {   // output row r-1 (>= f0) is complete
+        float v3[3];
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {   // sum over the quad's channel groups
+          float v = A[0][dx];
+          v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+          v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+          v3[dx] = v;
+        }
+        const float l = __shfl_up(v3[0], 4, 64), rr = __shfl_down(v3[2], 4, 64);
+        const float v = bv + ((l + v3[1]) + rr);
+        if (own && q == 0) {
+          y[(int64_t)n * HW + (int64_t)(r - 1) * W + t] = v;
+          s1 += v;
+          s2 = fmaf(v, v, s2);
+        }
+      }
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) {
+        A[0][dx] = A[1][dx];
+        A[1][dx] = A[2][dx];
+        A[2][dx] = 0.f;
+      }
+    };
+    for (int i = 0; i < nrow; i += 3) {
+      step(i, b0);
+      if (i + 1 < nrow) step(i + 1, b1);
+      if (i + 2 < nrow) step(i + 2, b2);
+    }
+  }
+  if (!stats) return;   // uniform: no barrier without statistics
+  s1 = wave_sum(s1);
+  s2 = wave_sum(s2);
+  if (lane == 0) {
+    red[wave][0] = s1;
+    red[wave][1] = s2;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += red[k][threadIdx.x];
+    stats[(int64_t)blockIdx.x * 2 + threadIdx.x] = v;
+  }
+}
+
+// Round 6: the 1 -> 16 convs on row strips, their 16-channel side channel-
+// last: the encoder's first forward (encoder.0, models/CNNBLSTM/model.py:35-36)
+// with its BatchNorm partials, and the decoder's last data gradient (dy of one
+// channel -> dx of 16, decoder.6, model.py:59-60) with the fused BatchNorm-
+// backward reduce of the layer it feeds (Bnr).  conv3x3_small_fwd took 86 /
+// 126 us for them at the C2 shape.  Lane 4p + q of a wave: pixel column
+// t0 - 1 + p (p < 16; p = 1 .. 14 own outputs) and channels 4q .. 4q+3, whose
+// 36 weights, biases and BatchNorm constants sit in its VGPRs; each output
+// pixel row is one float4 per lane (a wave: 1 KB contiguous).  The one-channel
+// input row is read by the four lanes of a pixel and shifted by one pixel
+// (four lanes) for the outer taps: a rolling 3 x 3 window, rows prefetched two
+// ahead.  Per output the fma chain of conv3x3_small_fwd (bias, then the nine
+// taps in order; data gradient: flipped taps, no bias), so y / dx are bit-
+// identical to it.  BatchNorm partials: one row per workgroup of four strips,
+// [sum | sum of squares] (forward) or [sum gz | sum gz * xhat] (Bnr) x 16
+// channels, lanes in fp32, workgroup in fp64 (<= exact_stat_parts rows).
+constexpr int R16_TW = 14;   // output columns per wave
+constexpr int R16_RS = 16;   // rows per strip
+
+template <bool DG, bool PRO, bool FZ>
+__global__ __launch_bounds__(256) void conv3x3_rows_1to16(
+    const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
+    const float* __restrict__ in_scale, const float* __restrict__ in_shift,
+    float* __restrict__ y, double* __restrict__ stats, Bnr bnr, int H, int W, int nfs, int nts,
+    int nstrips) {
+  __shared__ double red[4][32];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, p = lane >> 2, q = lane & 3;
+  const int strip = blockIdx.x * 4 + wave;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (strip < nstrips) {
+    const int ts = strip % nts, fs = (strip / nts) % nfs, n = strip / (nts * nfs);
+    const int f0 = fs * R16_RS, t = ts * R16_TW - 1 + p;
+    const bool tin = t >= 0 && t < W;
+    const bool own = p >= 1 && p <= R16_TW && tin;
+    const int64_t HW = (int64_t)H * W;
+    const float* xs = x + (int64_t)n * HW + (tin ? t : 0);
+    float wr[4][9], bq[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) wr[c][k] = w[(4 * q + c) * 9 + (DG ? 8 - k : k)];
+      bq[c] = (!DG && bias) ? bias[4 * q + c] : 0.f;
+    }
+    const float sc0 = PRO ? in_scale[0] : 1.f, sh0 = PRO ? in_shift[0] : 0.f;
+    float bsc[4], bsh[4], bmu[4], brs[4];
+    if constexpr (FZ) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        bsc[c] = bnr.sc[4 * q + c];
+        bsh[c] = bnr.sh[4 * q + c];
+        bmu[c] = bnr.save[4 * q + c];
+        brs[c] = bnr.save[16 + 4 * q + c];
+      }
+    }
+    const int rows = (H - f0) < R16_RS ? (H - f0) : R16_RS;
+    auto ldx = [&](int r) -> float { return (r >= 0 && r < H && tin) ? xs[(int64_t)r * W] : 0.f; };
+    auto act = [&](int r, float v) -> float {   // zero padding stays zero
+      return (PRO && r >= 0 && r < H && tin) ? fmaxf(fmaf(v, sc0, sh0), 0.f) : v;
+    };
+    auto ldy = [&](int f) -> uint4 {   // Bnr: y of output row f, channels 4q .. 4q+3
+      const int64_t e = ((((int64_t)n * H + (f < H ? f : H - 1)) * W) + (tin ? t : 0)) * 16 + 4 * q;
+      return bnr_ld4(bnr, e);
+    };
+    // window rows f-1, f, f+1 (left, centre, right)
+    float wl[3], wc[3], wrr[3];
+    wc[0] = act(f0 - 1, ldx(f0 - 1));
+    wc[1] = act(f0, ldx(f0));
+    wl[0] = __shfl_up(wc[0], 4, 64); wrr[0] = __shfl_down(wc[0], 4, 64);
+    wl[1] = __shfl_up(wc[1], 4, 64); wrr[1] = __shfl_down(wc[1], 4, 64);
+    float nx0 = ldx(f0 + 1), nx1 = ldx(f0 + 2);   // raw rows f+1, f+2 in flight
+    uint4 ny = make_uint4(0u, 0u, 0u, 0u);
+    if (FZ) ny = ldy(f0);
+    for (int i = 0; i < rows; ++i) {
+      const int f = f0 + i;
+      const float cv = act(f + 1, nx0);
+      nx0 = nx1;
+      nx1 = ldx(f + 3);
+      uint4 yc = ny;
+      if (FZ && i + 1 < rows) ny = ldy(f + 1);
+      wc[2] = cv;
+      wl[2] = __shfl_up(cv, 4, 64);
+      wrr[2] = __shfl_down(cv, 4, 64);
+      float o[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        float acc = bq[c];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          acc = fmaf(wr[c][3 * ky], wl[ky], acc);
+          acc = fmaf(wr[c][3 * ky + 1], wc[ky], acc);
+          acc = fmaf(wr[c][3 * ky + 2], wrr[ky], acc);
+        }
+        o[c] = acc;
+      }
+      if (own) {
+        *reinterpret_cast<float4*>(y + ((((int64_t)n * H + f) * W) + t) * 16 + 4 * q) =
+            make_float4(o[0], o[1], o[2], o[3]);
+        if constexpr (FZ) {
+          float yv[4];
+          bnr_dec4(bnr.y16, yc, yv);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float gz = fmaf(yv[c], bsc[c], bsh[c]) > 0.f ? o[c] : 0.f;
+            s1[c] += gz;
+            s2[c] += gz * ((yv[c] - bmu[c]) * brs[c]);
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            s1[c] += o[c];
+            s2[c] = fmaf(o[c], o[c], s2[c]);
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        wl[k] = wl[k + 1];
+        wc[k] = wc[k + 1];
+        wrr[k] = wrr[k + 1];
+      }
+    }
+  }
+  if (!stats) return;   // uniform: no barrier without statistics
+  // the 16 pixel lanes of each channel quad, fixed butterfly order
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) {
+      s1[c] += __shfl_xor(s1[c], o, 64);
+      s2[c] += __shfl_xor(s2[c], o, 64);
+    }
+  if (p == 0) {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      red[wave][4 * q + c] = s1[c];
+      red[wave][16 + 4 * q + c] = s2[c];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 32) {
+    double v = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v += red[k][threadIdx.x];
+    stats[(int64_t)blockIdx.x * 32 + threadIdx.x] = v;
+  }
+}
+
+// AINP_SMALL_ROWS=0: the 8 x 48 LDS tile kernel for the 16 -> 1 forward (A/B)
+static bool small_rows_env() {
+  static const bool v = [] {
+    const char* e = getenv("AINP_SMALL_ROWS");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+static int64_t rows16to1_strips(int64_t N, int64_t H, int64_t W) {
+  return N * cdiv(H, R1_RS) * cdiv(W, R1_TW);
+}
+
 // dw[o] (o < COUT*CIN*9, [co][ci][tap] order) and dbias from the group sums
 __global__ void small_wgrad_final(const double* __restrict__ tmp, int ngroups, int nw, int nout,
                                   float* __restrict__ dw, float* __restrict__ dbias) {
@@ -1192,10 +1480,47 @@ static void launch_small_fwd(bool dgrad, const float* x, const float* w, const f
   else launch_small_fwd_l<CIN, COUT, false, false>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, bnr);
 }
 
+// *used: the BatchNorm partial rows written (<= exact_stat_parts)
 static int small_fwd_dispatch(bool dgrad, const float* x, const float* w, const float* bias,
                               const float* sc, const float* sh, float* y, double* stats,
                               int64_t N, int Cin, int Cout, int64_t H, int64_t W, hipStream_t s,
-                              int lay = 0, const Bnr& bnr = Bnr{}) {
+                              int lay = 0, const Bnr& bnr = Bnr{}, int64_t* used = nullptr) {
+  if (used) *used = N * cdiv(H, CV_FT) * cdiv(W, CV_TT);   // exact_stat_parts
+  // (the BatchNorm partial rows of a row-strip launch stay within
+  // exact_stat_parts; otherwise the tile kernel runs)
+  if (!dgrad && Cin == 16 && Cout == 1 && (lay & 1) && small_rows_env() &&
+      N * H * W * 16 < ((int64_t)1 << 40) && rows16to1_strips(N, H, W) < ((int64_t)1 << 31) &&
+      cdiv(rows16to1_strips(N, H, W), 4) <= N * cdiv(H, CV_FT) * cdiv(W, CV_TT)) {
+    const int nfs = (int)cdiv(H, R1_RS), nts = (int)cdiv(W, R1_TW);
+    const int64_t ns = rows16to1_strips(N, H, W), nb = cdiv(ns, 4);
+    if (used) *used = nb;
+    const dim3 grid((unsigned)nb);
+    if (sc)
+      hipLaunchKernelGGL(conv3x3_rows_16to1<true>, grid, dim3(256), 0, s, x, w, bias, sc, sh, y,
+                         stats, (int)H, (int)W, nfs, nts, (int)ns);
+    else
+      hipLaunchKernelGGL(conv3x3_rows_16to1<false>, grid, dim3(256), 0, s, x, w, bias, sc, sh, y,
+                         stats, (int)H, (int)W, nfs, nts, (int)ns);
+    return check_launch("conv3x3_rows_16to1");
+  }
+  if (Cin == 1 && Cout == 16 && (lay & 2) && small_rows_env() &&
+      N * H * W * 16 < ((int64_t)1 << 40) && (dgrad || !bnr.y)) {
+    const int nfs = (int)cdiv(H, R16_RS), nts = (int)cdiv(W, R16_TW);
+    const int64_t ns = N * nfs * nts, nb = cdiv(ns, 4);
+    if (nb <= N * cdiv(H, CV_FT) * cdiv(W, CV_TT) && ns < ((int64_t)1 << 31)) {
+      if (used) *used = nb;
+      const bool fz = dgrad && bnr.y && stats;
+#define AINP_R16(DGV, PROV, FZV)                                                                   \
+  hipLaunchKernelGGL((conv3x3_rows_1to16<DGV, PROV, FZV>), dim3((unsigned)nb), dim3(256), 0, s, x, \
+                     w, bias, sc, sh, y, stats, bnr, (int)H, (int)W, nfs, nts, (int)ns)
+      if (dgrad && fz) AINP_R16(true, false, true);
+      else if (dgrad) AINP_R16(true, false, false);
+      else if (sc) AINP_R16(false, true, false);
+      else AINP_R16(false, false, false);
+#undef AINP_R16
+      return check_launch("conv3x3_rows_1to16");
+    }
+  }
 #define AINP_SF(A, B) \
   if (Cin == A && Cout == B) { launch_small_fwd<A, B>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, lay, bnr); return check_launch("conv3x3_small_fwd"); }
   AINP_SF(1, 16) AINP_SF(2, 16) AINP_SF(16, 1) AINP_SF(16, 2)
@@ -1209,6 +1534,12 @@ static bool small_wgrad_tile_env() {
   return e && e[0] == '1';
 }
 
+// first-stage groups of the small weight gradients' slab sum: their slabs are
+// only 145-160 floats wide, so WG_GROUPS (16) groups left one thread per
+// output summing 430 rows one after another (47 us at the C2 shape, on the
+// critical path at the end of the backward); 128 groups of ~54 rows
+constexpr int SWG_GROUPS = 128;
+
 static int64_t strip_tiles(int64_t N, int64_t H, int64_t W) {
   return N * cdiv(H, SW_RS) * cdiv(W, SW_TW);
 }
@@ -1219,7 +1550,7 @@ static size_t small_wgrad_ws(int64_t N, int Cin, int Cout, int64_t H, int64_t W)
   if (ns > nblk) nblk = ns;
   if (nc > nblk) nblk = nc;
   const int nout = Cout * Cin * 9 + Cout;
-  return (size_t)nblk * nout * sizeof(float) + (size_t)WG_GROUPS * nout * sizeof(double) + 16;
+  return (size_t)nblk * nout * sizeof(float) + (size_t)SWG_GROUPS * nout * sizeof(double) + 16;
 }
 
 static int64_t strip_cl_tiles(int64_t N, int64_t H, int64_t W) {
@@ -1281,12 +1612,12 @@ static int small_wgrad(const float* x, const float* sc, const float* sh, const f
   uintptr_t tp = reinterpret_cast<uintptr_t>(partial + nblk * nout);
   tp = (tp + 15) & ~(uintptr_t)15;
   double* tmp = reinterpret_cast<double*>(tp);
-  const int per_group = (int)cdiv(nblk, WG_GROUPS);
-  hipLaunchKernelGGL(wgrad_reduce1, dim3((nout + 255) / 256, WG_GROUPS), dim3(256), 0, s, partial,
+  const int per_group = (int)cdiv(nblk, SWG_GROUPS);
+  hipLaunchKernelGGL(wgrad_reduce1, dim3((nout + 255) / 256, SWG_GROUPS), dim3(256), 0, s, partial,
                      (int)nblk, nout, per_group, tmp);
   rc = check_launch("wgrad_reduce1");
   if (rc) return rc;
-  hipLaunchKernelGGL(small_wgrad_final, dim3((nout + 255) / 256), dim3(256), 0, s, tmp, WG_GROUPS,
+  hipLaunchKernelGGL(small_wgrad_final, dim3((nout + 255) / 256), dim3(256), 0, s, tmp, SWG_GROUPS,
                      Cout * Cin * 9, nout, dw, dbias);
   return check_launch("small_wgrad_final");
 }
@@ -1379,9 +1710,10 @@ static int conv_fwd_dispatch(const float* x, const float* w, const float* bias,
       "conv3x3: bf16 storage (AINP_CONV_DY16 / _X16 / _Y16) needs a split-bf16 kernel for this pair";
   if (small_pair(Cin, Cout)) {
     if (x16 || y16) return record_msg(kNo16);
+    int64_t used = 0;
     const int rc = small_fwd_dispatch(DG, x, w, bias, sc, sh, y, stats, N, Cin, Cout, H, W, s,
-                                      lay);
-    return rc ? rc : zero_tail(exact_stat_parts(N, H, W));
+                                      lay, Bnr{}, &used);
+    return rc ? rc : zero_tail(used);
   }
   if (!conv_exact_env()) {
     int64_t parts = 0;
@@ -1551,10 +1883,11 @@ extern "C" int ainp_conv3x3_dgrad_bnr(const float* dy, const float* w, float* dx
   double* partial = reinterpret_cast<double*>(workspace);
   if (dgrad_bnr_env() && small_pair(Cout, Cin) && Cin % 4 == 0 && !(flags & AINP_CONV_DY16)) {
     // 1 -> 16 channels: the small kernel's channel-last epilogue
+    int64_t used = 0;
     const int rc = small_fwd_dispatch(true, dy, w, nullptr, nullptr, nullptr, dx, partial, N,
-                                      Cout, Cin, H, W, s, conv_lay(flags), bnr);
+                                      Cout, Cin, H, W, s, conv_lay(flags), bnr, &used);
     if (rc) return rc;
-    return bn_cl_sum_partials(partial, (int)exact_stat_parts(N, H, W), 2 * Cin, sums, s);
+    return bn_cl_sum_partials(partial, (int)used, 2 * Cin, sums, s);
   }
   if (dgrad_bnr_env() && !small_pair(Cout, Cin) && !conv_exact_env()) {
     int64_t parts = 0;

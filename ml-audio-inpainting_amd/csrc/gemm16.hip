@@ -559,6 +559,147 @@ __device__ __forceinline__ void tile256(int64_t M, int64_t N, const uint16_t* __
   }
 }
 
+// Round 6: the same tile on 64-deep K-tiles (tools/g256b_lab.hip: 3-10 %
+// faster on the layer-0 shapes, bit-identical -- the same MFMAs in the same k
+// order).  Two 64 KB LDS stages (A + B): k-contiguous images of 256 rows x
+// 128 B, 16-byte chunk c of row r at physical chunk c ^ (r & 7) (a ds_read_b128
+// quarter: 16 rows of one chunk, 16 distinct bank groups); k-major images of
+// 64 k-rows x 512 B read by frag_km as above.  32 MFMAs per wave between
+// barriers (twice the 32-deep ring's), one K-tile in flight across each
+// barrier, the next k-step's fragments read while the current one's MFMAs run.
+namespace b64 {
+constexpr int BK = 64, NST = 2, ROWB = 2 * BK, IMG = BM * ROWB, STAGE = 2 * IMG;
+static_assert(NST * STAGE == LDS_BYTES, "the 32-deep ring's 128 KB");
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
+
+// k-contiguous operand: wave w, instruction i covers image rows 8 (4w + i) .. +8;
+// lane L -> row + L/8, physical chunk L % 8
+__device__ __forceinline__ void stage(const uint16_t* __restrict__ P, int64_t ld, int64_t r0,
+                                      int64_t R, int64_t k0, unsigned char* img, int wave,
+                                      int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = 4 * wave + i;
+    const int row = 8 * blk + (lane >> 3);
+    const int c = swz(row, lane & 7);
+    int64_t gr = r0 + row;
+    gr = gr < R ? gr : R - 1;  // rows past the end: any valid row (never stored)
+    const uint16_t* src = P + gr * ld + k0 + 8 * c;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)src, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16, 0, 0);
+  }
+}
+
+// k-major operand: wave w, instruction i covers k-rows 2 (4w + i), +1 (stage_km's map)
+__device__ __forceinline__ void stage_km(const uint16_t* __restrict__ P, int64_t ld, int64_t r0,
+                                         int64_t R, int64_t k0, unsigned char* img, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = 4 * wave + i;
+    const int kr = 2 * blk + (lane >> 5);
+    const int c = kswz(kr, lane & 31);
+    int64_t col = r0 + 8 * c;
+    col = col + 8 <= R ? col : R - 8;
+    const uint16_t* src = P + (k0 + kr) * ld + col;
+    __builtin_amdgcn_global_load_lds(
+        (const void*)src, (__attribute__((address_space(3))) void*)(img + blk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8v frag(const unsigned char* img, int row, int chunk) {
+  return __builtin_bit_cast(bf16x8v,
+                            *reinterpret_cast<const uint4*>(img + row * ROWB + 16 * swz(row, chunk)));
+}
+}  // namespace b64
+
+template <bool AKM, bool BKM>
+__device__ __forceinline__ void tile256b(int64_t M, int64_t N, const uint16_t* __restrict__ A,
+                                         int64_t lda, const uint16_t* __restrict__ B, int64_t ldb,
+                                         float* __restrict__ Cs, int64_t ldc, int64_t m0,
+                                         int64_t n0, int64_t kbeg, int nk, int64_t split,
+                                         const Bias& bias, unsigned char* smem) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm = (wave >> 2) * 128, wn = (wave & 3) * 64;
+  const int li = lane & 31, lh = lane >> 5;
+  f32x16v acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  auto issue = [&](int kt) {
+    unsigned char* st = smem + (kt % b64::NST) * b64::STAGE;
+    const int64_t k0 = kbeg + (int64_t)kt * b64::BK;
+    if (AKM) b64::stage_km(A, lda, m0, M, k0, st, wave, lane);
+    else b64::stage(A, lda, m0, M, k0, st, wave, lane);
+    if (BKM) b64::stage_km(B, ldb, n0, N, k0, st + b64::IMG, wave, lane);
+    else b64::stage(B, ldb, n0, N, k0, st + b64::IMG, wave, lane);
+  };
+  auto fa_ = [&](const unsigned char* sa, int i, int ks) {
+    return AKM ? frag_km(sa, wm + i * 32, ks, lane) : b64::frag(sa, wm + i * 32 + li, 2 * ks + lh);
+  };
+  auto fb_ = [&](const unsigned char* sb, int j, int ks) {
+    return BKM ? frag_km(sb, wn + j * 32, ks, lane) : b64::frag(sb, wn + j * 32 + li, 2 * ks + lh);
+  };
+  if (nk > 0) issue(0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile kt: the only DMA in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();   // every wave's DMAs of tile kt; stage of kt-1 free
+    asm volatile("" ::: "memory");
+    if (kt + 1 < nk) issue(kt + 1);
+    const unsigned char* sa = smem + (kt % b64::NST) * b64::STAGE;
+    const unsigned char* sb = sa + b64::IMG;
+    bf16x8v fa[2][4], fb[2][2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) fb[0][j] = fb_(sb, j, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[0][i] = fa_(sa, i, 0);
+#pragma unroll
+    for (int ks = 0; ks < b64::BK / 16; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < b64::BK / 16) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j) fb[cur ^ 1][j] = fb_(sb, j, ks + 1);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[cur ^ 1][i] = fa_(sa, i, ks + 1);
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the prefetch ahead of the MFMAs
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][i], fb[cur][j], acc[i][j], 0,
+                                                              0, 0);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t n = n0 + wn + j * 32 + li;
+    if (n >= N) continue;
+    float bv = 0.f;
+    if (split != 0) {   // split-K: the bias goes into slab 0 only
+    } else if (n < bias.nsplit) {
+      if (bias.a1) bv += bias.a1[n];
+      if (bias.a2) bv += bias.a2[n];
+    } else {
+      if (bias.b1) bv += bias.b1[n - bias.nsplit];
+      if (bias.b2) bv += bias.b2[n - bias.nsplit];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t m = m0 + wm + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (m < M) Cs[m * ldc + n] = acc[i][j][r] + bv;
+      }
+  }
+}
+
 __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
     int64_t M, int64_t N, int64_t K, const uint16_t* __restrict__ A, int64_t lda,
     const uint16_t* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
@@ -584,6 +725,29 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_kernel(
                         bias, smem);
 }
 
+// the same grid on 64-deep K-tiles (BK = 64 divides K and kc)
+__global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256b_kernel(
+    int64_t M, int64_t N, int64_t K, const uint16_t* __restrict__ A, int64_t lda,
+    const uint16_t* __restrict__ B, int64_t ldb, float* __restrict__ C, int64_t ldc,
+    int64_t kc, int64_t strideC, Bias bias, int tiles_n) {
+  extern __shared__ __attribute__((aligned(1024))) unsigned char smem[];
+  const int64_t nwg = gridDim.x, bid0 = blockIdx.x;
+  const int64_t xcd = bid0 % 8, slot = bid0 / 8, q8 = nwg / 8, r8 = nwg % 8;
+  const int64_t bid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + slot;
+  const int64_t tiles_m = (M + BM - 1) / BM;
+  const int64_t per_group = 8 * tiles_m;
+  const int64_t first_n = (bid / per_group) * 8;
+  const int64_t gsize = (tiles_n - first_n) < 8 ? (tiles_n - first_n) : 8;
+  const int64_t in_g = bid % per_group;
+  const int64_t m0 = (in_g / gsize) * BM, n0 = (first_n + in_g % gsize) * BN;
+  const int64_t split = blockIdx.y;
+  const int64_t kbeg = split * kc;
+  const int64_t kend = (kbeg + kc) < K ? (kbeg + kc) : K;
+  const int nk = (int)((kend - kbeg) / b64::BK);
+  tile256b<false, false>(M, N, A, lda, B, ldb, C + split * strideC, ldc, m0, n0, kbeg, nk, split,
+                         bias, smem);
+}
+
 // Several bf16 GEMMs in ONE grid (ainp_gemm_bf16nt_multi): problem q's work
 // items (tiles x splits) follow problem q-1's, each problem starting on a
 // multiple of 8 blocks.  Per problem the items are spread over the XCDs in
@@ -600,6 +764,7 @@ struct MProb {
 struct MJob {
   MProb p[MAXP];
   int np;
+  int bk64;   // every problem's K and kc multiples of 64: tile256b
 };
 
 __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_multi_kernel(MJob job) {
@@ -624,8 +789,24 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_bf16nt_256_multi_kernel(MJob 
   const int64_t kbeg = split * P.kc;
   const int64_t kend = (kbeg + P.kc) < P.K ? (kbeg + P.kc) : P.K;
   const Bias nob{nullptr, nullptr, nullptr, nullptr, 0};
-  const int nk = (int)((kend - kbeg) / BK);
   float* Cs = P.C + split * P.strideC;
+  if (job.bk64) {
+    const int nk = (int)((kend - kbeg) / b64::BK);
+    if (P.a_km && P.b_km)
+      tile256b<true, true>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split,
+                           nob, smem);
+    else if (P.a_km)
+      tile256b<true, false>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split,
+                            nob, smem);
+    else if (P.b_km)
+      tile256b<false, true>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split,
+                            nob, smem);
+    else
+      tile256b<false, false>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split,
+                             nob, smem);
+    return;
+  }
+  const int nk = (int)((kend - kbeg) / BK);
   if (P.a_km && P.b_km)
     tile256<true, true>(P.M, P.N, P.A, P.lda, P.B, P.ldb, Cs, P.ldc, m0, n0, kbeg, nk, split, nob,
                         smem);
@@ -969,6 +1150,15 @@ __global__ __launch_bounds__(THREADS, 1) void gemm_x6nt_256s_kernel(
 
 using namespace ainp;
 
+// AINP_G256_BK64=0: the 32-deep 4-stage ring for every g256 GEMM (A/B)
+static bool g256_bk64() {
+  static const bool v = [] {
+    const char* e = getenv("AINP_G256_BK64");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t* A, int64_t lda,
                                 const uint16_t* B, int64_t ldb, float* C, int64_t ldc,
                                 const float* bias_a1, const float* bias_a2, const float* bias_b1,
@@ -1005,12 +1195,21 @@ extern "C" int ainp_gemm_bf16nt(int64_t M, int64_t N, int64_t K, const uint16_t*
     static const bool lds_ok =
         hipFuncSetAttribute((const void*)g256::gemm_bf16nt_256_kernel,
                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                            g256::LDS_BYTES) == hipSuccess &&
+        hipFuncSetAttribute((const void*)g256::gemm_bf16nt_256b_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize,
                             g256::LDS_BYTES) == hipSuccess;
     if (!lds_ok) return record_msg("ainp_gemm_bf16nt: cannot reserve 128 KB of LDS");
     const int64_t tn = cdiv(N, g256::BN);
     const dim3 grid((unsigned)(cdiv(M, g256::BM) * tn), (unsigned)nsplit);
-    hipLaunchKernelGGL(g256::gemm_bf16nt_256_kernel, grid, dim3(g256::THREADS), g256::LDS_BYTES,
-                       as_stream(stream), M, N, K, A, lda, B, ldb, C, ldc, kc, strideC, b, (int)tn);
+    if (g256_bk64() && K % g256::b64::BK == 0 && kc % g256::b64::BK == 0)
+      hipLaunchKernelGGL(g256::gemm_bf16nt_256b_kernel, grid, dim3(g256::THREADS), g256::LDS_BYTES,
+                         as_stream(stream), M, N, K, A, lda, B, ldb, C, ldc, kc, strideC, b,
+                         (int)tn);
+    else
+      hipLaunchKernelGGL(g256::gemm_bf16nt_256_kernel, grid, dim3(g256::THREADS), g256::LDS_BYTES,
+                         as_stream(stream), M, N, K, A, lda, B, ldb, C, ldc, kc, strideC, b,
+                         (int)tn);
     return check_launch("gemm_bf16nt_256");
   }
   const int64_t tiles_n = cdiv(N, g16::BN);
@@ -1052,6 +1251,9 @@ extern "C" int ainp_gemm_bf16nt_multi(const ainp_bf16_problem* probs, int nprobs
     d.first = first;
     first += (d.items + 7) / 8 * 8;
   }
+  job.bk64 = g256_bk64() ? 1 : 0;
+  for (int q = 0; q < nprobs; ++q)
+    if (job.p[q].K % g256::b64::BK || job.p[q].kc % g256::b64::BK) job.bk64 = 0;
   static const bool lds_ok =
       hipFuncSetAttribute((const void*)g256::gemm_bf16nt_256_multi_kernel,
                           hipFuncAttributeMaxDynamicSharedMemorySize, g256::LDS_BYTES) == hipSuccess;

@@ -120,7 +120,13 @@ def test_dgrad_cfnt_bit_identical(N, H, W, bf16):
 def test_cl_small_channel_convs(N, H, W, pro):
     """1 -> 16 and 16 -> 1 (encoder.0, decoder.6): forward and data gradient
     bit-identical, the channel-last row-strip weight gradient within 1e-6 of
-    the NCHW one (another summation order) and run-to-run identical."""
+    the NCHW one (another summation order) and run-to-run identical.  Round 6:
+    the 16 -> 1 forward with channel-last input runs on row strips (another
+    summation order): y and the summed BatchNorm partials within 1e-6 of the
+    NCHW kernel and of an fp64 conv of the same act(x), run-to-run identical;
+    the 1 -> 16 forward and data gradient on row strips keep each output's
+    fma chain (bit-identical), their partials grouped per strip (1e-6)."""
+    import torch.nn.functional as F
     from ainp import ops
     for cin, cout in ((1, 16), (16, 1)):
         x, dy, w, b, sc, sh = _data(N, cin, cout, H, W, 5 + cin)
@@ -129,7 +135,18 @@ def test_cl_small_channel_convs(N, H, W, pro):
         xcl, ycl = cin == 16, cout == 16
         y, st = ops.conv3x3_fwd(_cl(x) if xcl else x, w, b, s_, h_, want_stats=True, xcl=xcl,
                                 ycl=ycl)
-        assert torch.equal(_nchw(y) if ycl else y, y0) and torch.equal(st, st0)
+        if cin == 16:
+            a = x.double()
+            if pro:
+                a = torch.relu(a * sc.double().view(1, -1, 1, 1) + sh.double().view(1, -1, 1, 1))
+            ref = F.conv2d(a, w.double(), b.double(), padding=1)
+            assert rel(y, ref) < 1e-6 and rel(y, y0) < 1e-6
+            assert rel(st.sum(0), st0.sum(0)) < 1e-6
+            y2, st2 = ops.conv3x3_fwd(_cl(x), w, b, s_, h_, want_stats=True, xcl=True)
+            assert torch.equal(y2, y) and torch.equal(st2, st)
+        else:   # 1 -> 16 (round 6: row strips, the same fma chain per output)
+            assert torch.equal(_nchw(y) if ycl else y, y0)
+            assert rel(st.sum(0), st0.sum(0)) < 1e-6
         dx0 = ops.conv3x3_dgrad(dy, w)
         dx = ops.conv3x3_dgrad(_cl(dy) if ycl else dy, w, xcl=ycl, ycl=xcl)
         assert torch.equal(_nchw(dx) if xcl else dx, dx0)

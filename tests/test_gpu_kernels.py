@@ -851,6 +851,34 @@ def test_gemm_bf16nt_multi_kmajor_operands_bit_identical(akm, bkm):
         assert float((got.double() - ref).norm() / ref.norm()) < 1e-5
 
 
+@pytest.mark.parametrize("akm,bkm", [(False, False), (True, True), (False, True)])
+def test_gemm_bf16nt_multi_bk64_matches_bk32(akm, bkm):
+    """Round 6: the 64-deep K-tile variant of the 256 x 256 tile (gemm16.hip
+    tile256b, taken when 64 divides every problem's K and kc) against the
+    32-deep ring (forced by a second problem with K % 64 != 0 in the same job):
+    bit-identical -- the same MFMAs in the same k order -- for k-contiguous
+    and k-major operands, ragged tiles, split-K slabs."""
+    from ainp import ops
+    g = torch.Generator().manual_seed(21)
+    M, N, K, S = 1000, 776, 2112, 3
+    A = _tobf16(torch.randn(M, K, generator=g)).cuda()
+    B = _tobf16(torch.randn(N, K, generator=g)).cuda()
+    Akm = A.T.contiguous() if akm else A
+    Bkm = B.T.contiguous() if bkm else B
+    kc = -(-K // S // 64) * 64
+    A2 = _tobf16(torch.randn(300, 1056, generator=g)).cuda()
+    B2 = _tobf16(torch.randn(520, 1056, generator=g)).cuda()
+    C64 = torch.full((S, M, N), float("nan"), device="cuda")
+    C32 = torch.full((S, M, N), float("nan"), device="cuda")
+    C2 = torch.full((300, 520), float("nan"), device="cuda")
+    ops.gemm_bf16nt_multi([(Akm, Bkm, C64, K, S, kc, akm, bkm)])
+    ops.gemm_bf16nt_multi([(Akm, Bkm, C32, K, S, kc, akm, bkm), (A2, B2, C2, 1056, 1, 1056)])
+    torch.cuda.synchronize()
+    assert torch.equal(C64, C32)
+    ref = A.double() @ B.double().T
+    assert float((C64.sum(0).double() - ref).norm() / ref.norm()) < 1e-5
+
+
 def test_lstm_l0_bwd_bf16_pair_kmajor_bit_identical():
     """ops.lstm_l0_bwd_bf16(km=True) -- dW_cat from dg [NT, 8H] and X [NT, I]
     k-major -- equals the transposed-copy pair bit for bit."""
