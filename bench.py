@@ -483,6 +483,12 @@ def _cnn_step_work(B=32, F=257, T=334, H=128, bf16=False):
         ("bn_relu_bwd_ntcf_cl<true", "hbm", (y + 4.0 + gy) * big),
         # the bridge: y -> fp32 X [N, T, 64F], or bf16 X and X^T
         ("bn_relu_apply_ntcf_cl", "hbm", (2.0 + 4.0 if bf16 else 8.0) * big),
+        # round 6: the 1 <-> 16 channel convs on row strips (fp32 in both
+        # configurations): 16-channel side read / written once, the 1-channel
+        # side once; the data gradient's fused BatchNorm reduce also reads y
+        ("conv3x3_rows_16to1", "hbm", (16 * 4.0 + 4.0) * P),
+        ("conv3x3_rows_1to16<false", "hbm", (4.0 + 16 * 4.0) * P),
+        ("conv3x3_rows_1to16<true, false, true", "hbm", (4.0 + 16 * 4.0 + 16 * y) * P),
     ]
 
 

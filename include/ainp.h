@@ -383,6 +383,24 @@ int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,
                           const float* in_shift, const float* dy, float* dw,
                           float* dbias, void* workspace, int64_t N, int Cin,
                           int Cout, int64_t H, int64_t W, int flags, void* stream);
+/* Round 6: the weight gradient of Conv2d(1, 16) (x one channel; the encoder's
+ * first conv, models/CNNBLSTM/model.py:35-36) with the step-2 apply of the
+ * BatchNorm+ReLU backward of its output fused in: dy = gy is formed per
+ * element from g (gradient of the BatchNorm+ReLU output) and y (its pre-BN
+ * input), both channel-last [N][H][W][16] fp32, 16-byte aligned, with the
+ * constants and arithmetic of ainp_bn_relu_bwd_apply_ex (scale / shift /
+ * gamma / save_mean_rstd / sums / count as there) -- the values are that
+ * apply's gy bit for bit -- and gy is not written (for a conv whose input needs
+ * no gradient it has no other consumer).  dw / dbias as ainp_conv3x3_wgrad_ex
+ * (lay: dy channel-last), dgamma / dbeta as the apply writes them.  workspace:
+ * ainp_conv3x3_wgrad_workspace(N, 1, 16, H, W) bytes. */
+int ainp_conv3x3_wgrad_bnapply(const float* x, const float* in_scale, const float* in_shift,
+                               const float* g, const float* y, const float* scale,
+                               const float* shift, const float* gamma,
+                               const float* save_mean_rstd, const double* sums, int64_t count,
+                               float* dw, float* dbias, float* dgamma, float* dbeta,
+                               void* workspace, int64_t N, int Cin, int Cout, int64_t H,
+                               int64_t W, void* stream);
 /* 1 if both ainp_conv3x3_dgrad_ex and ainp_conv3x3_wgrad_ex of this
  * nn.Conv2d(Cin, Cout) accept AINP_CONV_BF16 | AINP_CONV_DY16 (host-only). */
 int ainp_conv3x3_dy16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
@@ -489,6 +507,19 @@ int ainp_bn_relu_bwd_apply_ex(const float* g, const float* y, const float* scale
  * models/CNNBLSTM/model.py:35-60.  workspace:
  * ainp_conv3x3_dgrad_bnr_workspace(...) bytes. */
 int64_t ainp_conv3x3_dgrad_bnr_workspace(int64_t N, int Cin, int Cout, int64_t H, int64_t W);
+/* Round 6: with dx == NULL, ainp_conv3x3_dgrad_bnr writes only the sums, for
+ * Conv2d(16, 1) (dy one channel -> dx 16): its dx is recomputed by
+ * ainp_conv3x3_dgrad_bnapply, which forms the data gradient again (the same
+ * fma chains) and writes the BatchNorm+ReLU backward apply of it, gy
+ * (channel-last [N][H][W][16]; gy16: bf16 nearest-even storage), as
+ * ainp_bn_relu_bwd_apply_ex would from that dx and y (fp32 channel-last),
+ * with dgamma / dbeta -- dx is never written or read back (decoder.5 ->
+ * decoder.6 of models/CNNBLSTM/model.py:57-60).  sums / count as the apply. */
+int ainp_conv3x3_dgrad_bnapply(const float* dy, const float* w, const float* y,
+                               const float* scale, const float* shift, const float* gamma,
+                               const float* save_mean_rstd, const double* sums, int64_t count,
+                               void* gy, int gy16, float* dgamma, float* dbeta, int64_t N,
+                               int Cin, int Cout, int64_t H, int64_t W, void* stream);
 int ainp_conv3x3_dgrad_bnr(const float* dy, const float* w, float* dx, int64_t N, int Cin,
                            int Cout, int64_t H, int64_t W, int flags, const void* y,
                            const float* scale, const float* shift, const float* save_mean_rstd,

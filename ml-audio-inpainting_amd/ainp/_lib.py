@@ -88,6 +88,10 @@ _SIGS = {
     "ainp_conv3x3_io16_ok": (c_int, [c_int64, c_int, c_int, c_int64, c_int64]),
     "ainp_conv3x3_cl_ok": (c_int, [c_int64, c_int, c_int, c_int64, c_int64]),
     "ainp_conv3x3_dgrad_cfnt_ok": (c_int, [c_int64, c_int, c_int, c_int64, c_int64]),
+    "ainp_conv3x3_dgrad_bnapply": (c_int, [P, P, P, P, P, P, P, P, c_int64, P, c_int, P, P,
+                                           c_int64, c_int, c_int, c_int64, c_int64, P]),
+    "ainp_conv3x3_wgrad_bnapply": (c_int, [P, P, P, P, P, P, P, P, P, P, c_int64, P, P, P, P, P,
+                                           c_int64, c_int, c_int, c_int64, c_int64, P]),
     "ainp_bn_relu_bwd_reduce_ex": (c_int, [P, P, P, P, P, P, P, c_int64, c_int, c_int64, c_int64,
                                            c_int, c_int, P]),
     "ainp_lstm_rec_fwd": (c_int, [P, PP, P, P, P, c_int64, c_int64, c_int, P]),

@@ -186,6 +186,7 @@ class _ConvStackFn(torch.autograd.Function):
         g = g.contiguous()
         gx = None
         pre_sums = None   # the next block's BatchNorm reduce, fused into this dgrad
+        pend = None       # (dy, w) of a data gradient the next apply recomputes
         N, H, W = x.shape[0], x.shape[2], x.shape[3]
         for bi in range(nb - 1, -1, -1):
             has_bn, _ = ctx.spec[bi]
@@ -202,11 +203,27 @@ class _ConvStackFn(torch.autograd.Function):
                 cnt = ctx.count
                 if ctx.count_dev is not None:
                     sums, cnt = torch.cat([sums, ctx.count_dev]), 0
+                if (FUSE_BNA0 and bi == 0 and ycl and not ntcf and not ctx.needs_input_grad[0]
+                        and WGRAD_LAST_MAIN and ctx.sink is None and tuple(w.shape[:2]) == (16, 1)
+                        and g.dtype == torch.float32 and y.dtype == torch.float32):
+                    # round 6: the first conv's weight gradient forms its dy from
+                    # g and y itself (ops.conv3x3_wgrad_bnapply): gy, whose only
+                    # consumer it is, is never written or read back
+                    dw, db, dgam, dbet = ops.conv3x3_wgrad_bnapply(
+                        x, None, None, g, y, sc, sh, params[p0 + 2], sv, sums, cnt)
+                    grads[p0], grads[p0 + 1], grads[p0 + 2], grads[p0 + 3] = dw, db, dgam, dbet
+                    continue
                 # bf16 configuration: gy in bf16 storage where this conv's data
                 # and weight gradients take it (they round it to bf16 anyway)
                 gy16 = ctx.bf16 and GY16 and ops.dy16_ok(N, w.shape[1], w.shape[0], H, W)
-                gy, dgam, dbet = ops.bn_relu_bwd_apply(g, y, sc, sh, params[p0 + 2], sv, sums,
-                                                       cnt, ntcf, gy16=gy16, cl=ycl)
+                if pend is not None:   # dx of the 16 -> 1 conv recomputed into the apply
+                    gy, dgam, dbet = ops.conv3x3_dgrad_bnapply(pend[0], pend[1], y, sc, sh,
+                                                               params[p0 + 2], sv, sums, cnt,
+                                                               gy16=gy16)
+                    pend = None
+                else:
+                    gy, dgam, dbet = ops.bn_relu_bwd_apply(g, y, sc, sh, params[p0 + 2], sv, sums,
+                                                           cnt, ntcf, gy16=gy16, cl=ycl)
                 grads[p0 + 2], grads[p0 + 3] = dgam, dbet
             else:
                 gy = g.view_as(y) if g.shape != y.shape else g
@@ -271,8 +288,16 @@ class _ConvStackFn(torch.autograd.Function):
                 # dx channel-last into a BatchNorm+ReLU: its backward reduce
                 # is summed by the data gradient's epilogue
                 psc, psh, psv = ctx.affine[bi - 1]
-                g, pre_sums = ops.conv3x3_dgrad_bnr(gy, w, ys[bi - 1], psc, psh, psv,
-                                                    bf16=ctx.bf16, xcl=ycl)
+                if (FUSE_BNA6 and tuple(w.shape[:2]) == (1, 16) and not ycl
+                        and gy.dtype == torch.float32 and ys[bi - 1].dtype == torch.float32):
+                    # round 6: Conv2d(16, 1) -- the sums now, dx recomputed by the
+                    # apply (ops.conv3x3_dgrad_bnapply): never written or read back
+                    _, pre_sums = ops.conv3x3_dgrad_bnr(gy, w, ys[bi - 1], psc, psh, psv,
+                                                        bf16=ctx.bf16, xcl=ycl, want_dx=False)
+                    g, pend = None, (gy, w)
+                else:
+                    g, pre_sums = ops.conv3x3_dgrad_bnr(gy, w, ys[bi - 1], psc, psh, psv,
+                                                        bf16=ctx.bf16, xcl=ycl)
             elif (bi == 0 and ctx.needs_input_grad[0] and ctx.gx_cfnt and not xcl
                   and ops.dgrad_cfnt_ok(N, w.shape[1], w.shape[0], H, W)):
                 # round 6: dx as [C, F, N, T] (an [N, C, F, T] view of it) --
@@ -284,6 +309,19 @@ class _ConvStackFn(torch.autograd.Function):
                 if bi == 0:
                     gx = g
         return (gx, None, None, None, None, None, None, None, *grads)
+
+
+# Round 6: the decoder's last conv (16 -> 1): its data gradient only sums the
+# BatchNorm reduce of decoder.5, and that layer's apply recomputes it
+# (AINP_FUSE_BNA6=0: dx written and read back)
+FUSE_BNA6 = (os.environ.get("AINP_FUSE_BNA6", "1") != "0"
+             and os.environ.get("AINP_SMALL_ROWS", "1") != "0")   # the row-strip kernel
+
+
+# Round 6: the encoder's first conv (1 -> 16) weight gradient with its
+# BatchNorm+ReLU backward apply fused in (AINP_FUSE_BNA0=0: the apply pass
+# writes gy, the strip weight gradient reads it)
+FUSE_BNA0 = os.environ.get("AINP_FUSE_BNA0", "1") != "0"
 
 
 # Round 6: the decoder's input gradient written [C, F, N, T] by its first

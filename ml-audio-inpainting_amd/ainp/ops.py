@@ -861,24 +861,44 @@ def dgrad_cfnt_ok(N, Cin, Cout, H, W) -> bool:
     return bool(_lib.lib.ainp_conv3x3_dgrad_cfnt_ok(N, Cin, Cout, H, W))
 
 
-def conv3x3_dgrad_bnr(dy, w, y, scale, shift, save, bf16=False, xcl=False):
+def conv3x3_dgrad_bnr(dy, w, y, scale, shift, save, bf16=False, xcl=False, want_dx=True):
     """The data gradient (dx channel-last [N, H, W, Cin]) and the reduce step
     of the BatchNorm+ReLU backward it feeds (ainp_conv3x3_dgrad_bnr): y is that
     layer's pre-BatchNorm output [N, H, W, Cin] (fp32 or bf16 storage).
-    Returns (dx, sums) -- sums as bn_relu_bwd_reduce(dx, y, ..., cl=True)."""
+    Returns (dx, sums) -- sums as bn_relu_bwd_reduce(dx, y, ..., cl=True).
+    want_dx=False (Conv2d(16, 1), round 6): dx is not written (returned None);
+    conv3x3_dgrad_bnapply recomputes it into the apply."""
     _req(dy, "dy", None); _req(w, "w"); _req(y, "y", None)
     if xcl:
         N, H, W, Cout = dy.shape
     else:
         N, Cout, H, W = dy.shape
     Cin = w.shape[1]
-    dx = torch.empty((N, H, W, Cin), device=dy.device, dtype=torch.float32)
+    dx = torch.empty((N, H, W, Cin) if want_dx else (0,), device=dy.device,
+                     dtype=torch.float32)
     ws = torch.empty(_lib.lib.ainp_conv3x3_dgrad_bnr_workspace(N, Cin, Cout, H, W),
                      device=dy.device, dtype=torch.uint8)
     sums = torch.empty(2 * Cin, device=dy.device, dtype=torch.float64)
     _T.conv3x3_dgrad_bnr(dy, w, dx, _dy_flags(dy, bf16) | (CONV_XCL if xcl else 0) | CONV_YCL,
                          y, scale, shift, save, ws, sums, _y_flag(y))
-    return dx, sums
+    return (dx if want_dx else None), sums
+
+
+def conv3x3_dgrad_bnapply(dy, w, y, scale, shift, gamma, save, sums, count, gy16=False):
+    """Round 6 (ainp_conv3x3_dgrad_bnapply): Conv2d(16, 1)'s data gradient
+    (dy [N, 1, H, W]) recomputed and fed through the BatchNorm+ReLU backward
+    apply of the 16-channel layer (y fp32 [N, H, W, 16], sums from
+    conv3x3_dgrad_bnr(want_dx=False)).  Returns (gy, dgamma, dbeta) as
+    bn_relu_bwd_apply(dx, y, ..., cl=True) would (gy16: bf16 storage)."""
+    _req(dy, "dy"); _req(w, "w"); _req(y, "y")
+    N, _, H, W = dy.shape
+    gy = torch.empty(N, H, W, 16, device=dy.device,
+                     dtype=torch.bfloat16 if gy16 else torch.float32)
+    dgamma = torch.empty(16, device=dy.device, dtype=torch.float32)
+    dbeta = torch.empty(16, device=dy.device, dtype=torch.float32)
+    _T.conv3x3_dgrad_bnapply(dy, w, y, scale, shift, gamma, save, sums, int(count), gy, dgamma,
+                             dbeta)
+    return gy, dgamma, dbeta
 
 
 def conv3x3_wgrad(x, dy, in_scale=None, in_shift=None, want_bias=True, bf16=False, out=None,
@@ -1004,6 +1024,25 @@ def bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, count, ntcf=False, 
     _T.bn_relu_bwd_apply(g, y, scale, shift, gamma, save, sums, int(count), gy, dgamma, dbeta,
                          bool(ntcf), (BN_GY16 if gy16 else 0) | _y_flag(y) | flags)
     return gy, dgamma, dbeta
+
+
+def conv3x3_wgrad_bnapply(x, in_scale, in_shift, g, y, scale, shift, gamma, save, sums, count):
+    """Round 6 (ainp_conv3x3_wgrad_bnapply): the Conv2d(1, 16) weight gradient
+    (x [N, 1, H, W]) whose dy is the BatchNorm+ReLU backward apply of its
+    output -- g, y channel-last [N, H, W, 16] fp32 -- formed per element and
+    never written.  Returns (dw, db, dgamma, dbeta): conv3x3_wgrad(x, gy, ...,
+    gcl=True) and bn_relu_bwd_apply(g, y, ..., cl=True)'s dgamma / dbeta."""
+    _req(x, "x"); _req(g, "g"); _req(y, "y")
+    N, _, H, W = x.shape
+    dw = torch.empty(16, 1, 3, 3, device=x.device, dtype=torch.float32)
+    db = torch.empty(16, device=x.device, dtype=torch.float32)
+    dgamma = torch.empty(16, device=x.device, dtype=torch.float32)
+    dbeta = torch.empty(16, device=x.device, dtype=torch.float32)
+    ws = torch.empty(_lib.lib.ainp_conv3x3_wgrad_workspace(N, 1, 16, H, W), device=x.device,
+                     dtype=torch.uint8)
+    _T.conv3x3_wgrad_bnapply(x, in_scale, in_shift, g, y, scale, shift, gamma, save, sums,
+                             int(count), dw, db, dgamma, dbeta, ws)
+    return dw, db, dgamma, dbeta
 
 
 def dy16_ok(N, Cin, Cout, H, W) -> bool:

@@ -1007,13 +1007,37 @@ __global__ __launch_bounds__(256) void conv3x3_strip_wgrad(
 // 16-channel side (16 -> 1 conv, dy one plane); else dy is (1 -> 16).
 constexpr int SWC_TW = 14;         // output columns per wave
 
-template <bool ACL, bool PRO>
+// Round 6, BNA (1 -> 16 only, !ACL): dy is not read but formed per element
+// from the BatchNorm+ReLU backward of the 16-channel layer -- g (the gradient
+// of its output) and y (its pre-BN input), both channel-last fp32 -- with
+// bn_relu_bwd_apply_cl's constants and arithmetic, so the values are that
+// pass's gy bit for bit and gy is never written: the encoder's first conv,
+// whose input needs no gradient, is the only consumer of its gy.
+struct BnApply {
+  const float* g;       // [N][H][W][16]
+  const float* y;       // [N][H][W][16]
+  const float* scale;   // forward BatchNorm scale / shift (ReLU mask)
+  const float* shift;
+  const float* gamma;   // nullable
+  const float* save;    // mean [16], rstd [16]
+  const double* sums;   // [sum gz | sum gz*xhat] (16 each), [2C] = count if inv_count == 0
+  float* dgamma;
+  float* dbeta;
+  double inv_count;
+};
+
+template <bool ACL, bool PRO, bool BNA = false>
 __global__ __launch_bounds__(256) void conv3x3_strip_wgrad_cl(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
-    float* __restrict__ partial, int H, int W, int ntf, int ntt, int ntiles) {
+    float* __restrict__ partial, int H, int W, int ntf, int ntt, int ntiles, BnApply bna = {}) {
+  static_assert(!(BNA && ACL), "the fused BatchNorm apply forms the 16-channel dy");
   constexpr int NOUT = 16 * 9 + (ACL ? 1 : 16);
   const int lane = threadIdx.x & 63, q = lane & 3, pj = lane >> 2;
+  if (BNA && blockIdx.x == 0 && threadIdx.x < 16) {   // as bn_relu_bwd_apply_cl
+    if (bna.dbeta) bna.dbeta[threadIdx.x] = (float)bna.sums[threadIdx.x];
+    if (bna.dgamma) bna.dgamma[threadIdx.x] = (float)bna.sums[16 + threadIdx.x];
+  }
   const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);     // one tile per wave
   if (tile >= ntiles) return;                               // whole waves: no barrier below
   const int tt = tile % ntt, fs = (tile / ntt) % ntf, n = tile / (ntt * ntf);
@@ -1022,8 +1046,26 @@ __global__ __launch_bounds__(256) void conv3x3_strip_wgrad_cl(
   const bool own = pj >= 1 && pj <= SWC_TW && tin;
   const int64_t HW = (int64_t)H * W;
   // the 16-channel side: element (pixel, 4q..4q+3); the 1-channel side: pixel
-  const float* vsrc = (ACL ? x : dy) + ((int64_t)n * HW + t) * 16 + 4 * q;
+  const float* vsrc = (ACL ? x : (BNA ? bna.g : dy)) + ((int64_t)n * HW + t) * 16 + 4 * q;
+  const float* ysrc = BNA ? bna.y + ((int64_t)n * HW + t) * 16 + 4 * q : nullptr;
   const float* ssrc = (ACL ? dy : x) + (int64_t)n * HW + t;
+  // BNA: this lane's four channels' constants (scale, shift, mean, rstd,
+  // k = gamma * rstd, m1, m2), computed as bn_relu_bwd_apply_cl stages them
+  float bc[7][4];
+  if constexpr (BNA) {
+    const double ic = bna.inv_count > 0.0 ? bna.inv_count : 1.0 / bna.sums[32];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * q + e;
+      bc[0][e] = bna.scale[c];
+      bc[1][e] = bna.shift[c];
+      bc[2][e] = bna.save[c];
+      bc[3][e] = bna.save[16 + c];
+      bc[4][e] = (bna.gamma ? bna.gamma[c] : 1.f) * bna.save[16 + c];
+      bc[5][e] = (float)(bna.sums[c] * ic);
+      bc[6][e] = (float)(bna.sums[16 + c] * ic);
+    }
+  }
   float4 sc = make_float4(1.f, 1.f, 1.f, 1.f), sh = make_float4(0.f, 0.f, 0.f, 0.f);
   float ssc = 1.f, ssh = 0.f;
   if (PRO) {
@@ -1063,6 +1105,17 @@ __global__ __launch_bounds__(256) void conv3x3_strip_wgrad_cl(
       const float4 v = ok ? *reinterpret_cast<const float4*>(vsrc + (int64_t)f * W * 16)
                           : make_float4(0.f, 0.f, 0.f, 0.f);
       g[0] = v.x; g[1] = v.y; g[2] = v.z; g[3] = v.w;
+      if constexpr (BNA) {   // gy of the BatchNorm+ReLU backward (0 outside the image)
+        const float4 u = ok ? *reinterpret_cast<const float4*>(ysrc + (int64_t)f * W * 16)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float yv[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float gz = fmaf(yv[e], bc[0][e], bc[1][e]) > 0.f ? g[e] : 0.f;
+          const float o = bc[4][e] * (gz - bc[5][e] - ((yv[e] - bc[2][e]) * bc[3][e]) * bc[6][e]);
+          g[e] = ok ? o : 0.f;
+        }
+      }
     }
   };
   float acc[9][4], accb[4];
@@ -1291,14 +1344,25 @@ __global__ __launch_bounds__(256) void conv3x3_rows_16to1(
 constexpr int R16_TW = 14;   // output columns per wave
 constexpr int R16_RS = 16;   // rows per strip
 
-template <bool DG, bool PRO, bool FZ>
+// OUT (data gradient of Conv2d(16, 1) feeding a BatchNorm+ReLU, decoder.5 ->
+// decoder.6): 0 = store dx; 1 = store nothing (the fused reduce's partials
+// only: the apply pass recomputes dx); 2 / 3 = the BatchNorm+ReLU backward
+// apply of the recomputed dx (bna: constants as bn_relu_bwd_apply_cl forms
+// them, y = bnr.y fp32) stored as gy in fp32 / bf16 -- dx is never written.
+template <bool DG, bool PRO, bool FZ, int OUT = 0>
 __global__ __launch_bounds__(256) void conv3x3_rows_1to16(
     const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ bias,
     const float* __restrict__ in_scale, const float* __restrict__ in_shift,
     float* __restrict__ y, double* __restrict__ stats, Bnr bnr, int H, int W, int nfs, int nts,
-    int nstrips) {
+    int nstrips, BnApply bna = {}) {
+  static_assert(OUT < 2 || (DG && !FZ), "the apply mode is a data gradient without partials");
+  constexpr bool LY = FZ || OUT >= 2;   // y of each output pixel loaded (prefetched a row ahead)
   __shared__ double red[4][32];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, p = lane >> 2, q = lane & 3;
+  if (OUT >= 2 && blockIdx.x == 0 && threadIdx.x < 16) {   // as bn_relu_bwd_apply_cl
+    if (bna.dbeta) bna.dbeta[threadIdx.x] = (float)bna.sums[threadIdx.x];
+    if (bna.dgamma) bna.dgamma[threadIdx.x] = (float)bna.sums[16 + threadIdx.x];
+  }
   const int strip = blockIdx.x * 4 + wave;
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   if (strip < nstrips) {
@@ -1316,7 +1380,7 @@ __global__ __launch_bounds__(256) void conv3x3_rows_1to16(
       bq[c] = (!DG && bias) ? bias[4 * q + c] : 0.f;
     }
     const float sc0 = PRO ? in_scale[0] : 1.f, sh0 = PRO ? in_shift[0] : 0.f;
-    float bsc[4], bsh[4], bmu[4], brs[4];
+    float bsc[4], bsh[4], bmu[4], brs[4], bk[4], bm1[4], bm2[4];
     if constexpr (FZ) {
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
@@ -1324,6 +1388,20 @@ __global__ __launch_bounds__(256) void conv3x3_rows_1to16(
         bsh[c] = bnr.sh[4 * q + c];
         bmu[c] = bnr.save[4 * q + c];
         brs[c] = bnr.save[16 + 4 * q + c];
+      }
+    }
+    if constexpr (OUT >= 2) {   // bn_relu_bwd_apply_cl's staging, per lane
+      const double ic = bna.inv_count > 0.0 ? bna.inv_count : 1.0 / bna.sums[32];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int ch = 4 * q + c;
+        bsc[c] = bna.scale[ch];
+        bsh[c] = bna.shift[ch];
+        bmu[c] = bna.save[ch];
+        brs[c] = bna.save[16 + ch];
+        bk[c] = (bna.gamma ? bna.gamma[ch] : 1.f) * bna.save[16 + ch];
+        bm1[c] = (float)(bna.sums[ch] * ic);
+        bm2[c] = (float)(bna.sums[16 + ch] * ic);
       }
     }
     const int rows = (H - f0) < R16_RS ? (H - f0) : R16_RS;
@@ -1343,14 +1421,14 @@ __global__ __launch_bounds__(256) void conv3x3_rows_1to16(
     wl[1] = __shfl_up(wc[1], 4, 64); wrr[1] = __shfl_down(wc[1], 4, 64);
     float nx0 = ldx(f0 + 1), nx1 = ldx(f0 + 2);   // raw rows f+1, f+2 in flight
     uint4 ny = make_uint4(0u, 0u, 0u, 0u);
-    if (FZ) ny = ldy(f0);
+    if (LY) ny = ldy(f0);
     for (int i = 0; i < rows; ++i) {
       const int f = f0 + i;
       const float cv = act(f + 1, nx0);
       nx0 = nx1;
       nx1 = ldx(f + 3);
       uint4 yc = ny;
-      if (FZ && i + 1 < rows) ny = ldy(f + 1);
+      if (LY && i + 1 < rows) ny = ldy(f + 1);
       wc[2] = cv;
       wl[2] = __shfl_up(cv, 4, 64);
       wrr[2] = __shfl_down(cv, 4, 64);
@@ -1367,8 +1445,24 @@ __global__ __launch_bounds__(256) void conv3x3_rows_1to16(
         o[c] = acc;
       }
       if (own) {
-        *reinterpret_cast<float4*>(y + ((((int64_t)n * H + f) * W) + t) * 16 + 4 * q) =
-            make_float4(o[0], o[1], o[2], o[3]);
+        float* yo = y + ((((int64_t)n * H + f) * W) + t) * 16 + 4 * q;
+        if constexpr (OUT == 0) {
+          *reinterpret_cast<float4*>(yo) = make_float4(o[0], o[1], o[2], o[3]);
+        } else if constexpr (OUT >= 2) {
+          float yv[4], gy[4];
+          bnr_dec4(0, yc, yv);
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const float gz = fmaf(yv[c], bsc[c], bsh[c]) > 0.f ? o[c] : 0.f;
+            gy[c] = bk[c] * (gz - bm1[c] - ((yv[c] - bmu[c]) * brs[c]) * bm2[c]);
+          }
+          if constexpr (OUT == 3) {
+            uint16_t* yb = reinterpret_cast<uint16_t*>(y) + ((((int64_t)n * H + f) * W) + t) * 16 + 4 * q;
+            *reinterpret_cast<uint2*>(yb) = make_uint2(cvt_pk_bf16(gy[0], gy[1]), cvt_pk_bf16(gy[2], gy[3]));
+          } else {
+            *reinterpret_cast<float4*>(yo) = make_float4(gy[0], gy[1], gy[2], gy[3]);
+          }
+        }
         if constexpr (FZ) {
           float yv[4];
           bnr_dec4(bnr.y16, yc, yv);
@@ -1378,7 +1472,7 @@ __global__ __launch_bounds__(256) void conv3x3_rows_1to16(
             s1[c] += gz;
             s2[c] += gz * ((yv[c] - bmu[c]) * brs[c]);
           }
-        } else {
+        } else if constexpr (OUT < 2) {
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             s1[c] += o[c];
@@ -1433,14 +1527,30 @@ static int64_t rows16to1_strips(int64_t N, int64_t H, int64_t W) {
 }
 
 // dw[o] (o < COUT*CIN*9, [co][ci][tap] order) and dbias from the group sums
-__global__ void small_wgrad_final(const double* __restrict__ tmp, int ngroups, int nw, int nout,
-                                  float* __restrict__ dw, float* __restrict__ dbias) {
-  const int o = blockIdx.x * blockDim.x + threadIdx.x;
-  if (o >= nout) return;
-  double s = 0.0;
-  for (int g = 0; g < ngroups; ++g) s += tmp[(int64_t)g * nout + o];
-  if (o < nw) dw[o] = (float)s;
-  else if (dbias) dbias[o - nw] = (float)s;
+// first-stage groups of the small weight gradients' slab sum: their slabs are
+// only 145-160 floats wide, so WG_GROUPS (16) groups left one thread per
+// output summing 430 rows one after another (47 us at the C2 shape, on the
+// critical path at the end of the backward); 128 groups of ~54 rows
+constexpr int SWG_GROUPS = 128, SWG_GROUPS_MAX = 128;
+
+__global__ __launch_bounds__(SWG_GROUPS_MAX) void small_wgrad_final(
+    const double* __restrict__ tmp, int ngroups, int nw, int nout, float* __restrict__ dw,
+    float* __restrict__ dbias) {
+  // one workgroup per output o: group g's partial in thread g, then a fixed
+  // pairwise tree in LDS (round 6: a serial loop over the 128 groups took 32 us)
+  __shared__ double red[SWG_GROUPS_MAX];
+  const int o = blockIdx.x, g = threadIdx.x;
+  red[g] = g < ngroups ? tmp[(int64_t)g * nout + o] : 0.0;
+  __syncthreads();
+  for (int h = SWG_GROUPS_MAX / 2; h > 0; h >>= 1) {
+    if (g < h) red[g] += red[g + h];
+    __syncthreads();
+  }
+  if (g == 0) {
+    const double v = red[0];
+    if (o < nw) dw[o] = (float)v;
+    else if (dbias) dbias[o - nw] = (float)v;
+  }
 }
 
 // (Cin, Cout) pairs with a dedicated small-channel kernel
@@ -1510,10 +1620,12 @@ static int small_fwd_dispatch(bool dgrad, const float* x, const float* w, const 
     if (nb <= N * cdiv(H, CV_FT) * cdiv(W, CV_TT) && ns < ((int64_t)1 << 31)) {
       if (used) *used = nb;
       const bool fz = dgrad && bnr.y && stats;
-#define AINP_R16(DGV, PROV, FZV)                                                                   \
-  hipLaunchKernelGGL((conv3x3_rows_1to16<DGV, PROV, FZV>), dim3((unsigned)nb), dim3(256), 0, s, x, \
-                     w, bias, sc, sh, y, stats, bnr, (int)H, (int)W, nfs, nts, (int)ns)
-      if (dgrad && fz) AINP_R16(true, false, true);
+#define AINP_R16(DGV, PROV, FZV, ...)                                                              \
+  hipLaunchKernelGGL((conv3x3_rows_1to16<DGV, PROV, FZV, ##__VA_ARGS__>), dim3((unsigned)nb),      \
+                     dim3(256), 0, s, x, w, bias, sc, sh, y, stats, bnr, (int)H, (int)W, nfs, nts, \
+                     (int)ns)
+      if (dgrad && fz && !y) AINP_R16(true, false, true, 1);   // partials only (dx recomputed)
+      else if (dgrad && fz) AINP_R16(true, false, true);
       else if (dgrad) AINP_R16(true, false, false);
       else if (sc) AINP_R16(false, true, false);
       else AINP_R16(false, false, false);
@@ -1521,6 +1633,7 @@ static int small_fwd_dispatch(bool dgrad, const float* x, const float* w, const 
       return check_launch("conv3x3_rows_1to16");
     }
   }
+  if (!y) return record_msg("conv3x3: a partials-only data gradient needs the row-strip kernel");
 #define AINP_SF(A, B) \
   if (Cin == A && Cout == B) { launch_small_fwd<A, B>(dgrad, x, w, bias, sc, sh, y, stats, N, H, W, s, lay, bnr); return check_launch("conv3x3_small_fwd"); }
   AINP_SF(1, 16) AINP_SF(2, 16) AINP_SF(16, 1) AINP_SF(16, 2)
@@ -1534,11 +1647,6 @@ static bool small_wgrad_tile_env() {
   return e && e[0] == '1';
 }
 
-// first-stage groups of the small weight gradients' slab sum: their slabs are
-// only 145-160 floats wide, so WG_GROUPS (16) groups left one thread per
-// output summing 430 rows one after another (47 us at the C2 shape, on the
-// critical path at the end of the backward); 128 groups of ~54 rows
-constexpr int SWG_GROUPS = 128;
 
 static int64_t strip_tiles(int64_t N, int64_t H, int64_t W) {
   return N * cdiv(H, SW_RS) * cdiv(W, SW_TW);
@@ -1562,16 +1670,24 @@ static int64_t strip_cl_tiles(int64_t N, int64_t H, int64_t W) {
 // in both layouts
 static int small_wgrad(const float* x, const float* sc, const float* sh, const float* dy,
                        float* dw, float* dbias, void* workspace, int64_t N, int Cin, int Cout,
-                       int64_t H, int64_t W, hipStream_t s, int lay = 0) {
+                       int64_t H, int64_t W, hipStream_t s, int lay = 0,
+                       const BnApply* bna = nullptr) {
   const int nout = Cout * Cin * 9 + Cout;
   float* partial = reinterpret_cast<float*>(workspace);
   int64_t nblk;
   const bool acl = (lay & 1) && Cin == 16, gcl = (lay & 4) && Cout == 16;
+  if (bna && !(gcl && Cin == 1)) return record_msg("conv3x3_wgrad: fused BatchNorm apply: 1 -> 16 only");
   if ((acl && Cout == 1) || (gcl && Cin == 1)) {
     const int ntf = (int)cdiv(H, SW_RS), ntt = (int)cdiv(W, SWC_TW);
     nblk = strip_cl_tiles(N, H, W);
     const dim3 grid((unsigned)cdiv(nblk, 4));
-    if (acl && sc)
+    if (bna && sc)
+      hipLaunchKernelGGL((conv3x3_strip_wgrad_cl<false, true, true>), grid, dim3(256), 0, s, x, sc,
+                         sh, dy, partial, (int)H, (int)W, ntf, ntt, (int)nblk, *bna);
+    else if (bna)
+      hipLaunchKernelGGL((conv3x3_strip_wgrad_cl<false, false, true>), grid, dim3(256), 0, s, x, sc,
+                         sh, dy, partial, (int)H, (int)W, ntf, ntt, (int)nblk, *bna);
+    else if (acl && sc)
       hipLaunchKernelGGL((conv3x3_strip_wgrad_cl<true, true>), grid, dim3(256), 0, s, x, sc, sh,
                          dy, partial, (int)H, (int)W, ntf, ntt, (int)nblk);
     else if (acl)
@@ -1617,7 +1733,7 @@ static int small_wgrad(const float* x, const float* sc, const float* sh, const f
                      (int)nblk, nout, per_group, tmp);
   rc = check_launch("wgrad_reduce1");
   if (rc) return rc;
-  hipLaunchKernelGGL(small_wgrad_final, dim3((nout + 255) / 256), dim3(256), 0, s, tmp, SWG_GROUPS,
+  hipLaunchKernelGGL(small_wgrad_final, dim3(nout), dim3(SWG_GROUPS_MAX), 0, s, tmp, SWG_GROUPS,
                      Cout * Cin * 9, nout, dw, dbias);
   return check_launch("small_wgrad_final");
 }
@@ -1871,8 +1987,12 @@ extern "C" int ainp_conv3x3_dgrad_bnr(const float* dy, const float* w, float* dx
                                       const float* save_mean_rstd, void* workspace, double* sums,
                                       int bn_flags, void* stream) {
   auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
-  if (!dy || !w || !dx || !y || !scale || !shift || !save_mean_rstd || !workspace || !sums ||
-      N < 1 || Cin < 1 || Cout < 1 || H < 1 || W < 1 || N > 65535 ||
+  // dx == nullptr (round 6): the partials only, for the 1 -> 16 data gradient
+  // whose dx the apply recomputes (ainp_conv3x3_dgrad_bnapply)
+  const bool nodx = !dx && small_pair(Cout, Cin) && Cin == 16 && dgrad_bnr_env() &&
+                    !(flags & AINP_CONV_DY16);
+  if (!dy || !w || (!dx && !nodx) || !y || !scale || !shift || !save_mean_rstd || !workspace ||
+      !sums || N < 1 || Cin < 1 || Cout < 1 || H < 1 || W < 1 || N > 65535 ||
       !conv_grad_flags_ok(flags, false) || !(flags & AINP_CONV_YCL) ||
       (bn_flags & ~AINP_BN_Y16) || !(Cin == 16 || Cin == 32 || Cin == 64) ||
       !al16(dx) || !al16(y) || !al16(scale) || !al16(shift) || !al16(save_mean_rstd))
@@ -1902,6 +2022,41 @@ extern "C" int ainp_conv3x3_dgrad_bnr(const float* dy, const float* w, float* dx
   return ainp_bn_relu_bwd_reduce_ex(dx, reinterpret_cast<const float*>(y), scale, shift,
                                     save_mean_rstd, workspace, sums, N, Cin, H, W, 0,
                                     AINP_BN_CL | (bn_flags & AINP_BN_Y16), stream);
+}
+
+// Round 6: Conv2d(16, 1)'s data gradient (dy one channel -> dx 16, decoder.6)
+// through the BatchNorm+ReLU backward apply of the 16-channel layer it feeds
+// (decoder.5), one row-strip pass: gy = apply(dx recomputed, y), dx never
+// written.  The reduce's sums come from ainp_conv3x3_dgrad_bnr with dx null.
+extern "C" int ainp_conv3x3_dgrad_bnapply(const float* dy, const float* w, const float* y,
+                                          const float* scale, const float* shift,
+                                          const float* gamma, const float* save_mean_rstd,
+                                          const double* sums, int64_t count, void* gy, int gy16,
+                                          float* dgamma, float* dbeta, int64_t N, int Cin,
+                                          int Cout, int64_t H, int64_t W, void* stream) {
+  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  const int nfs = (int)cdiv(H > 0 ? H : 1, R16_RS), nts = (int)cdiv(W > 0 ? W : 1, R16_TW);
+  const int64_t ns = N * nfs * nts;
+  if (!dy || !w || !y || !scale || !shift || !save_mean_rstd || !sums || !gy || N < 1 || H < 1 ||
+      W < 1 || Cin != 16 || Cout != 1 || count < 0 || !al16(y) || !al16(gy) ||
+      ns >= ((int64_t)1 << 31) || N * H * W * 16 >= ((int64_t)1 << 40))
+    return record_msg("ainp_conv3x3_dgrad_bnapply: bad argument (Conv2d(16, 1), channel-last "
+                      "16-byte aligned fp32 y, gy)");
+  const Bnr bnr{y, scale, shift, save_mean_rstd, 0};
+  const BnApply bna{nullptr, y, scale, shift, gamma, save_mean_rstd, sums, dgamma, dbeta,
+                    count > 0 ? 1.0 / (double)count : 0.0};
+  const dim3 grid((unsigned)cdiv(ns, 4));
+  if (gy16)
+    hipLaunchKernelGGL((conv3x3_rows_1to16<true, false, false, 3>), grid, dim3(256), 0,
+                       as_stream(stream), dy, w, nullptr, nullptr, nullptr,
+                       reinterpret_cast<float*>(gy), nullptr, bnr, (int)H, (int)W, nfs, nts,
+                       (int)ns, bna);
+  else
+    hipLaunchKernelGGL((conv3x3_rows_1to16<true, false, false, 2>), grid, dim3(256), 0,
+                       as_stream(stream), dy, w, nullptr, nullptr, nullptr,
+                       reinterpret_cast<float*>(gy), nullptr, bnr, (int)H, (int)W, nfs, nts,
+                       (int)ns, bna);
+  return check_launch("conv3x3_rows_1to16 (apply)");
 }
 
 extern "C" int ainp_conv3x3_dy16_ok(int64_t N, int Cin, int Cout, int64_t H, int64_t W) {
@@ -1967,6 +2122,29 @@ extern "C" int ainp_conv3x3_wgrad(const float* x, const float* in_scale,
                                   int64_t W, void* stream) {
   return ainp_conv3x3_wgrad_ex(x, in_scale, in_shift, dy, dw, dbias, workspace, N, Cin, Cout, H,
                                W, 0, stream);
+}
+
+// Round 6: the 1 -> 16 conv's weight gradient with the BatchNorm+ReLU
+// backward apply of its output fused in (conv3x3_strip_wgrad_cl<BNA>): gy is
+// formed per element from g and y instead of read, and never written.
+extern "C" int ainp_conv3x3_wgrad_bnapply(const float* x, const float* in_scale,
+                                          const float* in_shift, const float* g, const float* y,
+                                          const float* scale, const float* shift,
+                                          const float* gamma, const float* save_mean_rstd,
+                                          const double* sums, int64_t count, float* dw,
+                                          float* dbias, float* dgamma, float* dbeta,
+                                          void* workspace, int64_t N, int Cin, int Cout, int64_t H,
+                                          int64_t W, void* stream) {
+  auto al16 = [](const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; };
+  if (!x || !g || !y || !scale || !shift || !save_mean_rstd || !sums || !dw || !workspace ||
+      N < 1 || H < 1 || W < 1 || Cin != 1 || Cout != 16 || count < 0 || !al16(g) || !al16(y) ||
+      (in_scale == nullptr) != (in_shift == nullptr))
+    return record_msg("ainp_conv3x3_wgrad_bnapply: bad argument (Conv2d(1, 16), channel-last "
+                      "16-byte aligned fp32 g / y)");
+  const BnApply bna{g, y, scale, shift, gamma, save_mean_rstd, sums, dgamma, dbeta,
+                    count > 0 ? 1.0 / (double)count : 0.0};
+  return small_wgrad(x, in_scale, in_shift, nullptr, dw, dbias, workspace, N, Cin, Cout, H, W,
+                     as_stream(stream), 4, &bna);
 }
 
 extern "C" int ainp_conv3x3_wgrad_ex(const float* x, const float* in_scale,

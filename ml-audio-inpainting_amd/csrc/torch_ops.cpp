@@ -268,7 +268,9 @@ void conv3x3_dgrad_bnr(const Tensor& dy, const Tensor& w, const Tensor& dx, int6
               "conv3x3_dgrad_bnr: dy [N,Cout,H,W] (channel-last: [N,H,W,Cout]), w [Cout,Cin,3,3]");
   const int64_t N = dy.size(0), Cout = w.size(0), H = dy.size(gcl ? 1 : 2),
                 W = dy.size(gcl ? 2 : 3), Cin = w.size(1);
-  numel_is(dx, N * Cin * H * W, "dx");
+  // an empty dx: the sums only (ainp_conv3x3_dgrad_bnr with dx NULL, round 6)
+  const bool nodx = dx.numel() == 0;
+  if (!nodx) numel_is(dx, N * Cin * H * W, "dx");
   numel_is(y, N * Cin * H * W, "y");
   // the kernels stage 4*Cin BatchNorm constants (scale, shift, mean, rstd)
   numel_is(scale, Cin, "scale");
@@ -281,7 +283,8 @@ void conv3x3_dgrad_bnr(const Tensor& dy, const Tensor& w, const Tensor& dx, int6
                   ainp_conv3x3_dgrad_bnr_workspace(N, (int)Cin, (int)Cout, H, W),
               "conv3x3_dgrad_bnr workspace too small");
   chk(ainp_conv3x3_dgrad_bnr(f32_or_16(dy, "dy", flags & AINP_CONV_DY16), dev(w, "w"),
-                             dev(dx, "dx"), N, (int)Cin, (int)Cout, H, W, (int)flags,
+                             nodx ? nullptr : dev(dx, "dx"), N, (int)Cin, (int)Cout, H, W,
+                             (int)flags,
                              f32_or_16(y, "y", bn_flags & AINP_BN_Y16), dev(scale, "scale"),
                              dev(shift, "shift"), dev(save, "save"), workspace.data_ptr(),
                              dev<double>(sums, "sums", at::kDouble), (int)bn_flags,
@@ -309,6 +312,72 @@ void conv3x3_wgrad(const Tensor& x, const OptT& in_scale, const OptT& in_shift, 
                             workspace.data_ptr(), N, (int)Cin, (int)Cout, H, W, (int)flags,
                             stream_of(x)),
       "conv3x3_wgrad_ex");
+}
+
+// Conv2d(16, 1)'s data gradient through the BatchNorm+ReLU backward apply
+// (ainp_conv3x3_dgrad_bnapply): dy [N,1,H,W], y fp32 / gy [N,H,W,16]
+void conv3x3_dgrad_bnapply(const Tensor& dy, const Tensor& w, const Tensor& y,
+                           const Tensor& scale, const Tensor& shift, const OptT& gamma,
+                           const Tensor& save, const Tensor& sums, int64_t count, const Tensor& gy,
+                           const Tensor& dgamma, const Tensor& dbeta) {
+  GUARD(dy);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(1) == 1 && w.dim() == 4 && w.size(0) == 1 &&
+                  w.size(1) == 16 && y.dim() == 4 && y.size(3) == 16,
+              "conv3x3_dgrad_bnapply: dy [N,1,H,W], w [1,16,3,3], y / gy [N,H,W,16]");
+  const int64_t N = dy.size(0), H = dy.size(2), W = dy.size(3);
+  numel_is(y, N * H * W * 16, "y");
+  numel_is(gy, N * H * W * 16, "gy");
+  numel_is(scale, 16, "scale");
+  numel_is(shift, 16, "shift");
+  numel_is(save, 32, "save");
+  numel_is(dgamma, 16, "dgamma");
+  numel_is(dbeta, 16, "dbeta");
+  TORCH_CHECK(sums.numel() >= 32 && sums.scalar_type() == at::kDouble, "sums: >= 32 doubles");
+  for (const Tensor* t : {&w, &y, &scale, &shift, &save, &sums, &gy, &dgamma, &dbeta})
+    same_device(*t, dy);
+  const bool g16 = gy.scalar_type() == at::kBFloat16;
+  TORCH_CHECK(g16 || gy.scalar_type() == at::kFloat, "gy: float32 or bfloat16");
+  TORCH_CHECK(gy.is_contiguous(), "gy must be contiguous");
+  chk(ainp_conv3x3_dgrad_bnapply(dev(dy, "dy"), dev(w, "w"), dev(y, "y"), dev(scale, "scale"),
+                                 dev(shift, "shift"), opt(gamma, "gamma"), dev(save, "save"),
+                                 dev<double>(sums, "sums", at::kDouble), count, gy.data_ptr(),
+                                 g16 ? 1 : 0, dev(dgamma, "dgamma"), dev(dbeta, "dbeta"), N, 16,
+                                 1, H, W, stream_of(dy)),
+      "conv3x3_dgrad_bnapply");
+}
+
+// the 1 -> 16 weight gradient with the BatchNorm+ReLU backward apply fused
+// (ainp_conv3x3_wgrad_bnapply): x [N,1,H,W], g / y [N,H,W,16] fp32
+void conv3x3_wgrad_bnapply(const Tensor& x, const OptT& in_scale, const OptT& in_shift,
+                           const Tensor& g, const Tensor& y, const Tensor& scale,
+                           const Tensor& shift, const OptT& gamma, const Tensor& save,
+                           const Tensor& sums, int64_t count, const Tensor& dw,
+                           const OptT& dbias, const Tensor& dgamma, const Tensor& dbeta,
+                           const Tensor& workspace) {
+  GUARD(x);
+  TORCH_CHECK(x.dim() == 4 && x.size(1) == 1 && g.dim() == 4 && g.size(3) == 16 &&
+                  g.size(0) == x.size(0) && g.size(1) == x.size(2) && g.size(2) == x.size(3),
+              "conv3x3_wgrad_bnapply: x [N,1,H,W], g / y [N,H,W,16]");
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  numel_is(y, N * H * W * 16, "y");
+  numel_is(dw, 16 * 9, "dw");
+  numel_is(scale, 16, "scale");
+  numel_is(shift, 16, "shift");
+  numel_is(save, 32, "save");
+  numel_is(dgamma, 16, "dgamma");
+  numel_is(dbeta, 16, "dbeta");
+  TORCH_CHECK(sums.numel() >= 32 && sums.scalar_type() == at::kDouble, "sums: >= 32 doubles");
+  for (const Tensor* t : {&g, &y, &scale, &shift, &save, &sums, &dw, &dgamma, &dbeta, &workspace})
+    same_device(*t, x);
+  TORCH_CHECK((size_t)workspace.nbytes() >= ainp_conv3x3_wgrad_workspace(N, 1, 16, H, W),
+              "conv3x3_wgrad_bnapply workspace too small");
+  chk(ainp_conv3x3_wgrad_bnapply(dev(x, "x"), opt(in_scale, "in_scale"), opt(in_shift, "in_shift"),
+                                 dev(g, "g"), dev(y, "y"), dev(scale, "scale"),
+                                 dev(shift, "shift"), opt(gamma, "gamma"), dev(save, "save"),
+                                 dev<double>(sums, "sums", at::kDouble), count, dev(dw, "dw"),
+                                 opt(dbias, "dbias"), dev(dgamma, "dgamma"), dev(dbeta, "dbeta"),
+                                 workspace.data_ptr(), N, 1, 16, H, W, stream_of(x)),
+      "conv3x3_wgrad_bnapply");
 }
 
 // ------------------------------------------------------------------- BatchNorm
@@ -1594,6 +1663,13 @@ TORCH_LIBRARY(ainp, m) {
   m.def("conv3x3_dgrad(Tensor dy, Tensor w, Tensor(a!) dx, int flags) -> ()");
   m.def("conv3x3_dgrad_bnr(Tensor dy, Tensor w, Tensor(a!) dx, int flags, Tensor y, Tensor scale, "
         "Tensor shift, Tensor save, Tensor(b!) workspace, Tensor(c!) sums, int bn_flags) -> ()");
+  m.def("conv3x3_dgrad_bnapply(Tensor dy, Tensor w, Tensor y, Tensor scale, Tensor shift, "
+        "Tensor? gamma, Tensor save, Tensor sums, int count, Tensor(a!) gy, Tensor(b!) dgamma, "
+        "Tensor(c!) dbeta) -> ()");
+  m.def("conv3x3_wgrad_bnapply(Tensor x, Tensor? in_scale, Tensor? in_shift, Tensor g, Tensor y, "
+        "Tensor scale, Tensor shift, Tensor? gamma, Tensor save, Tensor sums, int count, "
+        "Tensor(a!) dw, Tensor(b!)? dbias, Tensor(c!) dgamma, Tensor(d!) dbeta, "
+        "Tensor(e!) workspace) -> ()");
   m.def("conv3x3_wgrad(Tensor x, Tensor? in_scale, Tensor? in_shift, Tensor dy, Tensor(a!) dw, "
         "Tensor(b!)? dbias, Tensor(c!) workspace, int flags) -> ()");
   m.def("bn_stats_reduce(Tensor stats, Tensor(a!) sums, int C) -> ()");
@@ -1724,6 +1800,8 @@ TORCH_LIBRARY_IMPL(ainp, CUDA, m) {
   m.impl("conv3x3_dgrad", &conv3x3_dgrad);
   m.impl("conv3x3_dgrad_bnr", &conv3x3_dgrad_bnr);
   m.impl("conv3x3_wgrad", &conv3x3_wgrad);
+  m.impl("conv3x3_wgrad_bnapply", &conv3x3_wgrad_bnapply);
+  m.impl("conv3x3_dgrad_bnapply", &conv3x3_dgrad_bnapply);
   m.impl("bn_stats_reduce", &bn_stats_reduce);
   m.impl("bn_finalize", &bn_finalize);
   m.impl("bn_reduce_finalize", &bn_reduce_finalize);
@@ -1809,6 +1887,8 @@ TORCH_LIBRARY_IMPL(ainp, Autograd, m) {
   m.impl("conv3x3_dgrad", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_dgrad_bnr", torch::CppFunction::makeFallthrough());
   m.impl("conv3x3_wgrad", torch::CppFunction::makeFallthrough());
+  m.impl("conv3x3_wgrad_bnapply", torch::CppFunction::makeFallthrough());
+  m.impl("conv3x3_dgrad_bnapply", torch::CppFunction::makeFallthrough());
   m.impl("bn_stats_reduce", torch::CppFunction::makeFallthrough());
   m.impl("bn_finalize", torch::CppFunction::makeFallthrough());
   m.impl("bn_reduce_finalize", torch::CppFunction::makeFallthrough());

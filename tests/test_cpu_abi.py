@@ -122,6 +122,13 @@ def test_dy16_routing_query():
     assert rc == -1 and b"YCFNT" in _lib.lib.ainp_last_error()
     rc = _lib.lib.ainp_conv3x3_dgrad_ex(1, 1, 1, None, 1, 16, 32, 8, 8, 256 | 64, None)
     assert rc == -1 and b"bad argument" in _lib.lib.ainp_last_error()
+    # the fused first-conv weight gradient + BatchNorm apply: Conv2d(1, 16) only
+    rc = _lib.lib.ainp_conv3x3_wgrad_bnapply(16, None, None, 16, 16, 16, 16, None, 16, 16, 8, 16,
+                                             16, 16, 16, 16, 1, 16, 32, 8, 8, None)
+    assert rc == -1 and b"wgrad_bnapply" in _lib.lib.ainp_last_error()
+    rc = _lib.lib.ainp_conv3x3_dgrad_bnapply(16, 16, 16, 16, 16, None, 16, 16, 8, 16, 0, 16, 16,
+                                             1, 32, 1, 8, 8, None)
+    assert rc == -1 and b"dgrad_bnapply" in _lib.lib.ainp_last_error()
 
 
 def test_ops_refuse_cpu_tensors():

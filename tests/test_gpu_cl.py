@@ -158,6 +158,70 @@ def test_cl_small_channel_convs(N, H, W, pro):
         assert rel(dw, dw0) < 1e-6 and rel(db, db0) < 1e-6, (cin, cout)
 
 
+@pytest.mark.parametrize("gy16", [False, True])
+@pytest.mark.parametrize("N,H,W", SHAPES)
+def test_dgrad_bnapply_fused_matches_two_pass(N, H, W, gy16):
+    """Round 6: Conv2d(16, 1)'s data gradient with the decoder.5 BatchNorm
+    backward -- conv3x3_dgrad_bnr(want_dx=False) gives the fused path's sums
+    bit for bit, and conv3x3_dgrad_bnapply (dx recomputed, never written)
+    gives the apply's gy within 1e-6 (fp32; bf16 storage: within one bf16
+    rounding) and its dgamma / dbeta exactly; run-to-run identical."""
+    from ainp import ops
+    g_ = torch.Generator(device=DEV).manual_seed(N + H + W)
+    dy = torch.randn(N, 1, H, W, device=DEV, generator=g_)
+    w = torch.randn(1, 16, 3, 3, device=DEV, generator=g_) * 0.2
+    y = torch.randn(N, H, W, 16, device=DEV, generator=g_)
+    sc = torch.rand(16, device=DEV, generator=g_) + 0.5
+    sh = torch.randn(16, device=DEV, generator=g_) * 0.3
+    gamma = torch.rand(16, device=DEV, generator=g_) + 0.5
+    save = torch.stack([torch.randn(16, device=DEV, generator=g_) * 0.1,
+                        torch.rand(16, device=DEV, generator=g_) + 0.5])
+    cnt = N * H * W
+    dx0, s0 = ops.conv3x3_dgrad_bnr(dy, w, y, sc, sh, save)
+    gy0, dg0, db0 = ops.bn_relu_bwd_apply(dx0, y, sc, sh, gamma, save, s0, cnt, gy16=gy16, cl=True)
+    none, s1 = ops.conv3x3_dgrad_bnr(dy, w, y, sc, sh, save, want_dx=False)
+    assert none is None and torch.equal(s1, s0)
+    gy, dg, db = ops.conv3x3_dgrad_bnapply(dy, w, y, sc, sh, gamma, save, s1, cnt, gy16=gy16)
+    assert gy.dtype == gy0.dtype and gy.shape == gy0.shape
+    assert rel(gy.float(), gy0.float()) < (4e-3 if gy16 else 1e-6)
+    assert torch.equal(dg, dg0) and torch.equal(db, db0)
+    gy2, _, _ = ops.conv3x3_dgrad_bnapply(dy, w, y, sc, sh, gamma, save, s1, cnt, gy16=gy16)
+    assert torch.equal(gy2, gy)
+
+
+@pytest.mark.parametrize("N,H,W", SHAPES)
+def test_wgrad_bnapply_fused_matches_two_pass(N, H, W):
+    """Round 6, ops.conv3x3_wgrad_bnapply: the encoder's first conv (1 -> 16)
+    weight gradient forming gy from g and y itself against the apply pass +
+    the channel-last strip weight gradient over the gy it wrote: dw / db within
+    1e-6 (the same terms; only fp contraction may differ), dgamma / dbeta the
+    apply's bit for bit, run-to-run identical; with and without a SyncBN-style
+    count in sums."""
+    from ainp import ops
+    g_ = torch.Generator(device=DEV).manual_seed(H + W)
+    x = torch.randn(N, 1, H, W, device=DEV, generator=g_)
+    g = torch.randn(N, H, W, 16, device=DEV, generator=g_)
+    y = torch.randn(N, H, W, 16, device=DEV, generator=g_)
+    sc = torch.rand(16, device=DEV, generator=g_) + 0.5
+    sh = torch.randn(16, device=DEV, generator=g_) * 0.3
+    gamma = torch.rand(16, device=DEV, generator=g_) + 0.5
+    save = torch.stack([torch.randn(16, device=DEV, generator=g_) * 0.1,
+                        torch.rand(16, device=DEV, generator=g_) + 0.5])
+    sums = ops.bn_relu_bwd_reduce(g, y, sc, sh, save, cl=True)
+    cnt = N * H * W
+    for s_, c_ in ((sums, cnt), (torch.cat([sums, torch.tensor([float(cnt)], device=DEV,
+                                                               dtype=torch.float64)]), 0)):
+        gy, dg0, db0 = ops.bn_relu_bwd_apply(g, y, sc, sh, gamma, save, s_, c_, cl=True)
+        dw0, dbias0 = ops.conv3x3_wgrad(x, gy, gcl=True)
+        dw, dbias, dg, db = ops.conv3x3_wgrad_bnapply(x, None, None, g, y, sc, sh, gamma, save,
+                                                      s_, c_)
+        assert rel(dw, dw0) < 1e-6 and rel(dbias, dbias0) < 1e-6
+        assert torch.equal(dg, dg0) and torch.equal(db, db0)
+        dw2, dbias2, _, _ = ops.conv3x3_wgrad_bnapply(x, None, None, g, y, sc, sh, gamma, save,
+                                                      s_, c_)
+        assert torch.equal(dw2, dw) and torch.equal(dbias2, dbias)
+
+
 @pytest.mark.parametrize("C", [16, 32, 64])
 @pytest.mark.parametrize("store", ["f32", "y16", "g16", "gy16"])
 def test_cl_bn_relu_backward(C, store):
@@ -196,8 +260,9 @@ def test_cl_bn_relu_backward(C, store):
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
 def test_cnnblstm_step_channel_last_matches_nchw(monkeypatch, dtype):
     """One training step of the CNNBLSTM at the C2 plane (N=4) with the
-    channel-last conv stacks (default) and with NCHW (AINP_CL=0): the same
-    loss, every gradient within 2e-4 (fp32) / 2e-3 (bf16)."""
+    channel-last conv stacks (default) and with NCHW (AINP_CL=0): the loss
+    within 1e-6 (fp32) / 1e-4 (bf16), every gradient within 2e-4 (fp32) /
+    5e-2 (bf16, see below)."""
     from ainp import cnnblstm
     cfg = {"data": {"sample_rate": 16000, "spectrogram": {"n_fft": 512, "hop_length": 192,
                                                           "win_length": 384}},
@@ -222,12 +287,23 @@ def test_cnnblstm_step_channel_last_matches_nchw(monkeypatch, dtype):
         torch.cuda.synchronize()
         res.append((float(loss.detach()),
                     {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
-    # the forward is bit-identical (same conv staging and MFMA chains, same
-    # BatchNorm partials); the BatchNorm backward sums in another order, which
-    # the cancellation in gamma*rstd*(gz - mean(gz) - xhat*mean(gz*xhat))
-    # amplifies towards the encoder's first conv (5e-5 there in fp32)
-    tol = 2e-4 if dtype == "fp32" else 2e-3
-    assert res[0][0] == res[1][0]
+    # the forward: the split-bf16 convs are bit-identical (same staging and
+    # MFMA chains, same BatchNorm partials); since round 6 the 1 <-> 16
+    # channel convs run on row strips in the channel-last layout (the 16 -> 1
+    # output and the 1 -> 16 BatchNorm partials summed in another order), so
+    # the loss agrees to fp32 rounding (bf16: to the bf16 rounding points'
+    # flips downstream of those ulps, 1e-4).  The BatchNorm backward sums in
+    # another order, which the cancellation in gamma*rstd*(gz - mean(gz) -
+    # xhat*mean(gz*xhat)) amplifies towards the encoder's first conv (5e-5
+    # there in fp32).  bf16: with the forward no longer bit-identical, a
+    # perturbation of a few fp32 ulps flips single bf16 roundings, and the
+    # pow10 loss concentrates the gradient on its largest outputs, so one flip
+    # there moves whole gradients by up to ~4 % at this N=4 shape (measured
+    # 3.7e-2 max; AINP_SMALL_ROWS=0, the tile kernels on both layouts: within
+    # 2e-3 as before) -- bf16 against the fp32 reference is gated in
+    # test_gpu_model.py
+    tol = 2e-4 if dtype == "fp32" else 5e-2
+    assert abs(res[0][0] - res[1][0]) <= (1e-6 if dtype == "fp32" else 1e-4) * abs(res[1][0])
     errs = {}
     for n, g1 in res[1][1].items():
         if n in ("encoder.0.bias", "encoder.3.bias", "encoder.6.bias", "decoder.0.bias",
@@ -343,6 +419,52 @@ def test_dgrad_bnr_fused_reduce(cin, cout, N, H, W, bf16):
             assert rel(s, s0) < 1e-6, (d.dtype, yy.dtype, rel(s, s0))
             dx2, s2 = ops.conv3x3_dgrad_bnr(d, w, yy, bsc, bsh, save, bf16=bf16, xcl=True)
             assert torch.equal(dx2, dx) and torch.equal(s2, s)
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cnnblstm_step_bn_apply_fusions_match_unfused(monkeypatch, dtype):
+    """Round 6: a CNNBLSTM step with the BatchNorm+ReLU backward applies of
+    the 16-channel layers fused into the 1 <-> 16 convs (cnnblstm.FUSE_BNA0:
+    encoder.0's weight gradient forms gy itself; FUSE_BNA6: decoder.6's data
+    gradient is recomputed into decoder.5's apply) against the unfused passes:
+    the same loss, every gradient within 2e-4 (fp32) / 2e-3 (bf16) -- the
+    same terms, only fp contraction may differ."""
+    from ainp import cnnblstm
+    cfg = {"data": {"sample_rate": 16000, "spectrogram": {"n_fft": 512, "hop_length": 192,
+                                                          "win_length": 384}},
+           "model": {"in_channels": 1, "num_lstm_layers": 2, "lstm_hidden_dim": 128,
+                     "enc_filters": [16, 32], "dec_filters": [16, 32]},
+           "accel": {"dtype": dtype}}
+    g = torch.Generator().manual_seed(9)
+    N, F, T = 4, 257, 334
+    x = (torch.randn(N, 1, F, T, generator=g) - 2.0).to(DEV)
+    mask = torch.zeros(N, F, T)
+    for i in range(N):
+        mask[i, :, 40 + 30 * i:57 + 30 * i] = 1.0
+    mask = mask.to(DEV)
+    tgt = torch.complex(torch.rand(N, F, T, generator=g), torch.rand(N, F, T, generator=g)).to(DEV)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(cnnblstm, "FUSE_BNA0", fused)
+        monkeypatch.setattr(cnnblstm, "FUSE_BNA6", fused)
+        torch.manual_seed(0)
+        m = cnnblstm.StackedBLSTMCNN(config=cfg).to(DEV).train()
+        loss = cnnblstm.l1_pow10_loss(m(x), mask, tgt)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((float(loss.detach()),
+                    {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    tol = 2e-4 if dtype == "fp32" else 2e-3
+    assert res[0][0] == res[1][0]
+    bad = {}
+    for n, g1 in res[1][1].items():
+        if n in ("encoder.0.bias", "encoder.3.bias", "encoder.6.bias", "decoder.0.bias",
+                 "decoder.3.bias"):
+            continue   # BatchNorm-fed conv biases: exact gradient 0 (SURVEY Q10)
+        e = rel(res[0][1][n], g1)
+        if e >= tol:
+            bad[n] = e
+    assert not bad, bad
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
