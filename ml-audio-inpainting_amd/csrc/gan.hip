@@ -875,6 +875,85 @@ __global__ __launch_bounds__(256) void conv_cout1_partial_kernel(ConvGenParams p
   partial[(int64_t)blockIdx.y * np + t] = acc;
 }
 
+// Round 6: the same stage 1 for one plain source (no concatenation, no
+// upsampling; the generator's last PartialConv2d, 64 -> 1, 3 x 3, and the
+// discriminator's logit conv, 512 -> 1, 4 x 4) with every tap's loads of CG
+// channels in flight together: the loop above waits out one load round trip
+// per tap (9 / 16 per chunk; C4: 311 us for the generator's 1.29 M pixels).
+// Each tap keeps its four channel chains (c & 3, c ascending) and the taps are
+// folded in (ky, kx) order with the same fmaf(a, mask, acc), so the partials
+// are bit-identical to conv_cout1_partial_kernel's.  Taps outside the input
+// load a clamped in-image element and are not folded in.
+template <int KT, int CG>
+__global__ __launch_bounds__(256) void conv_cout1_partial_b_kernel(ConvGenParams p, int Hc, int Wc,
+                                                                  float* partial) {
+  constexpr int KK = KT * KT;
+  __shared__ float sw[C1_CC * KK];
+  const int c0 = blockIdx.y * C1_CC;
+  for (int i = threadIdx.x; i < C1_CC * KK; i += blockDim.x) sw[i] = p.w[(int64_t)c0 * KK + i];
+  __syncthreads();
+  const int64_t np = (int64_t)p.N * Hc * Wc;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= np) return;
+  const int n = (int)(t / ((int64_t)Hc * Wc));
+  const int r = (int)(t - (int64_t)n * Hc * Wc);
+  const int oy = r / Wc, ox = r - oy * Wc;
+  const int by = oy * p.stride - p.pad, bx = ox * p.stride - p.pad;
+  const ConvSrcDev& s = p.s0;
+  const int64_t plane = (int64_t)s.Hs * s.Ws;
+  int off[KK];
+  bool ok[KK];
+#pragma unroll
+  for (int ky = 0; ky < KT; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < KT; ++kx) {
+      const int iy = by + ky, ix = bx + kx;
+      const bool v = iy >= 0 && iy < p.Hin && ix >= 0 && ix < p.Win;
+      ok[ky * KT + kx] = v;
+      off[ky * KT + kx] = v ? iy * s.Ws + ix : 0;
+    }
+  // one buffer resource over the source, 32-bit byte offsets (the launcher
+  // checks the tensor is < 2 GB): the pixel's tap offsets per lane, the
+  // channel step as a wave-uniform scalar offset
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(s.x), (short)0, 0x7fffffff, 0x00020000);
+  const int pb = (int)(((int64_t)n * s.C + c0) * plane * 4);
+  int vo[KK];
+#pragma unroll
+  for (int k = 0; k < KK; ++k) vo[k] = pb + off[k] * 4;
+  int cstep = (int)(plane * 4);
+  asm volatile("" : "+s"(cstep));
+  float a4[KK][4];
+#pragma unroll
+  for (int k = 0; k < KK; ++k) a4[k][0] = a4[k][1] = a4[k][2] = a4[k][3] = 0.f;
+#pragma unroll 1
+  for (int cg = 0; cg < C1_CC; cg += CG) {
+    float v[CG][KK];
+#pragma unroll
+    for (int c = 0; c < CG; ++c)
+#pragma unroll
+      for (int k = 0; k < KK; ++k)
+        v[c][k] = __uint_as_float(
+            __builtin_amdgcn_raw_buffer_load_b32(rx, vo[k], (cg + c) * cstep, 0));
+#pragma unroll
+    for (int c = 0; c < CG; ++c)
+#pragma unroll
+      for (int k = 0; k < KK; ++k) {
+        // CG % 4 == 0, so channel cg + c's chain is c & 3 (compile-time)
+        a4[k][c & 3] = fmaf(sw[(cg + c) * KK + k], v[c][k], a4[k][c & 3]);
+      }
+  }
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < KK; ++k) {
+    if (!ok[k]) continue;
+    const float a = (a4[k][0] + a4[k][1]) + (a4[k][2] + a4[k][3]);
+    const float mv = s.m ? s.m[(int64_t)n * plane + off[k]] : 1.f;
+    acc = fmaf(a, mv, acc);
+  }
+  partial[(int64_t)blockIdx.y * np + t] = acc;
+}
+
 __global__ void conv_cout1_finish_kernel(ConvGenParams p, int act, int Hc, int Wc, int nchunk,
                                          const float* partial) {
   const int64_t np = (int64_t)p.N * Hc * Wc;
@@ -2641,8 +2720,23 @@ extern "C" int ainp_conv_gen_fwd_out16(const float* x0, const float* m0, int C0,
     const int64_t np = N * (int64_t)Hc * Wc;
     const int nchunk = (int)cdiv(p.Cin, C1_CC);
     float* part = reinterpret_cast<float*>(workspace);
-    hipLaunchKernelGGL(conv_cout1_partial_kernel, dim3((unsigned)cdiv(np, 256), nchunk), dim3(256),
-                       0, s, p, Hc, Wc, part);
+    // one plain source, whole 32-channel chunks, square 3 / 4 kernels: the
+    // batched-tap variant (AINP_COUT1_B=0: the loop kernel, A/B)
+    static const bool c1b = [] {
+      const char* e = getenv("AINP_COUT1_B");
+      return !(e && e[0] == '0');
+    }();
+    const bool plain = p.s1.C == 0 && p.s0.up == 0 && p.Cin % C1_CC == 0 && KH == KW &&
+                       (int64_t)N * p.Cin * p.s0.Hs * p.s0.Ws * 4 < ((int64_t)1 << 31);
+    if (c1b && plain && KH == 3)
+      hipLaunchKernelGGL((conv_cout1_partial_b_kernel<3, 4>), dim3((unsigned)cdiv(np, 256), nchunk),
+                         dim3(256), 0, s, p, Hc, Wc, part);
+    else if (c1b && plain && KH == 4)
+      hipLaunchKernelGGL((conv_cout1_partial_b_kernel<4, 4>), dim3((unsigned)cdiv(np, 256), nchunk),
+                         dim3(256), 0, s, p, Hc, Wc, part);
+    else
+      hipLaunchKernelGGL(conv_cout1_partial_kernel, dim3((unsigned)cdiv(np, 256), nchunk),
+                         dim3(256), 0, s, p, Hc, Wc, part);
     hipLaunchKernelGGL(conv_cout1_finish_kernel, dim3((unsigned)cdiv(np, 256)), dim3(256), 0, s, p,
                        act, Hc, Wc, nchunk, part);
     return check_launch("conv_cout1");
