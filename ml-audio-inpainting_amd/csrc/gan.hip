@@ -2118,7 +2118,7 @@ struct Cfg {
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 2) & 3); }
 }  // namespace cgw
 
-template <int BM, int NW, bool EXP>
+template <int BM, int NW, bool EXP, bool PF = true>
 __global__ __launch_bounds__(NW * 64, 2) void conv_gen_nhwc16_wide_kernel(ConvGenParams p, Src16 s0,
                                                                       Src16 s1,
                                                                       const uint16_t* __restrict__ wt16,
@@ -2249,24 +2249,40 @@ __global__ __launch_bounds__(NW * 64, 2) void conv_gen_nhwc16_wide_kernel(ConvGe
     if (kt + cgw::NST - 1 < kt_end) issue(kt + cgw::NST - 1);
     const unsigned char* sa = ring + (kt % cgw::NST) * C::STAGE;
     const unsigned char* sb = sa + IMGA;
+    // round 6 (PF): both k-steps' fragments read up front, the second
+    // k-step's reads overlapping the first one's MFMAs (!PF, AINP_WIDE_PF=0:
+    // each k-step's read right before its MFMAs) -- the same MFMAs in the
+    // same order either way
+    cgx::bf16x8 a[2][MI], b[2][NJ];
 #pragma unroll
     for (int st = 0; st < CG_BK / 16; ++st) {
-      cgx::bf16x8 a[MI], b[NJ];
+      if (!PF && st > 0) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[st - 1][i], b[st - 1][j],
+                                                                acc[i][j], 0, 0, 0);
+      }
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         const int rb = wn * C::WNP + j * 32 + l31;
-        b[j] = cgx::frag(sb + rb * cgw::ROWB + 16 * cgw::swz(rb + BM, 2 * st + lh));
+        b[st][j] = cgx::frag(sb + rb * cgw::ROWB + 16 * cgw::swz(rb + BM, 2 * st + lh));
       }
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int ra = wm * C::WM + i * 32 + l31;
-        a[i] = cgx::frag(sa + ra * cgw::ROWB + 16 * cgw::swz(ra, 2 * st + lh));
+        a[st][i] = cgx::frag(sa + ra * cgw::ROWB + 16 * cgw::swz(ra, 2 * st + lh));
       }
+    }
+#pragma unroll
+    for (int st = PF ? 0 : CG_BK / 16 - 1; st < CG_BK / 16; ++st) {
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[st][i], b[st][j], acc[i][j], 0,
+                                                              0, 0);
     }
   }
   __syncthreads();     // every wave done with the ring: the epilogue reuses it
@@ -2997,9 +3013,23 @@ extern "C" int ainp_conv_gen_fwd_nhwc16_ex(const uint16_t* x0, int C0, int H0, i
 #define AINP_CGW(BMV, NWV, EXPV)                                                                 \
   hipLaunchKernelGGL((conv_gen_nhwc16_wide_kernel<BMV, NWV, EXPV>), gw, dim3(NWV * 64), 0, s, p, a, \
                      b, wt16, act, tco, tpx)
+    static const bool wide_pf = [] {
+      const char* e = getenv("AINP_WIDE_PF");
+      return !(e && e[0] == '0');
+    }();
+#define AINP_CGW8(BMV, EXPV)                                                                      \
+  do {                                                                                           \
+    if (wide_pf)                                                                                 \
+      hipLaunchKernelGGL((conv_gen_nhwc16_wide_kernel<BMV, 8, EXPV, true>), gw, dim3(512), 0, s, p, \
+                         a, b, wt16, act, tco, tpx);                                             \
+    else                                                                                         \
+      hipLaunchKernelGGL((conv_gen_nhwc16_wide_kernel<BMV, 8, EXPV, false>), gw, dim3(512), 0, s,  \
+                         p, a, b, wt16, act, tco, tpx);                                          \
+  } while (0)
     if (variant == 3 && BW > 64) {
-      if (BW == 256) { if (exp) AINP_CGW(256, 8, true); else AINP_CGW(256, 8, false); }
-      else { if (exp) AINP_CGW(128, 8, true); else AINP_CGW(128, 8, false); }
+      if (BW == 256) { if (exp) AINP_CGW8(256, true); else AINP_CGW8(256, false); }
+      else { if (exp) AINP_CGW8(128, true); else AINP_CGW8(128, false); }
+#undef AINP_CGW8
     } else if (BW == 256) { if (exp) AINP_CGW(256, 4, true); else AINP_CGW(256, 4, false); }
     else if (BW == 128) { if (exp) AINP_CGW(128, 4, true); else AINP_CGW(128, 4, false); }
     else { if (exp) AINP_CGW(64, 4, true); else AINP_CGW(64, 4, false); }
