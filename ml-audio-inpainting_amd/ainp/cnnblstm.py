@@ -467,7 +467,7 @@ class _BLSTMFn(torch.autograd.Function):
         # the BLSTM's weight gradients: on their own side stream (BLSTM_SIDE2),
         # so they start right behind their recurrence instead of queueing
         # behind the deferred decoder weight gradients
-        side = _side_stream(dh.device, 1 if BLSTM_SIDE2 else 0)
+        side = _side_stream(dh.device, 1 if _blstm_side2(bf16) else 0)
         # data parallel: the side stream's weight / bias gradients are
         # all-reduced from the side stream as they are produced, so the compute
         # stream never waits for them (AccumulateGrad stores non-view aliases)
@@ -731,8 +731,17 @@ DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "1") != "0"
 # stream (hipExtStreamCreateWithCUMask, 8 of 32 CUs kept free for the
 # recurrence) measured +3.3 ms/step on both and was dropped.
 DEFER_EARLY = os.environ.get("AINP_DEFER_EARLY", "1") != "0"
-# (C2 14.65 -> 14.43 / 14.79 -> 14.55 ms/step A/B, profiles/r05o_ab_x6r_apf_side2.txt)
-BLSTM_SIDE2 = os.environ.get("AINP_BLSTM_SIDE2", "1") != "0"
+# (C2 14.65 -> 14.43 / 14.79 -> 14.55 ms/step A/B, profiles/r05o_ab_x6r_apf_side2.txt).
+# Round 6: AINP_BLSTM_SIDE2 = 0 / 1 / fp32 (default) / bf16 -- in the bf16
+# configuration the second stream's GEMMs slowed the layer-0 BPTT beside them
+# (0.31 -> up to 0.48 ms) more than queueing them behind the deferred work
+# costs: C3 6.89 / 6.91 -> 6.86 / 6.81 ms/step, C2 13.53 -> 14.02 without it
+# (profiles/r06_ab_blstm_side2.txt)
+BLSTM_SIDE2 = os.environ.get("AINP_BLSTM_SIDE2", "fp32")
+
+
+def _blstm_side2(bf16):
+    return BLSTM_SIDE2 == "1" or BLSTM_SIDE2 == ("bf16" if bf16 else "fp32")
 # Round 6: AINP_ENC_SIDE2 = 0 / 1 / fp32 / bf16: in which configurations the
 # encoder's inner weight gradients use the second side stream (idle by then),
 # so the 16 -> 32 one starts behind its own data gradient instead of behind
