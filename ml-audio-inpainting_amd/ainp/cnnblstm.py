@@ -735,13 +735,15 @@ DEFER_EARLY = os.environ.get("AINP_DEFER_EARLY", "1") != "0"
 # Round 6: AINP_BLSTM_SIDE2 = 0 / 1 / fp32 (default) / bf16 -- in the bf16
 # configuration the second stream's GEMMs slowed the layer-0 BPTT beside them
 # (0.31 -> up to 0.48 ms) more than queueing them behind the deferred work
-# costs: C3 6.89 / 6.91 -> 6.86 / 6.81 ms/step, C2 13.53 -> 14.02 without it
-# (profiles/r06_ab_blstm_side2.txt)
+# costs: C3 6.89 / 6.91 -> 6.86 / 6.81 and, on a second box, 6.88 / 6.82 ->
+# 6.76 / 6.74 ms/step; C2 13.53 -> 14.02 without it (profiles/r06_ab_blstm_side2.txt)
 BLSTM_SIDE2 = os.environ.get("AINP_BLSTM_SIDE2", "fp32")
 
 
 def _blstm_side2(bf16):
     return BLSTM_SIDE2 == "1" or BLSTM_SIDE2 == ("bf16" if bf16 else "fp32")
+
+
 # Round 6: AINP_ENC_SIDE2 = 0 / 1 / fp32 / bf16: in which configurations the
 # encoder's inner weight gradients use the second side stream (idle by then),
 # so the 16 -> 32 one starts behind its own data gradient instead of behind
