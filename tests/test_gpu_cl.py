@@ -48,6 +48,9 @@ def _data(N, cin, cout, H, W, seed):
 
 PAIRS = [(16, 32), (32, 64), (32, 16)]
 SHAPES = [(2, 257, 334), (1, 19, 47)]
+# round 6's row-strip kernels (16 / 14 columns and 16 rows per strip): a lone
+# pixel, strips narrower than one wave, exactly one strip, one row past it
+EDGE_SHAPES = [(1, 1, 1), (2, 3, 5), (1, 16, 14), (3, 17, 15)]
 
 
 @pytest.mark.parametrize("bf16", [False, True])
@@ -115,7 +118,7 @@ def test_dgrad_cfnt_bit_identical(N, H, W, bf16):
                           xcl=True, cfnt=True)
 
 
-@pytest.mark.parametrize("N,H,W", SHAPES)
+@pytest.mark.parametrize("N,H,W", SHAPES + EDGE_SHAPES)
 @pytest.mark.parametrize("pro", [True, False])
 def test_cl_small_channel_convs(N, H, W, pro):
     """1 -> 16 and 16 -> 1 (encoder.0, decoder.6): forward and data gradient
@@ -159,7 +162,7 @@ def test_cl_small_channel_convs(N, H, W, pro):
 
 
 @pytest.mark.parametrize("gy16", [False, True])
-@pytest.mark.parametrize("N,H,W", SHAPES)
+@pytest.mark.parametrize("N,H,W", SHAPES + EDGE_SHAPES)
 def test_dgrad_bnapply_fused_matches_two_pass(N, H, W, gy16):
     """Round 6: Conv2d(16, 1)'s data gradient with the decoder.5 BatchNorm
     backward -- conv3x3_dgrad_bnr(want_dx=False) gives the fused path's sums
@@ -189,7 +192,7 @@ def test_dgrad_bnapply_fused_matches_two_pass(N, H, W, gy16):
     assert torch.equal(gy2, gy)
 
 
-@pytest.mark.parametrize("N,H,W", SHAPES)
+@pytest.mark.parametrize("N,H,W", SHAPES + EDGE_SHAPES)
 def test_wgrad_bnapply_fused_matches_two_pass(N, H, W):
     """Round 6, ops.conv3x3_wgrad_bnapply: the encoder's first conv (1 -> 16)
     weight gradient forming gy from g and y itself against the apply pass +
