@@ -1798,11 +1798,12 @@ static bool wgrad16_dma() {
 //    (8 consecutive pixels) and the reads (two groups 8 pixels apart, the
 //    halo row stride being == 8 mod 16) conflict-free.
 namespace wx6s {
-constexpr int FT = 4, TT = 24, NPX = FT * TT;  // 96 pixels, 3 k-steps of 32
-constexpr int HR = FT + 2, HC = TT + 2;
+constexpr int TT = 24, HC = TT + 2;            // tile columns (3 segments of 8), halo columns
 constexpr int HS = 40;                         // halo row stride (pixels, == 8 mod 16)
-constexpr int XPL = ((HR - 1) * HS + HC) * 64;
-constexpr int GPL = NPX * 64;
+// FT tile rows: NPX = 24 FT pixels, 3 FT / 4 k-steps of 32
+template <int FT> constexpr int npx() { return FT * TT; }
+template <int FT> constexpr int xpl() { return (FT + 1) * HS * 64 + HC * 64; }
+template <int FT> constexpr int gpl() { return npx<FT>() * 64; }
 }  // namespace wx6s
 
 __device__ __forceinline__ int wx6s_swz(int px) {
@@ -1810,17 +1811,19 @@ __device__ __forceinline__ int wx6s_swz(int px) {
 }
 
 template <int CP, int CO, int NP, bool G16 = false, bool XG16 = false, bool XL = false,
-          bool GL = false>
-__global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
+          bool GL = false, int FT = 4>
+__global__ __launch_bounds__(384, FT == 4 ? 3 : NP == 1 ? 2 : 1) void conv3x3_wgrad_x6s(
     const float* __restrict__ x, const float* __restrict__ in_scale,
     const float* __restrict__ in_shift, const float* __restrict__ dy,
     float* __restrict__ partial, int N, int Cin, int H, int W, int ci0) {
   using namespace wx6s;
   static_assert((CP == 32 && CO == 16) || (CP == 16 && CO == 32), "shape");
+  constexpr int NPX = npx<FT>(), HR = FT + 2, XPL = xpl<FT>(), GPL = gpl<FT>();
   constexpr int J = 9 * CP, NT = 384;
   constexpr int XG = CP / 8, XU = HR * HC * XG, XI = (XU + NT - 1) / NT;
   constexpr int GG = CO / 8, GU = NPX * GG;     // dy units (pixel, 8-co group)
-  static_assert(GU <= NT, "one dy unit per thread");
+  constexpr int GI = (GU + NT - 1) / NT;         // dy units per thread (unit tid + NT i)
+  static_assert(NT % NPX == 0 && NT % GG == 0, "a thread's dy units share a pixel (NCHW) / a group (CL)");
   // sx doubles as the bias reduction buffer [CO][NPX] floats after the loop
   constexpr int SXB = NP * XPL > CO * NPX * 4 ? NP * XPL : CO * NPX * 4;
   __shared__ __attribute__((aligned(16))) unsigned char sx[SXB];
@@ -1846,9 +1849,11 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
   f32x4 acc[3];
 #pragma unroll
   for (int t = 0; t < 3; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float bsum[8];
+  float bsum[GI][8];
 #pragma unroll
-  for (int c = 0; c < 8; ++c) bsum[c] = 0.f;
+  for (int i = 0; i < GI; ++i)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bsum[i][c] = 0.f;
 
   const int tiles_t = (W + TT - 1) / TT, tiles_f = (H + FT - 1) / FT;
   const int64_t ntiles = (int64_t)N * tiles_f * tiles_t;
@@ -1858,9 +1863,13 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     f0 = (int)((tile / tiles_t) % tiles_f) * FT;
     n = (int)(tile / ((int64_t)tiles_t * tiles_f));
   };
-  // this thread's dy unit (if tid < GU): pixel and 8-channel group; the
-  // channel-last order puts a pixel's groups on consecutive lanes
-  const int gpx = GL ? tid / GG : tid % NPX, ggrp = GL ? tid % GG : tid / NPX;
+  // dy unit i of this thread (unit tid + NT i < GU): pixel and 8-channel
+  // group; the channel-last order puts a pixel's groups on consecutive lanes
+  auto gunit = [&](int i, int& px_, int& grp_) {
+    const int gu = tid + NT * i;
+    px_ = GL ? gu / GG : gu % NPX;
+    grp_ = GL ? gu % GG : gu / NPX;
+  };
   auto xunit = [&](int u, int& hp_, int& grp_) {
     if constexpr (XL) {
       hp_ = u / XG;
@@ -1871,7 +1880,7 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     }
   };
 
-  float px[XI][8], pg[8];
+  float px[XI][8], pg[GI][8];
   auto fetch = [&](int64_t tile) {
     int n, f0, t0;
     tile_coords(tile, n, f0, t0);
@@ -1905,18 +1914,23 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
     }
     // dy: fp32 or bf16 storage (G16)
     constexpr int GES = act_es<G16>();
-    const int gpc = gpx < NPX ? gpx : NPX - 1;
-    const int gr = wx6_clamp(f0 + gpc / TT, 0, H - 1), gc = wx6_clamp(t0 + gpc % TT, 0, W - 1);
-    if constexpr (GL) {
-      const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * HW * CO);
-      cl_ld8<G16>(rg, ((gr * W + gc) * CO + 8 * (ggrp < GG ? ggrp : GG - 1)) * GES, pg);
-    } else {
-      int gplane = (int)(HW * GES);
-      asm volatile("" : "+s"(gplane));
-      const __amdgpu_buffer_rsrc_t rg = act_rsrc<G16>(dy, (int64_t)n * CO * HW);
-      const int vo = 8 * (ggrp < GG ? ggrp : GG - 1) * gplane + (gr * W + gc) * GES;
+    int gplane = (int)(HW * GES);
+    asm volatile("" : "+s"(gplane));
+    const __amdgpu_buffer_rsrc_t rg =
+        act_rsrc<G16>(dy, GL ? (int64_t)n * HW * CO : (int64_t)n * CO * HW);
 #pragma unroll
-      for (int c = 0; c < 8; ++c) pg[c] = act_ld<G16>(rg, vo, c * gplane);
+    for (int i = 0; i < GI; ++i) {
+      int gpx, ggrp;
+      gunit(i, gpx, ggrp);
+      const int gpc = gpx < NPX ? gpx : NPX - 1, ggc = ggrp < GG ? ggrp : GG - 1;
+      const int gr = wx6_clamp(f0 + gpc / TT, 0, H - 1), gc = wx6_clamp(t0 + gpc % TT, 0, W - 1);
+      if constexpr (GL) {
+        cl_ld8<G16>(rg, ((gr * W + gc) * CO + 8 * ggc) * GES, pg[i]);
+      } else {
+        const int vo = 8 * ggc * gplane + (gr * W + gc) * GES;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) pg[i][c] = act_ld<G16>(rg, vo, c * gplane);
+      }
     }
   };
   auto commit = [&](int64_t tile) {
@@ -1942,15 +1956,20 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
         cx6_stage<NP>(v, sx + sp * 64 + 16 * (grp ^ wx6s_swz(sp)), XPL);
       }
     }
-    if (tid < GU) {
-      const bool pok = f0 + gpx / TT < H && t0 + gpx % TT < W;
-      float v[8];
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        v[c] = pok ? pg[c] : 0.f;
-        bsum[c] += v[c];
+    for (int i = 0; i < GI; ++i) {
+      if (tid + NT * i < GU) {
+        int gpx, ggrp;
+        gunit(i, gpx, ggrp);
+        const bool pok = f0 + gpx / TT < H && t0 + gpx % TT < W;
+        float v[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          v[c] = pok ? pg[i][c] : 0.f;
+          bsum[i][c] += v[c];
+        }
+        cx6_stage<NP>(v, sg + gpx * 64 + 16 * (ggrp ^ wx6s_swz(gpx)), GPL);
       }
-      cx6_stage<NP>(v, sg + gpx * 64 + 16 * (ggrp ^ wx6s_swz(gpx)), GPL);
     }
   };
 
@@ -2004,9 +2023,14 @@ __global__ __launch_bounds__(384, 3) void conv3x3_wgrad_x6s(
       slab[co * (J + 1) + (3 * dyt + dx) * CP + 16 * cib + (lane & 15)] = acc[dx][r];
     }
   float* red = reinterpret_cast<float*>(sx);
-  if (tid < GU) {
 #pragma unroll
-    for (int c = 0; c < 8; ++c) red[(8 * ggrp + c) * NPX + gpx] = bsum[c];
+  for (int i = 0; i < GI; ++i) {
+    if (tid + NT * i < GU) {
+      int gpx, ggrp;
+      gunit(i, gpx, ggrp);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) red[(8 * ggrp + c) * NPX + gpx] = bsum[i][c];
+    }
   }
   __syncthreads();
   if (tid < CO) {
@@ -2756,6 +2780,22 @@ int conv_x6p_launch(bool dgrad, const float* x, const float* w, const float* bia
   return 1;
 }
 
+// conv3x3_wgrad_x6s tile rows, per plane count (AINP_X6S_FT1 for the bf16
+// configuration's NP = 1: 4, 8 or 16; AINP_X6S_FT3 for NP = 3: 4 or 8).
+// Defaults from profiles/r06_x6s_ft_lab.txt (standalone, C2 shape): NP = 3
+// 8-row tiles 0.304 -> 0.262 ms (16 -> 32) and 0.338 -> 0.293 ms (32 -> 16),
+// one workgroup per CU (111 KB of LDS); C2 14.16 -> 14.07 ms/step on one box
+// (profiles/r06_ab_x6s_ft.txt).  NP = 1: 4 rows stay fastest (0.166 ms vs
+// 0.210 / 0.201).
+static int x6s_ft(int np) {
+  auto rd = [](const char* name, int def) {
+    const char* e = getenv(name);
+    const int v = e ? atoi(e) : def;
+    return v == 8 || v == 16 ? v : 4;
+  };
+  return np == 1 ? rd("AINP_X6S_FT1", 4) : rd("AINP_X6S_FT3", 8);   // read per launch (tests)
+}
+
 // the split-bf16 weight-gradient kernels of one pass (NP planes, storage
 // G16 / XG16) for the (cp, Cout) pair; returns 1 if it has none
 template <int NP, bool G16, bool XG16>
@@ -2763,15 +2803,23 @@ static int wgrad_x6_go(const float* x, const float* sc, const float* sh, const f
                        float* partial, int64_t N, int Cin, int Cout, int64_t H, int64_t W,
                        int ci0, int cp, int grid, hipStream_t s, int lay) {
   int rc = 1;
+  const int ft = x6s_ft(NP);
   auto go = [&](auto xlc, auto glc) {
     constexpr bool XL = decltype(xlc)::value, GL = decltype(glc)::value;
-    if (cp == 32 && Cout == 16) {
-      hipLaunchKernelGGL((conv3x3_wgrad_x6s<32, 16, NP, G16, XG16, XL, GL>), dim3(grid),
-                         dim3(384), 0, s, x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
-      rc = check_launch("conv3x3_wgrad_x6s");
-    } else if (cp == 16 && Cout == 32) {
-      hipLaunchKernelGGL((conv3x3_wgrad_x6s<16, 32, NP, G16, XG16, XL, GL>), dim3(grid),
-                         dim3(384), 0, s, x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0);
+    if ((cp == 32 && Cout == 16) || (cp == 16 && Cout == 32)) {
+#define AINP_X6S(CPV, COV, FTV)                                                                  \
+  hipLaunchKernelGGL((conv3x3_wgrad_x6s<CPV, COV, NP, G16, XG16, XL, GL, FTV>), dim3(grid),     \
+                     dim3(384), 0, s, x, sc, sh, dy, partial, (int)N, Cin, (int)H, (int)W, ci0)
+      if (cp == 32) {
+        if (NP == 1 && ft == 16) AINP_X6S(32, 16, NP == 1 ? 16 : 8);
+        else if (ft == 8) AINP_X6S(32, 16, 8);
+        else AINP_X6S(32, 16, 4);
+      } else {
+        if (NP == 1 && ft == 16) AINP_X6S(16, 32, NP == 1 ? 16 : 8);
+        else if (ft == 8) AINP_X6S(16, 32, 8);
+        else AINP_X6S(16, 32, 4);
+      }
+#undef AINP_X6S
       rc = check_launch("conv3x3_wgrad_x6s");
     } else if (cp == 32 && Cout == 64) {
       hipLaunchKernelGGL((conv3x3_wgrad_x6<64, NP, G16, XG16, XL, GL>), dim3(grid), dim3(384), 0,

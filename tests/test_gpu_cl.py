@@ -539,3 +539,38 @@ def test_wgrad16_dma_matches_register_kernel(N, H, W, pro):
     dwr = torch.nn.grad.conv2d_weight(xa, w.shape, dy16.double(), padding=1)
     assert rel(dw, dwr) < 2e-5, rel(dw, dwr)
     assert rel(db, dy16.double().sum((0, 2, 3))) < 1e-6
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+@pytest.mark.parametrize("N,H,W", SHAPES + [(3, 17, 15), (1, 1, 1)])
+@pytest.mark.parametrize("cin,cout", [(16, 32), (32, 16)])
+def test_wgrad_x6s_tile_rows(monkeypatch, cin, cout, N, H, W, bf16):
+    """Round 6: conv3x3_wgrad_x6s (the 16 <-> 32 channel weight gradients) on
+    4-, 8- and 16-row tiles (AINP_X6S_FT3 / _FT1; NP = 3 defaults to 8 rows,
+    NP = 1 to 4, 16 rows only with one plane).  Another tile partition sums
+    the slabs in another fixed order: dw / db within 1e-5 of the 4-row tiles,
+    run-to-run identical, and within 1e-5 (fp32) / 2e-5 (bf16 operands) of an
+    fp64 weight gradient; channel-last and NCHW launches bit-identical."""
+    from ainp import ops
+    x, dy, w, b, sc, sh = _data(N, cin, cout, H, W, 77 + cin + H)
+    if bf16:
+        dy = dy.to(torch.bfloat16)
+    key, fts = ("AINP_X6S_FT1", (4, 8, 16)) if bf16 else ("AINP_X6S_FT3", (4, 8))
+    xa = torch.relu(torch.addcmul(sh.view(1, -1, 1, 1), x, sc.view(1, -1, 1, 1)))
+    if bf16:   # the kernels stage act(x) rounded to bf16
+        xa = xa.to(torch.bfloat16)
+    dwr = torch.nn.grad.conv2d_weight(xa.double(), w.shape, dy.double(), padding=1)
+    dbr = dy.double().sum((0, 2, 3))
+    ref = None
+    for ft in fts:
+        monkeypatch.setenv(key, str(ft))
+        dw, db = ops.conv3x3_wgrad(_cl(x), _cl(dy), sc, sh, bf16=bf16, xcl=True, gcl=True)
+        dw2, db2 = ops.conv3x3_wgrad(_cl(x), _cl(dy), sc, sh, bf16=bf16, xcl=True, gcl=True)
+        dwn, dbn = ops.conv3x3_wgrad(x, dy, sc, sh, bf16=bf16)
+        assert torch.equal(dw, dw2) and torch.equal(db, db2), ft
+        assert torch.equal(dw, dwn) and torch.equal(db, dbn), ft
+        assert rel(dw, dwr) < (2e-5 if bf16 else 1e-5), (ft, rel(dw, dwr))
+        assert rel(db, dbr) < 1e-6, (ft, rel(db, dbr))
+        if ref is None:
+            ref = (dw, db)
+        assert rel(dw, ref[0]) < 1e-5 and rel(db, ref[1]) < 1e-5, ft
