@@ -405,8 +405,8 @@ def spawn_ranks(n):
 # profiles/steps/ so they travel with gpurun / the driver's snapshot
 # (.gpurunignore drops profiles/r0*)
 STEP_TABLES = {
-    ("cnnblstm", "fp32"): ("profiles/steps/r06x_cnn_fp32_step_kernel_stats.csv", 13),
-    ("cnnblstm", "bf16"): ("profiles/steps/r06x_cnn_bf16_step_kernel_stats.csv", 13),
+    ("cnnblstm", "fp32"): ("profiles/steps/r06z_cnn_fp32_step_kernel_stats.csv", 13),
+    ("cnnblstm", "bf16"): ("profiles/steps/r06z_cnn_bf16_step_kernel_stats.csv", 13),
     ("gan", "bf16", 626): ("profiles/steps/r05e_gan_c4_step_kernel_stats.csv", 13),
     ("gan", "bf16", 1001): ("profiles/steps/r05e_gan_c5_step_kernel_stats.csv", 13),
 }
@@ -417,8 +417,8 @@ STEP_TABLES = {
 # time -- the in-step kernel times above add up to more than the step, because
 # the side stream's weight gradients overlap the main stream.
 STEP_TRACES = {
-    ("cnnblstm", "fp32"): "profiles/steps/r06x_cnn_fp32_step_trace.csv",
-    ("cnnblstm", "bf16"): "profiles/steps/r06x_cnn_bf16_step_trace.csv",
+    ("cnnblstm", "fp32"): "profiles/steps/r06z_cnn_fp32_step_trace.csv",
+    ("cnnblstm", "bf16"): "profiles/steps/r06z_cnn_bf16_step_trace.csv",
 }
 
 

@@ -459,6 +459,7 @@ class _BLSTMFn(torch.autograd.Function):
         N, T, _ = dh.shape
         NT = N * T
         grads = [None] * len(params)
+        gwi_of = {}                       # layer -> the pair's [dW_ih, dW_ih_rev]
         dx = None
         # The weight/bias gradients of layer l depend only on its gate
         # gradients, so they run on a side stream while the main stream goes
@@ -539,6 +540,12 @@ class _BLSTMFn(torch.autograd.Function):
                 dxi = ops.sum_slabs(sl, 4).view(NT, Il)
             return dxi, gwi
 
+        # SIDE_LAG: layer l's side-stream launches are issued (host side) after
+        # layer l-1's recurrence launch instead of before it: the GPU runs the
+        # same work in the same stream order, but the ~10 launches' host time
+        # overlaps that recurrence instead of delaying its launch
+        lag = main_first and SIDE_LAG
+        pending = None
         for l in range(L - 1, -1, -1):
             inp, h, gates, cell = saved[4 * l:4 * l + 4]
             wf, hf, bif, bhf, wr, hr, bir, bhr = params[8 * l:8 * l + 8]
@@ -553,6 +560,9 @@ class _BLSTMFn(torch.autograd.Function):
                 # first BPTT launch (DEFER_EARLY: waiting only for the decoder
                 # backward, so they run beside that recurrence too)
                 _Deferred.flush(dh.device, after=pre if DEFER_EARLY else None)
+            if pending is not None:
+                pending()
+                pending = None
             dg2 = dg.view(NT, 8 * H)
             if l016 is not None:
                 # bf16 operands of the layer-0 data / weight gradients (k-major
@@ -587,57 +597,73 @@ class _BLSTMFn(torch.autograd.Function):
                 # encoder backward wait for it) is issued before the side
                 # stream's weight-gradient launches, whose host-side issue
                 # would otherwise leave the current stream idle
-                dxi, gwi_pair = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
-                                        dg16 if l016 is not None else None,
-                                        dgT16 if l016 is not None else None, pair16)
-            with torch.cuda.stream(side):
-                # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
-                # for the recurrent / upper layers -> parallel split-K over row chunks
-                gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H, offsets_b=(0, H),
-                                         bf16=bf16)
-                if pair or pair16:
-                    gwi = None
-                elif early:
-                    gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0,
-                                            l016=((dg16 if ctx.l016_km else dgT16), l016[0],
-                                                  ctx.l016_km) if l016 is not None else None)
-                elif l016 is not None:
-                    if ctx.l016_km:
-                        gcat = ops.wgrad_bf16_km(dg16, l016[0], NT,
-                                                 torch.empty(8 * H, Il, device=dh.device))
+                dxi, gwi_of[l] = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
+                                         dg16 if l016 is not None else None,
+                                         dgT16 if l016 is not None else None, pair16)
+            def side_work(l=l, dg=dg, dg2=dg2, hp=hp, inp=inp, Il=Il, l016=l016, pair=pair,
+                          pair16=pair16, early=early, to_sink=to_sink,
+                          dg16=dg16 if l016 is not None else None,
+                          dgT16=dgT16 if l016 is not None else None):
+                """Layer l's weight / bias gradients on the side stream (and
+                its slots in grads; gwi_of[l] holds the pair's dW_ih)."""
+                with torch.cuda.stream(side):
+                    # dW_hh = dg^T hprev, dW_ih = dg^T inp: K = N*T rows, tiny outputs
+                    # for the recurrent / upper layers -> parallel split-K over row chunks
+                    gwh = ops.gemm_tn_splitk(dg2, 8 * H, hp, 2 * H, NT, 4 * H, H,
+                                             offsets_b=(0, H), bf16=bf16)
+                    if pair or pair16:
+                        gwi = None
+                    elif early:
+                        gwi = _wih_grad_chunked(dg2, inp, H, Il, NT, bf16, ctx.sink, ctx.wih0,
+                                                l016=((dg16 if ctx.l016_km else dgT16), l016[0],
+                                                      ctx.l016_km) if l016 is not None else None)
+                    elif l016 is not None:
+                        if ctx.l016_km:
+                            gcat = ops.wgrad_bf16_km(dg16, l016[0], NT,
+                                                     torch.empty(8 * H, Il, device=dh.device))
+                        else:
+                            gcat = ops.gemm_bf16nt_splitk(dgT16, l016[0], NT)     # [8H, I]
+                        gwi = [gcat[:4 * H], gcat[4 * H:]]
                     else:
-                        gcat = ops.gemm_bf16nt_splitk(dgT16, l016[0], NT)     # [8H, I]
-                    gwi = [gcat[:4 * H], gcat[4 * H:]]
-                else:
-                    gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il,
-                                             offsets_b=(0, 0), bf16=bf16)
-                db_ih = ops.colsum(dg2)           # b_ih and b_hh get the same gradient
-                db_hh = db_ih.clone()
-                if dp_side:
-                    po = ctx.param_objs[8 * l:8 * l + 8]
-                    wi = [None, None] if (early or gwi is None) else gwi
-                    _reduce_side(ctx.sink, po, (wi[0], gwh[0], db_ih[:4 * H], db_hh[:4 * H],
-                                                wi[1], gwh[1], db_ih[4 * H:], db_hh[4 * H:]))
-            for t in (dg, hp, inp) + ((dg16, dgT16, l016[0]) if l016 is not None else ()):
-                if t is not None:
-                    t.record_stream(side)     # main-stream memory read on the side stream
-            base = 8 * l
-            if not main_first:
-                dxi, gwi_pair = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
-                                        dg16 if l016 is not None else None,
-                                        dgT16 if l016 is not None else None, pair16)
-            if pair or pair16:
-                gwi = gwi_pair
-            if to_sink:   # p.grad set and reduced above / by _wih_grad_chunked
-                gwi = [None, None]
-                ctx.early_done = True
-            grads[base + 0], grads[base + 1] = gwi[0], gwh[0]
-            grads[base + 2], grads[base + 3] = db_ih[:4 * H], db_hh[:4 * H]
-            grads[base + 4], grads[base + 5] = gwi[1], gwh[1]
-            grads[base + 6], grads[base + 7] = db_ih[4 * H:], db_hh[4 * H:]
+                        gwi = ops.gemm_tn_splitk(dg2, 8 * H, inp, Il, NT, 4 * H, Il,
+                                                 offsets_b=(0, 0), bf16=bf16)
+                    db_ih = ops.colsum(dg2)           # b_ih and b_hh get the same gradient
+                    db_hh = db_ih.clone()
+                    if dp_side:
+                        po = ctx.param_objs[8 * l:8 * l + 8]
+                        wi = [None, None] if (early or gwi is None) else gwi
+                        _reduce_side(ctx.sink, po, (wi[0], gwh[0], db_ih[:4 * H], db_hh[:4 * H],
+                                                    wi[1], gwh[1], db_ih[4 * H:], db_hh[4 * H:]))
+                for t in (dg, hp, inp) + ((dg16, dgT16, l016[0]) if l016 is not None else ()):
+                    if t is not None:
+                        t.record_stream(side)     # main-stream memory read on the side stream
+                if pair or pair16:   # (not MAIN_FIRST: set behind main_dx below)
+                    gwi = gwi_of.get(l, [None, None])
+                if to_sink:   # p.grad set and reduced above / by _wih_grad_chunked
+                    gwi = [None, None]
+                    ctx.early_done = True
+                base = 8 * l
+                grads[base + 0], grads[base + 1] = gwi[0], gwh[0]
+                grads[base + 2], grads[base + 3] = db_ih[:4 * H], db_hh[:4 * H]
+                grads[base + 4], grads[base + 5] = gwi[1], gwh[1]
+                grads[base + 6], grads[base + 7] = db_ih[4 * H:], db_hh[4 * H:]
+
+            if lag:
+                pending = side_work
+            elif main_first:
+                side_work()
+            else:
+                side_work()
+                dxi, gwi_of[l] = main_dx(l, dg2, inp, Il, wf, wr, l016, pair, to_sink,
+                                         dg16 if l016 is not None else None,
+                                         dgT16 if l016 is not None else None, pair16)
+                if (pair or pair16) and not to_sink:
+                    grads[8 * l], grads[8 * l + 4] = gwi_of[l]
             if l > 0 or ctx.needs_input_grad[0]:
                 dh = dxi.view(N, T, Il)
                 dx = dh
+        if pending is not None:
+            pending()
         for gr in grads:
             if gr is not None:
                 gr.record_stream(main)    # side-stream memory handed to autograd
@@ -731,6 +757,10 @@ DEFER_LIFO = os.environ.get("AINP_DEFER_LIFO", "1") != "0"
 # stream (hipExtStreamCreateWithCUMask, 8 of 32 CUs kept free for the
 # recurrence) measured +3.3 ms/step on both and was dropped.
 DEFER_EARLY = os.environ.get("AINP_DEFER_EARLY", "1") != "0"
+# BLSTM backward: each layer's side-stream weight-gradient launches issued
+# behind the next layer's recurrence launch (_BLSTMFn.backward; A/B:
+# AINP_SIDE_LAG=0)
+SIDE_LAG = os.environ.get("AINP_SIDE_LAG", "1") != "0"
 # (C2 14.65 -> 14.43 / 14.79 -> 14.55 ms/step A/B, profiles/r05o_ab_x6r_apf_side2.txt).
 # Round 6: AINP_BLSTM_SIDE2 = 0 / 1 / fp32 (default) / bf16 -- in the bf16
 # configuration the second stream's GEMMs slowed the layer-0 BPTT beside them
