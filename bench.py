@@ -407,8 +407,8 @@ def spawn_ranks(n):
 STEP_TABLES = {
     ("cnnblstm", "fp32"): ("profiles/steps/r06z_cnn_fp32_step_kernel_stats.csv", 13),
     ("cnnblstm", "bf16"): ("profiles/steps/r06z_cnn_bf16_step_kernel_stats.csv", 13),
-    ("gan", "bf16", 626): ("profiles/steps/r05e_gan_c4_step_kernel_stats.csv", 13),
-    ("gan", "bf16", 1001): ("profiles/steps/r05e_gan_c5_step_kernel_stats.csv", 13),
+    ("gan", "bf16", 626): ("profiles/steps/r06z_gan_c4_step_kernel_stats.csv", 13),
+    ("gan", "bf16", 1001): ("profiles/steps/r06z_gan_c5_step_kernel_stats.csv", 13),
 }
 
 

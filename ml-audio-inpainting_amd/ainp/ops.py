@@ -1335,7 +1335,9 @@ def conv_gen(src0, w, *, src1=None, Hin=None, Win=None, stride=1, pad=0, bias=No
             nm = ("conv_gen_nhwc16_wide_kernel<256" if Cout > 128 else
                   "conv_gen_nhwc16_wide_kernel<128" if Cout > 64 else "conv_gen_nhwc16_kernel<64")
         elif Cout == 1:
-            nm = "conv_cout1_partial_kernel"
+            # both Cout = 1 kernels: conv_cout1_partial_kernel and the batched-
+            # tap conv_cout1_partial_b_kernel<KT, CG> (round 6)
+            nm = "conv_cout1_partial"
         elif _direct_route(C0, C1, H0, W0, Hin, Win, KH, KW, Cout, want_stats):
             nm = "conv_gen_smallcin_kernel"
         else:
