@@ -574,3 +574,41 @@ def test_wgrad_x6s_tile_rows(monkeypatch, cin, cout, N, H, W, bf16):
         if ref is None:
             ref = (dw, db)
         assert rel(dw, ref[0]) < 1e-5 and rel(db, ref[1]) < 1e-5, ft
+
+
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_cnnblstm_step_blstm_issue_order_bit_identical(monkeypatch, dtype):
+    """Round 6, cnnblstm.SIDE_LAG: the BLSTM backward issues each layer's
+    side-stream weight-gradient launches after the next layer's recurrence
+    launch (default), right after the layer's data gradient (SIDE_LAG off), or
+    before it (ops.MAIN_FIRST off) -- the same kernels on the same streams, so
+    the loss and every gradient are bit-identical."""
+    from ainp import cnnblstm, ops
+    cfg = {"data": {"sample_rate": 16000, "spectrogram": {"n_fft": 512, "hop_length": 192,
+                                                          "win_length": 384}},
+           "model": {"in_channels": 1, "num_lstm_layers": 3, "lstm_hidden_dim": 128,
+                     "enc_filters": [16, 32], "dec_filters": [16, 32]},
+           "accel": {"dtype": dtype}}
+    g = torch.Generator().manual_seed(13)
+    N, F, T = 3, 257, 96
+    x = (torch.randn(N, 1, F, T, generator=g) - 2.0).to(DEV)
+    mask = torch.zeros(N, F, T)
+    for i in range(N):
+        mask[i, :, 10 + 20 * i:27 + 20 * i] = 1.0
+    mask = mask.to(DEV)
+    tgt = torch.complex(torch.rand(N, F, T, generator=g), torch.rand(N, F, T, generator=g)).to(DEV)
+    res = []
+    for lag, main_first in ((True, True), (False, True), (False, False)):
+        monkeypatch.setattr(cnnblstm, "SIDE_LAG", lag)
+        monkeypatch.setattr(ops, "MAIN_FIRST", main_first)
+        torch.manual_seed(0)
+        m = cnnblstm.StackedBLSTMCNN(config=cfg).to(DEV).train()
+        loss = cnnblstm.l1_pow10_loss(m(x), mask, tgt)
+        loss.backward()
+        torch.cuda.synchronize()
+        res.append((float(loss.detach()),
+                    {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    for loss_k, grads_k in res[1:]:
+        assert loss_k == res[0][0]
+        diff = [n for n, g0 in res[0][1].items() if not torch.equal(g0, grads_k[n])]
+        assert not diff, diff
